@@ -1,0 +1,109 @@
+"""ctypes binding of libcgan3d.so — the C-ABI declared in include/cgan3d.h.
+
+The library is built in-tree (``contrast-gan-3d_amd/csrc/Makefile`` → ``cgan3d_amd/libcgan3d.so``).
+It is loaded *after* torch so that its ``libamdhip64.so.7`` dependency binds to the HIP runtime
+torch already mapped (one runtime per process: torch's streams and device pointers are valid in
+our kernels).  There is no fallback: if the library or a GPU is missing, calls raise.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from pathlib import Path
+
+import torch  # noqa: F401  (must be imported first: see module docstring)
+
+LIB_PATH = Path(__file__).resolve().parent / "libcgan3d.so"
+
+ACT_NONE, ACT_RELU, ACT_LRELU, ACT_TANH = 0, 1, 2, 3
+# device loss slots written by the loss kernels (include/cgan3d.h)
+L_D, L_WD, L_GP, L_G, L_SIM, L_HU, L_GFULL = range(7)
+
+
+class ConvGeom(C.Structure):
+    _fields_ = [("n", C.c_int32), ("di", C.c_int32), ("hi", C.c_int32), ("wi", C.c_int32),
+                ("do_", C.c_int32), ("ho", C.c_int32), ("wo", C.c_int32),
+                ("cin", C.c_int32), ("cout", C.c_int32), ("k", C.c_int32), ("stride", C.c_int32),
+                ("pad", C.c_int32), ("transposed", C.c_int32), ("reflect", C.c_int32),
+                ("w_sa", C.c_int64), ("w_sb", C.c_int64)]
+
+
+class Epilogue(C.Structure):
+    _fields_ = [("bias", C.c_void_p), ("residual", C.c_void_p), ("mask_src", C.c_void_p),
+                ("minuend", C.c_void_p), ("out2", C.c_void_p), ("stats", C.c_void_p),
+                ("act", C.c_int32), ("slope", C.c_float)]
+
+
+_P, _I32, _I64, _F = C.c_void_p, C.c_int32, C.c_int64, C.c_float
+_SIGS = {
+    "cgan3d_version": ([], C.c_char_p),
+    "cgan3d_get_last_error": ([], C.c_char_p),
+    "cgan3d_conv3d_stats_floats": ([_P], _I64),
+    "cgan3d_conv3d_fwd": ([_P, _P, _P, _P, _P, _P], _I32),
+    "cgan3d_conv3d_wgrad_ws_floats": ([_P], _I64),
+    "cgan3d_conv3d_wgrad": ([_P, _P, _P, _P, _I32, _P, _P], _I32),
+    "cgan3d_bn_finalize": ([_P, _I64, _I32, _P, _P, _P, _P, _P, _F, _F, _P, _P, _P], _I32),
+    "cgan3d_bn_apply": ([_P, _I64, _I32, _P, _I32, _F, _P, _P, _P], _I32),
+    "cgan3d_bn_backward_ws_floats": ([_I64, _I32], _I64),
+    "cgan3d_bn_backward": ([_P, _P, _I64, _I32, _P, _P, _P, _I32, _F, _P, _P, _P, _P, _P], _I32),
+    "cgan3d_channel_sum_ws_floats": ([_I64, _I32], _I64),
+    "cgan3d_channel_sum": ([_P, _I64, _I32, _P, _P, _P], _I32),
+    "cgan3d_reflect_fold": ([_P, _P, _I32, _I32, _I32, _I32, _I32, _I32, _P], _I32),
+    "cgan3d_gp_interpolate": ([_P, _P, _P, _P, _I32, _I64, _P], _I32),
+    "cgan3d_tanh_backward": ([_P, _P, _P, _I64, _P], _I32),
+    "cgan3d_loss_ws_floats": ([_I64], _I64),
+    "cgan3d_critic_logits_grad": ([_P, _I32, _I32, _I32, _I32, _F, _P, _P, _P], _I32),
+    "cgan3d_gradient_penalty": ([_P, _I32, _I64, _F, _P, _P, _P, _P], _I32),
+    "cgan3d_generator_logits_grad": ([_P, _I32, _F, _P, _P, _P], _I32),
+    "cgan3d_generator_output_grad": ([_P, _P, _P, _P, _P, _I64, _F, _F, _F, _F, _P, _P, _P, _P], _I32),
+    "cgan3d_adam_tick": ([_P, _P], _I32),
+    "cgan3d_adam": ([_P, _P, _P, _P, _I64, _P, _P], _I32),
+}
+
+_lib = None
+
+
+def exported_symbols():
+    return list(_SIGS)
+
+
+def load(path: os.PathLike | str | None = None) -> C.CDLL:
+    """Load and type the library (no GPU needed to load; kernels need one to run)."""
+    global _lib
+    if _lib is not None and path is None:
+        return _lib
+    p = Path(path) if path is not None else LIB_PATH
+    if not p.is_file():
+        raise RuntimeError(f"cgan3d: HIP library not built: {p} (run __graft_entry__.build() or make -C csrc)")
+    lib = C.CDLL(str(p))
+    for name, (args, res) in _SIGS.items():
+        fn = getattr(lib, name)
+        fn.argtypes = args
+        fn.restype = res
+    if path is None:
+        _lib = lib
+    return lib
+
+
+def lib() -> C.CDLL:
+    if _lib is None:
+        if not torch.cuda.is_available():
+            raise RuntimeError("cgan3d: the HIP path needs a GPU (torch.cuda.is_available() is False)")
+        load()
+    return _lib
+
+
+def check(rc: int, what: str = "") -> None:
+    if rc != 0:
+        msg = _lib.cgan3d_get_last_error().decode() if _lib is not None else ""
+        raise RuntimeError(f"cgan3d {what} failed (status {rc}): {msg}")
+
+
+def ptr(t: "torch.Tensor | None") -> int | None:
+    if t is None:
+        return None
+    return t.data_ptr()
+
+
+def stream() -> int:
+    return torch.cuda.current_stream().cuda_stream

@@ -1,0 +1,417 @@
+"""The G+D training step as an explicit, hand-scheduled sequence of HIP launches.
+
+This is the hot path (BASELINE.json north_star): ``Trainer.train_step``
+(contrast_gan_3D/trainer/Trainer.py:163-203) = generator forward, critic update with the WGAN
+gradient penalty (Trainer.py:108-142, model/utils.py:12-41), generator update
+(Trainer.py:144-161), Adam on both (basic_conf.py:55,67).
+
+Instead of recording an autograd graph (and a double-backward graph for the GP), the backward
+passes are derived by hand and scheduled explicitly:
+
+* Generator backward: BN / ReLU / residual / ConvTranspose / reflect-pad chain rule.
+* Critic update: one batched forward over ``[real | fake | interpolation]`` (exact: the GP-conf
+  critic has no batch coupling), one batched input-grad chain (the interpolation rows seeded
+  with ones give g = dD/dx), the GP reduction producing gamma = dGP/dg, then the *forward-mode*
+  chain nu_l = mask_l * conv_l(nu_{l-1}) from gamma, which turns the double backward into plain
+  weight-gradients: dW_l += wgrad(nu_{l-1}, dz_l[interp]).  Biases get no GP gradient and
+  LeakyReLU masks are piecewise constant, so this equals torch's double backward exactly in
+  real arithmetic.  The reference's zero-valued generator backward through the GP
+   is not executed.
+* The critic weight-gradients the reference computes during the generator update are discarded
+  by its next ``zero_grad`` (Trainer.py:111) and are not computed here.
+
+All buffers are allocated once per (batch, patch) shape; every launch goes to the current
+stream with device-resident scalars (Adam step/lr), so ``step`` can be captured in a HIP graph.
+Activations are channels-last fp32 (see include/cgan3d.h).
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import torch
+
+from . import _lib as L
+from . import ops
+
+Dims = Tuple[int, int, int]
+
+
+def _half(d: Dims) -> Dims:
+    return tuple((x + 2 * 1 - 3) // 2 + 1 for x in d)
+
+
+def _conv_out(d: Dims, k, s, p) -> Dims:
+    return tuple((x + 2 * p - k) // s + 1 for x in d)
+
+
+class Arena:
+    """One flat fp32 buffer for a module's parameters (+ grads + Adam moments).
+
+    ``p.data`` and ``p.grad`` become views into the arena, so one launch updates every tensor
+    (fused multi-tensor Adam) and the module's ``state_dict`` stays the reference's.
+    """
+
+    def __init__(self, module: torch.nn.Module, device):
+        self.names, self.params = [], []
+        for n, p in module.named_parameters():
+            self.names.append(n)
+            self.params.append(p)
+        total = sum(p.numel() for p in self.params)
+        self.flat = torch.empty(total, device=device, dtype=torch.float32)
+        self.grad = torch.zeros(total, device=device, dtype=torch.float32)
+        self.exp_avg = torch.zeros(total, device=device, dtype=torch.float32)
+        self.exp_avg_sq = torch.zeros(total, device=device, dtype=torch.float32)
+        self.views, self.gviews = {}, {}
+        off = 0
+        with torch.no_grad():
+            for n, p in zip(self.names, self.params):
+                k = p.numel()
+                v = self.flat[off:off + k].view_as(p)
+                v.copy_(p.data)
+                p.data = v
+                p.grad = self.grad[off:off + k].view_as(p)
+                self.views[n] = v
+                self.gviews[n] = p.grad
+                off += k
+        self.numel = total
+
+    def rebind_grads(self):
+        """Re-attach ``p.grad`` views (a user ``zero_grad(set_to_none=True)`` drops them)."""
+        for p, g in zip(self.params, self.gviews.values()):
+            p.grad = g
+
+
+# ----------------------------------------------------------------------------------------------
+@dataclass
+class _GLayer:
+    kind: str            # conv | convt | last
+    name: str            # state_dict prefix
+    k: int
+    s: int
+    p: int
+    reflect: bool
+    cin: int
+    cout: int
+    din: Dims
+    dout: Dims
+    act: int = L.ACT_RELU
+    residual: bool = False
+
+
+class GeneratorPlan:
+    """Buffers + launch geometry of ResnetGenerator (model/generator.py:9-90) for a batch shape."""
+
+    def __init__(self, cfg, n: int, dims: Dims, device):
+        c0 = cfg.init_channels_out
+        self.n, self.dims, self.device = n, tuple(dims), device
+        layers: List[_GLayer] = [_GLayer("conv", "model.first", 7, 1, 3, True, 1, c0, dims, dims)]
+        d = tuple(dims)
+        for i in range(cfg.n_updownsample_blocks):
+            ci = c0 * 2**i
+            dn = _conv_out(d, 3, 2, 1)
+            layers.append(_GLayer("conv", f"model.downsampling.{i}", 3, 2, 1, False, ci, 2 * ci, d, dn))
+            d = dn
+        cr = c0 * 2**cfg.n_updownsample_blocks
+        for r in range(cfg.n_resnet_blocks):
+            layers.append(_GLayer("conv", f"model.resnet_backbone.{r}.block0", 3, 1, 1, False, cr, cr, d, d,
+                                  act=L.ACT_NONE))
+            layers.append(_GLayer("conv", f"model.resnet_backbone.{r}.block1", 3, 1, 1, False, cr, cr, d, d,
+                                  residual=True))
+        for j, i in enumerate(range(cfg.n_updownsample_blocks, 0, -1)):
+            ci = c0 * 2**i
+            up = tuple(2 * x for x in d)  # k3 s2 p1 output_padding 1
+            layers.append(_GLayer("convt", f"model.upsampling.{j}", 3, 2, 1, False, ci, ci // 2, d, up))
+            d = up
+        assert d == tuple(dims), f"generator output dims {d} != input dims {dims} (need dims % 4 == 0)"
+        self.last = _GLayer("last", "model.last_conv", 7, 1, 3, True, c0, 1, d, d, act=L.ACT_TANH)
+        self.layers = layers
+
+        def buf(dd, c):
+            return torch.empty((n, *dd, c), device=device, dtype=torch.float32)
+
+        self.geo_fwd, self.geo_dgrad, self.geo_wgrad = [], [], []
+        self.z, self.y, self.dy, self.dz, self.stats, self.ss, self.mi, self.nstat = [], [], [], [], [], [], [], []
+        ws = 0
+        for ly in layers:
+            if ly.kind == "conv":
+                gf = ops.conv_fwd_geom(n, ly.din, ly.dout, ly.cin, ly.cout, ly.k, ly.s, ly.p, ly.reflect)
+                gd = ops.conv_dgrad_geom(n, ly.din, ly.dout, ly.cin, ly.cout, ly.k, ly.s, ly.p)
+                gw = ops.conv_wgrad_geom(n, ly.din, ly.dout, ly.cin, ly.cout, ly.k, ly.s, ly.p, ly.reflect)
+            else:
+                gf = ops.convt_fwd_geom(n, ly.din, ly.dout, ly.cin, ly.cout, ly.k, ly.s, ly.p)
+                gd = ops.convt_dgrad_geom(n, ly.din, ly.dout, ly.cin, ly.cout, ly.k, ly.s, ly.p)
+                gw = ops.convt_wgrad_geom(n, ly.din, ly.dout, ly.cin, ly.cout, ly.k, ly.s, ly.p)
+            self.geo_fwd.append(gf)
+            self.geo_dgrad.append(gd)
+            self.geo_wgrad.append(gw)
+            self.z.append(buf(ly.dout, ly.cout))
+            self.y.append(buf(ly.dout, ly.cout))
+            self.dy.append(buf(ly.dout, ly.cout))
+            self.dz.append(buf(ly.dout, ly.cout))
+            ns = ops.stats_floats(gf)
+            self.nstat.append(ns // (2 * ly.cout + 1))
+            self.stats.append(torch.empty(ns, device=device))
+            self.ss.append(torch.empty(2 * ly.cout, device=device))
+            self.mi.append(torch.empty(2 * ly.cout, device=device))
+            nvox = n * ly.dout[0] * ly.dout[1] * ly.dout[2]
+            ws = max(ws, ops.wgrad_ws_floats(gw), ops.bn_backward_ws_floats(nvox, ly.cout))
+        la = self.last
+        pd = tuple(x + 2 * la.p for x in la.din)
+        self.geo_last_fwd = ops.conv_fwd_geom(n, la.din, la.dout, la.cin, 1, la.k, 1, la.p, True)
+        self.geo_last_wgrad = ops.conv_wgrad_geom(n, la.din, la.dout, la.cin, 1, la.k, 1, la.p, True)
+        self.geo_last_dgrad = ops.conv_dgrad_geom(n, pd, la.dout, la.cin, 1, la.k, 1, 0)  # onto the padded grid
+        self.att = buf(la.dout, 1)
+        self.dz_last = buf(la.dout, 1)
+        self.dpad = buf(pd, la.cin)
+        ws = max(ws, ops.wgrad_ws_floats(self.geo_last_wgrad), ops.channel_sum_ws_floats(n * la.dout[0] * la.dout[1] * la.dout[2], 1))
+        self.ws = torch.empty(ws, device=device)
+
+    # -- forward: x [n,D,H,W,1] -> att (tanh output); opt_hat_out = x - att (Trainer.py:170-171)
+    def forward(self, P: Dict[str, torch.Tensor], x: torch.Tensor, opt_hat_out: Optional[torch.Tensor] = None,
+                training: bool = True):
+        h = x
+        h_res = None
+        for i, ly in enumerate(self.layers):
+            if ly.name.endswith("block0"):
+                h_res = h
+            stats = self.stats[i] if training else None
+            ops.conv(self.geo_fwd[i], h, P[f"{ly.name}.conv.weight"], self.z[i], ops.epilogue(stats=stats))
+            nb = f"{ly.name}.normalization"
+            if training:
+                ops.bn_finalize(self.stats[i], self.nstat[i], ly.cout, P[f"{nb}.weight"], P[f"{nb}.bias"],
+                                P[f"{nb}.running_mean"], P[f"{nb}.running_var"], P[f"{nb}.num_batches_tracked"],
+                                self.ss[i], self.mi[i])
+            else:
+                self._eval_scale_shift(P, nb, i)
+            nvox = self.n * ly.dout[0] * ly.dout[1] * ly.dout[2]
+            ops.bn_apply(self.z[i], nvox, ly.cout, self.ss[i], ly.act, self.y[i],
+                         residual=h_res if ly.residual else None)
+            h = self.y[i]
+        la = self.last
+        ep = ops.epilogue(bias=P["model.last_conv.bias"], act=L.ACT_TANH,
+                          minuend=x if opt_hat_out is not None else None, out2=opt_hat_out)
+        ops.conv(self.geo_last_fwd, h, P["model.last_conv.weight"], self.att, ep)
+        return self.att
+
+    def _eval_scale_shift(self, P, nb, i):
+        # eval-mode BN (Trainer.validate, Trainer.py:248-249): running statistics
+        with torch.no_grad():
+            inv = torch.rsqrt(P[f"{nb}.running_var"] + 1e-5)
+            sc = P[f"{nb}.weight"] * inv
+            c = sc.numel()
+            self.ss[i][:c].copy_(sc)
+            self.ss[i][c:].copy_(P[f"{nb}.bias"] - P[f"{nb}.running_mean"] * sc)
+
+    # -- backward from dz_last = dL/d(pre-tanh) ; writes parameter grads into G (grad views)
+    def backward(self, P: Dict[str, torch.Tensor], G: Dict[str, torch.Tensor], x: torch.Tensor):
+        la = self.last
+        n = self.n
+        u = self.y[-1]
+        ops.wgrad(self.geo_last_wgrad, u, self.dz_last, G["model.last_conv.weight"], self.ws)
+        nvl = n * la.dout[0] * la.dout[1] * la.dout[2]
+        ops.channel_sum(self.dz_last, nvl, 1, G["model.last_conv.bias"], self.ws)
+        ops.conv(self.geo_last_dgrad, self.dz_last, P["model.last_conv.weight"], self.dpad)
+        ops.reflect_fold(self.dpad, self.dy[-1], n, la.din, la.cin, la.p)
+        for i in range(len(self.layers) - 1, -1, -1):
+            ly = self.layers[i]
+            nb = f"{ly.name}.normalization"
+            nvox = n * ly.dout[0] * ly.dout[1] * ly.dout[2]
+            ops.bn_backward(self.dy[i], self.z[i], nvox, ly.cout, self.ss[i], self.mi[i], P[f"{nb}.weight"], ly.act,
+                            G[f"{nb}.weight"], G[f"{nb}.bias"], self.dz[i], self.ws)
+            xin = self.y[i - 1] if i > 0 else x
+            if ly.kind == "convt":  # ConvTranspose3d: the output-grad is the gathered operand
+                ops.wgrad(self.geo_wgrad[i], self.dz[i], xin, G[f"{ly.name}.conv.weight"], self.ws)
+            else:
+                ops.wgrad(self.geo_wgrad[i], xin, self.dz[i], G[f"{ly.name}.conv.weight"], self.ws)
+            if i == 0:
+                break
+            # input-grad; a ResNet block0 also receives the skip gradient dL/dh_{r+1}
+            res = self.dy[i + 1] if ly.name.endswith("block0") else None
+            ops.conv(self.geo_dgrad[i], self.dz[i], P[f"{ly.name}.conv.weight"], self.dy[i - 1],
+                     ops.epilogue(residual=res))
+
+
+# ----------------------------------------------------------------------------------------------
+@dataclass
+class _DLayer:
+    name: str
+    k: int
+    s: int
+    p: int
+    cin: int
+    cout: int
+    din: Dims
+    dout: Dims
+
+
+class CriticPlan:
+    """Buffers + geometry of PatchGANDiscriminator (model/discriminator.py:9-84), GP conf
+    (Identity norm, gradient_penalty_conf.py:14), for up to ``nmax`` samples."""
+
+    def __init__(self, cfg, nmax: int, dims: Dims, device):
+        self.cfg, self.nmax, self.dims, self.device = cfg, nmax, tuple(dims), device
+        c0, s = cfg.init_channels_out, cfg.negative_slope
+        self.slope = s
+        d = tuple(dims)
+        ls = []
+        dn = _conv_out(d, 4, 2, 1)
+        ls.append(_DLayer("model.first.conv", 4, 2, 1, cfg.channels_in, c0, d, dn))
+        d = dn
+        out_ = c0
+        for m in range(cfg.discriminator_depth):
+            in_, out_ = min(2**m, 8) * c0, min(2 ** (m + 1), 8) * c0
+            dn = _conv_out(d, 4, 2, 1)
+            ls.append(_DLayer(f"model.middle.{m}.conv", 4, 2, 1, in_, out_, d, dn))
+            d = dn
+        dn = _conv_out(d, 4, 1, 1)
+        assert min(dn) > 0, f"patch {dims} too small for the critic"
+        ls.append(_DLayer("model.last", 4, 1, 1, out_, 1, d, dn))
+        self.layers = ls
+        self.logit_ps = dn[0] * dn[1] * dn[2]
+        self.a = [torch.empty((nmax, *ly.dout, ly.cout), device=device) for ly in ls]   # activations (last = logits)
+        self.dz = [torch.empty((nmax, *ly.dout, ly.cout), device=device) for ly in ls]  # dL/dz (last = dlogits)
+        ws = 0
+        for ly in ls:
+            g = ops.conv_wgrad_geom(nmax, ly.din, ly.dout, ly.cin, ly.cout, ly.k, ly.s, ly.p)
+            ws = max(ws, ops.wgrad_ws_floats(g),
+                     ops.channel_sum_ws_floats(nmax * ly.dout[0] * ly.dout[1] * ly.dout[2], ly.cout))
+        self.ws = torch.empty(ws, device=device)
+
+    def _sl(self, t, off, n):
+        return t[off:off + n]
+
+    def forward(self, P, x, off: int, n: int):
+        """a_l[off:off+n] = critic activations of x (n samples); logits in a[-1]."""
+        h = x
+        for i, ly in enumerate(self.layers):
+            g = ops.conv_fwd_geom(n, ly.din, ly.dout, ly.cin, ly.cout, ly.k, ly.s, ly.p)
+            last = i == len(self.layers) - 1
+            ep = ops.epilogue(bias=P[f"{ly.name}.bias"], act=L.ACT_NONE if last else L.ACT_LRELU, slope=self.slope)
+            out = self._sl(self.a[i], off, n)
+            ops.conv(g, h, P[f"{ly.name}.weight"], out, ep)
+            h = out
+        return self._sl(self.a[-1], off, n)
+
+    def input_grad(self, P, off: int, n: int, dx_out: torch.Tensor, dx_off: int, dx_n: int):
+        """dz chain from dz[-1][off:off+n] (dlogits) down to dz[0]; then dD/dx for samples
+        [dx_off, dx_off+dx_n) (absolute indices inside the batch) into dx_out."""
+        for i in range(len(self.layers) - 1, 0, -1):
+            ly = self.layers[i]
+            g = ops.conv_dgrad_geom(n, ly.din, ly.dout, ly.cin, ly.cout, ly.k, ly.s, ly.p)
+            ops.conv(g, self._sl(self.dz[i], off, n), P[f"{ly.name}.weight"], self._sl(self.dz[i - 1], off, n),
+                     ops.epilogue(mask_src=self._sl(self.a[i - 1], off, n), slope=self.slope))
+        ly = self.layers[0]
+        if dx_n > 0:
+            g = ops.conv_dgrad_geom(dx_n, ly.din, ly.dout, ly.cin, ly.cout, ly.k, ly.s, ly.p)
+            ops.conv(g, self._sl(self.dz[0], dx_off, dx_n), P[f"{ly.name}.weight"], dx_out)
+
+    def gp_forward_mode(self, P, gamma: torch.Tensor, off: int, n: int):
+        """nu_l = mask_l * conv_l(nu_{l-1}) (no bias), nu_0 = gamma, written in place over
+        a_l[off:off+n] (after the masks there have been consumed)."""
+        h = gamma
+        for i, ly in enumerate(self.layers[:-1]):
+            g = ops.conv_fwd_geom(n, ly.din, ly.dout, ly.cin, ly.cout, ly.k, ly.s, ly.p)
+            out = self._sl(self.a[i], off, n)
+            ops.conv(g, h, P[f"{ly.name}.weight"], out, ops.epilogue(mask_src=out, slope=self.slope))
+            h = out
+
+    def weight_grads(self, P, G, x_all: torch.Tensor, n_all: int, n_bias: int):
+        """dW_l = wgrad(a_{l-1}, dz_l) over n_all samples; db_l = sum dz_l over the first n_bias."""
+        prev = x_all
+        for i, ly in enumerate(self.layers):
+            g = ops.conv_wgrad_geom(n_all, ly.din, ly.dout, ly.cin, ly.cout, ly.k, ly.s, ly.p)
+            ops.wgrad(g, prev, self.dz[i][:n_all], G[f"{ly.name}.weight"], self.ws)
+            nv = n_bias * ly.dout[0] * ly.dout[1] * ly.dout[2]
+            ops.channel_sum(self.dz[i][:n_bias], nv, ly.cout, G[f"{ly.name}.bias"], self.ws)
+            prev = self.a[i][:n_all]
+
+
+# ----------------------------------------------------------------------------------------------
+class StepEngine:
+    """One fused G+D train step for fixed (b_opt, b_sub, patch dims) on one GPU."""
+
+    def __init__(self, generator, critic, g_cfg, d_cfg, b_opt: int, b_sub: int, dims: Dims, *,
+                 g_hyper: Sequence[float], d_hyper: Sequence[float], gp_weight: float = 10.0,
+                 hu_bounds=(112.0 / 600.0, 212.0 / 600.0), gan_w=1.0, sim_w=1.0, hu_w=1.0,
+                 device=None, g_arena: Optional[Arena] = None, d_arena: Optional[Arena] = None):
+        if b_opt != b_sub:
+            raise NotImplementedError("StepEngine: the GP path assumes |OPT| == |LOW|+|HIGH| (basic_conf.py:74-79)")
+        if d_cfg.norm != "identity":
+            raise NotImplementedError("StepEngine: critic with BatchNorm (weight-clip conf) not built yet")
+        device = device or torch.device("cuda", torch.cuda.current_device())
+        self.device = device
+        self.dims = tuple(dims)
+        self.b_opt, self.b_sub, self.b_gp = b_opt, b_sub, min(b_opt, b_sub)
+        self.vox = dims[0] * dims[1] * dims[2]
+        self.gp_weight, self.gan_w, self.sim_w, self.hu_w = gp_weight, gan_w, sim_w, hu_w
+        self.lo, self.hi = hu_bounds
+        self.G = GeneratorPlan(g_cfg, b_sub, dims, device)
+        nmax = b_opt + b_sub + self.b_gp
+        self.D = CriticPlan(d_cfg, nmax, dims, device)
+        self.g_arena = g_arena or Arena(generator, device)
+        self.d_arena = d_arena or Arena(critic, device)
+        self.gP = dict(self.g_arena.views)
+        self.gP.update({k: v for k, v in generator.state_dict(keep_vars=True).items() if k not in self.gP})
+        self.dP = dict(self.d_arena.views)
+        self.gG, self.dG = self.g_arena.gviews, self.d_arena.gviews
+        # critic input slots [real | fake(opt_hat) | interpolation -> gamma]
+        self.xc = torch.empty((nmax, *dims, 1), device=device)
+        self.subopt = torch.empty((b_sub, *dims, 1), device=device)
+        self.mask = torch.empty((b_sub, *dims, 1), device=device, dtype=torch.uint8)
+        self.eps = torch.empty(self.b_gp, device=device)
+        self.gbuf = torch.empty((self.b_gp, *dims, 1), device=device)    # g = dD/dx at the interpolation
+        self.dcrit = torch.empty((b_sub, *dims, 1), device=device)       # dL_G/d opt_hat via the critic
+        self.losses = torch.zeros(8, device=device)
+        self.loss_ws = torch.empty(ops.loss_ws_floats(), device=device)
+        self.g_hyper = torch.tensor(list(g_hyper) + [0.0, 0.0], device=device, dtype=torch.float32)[:6].contiguous()
+        self.d_hyper = torch.tensor(list(d_hyper) + [0.0, 0.0], device=device, dtype=torch.float32)[:6].contiguous()
+
+    @property
+    def opt_hat(self):
+        return self.xc[self.b_opt:self.b_opt + self.b_sub]
+
+    def load_inputs(self, opt: torch.Tensor, subopt: torch.Tensor, mask: torch.Tensor, eps: torch.Tensor):
+        """Copy a batch (NCDHW with C=1 == NDHWC) into the engine's resident input slots."""
+        self.xc[:self.b_opt].view(-1).copy_(opt.reshape(-1), non_blocking=True)
+        self.subopt.view(-1).copy_(subopt.reshape(-1), non_blocking=True)
+        self.mask.view(-1).copy_(mask.reshape(-1), non_blocking=True)
+        self.eps.copy_(eps.reshape(-1), non_blocking=True)
+
+    # -------------------------------------------------------------------------------------------
+    def generator_forward(self):
+        self.G.forward(self.gP, self.subopt, opt_hat_out=self.opt_hat, training=True)
+
+    def critic_update(self):
+        D, bo, bs, bg, V = self.D, self.b_opt, self.b_sub, self.b_gp, self.vox
+        nall = bo + bs + bg
+        ops.gp_interpolate(self.xc[:bg], self.xc[bo:bo + bg], self.eps, self.xc[bo + bs:], bg, V)
+        D.forward(self.dP, self.xc, 0, nall)
+        ops.critic_logits_grad(D.a[-1], bo, bs, bg, D.logit_ps, self.gan_w, D.dz[-1], self.losses)
+        D.input_grad(self.dP, 0, nall, self.gbuf, bo + bs, bg)
+        gamma = self.xc[bo + bs:]
+        ops.gradient_penalty(self.gbuf, bg, V, self.gp_weight, gamma, self.losses, self.loss_ws)
+        D.gp_forward_mode(self.dP, gamma, bo + bs, bg)
+        D.weight_grads(self.dP, self.dG, self.xc, nall, bo + bs)
+        ops.adam_tick(self.d_hyper)
+        ops.adam(self.d_arena.flat, self.d_arena.grad, self.d_arena.exp_avg, self.d_arena.exp_avg_sq, self.d_hyper)
+
+    def generator_update(self):
+        D, bs, V = self.D, self.b_sub, self.vox
+        D.forward(self.dP, self.opt_hat, 0, bs)
+        ops.generator_logits_grad(D.a[-1][:bs], bs * D.logit_ps, self.gan_w, D.dz[-1], self.losses)
+        D.input_grad(self.dP, 0, bs, self.dcrit, 0, bs)
+        ops.generator_output_grad(self.opt_hat, self.subopt, self.G.att, self.mask, self.dcrit, bs * V, self.lo,
+                                  self.hi, self.sim_w, self.hu_w, self.G.dz_last, self.losses, self.loss_ws)
+        self.G.backward(self.gP, self.gG, self.subopt)
+        ops.adam_tick(self.g_hyper)
+        ops.adam(self.g_arena.flat, self.g_arena.grad, self.g_arena.exp_avg, self.g_arena.exp_avg_sq, self.g_hyper)
+
+    def step(self, do_critic: bool = True, do_generator: bool = True):
+        """Trainer.train_step body (Trainer.py:169-184) on the resident inputs."""
+        self.generator_forward()
+        if do_critic:
+            self.critic_update()
+        if do_generator:
+            self.generator_update()
+        return self.losses

@@ -1,0 +1,279 @@
+"""Thin launch wrappers over the C-ABI (include/cgan3d.h), operating on device tensors.
+
+Activations are fp32 NDHWC tensors ``[N, D, H, W, C]``; weights stay in torch layout.  Every
+wrapper launches on the current torch stream and never synchronises, so a whole step can be
+captured in a HIP graph.  Geometry helpers build the gather descriptors for each role a conv
+plays in the step (forward, input-grad, weight-grad; Conv3d and ConvTranspose3d).
+
+Every wrapper first checks on the host that each operand's extent matches what the kernel and
+its grid will touch (a kernel fault on the GPU box can reset the node).  With ``DRY_RUN = True``
+only these checks run — the whole step can be shape-checked on CPU tensors without a GPU.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Optional, Sequence
+
+import torch
+
+from . import _lib as L
+from ._lib import ConvGeom, Epilogue, check, ptr
+
+DRY_RUN = False
+
+
+def _geom(n, di, do, cin, cout, k, s, p, transposed, reflect, sa, sb) -> ConvGeom:
+    g = ConvGeom()
+    g.n = n
+    g.di, g.hi, g.wi = di
+    g.do_, g.ho, g.wo = do
+    g.cin, g.cout, g.k, g.stride, g.pad = cin, cout, k, s, p
+    g.transposed, g.reflect = int(transposed), int(reflect)
+    g.w_sa, g.w_sb = sa, sb
+    return g
+
+
+# --- geometry per role ------------------------------------------------------------------------
+# Conv3d(cin -> cout), weight [cout, cin, k,k,k]; din = input dims, dout = output dims
+def conv_fwd_geom(n, din, dout, cin, cout, k, s, p, reflect=False):
+    t = k**3
+    return _geom(n, din, dout, cin, cout, k, s, p, 0, reflect, t, cin * t)
+
+
+def conv_dgrad_geom(n, din, dout, cin, cout, k, s, p):
+    t = k**3
+    return _geom(n, dout, din, cout, cin, k, s, p, 1, 0, cin * t, t)
+
+
+def conv_wgrad_geom(n, din, dout, cin, cout, k, s, p, reflect=False):
+    t = k**3
+    return _geom(n, din, dout, cin, cout, k, s, p, 0, reflect, t, cin * t)
+
+
+# ConvTranspose3d(cin -> cout), weight [cin, cout, k,k,k]; din = input dims, dout = output dims
+def convt_fwd_geom(n, din, dout, cin, cout, k, s, p):
+    t = k**3
+    return _geom(n, din, dout, cin, cout, k, s, p, 1, 0, cout * t, t)
+
+
+def convt_dgrad_geom(n, din, dout, cin, cout, k, s, p):
+    t = k**3
+    return _geom(n, dout, din, cout, cin, k, s, p, 0, 0, t, cout * t)
+
+
+def convt_wgrad_geom(n, din, dout, cin, cout, k, s, p):
+    """gathered operand = the ConvTranspose output-grad; aligned operand = its input."""
+    t = k**3
+    return _geom(n, dout, din, cout, cin, k, s, p, 0, 0, t, cout * t)
+
+
+class Epi:
+    """Fused-epilogue operands (include/cgan3d.h cgan3d_epilogue), kept as tensors for checks."""
+
+    def __init__(self, bias=None, residual=None, mask_src=None, minuend=None, out2=None, stats=None,
+                 act=L.ACT_NONE, slope=0.0):
+        self.bias, self.residual, self.mask_src = bias, residual, mask_src
+        self.minuend, self.out2, self.stats = minuend, out2, stats
+        self.act, self.slope = act, float(slope)
+
+    def c(self) -> Epilogue:
+        e = Epilogue()
+        e.bias, e.residual, e.mask_src = ptr(self.bias), ptr(self.residual), ptr(self.mask_src)
+        e.minuend, e.out2, e.stats = ptr(self.minuend), ptr(self.out2), ptr(self.stats)
+        e.act, e.slope = self.act, self.slope
+        return e
+
+
+def epilogue(**kw) -> Epi:
+    return Epi(**kw)
+
+
+# --- host-side operand checks -------------------------------------------------------------------
+def _need(t, n, what, dtype=torch.float32, exact=True):
+    if t is None:
+        raise ValueError(f"{what}: missing operand")
+    if t.dtype != dtype:
+        raise TypeError(f"{what}: dtype {t.dtype} != {dtype}")
+    if not t.is_contiguous():
+        raise ValueError(f"{what}: operand must be contiguous")
+    if (t.numel() != n) if exact else (t.numel() < n):
+        raise ValueError(f"{what}: has {t.numel()} elements, kernel touches {n}")
+
+
+def _vox_in(g):
+    return g.n * g.di * g.hi * g.wi
+
+
+def _vox_out(g):
+    return g.n * g.do_ * g.ho * g.wo
+
+
+def _w_extent(g):
+    return (g.cin - 1) * g.w_sa + (g.cout - 1) * g.w_sb + g.k**3
+
+
+def _launch(name, *args):
+    if DRY_RUN:
+        return 0
+    return getattr(L.lib(), name)(*args, L.stream())
+
+
+# --- launches -----------------------------------------------------------------------------------
+def stats_floats(g: ConvGeom) -> int:
+    return int(L.load().cgan3d_conv3d_stats_floats(ctypes.byref(g)))
+
+
+def conv(g: ConvGeom, x: torch.Tensor, w: torch.Tensor, y: torch.Tensor, ep: Optional[Epi] = None):
+    _need(x, _vox_in(g) * g.cin, "conv x")
+    _need(w, _w_extent(g), "conv w", exact=False)
+    ny = _vox_out(g) * g.cout
+    _need(y, ny, "conv y")
+    if ep is not None:
+        if ep.bias is not None:
+            _need(ep.bias, g.cout, "conv bias")
+        for nm in ("residual", "mask_src", "minuend", "out2"):
+            if getattr(ep, nm) is not None:
+                _need(getattr(ep, nm), ny, f"conv {nm}")
+        if ep.stats is not None:
+            _need(ep.stats, stats_floats(g), "conv stats", exact=False)
+    check(_launch("cgan3d_conv3d_fwd", ctypes.byref(g), ptr(x), ptr(w), ptr(y),
+                  ctypes.byref(ep.c()) if ep is not None else None), "conv3d_fwd")
+
+
+def wgrad_ws_floats(g: ConvGeom) -> int:
+    return int(L.load().cgan3d_conv3d_wgrad_ws_floats(ctypes.byref(g)))
+
+
+def wgrad(g: ConvGeom, gathered, aligned, dw, ws, accumulate=False):
+    _need(gathered, _vox_in(g) * g.cin, "wgrad gathered")
+    _need(aligned, _vox_out(g) * g.cout, "wgrad aligned")
+    _need(dw, g.cin * g.cout * g.k**3, "wgrad dw")
+    if _w_extent(g) > dw.numel():
+        raise ValueError("wgrad: weight strides exceed dw")
+    _need(ws, wgrad_ws_floats(g), "wgrad ws", exact=False)
+    check(_launch("cgan3d_conv3d_wgrad", ctypes.byref(g), ptr(gathered), ptr(aligned), ptr(dw), int(accumulate),
+                  ptr(ws)), "conv3d_wgrad")
+
+
+def bn_finalize(stats, nblk, c, gamma, beta, rmean, rvar, nbt, scale_shift, mean_invstd, momentum=0.1, eps=1e-5):
+    _need(stats, nblk * (2 * c + 1), "bn_finalize stats", exact=False)
+    for t, nm in ((gamma, "gamma"), (beta, "beta"), (rmean, "running_mean"), (rvar, "running_var")):
+        _need(t, c, f"bn_finalize {nm}")
+    _need(nbt, 1, "bn_finalize num_batches_tracked", dtype=torch.int64)
+    _need(scale_shift, 2 * c, "bn_finalize scale_shift")
+    _need(mean_invstd, 2 * c, "bn_finalize mean_invstd")
+    check(_launch("cgan3d_bn_finalize", ptr(stats), nblk, c, ptr(gamma), ptr(beta), ptr(rmean), ptr(rvar), ptr(nbt),
+                  momentum, eps, ptr(scale_shift), ptr(mean_invstd)), "bn_finalize")
+
+
+def bn_apply(z, nvox, c, scale_shift, act, y, residual=None, slope=0.0):
+    _need(z, nvox * c, "bn_apply z")
+    _need(y, nvox * c, "bn_apply y")
+    _need(scale_shift, 2 * c, "bn_apply scale_shift")
+    if residual is not None:
+        _need(residual, nvox * c, "bn_apply residual")
+    check(_launch("cgan3d_bn_apply", ptr(z), nvox, c, ptr(scale_shift), act, slope, ptr(residual), ptr(y)),
+          "bn_apply")
+
+
+def bn_backward_ws_floats(nvox, c) -> int:
+    return int(L.load().cgan3d_bn_backward_ws_floats(nvox, c))
+
+
+def bn_backward(dy, z, nvox, c, scale_shift, mean_invstd, gamma, act, dgamma, dbeta, dz, ws, slope=0.0):
+    for t, nm in ((dy, "dy"), (z, "z"), (dz, "dz")):
+        _need(t, nvox * c, f"bn_backward {nm}")
+    for t, nm in ((scale_shift, "scale_shift"), (mean_invstd, "mean_invstd")):
+        _need(t, 2 * c, f"bn_backward {nm}")
+    for t, nm in ((gamma, "gamma"), (dgamma, "dgamma"), (dbeta, "dbeta")):
+        _need(t, c, f"bn_backward {nm}")
+    _need(ws, bn_backward_ws_floats(nvox, c), "bn_backward ws", exact=False)
+    check(_launch("cgan3d_bn_backward", ptr(dy), ptr(z), nvox, c, ptr(scale_shift), ptr(mean_invstd), ptr(gamma),
+                  act, slope, ptr(dgamma), ptr(dbeta), ptr(dz), ptr(ws)), "bn_backward")
+
+
+def channel_sum_ws_floats(nvox, c) -> int:
+    return int(L.load().cgan3d_channel_sum_ws_floats(nvox, c))
+
+
+def channel_sum(x, nvox, c, out, ws):
+    _need(x, nvox * c, "channel_sum x")
+    _need(out, c, "channel_sum out")
+    _need(ws, channel_sum_ws_floats(nvox, c), "channel_sum ws", exact=False)
+    check(_launch("cgan3d_channel_sum", ptr(x), nvox, c, ptr(out), ptr(ws)), "channel_sum")
+
+
+def reflect_fold(padded, out, n, dims: Sequence[int], c, pad):
+    d, h, w = dims
+    _need(padded, n * (d + 2 * pad) * (h + 2 * pad) * (w + 2 * pad) * c, "reflect_fold padded")
+    _need(out, n * d * h * w * c, "reflect_fold out")
+    check(_launch("cgan3d_reflect_fold", ptr(padded), ptr(out), n, d, h, w, c, pad), "reflect_fold")
+
+
+def gp_interpolate(real, fake, eps, out, b, per_sample):
+    for t, nm in ((real, "real"), (fake, "fake"), (out, "out")):
+        _need(t, b * per_sample, f"gp_interpolate {nm}")
+    _need(eps, b, "gp_interpolate eps")
+    check(_launch("cgan3d_gp_interpolate", ptr(real), ptr(fake), ptr(eps), ptr(out), b, per_sample),
+          "gp_interpolate")
+
+
+def tanh_backward(y, dy, dz):
+    _need(dy, y.numel(), "tanh_backward dy")
+    _need(dz, y.numel(), "tanh_backward dz")
+    check(_launch("cgan3d_tanh_backward", ptr(y), ptr(dy), ptr(dz), y.numel()), "tanh_backward")
+
+
+def loss_ws_floats() -> int:
+    return int(L.load().cgan3d_loss_ws_floats(0))
+
+
+def critic_logits_grad(logits, n_real, n_fake, n_gp, per_sample, gan_w, dlogits, losses):
+    n = (n_real + n_fake + n_gp) * per_sample
+    _need(logits, n, "critic_logits_grad logits", exact=False)
+    _need(dlogits, n, "critic_logits_grad dlogits", exact=False)
+    _need(losses, 8, "losses")
+    check(_launch("cgan3d_critic_logits_grad", ptr(logits), n_real, n_fake, n_gp, per_sample, gan_w, ptr(dlogits),
+                  ptr(losses)), "critic_logits_grad")
+
+
+def gradient_penalty(grad, b, per_sample, lambda_, gamma_out, losses, ws):
+    _need(grad, b * per_sample, "gradient_penalty grad")
+    _need(gamma_out, b * per_sample, "gradient_penalty gamma")
+    _need(losses, 8, "losses")
+    _need(ws, loss_ws_floats(), "gradient_penalty ws", exact=False)
+    check(_launch("cgan3d_gradient_penalty", ptr(grad), b, per_sample, lambda_, ptr(gamma_out), ptr(losses),
+                  ptr(ws)), "gradient_penalty")
+
+
+def generator_logits_grad(logits, n, gan_w, dlogits, losses):
+    _need(logits, n, "generator_logits_grad logits", exact=False)
+    _need(dlogits, n, "generator_logits_grad dlogits", exact=False)
+    _need(losses, 8, "losses")
+    check(_launch("cgan3d_generator_logits_grad", ptr(logits), n, gan_w, ptr(dlogits), ptr(losses)),
+          "generator_logits_grad")
+
+
+def generator_output_grad(opt_hat, subopt, att, mask_u8, d_critic, n, lo, hi, sim_w, hu_w, dz_last, losses, ws):
+    for t, nm in ((opt_hat, "opt_hat"), (subopt, "subopt"), (att, "att"), (dz_last, "dz_last")):
+        _need(t, n, f"generator_output_grad {nm}")
+    _need(mask_u8, n, "generator_output_grad mask", dtype=torch.uint8)
+    if d_critic is not None:
+        _need(d_critic, n, "generator_output_grad d_critic")
+    _need(losses, 8, "losses")
+    _need(ws, loss_ws_floats(), "generator_output_grad ws", exact=False)
+    check(_launch("cgan3d_generator_output_grad", ptr(opt_hat), ptr(subopt), ptr(att), ptr(mask_u8), ptr(d_critic),
+                  n, lo, hi, sim_w, hu_w, ptr(dz_last), ptr(losses), ptr(ws)), "generator_output_grad")
+
+
+def adam_tick(hyper):
+    _need(hyper, 6, "adam hyper")
+    check(_launch("cgan3d_adam_tick", ptr(hyper)), "adam_tick")
+
+
+def adam(param, grad, exp_avg, exp_avg_sq, hyper):
+    for t, nm in ((grad, "grad"), (exp_avg, "exp_avg"), (exp_avg_sq, "exp_avg_sq")):
+        _need(t, param.numel(), f"adam {nm}")
+    _need(hyper, 6, "adam hyper")
+    check(_launch("cgan3d_adam", ptr(param), ptr(grad), ptr(exp_avg), ptr(exp_avg_sq), param.numel(), ptr(hyper)),
+          "adam")

@@ -1,0 +1,253 @@
+// Training-mode BatchNorm3d (+ ReLU / Identity / LeakyReLU) for gfx950, channels-last fp32.
+//
+// Replaces aten native_batch_norm / native_batch_norm_backward + relu / threshold_backward of
+// ConvBlock (contrast_gan_3D/model/blocks.py:26-27,45-53): per-channel batch statistics over
+// N*D*H*W, biased variance to normalise, unbiased variance into running_var, eps 1e-5,
+// momentum 0.1 (torch.nn.BatchNorm3d defaults).
+//
+// Forward statistics come from the producing conv's epilogue as per-block (sum, M2, count)
+// partials (conv.hip) combined here with Chan's formula in fp64, so the activation tensor is not
+// re-read for statistics.  Backward is a two-pass reduction (sum dy, sum dy*xhat per channel,
+// per-block partials -> fp64 combine) followed by one elementwise pass.
+#include "common.h"
+
+namespace cg {
+
+// one block per channel
+__global__ __launch_bounds__(256) void bn_finalize_kernel(const float* __restrict__ stats, long long nblk, int C,
+                                                          const float* gamma, const float* beta, float* rmean,
+                                                          float* rvar, long long* nbt, float momentum, float eps,
+                                                          float* scale_shift, float* mean_invstd) {
+  __shared__ double red[2][4];
+  __shared__ double sh_mean;
+  const int c = blockIdx.x, tid = threadIdx.x;
+  const long long stride = 2LL * C + 1;
+  double s = 0.0, n = 0.0;
+  for (long long b = tid; b < nblk; b += blockDim.x) {
+    s += stats[b * stride + c];
+    n += stats[b * stride + 2 * C];
+  }
+  s = wave_sum_d(s);
+  n = wave_sum_d(n);
+  if ((tid & 63) == 0) { red[0][tid >> 6] = s; red[1][tid >> 6] = n; }
+  __syncthreads();
+  const double S = red[0][0] + red[0][1] + red[0][2] + red[0][3];
+  const double N = red[1][0] + red[1][1] + red[1][2] + red[1][3];
+  const double mean = S / N;
+  __syncthreads();
+  double m2 = 0.0;
+  for (long long b = tid; b < nblk; b += blockDim.x) {
+    const double nb = stats[b * stride + 2 * C];
+    if (nb > 0) {
+      const double d = stats[b * stride + c] / nb - mean;
+      m2 += stats[b * stride + C + c] + nb * d * d;
+    }
+  }
+  m2 = wave_sum_d(m2);
+  if ((tid & 63) == 0) red[0][tid >> 6] = m2;
+  __syncthreads();
+  if (tid == 0) {
+    const double M2 = red[0][0] + red[0][1] + red[0][2] + red[0][3];
+    const double var = M2 / N;
+    const double invstd = 1.0 / sqrt(var + (double)eps);
+    const double sc = (double)gamma[c] * invstd;
+    scale_shift[c] = (float)sc;
+    scale_shift[C + c] = (float)((double)beta[c] - mean * sc);
+    mean_invstd[c] = (float)mean;
+    mean_invstd[C + c] = (float)invstd;
+    if (rmean) rmean[c] = (float)((1.0 - momentum) * rmean[c] + momentum * mean);
+    if (rvar) rvar[c] = (float)((1.0 - momentum) * rvar[c] + momentum * var * N / (N > 1 ? N - 1 : 1));
+    if (nbt && c == 0) *nbt += 1;
+  }
+  (void)sh_mean;
+}
+
+__device__ __forceinline__ float act_f(float v, int act, float slope) {
+  if (act == CGAN3D_ACT_RELU) return fmaxf(v, 0.f);
+  if (act == CGAN3D_ACT_LRELU) return v > 0.f ? v : v * slope;
+  return v;
+}
+
+__device__ __forceinline__ float act_grad(float pre, int act, float slope) {
+  if (act == CGAN3D_ACT_RELU) return pre > 0.f ? 1.f : 0.f;
+  if (act == CGAN3D_ACT_LRELU) return pre > 0.f ? 1.f : slope;
+  return 1.f;
+}
+
+// y = act(z*scale + shift) (+ residual); C % 4 == 0, float4 vectorised grid-stride
+__global__ __launch_bounds__(256) void bn_apply_kernel(const float* __restrict__ z, long long n4, int C,
+                                                       const float* __restrict__ ss, int act, float slope,
+                                                       const float* __restrict__ res, float* __restrict__ y) {
+  const int C4 = C >> 2;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (long long)gridDim.x * blockDim.x) {
+    const int c = (int)(i % C4) * 4;
+    f32x4 v = reinterpret_cast<const f32x4*>(z)[i];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[e] = act_f(v[e] * ss[c + e] + ss[C + c + e], act, slope);
+    if (res) v += reinterpret_cast<const f32x4*>(res)[i];
+    reinterpret_cast<f32x4*>(y)[i] = v;
+  }
+}
+
+// per-block partials of sum(dyh) and sum(dyh * xhat); 256 % C == 0 so each thread keeps one channel
+__global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const float* __restrict__ dy, const float* __restrict__ z,
+                                                            long long total, int C, const float* __restrict__ ss,
+                                                            const float* __restrict__ mi, int act, float slope,
+                                                            float* part) {
+  __shared__ float r0[256], r1[256];
+  const int tid = threadIdx.x;
+  const int c = tid % C;
+  const float sc = ss[c], sf = ss[C + c], mean = mi[c], inv = mi[C + c];
+  float a0 = 0.f, a1 = 0.f;
+  for (long long i = (long long)blockIdx.x * blockDim.x + tid; i < total; i += (long long)gridDim.x * blockDim.x) {
+    const float zz = z[i];
+    const float g = dy[i] * act_grad(zz * sc + sf, act, slope);
+    a0 += g;
+    a1 += g * (zz - mean) * inv;
+  }
+  r0[tid] = a0;
+  r1[tid] = a1;
+  __syncthreads();
+  if (tid < C) {
+    float s0 = 0.f, s1 = 0.f;
+    for (int k = tid; k < 256; k += C) { s0 += r0[k]; s1 += r1[k]; }
+    part[(long long)blockIdx.x * 2 * C + tid] = s0;
+    part[(long long)blockIdx.x * 2 * C + C + tid] = s1;
+  }
+}
+
+// fp64 combine of the partials -> dgamma, dbeta and the apply coefficients
+__global__ void bn_bwd_finalize_kernel(const float* __restrict__ part, int nblk, int C, long long nvox,
+                                       const float* __restrict__ gamma, const float* __restrict__ mi, float* dgamma,
+                                       float* dbeta, float* coef) {
+  const int c = threadIdx.x;
+  if (c >= C) return;
+  double s0 = 0.0, s1 = 0.0;
+  for (int b = 0; b < nblk; ++b) {
+    s0 += part[(long long)b * 2 * C + c];
+    s1 += part[(long long)b * 2 * C + C + c];
+  }
+  if (dbeta) dbeta[c] = (float)s0;
+  if (dgamma) dgamma[c] = (float)s1;
+  const float k1 = gamma[c] * mi[C + c];
+  coef[c] = k1;
+  coef[C + c] = (float)(s0 / (double)nvox);
+  coef[2 * C + c] = (float)(s1 / (double)nvox);
+}
+
+// dz = gamma*invstd*(dyh - mean(dyh) - xhat*mean(dyh*xhat))
+__global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const float* __restrict__ dy, const float* __restrict__ z,
+                                                           long long total, int C, const float* __restrict__ ss,
+                                                           const float* __restrict__ mi, int act, float slope,
+                                                           const float* __restrict__ coef, float* dz) {
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long long)gridDim.x * blockDim.x) {
+    const int c = (int)(i % C);
+    const float zz = z[i];
+    const float g = dy[i] * act_grad(zz * ss[c] + ss[C + c], act, slope);
+    const float xh = (zz - mi[c]) * mi[C + c];
+    dz[i] = coef[c] * (g - coef[C + c] - xh * coef[2 * C + c]);
+  }
+}
+
+__global__ __launch_bounds__(256) void channel_sum_kernel(const float* __restrict__ x, long long total, int C,
+                                                          float* part) {
+  __shared__ float r0[256];
+  const int tid = threadIdx.x;
+  float a0 = 0.f;
+  for (long long i = (long long)blockIdx.x * blockDim.x + tid; i < total; i += (long long)gridDim.x * blockDim.x)
+    a0 += x[i];
+  r0[tid] = a0;
+  __syncthreads();
+  if (tid < C) {
+    float s0 = 0.f;
+    for (int k = tid; k < 256; k += C) s0 += r0[k];
+    part[(long long)blockIdx.x * C + tid] = s0;
+  }
+}
+
+__global__ void channel_sum_finalize_kernel(const float* __restrict__ part, int nblk, int C, float* out) {
+  const int c = threadIdx.x;
+  if (c >= C) return;
+  double s = 0.0;
+  for (int b = 0; b < nblk; ++b) s += part[(long long)b * C + c];
+  out[c] = (float)s;
+}
+
+static int reduce_blocks(long long total) {
+  long long b = (total + 256 * 8 - 1) / (256 * 8);
+  if (b > 1024) b = 1024;
+  if (b < 1) b = 1;
+  return (int)b;
+}
+
+}  // namespace cg
+
+using namespace cg;
+
+extern "C" int cgan3d_bn_finalize(const float* stats, int64_t nblk, int32_t c, const float* gamma, const float* beta,
+                                  float* running_mean, float* running_var, int64_t* num_batches_tracked,
+                                  float momentum, float eps, float* scale_shift, float* mean_invstd, void* stream) {
+  CG_CHECK_ARG(stats && gamma && beta && scale_shift && mean_invstd, "cgan3d_bn_finalize: null pointer");
+  CG_CHECK_ARG(nblk > 0 && c > 0 && c <= 1024, "cgan3d_bn_finalize: bad sizes");
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3(c), dim3(256), 0, (hipStream_t)stream, stats, (long long)nblk, c, gamma,
+                     beta, running_mean, running_var, (long long*)num_batches_tracked, momentum, eps, scale_shift,
+                     mean_invstd);
+  CG_LAUNCH_CHECK("bn_finalize_kernel");
+  return CGAN3D_OK;
+}
+
+extern "C" int cgan3d_bn_apply(const float* z, int64_t nvox, int32_t c, const float* scale_shift, int32_t act,
+                               float slope, const float* residual, float* y, void* stream) {
+  CG_CHECK_ARG(z && scale_shift && y, "cgan3d_bn_apply: null pointer");
+  CG_CHECK_ARG(nvox > 0 && c > 0 && c % 4 == 0, "cgan3d_bn_apply: channels must be a multiple of 4");
+  const long long n4 = (long long)nvox * c / 4;
+  int blocks = (int)std::min<long long>((n4 + 255) / 256, 4096);
+  hipLaunchKernelGGL(bn_apply_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, z, n4, c, scale_shift, act,
+                     slope, residual, y);
+  CG_LAUNCH_CHECK("bn_apply_kernel");
+  return CGAN3D_OK;
+}
+
+extern "C" int64_t cgan3d_bn_backward_ws_floats(int64_t nvox, int32_t c) {
+  return (int64_t)reduce_blocks((long long)nvox * c) * 2 * c + 3 * c;
+}
+
+extern "C" int cgan3d_bn_backward(const float* dy, const float* z, int64_t nvox, int32_t c, const float* scale_shift,
+                                  const float* mean_invstd, const float* gamma, int32_t act, float slope, float* dgamma,
+                                  float* dbeta, float* dz, float* ws, void* stream) {
+  CG_CHECK_ARG(dy && z && scale_shift && mean_invstd && gamma && dz && ws, "cgan3d_bn_backward: null pointer");
+  CG_CHECK_ARG(nvox > 1 && c > 0 && c <= 256 && 256 % c == 0, "cgan3d_bn_backward: channels must divide 256");
+  hipStream_t s = (hipStream_t)stream;
+  const long long total = (long long)nvox * c;
+  const int nblk = reduce_blocks(total);
+  float* part = ws;
+  float* coef = ws + (long long)nblk * 2 * c;
+  hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(nblk), dim3(256), 0, s, dy, z, total, c, scale_shift, mean_invstd,
+                     act, slope, part);
+  CG_LAUNCH_CHECK("bn_bwd_reduce_kernel");
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(1), dim3(256), 0, s, part, nblk, c, (long long)nvox, gamma,
+                     mean_invstd, dgamma, dbeta, coef);
+  CG_LAUNCH_CHECK("bn_bwd_finalize_kernel");
+  int blocks = (int)std::min<long long>((total + 255) / 256, 4096);
+  hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(blocks), dim3(256), 0, s, dy, z, total, c, scale_shift, mean_invstd,
+                     act, slope, coef, dz);
+  CG_LAUNCH_CHECK("bn_bwd_apply_kernel");
+  return CGAN3D_OK;
+}
+
+extern "C" int64_t cgan3d_channel_sum_ws_floats(int64_t nvox, int32_t c) {
+  return (int64_t)reduce_blocks((long long)nvox * c) * c;
+}
+
+extern "C" int cgan3d_channel_sum(const float* x, int64_t nvox, int32_t c, float* out, float* ws, void* stream) {
+  CG_CHECK_ARG(x && out && ws, "cgan3d_channel_sum: null pointer");
+  CG_CHECK_ARG(nvox > 0 && c > 0 && c <= 256 && 256 % c == 0, "cgan3d_channel_sum: channels must divide 256");
+  hipStream_t s = (hipStream_t)stream;
+  const long long total = (long long)nvox * c;
+  const int nblk = reduce_blocks(total);
+  hipLaunchKernelGGL(channel_sum_kernel, dim3(nblk), dim3(256), 0, s, x, total, c, ws);
+  CG_LAUNCH_CHECK("channel_sum_kernel");
+  hipLaunchKernelGGL(channel_sum_finalize_kernel, dim3(1), dim3(256), 0, s, ws, nblk, c, out);
+  CG_LAUNCH_CHECK("channel_sum_finalize_kernel");
+  return CGAN3D_OK;
+}

@@ -1,0 +1,58 @@
+// Shared helpers for the cgan3d HIP library (gfx950 / CDNA4 only).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdint>
+#include <cstdio>
+
+#include "../../include/cgan3d.h"
+
+namespace cg {
+
+// last-error slot, per host thread (the C-ABI is callable from any thread)
+void set_error(const char* fmt, ...);
+
+#define CG_CHECK_ARG(cond, ...)          \
+  do {                                   \
+    if (!(cond)) {                       \
+      ::cg::set_error(__VA_ARGS__);      \
+      return CGAN3D_EINVAL;              \
+    }                                    \
+  } while (0)
+
+#define CG_LAUNCH_CHECK(what)                                                   \
+  do {                                                                          \
+    hipError_t e_ = hipGetLastError();                                          \
+    if (e_ != hipSuccess) {                                                     \
+      ::cg::set_error("%s: launch failed: %s", what, hipGetErrorString(e_));   \
+      return CGAN3D_EHIP;                                                       \
+    }                                                                           \
+  } while (0)
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int kWave = 64;
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+__device__ __forceinline__ double wave_sum_d(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// reflect index into [0, n) without edge repeat (torch "reflect"), valid for |overhang| < n
+__device__ __forceinline__ int reflect_idx(int i, int n) {
+  i = i < 0 ? -i : i;
+  return i >= n ? 2 * (n - 1) - i : i;
+}
+
+inline int ceil_div(long long a, long long b) { return (int)((a + b - 1) / b); }
+
+}  // namespace cg

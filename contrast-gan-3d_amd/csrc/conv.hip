@@ -1,0 +1,690 @@
+// Implicit-GEMM 3-D convolutions for gfx950 (fp32, exact-f32 MFMA v_mfma_f32_16x16x4_f32).
+//
+// Replaces the aten convolution / convolution_backward calls the reference's hot path makes:
+// Conv3d and ConvTranspose3d in ConvBlock (contrast_gan_3D/model/blocks.py:29-38), the
+// generator's reflect-padded k7 first/last convs (model/generator.py:31-35,78-84) and the
+// critic's k4 s2 pyramid (model/discriminator.py:24-80), forward, input-grad and weight-grad.
+//
+// One gather formulation covers every case (see include/cgan3d.h): a tap t links output
+// voxel o and gathered voxel i either as i = o*s - p + t ("forward") or o = i*s - p + t
+// ("transposed").  Transposed launches are split into s^3 parity classes so every voxel of a
+// 64-voxel tile has the same valid tap list (no wasted MFMA work on the 7/8 invalid taps of a
+// stride-2 ConvTranspose3d).  The reduction index K = (valid tap, channel) is walked in chunks
+// of 32 staged through LDS; each wave owns 16 output voxels x up to 64 output channels.
+#include "common.h"
+
+namespace cg {
+
+struct ConvArgs {
+  int n, di, hi, wi, do_, ho, wo, cin, cout, k, s, p, transposed, reflect;
+  long long sa, sb;
+  int cd, ch, cw;          // grid walked by the tiles: output grid, or one parity class
+  long long class_vox;     // voxels per class (or all output voxels)
+  int tiles_per_class;
+  int nclass;
+};
+
+struct Epi {
+  const float* bias;
+  const float* residual;
+  const float* mask_src;
+  const float* minuend;
+  float* out2;
+  float* stats;
+  int act;
+  float slope;
+};
+
+static bool make_args(const cgan3d_conv_geom* g, ConvArgs* a, int bm) {
+  a->n = g->n; a->di = g->di; a->hi = g->hi; a->wi = g->wi;
+  a->do_ = g->do_; a->ho = g->ho; a->wo = g->wo; a->cin = g->cin; a->cout = g->cout;
+  a->k = g->k; a->s = g->stride; a->p = g->pad; a->transposed = g->transposed; a->reflect = g->reflect;
+  a->sa = g->w_sa; a->sb = g->w_sb;
+  if (g->transposed && g->stride > 1) {
+    if (g->do_ % g->stride || g->ho % g->stride || g->wo % g->stride) return false;
+    a->cd = g->do_ / g->stride; a->ch = g->ho / g->stride; a->cw = g->wo / g->stride;
+    a->nclass = g->stride * g->stride * g->stride;
+  } else {
+    a->cd = g->do_; a->ch = g->ho; a->cw = g->wo; a->nclass = 1;
+  }
+  a->class_vox = (long long)g->n * a->cd * a->ch * a->cw;
+  a->tiles_per_class = (int)((a->class_vox + bm - 1) / bm);
+  return true;
+}
+
+static int validate(const cgan3d_conv_geom* g, const char* who) {
+  CG_CHECK_ARG(g != nullptr, "%s: null geometry", who);
+  CG_CHECK_ARG(g->n > 0 && g->di > 0 && g->hi > 0 && g->wi > 0 && g->do_ > 0 && g->ho > 0 && g->wo > 0,
+               "%s: non-positive dims", who);
+  CG_CHECK_ARG(g->cin > 0 && g->cout > 0 && g->cout <= 64, "%s: channels cin=%d cout=%d (cout<=64)", who,
+               g->cin, g->cout);
+  CG_CHECK_ARG(g->k > 0 && g->k <= 7 && g->stride >= 1 && g->stride <= 2 && g->pad >= 0 && g->pad < g->k,
+               "%s: kernel k=%d s=%d p=%d unsupported", who, g->k, g->stride, g->pad);
+  CG_CHECK_ARG(!(g->reflect && g->transposed), "%s: reflect padding only in forward mapping", who);
+  CG_CHECK_ARG(!g->reflect || (g->pad < g->di && g->pad < g->hi && g->pad < g->wi),
+               "%s: reflect pad %d >= dim", who, g->pad);
+  if (!g->transposed) {
+    CG_CHECK_ARG((long long)(g->do_ - 1) * g->stride - g->pad + g->k - 1 < (long long)g->di + g->pad &&
+                 (long long)(g->ho - 1) * g->stride - g->pad + g->k - 1 < (long long)g->hi + g->pad &&
+                 (long long)(g->wo - 1) * g->stride - g->pad + g->k - 1 < (long long)g->wi + g->pad,
+                 "%s: output dims exceed padded input", who);
+  }
+  CG_CHECK_ARG((long long)g->n * g->do_ * g->ho * g->wo < (1LL << 31) &&
+               (long long)g->n * g->di * g->hi * g->wi < (1LL << 31), "%s: voxel count exceeds int32", who);
+  return CGAN3D_OK;
+}
+
+// Per-dimension valid tap list of a parity class: taps t = first + step*m, m < count.
+__device__ __forceinline__ void class_taps(int r, int k, int s, int p, int transposed, int* first, int* step,
+                                           int* count) {
+  if (transposed) {
+    int f = (r + p) % s;
+    *first = f;
+    *step = s;
+    *count = f < k ? (k - f + s - 1) / s : 0;
+  } else {
+    *first = 0;
+    *step = 1;
+    *count = k;
+  }
+}
+
+// gathered coordinate along one dim (returns -1 when the tap contributes zero)
+__device__ __forceinline__ int gcoord(int base, int off, int n, int reflect) {
+  int i = base + off;
+  if (reflect) return reflect_idx(i, n);
+  return (i >= 0 && i < n) ? i : -1;
+}
+
+// ------------------------------------------------------------------------------------------
+// Forward / input-grad kernel (cout >= 2).  VEC = 4 when cin % 4 == 0, else 1.  NB = ceil(cout/16).
+template <int VEC, int NB>
+__global__ __launch_bounds__(256) void conv_mfma_kernel(ConvArgs a, const float* __restrict__ x,
+                                                        const float* __restrict__ w, float* y, Epi ep) {
+  constexpr int BM = 64, KC = 32, LD = KC + 4;
+  __shared__ __attribute__((aligned(16))) float As[BM * LD];
+  __shared__ __attribute__((aligned(16))) float Bs[64 * LD];
+  __shared__ int row_n[BM], row_b[3][BM], row_out[BM];
+  __shared__ int tab_off[3][KC], tab_ci[KC], tab_t[KC];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int cls = blockIdx.x / a.tiles_per_class;
+  const int tile = blockIdx.x - cls * a.tiles_per_class;
+  const int s = a.s, k = a.k, p = a.p;
+  int rd = 0, rh = 0, rw = 0;
+  if (a.transposed) { rd = cls / (s * s); rh = (cls / s) % s; rw = cls % s; }
+  int fd, sd, nd, fh, sh, nh, fw, sw, nw;
+  class_taps(rd, k, s, p, a.transposed, &fd, &sd, &nd);
+  class_taps(rh, k, s, p, a.transposed, &fh, &sh, &nh);
+  class_taps(rw, k, s, p, a.transposed, &fw, &sw, &nw);
+  const int KT = nd * nh * nw * a.cin;
+  const long long v0 = (long long)tile * BM;
+
+  if (tid < BM) {
+    long long lin = v0 + tid;
+    if (lin < a.class_vox) {
+      int jw = (int)(lin % a.cw); long long t = lin / a.cw;
+      int jh = (int)(t % a.ch); t /= a.ch;
+      int jd = (int)(t % a.cd); int nb = (int)(t / a.cd);
+      int od, oh, ow;
+      if (a.transposed) {
+        od = jd * s + rd; oh = jh * s + rh; ow = jw * s + rw;
+        row_b[0][tid] = jd; row_b[1][tid] = jh; row_b[2][tid] = jw;
+      } else {
+        od = jd; oh = jh; ow = jw;
+        row_b[0][tid] = jd * s - p; row_b[1][tid] = jh * s - p; row_b[2][tid] = jw * s - p;
+      }
+      row_n[tid] = nb * a.di;
+      row_out[tid] = ((nb * a.do_ + od) * a.ho + oh) * a.wo + ow;
+    } else {
+      row_n[tid] = -1; row_out[tid] = -1;
+      row_b[0][tid] = row_b[1][tid] = row_b[2][tid] = 0;
+    }
+  }
+  __syncthreads();
+
+  f32x4 acc[NB];
+#pragma unroll
+  for (int n = 0; n < NB; ++n) acc[n] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int g = lane >> 4, r16 = lane & 15;
+  for (int kc0 = 0; kc0 < KT; kc0 += KC) {
+    if (tid < KC) {
+      int kk = kc0 + tid;
+      if (kk < KT) {
+        int j = kk / a.cin, ci = kk - j * a.cin;
+        int mw = j % nw; j /= nw;
+        int mh = j % nh, md = j / nh;
+        int td = fd + sd * md, th = fh + sh * mh, tw = fw + sw * mw;
+        if (a.transposed) {
+          tab_off[0][tid] = (rd + p - td) / s; tab_off[1][tid] = (rh + p - th) / s; tab_off[2][tid] = (rw + p - tw) / s;
+        } else {
+          tab_off[0][tid] = td; tab_off[1][tid] = th; tab_off[2][tid] = tw;
+        }
+        tab_ci[tid] = ci;
+        tab_t[tid] = (td * k + th) * k + tw;
+      } else {
+        tab_t[tid] = -1; tab_ci[tid] = 0;
+        tab_off[0][tid] = tab_off[1][tid] = tab_off[2][tid] = 0;
+      }
+    }
+    __syncthreads();
+    // A tile: gathered activations [64 voxels][32 k]
+    if (VEC == 4) {
+      const int e0 = (tid & 7) * 4;
+      const int tl = tab_t[e0];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int r = (tid >> 3) + 32 * i;
+        f32x4 v = {0.f, 0.f, 0.f, 0.f};
+        const int nb = row_n[r];
+        if (nb >= 0 && tl >= 0) {
+          int id = gcoord(row_b[0][r], tab_off[0][e0], a.di, a.reflect);
+          int ih = gcoord(row_b[1][r], tab_off[1][e0], a.hi, a.reflect);
+          int iw = gcoord(row_b[2][r], tab_off[2][e0], a.wi, a.reflect);
+          if ((id | ih | iw) >= 0) {
+            long long off = ((long long)((nb + id) * a.hi + ih) * a.wi + iw) * a.cin + tab_ci[e0];
+            v = *reinterpret_cast<const f32x4*>(x + off);
+          }
+        }
+        *reinterpret_cast<f32x4*>(&As[r * LD + e0]) = v;
+      }
+    } else {
+      const int e = tid & 31;
+      const int tl = tab_t[e];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int r = (tid >> 5) + 8 * i;
+        float v = 0.f;
+        const int nb = row_n[r];
+        if (nb >= 0 && tl >= 0) {
+          int id = gcoord(row_b[0][r], tab_off[0][e], a.di, a.reflect);
+          int ih = gcoord(row_b[1][r], tab_off[1][e], a.hi, a.reflect);
+          int iw = gcoord(row_b[2][r], tab_off[2][e], a.wi, a.reflect);
+          if ((id | ih | iw) >= 0)
+            v = x[((long long)((nb + id) * a.hi + ih) * a.wi + iw) * a.cin + tab_ci[e]];
+        }
+        As[r * LD + e] = v;
+      }
+    }
+    // B tile: weights [64 out channels][32 k]
+    {
+      const int co = tid >> 2;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int e = (tid & 3) * 8 + i;
+        const int tl = tab_t[e];
+        float v = 0.f;
+        if (co < a.cout && tl >= 0) v = w[(long long)tab_ci[e] * a.sa + (long long)co * a.sb + tl];
+        Bs[co * LD + e] = v;
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < KC / 16; ++q) {
+      const f32x4 av = *reinterpret_cast<const f32x4*>(&As[(wave * 16 + r16) * LD + 16 * q + 4 * g]);
+#pragma unroll
+      for (int n = 0; n < NB; ++n) {
+        const f32x4 bv = *reinterpret_cast<const f32x4*>(&Bs[(16 * n + r16) * LD + 16 * q + 4 * g]);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) acc[n] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[e], bv[e], acc[n], 0, 0, 0);
+      }
+    }
+    __syncthreads();
+  }
+
+  // epilogue: lane holds rows 4g..4g+3 (of the wave's 16) for channel 16n + r16
+  float vals[NB][4];
+  bool rowv[4];
+  int rowo[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    rowo[j] = row_out[wave * 16 + 4 * g + j];
+    rowv[j] = rowo[j] >= 0;
+  }
+#pragma unroll
+  for (int n = 0; n < NB; ++n) {
+    const int c = 16 * n + r16;
+    const bool cv = c < a.cout;
+    const float b = (ep.bias && cv) ? ep.bias[c] : 0.f;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float v = acc[n][j] + b;
+      if (ep.act == CGAN3D_ACT_RELU) v = fmaxf(v, 0.f);
+      else if (ep.act == CGAN3D_ACT_LRELU) v = v > 0.f ? v : v * ep.slope;
+      else if (ep.act == CGAN3D_ACT_TANH) v = tanhf(v);
+      if (rowv[j] && cv) {
+        const long long o = (long long)rowo[j] * a.cout + c;
+        if (ep.mask_src) v = ep.mask_src[o] > 0.f ? v : v * ep.slope;
+        if (ep.residual) v += ep.residual[o];
+        y[o] = v;
+      }
+      vals[n][j] = (rowv[j] && cv) ? v : 0.f;
+    }
+  }
+
+  if (ep.stats) {
+    // per-block BatchNorm partials: (sum, M2 about the block mean, count)
+    float* red = As;  // reuse LDS: [4 waves][64 channels]
+    __shared__ float bmean[64];
+    int cnt = 0;
+    for (int r = 0; r < BM; ++r) cnt += row_out[r] >= 0;
+#pragma unroll
+    for (int n = 0; n < NB; ++n) {
+      float sum = vals[n][0] + vals[n][1] + vals[n][2] + vals[n][3];
+      sum += __shfl_xor(sum, 16, 64);
+      sum += __shfl_xor(sum, 32, 64);
+      if (g == 0) red[wave * 64 + 16 * n + r16] = sum;
+    }
+    __syncthreads();
+    if (tid < a.cout) {
+      float S = red[tid] + red[64 + tid] + red[128 + tid] + red[192 + tid];
+      bmean[tid] = cnt ? S / cnt : 0.f;
+      ep.stats[(long long)blockIdx.x * (2 * a.cout + 1) + tid] = S;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int n = 0; n < NB; ++n) {
+      const int c = 16 * n + r16;
+      const float m = c < a.cout ? bmean[c] : 0.f;
+      float q = 0.f;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        float d = (rowv[j] && c < a.cout) ? vals[n][j] - m : 0.f;
+        q += d * d;
+      }
+      q += __shfl_xor(q, 16, 64);
+      q += __shfl_xor(q, 32, 64);
+      if (g == 0) red[wave * 64 + 16 * n + r16] = q;
+    }
+    __syncthreads();
+    if (tid < a.cout) {
+      float M2 = red[tid] + red[64 + tid] + red[128 + tid] + red[192 + tid];
+      ep.stats[(long long)blockIdx.x * (2 * a.cout + 1) + a.cout + tid] = M2;
+    }
+    if (tid == 0) ep.stats[(long long)blockIdx.x * (2 * a.cout + 1) + 2 * a.cout] = (float)cnt;
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// cout == 1 forward / input-grad (VALU): one thread per output voxel, weights in LDS.
+// Used by the generator's last conv (16 -> 1, k7 reflect, + bias, tanh, opt_hat = subopt - .)
+// and the critic's first-layer input-grad and last layer.
+__global__ __launch_bounds__(256) void conv_cout1_kernel(ConvArgs a, const float* __restrict__ x,
+                                                         const float* __restrict__ w, float* y, Epi ep) {
+  extern __shared__ __attribute__((aligned(16))) float Ws[];  // [T][cin]
+  const int T = a.k * a.k * a.k;
+  for (int i = threadIdx.x; i < T * a.cin; i += blockDim.x) {
+    int t = i / a.cin, ci = i - t * a.cin;
+    Ws[i] = w[(long long)ci * a.sa + t];
+  }
+  __syncthreads();
+  const int cls = blockIdx.x / a.tiles_per_class;
+  const int tile = blockIdx.x - cls * a.tiles_per_class;
+  const long long lin = (long long)tile * blockDim.x + threadIdx.x;
+  if (lin >= a.class_vox) return;
+  const int s = a.s, k = a.k, p = a.p;
+  int rd = 0, rh = 0, rw = 0;
+  if (a.transposed) { rd = cls / (s * s); rh = (cls / s) % s; rw = cls % s; }
+  int fd, sd, nd, fh, sh, nh, fw, sw, nw;
+  class_taps(rd, k, s, p, a.transposed, &fd, &sd, &nd);
+  class_taps(rh, k, s, p, a.transposed, &fh, &sh, &nh);
+  class_taps(rw, k, s, p, a.transposed, &fw, &sw, &nw);
+  int jw = (int)(lin % a.cw); long long tt = lin / a.cw;
+  int jh = (int)(tt % a.ch); tt /= a.ch;
+  int jd = (int)(tt % a.cd); int nb = (int)(tt / a.cd);
+  int od, oh, ow, bd, bh, bw;
+  if (a.transposed) { od = jd * s + rd; oh = jh * s + rh; ow = jw * s + rw; bd = jd; bh = jh; bw = jw; }
+  else { od = jd; oh = jh; ow = jw; bd = jd * s - p; bh = jh * s - p; bw = jw * s - p; }
+  float acc = 0.f;
+  for (int md = 0; md < nd; ++md) {
+    const int td = fd + sd * md;
+    const int id = gcoord(bd, a.transposed ? (rd + p - td) / s : td, a.di, a.reflect);
+    if (id < 0) continue;
+    for (int mh = 0; mh < nh; ++mh) {
+      const int th = fh + sh * mh;
+      const int ih = gcoord(bh, a.transposed ? (rh + p - th) / s : th, a.hi, a.reflect);
+      if (ih < 0) continue;
+      for (int mw = 0; mw < nw; ++mw) {
+        const int tw = fw + sw * mw;
+        const int iw = gcoord(bw, a.transposed ? (rw + p - tw) / s : tw, a.wi, a.reflect);
+        if (iw < 0) continue;
+        const float* xp = x + ((long long)((nb * a.di + id) * a.hi + ih) * a.wi + iw) * a.cin;
+        const float* wp = Ws + ((td * k + th) * k + tw) * a.cin;
+        if ((a.cin & 3) == 0) {
+          for (int ci = 0; ci < a.cin; ci += 4) {
+            f32x4 xv = *reinterpret_cast<const f32x4*>(xp + ci);
+            f32x4 wv = *reinterpret_cast<const f32x4*>(wp + ci);
+            acc += xv[0] * wv[0] + xv[1] * wv[1] + xv[2] * wv[2] + xv[3] * wv[3];
+          }
+        } else {
+          for (int ci = 0; ci < a.cin; ++ci) acc += xp[ci] * wp[ci];
+        }
+      }
+    }
+  }
+  float v = acc + (ep.bias ? ep.bias[0] : 0.f);
+  if (ep.act == CGAN3D_ACT_RELU) v = fmaxf(v, 0.f);
+  else if (ep.act == CGAN3D_ACT_LRELU) v = v > 0.f ? v : v * ep.slope;
+  else if (ep.act == CGAN3D_ACT_TANH) v = tanhf(v);
+  const long long o = ((long long)(nb * a.do_ + od) * a.ho + oh) * a.wo + ow;
+  if (ep.mask_src) v = ep.mask_src[o] > 0.f ? v : v * ep.slope;
+  if (ep.residual) v += ep.residual[o];
+  y[o] = v;
+  if (ep.out2) ep.out2[o] = ep.minuend[o] - v;
+}
+
+// ------------------------------------------------------------------------------------------
+// Weight gradient (cout >= 2): dwp[(t*cin + a)*cout + b] += sum_o gathered(o, t, a) * aligned(o, b)
+// Forward mapping i = o*s - p + t (reflect optional).  Block = 64 (t,a) rows x all cout columns
+// over a chunk of output voxels; 32 voxels per LDS stage.
+template <int VEC, int NB>
+__global__ __launch_bounds__(256) void conv_wgrad_kernel(ConvArgs a, const float* __restrict__ gx,
+                                                         const float* __restrict__ go, float* dwp, long long vpb) {
+  constexpr int KV = 32, LD = 80;
+  __shared__ __attribute__((aligned(16))) float As[KV * LD];  // [voxel][r]
+  __shared__ __attribute__((aligned(16))) float Gs[KV * LD];  // [voxel][b]
+  __shared__ int rtab[4][64];                                  // td, th, tw, a   (td = -1: pad row)
+  __shared__ int vtab[5][KV];                                  // n*di, bd, bh, bw, aligned voxel
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int R = a.k * a.k * a.k * a.cin;
+  const int r0 = blockIdx.x * 64;
+  if (tid < 64) {
+    int r = r0 + tid;
+    if (r < R) {
+      int t = r / a.cin, ci = r - t * a.cin;
+      rtab[0][tid] = t / (a.k * a.k); rtab[1][tid] = (t / a.k) % a.k; rtab[2][tid] = t % a.k; rtab[3][tid] = ci;
+    } else {
+      rtab[0][tid] = -1; rtab[1][tid] = rtab[2][tid] = rtab[3][tid] = 0;
+    }
+  }
+  const long long V = (long long)a.n * a.do_ * a.ho * a.wo;
+  const long long vbeg = (long long)blockIdx.y * vpb;
+  const long long vend = vbeg + vpb < V ? vbeg + vpb : V;
+
+  f32x4 acc[NB];
+#pragma unroll
+  for (int n = 0; n < NB; ++n) acc[n] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int g = lane >> 4, r16 = lane & 15;
+
+  for (long long vb = vbeg; vb < vend; vb += KV) {
+    if (tid < KV) {
+      long long lin = vb + tid;
+      if (lin < vend) {
+        int ow = (int)(lin % a.wo); long long t = lin / a.wo;
+        int oh = (int)(t % a.ho); t /= a.ho;
+        int od = (int)(t % a.do_); int nb = (int)(t / a.do_);
+        vtab[0][tid] = nb * a.di; vtab[1][tid] = od * a.s - a.p; vtab[2][tid] = oh * a.s - a.p;
+        vtab[3][tid] = ow * a.s - a.p; vtab[4][tid] = (int)lin;
+      } else {
+        vtab[0][tid] = -1; vtab[4][tid] = -1;
+      }
+    }
+    __syncthreads();
+    if (VEC == 4) {
+      const int r4 = tid & 15;
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int v = (tid >> 4) + 16 * i;
+        f32x4 val = {0.f, 0.f, 0.f, 0.f};
+        const int nb = vtab[0][v], rr = 4 * r4;
+        if (nb >= 0 && rtab[0][rr] >= 0) {
+          int id = gcoord(vtab[1][v], rtab[0][rr], a.di, a.reflect);
+          int ih = gcoord(vtab[2][v], rtab[1][rr], a.hi, a.reflect);
+          int iw = gcoord(vtab[3][v], rtab[2][rr], a.wi, a.reflect);
+          if ((id | ih | iw) >= 0)
+            val = *reinterpret_cast<const f32x4*>(gx + ((long long)((nb + id) * a.hi + ih) * a.wi + iw) * a.cin + rtab[3][rr]);
+        }
+        *reinterpret_cast<f32x4*>(&As[v * LD + rr]) = val;
+      }
+    } else {
+      const int rr = tid & 63;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int v = (tid >> 6) + 4 * i;
+        float val = 0.f;
+        const int nb = vtab[0][v];
+        if (nb >= 0 && rtab[0][rr] >= 0) {
+          int id = gcoord(vtab[1][v], rtab[0][rr], a.di, a.reflect);
+          int ih = gcoord(vtab[2][v], rtab[1][rr], a.hi, a.reflect);
+          int iw = gcoord(vtab[3][v], rtab[2][rr], a.wi, a.reflect);
+          if ((id | ih | iw) >= 0) val = gx[((long long)((nb + id) * a.hi + ih) * a.wi + iw) * a.cin + rtab[3][rr]];
+        }
+        As[v * LD + rr] = val;
+      }
+    }
+    {
+      const int c4 = tid & 15;
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int v = (tid >> 4) + 16 * i;
+        f32x4 val = {0.f, 0.f, 0.f, 0.f};
+        const int ov = vtab[4][v];
+        if (ov >= 0 && 4 * c4 < a.cout) val = *reinterpret_cast<const f32x4*>(go + (long long)ov * a.cout + 4 * c4);
+        *reinterpret_cast<f32x4*>(&Gs[v * LD + 4 * c4]) = val;
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int kk = 0; kk < KV; kk += 4) {
+      const float av = As[(kk + g) * LD + 16 * wave + r16];
+#pragma unroll
+      for (int n = 0; n < NB; ++n) {
+        const float bv = Gs[(kk + g) * LD + 16 * n + r16];
+        acc[n] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, acc[n], 0, 0, 0);
+      }
+    }
+    __syncthreads();
+  }
+  // D[row = 4g + j][col = r16]: row -> r = r0 + 16*wave + 4g + j, col -> b = 16n + r16
+#pragma unroll
+  for (int n = 0; n < NB; ++n) {
+    const int b = 16 * n + r16;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int r = r0 + 16 * wave + 4 * g + j;
+      if (r < R && b < a.cout) atomicAdd(dwp + (long long)r * a.cout + b, acc[n][j]);
+    }
+  }
+}
+
+// cout == 1 weight gradient (VALU): dwp[t*cin + a] += sum_o gathered(o,t,a) * aligned(o)
+template <int MAXJ>
+__global__ __launch_bounds__(256) void conv_wgrad_cout1_kernel(ConvArgs a, const float* __restrict__ gx,
+                                                               const float* __restrict__ go, float* dwp,
+                                                               long long vpb) {
+  constexpr int VB = 64;
+  __shared__ int vtab[5][VB];
+  __shared__ float gv[VB];
+  const int tid = threadIdx.x;
+  const int R4 = a.k * a.k * a.k * a.cin / 4;
+  int td[MAXJ], th[MAXJ], tw[MAXJ], ca[MAXJ];
+  f32x4 acc[MAXJ];
+#pragma unroll
+  for (int j = 0; j < MAXJ; ++j) {
+    int r4 = tid + 256 * j;
+    acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (r4 < R4) {
+      int r = 4 * r4, t = r / a.cin;
+      ca[j] = r - t * a.cin; td[j] = t / (a.k * a.k); th[j] = (t / a.k) % a.k; tw[j] = t % a.k;
+    } else {
+      td[j] = -1; th[j] = tw[j] = ca[j] = 0;
+    }
+  }
+  const long long V = (long long)a.n * a.do_ * a.ho * a.wo;
+  const long long vbeg = (long long)blockIdx.x * vpb;
+  const long long vend = vbeg + vpb < V ? vbeg + vpb : V;
+  for (long long vb = vbeg; vb < vend; vb += VB) {
+    __syncthreads();
+    if (tid < VB) {
+      long long lin = vb + tid;
+      if (lin < vend) {
+        int ow = (int)(lin % a.wo); long long t = lin / a.wo;
+        int oh = (int)(t % a.ho); t /= a.ho;
+        int od = (int)(t % a.do_); int nb = (int)(t / a.do_);
+        vtab[0][tid] = nb * a.di; vtab[1][tid] = od * a.s - a.p; vtab[2][tid] = oh * a.s - a.p;
+        vtab[3][tid] = ow * a.s - a.p;
+        gv[tid] = go[lin];
+      } else {
+        vtab[0][tid] = -1; gv[tid] = 0.f;
+      }
+    }
+    __syncthreads();
+    const int nv = (int)((vend - vb) < VB ? (vend - vb) : VB);
+    for (int v = 0; v < nv; ++v) {
+      const int nb = vtab[0][v];
+      const float gval = gv[v];
+      const int bd = vtab[1][v], bh = vtab[2][v], bw = vtab[3][v];
+#pragma unroll
+      for (int j = 0; j < MAXJ; ++j) {
+        if (td[j] < 0) continue;
+        int id = gcoord(bd, td[j], a.di, a.reflect);
+        int ih = gcoord(bh, th[j], a.hi, a.reflect);
+        int iw = gcoord(bw, tw[j], a.wi, a.reflect);
+        if ((id | ih | iw) >= 0) {
+          f32x4 xv = *reinterpret_cast<const f32x4*>(gx + ((long long)((nb + id) * a.hi + ih) * a.wi + iw) * a.cin + ca[j]);
+          acc[j] += xv * gval;
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < MAXJ; ++j) {
+    if (td[j] < 0) continue;
+    int r = 4 * (tid + 256 * j);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) atomicAdd(dwp + r + e, acc[j][e]);
+  }
+}
+
+// dw[a*sa + b*sb + t] (+)= dwp[(t*cin + a)*cout + b]
+__global__ void wgrad_unpack_kernel(const float* __restrict__ dwp, float* dw, int T, int cin, int cout, long long sa,
+                                    long long sb, int accumulate) {
+  long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  long long total = (long long)T * cin * cout;
+  if (i >= total) return;
+  int b = (int)(i % cout); long long r = i / cout;
+  int ca = (int)(r % cin); int t = (int)(r / cin);
+  float* d = dw + ca * sa + b * sb + t;
+  *d = accumulate ? *d + dwp[i] : dwp[i];
+}
+
+}  // namespace cg
+
+using namespace cg;
+
+static Epi to_epi(const cgan3d_epilogue* ep) {
+  Epi e{};
+  if (ep) {
+    e.bias = ep->bias; e.residual = ep->residual; e.mask_src = ep->mask_src; e.minuend = ep->minuend;
+    e.out2 = ep->out2; e.stats = ep->stats; e.act = ep->act; e.slope = ep->slope;
+  }
+  return e;
+}
+
+extern "C" int64_t cgan3d_conv3d_stats_floats(const cgan3d_conv_geom* g) {
+  ConvArgs a;
+  if (!g || !make_args(g, &a, 64)) return -1;
+  return (int64_t)a.nclass * a.tiles_per_class * (2 * g->cout + 1);
+}
+
+extern "C" int cgan3d_conv3d_fwd(const cgan3d_conv_geom* g, const float* x, const float* w, float* y,
+                                 const cgan3d_epilogue* ep, void* stream) {
+  int st = validate(g, "cgan3d_conv3d_fwd");
+  if (st) return st;
+  CG_CHECK_ARG(x && w && y, "cgan3d_conv3d_fwd: null pointer");
+  Epi e = to_epi(ep);
+  CG_CHECK_ARG(!(e.out2 && (!e.minuend || g->cout != 1)), "cgan3d_conv3d_fwd: out2 needs minuend and cout==1");
+  hipStream_t s = (hipStream_t)stream;
+  if (g->cout == 1) {
+    CG_CHECK_ARG(!e.stats, "cgan3d_conv3d_fwd: stats unsupported for cout==1");
+    ConvArgs a;
+    CG_CHECK_ARG(make_args(g, &a, 256), "cgan3d_conv3d_fwd: transposed output dims must divide stride");
+    size_t lds = (size_t)g->k * g->k * g->k * g->cin * sizeof(float);
+    CG_CHECK_ARG(lds <= 64 * 1024, "cgan3d_conv3d_fwd: cout==1 weights exceed LDS");
+    hipLaunchKernelGGL(conv_cout1_kernel, dim3(a.nclass * a.tiles_per_class), dim3(256), lds, s, a, x, w, y, e);
+    CG_LAUNCH_CHECK("conv_cout1_kernel");
+    return CGAN3D_OK;
+  }
+  ConvArgs a;
+  CG_CHECK_ARG(make_args(g, &a, 64), "cgan3d_conv3d_fwd: transposed output dims must divide stride");
+  dim3 grid(a.nclass * a.tiles_per_class);
+  const int nb = (g->cout + 15) / 16;
+  const bool v4 = (g->cin % 4) == 0;
+#define CG_LAUNCH_FWD(V, N) hipLaunchKernelGGL((conv_mfma_kernel<V, N>), grid, dim3(256), 0, s, a, x, w, y, e)
+  if (v4) {
+    if (nb == 1) CG_LAUNCH_FWD(4, 1); else if (nb == 2) CG_LAUNCH_FWD(4, 2); else if (nb == 3) CG_LAUNCH_FWD(4, 3); else CG_LAUNCH_FWD(4, 4);
+  } else {
+    if (nb == 1) CG_LAUNCH_FWD(1, 1); else if (nb == 2) CG_LAUNCH_FWD(1, 2); else if (nb == 3) CG_LAUNCH_FWD(1, 3); else CG_LAUNCH_FWD(1, 4);
+  }
+#undef CG_LAUNCH_FWD
+  CG_LAUNCH_CHECK("conv_mfma_kernel");
+  return CGAN3D_OK;
+}
+
+static long long wgrad_vpb(long long V, int gx_blocks) {
+  // enough blocks to fill the chip (>= ~1024), but >= 256 voxels per block to bound atomics
+  long long target = 2048 / (gx_blocks > 0 ? gx_blocks : 1);
+  if (target < 1) target = 1;
+  long long vpb = (V + target - 1) / target;
+  if (vpb < 256) vpb = 256;
+  return (vpb + 63) / 64 * 64;
+}
+
+extern "C" int64_t cgan3d_conv3d_wgrad_ws_floats(const cgan3d_conv_geom* g) {
+  if (!g) return -1;
+  return (int64_t)g->k * g->k * g->k * g->cin * g->cout;
+}
+
+extern "C" int cgan3d_conv3d_wgrad(const cgan3d_conv_geom* g, const float* gathered, const float* aligned, float* dw,
+                                   int32_t accumulate, float* ws, void* stream) {
+  int st = validate(g, "cgan3d_conv3d_wgrad");
+  if (st) return st;
+  CG_CHECK_ARG(!g->transposed, "cgan3d_conv3d_wgrad: use the forward mapping (see header)");
+  CG_CHECK_ARG(gathered && aligned && dw && ws, "cgan3d_conv3d_wgrad: null pointer");
+  CG_CHECK_ARG(g->cout == 1 || g->cout % 4 == 0, "cgan3d_conv3d_wgrad: cout must be 1 or a multiple of 4");
+  hipStream_t s = (hipStream_t)stream;
+  ConvArgs a;
+  make_args(g, &a, 64);
+  const int T = g->k * g->k * g->k;
+  const long long R = (long long)T * g->cin;
+  const long long V = (long long)g->n * g->do_ * g->ho * g->wo;
+  if (hipMemsetAsync(ws, 0, R * g->cout * sizeof(float), s) != hipSuccess) {
+    set_error("cgan3d_conv3d_wgrad: memset failed");
+    return CGAN3D_EHIP;
+  }
+  if (g->cout == 1) {
+    CG_CHECK_ARG(g->cin % 4 == 0, "cgan3d_conv3d_wgrad: cout==1 needs cin%%4==0");
+    const long long R4 = R / 4;
+    CG_CHECK_ARG(R4 <= 256 * 8, "cgan3d_conv3d_wgrad: cout==1 reduction too long");
+    long long vpb = V / 512 + 1;
+    if (vpb < 256) vpb = 256;
+    vpb = (vpb + 63) / 64 * 64;
+    dim3 grid(cg::ceil_div(V, vpb));
+    if (R4 <= 256) hipLaunchKernelGGL((conv_wgrad_cout1_kernel<1>), grid, dim3(256), 0, s, a, gathered, aligned, ws, vpb);
+    else if (R4 <= 512) hipLaunchKernelGGL((conv_wgrad_cout1_kernel<2>), grid, dim3(256), 0, s, a, gathered, aligned, ws, vpb);
+    else if (R4 <= 1024) hipLaunchKernelGGL((conv_wgrad_cout1_kernel<4>), grid, dim3(256), 0, s, a, gathered, aligned, ws, vpb);
+    else hipLaunchKernelGGL((conv_wgrad_cout1_kernel<8>), grid, dim3(256), 0, s, a, gathered, aligned, ws, vpb);
+    CG_LAUNCH_CHECK("conv_wgrad_cout1_kernel");
+  } else {
+    const int gxb = cg::ceil_div(R, 64);
+    long long vpb = wgrad_vpb(V, gxb);
+    dim3 grid(gxb, cg::ceil_div(V, vpb));
+    const int nb = (g->cout + 15) / 16;
+    const bool v4 = (g->cin % 4) == 0;
+#define CG_LAUNCH_WG(VV, N) hipLaunchKernelGGL((conv_wgrad_kernel<VV, N>), grid, dim3(256), 0, s, a, gathered, aligned, ws, vpb)
+    if (v4) {
+      if (nb == 1) CG_LAUNCH_WG(4, 1); else if (nb == 2) CG_LAUNCH_WG(4, 2); else if (nb == 3) CG_LAUNCH_WG(4, 3); else CG_LAUNCH_WG(4, 4);
+    } else {
+      if (nb == 1) CG_LAUNCH_WG(1, 1); else if (nb == 2) CG_LAUNCH_WG(1, 2); else if (nb == 3) CG_LAUNCH_WG(1, 3); else CG_LAUNCH_WG(1, 4);
+    }
+#undef CG_LAUNCH_WG
+    CG_LAUNCH_CHECK("conv_wgrad_kernel");
+  }
+  const long long total = R * g->cout;
+  hipLaunchKernelGGL(wgrad_unpack_kernel, dim3(cg::ceil_div(total, 256)), dim3(256), 0, s, ws, dw, T, g->cin, g->cout,
+                     (long long)g->w_sa, (long long)g->w_sb, accumulate);
+  CG_LAUNCH_CHECK("wgrad_unpack_kernel");
+  return CGAN3D_OK;
+}

@@ -1,0 +1,277 @@
+// Loss reductions and their gradients for the G+D step (gfx950).
+//
+//  * Wasserstein critic/generator terms   — model/loss.py:74-80, Trainer.py:119-121,151
+//  * WGAN gradient penalty                — model/utils.py:12-41 (lambda * mean_b (||g_b||-1)^2)
+//  * ZNCC with the StableStd custom grad  — model/loss.py:11-41 (batch-global, 1e-6 / 1e-8 eps)
+//  * masked HU-range loss                 — model/loss.py:44-71
+//  * opt_hat = subopt - tanh(.) backward  — Trainer.py:170-171, generator.py:85
+//
+// Reductions accumulate per-block partials in fp64 and combine them in a single block, so no
+// atomics and bit-reproducible results.  Loss values are written to a device array (no host
+// sync); the Trainer reads them only on logging iterations, as the reference does.
+#include "common.h"
+
+namespace cg {
+
+enum { L_D = 0, L_WD = 1, L_GP = 2, L_G = 3, L_SIM = 4, L_HU = 5, L_GFULL = 6 };
+
+__device__ __forceinline__ double block_sum_d(double v, double* red) {
+  v = wave_sum_d(v);
+  const int w = threadIdx.x >> 6;
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) red[w] = v;
+  __syncthreads();
+  double s = 0.0;
+  for (int i = 0; i < (int)(blockDim.x >> 6); ++i) s += red[i];
+  return s;
+}
+
+// dlogits layout [real | fake | gp] (samples x per_sample)
+__global__ __launch_bounds__(256) void critic_logits_kernel(const float* __restrict__ logits, int nr, int nf, int ng,
+                                                            int ps, float gan_w, float* dl, float* losses) {
+  __shared__ double red[4];
+  double sr = 0.0, sf = 0.0;
+  const long long er = (long long)nr * ps, ef = (long long)nf * ps, eg = (long long)ng * ps;
+  for (long long i = threadIdx.x; i < er; i += blockDim.x) sr += logits[i];
+  for (long long i = threadIdx.x; i < ef; i += blockDim.x) sf += logits[er + i];
+  sr = block_sum_d(sr, red);
+  sf = block_sum_d(sf, red);
+  const float gr = -gan_w / (float)er, gf = gan_w / (float)ef;
+  for (long long i = threadIdx.x; i < er; i += blockDim.x) dl[i] = gr;
+  for (long long i = threadIdx.x; i < ef; i += blockDim.x) dl[er + i] = gf;
+  for (long long i = threadIdx.x; i < eg; i += blockDim.x) dl[er + ef + i] = 1.f;
+  if (threadIdx.x == 0) {
+    const float wd = (float)(gan_w * (sf / ef - sr / er));
+    losses[L_WD] = wd;
+    losses[L_D] = wd;
+    losses[L_GP] = 0.f;
+  }
+}
+
+__global__ __launch_bounds__(256) void gen_logits_kernel(const float* __restrict__ logits, int n, float gan_w,
+                                                         float* dl, float* losses) {
+  __shared__ double red[4];
+  double s = 0.0;
+  for (int i = threadIdx.x; i < n; i += blockDim.x) s += logits[i];
+  s = block_sum_d(s, red);
+  for (int i = threadIdx.x; i < n; i += blockDim.x) dl[i] = -gan_w / (float)n;
+  if (threadIdx.x == 0) losses[L_G] = (float)(-gan_w * s / n);
+}
+
+// --- gradient penalty -------------------------------------------------------------------
+__global__ __launch_bounds__(256) void sumsq_kernel(const float* __restrict__ g, long long ps, int chunks, float* part) {
+  __shared__ double red[4];
+  const int b = blockIdx.y;
+  const long long per = (ps + chunks - 1) / chunks;
+  const long long beg = per * blockIdx.x, end = beg + per < ps ? beg + per : ps;
+  double s = 0.0;
+  for (long long i = beg + threadIdx.x; i < end; i += blockDim.x) {
+    const double v = g[(long long)b * ps + i];
+    s += v * v;
+  }
+  s = block_sum_d(s, red);
+  if (threadIdx.x == 0) part[(long long)b * chunks + blockIdx.x] = (float)s;
+}
+
+__global__ void gp_finalize_kernel(const float* __restrict__ part, int B, int chunks, float lambda_, float* coef,
+                                   float* losses) {
+  __shared__ double red[4];
+  double acc = 0.0;
+  for (int b = threadIdx.x; b < B; b += blockDim.x) {
+    double ss = 0.0;
+    for (int c = 0; c < chunks; ++c) ss += part[(long long)b * chunks + c];
+    const double nrm = sqrt(ss);
+    acc += (nrm - 1.0) * (nrm - 1.0);
+    // d/dg_b of lambda*mean((||g_b||-1)^2) = lambda * 2/B * (||g_b||-1) * g_b/||g_b||  (0 at ||g_b||=0)
+    coef[b] = nrm > 0.0 ? (float)(lambda_ * 2.0 / B * (nrm - 1.0) / nrm) : 0.f;
+  }
+  acc = block_sum_d(acc, red);
+  if (threadIdx.x == 0) {
+    const float gp = (float)(lambda_ * acc / B);
+    losses[L_GP] = gp;
+    losses[L_D] = losses[L_WD] + gp;
+  }
+}
+
+__global__ __launch_bounds__(256) void scale_rows_kernel(const float* __restrict__ g, long long ps, long long total,
+                                                         const float* __restrict__ coef, float* out) {
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long long)gridDim.x * blockDim.x)
+    out[i] = coef[i / ps] * g[i];
+}
+
+// --- generator losses ---------------------------------------------------------------------
+// pass 1: sum s, sum t, sum mask, sum mask*hu
+__global__ __launch_bounds__(256) void gen_pass1_kernel(const float* __restrict__ s, const float* __restrict__ t,
+                                                        const uint8_t* __restrict__ m, long long n, float lo, float hi,
+                                                        double* part) {
+  __shared__ double red[4];
+  double a0 = 0, a1 = 0, a2 = 0, a3 = 0;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+    const float x = s[i];
+    a0 += x;
+    a1 += t[i];
+    if (m[i]) {
+      const float lb = fminf(x, lo) - lo, ub = fmaxf(x, hi) - hi;
+      a2 += 1.0;
+      a3 += (double)(lb * lb + ub * ub);
+    }
+  }
+  a0 = block_sum_d(a0, red); a1 = block_sum_d(a1, red); a2 = block_sum_d(a2, red); a3 = block_sum_d(a3, red);
+  if (threadIdx.x == 0) {
+    part[blockIdx.x * 4 + 0] = a0; part[blockIdx.x * 4 + 1] = a1;
+    part[blockIdx.x * 4 + 2] = a2; part[blockIdx.x * 4 + 3] = a3;
+  }
+}
+
+// means -> stat[0..3] = s_mean, t_mean, mask_sum, hu_sum
+__global__ void gen_fin1_kernel(const double* __restrict__ part, int nblk, long long n, double* stat) {
+  if (threadIdx.x < 4) {
+    double acc = 0;
+    for (int b = 0; b < nblk; ++b) acc += part[b * 4 + threadIdx.x];
+    stat[threadIdx.x] = threadIdx.x < 2 ? acc / (double)n : acc;
+  }
+}
+
+// pass 2: sum (s-sm)(t-tm), (s-sm)^2, (t-tm)^2, (t-tm)
+__global__ __launch_bounds__(256) void gen_pass2_kernel(const float* __restrict__ s, const float* __restrict__ t,
+                                                        long long n, const double* __restrict__ stat, double* part) {
+  __shared__ double red[4];
+  const float sm = (float)stat[0], tm = (float)stat[1];
+  double a0 = 0, a1 = 0, a2 = 0, a3 = 0;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+    const float u = s[i] - sm, w = t[i] - tm;
+    a0 += (double)(u * w);
+    a1 += (double)(u * u);
+    a2 += (double)(w * w);
+    a3 += (double)w;
+  }
+  a0 = block_sum_d(a0, red); a1 = block_sum_d(a1, red); a2 = block_sum_d(a2, red); a3 = block_sum_d(a3, red);
+  if (threadIdx.x == 0) {
+    part[blockIdx.x * 4 + 0] = a0; part[blockIdx.x * 4 + 1] = a1;
+    part[blockIdx.x * 4 + 2] = a2; part[blockIdx.x * 4 + 3] = a3;
+  }
+}
+
+// losses + gradient coefficients: stat[4..] = A (w coef), Bc (u coef), w_mean, hu_scale
+__global__ void gen_fin2_kernel(const double* __restrict__ part, int nblk, long long n, float sim_w, float hu_w,
+                                double* stat, float* losses) {
+  if (threadIdx.x != 0) return;
+  double suw = 0, suu = 0, sww = 0, sw = 0;
+  for (int b = 0; b < nblk; ++b) {
+    suw += part[b * 4 + 0]; suu += part[b * 4 + 1]; sww += part[b * 4 + 2]; sw += part[b * 4 + 3];
+  }
+  const double nn = (double)n;
+  const double cc = suw / nn;
+  const double ss = sqrt(suu / (nn - 1.0)), st = sqrt(sww / (nn - 1.0));  // torch.std (unbiased)
+  const double D = ss * st + 1e-8;
+  const double zncc = -cc / D;
+  const double hu = stat[3] / (stat[2] + 1e-8);
+  // dL/ds_j = -(1/D) (w_j - mean w)/n  +  cc*st/D^2 * 2/(n-1) * (s_j - s_mean)/(2 ss + 1e-6)
+  stat[4] = sim_w * (-1.0 / (D * nn));
+  stat[5] = sim_w * (cc * st / (D * D)) * (2.0 / (nn - 1.0)) / (2.0 * ss + 1e-6);
+  stat[6] = sw / nn;
+  stat[7] = hu_w * 2.0 / (stat[2] + 1e-8);
+  losses[L_SIM] = (float)(sim_w * zncc);
+  losses[L_HU] = (float)(hu_w * hu);
+  losses[L_GFULL] = losses[L_G] + (float)(sim_w * zncc) + (float)(hu_w * hu);
+}
+
+// dz_last = d(opt_hat)/d(z) chain: opt_hat = subopt - tanh(z)  =>  dz = -dL/dopt_hat * (1 - att^2)
+__global__ __launch_bounds__(256) void gen_grad_kernel(const float* __restrict__ s, const float* __restrict__ t,
+                                                       const float* __restrict__ att, const uint8_t* __restrict__ m,
+                                                       const float* __restrict__ dcrit, long long n, float lo, float hi,
+                                                       const double* __restrict__ stat, float* dz) {
+  const float sm = (float)stat[0], tm = (float)stat[1];
+  const float A = (float)stat[4], Bc = (float)stat[5], wm = (float)stat[6], hs = (float)stat[7];
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+    const float x = s[i];
+    float g = A * ((t[i] - tm) - wm) + Bc * (x - sm);
+    if (m[i]) g += hs * ((fminf(x, lo) - lo) + (fmaxf(x, hi) - hi));
+    if (dcrit) g += dcrit[i];
+    const float a = att[i];
+    dz[i] = -g * (1.f - a * a);
+  }
+}
+
+static int red_blocks(long long n) {
+  long long b = (n + 2047) / 2048;
+  if (b > 512) b = 512;
+  if (b < 1) b = 1;
+  return (int)b;
+}
+
+}  // namespace cg
+
+using namespace cg;
+
+extern "C" int64_t cgan3d_loss_ws_floats(int64_t n) {
+  // generator losses: (512 x 4 partials + 8 stats) doubles; GP: b x (<=64 chunks + 1) floats, b <= 1024
+  (void)n;
+  return 2 * (512 * 4 + 8) + 65 * 1024;
+}
+
+extern "C" int cgan3d_critic_logits_grad(const float* logits, int32_t n_real, int32_t n_fake, int32_t n_gp,
+                                         int32_t per_sample, float gan_w, float* dlogits, float* losses,
+                                         void* stream) {
+  CG_CHECK_ARG(logits && dlogits && losses, "cgan3d_critic_logits_grad: null pointer");
+  CG_CHECK_ARG(n_real > 0 && n_fake > 0 && n_gp >= 0 && per_sample > 0, "cgan3d_critic_logits_grad: bad sizes");
+  hipLaunchKernelGGL(critic_logits_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, logits, n_real, n_fake, n_gp,
+                     per_sample, gan_w, dlogits, losses);
+  CG_LAUNCH_CHECK("critic_logits_kernel");
+  return CGAN3D_OK;
+}
+
+extern "C" int cgan3d_generator_logits_grad(const float* logits, int32_t n, float gan_w, float* dlogits, float* losses,
+                                            void* stream) {
+  CG_CHECK_ARG(logits && dlogits && losses && n > 0, "cgan3d_generator_logits_grad: bad args");
+  hipLaunchKernelGGL(gen_logits_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, logits, n, gan_w, dlogits, losses);
+  CG_LAUNCH_CHECK("gen_logits_kernel");
+  return CGAN3D_OK;
+}
+
+extern "C" int cgan3d_gradient_penalty(const float* grad, int32_t b, int64_t per_sample, float lambda_,
+                                       float* gamma_out, float* losses, float* ws, void* stream) {
+  CG_CHECK_ARG(grad && gamma_out && losses && ws, "cgan3d_gradient_penalty: null pointer");
+  CG_CHECK_ARG(b > 0 && b <= 1024 && per_sample > 0, "cgan3d_gradient_penalty: bad sizes");
+  hipStream_t s = (hipStream_t)stream;
+  int chunks = (int)((per_sample + 8191) / 8192);
+  if (chunks > 64) chunks = 64;
+  float* part = ws;
+  float* coef = ws + (long long)b * chunks;
+  hipLaunchKernelGGL(sumsq_kernel, dim3(chunks, b), dim3(256), 0, s, grad, (long long)per_sample, chunks, part);
+  CG_LAUNCH_CHECK("sumsq_kernel");
+  hipLaunchKernelGGL(gp_finalize_kernel, dim3(1), dim3(256), 0, s, part, b, chunks, lambda_, coef, losses);
+  CG_LAUNCH_CHECK("gp_finalize_kernel");
+  const long long total = (long long)b * per_sample;
+  int blocks = (int)std::min<long long>((total + 255) / 256, 4096);
+  hipLaunchKernelGGL(scale_rows_kernel, dim3(blocks), dim3(256), 0, s, grad, (long long)per_sample, total, coef,
+                     gamma_out);
+  CG_LAUNCH_CHECK("scale_rows_kernel");
+  return CGAN3D_OK;
+}
+
+extern "C" int cgan3d_generator_output_grad(const float* opt_hat, const float* subopt, const float* att,
+                                            const uint8_t* mask, const float* d_critic, int64_t n, float lo, float hi,
+                                            float sim_w, float hu_w, float* dz_last, float* losses, float* ws,
+                                            void* stream) {
+  CG_CHECK_ARG(opt_hat && subopt && att && mask && dz_last && losses && ws, "cgan3d_generator_output_grad: null");
+  CG_CHECK_ARG(n > 1, "cgan3d_generator_output_grad: need n > 1");
+  CG_CHECK_ARG(((uintptr_t)ws & 7) == 0, "cgan3d_generator_output_grad: workspace must be 8-byte aligned");
+  hipStream_t s = (hipStream_t)stream;
+  double* part = reinterpret_cast<double*>(ws);
+  double* stat = part + 512 * 4;
+  const int nblk = red_blocks(n);
+  hipLaunchKernelGGL(gen_pass1_kernel, dim3(nblk), dim3(256), 0, s, opt_hat, subopt, mask, (long long)n, lo, hi, part);
+  CG_LAUNCH_CHECK("gen_pass1_kernel");
+  hipLaunchKernelGGL(gen_fin1_kernel, dim3(1), dim3(64), 0, s, part, nblk, (long long)n, stat);
+  CG_LAUNCH_CHECK("gen_fin1_kernel");
+  hipLaunchKernelGGL(gen_pass2_kernel, dim3(nblk), dim3(256), 0, s, opt_hat, subopt, (long long)n, stat, part);
+  CG_LAUNCH_CHECK("gen_pass2_kernel");
+  hipLaunchKernelGGL(gen_fin2_kernel, dim3(1), dim3(64), 0, s, part, nblk, (long long)n, sim_w, hu_w, stat, losses);
+  CG_LAUNCH_CHECK("gen_fin2_kernel");
+  int blocks = (int)std::min<long long>((n + 255) / 256, 4096);
+  hipLaunchKernelGGL(gen_grad_kernel, dim3(blocks), dim3(256), 0, s, opt_hat, subopt, att, mask, d_critic,
+                     (long long)n, lo, hi, stat, dz_last);
+  CG_LAUNCH_CHECK("gen_grad_kernel");
+  return CGAN3D_OK;
+}

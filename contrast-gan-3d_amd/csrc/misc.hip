@@ -1,0 +1,148 @@
+// Small device kernels of the step: fused Adam, reflect-pad fold, GP interpolation,
+// plus the library's version / error plumbing.
+#include <cstring>
+
+#include "common.h"
+
+namespace cg {
+
+static thread_local char g_err[512] = "";
+
+void set_error(const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_err, sizeof(g_err), fmt, ap);
+  va_end(ap);
+}
+
+// torch.optim.Adam single-tensor update (no weight decay / amsgrad / maximize), followed by the
+// optional WGAN weight clip of Trainer.py:136-138.  hyper = [lr, beta1, beta2, eps, step, clip].
+__global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, const float* __restrict__ g,
+                                                   float* __restrict__ m, float* __restrict__ v, long long n,
+                                                   const float* __restrict__ hyper) {
+  const float lr = hyper[0], b1 = hyper[1], b2 = hyper[2], eps = hyper[3], step = hyper[4], clip = hyper[5];
+  const float bc1 = 1.f - powf(b1, step);
+  const float bc2s = sqrtf(1.f - powf(b2, step));
+  const float wgt = 1.f - b1;
+  const float step_size = lr / bc1;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+    const float gi = g[i];
+    float mi = m[i];
+    // torch lerp: weight < 0.5 ? self + w*(end-self) : end - (end-self)*(1-w)
+    mi = wgt < 0.5f ? mi + wgt * (gi - mi) : gi - (gi - mi) * (1.f - wgt);
+    const float vi = v[i] * b2 + (1.f - b2) * gi * gi;
+    m[i] = mi;
+    v[i] = vi;
+    const float denom = sqrtf(vi) / bc2s + eps;
+    float pi = p[i] - step_size * (mi / denom);
+    if (clip > 0.f) pi = fminf(fmaxf(pi, -clip), clip);
+    p[i] = pi;
+  }
+}
+
+__global__ void adam_tick_kernel(float* hyper) { hyper[4] += 1.f; }
+
+// out[i] = sum of padded[q] over the reflect-pad preimages q of interior voxel i
+__global__ __launch_bounds__(256) void reflect_fold_kernel(const float* __restrict__ pad_in, float* __restrict__ out,
+                                                           int N, int D, int H, int W, int C, int P) {
+  const long long total = (long long)N * D * H * W * C;
+  const int Dp = D + 2 * P, Hp = H + 2 * P, Wp = W + 2 * P;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long long)gridDim.x * blockDim.x) {
+    int c = (int)(i % C); long long t = i / C;
+    int w = (int)(t % W); t /= W;
+    int h = (int)(t % H); t /= H;
+    int d = (int)(t % D); int n = (int)(t / D);
+    int qd[2], qh[2], qw[2], nd = 0, nh = 0, nw = 0;
+    qd[nd++] = d + P;
+    if (d >= 1 && d <= P) qd[nd++] = P - d;
+    else if (d <= D - 2 && d >= D - 1 - P) qd[nd++] = 2 * (D - 1) - d + P;
+    qh[nh++] = h + P;
+    if (h >= 1 && h <= P) qh[nh++] = P - h;
+    else if (h <= H - 2 && h >= H - 1 - P) qh[nh++] = 2 * (H - 1) - h + P;
+    qw[nw++] = w + P;
+    if (w >= 1 && w <= P) qw[nw++] = P - w;
+    else if (w <= W - 2 && w >= W - 1 - P) qw[nw++] = 2 * (W - 1) - w + P;
+    float s = 0.f;
+    for (int a = 0; a < nd; ++a)
+      for (int b = 0; b < nh; ++b)
+        for (int e = 0; e < nw; ++e)
+          s += pad_in[((((long long)n * Dp + qd[a]) * Hp + qh[b]) * Wp + qw[e]) * C + c];
+    out[i] = s;
+  }
+}
+
+// interpolation = eps*real + (1-eps)*fake  (model/utils.py:27-28)
+__global__ __launch_bounds__(256) void interp_kernel(const float* __restrict__ real, const float* __restrict__ fake,
+                                                     const float* __restrict__ eps, float* __restrict__ out,
+                                                     long long ps, long long total) {
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long long)gridDim.x * blockDim.x) {
+    const float e = eps[i / ps];
+    out[i] = e * real[i] + (1.f - e) * fake[i];
+  }
+}
+
+// dz = dy * (1 - y^2)   (tanh backward from its output, generator.py:85)
+__global__ __launch_bounds__(256) void tanh_bwd_kernel(const float* __restrict__ y, const float* __restrict__ dy,
+                                                       float* __restrict__ dz, long long n) {
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+    const float t = y[i];
+    dz[i] = dy[i] * (1.f - t * t);
+  }
+}
+
+}  // namespace cg
+
+using namespace cg;
+
+extern "C" int cgan3d_tanh_backward(const float* y, const float* dy, float* dz, int64_t n, void* stream) {
+  CG_CHECK_ARG(y && dy && dz && n > 0, "cgan3d_tanh_backward: bad args");
+  int blocks = (int)std::min<long long>((n + 255) / 256, 4096);
+  hipLaunchKernelGGL(tanh_bwd_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, y, dy, dz, (long long)n);
+  CG_LAUNCH_CHECK("tanh_bwd_kernel");
+  return CGAN3D_OK;
+}
+
+extern "C" const char* cgan3d_version(void) { return "cgan3d 0.1.0 gfx950"; }
+extern "C" const char* cgan3d_get_last_error(void) { return g_err; }
+
+extern "C" int cgan3d_adam_tick(float* hyper, void* stream) {
+  CG_CHECK_ARG(hyper, "cgan3d_adam_tick: null pointer");
+  hipLaunchKernelGGL(adam_tick_kernel, dim3(1), dim3(1), 0, (hipStream_t)stream, hyper);
+  CG_LAUNCH_CHECK("adam_tick_kernel");
+  return CGAN3D_OK;
+}
+
+extern "C" int cgan3d_adam(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, int64_t n,
+                           const float* hyper, void* stream) {
+  CG_CHECK_ARG(param && grad && exp_avg && exp_avg_sq && hyper, "cgan3d_adam: null pointer");
+  CG_CHECK_ARG(n > 0, "cgan3d_adam: n must be positive");
+  int blocks = (int)std::min<long long>((n + 255) / 256, 2048);
+  hipLaunchKernelGGL(adam_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, param, grad, exp_avg, exp_avg_sq,
+                     (long long)n, hyper);
+  CG_LAUNCH_CHECK("adam_kernel");
+  return CGAN3D_OK;
+}
+
+extern "C" int cgan3d_reflect_fold(const float* padded, float* out, int32_t n, int32_t d, int32_t h, int32_t w,
+                                   int32_t c, int32_t pad, void* stream) {
+  CG_CHECK_ARG(padded && out, "cgan3d_reflect_fold: null pointer");
+  CG_CHECK_ARG(n > 0 && d > 2 * pad && h > 2 * pad && w > 2 * pad && c > 0 && pad >= 0,
+               "cgan3d_reflect_fold: dims must exceed 2*pad");
+  const long long total = (long long)n * d * h * w * c;
+  int blocks = (int)std::min<long long>((total + 255) / 256, 8192);
+  hipLaunchKernelGGL(reflect_fold_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, padded, out, n, d, h, w, c,
+                     pad);
+  CG_LAUNCH_CHECK("reflect_fold_kernel");
+  return CGAN3D_OK;
+}
+
+extern "C" int cgan3d_gp_interpolate(const float* real, const float* fake, const float* eps, float* out, int32_t b,
+                                     int64_t per_sample, void* stream) {
+  CG_CHECK_ARG(real && fake && eps && out && b > 0 && per_sample > 0, "cgan3d_gp_interpolate: bad args");
+  const long long total = (long long)b * per_sample;
+  int blocks = (int)std::min<long long>((total + 255) / 256, 4096);
+  hipLaunchKernelGGL(interp_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, real, fake, eps, out,
+                     (long long)per_sample, total);
+  CG_LAUNCH_CHECK("interp_kernel");
+  return CGAN3D_OK;
+}

@@ -1,0 +1,137 @@
+/*
+ * cgan3d — C-ABI of the MI355X (gfx950) HIP kernels behind the contrast-GAN-3D G+D train step.
+ *
+ * Drop-in boundary.  The reference (xqz-u/contrast-gan-3D) is pure Python over torch aten ops,
+ * so there is no reference FFI; the entry points below replace the aten ops its hot path
+ * dispatches and are bound from Python with ctypes by
+ * contrast-gan-3d_amd/cgan3d_amd/_lib.py.  Each function cites the
+ * reference call site whose arithmetic it implements.
+ *
+ * Conventions
+ *  - Plain device pointers, sizes and a hipStream_t passed as void*; no torch types.
+ *  - Activations are fp32 NDHWC (channels-last): element (n, d, h, w, c) at
+ *    (((n*D + d)*H + h)*W + w)*C + c.  For C == 1 this equals the reference's NCDHW layout,
+ *    so the generator input/output and the critic input cross the boundary without copies.
+ *  - Weights stay in torch layout ([Cout, Cin, k, k, k] for Conv3d, [Cin, Cout, k, k, k] for
+ *    ConvTranspose3d); the geometry carries the strides of the two channel indices.
+ *  - The library never allocates: scratch comes from caller-provided workspace.
+ *  - All launches are asynchronous on `stream`; no host synchronisation; every entry point is
+ *    safe to capture in a hipGraph.
+ *  - Return 0 on success; otherwise an errno-style code and cgan3d_get_last_error() (per host
+ *    thread) describes the failure.  Shapes are validated on the host before any launch.
+ */
+#ifndef CGAN3D_H_
+#define CGAN3D_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CGAN3D_OK 0
+#define CGAN3D_EINVAL 22
+#define CGAN3D_EHIP 100
+
+/* Conv geometry.  "Gathered" operand G has spatial dims (di,hi,wi) and `cin` channels; the
+ * voxel-aligned operand/output O has dims (do_,ho,wo) and `cout` channels.  Tap t = (td,th,tw)
+ * of a k^3 kernel links O-voxel o and G-voxel i by
+ *   transposed == 0 :  i = o*stride - pad + t   (Conv3d forward; ConvTranspose3d input-grad)
+ *   transposed == 1 :  o = i*stride - pad + t   (ConvTranspose3d forward; Conv3d input-grad)
+ * reflect != 0 (transposed == 0 only) mirrors out-of-range i (torch padding_mode="reflect"),
+ * otherwise out-of-range taps contribute zero.  Weight element for (G channel a, O channel b,
+ * tap index t = (td*k + th)*k + tw) is w[a*w_sa + b*w_sb + t]. */
+typedef struct cgan3d_conv_geom {
+  int32_t n;
+  int32_t di, hi, wi;
+  int32_t do_, ho, wo;
+  int32_t cin, cout;
+  int32_t k, stride, pad;
+  int32_t transposed;
+  int32_t reflect;
+  int64_t w_sa, w_sb;
+} cgan3d_conv_geom;
+
+#define CGAN3D_ACT_NONE 0
+#define CGAN3D_ACT_RELU 1
+#define CGAN3D_ACT_LRELU 2
+#define CGAN3D_ACT_TANH 3
+
+/* Fused epilogue: v = acc (+ bias[c]); v = act(v); v *= (mask_src > 0 ? 1 : slope) if mask_src;
+ * v += residual if residual; out = v; if out2: out2 = minuend - v (cout == 1 only).
+ * stats != NULL: per-block BatchNorm partials (sum, M2, count) of v, consumed by
+ * cgan3d_bn_finalize; size cgan3d_conv3d_stats_floats(). */
+typedef struct cgan3d_epilogue {
+  const float* bias;
+  const float* residual;
+  const float* mask_src;
+  const float* minuend;
+  float* out2;
+  float* stats;
+  int32_t act;
+  float slope;
+} cgan3d_epilogue;
+
+const char* cgan3d_version(void);
+const char* cgan3d_get_last_error(void);
+
+/* --- convolutions (model/blocks.py:29-38 Conv3d / ConvTranspose3d; generator.py:78-84 last
+ *     conv; discriminator.py:24-80 critic convs; and their autograd backward) --- */
+int64_t cgan3d_conv3d_stats_floats(const cgan3d_conv_geom* g);
+int cgan3d_conv3d_fwd(const cgan3d_conv_geom* g, const float* x, const float* w, float* y,
+                      const cgan3d_epilogue* ep, void* stream);
+/* weight gradient: dw[a*w_sa + b*w_sb + t] (+)= sum_o G_gathered(o,t,a) * O(o,b) with the
+ * transposed==0 mapping.  Workspace: cgan3d_conv3d_wgrad_ws_floats() floats. */
+int64_t cgan3d_conv3d_wgrad_ws_floats(const cgan3d_conv_geom* g);
+int cgan3d_conv3d_wgrad(const cgan3d_conv_geom* g, const float* gathered, const float* aligned,
+                        float* dw, int32_t accumulate, float* ws, void* stream);
+
+/* --- BatchNorm3d, training mode (model/blocks.py:26-27,45; torch.nn.BatchNorm3d) --- */
+int cgan3d_bn_finalize(const float* stats, int64_t nblk, int32_t c, const float* gamma,
+                       const float* beta, float* running_mean, float* running_var,
+                       int64_t* num_batches_tracked, float momentum, float eps,
+                       float* scale_shift, float* mean_invstd, void* stream);
+int cgan3d_bn_apply(const float* z, int64_t nvox, int32_t c, const float* scale_shift,
+                    int32_t act, float slope, const float* residual, float* y, void* stream);
+int64_t cgan3d_bn_backward_ws_floats(int64_t nvox, int32_t c);
+int cgan3d_bn_backward(const float* dy, const float* z, int64_t nvox, int32_t c,
+                       const float* scale_shift, const float* mean_invstd, const float* gamma,
+                       int32_t act, float slope, float* dgamma, float* dbeta, float* dz,
+                       float* ws, void* stream);
+
+/* --- reductions / elementwise --- */
+int64_t cgan3d_channel_sum_ws_floats(int64_t nvox, int32_t c);
+int cgan3d_channel_sum(const float* x, int64_t nvox, int32_t c, float* out, float* ws,
+                       void* stream);
+int cgan3d_reflect_fold(const float* padded, float* out, int32_t n, int32_t d, int32_t h,
+                        int32_t w, int32_t c, int32_t pad, void* stream);
+int cgan3d_gp_interpolate(const float* real, const float* fake, const float* eps, float* out,
+                          int32_t b, int64_t per_sample, void* stream);
+
+int cgan3d_tanh_backward(const float* y, const float* dy, float* dz, int64_t n, void* stream);
+
+/* --- losses (model/loss.py:11-80, model/utils.py:12-41, Trainer.py:119-154) ---
+ * losses[] slots: 0 D total, 1 W_D, 2 GP, 3 G (adversarial), 4 sim (ZNCC), 5 HU, 6 G-full. */
+int64_t cgan3d_loss_ws_floats(int64_t n);
+int cgan3d_critic_logits_grad(const float* logits, int32_t n_real, int32_t n_fake, int32_t n_gp,
+                              int32_t per_sample, float gan_w, float* dlogits, float* losses,
+                              void* stream);
+int cgan3d_gradient_penalty(const float* grad, int32_t b, int64_t per_sample, float lambda_,
+                            float* gamma_out, float* losses, float* ws, void* stream);
+int cgan3d_generator_logits_grad(const float* logits, int32_t n, float gan_w, float* dlogits,
+                                 float* losses, void* stream);
+int cgan3d_generator_output_grad(const float* opt_hat, const float* subopt, const float* att,
+                                 const uint8_t* mask, const float* d_critic, int64_t n, float lo,
+                                 float hi, float sim_w, float hu_w, float* dz_last, float* losses,
+                                 float* ws, void* stream);
+
+/* --- optimiser (torch.optim.Adam, experiments/basic_conf.py:55,67) ---
+ * hyper (device): [lr, beta1, beta2, eps, step, weight_clip]; cgan3d_adam_tick increments step. */
+int cgan3d_adam_tick(float* hyper, void* stream);
+int cgan3d_adam(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, int64_t n,
+                const float* hyper, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CGAN3D_H_ */

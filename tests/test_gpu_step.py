@@ -1,0 +1,119 @@
+"""HIP step engine vs the reference (golden fixtures) and vs the oracle — on an MI355X.
+
+Tolerance: the north_star's "within 1e-3 relative fp32" (conftest.assert_close: max-abs error
+<= 1e-3 x max|ref| and relative L2 <= 1e-3), per tensor.
+"""
+import ast
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import assert_close
+
+pytestmark = pytest.mark.gpu
+
+D_ARGS = dict(channels_in=1, init_channels_out=8, discriminator_depth=3, negative_slope=0.2)
+
+
+def _models(g_args):
+    from torch import nn
+    from cgan3d_amd.model.discriminator import PatchGANDiscriminator
+    from cgan3d_amd.model.generator import ResnetGenerator
+    from cgan3d_amd.model.init import pcg64_init_
+    g = pcg64_init_(ResnetGenerator(**g_args), 0).cuda()
+    d = pcg64_init_(PatchGANDiscriminator(**D_ARGS, norm_layer=nn.Identity), 1).cuda()
+    return g, d
+
+
+def _engine(g, d, b, S, lr, b1, b2):
+    from cgan3d_amd.engine import StepEngine
+    return StepEngine(g, d, g.config, d.config, b, b, (S, S, S), g_hyper=(lr, b1, b2, 1e-8),
+                      d_hyper=(lr, b1, b2, 1e-8))
+
+
+@pytest.mark.parametrize("tag", ["gp_small", "gp_full"])
+def test_step_matches_reference_fixture(golden, tag):
+    f = golden(f"step_{tag}")
+    meta = ast.literal_eval(str(f["meta"]))
+    g_args = dict(n_resnet_blocks=meta["g_n_resnet_blocks"], n_updownsample_blocks=meta["g_n_updownsample_blocks"],
+                  init_channels_out=meta["g_init_channels_out"])
+    S, b = meta["S"], meta["b_opt"]
+    g, d = _models(g_args)
+    eng = _engine(g, d, b, S, meta["lr"], meta["beta1"], meta["beta2"])
+    names = {"L_D": 0, "D": 0, "G": 3, "sim": 4, "HU": 5, "G-full": 6}
+    for it in range(meta["iters"]):
+        sub = np.concatenate([f[f"it{it}/low"], f[f"it{it}/high"]])
+        mask = np.concatenate([f[f"it{it}/low_seg"], f[f"it{it}/high_seg"]])
+        eng.load_inputs(torch.from_numpy(f[f"it{it}/opt"]).cuda(), torch.from_numpy(sub).cuda(),
+                        torch.from_numpy(mask).cuda(), torch.from_numpy(f[f"it{it}/eps"]).cuda())
+        eng.step()
+        losses = eng.losses.cpu().numpy()
+        for k in ("D", "G", "sim", "HU", "G-full"):
+            assert_close(losses[names[k]], f[f"it{it}/loss/{k}"], 1e-3, f"it{it} loss {k}")
+        for net, arena in (("G", eng.g_arena), ("D", eng.d_arena)):
+            for k, gv in arena.gviews.items():
+                key = f"it{it}/grad/{net}/{k}"
+                if key in f:
+                    assert_close(gv.cpu().numpy(), f[key], 1e-3, key)
+    for net, mod in (("G", g), ("D", d)):
+        sd = mod.state_dict()
+        for k in f:
+            if k.startswith(f"final/{net}/"):
+                name = k.split("/", 2)[2]
+                assert_close(sd[name].cpu().numpy(), f[k], 1e-3, k)
+
+
+def test_generator_forward_matches_reference(golden):
+    from cgan3d_amd.model.generator import ResnetGenerator
+    from cgan3d_amd.model.init import pcg64_init_
+    f = golden("g_fwd_32")
+    g = pcg64_init_(ResnetGenerator(4, 2, 16), 0).cuda().train()
+    with torch.no_grad():
+        y = g(torch.from_numpy(f["x"]).cuda())
+    assert_close(y.cpu().numpy(), f["y"], 1e-3, "G(x)")
+    sd = g.state_dict()
+    for k in f:
+        if k.startswith("sd/"):
+            assert_close(sd[k[3:]].cpu().numpy(), f[k], 1e-3, k)
+
+
+def test_critic_forward_matches_reference(golden):
+    from torch import nn
+    from cgan3d_amd.model.discriminator import PatchGANDiscriminator
+    from cgan3d_amd.model.init import pcg64_init_
+    f = golden("d_fwd_32")
+    d = pcg64_init_(PatchGANDiscriminator(**D_ARGS, norm_layer=nn.Identity), 1).cuda()
+    with torch.no_grad():
+        y = d(torch.from_numpy(f["x"]).cuda())
+    assert_close(y.cpu().numpy(), f["gp/y"], 1e-3, "D(x)")
+
+
+@pytest.mark.parametrize("S,b", [(64, 2)])
+def test_step_matches_oracle_64(S, b):
+    """Full config at the benchmark patch size, against the CPU oracle (2 steps)."""
+    from oracle import reference_torch as R
+    from cgan3d_amd.data.synthetic import synth_patches
+    g_args = dict(n_resnet_blocks=4, n_updownsample_blocks=2, init_channels_out=16)
+    g, d = _models(g_args)
+    gpar = {k: v.detach().cpu().clone() for k, v in g.state_dict().items()}
+    dpar = {k: v.detach().cpu().clone() for k, v in d.state_dict().items()}
+    eng = _engine(g, d, b, S, 1e-4, 0.0, 0.9)
+    cfg = R.StepConfig(gen=R.GenConfig(**g_args), critic=R.CriticConfig())
+    gopt, dopt = R.AdamState(1e-4, 0.0, 0.9), R.AdamState(1e-4, 0.0, 0.9)
+    for it in range(2):
+        opt, _ = synth_patches(b, S, 10 + it)
+        sub, seg = synth_patches(b, S, 20 + it)
+        eps = np.random.Generator(np.random.PCG64(30 + it)).random((b, 1, 1, 1, 1)).astype(np.float32)
+        rec = {}
+        ref = R.train_step(gpar, dpar, gopt, dopt, torch.from_numpy(opt), torch.from_numpy(sub),
+                           torch.from_numpy(seg), torch.from_numpy(eps), cfg, record=rec)
+        eng.load_inputs(torch.from_numpy(opt).cuda(), torch.from_numpy(sub).cuda(), torch.from_numpy(seg).cuda(),
+                        torch.from_numpy(eps).cuda())
+        eng.step()
+        losses = eng.losses.cpu().numpy()
+        for k, slot in (("D", 0), ("G", 3), ("sim", 4), ("HU", 5), ("G-full", 6)):
+            assert_close(losses[slot], ref[k], 1e-3, f"it{it} {k}")
+        for net, arena in (("G", eng.g_arena), ("D", eng.d_arena)):
+            for k, gv in arena.gviews.items():
+                assert_close(gv.cpu().numpy(), rec[net][k].numpy(), 1e-3, f"it{it} grad {net} {k}")

@@ -1,0 +1,74 @@
+"""Host-side tests (no GPU): C-ABI symbol table, module layout, dry-run shape checks of the step."""
+import re
+from pathlib import Path
+
+import pytest
+import torch
+from torch import nn
+
+from conftest import REPO
+
+D_ARGS = dict(channels_in=1, init_channels_out=8, discriminator_depth=3, negative_slope=0.2)
+
+
+def test_library_exports_every_header_symbol():
+    from cgan3d_amd import _lib
+    header = (REPO / "include" / "cgan3d.h").read_text()
+    declared = set(re.findall(r"\b(cgan3d_[a-z0-9_]+)\s*\(", header))
+    assert declared, "no declarations parsed"
+    lib = _lib.load()  # loading needs no GPU
+    for name in declared:
+        assert hasattr(lib, name), f"libcgan3d.so lacks {name}"
+    assert declared == set(_lib.exported_symbols()), declared ^ set(_lib.exported_symbols())
+    assert lib.cgan3d_version().decode().startswith("cgan3d")
+
+
+def test_state_dict_layout_matches_reference():
+    """Same keys, order and shapes as the reference modules (pinned via the oracle's layout, which
+    tests/test_oracle.py checks against the reference's own state_dict order)."""
+    from oracle import reference_torch as R
+    from cgan3d_amd.model.discriminator import PatchGANDiscriminator
+    from cgan3d_amd.model.generator import ResnetGenerator
+    g = ResnetGenerator(4, 2, 16)
+    assert [(k, tuple(v.shape)) for k, v in g.state_dict().items()] == list(R.gen_param_shapes(R.GenConfig()).items())
+    d = PatchGANDiscriminator(**D_ARGS, norm_layer=nn.Identity)
+    assert [(k, tuple(v.shape)) for k, v in d.state_dict().items()] == \
+        list(R.critic_param_shapes(R.CriticConfig()).items())
+    assert sum(p.numel() for p in g.parameters()) == 1_035_297
+    assert sum(p.numel() for p in d.parameters()) == 176_761
+
+
+@pytest.mark.parametrize("g_args,S,b", [
+    (dict(n_resnet_blocks=1, n_updownsample_blocks=2, init_channels_out=8), 32, 1),
+    (dict(n_resnet_blocks=4, n_updownsample_blocks=2, init_channels_out=16), 64, 4),
+    (dict(n_resnet_blocks=4, n_updownsample_blocks=2, init_channels_out=16), 32, 2),
+])
+def test_engine_step_dry_run_shapes(g_args, S, b):
+    """Every launch of a full step gets operands whose extents match the kernel's footprint."""
+    from cgan3d_amd import ops
+    from cgan3d_amd.engine import StepEngine
+    from cgan3d_amd.model.discriminator import PatchGANDiscriminator
+    from cgan3d_amd.model.generator import ResnetGenerator
+    g = ResnetGenerator(**g_args)
+    d = PatchGANDiscriminator(**D_ARGS, norm_layer=nn.Identity)
+    ops.DRY_RUN = True
+    try:
+        eng = StepEngine(g, d, g.config, d.config, b, b, (S, S, S), g_hyper=(1e-4, 0.0, 0.9, 1e-8),
+                         d_hyper=(1e-4, 0.0, 0.9, 1e-8), device=torch.device("cpu"))
+        eng.step()
+    finally:
+        ops.DRY_RUN = False
+
+
+def test_conv_wrapper_rejects_mismatched_operand():
+    from cgan3d_amd import ops
+    g = ops.conv_fwd_geom(1, (8, 8, 8), (8, 8, 8), 16, 16, 3, 1, 1)
+    x = torch.empty(1, 8, 8, 8, 16)
+    w = torch.empty(16, 16, 3, 3, 3)
+    ops.DRY_RUN = True
+    try:
+        ops.conv(g, x, w, torch.empty(1, 8, 8, 8, 16))
+        with pytest.raises(ValueError):
+            ops.conv(g, x, w, torch.empty(1, 4, 4, 4, 16))
+    finally:
+        ops.DRY_RUN = False
