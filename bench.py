@@ -1,0 +1,175 @@
+"""Benchmark: 3D patches/s of the G+D train step (BASELINE.json metric), HIP step engine.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--size 64] [--batch 4]
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N
+
+Workload (BASELINE.json configs[1]): 64^3 patches, 4 OPT + 4 (LOW+HIGH) subopt patches per GPU per
+step, full G+D step of the gradient-penalty configuration (generator forward, critic update with
+WGAN-GP, generator update, Adam on both).  Synthetic HU patches, PCG64-initialised weights of the
+reference architecture.  "patches" = subopt patches corrected per second;
+value = all ranks' patches / max-over-ranks wall time of the K timed steps.  Inputs are resident in
+HBM when the timed region starts (a device-to-device copy into the engine's slots is inside it).
+
+Extra JSON fields: ``roofline`` for the dominant kernel (HIP events around its launches during
+the timed steps; algorithmic FLOPs from the layer geometry) and ``cpu_baseline`` (the oracle —
+torch fp32 on the host cores — on a bounded sample, rank 0 only, N=1 only).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+REPO = Path(__file__).resolve().parent
+sys.path.insert(0, str(REPO / "contrast-gan-3d_amd"))
+sys.path.insert(0, str(REPO))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+F32_PEAK_TFLOPS = 157.3   # MI355X f32 MFMA == f32 vector peak (MI355X_MICROARCH.md)
+BF16_PEAK_TFLOPS = 2500.0  # dense bf16 MFMA
+HBM_PEAK_GBS = 8000.0
+
+
+def conv_flops(n, dout, cin, cout, k):
+    """FlopCounterMode-style conv FLOPs: 2 * N * Cout * |out| * Cin * k^3."""
+    return 2.0 * n * cout * dout[0] * dout[1] * dout[2] * cin * k**3
+
+
+def cpu_baseline(size, seconds, g_args):
+    """Oracle (torch fp32 CPU restatement of the reference step) on the host cores."""
+    from cgan3d_amd.data.synthetic import synth_patches
+    from cgan3d_amd.model.init import pcg64_state_dict
+    from oracle import reference_torch as R
+
+    threads = max(1, min(16, len(os.sched_getaffinity(0))))
+    torch.set_num_threads(threads)
+    gcfg = R.GenConfig(**g_args)
+    cfg = R.StepConfig(gen=gcfg, critic=R.CriticConfig())
+    gp = {k: torch.from_numpy(v.copy()) for k, v in pcg64_state_dict(list(R.gen_param_shapes(gcfg).items()), 0).items()}
+    dp = {k: torch.from_numpy(v.copy()) for k, v in
+          pcg64_state_dict(list(R.critic_param_shapes(R.CriticConfig()).items()), 1).items()}
+    gopt, dopt = R.AdamState(1e-4, 0.0, 0.9), R.AdamState(1e-4, 0.0, 0.9)
+    b = 1
+    opt, _ = synth_patches(b, size, 1)
+    sub, seg = synth_patches(b, size, 2)
+    eps = torch.full((b, 1, 1, 1, 1), 0.5)
+    args = (torch.from_numpy(opt), torch.from_numpy(sub), torch.from_numpy(seg), eps, cfg)
+    R.train_step(gp, dp, gopt, dopt, *args)  # warm-up
+    n, t0 = 0, time.perf_counter()
+    while True:
+        R.train_step(gp, dp, gopt, dopt, *args)
+        n += 1
+        el = time.perf_counter() - t0
+        if el >= seconds or n >= 50:
+            break
+    return {"value": round(n * b / el, 4), "unit": "patches/s", "cores": threads, "kind": "port",
+            "sample": f"oracle/reference_torch.py train_step, {size}^3, batch 1+1, GP conf, fp32, {n} steps in "
+                      f"{el:.1f}s after 1 warm-up step"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--size", type=int, default=64)
+    ap.add_argument("--batch", type=int, default=4)
+    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=dev)
+
+    from torch import nn
+    from cgan3d_amd.data.synthetic import synth_patches
+    from cgan3d_amd.engine import StepEngine
+    from cgan3d_amd.model.discriminator import PatchGANDiscriminator
+    from cgan3d_amd.model.generator import ResnetGenerator
+    from cgan3d_amd.model.init import pcg64_init_
+
+    g_args = dict(n_resnet_blocks=4, n_updownsample_blocks=2, init_channels_out=16)  # basic_conf.py:49-53
+    S, B = args.size, args.batch
+    g = pcg64_init_(ResnetGenerator(**g_args), 0).to(dev)
+    d = pcg64_init_(PatchGANDiscriminator(1, 8, 3, negative_slope=0.2, norm_layer=nn.Identity), 1).to(dev)
+    eng = StepEngine(g, d, g.config, d.config, B, B, (S, S, S), g_hyper=(1e-4, 0.0, 0.9, 1e-8),
+                     d_hyper=(1e-4, 0.0, 0.9, 1e-8), device=dev)
+    batches = []
+    for j in range(2):
+        opt, _ = synth_patches(B, S, 1000 * rank + 10 * j)
+        sub, seg = synth_patches(B, S, 1000 * rank + 10 * j + 1)
+        batches.append((torch.from_numpy(opt).to(dev), torch.from_numpy(sub).to(dev),
+                        torch.from_numpy(seg).to(dev), torch.rand(B, device=dev)))
+
+    # dominant kernel: the generator's last conv (16 -> 1, k7 reflect, bias, tanh) forward
+    la = eng.G.last
+    roof_flops = conv_flops(B, la.dout, la.cin, 1, la.k)
+    ev = []
+
+    def one_step(i, timed):
+        eng.load_inputs(*batches[i % len(batches)])
+        if timed:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            eng.G.timer = (e0, e1)
+            ev.append((e0, e1))
+        eng.step()
+        eng.G.timer = None
+
+    for i in range(args.warmup):
+        one_step(i, False)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        one_step(i, True)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    if dist:
+        t = torch.tensor([el], device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    losses = eng.losses.cpu().numpy()
+    assert np.isfinite(losses).all(), f"non-finite losses {losses}"
+    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    achieved = roof_flops / (kern_ms * 1e-3) / 1e12
+    ms = el / args.steps * 1e3
+    value = world * B * args.steps / el
+    out = {
+        "metric": "3D patches/sec (G+D train step), 64³ bf16, at 1/2/4/8 MI355X",
+        "value": round(value, 3), "unit": "patches/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+        "config": {"workload": f"{S}^3 patches, {B} OPT + {B} LOW/HIGH per GPU, full G+D step (WGAN-GP conf)",
+                   "global_batch": world * B, "patch": S, "parallelism": f"dp{world}"},
+        "roofline": {"kernel": "conv_cout1_kernel (generator last conv fwd)", "bound": "mfma",
+                     "achieved": round(achieved, 3), "peak": F32_PEAK_TFLOPS, "unit": "TFLOP/s",
+                     "frac": round(achieved / F32_PEAK_TFLOPS, 4), "traffic": None,
+                     "avg_launch_ms": round(kern_ms, 4), "flops_per_launch": roof_flops},
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(S, args.cpu_seconds, g_args)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -105,6 +105,7 @@ class GeneratorPlan:
     def __init__(self, cfg, n: int, dims: Dims, device):
         c0 = cfg.init_channels_out
         self.n, self.dims, self.device = n, tuple(dims), device
+        self.timer = None
         layers: List[_GLayer] = [_GLayer("conv", "model.first", 7, 1, 3, True, 1, c0, dims, dims)]
         d = tuple(dims)
         for i in range(cfg.n_updownsample_blocks):
@@ -191,7 +192,11 @@ class GeneratorPlan:
         la = self.last
         ep = ops.epilogue(bias=P["model.last_conv.bias"], act=L.ACT_TANH,
                           minuend=x if opt_hat_out is not None else None, out2=opt_hat_out)
+        if self.timer is not None:  # bench.py: HIP events around this launch, same stream
+            self.timer[0].record()
         ops.conv(self.geo_last_fwd, h, P["model.last_conv.weight"], self.att, ep)
+        if self.timer is not None:
+            self.timer[1].record()
         return self.att
 
     def _eval_scale_shift(self, P, nb, i):
@@ -332,9 +337,9 @@ class StepEngine:
     """One fused G+D train step for fixed (b_opt, b_sub, patch dims) on one GPU."""
 
     def __init__(self, generator, critic, g_cfg, d_cfg, b_opt: int, b_sub: int, dims: Dims, *,
-                 g_hyper: Sequence[float], d_hyper: Sequence[float], gp_weight: float = 10.0,
-                 hu_bounds=(112.0 / 600.0, 212.0 / 600.0), gan_w=1.0, sim_w=1.0, hu_w=1.0,
-                 device=None, g_arena: Optional[Arena] = None, d_arena: Optional[Arena] = None):
+                 g_hyper: Sequence[float] = (1e-4, 0.0, 0.9, 1e-8), d_hyper: Sequence[float] = (1e-4, 0.0, 0.9, 1e-8),
+                 gp_weight: float = 10.0, hu_bounds=(112.0 / 600.0, 212.0 / 600.0), gan_w=1.0, sim_w=1.0, hu_w=1.0,
+                 device=None, g_optim=None, d_optim=None, process_group=None):
         if b_opt != b_sub:
             raise NotImplementedError("StepEngine: the GP path assumes |OPT| == |LOW|+|HIGH| (basic_conf.py:74-79)")
         if d_cfg.norm != "identity":
@@ -349,8 +354,20 @@ class StepEngine:
         self.G = GeneratorPlan(g_cfg, b_sub, dims, device)
         nmax = b_opt + b_sub + self.b_gp
         self.D = CriticPlan(d_cfg, nmax, dims, device)
-        self.g_arena = g_arena or Arena(generator, device)
-        self.d_arena = d_arena or Arena(critic, device)
+        from .trainer.optim import FusedAdam
+        if g_optim is None:
+            lr, b1, b2, eps = g_hyper
+            g_optim = FusedAdam(Arena(generator, device), lr, (b1, b2), eps)
+        if d_optim is None:
+            lr, b1, b2, eps = d_hyper
+            d_optim = FusedAdam(Arena(critic, device), lr, (b1, b2), eps)
+        self.g_optim, self.d_optim = g_optim, d_optim
+        # patch-level data parallelism: one gradient all-reduce per update
+        self.pg = process_group
+        self.world = 1
+        if process_group is not None or (torch.distributed.is_available() and torch.distributed.is_initialized()):
+            self.world = torch.distributed.get_world_size(process_group)
+        self.g_arena, self.d_arena = g_optim.arena, d_optim.arena
         self.gP = dict(self.g_arena.views)
         self.gP.update({k: v for k, v in generator.state_dict(keep_vars=True).items() if k not in self.gP})
         self.dP = dict(self.d_arena.views)
@@ -364,8 +381,6 @@ class StepEngine:
         self.dcrit = torch.empty((b_sub, *dims, 1), device=device)       # dL_G/d opt_hat via the critic
         self.losses = torch.zeros(8, device=device)
         self.loss_ws = torch.empty(ops.loss_ws_floats(), device=device)
-        self.g_hyper = torch.tensor(list(g_hyper) + [0.0, 0.0], device=device, dtype=torch.float32)[:6].contiguous()
-        self.d_hyper = torch.tensor(list(d_hyper) + [0.0, 0.0], device=device, dtype=torch.float32)[:6].contiguous()
 
     @property
     def opt_hat(self):
@@ -393,8 +408,8 @@ class StepEngine:
         ops.gradient_penalty(self.gbuf, bg, V, self.gp_weight, gamma, self.losses, self.loss_ws)
         D.gp_forward_mode(self.dP, gamma, bo + bs, bg)
         D.weight_grads(self.dP, self.dG, self.xc, nall, bo + bs)
-        ops.adam_tick(self.d_hyper)
-        ops.adam(self.d_arena.flat, self.d_arena.grad, self.d_arena.exp_avg, self.d_arena.exp_avg_sq, self.d_hyper)
+        self._allreduce(self.d_arena.grad)  # on the critical path: the G update uses the new critic
+        self.d_optim.launch()
 
     def generator_update(self):
         D, bs, V = self.D, self.b_sub, self.vox
@@ -404,8 +419,19 @@ class StepEngine:
         ops.generator_output_grad(self.opt_hat, self.subopt, self.G.att, self.mask, self.dcrit, bs * V, self.lo,
                                   self.hi, self.sim_w, self.hu_w, self.G.dz_last, self.losses, self.loss_ws)
         self.G.backward(self.gP, self.gG, self.subopt)
-        ops.adam_tick(self.g_hyper)
-        ops.adam(self.g_arena.flat, self.g_arena.grad, self.g_arena.exp_avg, self.g_arena.exp_avg_sq, self.g_hyper)
+        self._allreduce(self.g_arena.grad)
+        self.g_optim.launch()
+
+    def _allreduce(self, flat_grad: torch.Tensor):
+        """Mean of the per-rank gradients (RCCL over xGMI with the nccl backend; gloo on CPU)."""
+        if self.world == 1:
+            return
+        dist = torch.distributed
+        if dist.get_backend(self.pg) == "nccl":
+            dist.all_reduce(flat_grad, op=dist.ReduceOp.AVG, group=self.pg)
+        else:
+            dist.all_reduce(flat_grad, op=dist.ReduceOp.SUM, group=self.pg)
+            flat_grad.mul_(1.0 / self.world)
 
     def step(self, do_critic: bool = True, do_generator: bool = True):
         """Trainer.train_step body (Trainer.py:169-184) on the resident inputs."""

@@ -1,0 +1,278 @@
+"""Trainer — drop-in for ``contrast_gan_3D/trainer/Trainer.py:34-363`` on the HIP step engine.
+
+Same constructor (positional order of ``train.py:154-176``), same methods and ``log_dict`` keys
+(``"D"``, ``"G"``, ``"G-full"``, ``"sim"``, ``"HU"``), same checkpoint layout.  ``train_step``
+runs ``cgan3d_amd.engine.StepEngine``: the generator forward once, the critic update with the
+gradient penalty and the generator update as explicit HIP launches over resident buffers, Adam
+fused over a parameter arena.  Loss values stay on the device and are read only on logging
+iterations (as in the reference, ``Trainer.py:187-190``).
+
+Differences from the reference, all deliberate and documented in DESIGN.md:
+* the critic weights are checkpointed under ``"critic"`` (the reference lists the non-existent
+  attribute ``"discriminator"``, Trainer.py:316, so its critic is never saved); the
+  ``"discriminator": None`` entry is kept so either kind of checkpoint loads;
+* ``train_critic`` / ``train_generator`` act on the engine's resident batch (``train_step``
+  loads it); they keep the reference signatures for callers that drive them directly.
+"""
+from __future__ import annotations
+
+from functools import partial
+from pathlib import Path
+from typing import Dict, List, Optional, Union
+
+import numpy as np
+import torch
+from torch import Tensor, nn
+
+from .. import _lib as L
+from ..engine import Arena, StepEngine
+from ..model.loss import WassersteinLoss, ZNCCLoss
+from .optim import FusedAdam, adam_hyper_from_partial
+
+try:  # tqdm is what the reference uses for progress; optional here
+    from tqdm.auto import trange
+except Exception:  # pragma: no cover
+    trange = range
+
+import logging
+
+logger = logging.getLogger(__name__)
+
+ScanTypes = (0, -1, 1)  # ScanType.OPT, LOW, HIGH (contrast_gan_3D/alias.py:24-27)
+
+
+class Trainer:
+    def __init__(self, train_iterations: int, val_iterations: int, validate_every: int, train_generator_every: int,
+                 train_critic_every: int, log_every: int, log_images_every: int, generator_class: partial,
+                 critic_class: partial, generator_optim_class: partial, critic_optim_class: partial,
+                 hu_loss_instance: nn.Module, logger_interface, device: torch.device, debug: bool = False,
+                 checkpoint_dir: Optional[Union[str, Path]] = None, weight_clip: Optional[float] = None,
+                 generator_lr_scheduler_class: Optional[partial] = None,
+                 critic_lr_scheduler_class: Optional[partial] = None, hu_loss_weight: float = 1.0,
+                 sim_loss_weight: float = 1.0, gan_loss_weight: float = 1.0, gp_weight: float = 10,
+                 checkpoint_every: Optional[int] = 1000, rng: Optional[np.random.Generator] = None):
+        self.rng = rng
+        self.device = torch.device(device)
+        self.debug = debug
+        self.train_log_sample_size, self.val_log_sample_size = None, None
+        self.train_iterations, self.val_iterations = train_iterations, val_iterations
+        self.val_every = validate_every
+        self.train_generator_every, self.train_critic_every = train_generator_every, train_critic_every
+        self.log_every, self.log_images_every = log_every, log_images_every
+        self.hu_loss_w, self.sim_loss_w, self.gan_loss_w = hu_loss_weight, sim_loss_weight, gan_loss_weight
+        self.gp_w, self.weight_clip = gp_weight, weight_clip
+        if weight_clip is not None:
+            raise NotImplementedError("weight-clipping WGAN (BatchNorm critic) is SURVEY.md §8f row 4; "
+                                      "the HIP step implements the gradient-penalty configuration")
+
+        self.generator: nn.Module = generator_class().to(self.device)
+        g_h = adam_hyper_from_partial(generator_optim_class)
+        self.optimizer_G = FusedAdam(Arena(self.generator, self.device), **g_h)
+        self.lr_scheduler_G = generator_lr_scheduler_class(self.optimizer_G) if generator_lr_scheduler_class else None
+
+        self.critic: nn.Module = critic_class().to(self.device)
+        d_h = adam_hyper_from_partial(critic_optim_class)
+        self.optimizer_D = FusedAdam(Arena(self.critic, self.device), **d_h)
+        self.lr_scheduler_D = critic_lr_scheduler_class(self.optimizer_D) if critic_lr_scheduler_class else None
+
+        self.loss_GAN = WassersteinLoss()
+        self.loss_similarity = ZNCCLoss()
+        self.loss_HU = hu_loss_instance
+        self.logger_interface = logger_interface
+        self.engine: Optional[StepEngine] = None
+
+        self.iteration = 0
+        self.checkpoint_every = checkpoint_every
+        self.checkpoint_dir = checkpoint_dir
+        if self.checkpoint_dir is not None:
+            self.checkpoint_dir = Path(self.checkpoint_dir)
+            self.checkpoint_dir.mkdir(exist_ok=True, parents=True)
+            self.load_checkpoint(_find_latest_checkpoint(self.checkpoint_dir))
+
+    # ------------------------------------------------------------------------------------------
+    def _engine_for(self, b_opt: int, b_sub: int, dims) -> StepEngine:
+        e = self.engine
+        if e is None or (e.b_opt, e.b_sub, e.dims) != (b_opt, b_sub, tuple(dims)):
+            lo, hi = _hu_bounds(self.loss_HU)
+            self.engine = StepEngine(self.generator, self.critic, self.generator.config, self.critic.config, b_opt,
+                                     b_sub, tuple(dims), gp_weight=float(self.gp_w), hu_bounds=(lo, hi),
+                                     gan_w=self.gan_loss_w, sim_w=self.sim_loss_w, hu_w=self.hu_loss_w,
+                                     device=self.device, g_optim=self.optimizer_G, d_optim=self.optimizer_D)
+        return self.engine
+
+    def _losses(self, keys) -> Dict[str, Tensor]:
+        slots = {"D": L.L_D, "G": L.L_G, "G-full": L.L_GFULL, "sim": L.L_SIM, "HU": L.L_HU}
+        return {k: self.engine.losses[slots[k]] for k in keys}
+
+    def train_critic(self, real: Tensor, reconstructions: Tensor, retain_graph: bool) -> Dict[str, Tensor]:
+        """Critic update (Trainer.py:108-142) on the engine's resident batch."""
+        self.optimizer_D.sync_hyper()
+        self.engine.critic_update()
+        if self.lr_scheduler_D is not None:
+            self.lr_scheduler_D.step()
+        return self._losses(["D"])
+
+    def train_generator(self, inputs: Tensor, reconstructions: Tensor, centerlines_masks: Tensor
+                        ) -> Dict[str, Tensor]:
+        """Generator update (Trainer.py:144-161) on the engine's resident batch."""
+        self.optimizer_G.sync_hyper()
+        self.engine.generator_update()
+        if self.lr_scheduler_G is not None:
+            self.lr_scheduler_G.step()
+        return self._losses(["G", "G-full", "sim", "HU"])
+
+    def train_step(self, patches: List[dict], iteration: int):
+        opt, low, high = patches
+        b_opt, b_sub = len(opt["data"]), len(low["data"]) + len(high["data"])
+        dims = tuple(opt["data"].shape[2:])
+        eng = self._engine_for(b_opt, b_sub, dims)
+        # host -> HBM into the resident slots (Trainer.py:165-167,182-183)
+        eng.xc[:b_opt].view(-1).copy_(opt["data"].reshape(-1), non_blocking=True)
+        nl = low["data"].numel()
+        eng.subopt.view(-1)[:nl].copy_(low["data"].reshape(-1), non_blocking=True)
+        eng.subopt.view(-1)[nl:].copy_(high["data"].reshape(-1), non_blocking=True)
+        do_g = iteration % self.train_generator_every == 0
+        if do_g:
+            ml = low["seg"].numel()
+            eng.mask.view(-1)[:ml].copy_(low["seg"].reshape(-1), non_blocking=True)
+            eng.mask.view(-1)[ml:].copy_(high["seg"].reshape(-1), non_blocking=True)
+        # eps ~ U[0,1) per interpolated sample, drawn on the device (model/utils.py:26)
+        eng.eps.uniform_(0.0, 1.0)
+        eng.generator_forward()
+        log_dict = {}
+        if iteration % self.train_critic_every == 0:
+            log_dict = self.train_critic(None, None, do_g)
+        if do_g:
+            log_dict |= self.train_generator(None, None, None)
+
+        if iteration % self.log_every == 0:
+            self.logger_interface.logger.log_loss({k: v.mean() for k, v in log_dict.items()}, iteration, "train")
+        if iteration % self.log_images_every == 0:
+            self.maybe_set_log_images_sample_size("train", patches[0]["data"].shape)
+            cut = len(low["data"])
+            opt_hat = eng.opt_hat.view(b_sub, 1, *dims)
+            att = eng.G.att.view(b_sub, 1, *dims)
+            self.logger_interface(patches, [None, opt_hat[:cut], opt_hat[cut:]], [None, att[:cut], att[cut:]],
+                                  _scan_types(), iteration, "train", self.train_log_sample_size)
+        return log_dict
+
+    def fit(self, train_loaders, val_loaders, profiler=None):
+        self.generator.train()
+        self.critic.train()
+        augmenters = {"train": train_loaders, "val": val_loaders}
+        self._manage_augmenters(augmenters, "start")
+        for iteration in trange(self.iteration, self.train_iterations):
+            patches = [next(train_loaders[st]) for st in ScanTypes]
+            self.train_step(patches, iteration)
+            if self.val_every is not None and iteration != 0 and iteration % self.val_every == 0:
+                self.validate(val_loaders, iteration)
+            if self.checkpoint_every is not None and iteration != 0 and iteration % self.checkpoint_every == 0:
+                self.save_checkpoint(iteration)
+            if profiler:
+                profiler.step()
+        if profiler:
+            profiler.stop()
+        if self.checkpoint_every is not None:
+            self.save_checkpoint(self.train_iterations)
+        self._manage_augmenters(augmenters, "end")
+        self.logger_interface.end_hook()
+
+    @torch.no_grad()
+    def validate(self, val_loaders, train_iteration: int):
+        """Eval-mode pass (Trainer.py:247-308): running-stat BN, no gradients."""
+        self.critic.eval()
+        self.generator.eval()
+        z = torch.zeros(4, dtype=torch.float32, device=self.device)
+        loss_sim, loss_G, loss_real_C, loss_fake_C = z.chunk(4)
+        loggable = []
+        for i in range(self.val_iterations):
+            for st in ScanTypes:
+                batch = next(val_loaders[st])
+                sample = batch["data"].to(self.device, non_blocking=True)
+                if st == 0:
+                    loss_real_C -= self.loss_GAN(self.critic(sample))
+                else:
+                    attenuation = self.generator(sample)
+                    sample_hat = sample - attenuation
+                    loss_fake = self.loss_GAN(self.critic(sample_hat))
+                    loss_fake_C += loss_fake
+                    loss_G -= loss_fake
+                    loss_sim += self.loss_similarity(sample_hat, sample)
+                    if i == 0 and loggable is not None:
+                        loggable.append([batch, sample_hat, attenuation])
+                        if len(loggable) == 2:
+                            patches, recs, atts = list(zip(*loggable))
+                            self.maybe_set_log_images_sample_size("val", patches[0]["data"].shape)
+                            self.logger_interface(patches, list(recs), list(atts), _scan_types()[1:],
+                                                  train_iteration, "validation", self.val_log_sample_size)
+                            loggable = None
+        self.critic.train()
+        self.generator.train()
+        val_loss = {"D": (loss_real_C + loss_fake_C) / self.val_iterations,
+                    "G": loss_G / (self.val_iterations * 2), "sim": loss_sim / (self.val_iterations * 2)}
+        self.logger_interface.logger.log_loss(val_loss, train_iteration, "validation")
+        return val_loss
+
+    @property
+    def model_torch_attrs(self) -> List[str]:
+        return ["generator", "optimizer_G", "lr_scheduler_G", "discriminator", "critic", "optimizer_D",
+                "lr_scheduler_D"]
+
+    def save_checkpoint(self, iteration: int):
+        state = {"iteration": iteration}
+        for attr in self.model_torch_attrs:
+            el = getattr(self, attr, None)
+            state[attr] = el if el is None else el.state_dict()
+        torch.save(state, self.checkpoint_dir / f"{iteration}.pt")
+        logger.info("Checkpoint iteration %d", iteration)
+
+    def load_checkpoint(self, ckpt_path: Optional[Path]):
+        if ckpt_path is not None and Path(ckpt_path).is_file():
+            logger.info("Resuming run from '%s'", str(ckpt_path))
+            checkpoint: dict = torch.load(ckpt_path, map_location="cpu", weights_only=True)
+            for k, v in checkpoint.items():
+                if k in self.model_torch_attrs:
+                    if v is not None and getattr(self, k, None) is not None:
+                        getattr(self, k).load_state_dict(v)
+                else:
+                    setattr(self, k, v)
+        logger.info("Starting from iteration %d", self.iteration)
+
+    def _manage_augmenters(self, augmenters, event: str):
+        assert event in ["start", "end"], f"Unknown event {event!r}"
+        for mode, d in augmenters.items():
+            if mode == "val" and self.val_every is None:
+                continue
+            for aug in d.values():
+                if event == "start" and hasattr(aug, "restart"):
+                    aug.restart()
+                elif hasattr(aug, "_finish"):
+                    aug._finish()
+
+    def maybe_set_log_images_sample_size(self, mode: str, batch_shape):
+        attr = f"{mode}_log_sample_size"
+        if getattr(self, attr) is None:
+            bs = batch_shape[-1 if len(batch_shape) == 5 else 0]
+            setattr(self, attr, min(bs, 64))
+
+
+def _hu_bounds(hu_loss) -> tuple:
+    if hasattr(hu_loss, "lo"):
+        return float(hu_loss.lo), float(hu_loss.hi)
+    if hasattr(hu_loss, "min_HU"):  # the reference's HULoss stores full constant tensors (loss.py:51-56)
+        return float(hu_loss.min_HU.reshape(-1)[0]), float(hu_loss.max_HU.reshape(-1)[0])
+    raise TypeError("hu_loss_instance must be a HULoss")
+
+
+def _scan_types():
+    try:
+        from contrast_gan_3D.alias import ScanType  # the caller's enum when running under train.py
+        return list(ScanType)
+    except Exception:
+        return list(ScanTypes)
+
+
+def _find_latest_checkpoint(d: Path) -> Optional[Path]:
+    """``<int>.pt`` with the largest iteration (trainer/utils.py:26-34)."""
+    cands = [p for p in Path(d).glob("*.pt") if p.stem.isdigit()]
+    return max(cands, key=lambda p: int(p.stem)) if cands else None
