@@ -258,12 +258,15 @@ def trainable(p: Dict[str, Tensor]) -> List[str]:
 
 def train_step(gp_: Dict[str, Tensor], dp: Dict[str, Tensor], g_opt: AdamState, d_opt: AdamState,
                opt: Tensor, subopt: Tensor, mask: Tensor, eps: Optional[Tensor], cfg: StepConfig,
-               record: Optional[dict] = None) -> Dict[str, float]:
+               record: Optional[dict] = None, after_critic=None) -> Dict[str, float]:
     """Trainer.train_step (Trainer.py:163-203) with both updates on this iteration.
 
     ``gp_``/``dp``: generator / critic state dicts (modified in place: params, BN buffers).
     Returns the reference's log_dict values {"D", "G", "G-full", "sim", "HU"}.
     ``record`` (optional) receives the gradients each optimiser step consumed.
+    ``after_critic`` (optional, tests) is called with the critic state dict after its update, so a
+    checker can substitute the device's updated critic and compare the generator update alone
+    (Adam's first steps are ~lr*sign(g), which amplifies last-bit gradient differences).
     """
     gkeys, dkeys = trainable(gp_), trainable(dp)
     for k in gkeys:
@@ -290,6 +293,8 @@ def train_step(gp_: Dict[str, Tensor], dp: Dict[str, Tensor], g_opt: AdamState, 
         if cfg.weight_clip is not None:
             for k in dkeys:
                 dp[k].clamp_(-cfg.weight_clip, cfg.weight_clip)
+        if after_critic is not None:
+            after_critic(dp)
     # generator update (Trainer.py:144-161), with the updated critic
     loss_g = cfg.gan_w * -wasserstein(critic_forward(dp, opt_hat, cfg.critic))
     loss_sim = cfg.sim_w * zncc_loss(opt_hat, subopt)

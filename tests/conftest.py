@@ -41,16 +41,19 @@ def golden():
     return load
 
 
-def assert_close(actual, expected, rtol=1e-3, name=""):
+def assert_close(actual, expected, rtol=1e-3, name="", atol=0.0):
     """Parity bar (north_star: 'within 1e-3 relative fp32 tolerance'), scale-aware:
-    max|a-e| <= rtol * max(|e|, tiny) and ||a-e||_2 <= rtol * ||e||_2."""
+    max|a-e| <= rtol * max|e| + atol and ||a-e||_2 <= rtol * ||e||_2 + atol * sqrt(n).
+    ``atol`` is only for quantities that are exactly zero in real arithmetic (e.g. the critic's
+    last bias gradient, d/db [mean(D(fake)) - mean(D(real))] = 1 - 1)."""
     import numpy as np
     a = np.asarray(actual, dtype=np.float64)
     e = np.asarray(expected, dtype=np.float64)
     assert a.shape == e.shape, f"{name}: shape {a.shape} != {e.shape}"
     scale = max(float(np.abs(e).max()) if e.size else 0.0, 1e-30)
     err = float(np.abs(a - e).max()) if e.size else 0.0
-    nrm = float(np.linalg.norm(e)) or 1e-30
-    rel2 = float(np.linalg.norm(a - e)) / nrm
-    assert err <= rtol * scale and rel2 <= rtol, (
-        f"{name}: max abs err {err:.3e} (scale {scale:.3e}), rel L2 {rel2:.3e} > {rtol}")
+    nrm = float(np.linalg.norm(e))
+    dif = float(np.linalg.norm(a - e))
+    ok = err <= rtol * scale + atol and dif <= rtol * nrm + atol * np.sqrt(max(e.size, 1))
+    assert ok, (f"{name}: max abs err {err:.3e} (scale {scale:.3e}), rel L2 {dif / (nrm or 1e-30):.3e} "
+                f"> {rtol} (atol {atol})")

@@ -96,8 +96,12 @@ def test_step_matches_oracle_64(S, b):
     from cgan3d_amd.data.synthetic import synth_patches
     g_args = dict(n_resnet_blocks=4, n_updownsample_blocks=2, init_channels_out=16)
     g, d = _models(g_args)
-    gpar = {k: v.detach().cpu().clone() for k, v in g.state_dict().items()}
-    dpar = {k: v.detach().cpu().clone() for k, v in d.state_dict().items()}
+    # the checker runs in float64: at 64^3 the weight-gradient reductions span ~10^6 terms with
+    # heavy cancellation (BatchNorm backward makes sum(dz) ~ 0), where a float32 CPU reference is
+    # itself only good to a few 1e-3; the device result is held to 1e-3 of the exact value
+    dbl = lambda v: v.detach().cpu().clone().double() if v.is_floating_point() else v.detach().cpu().clone()  # noqa
+    gpar = {k: dbl(v) for k, v in g.state_dict().items()}
+    dpar = {k: dbl(v) for k, v in d.state_dict().items()}
     eng = _engine(g, d, b, S, 1e-4, 0.0, 0.9)
     cfg = R.StepConfig(gen=R.GenConfig(**g_args), critic=R.CriticConfig())
     gopt, dopt = R.AdamState(1e-4, 0.0, 0.9), R.AdamState(1e-4, 0.0, 0.9)
@@ -105,15 +109,33 @@ def test_step_matches_oracle_64(S, b):
         opt, _ = synth_patches(b, S, 10 + it)
         sub, seg = synth_patches(b, S, 20 + it)
         eps = np.random.Generator(np.random.PCG64(30 + it)).random((b, 1, 1, 1, 1)).astype(np.float32)
-        rec = {}
-        ref = R.train_step(gpar, dpar, gopt, dopt, torch.from_numpy(opt), torch.from_numpy(sub),
-                           torch.from_numpy(seg), torch.from_numpy(eps), cfg, record=rec)
         eng.load_inputs(torch.from_numpy(opt).cuda(), torch.from_numpy(sub).cuda(), torch.from_numpy(seg).cuda(),
                         torch.from_numpy(eps).cuda())
-        eng.step()
+        eng.generator_forward()
+        eng.critic_update()
+        d_after = {k: v.detach().cpu().clone() for k, v in d.state_dict().items()}
+        eng.generator_update()
+        rec = {}
+
+        def use_device_critic(dp):
+            for k in dp:
+                dp[k].data.copy_(d_after[k])
+        ref = R.train_step(gpar, dpar, gopt, dopt, torch.from_numpy(opt).double(), torch.from_numpy(sub).double(),
+                           torch.from_numpy(seg), torch.from_numpy(eps).double(), cfg, record=rec,
+                           after_critic=use_device_critic)
         losses = eng.losses.cpu().numpy()
         for k, slot in (("D", 0), ("G", 3), ("sim", 4), ("HU", 5), ("G-full", 6)):
             assert_close(losses[slot], ref[k], 1e-3, f"it{it} {k}")
         for net, arena in (("G", eng.g_arena), ("D", eng.d_arena)):
             for k, gv in arena.gviews.items():
-                assert_close(gv.cpu().numpy(), rec[net][k].numpy(), 1e-3, f"it{it} grad {net} {k}")
+                atol = 1e-7 if k == "model.last.bias" else 0.0  # exactly 0 in real arithmetic
+                assert_close(gv.cpu().numpy(), rec[net][k].numpy(), 1e-3, f"it{it} grad {net} {k}", atol=atol)
+        # start the next iteration from the device's state (params, BN buffers, Adam moments)
+        for k, v in g.state_dict().items():
+            gpar[k].copy_(v.detach().cpu())
+        for k, v in d.state_dict().items():
+            dpar[k].copy_(v.detach().cpu())
+        for st, opt_ in ((gopt, eng.g_optim), (dopt, eng.d_optim)):
+            for k, p in zip(opt_.arena.names, opt_.arena.params):
+                st.exp_avg[k] = opt_.state[p]["exp_avg"].detach().cpu().double()
+                st.exp_avg_sq[k] = opt_.state[p]["exp_avg_sq"].detach().cpu().double()
