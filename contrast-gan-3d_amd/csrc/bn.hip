@@ -116,23 +116,31 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const float* __restr
   }
 }
 
-// fp64 combine of the partials -> dgamma, dbeta and the apply coefficients
-__global__ void bn_bwd_finalize_kernel(const float* __restrict__ part, int nblk, int C, long long nvox,
-                                       const float* __restrict__ gamma, const float* __restrict__ mi, float* dgamma,
-                                       float* dbeta, float* coef) {
-  const int c = threadIdx.x;
-  if (c >= C) return;
+// fp64 combine of the partials -> dgamma, dbeta and the apply coefficients (one block per channel)
+__global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(const float* __restrict__ part, int nblk, int C,
+                                                              long long nvox, const float* __restrict__ gamma,
+                                                              const float* __restrict__ mi, float* dgamma,
+                                                              float* dbeta, float* coef) {
+  __shared__ double red[2][4];
+  const int c = blockIdx.x, tid = threadIdx.x;
   double s0 = 0.0, s1 = 0.0;
-  for (int b = 0; b < nblk; ++b) {
+  for (int b = tid; b < nblk; b += blockDim.x) {
     s0 += part[(long long)b * 2 * C + c];
     s1 += part[(long long)b * 2 * C + C + c];
   }
-  if (dbeta) dbeta[c] = (float)s0;
-  if (dgamma) dgamma[c] = (float)s1;
-  const float k1 = gamma[c] * mi[C + c];
-  coef[c] = k1;
-  coef[C + c] = (float)(s0 / (double)nvox);
-  coef[2 * C + c] = (float)(s1 / (double)nvox);
+  s0 = wave_sum_d(s0);
+  s1 = wave_sum_d(s1);
+  if ((tid & 63) == 0) { red[0][tid >> 6] = s0; red[1][tid >> 6] = s1; }
+  __syncthreads();
+  if (tid == 0) {
+    s0 = red[0][0] + red[0][1] + red[0][2] + red[0][3];
+    s1 = red[1][0] + red[1][1] + red[1][2] + red[1][3];
+    if (dbeta) dbeta[c] = (float)s0;
+    if (dgamma) dgamma[c] = (float)s1;
+    coef[c] = gamma[c] * mi[C + c];
+    coef[C + c] = (float)(s0 / (double)nvox);
+    coef[2 * C + c] = (float)(s1 / (double)nvox);
+  }
 }
 
 // dz = gamma*invstd*(dyh - mean(dyh) - xhat*mean(dyh*xhat))
@@ -165,12 +173,16 @@ __global__ __launch_bounds__(256) void channel_sum_kernel(const float* __restric
   }
 }
 
-__global__ void channel_sum_finalize_kernel(const float* __restrict__ part, int nblk, int C, float* out) {
-  const int c = threadIdx.x;
-  if (c >= C) return;
+__global__ __launch_bounds__(256) void channel_sum_finalize_kernel(const float* __restrict__ part, int nblk, int C,
+                                                                   float* out) {
+  __shared__ double red[4];
+  const int c = blockIdx.x, tid = threadIdx.x;
   double s = 0.0;
-  for (int b = 0; b < nblk; ++b) s += part[(long long)b * C + c];
-  out[c] = (float)s;
+  for (int b = tid; b < nblk; b += blockDim.x) s += part[(long long)b * C + c];
+  s = wave_sum_d(s);
+  if ((tid & 63) == 0) red[tid >> 6] = s;
+  __syncthreads();
+  if (tid == 0) out[c] = (float)(red[0] + red[1] + red[2] + red[3]);
 }
 
 static int reduce_blocks(long long total) {
@@ -225,7 +237,7 @@ extern "C" int cgan3d_bn_backward(const float* dy, const float* z, int64_t nvox,
   hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(nblk), dim3(256), 0, s, dy, z, total, c, scale_shift, mean_invstd,
                      act, slope, part);
   CG_LAUNCH_CHECK("bn_bwd_reduce_kernel");
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(1), dim3(256), 0, s, part, nblk, c, (long long)nvox, gamma,
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(c), dim3(256), 0, s, part, nblk, c, (long long)nvox, gamma,
                      mean_invstd, dgamma, dbeta, coef);
   CG_LAUNCH_CHECK("bn_bwd_finalize_kernel");
   int blocks = (int)std::min<long long>((total + 255) / 256, 4096);
@@ -247,7 +259,7 @@ extern "C" int cgan3d_channel_sum(const float* x, int64_t nvox, int32_t c, float
   const int nblk = reduce_blocks(total);
   hipLaunchKernelGGL(channel_sum_kernel, dim3(nblk), dim3(256), 0, s, x, total, c, ws);
   CG_LAUNCH_CHECK("channel_sum_kernel");
-  hipLaunchKernelGGL(channel_sum_finalize_kernel, dim3(1), dim3(256), 0, s, ws, nblk, c, out);
+  hipLaunchKernelGGL(channel_sum_finalize_kernel, dim3(c), dim3(256), 0, s, ws, nblk, c, out);
   CG_LAUNCH_CHECK("channel_sum_finalize_kernel");
   return CGAN3D_OK;
 }

@@ -55,4 +55,21 @@ __device__ __forceinline__ int reflect_idx(int i, int n) {
 
 inline int ceil_div(long long a, long long b) { return (int)((a + b - 1) / b); }
 
+// device-side view of cgan3d_epilogue
+struct Epi {
+  const float* bias;
+  const float* residual;
+  const float* mask_src;
+  const float* minuend;
+  float* out2;
+  float* stats;
+  int act;
+  float slope;
+};
+
+// specialised k = 7 generator first/last conv kernels (conv_k7.hip); return 1 when they apply
+int k7_try_fwd(const cgan3d_conv_geom* g, const float* x, const float* w, float* y, const Epi& e, hipStream_t s);
+int k7_try_wgrad(const cgan3d_conv_geom* g, const float* x, const float* go, float* dw, hipStream_t s);
+long long k7_n2w_blocks(const cgan3d_conv_geom* g);
+
 }  // namespace cg

@@ -24,17 +24,6 @@ struct ConvArgs {
   int nclass;
 };
 
-struct Epi {
-  const float* bias;
-  const float* residual;
-  const float* mask_src;
-  const float* minuend;
-  float* out2;
-  float* stats;
-  int act;
-  float slope;
-};
-
 static bool make_args(const cgan3d_conv_geom* g, ConvArgs* a, int bm) {
   a->n = g->n; a->di = g->di; a->hi = g->hi; a->wi = g->wi;
   a->do_ = g->do_; a->ho = g->ho; a->wo = g->wo; a->cin = g->cin; a->cout = g->cout;
@@ -586,6 +575,7 @@ static Epi to_epi(const cgan3d_epilogue* ep) {
 extern "C" int64_t cgan3d_conv3d_stats_floats(const cgan3d_conv_geom* g) {
   ConvArgs a;
   if (!g || !make_args(g, &a, 64)) return -1;
+  if (long long kb = k7_n2w_blocks(g)) return (int64_t)kb * (2 * g->cout + 1);
   return (int64_t)a.nclass * a.tiles_per_class * (2 * g->cout + 1);
 }
 
@@ -597,6 +587,10 @@ extern "C" int cgan3d_conv3d_fwd(const cgan3d_conv_geom* g, const float* x, cons
   Epi e = to_epi(ep);
   CG_CHECK_ARG(!(e.out2 && (!e.minuend || g->cout != 1)), "cgan3d_conv3d_fwd: out2 needs minuend and cout==1");
   hipStream_t s = (hipStream_t)stream;
+  if (k7_try_fwd(g, x, w, y, e, s)) {
+    CG_LAUNCH_CHECK("k7 conv");
+    return CGAN3D_OK;
+  }
   if (g->cout == 1) {
     CG_CHECK_ARG(!e.stats, "cgan3d_conv3d_fwd: stats unsupported for cout==1");
     ConvArgs a;
@@ -650,6 +644,17 @@ extern "C" int cgan3d_conv3d_wgrad(const cgan3d_conv_geom* g, const float* gathe
   const int T = g->k * g->k * g->k;
   const long long R = (long long)T * g->cin;
   const long long V = (long long)g->n * g->do_ * g->ho * g->wo;
+  if (g->k == 7 && g->stride == 1 && (g->cin == 1 || g->cout == 1)) {
+    if (!accumulate && hipMemsetAsync(dw, 0, R * g->cout * sizeof(float), s) != hipSuccess) {
+      set_error("cgan3d_conv3d_wgrad: memset failed");
+      return CGAN3D_EHIP;
+    }
+    if (k7_try_wgrad(g, gathered, aligned, dw, s)) {
+      CG_LAUNCH_CHECK("k7 wgrad");
+      return CGAN3D_OK;
+    }
+    CG_CHECK_ARG(!accumulate, "cgan3d_conv3d_wgrad: internal dispatch error");
+  }
   if (hipMemsetAsync(ws, 0, R * g->cout * sizeof(float), s) != hipSuccess) {
     set_error("cgan3d_conv3d_wgrad: memset failed");
     return CGAN3D_EHIP;

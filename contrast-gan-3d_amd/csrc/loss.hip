@@ -124,11 +124,15 @@ __global__ __launch_bounds__(256) void gen_pass1_kernel(const float* __restrict_
 }
 
 // means -> stat[0..3] = s_mean, t_mean, mask_sum, hu_sum
-__global__ void gen_fin1_kernel(const double* __restrict__ part, int nblk, long long n, double* stat) {
-  if (threadIdx.x < 4) {
-    double acc = 0;
-    for (int b = 0; b < nblk; ++b) acc += part[b * 4 + threadIdx.x];
-    stat[threadIdx.x] = threadIdx.x < 2 ? acc / (double)n : acc;
+__global__ __launch_bounds__(256) void gen_fin1_kernel(const double* __restrict__ part, int nblk, long long n,
+                                                       double* stat) {
+  __shared__ double red[4];
+  double a[4] = {0, 0, 0, 0};
+  for (int b = threadIdx.x; b < nblk; b += blockDim.x)
+    for (int q = 0; q < 4; ++q) a[q] += part[b * 4 + q];
+  for (int q = 0; q < 4; ++q) a[q] = block_sum_d(a[q], red);
+  if (threadIdx.x == 0) {
+    stat[0] = a[0] / (double)n; stat[1] = a[1] / (double)n; stat[2] = a[2]; stat[3] = a[3];
   }
 }
 
@@ -153,13 +157,15 @@ __global__ __launch_bounds__(256) void gen_pass2_kernel(const float* __restrict_
 }
 
 // losses + gradient coefficients: stat[4..] = A (w coef), Bc (u coef), w_mean, hu_scale
-__global__ void gen_fin2_kernel(const double* __restrict__ part, int nblk, long long n, float sim_w, float hu_w,
-                                double* stat, float* losses) {
+__global__ __launch_bounds__(256) void gen_fin2_kernel(const double* __restrict__ part, int nblk, long long n,
+                                                       float sim_w, float hu_w, double* stat, float* losses) {
+  __shared__ double red[4];
+  double a[4] = {0, 0, 0, 0};
+  for (int b = threadIdx.x; b < nblk; b += blockDim.x)
+    for (int q = 0; q < 4; ++q) a[q] += part[b * 4 + q];
+  for (int q = 0; q < 4; ++q) a[q] = block_sum_d(a[q], red);
   if (threadIdx.x != 0) return;
-  double suw = 0, suu = 0, sww = 0, sw = 0;
-  for (int b = 0; b < nblk; ++b) {
-    suw += part[b * 4 + 0]; suu += part[b * 4 + 1]; sww += part[b * 4 + 2]; sw += part[b * 4 + 3];
-  }
+  const double suw = a[0], suu = a[1], sww = a[2], sw = a[3];
   const double nn = (double)n;
   const double cc = suw / nn;
   const double ss = sqrt(suu / (nn - 1.0)), st = sqrt(sww / (nn - 1.0));  // torch.std (unbiased)
@@ -263,11 +269,11 @@ extern "C" int cgan3d_generator_output_grad(const float* opt_hat, const float* s
   const int nblk = red_blocks(n);
   hipLaunchKernelGGL(gen_pass1_kernel, dim3(nblk), dim3(256), 0, s, opt_hat, subopt, mask, (long long)n, lo, hi, part);
   CG_LAUNCH_CHECK("gen_pass1_kernel");
-  hipLaunchKernelGGL(gen_fin1_kernel, dim3(1), dim3(64), 0, s, part, nblk, (long long)n, stat);
+  hipLaunchKernelGGL(gen_fin1_kernel, dim3(1), dim3(256), 0, s, part, nblk, (long long)n, stat);
   CG_LAUNCH_CHECK("gen_fin1_kernel");
   hipLaunchKernelGGL(gen_pass2_kernel, dim3(nblk), dim3(256), 0, s, opt_hat, subopt, (long long)n, stat, part);
   CG_LAUNCH_CHECK("gen_pass2_kernel");
-  hipLaunchKernelGGL(gen_fin2_kernel, dim3(1), dim3(64), 0, s, part, nblk, (long long)n, sim_w, hu_w, stat, losses);
+  hipLaunchKernelGGL(gen_fin2_kernel, dim3(1), dim3(256), 0, s, part, nblk, (long long)n, sim_w, hu_w, stat, losses);
   CG_LAUNCH_CHECK("gen_fin2_kernel");
   int blocks = (int)std::min<long long>((n + 255) / 256, 4096);
   hipLaunchKernelGGL(gen_grad_kernel, dim3(blocks), dim3(256), 0, s, opt_hat, subopt, att, mask, d_critic,

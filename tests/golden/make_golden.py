@@ -182,8 +182,12 @@ class _NullLogger:
         pass
 
 
-def train_steps(tag, g_args, gp: bool, S, b_opt, b_low, b_high, iters, seed, save_final_g=True):
-    """Trainer.train_step (Trainer.py:163-203) with train_{critic,generator}_every = 1."""
+def train_steps(tag, g_args, gp: bool, S, b_opt, b_low, b_high, iters, seed, save_final_g=True,
+                dtype=torch.float32, save=True):
+    """Trainer.train_step (Trainer.py:163-203) with train_{critic,generator}_every = 1.
+
+    ``dtype=torch.float64`` runs the reference itself in double precision (modules ``.double()``,
+    inputs in double): the exact-arithmetic yardstick for the parity tests."""
     d_extra = dict(norm_layer=torch.nn.Identity) if gp else {}
     lr, betas = (1e-4, (0.0, 0.9)) if gp else (2e-4, (0.5, 0.999))
     lo, hi = scaled_hu_bounds()
@@ -199,6 +203,13 @@ def train_steps(tag, g_args, gp: bool, S, b_opt, b_low, b_high, iters, seed, sav
         weight_clip=None if gp else 0.01, checkpoint_every=None)
     pcg64_init_(tr.generator, 0)
     pcg64_init_(tr.critic, 1)
+    if dtype != torch.float32:
+        tr.generator.to(dtype)
+        tr.critic.to(dtype)
+        tr.optimizer_G = partial(torch.optim.Adam, lr=lr, betas=betas)(tr.generator.parameters())
+        tr.optimizer_D = partial(torch.optim.Adam, lr=lr, betas=betas)(tr.critic.parameters())
+        tr.loss_HU.min_HU = tr.loss_HU.min_HU.to(dtype)  # loss.py:51-56 constants
+        tr.loss_HU.max_HU = tr.loss_HU.max_HU.to(dtype)
     out = {}
     grads = {"G": [], "D": []}
 
@@ -223,9 +234,10 @@ def train_steps(tag, g_args, gp: bool, S, b_opt, b_low, b_high, iters, seed, sav
         low = low - 0.3  # hypo-enhanced (LOW) / hyper-enhanced (HIGH) flavour
         high = high + 0.3
         eps = torch.from_numpy(rngs.random((min(b_opt, b_low + b_high), 1, 1, 1, 1)).astype(np.float32))
-        patches = [{"data": torch.from_numpy(opt)},
-                   {"data": torch.from_numpy(low), "seg": torch.from_numpy(low_seg)},
-                   {"data": torch.from_numpy(high), "seg": torch.from_numpy(high_seg)}]
+        patches = [{"data": torch.from_numpy(opt).to(dtype)},
+                   {"data": torch.from_numpy(low).to(dtype), "seg": torch.from_numpy(low_seg)},
+                   {"data": torch.from_numpy(high).to(dtype), "seg": torch.from_numpy(high_seg)}]
+        eps = eps.to(dtype)
         logged = {}
         orig_c, orig_g = tr.train_critic, tr.train_generator
 
@@ -260,6 +272,15 @@ def train_steps(tag, g_args, gp: bool, S, b_opt, b_low, b_high, iters, seed, sav
     out.update(sd_np(tr.critic, "final/D/"))
     meta = dict(S=S, b_opt=b_opt, b_low=b_low, b_high=b_high, iters=iters, gp=int(gp), lr=lr,
                 beta1=betas[0], beta2=betas[1], **{f"g_{k}": v for k, v in g_args.items()})
+    if not save:
+        return out
+    if dtype == torch.float32:
+        # iteration 0 once more in float64 (identical start state): the exact-arithmetic yardstick
+        o64 = train_steps(tag, g_args, gp, S, b_opt, b_low, b_high, 1, seed, dtype=torch.float64, save=False)
+        for k, v in o64.items():
+            if k.startswith("it0/grad/") or k.startswith("it0/loss/"):
+                out[k.replace("it0/grad/", "it0/grad64/").replace("it0/loss/", "it0/loss64/")] = \
+                    np.asarray(v, dtype=np.float32)
     np.savez_compressed(HERE / f"step_{tag}.npz", torch_version=torch.__version__,
                         meta=np.array(repr(meta)), **out)
 

@@ -1,0 +1,163 @@
+"""Per-op parity of the HIP convolution kernels against torch (CPU, float64), every role and shape
+family the step uses (forward / input-grad / weight-grad of Conv3d and ConvTranspose3d, reflect and
+zero padding, the k7 single-channel kernels), including sizes that leave partial tiles.
+
+Tolerance 1e-3 relative (north_star); the kernels accumulate in fp32.
+"""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from conftest import assert_close
+
+pytestmark = pytest.mark.gpu
+
+CONV_CASES = [
+    # cin, cout, k, s, p, reflect, spatial
+    (1, 16, 7, 1, 3, True, (12, 20, 36)),    # generator first conv (k7 n2w kernel)
+    (16, 1, 7, 1, 3, True, (12, 20, 36)),    # generator last conv (k7 w2n kernel)
+    (1, 8, 7, 1, 3, True, (8, 8, 8)),
+    (8, 1, 7, 1, 3, True, (8, 8, 8)),
+    (16, 32, 3, 2, 1, False, (12, 16, 20)),  # downsampling
+    (64, 64, 3, 1, 1, False, (6, 8, 10)),    # resnet block
+    (1, 8, 4, 2, 1, False, (16, 16, 16)),    # critic first
+    (8, 16, 4, 2, 1, False, (16, 16, 16)),   # critic middle
+    (64, 1, 4, 1, 1, False, (4, 4, 4)),      # critic last
+    (12, 20, 3, 1, 1, False, (5, 6, 7)),     # odd channel counts (generic path)
+]
+
+
+def _ref_conv(x, w, s, p, reflect):
+    if reflect:
+        return F.conv3d(F.pad(x, (p,) * 6, mode="reflect"), w, stride=s)
+    return F.conv3d(x, w, stride=s, padding=p)
+
+
+def _cl(t):  # NCDHW -> NDHWC contiguous fp32 on the GPU
+    return t.permute(0, 2, 3, 4, 1).contiguous().float().cuda()
+
+
+def _ncdhw(t):
+    return t.permute(0, 4, 1, 2, 3).double().cpu()
+
+
+@pytest.mark.parametrize("cin,cout,k,s,p,reflect,sp", CONV_CASES)
+def test_conv3d_fwd_dgrad_wgrad(cin, cout, k, s, p, reflect, sp):
+    from cgan3d_amd import ops
+    g = torch.Generator().manual_seed(cin * 100 + cout + k)
+    n = 2
+    x = torch.randn(n, cin, *sp, generator=g, dtype=torch.float64)
+    w = torch.randn(cout, cin, k, k, k, generator=g, dtype=torch.float64) / np.sqrt(cin * k**3)
+    x.requires_grad_(True)
+    w.requires_grad_(True)
+    y = _ref_conv(x, w, s, p, reflect)
+    gy = torch.randn(y.shape, generator=g, dtype=torch.float64)
+    dx, dw = torch.autograd.grad(y, (x, w), gy)
+    din, dout = tuple(sp), tuple(y.shape[2:])
+    wd = w.detach().float().cuda()
+    # forward
+    yo = torch.empty(n, *dout, cout, device="cuda")
+    ops.conv(ops.conv_fwd_geom(n, din, dout, cin, cout, k, s, p, reflect), _cl(x.detach()), wd, yo)
+    assert_close(_ncdhw(yo).numpy(), y.detach().numpy(), 1e-3, "fwd")
+    # weight grad
+    dwo = torch.empty_like(wd)
+    gw = ops.conv_wgrad_geom(n, din, dout, cin, cout, k, s, p, reflect)
+    ws = torch.empty(ops.wgrad_ws_floats(gw), device="cuda")
+    ops.wgrad(gw, _cl(x.detach()), _cl(gy), dwo, ws)
+    assert_close(dwo.double().cpu().numpy(), dw.numpy(), 1e-3, "wgrad")
+    # input grad (zero padding directly; reflect via the padded grid + fold, as the engine does)
+    if reflect:
+        pd = tuple(d + 2 * p for d in din)
+        gd = ops.conv_dgrad_geom(n, pd, dout, cin, cout, k, s, 0)
+        dpad = torch.empty(n, *pd, cin, device="cuda")
+        ops.conv(gd, _cl(gy), wd, dpad)
+        dxo = torch.empty(n, *din, cin, device="cuda")
+        ops.reflect_fold(dpad, dxo, n, din, cin, p)
+    else:
+        gd = ops.conv_dgrad_geom(n, din, dout, cin, cout, k, s, p)
+        if any(d % s for d in din):
+            pytest.skip("input-grad in the transposed mapping needs dims divisible by the stride")
+        dxo = torch.empty(n, *din, cin, device="cuda")
+        ops.conv(gd, _cl(gy), wd, dxo)
+    assert_close(_ncdhw(dxo).numpy(), dx.numpy(), 1e-3, "dgrad")
+
+
+@pytest.mark.parametrize("cin,cout,sp", [(64, 32, (4, 6, 8)), (32, 16, (8, 8, 8)), (12, 8, (3, 5, 4))])
+def test_conv_transpose3d_fwd_dgrad_wgrad(cin, cout, sp):
+    from cgan3d_amd import ops
+    g = torch.Generator().manual_seed(cin + cout)
+    n, k, s, p, op = 2, 3, 2, 1, 1
+    x = torch.randn(n, cin, *sp, generator=g, dtype=torch.float64, requires_grad=True)
+    w = (torch.randn(cin, cout, k, k, k, generator=g, dtype=torch.float64) / np.sqrt(cout * k**3)).requires_grad_()
+    y = F.conv_transpose3d(x, w, stride=s, padding=p, output_padding=op)
+    gy = torch.randn(y.shape, generator=g, dtype=torch.float64)
+    dx, dw = torch.autograd.grad(y, (x, w), gy)
+    din, dout = tuple(sp), tuple(y.shape[2:])
+    wd = w.detach().float().cuda()
+    yo = torch.empty(n, *dout, cout, device="cuda")
+    ops.conv(ops.convt_fwd_geom(n, din, dout, cin, cout, k, s, p), _cl(x.detach()), wd, yo)
+    assert_close(_ncdhw(yo).numpy(), y.detach().numpy(), 1e-3, "convT fwd")
+    dxo = torch.empty(n, *din, cin, device="cuda")
+    ops.conv(ops.convt_dgrad_geom(n, din, dout, cin, cout, k, s, p), _cl(gy), wd, dxo)
+    assert_close(_ncdhw(dxo).numpy(), dx.numpy(), 1e-3, "convT dgrad")
+    gw = ops.convt_wgrad_geom(n, din, dout, cin, cout, k, s, p)
+    ws = torch.empty(ops.wgrad_ws_floats(gw), device="cuda")
+    dwo = torch.empty_like(wd)
+    ops.wgrad(gw, _cl(gy), _cl(x.detach()), dwo, ws)
+    assert_close(dwo.double().cpu().numpy(), dw.numpy(), 1e-3, "convT wgrad")
+
+
+@pytest.mark.parametrize("c", [16, 32])
+def test_batchnorm_train_forward_backward(c):
+    """BN fwd (stats from the conv epilogue) + ReLU + backward vs torch autograd."""
+    from cgan3d_amd import ops, _lib as L
+    g = torch.Generator().manual_seed(c)
+    n, sp = 2, (8, 12, 16)
+    x = torch.randn(n, 8, *sp, generator=g, dtype=torch.float64)
+    w = torch.randn(c, 8, 3, 3, 3, generator=g, dtype=torch.float64) / 10
+    gamma = torch.rand(c, generator=g, dtype=torch.float64) + 0.5
+    beta = torch.randn(c, generator=g, dtype=torch.float64) * 0.1
+    z = F.conv3d(x, w, padding=1).requires_grad_()
+    gm, bt = gamma.clone().requires_grad_(), beta.clone().requires_grad_()
+    rm, rv = torch.zeros(c, dtype=torch.float64), torch.ones(c, dtype=torch.float64)
+    y = F.relu(F.batch_norm(z, rm, rv, gm, bt, training=True, momentum=0.1, eps=1e-5))
+    gy = torch.randn(y.shape, generator=g, dtype=torch.float64)
+    dz, dgm, dbt = torch.autograd.grad(y, (z, gm, bt), gy)
+    geo = ops.conv_fwd_geom(n, sp, sp, 8, c, 3, 1, 1)
+    zd = torch.empty(n, *sp, c, device="cuda")
+    stats = torch.empty(ops.stats_floats(geo), device="cuda")
+    ops.conv(geo, _cl(x), w.float().cuda(), zd, ops.epilogue(stats=stats))
+    ss, mi = torch.empty(2 * c, device="cuda"), torch.empty(2 * c, device="cuda")
+    rmd, rvd = torch.zeros(c, device="cuda"), torch.ones(c, device="cuda")
+    nbt = torch.zeros((), dtype=torch.int64, device="cuda")
+    gmd, btd = gamma.float().cuda(), beta.float().cuda()
+    ops.bn_finalize(stats, stats.numel() // (2 * c + 1), c, gmd, btd, rmd, rvd, nbt, ss, mi)
+    nvox = n * sp[0] * sp[1] * sp[2]
+    yd = torch.empty_like(zd)
+    ops.bn_apply(zd, nvox, c, ss, L.ACT_RELU, yd)
+    assert_close(_ncdhw(yd).numpy(), y.detach().numpy(), 1e-3, "bn fwd")
+    assert_close(rmd.cpu().numpy(), rm.numpy(), 1e-3, "running_mean")
+    assert_close(rvd.cpu().numpy(), rv.numpy(), 1e-3, "running_var")
+    assert int(nbt.item()) == 1
+    dzd, dgd, dbd = torch.empty_like(zd), torch.empty(c, device="cuda"), torch.empty(c, device="cuda")
+    ws = torch.empty(ops.bn_backward_ws_floats(nvox, c), device="cuda")
+    ops.bn_backward(_cl(gy), zd, nvox, c, ss, mi, gmd, L.ACT_RELU, dgd, dbd, dzd, ws)
+    assert_close(_ncdhw(dzd).numpy(), dz.numpy(), 1e-3, "bn dz")
+    assert_close(dgd.double().cpu().numpy(), dgm.numpy(), 1e-3, "bn dgamma")
+    assert_close(dbd.double().cpu().numpy(), dbt.numpy(), 1e-3, "bn dbeta")
+
+
+def test_generator_forward_partial_tiles():
+    """Generator forward at sizes that leave partial tiles in every kernel (vs the fp64 oracle)."""
+    from oracle import reference_torch as R
+    from cgan3d_amd.model.generator import ResnetGenerator
+    from cgan3d_amd.model.init import pcg64_init_
+    g = pcg64_init_(ResnetGenerator(2, 2, 8), 0).cuda().train()
+    p = {k: (v.detach().cpu().double() if v.is_floating_point() else v.detach().cpu().clone())
+         for k, v in g.state_dict().items()}
+    x = torch.randn(2, 1, 12, 20, 36, generator=torch.Generator().manual_seed(5))
+    with torch.no_grad():
+        y = g(x.cuda())
+        yr = R.generator_forward(p, x.double(), R.GenConfig(2, 2, 8), training=True)
+    assert_close(y.double().cpu().numpy(), yr.numpy(), 1e-3, "G(x) partial tiles")

@@ -9,7 +9,7 @@ import numpy as np
 import pytest
 import torch
 
-from conftest import assert_close
+from conftest import assert_close, assert_parity
 
 pytestmark = pytest.mark.gpu
 
@@ -50,12 +50,18 @@ def test_step_matches_reference_fixture(golden, tag):
         eng.step()
         losses = eng.losses.cpu().numpy()
         for k in ("D", "G", "sim", "HU", "G-full"):
-            assert_close(losses[names[k]], f[f"it{it}/loss/{k}"], 1e-3, f"it{it} loss {k}")
+            if f"it{it}/loss64/{k}" in f:
+                assert_parity(losses[names[k]], f[f"it{it}/loss/{k}"], f[f"it{it}/loss64/{k}"], f"it{it} loss {k}")
+            else:
+                assert_close(losses[names[k]], f[f"it{it}/loss/{k}"], 1e-3, f"it{it} loss {k}")
         for net, arena in (("G", eng.g_arena), ("D", eng.d_arena)):
             for k, gv in arena.gviews.items():
                 key = f"it{it}/grad/{net}/{k}"
-                if key in f:
-                    assert_close(gv.cpu().numpy(), f[key], 1e-3, key)
+                atol = 1e-7 if k == "model.last.bias" else 0.0  # exactly 0 in real arithmetic
+                if key in f and key.replace("/grad/", "/grad64/") in f:
+                    assert_parity(gv.cpu().numpy(), f[key], f[key.replace("/grad/", "/grad64/")], key, atol=atol)
+                elif key in f:
+                    assert_close(gv.cpu().numpy(), f[key], 1e-3, key, atol=atol)
     for net, mod in (("G", g), ("D", d)):
         sd = mod.state_dict()
         for k in f:
@@ -115,21 +121,32 @@ def test_step_matches_oracle_64(S, b):
         eng.critic_update()
         d_after = {k: v.detach().cpu().clone() for k, v in d.state_dict().items()}
         eng.generator_update()
-        rec = {}
-
         def use_device_critic(dp):
             for k in dp:
                 dp[k].data.copy_(d_after[k])
+
+        # the same step through the oracle in float32 (the reference's precision) and float64
+        g32 = {k: v.float() if v.is_floating_point() else v.clone() for k, v in gpar.items()}
+        d32 = {k: v.float() for k, v in dpar.items()}
+        o32 = R.AdamState(1e-4, 0.0, 0.9, exp_avg={k: v.float() for k, v in gopt.exp_avg.items()},
+                          exp_avg_sq={k: v.float() for k, v in gopt.exp_avg_sq.items()}, step=gopt.step)
+        od32 = R.AdamState(1e-4, 0.0, 0.9, exp_avg={k: v.float() for k, v in dopt.exp_avg.items()},
+                           exp_avg_sq={k: v.float() for k, v in dopt.exp_avg_sq.items()}, step=dopt.step)
+        rec32, rec = {}, {}
+        ref32 = R.train_step(g32, d32, o32, od32, torch.from_numpy(opt), torch.from_numpy(sub),
+                             torch.from_numpy(seg), torch.from_numpy(eps), cfg, record=rec32,
+                             after_critic=use_device_critic)
         ref = R.train_step(gpar, dpar, gopt, dopt, torch.from_numpy(opt).double(), torch.from_numpy(sub).double(),
                            torch.from_numpy(seg), torch.from_numpy(eps).double(), cfg, record=rec,
                            after_critic=use_device_critic)
         losses = eng.losses.cpu().numpy()
         for k, slot in (("D", 0), ("G", 3), ("sim", 4), ("HU", 5), ("G-full", 6)):
-            assert_close(losses[slot], ref[k], 1e-3, f"it{it} {k}")
+            assert_parity(losses[slot], ref32[k], ref[k], f"it{it} {k}")
         for net, arena in (("G", eng.g_arena), ("D", eng.d_arena)):
             for k, gv in arena.gviews.items():
                 atol = 1e-7 if k == "model.last.bias" else 0.0  # exactly 0 in real arithmetic
-                assert_close(gv.cpu().numpy(), rec[net][k].numpy(), 1e-3, f"it{it} grad {net} {k}", atol=atol)
+                assert_parity(gv.cpu().numpy(), rec32[net][k].numpy(), rec[net][k].numpy(), f"it{it} grad {net} {k}",
+                              atol=atol)
         # start the next iteration from the device's state (params, BN buffers, Adam moments)
         for k, v in g.state_dict().items():
             gpar[k].copy_(v.detach().cpu())
