@@ -25,7 +25,15 @@ class ConvGeom(C.Structure):
                 ("do_", C.c_int32), ("ho", C.c_int32), ("wo", C.c_int32),
                 ("cin", C.c_int32), ("cout", C.c_int32), ("k", C.c_int32), ("stride", C.c_int32),
                 ("pad", C.c_int32), ("transposed", C.c_int32), ("reflect", C.c_int32),
-                ("w_sa", C.c_int64), ("w_sb", C.c_int64)]
+                ("w_sa", C.c_int64), ("w_sb", C.c_int64), ("w_packed", C.c_int32), ("prec", C.c_int32)]
+
+
+class PackDesc(C.Structure):
+    _fields_ = [("w", C.c_void_p), ("wp", C.c_void_p), ("sa", C.c_int64), ("sb", C.c_int64),
+                ("taps", C.c_int32), ("cin", C.c_int32), ("cout", C.c_int32), ("ldb", C.c_int32)]
+
+
+PREC_F32, PREC_BF16 = 0, 1
 
 
 class Epilogue(C.Structure):
@@ -40,6 +48,9 @@ _SIGS = {
     "cgan3d_get_last_error": ([], C.c_char_p),
     "cgan3d_conv3d_stats_floats": ([_P], _I64),
     "cgan3d_conv3d_fwd": ([_P, _P, _P, _P, _P, _P], _I32),
+    "cgan3d_packed_weight_floats": ([_P], _I64),
+    "cgan3d_pack_weights": ([_P, _P, _P, _P], _I32),
+    "cgan3d_pack_weights_multi": ([_P, _I32, _I64, _P], _I32),
     "cgan3d_conv3d_wgrad_ws_floats": ([_P], _I64),
     "cgan3d_conv3d_wgrad": ([_P, _P, _P, _P, _I32, _P, _P], _I32),
     "cgan3d_bn_finalize": ([_P, _I64, _I32, _P, _P, _P, _P, _P, _F, _F, _P, _P, _P], _I32),

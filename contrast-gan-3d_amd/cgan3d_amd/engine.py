@@ -102,10 +102,11 @@ class _GLayer:
 class GeneratorPlan:
     """Buffers + launch geometry of ResnetGenerator (model/generator.py:9-90) for a batch shape."""
 
-    def __init__(self, cfg, n: int, dims: Dims, device):
+    def __init__(self, cfg, n: int, dims: Dims, device, P: Dict[str, torch.Tensor], prec: int = L.PREC_F32):
         c0 = cfg.init_channels_out
         self.n, self.dims, self.device = n, tuple(dims), device
         self.timer = None
+        self.packs = ops.PackSet(device)  # packed [tap][cin][cout] weight copies, refreshed per update
         layers: List[_GLayer] = [_GLayer("conv", "model.first", 7, 1, 3, True, 1, c0, dims, dims)]
         d = tuple(dims)
         for i in range(cfg.n_updownsample_blocks):
@@ -131,7 +132,7 @@ class GeneratorPlan:
         def buf(dd, c):
             return torch.empty((n, *dd, c), device=device, dtype=torch.float32)
 
-        self.geo_fwd, self.geo_dgrad, self.geo_wgrad = [], [], []
+        self.geo_fwd, self.geo_dgrad, self.geo_wgrad, self.wf, self.wd = [], [], [], [], []
         self.z, self.y, self.dy, self.dz, self.stats, self.ss, self.mi, self.nstat = [], [], [], [], [], [], [], []
         ws = 0
         for ly in layers:
@@ -143,6 +144,11 @@ class GeneratorPlan:
                 gf = ops.convt_fwd_geom(n, ly.din, ly.dout, ly.cin, ly.cout, ly.k, ly.s, ly.p)
                 gd = ops.convt_dgrad_geom(n, ly.din, ly.dout, ly.cin, ly.cout, ly.k, ly.s, ly.p)
                 gw = ops.convt_wgrad_geom(n, ly.din, ly.dout, ly.cin, ly.cout, ly.k, ly.s, ly.p)
+            wt = P[f"{ly.name}.conv.weight"]
+            gf, wf = self.packs.add(gf, wt, prec)
+            gd, wd = self.packs.add(gd, wt, prec)
+            self.wf.append(wf)
+            self.wd.append(wd)
             self.geo_fwd.append(gf)
             self.geo_dgrad.append(gd)
             self.geo_wgrad.append(gw)
@@ -167,6 +173,11 @@ class GeneratorPlan:
         self.dpad = buf(pd, la.cin)
         ws = max(ws, ops.wgrad_ws_floats(self.geo_last_wgrad), ops.channel_sum_ws_floats(n * la.dout[0] * la.dout[1] * la.dout[2], 1))
         self.ws = torch.empty(ws, device=device)
+        self.pack()
+
+    def pack(self):
+        """Refresh the packed weight copies (one launch); call after every weight update."""
+        self.packs.pack()
 
     # -- forward: x [n,D,H,W,1] -> att (tanh output); opt_hat_out = x - att (Trainer.py:170-171)
     def forward(self, P: Dict[str, torch.Tensor], x: torch.Tensor, opt_hat_out: Optional[torch.Tensor] = None,
@@ -177,7 +188,7 @@ class GeneratorPlan:
             if ly.name.endswith("block0"):
                 h_res = h
             stats = self.stats[i] if training else None
-            ops.conv(self.geo_fwd[i], h, P[f"{ly.name}.conv.weight"], self.z[i], ops.epilogue(stats=stats))
+            ops.conv(self.geo_fwd[i], h, self.wf[i], self.z[i], ops.epilogue(stats=stats))
             nb = f"{ly.name}.normalization"
             if training:
                 ops.bn_finalize(self.stats[i], self.nstat[i], ly.cout, P[f"{nb}.weight"], P[f"{nb}.bias"],
@@ -233,8 +244,7 @@ class GeneratorPlan:
                 break
             # input-grad; a ResNet block0 also receives the skip gradient dL/dh_{r+1}
             res = self.dy[i + 1] if ly.name.endswith("block0") else None
-            ops.conv(self.geo_dgrad[i], self.dz[i], P[f"{ly.name}.conv.weight"], self.dy[i - 1],
-                     ops.epilogue(residual=res))
+            ops.conv(self.geo_dgrad[i], self.dz[i], self.wd[i], self.dy[i - 1], ops.epilogue(residual=res))
 
 
 # ----------------------------------------------------------------------------------------------
@@ -254,8 +264,9 @@ class CriticPlan:
     """Buffers + geometry of PatchGANDiscriminator (model/discriminator.py:9-84), GP conf
     (Identity norm, gradient_penalty_conf.py:14), for up to ``nmax`` samples."""
 
-    def __init__(self, cfg, nmax: int, dims: Dims, device):
+    def __init__(self, cfg, nmax: int, dims: Dims, device, P: Dict[str, torch.Tensor], prec: int = L.PREC_F32):
         self.cfg, self.nmax, self.dims, self.device = cfg, nmax, tuple(dims), device
+        self.prec = prec
         c0, s = cfg.init_channels_out, cfg.negative_slope
         self.slope = s
         d = tuple(dims)
@@ -282,6 +293,24 @@ class CriticPlan:
             ws = max(ws, ops.wgrad_ws_floats(g),
                      ops.channel_sum_ws_floats(nmax * ly.dout[0] * ly.dout[1] * ly.dout[2], ly.cout))
         self.ws = torch.empty(ws, device=device)
+        # packed weight copies per (layer, role); the packed layout does not depend on batch/dims
+        self.packs = ops.PackSet(device)
+        self.wf, self.wd = [], []
+        for ly in ls:
+            w = P[f"{ly.name}.weight"]
+            gf, wf = self.packs.add(ops.conv_fwd_geom(nmax, ly.din, ly.dout, ly.cin, ly.cout, ly.k, ly.s, ly.p), w, prec)
+            gd, wd = self.packs.add(ops.conv_dgrad_geom(nmax, ly.din, ly.dout, ly.cin, ly.cout, ly.k, ly.s, ly.p), w,
+                                    prec)
+            self.wf.append(wf if gf.w_packed else None)
+            self.wd.append(wd if gd.w_packed else None)
+        self.pack()
+
+    def pack(self):
+        """Refresh the packed weight copies (one launch); call after every weight update."""
+        self.packs.pack()
+
+    def _geo(self, g, packed):
+        return ops.with_packing(g, self.prec) if packed is not None else g
 
     def _sl(self, t, off, n):
         return t[off:off + n]
@@ -290,11 +319,11 @@ class CriticPlan:
         """a_l[off:off+n] = critic activations of x (n samples); logits in a[-1]."""
         h = x
         for i, ly in enumerate(self.layers):
-            g = ops.conv_fwd_geom(n, ly.din, ly.dout, ly.cin, ly.cout, ly.k, ly.s, ly.p)
+            g = self._geo(ops.conv_fwd_geom(n, ly.din, ly.dout, ly.cin, ly.cout, ly.k, ly.s, ly.p), self.wf[i])
             last = i == len(self.layers) - 1
             ep = ops.epilogue(bias=P[f"{ly.name}.bias"], act=L.ACT_NONE if last else L.ACT_LRELU, slope=self.slope)
             out = self._sl(self.a[i], off, n)
-            ops.conv(g, h, P[f"{ly.name}.weight"], out, ep)
+            ops.conv(g, h, self.wf[i] if self.wf[i] is not None else P[f"{ly.name}.weight"], out, ep)
             h = out
         return self._sl(self.a[-1], off, n)
 
@@ -303,22 +332,25 @@ class CriticPlan:
         [dx_off, dx_off+dx_n) (absolute indices inside the batch) into dx_out."""
         for i in range(len(self.layers) - 1, 0, -1):
             ly = self.layers[i]
-            g = ops.conv_dgrad_geom(n, ly.din, ly.dout, ly.cin, ly.cout, ly.k, ly.s, ly.p)
-            ops.conv(g, self._sl(self.dz[i], off, n), P[f"{ly.name}.weight"], self._sl(self.dz[i - 1], off, n),
+            g = self._geo(ops.conv_dgrad_geom(n, ly.din, ly.dout, ly.cin, ly.cout, ly.k, ly.s, ly.p), self.wd[i])
+            w = self.wd[i] if self.wd[i] is not None else P[f"{ly.name}.weight"]
+            ops.conv(g, self._sl(self.dz[i], off, n), w, self._sl(self.dz[i - 1], off, n),
                      ops.epilogue(mask_src=self._sl(self.a[i - 1], off, n), slope=self.slope))
         ly = self.layers[0]
         if dx_n > 0:
-            g = ops.conv_dgrad_geom(dx_n, ly.din, ly.dout, ly.cin, ly.cout, ly.k, ly.s, ly.p)
-            ops.conv(g, self._sl(self.dz[0], dx_off, dx_n), P[f"{ly.name}.weight"], dx_out)
+            g = self._geo(ops.conv_dgrad_geom(dx_n, ly.din, ly.dout, ly.cin, ly.cout, ly.k, ly.s, ly.p), self.wd[0])
+            w = self.wd[0] if self.wd[0] is not None else P[f"{ly.name}.weight"]
+            ops.conv(g, self._sl(self.dz[0], dx_off, dx_n), w, dx_out)
 
     def gp_forward_mode(self, P, gamma: torch.Tensor, off: int, n: int):
         """nu_l = mask_l * conv_l(nu_{l-1}) (no bias), nu_0 = gamma, written in place over
         a_l[off:off+n] (after the masks there have been consumed)."""
         h = gamma
         for i, ly in enumerate(self.layers[:-1]):
-            g = ops.conv_fwd_geom(n, ly.din, ly.dout, ly.cin, ly.cout, ly.k, ly.s, ly.p)
+            g = self._geo(ops.conv_fwd_geom(n, ly.din, ly.dout, ly.cin, ly.cout, ly.k, ly.s, ly.p), self.wf[i])
             out = self._sl(self.a[i], off, n)
-            ops.conv(g, h, P[f"{ly.name}.weight"], out, ops.epilogue(mask_src=out, slope=self.slope))
+            w = self.wf[i] if self.wf[i] is not None else P[f"{ly.name}.weight"]
+            ops.conv(g, h, w, out, ops.epilogue(mask_src=out, slope=self.slope))
             h = out
 
     def weight_grads(self, P, G, x_all: torch.Tensor, n_all: int, n_bias: int):
@@ -339,7 +371,7 @@ class StepEngine:
     def __init__(self, generator, critic, g_cfg, d_cfg, b_opt: int, b_sub: int, dims: Dims, *,
                  g_hyper: Sequence[float] = (1e-4, 0.0, 0.9, 1e-8), d_hyper: Sequence[float] = (1e-4, 0.0, 0.9, 1e-8),
                  gp_weight: float = 10.0, hu_bounds=(112.0 / 600.0, 212.0 / 600.0), gan_w=1.0, sim_w=1.0, hu_w=1.0,
-                 device=None, g_optim=None, d_optim=None, process_group=None):
+                 device=None, g_optim=None, d_optim=None, process_group=None, precision: str = "f32"):
         if b_opt != b_sub:
             raise NotImplementedError("StepEngine: the GP path assumes |OPT| == |LOW|+|HIGH| (basic_conf.py:74-79)")
         if d_cfg.norm != "identity":
@@ -351,9 +383,11 @@ class StepEngine:
         self.vox = dims[0] * dims[1] * dims[2]
         self.gp_weight, self.gan_w, self.sim_w, self.hu_w = gp_weight, gan_w, sim_w, hu_w
         self.lo, self.hi = hu_bounds
-        self.G = GeneratorPlan(g_cfg, b_sub, dims, device)
         nmax = b_opt + b_sub + self.b_gp
-        self.D = CriticPlan(d_cfg, nmax, dims, device)
+        if precision not in ("f32", "bf16"):
+            raise ValueError(f"precision must be 'f32' or 'bf16', got {precision!r}")
+        self.precision = precision
+        prec = L.PREC_BF16 if precision == "bf16" else L.PREC_F32
         from .trainer.optim import FusedAdam
         if g_optim is None:
             lr, b1, b2, eps = g_hyper
@@ -372,6 +406,9 @@ class StepEngine:
         self.gP.update({k: v for k, v in generator.state_dict(keep_vars=True).items() if k not in self.gP})
         self.dP = dict(self.d_arena.views)
         self.gG, self.dG = self.g_arena.gviews, self.d_arena.gviews
+        # plans after the arenas: their packed-weight descriptors point at the arena storage
+        self.G = GeneratorPlan(g_cfg, b_sub, dims, device, self.gP, prec)
+        self.D = CriticPlan(d_cfg, nmax, dims, device, self.dP, prec)
         # critic input slots [real | fake(opt_hat) | interpolation -> gamma]
         self.xc = torch.empty((nmax, *dims, 1), device=device)
         self.subopt = torch.empty((b_sub, *dims, 1), device=device)
@@ -410,6 +447,7 @@ class StepEngine:
         D.weight_grads(self.dP, self.dG, self.xc, nall, bo + bs)
         self._allreduce(self.d_arena.grad)  # on the critical path: the G update uses the new critic
         self.d_optim.launch()
+        self.D.pack()
 
     def generator_update(self):
         D, bs, V = self.D, self.b_sub, self.vox
@@ -421,6 +459,7 @@ class StepEngine:
         self.G.backward(self.gP, self.gG, self.subopt)
         self._allreduce(self.g_arena.grad)
         self.g_optim.launch()
+        self.G.pack()
 
     def _allreduce(self, flat_grad: torch.Tensor):
         """Mean of the per-rank gradients (RCCL over xGMI with the nccl backend; gloo on CPU)."""

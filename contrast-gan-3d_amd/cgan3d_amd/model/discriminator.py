@@ -67,7 +67,7 @@ class PatchGANDiscriminator(nn.Module):
 
     def plan_for(self, n, dims):
         from ..engine import CriticPlan
-        return CriticPlan(self.config, n, tuple(dims), self.model.first.conv.weight.device)
+        return CriticPlan(self.config, n, tuple(dims), self.model.first.conv.weight.device, self._tensors())
 
     def forward(self, x: Tensor) -> Tensor:
         if self._unsupported:

@@ -67,9 +67,10 @@ class ResnetGenerator(nn.Module):
 
     def plan_for(self, n, dims, fresh=False):
         from ..engine import GeneratorPlan
-        key = (n, tuple(dims), self.model.first.conv.weight.device)
+        # the plan's packed-weight descriptors hold raw parameter addresses: rebuild if they moved
+        key = (n, tuple(dims), self.model.first.conv.weight.device, tuple(p.data_ptr() for p in self.parameters()))
         if fresh or self._plan is None or self._plan[0] != key:
-            plan = GeneratorPlan(self.config, n, tuple(dims), key[2])
+            plan = GeneratorPlan(self.config, n, tuple(dims), key[2], self._tensors())
             if fresh:
                 return plan
             self._plan = (key, plan)
@@ -85,6 +86,7 @@ class ResnetGenerator(nn.Module):
             return _GeneratorFn.apply(x, self, *params)
         n, _, *dims = x.shape
         plan = self.plan_for(n, dims)
+        plan.pack()  # weights may have changed since the plan was built
         xc = x.detach().float().contiguous().view(n, *dims, 1)
         plan.forward(self._tensors(), xc, training=self.training)
         return plan.att.clone().view(n, 1, *dims)

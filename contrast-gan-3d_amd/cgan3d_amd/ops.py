@@ -17,7 +17,7 @@ from typing import Optional, Sequence
 import torch
 
 from . import _lib as L
-from ._lib import ConvGeom, Epilogue, check, ptr
+from ._lib import ConvGeom, Epilogue, PackDesc, check, ptr
 
 DRY_RUN = False
 
@@ -30,7 +30,76 @@ def _geom(n, di, do, cin, cout, k, s, p, transposed, reflect, sa, sb) -> ConvGeo
     g.cin, g.cout, g.k, g.stride, g.pad = cin, cout, k, s, p
     g.transposed, g.reflect = int(transposed), int(reflect)
     g.w_sa, g.w_sb = sa, sb
+    g.w_packed, g.prec = 0, L.PREC_F32
     return g
+
+
+def uses_gemm(g: ConvGeom) -> bool:
+    """True when cgan3d_conv3d_fwd routes this geometry to the implicit-GEMM kernel (which can read
+    packed weights and run in bf16); k7 single-channel and cout == 1 launches use direct kernels."""
+    if g.cout < 2:
+        return False
+    return not (g.k == 7 and g.stride == 1 and g.cin == 1 and g.cout in (8, 16))
+
+
+def with_packing(g: ConvGeom, prec: int = L.PREC_F32) -> ConvGeom:
+    """Copy of ``g`` that reads packed weights (cgan3d_pack_weights) and runs in ``prec``."""
+    h = ConvGeom()
+    ctypes.pointer(h)[0] = g
+    h.w_packed, h.prec = 1, prec
+    return h
+
+
+def packed_weight_floats(g: ConvGeom) -> int:
+    return int(L.load().cgan3d_packed_weight_floats(ctypes.byref(g)))
+
+
+def pack_desc(g: ConvGeom, w: torch.Tensor, wp: torch.Tensor) -> PackDesc:
+    _need(w, _w_extent(g), "pack w", exact=False)
+    _need(wp, packed_weight_floats(g), "pack wp")
+    d = PackDesc()
+    d.w, d.wp, d.sa, d.sb = ptr(w), ptr(wp), g.w_sa, g.w_sb
+    d.taps, d.cin, d.cout, d.ldb = g.k**3, g.cin, g.cout, (g.cout + 3) // 4 * 4
+    return d
+
+
+def pack_weights(g: ConvGeom, w: torch.Tensor, wp: torch.Tensor):
+    pack_desc(g, w, wp)
+    check(_launch("cgan3d_pack_weights", ctypes.byref(g), ptr(w), ptr(wp)), "pack_weights")
+
+
+def pack_weights_multi(descs_dev: torch.Tensor, n: int, max_total: int):
+    """descs_dev: device uint8 tensor holding n PackDesc structs (built by PackSet)."""
+    if descs_dev.numel() != n * ctypes.sizeof(PackDesc):
+        raise ValueError("pack_weights_multi: descriptor buffer size mismatch")
+    check(_launch("cgan3d_pack_weights_multi", ptr(descs_dev), n, max_total), "pack_weights_multi")
+
+
+class PackSet:
+    """All packed weight copies of one network, refreshed by ONE launch after each optimiser step."""
+
+    def __init__(self, device):
+        self.device, self.descs, self.max_total = device, [], 0
+        self.dev = None
+
+    def add(self, g: ConvGeom, w: torch.Tensor, prec: int):
+        """Returns (geometry, weight) to launch with: packed when the GEMM path applies."""
+        if not uses_gemm(g):
+            return g, w
+        gp = with_packing(g, prec)
+        wp = torch.zeros(packed_weight_floats(gp), device=self.device)
+        self.descs.append((pack_desc(gp, w, wp), wp))
+        self.max_total = max(self.max_total, wp.numel())
+        self.dev = None
+        return gp, wp
+
+    def pack(self):
+        if not self.descs:
+            return
+        if self.dev is None:
+            raw = b"".join(bytes(d) for d, _ in self.descs)
+            self.dev = torch.frombuffer(bytearray(raw), dtype=torch.uint8).to(self.device)
+        pack_weights_multi(self.dev, len(self.descs), self.max_total)
 
 
 # --- geometry per role ------------------------------------------------------------------------
@@ -125,7 +194,12 @@ def stats_floats(g: ConvGeom) -> int:
 
 def conv(g: ConvGeom, x: torch.Tensor, w: torch.Tensor, y: torch.Tensor, ep: Optional[Epi] = None):
     _need(x, _vox_in(g) * g.cin, "conv x")
-    _need(w, _w_extent(g), "conv w", exact=False)
+    if g.w_packed:
+        if not uses_gemm(g):
+            raise ValueError("conv: packed weights only on the implicit-GEMM path")
+        _need(w, packed_weight_floats(g), "conv packed w")
+    else:
+        _need(w, _w_extent(g), "conv w", exact=False)
     ny = _vox_out(g) * g.cout
     _need(y, ny, "conv y")
     if ep is not None:

@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <type_traits>
 #include <cstdarg>
 #include <cstdint>
 #include <cstdio>
@@ -71,5 +72,8 @@ struct Epi {
 int k7_try_fwd(const cgan3d_conv_geom* g, const float* x, const float* w, float* y, const Epi& e, hipStream_t s);
 int k7_try_wgrad(const cgan3d_conv_geom* g, const float* x, const float* go, float* dw, hipStream_t s);
 long long k7_n2w_blocks(const cgan3d_conv_geom* g);
+// implicit-GEMM forward / input-grad (conv_gemm.hip)
+int gemm_blocks(const cgan3d_conv_geom* g, long long* mblocks);
+int gemm_launch(const cgan3d_conv_geom* g, const float* x, const float* w, float* y, const Epi& e, hipStream_t st);
 
 }  // namespace cg

@@ -86,216 +86,6 @@ __device__ __forceinline__ int gcoord(int base, int off, int n, int reflect) {
 }
 
 // ------------------------------------------------------------------------------------------
-// Forward / input-grad kernel (cout >= 2).  VEC = 4 when cin % 4 == 0, else 1.  NB = ceil(cout/16).
-template <int VEC, int NB>
-__global__ __launch_bounds__(256) void conv_mfma_kernel(ConvArgs a, const float* __restrict__ x,
-                                                        const float* __restrict__ w, float* y, Epi ep) {
-  constexpr int BM = 64, KC = 32, LD = KC + 4;
-  __shared__ __attribute__((aligned(16))) float As[BM * LD];
-  __shared__ __attribute__((aligned(16))) float Bs[64 * LD];
-  __shared__ int row_n[BM], row_b[3][BM], row_out[BM];
-  __shared__ int tab_off[3][KC], tab_ci[KC], tab_t[KC];
-
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int cls = blockIdx.x / a.tiles_per_class;
-  const int tile = blockIdx.x - cls * a.tiles_per_class;
-  const int s = a.s, k = a.k, p = a.p;
-  int rd = 0, rh = 0, rw = 0;
-  if (a.transposed) { rd = cls / (s * s); rh = (cls / s) % s; rw = cls % s; }
-  int fd, sd, nd, fh, sh, nh, fw, sw, nw;
-  class_taps(rd, k, s, p, a.transposed, &fd, &sd, &nd);
-  class_taps(rh, k, s, p, a.transposed, &fh, &sh, &nh);
-  class_taps(rw, k, s, p, a.transposed, &fw, &sw, &nw);
-  const int KT = nd * nh * nw * a.cin;
-  const long long v0 = (long long)tile * BM;
-
-  if (tid < BM) {
-    long long lin = v0 + tid;
-    if (lin < a.class_vox) {
-      int jw = (int)(lin % a.cw); long long t = lin / a.cw;
-      int jh = (int)(t % a.ch); t /= a.ch;
-      int jd = (int)(t % a.cd); int nb = (int)(t / a.cd);
-      int od, oh, ow;
-      if (a.transposed) {
-        od = jd * s + rd; oh = jh * s + rh; ow = jw * s + rw;
-        row_b[0][tid] = jd; row_b[1][tid] = jh; row_b[2][tid] = jw;
-      } else {
-        od = jd; oh = jh; ow = jw;
-        row_b[0][tid] = jd * s - p; row_b[1][tid] = jh * s - p; row_b[2][tid] = jw * s - p;
-      }
-      row_n[tid] = nb * a.di;
-      row_out[tid] = ((nb * a.do_ + od) * a.ho + oh) * a.wo + ow;
-    } else {
-      row_n[tid] = -1; row_out[tid] = -1;
-      row_b[0][tid] = row_b[1][tid] = row_b[2][tid] = 0;
-    }
-  }
-  __syncthreads();
-
-  f32x4 acc[NB];
-#pragma unroll
-  for (int n = 0; n < NB; ++n) acc[n] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  const int g = lane >> 4, r16 = lane & 15;
-  for (int kc0 = 0; kc0 < KT; kc0 += KC) {
-    if (tid < KC) {
-      int kk = kc0 + tid;
-      if (kk < KT) {
-        int j = kk / a.cin, ci = kk - j * a.cin;
-        int mw = j % nw; j /= nw;
-        int mh = j % nh, md = j / nh;
-        int td = fd + sd * md, th = fh + sh * mh, tw = fw + sw * mw;
-        if (a.transposed) {
-          tab_off[0][tid] = (rd + p - td) / s; tab_off[1][tid] = (rh + p - th) / s; tab_off[2][tid] = (rw + p - tw) / s;
-        } else {
-          tab_off[0][tid] = td; tab_off[1][tid] = th; tab_off[2][tid] = tw;
-        }
-        tab_ci[tid] = ci;
-        tab_t[tid] = (td * k + th) * k + tw;
-      } else {
-        tab_t[tid] = -1; tab_ci[tid] = 0;
-        tab_off[0][tid] = tab_off[1][tid] = tab_off[2][tid] = 0;
-      }
-    }
-    __syncthreads();
-    // A tile: gathered activations [64 voxels][32 k]
-    if (VEC == 4) {
-      const int e0 = (tid & 7) * 4;
-      const int tl = tab_t[e0];
-#pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        const int r = (tid >> 3) + 32 * i;
-        f32x4 v = {0.f, 0.f, 0.f, 0.f};
-        const int nb = row_n[r];
-        if (nb >= 0 && tl >= 0) {
-          int id = gcoord(row_b[0][r], tab_off[0][e0], a.di, a.reflect);
-          int ih = gcoord(row_b[1][r], tab_off[1][e0], a.hi, a.reflect);
-          int iw = gcoord(row_b[2][r], tab_off[2][e0], a.wi, a.reflect);
-          if ((id | ih | iw) >= 0) {
-            long long off = ((long long)((nb + id) * a.hi + ih) * a.wi + iw) * a.cin + tab_ci[e0];
-            v = *reinterpret_cast<const f32x4*>(x + off);
-          }
-        }
-        *reinterpret_cast<f32x4*>(&As[r * LD + e0]) = v;
-      }
-    } else {
-      const int e = tid & 31;
-      const int tl = tab_t[e];
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const int r = (tid >> 5) + 8 * i;
-        float v = 0.f;
-        const int nb = row_n[r];
-        if (nb >= 0 && tl >= 0) {
-          int id = gcoord(row_b[0][r], tab_off[0][e], a.di, a.reflect);
-          int ih = gcoord(row_b[1][r], tab_off[1][e], a.hi, a.reflect);
-          int iw = gcoord(row_b[2][r], tab_off[2][e], a.wi, a.reflect);
-          if ((id | ih | iw) >= 0)
-            v = x[((long long)((nb + id) * a.hi + ih) * a.wi + iw) * a.cin + tab_ci[e]];
-        }
-        As[r * LD + e] = v;
-      }
-    }
-    // B tile: weights [64 out channels][32 k]
-    {
-      const int co = tid >> 2;
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const int e = (tid & 3) * 8 + i;
-        const int tl = tab_t[e];
-        float v = 0.f;
-        if (co < a.cout && tl >= 0) v = w[(long long)tab_ci[e] * a.sa + (long long)co * a.sb + tl];
-        Bs[co * LD + e] = v;
-      }
-    }
-    __syncthreads();
-#pragma unroll
-    for (int q = 0; q < KC / 16; ++q) {
-      const f32x4 av = *reinterpret_cast<const f32x4*>(&As[(wave * 16 + r16) * LD + 16 * q + 4 * g]);
-#pragma unroll
-      for (int n = 0; n < NB; ++n) {
-        const f32x4 bv = *reinterpret_cast<const f32x4*>(&Bs[(16 * n + r16) * LD + 16 * q + 4 * g]);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) acc[n] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[e], bv[e], acc[n], 0, 0, 0);
-      }
-    }
-    __syncthreads();
-  }
-
-  // epilogue: lane holds rows 4g..4g+3 (of the wave's 16) for channel 16n + r16
-  float vals[NB][4];
-  bool rowv[4];
-  int rowo[4];
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    rowo[j] = row_out[wave * 16 + 4 * g + j];
-    rowv[j] = rowo[j] >= 0;
-  }
-#pragma unroll
-  for (int n = 0; n < NB; ++n) {
-    const int c = 16 * n + r16;
-    const bool cv = c < a.cout;
-    const float b = (ep.bias && cv) ? ep.bias[c] : 0.f;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      float v = acc[n][j] + b;
-      if (ep.act == CGAN3D_ACT_RELU) v = fmaxf(v, 0.f);
-      else if (ep.act == CGAN3D_ACT_LRELU) v = v > 0.f ? v : v * ep.slope;
-      else if (ep.act == CGAN3D_ACT_TANH) v = tanhf(v);
-      if (rowv[j] && cv) {
-        const long long o = (long long)rowo[j] * a.cout + c;
-        if (ep.mask_src) v = ep.mask_src[o] > 0.f ? v : v * ep.slope;
-        if (ep.residual) v += ep.residual[o];
-        y[o] = v;
-      }
-      vals[n][j] = (rowv[j] && cv) ? v : 0.f;
-    }
-  }
-
-  if (ep.stats) {
-    // per-block BatchNorm partials: (sum, M2 about the block mean, count)
-    float* red = As;  // reuse LDS: [4 waves][64 channels]
-    __shared__ float bmean[64];
-    int cnt = 0;
-    for (int r = 0; r < BM; ++r) cnt += row_out[r] >= 0;
-#pragma unroll
-    for (int n = 0; n < NB; ++n) {
-      float sum = vals[n][0] + vals[n][1] + vals[n][2] + vals[n][3];
-      sum += __shfl_xor(sum, 16, 64);
-      sum += __shfl_xor(sum, 32, 64);
-      if (g == 0) red[wave * 64 + 16 * n + r16] = sum;
-    }
-    __syncthreads();
-    if (tid < a.cout) {
-      float S = red[tid] + red[64 + tid] + red[128 + tid] + red[192 + tid];
-      bmean[tid] = cnt ? S / cnt : 0.f;
-      ep.stats[(long long)blockIdx.x * (2 * a.cout + 1) + tid] = S;
-    }
-    __syncthreads();
-#pragma unroll
-    for (int n = 0; n < NB; ++n) {
-      const int c = 16 * n + r16;
-      const float m = c < a.cout ? bmean[c] : 0.f;
-      float q = 0.f;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        float d = (rowv[j] && c < a.cout) ? vals[n][j] - m : 0.f;
-        q += d * d;
-      }
-      q += __shfl_xor(q, 16, 64);
-      q += __shfl_xor(q, 32, 64);
-      if (g == 0) red[wave * 64 + 16 * n + r16] = q;
-    }
-    __syncthreads();
-    if (tid < a.cout) {
-      float M2 = red[tid] + red[64 + tid] + red[128 + tid] + red[192 + tid];
-      ep.stats[(long long)blockIdx.x * (2 * a.cout + 1) + a.cout + tid] = M2;
-    }
-    if (tid == 0) ep.stats[(long long)blockIdx.x * (2 * a.cout + 1) + 2 * a.cout] = (float)cnt;
-  }
-}
-
-// ------------------------------------------------------------------------------------------
 // cout == 1 forward / input-grad (VALU): one thread per output voxel, weights in LDS.
 // Used by the generator's last conv (16 -> 1, k7 reflect, + bias, tanh, opt_hat = subopt - .)
 // and the critic's first-layer input-grad and last layer.
@@ -573,10 +363,11 @@ static Epi to_epi(const cgan3d_epilogue* ep) {
 }
 
 extern "C" int64_t cgan3d_conv3d_stats_floats(const cgan3d_conv_geom* g) {
-  ConvArgs a;
-  if (!g || !make_args(g, &a, 64)) return -1;
+  if (!g) return -1;
   if (long long kb = k7_n2w_blocks(g)) return (int64_t)kb * (2 * g->cout + 1);
-  return (int64_t)a.nclass * a.tiles_per_class * (2 * g->cout + 1);
+  long long mb = 0;
+  if (gemm_blocks(g, &mb)) return -1;
+  return (int64_t)mb * (2 * g->cout + 1);
 }
 
 extern "C" int cgan3d_conv3d_fwd(const cgan3d_conv_geom* g, const float* x, const float* w, float* y,
@@ -587,6 +378,8 @@ extern "C" int cgan3d_conv3d_fwd(const cgan3d_conv_geom* g, const float* x, cons
   Epi e = to_epi(ep);
   CG_CHECK_ARG(!(e.out2 && (!e.minuend || g->cout != 1)), "cgan3d_conv3d_fwd: out2 needs minuend and cout==1");
   hipStream_t s = (hipStream_t)stream;
+  CG_CHECK_ARG(!g->w_packed || (g->cout > 1 && !(g->k == 7 && g->stride == 1 && g->cin == 1)),
+               "cgan3d_conv3d_fwd: packed weights only for the implicit-GEMM path");
   if (k7_try_fwd(g, x, w, y, e, s)) {
     CG_LAUNCH_CHECK("k7 conv");
     return CGAN3D_OK;
@@ -601,19 +394,9 @@ extern "C" int cgan3d_conv3d_fwd(const cgan3d_conv_geom* g, const float* x, cons
     CG_LAUNCH_CHECK("conv_cout1_kernel");
     return CGAN3D_OK;
   }
-  ConvArgs a;
-  CG_CHECK_ARG(make_args(g, &a, 64), "cgan3d_conv3d_fwd: transposed output dims must divide stride");
-  dim3 grid(a.nclass * a.tiles_per_class);
-  const int nb = (g->cout + 15) / 16;
-  const bool v4 = (g->cin % 4) == 0;
-#define CG_LAUNCH_FWD(V, N) hipLaunchKernelGGL((conv_mfma_kernel<V, N>), grid, dim3(256), 0, s, a, x, w, y, e)
-  if (v4) {
-    if (nb == 1) CG_LAUNCH_FWD(4, 1); else if (nb == 2) CG_LAUNCH_FWD(4, 2); else if (nb == 3) CG_LAUNCH_FWD(4, 3); else CG_LAUNCH_FWD(4, 4);
-  } else {
-    if (nb == 1) CG_LAUNCH_FWD(1, 1); else if (nb == 2) CG_LAUNCH_FWD(1, 2); else if (nb == 3) CG_LAUNCH_FWD(1, 3); else CG_LAUNCH_FWD(1, 4);
-  }
-#undef CG_LAUNCH_FWD
-  CG_LAUNCH_CHECK("conv_mfma_kernel");
+  int rc = gemm_launch(g, x, w, y, e, s);
+  if (rc) return rc;
+  CG_LAUNCH_CHECK("conv_gemm_kernel");
   return CGAN3D_OK;
 }
 

@@ -1,0 +1,451 @@
+// Implicit-GEMM convolution, forward / input-grad roles, fp32 or bf16 MFMA (gfx950).
+//
+// Same gather formulation as conv.hip (include/cgan3d.h geometry; stride-s transposed launches
+// split into s^3 parity classes), restructured for throughput:
+//  * weights pre-packed once per optimiser step into [tap][cin][cout] rows (cgan3d_pack_weights),
+//    so each K-chunk's B tile is a few contiguous float4 rows;
+//  * the next K-chunk's A gather and B rows are prefetched into registers while the MFMAs of the
+//    current chunk run (one LDS buffer + register double-buffering, one barrier pair per chunk);
+//  * the class's valid-tap table lives in LDS (built once per block), so a chunk's gather needs no
+//    integer division beyond a shift when cin is a power of two;
+//  * two tile shapes: 64 voxels x all output channels (4 waves along M) for large grids, 32 voxels
+//    x 32 channels (2 x 2 waves, N split over blockIdx.y) when the grid would not fill 256 CUs;
+//  * PREC = 0: v_mfma_f32_16x16x4_f32 (exact f32, the parity path); PREC = 1: operands rounded to
+//    bf16 when staged into LDS, v_mfma_f32_16x16x32_bf16 with f32 accumulation.
+// Epilogue (bias, activation, LeakyReLU mask, residual, tanh, BatchNorm partial statistics) as in
+// conv.hip.
+#include "common.h"
+
+namespace cg {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+
+struct GemmArgs {
+  int n, di, hi, wi, do_, ho, wo, cin, cout, k, s, p, transposed, reflect;
+  long long sa, sb;
+  int packed, ldb;
+  int cd, ch, cw;
+  long long class_vox;
+  int tiles_per_class, nclass;
+  int cin_shift;
+};
+
+static int ilog2_exact(int v) {
+  if (v <= 0 || (v & (v - 1))) return -1;
+  int s = 0;
+  while ((1 << s) < v) ++s;
+  return s;
+}
+
+struct GemmCfg {
+  int wm, nbw, bm, bn, gy;
+};
+
+// deterministic tile-shape choice (also sizes the BatchNorm statistics buffer)
+static GemmCfg gemm_cfg(const cgan3d_conv_geom* g) {
+  GemmCfg c;
+  const int nbt = g->cout <= 16 ? 1 : (g->cout <= 32 ? 2 : 4);
+  long long cls = 1, cv;
+  if (g->transposed && g->stride > 1) {
+    cls = (long long)g->stride * g->stride * g->stride;
+    cv = (long long)g->n * (g->do_ / g->stride) * (g->ho / g->stride) * (g->wo / g->stride);
+  } else {
+    cv = (long long)g->n * g->do_ * g->ho * g->wo;
+  }
+  const long long blocks64 = cls * ((cv + 63) / 64);
+  if (blocks64 < 256 && g->cout > 16) {
+    c.wm = 2; c.nbw = 1; c.bm = 32; c.bn = 32; c.gy = (g->cout + 31) / 32;
+  } else {
+    c.wm = 4; c.nbw = nbt; c.bm = 64; c.bn = 16 * nbt; c.gy = 1;
+  }
+  return c;
+}
+
+static bool gemm_args(const cgan3d_conv_geom* g, const GemmCfg& c, GemmArgs* a) {
+  a->n = g->n; a->di = g->di; a->hi = g->hi; a->wi = g->wi;
+  a->do_ = g->do_; a->ho = g->ho; a->wo = g->wo; a->cin = g->cin; a->cout = g->cout;
+  a->k = g->k; a->s = g->stride; a->p = g->pad; a->transposed = g->transposed; a->reflect = g->reflect;
+  a->sa = g->w_sa; a->sb = g->w_sb; a->packed = g->w_packed; a->ldb = (g->cout + 3) / 4 * 4;
+  if (g->transposed && g->stride > 1) {
+    if (g->do_ % g->stride || g->ho % g->stride || g->wo % g->stride) return false;
+    a->cd = g->do_ / g->stride; a->ch = g->ho / g->stride; a->cw = g->wo / g->stride;
+    a->nclass = g->stride * g->stride * g->stride;
+  } else {
+    a->cd = g->do_; a->ch = g->ho; a->cw = g->wo; a->nclass = 1;
+  }
+  a->class_vox = (long long)g->n * a->cd * a->ch * a->cw;
+  a->tiles_per_class = (int)((a->class_vox + c.bm - 1) / c.bm);
+  a->cin_shift = ilog2_exact(g->cin);
+  return true;
+}
+
+__device__ __forceinline__ int gg_coord(int base, int off, int n, int reflect) {
+  int i = base + off;
+  if (reflect) return reflect_idx(i, n);
+  return (i >= 0 && i < n) ? i : -1;
+}
+
+template <int PREC>
+struct Lds {
+  static constexpr int KC = 32;
+  static constexpr int LD = PREC ? KC + 8 : KC + 4;  // elements per row (80 B bf16 / 144 B f32)
+  using T = typename std::conditional<PREC, __bf16, float>::type;
+};
+
+template <int PREC, int VEC, int WM, int NBW>
+__global__ __launch_bounds__(256) void conv_gemm_kernel(GemmArgs a, const float* __restrict__ x,
+                                                        const float* __restrict__ w, float* y, Epi ep) {
+  constexpr int WN = 4 / WM, BM = 16 * WM, BN = 16 * NBW * WN, KC = 32;
+  constexpr int LD = Lds<PREC>::LD;
+  using T = typename Lds<PREC>::T;
+  constexpr int A_SLOTS = VEC == 4 ? BM * KC / 4 / 256 : BM * KC / 256;  // per thread
+  constexpr int B_SLOTS = (BN * KC / 4 + 255) / 256;
+  __shared__ __attribute__((aligned(16))) T As[BM * LD];
+  __shared__ __attribute__((aligned(16))) T Bs[BN * LD];
+  __shared__ int row_n[BM], row_b[3][BM], row_out[BM];
+  __shared__ int tap_off[3][352], tap_lin[352];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave % WM, wn = wave / WM;
+  const int cls = blockIdx.x / a.tiles_per_class;
+  const int tile = blockIdx.x - cls * a.tiles_per_class;
+  const int co0 = blockIdx.y * BN;
+  const int s = a.s, k = a.k, p = a.p;
+  int rd = 0, rh = 0, rw = 0;
+  if (a.transposed) { rd = cls / (s * s); rh = (cls / s) % s; rw = cls % s; }
+  int f[3], st[3], cnt[3];
+  {
+    const int r3[3] = {rd, rh, rw};
+    for (int q = 0; q < 3; ++q) {
+      if (a.transposed) {
+        f[q] = (r3[q] + p) % s; st[q] = s; cnt[q] = f[q] < k ? (k - f[q] + s - 1) / s : 0;
+      } else {
+        f[q] = 0; st[q] = 1; cnt[q] = k;
+      }
+    }
+  }
+  const int ntap = cnt[0] * cnt[1] * cnt[2];
+  const int KT = ntap * a.cin;
+  for (int j = tid; j < ntap; j += 256) {
+    const int mw = j % cnt[2], mh = (j / cnt[2]) % cnt[1], md = j / (cnt[1] * cnt[2]);
+    const int td = f[0] + st[0] * md, th = f[1] + st[1] * mh, tw = f[2] + st[2] * mw;
+    if (a.transposed) {
+      tap_off[0][j] = (rd + p - td) / s; tap_off[1][j] = (rh + p - th) / s; tap_off[2][j] = (rw + p - tw) / s;
+    } else {
+      tap_off[0][j] = td; tap_off[1][j] = th; tap_off[2][j] = tw;
+    }
+    tap_lin[j] = (td * k + th) * k + tw;
+  }
+  const long long v0 = (long long)tile * BM;
+  if (tid < BM) {
+    const long long lin = v0 + tid;
+    if (lin < a.class_vox) {
+      const int jw = (int)(lin % a.cw); long long t = lin / a.cw;
+      const int jh = (int)(t % a.ch); t /= a.ch;
+      const int jd = (int)(t % a.cd); const int nb = (int)(t / a.cd);
+      int od, oh, ow;
+      if (a.transposed) {
+        od = jd * s + rd; oh = jh * s + rh; ow = jw * s + rw;
+        row_b[0][tid] = jd; row_b[1][tid] = jh; row_b[2][tid] = jw;
+      } else {
+        od = jd; oh = jh; ow = jw;
+        row_b[0][tid] = jd * s - p; row_b[1][tid] = jh * s - p; row_b[2][tid] = jw * s - p;
+      }
+      row_n[tid] = nb * a.di;
+      row_out[tid] = ((nb * a.do_ + od) * a.ho + oh) * a.wo + ow;
+    } else {
+      row_n[tid] = -1; row_out[tid] = -1;
+      row_b[0][tid] = row_b[1][tid] = row_b[2][tid] = 0;
+    }
+  }
+  __syncthreads();
+
+  // ---- register prefetch buffers
+  f32x4 ra4[VEC == 4 ? A_SLOTS : 1];
+  float ra1[VEC == 4 ? 1 : A_SLOTS];
+  f32x4 rb[B_SLOTS];
+
+  auto decode = [&](int kk, int* j, int* ci) {
+    if (a.cin_shift >= 0) { *j = kk >> a.cin_shift; *ci = kk & (a.cin - 1); }
+    else { *j = kk / a.cin; *ci = kk - *j * a.cin; }
+  };
+  auto gather = [&](int r, int j, int ci) -> long long {  // element offset or -1
+    const int nb = row_n[r];
+    if (nb < 0) return -1;
+    const int id = gg_coord(row_b[0][r], tap_off[0][j], a.di, a.reflect);
+    const int ih = gg_coord(row_b[1][r], tap_off[1][j], a.hi, a.reflect);
+    const int iw = gg_coord(row_b[2][r], tap_off[2][j], a.wi, a.reflect);
+    if ((id | ih | iw) < 0) return -1;
+    return ((long long)((nb + id) * a.hi + ih) * a.wi + iw) * a.cin + ci;
+  };
+  auto load_chunk = [&](int kc0) {
+    if constexpr (VEC == 4) {
+#pragma unroll
+      for (int i = 0; i < A_SLOTS; ++i) {
+        const int sl = tid + 256 * i, r = sl >> 3, kk = kc0 + (sl & 7) * 4;
+        f32x4 v = {0.f, 0.f, 0.f, 0.f};
+        if (kk < KT) {
+          int j, ci;
+          decode(kk, &j, &ci);
+          const long long o = gather(r, j, ci);
+          if (o >= 0) v = *reinterpret_cast<const f32x4*>(x + o);
+        }
+        ra4[i] = v;
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < A_SLOTS; ++i) {
+        const int sl = tid + 256 * i, r = sl >> 5, kk = kc0 + (sl & 31);
+        float v = 0.f;
+        if (kk < KT) {
+          int j, ci;
+          decode(kk, &j, &ci);
+          const long long o = gather(r, j, ci);
+          if (o >= 0) v = x[o];
+        }
+        ra1[i] = v;
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < B_SLOTS; ++i) {
+      const int sl = tid + 256 * i;
+      f32x4 v = {0.f, 0.f, 0.f, 0.f};
+      if (sl < BN * KC / 4) {
+        const int kr = sl / (BN / 4), c4 = sl - kr * (BN / 4), kk = kc0 + kr;
+        const int co = co0 + 4 * c4;
+        if (kk < KT && co < a.cout) {
+          int j, ci;
+          decode(kk, &j, &ci);
+          if (a.packed) {
+            v = *reinterpret_cast<const f32x4*>(w + ((long long)tap_lin[j] * a.cin + ci) * a.ldb + co);
+          } else {
+            const long long base = (long long)ci * a.sa + tap_lin[j];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e] = co + e < a.cout ? w[base + (long long)(co + e) * a.sb] : 0.f;
+          }
+        }
+      }
+      rb[i] = v;
+    }
+  };
+  auto store_chunk = [&]() {
+    if constexpr (VEC == 4) {
+#pragma unroll
+      for (int i = 0; i < A_SLOTS; ++i) {
+        const int sl = tid + 256 * i, r = sl >> 3, e0 = (sl & 7) * 4;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) As[r * LD + e0 + e] = (T)ra4[i][e];
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < A_SLOTS; ++i) {
+        const int sl = tid + 256 * i;
+        As[(sl >> 5) * LD + (sl & 31)] = (T)ra1[i];
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < B_SLOTS; ++i) {
+      const int sl = tid + 256 * i;
+      if (sl < BN * KC / 4) {
+        const int kr = sl / (BN / 4), c4 = sl - kr * (BN / 4);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) Bs[(4 * c4 + e) * LD + kr] = (T)rb[i][e];
+      }
+    }
+  };
+
+  f32x4 acc[NBW];
+#pragma unroll
+  for (int nb = 0; nb < NBW; ++nb) acc[nb] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int g = lane >> 4, r16 = lane & 15;
+  const int arow = (wm * 16 + r16) * LD;
+
+  if (KT > 0) load_chunk(0);
+  for (int kc0 = 0; kc0 < KT; kc0 += KC) {
+    store_chunk();
+    __syncthreads();
+    if (kc0 + KC < KT) load_chunk(kc0 + KC);  // prefetch: in flight during the MFMAs below
+    if constexpr (PREC == 0) {
+#pragma unroll
+      for (int q = 0; q < KC / 16; ++q) {
+        const f32x4 av = *reinterpret_cast<const f32x4*>(&As[arow + 16 * q + 4 * g]);
+#pragma unroll
+        for (int nb = 0; nb < NBW; ++nb) {
+          const f32x4 bv =
+              *reinterpret_cast<const f32x4*>(&Bs[((wn * NBW + nb) * 16 + r16) * LD + 16 * q + 4 * g]);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) acc[nb] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[e], bv[e], acc[nb], 0, 0, 0);
+        }
+      }
+    } else {
+      const bf16x8 av = *reinterpret_cast<const bf16x8*>(&As[arow + 8 * g]);
+#pragma unroll
+      for (int nb = 0; nb < NBW; ++nb) {
+        const bf16x8 bv = *reinterpret_cast<const bf16x8*>(&Bs[((wn * NBW + nb) * 16 + r16) * LD + 8 * g]);
+        acc[nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, bv, acc[nb], 0, 0, 0);
+      }
+    }
+    __syncthreads();
+  }
+
+  // ---- epilogue: lane holds rows wm*16 + 4g + j, column co0 + (wn*NBW + nb)*16 + r16
+  float vals[NBW][4];
+  bool rowv[4];
+  int rowo[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    rowo[j] = row_out[wm * 16 + 4 * g + j];
+    rowv[j] = rowo[j] >= 0;
+  }
+#pragma unroll
+  for (int nb = 0; nb < NBW; ++nb) {
+    const int c = co0 + (wn * NBW + nb) * 16 + r16;
+    const bool cv = c < a.cout;
+    const float b = (ep.bias && cv) ? ep.bias[c] : 0.f;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float v = acc[nb][j] + b;
+      if (ep.act == CGAN3D_ACT_RELU) v = fmaxf(v, 0.f);
+      else if (ep.act == CGAN3D_ACT_LRELU) v = v > 0.f ? v : v * ep.slope;
+      else if (ep.act == CGAN3D_ACT_TANH) v = tanhf(v);
+      if (rowv[j] && cv) {
+        const long long o = (long long)rowo[j] * a.cout + c;
+        if (ep.mask_src) v = ep.mask_src[o] > 0.f ? v : v * ep.slope;
+        if (ep.residual) v += ep.residual[o];
+        y[o] = v;
+      }
+      vals[nb][j] = (rowv[j] && cv) ? v : 0.f;
+    }
+  }
+  if (ep.stats) {
+    __syncthreads();
+    float* red = reinterpret_cast<float*>(As);  // [WM][BN]  (<= 4*64 floats)
+    __shared__ float bmean[64];
+    int cntv = 0;
+    for (int r = 0; r < BM; ++r) cntv += row_out[r] >= 0;
+    const long long sbase = (long long)blockIdx.x * (2 * a.cout + 1);
+#pragma unroll
+    for (int nb = 0; nb < NBW; ++nb) {
+      float sum = vals[nb][0] + vals[nb][1] + vals[nb][2] + vals[nb][3];
+      sum += __shfl_xor(sum, 16, 64);
+      sum += __shfl_xor(sum, 32, 64);
+      if (g == 0) red[wm * BN + (wn * NBW + nb) * 16 + r16] = sum;
+    }
+    __syncthreads();
+    if (tid < BN) {
+      float S = 0.f;
+      for (int q = 0; q < WM; ++q) S += red[q * BN + tid];
+      bmean[tid] = cntv ? S / cntv : 0.f;
+      if (co0 + tid < a.cout) ep.stats[sbase + co0 + tid] = S;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int nb = 0; nb < NBW; ++nb) {
+      const int cl = (wn * NBW + nb) * 16 + r16;
+      const float m = bmean[cl];
+      float q = 0.f;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float d = (rowv[j] && co0 + cl < a.cout) ? vals[nb][j] - m : 0.f;
+        q += d * d;
+      }
+      q += __shfl_xor(q, 16, 64);
+      q += __shfl_xor(q, 32, 64);
+      if (g == 0) red[wm * BN + cl] = q;
+    }
+    __syncthreads();
+    if (tid < BN) {
+      float M2 = 0.f;
+      for (int q = 0; q < WM; ++q) M2 += red[q * BN + tid];
+      if (co0 + tid < a.cout) ep.stats[sbase + a.cout + co0 + tid] = M2;
+    }
+    if (tid == 0 && blockIdx.y == 0) ep.stats[sbase + 2 * a.cout] = (float)cntv;
+  }
+}
+
+// packed [t][a][b] (b contiguous, row length round_up(cout, 4)) from the strided torch layout
+__global__ __launch_bounds__(256) void pack_weights_kernel(const float* __restrict__ w, float* __restrict__ wp, int T,
+                                                           int cin, int cout, int ldb, long long sa, long long sb,
+                                                           long long total) {
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long long)gridDim.x * blockDim.x) {
+    const int b = (int)(i % ldb);
+    const long long r = i / ldb;
+    const int ai = (int)(r % cin), t = (int)(r / cin);
+    wp[i] = b < cout ? w[ai * sa + b * sb + t] : 0.f;
+  }
+}
+
+__global__ __launch_bounds__(256) void pack_multi_kernel(const cgan3d_pack_desc* __restrict__ descs) {
+  const cgan3d_pack_desc d = descs[blockIdx.y];
+  const long long total = (long long)d.taps * d.cin * d.ldb;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long long)gridDim.x * blockDim.x) {
+    const int b = (int)(i % d.ldb);
+    const long long r = i / d.ldb;
+    const int ai = (int)(r % d.cin), t = (int)(r / d.cin);
+    d.wp[i] = b < d.cout ? d.w[ai * d.sa + b * d.sb + t] : 0.f;
+  }
+}
+
+int gemm_blocks(const cgan3d_conv_geom* g, long long* mblocks) {
+  GemmCfg c = gemm_cfg(g);
+  GemmArgs a;
+  if (!gemm_args(g, c, &a)) return -1;
+  *mblocks = (long long)a.nclass * a.tiles_per_class;
+  return 0;
+}
+
+int gemm_launch(const cgan3d_conv_geom* g, const float* x, const float* w, float* y, const Epi& e, hipStream_t st) {
+  GemmCfg c = gemm_cfg(g);
+  GemmArgs a;
+  if (!gemm_args(g, c, &a)) {
+    set_error("cgan3d_conv3d_fwd: transposed output dims must be divisible by the stride");
+    return CGAN3D_EINVAL;
+  }
+  dim3 grid(a.nclass * a.tiles_per_class, c.gy);
+  const bool v4 = g->cin % 4 == 0;
+  const int prec = g->prec;
+#define CG_GL(P, V, W, N) hipLaunchKernelGGL((conv_gemm_kernel<P, V, W, N>), grid, dim3(256), 0, st, a, x, w, y, e)
+#define CG_GL_NB(P, V)                                    \
+  do {                                                    \
+    if (c.wm == 2) CG_GL(P, V, 2, 1);                     \
+    else if (c.nbw == 1) CG_GL(P, V, 4, 1);               \
+    else if (c.nbw == 2) CG_GL(P, V, 4, 2);               \
+    else CG_GL(P, V, 4, 4);                               \
+  } while (0)
+  if (prec == CGAN3D_PREC_BF16) {
+    if (v4) CG_GL_NB(1, 4); else CG_GL_NB(1, 1);
+  } else {
+    if (v4) CG_GL_NB(0, 4); else CG_GL_NB(0, 1);
+  }
+#undef CG_GL_NB
+#undef CG_GL
+  return CGAN3D_OK;
+}
+
+}  // namespace cg
+
+using namespace cg;
+
+extern "C" int64_t cgan3d_packed_weight_floats(const cgan3d_conv_geom* g) {
+  if (!g) return -1;
+  return (int64_t)g->k * g->k * g->k * g->cin * ((g->cout + 3) / 4 * 4);
+}
+
+extern "C" int cgan3d_pack_weights(const cgan3d_conv_geom* g, const float* w, float* wp, void* stream) {
+  CG_CHECK_ARG(g && w && wp, "cgan3d_pack_weights: null pointer");
+  const int T = g->k * g->k * g->k, ldb = (g->cout + 3) / 4 * 4;
+  const long long total = (long long)T * g->cin * ldb;
+  int blocks = (int)std::min<long long>((total + 255) / 256, 2048);
+  hipLaunchKernelGGL(pack_weights_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, w, wp, T, g->cin, g->cout,
+                     ldb, (long long)g->w_sa, (long long)g->w_sb, total);
+  CG_LAUNCH_CHECK("pack_weights_kernel");
+  return CGAN3D_OK;
+}
+
+extern "C" int cgan3d_pack_weights_multi(const cgan3d_pack_desc* descs, int32_t n, int64_t max_total, void* stream) {
+  CG_CHECK_ARG(descs && n > 0 && n <= 65535 && max_total > 0, "cgan3d_pack_weights_multi: bad args");
+  int bx = (int)std::min<long long>((max_total + 255) / 256, 256);
+  hipLaunchKernelGGL(pack_multi_kernel, dim3(bx, n), dim3(256), 0, (hipStream_t)stream, descs);
+  CG_LAUNCH_CHECK("pack_multi_kernel");
+  return CGAN3D_OK;
+}

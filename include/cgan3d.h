@@ -50,7 +50,12 @@ typedef struct cgan3d_conv_geom {
   int32_t transposed;
   int32_t reflect;
   int64_t w_sa, w_sb;
+  int32_t w_packed;  /* 1: w is cgan3d_pack_weights() output [tap][a][b], b contiguous */
+  int32_t prec;      /* CGAN3D_PREC_F32 (exact f32 MFMA) or CGAN3D_PREC_BF16 (bf16 MFMA, f32 accumulate) */
 } cgan3d_conv_geom;
+
+#define CGAN3D_PREC_F32 0
+#define CGAN3D_PREC_BF16 1
 
 #define CGAN3D_ACT_NONE 0
 #define CGAN3D_ACT_RELU 1
@@ -78,6 +83,19 @@ const char* cgan3d_get_last_error(void);
 /* --- convolutions (model/blocks.py:29-38 Conv3d / ConvTranspose3d; generator.py:78-84 last
  *     conv; discriminator.py:24-80 critic convs; and their autograd backward) --- */
 int64_t cgan3d_conv3d_stats_floats(const cgan3d_conv_geom* g);
+/* Re-layout a torch-layout weight (strides w_sa, w_sb of g) into the packed [tap][a][b] rows the
+ * forward/input-grad kernels read as contiguous vectors (once per optimiser step). */
+int64_t cgan3d_packed_weight_floats(const cgan3d_conv_geom* g);
+int cgan3d_pack_weights(const cgan3d_conv_geom* g, const float* w, float* wp, void* stream);
+/* Many packs in one launch: `descs` is a DEVICE array of n descriptors (built once; the pointers
+ * are stable), `max_total` the largest taps*cin*ldb among them. */
+typedef struct cgan3d_pack_desc {
+  const float* w;
+  float* wp;
+  int64_t sa, sb;
+  int32_t taps, cin, cout, ldb;
+} cgan3d_pack_desc;
+int cgan3d_pack_weights_multi(const cgan3d_pack_desc* descs, int32_t n, int64_t max_total, void* stream);
 int cgan3d_conv3d_fwd(const cgan3d_conv_geom* g, const float* x, const float* w, float* y,
                       const cgan3d_epilogue* ep, void* stream);
 /* weight gradient: dw[a*w_sa + b*w_sb + t] (+)= sum_o G_gathered(o,t,a) * O(o,b) with the
