@@ -81,6 +81,9 @@ def main():
     ap.add_argument("--batch", type=int, default=4)
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--precision", choices=["f32", "bf16"], default="f32",
+                    help="MFMA operand precision of the implicit-GEMM convs (accumulation is f32)")
+    ap.add_argument("--no-graph", action="store_true", help="launch eagerly instead of replaying a HIP graph")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -105,7 +108,8 @@ def main():
     g = pcg64_init_(ResnetGenerator(**g_args), 0).to(dev)
     d = pcg64_init_(PatchGANDiscriminator(1, 8, 3, negative_slope=0.2, norm_layer=nn.Identity), 1).to(dev)
     eng = StepEngine(g, d, g.config, d.config, B, B, (S, S, S), g_hyper=(1e-4, 0.0, 0.9, 1e-8),
-                     d_hyper=(1e-4, 0.0, 0.9, 1e-8), device=dev)
+                     d_hyper=(1e-4, 0.0, 0.9, 1e-8), device=dev, precision=args.precision)
+    use_graph = not args.no_graph and world == 1
     batches = []
     for j in range(2):
         opt, _ = synth_patches(B, S, 1000 * rank + 10 * j)
@@ -127,20 +131,34 @@ def main():
         eng.step()
         eng.G.timer = None
 
+    def graph_step(i):
+        eng.load_inputs(*batches[i % len(batches)])
+        eng.replay()
+
     for i in range(args.warmup):
         one_step(i, False)
+    if use_graph:
+        torch.cuda.synchronize()
+        eng.capture()  # records one step; replays below run the whole step as one graph launch
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(args.steps):
-        one_step(i, True)
+        if use_graph:
+            graph_step(i)
+        else:
+            one_step(i, True)
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
+    if use_graph:  # the roofline kernel's launch time: HIP events around it over eager steps
+        for i in range(min(args.steps, 10)):
+            one_step(i, True)
+        torch.cuda.synchronize()
     if dist:
         t = torch.tensor([el], device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -155,9 +173,12 @@ def main():
         "metric": "3D patches/sec (G+D train step), 64³ bf16, at 1/2/4/8 MI355X",
         "value": round(value, 3), "unit": "patches/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True, "scaling": "weak",
-        "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+        "vs_baseline": None,
+        "dtype": "f32" if args.precision == "f32" else "bf16 MFMA operands (implicit-GEMM convs), f32 elsewhere",
+        "data": "synthetic",
         "config": {"workload": f"{S}^3 patches, {B} OPT + {B} LOW/HIGH per GPU, full G+D step (WGAN-GP conf)",
-                   "global_batch": world * B, "patch": S, "parallelism": f"dp{world}"},
+                   "global_batch": world * B, "patch": S, "parallelism": f"dp{world}",
+                   "hip_graph": use_graph},
         "roofline": {"kernel": "conv_cout1_kernel (generator last conv fwd)", "bound": "mfma",
                      "achieved": round(achieved, 3), "peak": F32_PEAK_TFLOPS, "unit": "TFLOP/s",
                      "frac": round(achieved / F32_PEAK_TFLOPS, 4), "traffic": None,

@@ -472,6 +472,28 @@ class StepEngine:
             dist.all_reduce(flat_grad, op=dist.ReduceOp.SUM, group=self.pg)
             flat_grad.mul_(1.0 / self.world)
 
+    def capture(self, do_critic: bool = True, do_generator: bool = True):
+        """Record one whole step (~200 launches) as a HIP graph; ``replay()`` then costs one launch.
+
+        Valid because every launch reads its scalars from device memory (Adam step/lr) and every
+        buffer is resident; inputs are loaded into the same slots before each replay.  Run one
+        eager ``step()`` first (kernel code objects load lazily, which capture cannot record)."""
+        if self.world > 1:
+            raise NotImplementedError("graph capture with collectives: launch eagerly under DDP")
+        s = torch.cuda.Stream(device=self.device)
+        s.wait_stream(torch.cuda.current_stream(self.device))
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.stream(s):
+            with torch.cuda.graph(graph, stream=s):
+                self.step(do_critic, do_generator)
+        torch.cuda.current_stream(self.device).wait_stream(s)
+        self.graph = graph
+        return graph
+
+    def replay(self):
+        self.graph.replay()
+        return self.losses
+
     def step(self, do_critic: bool = True, do_generator: bool = True):
         """Trainer.train_step body (Trainer.py:169-184) on the resident inputs."""
         self.generator_forward()

@@ -77,8 +77,9 @@ class FusedAdam(torch.optim.Optimizer):
         self.arena.rebind_grads()
 
     def state_dict(self):
+        step = float(self.hyper[4].item())  # device counter (correct under graph replay too)
         for p in self.arena.params:
-            self.state[p]["step"] = torch.tensor(float(self._host_step))
+            self.state[p]["step"] = torch.tensor(step)
         return super().state_dict()
 
     def load_state_dict(self, state_dict):

@@ -87,8 +87,54 @@ __device__ __forceinline__ int gcoord(int base, int off, int n, int reflect) {
 
 // ------------------------------------------------------------------------------------------
 // cout == 1 forward / input-grad (VALU): one thread per output voxel, weights in LDS.
-// Used by the generator's last conv (16 -> 1, k7 reflect, + bias, tanh, opt_hat = subopt - .)
-// and the critic's first-layer input-grad and last layer.
+// Used by the critic's first-layer input-grad (8 -> 1 channel, transposed s2) and, when the
+// output is large, its last layer.
+//
+// conv_cout1_wave_kernel: the same contraction with one wave per output voxel and the
+// (tap, channel) reduction spread over the 64 lanes — for the critic's last layer, whose output
+// is only N x 3^3 voxels but each voxel reduces 64 taps x 64 channels (forward mapping only).
+__global__ __launch_bounds__(256) void conv_cout1_wave_kernel(ConvArgs a, const float* __restrict__ x,
+                                                              const float* __restrict__ w, float* y, Epi ep) {
+  extern __shared__ __attribute__((aligned(16))) float Ws[];  // [T][cin]
+  const int T = a.k * a.k * a.k;
+  for (int i = threadIdx.x; i < T * a.cin; i += blockDim.x) {
+    int t = i / a.cin, ci = i - t * a.cin;
+    Ws[i] = w[(long long)ci * a.sa + t];
+  }
+  __syncthreads();
+  const int lane = threadIdx.x & 63;
+  const long long lin = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (lin >= a.class_vox) return;  // wave-uniform
+  int ow = (int)(lin % a.wo); long long tt = lin / a.wo;
+  int oh = (int)(tt % a.ho); tt /= a.ho;
+  int od = (int)(tt % a.do_); int nb = (int)(tt / a.do_);
+  const int bd = od * a.s - a.p, bh = oh * a.s - a.p, bw = ow * a.s - a.p;
+  const int C4 = a.cin >> 2, R4 = T * C4;
+  float acc = 0.f;
+  for (int r4 = lane; r4 < R4; r4 += 64) {
+    const int t = r4 / C4, c = (r4 - t * C4) * 4;
+    const int td = t / (a.k * a.k), th = (t / a.k) % a.k, tw = t % a.k;
+    const int id = gcoord(bd, td, a.di, a.reflect), ih = gcoord(bh, th, a.hi, a.reflect), iw = gcoord(bw, tw, a.wi, a.reflect);
+    if ((id | ih | iw) >= 0) {
+      const f32x4 xv = *reinterpret_cast<const f32x4*>(x + ((long long)((nb * a.di + id) * a.hi + ih) * a.wi + iw) * a.cin + c);
+      const f32x4 wv = *reinterpret_cast<const f32x4*>(Ws + t * a.cin + c);
+      acc += xv[0] * wv[0] + xv[1] * wv[1] + xv[2] * wv[2] + xv[3] * wv[3];
+    }
+  }
+  acc = wave_sum(acc);
+  if (lane == 0) {
+    float v = acc + (ep.bias ? ep.bias[0] : 0.f);
+    if (ep.act == CGAN3D_ACT_RELU) v = fmaxf(v, 0.f);
+    else if (ep.act == CGAN3D_ACT_LRELU) v = v > 0.f ? v : v * ep.slope;
+    else if (ep.act == CGAN3D_ACT_TANH) v = tanhf(v);
+    if (ep.mask_src) v = ep.mask_src[lin] > 0.f ? v : v * ep.slope;
+    if (ep.residual) v += ep.residual[lin];
+    y[lin] = v;
+    if (ep.out2) ep.out2[lin] = ep.minuend[lin] - v;
+  }
+}
+
+// One thread per output voxel, weights in LDS.
 __global__ __launch_bounds__(256) void conv_cout1_kernel(ConvArgs a, const float* __restrict__ x,
                                                          const float* __restrict__ w, float* y, Epi ep) {
   extern __shared__ __attribute__((aligned(16))) float Ws[];  // [T][cin]
@@ -282,7 +328,7 @@ __global__ __launch_bounds__(256) void conv_wgrad_cout1_kernel(ConvArgs a, const
   f32x4 acc[MAXJ];
 #pragma unroll
   for (int j = 0; j < MAXJ; ++j) {
-    int r4 = tid + 256 * j;
+    int r4 = tid + 256 * (j + MAXJ * (int)blockIdx.y);
     acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
     if (r4 < R4) {
       int r = 4 * r4, t = r / a.cin;
@@ -331,7 +377,7 @@ __global__ __launch_bounds__(256) void conv_wgrad_cout1_kernel(ConvArgs a, const
 #pragma unroll
   for (int j = 0; j < MAXJ; ++j) {
     if (td[j] < 0) continue;
-    int r = 4 * (tid + 256 * j);
+    int r = 4 * (tid + 256 * (j + MAXJ * (int)blockIdx.y));
 #pragma unroll
     for (int e = 0; e < 4; ++e) atomicAdd(dwp + r + e, acc[j][e]);
   }
@@ -390,6 +436,11 @@ extern "C" int cgan3d_conv3d_fwd(const cgan3d_conv_geom* g, const float* x, cons
     CG_CHECK_ARG(make_args(g, &a, 256), "cgan3d_conv3d_fwd: transposed output dims must divide stride");
     size_t lds = (size_t)g->k * g->k * g->k * g->cin * sizeof(float);
     CG_CHECK_ARG(lds <= 64 * 1024, "cgan3d_conv3d_fwd: cout==1 weights exceed LDS");
+    if (!g->transposed && g->cin % 4 == 0 && a.class_vox <= 16384) {  // few outputs, long reductions
+      hipLaunchKernelGGL(conv_cout1_wave_kernel, dim3(cg::ceil_div(a.class_vox, 4)), dim3(256), lds, s, a, x, w, y, e);
+      CG_LAUNCH_CHECK("conv_cout1_wave_kernel");
+      return CGAN3D_OK;
+    }
     hipLaunchKernelGGL(conv_cout1_kernel, dim3(a.nclass * a.tiles_per_class), dim3(256), lds, s, a, x, w, y, e);
     CG_LAUNCH_CHECK("conv_cout1_kernel");
     return CGAN3D_OK;
@@ -445,15 +496,13 @@ extern "C" int cgan3d_conv3d_wgrad(const cgan3d_conv_geom* g, const float* gathe
   if (g->cout == 1) {
     CG_CHECK_ARG(g->cin % 4 == 0, "cgan3d_conv3d_wgrad: cout==1 needs cin%%4==0");
     const long long R4 = R / 4;
-    CG_CHECK_ARG(R4 <= 256 * 8, "cgan3d_conv3d_wgrad: cout==1 reduction too long");
-    long long vpb = V / 512 + 1;
-    if (vpb < 256) vpb = 256;
+    // one float4 of (tap, channel) accumulators per thread; r4 chunks over blockIdx.y, voxels over x
+    const int gy = cg::ceil_div(R4, 256);
+    long long vpb = (V * gy + 1023) / 1024;
+    if (vpb < 64) vpb = 64;
     vpb = (vpb + 63) / 64 * 64;
-    dim3 grid(cg::ceil_div(V, vpb));
-    if (R4 <= 256) hipLaunchKernelGGL((conv_wgrad_cout1_kernel<1>), grid, dim3(256), 0, s, a, gathered, aligned, ws, vpb);
-    else if (R4 <= 512) hipLaunchKernelGGL((conv_wgrad_cout1_kernel<2>), grid, dim3(256), 0, s, a, gathered, aligned, ws, vpb);
-    else if (R4 <= 1024) hipLaunchKernelGGL((conv_wgrad_cout1_kernel<4>), grid, dim3(256), 0, s, a, gathered, aligned, ws, vpb);
-    else hipLaunchKernelGGL((conv_wgrad_cout1_kernel<8>), grid, dim3(256), 0, s, a, gathered, aligned, ws, vpb);
+    dim3 grid(cg::ceil_div(V, vpb), gy);
+    hipLaunchKernelGGL((conv_wgrad_cout1_kernel<1>), grid, dim3(256), 0, s, a, gathered, aligned, ws, vpb);
     CG_LAUNCH_CHECK("conv_wgrad_cout1_kernel");
   } else {
     const int gxb = cg::ceil_div(R, 64);
