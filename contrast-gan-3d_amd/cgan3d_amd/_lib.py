@@ -46,6 +46,7 @@ _P, _I32, _I64, _F = C.c_void_p, C.c_int32, C.c_int64, C.c_float
 _SIGS = {
     "cgan3d_version": ([], C.c_char_p),
     "cgan3d_get_last_error": ([], C.c_char_p),
+    "cgan3d_set_tuning": ([_I32, _I32], _I32),
     "cgan3d_conv3d_stats_floats": ([_P], _I64),
     "cgan3d_conv3d_fwd": ([_P, _P, _P, _P, _P, _P], _I32),
     "cgan3d_packed_weight_floats": ([_P], _I64),

@@ -41,6 +41,10 @@ struct GemmCfg {
   int wm, nbw, bm, bn, gy;
 };
 
+// tuning knob (cgan3d_set_tuning key 0): grids with fewer 64-voxel tiles than this use the
+// 32 x 32 tile (more, smaller blocks: latency hiding for the 16^3-voxel ResNet layers)
+static int g_small_tile_below = 1024;
+
 // deterministic tile-shape choice (also sizes the BatchNorm statistics buffer)
 static GemmCfg gemm_cfg(const cgan3d_conv_geom* g) {
   GemmCfg c;
@@ -53,7 +57,7 @@ static GemmCfg gemm_cfg(const cgan3d_conv_geom* g) {
     cv = (long long)g->n * g->do_ * g->ho * g->wo;
   }
   const long long blocks64 = cls * ((cv + 63) / 64);
-  if (blocks64 < 256 && g->cout > 16) {
+  if (blocks64 < g_small_tile_below && g->cout > 16) {
     c.wm = 2; c.nbw = 1; c.bm = 32; c.bn = 32; c.gy = (g->cout + 31) / 32;
   } else {
     c.wm = 4; c.nbw = nbt; c.bm = 64; c.bn = 16 * nbt; c.gy = 1;
@@ -448,4 +452,10 @@ extern "C" int cgan3d_pack_weights_multi(const cgan3d_pack_desc* descs, int32_t 
   hipLaunchKernelGGL(pack_multi_kernel, dim3(bx, n), dim3(256), 0, (hipStream_t)stream, descs);
   CG_LAUNCH_CHECK("pack_multi_kernel");
   return CGAN3D_OK;
+}
+
+extern "C" int cgan3d_set_tuning(int32_t key, int32_t value) {
+  if (key == 0) { g_small_tile_below = value; return CGAN3D_OK; }
+  set_error("cgan3d_set_tuning: unknown key %d", key);
+  return CGAN3D_EINVAL;
 }

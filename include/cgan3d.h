@@ -79,6 +79,10 @@ typedef struct cgan3d_epilogue {
 
 const char* cgan3d_version(void);
 const char* cgan3d_get_last_error(void);
+/* Launch-shape tuning (process-wide; set before building plans: BatchNorm statistics buffers are
+ * sized from the tile shape).  key 0: implicit-GEMM grids with fewer 64-voxel tiles than `value`
+ * use 32x32 tiles (default 1024). */
+int cgan3d_set_tuning(int32_t key, int32_t value);
 
 /* --- convolutions (model/blocks.py:29-38 Conv3d / ConvTranspose3d; generator.py:78-84 last
  *     conv; discriminator.py:24-80 critic convs; and their autograd backward) --- */
