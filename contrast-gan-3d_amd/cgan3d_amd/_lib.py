@@ -30,7 +30,8 @@ class ConvGeom(C.Structure):
 
 class PackDesc(C.Structure):
     _fields_ = [("w", C.c_void_p), ("wp", C.c_void_p), ("sa", C.c_int64), ("sb", C.c_int64),
-                ("taps", C.c_int32), ("cin", C.c_int32), ("cout", C.c_int32), ("ldb", C.c_int32)]
+                ("taps", C.c_int32), ("cin", C.c_int32), ("cout", C.c_int32), ("ldb", C.c_int32),
+                ("format", C.c_int32), ("reserved", C.c_int32)]
 
 
 PREC_F32, PREC_BF16 = 0, 1
@@ -50,6 +51,7 @@ _SIGS = {
     "cgan3d_conv3d_stats_floats": ([_P], _I64),
     "cgan3d_conv3d_fwd": ([_P, _P, _P, _P, _P, _P], _I32),
     "cgan3d_packed_weight_floats": ([_P], _I64),
+    "cgan3d_halo_eligible": ([_P], _I32),
     "cgan3d_pack_weights": ([_P, _P, _P, _P], _I32),
     "cgan3d_pack_weights_multi": ([_P, _I32, _I64, _P], _I32),
     "cgan3d_conv3d_wgrad_ws_floats": ([_P], _I64),

@@ -12,6 +12,7 @@ only these checks run — the whole step can be shape-checked on CPU tensors wit
 from __future__ import annotations
 
 import ctypes
+import os
 from typing import Optional, Sequence
 
 import torch
@@ -42,12 +43,31 @@ def uses_gemm(g: ConvGeom) -> bool:
     return not (g.k == 7 and g.stride == 1 and g.cin == 1 and g.cout in (8, 16))
 
 
+# bf16 launches whose geometry the halo-tiled kernel takes use it (conv_halo.hip); the env switch
+# CGAN3D_NO_HALO=1 keeps them on the implicit-GEMM kernel (A/B measurements).
+HALO = os.environ.get("CGAN3D_NO_HALO", "0") != "1"
+
+
+def halo_eligible(g: ConvGeom) -> bool:
+    return bool(L.load().cgan3d_halo_eligible(ctypes.byref(g)))
+
+
 def with_packing(g: ConvGeom, prec: int = L.PREC_F32) -> ConvGeom:
-    """Copy of ``g`` that reads packed weights (cgan3d_pack_weights) and runs in ``prec``."""
+    """Copy of ``g`` that reads packed weights (cgan3d_pack_weights) and runs in ``prec``:
+    format 2 (halo kernel, bf16 [tap][b][a]) where eligible, else format 1 ([tap][a][b] f32)."""
     h = ConvGeom()
     ctypes.pointer(h)[0] = g
     h.w_packed, h.prec = 1, prec
+    if prec == L.PREC_BF16 and HALO and halo_eligible(h):
+        h.w_packed = 2
     return h
+
+
+def packed_elements(g: ConvGeom) -> int:
+    """Elements (f32 or bf16) the pack kernel writes for ``g``."""
+    if g.w_packed == 2:
+        return g.k**3 * g.cin * g.cout
+    return g.k**3 * g.cin * ((g.cout + 3) // 4 * 4)
 
 
 def packed_weight_floats(g: ConvGeom) -> int:
@@ -60,6 +80,7 @@ def pack_desc(g: ConvGeom, w: torch.Tensor, wp: torch.Tensor) -> PackDesc:
     d = PackDesc()
     d.w, d.wp, d.sa, d.sb = ptr(w), ptr(wp), g.w_sa, g.w_sb
     d.taps, d.cin, d.cout, d.ldb = g.k**3, g.cin, g.cout, (g.cout + 3) // 4 * 4
+    d.format = g.w_packed
     return d
 
 
@@ -89,7 +110,7 @@ class PackSet:
         gp = with_packing(g, prec)
         wp = torch.zeros(packed_weight_floats(gp), device=self.device)
         self.descs.append((pack_desc(gp, w, wp), wp))
-        self.max_total = max(self.max_total, wp.numel())
+        self.max_total = max(self.max_total, packed_elements(gp))
         self.dev = None
         return gp, wp
 

@@ -74,6 +74,11 @@ int k7_try_wgrad(const cgan3d_conv_geom* g, const float* x, const float* go, flo
 long long k7_n2w_blocks(const cgan3d_conv_geom* g);
 // implicit-GEMM forward / input-grad (conv_gemm.hip)
 int gemm_blocks(const cgan3d_conv_geom* g, long long* mblocks);
+bool halo_ok(const cgan3d_conv_geom* g);         // w_packed == 2 and eligible
+bool halo_format_ok(const cgan3d_conv_geom* g);  // eligible ignoring w_packed
+long long halo_mblocks(const cgan3d_conv_geom* g);
+int halo_launch(const cgan3d_conv_geom* g, const float* x, const float* w, float* y, const Epi& e, hipStream_t st);
+int halo_pack(const cgan3d_conv_geom* g, const float* w, void* wp, hipStream_t st);
 int gemm_launch(const cgan3d_conv_geom* g, const float* x, const float* w, float* y, const Epi& e, hipStream_t st);
 
 }  // namespace cg

@@ -411,6 +411,7 @@ static Epi to_epi(const cgan3d_epilogue* ep) {
 extern "C" int64_t cgan3d_conv3d_stats_floats(const cgan3d_conv_geom* g) {
   if (!g) return -1;
   if (long long kb = k7_n2w_blocks(g)) return (int64_t)kb * (2 * g->cout + 1);
+  if (halo_ok(g)) return (int64_t)halo_mblocks(g) * (2 * g->cout + 1);
   long long mb = 0;
   if (gemm_blocks(g, &mb)) return -1;
   return (int64_t)mb * (2 * g->cout + 1);
@@ -443,6 +444,14 @@ extern "C" int cgan3d_conv3d_fwd(const cgan3d_conv_geom* g, const float* x, cons
     }
     hipLaunchKernelGGL(conv_cout1_kernel, dim3(a.nclass * a.tiles_per_class), dim3(256), lds, s, a, x, w, y, e);
     CG_LAUNCH_CHECK("conv_cout1_kernel");
+    return CGAN3D_OK;
+  }
+  if (g->w_packed == 2) {
+    CG_CHECK_ARG(halo_ok(g), "cgan3d_conv3d_fwd: w_packed 2 on a geometry the halo kernel does not take");
+    CG_CHECK_ARG(!e.out2 && !e.minuend, "cgan3d_conv3d_fwd: halo kernel has no out2 epilogue");
+    int rc = halo_launch(g, x, w, y, e, s);
+    if (rc) return rc;
+    CG_LAUNCH_CHECK("conv_halo_kernel");
     return CGAN3D_OK;
   }
   int rc = gemm_launch(g, x, w, y, e, s);

@@ -1,0 +1,358 @@
+// Halo-tiled direct convolution, bf16 MFMA (gfx950) — the generator's 32/64-channel convs.
+//
+// ResNetBlock convs (model/blocks.py:68-85; k3 s1 p1, 64 -> 64), the 32 -> 64 downsampling conv
+// and both ConvTranspose3d upsampling layers (generator.py:40-47,61-77), their input-grads, and the
+// critic's 32/64-channel layers.  conv_gemm.hip re-gathers every input row once per tap through
+// L1/L2; here each 4x4x4 output tile loads its input halo ONCE:
+//
+//  * halo [Ez][Ey][Ex][cin(+8 pad)] bf16 in LDS, converted from the fp32 NDHWC activations while
+//    staging (one pass of coalesced float4 loads);
+//  * the packed weights (bf16, [tap][cout][cin], 16-byte granules XOR-swizzled by cout so the
+//    MFMA B-fragment reads are conflict-free) stream through a 3-slot LDS ring by LDS-DMA
+//    (global_load_lds_dwordx4), two taps ahead, with counted vmcnt waits and raw s_barrier so the
+//    DMAs stay in flight across barriers (cdna_hip_programming.md §5 "Pipelining across barriers");
+//  * per tap each wave (one z-slice = 16 output voxels) runs cin/32 x (BN/16)
+//    v_mfma_f32_16x16x32_bf16 whose A fragments are b128 reads of the halo at the tap's offset.
+//
+// Stride-2 transposed launches keep conv.hip's parity classes; a class's valid taps map a tile of
+// class coordinates j to gathered coordinates j + off(t), so its halo is tile + (max-min) offset.
+// Epilogue (bias, act, mask, residual, BatchNorm partial statistics) as in conv_gemm.hip.
+#include "common.h"
+
+namespace cg {
+
+typedef __bf16 bf16x8_h __attribute__((ext_vector_type(8)));
+
+struct HaloArgs {
+  int n, di, hi, wi, do_, ho, wo, cin, cout, k, s, p, transposed;
+  int cd, ch, cw;             // class-local grid (transposed s>1) or output grid
+  int td, th, tw;             // tiles per dim (4 each)
+  int nclass;
+  int ez, ey, ex;             // halo extents
+  int halo_bytes;
+  int bn;                     // output channels per block
+};
+
+constexpr int HT = 4;  // tile edge (4 x 4 x 4 = 64 output voxels)
+
+struct ClassTaps {
+  int f, st, n;   // first tap, step, count
+  int omin, omax; // gathered offset range (transposed) / tap range (forward)
+};
+
+__host__ __device__ inline ClassTaps class_info(int r, int k, int s, int p, int transposed) {
+  ClassTaps c;
+  if (transposed) {
+    c.f = (r + p) % s; c.st = s; c.n = c.f < k ? (k - c.f + s - 1) / s : 0;
+    // off(t) = (r + p - t)/s decreases with t
+    c.omax = c.n ? (r + p - c.f) / s : 0;
+    c.omin = c.n ? (r + p - (c.f + s * (c.n - 1))) / s : 0;
+  } else {
+    c.f = 0; c.st = 1; c.n = k; c.omin = 0; c.omax = k - 1;
+  }
+  return c;
+}
+
+// halo extent along one dim for a 4-wide tile
+__host__ __device__ inline int halo_extent(const ClassTaps& c, int s, int transposed) {
+  return transposed ? HT + c.omax - c.omin : (HT - 1) * s + c.omax + 1;
+}
+
+template <int CIN, int NT>  // NT = BN/16 output-channel tiles per wave
+__global__ __launch_bounds__(256) void conv_halo_kernel(HaloArgs a, const float* __restrict__ x,
+                                                        const __bf16* __restrict__ wpk, float* y, Epi ep) {
+  constexpr int BN = 16 * NT;
+  constexpr int ROW = CIN + 8;                 // halo row (elements), 16 B pad
+  constexpr int NG = CIN / 8;                  // 16-byte granules per weight row
+  constexpr int SLOT = BN * CIN;               // bf16 elements per tap slab
+  constexpr int DMA_PER_TAP = (SLOT * 2 + 4095) / 4096;  // global_load_lds_dwordx4 per thread per tap
+  static_assert(SLOT * 2 % 1024 == 0 && DMA_PER_TAP <= 2, "slab must be 2, 4 or 8 KB");
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  __bf16* wring = reinterpret_cast<__bf16*>(smem);                // [3][SLOT]
+  __bf16* halo = reinterpret_cast<__bf16*>(smem + 3 * SLOT * 2);  // [E][ROW]
+  __shared__ int tq[3][64];                                        // per-tap halo offsets
+  __shared__ int tlin[64];
+  __shared__ int row_out[64];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tiles = a.td * a.th * a.tw;
+  int bid = blockIdx.x;
+  const int cls = bid / (a.n * tiles);
+  bid -= cls * a.n * tiles;
+  const int nb = bid / tiles;
+  bid -= nb * tiles;
+  const int tz = bid / (a.th * a.tw), ty = (bid / a.tw) % a.th, tx = bid % a.tw;
+  const int co0 = blockIdx.y * BN;
+  const int s = a.s;
+  int r3[3] = {0, 0, 0};
+  if (a.transposed) { r3[0] = cls / (s * s); r3[1] = (cls / s) % s; r3[2] = cls % s; }
+  const ClassTaps cz = class_info(r3[0], a.k, s, a.p, a.transposed);
+  const ClassTaps cy = class_info(r3[1], a.k, s, a.p, a.transposed);
+  const ClassTaps cx = class_info(r3[2], a.k, s, a.p, a.transposed);
+  const int ntap = cz.n * cy.n * cx.n;
+  // gathered-grid origin of the halo
+  int oz, oy, ox;
+  if (a.transposed) { oz = tz * HT + cz.omin; oy = ty * HT + cy.omin; ox = tx * HT + cx.omin; }
+  else { oz = tz * HT * s - a.p; oy = ty * HT * s - a.p; ox = tx * HT * s - a.p; }
+  const int se = a.transposed ? 1 : s;
+
+  // ---- tap table: halo offsets and packed-weight slab index
+  if (tid < ntap) {
+    const int mw = tid % cx.n, mh = (tid / cx.n) % cy.n, md = tid / (cx.n * cy.n);
+    const int t0 = cz.f + cz.st * md, t1 = cy.f + cy.st * mh, t2 = cx.f + cx.st * mw;
+    if (a.transposed) {
+      tq[0][tid] = (r3[0] + a.p - t0) / s - cz.omin;
+      tq[1][tid] = (r3[1] + a.p - t1) / s - cy.omin;
+      tq[2][tid] = (r3[2] + a.p - t2) / s - cx.omin;
+    } else {
+      tq[0][tid] = t0; tq[1][tid] = t1; tq[2][tid] = t2;
+    }
+    tlin[tid] = (t0 * a.k + t1) * a.k + t2;
+  }
+  if (tid < 64) {  // output voxel of tile row tid = (z, y, x) = (tid>>4, (tid>>2)&3, tid&3)
+    const int jz = tz * HT + (tid >> 4), jy = ty * HT + ((tid >> 2) & 3), jx = tx * HT + (tid & 3);
+    int od = jz, oh = jy, ow = jx;
+    if (a.transposed) { od = jz * s + r3[0]; oh = jy * s + r3[1]; ow = jx * s + r3[2]; }
+    const bool ok = jz < a.cd && jy < a.ch && jx < a.cw;
+    row_out[tid] = ok ? ((nb * a.do_ + od) * a.ho + oh) * a.wo + ow : -1;
+  }
+  __syncthreads();
+
+  // ---- weight ring: slab of tap j (channels co0..co0+BN) -> slot j % 3 by LDS-DMA
+  auto issue = [&](int j) {
+    const __bf16* src = wpk + ((long long)tlin[j] * a.cout + co0) * CIN;
+    __bf16* dst = wring + (j % 3) * SLOT;
+#pragma unroll
+    for (int q = 0; q < DMA_PER_TAP; ++q) {
+      const int byte = (q * 256 + tid) * 16;
+      if (byte >= SLOT * 2) break;  // 2 KB slabs: waves 2-3 idle (wave-uniform)
+      // LDS destination = wave-uniform base + lane * 16 (M0 holds the base)
+      __builtin_amdgcn_global_load_lds((const void*)(reinterpret_cast<const char*>(src) + byte),
+                                       (__attribute__((address_space(3))) void*)(reinterpret_cast<char*>(dst) + (q * 256 + wave * 64) * 16),
+                                       16, 0, 0);
+    }
+  };
+  if (ntap > 0) issue(0);
+  if (ntap > 1) issue(1);
+
+  // ---- halo: fp32 NDHWC -> bf16 LDS (zero outside the gathered volume)
+  {
+    const int nvox = a.ez * a.ey * a.ex;
+    constexpr int C4 = CIN / 4;
+    for (int i = tid; i < nvox * C4; i += 256) {
+      const int v = i / C4, c4 = i - v * C4;
+      const int hx = v % a.ex, hy = (v / a.ex) % a.ey, hz = v / (a.ex * a.ey);
+      const int iz = oz + hz, iy = oy + hy, ix = ox + hx;
+      f32x4 val = {0.f, 0.f, 0.f, 0.f};
+      if (iz >= 0 && iz < a.di && iy >= 0 && iy < a.hi && ix >= 0 && ix < a.wi)
+        val = *reinterpret_cast<const f32x4*>(x + (((long long)(nb * a.di + iz) * a.hi + iy) * a.wi + ix) * CIN + 4 * c4);
+      __bf16* d = halo + v * ROW + 4 * c4;
+      d[0] = (__bf16)val[0]; d[1] = (__bf16)val[1]; d[2] = (__bf16)val[2]; d[3] = (__bf16)val[3];
+    }
+  }
+  // the halo stores and tap tables must be visible before the first MFMA; the weight DMAs are
+  // waited for per tap below
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+
+  f32x4 acc[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int g = lane >> 4, r16 = lane & 15;
+  // this lane's output voxel (A row): z = wave, y = r16 >> 2, x = r16 & 3
+  const int lane_vox = ((wave * se) * a.ey + ((r16 >> 2) * se)) * a.ex + (r16 & 3) * se;
+
+  for (int j = 0; j < ntap; ++j) {
+    if (j + 2 < ntap) issue(j + 2);
+    // wait for tap j's DMA: leave the (up to) two younger taps in flight
+    if (j + 2 < ntap) {
+      if constexpr (DMA_PER_TAP == 1) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    } else if (j + 1 < ntap) {
+      if constexpr (DMA_PER_TAP == 1) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();
+    const __bf16* ws = wring + (j % 3) * SLOT;
+    const int voff = (tq[0][j] * a.ey + tq[1][j]) * a.ex + tq[2][j];
+    const __bf16* arow = halo + (lane_vox + voff) * ROW;
+#pragma unroll
+    for (int ks = 0; ks < CIN / 32; ++ks) {
+      const bf16x8_h av = *reinterpret_cast<const bf16x8_h*>(arow + ks * 32 + 8 * g);
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        const int col = t * 16 + r16;  // channel within the block
+        const int gr = (ks * 4 + g) ^ (col & (NG - 1));
+        const bf16x8_h bv = *reinterpret_cast<const bf16x8_h*>(ws + col * CIN + gr * 8);
+        acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, bv, acc[t], 0, 0, 0);
+      }
+    }
+    // every wave has read slot j % 3 before tap j + 3 may overwrite it
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+  }
+
+  // ---- epilogue: lane holds tile rows wave*16 + 4g + jj for channel co0 + t*16 + r16
+  float vals[NT][4];
+  bool rowv[4];
+  int rowo[4];
+#pragma unroll
+  for (int jj = 0; jj < 4; ++jj) {
+    rowo[jj] = row_out[wave * 16 + 4 * g + jj];
+    rowv[jj] = rowo[jj] >= 0;
+  }
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    const int c = co0 + t * 16 + r16;
+    const bool cv = c < a.cout;
+    const float b = (ep.bias && cv) ? ep.bias[c] : 0.f;
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj) {
+      float v = acc[t][jj] + b;
+      if (ep.act == CGAN3D_ACT_RELU) v = fmaxf(v, 0.f);
+      else if (ep.act == CGAN3D_ACT_LRELU) v = v > 0.f ? v : v * ep.slope;
+      if (rowv[jj] && cv) {
+        const long long o = (long long)rowo[jj] * a.cout + c;
+        if (ep.mask_src) v = ep.mask_src[o] > 0.f ? v : v * ep.slope;
+        if (ep.residual) v += ep.residual[o];
+        y[o] = v;
+      }
+      vals[t][jj] = (rowv[jj] && cv) ? v : 0.f;
+    }
+  }
+  if (ep.stats) {
+    __syncthreads();
+    float* red = reinterpret_cast<float*>(smem);  // [4 waves][BN]
+    __shared__ float bmean[64];
+    int cntv = 0;
+    for (int r = 0; r < 64; ++r) cntv += row_out[r] >= 0;
+    const long long sbase = (long long)blockIdx.x * (2 * a.cout + 1);
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      float sum = vals[t][0] + vals[t][1] + vals[t][2] + vals[t][3];
+      sum += __shfl_xor(sum, 16, 64);
+      sum += __shfl_xor(sum, 32, 64);
+      if (g == 0) red[wave * BN + t * 16 + r16] = sum;
+    }
+    __syncthreads();
+    if (tid < BN) {
+      const float S = red[tid] + red[BN + tid] + red[2 * BN + tid] + red[3 * BN + tid];
+      bmean[tid] = cntv ? S / cntv : 0.f;
+      if (co0 + tid < a.cout) ep.stats[sbase + co0 + tid] = S;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      const int cl = t * 16 + r16;
+      const float m = bmean[cl];
+      float q = 0.f;
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj) {
+        const float d = (rowv[jj] && co0 + cl < a.cout) ? vals[t][jj] - m : 0.f;
+        q += d * d;
+      }
+      q += __shfl_xor(q, 16, 64);
+      q += __shfl_xor(q, 32, 64);
+      if (g == 0) red[wave * BN + cl] = q;
+    }
+    __syncthreads();
+    if (tid < BN) {
+      const float M2 = red[tid] + red[BN + tid] + red[2 * BN + tid] + red[3 * BN + tid];
+      if (co0 + tid < a.cout) ep.stats[sbase + a.cout + co0 + tid] = M2;
+    }
+    if (tid == 0 && blockIdx.y == 0) ep.stats[sbase + 2 * a.cout] = (float)cntv;
+  }
+}
+
+// bf16 [tap][b][a] with 16-byte granules of a XOR-swizzled by (b mod granules-per-row)
+__global__ __launch_bounds__(256) void pack_halo_kernel(const float* __restrict__ w, __bf16* __restrict__ wp, int T,
+                                                        int cin, int cout, long long sa, long long sb) {
+  const long long total = (long long)T * cout * cin;
+  const int ng = cin / 8;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long long)gridDim.x * blockDim.x) {
+    const int ai = (int)(i % cin);
+    const long long r = i / cin;
+    const int b = (int)(r % cout), t = (int)(r / cout);
+    const int gsw = (ai / 8) ^ (b & (ng - 1));
+    wp[r * cin + gsw * 8 + (ai & 7)] = (__bf16)w[ai * sa + b * sb + t];
+  }
+}
+
+static bool halo_setup(const cgan3d_conv_geom* g, HaloArgs* a) {
+  if (g->prec != CGAN3D_PREC_BF16 || g->reflect) return false;
+  if (!(g->cin == 32 || g->cin == 64) || g->cout % 16 || g->k > 4 || g->stride < 1 || g->stride > 2) return false;
+  a->n = g->n; a->di = g->di; a->hi = g->hi; a->wi = g->wi; a->do_ = g->do_; a->ho = g->ho; a->wo = g->wo;
+  a->cin = g->cin; a->cout = g->cout; a->k = g->k; a->s = g->stride; a->p = g->pad; a->transposed = g->transposed;
+  if (g->transposed && g->stride > 1) {
+    if (g->do_ % g->stride || g->ho % g->stride || g->wo % g->stride) return false;
+    a->cd = g->do_ / g->stride; a->ch = g->ho / g->stride; a->cw = g->wo / g->stride;
+    a->nclass = g->stride * g->stride * g->stride;
+  } else {
+    a->cd = g->do_; a->ch = g->ho; a->cw = g->wo; a->nclass = 1;
+  }
+  a->td = (a->cd + HT - 1) / HT; a->th = (a->ch + HT - 1) / HT; a->tw = (a->cw + HT - 1) / HT;
+  // largest halo over the classes (all classes share the allocation)
+  int ez = 0, ey = 0, ex = 0;
+  for (int r = 0; r < (g->transposed ? g->stride : 1); ++r) {
+    ClassTaps c = class_info(r, g->k, g->stride, g->pad, g->transposed);
+    const int e = halo_extent(c, g->stride, g->transposed);
+    ez = std::max(ez, e);
+  }
+  ey = ex = ez;
+  a->ez = ez; a->ey = ey; a->ex = ex;
+  a->bn = g->cout % 64 == 0 ? 64 : (g->cout % 32 == 0 ? 32 : 16);
+  const int slot = a->bn * g->cin * 2;
+  if (slot != 2048 && slot != 4096 && slot != 8192) return false;
+  a->halo_bytes = ez * ey * ex * (g->cin + 8) * 2;
+  if (3 * slot + a->halo_bytes > 96 * 1024) return false;
+  if (g->k * g->k * g->k > 64) return false;
+  return true;
+}
+
+bool halo_ok(const cgan3d_conv_geom* g) {
+  HaloArgs a;
+  return g->w_packed == 2 && halo_setup(g, &a);
+}
+
+bool halo_format_ok(const cgan3d_conv_geom* g) {
+  HaloArgs a;
+  return halo_setup(g, &a);
+}
+
+long long halo_mblocks(const cgan3d_conv_geom* g) {
+  HaloArgs a;
+  if (!halo_setup(g, &a)) return 0;
+  return (long long)a.nclass * a.n * a.td * a.th * a.tw;
+}
+
+int halo_launch(const cgan3d_conv_geom* g, const float* x, const float* w, float* y, const Epi& e, hipStream_t st) {
+  HaloArgs a;
+  if (!halo_setup(g, &a)) {
+    set_error("conv_halo: geometry not supported");
+    return CGAN3D_EINVAL;
+  }
+  dim3 grid((unsigned)(a.nclass * a.n * a.td * a.th * a.tw), g->cout / a.bn);
+  const size_t lds = 3 * (size_t)a.bn * g->cin * 2 + a.halo_bytes;
+  const __bf16* wp = reinterpret_cast<const __bf16*>(w);
+#define CG_HL(CI, NT) hipLaunchKernelGGL((conv_halo_kernel<CI, NT>), grid, dim3(256), lds, st, a, x, wp, y, e)
+  if (g->cin == 64) {
+    if (a.bn == 64) CG_HL(64, 4); else if (a.bn == 32) CG_HL(64, 2); else return CGAN3D_EINVAL;
+  } else {
+    if (a.bn == 64) CG_HL(32, 4); else if (a.bn == 32) CG_HL(32, 2); else return CGAN3D_EINVAL;
+  }
+#undef CG_HL
+  return CGAN3D_OK;
+}
+
+int halo_pack(const cgan3d_conv_geom* g, const float* w, void* wp, hipStream_t st) {
+  const int T = g->k * g->k * g->k;
+  const long long total = (long long)T * g->cout * g->cin;
+  int blocks = (int)std::min<long long>((total + 255) / 256, 2048);
+  hipLaunchKernelGGL(pack_halo_kernel, dim3(blocks), dim3(256), 0, st, w, reinterpret_cast<__bf16*>(wp), T, g->cin,
+                     g->cout, (long long)g->w_sa, (long long)g->w_sb);
+  return CGAN3D_OK;
+}
+
+}  // namespace cg

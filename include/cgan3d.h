@@ -50,7 +50,10 @@ typedef struct cgan3d_conv_geom {
   int32_t transposed;
   int32_t reflect;
   int64_t w_sa, w_sb;
-  int32_t w_packed;  /* 1: w is cgan3d_pack_weights() output [tap][a][b], b contiguous */
+  int32_t w_packed;  /* 1: w is cgan3d_pack_weights() output [tap][a][b] f32, b contiguous;
+                      * 2: halo format, bf16 [tap][b][a] with 16-byte granules of a XOR-swizzled
+                      *    by (b mod a/8) — prec BF16, cin 32|64, cout%16==0, no reflect, k<=4,
+                      *    stride<=2 (cgan3d_halo_eligible) */
   int32_t prec;      /* CGAN3D_PREC_F32 (exact f32 MFMA) or CGAN3D_PREC_BF16 (bf16 MFMA, f32 accumulate) */
 } cgan3d_conv_geom;
 
@@ -90,14 +93,18 @@ int64_t cgan3d_conv3d_stats_floats(const cgan3d_conv_geom* g);
 /* Re-layout a torch-layout weight (strides w_sa, w_sb of g) into the packed [tap][a][b] rows the
  * forward/input-grad kernels read as contiguous vectors (once per optimiser step). */
 int64_t cgan3d_packed_weight_floats(const cgan3d_conv_geom* g);
+/* 1 when the geometry (ignoring w_packed) can run the halo-tiled bf16 kernel (w_packed = 2). */
+int32_t cgan3d_halo_eligible(const cgan3d_conv_geom* g);
 int cgan3d_pack_weights(const cgan3d_conv_geom* g, const float* w, float* wp, void* stream);
 /* Many packs in one launch: `descs` is a DEVICE array of n descriptors (built once; the pointers
- * are stable), `max_total` the largest taps*cin*ldb among them. */
+ * are stable), `max_total` the largest element count (taps*cin*ldb or taps*cin*cout) among them. */
 typedef struct cgan3d_pack_desc {
   const float* w;
   float* wp;
   int64_t sa, sb;
   int32_t taps, cin, cout, ldb;
+  int32_t format;  /* w_packed value: 1 f32 [tap][a][b] (ldb-padded), 2 halo bf16 [tap][b][a] */
+  int32_t reserved;
 } cgan3d_pack_desc;
 int cgan3d_pack_weights_multi(const cgan3d_pack_desc* descs, int32_t n, int64_t max_total, void* stream);
 int cgan3d_conv3d_fwd(const cgan3d_conv_geom* g, const float* x, const float* w, float* y,

@@ -169,10 +169,11 @@ GEMM_CASES = [(16, 32, 3, 2, 1, (12, 16, 20)), (64, 64, 3, 1, 1, (6, 8, 10)), (1
 
 @pytest.mark.parametrize("cin,cout,k,s,p,sp", GEMM_CASES)
 @pytest.mark.parametrize("prec", ["f32", "bf16"])
-def test_conv_gemm_packed(cin, cout, k, s, p, sp, prec):
+def test_conv_gemm_packed(cin, cout, k, s, p, sp, prec, monkeypatch):
     """Implicit-GEMM path with packed weights: f32 within 1e-3; bf16 operands (f32 accumulate)
     within 2e-2 (8-bit mantissa inputs), against torch float64."""
     from cgan3d_amd import ops, _lib as L
+    monkeypatch.setattr(ops, "HALO", False)  # the halo-tiled kernel has its own test below
     g = torch.Generator().manual_seed(7 + cin + cout)
     n = 2
     x = torch.randn(n, cin, *sp, generator=g, dtype=torch.float64)
@@ -223,3 +224,69 @@ def test_bf16_step_tracks_f32_step():
     for slot in (0, 2, 4, 5, 6):  # D, GP, sim, HU, G-full
         a, e = float(out["bf16"][slot]), float(out["f32"][slot])
         assert abs(a - e) <= 2e-2 * max(abs(e), 1e-3), (slot, a, e)
+
+
+HALO_CASES = [
+    # transposed-module?, cin, cout, k, s, p, spatial (input of the module)
+    (False, 64, 64, 3, 1, 1, (6, 8, 10)),     # ResNet block conv (partial 4^3 tiles)
+    (False, 64, 64, 3, 1, 1, (16, 16, 16)),
+    (False, 32, 64, 3, 2, 1, (12, 16, 20)),   # downsampling 32 -> 64
+    (False, 32, 64, 4, 2, 1, (16, 16, 16)),   # critic middle layer (k4 s2, 10^3 halo)
+    (False, 64, 32, 3, 1, 1, (5, 7, 9)),      # 32-channel output tiles
+    (True, 64, 32, 3, 2, 1, (4, 6, 8)),       # upsampling ConvTranspose3d 64 -> 32
+]
+
+
+@pytest.mark.parametrize("transposed,cin,cout,k,s,p,sp", HALO_CASES)
+def test_conv_halo_bf16(transposed, cin, cout, k, s, p, sp):
+    """Halo-tiled bf16 kernel (conv_halo.hip): forward with a residual + ReLU + BN-statistics
+    epilogue and the input-grad launch, each against torch float64 within 2e-2 (bf16 operands,
+    f32 accumulate); the BN partials against the kernel's own output within 1e-4."""
+    from cgan3d_amd import ops, _lib as L
+    g = torch.Generator().manual_seed(11 + cin + cout + k)
+    n = 2
+    x = torch.randn(n, cin, *sp, generator=g, dtype=torch.float64)
+    if transposed:
+        w = torch.randn(cin, cout, k, k, k, generator=g, dtype=torch.float64) / np.sqrt(cout * k**3)
+        y = F.conv_transpose3d(x, w, stride=s, padding=p, output_padding=s - 1)
+    else:
+        w = torch.randn(cout, cin, k, k, k, generator=g, dtype=torch.float64) / np.sqrt(cin * k**3)
+        y = F.conv3d(x, w, stride=s, padding=p)
+    res = torch.randn(y.shape, generator=g, dtype=torch.float64)
+    yref = torch.relu(y) + res
+    gy = torch.randn(y.shape, generator=g, dtype=torch.float64)
+    if transposed:
+        dx = F.conv3d(gy, w, stride=s, padding=p)
+    else:
+        dx = torch.nn.grad.conv3d_input(x.shape, w, gy, stride=s, padding=p)
+    din, dout = tuple(sp), tuple(y.shape[2:])
+    wd = w.float().cuda()
+    ps = ops.PackSet(torch.device("cuda"))
+    if transposed:
+        gf0 = ops.convt_fwd_geom(n, din, dout, cin, cout, k, s, p)
+        gd0 = ops.convt_dgrad_geom(n, din, dout, cin, cout, k, s, p)
+    else:
+        gf0 = ops.conv_fwd_geom(n, din, dout, cin, cout, k, s, p)
+        gd0 = ops.conv_dgrad_geom(n, din, dout, cin, cout, k, s, p)
+    gf, wf = ps.add(gf0, wd, L.PREC_BF16)
+    gd, wdp = ps.add(gd0, wd, L.PREC_BF16)
+    ps.pack()
+    assert gf.w_packed == 2 and gd.w_packed == 2, "expected the halo kernel for both launches"
+    yo = torch.empty(n, *dout, cout, device="cuda")
+    stats = torch.empty(ops.stats_floats(gf), device="cuda")
+    ops.conv(gf, _cl(x), wf, yo, ops.epilogue(act=L.ACT_RELU, residual=_cl(res), stats=stats))
+    assert_close(_ncdhw(yo).numpy(), yref.numpy(), 2e-2, "halo fwd")
+    # BN partials -> per-channel mean / biased variance of the kernel's output
+    st = stats.double().cpu().view(-1, 2 * cout + 1)
+    cnt = st[:, 2 * cout]
+    tot = cnt.sum()
+    mean = st[:, :cout].sum(0) / tot
+    bm = st[:, :cout] / cnt.clamp(min=1)[:, None]
+    m2 = st[:, cout:2 * cout].sum(0) + (cnt[:, None] * (bm - mean) ** 2).sum(0)
+    yk = yo.double().cpu().view(-1, cout)
+    assert int(tot) == yk.shape[0]
+    assert_close(mean.numpy(), yk.mean(0).numpy(), 1e-4, "halo stats mean")
+    assert_close((m2 / tot).numpy(), yk.var(0, unbiased=False).numpy(), 1e-4, "halo stats var")
+    dxo = torch.empty(n, *din, cin, device="cuda")
+    ops.conv(gd, _cl(gy), wdp, dxo)
+    assert_close(_ncdhw(dxo).numpy(), dx.numpy(), 2e-2, "halo dgrad")
