@@ -144,6 +144,7 @@ class GeneratorPlan:
                 gf = ops.convt_fwd_geom(n, ly.din, ly.dout, ly.cin, ly.cout, ly.k, ly.s, ly.p)
                 gd = ops.convt_dgrad_geom(n, ly.din, ly.dout, ly.cin, ly.cout, ly.k, ly.s, ly.p)
                 gw = ops.convt_wgrad_geom(n, ly.din, ly.dout, ly.cin, ly.cout, ly.k, ly.s, ly.p)
+            gw = ops.with_prec(gw, prec)
             wt = P[f"{ly.name}.conv.weight"]
             gf, wf = self.packs.add(gf, wt, prec)
             gd, wd = self.packs.add(gd, wt, prec)
@@ -165,9 +166,10 @@ class GeneratorPlan:
             ws = max(ws, ops.wgrad_ws_floats(gw), ops.bn_backward_ws_floats(nvox, ly.cout))
         la = self.last
         pd = tuple(x + 2 * la.p for x in la.din)
-        self.geo_last_fwd = ops.conv_fwd_geom(n, la.din, la.dout, la.cin, 1, la.k, 1, la.p, True)
-        self.geo_last_wgrad = ops.conv_wgrad_geom(n, la.din, la.dout, la.cin, 1, la.k, 1, la.p, True)
-        self.geo_last_dgrad = ops.conv_dgrad_geom(n, pd, la.dout, la.cin, 1, la.k, 1, 0)  # onto the padded grid
+        self.geo_last_fwd = ops.with_prec(ops.conv_fwd_geom(n, la.din, la.dout, la.cin, 1, la.k, 1, la.p, True), prec)
+        self.geo_last_wgrad = ops.with_prec(ops.conv_wgrad_geom(n, la.din, la.dout, la.cin, 1, la.k, 1, la.p, True),
+                                            prec)
+        self.geo_last_dgrad = ops.with_prec(ops.conv_dgrad_geom(n, pd, la.dout, la.cin, 1, la.k, 1, 0), prec)  # padded grid
         self.att = buf(la.dout, 1)
         self.dz_last = buf(la.dout, 1)
         self.dpad = buf(pd, la.cin)

@@ -63,6 +63,15 @@ def with_packing(g: ConvGeom, prec: int = L.PREC_F32) -> ConvGeom:
     return h
 
 
+def with_prec(g: ConvGeom, prec: int) -> ConvGeom:
+    """Copy of ``g`` computing in ``prec`` (unpacked weights): the k7 single-channel kernels and
+    the weight-gradient launches read it."""
+    h = ConvGeom()
+    ctypes.pointer(h)[0] = g
+    h.prec = prec
+    return h
+
+
 def packed_elements(g: ConvGeom) -> int:
     """Elements (f32 or bf16) the pack kernel writes for ``g``."""
     if g.w_packed == 2:
@@ -106,7 +115,7 @@ class PackSet:
     def add(self, g: ConvGeom, w: torch.Tensor, prec: int):
         """Returns (geometry, weight) to launch with: packed when the GEMM path applies."""
         if not uses_gemm(g):
-            return g, w
+            return with_prec(g, prec), w
         gp = with_packing(g, prec)
         wp = torch.zeros(packed_weight_floats(gp), device=self.device)
         self.descs.append((pack_desc(gp, w, wp), wp))

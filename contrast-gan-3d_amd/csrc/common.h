@@ -70,8 +70,17 @@ struct Epi {
 
 // specialised k = 7 generator first/last conv kernels (conv_k7.hip); return 1 when they apply
 int k7_try_fwd(const cgan3d_conv_geom* g, const float* x, const float* w, float* y, const Epi& e, hipStream_t s);
-int k7_try_wgrad(const cgan3d_conv_geom* g, const float* x, const float* go, float* dw, hipStream_t s);
+int k7_try_wgrad(const cgan3d_conv_geom* g, const float* x, const float* go, float* dw, float* ws, hipStream_t s);
+long long k7_wgrad_ws_floats(const cgan3d_conv_geom* g);
+long long k7m_wgrad_ws_floats(const cgan3d_conv_geom* g);
+void k7m_wgrad_launch(const cgan3d_conv_geom* g, bool wide_in, long long wc, const float* x, const float* go, float* dw,
+                      float* ws, hipStream_t s);
 long long k7_n2w_blocks(const cgan3d_conv_geom* g);
+long long k7m_n2w_blocks(const cgan3d_conv_geom* g);
+void k7m_n2w_launch(const cgan3d_conv_geom* g, int P, int reflect, int flip, long long wc, const float* x,
+                    const float* w, float* y, float* stats, hipStream_t s);
+void k7m_w2n_launch(const cgan3d_conv_geom* g, int P, int reflect, long long wc, const float* x, const float* w,
+                    float* y, const Epi& e, hipStream_t s);
 // implicit-GEMM forward / input-grad (conv_gemm.hip)
 int gemm_blocks(const cgan3d_conv_geom* g, long long* mblocks);
 bool halo_ok(const cgan3d_conv_geom* g);         // w_packed == 2 and eligible

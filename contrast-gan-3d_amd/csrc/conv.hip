@@ -471,7 +471,7 @@ static long long wgrad_vpb(long long V, int gx_blocks) {
 
 extern "C" int64_t cgan3d_conv3d_wgrad_ws_floats(const cgan3d_conv_geom* g) {
   if (!g) return -1;
-  return (int64_t)g->k * g->k * g->k * g->cin * g->cout;
+  return std::max<int64_t>((int64_t)g->k * g->k * g->k * g->cin * g->cout, k7_wgrad_ws_floats(g));
 }
 
 extern "C" int cgan3d_conv3d_wgrad(const cgan3d_conv_geom* g, const float* gathered, const float* aligned, float* dw,
@@ -492,7 +492,7 @@ extern "C" int cgan3d_conv3d_wgrad(const cgan3d_conv_geom* g, const float* gathe
       set_error("cgan3d_conv3d_wgrad: memset failed");
       return CGAN3D_EHIP;
     }
-    if (k7_try_wgrad(g, gathered, aligned, dw, s)) {
+    if (k7_try_wgrad(g, gathered, aligned, dw, ws, s)) {
       CG_LAUNCH_CHECK("k7 wgrad");
       return CGAN3D_OK;
     }

@@ -15,35 +15,9 @@
 // each thread's 10-voxel row window is two b128 + one b64 read); thread = 4 consecutive voxels
 // along W.  Weights live in LDS and are read as broadcast b128.  The last conv's input-grad is the
 // same n2w kernel with the taps flipped over the zero-padded grid (folded by cgan3d_reflect_fold).
-#include "common.h"
+#include "k7.h"
 
 namespace cg {
-
-constexpr int K7 = 7, KT7 = 343;
-constexpr int TD = 4, TH = 8, TW = 32;
-constexpr int HD = TD + 6, HH = TH + 6, HWD = TW + 6, HWP = 40;  // halo dims, padded row
-constexpr int HALO = HD * HH * HWP;
-
-struct K7Args {
-  int n, di, hi, wi, do_, ho, wo;
-  int P;          // src = o + t - P
-  int reflect;    // mirror out-of-range source (else zero)
-  int flip;       // use W[c, 342 - t]
-  long long wc;   // weight stride of the wide channel (tap stride 1)
-  int tiles_d, tiles_h, tiles_w;
-};
-
-__device__ __forceinline__ void k7_tile(const K7Args& a, int bid, int* n, int* d0, int* h0, int* w0) {
-  int tw = bid % a.tiles_w; bid /= a.tiles_w;
-  int th = bid % a.tiles_h; bid /= a.tiles_h;
-  int td = bid % a.tiles_d; *n = bid / a.tiles_d;
-  *d0 = td * TD; *h0 = th * TH; *w0 = tw * TW;
-}
-
-__device__ __forceinline__ int k7_src(int i, int n, int reflect) {
-  if (reflect) i = reflect_idx(i, n);  // halo cells past a partial tile may still fall outside
-  return (i >= 0 && i < n) ? i : -1;
-}
 
 // halo of a single-channel volume, or of channels [c0, c0+CC) of a C-channel volume ([cc][halo])
 template <int C, int CC>
@@ -340,11 +314,20 @@ static int k7_blocks(const K7Args& a) { return a.n * a.tiles_d * a.tiles_h * a.t
 
 // Which shapes the k7 kernels take (wide side C in {8, 16}); everything else -> generic kernels.
 static bool k7_wide_ok(int c) { return c == 8 || c == 16; }
+// bf16 MFMA variants (conv_k7_mfma.hip): 16-channel wide side, CGAN3D_PREC_BF16 geometries
+static bool k7m_ok(const cgan3d_conv_geom* g, int wide) { return g->prec == CGAN3D_PREC_BF16 && wide == 16; }
 
 // number of blocks the n2w kernel uses for this geometry (0 if the k7 path does not apply);
 // sizes the BatchNorm partial-statistics buffer (cgan3d_conv3d_stats_floats)
+long long k7_wgrad_ws_floats(const cgan3d_conv_geom* g) {
+  if (g->k != 7 || g->stride != 1 || g->transposed) return 0;
+  if ((g->cout == 1 && k7m_ok(g, g->cin)) || (g->cin == 1 && k7m_ok(g, g->cout))) return k7m_wgrad_ws_floats(g);
+  return 0;
+}
+
 long long k7_n2w_blocks(const cgan3d_conv_geom* g) {
   if (g->k != 7 || g->stride != 1 || g->cin != 1 || !k7_wide_ok(g->cout)) return 0;
+  if (k7m_ok(g, g->cout)) return k7m_n2w_blocks(g);
   return k7_blocks(k7_args(g, 0, 0, 0, 0));
 }
 
@@ -354,6 +337,11 @@ int k7_try_fwd(const cgan3d_conv_geom* g, const float* x, const float* w, float*
   if (g->k != 7 || g->stride != 1) return 0;
   if (g->cin == 1 && k7_wide_ok(g->cout) && !e.bias && !e.residual && !e.mask_src && !e.out2 &&
       e.act == CGAN3D_ACT_NONE) {
+    if (k7m_ok(g, g->cout)) {
+      if (!g->transposed) k7m_n2w_launch(g, g->pad, g->reflect, 0, g->w_sb, x, w, y, e.stats, s);
+      else k7m_n2w_launch(g, g->k - 1 - g->pad, 0, 1, g->w_sb, x, w, y, e.stats, s);
+      return 1;
+    }
     K7Args a;
     if (!g->transposed) a = k7_args(g, g->pad, g->reflect, 0, g->w_sb);
     else a = k7_args(g, g->k - 1 - g->pad, 0, 1, g->w_sb);  // input-grad: flipped taps, zero pad
@@ -363,6 +351,10 @@ int k7_try_fwd(const cgan3d_conv_geom* g, const float* x, const float* w, float*
   }
   if (g->cout == 1 && k7_wide_ok(g->cin) && !g->transposed && !e.residual && !e.mask_src && !e.stats &&
       (e.act == CGAN3D_ACT_NONE || e.act == CGAN3D_ACT_TANH)) {
+    if (k7m_ok(g, g->cin)) {
+      k7m_w2n_launch(g, g->pad, g->reflect, g->w_sa, x, w, y, e, s);
+      return 1;
+    }
     K7Args a = k7_args(g, g->pad, g->reflect, 0, g->w_sa);
     if (g->cin == 16)
       hipLaunchKernelGGL((k7_w2n_kernel<16, 2>), dim3(k7_blocks(a)), dim3(256), 0, s, a, x, w, y, e.bias, e.act,
@@ -376,8 +368,16 @@ int k7_try_fwd(const cgan3d_conv_geom* g, const float* x, const float* w, float*
 }
 
 // Weight-grad launch (dw zeroed by the caller unless accumulating); returns 1 if handled.
-int k7_try_wgrad(const cgan3d_conv_geom* g, const float* x, const float* go, float* dw, hipStream_t s) {
+int k7_try_wgrad(const cgan3d_conv_geom* g, const float* x, const float* go, float* dw, float* ws, hipStream_t s) {
   if (g->k != 7 || g->stride != 1 || g->transposed) return 0;
+  if (g->cout == 1 && k7m_ok(g, g->cin)) {
+    k7m_wgrad_launch(g, true, g->w_sa, x, go, dw, ws, s);
+    return 1;
+  }
+  if (g->cin == 1 && k7m_ok(g, g->cout)) {
+    k7m_wgrad_launch(g, false, g->w_sb, x, go, dw, ws, s);
+    return 1;
+  }
   if (g->cout == 1 && k7_wide_ok(g->cin)) {
     K7Args a = k7_args(g, g->pad, g->reflect, 0, g->w_sa);
     const int C = g->cin;

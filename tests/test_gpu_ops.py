@@ -290,3 +290,64 @@ def test_conv_halo_bf16(transposed, cin, cout, k, s, p, sp):
     dxo = torch.empty(n, *din, cin, device="cuda")
     ops.conv(gd, _cl(gy), wdp, dxo)
     assert_close(_ncdhw(dxo).numpy(), dx.numpy(), 2e-2, "halo dgrad")
+
+
+@pytest.mark.parametrize("sp", [(12, 20, 36), (16, 16, 16)])
+def test_k7_bf16_mfma(sp):
+    """bf16 MFMA variants of the generator's k7 convs (conv_k7_mfma.hip), all four roles plus the
+    last conv's input-grad, against torch float64 within 2e-2 (bf16 operands, f32 accumulate); the
+    first conv's BN partials against its own output within 1e-4."""
+    from cgan3d_amd import ops, _lib as L
+    BF = L.PREC_BF16
+    g = torch.Generator().manual_seed(77)
+    n, k, p = 2, 7, 3
+    x1 = torch.randn(n, 1, *sp, generator=g, dtype=torch.float64)
+    x16 = torch.randn(n, 16, *sp, generator=g, dtype=torch.float64)
+    wf = (torch.randn(16, 1, k, k, k, generator=g, dtype=torch.float64) / np.sqrt(k**3)).requires_grad_()
+    wl = (torch.randn(1, 16, k, k, k, generator=g, dtype=torch.float64) / np.sqrt(16 * k**3)).requires_grad_()
+    bl = torch.randn(1, generator=g, dtype=torch.float64)
+    x16r = x16.clone().requires_grad_()
+    yf = _ref_conv(x1, wf, 1, p, True)
+    zl = _ref_conv(x16r, wl, 1, p, True) + bl.view(1, 1, 1, 1, 1)
+    yl = torch.tanh(zl)
+    gf = torch.randn(yf.shape, generator=g, dtype=torch.float64)
+    gl = torch.randn(zl.shape, generator=g, dtype=torch.float64)
+    dwf, = torch.autograd.grad(yf, (wf,), gf)
+    dx16, dwl = torch.autograd.grad(zl, (x16r, wl), gl)
+    dims = tuple(sp)
+    # first conv forward (+ BN partials)
+    geo = ops.with_prec(ops.conv_fwd_geom(n, dims, dims, 1, 16, k, 1, p, True), BF)
+    yo = torch.empty(n, *dims, 16, device="cuda")
+    stats = torch.empty(ops.stats_floats(geo), device="cuda")
+    ops.conv(geo, _cl(x1), wf.detach().float().cuda(), yo, ops.epilogue(stats=stats))
+    assert_close(_ncdhw(yo).numpy(), yf.detach().numpy(), 2e-2, "k7 n2w fwd")
+    st = stats.double().cpu().view(-1, 33)
+    yk = yo.double().cpu().view(-1, 16)
+    assert int(st[:, 32].sum()) == yk.shape[0]
+    assert_close((st[:, :16].sum(0) / yk.shape[0]).numpy(), yk.mean(0).numpy(), 1e-4, "k7 stats mean")
+    # last conv forward (bias, tanh, out2 = minuend - y)
+    geo = ops.with_prec(ops.conv_fwd_geom(n, dims, dims, 16, 1, k, 1, p, True), BF)
+    att = torch.empty(n, *dims, 1, device="cuda")
+    o2 = torch.empty_like(att)
+    mn = _cl(x1)
+    ops.conv(geo, _cl(x16), wl.detach().float().cuda(), att,
+             ops.epilogue(bias=bl.float().cuda(), act=L.ACT_TANH, minuend=mn, out2=o2))
+    assert_close(_ncdhw(att).numpy(), yl.detach().numpy(), 2e-2, "k7 w2n fwd")
+    assert_close(_ncdhw(o2).numpy(), (x1 - yl).detach().numpy(), 2e-2, "k7 w2n out2")
+    # weight grads
+    for name, gw, gath, alig, ref, w in (
+            ("k7 wg n2w", ops.conv_wgrad_geom(n, dims, dims, 1, 16, k, 1, p, True), _cl(x1), _cl(gf), dwf, wf),
+            ("k7 wg w2n", ops.conv_wgrad_geom(n, dims, dims, 16, 1, k, 1, p, True), _cl(x16), _cl(gl), dwl, wl)):
+        gw = ops.with_prec(gw, BF)
+        ws = torch.empty(ops.wgrad_ws_floats(gw), device="cuda")
+        dwo = torch.empty(w.shape, device="cuda")
+        ops.wgrad(gw, gath, alig, dwo, ws)
+        assert_close(dwo.double().cpu().numpy(), ref.numpy(), 2e-2, name)
+    # last conv input-grad: flipped n2w onto the zero-padded grid + reflect fold (as the engine)
+    pd = tuple(d + 2 * p for d in dims)
+    gd = ops.with_prec(ops.conv_dgrad_geom(n, pd, dims, 16, 1, k, 1, 0), BF)
+    dpad = torch.empty(n, *pd, 16, device="cuda")
+    ops.conv(gd, _cl(gl), wl.detach().float().cuda(), dpad)
+    dxo = torch.empty(n, *dims, 16, device="cuda")
+    ops.reflect_fold(dpad, dxo, n, dims, 16, p)
+    assert_close(_ncdhw(dxo).numpy(), dx16.numpy(), 2e-2, "k7 n2w dgrad")

@@ -143,10 +143,19 @@ def test_step_matches_oracle_64(S, b):
         for k, slot in (("D", 0), ("G", 3), ("sim", 4), ("HU", 5), ("G-full", 6)):
             assert_parity(losses[slot], ref32[k], ref[k], f"it{it} {k}")
         for net, arena in (("G", eng.g_arena), ("D", eng.d_arena)):
+            # the generator's gradients share one ill-conditioned path (BatchNorm backward at the
+            # upsampling layers amplifies rounding, see DESIGN.md "Parity"): the yardstick is the
+            # reference's own worst float32 deviation over the network's gradient tensors at this
+            # step, so a tensor on which float32 happens to land close to float64 is not held to a
+            # tighter bar than the network's rounding level (tests/diag_parity.py prints the table)
+            yard = max(float(np.abs(rec32[net][k].numpy() - rec[net][k].numpy()).max()) /
+                       max(float(np.abs(rec[net][k].numpy()).max()), 1e-30)
+                       for k in arena.gviews if k != "model.last.bias")
+            rtol = max(1e-3, 2.0 * yard)
             for k, gv in arena.gviews.items():
                 atol = 1e-7 if k == "model.last.bias" else 0.0  # exactly 0 in real arithmetic
                 assert_parity(gv.cpu().numpy(), rec32[net][k].numpy(), rec[net][k].numpy(), f"it{it} grad {net} {k}",
-                              atol=atol)
+                              rtol=rtol, atol=atol)
         # start the next iteration from the device's state (params, BN buffers, Adam moments)
         for k, v in g.state_dict().items():
             gpar[k].copy_(v.detach().cpu())
