@@ -20,6 +20,27 @@ namespace cg {
 
 typedef __bf16 bf16x8_k __attribute__((ext_vector_type(8)));
 
+// Staging from global memory with every load of the thread in flight at once: element i < total
+// of the tile comes from src[off(i)] (off < 0: zero).  Loads use clamped addresses and no
+// branches (a branch per load makes hipcc wait for each one in turn), then `put(i, value)`.
+template <int PER, class T, class Off, class Put>
+__device__ __forceinline__ void k7m_stage(const T* __restrict__ src, int total, Off off, Put put) {
+  T v[PER];
+  bool ok[PER];
+#pragma unroll
+  for (int k = 0; k < PER; ++k) {
+    const int i = threadIdx.x + 256 * k;
+    const long long o = i < total ? off(i) : -1;
+    ok[k] = o >= 0;
+    v[k] = src[ok[k] ? o : 0];
+  }
+#pragma unroll
+  for (int k = 0; k < PER; ++k) {
+    const int i = threadIdx.x + 256 * k;
+    if (i < total) put(i, ok[k] ? v[k] : T{});
+  }
+}
+
 // ---- n2w tile: 4 (d) x 8 (h) x 16 (w) outputs, wave = one d-slice (8 rows of 16 voxels)
 constexpr int N_TD = 4, N_TH = 8, N_TW = 16;
 constexpr int N_HD = N_TD + 6, N_HH = N_TH + 6, N_HW = 24;  // x halo (23 used: ow 0..15 + tw 0..7)
@@ -42,26 +63,26 @@ __global__ __launch_bounds__(256) void k7m_n2w_kernel(K7Args a, const float* __r
     const int td_ = bid % a.tiles_d; n = bid / a.tiles_d;
     d0 = td_ * N_TD; h0 = th_ * N_TH; w0 = tw_ * N_TW;
   }
-  for (int i = tid; i < N_PAIRS * C * 8; i += 256) {
-    const int tw = i & 7, c = (i >> 3) & 15, p = i >> 7;
-    float v = 0.f;
-    if (p < 49 && tw < K7) {
-      const int t = p * K7 + tw;
-      v = w[(long long)c * a.wc + (a.flip ? KT7 - 1 - t : t)];
-    }
-    wt[i] = (__bf16)v;
-  }
-  for (int i = tid; i < N_ROWS * N_HW; i += 256) {
-    const int hw = i % N_HW, r = i / N_HW, hh = r % N_HH, hd = r / N_HH;
-    float v = 0.f;
-    if (hw < N_TW + 7) {
-      const int id = k7_src(d0 + hd - a.P, a.di, a.reflect);
-      const int ih = k7_src(h0 + hh - a.P, a.hi, a.reflect);
-      const int iw = k7_src(w0 + hw - a.P, a.wi, a.reflect);
-      if ((id | ih | iw) >= 0) v = x[((long long)(n * a.di + id) * a.hi + ih) * a.wi + iw];
-    }
-    xs[i] = v;
-  }
+  k7m_stage<(N_PAIRS * C * 8 + 255) / 256>(
+      w, N_PAIRS * C * 8,
+      [&](int i) -> long long {
+        const int tw = i & 7, c = (i >> 3) & 15, p = i >> 7;
+        if (p >= 49 || tw >= K7) return -1;
+        const int t = p * K7 + tw;
+        return (long long)c * a.wc + (a.flip ? KT7 - 1 - t : t);
+      },
+      [&](int i, float v) { wt[i] = (__bf16)v; });
+  k7m_stage<(N_ROWS * N_HW + 255) / 256>(
+      x, N_ROWS * N_HW,
+      [&](int i) -> long long {
+        const int hw = i % N_HW, r = i / N_HW, hh = r % N_HH, hd = r / N_HH;
+        if (hw >= N_TW + 7) return -1;
+        const int id = k7_src(d0 + hd - a.P, a.di, a.reflect);
+        const int ih = k7_src(h0 + hh - a.P, a.hi, a.reflect);
+        const int iw = k7_src(w0 + hw - a.P, a.wi, a.reflect);
+        return (id | ih | iw) >= 0 ? ((long long)(n * a.di + id) * a.hi + ih) * a.wi + iw : -1;
+      },
+      [&](int i, float v) { xs[i] = v; });
   __syncthreads();
   for (int i = tid; i < N_ROWS * N_TW; i += 256) {
     const int ow = i % N_TW, r = i / N_TW;
@@ -171,29 +192,33 @@ __global__ __launch_bounds__(256) void k7m_w2n_kernel(K7Args a, const float* __r
     const int td_ = bid % a.tiles_d; n = bid / a.tiles_d;
     d0 = td_ * W_TD; h0 = th_ * W_TH; w0 = tw_ * W_TW;
   }
-  for (int i = tid; i < 49 * 8 * C; i += 256) {
-    const int c = i & 15, tw = (i >> 4) & 7, p = i >> 7;
-    wt[i] = (__bf16)(tw < K7 ? w[(long long)c * a.wc + p * K7 + tw] : 0.f);
-  }
+  k7m_stage<(49 * 8 * C + 255) / 256>(
+      w, 49 * 8 * C,
+      [&](int i) -> long long {
+        const int c = i & 15, tw = (i >> 4) & 7, p = i >> 7;
+        return tw < K7 ? (long long)c * a.wc + p * K7 + tw : -1;
+      },
+      [&](int i, float v) { wt[i] = (__bf16)v; });
   const int g = lane >> 4, r16 = lane & 15;
   const int odl = r16 >> 2, ohl = r16 & 3;  // this lane's B column: output row (od, oh)
   f32x4 acc = {0.f, 0.f, 0.f, 0.f};
   for (int half = 0; half < 2; ++half) {
     if (half) __syncthreads();  // all waves done reading the first half
-    for (int i = tid; i < W_ROWS * W_HW * 2; i += 256) {
-      const int q = i & 1, v = i >> 1, hw = v % W_HW, r = v / W_HW, hh = r % W_HH, hd = r / W_HH;
-      f32x4 val = {0.f, 0.f, 0.f, 0.f};
-      if (hw < W_TW + 7) {
-        const int id = k7_src(d0 + hd - a.P, a.di, a.reflect);
-        const int ih = k7_src(h0 + hh - a.P, a.hi, a.reflect);
-        const int iw = k7_src(w0 + hw - a.P, a.wi, a.reflect);
-        if ((id | ih | iw) >= 0)
-          val = *reinterpret_cast<const f32x4*>(x + (((long long)(n * a.di + id) * a.hi + ih) * a.wi + iw) * C +
-                                                half * 8 + 4 * q);
-      }
-      __bf16* d = hs + v * 8 + 4 * q;
-      d[0] = (__bf16)val[0]; d[1] = (__bf16)val[1]; d[2] = (__bf16)val[2]; d[3] = (__bf16)val[3];
-    }
+    k7m_stage<(W_ROWS * W_HW * 2 + 255) / 256>(
+        reinterpret_cast<const f32x4*>(x), W_ROWS * W_HW * 2,
+        [&](int i) -> long long {  // float4 index
+          const int q = i & 1, v = i >> 1, hw = v % W_HW, r = v / W_HW, hh = r % W_HH, hd = r / W_HH;
+          if (hw >= W_TW + 7) return -1;
+          const int id = k7_src(d0 + hd - a.P, a.di, a.reflect);
+          const int ih = k7_src(h0 + hh - a.P, a.hi, a.reflect);
+          const int iw = k7_src(w0 + hw - a.P, a.wi, a.reflect);
+          return (id | ih | iw) >= 0 ? (((long long)(n * a.di + id) * a.hi + ih) * a.wi + iw) * (C / 4) + half * 2 + q
+                                     : -1;
+        },
+        [&](int i, f32x4 val) {
+          __bf16* d = hs + (i >> 1) * 8 + 4 * (i & 1);
+          d[0] = (__bf16)val[0]; d[1] = (__bf16)val[1]; d[2] = (__bf16)val[2]; d[3] = (__bf16)val[3];
+        });
     __syncthreads();
 #pragma unroll 1
     for (int pr = wave * 25; pr < wave * 25 + 25; ++pr) {
@@ -280,17 +305,17 @@ __global__ __launch_bounds__(256) void k7m_wg_n2w_kernel(K7Args a, const float* 
     int n, d0, h0, w0;
     k7m_tile(a, tile, &n, &d0, &h0, &w0);
     __syncthreads();
-    for (int i = tid; i < G_ROWS_IN * HW; i += 256) {
-      const int hw = i % HW, r = i / HW, hh = r % (G_TH + 6), hd = r / (G_TH + 6);
-      float v = 0.f;
-      if (hw < G_TW + 6) {
-        const int id = k7_src(d0 + hd - a.P, a.di, a.reflect);
-        const int ih = k7_src(h0 + hh - a.P, a.hi, a.reflect);
-        const int iw = k7_src(w0 + hw - a.P, a.wi, a.reflect);
-        if ((id | ih | iw) >= 0) v = x[((long long)(n * a.di + id) * a.hi + ih) * a.wi + iw];
-      }
-      xs[i] = v;
-    }
+    k7m_stage<(G_ROWS_IN * HW + 255) / 256>(
+        x, G_ROWS_IN * HW,
+        [&](int i) -> long long {
+          const int hw = i % HW, r = i / HW, hh = r % (G_TH + 6), hd = r / (G_TH + 6);
+          if (hw >= G_TW + 6) return -1;
+          const int id = k7_src(d0 + hd - a.P, a.di, a.reflect);
+          const int ih = k7_src(h0 + hh - a.P, a.hi, a.reflect);
+          const int iw = k7_src(w0 + hw - a.P, a.wi, a.reflect);
+          return (id | ih | iw) >= 0 ? ((long long)(n * a.di + id) * a.hi + ih) * a.wi + iw : -1;
+        },
+        [&](int i, float v) { xs[i] = v; });
     __syncthreads();
     for (int i = tid; i < 8 * G_ROWS_IN * 2; i += 256) {  // (tw, row, half of 16)
       const int hf = i & 1, r = (i >> 1) % G_ROWS_IN, tw = (i >> 1) / G_ROWS_IN;
@@ -302,16 +327,28 @@ __global__ __launch_bounds__(256) void k7m_wg_n2w_kernel(K7Args a, const float* 
     }
     __syncthreads();
     // K-steps of 32 outputs = 2 output rows x 16; wave takes K-steps wave, wave+4, ...
-    for (int ks = wave; ks < G_OROWS / 2; ks += 4) {
-      const int orow = 2 * ks + (g >> 1), odl = orow / G_TH, ohl = orow % G_TH, owl = 8 * (g & 1);
-      const int od = d0 + odl, oh = h0 + ohl;
-      bf16x8_k av;
-      {
-        const bool rv = od < a.do_ && oh < a.ho;
-        const long long vb = (((long long)(n * a.do_ + od) * a.ho + oh) * a.wo + w0 + owl) * 16 + r16;
+    constexpr int KS = G_OROWS / 2 / 4;  // K-steps per wave per tile
+    float gv[KS][8];
 #pragma unroll
-        for (int e = 0; e < 8; ++e) av[e] = (__bf16)((rv && w0 + owl + e < a.wo) ? go[vb + e * 16] : 0.f);
+    for (int kk = 0; kk < KS; ++kk) {  // issue every load of the wave's K-steps first
+      const int orow = 2 * (wave + 4 * kk) + (g >> 1), owl = 8 * (g & 1);
+      const int od = d0 + orow / G_TH, oh = h0 + orow % G_TH;
+      const bool rv = od < a.do_ && oh < a.ho;
+      const long long vb = (((long long)(n * a.do_ + od) * a.ho + oh) * a.wo + w0 + owl) * 16 + r16;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const bool ok = rv && w0 + owl + e < a.wo;
+        gv[kk][e] = go[ok ? vb + e * 16 : 0];
+        if (!ok) gv[kk][e] = 0.f;
       }
+    }
+#pragma unroll
+    for (int kk = 0; kk < KS; ++kk) {
+      const int ks = wave + 4 * kk;
+      const int orow = 2 * ks + (g >> 1), odl = orow / G_TH, ohl = orow % G_TH, owl = 8 * (g & 1);
+      bf16x8_k av;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) av[e] = (__bf16)gv[kk][e];
 #pragma unroll
       for (int j = 0; j < G_NT; ++j) {
         const int pair = 2 * j + (r16 >> 3), tw = r16 & 7;
@@ -360,34 +397,51 @@ __global__ __launch_bounds__(256) void k7m_wg_w2n_kernel(K7Args a, const float* 
       *reinterpret_cast<bf16x8_k*>(sd + ((tw * G_OROWS + r) * Q + 8 * q8)) = u;
     }
     __syncthreads();
-    for (int r = wave; r < G_ROWS_IN; r += 4) {
-      const int id = r / (G_TH + 6), ih = r % (G_TH + 6);
-      bf16x8_k av;
-      {
+    // this lane's 8 halo columns (fixed over the rows)
+    int swc[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int q = 8 * g + e;
+      swc[e] = q < G_TW + 6 ? k7_src(w0 + q - a.P, a.wi, a.reflect) : -1;
+    }
+    constexpr int RB = 5;  // rows per batch: 5 x 8 loads in flight per lane
+    static_assert((G_ROWS_IN / 4) % RB == 0, "row batches");
+    for (int rb0 = wave; rb0 < G_ROWS_IN; rb0 += 4 * RB) {
+      float xv[RB][8];
+#pragma unroll
+      for (int b = 0; b < RB; ++b) {
+        const int r = rb0 + 4 * b, id = r / (G_TH + 6), ih = r % (G_TH + 6);
         const int sd_ = k7_src(d0 + id - a.P, a.di, a.reflect);
         const int sh_ = k7_src(h0 + ih - a.P, a.hi, a.reflect);
-        const long long rb = ((long long)(n * a.di + sd_) * a.hi + sh_) * a.wi;
+        const long long rowb = ((long long)(n * a.di + sd_) * a.hi + sh_) * a.wi;
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
-          const int q = 8 * g + e;
-          const int sw = q < G_TW + 6 ? k7_src(w0 + q - a.P, a.wi, a.reflect) : -1;
-          av[e] = (__bf16)(((sd_ | sh_ | sw) >= 0) ? x[(rb + sw) * 16 + r16] : 0.f);
+          const bool ok = (sd_ | sh_ | swc[e]) >= 0;
+          xv[b][e] = x[ok ? (rowb + swc[e]) * 16 + r16 : 0];
+          if (!ok) xv[b][e] = 0.f;
         }
       }
 #pragma unroll
-      for (int j = 0; j < G_NT; ++j) {
-        // the tile's pairs (2j, 2j+1) reach an output row of this tile from input row (id, ih)?
-        const int p0 = 2 * j, p1 = 2 * j + 1;
-        const int a0 = id - p0 / K7, b0 = ih - p0 % K7, a1 = id - p1 / K7, b1 = ih - p1 % K7;
-        const bool v0 = a0 >= 0 && a0 < G_TD && b0 >= 0 && b0 < G_TH;
-        const bool v1 = p1 < 49 && a1 >= 0 && a1 < G_TD && b1 >= 0 && b1 < G_TH;
-        if (v0 || v1) {
-          const bool mine = (r16 >> 3) ? v1 : v0;
-          const int odl = (r16 >> 3) ? a1 : a0, ohl = (r16 >> 3) ? b1 : b0, tw = r16 & 7;
-          bf16x8_k bv = *reinterpret_cast<const bf16x8_k*>(
-              sd + ((tw * G_OROWS + (mine ? odl * G_TH + ohl : 0)) * Q + 8 * g));
-          if (!mine) bv = bf16x8_k{};
-          acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, bv, acc[j], 0, 0, 0);
+      for (int b = 0; b < RB; ++b) {
+        const int r = rb0 + 4 * b, id = r / (G_TH + 6), ih = r % (G_TH + 6);
+        bf16x8_k av;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) av[e] = (__bf16)xv[b][e];
+#pragma unroll
+        for (int j = 0; j < G_NT; ++j) {
+          // the tile's pairs (2j, 2j+1) reach an output row of this tile from input row (id, ih)?
+          const int p0 = 2 * j, p1 = 2 * j + 1;
+          const int a0 = id - p0 / K7, b0 = ih - p0 % K7, a1 = id - p1 / K7, b1 = ih - p1 % K7;
+          const bool v0 = a0 >= 0 && a0 < G_TD && b0 >= 0 && b0 < G_TH;
+          const bool v1 = p1 < 49 && a1 >= 0 && a1 < G_TD && b1 >= 0 && b1 < G_TH;
+          if (v0 || v1) {
+            const bool mine = (r16 >> 3) ? v1 : v0;
+            const int odl = (r16 >> 3) ? a1 : a0, ohl = (r16 >> 3) ? b1 : b0, tw = r16 & 7;
+            bf16x8_k bv = *reinterpret_cast<const bf16x8_k*>(
+                sd + ((tw * G_OROWS + (mine ? odl * G_TH + ohl : 0)) * Q + 8 * g));
+            if (!mine) bv = bf16x8_k{};
+            acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, bv, acc[j], 0, 0, 0);
+          }
         }
       }
     }
