@@ -10,9 +10,14 @@ reference architecture.  "patches" = subopt patches corrected per second (SURVEY
 value = all ranks' patches / max-over-ranks wall time of the K timed steps.  Inputs are resident in
 HBM when the timed region starts (a device-to-device copy into the engine's slots is inside it).
 
-Extra JSON fields: ``roofline`` for the dominant kernel (HIP events around its launches during
-the timed steps; algorithmic FLOPs from the layer geometry) and ``cpu_baseline`` (the oracle —
-torch fp32 on the host cores — on a bounded sample, rank 0 only, N=1 only).
+Extra JSON fields: ``roofline`` for the dominant kernel (HIP events around each of its launches
+over eager steps run after the timed region, on the launch stream; algorithmic FLOPs from the
+launch geometry, 2 * out-voxels * Cout * Cin * k^3) and ``cpu_baseline`` (the oracle — torch fp32
+on the host cores — on a bounded sample, rank 0 only, N=1 only).
+
+Precision: ``--precision bf16`` (default; BASELINE.json's metric is quoted in bf16) runs every
+convolution on bf16 MFMA operands with fp32 accumulation, BatchNorm / losses / Adam in fp32;
+``--precision f32`` is the exact-fp32 parity path.
 """
 from __future__ import annotations
 
@@ -38,6 +43,15 @@ HBM_PEAK_GBS = 8000.0
 def conv_flops(n, dout, cin, cout, k):
     """FlopCounterMode-style conv FLOPs: 2 * N * Cout * |out| * Cin * k^3."""
     return 2.0 * n * cout * dout[0] * dout[1] * dout[2] * cin * k**3
+
+
+# roofline candidates: kernel description, launch role, geometry predicate, bound, precision of the MFMA
+ROOFLINES = {
+    "halo_res": ("conv_halo_kernel<64,4>: ResNet-block Conv3d 64->64 k3 s1 at (S/4)^3, forward + input-grad",
+                 "conv", lambda g: g.w_packed == 2 and g.cin == 64 and g.cout == 64 and g.k == 3 and g.stride == 1),
+    "k7_w2n": ("k7m_w2n_kernel: generator last Conv3d 16->1 k7 (+bias, tanh, opt_hat) forward",
+               "conv", lambda g: g.k == 7 and g.cin == 16 and g.cout == 1),
+}
 
 
 def cpu_baseline(size, seconds, g_args):
@@ -81,8 +95,9 @@ def main():
     ap.add_argument("--batch", type=int, default=4)
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--precision", choices=["f32", "bf16"], default="f32",
-                    help="MFMA operand precision of the implicit-GEMM convs (accumulation is f32)")
+    ap.add_argument("--precision", choices=["f32", "bf16"], default="bf16",
+                    help="MFMA operand precision of the convolutions (accumulation is f32)")
+    ap.add_argument("--roofline", choices=sorted(ROOFLINES), default="halo_res")
     ap.add_argument("--no-graph", action="store_true", help="launch eagerly instead of replaying a HIP graph")
     args = ap.parse_args()
 
@@ -121,19 +136,22 @@ def main():
         batches.append((torch.from_numpy(opt).to(dev), torch.from_numpy(sub).to(dev),
                         torch.from_numpy(seg).to(dev), torch.rand(B, device=dev)))
 
-    # dominant kernel: the generator's last conv (16 -> 1, k7 reflect, bias, tanh) forward
-    la = eng.G.last
-    roof_flops = conv_flops(B, la.dout, la.cin, 1, la.k)
-    ev = []
+    from cgan3d_amd import ops
+    roof_desc, roof_role, roof_match = ROOFLINES[args.roofline]
+    ev = []  # (start, end, algorithmic flops) per timed launch
+
+    def hook(role, geo):
+        if role != roof_role or not roof_match(geo):
+            return None
+        e = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+        ev.append((*e, conv_flops(geo.n, (geo.do_, geo.ho, geo.wo), geo.cin, geo.cout, geo.k)))
+        return e
 
     def one_step(i, timed):
         eng.load_inputs(*batches[i % len(batches)])
-        if timed:
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            eng.G.timer = (e0, e1)
-            ev.append((e0, e1))
+        ops.LAUNCH_HOOK = hook if timed else None
         eng.step()
-        eng.G.timer = None
+        ops.LAUNCH_HOOK = None
 
     def graph_step(i):
         eng.load_inputs(*batches[i % len(batches)])
@@ -153,24 +171,26 @@ def main():
         if use_graph:
             graph_step(i)
         else:
-            one_step(i, True)
+            one_step(i, False)
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
-    if use_graph:  # the roofline kernel's launch time: HIP events around it over eager steps
-        for i in range(min(args.steps, 10)):
-            one_step(i, True)
-        torch.cuda.synchronize()
+    # the roofline kernel's launch times: HIP events around each launch over eager steps
+    for i in range(min(args.steps, 10)):
+        one_step(i, True)
+    torch.cuda.synchronize()
     if dist:
         t = torch.tensor([el], device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
     losses = eng.losses.cpu().numpy()
     assert np.isfinite(losses).all(), f"non-finite losses {losses}"
-    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    kern_ms = float(np.mean([a.elapsed_time(b) for a, b, _ in ev]))
+    roof_flops = float(np.mean([f for _, _, f in ev]))
     achieved = roof_flops / (kern_ms * 1e-3) / 1e12
+    peak = BF16_PEAK_TFLOPS if args.precision == "bf16" else F32_PEAK_TFLOPS
     ms = el / args.steps * 1e3
     value = world * B * args.steps / el
     out = {
@@ -178,15 +198,14 @@ def main():
         "value": round(value, 3), "unit": "patches/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "f32" if args.precision == "f32" else "bf16 MFMA operands (implicit-GEMM convs), f32 elsewhere",
+        "dtype": args.precision,
         "data": "synthetic",
         "config": {"workload": f"{S}^3 patches, {B} OPT + {B} LOW/HIGH per GPU, full G+D step (WGAN-GP conf)",
                    "global_batch": world * B, "patch": S, "parallelism": f"dp{world}",
                    "hip_graph": use_graph},
-        "roofline": {"kernel": "conv_cout1_kernel (generator last conv fwd)", "bound": "mfma",
-                     "achieved": round(achieved, 3), "peak": F32_PEAK_TFLOPS, "unit": "TFLOP/s",
-                     "frac": round(achieved / F32_PEAK_TFLOPS, 4), "traffic": None,
-                     "avg_launch_ms": round(kern_ms, 4), "flops_per_launch": roof_flops},
+        "roofline": {"kernel": roof_desc, "bound": "mfma", "achieved": round(achieved, 3), "peak": peak,
+                     "unit": "TFLOP/s", "frac": round(achieved / peak, 4), "traffic": None,
+                     "avg_launch_ms": round(kern_ms, 4), "flops_per_launch": roof_flops, "launches_timed": len(ev)},
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(S, args.cpu_seconds, g_args)

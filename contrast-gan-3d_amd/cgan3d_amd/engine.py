@@ -105,7 +105,6 @@ class GeneratorPlan:
     def __init__(self, cfg, n: int, dims: Dims, device, P: Dict[str, torch.Tensor], prec: int = L.PREC_F32):
         c0 = cfg.init_channels_out
         self.n, self.dims, self.device = n, tuple(dims), device
-        self.timer = None
         self.packs = ops.PackSet(device)  # packed [tap][cin][cout] weight copies, refreshed per update
         layers: List[_GLayer] = [_GLayer("conv", "model.first", 7, 1, 3, True, 1, c0, dims, dims)]
         d = tuple(dims)
@@ -205,11 +204,7 @@ class GeneratorPlan:
         la = self.last
         ep = ops.epilogue(bias=P["model.last_conv.bias"], act=L.ACT_TANH,
                           minuend=x if opt_hat_out is not None else None, out2=opt_hat_out)
-        if self.timer is not None:  # bench.py: HIP events around this launch, same stream
-            self.timer[0].record()
         ops.conv(self.geo_last_fwd, h, P["model.last_conv.weight"], self.att, ep)
-        if self.timer is not None:
-            self.timer[1].record()
         return self.att
 
     def _eval_scale_shift(self, P, nb, i):
@@ -420,6 +415,21 @@ class StepEngine:
         self.dcrit = torch.empty((b_sub, *dims, 1), device=device)       # dL_G/d opt_hat via the critic
         self.losses = torch.zeros(8, device=device)
         self.loss_ws = torch.empty(ops.loss_ws_floats(), device=device)
+        if self.world > 1:
+            self.broadcast_state()
+
+    def broadcast_state(self, src: int = 0):
+        """Start every rank from rank ``src``'s weights, BatchNorm buffers and Adam moments (what
+        DistributedDataParallel does at construction); the packed weight copies are refreshed."""
+        dist = torch.distributed
+        for ar in (self.g_arena, self.d_arena):
+            for t in (ar.flat, ar.exp_avg, ar.exp_avg_sq):
+                dist.broadcast(t, src, group=self.pg)
+        for k, v in self.gP.items():
+            if k.endswith(("running_mean", "running_var", "num_batches_tracked")):
+                dist.broadcast(v.data, src, group=self.pg)
+        self.G.pack()
+        self.D.pack()
 
     @property
     def opt_hat(self):

@@ -217,6 +217,21 @@ def _launch(name, *args):
     return getattr(L.lib(), name)(*args, L.stream())
 
 
+# bench.py's roofline timer: LAUNCH_HOOK(role, geometry) returns a (start, end) pair of
+# torch.cuda.Event to record around that launch (on the launch stream), or None.
+LAUNCH_HOOK = None
+
+
+def _timed(role, g, name, *args):
+    ev = LAUNCH_HOOK(role, g) if LAUNCH_HOOK is not None else None
+    if ev is None:
+        return _launch(name, *args)
+    ev[0].record()
+    rc = _launch(name, *args)
+    ev[1].record()
+    return rc
+
+
 # --- launches -----------------------------------------------------------------------------------
 def stats_floats(g: ConvGeom) -> int:
     return int(L.load().cgan3d_conv3d_stats_floats(ctypes.byref(g)))
@@ -240,8 +255,8 @@ def conv(g: ConvGeom, x: torch.Tensor, w: torch.Tensor, y: torch.Tensor, ep: Opt
                 _need(getattr(ep, nm), ny, f"conv {nm}")
         if ep.stats is not None:
             _need(ep.stats, stats_floats(g), "conv stats", exact=False)
-    check(_launch("cgan3d_conv3d_fwd", ctypes.byref(g), ptr(x), ptr(w), ptr(y),
-                  ctypes.byref(ep.c()) if ep is not None else None), "conv3d_fwd")
+    check(_timed("conv", g, "cgan3d_conv3d_fwd", ctypes.byref(g), ptr(x), ptr(w), ptr(y),
+                 ctypes.byref(ep.c()) if ep is not None else None), "conv3d_fwd")
 
 
 def wgrad_ws_floats(g: ConvGeom) -> int:
@@ -255,8 +270,8 @@ def wgrad(g: ConvGeom, gathered, aligned, dw, ws, accumulate=False):
     if _w_extent(g) > dw.numel():
         raise ValueError("wgrad: weight strides exceed dw")
     _need(ws, wgrad_ws_floats(g), "wgrad ws", exact=False)
-    check(_launch("cgan3d_conv3d_wgrad", ctypes.byref(g), ptr(gathered), ptr(aligned), ptr(dw), int(accumulate),
-                  ptr(ws)), "conv3d_wgrad")
+    check(_timed("wgrad", g, "cgan3d_conv3d_wgrad", ctypes.byref(g), ptr(gathered), ptr(aligned), ptr(dw),
+                 int(accumulate), ptr(ws)), "conv3d_wgrad")
 
 
 def bn_finalize(stats, nblk, c, gamma, beta, rmean, rvar, nbt, scale_shift, mean_invstd, momentum=0.1, eps=1e-5):

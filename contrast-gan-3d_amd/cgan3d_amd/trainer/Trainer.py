@@ -50,8 +50,10 @@ class Trainer:
                  generator_lr_scheduler_class: Optional[partial] = None,
                  critic_lr_scheduler_class: Optional[partial] = None, hu_loss_weight: float = 1.0,
                  sim_loss_weight: float = 1.0, gan_loss_weight: float = 1.0, gp_weight: float = 10,
-                 checkpoint_every: Optional[int] = 1000, rng: Optional[np.random.Generator] = None):
+                 checkpoint_every: Optional[int] = 1000, rng: Optional[np.random.Generator] = None,
+                 precision: str = "f32"):
         self.rng = rng
+        self.precision = precision  # "f32" (the reference's arithmetic) or "bf16" MFMA convolutions
         self.device = torch.device(device)
         self.debug = debug
         self.train_log_sample_size, self.val_log_sample_size = None, None
@@ -97,7 +99,8 @@ class Trainer:
             self.engine = StepEngine(self.generator, self.critic, self.generator.config, self.critic.config, b_opt,
                                      b_sub, tuple(dims), gp_weight=float(self.gp_w), hu_bounds=(lo, hi),
                                      gan_w=self.gan_loss_w, sim_w=self.sim_loss_w, hu_w=self.hu_loss_w,
-                                     device=self.device, g_optim=self.optimizer_G, d_optim=self.optimizer_D)
+                                     device=self.device, g_optim=self.optimizer_G, d_optim=self.optimizer_D,
+                                     precision=self.precision)
         return self.engine
 
     def _losses(self, keys) -> Dict[str, Tensor]:

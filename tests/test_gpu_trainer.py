@@ -1,0 +1,89 @@
+"""Trainer drop-in (contrast_gan_3D/trainer/Trainer.py:34-363) on the GPU: constructor in the
+positional order train.py:154-176 uses, train_step's log_dict keys and finiteness, validation,
+and a checkpoint round trip that resumes with identical weights, BN buffers and Adam state."""
+from functools import partial
+
+import numpy as np
+import pytest
+import torch
+from torch import nn
+
+pytestmark = pytest.mark.gpu
+
+
+class _Log:
+    def __init__(self):
+        self.losses = []
+
+    def log_loss(self, d, it, mode):
+        self.losses.append((mode, it, {k: float(v) for k, v in d.items()}))
+
+
+class _LoggerInterface:
+    def __init__(self):
+        self.logger = _Log()
+        self.calls = 0
+
+    def __call__(self, *a, **k):
+        self.calls += 1
+
+    def end_hook(self):
+        pass
+
+
+def _trainer(ckpt_dir, precision="f32"):
+    from cgan3d_amd.model.discriminator import PatchGANDiscriminator
+    from cgan3d_amd.model.generator import ResnetGenerator
+    from cgan3d_amd.model.loss import HULoss
+    from cgan3d_amd.trainer.Trainer import Trainer
+    torch.manual_seed(0)
+    return Trainer(
+        3, 1, 2, 1, 1, 1, 1000,
+        partial(ResnetGenerator, 2, 2, 8),
+        partial(PatchGANDiscriminator, channels_in=1, init_channels_out=8, discriminator_depth=3,
+                negative_slope=0.2, norm_layer=nn.Identity),
+        partial(torch.optim.Adam, lr=1e-4, betas=(0.0, 0.9)),
+        partial(torch.optim.Adam, lr=1e-4, betas=(0.0, 0.9)),
+        HULoss(-0.2, 0.6), _LoggerInterface(), torch.device("cuda"),
+        checkpoint_dir=ckpt_dir, checkpoint_every=2, precision=precision)
+
+
+def _patches(rng, b=2, S=32):
+    """[OPT, LOW, HIGH] batches; |OPT| = |LOW| + |HIGH| as in basic_conf.py:74-79."""
+    def one(bb):
+        x = rng.uniform(-1, 1, (bb, 1, S, S, S)).astype(np.float32)
+        seg = (rng.random((bb, 1, S, S, S)) < 0.1)
+        return {"data": torch.from_numpy(x), "seg": torch.from_numpy(seg)}
+    return [one(2 * b), one(b), one(b)]
+
+
+@pytest.mark.parametrize("precision", ["f32", "bf16"])
+def test_trainer_step_validate_checkpoint(tmp_path, precision):
+    rng = np.random.default_rng(0)
+    tr = _trainer(tmp_path, precision)
+    for it in range(2):
+        log = tr.train_step(_patches(rng), it)
+        assert set(log) == {"D", "G", "G-full", "sim", "HU"}
+        assert all(np.isfinite(float(v)) for v in log.values())
+    vals = iter([_patches(rng)[i] for i in range(3)] * 2)
+    loaders = {st: vals for st in (0, -1, 1)}
+    v = tr.validate(loaders, 2)
+    assert set(v) == {"D", "G", "sim"} and all(np.isfinite(float(x)) for x in v.values())
+    tr.save_checkpoint(2)
+    sd_g = {k: t.detach().cpu().clone() for k, t in tr.generator.state_dict().items()}
+    sd_d = {k: t.detach().cpu().clone() for k, t in tr.critic.state_dict().items()}
+    opt_g = tr.optimizer_G.state_dict()
+    ck = torch.load(tmp_path / "2.pt", map_location="cpu", weights_only=True)
+    assert {"generator", "critic", "optimizer_G", "optimizer_D", "iteration"} <= set(ck)
+    tr2 = _trainer(tmp_path, precision)  # resumes from the latest checkpoint in the directory
+    for k, t in tr2.generator.state_dict().items():
+        assert torch.equal(t.cpu(), sd_g[k]), k
+    for k, t in tr2.critic.state_dict().items():
+        assert torch.equal(t.cpu(), sd_d[k]), k
+    o2 = tr2.optimizer_G.state_dict()
+    for pid, st in opt_g["state"].items():
+        assert torch.equal(o2["state"][pid]["exp_avg"].cpu(), st["exp_avg"].cpu())
+        assert float(o2["state"][pid]["step"]) == float(st["step"])
+    # and keeps training from there
+    log = tr2.train_step(_patches(rng), 2)
+    assert all(np.isfinite(float(x)) for x in log.values())
