@@ -45,13 +45,23 @@ def conv_flops(n, dout, cin, cout, k):
     return 2.0 * n * cout * dout[0] * dout[1] * dout[2] * cin * k**3
 
 
-# roofline candidates: kernel description, launch role, geometry predicate, bound, precision of the MFMA
+# roofline candidates: kernel description, launch role, geometry predicate, committed PMC summary
+# (HBM bytes per launch from rocprofv3 FETCH_SIZE / WRITE_SIZE passes, profiles/)
 ROOFLINES = {
     "halo_res": ("conv_halo_kernel<64,4>: ResNet-block Conv3d 64->64 k3 s1 at (S/4)^3, forward + input-grad",
-                 "conv", lambda g: g.w_packed == 2 and g.cin == 64 and g.cout == 64 and g.k == 3 and g.stride == 1),
+                 "conv", lambda g: g.w_packed == 2 and g.cin == 64 and g.cout == 64 and g.k == 3 and g.stride == 1,
+                 "profiles/r01_pmc_conv_halo_64_4.json"),
     "k7_w2n": ("k7m_w2n_kernel: generator last Conv3d 16->1 k7 (+bias, tanh, opt_hat) forward",
-               "conv", lambda g: g.k == 7 and g.cin == 16 and g.cout == 1),
+               "conv", lambda g: g.k == 7 and g.cin == 16 and g.cout == 1, None),
 }
+
+
+def pmc_traffic(path, size, batch):
+    """HBM bytes per launch from a committed PMC summary measured on this workload (else None)."""
+    f = REPO / path if path else None
+    if f is None or not f.is_file() or (size, batch) != (64, 4):
+        return None
+    return json.loads(f.read_text()).get("hbm_bytes_per_launch")
 
 
 def cpu_baseline(size, seconds, g_args):
@@ -137,15 +147,17 @@ def main():
                         torch.from_numpy(seg).to(dev), torch.rand(B, device=dev)))
 
     from cgan3d_amd import ops
-    roof_desc, roof_role, roof_match = ROOFLINES[args.roofline]
+    roof_desc, roof_role, roof_match, roof_pmc = ROOFLINES[args.roofline]
     ev = []  # (start, end, algorithmic flops) per timed launch
+
+    reps = 8
 
     def hook(role, geo):
         if role != roof_role or not roof_match(geo):
             return None
         e = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
         ev.append((*e, conv_flops(geo.n, (geo.do_, geo.ho, geo.wo), geo.cin, geo.cout, geo.k)))
-        return e
+        return (*e, reps)
 
     def one_step(i, timed):
         eng.load_inputs(*batches[i % len(batches)])
@@ -177,18 +189,21 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
-    # the roofline kernel's launch times: HIP events around each launch over eager steps
+    # the roofline kernel's launch time: after the timed region, eager steps in which each of its
+    # launches is followed by `reps` back-to-back repeats between two HIP events on its stream
+    # (repeats keep the queue full, so host launch gaps stay out of the measurement)
     for i in range(min(args.steps, 10)):
         one_step(i, True)
     torch.cuda.synchronize()
+    kern = [(a.elapsed_time(b) / reps, f) for a, b, f in ev]
     if dist:
         t = torch.tensor([el], device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
     losses = eng.losses.cpu().numpy()
     assert np.isfinite(losses).all(), f"non-finite losses {losses}"
-    kern_ms = float(np.mean([a.elapsed_time(b) for a, b, _ in ev]))
-    roof_flops = float(np.mean([f for _, _, f in ev]))
+    kern_ms = float(np.mean([t for t, _ in kern]))
+    roof_flops = float(np.mean([f for _, f in kern]))
     achieved = roof_flops / (kern_ms * 1e-3) / 1e12
     peak = BF16_PEAK_TFLOPS if args.precision == "bf16" else F32_PEAK_TFLOPS
     ms = el / args.steps * 1e3
@@ -204,8 +219,10 @@ def main():
                    "global_batch": world * B, "patch": S, "parallelism": f"dp{world}",
                    "hip_graph": use_graph},
         "roofline": {"kernel": roof_desc, "bound": "mfma", "achieved": round(achieved, 3), "peak": peak,
-                     "unit": "TFLOP/s", "frac": round(achieved / peak, 4), "traffic": None,
-                     "avg_launch_ms": round(kern_ms, 4), "flops_per_launch": roof_flops, "launches_timed": len(ev)},
+                     "unit": "TFLOP/s", "frac": round(achieved / peak, 4),
+                     "traffic": pmc_traffic(roof_pmc, S, B), "traffic_source": roof_pmc,
+                     "avg_launch_ms": round(kern_ms, 4), "flops_per_launch": roof_flops, "launches_timed": len(kern),
+                     "timing": f"HIP events around {reps} back-to-back repeats of each launch, eager steps"},
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(S, args.cpu_seconds, g_args)

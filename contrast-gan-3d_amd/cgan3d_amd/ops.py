@@ -217,8 +217,9 @@ def _launch(name, *args):
     return getattr(L.lib(), name)(*args, L.stream())
 
 
-# bench.py's roofline timer: LAUNCH_HOOK(role, geometry) returns a (start, end) pair of
-# torch.cuda.Event to record around that launch (on the launch stream), or None.
+# bench.py's roofline timer: LAUNCH_HOOK(role, geometry) returns (start, end, reps) — two
+# torch.cuda.Event recorded on the launch stream around ``reps`` back-to-back repeats of that
+# launch (idempotent: same operands, same outputs) — or None.
 LAUNCH_HOOK = None
 
 
@@ -226,8 +227,10 @@ def _timed(role, g, name, *args):
     ev = LAUNCH_HOOK(role, g) if LAUNCH_HOOK is not None else None
     if ev is None:
         return _launch(name, *args)
+    rc = _launch(name, *args)  # the step's own launch; then the timed repeats
     ev[0].record()
-    rc = _launch(name, *args)
+    for _ in range(ev[2]):
+        rc = rc or _launch(name, *args)
     ev[1].record()
     return rc
 
