@@ -72,3 +72,31 @@ def test_conv_wrapper_rejects_mismatched_operand():
             ops.conv(g, x, w, torch.empty(1, 4, 4, 4, 16))
     finally:
         ops.DRY_RUN = False
+
+
+def test_conf_overwrites_module_builds_trainer_like_train_py(tmp_path):
+    """integration/cgan3d_gp_overrides.py replaces train.py's globals (train.py:106-107); the
+    Trainer it exports accepts train.py's positional call (train.py:154-176) and builds the
+    reference-shaped models and Adam optimisers (on the CPU here: no kernel runs until a step)."""
+    import importlib.util
+    from functools import partial
+    from pathlib import Path
+    spec = importlib.util.spec_from_file_location(
+        "cgan3d_gp_overrides", Path(__file__).resolve().parents[1] / "integration" / "cgan3d_gp_overrides.py")
+    m = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(m)
+
+    class _LI:
+        logger = None
+
+        def end_hook(self):
+            pass
+
+    opt = partial(torch.optim.Adam, lr=1e-4, betas=(0.0, 0.9))
+    tr = m.Trainer(10, 2, 400, 5, 1, 100, 500, m.generator_class, m.critic_class, opt, opt,
+                   m.HULoss(0.18667, 0.35333, (6, 1, 128, 128, 128)), _LI(), torch.device("cpu"), False,
+                   checkpoint_dir=tmp_path, weight_clip=m.weight_clip, generator_lr_scheduler_class=None,
+                   critic_lr_scheduler_class=None, checkpoint_every=1000, rng=None)
+    from cgan3d_amd.model.utils import count_parameters
+    assert count_parameters(tr.generator) == 1035297 and count_parameters(tr.critic) == 176761
+    assert set(tr.optimizer_G.state_dict()["param_groups"][0]) >= {"lr", "betas", "eps"}
