@@ -354,7 +354,7 @@ class CriticPlan:
         """dW_l = wgrad(a_{l-1}, dz_l) over n_all samples; db_l = sum dz_l over the first n_bias."""
         prev = x_all
         for i, ly in enumerate(self.layers):
-            g = ops.conv_wgrad_geom(n_all, ly.din, ly.dout, ly.cin, ly.cout, ly.k, ly.s, ly.p)
+            g = ops.with_prec(ops.conv_wgrad_geom(n_all, ly.din, ly.dout, ly.cin, ly.cout, ly.k, ly.s, ly.p), self.prec)
             ops.wgrad(g, prev, self.dz[i][:n_all], G[f"{ly.name}.weight"], self.ws)
             nv = n_bias * ly.dout[0] * ly.dout[1] * ly.dout[2]
             ops.channel_sum(self.dz[i][:n_bias], nv, ly.cout, G[f"{ly.name}.bias"], self.ws)

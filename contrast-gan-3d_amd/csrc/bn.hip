@@ -74,45 +74,64 @@ __device__ __forceinline__ float act_grad(float pre, int act, float slope) {
   return 1.f;
 }
 
-// y = act(z*scale + shift) (+ residual); C % 4 == 0, float4 vectorised grid-stride
+// y = act(z*scale + shift) (+ residual); C % 4 == 0, float4 vectorised grid-stride.  With
+// 256 % (C/4) == 0 the grid stride is a multiple of C/4, so a thread keeps its 4 channels (and
+// their scale/shift in registers) for the whole loop.
 __global__ __launch_bounds__(256) void bn_apply_kernel(const float* __restrict__ z, long long n4, int C,
                                                        const float* __restrict__ ss, int act, float slope,
                                                        const float* __restrict__ res, float* __restrict__ y) {
   const int C4 = C >> 2;
-  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (long long)gridDim.x * blockDim.x) {
-    const int c = (int)(i % C4) * 4;
-    f32x4 v = reinterpret_cast<const f32x4*>(z)[i];
+  const int c = (threadIdx.x % C4) * 4;
+  f32x4 sc, sf;
 #pragma unroll
-    for (int e = 0; e < 4; ++e) v[e] = act_f(v[e] * ss[c + e] + ss[C + c + e], act, slope);
-    if (res) v += reinterpret_cast<const f32x4*>(res)[i];
-    reinterpret_cast<f32x4*>(y)[i] = v;
+  for (int e = 0; e < 4; ++e) { sc[e] = ss[c + e]; sf[e] = ss[C + c + e]; }
+  const f32x4* z4 = reinterpret_cast<const f32x4*>(z);
+  const f32x4* r4 = reinterpret_cast<const f32x4*>(res);
+  f32x4* y4 = reinterpret_cast<f32x4*>(y);
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (long long)gridDim.x * blockDim.x) {
+    f32x4 v = z4[i];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[e] = act_f(v[e] * sc[e] + sf[e], act, slope);
+    if (res) v += r4[i];
+    y4[i] = v;
   }
 }
 
-// per-block partials of sum(dyh) and sum(dyh * xhat); 256 % C == 0 so each thread keeps one channel
+// per-block partials of sum(dyh) and sum(dyh * xhat), float4 per thread (4 channels fixed per
+// thread: 256 % (C/4) == 0)
 __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const float* __restrict__ dy, const float* __restrict__ z,
-                                                            long long total, int C, const float* __restrict__ ss,
+                                                            long long n4, int C, const float* __restrict__ ss,
                                                             const float* __restrict__ mi, int act, float slope,
                                                             float* part) {
-  __shared__ float r0[256], r1[256];
-  const int tid = threadIdx.x;
-  const int c = tid % C;
-  const float sc = ss[c], sf = ss[C + c], mean = mi[c], inv = mi[C + c];
-  float a0 = 0.f, a1 = 0.f;
-  for (long long i = (long long)blockIdx.x * blockDim.x + tid; i < total; i += (long long)gridDim.x * blockDim.x) {
-    const float zz = z[i];
-    const float g = dy[i] * act_grad(zz * sc + sf, act, slope);
-    a0 += g;
-    a1 += g * (zz - mean) * inv;
+  __shared__ f32x4 r0[256], r1[256];
+  const int tid = threadIdx.x, C4 = C >> 2;
+  const int c = (tid % C4) * 4;
+  f32x4 sc, sf, mean, inv;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) { sc[e] = ss[c + e]; sf[e] = ss[C + c + e]; mean[e] = mi[c + e]; inv[e] = mi[C + c + e]; }
+  f32x4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = {0.f, 0.f, 0.f, 0.f};
+  const f32x4* z4 = reinterpret_cast<const f32x4*>(z);
+  const f32x4* d4 = reinterpret_cast<const f32x4*>(dy);
+  for (long long i = (long long)blockIdx.x * blockDim.x + tid; i < n4; i += (long long)gridDim.x * blockDim.x) {
+    const f32x4 zz = z4[i], dd = d4[i];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float g = dd[e] * act_grad(zz[e] * sc[e] + sf[e], act, slope);
+      a0[e] += g;
+      a1[e] += g * (zz[e] - mean[e]) * inv[e];
+    }
   }
   r0[tid] = a0;
   r1[tid] = a1;
   __syncthreads();
-  if (tid < C) {
-    float s0 = 0.f, s1 = 0.f;
-    for (int k = tid; k < 256; k += C) { s0 += r0[k]; s1 += r1[k]; }
-    part[(long long)blockIdx.x * 2 * C + tid] = s0;
-    part[(long long)blockIdx.x * 2 * C + C + tid] = s1;
+  if (tid < C4) {
+    f32x4 s0 = {0.f, 0.f, 0.f, 0.f}, s1 = {0.f, 0.f, 0.f, 0.f};
+    for (int k = tid; k < 256; k += C4) { s0 += r0[k]; s1 += r1[k]; }
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      part[(long long)blockIdx.x * 2 * C + 4 * tid + e] = s0[e];
+      part[(long long)blockIdx.x * 2 * C + C + 4 * tid + e] = s1[e];
+    }
   }
 }
 
@@ -143,17 +162,32 @@ __global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(const float* __res
   }
 }
 
-// dz = gamma*invstd*(dyh - mean(dyh) - xhat*mean(dyh*xhat))
+// dz = gamma*invstd*(dyh - mean(dyh) - xhat*mean(dyh*xhat)), float4, channels fixed per thread
 __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const float* __restrict__ dy, const float* __restrict__ z,
-                                                           long long total, int C, const float* __restrict__ ss,
+                                                           long long n4, int C, const float* __restrict__ ss,
                                                            const float* __restrict__ mi, int act, float slope,
                                                            const float* __restrict__ coef, float* dz) {
-  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long long)gridDim.x * blockDim.x) {
-    const int c = (int)(i % C);
-    const float zz = z[i];
-    const float g = dy[i] * act_grad(zz * ss[c] + ss[C + c], act, slope);
-    const float xh = (zz - mi[c]) * mi[C + c];
-    dz[i] = coef[c] * (g - coef[C + c] - xh * coef[2 * C + c]);
+  const int C4 = C >> 2;
+  const int c = (threadIdx.x % C4) * 4;
+  f32x4 sc, sf, mean, inv, k0, k1, k2;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    sc[e] = ss[c + e]; sf[e] = ss[C + c + e]; mean[e] = mi[c + e]; inv[e] = mi[C + c + e];
+    k0[e] = coef[c + e]; k1[e] = coef[C + c + e]; k2[e] = coef[2 * C + c + e];
+  }
+  const f32x4* z4 = reinterpret_cast<const f32x4*>(z);
+  const f32x4* d4 = reinterpret_cast<const f32x4*>(dy);
+  f32x4* o4 = reinterpret_cast<f32x4*>(dz);
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (long long)gridDim.x * blockDim.x) {
+    const f32x4 zz = z4[i], dd = d4[i];
+    f32x4 o;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float g = dd[e] * act_grad(zz[e] * sc[e] + sf[e], act, slope);
+      const float xh = (zz[e] - mean[e]) * inv[e];
+      o[e] = k0[e] * (g - k1[e] - xh * k2[e]);
+    }
+    o4[i] = o;
   }
 }
 
@@ -211,7 +245,8 @@ extern "C" int cgan3d_bn_finalize(const float* stats, int64_t nblk, int32_t c, c
 extern "C" int cgan3d_bn_apply(const float* z, int64_t nvox, int32_t c, const float* scale_shift, int32_t act,
                                float slope, const float* residual, float* y, void* stream) {
   CG_CHECK_ARG(z && scale_shift && y, "cgan3d_bn_apply: null pointer");
-  CG_CHECK_ARG(nvox > 0 && c > 0 && c % 4 == 0, "cgan3d_bn_apply: channels must be a multiple of 4");
+  CG_CHECK_ARG(nvox > 0 && c > 0 && c % 4 == 0 && 256 % (c / 4) == 0,
+               "cgan3d_bn_apply: channels must be a multiple of 4 dividing 1024");
   const long long n4 = (long long)nvox * c / 4;
   int blocks = (int)std::min<long long>((n4 + 255) / 256, 4096);
   hipLaunchKernelGGL(bn_apply_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, z, n4, c, scale_shift, act,
@@ -228,20 +263,21 @@ extern "C" int cgan3d_bn_backward(const float* dy, const float* z, int64_t nvox,
                                   const float* mean_invstd, const float* gamma, int32_t act, float slope, float* dgamma,
                                   float* dbeta, float* dz, float* ws, void* stream) {
   CG_CHECK_ARG(dy && z && scale_shift && mean_invstd && gamma && dz && ws, "cgan3d_bn_backward: null pointer");
-  CG_CHECK_ARG(nvox > 1 && c > 0 && c <= 256 && 256 % c == 0, "cgan3d_bn_backward: channels must divide 256");
+  CG_CHECK_ARG(nvox > 1 && c >= 4 && c <= 256 && 256 % c == 0,
+               "cgan3d_bn_backward: channels must divide 256 and be >= 4");
   hipStream_t s = (hipStream_t)stream;
-  const long long total = (long long)nvox * c;
+  const long long total = (long long)nvox * c, n4 = total / 4;
   const int nblk = reduce_blocks(total);
   float* part = ws;
   float* coef = ws + (long long)nblk * 2 * c;
-  hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(nblk), dim3(256), 0, s, dy, z, total, c, scale_shift, mean_invstd,
+  hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(nblk), dim3(256), 0, s, dy, z, n4, c, scale_shift, mean_invstd,
                      act, slope, part);
   CG_LAUNCH_CHECK("bn_bwd_reduce_kernel");
   hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(c), dim3(256), 0, s, part, nblk, c, (long long)nvox, gamma,
                      mean_invstd, dgamma, dbeta, coef);
   CG_LAUNCH_CHECK("bn_bwd_finalize_kernel");
-  int blocks = (int)std::min<long long>((total + 255) / 256, 4096);
-  hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(blocks), dim3(256), 0, s, dy, z, total, c, scale_shift, mean_invstd,
+  int blocks = (int)std::min<long long>((n4 + 255) / 256, 4096);
+  hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(blocks), dim3(256), 0, s, dy, z, n4, c, scale_shift, mean_invstd,
                      act, slope, coef, dz);
   CG_LAUNCH_CHECK("bn_bwd_apply_kernel");
   return CGAN3D_OK;

@@ -212,7 +212,7 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(ConvArgs a, const float
   __shared__ int rtab[4][64];                                  // td, th, tw, a   (td = -1: pad row)
   __shared__ int vtab[5][KV];                                  // n*di, bd, bh, bw, aligned voxel
 
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int R = a.k * a.k * a.k * a.cin;
   const int r0 = blockIdx.x * 64;
   if (tid < 64) {
@@ -513,6 +513,10 @@ extern "C" int cgan3d_conv3d_wgrad(const cgan3d_conv_geom* g, const float* gathe
     dim3 grid(cg::ceil_div(V, vpb), gy);
     hipLaunchKernelGGL((conv_wgrad_cout1_kernel<1>), grid, dim3(256), 0, s, a, gathered, aligned, ws, vpb);
     CG_LAUNCH_CHECK("conv_wgrad_cout1_kernel");
+  } else if (wgrad_bf16_ok(g)) {
+    int rc = wgrad_bf16_launch(g, gathered, aligned, ws, s);
+    if (rc) return rc;
+    CG_LAUNCH_CHECK("conv_wgrad_bf16_kernel");
   } else {
     const int gxb = cg::ceil_div(R, 64);
     long long vpb = wgrad_vpb(V, gxb);

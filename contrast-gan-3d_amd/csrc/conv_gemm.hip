@@ -109,7 +109,7 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(GemmArgs a, const float*
   __shared__ int row_n[BM], row_b[3][BM], row_out[BM];
   __shared__ int tap_off[3][352], tap_lin[352];
 
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave % WM, wn = wave / WM;
   const int cls = blockIdx.x / a.tiles_per_class;
   const int tile = blockIdx.x - cls * a.tiles_per_class;
@@ -477,6 +477,7 @@ extern "C" int32_t cgan3d_halo_eligible(const cgan3d_conv_geom* g) { return g &&
 
 extern "C" int cgan3d_set_tuning(int32_t key, int32_t value) {
   if (key == 0) { g_small_tile_below = value; return CGAN3D_OK; }
+  if (key == 1) { wgrad_bf16_set_blocks(value); return CGAN3D_OK; }
   set_error("cgan3d_set_tuning: unknown key %d", key);
   return CGAN3D_EINVAL;
 }

@@ -74,7 +74,7 @@ __global__ __launch_bounds__(256) void conv_halo_kernel(HaloArgs a, const float*
   __shared__ int tlin[64];
   __shared__ int row_out[64];
 
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int tiles = a.td * a.th * a.tw;
   int bid = blockIdx.x;
   const int cls = bid / (a.n * tiles);

@@ -54,7 +54,7 @@ __global__ __launch_bounds__(256) void k7m_n2w_kernel(K7Args a, const float* __r
   __shared__ __attribute__((aligned(16))) float xs[N_ROWS * N_HW];
   __shared__ __attribute__((aligned(16))) __bf16 us[N_ROWS * N_TW * 8];  // [row][ow][8 taps]
   __shared__ __attribute__((aligned(16))) __bf16 wt[N_PAIRS * C * 8];    // [pair][c][tw8]
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   int n, d0, h0, w0;
   {
     int bid = blockIdx.x;
@@ -181,9 +181,11 @@ __global__ __launch_bounds__(256) void k7m_w2n_kernel(K7Args a, const float* __r
                                                       const float* __restrict__ minuend, float* __restrict__ out2) {
   constexpr int C = 16;
   __shared__ __attribute__((aligned(16))) __bf16 hs[W_ROWS * W_HW * 8];  // [row][iw][8 channels]
-  __shared__ __attribute__((aligned(16))) __bf16 wt[49 * 8 * C];        // [td*7+th][tw8][c]
+  constexpr int WP = 8 * C + 8;  // (td, th) block of the weight table, padded: lanes of one B read
+                                 // hit 16 different blocks, 4 banks apart instead of 64
+  __shared__ __attribute__((aligned(16))) __bf16 wt[49 * WP];           // [td*7+th][tw8][c]
   __shared__ float red[4][256];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   int n, d0, h0, w0;
   {
     int bid = blockIdx.x;
@@ -198,7 +200,7 @@ __global__ __launch_bounds__(256) void k7m_w2n_kernel(K7Args a, const float* __r
         const int c = i & 15, tw = (i >> 4) & 7, p = i >> 7;
         return tw < K7 ? (long long)c * a.wc + p * K7 + tw : -1;
       },
-      [&](int i, float v) { wt[i] = (__bf16)v; });
+      [&](int i, float v) { wt[(i >> 7) * WP + (i & 127)] = (__bf16)v; });
   const int g = lane >> 4, r16 = lane & 15;
   const int odl = r16 >> 2, ohl = r16 & 3;  // this lane's B column: output row (od, oh)
   f32x4 acc = {0.f, 0.f, 0.f, 0.f};
@@ -225,7 +227,7 @@ __global__ __launch_bounds__(256) void k7m_w2n_kernel(K7Args a, const float* __r
       const int id = pr / W_HH, ih = pr - id * W_HH;
       const int td = id - odl, th = ih - ohl;
       const bool band = td >= 0 && td < K7 && th >= 0 && th < K7;
-      const __bf16* wrow = wt + ((band ? td * K7 + th : 0) * 8) * C + half * 8;
+      const __bf16* wrow = wt + (band ? td * K7 + th : 0) * WP + half * 8;
       const __bf16* hrow = hs + (pr * W_HW + r16) * 8;
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
@@ -271,20 +273,29 @@ __device__ __forceinline__ void k7m_tile(const K7Args& a, int tile, int* n, int*
   *d0 = td_ * G_TD; *h0 = th_ * G_TH; *w0 = tw_ * G_TW;
 }
 
-// combine the 4 waves' accumulators and write this block's partial [c][t]
-__device__ __forceinline__ void k7m_wg_store(f32x4 (&acc)[G_NT], float* red, float* part) {
+// combine the 4 waves' accumulators and write this block's partial [c][t].  Column n of N-tile
+// j holds tap (pair, tw) = (2j + (n >> 3), n & 7) when TD_TILES is false (25 tiles), and
+// (td, th, tw) = (j >> 2, 2 (j & 3) + (n >> 3), n & 7) when it is true (28 tiles).
+template <int NT, bool TD_TILES>
+__device__ __forceinline__ void k7m_wg_store(f32x4 (&acc)[NT], float* red, float* part) {
   const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, r16 = lane & 15;
-  for (int i = tid; i < G_NT * 256; i += 256) red[i] = 0.f;
+  for (int i = tid; i < NT * 256; i += 256) red[i] = 0.f;
   __syncthreads();
 #pragma unroll
-  for (int j = 0; j < G_NT; ++j)
+  for (int j = 0; j < NT; ++j)
 #pragma unroll
     for (int jj = 0; jj < 4; ++jj) atomicAdd(&red[j * 256 + (4 * g + jj) * 16 + r16], acc[j][jj]);
   __syncthreads();
   float* pb = part + (long long)blockIdx.x * G_COLS;
-  for (int i = tid; i < G_NT * 256; i += 256) {
-    const int j = i >> 8, c = (i >> 4) & 15, col = i & 15;
-    const int pair = 2 * j + (col >> 3), tw = col & 7;
+  for (int i = tid; i < NT * 256; i += 256) {
+    const int j = i >> 8, c = (i >> 4) & 15, col = i & 15, tw = col & 7;
+    int pair;
+    if (TD_TILES) {
+      const int th = 2 * (j & 3) + (col >> 3);
+      pair = th < K7 ? (j >> 2) * K7 + th : 99;
+    } else {
+      pair = 2 * j + (col >> 3);
+    }
     if (pair < 49 && tw < K7) pb[c * KT7 + pair * K7 + tw] = red[i];
   }
 }
@@ -294,10 +305,13 @@ __global__ __launch_bounds__(256) void k7m_wg_n2w_kernel(K7Args a, const float* 
                                                          const float* __restrict__ go, float* __restrict__ part,
                                                          int ntiles) {
   constexpr int HW = G_TW + 8;  // x halo row: ow 0..15 + tw 0..7
-  __shared__ __attribute__((aligned(16))) unsigned char lds[8 * G_ROWS_IN * G_TW * 2 + G_ROWS_IN * HW * 4];
-  __bf16* sx = reinterpret_cast<__bf16*>(lds);                          // [tw][row][16]
-  float* xs = reinterpret_cast<float*>(lds + 8 * G_ROWS_IN * G_TW * 2);  // [row][24]
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4, r16 = lane & 15;
+  constexpr int SXW = G_TW + 8;  // shifted-copy row (bf16), padded: the 8 tw copies of a row fall
+                                 // on distinct banks
+  __shared__ __attribute__((aligned(16))) unsigned char lds[8 * G_ROWS_IN * SXW * 2 + G_ROWS_IN * HW * 4];
+  __bf16* sx = reinterpret_cast<__bf16*>(lds);                           // [row][tw][SXW]
+  float* xs = reinterpret_cast<float*>(lds + 8 * G_ROWS_IN * SXW * 2);  // [row][24]
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6), g = lane >> 4,
+            r16 = lane & 15;
   f32x4 acc[G_NT];
 #pragma unroll
   for (int j = 0; j < G_NT; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -323,7 +337,7 @@ __global__ __launch_bounds__(256) void k7m_wg_n2w_kernel(K7Args a, const float* 
       bf16x8_k u;
 #pragma unroll
       for (int e = 0; e < 8; ++e) u[e] = (__bf16)src[e];
-      *reinterpret_cast<bf16x8_k*>(sx + ((tw * G_ROWS_IN + r) * G_TW + 8 * hf)) = u;
+      *reinterpret_cast<bf16x8_k*>(sx + ((r * 8 + tw) * SXW + 8 * hf)) = u;
     }
     __syncthreads();
     // K-steps of 32 outputs = 2 output rows x 16; wave takes K-steps wave, wave+4, ...
@@ -355,13 +369,13 @@ __global__ __launch_bounds__(256) void k7m_wg_n2w_kernel(K7Args a, const float* 
         const int pa = pair < 49 ? pair : 48;
         const int td = pa / K7, th = pa - td * K7;
         const bf16x8_k bv = *reinterpret_cast<const bf16x8_k*>(
-            sx + ((tw * G_ROWS_IN + (odl + td) * (G_TH + 6) + ohl + th) * G_TW + owl));
+            sx + ((((odl + td) * (G_TH + 6) + ohl + th) * 8 + tw) * SXW + owl));
         acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, bv, acc[j], 0, 0, 0);
       }
     }
   }
   __syncthreads();
-  k7m_wg_store(acc, reinterpret_cast<float*>(lds), part);
+  k7m_wg_store<G_NT, false>(acc, reinterpret_cast<float*>(lds), part);
 }
 
 // dW[c, t] = sum_i x[src(i), c] * g[i - t]   (last conv; x 16 channels on the input halo, g single-
@@ -370,13 +384,16 @@ __global__ __launch_bounds__(256) void k7m_wg_w2n_kernel(K7Args a, const float* 
                                                          const float* __restrict__ go, float* __restrict__ part,
                                                          int ntiles) {
   constexpr int Q = 32;  // halo columns per input row (22 used)
-  __shared__ __attribute__((aligned(16))) unsigned char lds[G_NT * 256 * 4];
-  __bf16* sd = reinterpret_cast<__bf16*>(lds);                  // [tw][orow][Q]: g[orow][q - tw]
-  float* gs = reinterpret_cast<float*>(lds + 8 * G_OROWS * Q * 2);  // [orow][16]
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4, r16 = lane & 15;
-  f32x4 acc[G_NT];
+  __shared__ __attribute__((aligned(16))) unsigned char lds[28 * 256 * 4];
+  constexpr int QP = Q + 8;  // padded row: a B read's 8 tw copies fall on distinct banks
+  __bf16* sd = reinterpret_cast<__bf16*>(lds);                   // [orow][tw][QP]: g[orow][q - tw]
+  float* gs = reinterpret_cast<float*>(lds + 8 * G_OROWS * QP * 2);  // [orow][16]
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6), g = lane >> 4,
+            r16 = lane & 15;
+  constexpr int NT = 28;  // N tiles (td, th pair (0,1) (2,3) (4,5) (6,-)) x tw 0..7
+  f32x4 acc[NT];
 #pragma unroll
-  for (int j = 0; j < G_NT; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int j = 0; j < NT; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
   for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
     int n, d0, h0, w0;
     k7m_tile(a, tile, &n, &d0, &h0, &w0);
@@ -394,7 +411,7 @@ __global__ __launch_bounds__(256) void k7m_wg_w2n_kernel(K7Args a, const float* 
         const int ow = 8 * q8 + e - tw;
         u[e] = (__bf16)((ow >= 0 && ow < G_TW) ? gs[r * G_TW + ow] : 0.f);
       }
-      *reinterpret_cast<bf16x8_k*>(sd + ((tw * G_OROWS + r) * Q + 8 * q8)) = u;
+      *reinterpret_cast<bf16x8_k*>(sd + ((r * 8 + tw) * QP + 8 * q8)) = u;
     }
     __syncthreads();
     // this lane's 8 halo columns (fixed over the rows)
@@ -427,27 +444,31 @@ __global__ __launch_bounds__(256) void k7m_wg_w2n_kernel(K7Args a, const float* 
         bf16x8_k av;
 #pragma unroll
         for (int e = 0; e < 8; ++e) av[e] = (__bf16)xv[b][e];
+        // taps reaching an output row of this tile from input row (id, ih): td in [id-3, id],
+        // th in [ih-7, ih] (intersected with 0..6); branch per td (scalar), 4 th-pair tiles each
+        const int thl = ih - (G_TH - 1) > 0 ? ih - (G_TH - 1) : 0, thh = ih < K7 - 1 ? ih : K7 - 1;
+        const int th0 = r16 >> 3, tw = r16 & 7;  // this lane's column: th = 2q + th0, tw
 #pragma unroll
-        for (int j = 0; j < G_NT; ++j) {
-          // the tile's pairs (2j, 2j+1) reach an output row of this tile from input row (id, ih)?
-          const int p0 = 2 * j, p1 = 2 * j + 1;
-          const int a0 = id - p0 / K7, b0 = ih - p0 % K7, a1 = id - p1 / K7, b1 = ih - p1 % K7;
-          const bool v0 = a0 >= 0 && a0 < G_TD && b0 >= 0 && b0 < G_TH;
-          const bool v1 = p1 < 49 && a1 >= 0 && a1 < G_TD && b1 >= 0 && b1 < G_TH;
-          if (v0 || v1) {
-            const bool mine = (r16 >> 3) ? v1 : v0;
-            const int odl = (r16 >> 3) ? a1 : a0, ohl = (r16 >> 3) ? b1 : b0, tw = r16 & 7;
-            bf16x8_k bv = *reinterpret_cast<const bf16x8_k*>(
-                sd + ((tw * G_OROWS + (mine ? odl * G_TH + ohl : 0)) * Q + 8 * g));
-            if (!mine) bv = bf16x8_k{};
-            acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, bv, acc[j], 0, 0, 0);
+        for (int td = 0; td < K7; ++td) {
+          const int odl = id - td;
+          if (odl < 0 || odl >= G_TD) continue;
+          bf16x8_k bv[4];
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {  // all four B reads before the MFMAs
+            const int thq = 2 * q + th0, ohl = ih - thq;
+            const bool mine = thq >= thl && thq <= thh;
+            bv[q] = *reinterpret_cast<const bf16x8_k*>(sd + (((mine ? odl * G_TH + ohl : 0) * 8 + tw) * QP + 8 * g));
+            if (!mine) bv[q] = bf16x8_k{};
           }
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+            acc[td * 4 + q] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, bv[q], acc[td * 4 + q], 0, 0, 0);
         }
       }
     }
   }
   __syncthreads();
-  k7m_wg_store(acc, reinterpret_cast<float*>(lds), part);
+  k7m_wg_store<NT, true>(acc, reinterpret_cast<float*>(lds), part);
 }
 
 // dW[c * wc + t] += sum_b part[b][c * 343 + t]; grid (cols / 256, row splits)

@@ -351,3 +351,49 @@ def test_k7_bf16_mfma(sp):
     dxo = torch.empty(n, *dims, 16, device="cuda")
     ops.reflect_fold(dpad, dxo, n, dims, 16, p)
     assert_close(_ncdhw(dxo).numpy(), dx16.numpy(), 2e-2, "k7 n2w dgrad")
+
+
+WGRAD_BF16_CASES = [
+    # cin, cout, k, s, p, reflect, spatial (module input)
+    (64, 64, 3, 1, 1, False, (8, 10, 12)),   # ResNet block
+    (16, 32, 3, 2, 1, False, (12, 16, 20)),  # downsampling
+    (8, 16, 4, 2, 1, False, (16, 16, 16)),   # critic middle
+    (32, 64, 4, 2, 1, False, (8, 8, 8)),
+    (12, 20, 3, 1, 1, True, (5, 6, 7)),      # odd channel counts, reflect
+    (1, 8, 4, 2, 1, False, (16, 16, 16)),    # critic first layer (single-channel input)
+]
+
+
+@pytest.mark.parametrize("cin,cout,k,s,p,reflect,sp", WGRAD_BF16_CASES)
+def test_wgrad_bf16(cin, cout, k, s, p, reflect, sp):
+    """bf16-MFMA weight gradient (conv_wgrad.hip) against torch float64 within 2e-2, plus the
+    ConvTranspose3d role (operands swapped) at the generator's upsampling shape."""
+    from cgan3d_amd import ops, _lib as L
+    g = torch.Generator().manual_seed(5 + cin + cout)
+    n = 2
+    x = torch.randn(n, cin, *sp, generator=g, dtype=torch.float64)
+    w = (torch.randn(cout, cin, k, k, k, generator=g, dtype=torch.float64) / np.sqrt(cin * k**3)).requires_grad_()
+    y = _ref_conv(x, w, s, p, reflect)
+    gy = torch.randn(y.shape, generator=g, dtype=torch.float64)
+    dw, = torch.autograd.grad(y, (w,), gy)
+    gw = ops.with_prec(ops.conv_wgrad_geom(n, tuple(sp), tuple(y.shape[2:]), cin, cout, k, s, p, reflect), L.PREC_BF16)
+    ws = torch.empty(ops.wgrad_ws_floats(gw), device="cuda")
+    dwo = torch.empty(w.shape, device="cuda")
+    ops.wgrad(gw, _cl(x), _cl(gy), dwo, ws)
+    assert_close(dwo.double().cpu().numpy(), dw.numpy(), 2e-2, "bf16 wgrad")
+
+
+def test_wgrad_bf16_conv_transpose():
+    from cgan3d_amd import ops, _lib as L
+    g = torch.Generator().manual_seed(9)
+    n, cin, cout, k, s, p, sp = 2, 64, 32, 3, 2, 1, (4, 6, 8)
+    x = torch.randn(n, cin, *sp, generator=g, dtype=torch.float64)
+    w = (torch.randn(cin, cout, k, k, k, generator=g, dtype=torch.float64) / np.sqrt(cout * k**3)).requires_grad_()
+    y = F.conv_transpose3d(x, w, stride=s, padding=p, output_padding=1)
+    gy = torch.randn(y.shape, generator=g, dtype=torch.float64)
+    dw, = torch.autograd.grad(y, (w,), gy)
+    gw = ops.with_prec(ops.convt_wgrad_geom(n, sp, tuple(y.shape[2:]), cin, cout, k, s, p), L.PREC_BF16)
+    ws = torch.empty(ops.wgrad_ws_floats(gw), device="cuda")
+    dwo = torch.empty(w.shape, device="cuda")
+    ops.wgrad(gw, _cl(gy), _cl(x), dwo, ws)
+    assert_close(dwo.double().cpu().numpy(), dw.numpy(), 2e-2, "bf16 convT wgrad")

@@ -1,0 +1,90 @@
+"""Per-launch timing of single HIP kernels at the benchmark's shapes (kernel tuning aid).
+
+    python tools/bench_ops.py [--case res_wgrad ...] [--tune KEY=V1,V2,...]
+
+Each case builds its operands once, warms up, then times 20 back-to-back launches between two
+HIP events; prints one line per (case, tuning value) with µs/launch and TFLOP/s (algorithmic).
+"""
+import argparse
+import sys
+from pathlib import Path
+
+REPO = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(REPO / "contrast-gan-3d_amd"))
+
+import torch  # noqa: E402
+
+
+def _cases(B=4, S=64):
+    from cgan3d_amd import ops, _lib as L
+    BF = L.PREC_BF16
+    r = S // 4
+    dev = torch.device("cuda")
+
+    def t(*shape):
+        return torch.randn(*shape, device=dev)
+
+    def conv_case(geo, cin, cout, din, dout, packed=True):
+        w = t(cout, cin, geo.k, geo.k, geo.k) * 0.05
+        if packed:
+            ps = ops.PackSet(dev)
+            geo, w = ps.add(geo, w, BF)
+            ps.pack()
+        x, y = t(B, *din, geo.cin), torch.empty(B, *dout, geo.cout, device=dev)
+        flops = 2.0 * B * dout[0] * dout[1] * dout[2] * geo.cin * geo.cout * geo.k**3
+        return (lambda: ops.conv(geo, x, w, y)), flops
+
+    def wgrad_case(geo, din, dout):
+        x, go = t(B, *din, geo.cin), t(B, *dout, geo.cout)
+        dw = torch.empty(geo.cout, geo.cin, geo.k, geo.k, geo.k, device=dev)
+        ws = torch.empty(ops.wgrad_ws_floats(geo), device=dev)
+        flops = 2.0 * B * dout[0] * dout[1] * dout[2] * geo.cin * geo.cout * geo.k**3
+        return (lambda: ops.wgrad(geo, x, go, dw, ws)), flops
+
+    R3, H3, F3 = (r,) * 3, (2 * r,) * 3, (S,) * 3
+    return {
+        "res_fwd": lambda: conv_case(ops.conv_fwd_geom(B, R3, R3, 64, 64, 3, 1, 1), 64, 64, R3, R3),
+        "res_wgrad": lambda: wgrad_case(ops.with_prec(ops.conv_wgrad_geom(B, R3, R3, 64, 64, 3, 1, 1), BF), R3, R3),
+        "down0_wgrad": lambda: wgrad_case(ops.with_prec(ops.conv_wgrad_geom(B, F3, H3, 16, 32, 3, 2, 1), BF), F3, H3),
+        "down0_fwd": lambda: conv_case(ops.conv_fwd_geom(B, F3, H3, 16, 32, 3, 2, 1), 16, 32, F3, H3),
+        "up1_fwd": lambda: conv_case(ops.convt_fwd_geom(B, H3, F3, 32, 16, 3, 2, 1), 32, 16, H3, F3),
+        "k7_last_fwd": lambda: conv_case(ops.with_prec(ops.conv_fwd_geom(B, F3, F3, 16, 1, 7, 1, 3, True), BF), 16, 1,
+                                         F3, F3, packed=False),
+    }
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--case", nargs="*", default=None)
+    ap.add_argument("--tune", default=None, help="KEY=v1,v2,... (cgan3d_set_tuning)")
+    ap.add_argument("--reps", type=int, default=20)
+    args = ap.parse_args()
+    from cgan3d_amd import _lib as L
+    lib = L.load()
+    cases = _cases()
+    names = args.case or list(cases)
+    tunes = [(None, None)]
+    if args.tune:
+        k, vs = args.tune.split("=")
+        tunes = [(int(k), int(v)) for v in vs.split(",")]
+    for key, val in tunes:
+        if key is not None:
+            L.check(lib.cgan3d_set_tuning(key, val), "set_tuning")
+        for nm in names:
+            fn, flops = cases[nm]()
+            for _ in range(3):
+                fn()
+            torch.cuda.synchronize()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(args.reps):
+                fn()
+            e1.record()
+            torch.cuda.synchronize()
+            us = e0.elapsed_time(e1) * 1e3 / args.reps
+            tag = f" tune{key}={val}" if key is not None else ""
+            print(f"{nm:14s}{tag:16s} {us:9.2f} us  {flops / us / 1e6:8.1f} TFLOP/s", flush=True)
+
+
+if __name__ == "__main__":
+    main()
