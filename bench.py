@@ -48,7 +48,7 @@ def conv_flops(n, dout, cin, cout, k):
 # roofline candidates: kernel description, launch role, geometry predicate, committed PMC summary
 # (HBM bytes per launch from rocprofv3 FETCH_SIZE / WRITE_SIZE passes, profiles/)
 ROOFLINES = {
-    "halo_res": ("conv_halo_kernel<64,4>: ResNet-block Conv3d 64->64 k3 s1 at (S/4)^3, forward + input-grad",
+    "halo_res": ("conv_halo_kernel: ResNet-block Conv3d 64->64 k3 s1 at (S/4)^3, forward + input-grad",
                  "conv", lambda g: g.w_packed == 2 and g.cin == 64 and g.cout == 64 and g.k == 3 and g.stride == 1,
                  "profiles/r01_pmc_conv_halo_64_4.json"),
     "k7_w2n": ("k7m_w2n_kernel: generator last Conv3d 16->1 k7 (+bias, tanh, opt_hat) forward",
@@ -108,7 +108,9 @@ def main():
     ap.add_argument("--precision", choices=["f32", "bf16"], default="bf16",
                     help="MFMA operand precision of the convolutions (accumulation is f32)")
     ap.add_argument("--roofline", choices=sorted(ROOFLINES), default="halo_res")
-    ap.add_argument("--no-graph", action="store_true", help="launch eagerly instead of replaying a HIP graph")
+    ap.add_argument("--graph", action="store_true",
+                    help="replay the step as one captured HIP graph (default: eager launches, which let the "
+                         "weight-gradient side stream run concurrently on its own hardware queue)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -138,7 +140,7 @@ def main():
     d = pcg64_init_(PatchGANDiscriminator(1, 8, 3, negative_slope=0.2, norm_layer=nn.Identity), 1).to(dev)
     eng = StepEngine(g, d, g.config, d.config, B, B, (S, S, S), g_hyper=(1e-4, 0.0, 0.9, 1e-8),
                      d_hyper=(1e-4, 0.0, 0.9, 1e-8), device=dev, precision=args.precision)
-    use_graph = not args.no_graph and world == 1
+    use_graph = args.graph and world == 1
     batches = []
     for j in range(2):
         opt, _ = synth_patches(B, S, 1000 * rank + 10 * j)

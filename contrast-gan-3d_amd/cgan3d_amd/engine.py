@@ -174,7 +174,20 @@ class GeneratorPlan:
         self.dpad = buf(pd, la.cin)
         ws = max(ws, ops.wgrad_ws_floats(self.geo_last_wgrad), ops.channel_sum_ws_floats(n * la.dout[0] * la.dout[1] * la.dout[2], 1))
         self.ws = torch.empty(ws, device=device)
+        # weight gradients run on a side stream, beside the input-gradient chain (each wgrad only
+        # needs its layer's dz and input, both final when it is enqueued); own workspace
+        wsw = max([ops.wgrad_ws_floats(gw) for gw in self.geo_wgrad] + [ops.wgrad_ws_floats(self.geo_last_wgrad)])
+        self.ws_side = torch.empty(wsw, device=device)
+        self.side = torch.cuda.Stream(device=device) if torch.device(device).type == "cuda" else None
         self.pack()
+
+    def _on_side(self, fn):
+        """Enqueue ``fn``'s launches on the side stream after everything enqueued so far."""
+        if self.side is None:
+            return fn()
+        self.side.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(self.side):
+            fn()
 
     def pack(self):
         """Refresh the packed weight copies (one launch); call after every weight update."""
@@ -221,7 +234,8 @@ class GeneratorPlan:
         la = self.last
         n = self.n
         u = self.y[-1]
-        ops.wgrad(self.geo_last_wgrad, u, self.dz_last, G["model.last_conv.weight"], self.ws)
+        self._on_side(lambda: ops.wgrad(self.geo_last_wgrad, u, self.dz_last, G["model.last_conv.weight"],
+                                        self.ws_side))
         nvl = n * la.dout[0] * la.dout[1] * la.dout[2]
         ops.channel_sum(self.dz_last, nvl, 1, G["model.last_conv.bias"], self.ws)
         ops.conv(self.geo_last_dgrad, self.dz_last, P["model.last_conv.weight"], self.dpad)
@@ -233,15 +247,20 @@ class GeneratorPlan:
             ops.bn_backward(self.dy[i], self.z[i], nvox, ly.cout, self.ss[i], self.mi[i], P[f"{nb}.weight"], ly.act,
                             G[f"{nb}.weight"], G[f"{nb}.bias"], self.dz[i], self.ws)
             xin = self.y[i - 1] if i > 0 else x
+            wname = f"{ly.name}.conv.weight"
             if ly.kind == "convt":  # ConvTranspose3d: the output-grad is the gathered operand
-                ops.wgrad(self.geo_wgrad[i], self.dz[i], xin, G[f"{ly.name}.conv.weight"], self.ws)
+                self._on_side(lambda g=self.geo_wgrad[i], a=self.dz[i], b=xin, w=G[wname]:
+                              ops.wgrad(g, a, b, w, self.ws_side))
             else:
-                ops.wgrad(self.geo_wgrad[i], xin, self.dz[i], G[f"{ly.name}.conv.weight"], self.ws)
+                self._on_side(lambda g=self.geo_wgrad[i], a=xin, b=self.dz[i], w=G[wname]:
+                              ops.wgrad(g, a, b, w, self.ws_side))
             if i == 0:
                 break
             # input-grad; a ResNet block0 also receives the skip gradient dL/dh_{r+1}
             res = self.dy[i + 1] if ly.name.endswith("block0") else None
             ops.conv(self.geo_dgrad[i], self.dz[i], self.wd[i], self.dy[i - 1], ops.epilogue(residual=res))
+        if self.side is not None:  # the weight gradients are complete before anything reads them
+            torch.cuda.current_stream(self.device).wait_stream(self.side)
 
 
 # ----------------------------------------------------------------------------------------------

@@ -85,6 +85,7 @@ void k7m_w2n_launch(const cgan3d_conv_geom* g, int P, int reflect, long long wc,
 int gemm_blocks(const cgan3d_conv_geom* g, long long* mblocks);
 bool wgrad_bf16_ok(const cgan3d_conv_geom* g);
 void wgrad_bf16_set_blocks(int v);
+void halo_set_min_blocks(int v);
 int wgrad_bf16_launch(const cgan3d_conv_geom* g, const float* gathered, const float* aligned, float* dwp,
                       hipStream_t st);
 bool halo_ok(const cgan3d_conv_geom* g);         // w_packed == 2 and eligible

@@ -280,6 +280,10 @@ __global__ __launch_bounds__(256) void pack_halo_kernel(const float* __restrict_
   }
 }
 
+static int g_halo_min_blocks = 512;  // cgan3d_set_tuning key 2
+
+void halo_set_min_blocks(int v) { g_halo_min_blocks = v; }
+
 static bool halo_setup(const cgan3d_conv_geom* g, HaloArgs* a) {
   if (g->prec != CGAN3D_PREC_BF16 || g->reflect) return false;
   if (!(g->cin == 32 || g->cin == 64) || g->cout % 16 || g->k > 4 || g->stride < 1 || g->stride > 2) return false;
@@ -303,6 +307,9 @@ static bool halo_setup(const cgan3d_conv_geom* g, HaloArgs* a) {
   ey = ex = ez;
   a->ez = ez; a->ey = ey; a->ex = ex;
   a->bn = g->cout % 64 == 0 ? 64 : (g->cout % 32 == 0 ? 32 : 16);
+  // small grids: split the output channels over more blocks (more waves in flight per CU)
+  const long long tiles = (long long)a->nclass * a->n * a->td * a->th * a->tw;
+  while (a->bn > 32 && tiles * (g->cout / a->bn) < g_halo_min_blocks) a->bn /= 2;
   const int slot = a->bn * g->cin * 2;
   if (slot != 2048 && slot != 4096 && slot != 8192) return false;
   a->halo_bytes = ez * ey * ex * (g->cin + 8) * 2;

@@ -2,8 +2,9 @@
 
     python tools/bench_ops.py [--case res_wgrad ...] [--tune KEY=V1,V2,...]
 
-Each case builds its operands once, warms up, then times 20 back-to-back launches between two
-HIP events; prints one line per (case, tuning value) with µs/launch and TFLOP/s (algorithmic).
+Each case builds its operands once, warms up, captures 20 back-to-back launches in a HIP graph
+and times one replay between two HIP events; prints one line per (case, tuning value) with
+µs/launch and TFLOP/s (algorithmic).
 """
 import argparse
 import sys
@@ -75,10 +76,16 @@ def main():
             for _ in range(3):
                 fn()
             torch.cuda.synchronize()
+            # the repeats are captured in a HIP graph: host launch overhead stays out of the timing
+            graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(graph):
+                for _ in range(args.reps):
+                    fn()
+            graph.replay()
+            torch.cuda.synchronize()
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
-            for _ in range(args.reps):
-                fn()
+            graph.replay()
             e1.record()
             torch.cuda.synchronize()
             us = e0.elapsed_time(e1) * 1e3 / args.reps
