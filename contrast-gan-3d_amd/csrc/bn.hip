@@ -13,42 +13,49 @@
 
 namespace cg {
 
-// one block per channel
+// Chan's pairwise combine of (count, mean, M2) triples
+__device__ __forceinline__ void chan_merge(double& n, double& m, double& q, double nb, double mb, double qb) {
+  const double t = n + nb;
+  if (t <= 0.0) return;
+  const double d = mb - m;
+  m += d * (nb / t);
+  q += qb + d * d * (n * nb / t);
+  n = t;
+}
+
+// one block per channel; single pass over the per-block (sum, M2, count) partials, each thread
+// folding its partials with Chan's formula, then a shuffle / LDS tree of the same combine (fp64)
 __global__ __launch_bounds__(256) void bn_finalize_kernel(const float* __restrict__ stats, long long nblk, int C,
                                                           const float* gamma, const float* beta, float* rmean,
                                                           float* rvar, long long* nbt, float momentum, float eps,
                                                           float* scale_shift, float* mean_invstd) {
-  __shared__ double red[2][4];
-  __shared__ double sh_mean;
+  __shared__ double red[3][4];
   const int c = blockIdx.x, tid = threadIdx.x;
   const long long stride = 2LL * C + 1;
-  double s = 0.0, n = 0.0;
-  for (long long b = tid; b < nblk; b += blockDim.x) {
-    s += stats[b * stride + c];
-    n += stats[b * stride + 2 * C];
-  }
-  s = wave_sum_d(s);
-  n = wave_sum_d(n);
-  if ((tid & 63) == 0) { red[0][tid >> 6] = s; red[1][tid >> 6] = n; }
-  __syncthreads();
-  const double S = red[0][0] + red[0][1] + red[0][2] + red[0][3];
-  const double N = red[1][0] + red[1][1] + red[1][2] + red[1][3];
-  const double mean = S / N;
-  __syncthreads();
-  double m2 = 0.0;
-  for (long long b = tid; b < nblk; b += blockDim.x) {
-    const double nb = stats[b * stride + 2 * C];
-    if (nb > 0) {
-      const double d = stats[b * stride + c] / nb - mean;
-      m2 += stats[b * stride + C + c] + nb * d * d;
+  double n = 0.0, m = 0.0, q = 0.0;
+  for (long long b0 = tid; b0 < nblk; b0 += 4 * blockDim.x) {
+    float sv[4], qv[4], nv[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {  // four partials in flight
+      const long long b = b0 + k * blockDim.x;
+      const long long o = (b < nblk ? b : 0) * stride;
+      sv[k] = stats[o + c]; qv[k] = stats[o + C + c]; nv[k] = b < nblk ? stats[o + 2 * C] : 0.f;
     }
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      if (nv[k] > 0.f) chan_merge(n, m, q, nv[k], (double)sv[k] / nv[k], qv[k]);
   }
-  m2 = wave_sum_d(m2);
-  if ((tid & 63) == 0) red[0][tid >> 6] = m2;
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    const double nb = __shfl_xor(n, off, 64), mb = __shfl_xor(m, off, 64), qb = __shfl_xor(q, off, 64);
+    chan_merge(n, m, q, nb, mb, qb);
+  }
+  if ((tid & 63) == 0) { red[0][tid >> 6] = n; red[1][tid >> 6] = m; red[2][tid >> 6] = q; }
   __syncthreads();
   if (tid == 0) {
-    const double M2 = red[0][0] + red[0][1] + red[0][2] + red[0][3];
-    const double var = M2 / N;
+    for (int w = 1; w < 4; ++w) chan_merge(n, m, q, red[0][w], red[1][w], red[2][w]);
+    const double N = n, mean = m;
+    const double var = q / N;
     const double invstd = 1.0 / sqrt(var + (double)eps);
     const double sc = (double)gamma[c] * invstd;
     scale_shift[c] = (float)sc;
@@ -59,7 +66,6 @@ __global__ __launch_bounds__(256) void bn_finalize_kernel(const float* __restric
     if (rvar) rvar[c] = (float)((1.0 - momentum) * rvar[c] + momentum * var * N / (N > 1 ? N - 1 : 1));
     if (nbt && c == 0) *nbt += 1;
   }
-  (void)sh_mean;
 }
 
 __device__ __forceinline__ float act_f(float v, int act, float slope) {

@@ -43,31 +43,37 @@ __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, const 
 __global__ void adam_tick_kernel(float* hyper) { hyper[4] += 1.f; }
 
 // out[i] = sum of padded[q] over the reflect-pad preimages q of interior voxel i
+__device__ __forceinline__ int fold_src(int d, int D, int P, int* q) {  // padded rows mirroring onto d
+  int n = 0;
+  q[n++] = d + P;
+  if (d >= 1 && d <= P) q[n++] = P - d;
+  else if (d <= D - 2 && d >= D - 1 - P) q[n++] = 2 * (D - 1) - d + P;
+  return n;
+}
+
+// one thread per (voxel, V channels); 32-bit index math (element count < 2^31)
+template <int V>
 __global__ __launch_bounds__(256) void reflect_fold_kernel(const float* __restrict__ pad_in, float* __restrict__ out,
                                                            int N, int D, int H, int W, int C, int P) {
-  const long long total = (long long)N * D * H * W * C;
+  typedef float fv __attribute__((ext_vector_type(V)));
+  const int C4 = C / V;
+  const int total = N * D * H * W * C4;
   const int Dp = D + 2 * P, Hp = H + 2 * P, Wp = W + 2 * P;
-  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long long)gridDim.x * blockDim.x) {
-    int c = (int)(i % C); long long t = i / C;
-    int w = (int)(t % W); t /= W;
-    int h = (int)(t % H); t /= H;
-    int d = (int)(t % D); int n = (int)(t / D);
-    int qd[2], qh[2], qw[2], nd = 0, nh = 0, nw = 0;
-    qd[nd++] = d + P;
-    if (d >= 1 && d <= P) qd[nd++] = P - d;
-    else if (d <= D - 2 && d >= D - 1 - P) qd[nd++] = 2 * (D - 1) - d + P;
-    qh[nh++] = h + P;
-    if (h >= 1 && h <= P) qh[nh++] = P - h;
-    else if (h <= H - 2 && h >= H - 1 - P) qh[nh++] = 2 * (H - 1) - h + P;
-    qw[nw++] = w + P;
-    if (w >= 1 && w <= P) qw[nw++] = P - w;
-    else if (w <= W - 2 && w >= W - 1 - P) qw[nw++] = 2 * (W - 1) - w + P;
-    float s = 0.f;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+    const int c4 = i % C4;
+    int t = i / C4;
+    const int w = t % W; t /= W;
+    const int h = t % H; t /= H;
+    const int d = t % D, n = t / D;
+    int qd[2], qh[2], qw[2];
+    const int nd = fold_src(d, D, P, qd), nh = fold_src(h, H, P, qh), nw = fold_src(w, W, P, qw);
+    fv s = {};
     for (int a = 0; a < nd; ++a)
       for (int b = 0; b < nh; ++b)
         for (int e = 0; e < nw; ++e)
-          s += pad_in[((((long long)n * Dp + qd[a]) * Hp + qh[b]) * Wp + qw[e]) * C + c];
-    out[i] = s;
+          s += *reinterpret_cast<const fv*>(pad_in + ((((long long)n * Dp + qd[a]) * Hp + qh[b]) * Wp + qw[e]) * C +
+                                            V * c4);
+    reinterpret_cast<fv*>(out)[i] = s;
   }
 }
 
@@ -129,9 +135,15 @@ extern "C" int cgan3d_reflect_fold(const float* padded, float* out, int32_t n, i
   CG_CHECK_ARG(n > 0 && d > 2 * pad && h > 2 * pad && w > 2 * pad && c > 0 && pad >= 0,
                "cgan3d_reflect_fold: dims must exceed 2*pad");
   const long long total = (long long)n * d * h * w * c;
-  int blocks = (int)std::min<long long>((total + 255) / 256, 8192);
-  hipLaunchKernelGGL(reflect_fold_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, padded, out, n, d, h, w, c,
-                     pad);
+  CG_CHECK_ARG(total < (1LL << 31), "cgan3d_reflect_fold: volume too large");
+  const bool v4 = c % 4 == 0;
+  int blocks = (int)std::min<long long>((total / (v4 ? 4 : 1) + 255) / 256, 8192);
+  if (v4)
+    hipLaunchKernelGGL(reflect_fold_kernel<4>, dim3(blocks), dim3(256), 0, (hipStream_t)stream, padded, out, n, d, h, w,
+                       c, pad);
+  else
+    hipLaunchKernelGGL(reflect_fold_kernel<1>, dim3(blocks), dim3(256), 0, (hipStream_t)stream, padded, out, n, d, h, w,
+                       c, pad);
   CG_LAUNCH_CHECK("reflect_fold_kernel");
   return CGAN3D_OK;
 }

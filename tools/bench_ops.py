@@ -43,7 +43,30 @@ def _cases(B=4, S=64):
         return (lambda: ops.wgrad(geo, x, go, dw, ws)), flops
 
     R3, H3, F3 = (r,) * 3, (2 * r,) * 3, (S,) * 3
+
+    def crit(cin, cout, din, halo=True):
+        """critic layer forward over the 3B critic batch (real | fake | interpolation)"""
+        n3 = 3 * B
+        dout = tuple(d // 2 for d in din)
+        old, ops.HALO = ops.HALO, halo
+        try:
+            geo = ops.conv_fwd_geom(n3, din, dout, cin, cout, 4, 2, 1)
+            w = t(cout, cin, 4, 4, 4) * 0.05
+            ps = ops.PackSet(dev)
+            geo, w = ps.add(geo, w, BF)
+            ps.pack()
+        finally:
+            ops.HALO = old
+        x, y = t(n3, *din, cin), torch.empty(n3, *dout, cout, device=dev)
+        flops = 2.0 * n3 * dout[0] * dout[1] * dout[2] * cin * cout * 64
+        return (lambda: ops.conv(geo, x, w, y)), flops
+
     return {
+        "crit_first": lambda: crit(1, 8, F3),
+        "crit_m0": lambda: crit(8, 16, H3),
+        "crit_m1": lambda: crit(16, 32, R3),
+        "crit_m2": lambda: crit(32, 64, (r // 2,) * 3),
+        "crit_m2_gemm": lambda: crit(32, 64, (r // 2,) * 3, halo=False),
         "res_fwd": lambda: conv_case(ops.conv_fwd_geom(B, R3, R3, 64, 64, 3, 1, 1), 64, 64, R3, R3),
         "res_wgrad": lambda: wgrad_case(ops.with_prec(ops.conv_wgrad_geom(B, R3, R3, 64, 64, 3, 1, 1), BF), R3, R3),
         "down0_wgrad": lambda: wgrad_case(ops.with_prec(ops.conv_wgrad_geom(B, F3, H3, 16, 32, 3, 2, 1), BF), F3, H3),
