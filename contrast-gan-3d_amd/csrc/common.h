@@ -84,6 +84,8 @@ void k7m_w2n_launch(const cgan3d_conv_geom* g, int P, int reflect, long long wc,
 // implicit-GEMM forward / input-grad (conv_gemm.hip)
 int gemm_blocks(const cgan3d_conv_geom* g, long long* mblocks);
 bool wgrad_bf16_ok(const cgan3d_conv_geom* g);
+bool wgrad_c1_ok(const cgan3d_conv_geom* g);
+int wgrad_c1_launch(const cgan3d_conv_geom* g, const float* gathered, const float* aligned, float* dw, hipStream_t st);
 void wgrad_bf16_set_blocks(int v);
 void halo_set_min_blocks(int v);
 int wgrad_bf16_launch(const cgan3d_conv_geom* g, const float* gathered, const float* aligned, float* dwp,

@@ -498,6 +498,15 @@ extern "C" int cgan3d_conv3d_wgrad(const cgan3d_conv_geom* g, const float* gathe
     }
     CG_CHECK_ARG(!accumulate, "cgan3d_conv3d_wgrad: internal dispatch error");
   }
+  if (wgrad_c1_ok(g)) {  // single-channel input: straight into dW, no workspace
+    if (!accumulate && hipMemsetAsync(dw, 0, R * g->cout * sizeof(float), s) != hipSuccess) {
+      set_error("cgan3d_conv3d_wgrad: memset failed");
+      return CGAN3D_EHIP;
+    }
+    wgrad_c1_launch(g, gathered, aligned, dw, s);
+    CG_LAUNCH_CHECK("conv_wgrad_c1_kernel");
+    return CGAN3D_OK;
+  }
   if (hipMemsetAsync(ws, 0, R * g->cout * sizeof(float), s) != hipSuccess) {
     set_error("cgan3d_conv3d_wgrad: memset failed");
     return CGAN3D_EHIP;

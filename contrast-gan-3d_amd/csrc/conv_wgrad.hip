@@ -163,6 +163,89 @@ __global__ __launch_bounds__(256) void conv_wgrad_bf16_kernel(WgArgs a, const fl
   }
 }
 
+// ---- single-channel input, few output channels (the critic's first layer, 1 -> 8, k4 s2):
+// M x N = 64 taps x 8 is too small for MFMA tiles, K = every output voxel.  A thread owns one tap
+// and all output channels; the 64 lanes of a wave are the 64 taps of ONE output voxel, so the
+// aligned-operand loads are wave-wide broadcasts and the gathered loads hit one 4x4x4 window.
+// Per block: fp32 partial sums over its voxel chunk, combined across the waves in LDS, then one
+// atomic add per (tap, channel) into dW (zeroed by the caller unless accumulating).  fp32 FMA.
+template <int COUT>
+__global__ __launch_bounds__(256) void conv_wgrad_c1_kernel(WgArgs a, const float* __restrict__ gx,
+                                                            const float* __restrict__ go, float* dw, long long w_sb) {
+  constexpr int VL = 4;  // voxel lanes (waves) per block; T = 64 taps per wave
+  __shared__ float red[VL][64][COUT + 1];
+  const int tid = threadIdx.x, t = tid & 63, vl = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const bool tok = t < a.R;
+  const int td = t / (a.k * a.k), th = (t / a.k) % a.k, tw = t % a.k;
+  const long long vbeg = (long long)blockIdx.x * a.vpb;
+  const long long vend = vbeg + a.vpb < a.V ? vbeg + a.vpb : a.V;
+  float acc[COUT];
+#pragma unroll
+  for (int c = 0; c < COUT; ++c) acc[c] = 0.f;
+  long long v = vbeg + vl;
+  int ow = (int)(v % a.wo), q = (int)(v / a.wo);
+  int oh = q % a.ho;
+  q /= a.ho;
+  int od = q % a.do_, nb = q / a.do_;
+  for (; v < vend; v += VL) {
+    const int id = wg_coord(od * a.s - a.p + td, a.di, a.reflect);
+    const int ih = wg_coord(oh * a.s - a.p + th, a.hi, a.reflect);
+    const int iw = wg_coord(ow * a.s - a.p + tw, a.wi, a.reflect);
+    const bool ok = tok && (id | ih | iw) >= 0;
+    float xv = gx[ok ? (((long long)nb * a.di + id) * a.hi + ih) * a.wi + iw : 0];
+    xv = ok ? xv : 0.f;
+    const f32x4* g4 = reinterpret_cast<const f32x4*>(go + v * COUT);
+#pragma unroll
+    for (int c4 = 0; c4 < COUT / 4; ++c4) {
+      const f32x4 gv = g4[c4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) acc[4 * c4 + e] = fmaf(xv, gv[e], acc[4 * c4 + e]);
+    }
+    ow += VL;
+    while (ow >= a.wo) {
+      ow -= a.wo;
+      if (++oh == a.ho) {
+        oh = 0;
+        if (++od == a.do_) { od = 0; ++nb; }
+      }
+    }
+  }
+#pragma unroll
+  for (int c = 0; c < COUT; ++c) red[vl][t][c] = acc[c];
+  __syncthreads();
+  for (int i = tid; i < 64 * COUT; i += 256) {
+    const int tt = i / COUT, c = i - tt * COUT;
+    if (tt < a.R) {
+      float sum = 0.f;
+#pragma unroll
+      for (int l = 0; l < VL; ++l) sum += red[l][tt][c];
+      atomicAdd(dw + c * w_sb + tt, sum);
+    }
+  }
+}
+
+bool wgrad_c1_ok(const cgan3d_conv_geom* g) {
+  return !g->transposed && g->cin == 1 && g->k * g->k * g->k <= 64 && (g->cout == 4 || g->cout == 8 || g->cout == 16);
+}
+
+// atomically adds into dw (torch layout, zeroed by the caller unless accumulating)
+int wgrad_c1_launch(const cgan3d_conv_geom* g, const float* gathered, const float* aligned, float* dw, hipStream_t st) {
+  WgArgs a;
+  a.n = g->n; a.di = g->di; a.hi = g->hi; a.wi = g->wi; a.do_ = g->do_; a.ho = g->ho; a.wo = g->wo;
+  a.cin = 1; a.cout = g->cout; a.k = g->k; a.s = g->stride; a.p = g->pad; a.reflect = g->reflect;
+  a.R = g->k * g->k * g->k;
+  a.V = (long long)g->n * g->do_ * g->ho * g->wo;
+  long long blocks = (a.V + 255) / 256;
+  if (blocks > 1024) blocks = 1024;
+  a.vpb = (a.V + blocks - 1) / blocks;
+  a.vpb = (a.vpb + 3) / 4 * 4;
+  dim3 grid((unsigned)((a.V + a.vpb - 1) / a.vpb));
+#define CG_WC1(C) hipLaunchKernelGGL((conv_wgrad_c1_kernel<C>), grid, dim3(256), 0, st, a, gathered, aligned, dw, (long long)g->w_sb)
+  if (g->cout == 4) CG_WC1(4); else if (g->cout == 8) CG_WC1(8); else CG_WC1(16);
+#undef CG_WC1
+  return CGAN3D_OK;
+}
+
 static int g_wgrad_blocks = 2048;  // target grid size (cgan3d_set_tuning key 1)
 
 void wgrad_bf16_set_blocks(int v) { g_wgrad_blocks = v > 0 ? v : 2048; }
