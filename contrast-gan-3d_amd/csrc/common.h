@@ -12,6 +12,16 @@
 
 namespace cg {
 
+// Workgroup barrier for LDS hand-offs that leaves outstanding global loads in flight: hipcc's
+// __syncthreads() waits vmcnt(0) first, which serialises a register-prefetch pipeline on the
+// memory latency (cdna_hip_programming.md §5 "Pipelining across barriers").
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+
 // last-error slot, per host thread (the C-ABI is callable from any thread)
 void set_error(const char* fmt, ...);
 

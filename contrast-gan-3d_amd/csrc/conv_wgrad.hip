@@ -6,8 +6,8 @@
 // voxels.  A block owns 64 rows (one tap x 64 channels, or 2-4 taps of 32/16 channels) x all
 // output channels (<= 64) and walks a chunk of output voxels 64 at a time:
 //
-//  * staging: half the threads gather G (f32x4 = 4 channels of one voxel, or 4 taps of a
-//    single-channel input; 8 voxels each), half load O; both are written TRANSPOSED as bf16 —
+//  * staging: half the threads gather G (f32x4 = 4 channels of one voxel, 8 voxels each), half
+//    load O; both are written TRANSPOSED as bf16 —
 //    [row][voxel] and [b][voxel] with voxels contiguous — 16 bytes per store, so each MFMA
 //    fragment (8 consecutive voxels of one row or column) is one ds_read_b128;
 //  * the next chunk's global loads are issued before the MFMAs of the current one;
@@ -33,7 +33,7 @@ __device__ __forceinline__ int wg_coord(int i, int n, int reflect) {
   return (i >= 0 && i < n) ? i : -1;
 }
 
-template <int NB, bool CIN1>
+template <int NB, bool ROW8>
 __global__ __launch_bounds__(256) void conv_wgrad_bf16_kernel(WgArgs a, const float* __restrict__ gx,
                                                               const float* __restrict__ go, float* dwp) {
   __shared__ __attribute__((aligned(16))) __bf16 As[64 * WG_LD];  // [row][voxel]
@@ -43,24 +43,14 @@ __global__ __launch_bounds__(256) void conv_wgrad_bf16_kernel(WgArgs a, const fl
   const long long vbeg = (long long)blockIdx.y * a.vpb;
   const long long vend = vbeg + a.vpb < a.V ? vbeg + a.vpb : a.V;
 
-  // staging role: tid < 128 gathers G rows (4rq..4rq+3), else loads O columns (4rq..4rq+3)
-  // lanes with consecutive vo write consecutive 16-byte chunks of one LDS row (conflict-free);
-  // 8 lanes with consecutive rq read 128 contiguous bytes of a voxel
-  const bool isA = tid < 128;
+  // staging role (wave-uniform): waves 0-1 gather G rows (4rq..4rq+3 = one tap, 4 channels),
+  // waves 2-3 load O columns (4rq..4rq+3); lanes with consecutive vo write consecutive 16-byte
+  // chunks of one LDS row (conflict-free), 8 lanes with consecutive rq read 128 contiguous bytes
+  const bool isA = wave < 2;
   const int vo = tid & 7, rq = (tid >> 3) & 15;
   int td = 0, th = 0, tw = 0, ca = 0;
-  bool rowok = false;
-  int td4[4], th4[4], tw4[4];  // single-channel input: the 4 rows are 4 taps
-  bool ok4[4];
-  if (CIN1 && isA) {
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const int t = r0 + 4 * rq + e;
-      ok4[e] = t < a.R;
-      td4[e] = t / (a.k * a.k); th4[e] = (t / a.k) % a.k; tw4[e] = t % a.k;
-    }
-    rowok = ok4[0];
-  } else if (isA) {
+  bool rowok;
+  if (isA) {
     const int r = r0 + 4 * rq;
     rowok = r < a.R;
     const int t = rowok ? r / a.cin : 0;
@@ -70,47 +60,40 @@ __global__ __launch_bounds__(256) void conv_wgrad_bf16_kernel(WgArgs a, const fl
     rowok = 4 * rq < a.cout;
   }
 
-  f32x4 st[8];
-  auto load = [&](long long vb) {
-    // 8 consecutive output voxels: decode the first (32-bit), then step along W with carries
+  auto load = [&](f32x4 (&st)[8], long long vb) {
+    // 8 consecutive output voxels 8vo..8vo+7 of the chunk; ROW8 (W % 8 == 0, chunk starts at a
+    // multiple of 8): one output row, decoded once
     const int lin0 = (int)(vb + 8 * vo);
     int ow = lin0 % a.wo, q = lin0 / a.wo;
     int oh = q % a.ho;
     q /= a.ho;
     int od = q % a.do_, nb = q / a.do_;
+    const int id = wg_coord(od * a.s - a.p + td, a.di, a.reflect);
+    const int ih = wg_coord(oh * a.s - a.p + th, a.hi, a.reflect);
+    const long long rowA = (((long long)nb * a.di + id) * a.hi + ih) * a.wi;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const int lin = lin0 + j;
       long long off = -1;
-      if (CIN1 && isA) {
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          long long o1 = -1;
-          if (ok4[e] && lin < vend) {
-            const int id = wg_coord(od * a.s - a.p + td4[e], a.di, a.reflect);
-            const int ih = wg_coord(oh * a.s - a.p + th4[e], a.hi, a.reflect);
-            const int iw = wg_coord(ow * a.s - a.p + tw4[e], a.wi, a.reflect);
-            if ((id | ih | iw) >= 0) o1 = (((long long)nb * a.di + id) * a.hi + ih) * a.wi + iw;
-          }
-          st[j][e] = gx[o1 >= 0 ? o1 : 0];
-          if (o1 < 0) st[j][e] = 0.f;
-        }
-      } else {
-        if (rowok && lin < vend) {
-          if (isA) {
-            const int id = wg_coord(od * a.s - a.p + td, a.di, a.reflect);
-            const int ih = wg_coord(oh * a.s - a.p + th, a.hi, a.reflect);
-            const int iw = wg_coord(ow * a.s - a.p + tw, a.wi, a.reflect);
-            if ((id | ih | iw) >= 0) off = ((((long long)nb * a.di + id) * a.hi + ih) * a.wi + iw) * a.cin + ca;
+      if (rowok && lin < vend) {
+        if (isA) {
+          if (ROW8) {
+            const int iw = wg_coord((ow + j) * a.s - a.p + tw, a.wi, a.reflect);
+            if ((id | ih | iw) >= 0) off = (rowA + iw) * a.cin + ca;
           } else {
-            off = (long long)lin * a.cout + 4 * rq;
+            const int id2 = wg_coord(od * a.s - a.p + td, a.di, a.reflect);
+            const int ih2 = wg_coord(oh * a.s - a.p + th, a.hi, a.reflect);
+            const int iw2 = wg_coord(ow * a.s - a.p + tw, a.wi, a.reflect);
+            if ((id2 | ih2 | iw2) >= 0) off = ((((long long)nb * a.di + id2) * a.hi + ih2) * a.wi + iw2) * a.cin + ca;
           }
+        } else {
+          off = (long long)lin * a.cout + 4 * rq;
         }
-        const float* src = isA ? gx : go;
-        st[j] = *reinterpret_cast<const f32x4*>(src + (off >= 0 ? off : 0));
-        if (off < 0) st[j] = f32x4{0.f, 0.f, 0.f, 0.f};
       }
-      if (++ow == a.wo) {
+      const float* src = isA ? gx : go;
+      st[j] = *reinterpret_cast<const f32x4*>(src + (off >= 0 ? off : 0));
+      if (off < 0) st[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (!ROW8 && ++ow == a.wo) {
         ow = 0;
         if (++oh == a.ho) {
           oh = 0;
@@ -119,7 +102,7 @@ __global__ __launch_bounds__(256) void conv_wgrad_bf16_kernel(WgArgs a, const fl
       }
     }
   };
-  auto store = [&]() {
+  auto store = [&](const f32x4 (&st)[8]) {
     __bf16* base = (isA ? As : Gs) + (4 * rq) * WG_LD + 8 * vo;
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
@@ -134,12 +117,15 @@ __global__ __launch_bounds__(256) void conv_wgrad_bf16_kernel(WgArgs a, const fl
 #pragma unroll
   for (int nt = 0; nt < NB; ++nt) acc[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
   const int g = lane >> 4, r16 = lane & 15;
-  load(vbeg);
+  // the next chunk's global loads are in flight during this chunk's MFMAs; lds_barrier() keeps
+  // them in flight across the barriers
+  f32x4 st[8];
+  load(st, vbeg);
   for (long long vb = vbeg; vb < vend; vb += WG_KV) {
-    __syncthreads();  // the previous stage's fragments have been read
-    store();
-    __syncthreads();
-    if (vb + WG_KV < vend) load(vb + WG_KV);  // in flight during the MFMAs below
+    lds_barrier();  // the previous stage's fragments have been read
+    store(st);
+    lds_barrier();
+    if (vb + WG_KV < vend) load(st, vb + WG_KV);
 #pragma unroll
     for (int ks = 0; ks < WG_KV / 32; ++ks) {
       const bf16x8_w av = *reinterpret_cast<const bf16x8_w*>(As + (wave * 16 + r16) * WG_LD + ks * 32 + 8 * g);
@@ -246,13 +232,13 @@ int wgrad_c1_launch(const cgan3d_conv_geom* g, const float* gathered, const floa
   return CGAN3D_OK;
 }
 
-static int g_wgrad_blocks = 2048;  // target grid size (cgan3d_set_tuning key 1)
+static int g_wgrad_blocks = 1024;  // target grid size (cgan3d_set_tuning key 1)
 
-void wgrad_bf16_set_blocks(int v) { g_wgrad_blocks = v > 0 ? v : 2048; }
+void wgrad_bf16_set_blocks(int v) { g_wgrad_blocks = v > 0 ? v : 1024; }
 
 bool wgrad_bf16_ok(const cgan3d_conv_geom* g) {
-  return g->prec == CGAN3D_PREC_BF16 && !g->transposed && (g->cin % 4 == 0 || g->cin == 1) && g->cout % 4 == 0 &&
-         g->cout <= 64 && g->cout >= 4;
+  return g->prec == CGAN3D_PREC_BF16 && !g->transposed && g->cin % 4 == 0 && g->cout % 4 == 0 && g->cout <= 64 &&
+         g->cout >= 4;
 }
 
 // adds into the packed [t][a][b] workspace dwp (zeroed by the caller)
@@ -264,7 +250,7 @@ int wgrad_bf16_launch(const cgan3d_conv_geom* g, const float* gathered, const fl
   a.R = g->k * g->k * g->k * g->cin;
   a.V = (long long)g->n * g->do_ * g->ho * g->wo;
   const int gx = (a.R + 63) / 64;
-  // ~2048 blocks over the chip, >= 4 stages (256 voxels) per block
+  // ~1024 blocks over the chip (fewer partial sums to add), >= 4 stages (256 voxels) per block
   long long gy = g_wgrad_blocks / gx;
   if (gy < 1) gy = 1;
   long long vpb = (a.V + gy - 1) / gy;
@@ -272,8 +258,8 @@ int wgrad_bf16_launch(const cgan3d_conv_geom* g, const float* gathered, const fl
   a.vpb = (vpb + WG_KV - 1) / WG_KV * WG_KV;
   dim3 grid(gx, (unsigned)((a.V + a.vpb - 1) / a.vpb));
   const int nb = (g->cout + 15) / 16;
-#define CG_WGB(N, C1) hipLaunchKernelGGL((conv_wgrad_bf16_kernel<N, C1>), grid, dim3(256), 0, st, a, gathered, aligned, dwp)
-  if (g->cin == 1) {
+#define CG_WGB(N, R8) hipLaunchKernelGGL((conv_wgrad_bf16_kernel<N, R8>), grid, dim3(256), 0, st, a, gathered, aligned, dwp)
+  if (g->wo % 8 == 0) {  // chunks are 64-voxel aligned: 8 | W keeps each thread's 8 voxels in one row
     if (nb == 1) CG_WGB(1, true); else if (nb == 2) CG_WGB(2, true); else if (nb == 3) CG_WGB(3, true); else CG_WGB(4, true);
   } else {
     if (nb == 1) CG_WGB(1, false); else if (nb == 2) CG_WGB(2, false); else if (nb == 3) CG_WGB(3, false);

@@ -85,7 +85,7 @@ const char* cgan3d_get_last_error(void);
 /* Launch-shape tuning (process-wide; set before building plans: BatchNorm statistics buffers are
  * sized from the tile shape).  key 0: implicit-GEMM grids with fewer 64-voxel tiles than `value`
  * use 32x32 tiles (default 1024); key 1: target grid size of the bf16 weight-gradient kernel (default
- * 2048 blocks); key 2: the halo-tiled kernel halves its output-channel block (64 -> 32) while its grid
+ * 1024 blocks); key 2: the halo-tiled kernel halves its output-channel block (64 -> 32) while its grid
  * has fewer blocks than `value` (default 512). */
 int cgan3d_set_tuning(int32_t key, int32_t value);
 
