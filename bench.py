@@ -48,18 +48,19 @@ def conv_flops(n, dout, cin, cout, k):
 # roofline candidates: kernel description, launch role, geometry predicate, committed PMC summary
 # (HBM bytes per launch from rocprofv3 FETCH_SIZE / WRITE_SIZE passes, profiles/)
 ROOFLINES = {
-    "halo_res": ("conv_halo_kernel: ResNet-block Conv3d 64->64 k3 s1 at (S/4)^3, forward + input-grad",
-                 "conv", lambda g: g.w_packed == 2 and g.cin == 64 and g.cout == 64 and g.k == 3 and g.stride == 1,
+    "halo_res": ("ResNet-block Conv3d 64->64 k3 s1 at (S/4)^3, forward + input-grad "
+                 "(bf16: conv_halo_kernel; f32: conv_gemm_kernel)",
+                 "conv", lambda g: g.cin == 64 and g.cout == 64 and g.k == 3 and g.stride == 1,
                  "profiles/r01_pmc_conv_halo_64_4.json"),
     "k7_w2n": ("k7m_w2n_kernel: generator last Conv3d 16->1 k7 (+bias, tanh, opt_hat) forward",
                "conv", lambda g: g.k == 7 and g.cin == 16 and g.cout == 1, None),
 }
 
 
-def pmc_traffic(path, size, batch):
+def pmc_traffic(path, size, batch, precision):
     """HBM bytes per launch from a committed PMC summary measured on this workload (else None)."""
     f = REPO / path if path else None
-    if f is None or not f.is_file() or (size, batch) != (64, 4):
+    if f is None or not f.is_file() or (size, batch, precision) != (64, 4, "bf16"):
         return None
     return json.loads(f.read_text()).get("hbm_bytes_per_launch")
 
@@ -222,7 +223,7 @@ def main():
                    "hip_graph": use_graph},
         "roofline": {"kernel": roof_desc, "bound": "mfma", "achieved": round(achieved, 3), "peak": peak,
                      "unit": "TFLOP/s", "frac": round(achieved / peak, 4),
-                     "traffic": pmc_traffic(roof_pmc, S, B), "traffic_source": roof_pmc,
+                     "traffic": pmc_traffic(roof_pmc, S, B, args.precision), "traffic_source": roof_pmc,
                      "avg_launch_ms": round(kern_ms, 4), "flops_per_launch": roof_flops, "launches_timed": len(kern),
                      "timing": f"HIP events around {reps} back-to-back repeats of each launch, eager steps"},
     }

@@ -263,6 +263,17 @@ class GeneratorPlan:
             torch.cuda.current_stream(self.device).wait_stream(self.side)
 
 
+def _running_scale_shift(P, nb, ss):
+    """Eval-mode BatchNorm (Trainer.validate, Trainer.py:248-249): scale/shift from the running
+    statistics, written into ``ss`` = [scale | shift]."""
+    with torch.no_grad():
+        inv = torch.rsqrt(P[f"{nb}.running_var"] + 1e-5)
+        sc = P[f"{nb}.weight"] * inv
+        c = sc.numel()
+        ss[:c].copy_(sc)
+        ss[c:].copy_(P[f"{nb}.bias"] - P[f"{nb}.running_mean"] * sc)
+
+
 # ----------------------------------------------------------------------------------------------
 @dataclass
 class _DLayer:
@@ -277,8 +288,13 @@ class _DLayer:
 
 
 class CriticPlan:
-    """Buffers + geometry of PatchGANDiscriminator (model/discriminator.py:9-84), GP conf
-    (Identity norm, gradient_penalty_conf.py:14), for up to ``nmax`` samples."""
+    """Buffers + geometry of PatchGANDiscriminator (model/discriminator.py:9-84) for up to ``nmax``
+    samples: the GP conf (Identity norm, gradient_penalty_conf.py:14; conv bias + LeakyReLU in
+    the conv epilogue) and the BatchNorm critic of the weight-clip conf (basic_conf.py:60-66;
+    middle convs without bias, BatchNorm3d + LeakyReLU).  With BatchNorm every ``forward`` call
+    normalises its own batch (the reference calls the critic on the real and on the fake batch
+    separately, Trainer.py:119-120); ``bn_pass`` selects the slot that keeps that call's
+    statistics for its backward."""
 
     def __init__(self, cfg, nmax: int, dims: Dims, device, P: Dict[str, torch.Tensor], prec: int = L.PREC_F32):
         self.cfg, self.nmax, self.dims, self.device = cfg, nmax, tuple(dims), device
@@ -300,15 +316,26 @@ class CriticPlan:
         assert min(dn) > 0, f"patch {dims} too small for the critic"
         ls.append(_DLayer("model.last", 4, 1, 1, out_, 1, d, dn))
         self.layers = ls
+        self.bn = cfg.norm == "batch"
+        # BatchNorm layers: the middle convs of the BN critic (no conv bias, blocks.py:34)
+        self.is_bn = [self.bn and ly.name.startswith("model.middle.") for ly in ls]
         self.logit_ps = dn[0] * dn[1] * dn[2]
         self.a = [torch.empty((nmax, *ly.dout, ly.cout), device=device) for ly in ls]   # activations (last = logits)
         self.dz = [torch.empty((nmax, *ly.dout, ly.cout), device=device) for ly in ls]  # dL/dz (last = dlogits)
         ws = 0
         for ly in ls:
             g = ops.conv_wgrad_geom(nmax, ly.din, ly.dout, ly.cin, ly.cout, ly.k, ly.s, ly.p)
-            ws = max(ws, ops.wgrad_ws_floats(g),
-                     ops.channel_sum_ws_floats(nmax * ly.dout[0] * ly.dout[1] * ly.dout[2], ly.cout))
+            nv = nmax * ly.dout[0] * ly.dout[1] * ly.dout[2]
+            ws = max(ws, ops.wgrad_ws_floats(g), ops.channel_sum_ws_floats(nv, ly.cout),
+                     ops.bn_backward_ws_floats(nv, ly.cout))
         self.ws = torch.empty(ws, device=device)
+        if self.bn:  # conv outputs, pre-activation grads, statistics and per-pass scale/shift
+            self.z = [torch.empty_like(self.a[i]) if b else None for i, b in enumerate(self.is_bn)]
+            self.dy = [torch.empty_like(self.a[i]) if b else None for i, b in enumerate(self.is_bn)]
+            self.stats = [None] * len(ls)  # sized below from the launch geometry (packed / bf16 choice)
+            self.ss = [[torch.empty(2 * ly.cout, device=device) for ly in ls] for _ in range(2)]
+            self.mi = [[torch.empty(2 * ly.cout, device=device) for ly in ls] for _ in range(2)]
+            self.bn_scratch = [torch.empty(2 * ly.cout, device=device) for ly in ls]  # discarded dgamma/dbeta
         # packed weight copies per (layer, role); the packed layout does not depend on batch/dims
         self.packs = ops.PackSet(device)
         self.wf, self.wd = [], []
@@ -319,6 +346,10 @@ class CriticPlan:
                                     prec)
             self.wf.append(wf if gf.w_packed else None)
             self.wd.append(wd if gd.w_packed else None)
+        for i, ly in enumerate(ls):
+            if self.is_bn[i]:
+                gs = self._geo(ops.conv_fwd_geom(nmax, ly.din, ly.dout, ly.cin, ly.cout, ly.k, ly.s, ly.p), self.wf[i])
+                self.stats[i] = torch.empty(ops.stats_floats(gs), device=device)
         self.pack()
 
     def pack(self):
@@ -331,27 +362,62 @@ class CriticPlan:
     def _sl(self, t, off, n):
         return t[off:off + n]
 
-    def forward(self, P, x, off: int, n: int):
-        """a_l[off:off+n] = critic activations of x (n samples); logits in a[-1]."""
+    def forward(self, P, x, off: int, n: int, bn_pass: int = 0, training: bool = True):
+        """a_l[off:off+n] = critic activations of x (n samples); logits in a[-1].  BatchNorm
+        layers normalise over these n samples (training: batch statistics, running buffers
+        updated; eval: running statistics) and keep scale/shift in slot ``bn_pass``."""
         h = x
         for i, ly in enumerate(self.layers):
             g = self._geo(ops.conv_fwd_geom(n, ly.din, ly.dout, ly.cin, ly.cout, ly.k, ly.s, ly.p), self.wf[i])
-            last = i == len(self.layers) - 1
-            ep = ops.epilogue(bias=P[f"{ly.name}.bias"], act=L.ACT_NONE if last else L.ACT_LRELU, slope=self.slope)
+            w = self.wf[i] if self.wf[i] is not None else P[f"{ly.name}.weight"]
             out = self._sl(self.a[i], off, n)
-            ops.conv(g, h, self.wf[i] if self.wf[i] is not None else P[f"{ly.name}.weight"], out, ep)
+            if self.is_bn[i]:
+                nb = ly.name[:-len(".conv")] + ".normalization"
+                z = self._sl(self.z[i], off, n)
+                ss, mi = self.ss[bn_pass][i], self.mi[bn_pass][i]
+                if training:
+                    ops.conv(g, h, w, z, ops.epilogue(stats=self.stats[i]))
+                    ops.bn_finalize(self.stats[i], ops.stats_floats(g) // (2 * ly.cout + 1), ly.cout, P[f"{nb}.weight"],
+                                    P[f"{nb}.bias"], P[f"{nb}.running_mean"], P[f"{nb}.running_var"],
+                                    P[f"{nb}.num_batches_tracked"], ss, mi)
+                else:
+                    ops.conv(g, h, w, z)
+                    _running_scale_shift(P, nb, ss)
+                nvox = n * ly.dout[0] * ly.dout[1] * ly.dout[2]
+                ops.bn_apply(z, nvox, ly.cout, ss, L.ACT_LRELU, out, slope=self.slope)
+            else:
+                last = i == len(self.layers) - 1
+                ep = ops.epilogue(bias=P[f"{ly.name}.bias"], act=L.ACT_NONE if last else L.ACT_LRELU,
+                                  slope=self.slope)
+                ops.conv(g, h, w, out, ep)
             h = out
         return self._sl(self.a[-1], off, n)
 
-    def input_grad(self, P, off: int, n: int, dx_out: torch.Tensor, dx_off: int, dx_n: int):
+    def input_grad(self, P, off: int, n: int, dx_out: torch.Tensor, dx_off: int, dx_n: int, bn_pass: int = 0,
+                   G=None, bn_accumulate: bool = False):
         """dz chain from dz[-1][off:off+n] (dlogits) down to dz[0]; then dD/dx for samples
-        [dx_off, dx_off+dx_n) (absolute indices inside the batch) into dx_out."""
+        [dx_off, dx_off+dx_n) (absolute indices inside the batch) into dx_out.  BatchNorm layers
+        back-propagate with the statistics of ``bn_pass``; their gamma/beta gradients go to ``G``
+        (added when ``bn_accumulate``) or are discarded when ``G`` is None."""
         for i in range(len(self.layers) - 1, 0, -1):
             ly = self.layers[i]
             g = self._geo(ops.conv_dgrad_geom(n, ly.din, ly.dout, ly.cin, ly.cout, ly.k, ly.s, ly.p), self.wd[i])
             w = self.wd[i] if self.wd[i] is not None else P[f"{ly.name}.weight"]
-            ops.conv(g, self._sl(self.dz[i], off, n), w, self._sl(self.dz[i - 1], off, n),
-                     ops.epilogue(mask_src=self._sl(self.a[i - 1], off, n), slope=self.slope))
+            if self.is_bn[i - 1]:  # dL/da -> BatchNorm + LeakyReLU backward -> dL/dz
+                lp = self.layers[i - 1]
+                nb = lp.name[:-len(".conv")] + ".normalization"
+                dy = self._sl(self.dy[i - 1], off, n)
+                ops.conv(g, self._sl(self.dz[i], off, n), w, dy)
+                nvox = n * lp.dout[0] * lp.dout[1] * lp.dout[2]
+                dg, db = ((G[f"{nb}.weight"], G[f"{nb}.bias"]) if G is not None else
+                          (self.bn_scratch[i - 1][:lp.cout], self.bn_scratch[i - 1][lp.cout:]))
+                ops.bn_backward(dy, self._sl(self.z[i - 1], off, n), nvox, lp.cout, self.ss[bn_pass][i - 1],
+                                self.mi[bn_pass][i - 1], P[f"{nb}.weight"], L.ACT_LRELU, dg, db,
+                                self._sl(self.dz[i - 1], off, n), self.ws, slope=self.slope,
+                                accumulate=bn_accumulate and G is not None)
+            else:
+                ops.conv(g, self._sl(self.dz[i], off, n), w, self._sl(self.dz[i - 1], off, n),
+                         ops.epilogue(mask_src=self._sl(self.a[i - 1], off, n), slope=self.slope))
         ly = self.layers[0]
         if dx_n > 0:
             g = self._geo(ops.conv_dgrad_geom(dx_n, ly.din, ly.dout, ly.cin, ly.cout, ly.k, ly.s, ly.p), self.wd[0])
@@ -375,8 +441,9 @@ class CriticPlan:
         for i, ly in enumerate(self.layers):
             g = ops.with_prec(ops.conv_wgrad_geom(n_all, ly.din, ly.dout, ly.cin, ly.cout, ly.k, ly.s, ly.p), self.prec)
             ops.wgrad(g, prev, self.dz[i][:n_all], G[f"{ly.name}.weight"], self.ws)
-            nv = n_bias * ly.dout[0] * ly.dout[1] * ly.dout[2]
-            ops.channel_sum(self.dz[i][:n_bias], nv, ly.cout, G[f"{ly.name}.bias"], self.ws)
+            if not self.is_bn[i]:
+                nv = n_bias * ly.dout[0] * ly.dout[1] * ly.dout[2]
+                ops.channel_sum(self.dz[i][:n_bias], nv, ly.cout, G[f"{ly.name}.bias"], self.ws)
             prev = self.a[i][:n_all]
 
 
@@ -387,11 +454,18 @@ class StepEngine:
     def __init__(self, generator, critic, g_cfg, d_cfg, b_opt: int, b_sub: int, dims: Dims, *,
                  g_hyper: Sequence[float] = (1e-4, 0.0, 0.9, 1e-8), d_hyper: Sequence[float] = (1e-4, 0.0, 0.9, 1e-8),
                  gp_weight: float = 10.0, hu_bounds=(112.0 / 600.0, 212.0 / 600.0), gan_w=1.0, sim_w=1.0, hu_w=1.0,
-                 device=None, g_optim=None, d_optim=None, process_group=None, precision: str = "f32"):
+                 device=None, g_optim=None, d_optim=None, process_group=None, precision: str = "f32",
+                 weight_clip: Optional[float] = None):
         if b_opt != b_sub:
             raise NotImplementedError("StepEngine: the GP path assumes |OPT| == |LOW|+|HIGH| (basic_conf.py:74-79)")
-        if d_cfg.norm != "identity":
-            raise NotImplementedError("StepEngine: critic with BatchNorm (weight-clip conf) not built yet")
+        if d_cfg.norm not in ("identity", "batch"):
+            raise NotImplementedError(f"StepEngine: critic norm {d_cfg.norm!r} (LayerNorm critic: SURVEY.md §8f row 4)")
+        # gradient penalty unless weight clipping (Trainer.py:122-131): the GP conf (Identity-norm
+        # critic) or the weight-clip conf (BatchNorm critic, basic_conf.py:37,60-66)
+        self.use_gp = weight_clip is None
+        if self.use_gp and d_cfg.norm != "identity":
+            raise NotImplementedError("gradient penalty through a BatchNorm critic needs BatchNorm double backward "
+                                      "(SURVEY.md §8f row 4)")
         device = device or torch.device("cuda", torch.cuda.current_device())
         self.device = device
         self.dims = tuple(dims)
@@ -410,7 +484,7 @@ class StepEngine:
             g_optim = FusedAdam(Arena(generator, device), lr, (b1, b2), eps)
         if d_optim is None:
             lr, b1, b2, eps = d_hyper
-            d_optim = FusedAdam(Arena(critic, device), lr, (b1, b2), eps)
+            d_optim = FusedAdam(Arena(critic, device), lr, (b1, b2), eps, weight_clip=weight_clip)
         self.g_optim, self.d_optim = g_optim, d_optim
         # patch-level data parallelism: one gradient all-reduce per update
         self.pg = process_group
@@ -421,6 +495,7 @@ class StepEngine:
         self.gP = dict(self.g_arena.views)
         self.gP.update({k: v for k, v in generator.state_dict(keep_vars=True).items() if k not in self.gP})
         self.dP = dict(self.d_arena.views)
+        self.dP.update({k: v for k, v in critic.state_dict(keep_vars=True).items() if k not in self.dP})
         self.gG, self.dG = self.g_arena.gviews, self.d_arena.gviews
         # plans after the arenas: their packed-weight descriptors point at the arena storage
         self.G = GeneratorPlan(g_cfg, b_sub, dims, device, self.gP, prec)
@@ -444,9 +519,10 @@ class StepEngine:
         for ar in (self.g_arena, self.d_arena):
             for t in (ar.flat, ar.exp_avg, ar.exp_avg_sq):
                 dist.broadcast(t, src, group=self.pg)
-        for k, v in self.gP.items():
-            if k.endswith(("running_mean", "running_var", "num_batches_tracked")):
-                dist.broadcast(v.data, src, group=self.pg)
+        for P in (self.gP, self.dP):
+            for k, v in P.items():
+                if k.endswith(("running_mean", "running_var", "num_batches_tracked")):
+                    dist.broadcast(v.data, src, group=self.pg)
         self.G.pack()
         self.D.pack()
 
@@ -466,6 +542,8 @@ class StepEngine:
         self.G.forward(self.gP, self.subopt, opt_hat_out=self.opt_hat, training=True)
 
     def critic_update(self):
+        if not self.use_gp:
+            return self._critic_update_clip()
         D, bo, bs, bg, V = self.D, self.b_opt, self.b_sub, self.b_gp, self.vox
         nall = bo + bs + bg
         ops.gp_interpolate(self.xc[:bg], self.xc[bo:bo + bg], self.eps, self.xc[bo + bs:], bg, V)
@@ -477,6 +555,21 @@ class StepEngine:
         D.gp_forward_mode(self.dP, gamma, bo + bs, bg)
         D.weight_grads(self.dP, self.dG, self.xc, nall, bo + bs)
         self._allreduce(self.d_arena.grad)  # on the critical path: the G update uses the new critic
+        self.d_optim.launch()
+        self.D.pack()
+
+    def _critic_update_clip(self):
+        """Weight-clip conf (basic_conf.py:37,60-66): BatchNorm critic run on the real and on the
+        fake batch separately (each with its own batch statistics, Trainer.py:119-120), W-loss
+        without GP, Adam, then clamp to +-weight_clip (Trainer.py:136-138, inside the Adam kernel)."""
+        D, bo, bs = self.D, self.b_opt, self.b_sub
+        D.forward(self.dP, self.xc[:bo], 0, bo, bn_pass=0)
+        D.forward(self.dP, self.opt_hat, bo, bs, bn_pass=1)
+        ops.critic_logits_grad(D.a[-1], bo, bs, 0, D.logit_ps, self.gan_w, D.dz[-1], self.losses)
+        D.input_grad(self.dP, 0, bo, self.gbuf, 0, 0, bn_pass=0, G=self.dG)
+        D.input_grad(self.dP, bo, bs, self.gbuf, 0, 0, bn_pass=1, G=self.dG, bn_accumulate=True)
+        D.weight_grads(self.dP, self.dG, self.xc[:bo + bs], bo + bs, bo + bs)
+        self._allreduce(self.d_arena.grad)
         self.d_optim.launch()
         self.D.pack()
 

@@ -40,9 +40,9 @@ class PatchGANDiscriminator(nn.Module):
             norm_layer, "other")
         self.config = CriticConfig(channels_in, init_channels_out, discriminator_depth, slope, norm)
         self._unsupported = None
-        if is_2D or kernel_size != 4 or padding != 1 or norm != "identity":
-            self._unsupported = ("the HIP critic implements the gradient-penalty configuration (3-D, k4 p1, "
-                                 "Identity norm); BatchNorm/LayerNorm/2-D critics are SURVEY.md §8f row 4")
+        if is_2D or kernel_size != 4 or padding != 1 or norm not in ("identity", "batch"):
+            self._unsupported = ("the HIP critic implements the 3-D k4 p1 critic with Identity norm (GP conf) or "
+                                 "BatchNorm (weight-clip conf); LayerNorm/2-D critics are SURVEY.md §8f row 4")
         model = [("first", ConvBlock(is_2D, channels_in, init_channels_out, kernel_size, stride=stride,
                                      padding=padding, norm_layer=nn.Identity, activation_fn=nn.LeakyReLU, **kwargs))]
         middle = []
@@ -63,7 +63,7 @@ class PatchGANDiscriminator(nn.Module):
         self.model = nn.Sequential(OrderedDict(model))
 
     def _tensors(self):
-        return dict(self.named_parameters())
+        return dict(self.state_dict(keep_vars=True))  # parameters and BatchNorm buffers
 
     def plan_for(self, n, dims):
         from ..engine import CriticPlan
@@ -79,7 +79,8 @@ class PatchGANDiscriminator(nn.Module):
             return _CriticFn.apply(x, self, *params)
         n, _, *dims = x.shape
         plan = self.plan_for(n, dims)
-        logits = plan.forward(self._tensors(), x.detach().float().contiguous().view(n, *dims, 1), 0, n)
+        logits = plan.forward(self._tensors(), x.detach().float().contiguous().view(n, *dims, 1), 0, n,
+                              training=self.training)
         return logits.clone().view(n, 1, *logits.shape[1:4])
 
 
@@ -89,7 +90,7 @@ class _CriticFn(torch.autograd.Function):
         n, _, *dims = x.shape
         plan = module.plan_for(n, dims)
         xc = x.detach().float().contiguous().view(n, *dims, 1)
-        logits = plan.forward(module._tensors(), xc, 0, n)
+        logits = plan.forward(module._tensors(), xc, 0, n, training=module.training)
         ctx.plan, ctx.module, ctx.xc, ctx.needs_x = plan, module, xc, x.requires_grad
         return logits.clone().view(n, 1, *logits.shape[1:4])
 
@@ -102,9 +103,12 @@ class _CriticFn(torch.autograd.Function):
         n = xc.shape[0]
         plan.dz[-1].view(-1).copy_(grad_out.reshape(-1))
         dx = torch.empty_like(xc) if ctx.needs_x else None
-        plan.input_grad(module._tensors(), 0, n, dx if dx is not None else xc, 0, n if dx is not None else 0)
         names = [nm for nm, _ in module.named_parameters()]
         grads = {nm: torch.zeros_like(p) for nm, p in module.named_parameters()}
+        if plan.bn and not module.training:
+            raise NotImplementedError("backward through the eval-mode BatchNorm critic")
+        plan.input_grad(module._tensors(), 0, n, dx if dx is not None else xc, 0, n if dx is not None else 0,
+                        G=grads)
         plan.weight_grads(module._tensors(), grads, xc, n, n)
         dxo = dx.view(n, 1, *xc.shape[1:4]) if dx is not None else None
         return (dxo, None, *[grads[nm] for nm in names])

@@ -302,7 +302,8 @@ def bn_backward_ws_floats(nvox, c) -> int:
     return int(L.load().cgan3d_bn_backward_ws_floats(nvox, c))
 
 
-def bn_backward(dy, z, nvox, c, scale_shift, mean_invstd, gamma, act, dgamma, dbeta, dz, ws, slope=0.0):
+def bn_backward(dy, z, nvox, c, scale_shift, mean_invstd, gamma, act, dgamma, dbeta, dz, ws, slope=0.0,
+                accumulate=False):
     for t, nm in ((dy, "dy"), (z, "z"), (dz, "dz")):
         _need(t, nvox * c, f"bn_backward {nm}")
     for t, nm in ((scale_shift, "scale_shift"), (mean_invstd, "mean_invstd")):
@@ -311,7 +312,7 @@ def bn_backward(dy, z, nvox, c, scale_shift, mean_invstd, gamma, act, dgamma, db
         _need(t, c, f"bn_backward {nm}")
     _need(ws, bn_backward_ws_floats(nvox, c), "bn_backward ws", exact=False)
     check(_launch("cgan3d_bn_backward", ptr(dy), ptr(z), nvox, c, ptr(scale_shift), ptr(mean_invstd), ptr(gamma),
-                  act, slope, ptr(dgamma), ptr(dbeta), ptr(dz), ptr(ws)), "bn_backward")
+                  act, slope, ptr(dgamma), ptr(dbeta), ptr(dz), int(accumulate), ptr(ws)), "bn_backward")
 
 
 def channel_sum_ws_floats(nvox, c) -> int:

@@ -63,9 +63,6 @@ class Trainer:
         self.log_every, self.log_images_every = log_every, log_images_every
         self.hu_loss_w, self.sim_loss_w, self.gan_loss_w = hu_loss_weight, sim_loss_weight, gan_loss_weight
         self.gp_w, self.weight_clip = gp_weight, weight_clip
-        if weight_clip is not None:
-            raise NotImplementedError("weight-clipping WGAN (BatchNorm critic) is SURVEY.md §8f row 4; "
-                                      "the HIP step implements the gradient-penalty configuration")
 
         self.generator: nn.Module = generator_class().to(self.device)
         g_h = adam_hyper_from_partial(generator_optim_class)
@@ -74,7 +71,8 @@ class Trainer:
 
         self.critic: nn.Module = critic_class().to(self.device)
         d_h = adam_hyper_from_partial(critic_optim_class)
-        self.optimizer_D = FusedAdam(Arena(self.critic, self.device), **d_h)
+        # weight clipping (Trainer.py:136-138) is applied by the critic's Adam kernel after the update
+        self.optimizer_D = FusedAdam(Arena(self.critic, self.device), **d_h, weight_clip=weight_clip)
         self.lr_scheduler_D = critic_lr_scheduler_class(self.optimizer_D) if critic_lr_scheduler_class else None
 
         self.loss_GAN = WassersteinLoss()
@@ -100,7 +98,7 @@ class Trainer:
                                      b_sub, tuple(dims), gp_weight=float(self.gp_w), hu_bounds=(lo, hi),
                                      gan_w=self.gan_loss_w, sim_w=self.sim_loss_w, hu_w=self.hu_loss_w,
                                      device=self.device, g_optim=self.optimizer_G, d_optim=self.optimizer_D,
-                                     precision=self.precision)
+                                     precision=self.precision, weight_clip=self.weight_clip)
         return self.engine
 
     def _losses(self, keys) -> Dict[str, Tensor]:

@@ -145,7 +145,7 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const float* __restr
 __global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(const float* __restrict__ part, int nblk, int C,
                                                               long long nvox, const float* __restrict__ gamma,
                                                               const float* __restrict__ mi, float* dgamma,
-                                                              float* dbeta, float* coef) {
+                                                              float* dbeta, float* coef, int accumulate) {
   __shared__ double red[2][4];
   const int c = blockIdx.x, tid = threadIdx.x;
   double s0 = 0.0, s1 = 0.0;
@@ -160,8 +160,8 @@ __global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(const float* __res
   if (tid == 0) {
     s0 = red[0][0] + red[0][1] + red[0][2] + red[0][3];
     s1 = red[1][0] + red[1][1] + red[1][2] + red[1][3];
-    if (dbeta) dbeta[c] = (float)s0;
-    if (dgamma) dgamma[c] = (float)s1;
+    if (dbeta) dbeta[c] = accumulate ? dbeta[c] + (float)s0 : (float)s0;
+    if (dgamma) dgamma[c] = accumulate ? dgamma[c] + (float)s1 : (float)s1;
     coef[c] = gamma[c] * mi[C + c];
     coef[C + c] = (float)(s0 / (double)nvox);
     coef[2 * C + c] = (float)(s1 / (double)nvox);
@@ -267,7 +267,7 @@ extern "C" int64_t cgan3d_bn_backward_ws_floats(int64_t nvox, int32_t c) {
 
 extern "C" int cgan3d_bn_backward(const float* dy, const float* z, int64_t nvox, int32_t c, const float* scale_shift,
                                   const float* mean_invstd, const float* gamma, int32_t act, float slope, float* dgamma,
-                                  float* dbeta, float* dz, float* ws, void* stream) {
+                                  float* dbeta, float* dz, int32_t accumulate, float* ws, void* stream) {
   CG_CHECK_ARG(dy && z && scale_shift && mean_invstd && gamma && dz && ws, "cgan3d_bn_backward: null pointer");
   CG_CHECK_ARG(nvox > 1 && c >= 4 && c <= 256 && 256 % c == 0,
                "cgan3d_bn_backward: channels must divide 256 and be >= 4");
@@ -280,7 +280,7 @@ extern "C" int cgan3d_bn_backward(const float* dy, const float* z, int64_t nvox,
                      act, slope, part);
   CG_LAUNCH_CHECK("bn_bwd_reduce_kernel");
   hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(c), dim3(256), 0, s, part, nblk, c, (long long)nvox, gamma,
-                     mean_invstd, dgamma, dbeta, coef);
+                     mean_invstd, dgamma, dbeta, coef, accumulate);
   CG_LAUNCH_CHECK("bn_bwd_finalize_kernel");
   int blocks = (int)std::min<long long>((n4 + 255) / 256, 4096);
   hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(blocks), dim3(256), 0, s, dy, z, n4, c, scale_shift, mean_invstd,

@@ -125,10 +125,12 @@ int cgan3d_bn_finalize(const float* stats, int64_t nblk, int32_t c, const float*
 int cgan3d_bn_apply(const float* z, int64_t nvox, int32_t c, const float* scale_shift,
                     int32_t act, float slope, const float* residual, float* y, void* stream);
 int64_t cgan3d_bn_backward_ws_floats(int64_t nvox, int32_t c);
+/* accumulate != 0: dgamma/dbeta += this batch's gradients (a module called on several batches in
+ * one step, e.g. the BatchNorm critic on the real and the fake batch, Trainer.py:119-121). */
 int cgan3d_bn_backward(const float* dy, const float* z, int64_t nvox, int32_t c,
                        const float* scale_shift, const float* mean_invstd, const float* gamma,
                        int32_t act, float slope, float* dgamma, float* dbeta, float* dz,
-                       float* ws, void* stream);
+                       int32_t accumulate, float* ws, void* stream);
 
 /* --- reductions / elementwise --- */
 int64_t cgan3d_channel_sum_ws_floats(int64_t nvox, int32_t c);

@@ -16,31 +16,35 @@ pytestmark = pytest.mark.gpu
 D_ARGS = dict(channels_in=1, init_channels_out=8, discriminator_depth=3, negative_slope=0.2)
 
 
-def _models(g_args):
+def _models(g_args, critic_bn=False):
     from torch import nn
     from cgan3d_amd.model.discriminator import PatchGANDiscriminator
     from cgan3d_amd.model.generator import ResnetGenerator
     from cgan3d_amd.model.init import pcg64_init_
     g = pcg64_init_(ResnetGenerator(**g_args), 0).cuda()
-    d = pcg64_init_(PatchGANDiscriminator(**D_ARGS, norm_layer=nn.Identity), 1).cuda()
+    norm = {} if critic_bn else dict(norm_layer=nn.Identity)  # BatchNorm critic: basic_conf.py:60-66
+    d = pcg64_init_(PatchGANDiscriminator(**D_ARGS, **norm), 1).cuda()
     return g, d
 
 
-def _engine(g, d, b, S, lr, b1, b2):
+def _engine(g, d, b, S, lr, b1, b2, weight_clip=None):
     from cgan3d_amd.engine import StepEngine
     return StepEngine(g, d, g.config, d.config, b, b, (S, S, S), g_hyper=(lr, b1, b2, 1e-8),
-                      d_hyper=(lr, b1, b2, 1e-8))
+                      d_hyper=(lr, b1, b2, 1e-8), weight_clip=weight_clip)
 
 
-@pytest.mark.parametrize("tag", ["gp_small", "gp_full"])
+@pytest.mark.parametrize("tag", ["gp_small", "gp_full", "clip_small"])
 def test_step_matches_reference_fixture(golden, tag):
+    """Trainer.train_step of the reference (GP conf; weight-clip conf with the BatchNorm critic)
+    against the device step: losses, every gradient, final parameters and BN buffers."""
     f = golden(f"step_{tag}")
     meta = ast.literal_eval(str(f["meta"]))
     g_args = dict(n_resnet_blocks=meta["g_n_resnet_blocks"], n_updownsample_blocks=meta["g_n_updownsample_blocks"],
                   init_channels_out=meta["g_init_channels_out"])
     S, b = meta["S"], meta["b_opt"]
-    g, d = _models(g_args)
-    eng = _engine(g, d, b, S, meta["lr"], meta["beta1"], meta["beta2"])
+    gp = bool(meta["gp"])
+    g, d = _models(g_args, critic_bn=not gp)
+    eng = _engine(g, d, b, S, meta["lr"], meta["beta1"], meta["beta2"], weight_clip=None if gp else 0.01)
     names = {"L_D": 0, "D": 0, "G": 3, "sim": 4, "HU": 5, "G-full": 6}
     for it in range(meta["iters"]):
         sub = np.concatenate([f[f"it{it}/low"], f[f"it{it}/high"]])
@@ -93,6 +97,15 @@ def test_critic_forward_matches_reference(golden):
     with torch.no_grad():
         y = d(torch.from_numpy(f["x"]).cuda())
     assert_close(y.cpu().numpy(), f["gp/y"], 1e-3, "D(x)")
+    # BatchNorm critic (basic_conf.py:60-66), train mode: batch statistics and running buffers
+    d = pcg64_init_(PatchGANDiscriminator(**D_ARGS), 1).cuda().train()
+    with torch.no_grad():
+        y = d(torch.from_numpy(f["x"]).cuda())
+    assert_close(y.cpu().numpy(), f["bn/y"], 1e-3, "D_bn(x)")
+    sd = d.state_dict()
+    for k in f:
+        if k.startswith("bn/sd/"):
+            assert_close(sd[k[6:]].cpu().numpy(), f[k], 1e-3, k)
 
 
 @pytest.mark.parametrize("S,b", [(64, 2)])

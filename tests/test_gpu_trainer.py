@@ -31,7 +31,7 @@ class _LoggerInterface:
         pass
 
 
-def _trainer(ckpt_dir, precision="f32"):
+def _trainer(ckpt_dir, precision="f32", clip=False):
     from cgan3d_amd.model.discriminator import PatchGANDiscriminator
     from cgan3d_amd.model.generator import ResnetGenerator
     from cgan3d_amd.model.loss import HULoss
@@ -41,11 +41,11 @@ def _trainer(ckpt_dir, precision="f32"):
         3, 1, 2, 1, 1, 1, 1000,
         partial(ResnetGenerator, 2, 2, 8),
         partial(PatchGANDiscriminator, channels_in=1, init_channels_out=8, discriminator_depth=3,
-                negative_slope=0.2, norm_layer=nn.Identity),
+                negative_slope=0.2, **({} if clip else dict(norm_layer=nn.Identity))),
         partial(torch.optim.Adam, lr=1e-4, betas=(0.0, 0.9)),
         partial(torch.optim.Adam, lr=1e-4, betas=(0.0, 0.9)),
         HULoss(-0.2, 0.6), _LoggerInterface(), torch.device("cuda"),
-        checkpoint_dir=ckpt_dir, checkpoint_every=2, precision=precision)
+        checkpoint_dir=ckpt_dir, checkpoint_every=2, precision=precision, weight_clip=0.01 if clip else None)
 
 
 def _patches(rng, b=2, S=32):
@@ -57,10 +57,10 @@ def _patches(rng, b=2, S=32):
     return [one(2 * b), one(b), one(b)]
 
 
-@pytest.mark.parametrize("precision", ["f32", "bf16"])
-def test_trainer_step_validate_checkpoint(tmp_path, precision):
+@pytest.mark.parametrize("precision,clip", [("f32", False), ("bf16", False), ("f32", True), ("bf16", True)])
+def test_trainer_step_validate_checkpoint(tmp_path, precision, clip):
     rng = np.random.default_rng(0)
-    tr = _trainer(tmp_path, precision)
+    tr = _trainer(tmp_path, precision, clip)
     for it in range(2):
         log = tr.train_step(_patches(rng), it)
         assert set(log) == {"D", "G", "G-full", "sim", "HU"}
@@ -75,7 +75,9 @@ def test_trainer_step_validate_checkpoint(tmp_path, precision):
     opt_g = tr.optimizer_G.state_dict()
     ck = torch.load(tmp_path / "2.pt", map_location="cpu", weights_only=True)
     assert {"generator", "critic", "optimizer_G", "optimizer_D", "iteration"} <= set(ck)
-    tr2 = _trainer(tmp_path, precision)  # resumes from the latest checkpoint in the directory
+    if clip:  # WGAN weight clipping (Trainer.py:136-138) holds after the critic update
+        assert max(float(p.detach().abs().max()) for p in tr.critic.parameters()) <= 0.01 + 1e-7
+    tr2 = _trainer(tmp_path, precision, clip)  # resumes from the latest checkpoint in the directory
     for k, t in tr2.generator.state_dict().items():
         assert torch.equal(t.cpu(), sd_g[k]), k
     for k, t in tr2.critic.state_dict().items():

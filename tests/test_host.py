@@ -38,23 +38,25 @@ def test_state_dict_layout_matches_reference():
     assert sum(p.numel() for p in d.parameters()) == 176_761
 
 
-@pytest.mark.parametrize("g_args,S,b", [
-    (dict(n_resnet_blocks=1, n_updownsample_blocks=2, init_channels_out=8), 32, 1),
-    (dict(n_resnet_blocks=4, n_updownsample_blocks=2, init_channels_out=16), 64, 4),
-    (dict(n_resnet_blocks=4, n_updownsample_blocks=2, init_channels_out=16), 32, 2),
+@pytest.mark.parametrize("g_args,S,b,clip", [
+    (dict(n_resnet_blocks=1, n_updownsample_blocks=2, init_channels_out=8), 32, 1, False),
+    (dict(n_resnet_blocks=4, n_updownsample_blocks=2, init_channels_out=16), 64, 4, False),
+    (dict(n_resnet_blocks=4, n_updownsample_blocks=2, init_channels_out=16), 32, 2, False),
+    (dict(n_resnet_blocks=4, n_updownsample_blocks=2, init_channels_out=16), 64, 4, True),  # BN critic, clip
 ])
-def test_engine_step_dry_run_shapes(g_args, S, b):
+def test_engine_step_dry_run_shapes(g_args, S, b, clip):
     """Every launch of a full step gets operands whose extents match the kernel's footprint."""
     from cgan3d_amd import ops
     from cgan3d_amd.engine import StepEngine
     from cgan3d_amd.model.discriminator import PatchGANDiscriminator
     from cgan3d_amd.model.generator import ResnetGenerator
     g = ResnetGenerator(**g_args)
-    d = PatchGANDiscriminator(**D_ARGS, norm_layer=nn.Identity)
+    d = PatchGANDiscriminator(**D_ARGS, **({} if clip else dict(norm_layer=nn.Identity)))
     ops.DRY_RUN = True
     try:
         eng = StepEngine(g, d, g.config, d.config, b, b, (S, S, S), g_hyper=(1e-4, 0.0, 0.9, 1e-8),
-                         d_hyper=(1e-4, 0.0, 0.9, 1e-8), device=torch.device("cpu"))
+                         d_hyper=(1e-4, 0.0, 0.9, 1e-8), device=torch.device("cpu"),
+                         weight_clip=0.01 if clip else None)
         eng.step()
     finally:
         ops.DRY_RUN = False
