@@ -1,0 +1,196 @@
+"""Pinned-host -> HBM patch loader: drop-in for the reference's 3-D training loaders.
+
+Replaces ``CCTADataLoader`` + the batchgenerators augmenter wrapped around it
+(``contrast_gan_3D/data/CCTADataLoader.py:14-108``, built by ``trainer/utils.py:44-107``):
+``next(loader)`` returns the reference's batch dict ``{"data", "seg", "name", "path"}`` with
+``data`` a float32 [B,1,W,H,D] patch batch and ``seg`` the boolean centre-line mask, already in
+HBM.
+
+Per batch:
+* host worker threads copy each sample's crop straight out of the memory-mapped
+  ``<patient>.npy`` volume (4-D ``[W,H,D,(HU,label)]``, ``data/utils.py:34-54``) into a pinned
+  staging slot.  The crop follows ``generate_one`` (``CCTADataLoader.py:88-104``): dims smaller
+  than the patch are zero-padded symmetrically (batchgenerators ``pad_nd_image``:
+  below = diff // 2, above = the rest), the others are cropped at a uniformly random offset
+  (``crop(..., crop_type="random")``), drawn here from the loader's ``numpy.random.Generator``;
+* one asynchronous host-to-device copy per batch runs on the loader's own HIP stream, followed
+  by ``cgan3d_unpack_patches``, which de-interleaves and scales on the GPU
+  ((HU - shift) / factor, ``FactorZeroCenterScaler``, ``data/Scaler.py:37-45``);
+* ``depth`` batches are in flight: while the trainer computes on batch j, batch j+1 is being
+  read on the host and copied over PCIe.  A returned batch's tensors live in a ring slot and are
+  overwritten ``depth`` batches later (the Trainer consumes each batch within its step).
+
+Spatial augmentation (``SpatialTransform_2``: elastic deformation, scaling, rotation with
+per-sample probabilities, ``basic_conf.py:88-106``) is not applied.
+"""
+from __future__ import annotations
+
+import threading
+from concurrent.futures import ThreadPoolExecutor
+from pathlib import Path
+from typing import List, Optional, Sequence, Tuple
+
+import numpy as np
+import torch
+
+from .. import ops
+
+
+def _scaler_params(scaler) -> Tuple[float, float]:
+    """(shift, factor) of the reference's scalers: FactorZeroCenterScaler (shift, factor),
+    ZeroCenterScaler (shift), or the identity default of CCTADataLoader (``lambda x: x``)."""
+    if scaler is None:
+        return 0.0, 1.0
+    shift = getattr(scaler, "shift", None)
+    if shift is not None:
+        return float(shift), float(getattr(scaler, "factor", 1))
+    probe = np.array([-1000.0, 0.0, 1234.0], dtype=np.float32)
+    if np.array_equal(np.asarray(scaler(probe), dtype=np.float32), probe):
+        return 0.0, 1.0
+    raise TypeError("PatchLoader: scaler must be a (Factor)ZeroCenterScaler or the identity")
+
+
+def crop_box(shape: Sequence[int], patch: Sequence[int], rng: np.random.Generator):
+    """Per-dim (src_lo, dst_lo, length) of CCTADataLoader.generate_one's pad-then-random-crop."""
+    box = []
+    for s, p in zip(shape, patch):
+        if s < p:  # pad_nd_image: centred zero padding; the padded dim equals the patch (offset 0)
+            box.append((0, (p - s) // 2, s))
+        else:
+            lo = int(rng.integers(0, s - p + 1))
+            box.append((lo, 0, p))
+    return box
+
+
+def read_crop(vol: np.ndarray, patch: Sequence[int], box, out: np.ndarray):
+    """out[W,H,D,2] = zero-padded crop of vol[W,H,D,2] described by ``box``."""
+    (sx, dx, lx), (sy, dy, ly), (sz, dz, lz) = box
+    if (dx, dy, dz) != (0, 0, 0) or (lx, ly, lz) != tuple(patch):
+        out.fill(0)
+    out[dx:dx + lx, dy:dy + ly, dz:dz + lz] = vol[sx:sx + lx, sy:sy + ly, sz:sz + lz]
+
+
+class PatchLoader:
+    def __init__(self, data: List[str], patch_shape: Sequence[int], batch_size: int, rng: np.random.Generator,
+                 scaler=None, infinite: bool = True, shuffle: bool = True, device=None, depth: int = 3,
+                 num_threads: int = 4, seed_for_shuffle: Optional[int] = None):
+        if len(patch_shape) != 3:
+            raise NotImplementedError("PatchLoader: 3-D patches (the 2-D slice sampler is SURVEY.md §8f row 4)")
+        self.paths = [str(p) for p in data]
+        self.patch = tuple(int(p) for p in patch_shape)
+        self.batch_size, self.rng, self.infinite, self.shuffle = batch_size, rng, infinite, shuffle
+        self.shift, self.factor = _scaler_params(scaler)
+        self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+        self.depth = max(2, depth)
+        self._vols = {}
+        probe = self._volume(self.paths[0])
+        if probe.ndim != 4 or probe.shape[-1] != 2:
+            raise ValueError(f"PatchLoader: expected [W,H,D,2] volumes, got {probe.shape}")
+        # int16 scans travel as int16 (half the PCIe bytes); any other dtype is staged as float32,
+        # which is what generate_one casts to before cropping
+        self.dtype = torch.int16 if probe.dtype == np.int16 else torch.float32
+        shp = (batch_size, *self.patch, 2)
+        self._host = [torch.empty(shp, dtype=self.dtype).pin_memory() for _ in range(self.depth)]
+        self._raw = [torch.empty(shp, dtype=self.dtype, device=self.device) for _ in range(self.depth)]
+        self._data = [torch.empty((batch_size, 1, *self.patch), device=self.device) for _ in range(self.depth)]
+        self._seg = [torch.empty((batch_size, 1, *self.patch), dtype=torch.bool, device=self.device)
+                     for _ in range(self.depth)]
+        self._copied = [None] * self.depth  # HIP event: slot's H2D copy finished (host slot reusable)
+        self._stream = torch.cuda.Stream(device=self.device)
+        self._threads, self._pool = num_threads, None
+        self._lock = threading.Lock()
+        self._order_rng = np.random.default_rng(seed_for_shuffle)
+        self._order, self._pos = [], 0
+        self._pending, self._next_slot = {}, 0
+        self.restart()
+
+    # -- host side -----------------------------------------------------------------------------
+    def _volume(self, path: str) -> np.ndarray:
+        v = self._vols.get(path)
+        if v is None:
+            v = np.load(path + ".npy", mmap_mode="r")
+            if getattr(self, "dtype", None) is torch.int16 and v.dtype != np.int16:
+                raise TypeError(f"PatchLoader: {path}.npy is {v.dtype}, the other scans int16")
+            self._vols[path] = v
+        return v
+
+    def _indices(self) -> Optional[List[int]]:
+        with self._lock:
+            idx = []
+            for _ in range(self.batch_size):
+                if self._pos >= len(self._order):
+                    if not self.infinite and self._order:
+                        return None
+                    self._order = list(range(len(self.paths)))
+                    if self.shuffle:
+                        self._order_rng.shuffle(self._order)
+                    self._pos = 0
+                idx.append(self._order[self._pos])
+                self._pos += 1
+            boxes = [crop_box(self._volume(self.paths[i]).shape[:3], self.patch, self.rng) for i in idx]
+            return list(zip(idx, boxes))
+
+    def _fill(self, slot: int, picks):
+        ev = self._copied[slot]
+        if ev is not None:
+            ev.synchronize()  # the previous H2D copy out of this pinned slot has finished
+        host = self._host[slot].numpy()
+        for b, (i, box) in enumerate(picks):
+            read_crop(self._volume(self.paths[i]), self.patch, box, host[b])
+        return picks
+
+    def _submit(self):
+        picks = self._indices()
+        if picks is None:
+            return False
+        slot = self._next_slot
+        self._next_slot = (slot + 1) % self.depth
+        self._pending[slot] = self._pool.submit(self._fill, slot, picks)
+        return True
+
+    def restart(self):
+        """Re-prime the pipeline (the Trainer calls this at the start of fit, Trainer.py:241-250)."""
+        for f in self._pending.values():
+            f.result()
+        if self._pool is None:
+            self._pool = ThreadPoolExecutor(max_workers=self._threads)
+        self._pending, self._next_slot, self._pos, self._order = {}, 0, 0, []
+        self._consume = 0
+        for _ in range(self.depth - 1):
+            if not self._submit():
+                break
+
+    def _finish(self):
+        """Stop the host workers (Trainer end of fit); a later restart() starts them again."""
+        if self._pool is not None:
+            self._pool.shutdown(wait=True)
+            self._pool, self._pending = None, {}
+
+    # -- device side ---------------------------------------------------------------------------
+    def __iter__(self):
+        return self
+
+    def __next__(self) -> dict:
+        self._submit()  # keep depth - 1 batches ahead
+        slot = self._consume
+        fut = self._pending.pop(slot, None)
+        if fut is None:
+            raise StopIteration
+        picks = fut.result()
+        self._consume = (slot + 1) % self.depth
+        cur = torch.cuda.current_stream(self.device)
+        # work enqueued so far (the consumers of the batch that last used this slot) precedes the copy
+        self._stream.wait_stream(cur)
+        with torch.cuda.stream(self._stream):
+            self._raw[slot].copy_(self._host[slot], non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record(self._stream)
+            self._copied[slot] = ev
+            ops.unpack_patches(self._raw[slot], self._data[slot], self._seg[slot], self.shift, self.factor)
+        cur.wait_stream(self._stream)
+        names = [Path(self.paths[i]).name for i, _ in picks]
+        return {"data": self._data[slot], "seg": self._seg[slot], "name": names,
+                "path": [self.paths[i] for i, _ in picks]}
+
+    def __len__(self):
+        return len(self.paths)

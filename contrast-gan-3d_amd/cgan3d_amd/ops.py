@@ -400,3 +400,18 @@ def adam(param, grad, exp_avg, exp_avg_sq, hyper):
     _need(hyper, 6, "adam hyper")
     check(_launch("cgan3d_adam", ptr(param), ptr(grad), ptr(exp_avg), ptr(exp_avg_sq), param.numel(), ptr(hyper)),
           "adam")
+
+
+def unpack_patches(src: torch.Tensor, data: torch.Tensor, seg: torch.Tensor, shift: float, factor: float):
+    """src: device [..., 2] (HU, label) int16 or float32 -> data (float32) and seg (bool/uint8)."""
+    if src.dtype not in (torch.int16, torch.float32):
+        raise TypeError(f"unpack_patches: src dtype {src.dtype} (int16 or float32)")
+    if not src.is_contiguous() or src.shape[-1] != 2:
+        raise ValueError("unpack_patches: src must be contiguous [..., 2]")
+    nvox = src.numel() // 2
+    _need(data, nvox, "unpack_patches data")
+    _need(seg, nvox, "unpack_patches seg", dtype=seg.dtype)
+    if seg.dtype not in (torch.bool, torch.uint8):
+        raise TypeError("unpack_patches: seg must be bool or uint8")
+    check(_launch("cgan3d_unpack_patches", ptr(src), 0 if src.dtype == torch.int16 else 1, nvox, float(shift),
+                  float(factor), ptr(data), ptr(seg)), "unpack_patches")

@@ -1,0 +1,44 @@
+"""Loader factory with the signature of the reference's ``create_dataloaders``
+(``contrast_gan_3D/trainer/utils.py:44-107``), building one :class:`PatchLoader` per scan label
+instead of a batchgenerators augmenter around a ``CCTADataLoader``."""
+from __future__ import annotations
+
+import warnings
+from collections import defaultdict
+from pathlib import Path
+from typing import Dict, List, Optional, Tuple, Union
+
+import numpy as np
+
+from ..data.loader import PatchLoader
+
+DEFAULT_SEED = 42  # contrast_gan_3D/constants.py
+
+
+def divide_scans_in_fold(fold) -> Dict[int, List[Union[str, Path]]]:
+    """[(path, label), ...] -> {label: [path, ...]} (trainer/utils.py:36-40)."""
+    ret = defaultdict(list)
+    for path, label in fold:
+        ret[label].append(path)
+    return ret
+
+
+def create_dataloaders(train_fold, val_fold, train_patch_size, val_patch_size, train_batch_sizes: Dict[int, int],
+                       val_batch_sizes: Dict[int, int], rng: np.random.Generator, scaler=None,
+                       num_workers: Tuple[int, int] = (1, 1), train_transform: Optional[callable] = None,
+                       seed: int = DEFAULT_SEED, augmenter_class=None, device=None):
+    """Returns ({label: PatchLoader} for training, {label: PatchLoader} for validation).
+
+    ``augmenter_class`` is accepted for signature compatibility and ignored (the loader is its
+    own prefetching pipeline).  ``train_transform`` (SpatialTransform_2) is not applied yet: a
+    warning says so."""
+    if train_transform is not None:
+        warnings.warn("create_dataloaders: spatial augmentation (train_transform) is not applied by PatchLoader")
+
+    def build(fold, patch, sizes, workers):
+        return {label: PatchLoader(paths, patch, sizes[label], rng, scaler=scaler, shuffle=True, device=device,
+                                   num_threads=max(1, workers), seed_for_shuffle=seed)
+                for label, paths in divide_scans_in_fold(fold).items()}
+
+    return (build(train_fold, train_patch_size, train_batch_sizes, num_workers[0]),
+            build(val_fold, val_patch_size, val_batch_sizes, num_workers[1]))

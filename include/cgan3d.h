@@ -143,6 +143,12 @@ int cgan3d_gp_interpolate(const float* real, const float* fake, const float* eps
 
 int cgan3d_tanh_backward(const float* y, const float* dy, float* dz, int64_t n, void* stream);
 
+/* --- patch loader (data/CCTADataLoader.py:88-104, data/Scaler.py:37-45): src = nvox interleaved
+ *     (HU, label) pairs (src_dtype 0: int16, 1: float32), data = (HU - shift) / factor,
+ *     seg = label != 0 --- */
+int cgan3d_unpack_patches(const void* src, int32_t src_dtype, int64_t nvox, float shift, float factor,
+                          float* data, uint8_t* seg, void* stream);
+
 /* --- losses (model/loss.py:11-80, model/utils.py:12-41, Trainer.py:119-154) ---
  * losses[] slots: 0 D total, 1 W_D, 2 GP, 3 G (adversarial), 4 sim (ZNCC), 5 HU, 6 G-full. */
 int64_t cgan3d_loss_ws_floats(int64_t n);

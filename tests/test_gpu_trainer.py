@@ -89,3 +89,31 @@ def test_trainer_step_validate_checkpoint(tmp_path, precision, clip):
     # and keeps training from there
     log = tr2.train_step(_patches(rng), 2)
     assert all(np.isfinite(float(x)) for x in log.values())
+
+
+def test_fit_with_patch_loaders(tmp_path):
+    """Trainer.fit fed by create_dataloaders' PatchLoaders over int16 [W,H,D,2] scans on disk."""
+    from cgan3d_amd.trainer.utils import create_dataloaders
+    rng = np.random.default_rng(0)
+    fold = []
+    for i, label in enumerate([0, 0, -1, 1, 1]):
+        shape = (40, 36, 34) if i != 3 else (28, 40, 40)  # one scan smaller than the patch
+        hu = rng.integers(-1000, 1500, shape).astype(np.int16)
+        seg = (rng.random(shape) < 0.05).astype(np.int16)
+        p = tmp_path / f"scan{i}"
+        np.save(str(p) + ".npy", np.stack([hu, seg], -1))
+        fold.append((str(p), label))
+
+    class FZC:
+        shift, factor = 238, 600
+
+    sizes = {0: 4, -1: 2, 1: 2}
+    train, val = create_dataloaders(fold, fold, (32,) * 3, (32,) * 3, sizes, sizes, rng, scaler=FZC())
+    (tmp_path / "ck").mkdir()
+    tr = _trainer(tmp_path / "ck")
+    tr.logger_interface.logger.losses.clear()
+    tr.fit(train, val)
+    modes = [m for m, _, _ in tr.logger_interface.logger.losses]
+    assert "validation" in modes
+    assert all(np.isfinite(v) for _, _, d in tr.logger_interface.logger.losses for v in d.values())
+    assert (tmp_path / "ck" / "3.pt").exists()

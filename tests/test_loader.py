@@ -1,0 +1,112 @@
+"""Patch loader (cgan3d_amd/data/loader.py) against a numpy restatement of the reference's
+CCTADataLoader.generate_one (contrast_gan_3D/data/CCTADataLoader.py:88-104): pad_nd_image
+(zero padding, below = diff // 2) then a random crop, FactorZeroCenterScaler
+((HU - shift) / factor in float32, data/Scaler.py:37-45) and the bool mask (trainer/utils.py:100).
+
+CPU: the crop geometry and the host copy.  GPU: whole batches through the pinned ring, the H2D
+copy and the unpack kernel, bit-exact against numpy.
+"""
+import numpy as np
+import pytest
+
+from cgan3d_amd.data.loader import _scaler_params, crop_box, read_crop
+
+
+def _oracle_patch(vol, patch, box):
+    """pad_nd_image + crop at the box's offsets, numpy."""
+    pads = [(max(p - s, 0) // 2, max(p - s, 0) - max(p - s, 0) // 2) for s, p in zip(vol.shape[:3], patch)]
+    padded = np.pad(vol, pads + [(0, 0)])
+    lo = [b[0] if s >= p else 0 for b, s, p in zip(box, vol.shape[:3], patch)]
+    return padded[lo[0]:lo[0] + patch[0], lo[1]:lo[1] + patch[1], lo[2]:lo[2] + patch[2]]
+
+
+SHAPES = [(24, 24, 24), (16, 16, 16), (12, 20, 31), (5, 16, 40), (40, 9, 3)]
+
+
+@pytest.mark.parametrize("shape", SHAPES)
+def test_crop_matches_pad_then_crop(shape):
+    rng = np.random.default_rng(0)
+    patch = (16, 16, 16)
+    vol = rng.integers(-1024, 3000, size=(*shape, 2)).astype(np.int16)
+    out = np.full((*patch, 2), 77, dtype=np.int16)
+    for _ in range(20):
+        box = crop_box(shape, patch, rng)
+        read_crop(vol, patch, box, out)
+        np.testing.assert_array_equal(out, _oracle_patch(vol, patch, box))
+
+
+def test_crop_offsets_cover_range():
+    rng = np.random.default_rng(1)
+    seen = {crop_box((20, 16, 8), (16, 16, 16), rng)[0][0] for _ in range(400)}
+    assert seen == set(range(5))  # randint(0, S - P + 1): both extremes reachable
+    assert crop_box((20, 16, 8), (16, 16, 16), rng)[1:] == [(0, 0, 16), (0, 4, 8)]
+
+
+def test_scaler_params():
+    class FZC:  # FactorZeroCenterScaler(low=-260, high=736, factor=600): shift = 238
+        shift, factor = 238, 600
+
+    class ZC:
+        shift = 10
+
+    assert _scaler_params(FZC()) == (238.0, 600.0)
+    assert _scaler_params(ZC()) == (10.0, 1.0)
+    assert _scaler_params(None) == (0.0, 1.0)
+    assert _scaler_params(lambda x: x) == (0.0, 1.0)
+    with pytest.raises(TypeError):
+        _scaler_params(lambda x: 2 * x)
+
+
+def _coord_volume(shape):
+    """HU encodes the voxel's coordinates (so a patch reveals where it was cut); label 1 on a
+    lattice of voxels."""
+    x, y, z = np.meshgrid(*[np.arange(s) for s in shape], indexing="ij")
+    hu = (x * shape[1] * shape[2] + y * shape[2] + z - 2000).astype(np.int16)
+    lab = ((x + 2 * y + z) % 3 == 0).astype(np.int16)
+    return np.stack([hu, lab], -1)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("src_dtype", [np.int16, np.float32])
+def test_loader_batches_bit_exact(tmp_path, src_dtype):
+    import torch
+    from cgan3d_amd.data.loader import PatchLoader
+
+    patch = (16, 16, 16)
+    shapes = [(24, 20, 18), (12, 16, 30), (16, 16, 16)]
+    paths, vols = [], {}
+    for i, s in enumerate(shapes):
+        v = _coord_volume(s).astype(src_dtype)
+        p = str(tmp_path / f"patient{i}")
+        np.save(p + ".npy", v)
+        paths.append(p)
+        vols[p] = v
+
+    class FZC:
+        shift, factor = 238, 600
+
+    loader = PatchLoader(paths, patch, batch_size=2, rng=np.random.default_rng(3), scaler=FZC(), depth=3,
+                         num_threads=2, seed_for_shuffle=5)
+    seen = set()
+    for _ in range(7):
+        b = next(loader)
+        data, seg = b["data"], b["seg"]
+        assert data.shape == (2, 1, *patch) and data.dtype == torch.float32 and data.is_cuda
+        assert seg.shape == (2, 1, *patch) and seg.dtype == torch.bool
+        data, seg = data.cpu().numpy(), seg.cpu().numpy()
+        for j, p in enumerate(b["path"]):
+            seen.add(p)
+            assert b["name"][j] == p.rsplit("/", 1)[-1]
+            vol = vols[p]
+            # recover the crop origin from the coordinate encoding of the first unpadded voxel
+            box = [(0, (P - s) // 2, s) if s < P else None for s, P in zip(vol.shape[:3], patch)]
+            first = tuple(bx[1] if bx else 0 for bx in box)
+            hu0 = int(round(float(data[j, 0][first]) * 600 + 238)) + 2000
+            org = np.unravel_index(hu0, vol.shape[:3])
+            box = [bx if bx else (int(o), 0, P) for bx, o, P in zip(box, org, patch)]
+            ref = _oracle_patch(vol, patch, box).astype(np.float32)
+            want = (ref[..., 0] - np.float32(238)) / np.float32(600)
+            np.testing.assert_array_equal(data[j, 0], want)
+            np.testing.assert_array_equal(seg[j, 0], ref[..., 1] != 0)
+    assert seen == set(paths)
+    loader._finish()
