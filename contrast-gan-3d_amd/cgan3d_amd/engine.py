@@ -26,6 +26,7 @@ Activations are channels-last fp32 (see include/cgan3d.h).
 """
 from __future__ import annotations
 
+import os
 from dataclasses import dataclass
 from typing import Dict, List, Optional, Sequence, Tuple
 
@@ -178,7 +179,9 @@ class GeneratorPlan:
         # needs its layer's dz and input, both final when it is enqueued); own workspace
         wsw = max([ops.wgrad_ws_floats(gw) for gw in self.geo_wgrad] + [ops.wgrad_ws_floats(self.geo_last_wgrad)])
         self.ws_side = torch.empty(wsw, device=device)
-        self.side = torch.cuda.Stream(device=device) if torch.device(device).type == "cuda" else None
+        # (CGAN3D_NO_SIDE_STREAM=1 serialises them, so a kernel trace shows unshared durations)
+        on_gpu = torch.device(device).type == "cuda" and not os.environ.get("CGAN3D_NO_SIDE_STREAM")
+        self.side = torch.cuda.Stream(device=device) if on_gpu else None
         self.pack()
 
     def _on_side(self, fn):

@@ -98,6 +98,7 @@ bool wgrad_c1_ok(const cgan3d_conv_geom* g);
 int wgrad_c1_launch(const cgan3d_conv_geom* g, const float* gathered, const float* aligned, float* dw, hipStream_t st);
 void wgrad_bf16_set_blocks(int v);
 void halo_set_min_blocks(int v);
+void k7m_set_dbg(int v);
 int wgrad_bf16_launch(const cgan3d_conv_geom* g, const float* gathered, const float* aligned, float* dwp,
                       hipStream_t st);
 bool halo_ok(const cgan3d_conv_geom* g);         // w_packed == 2 and eligible

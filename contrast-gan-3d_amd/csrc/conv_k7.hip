@@ -315,7 +315,11 @@ static int k7_blocks(const K7Args& a) { return a.n * a.tiles_d * a.tiles_h * a.t
 // Which shapes the k7 kernels take (wide side C in {8, 16}); everything else -> generic kernels.
 static bool k7_wide_ok(int c) { return c == 8 || c == 16; }
 // bf16 MFMA variants (conv_k7_mfma.hip): 16-channel wide side, CGAN3D_PREC_BF16 geometries
-static bool k7m_ok(const cgan3d_conv_geom* g, int wide) { return g->prec == CGAN3D_PREC_BF16 && wide == 16; }
+// bf16 MFMA kernels (conv_k7_mfma.hip); their element indices are 32-bit
+static bool k7m_ok(const cgan3d_conv_geom* g, int wide) {
+  const long long vi = (long long)g->n * g->di * g->hi * g->wi, vo = (long long)g->n * g->do_ * g->ho * g->wo;
+  return g->prec == CGAN3D_PREC_BF16 && wide == 16 && std::max(vi, vo) * 16 < (1LL << 31);
+}
 
 // number of blocks the n2w kernel uses for this geometry (0 if the k7 path does not apply);
 // sizes the BatchNorm partial-statistics buffer (cgan3d_conv3d_stats_floats)

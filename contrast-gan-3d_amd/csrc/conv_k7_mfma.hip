@@ -19,6 +19,7 @@
 namespace cg {
 
 typedef __bf16 bf16x8_k __attribute__((ext_vector_type(8)));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 
 // Staging from global memory with every load of the thread in flight at once: element i < total
 // of the tile comes from src[off(i)] (off < 0: zero).  Loads use clamped addresses and no
@@ -256,219 +257,195 @@ __global__ __launch_bounds__(256) void k7m_w2n_kernel(K7Args a, const float* __r
   }
 }
 
-// ---- weight gradients: M = the 16 channels, N = taps (2 (td, th) pairs x 8 tw per 16-column
-// tile, 25 tiles), K = voxels.  The channel operand comes straight from global memory (8 strided
-// floats per lane, rounded to bf16); the single-channel operand is staged as 8 shifted bf16 copies
-// so that every B fragment is one aligned ds_read_b128.  Blocks loop over output tiles (4 x 8 x 16)
-// with the 25 accumulators resident, combine their waves in LDS and write one partial per block;
-// k7m_colsum_kernel adds the partials into dW.
-constexpr int G_TD = 4, G_TH = 8, G_TW = 16, G_ROWS_IN = (G_TD + 6) * (G_TH + 6), G_OROWS = G_TD * G_TH;
+// ---- weight gradients.  Both roles are  dW[c][t] = sum_v X16[v][c] * X1[v + t']  with one
+// operand on an exact tile (no halo, every voxel read once) and the single-channel one on a halo:
+//  * first conv (MODE 0):  X16 = g on the output grid, X1[u] = x[reflect(u - P)], t' = t;
+//  * last conv  (MODE 1):  X16 = reflect-padded x on the padded grid (di + 2P), X1[u] = g[u - 6]
+//    (zero outside), t' = flip(t) = 342 - t  — the reflection moves to the 16-channel side so the
+//    16-channel tensor is never re-read through a halo.
+// M = 16 channels, N = taps (2 (td, th) pairs x 8 tw per 16-column tile, 25 tiles), K = the tile's
+// voxels.  The four waves split the N tiles (no cross-wave reduction); A fragments come from the
+// X16 tile staged channel-major in LDS, B fragments from 8 shifted bf16 copies of the X1 halo.  Each
+// block loops over tiles (next tile's global loads in flight during the current tile's MFMAs) and
+// writes one partial [c][t]; k7m_colsum_kernel adds the partials into dW.
+constexpr int G_TD = 4, G_TH = 8, G_TW = 16, G_ROWS_IN = (G_TD + 6) * (G_TH + 6), G_VOX = G_TD * G_TH * G_TW;
 constexpr int G_NT = 25;                // N tiles: pairs (2j, 2j+1) x tw 0..7
 constexpr int G_COLS = 16 * KT7;        // partial row: [c][t]
+constexpr int G_HW = G_TW + 6;          // X1 halo row length (22)
+// shifted-copy row (bf16): w 0..15, unpadded.  With [row][tw][16] the ds_read_b128 lane groups
+// (MI355X_MICROARCH.md, LDS table) of a B-fragment read cover 16 distinct 16-byte bank blocks:
+// (pair half, w half) in {(0,0) tw 0-3, (1,0) tw 4-7, (0,1) tw 4-7, (1,1) tw 0-3} -> blocks 2tw + half.
+constexpr int G_SXW = G_TW;
+constexpr int G_X1 = G_ROWS_IN * G_HW;  // X1 halo values (3080)
+constexpr int G_HWP = 24;               // xh row stride: 16-byte aligned halves, zero tail
+constexpr int G_X1_PER = (G_X1 + 255) / 256;
 
-__device__ __forceinline__ void k7m_tile(const K7Args& a, int tile, int* n, int* d0, int* h0, int* w0) {
-  const int tw_ = tile % a.tiles_w; tile /= a.tiles_w;
-  const int th_ = tile % a.tiles_h; tile /= a.tiles_h;
-  const int td_ = tile % a.tiles_d; *n = tile / a.tiles_d;
-  *d0 = td_ * G_TD; *h0 = th_ * G_TH; *w0 = tw_ * G_TW;
-}
+template <int MODE>
+__global__ __launch_bounds__(256, 2) void k7m_wg_kernel(K7Args a, const float* __restrict__ x,
+                                                        const float* __restrict__ go, float* __restrict__ part,
+                                                        int tiles_per_block, int ntiles) {
+  constexpr int SX_BYTES = G_ROWS_IN * 8 * G_SXW * 2;    // 53760
+  constexpr int AS_BYTES = G_VOX * 16 * 2;               // 16384: [octet][c][8]
+  __shared__ __attribute__((aligned(16))) unsigned char lds[SX_BYTES + AS_BYTES + G_ROWS_IN * G_HWP * 2];
+  __bf16* sx = reinterpret_cast<__bf16*>(lds);                        // [row][tw][G_SXW]
+  __bf16* as = reinterpret_cast<__bf16*>(lds + SX_BYTES);             // [octet][c][8]
+  __bf16* xh = reinterpret_cast<__bf16*>(lds + SX_BYTES + AS_BYTES);  // [row][G_HWP]
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6), g = lane >> 4,
+            r16 = lane & 15;
+  // the X16 grid (tiles run over it) and the source of X1
+  const int gd = MODE ? a.di + 2 * a.P : a.do_, gh = MODE ? a.hi + 2 * a.P : a.ho, gw = MODE ? a.wi + 2 * a.P : a.wo;
+  const int td_n = (gd + G_TD - 1) / G_TD, th_n = (gh + G_TH - 1) / G_TH, tw_n = (gw + G_TW - 1) / G_TW;
 
-// combine the 4 waves' accumulators and write this block's partial [c][t].  Column n of N-tile
-// j holds tap (pair, tw) = (2j + (n >> 3), n & 7) when TD_TILES is false (25 tiles), and
-// (td, th, tw) = (j >> 2, 2 (j & 3) + (n >> 3), n & 7) when it is true (28 tiles).
-template <int NT, bool TD_TILES>
-__device__ __forceinline__ void k7m_wg_store(f32x4 (&acc)[NT], float* red, float* part) {
-  const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, r16 = lane & 15;
-  for (int i = tid; i < NT * 256; i += 256) red[i] = 0.f;
-  __syncthreads();
+  // staging registers: X16 = 8 voxels (one octet along w) x 4 channels per thread, X1 = G_X1_PER values
+  const int oct = tid >> 2, c4 = tid & 3;  // octet 0..63 -> (row, half) of the tile
+  f32x4 xa[8];
+  float xb[G_X1_PER];
+  // this thread's X1 halo values: packed (hd, hh, hw), -1 past the halo (fixed over tiles)
+  int x1c[G_X1_PER];
 #pragma unroll
-  for (int j = 0; j < NT; ++j)
+  for (int k = 0; k < G_X1_PER; ++k) {
+    const int i = tid + 256 * k;
+    const int hw = i % G_HW, row = i / G_HW;
+    x1c[k] = i < G_X1 ? ((row / (G_TH + 6)) | ((row % (G_TH + 6)) << 8) | (hw << 16)) : -1;
+  }
+  // 32-bit element indices (k7m_ok bounds the tensor sizes)
+  auto load = [&](int tile) {
+    int tw_ = tile % tw_n, r = tile / tw_n;
+    const int th_ = r % th_n; r /= th_n;
+    const int td_ = r % td_n, n = r / td_n;
+    const int d0 = td_ * G_TD, h0 = th_ * G_TH, w0 = tw_ * G_TW;
+    {  // X16 octet: one (d, h) row, 8 consecutive w
+      const int row = oct >> 1, wl = w0 + 8 * (oct & 1);
+      const int vd = d0 + row / G_TH, vh = h0 + row % G_TH;
+      int rowbase;  // element index of (n, d, h, w = 0) in the X16 source, -1 if the row is empty
+      if (MODE) {
+        const int id = k7_src(vd - a.P, a.di, a.reflect), ih = k7_src(vh - a.P, a.hi, a.reflect);
+        rowbase = (vd < gd && vh < gh && (id | ih) >= 0) ? ((n * a.di + id) * a.hi + ih) * a.wi : -1;
+      } else {
+        rowbase = (vd < gd && vh < gh) ? ((n * a.do_ + vd) * a.ho + vh) * a.wo : -1;
+      }
+      const f32x4* p = reinterpret_cast<const f32x4*>(MODE ? x : go);
 #pragma unroll
-    for (int jj = 0; jj < 4; ++jj) atomicAdd(&red[j * 256 + (4 * g + jj) * 16 + r16], acc[j][jj]);
-  __syncthreads();
+      for (int e = 0; e < 8; ++e) {
+        const int vw = wl + e;
+        const int iw = MODE ? k7_src(vw - a.P, a.wi, a.reflect) : (vw < gw ? vw : -1);
+        const bool ok = rowbase >= 0 && vw < gw && iw >= 0;
+        xa[e] = p[ok ? (rowbase + iw) * 4 + c4 : 0];
+        if (!ok) xa[e] = f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+    }
+    const float* p = MODE ? go : x;
+#pragma unroll
+    for (int k = 0; k < G_X1_PER; ++k) {  // X1 halo value (hd, hh, hw)
+      const int c = x1c[k], hd = c & 255, hh = (c >> 8) & 255, hw = c >> 16;
+      int src;
+      if (MODE) {  // g[u - 6], zero outside
+        const int ud = d0 + hd - (K7 - 1), uh = h0 + hh - (K7 - 1), uw = w0 + hw - (K7 - 1);
+        const bool ok = c >= 0 && (unsigned)ud < (unsigned)a.do_ && (unsigned)uh < (unsigned)a.ho &&
+                        (unsigned)uw < (unsigned)a.wo;
+        src = ok ? ((n * a.do_ + ud) * a.ho + uh) * a.wo + uw : -1;
+      } else {   // x[reflect(u - P)]
+        const int id = k7_src(d0 + hd - a.P, a.di, a.reflect), ih = k7_src(h0 + hh - a.P, a.hi, a.reflect),
+                  iw = k7_src(w0 + hw - a.P, a.wi, a.reflect);
+        src = (c >= 0 && (id | ih | iw) >= 0) ? ((n * a.di + id) * a.hi + ih) * a.wi + iw : -1;
+      }
+      xb[k] = p[src >= 0 ? src : 0];
+      if (src < 0) xb[k] = 0.f;
+    }
+  };
+  auto store = [&]() {  // staged registers -> LDS (X16 channel-major, X1 as bf16)
+#pragma unroll
+    for (int cc = 0; cc < 4; ++cc) {
+      bf16x8_k u;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) u[e] = (__bf16)xa[e][cc];
+      *reinterpret_cast<bf16x8_k*>(as + (oct * 16 + 4 * c4 + cc) * 8) = u;
+    }
+#pragma unroll
+    for (int k = 0; k < G_X1_PER; ++k) {
+      const int c = x1c[k];
+      if (c >= 0) xh[((c & 255) * (G_TH + 6) + ((c >> 8) & 255)) * G_HWP + (c >> 16)] = (__bf16)xb[k];
+    }
+  };
+  for (int r = tid; r < G_ROWS_IN; r += 256) {  // row tails (read by the shifted copies, never stored)
+    xh[r * G_HWP + G_HW] = (__bf16)0.f;
+    xh[r * G_HWP + G_HW + 1] = (__bf16)0.f;
+  }
+
+  f32x4 acc[7];
+#pragma unroll
+  for (int j = 0; j < 7; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  int boff[7];  // sx offset of this lane's B column in the wave's N tiles (j = wave + 4 jl)
+#pragma unroll
+  for (int jl = 0; jl < 7; ++jl) {
+    const int pair = min(2 * (wave + 4 * jl) + (r16 >> 3), 48);  // past tap 342: dropped at the store
+    const int td = pair / K7, th = pair - td * K7;
+    boff[jl] = ((td * (G_TH + 6) + th) * 8 + (r16 & 7)) * G_SXW;
+  }
+  const int t0 = blockIdx.x * tiles_per_block, t1 = min(ntiles, t0 + tiles_per_block);
+  if (t0 < t1 && !(a.dbg & 4)) load(t0);
+  for (int tile = t0; tile < t1; ++tile) {
+    __syncthreads();  // previous tile's reads of sx / as done
+    if (!(a.dbg & 8)) store();
+    if (tile + 1 < t1 && !(a.dbg & 4)) load(tile + 1);  // in flight during this tile's MFMAs
+    __syncthreads();
+    if (!(a.dbg & 1))
+    for (int i = tid; i < G_ROWS_IN * 2; i += 256) {  // shifted copies of (row, half): 8 tw
+      const int r = i >> 1, hf = i & 1;
+      const u32x4 lo = *reinterpret_cast<const u32x4*>(xh + r * G_HWP + 8 * hf);
+      const u32x4 hi = *reinterpret_cast<const u32x4*>(xh + r * G_HWP + 8 * hf + 8);
+      const unsigned w[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+#pragma unroll
+      for (int tw = 0; tw < 8; ++tw) {
+        u32x4 o;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const int m = tw / 2 + k;
+          o[k] = (tw & 1) ? __builtin_amdgcn_alignbyte(w[m + 1], w[m], 2) : w[m];
+        }
+        *reinterpret_cast<u32x4*>(sx + ((r * 8 + tw) * G_SXW + 8 * hf)) = o;
+      }
+    }
+    __syncthreads();
+    if (a.dbg & 2) continue;
+    // K-step ks = 32 voxels = tile rows 2ks, 2ks+1 (16 w each); lane group g: row 2ks + (g >> 1), w 8 (g & 1)
+    // K-step ks = 32 voxels = tile rows 2ks, 2ks+1; lane group g: row 2ks + (g >> 1), w 8 (g & 1).
+    // Two fragment sets in registers: K-step ks + 1's reads are in flight during ks's MFMAs.
+    bf16x8_k av[2], bv[2][7];
+    auto frag = [&](int ks, int buf) {
+      av[buf] = *reinterpret_cast<const bf16x8_k*>(as + ((ks * 4 + g) * 16 + r16) * 8);
+      const int row = 2 * ks + (g >> 1), dl = row / G_TH, hl = row % G_TH, wl = 8 * (g & 1);
+      const __bf16* sb = sx + ((dl * (G_TH + 6) + hl) * 8 * G_SXW + wl);
+#pragma unroll
+      for (int jl = 0; jl < 7; ++jl) bv[buf][jl] = *reinterpret_cast<const bf16x8_k*>(sb + boff[jl]);
+    };
+    frag(0, 0);
+#pragma unroll
+    for (int ks = 0; ks < G_VOX / 32; ++ks) {
+      const int cur = ks & 1;
+      if (ks + 1 < G_VOX / 32) frag(ks + 1, cur ^ 1);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int jl = 0; jl < 6; ++jl)
+        acc[jl] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[cur], bv[cur][jl], acc[jl], 0, 0, 0);
+      if (wave == 0) acc[6] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[cur], bv[cur][6], acc[6], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+  // lane holds dW[c = 4g + jj][column r16 of tile j]
   float* pb = part + (long long)blockIdx.x * G_COLS;
-  for (int i = tid; i < NT * 256; i += 256) {
-    const int j = i >> 8, c = (i >> 4) & 15, col = i & 15, tw = col & 7;
-    int pair;
-    if (TD_TILES) {
-      const int th = 2 * (j & 3) + (col >> 3);
-      pair = th < K7 ? (j >> 2) * K7 + th : 99;
-    } else {
-      pair = 2 * j + (col >> 3);
-    }
-    if (pair < 49 && tw < K7) pb[c * KT7 + pair * K7 + tw] = red[i];
-  }
-}
-
-// dW[c, t] = sum_o x[src(o + t - P)] * g[o, c]   (first conv; x single-channel, g 16 channels)
-__global__ __launch_bounds__(256) void k7m_wg_n2w_kernel(K7Args a, const float* __restrict__ x,
-                                                         const float* __restrict__ go, float* __restrict__ part,
-                                                         int ntiles) {
-  constexpr int HW = G_TW + 8;  // x halo row: ow 0..15 + tw 0..7
-  constexpr int SXW = G_TW + 8;  // shifted-copy row (bf16), padded: the 8 tw copies of a row fall
-                                 // on distinct banks
-  __shared__ __attribute__((aligned(16))) unsigned char lds[8 * G_ROWS_IN * SXW * 2 + G_ROWS_IN * HW * 4];
-  __bf16* sx = reinterpret_cast<__bf16*>(lds);                           // [row][tw][SXW]
-  float* xs = reinterpret_cast<float*>(lds + 8 * G_ROWS_IN * SXW * 2);  // [row][24]
-  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6), g = lane >> 4,
-            r16 = lane & 15;
-  f32x4 acc[G_NT];
 #pragma unroll
-  for (int j = 0; j < G_NT; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-    int n, d0, h0, w0;
-    k7m_tile(a, tile, &n, &d0, &h0, &w0);
-    __syncthreads();
-    k7m_stage<(G_ROWS_IN * HW + 255) / 256>(
-        x, G_ROWS_IN * HW,
-        [&](int i) -> long long {
-          const int hw = i % HW, r = i / HW, hh = r % (G_TH + 6), hd = r / (G_TH + 6);
-          if (hw >= G_TW + 6) return -1;
-          const int id = k7_src(d0 + hd - a.P, a.di, a.reflect);
-          const int ih = k7_src(h0 + hh - a.P, a.hi, a.reflect);
-          const int iw = k7_src(w0 + hw - a.P, a.wi, a.reflect);
-          return (id | ih | iw) >= 0 ? ((long long)(n * a.di + id) * a.hi + ih) * a.wi + iw : -1;
-        },
-        [&](int i, float v) { xs[i] = v; });
-    __syncthreads();
-    for (int i = tid; i < 8 * G_ROWS_IN * 2; i += 256) {  // (tw, row, half of 16)
-      const int hf = i & 1, r = (i >> 1) % G_ROWS_IN, tw = (i >> 1) / G_ROWS_IN;
-      const float* src = xs + r * HW + tw + 8 * hf;
-      bf16x8_k u;
+  for (int jl = 0; jl < 7; ++jl) {
+    const int j = wave + 4 * jl;
+    if (j >= G_NT) break;
+    const int pair = 2 * j + (r16 >> 3), tw = r16 & 7;
+    if (pair < 49 && tw < K7) {
+      const int tp = pair * K7 + tw;
+      const int t = MODE ? KT7 - 1 - tp : tp;
 #pragma unroll
-      for (int e = 0; e < 8; ++e) u[e] = (__bf16)src[e];
-      *reinterpret_cast<bf16x8_k*>(sx + ((r * 8 + tw) * SXW + 8 * hf)) = u;
-    }
-    __syncthreads();
-    // K-steps of 32 outputs = 2 output rows x 16; wave takes K-steps wave, wave+4, ...
-    constexpr int KS = G_OROWS / 2 / 4;  // K-steps per wave per tile
-    float gv[KS][8];
-#pragma unroll
-    for (int kk = 0; kk < KS; ++kk) {  // issue every load of the wave's K-steps first
-      const int orow = 2 * (wave + 4 * kk) + (g >> 1), owl = 8 * (g & 1);
-      const int od = d0 + orow / G_TH, oh = h0 + orow % G_TH;
-      const bool rv = od < a.do_ && oh < a.ho;
-      const long long vb = (((long long)(n * a.do_ + od) * a.ho + oh) * a.wo + w0 + owl) * 16 + r16;
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const bool ok = rv && w0 + owl + e < a.wo;
-        gv[kk][e] = go[ok ? vb + e * 16 : 0];
-        if (!ok) gv[kk][e] = 0.f;
-      }
-    }
-#pragma unroll
-    for (int kk = 0; kk < KS; ++kk) {
-      const int ks = wave + 4 * kk;
-      const int orow = 2 * ks + (g >> 1), odl = orow / G_TH, ohl = orow % G_TH, owl = 8 * (g & 1);
-      bf16x8_k av;
-#pragma unroll
-      for (int e = 0; e < 8; ++e) av[e] = (__bf16)gv[kk][e];
-#pragma unroll
-      for (int j = 0; j < G_NT; ++j) {
-        const int pair = 2 * j + (r16 >> 3), tw = r16 & 7;
-        const int pa = pair < 49 ? pair : 48;
-        const int td = pa / K7, th = pa - td * K7;
-        const bf16x8_k bv = *reinterpret_cast<const bf16x8_k*>(
-            sx + ((((odl + td) * (G_TH + 6) + ohl + th) * 8 + tw) * SXW + owl));
-        acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, bv, acc[j], 0, 0, 0);
-      }
+      for (int jj = 0; jj < 4; ++jj) pb[(4 * g + jj) * KT7 + t] = acc[jl][jj];
     }
   }
-  __syncthreads();
-  k7m_wg_store<G_NT, false>(acc, reinterpret_cast<float*>(lds), part);
-}
-
-// dW[c, t] = sum_i x[src(i), c] * g[i - t]   (last conv; x 16 channels on the input halo, g single-
-// channel on the output tile); K = the 32 halo columns of one input row
-__global__ __launch_bounds__(256) void k7m_wg_w2n_kernel(K7Args a, const float* __restrict__ x,
-                                                         const float* __restrict__ go, float* __restrict__ part,
-                                                         int ntiles) {
-  constexpr int Q = 32;  // halo columns per input row (22 used)
-  __shared__ __attribute__((aligned(16))) unsigned char lds[28 * 256 * 4];
-  constexpr int QP = Q + 8;  // padded row: a B read's 8 tw copies fall on distinct banks
-  __bf16* sd = reinterpret_cast<__bf16*>(lds);                   // [orow][tw][QP]: g[orow][q - tw]
-  float* gs = reinterpret_cast<float*>(lds + 8 * G_OROWS * QP * 2);  // [orow][16]
-  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6), g = lane >> 4,
-            r16 = lane & 15;
-  constexpr int NT = 28;  // N tiles (td, th pair (0,1) (2,3) (4,5) (6,-)) x tw 0..7
-  f32x4 acc[NT];
-#pragma unroll
-  for (int j = 0; j < NT; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-    int n, d0, h0, w0;
-    k7m_tile(a, tile, &n, &d0, &h0, &w0);
-    __syncthreads();
-    for (int i = tid; i < G_OROWS * G_TW; i += 256) {
-      const int owl = i % G_TW, r = i / G_TW, od = d0 + r / G_TH, oh = h0 + r % G_TH, ow = w0 + owl;
-      gs[i] = (od < a.do_ && oh < a.ho && ow < a.wo) ? go[((long long)(n * a.do_ + od) * a.ho + oh) * a.wo + ow] : 0.f;
-    }
-    __syncthreads();
-    for (int i = tid; i < 8 * G_OROWS * (Q / 8); i += 256) {
-      const int q8 = i % (Q / 8), r = (i / (Q / 8)) % G_OROWS, tw = i / (Q / 8 * G_OROWS);
-      bf16x8_k u;
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const int ow = 8 * q8 + e - tw;
-        u[e] = (__bf16)((ow >= 0 && ow < G_TW) ? gs[r * G_TW + ow] : 0.f);
-      }
-      *reinterpret_cast<bf16x8_k*>(sd + ((r * 8 + tw) * QP + 8 * q8)) = u;
-    }
-    __syncthreads();
-    // this lane's 8 halo columns (fixed over the rows)
-    int swc[8];
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      const int q = 8 * g + e;
-      swc[e] = q < G_TW + 6 ? k7_src(w0 + q - a.P, a.wi, a.reflect) : -1;
-    }
-    constexpr int RB = 5;  // rows per batch: 5 x 8 loads in flight per lane
-    static_assert((G_ROWS_IN / 4) % RB == 0, "row batches");
-    for (int rb0 = wave; rb0 < G_ROWS_IN; rb0 += 4 * RB) {
-      float xv[RB][8];
-#pragma unroll
-      for (int b = 0; b < RB; ++b) {
-        const int r = rb0 + 4 * b, id = r / (G_TH + 6), ih = r % (G_TH + 6);
-        const int sd_ = k7_src(d0 + id - a.P, a.di, a.reflect);
-        const int sh_ = k7_src(h0 + ih - a.P, a.hi, a.reflect);
-        const long long rowb = ((long long)(n * a.di + sd_) * a.hi + sh_) * a.wi;
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          const bool ok = (sd_ | sh_ | swc[e]) >= 0;
-          xv[b][e] = x[ok ? (rowb + swc[e]) * 16 + r16 : 0];
-          if (!ok) xv[b][e] = 0.f;
-        }
-      }
-#pragma unroll
-      for (int b = 0; b < RB; ++b) {
-        const int r = rb0 + 4 * b, id = r / (G_TH + 6), ih = r % (G_TH + 6);
-        bf16x8_k av;
-#pragma unroll
-        for (int e = 0; e < 8; ++e) av[e] = (__bf16)xv[b][e];
-        // taps reaching an output row of this tile from input row (id, ih): td in [id-3, id],
-        // th in [ih-7, ih] (intersected with 0..6); branch per td (scalar), 4 th-pair tiles each
-        const int thl = ih - (G_TH - 1) > 0 ? ih - (G_TH - 1) : 0, thh = ih < K7 - 1 ? ih : K7 - 1;
-        const int th0 = r16 >> 3, tw = r16 & 7;  // this lane's column: th = 2q + th0, tw
-#pragma unroll
-        for (int td = 0; td < K7; ++td) {
-          const int odl = id - td;
-          if (odl < 0 || odl >= G_TD) continue;
-          bf16x8_k bv[4];
-#pragma unroll
-          for (int q = 0; q < 4; ++q) {  // all four B reads before the MFMAs
-            const int thq = 2 * q + th0, ohl = ih - thq;
-            const bool mine = thq >= thl && thq <= thh;
-            bv[q] = *reinterpret_cast<const bf16x8_k*>(sd + (((mine ? odl * G_TH + ohl : 0) * 8 + tw) * QP + 8 * g));
-            if (!mine) bv[q] = bf16x8_k{};
-          }
-#pragma unroll
-          for (int q = 0; q < 4; ++q)
-            acc[td * 4 + q] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, bv[q], acc[td * 4 + q], 0, 0, 0);
-        }
-      }
-    }
-  }
-  __syncthreads();
-  k7m_wg_store<NT, true>(acc, reinterpret_cast<float*>(lds), part);
 }
 
 // dW[c * wc + t] += sum_b part[b][c * 343 + t]; grid (cols / 256, row splits)
@@ -484,10 +461,21 @@ __global__ __launch_bounds__(256) void k7m_colsum_kernel(const float* __restrict
   atomicAdd(dw + c * wc + t, s);
 }
 
-static int k7m_wg_grid(int ntiles) { return ntiles < 512 ? ntiles : 512; }
+// tiles of the wgrad X16 grid (output grid, or the padded input grid for the last conv)
+static void k7m_wg_split(const cgan3d_conv_geom* g, bool wide_in, int* grid, int* per, int* ntiles) {
+  const int gd = wide_in ? g->di + 2 * g->pad : g->do_, gh = wide_in ? g->hi + 2 * g->pad : g->ho,
+            gw = wide_in ? g->wi + 2 * g->pad : g->wo;
+  *ntiles = g->n * ((gd + G_TD - 1) / G_TD) * ((gh + G_TH - 1) / G_TH) * ((gw + G_TW - 1) / G_TW);
+  *per = (*ntiles + 511) / 512;
+  *grid = (*ntiles + *per - 1) / *per;
+}
+
+static int g_k7m_dbg = 0;
+void k7m_set_dbg(int v) { g_k7m_dbg = v; }
 
 static K7Args k7m_args(const cgan3d_conv_geom* g, int P, int reflect, int flip, long long wc, int td, int th, int tw) {
   K7Args a;
+  a.dbg = g_k7m_dbg;
   a.n = g->n; a.di = g->di; a.hi = g->hi; a.wi = g->wi; a.do_ = g->do_; a.ho = g->ho; a.wo = g->wo;
   a.P = P; a.reflect = reflect; a.flip = flip; a.wc = wc;
   a.tiles_d = (g->do_ + td - 1) / td; a.tiles_h = (g->ho + th - 1) / th; a.tiles_w = (g->wo + tw - 1) / tw;
@@ -514,18 +502,20 @@ void k7m_w2n_launch(const cgan3d_conv_geom* g, int P, int reflect, long long wc,
 }
 
 long long k7m_wgrad_ws_floats(const cgan3d_conv_geom* g) {
-  const K7Args a = k7m_args(g, 0, 0, 0, 0, G_TD, G_TH, G_TW);
-  return (long long)k7m_wg_grid(a.n * a.tiles_d * a.tiles_h * a.tiles_w) * G_COLS;
+  int grid, per, nt, grid2;
+  k7m_wg_split(g, true, &grid, &per, &nt);
+  k7m_wg_split(g, false, &grid2, &per, &nt);
+  return (long long)std::max(grid, grid2) * G_COLS;
 }
 
 // weight grad of a k7 conv with one single-channel side; dw already zeroed (or accumulating)
 void k7m_wgrad_launch(const cgan3d_conv_geom* g, bool wide_in, long long wc, const float* x, const float* go, float* dw,
                       float* ws, hipStream_t s) {
   const K7Args a = k7m_args(g, g->pad, g->reflect, 0, wc, G_TD, G_TH, G_TW);
-  const int ntiles = a.n * a.tiles_d * a.tiles_h * a.tiles_w;
-  const int grid = k7m_wg_grid(ntiles);
-  if (wide_in) hipLaunchKernelGGL(k7m_wg_w2n_kernel, dim3(grid), dim3(256), 0, s, a, x, go, ws, ntiles);
-  else hipLaunchKernelGGL(k7m_wg_n2w_kernel, dim3(grid), dim3(256), 0, s, a, x, go, ws, ntiles);
+  int grid, per, ntiles;
+  k7m_wg_split(g, wide_in, &grid, &per, &ntiles);
+  if (wide_in) hipLaunchKernelGGL(k7m_wg_kernel<1>, dim3(grid), dim3(256), 0, s, a, x, go, ws, per, ntiles);
+  else hipLaunchKernelGGL(k7m_wg_kernel<0>, dim3(grid), dim3(256), 0, s, a, x, go, ws, per, ntiles);
   const int rows_per = 32;
   hipLaunchKernelGGL(k7m_colsum_kernel, dim3((G_COLS + 255) / 256, (grid + rows_per - 1) / rows_per), dim3(256), 0, s,
                      ws, grid, rows_per, dw, wc);

@@ -42,7 +42,7 @@ def _cases(B=4, S=64):
         flops = 2.0 * B * dout[0] * dout[1] * dout[2] * geo.cin * geo.cout * geo.k**3
         return (lambda: ops.wgrad(geo, x, go, dw, ws)), flops
 
-    R3, H3, F3 = (r,) * 3, (2 * r,) * 3, (S,) * 3
+    R3, H3, F3, P3 = (r,) * 3, (2 * r,) * 3, (S,) * 3, (S + 6,) * 3
 
     def crit(cin, cout, din, halo=True):
         """critic layer forward over the 3B critic batch (real | fake | interpolation)"""
@@ -74,6 +74,14 @@ def _cases(B=4, S=64):
         "up1_fwd": lambda: conv_case(ops.convt_fwd_geom(B, H3, F3, 32, 16, 3, 2, 1), 32, 16, H3, F3),
         "k7_last_fwd": lambda: conv_case(ops.with_prec(ops.conv_fwd_geom(B, F3, F3, 16, 1, 7, 1, 3, True), BF), 16, 1,
                                          F3, F3, packed=False),
+        "k7_first_fwd": lambda: conv_case(ops.with_prec(ops.conv_fwd_geom(B, F3, F3, 1, 16, 7, 1, 3, True), BF), 1, 16,
+                                          F3, F3, packed=False),
+        "k7_last_dgrad": lambda: conv_case(ops.with_prec(ops.conv_dgrad_geom(B, P3, F3, 16, 1, 7, 1, 0), BF), 1, 16,
+                                           F3, P3, packed=False),
+        "k7_first_wgrad": lambda: wgrad_case(ops.with_prec(ops.conv_wgrad_geom(B, F3, F3, 1, 16, 7, 1, 3, True), BF),
+                                             F3, F3),
+        "k7_last_wgrad": lambda: wgrad_case(ops.with_prec(ops.conv_wgrad_geom(B, F3, F3, 16, 1, 7, 1, 3, True), BF),
+                                            F3, F3),
     }
 
 
