@@ -20,6 +20,7 @@ namespace cg {
 
 typedef __bf16 bf16x8_k __attribute__((ext_vector_type(8)));
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x4_k __attribute__((ext_vector_type(4)));
 
 // Staging from global memory with every load of the thread in flight at once: element i < total
 // of the tile comes from src[off(i)] (off < 0: zero).  Loads use clamped addresses and no
@@ -42,28 +43,28 @@ __device__ __forceinline__ void k7m_stage(const T* __restrict__ src, int total, 
   }
 }
 
-// ---- n2w tile: 4 (d) x 8 (h) x 16 (w) outputs, wave = one d-slice (8 rows of 16 voxels)
+// ---- n2w: 4 (d) x 8 (h) x 16 (w) output tiles, wave = one d-slice (8 rows of 16 voxels = 8 M tiles).
+// Persistent blocks loop over tiles: the 13 B fragments (weights) stay in registers for the whole
+// launch, the next tile's x halo is loaded into registers during the current tile's MFMAs, and the
+// "unfolded" A image us[row][ow][8 taps] = x[row][ow .. ow + 7] is built from the bf16 halo rows by
+// byte-aligning register pairs (no per-element LDS reads).  Bank-conflict-free: a b128 lane group
+// of the A read covers ow 0..15 = the 16 bank blocks.
 constexpr int N_TD = 4, N_TH = 8, N_TW = 16;
-constexpr int N_HD = N_TD + 6, N_HH = N_TH + 6, N_HW = 24;  // x halo (23 used: ow 0..15 + tw 0..7)
+constexpr int N_HD = N_TD + 6, N_HH = N_TH + 6, N_HW = N_TW + 6, N_HWP = 24;  // x halo rows (22 used)
 constexpr int N_ROWS = N_HD * N_HH;
 constexpr int N_PAIRS = 52;                                 // 49 (td, th) pairs padded to 13 K-steps
+constexpr int N_X = N_ROWS * N_HW, N_X_PER = (N_X + 255) / 256;
 
-__global__ __launch_bounds__(256) void k7m_n2w_kernel(K7Args a, const float* __restrict__ x,
-                                                      const float* __restrict__ w, float* __restrict__ y,
-                                                      float* stats) {
+__global__ __launch_bounds__(256, 2) void k7m_n2w_kernel(K7Args a, const float* __restrict__ x,
+                                                         const float* __restrict__ w, float* __restrict__ y,
+                                                         float* stats, int tiles_per_block, int ntiles) {
   constexpr int C = 16;
-  __shared__ __attribute__((aligned(16))) float xs[N_ROWS * N_HW];
   __shared__ __attribute__((aligned(16))) __bf16 us[N_ROWS * N_TW * 8];  // [row][ow][8 taps]
+  __shared__ __attribute__((aligned(16))) __bf16 xs[N_ROWS * N_HWP];     // [row][24]
   __shared__ __attribute__((aligned(16))) __bf16 wt[N_PAIRS * C * 8];    // [pair][c][tw8]
+  __shared__ float red[4][C];
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  int n, d0, h0, w0;
-  {
-    int bid = blockIdx.x;
-    const int tw_ = bid % a.tiles_w; bid /= a.tiles_w;
-    const int th_ = bid % a.tiles_h; bid /= a.tiles_h;
-    const int td_ = bid % a.tiles_d; n = bid / a.tiles_d;
-    d0 = td_ * N_TD; h0 = th_ * N_TH; w0 = tw_ * N_TW;
-  }
+  const int g = lane >> 4, r16 = lane & 15;
   k7m_stage<(N_PAIRS * C * 8 + 255) / 256>(
       w, N_PAIRS * C * 8,
       [&](int i) -> long long {
@@ -73,128 +74,173 @@ __global__ __launch_bounds__(256) void k7m_n2w_kernel(K7Args a, const float* __r
         return (long long)c * a.wc + (a.flip ? KT7 - 1 - t : t);
       },
       [&](int i, float v) { wt[i] = (__bf16)v; });
-  k7m_stage<(N_ROWS * N_HW + 255) / 256>(
-      x, N_ROWS * N_HW,
-      [&](int i) -> long long {
-        const int hw = i % N_HW, r = i / N_HW, hh = r % N_HH, hd = r / N_HH;
-        if (hw >= N_TW + 7) return -1;
-        const int id = k7_src(d0 + hd - a.P, a.di, a.reflect);
-        const int ih = k7_src(h0 + hh - a.P, a.hi, a.reflect);
-        const int iw = k7_src(w0 + hw - a.P, a.wi, a.reflect);
-        return (id | ih | iw) >= 0 ? ((long long)(n * a.di + id) * a.hi + ih) * a.wi + iw : -1;
-      },
-      [&](int i, float v) { xs[i] = v; });
-  __syncthreads();
-  for (int i = tid; i < N_ROWS * N_TW; i += 256) {
-    const int ow = i % N_TW, r = i / N_TW;
-    const float* src = xs + r * N_HW + ow;
-    bf16x8_k u;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) u[j] = (__bf16)src[j];
-    *reinterpret_cast<bf16x8_k*>(us + i * 8) = u;
+  for (int r = tid; r < N_ROWS; r += 256) {  // row tails (read by the unfold, never stored)
+    xs[r * N_HWP + N_HW] = (__bf16)0.f;
+    xs[r * N_HWP + N_HW + 1] = (__bf16)0.f;
   }
   __syncthreads();
-
-  const int g = lane >> 4, r16 = lane & 15;
-  f32x4 acc[N_TH];
+  bf16x8_k bv[N_PAIRS / 4];  // K-step ks: pair 4ks + g, tw 0..7, channel r16
 #pragma unroll
-  for (int r = 0; r < N_TH; ++r) acc[r] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll 1
+  for (int ks = 0; ks < N_PAIRS / 4; ++ks) bv[ks] = *reinterpret_cast<const bf16x8_k*>(wt + ((4 * ks + g) * C + r16) * 8);
+  int aoff[N_PAIRS / 4];  // A image offset of this lane's pair (rows past pair 48: any finite row)
+#pragma unroll
   for (int ks = 0; ks < N_PAIRS / 4; ++ks) {
-    const int p = 4 * ks + g;
-    const bf16x8_k bv = *reinterpret_cast<const bf16x8_k*>(wt + (p * C + r16) * 8);
-    const int pa = p < 49 ? p : 48;  // zero weights past 49: any finite A
-    const int td = pa / K7, th = pa - td * K7;
-    const __bf16* ub = us + (((wave + td) * N_HH + th) * N_TW + r16) * 8;
-#pragma unroll
-    for (int r = 0; r < N_TH; ++r) {
-      const bf16x8_k av = *reinterpret_cast<const bf16x8_k*>(ub + r * N_TW * 8);
-      acc[r] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, bv, acc[r], 0, 0, 0);
-    }
+    const int pa = min(4 * ks + g, 48), td = pa / K7, th = pa - td * K7;
+    aoff[ks] = ((td * N_HH + th) * N_TW + r16) * 8;
   }
-
-  // lane holds out[ow = 4g + jj][c = r16] of row r (oh = h0 + r, od = d0 + wave)
-  const int od = d0 + wave;
-  float s1 = 0.f;
-  int cntl = 0;
+  int xc[N_X_PER];  // this thread's halo values: packed (hd, hh, hw), -1 past the halo
 #pragma unroll
-  for (int r = 0; r < N_TH; ++r) {
-    const int oh = h0 + r;
+  for (int k = 0; k < N_X_PER; ++k) {
+    const int i = tid + 256 * k, hw = i % N_HW, row = i / N_HW;
+    xc[k] = i < N_X ? ((row / N_HH) | ((row % N_HH) << 8) | (hw << 16)) : -1;
+  }
+  float xb[N_X_PER];
+  auto tile_origin = [&](int tile, int* n, int* d0, int* h0, int* w0) {
+    int r = tile;
+    const int tw_ = r % a.tiles_w; r /= a.tiles_w;
+    const int th_ = r % a.tiles_h; r /= a.tiles_h;
+    const int td_ = r % a.tiles_d; *n = r / a.tiles_d;
+    *d0 = td_ * N_TD; *h0 = th_ * N_TH; *w0 = tw_ * N_TW;
+  };
+  auto load = [&](int tile) {
+    int n, d0, h0, w0;
+    tile_origin(tile, &n, &d0, &h0, &w0);
 #pragma unroll
-    for (int jj = 0; jj < 4; ++jj) {
-      const int ow = w0 + 4 * g + jj;
-      if (od < a.do_ && oh < a.ho && ow < a.wo) {
-        y[((((long long)(n * a.do_ + od) * a.ho + oh) * a.wo + ow) * C) + r16] = acc[r][jj];
-        s1 += acc[r][jj];
-        ++cntl;
+    for (int k = 0; k < N_X_PER; ++k) {
+      const int c = xc[k];
+      const int id = k7_src(d0 + (c & 255) - a.P, a.di, a.reflect), ih = k7_src(h0 + ((c >> 8) & 255) - a.P, a.hi, a.reflect),
+                iw = k7_src(w0 + (c >> 16) - a.P, a.wi, a.reflect);
+      const bool ok = c >= 0 && (id | ih | iw) >= 0;
+      xb[k] = x[ok ? ((n * a.di + id) * a.hi + ih) * a.wi + iw : 0];
+      if (!ok) xb[k] = 0.f;
+    }
+  };
+  // running BatchNorm statistics of this block (threads tid < 16, channel tid): Chan merge per tile
+  float run_n = 0.f, run_mean = 0.f, run_m2 = 0.f;
+  const int t0 = blockIdx.x * tiles_per_block, t1 = min(ntiles, t0 + tiles_per_block);
+  if (t0 < t1 && !(a.dbg & 4)) load(t0);
+  for (int tile = t0; tile < t1; ++tile) {
+    int n, d0, h0, w0;
+    tile_origin(tile, &n, &d0, &h0, &w0);
+    __syncthreads();  // previous tile's reads of us / red done
+#pragma unroll
+    for (int k = 0; k < N_X_PER; ++k) {
+      const int c = xc[k];
+      if (c >= 0) xs[((c & 255) * N_HH + ((c >> 8) & 255)) * N_HWP + (c >> 16)] = (__bf16)xb[k];
+    }
+    if (tile + 1 < t1 && !(a.dbg & 4)) load(tile + 1);  // in flight during this tile's MFMAs
+    __syncthreads();
+    if (!(a.dbg & 1)) for (int i = tid; i < N_ROWS * 2; i += 256) {  // unfold (row, half of ow): 8 shifted windows
+      const int r = i >> 1, hf = i & 1;
+      const u32x4 lo = *reinterpret_cast<const u32x4*>(xs + r * N_HWP + 8 * hf);
+      const u32x4 hi = *reinterpret_cast<const u32x4*>(xs + r * N_HWP + 8 * hf + 8);
+      const unsigned wv[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+#pragma unroll
+      for (int sft = 0; sft < 8; ++sft) {
+        u32x4 o;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const int m = sft / 2 + k;
+          o[k] = (sft & 1) ? __builtin_amdgcn_alignbyte(wv[m + 1], wv[m], 2) : wv[m];
+        }
+        *reinterpret_cast<u32x4*>(us + (r * N_TW + 8 * hf + sft) * 8) = o;
       }
     }
-  }
-  if (stats) {  // BatchNorm partials (sum, M2, count) per block, layout of conv.hip
-    __shared__ float red[4][C];
-    __shared__ float bmean[C];
-    __shared__ int bcnt;
-    s1 += __shfl_xor(s1, 16, 64);
-    s1 += __shfl_xor(s1, 32, 64);
-    if (tid == 0) bcnt = 0;
     __syncthreads();
-    if (r16 == 0) atomicAdd(&bcnt, cntl);  // count over the 4 g-groups of each wave
-    if (g == 0) red[wave][r16] = s1;
-    __syncthreads();
-    const long long sb = (long long)blockIdx.x * (2 * C + 1);
-    if (tid < C) {
-      const float S = red[0][tid] + red[1][tid] + red[2][tid] + red[3][tid];
-      bmean[tid] = bcnt ? S / bcnt : 0.f;
-      stats[sb + tid] = S;
+    f32x4 acc[N_TH];
+#pragma unroll
+    for (int r = 0; r < N_TH; ++r) acc[r] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const __bf16* ub = us + wave * N_HH * N_TW * 8;
+#pragma unroll
+    for (int ks = 0; ks < N_PAIRS / 4; ++ks) {
+      if (a.dbg & 2) break;
+      bf16x8_k av[N_TH];
+#pragma unroll
+      for (int r = 0; r < N_TH; ++r) av[r] = *reinterpret_cast<const bf16x8_k*>(ub + aoff[ks] + r * N_TW * 8);
+#pragma unroll
+      for (int r = 0; r < N_TH; ++r) acc[r] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[r], bv[ks], acc[r], 0, 0, 0);
     }
-    __syncthreads();
-    const float m = bmean[r16];
-    float q = 0.f;
+    // lane holds out[ow = 4g + jj][c = r16] of row r (oh = h0 + r, od = d0 + wave)
+    const int od = d0 + wave;
+    float s1 = 0.f;
+    int cntl = 0;
 #pragma unroll
     for (int r = 0; r < N_TH; ++r) {
       const int oh = h0 + r;
 #pragma unroll
       for (int jj = 0; jj < 4; ++jj) {
         const int ow = w0 + 4 * g + jj;
-        const float dv = (od < a.do_ && oh < a.ho && ow < a.wo) ? acc[r][jj] - m : 0.f;
-        q += dv * dv;
+        if (od < a.do_ && oh < a.ho && ow < a.wo) {
+          if (!(a.dbg & 8)) y[((((n * a.do_ + od) * a.ho + oh) * a.wo + ow) * C) + r16] = acc[r][jj];
+          s1 += acc[r][jj];
+          ++cntl;
+        }
       }
     }
-    q += __shfl_xor(q, 16, 64);
-    q += __shfl_xor(q, 32, 64);
-    __syncthreads();
-    if (g == 0) red[wave][r16] = q;
-    __syncthreads();
-    if (tid < C) stats[sb + C + tid] = red[0][tid] + red[1][tid] + red[2][tid] + red[3][tid];
-    if (tid == 0) stats[sb + 2 * C] = (float)bcnt;
+    if (stats) {  // tile (sum, M2 about the tile mean), merged into the block's running statistics
+      const int vd = min(N_TD, a.do_ - d0), vh = min(N_TH, a.ho - h0), vw = min(N_TW, a.wo - w0);
+      const float tn = (float)(vd * vh * vw);
+      s1 += __shfl_xor(s1, 16, 64);
+      s1 += __shfl_xor(s1, 32, 64);
+      if (g == 0) red[wave][r16] = s1;
+      __syncthreads();
+      const float tmean = (red[0][r16] + red[1][r16] + red[2][r16] + red[3][r16]) / tn;
+      float q = 0.f;
+#pragma unroll
+      for (int r = 0; r < N_TH; ++r) {
+        const int oh = h0 + r;
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) {
+          const int ow = w0 + 4 * g + jj;
+          const float dv = (od < a.do_ && oh < a.ho && ow < a.wo) ? acc[r][jj] - tmean : 0.f;
+          q += dv * dv;
+        }
+      }
+      q += __shfl_xor(q, 16, 64);
+      q += __shfl_xor(q, 32, 64);
+      __syncthreads();
+      if (g == 0) red[wave][r16] = q;
+      __syncthreads();
+      if (tid < C) {
+        const float tm2 = red[0][tid] + red[1][tid] + red[2][tid] + red[3][tid];
+        const float nn = run_n + tn, delta = tmean - run_mean;
+        run_mean += delta * (tn / nn);
+        run_m2 += tm2 + delta * delta * (run_n * tn / nn);
+        run_n = nn;
+      }
+    }
+    (void)cntl;
+  }
+  if (stats && tid < C) {  // BatchNorm partials (sum, M2, count) per block, layout of conv.hip
+    const long long sb = (long long)blockIdx.x * (2 * C + 1);
+    stats[sb + tid] = run_mean * run_n;
+    stats[sb + C + tid] = run_m2;
+    if (tid == 0) stats[sb + 2 * C] = run_n;
   }
 }
 
 // ---- w2n tile: 4 (d) x 4 (h) x 16 (w) outputs; the 4 waves split the 100 input rows; the 16
-// channels are staged in two halves of 8 (one 16-byte vector per halo voxel)
+// channels are staged in two halves of 8 (one 16-byte vector per halo voxel).  Persistent blocks:
+// the weight table is staged once per block and each half's halo is loaded into registers while
+// the previous half's MFMAs run.
 constexpr int W_TD = 4, W_TH = 4, W_TW = 16;
-constexpr int W_HD = W_TD + 6, W_HH = W_TH + 6, W_HW = 24;
+constexpr int W_HD = W_TD + 6, W_HH = W_TH + 6, W_HW = 24, W_HWU = W_TW + 6;
 constexpr int W_ROWS = W_HD * W_HH;  // 100
+constexpr int W_F4 = W_ROWS * W_HWU * 2, W_F4_PER = (W_F4 + 255) / 256;  // float4 per half
 
-__global__ __launch_bounds__(256) void k7m_w2n_kernel(K7Args a, const float* __restrict__ x,
-                                                      const float* __restrict__ w, float* __restrict__ y,
-                                                      const float* __restrict__ bias, int act,
-                                                      const float* __restrict__ minuend, float* __restrict__ out2) {
+__global__ __launch_bounds__(256, 2) void k7m_w2n_kernel(K7Args a, const float* __restrict__ x,
+                                                         const float* __restrict__ w, float* __restrict__ y,
+                                                         const float* __restrict__ bias, int act,
+                                                         const float* __restrict__ minuend, float* __restrict__ out2,
+                                                         int tiles_per_block, int ntiles) {
   constexpr int C = 16;
   __shared__ __attribute__((aligned(16))) __bf16 hs[W_ROWS * W_HW * 8];  // [row][iw][8 channels]
-  constexpr int WP = 8 * C + 8;  // (td, th) block of the weight table, padded: lanes of one B read
-                                 // hit 16 different blocks, 4 banks apart instead of 64
+  constexpr int WP = 8 * C + 8;  // (td, th) block of the weight table, padded
   __shared__ __attribute__((aligned(16))) __bf16 wt[49 * WP];           // [td*7+th][tw8][c]
   __shared__ float red[4][256];
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  int n, d0, h0, w0;
-  {
-    int bid = blockIdx.x;
-    const int tw_ = bid % a.tiles_w; bid /= a.tiles_w;
-    const int th_ = bid % a.tiles_h; bid /= a.tiles_h;
-    const int td_ = bid % a.tiles_d; n = bid / a.tiles_d;
-    d0 = td_ * W_TD; h0 = th_ * W_TH; w0 = tw_ * W_TW;
-  }
+  const int g = lane >> 4, r16 = lane & 15;
+  const int odl = r16 >> 2, ohl = r16 & 3;  // this lane's B column: output row (od, oh)
   k7m_stage<(49 * 8 * C + 255) / 256>(
       w, 49 * 8 * C,
       [&](int i) -> long long {
@@ -202,57 +248,100 @@ __global__ __launch_bounds__(256) void k7m_w2n_kernel(K7Args a, const float* __r
         return tw < K7 ? (long long)c * a.wc + p * K7 + tw : -1;
       },
       [&](int i, float v) { wt[(i >> 7) * WP + (i & 127)] = (__bf16)v; });
-  const int g = lane >> 4, r16 = lane & 15;
-  const int odl = r16 >> 2, ohl = r16 & 3;  // this lane's B column: output row (od, oh)
-  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-  for (int half = 0; half < 2; ++half) {
-    if (half) __syncthreads();  // all waves done reading the first half
-    k7m_stage<(W_ROWS * W_HW * 2 + 255) / 256>(
-        reinterpret_cast<const f32x4*>(x), W_ROWS * W_HW * 2,
-        [&](int i) -> long long {  // float4 index
-          const int q = i & 1, v = i >> 1, hw = v % W_HW, r = v / W_HW, hh = r % W_HH, hd = r / W_HH;
-          if (hw >= W_TW + 7) return -1;
-          const int id = k7_src(d0 + hd - a.P, a.di, a.reflect);
-          const int ih = k7_src(h0 + hh - a.P, a.hi, a.reflect);
-          const int iw = k7_src(w0 + hw - a.P, a.wi, a.reflect);
-          return (id | ih | iw) >= 0 ? (((long long)(n * a.di + id) * a.hi + ih) * a.wi + iw) * (C / 4) + half * 2 + q
-                                     : -1;
-        },
-        [&](int i, f32x4 val) {
-          __bf16* d = hs + (i >> 1) * 8 + 4 * (i & 1);
-          d[0] = (__bf16)val[0]; d[1] = (__bf16)val[1]; d[2] = (__bf16)val[2]; d[3] = (__bf16)val[3];
-        });
-    __syncthreads();
-#pragma unroll 1
-    for (int pr = wave * 25; pr < wave * 25 + 25; ++pr) {
-      const int id = pr / W_HH, ih = pr - id * W_HH;
-      const int td = id - odl, th = ih - ohl;
-      const bool band = td >= 0 && td < K7 && th >= 0 && th < K7;
-      const __bf16* wrow = wt + (band ? td * K7 + th : 0) * WP + half * 8;
-      const __bf16* hrow = hs + (pr * W_HW + r16) * 8;
+  for (int i = tid; i < W_ROWS * (W_HW - W_HWU) * 8; i += 256) {  // pad columns 22, 23: read with zero weights
+    const int r = i / ((W_HW - W_HWU) * 8), j = i % ((W_HW - W_HWU) * 8);
+    hs[(r * W_HW + W_HWU) * 8 + j] = (__bf16)0.f;
+  }
+  int hc[W_F4_PER];  // this thread's staged float4s: packed (hd, hh, hw, q), -1 past the halo
 #pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        const int tw = 4 * s + g;
-        const bf16x8_k av = *reinterpret_cast<const bf16x8_k*>(hrow + tw * 8);
-        bf16x8_k bv = *reinterpret_cast<const bf16x8_k*>(wrow + tw * C);
-        if (!band) bv = bf16x8_k{};
-        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, bv, acc, 0, 0, 0);
+  for (int k = 0; k < W_F4_PER; ++k) {
+    const int i = tid + 256 * k, q = i & 1, v = i >> 1, hw = v % W_HWU, r = v / W_HWU;
+    hc[k] = i < W_F4 ? ((r / W_HH) | ((r % W_HH) << 8) | (hw << 16) | (q << 24)) : -1;
+  }
+  f32x4 xv[W_F4_PER];
+  auto tile_origin = [&](int tile, int* n, int* d0, int* h0, int* w0) {
+    int r = tile;
+    const int tw_ = r % a.tiles_w; r /= a.tiles_w;
+    const int th_ = r % a.tiles_h; r /= a.tiles_h;
+    const int td_ = r % a.tiles_d; *n = r / a.tiles_d;
+    *d0 = td_ * W_TD; *h0 = th_ * W_TH; *w0 = tw_ * W_TW;
+  };
+  auto load = [&](int tile, int half) {
+    int n, d0, h0, w0;
+    tile_origin(tile, &n, &d0, &h0, &w0);
+    const f32x4* xp = reinterpret_cast<const f32x4*>(x);
+#pragma unroll
+    for (int k = 0; k < W_F4_PER; ++k) {
+      const int c = hc[k];
+      const int id = k7_src(d0 + (c & 255) - a.P, a.di, a.reflect),
+                ih = k7_src(h0 + ((c >> 8) & 255) - a.P, a.hi, a.reflect),
+                iw = k7_src(w0 + ((c >> 16) & 255) - a.P, a.wi, a.reflect);
+      const bool ok = c >= 0 && (id | ih | iw) >= 0;
+      xv[k] = xp[ok ? (((n * a.di + id) * a.hi + ih) * a.wi + iw) * (C / 4) + half * 2 + (c >> 24) : 0];
+      if (!ok) xv[k] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+  };
+  auto store = [&]() {
+#pragma unroll
+    for (int k = 0; k < W_F4_PER; ++k) {
+      const int c = hc[k];
+      if (c < 0) continue;
+      const int row = (c & 255) * W_HH + ((c >> 8) & 255);
+      bf16x4_k u;
+      u[0] = (__bf16)xv[k][0]; u[1] = (__bf16)xv[k][1]; u[2] = (__bf16)xv[k][2]; u[3] = (__bf16)xv[k][3];
+      *reinterpret_cast<bf16x4_k*>(hs + (row * W_HW + ((c >> 16) & 255)) * 8 + 4 * (c >> 24)) = u;
+    }
+  };
+  const int t0 = blockIdx.x * tiles_per_block, t1 = min(ntiles, t0 + tiles_per_block);
+  if (t0 < t1 && !(a.dbg & 2)) load(t0, 0);
+  for (int tile = t0; tile < t1; ++tile) {
+    f32x4 acc[2];  // independent accumulators: back-to-back MFMAs do not wait on each other
+#pragma unroll
+    for (int q = 0; q < 2; ++q) acc[q] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int half = 0; half < 2; ++half) {
+      __syncthreads();  // every wave done reading hs (and red) of the previous half / tile
+      if (!(a.dbg & 4)) store();
+      if (a.dbg & 2) {}
+      else if (half == 0) load(tile, 1);
+      else if (tile + 1 < t1) load(tile + 1, 0);
+      __syncthreads();
+      if (!(a.dbg & 1))
+#pragma unroll 5
+      for (int prl = 0; prl < 25; ++prl) {
+        const int pr = wave * 25 + prl;
+        const int id = pr / W_HH, ih = pr - id * W_HH;
+        const int td = id - odl, th = ih - ohl;
+        const bool band = td >= 0 && td < K7 && th >= 0 && th < K7;
+        const __bf16* wrow = wt + (band ? td * K7 + th : 0) * WP + half * 8;
+        const __bf16* hrow = hs + (pr * W_HW + r16) * 8;
+#pragma unroll
+        for (int sq = 0; sq < 2; ++sq) {
+          const int tw = 4 * sq + g;
+          const bf16x8_k av = *reinterpret_cast<const bf16x8_k*>(hrow + tw * 8);
+          bf16x8_k bv = *reinterpret_cast<const bf16x8_k*>(wrow + tw * C);
+          if (!band) bv = bf16x8_k{};
+          acc[sq] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, bv, acc[sq], 0, 0, 0);
+        }
       }
     }
-  }
-  // combine the 4 waves: lane holds out[ow = 4g + jj][(od, oh) = r16]
+    acc[0] += acc[1];
+    // combine the 4 waves: lane holds out[ow = 4g + jj][(od, oh) = r16]
 #pragma unroll
-  for (int jj = 0; jj < 4; ++jj) red[wave][(4 * g + jj) * 16 + r16] = acc[jj];
-  __syncthreads();
-  {
+    for (int jj = 0; jj < 4; ++jj) red[wave][(4 * g + jj) * 16 + r16] = acc[0][jj];
+    __syncthreads();
+    int n, d0, h0, w0;
+    tile_origin(tile, &n, &d0, &h0, &w0);
     const int m = tid >> 4, nn = tid & 15;  // ow_l = m, (odl, ohl) = nn
     const int od = d0 + (nn >> 2), oh = h0 + (nn & 3), ow = w0 + m;
     if (od < a.do_ && oh < a.ho && ow < a.wo) {
       float v = red[0][tid] + red[1][tid] + red[2][tid] + red[3][tid] + (bias ? bias[0] : 0.f);
       if (act == CGAN3D_ACT_TANH) v = tanhf(v);
-      const long long o = ((long long)(n * a.do_ + od) * a.ho + oh) * a.wo + ow;
+      const int o = ((n * a.do_ + od) * a.ho + oh) * a.wo + ow;
+      if (!(a.dbg & 8)) {
       y[o] = v;
       if (out2) out2[o] = minuend[o] - v;
+      }
     }
   }
 }
@@ -482,23 +571,34 @@ static K7Args k7m_args(const cgan3d_conv_geom* g, int P, int reflect, int flip, 
   return a;
 }
 
+static void k7m_n2w_split(const K7Args& a, int* grid, int* per, int* ntiles) {
+  *ntiles = a.n * a.tiles_d * a.tiles_h * a.tiles_w;
+  *per = (*ntiles + 511) / 512;
+  *grid = (*ntiles + *per - 1) / *per;
+}
+
 long long k7m_n2w_blocks(const cgan3d_conv_geom* g) {
   const K7Args a = k7m_args(g, 0, 0, 0, 0, N_TD, N_TH, N_TW);
-  return (long long)a.n * a.tiles_d * a.tiles_h * a.tiles_w;
+  int grid, per, nt;
+  k7m_n2w_split(a, &grid, &per, &nt);
+  return grid;
 }
 
 void k7m_n2w_launch(const cgan3d_conv_geom* g, int P, int reflect, int flip, long long wc, const float* x,
                     const float* w, float* y, float* stats, hipStream_t s) {
   const K7Args a = k7m_args(g, P, reflect, flip, wc, N_TD, N_TH, N_TW);
-  hipLaunchKernelGGL(k7m_n2w_kernel, dim3((unsigned)(a.n * a.tiles_d * a.tiles_h * a.tiles_w)), dim3(256), 0, s, a,
-                     x, w, y, stats);
+  int grid, per, nt;
+  k7m_n2w_split(a, &grid, &per, &nt);
+  hipLaunchKernelGGL(k7m_n2w_kernel, dim3(grid), dim3(256), 0, s, a, x, w, y, stats, per, nt);
 }
 
 void k7m_w2n_launch(const cgan3d_conv_geom* g, int P, int reflect, long long wc, const float* x, const float* w,
                     float* y, const Epi& e, hipStream_t s) {
   const K7Args a = k7m_args(g, P, reflect, 0, wc, W_TD, W_TH, W_TW);
-  hipLaunchKernelGGL(k7m_w2n_kernel, dim3((unsigned)(a.n * a.tiles_d * a.tiles_h * a.tiles_w)), dim3(256), 0, s, a,
-                     x, w, y, e.bias, e.act, e.minuend, e.out2);
+  int grid, per, nt;
+  k7m_n2w_split(a, &grid, &per, &nt);
+  hipLaunchKernelGGL(k7m_w2n_kernel, dim3(grid), dim3(256), 0, s, a, x, w, y, e.bias, e.act, e.minuend, e.out2, per,
+                     nt);
 }
 
 long long k7m_wgrad_ws_floats(const cgan3d_conv_geom* g) {
