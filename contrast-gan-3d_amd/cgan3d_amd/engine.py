@@ -133,7 +133,10 @@ class GeneratorPlan:
             return torch.empty((n, *dd, c), device=device, dtype=torch.float32)
 
         self.geo_fwd, self.geo_dgrad, self.geo_wgrad, self.wf, self.wd = [], [], [], [], []
-        self.z, self.y, self.dy, self.dz, self.stats, self.ss, self.mi, self.nstat = [], [], [], [], [], [], [], []
+        self.z, self.y, self.dy, self.dz, self.ss, self.mi = [], [], [], [], [], []
+        # fused BatchNorm accumulators, fp64: [layer][forward | backward][2 * 64]
+        self.bn_acc = torch.zeros((len(layers), 2, 128), device=device, dtype=torch.float64)
+        self.bn_fwd, self.bn_bwd = [], []
         ws = 0
         for ly in layers:
             if ly.kind == "conv":
@@ -157,9 +160,9 @@ class GeneratorPlan:
             self.y.append(buf(ly.dout, ly.cout))
             self.dy.append(buf(ly.dout, ly.cout))
             self.dz.append(buf(ly.dout, ly.cout))
-            ns = ops.stats_floats(gf)
-            self.nstat.append(ns // (2 * ly.cout + 1))
-            self.stats.append(torch.empty(ns, device=device))
+            li = len(self.bn_fwd)
+            self.bn_fwd.append(self.bn_acc[li, 0, :2 * ly.cout])
+            self.bn_bwd.append(self.bn_acc[li, 1, :2 * ly.cout])
             self.ss.append(torch.empty(2 * ly.cout, device=device))
             self.mi.append(torch.empty(2 * ly.cout, device=device))
             nvox = n * ly.dout[0] * ly.dout[1] * ly.dout[2]
@@ -197,31 +200,42 @@ class GeneratorPlan:
         self.packs.pack()
 
     # -- forward: x [n,D,H,W,1] -> att (tanh output); opt_hat_out = x - att (Trainer.py:170-171)
+    # Training-mode BatchNorm statistics are fused: each conv's epilogue accumulates the per-channel
+    # (sum, sum of squares) of its output in fp64 (bn_fwd[i]), bn_apply_acc turns them into
+    # scale/shift; backward, the kernel that produces dL/dy of a BatchNorm layer accumulates
+    # (sum g, sum g*xhat) into bn_bwd[i] for bn_backward_acc.  One memset per step zeroes both.
     def forward(self, P: Dict[str, torch.Tensor], x: torch.Tensor, opt_hat_out: Optional[torch.Tensor] = None,
                 training: bool = True):
         h = x
         h_res = None
+        if training:
+            self.bn_acc.zero_()
         for i, ly in enumerate(self.layers):
             if ly.name.endswith("block0"):
                 h_res = h
-            stats = self.stats[i] if training else None
-            ops.conv(self.geo_fwd[i], h, self.wf[i], self.z[i], ops.epilogue(stats=stats))
             nb = f"{ly.name}.normalization"
-            if training:
-                ops.bn_finalize(self.stats[i], self.nstat[i], ly.cout, P[f"{nb}.weight"], P[f"{nb}.bias"],
-                                P[f"{nb}.running_mean"], P[f"{nb}.running_var"], P[f"{nb}.num_batches_tracked"],
-                                self.ss[i], self.mi[i])
-            else:
-                self._eval_scale_shift(P, nb, i)
             nvox = self.n * ly.dout[0] * ly.dout[1] * ly.dout[2]
-            ops.bn_apply(self.z[i], nvox, ly.cout, self.ss[i], ly.act, self.y[i],
-                         residual=h_res if ly.residual else None)
+            res = h_res if ly.residual else None
+            if training:
+                ops.conv(self.geo_fwd[i], h, self.wf[i], self.z[i], ops.epilogue(bn_sum=self.bn_fwd[i]))
+                ops.bn_apply_acc(self.z[i], nvox, ly.cout, self.bn_fwd[i], P[f"{nb}.weight"], P[f"{nb}.bias"],
+                                 P[f"{nb}.running_mean"], P[f"{nb}.running_var"], P[f"{nb}.num_batches_tracked"],
+                                 ly.act, self.y[i], self.ss[i], self.mi[i], residual=res)
+            else:
+                ops.conv(self.geo_fwd[i], h, self.wf[i], self.z[i])
+                self._eval_scale_shift(P, nb, i)
+                ops.bn_apply(self.z[i], nvox, ly.cout, self.ss[i], ly.act, self.y[i], residual=res)
             h = self.y[i]
         la = self.last
         ep = ops.epilogue(bias=P["model.last_conv.bias"], act=L.ACT_TANH,
                           minuend=x if opt_hat_out is not None else None, out2=opt_hat_out)
         ops.conv(self.geo_last_fwd, h, P["model.last_conv.weight"], self.att, ep)
         return self.att
+
+    def _bn_grad_epi(self, i):
+        """Epilogue that accumulates BatchNorm layer i's backward statistics from its dL/dy."""
+        return ops.epilogue(bn_gsum=self.bn_bwd[i], bn_z=self.z[i], bn_ss=self.ss[i], bn_mi=self.mi[i],
+                            bn_act=self.layers[i].act)
 
     def _eval_scale_shift(self, P, nb, i):
         # eval-mode BN (Trainer.validate, Trainer.py:248-249): running statistics
@@ -242,13 +256,13 @@ class GeneratorPlan:
         nvl = n * la.dout[0] * la.dout[1] * la.dout[2]
         ops.channel_sum(self.dz_last, nvl, 1, G["model.last_conv.bias"], self.ws)
         ops.conv(self.geo_last_dgrad, self.dz_last, P["model.last_conv.weight"], self.dpad)
-        ops.reflect_fold(self.dpad, self.dy[-1], n, la.din, la.cin, la.p)
+        ops.reflect_fold(self.dpad, self.dy[-1], n, la.din, la.cin, la.p, ep=self._bn_grad_epi(len(self.layers) - 1))
         for i in range(len(self.layers) - 1, -1, -1):
             ly = self.layers[i]
             nb = f"{ly.name}.normalization"
             nvox = n * ly.dout[0] * ly.dout[1] * ly.dout[2]
-            ops.bn_backward(self.dy[i], self.z[i], nvox, ly.cout, self.ss[i], self.mi[i], P[f"{nb}.weight"], ly.act,
-                            G[f"{nb}.weight"], G[f"{nb}.bias"], self.dz[i], self.ws)
+            ops.bn_backward_acc(self.dy[i], self.z[i], nvox, ly.cout, self.bn_bwd[i], self.ss[i], self.mi[i],
+                                P[f"{nb}.weight"], ly.act, G[f"{nb}.weight"], G[f"{nb}.bias"], self.dz[i])
             xin = self.y[i - 1] if i > 0 else x
             wname = f"{ly.name}.conv.weight"
             if ly.kind == "convt":  # ConvTranspose3d: the output-grad is the gathered operand
@@ -261,7 +275,9 @@ class GeneratorPlan:
                 break
             # input-grad; a ResNet block0 also receives the skip gradient dL/dh_{r+1}
             res = self.dy[i + 1] if ly.name.endswith("block0") else None
-            ops.conv(self.geo_dgrad[i], self.dz[i], self.wd[i], self.dy[i - 1], ops.epilogue(residual=res))
+            ep = self._bn_grad_epi(i - 1)
+            ep.residual = res
+            ops.conv(self.geo_dgrad[i], self.dz[i], self.wd[i], self.dy[i - 1], ep)
         if self.side is not None:  # the weight gradients are complete before anything reads them
             torch.cuda.current_stream(self.device).wait_stream(self.side)
 

@@ -118,7 +118,7 @@ class PackSet:
             return with_prec(g, prec), w
         gp = with_packing(g, prec)
         wp = torch.zeros(packed_weight_floats(gp), device=self.device)
-        self.descs.append((pack_desc(gp, w, wp), wp))
+        self.descs.append((pack_desc(gp, w, wp), wp, w))  # keeps the source alive: the descriptor holds its pointer
         self.max_total = max(self.max_total, packed_elements(gp))
         self.dev = None
         return gp, wp
@@ -127,7 +127,7 @@ class PackSet:
         if not self.descs:
             return
         if self.dev is None:
-            raw = b"".join(bytes(d) for d, _ in self.descs)
+            raw = b"".join(bytes(d[0]) for d in self.descs)
             self.dev = torch.frombuffer(bytearray(raw), dtype=torch.uint8).to(self.device)
         pack_weights_multi(self.dev, len(self.descs), self.max_total)
 
@@ -170,16 +170,31 @@ class Epi:
     """Fused-epilogue operands (include/cgan3d.h cgan3d_epilogue), kept as tensors for checks."""
 
     def __init__(self, bias=None, residual=None, mask_src=None, minuend=None, out2=None, stats=None,
-                 act=L.ACT_NONE, slope=0.0):
+                 act=L.ACT_NONE, slope=0.0, bn_sum=None, bn_gsum=None, bn_z=None, bn_ss=None, bn_mi=None,
+                 bn_act=L.ACT_NONE, bn_slope=0.0):
         self.bias, self.residual, self.mask_src = bias, residual, mask_src
         self.minuend, self.out2, self.stats = minuend, out2, stats
         self.act, self.slope = act, float(slope)
+        # fused BatchNorm statistics (fp64 accumulators, caller-zeroed): see include/cgan3d.h
+        self.bn_sum, self.bn_gsum, self.bn_z, self.bn_ss, self.bn_mi = bn_sum, bn_gsum, bn_z, bn_ss, bn_mi
+        self.bn_act, self.bn_slope = bn_act, float(bn_slope)
+
+    def check_bn(self, nout, c, what):
+        for nm in ("bn_sum", "bn_gsum"):
+            if getattr(self, nm) is not None:
+                _need(getattr(self, nm), 2 * c, f"{what} {nm}", dtype=torch.float64)
+        if self.bn_gsum is not None:
+            _need(self.bn_z, nout, f"{what} bn_z")
+            _need(self.bn_ss, 2 * c, f"{what} bn_ss")
+            _need(self.bn_mi, 2 * c, f"{what} bn_mi")
 
     def c(self) -> Epilogue:
         e = Epilogue()
         e.bias, e.residual, e.mask_src = ptr(self.bias), ptr(self.residual), ptr(self.mask_src)
         e.minuend, e.out2, e.stats = ptr(self.minuend), ptr(self.out2), ptr(self.stats)
         e.act, e.slope = self.act, self.slope
+        e.bn_sum, e.bn_gsum, e.bn_z = ptr(self.bn_sum), ptr(self.bn_gsum), ptr(self.bn_z)
+        e.bn_ss, e.bn_mi, e.bn_act, e.bn_slope = ptr(self.bn_ss), ptr(self.bn_mi), self.bn_act, self.bn_slope
         return e
 
 
@@ -258,6 +273,7 @@ def conv(g: ConvGeom, x: torch.Tensor, w: torch.Tensor, y: torch.Tensor, ep: Opt
                 _need(getattr(ep, nm), ny, f"conv {nm}")
         if ep.stats is not None:
             _need(ep.stats, stats_floats(g), "conv stats", exact=False)
+        ep.check_bn(ny, g.cout, "conv")
     check(_timed("conv", g, "cgan3d_conv3d_fwd", ctypes.byref(g), ptr(x), ptr(w), ptr(y),
                  ctypes.byref(ep.c()) if ep is not None else None), "conv3d_fwd")
 
@@ -298,6 +314,43 @@ def bn_apply(z, nvox, c, scale_shift, act, y, residual=None, slope=0.0):
           "bn_apply")
 
 
+def bn_apply_acc(z, nvox, c, bn_sum, gamma, beta, rmean, rvar, nbt, act, y, scale_shift, mean_invstd,
+                 residual=None, slope=0.0, momentum=0.1, eps=1e-5):
+    """BatchNorm forward from the fused fp64 (sum, sum of squares) of the producing conv."""
+    _need(z, nvox * c, "bn_apply_acc z")
+    _need(y, nvox * c, "bn_apply_acc y")
+    _need(bn_sum, 2 * c, "bn_apply_acc bn_sum", dtype=torch.float64)
+    for t, nm in ((gamma, "gamma"), (beta, "beta")):
+        _need(t, c, f"bn_apply_acc {nm}")
+    for t, nm in ((rmean, "running_mean"), (rvar, "running_var")):
+        if t is not None:
+            _need(t, c, f"bn_apply_acc {nm}")
+    if nbt is not None:
+        _need(nbt, 1, "bn_apply_acc num_batches_tracked", dtype=torch.int64)
+    _need(scale_shift, 2 * c, "bn_apply_acc scale_shift")
+    _need(mean_invstd, 2 * c, "bn_apply_acc mean_invstd")
+    if residual is not None:
+        _need(residual, nvox * c, "bn_apply_acc residual")
+    check(_launch("cgan3d_bn_apply_acc", ptr(z), nvox, c, ptr(bn_sum), ptr(gamma), ptr(beta), ptr(rmean), ptr(rvar),
+                  ptr(nbt), momentum, eps, act, slope, ptr(residual), ptr(y), ptr(scale_shift), ptr(mean_invstd)),
+          "bn_apply_acc")
+
+
+def bn_backward_acc(dy, z, nvox, c, bn_gsum, scale_shift, mean_invstd, gamma, act, dgamma, dbeta, dz, slope=0.0,
+                    accumulate=False):
+    """BatchNorm backward from the fused fp64 (sum g, sum g*xhat) of the kernel that produced dy."""
+    for t, nm in ((dy, "dy"), (z, "z"), (dz, "dz")):
+        _need(t, nvox * c, f"bn_backward_acc {nm}")
+    _need(bn_gsum, 2 * c, "bn_backward_acc bn_gsum", dtype=torch.float64)
+    for t, nm in ((scale_shift, "scale_shift"), (mean_invstd, "mean_invstd")):
+        _need(t, 2 * c, f"bn_backward_acc {nm}")
+    for t, nm in ((gamma, "gamma"), (dgamma, "dgamma"), (dbeta, "dbeta")):
+        _need(t, c, f"bn_backward_acc {nm}")
+    check(_launch("cgan3d_bn_backward_acc", ptr(dy), ptr(z), nvox, c, ptr(bn_gsum), ptr(scale_shift),
+                  ptr(mean_invstd), ptr(gamma), act, slope, ptr(dgamma), ptr(dbeta), ptr(dz), int(accumulate)),
+          "bn_backward_acc")
+
+
 def bn_backward_ws_floats(nvox, c) -> int:
     return int(L.load().cgan3d_bn_backward_ws_floats(nvox, c))
 
@@ -326,11 +379,17 @@ def channel_sum(x, nvox, c, out, ws):
     check(_launch("cgan3d_channel_sum", ptr(x), nvox, c, ptr(out), ptr(ws)), "channel_sum")
 
 
-def reflect_fold(padded, out, n, dims: Sequence[int], c, pad):
+def reflect_fold(padded, out, n, dims: Sequence[int], c, pad, ep: Optional[Epi] = None):
+    """Adjoint of reflection padding; ``ep.bn_gsum`` adds the fused BatchNorm backward statistics."""
     d, h, w = dims
     _need(padded, n * (d + 2 * pad) * (h + 2 * pad) * (w + 2 * pad) * c, "reflect_fold padded")
     _need(out, n * d * h * w * c, "reflect_fold out")
-    check(_launch("cgan3d_reflect_fold", ptr(padded), ptr(out), n, d, h, w, c, pad), "reflect_fold")
+    if ep is None:
+        check(_launch("cgan3d_reflect_fold", ptr(padded), ptr(out), n, d, h, w, c, pad), "reflect_fold")
+        return
+    ep.check_bn(n * d * h * w * c, c, "reflect_fold")
+    check(_launch("cgan3d_reflect_fold_ex", ptr(padded), ptr(out), n, d, h, w, c, pad, ctypes.byref(ep.c())),
+          "reflect_fold_ex")
 
 
 def gp_interpolate(real, fake, eps, out, b, per_sample):

@@ -74,12 +74,6 @@ __device__ __forceinline__ float act_f(float v, int act, float slope) {
   return v;
 }
 
-__device__ __forceinline__ float act_grad(float pre, int act, float slope) {
-  if (act == CGAN3D_ACT_RELU) return pre > 0.f ? 1.f : 0.f;
-  if (act == CGAN3D_ACT_LRELU) return pre > 0.f ? 1.f : slope;
-  return 1.f;
-}
-
 // y = act(z*scale + shift) (+ residual); C % 4 == 0, float4 vectorised grid-stride.  With
 // 256 % (C/4) == 0 the grid stride is a multiple of C/4, so a thread keeps its 4 channels (and
 // their scale/shift in registers) for the whole loop.
@@ -197,6 +191,99 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const float* __restri
   }
 }
 
+// ---- fused-statistics path: the sums come from the producing kernel's epilogue (fp64 atomics)
+
+// (scale, shift, mean, invstd) of channel c from the fp64 (sum, sum of squares) over n values
+__device__ __forceinline__ void bn_coeffs(const double* sum, int C, int c, double n, const float* gamma,
+                                          const float* beta, float eps, double* mean, double* var, float* sc,
+                                          float* sf, float* inv) {
+  const double m = sum[c] / n;
+  const double v = fmax(sum[C + c] / n - m * m, 0.0);
+  const double is = 1.0 / sqrt(v + (double)eps);
+  const double s = (double)gamma[c] * is;
+  *mean = m;
+  *var = v;
+  *sc = (float)s;
+  *sf = (float)((double)beta[c] - m * s);
+  *inv = (float)is;
+}
+
+__global__ __launch_bounds__(256) void bn_apply_acc_kernel(const float* __restrict__ z, long long n4, int C,
+                                                           const double* __restrict__ sum, double nvox,
+                                                           const float* __restrict__ gamma,
+                                                           const float* __restrict__ beta, float* rmean, float* rvar,
+                                                           long long* nbt, float momentum, float eps, int act,
+                                                           float slope, const float* __restrict__ res,
+                                                           float* __restrict__ y, float* ss_out, float* mi_out) {
+  const int C4 = C >> 2;
+  const int c = (threadIdx.x % C4) * 4;
+  f32x4 sc, sf;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    double mean, var;
+    float inv, s0, s1;
+    bn_coeffs(sum, C, c + e, nvox, gamma, beta, eps, &mean, &var, &s0, &s1, &inv);
+    sc[e] = s0;
+    sf[e] = s1;
+    if (blockIdx.x == 0 && threadIdx.x < C4) {  // one writer per channel
+      ss_out[c + e] = sc[e];
+      ss_out[C + c + e] = sf[e];
+      mi_out[c + e] = (float)mean;
+      mi_out[C + c + e] = inv;
+      if (rmean) rmean[c + e] = (float)((1.0 - momentum) * rmean[c + e] + momentum * mean);
+      if (rvar) rvar[c + e] = (float)((1.0 - momentum) * rvar[c + e] + momentum * var * nvox / (nvox > 1 ? nvox - 1 : 1));
+    }
+  }
+  if (nbt && blockIdx.x == 0 && threadIdx.x == 0) *nbt += 1;
+  const f32x4* z4 = reinterpret_cast<const f32x4*>(z);
+  const f32x4* r4 = reinterpret_cast<const f32x4*>(res);
+  f32x4* y4 = reinterpret_cast<f32x4*>(y);
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (long long)gridDim.x * blockDim.x) {
+    f32x4 v = z4[i];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[e] = act_f(v[e] * sc[e] + sf[e], act, slope);
+    if (res) v += r4[i];
+    y4[i] = v;
+  }
+}
+
+__global__ __launch_bounds__(256) void bn_bwd_acc_kernel(const float* __restrict__ dy, const float* __restrict__ z,
+                                                         long long n4, int C, const double* __restrict__ gsum,
+                                                         double nvox, const float* __restrict__ ss,
+                                                         const float* __restrict__ mi, const float* __restrict__ gamma,
+                                                         int act, float slope, float* dgamma, float* dbeta,
+                                                         int accumulate, float* __restrict__ dz) {
+  const int C4 = C >> 2;
+  const int c = (threadIdx.x % C4) * 4;
+  f32x4 sc, sf, mean, inv, k0, k1, k2;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    sc[e] = ss[c + e]; sf[e] = ss[C + c + e]; mean[e] = mi[c + e]; inv[e] = mi[C + c + e];
+    k0[e] = gamma[c + e] * inv[e];
+    k1[e] = (float)(gsum[c + e] / nvox);
+    k2[e] = (float)(gsum[C + c + e] / nvox);
+    if (blockIdx.x == 0 && threadIdx.x < C4) {
+      const float db = (float)gsum[c + e], dg = (float)gsum[C + c + e];
+      if (dbeta) dbeta[c + e] = accumulate ? dbeta[c + e] + db : db;
+      if (dgamma) dgamma[c + e] = accumulate ? dgamma[c + e] + dg : dg;
+    }
+  }
+  const f32x4* z4 = reinterpret_cast<const f32x4*>(z);
+  const f32x4* d4 = reinterpret_cast<const f32x4*>(dy);
+  f32x4* o4 = reinterpret_cast<f32x4*>(dz);
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (long long)gridDim.x * blockDim.x) {
+    const f32x4 zz = z4[i], dd = d4[i];
+    f32x4 o;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float g = dd[e] * act_grad(zz[e] * sc[e] + sf[e], act, slope);
+      const float xh = (zz[e] - mean[e]) * inv[e];
+      o[e] = k0[e] * (g - k1[e] - xh * k2[e]);
+    }
+    o4[i] = o;
+  }
+}
+
 __global__ __launch_bounds__(256) void channel_sum_kernel(const float* __restrict__ x, long long total, int C,
                                                           float* part) {
   __shared__ float r0[256];
@@ -258,6 +345,38 @@ extern "C" int cgan3d_bn_apply(const float* z, int64_t nvox, int32_t c, const fl
   hipLaunchKernelGGL(bn_apply_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, z, n4, c, scale_shift, act,
                      slope, residual, y);
   CG_LAUNCH_CHECK("bn_apply_kernel");
+  return CGAN3D_OK;
+}
+
+extern "C" int cgan3d_bn_apply_acc(const float* z, int64_t nvox, int32_t c, const double* bn_sum, const float* gamma,
+                                   const float* beta, float* running_mean, float* running_var,
+                                   int64_t* num_batches_tracked, float momentum, float eps, int32_t act, float slope,
+                                   const float* residual, float* y, float* scale_shift, float* mean_invstd,
+                                   void* stream) {
+  CG_CHECK_ARG(z && bn_sum && gamma && beta && y && scale_shift && mean_invstd, "cgan3d_bn_apply_acc: null pointer");
+  CG_CHECK_ARG(nvox > 0 && c > 0 && c % 4 == 0 && 256 % (c / 4) == 0,
+               "cgan3d_bn_apply_acc: channels must be a multiple of 4 dividing 1024");
+  const long long n4 = (long long)nvox * c / 4;
+  int blocks = (int)std::min<long long>((n4 + 255) / 256, 4096);
+  hipLaunchKernelGGL(bn_apply_acc_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, z, n4, c, bn_sum,
+                     (double)nvox, gamma, beta, running_mean, running_var, (long long*)num_batches_tracked, momentum,
+                     eps, act, slope, residual, y, scale_shift, mean_invstd);
+  CG_LAUNCH_CHECK("bn_apply_acc_kernel");
+  return CGAN3D_OK;
+}
+
+extern "C" int cgan3d_bn_backward_acc(const float* dy, const float* z, int64_t nvox, int32_t c, const double* bn_gsum,
+                                      const float* scale_shift, const float* mean_invstd, const float* gamma,
+                                      int32_t act, float slope, float* dgamma, float* dbeta, float* dz,
+                                      int32_t accumulate, void* stream) {
+  CG_CHECK_ARG(dy && z && bn_gsum && scale_shift && mean_invstd && gamma && dz, "cgan3d_bn_backward_acc: null pointer");
+  CG_CHECK_ARG(nvox > 1 && c > 0 && c % 4 == 0 && 256 % (c / 4) == 0,
+               "cgan3d_bn_backward_acc: channels must be a multiple of 4 dividing 1024");
+  const long long n4 = (long long)nvox * c / 4;
+  int blocks = (int)std::min<long long>((n4 + 255) / 256, 4096);
+  hipLaunchKernelGGL(bn_bwd_acc_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, dy, z, n4, c, bn_gsum,
+                     (double)nvox, scale_shift, mean_invstd, gamma, act, slope, dgamma, dbeta, accumulate, dz);
+  CG_LAUNCH_CHECK("bn_bwd_acc_kernel");
   return CGAN3D_OK;
 }
 

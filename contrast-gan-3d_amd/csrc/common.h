@@ -76,7 +76,34 @@ struct Epi {
   float* stats;
   int act;
   float slope;
+  double* bn_sum;
+  double* bn_gsum;
+  const float* bn_z;
+  const float* bn_ss;
+  const float* bn_mi;
+  int bn_act;
+  float bn_slope;
 };
+
+__device__ __forceinline__ float act_grad(float pre, int act, float slope) {
+  if (act == CGAN3D_ACT_RELU) return pre > 0.f ? 1.f : 0.f;
+  if (act == CGAN3D_ACT_LRELU) return pre > 0.f ? 1.f : slope;
+  return 1.f;
+}
+
+// The fused BatchNorm statistic pair of an epilogue value v at output element o, channel c (C
+// channels): (v, v^2) for bn_sum, (g, g*xhat) of the layer whose dL/dy is v for bn_gsum.
+__device__ __forceinline__ void bn_pair(const Epi& e, float v, long long o, int c, int C, float* p1, float* p2) {
+  if (e.bn_sum) {
+    *p1 += v;
+    *p2 += v * v;
+  } else {
+    const float z = e.bn_z[o];
+    const float gg = v * act_grad(z * e.bn_ss[c] + e.bn_ss[C + c], e.bn_act, e.bn_slope);
+    *p1 += gg;
+    *p2 += gg * (z - e.bn_mi[c]) * e.bn_mi[C + c];
+  }
+}
 
 // specialised k = 7 generator first/last conv kernels (conv_k7.hip); return 1 when they apply
 int k7_try_fwd(const cgan3d_conv_geom* g, const float* x, const float* w, float* y, const Epi& e, hipStream_t s);
@@ -88,7 +115,7 @@ void k7m_wgrad_launch(const cgan3d_conv_geom* g, bool wide_in, long long wc, con
 long long k7_n2w_blocks(const cgan3d_conv_geom* g);
 long long k7m_n2w_blocks(const cgan3d_conv_geom* g);
 void k7m_n2w_launch(const cgan3d_conv_geom* g, int P, int reflect, int flip, long long wc, const float* x,
-                    const float* w, float* y, float* stats, hipStream_t s);
+                    const float* w, float* y, float* stats, double* bn_sum, hipStream_t s);
 void k7m_w2n_launch(const cgan3d_conv_geom* g, int P, int reflect, long long wc, const float* x, const float* w,
                     float* y, const Epi& e, hipStream_t s);
 // implicit-GEMM forward / input-grad (conv_gemm.hip)

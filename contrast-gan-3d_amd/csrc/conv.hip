@@ -404,6 +404,8 @@ static Epi to_epi(const cgan3d_epilogue* ep) {
   if (ep) {
     e.bias = ep->bias; e.residual = ep->residual; e.mask_src = ep->mask_src; e.minuend = ep->minuend;
     e.out2 = ep->out2; e.stats = ep->stats; e.act = ep->act; e.slope = ep->slope;
+    e.bn_sum = ep->bn_sum; e.bn_gsum = ep->bn_gsum; e.bn_z = ep->bn_z; e.bn_ss = ep->bn_ss; e.bn_mi = ep->bn_mi;
+    e.bn_act = ep->bn_act; e.bn_slope = ep->bn_slope;
   }
   return e;
 }
@@ -424,6 +426,9 @@ extern "C" int cgan3d_conv3d_fwd(const cgan3d_conv_geom* g, const float* x, cons
   CG_CHECK_ARG(x && w && y, "cgan3d_conv3d_fwd: null pointer");
   Epi e = to_epi(ep);
   CG_CHECK_ARG(!(e.out2 && (!e.minuend || g->cout != 1)), "cgan3d_conv3d_fwd: out2 needs minuend and cout==1");
+  CG_CHECK_ARG(!(e.bn_sum && e.bn_gsum), "cgan3d_conv3d_fwd: bn_sum and bn_gsum are exclusive");
+  CG_CHECK_ARG(!e.bn_gsum || (e.bn_z && e.bn_ss && e.bn_mi), "cgan3d_conv3d_fwd: bn_gsum needs bn_z, bn_ss, bn_mi");
+  CG_CHECK_ARG(!((e.bn_sum || e.bn_gsum) && g->cout == 1), "cgan3d_conv3d_fwd: fused BatchNorm statistics need cout > 1");
   hipStream_t s = (hipStream_t)stream;
   CG_CHECK_ARG(!g->w_packed || (g->cout > 1 && !(g->k == 7 && g->stride == 1 && g->cin == 1)),
                "cgan3d_conv3d_fwd: packed weights only for the implicit-GEMM path");

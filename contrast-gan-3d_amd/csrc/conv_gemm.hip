@@ -365,6 +365,41 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(GemmArgs a, const float*
     }
     if (tid == 0 && blockIdx.y == 0) ep.stats[sbase + 2 * a.cout] = (float)cntv;
   }
+  if (ep.bn_sum || ep.bn_gsum) {  // fused BatchNorm statistics: fp64 atomics per block and channel
+    double* acc64 = ep.bn_sum ? ep.bn_sum : ep.bn_gsum;
+    float p1[NBW], p2[NBW];
+#pragma unroll
+    for (int nb = 0; nb < NBW; ++nb) {
+      const int c = co0 + (wn * NBW + nb) * 16 + r16;
+      p1[nb] = 0.f;
+      p2[nb] = 0.f;
+      if (c < a.cout) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          if (rowv[j]) bn_pair(ep, vals[nb][j], (long long)rowo[j] * a.cout + c, c, a.cout, &p1[nb], &p2[nb]);
+      }
+      p1[nb] += __shfl_xor(p1[nb], 16, 64);
+      p1[nb] += __shfl_xor(p1[nb], 32, 64);
+      p2[nb] += __shfl_xor(p2[nb], 16, 64);
+      p2[nb] += __shfl_xor(p2[nb], 32, 64);
+    }
+    __syncthreads();
+    float* red = reinterpret_cast<float*>(As);  // [2][WM][BN]
+    if (g == 0) {
+#pragma unroll
+      for (int nb = 0; nb < NBW; ++nb) {
+        red[wm * BN + (wn * NBW + nb) * 16 + r16] = p1[nb];
+        red[(WM + wm) * BN + (wn * NBW + nb) * 16 + r16] = p2[nb];
+      }
+    }
+    __syncthreads();
+    if (tid < BN && co0 + tid < a.cout) {
+      float S1 = 0.f, S2 = 0.f;
+      for (int q = 0; q < WM; ++q) { S1 += red[q * BN + tid]; S2 += red[(WM + q) * BN + tid]; }
+      atomicAdd(acc64 + co0 + tid, (double)S1);
+      atomicAdd(acc64 + a.cout + co0 + tid, (double)S2);
+    }
+  }
 }
 
 // packed [t][a][b] (b contiguous, row length round_up(cout, 4)) from the strided torch layout

@@ -264,6 +264,40 @@ __global__ __launch_bounds__(256) void conv_halo_kernel(HaloArgs a, const float*
     }
     if (tid == 0 && blockIdx.y == 0) ep.stats[sbase + 2 * a.cout] = (float)cntv;
   }
+  if (ep.bn_sum || ep.bn_gsum) {  // fused BatchNorm statistics: fp64 atomics per block and channel
+    double* acc64 = ep.bn_sum ? ep.bn_sum : ep.bn_gsum;
+    float p1[NT], p2[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      const int c = co0 + t * 16 + r16;
+      p1[t] = 0.f;
+      p2[t] = 0.f;
+      if (c < a.cout) {
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj)
+          if (rowv[jj]) bn_pair(ep, vals[t][jj], (long long)rowo[jj] * a.cout + c, c, a.cout, &p1[t], &p2[t]);
+      }
+      p1[t] += __shfl_xor(p1[t], 16, 64);
+      p1[t] += __shfl_xor(p1[t], 32, 64);
+      p2[t] += __shfl_xor(p2[t], 16, 64);
+      p2[t] += __shfl_xor(p2[t], 32, 64);
+    }
+    __syncthreads();
+    float* red = reinterpret_cast<float*>(smem);  // [2][4 waves][BN]
+    if (g == 0) {
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        red[wave * BN + t * 16 + r16] = p1[t];
+        red[(4 + wave) * BN + t * 16 + r16] = p2[t];
+      }
+    }
+    __syncthreads();
+    if (tid < BN && co0 + tid < a.cout) {
+      atomicAdd(acc64 + co0 + tid, (double)(red[tid] + red[BN + tid] + red[2 * BN + tid] + red[3 * BN + tid]));
+      atomicAdd(acc64 + a.cout + co0 + tid,
+                (double)(red[4 * BN + tid] + red[5 * BN + tid] + red[6 * BN + tid] + red[7 * BN + tid]));
+    }
+  }
 }
 
 // bf16 [tap][b][a] with 16-byte granules of a XOR-swizzled by (b mod granules-per-row)

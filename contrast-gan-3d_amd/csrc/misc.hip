@@ -77,6 +77,51 @@ __global__ __launch_bounds__(256) void reflect_fold_kernel(const float* __restri
   }
 }
 
+// reflect_fold + the fused BatchNorm backward statistics of its output (cgan3d_epilogue bn_gsum):
+// V = 4 channels per thread, fixed for the whole grid-stride loop (256 % (C/4) == 0)
+__global__ __launch_bounds__(256) void reflect_fold_bn_kernel(const float* __restrict__ pad_in, float* __restrict__ out,
+                                                              int N, int D, int H, int W, int C, int P, Epi ep) {
+  __shared__ f32x4 r0[256], r1[256];
+  const int C4 = C / 4, tid = threadIdx.x;
+  const int total = N * D * H * W * C4;
+  const int Dp = D + 2 * P, Hp = H + 2 * P, Wp = W + 2 * P;
+  const int c0 = (tid % C4) * 4;
+  f32x4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = {0.f, 0.f, 0.f, 0.f};
+  for (int i = blockIdx.x * blockDim.x + tid; i < total; i += gridDim.x * blockDim.x) {
+    int t = i / C4;
+    const int w = t % W; t /= W;
+    const int h = t % H; t /= H;
+    const int d = t % D, n = t / D;
+    int qd[2], qh[2], qw[2];
+    const int nd = fold_src(d, D, P, qd), nh = fold_src(h, H, P, qh), nw = fold_src(w, W, P, qw);
+    f32x4 s = {0.f, 0.f, 0.f, 0.f};
+    for (int a = 0; a < nd; ++a)
+      for (int b = 0; b < nh; ++b)
+        for (int e = 0; e < nw; ++e)
+          s += *reinterpret_cast<const f32x4*>(pad_in + ((((long long)n * Dp + qd[a]) * Hp + qh[b]) * Wp + qw[e]) * C + c0);
+    reinterpret_cast<f32x4*>(out)[i] = s;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      float p1 = 0.f, p2 = 0.f;
+      bn_pair(ep, s[e], (long long)i * 4 + e, c0 + e, C, &p1, &p2);
+      a0[e] += p1;
+      a1[e] += p2;
+    }
+  }
+  r0[tid] = a0;
+  r1[tid] = a1;
+  __syncthreads();
+  if (tid < C4) {
+    f32x4 s0 = {0.f, 0.f, 0.f, 0.f}, s1 = {0.f, 0.f, 0.f, 0.f};
+    for (int k = tid; k < 256; k += C4) { s0 += r0[k]; s1 += r1[k]; }
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      atomicAdd(ep.bn_gsum + 4 * tid + e, (double)s0[e]);
+      atomicAdd(ep.bn_gsum + C + 4 * tid + e, (double)s1[e]);
+    }
+  }
+}
+
 // interpolation = eps*real + (1-eps)*fake  (model/utils.py:27-28)
 __global__ __launch_bounds__(256) void interp_kernel(const float* __restrict__ real, const float* __restrict__ fake,
                                                      const float* __restrict__ eps, float* __restrict__ out,
@@ -145,6 +190,25 @@ extern "C" int cgan3d_reflect_fold(const float* padded, float* out, int32_t n, i
     hipLaunchKernelGGL(reflect_fold_kernel<1>, dim3(blocks), dim3(256), 0, (hipStream_t)stream, padded, out, n, d, h, w,
                        c, pad);
   CG_LAUNCH_CHECK("reflect_fold_kernel");
+  return CGAN3D_OK;
+}
+
+extern "C" int cgan3d_reflect_fold_ex(const float* padded, float* out, int32_t n, int32_t d, int32_t h, int32_t w,
+                                      int32_t c, int32_t pad, const cgan3d_epilogue* ep, void* stream) {
+  if (!ep || !ep->bn_gsum) return cgan3d_reflect_fold(padded, out, n, d, h, w, c, pad, stream);
+  CG_CHECK_ARG(padded && out && ep->bn_z && ep->bn_ss && ep->bn_mi, "cgan3d_reflect_fold_ex: null pointer");
+  CG_CHECK_ARG(n > 0 && d > 2 * pad && h > 2 * pad && w > 2 * pad && pad >= 0,
+               "cgan3d_reflect_fold_ex: dims must exceed 2*pad");
+  CG_CHECK_ARG(c >= 4 && c % 4 == 0 && 256 % (c / 4) == 0, "cgan3d_reflect_fold_ex: channels must be 4k dividing 1024");
+  const long long total = (long long)n * d * h * w * c;
+  CG_CHECK_ARG(total < (1LL << 31), "cgan3d_reflect_fold_ex: volume too large");
+  Epi e{};
+  e.bn_gsum = ep->bn_gsum; e.bn_z = ep->bn_z; e.bn_ss = ep->bn_ss; e.bn_mi = ep->bn_mi;
+  e.bn_act = ep->bn_act; e.bn_slope = ep->bn_slope;
+  const int blocks = (int)std::min<long long>((total / 4 + 255) / 256, 2048);
+  hipLaunchKernelGGL(reflect_fold_bn_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, padded, out, n, d, h, w, c,
+                     pad, e);
+  CG_LAUNCH_CHECK("reflect_fold_bn_kernel");
   return CGAN3D_OK;
 }
 
