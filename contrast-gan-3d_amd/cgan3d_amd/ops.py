@@ -170,20 +170,21 @@ class Epi:
     """Fused-epilogue operands (include/cgan3d.h cgan3d_epilogue), kept as tensors for checks."""
 
     def __init__(self, bias=None, residual=None, mask_src=None, minuend=None, out2=None, stats=None,
-                 act=L.ACT_NONE, slope=0.0, bn_sum=None, bn_gsum=None, bn_z=None, bn_ss=None, bn_mi=None,
-                 bn_act=L.ACT_NONE, bn_slope=0.0):
+                 act=L.ACT_NONE, slope=0.0, bn_part=None, bn_mode=0, bn_slots=0, bn_z=None, bn_ss=None,
+                 bn_mi=None, bn_act=L.ACT_NONE, bn_slope=0.0):
         self.bias, self.residual, self.mask_src = bias, residual, mask_src
         self.minuend, self.out2, self.stats = minuend, out2, stats
         self.act, self.slope = act, float(slope)
-        # fused BatchNorm statistics (fp64 accumulators, caller-zeroed): see include/cgan3d.h
-        self.bn_sum, self.bn_gsum, self.bn_z, self.bn_ss, self.bn_mi = bn_sum, bn_gsum, bn_z, bn_ss, bn_mi
+        # fused BatchNorm statistics slab (per-block partial pairs): see include/cgan3d.h
+        self.bn_part, self.bn_mode, self.bn_slots = bn_part, int(bn_mode), int(bn_slots)
+        self.bn_z, self.bn_ss, self.bn_mi = bn_z, bn_ss, bn_mi
         self.bn_act, self.bn_slope = bn_act, float(bn_slope)
 
     def check_bn(self, nout, c, what):
-        for nm in ("bn_sum", "bn_gsum"):
-            if getattr(self, nm) is not None:
-                _need(getattr(self, nm), 2 * c, f"{what} {nm}", dtype=torch.float64)
-        if self.bn_gsum is not None:
+        if not self.bn_mode:
+            return
+        _need(self.bn_part, (2 * c + (self.bn_mode == 1)) * self.bn_slots, f"{what} bn_part", exact=False)
+        if self.bn_mode == 2:
             _need(self.bn_z, nout, f"{what} bn_z")
             _need(self.bn_ss, 2 * c, f"{what} bn_ss")
             _need(self.bn_mi, 2 * c, f"{what} bn_mi")
@@ -193,7 +194,7 @@ class Epi:
         e.bias, e.residual, e.mask_src = ptr(self.bias), ptr(self.residual), ptr(self.mask_src)
         e.minuend, e.out2, e.stats = ptr(self.minuend), ptr(self.out2), ptr(self.stats)
         e.act, e.slope = self.act, self.slope
-        e.bn_sum, e.bn_gsum, e.bn_z = ptr(self.bn_sum), ptr(self.bn_gsum), ptr(self.bn_z)
+        e.bn_part, e.bn_mode, e.bn_slots, e.bn_z = ptr(self.bn_part), self.bn_mode, self.bn_slots, ptr(self.bn_z)
         e.bn_ss, e.bn_mi, e.bn_act, e.bn_slope = ptr(self.bn_ss), ptr(self.bn_mi), self.bn_act, self.bn_slope
         return e
 
@@ -314,41 +315,46 @@ def bn_apply(z, nvox, c, scale_shift, act, y, residual=None, slope=0.0):
           "bn_apply")
 
 
-def bn_apply_acc(z, nvox, c, bn_sum, gamma, beta, rmean, rvar, nbt, act, y, scale_shift, mean_invstd,
-                 residual=None, slope=0.0, momentum=0.1, eps=1e-5):
-    """BatchNorm forward from the fused fp64 (sum, sum of squares) of the producing conv."""
-    _need(z, nvox * c, "bn_apply_acc z")
-    _need(y, nvox * c, "bn_apply_acc y")
-    _need(bn_sum, 2 * c, "bn_apply_acc bn_sum", dtype=torch.float64)
+def bn_slots(g: ConvGeom) -> int:
+    """Slots of the fused BatchNorm slab of a conv launch (0: the kernel has no fused statistics)."""
+    return int(L.load().cgan3d_conv3d_bn_slots(ctypes.byref(g)))
+
+
+def reflect_fold_slots(n, dims: Sequence[int], c) -> int:
+    return int(L.load().cgan3d_reflect_fold_slots(n, *dims, c))
+
+
+def bn_finalize_slab(part, nslots, c, nvox, gamma, beta, rmean, rvar, nbt, scale_shift, mean_invstd, momentum=0.1,
+                     eps=1e-5):
+    """BatchNorm forward statistics from a mode-1 slab (the producing conv's per-block partials)."""
+    _need(part, (2 * c + 1) * nslots, "bn_finalize_slab part", exact=False)
     for t, nm in ((gamma, "gamma"), (beta, "beta")):
-        _need(t, c, f"bn_apply_acc {nm}")
+        _need(t, c, f"bn_finalize_slab {nm}")
     for t, nm in ((rmean, "running_mean"), (rvar, "running_var")):
         if t is not None:
-            _need(t, c, f"bn_apply_acc {nm}")
+            _need(t, c, f"bn_finalize_slab {nm}")
     if nbt is not None:
-        _need(nbt, 1, "bn_apply_acc num_batches_tracked", dtype=torch.int64)
-    _need(scale_shift, 2 * c, "bn_apply_acc scale_shift")
-    _need(mean_invstd, 2 * c, "bn_apply_acc mean_invstd")
-    if residual is not None:
-        _need(residual, nvox * c, "bn_apply_acc residual")
-    check(_launch("cgan3d_bn_apply_acc", ptr(z), nvox, c, ptr(bn_sum), ptr(gamma), ptr(beta), ptr(rmean), ptr(rvar),
-                  ptr(nbt), momentum, eps, act, slope, ptr(residual), ptr(y), ptr(scale_shift), ptr(mean_invstd)),
-          "bn_apply_acc")
+        _need(nbt, 1, "bn_finalize_slab num_batches_tracked", dtype=torch.int64)
+    _need(scale_shift, 2 * c, "bn_finalize_slab scale_shift")
+    _need(mean_invstd, 2 * c, "bn_finalize_slab mean_invstd")
+    check(_launch("cgan3d_bn_finalize_slab", ptr(part), nslots, c, nvox, ptr(gamma), ptr(beta), ptr(rmean), ptr(rvar),
+                  ptr(nbt), momentum, eps, ptr(scale_shift), ptr(mean_invstd)), "bn_finalize_slab")
 
 
-def bn_backward_acc(dy, z, nvox, c, bn_gsum, scale_shift, mean_invstd, gamma, act, dgamma, dbeta, dz, slope=0.0,
-                    accumulate=False):
-    """BatchNorm backward from the fused fp64 (sum g, sum g*xhat) of the kernel that produced dy."""
+def bn_backward_slab(dy, z, nvox, c, part, nslots, scale_shift, mean_invstd, gamma, act, dgamma, dbeta, dz, ws,
+                     slope=0.0, accumulate=False):
+    """BatchNorm backward from a mode-2 slab (written by the kernel that produced dy)."""
     for t, nm in ((dy, "dy"), (z, "z"), (dz, "dz")):
-        _need(t, nvox * c, f"bn_backward_acc {nm}")
-    _need(bn_gsum, 2 * c, "bn_backward_acc bn_gsum", dtype=torch.float64)
+        _need(t, nvox * c, f"bn_backward_slab {nm}")
+    _need(part, 2 * c * nslots, "bn_backward_slab part", exact=False)
     for t, nm in ((scale_shift, "scale_shift"), (mean_invstd, "mean_invstd")):
-        _need(t, 2 * c, f"bn_backward_acc {nm}")
+        _need(t, 2 * c, f"bn_backward_slab {nm}")
     for t, nm in ((gamma, "gamma"), (dgamma, "dgamma"), (dbeta, "dbeta")):
-        _need(t, c, f"bn_backward_acc {nm}")
-    check(_launch("cgan3d_bn_backward_acc", ptr(dy), ptr(z), nvox, c, ptr(bn_gsum), ptr(scale_shift),
-                  ptr(mean_invstd), ptr(gamma), act, slope, ptr(dgamma), ptr(dbeta), ptr(dz), int(accumulate)),
-          "bn_backward_acc")
+        _need(t, c, f"bn_backward_slab {nm}")
+    _need(ws, 3 * c, "bn_backward_slab ws", exact=False)
+    check(_launch("cgan3d_bn_backward_slab", ptr(dy), ptr(z), nvox, c, ptr(part), nslots, ptr(scale_shift),
+                  ptr(mean_invstd), ptr(gamma), act, slope, ptr(dgamma), ptr(dbeta), ptr(dz), int(accumulate),
+                  ptr(ws)), "bn_backward_slab")
 
 
 def bn_backward_ws_floats(nvox, c) -> int:
@@ -387,6 +393,8 @@ def reflect_fold(padded, out, n, dims: Sequence[int], c, pad, ep: Optional[Epi] 
     if ep is None:
         check(_launch("cgan3d_reflect_fold", ptr(padded), ptr(out), n, d, h, w, c, pad), "reflect_fold")
         return
+    if ep.bn_mode and ep.bn_slots != reflect_fold_slots(n, dims, c):
+        raise ValueError("reflect_fold: bn_slots != reflect_fold_slots()")
     ep.check_bn(n * d * h * w * c, c, "reflect_fold")
     check(_launch("cgan3d_reflect_fold_ex", ptr(padded), ptr(out), n, d, h, w, c, pad, ctypes.byref(ep.c())),
           "reflect_fold_ex")

@@ -191,96 +191,94 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const float* __restri
   }
 }
 
-// ---- fused-statistics path: the sums come from the producing kernel's epilogue (fp64 atomics)
-
-// (scale, shift, mean, invstd) of channel c from the fp64 (sum, sum of squares) over n values
-__device__ __forceinline__ void bn_coeffs(const double* sum, int C, int c, double n, const float* gamma,
-                                          const float* beta, float eps, double* mean, double* var, float* sc,
-                                          float* sf, float* inv) {
-  const double m = sum[c] / n;
-  const double v = fmax(sum[C + c] / n - m * m, 0.0);
-  const double is = 1.0 / sqrt(v + (double)eps);
-  const double s = (double)gamma[c] * is;
-  *mean = m;
-  *var = v;
-  *sc = (float)s;
-  *sf = (float)((double)beta[c] - m * s);
-  *inv = (float)is;
+// ---- fused-statistics path: per-block partials written by the producing kernel's epilogue into
+// a channel-major slab part[(q * C + c) * nslots + b] (no atomics); one block per channel reads its
+// contiguous rows (coalesced) and combines them in fp64.
+__device__ __forceinline__ void slab_sums(const float* __restrict__ part, int nslots, int C, int c, double* s0,
+                                          double* s1) {
+  __shared__ double red[2][4];
+  const int tid = threadIdx.x;
+  const float* r0 = part + (long long)c * nslots;
+  const float* r1 = part + (long long)(C + c) * nslots;
+  double a0 = 0.0, a1 = 0.0;
+  for (int b0 = tid; b0 < nslots; b0 += 4 * blockDim.x) {
+    float v0[4], v1[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {  // four slots in flight
+      const int b = b0 + k * blockDim.x, bb = b < nslots ? b : 0;
+      v0[k] = b < nslots ? r0[bb] : 0.f;
+      v1[k] = b < nslots ? r1[bb] : 0.f;
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) { a0 += v0[k]; a1 += v1[k]; }
+  }
+  a0 = wave_sum_d(a0);
+  a1 = wave_sum_d(a1);
+  if ((tid & 63) == 0) { red[0][tid >> 6] = a0; red[1][tid >> 6] = a1; }
+  __syncthreads();
+  *s0 = red[0][0] + red[0][1] + red[0][2] + red[0][3];
+  *s1 = red[1][0] + red[1][1] + red[1][2] + red[1][3];
 }
 
-__global__ __launch_bounds__(256) void bn_apply_acc_kernel(const float* __restrict__ z, long long n4, int C,
-                                                           const double* __restrict__ sum, double nvox,
-                                                           const float* __restrict__ gamma,
-                                                           const float* __restrict__ beta, float* rmean, float* rvar,
-                                                           long long* nbt, float momentum, float eps, int act,
-                                                           float slope, const float* __restrict__ res,
-                                                           float* __restrict__ y, float* ss_out, float* mi_out) {
-  const int C4 = C >> 2;
-  const int c = (threadIdx.x % C4) * 4;
-  f32x4 sc, sf;
+// forward slab rows: sum (c), M2 about the block mean (C + c), block count (2C); Chan's combine
+// in fp64, read coalesced (one block per channel, threads striding the slots)
+__global__ __launch_bounds__(256) void bn_finalize_slab_kernel(const float* __restrict__ part, int nslots, int C,
+                                                               double nvox, const float* gamma, const float* beta,
+                                                               float* rmean, float* rvar, long long* nbt,
+                                                               float momentum, float eps, float* scale_shift,
+                                                               float* mean_invstd) {
+  __shared__ double red[3][4];
+  const int c = blockIdx.x, tid = threadIdx.x;
+  const float* rs = part + (long long)c * nslots;
+  const float* rq = part + (long long)(C + c) * nslots;
+  const float* rn = part + (long long)2 * C * nslots;
+  double n = 0.0, m = 0.0, q = 0.0;
+  for (int b0 = tid; b0 < nslots; b0 += 4 * blockDim.x) {
+    float sv[4], qv[4], nv[4];
 #pragma unroll
-  for (int e = 0; e < 4; ++e) {
-    double mean, var;
-    float inv, s0, s1;
-    bn_coeffs(sum, C, c + e, nvox, gamma, beta, eps, &mean, &var, &s0, &s1, &inv);
-    sc[e] = s0;
-    sf[e] = s1;
-    if (blockIdx.x == 0 && threadIdx.x < C4) {  // one writer per channel
-      ss_out[c + e] = sc[e];
-      ss_out[C + c + e] = sf[e];
-      mi_out[c + e] = (float)mean;
-      mi_out[C + c + e] = inv;
-      if (rmean) rmean[c + e] = (float)((1.0 - momentum) * rmean[c + e] + momentum * mean);
-      if (rvar) rvar[c + e] = (float)((1.0 - momentum) * rvar[c + e] + momentum * var * nvox / (nvox > 1 ? nvox - 1 : 1));
+    for (int k = 0; k < 4; ++k) {  // four slots in flight
+      const int b = b0 + k * blockDim.x, bb = b < nslots ? b : 0;
+      sv[k] = rs[bb]; qv[k] = rq[bb]; nv[k] = b < nslots ? rn[bb] : 0.f;
     }
-  }
-  if (nbt && blockIdx.x == 0 && threadIdx.x == 0) *nbt += 1;
-  const f32x4* z4 = reinterpret_cast<const f32x4*>(z);
-  const f32x4* r4 = reinterpret_cast<const f32x4*>(res);
-  f32x4* y4 = reinterpret_cast<f32x4*>(y);
-  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (long long)gridDim.x * blockDim.x) {
-    f32x4 v = z4[i];
 #pragma unroll
-    for (int e = 0; e < 4; ++e) v[e] = act_f(v[e] * sc[e] + sf[e], act, slope);
-    if (res) v += r4[i];
-    y4[i] = v;
+    for (int k = 0; k < 4; ++k)
+      if (nv[k] > 0.f) chan_merge(n, m, q, nv[k], (double)sv[k] / nv[k], qv[k]);
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    const double nb = __shfl_xor(n, off, 64), mb = __shfl_xor(m, off, 64), qb = __shfl_xor(q, off, 64);
+    chan_merge(n, m, q, nb, mb, qb);
+  }
+  if ((tid & 63) == 0) { red[0][tid >> 6] = n; red[1][tid >> 6] = m; red[2][tid >> 6] = q; }
+  __syncthreads();
+  if (tid == 0) {
+    for (int w = 1; w < 4; ++w) chan_merge(n, m, q, red[0][w], red[1][w], red[2][w]);
+    const double mean = m, var = q / n;
+    const double invstd = 1.0 / sqrt(var + (double)eps);
+    const double sc = (double)gamma[c] * invstd;
+    scale_shift[c] = (float)sc;
+    scale_shift[C + c] = (float)((double)beta[c] - mean * sc);
+    mean_invstd[c] = (float)mean;
+    mean_invstd[C + c] = (float)invstd;
+    if (rmean) rmean[c] = (float)((1.0 - momentum) * rmean[c] + momentum * mean);
+    if (rvar) rvar[c] = (float)((1.0 - momentum) * rvar[c] + momentum * var * nvox / (nvox > 1 ? nvox - 1 : 1));
+    if (nbt && c == 0) *nbt += 1;
   }
 }
 
-__global__ __launch_bounds__(256) void bn_bwd_acc_kernel(const float* __restrict__ dy, const float* __restrict__ z,
-                                                         long long n4, int C, const double* __restrict__ gsum,
-                                                         double nvox, const float* __restrict__ ss,
-                                                         const float* __restrict__ mi, const float* __restrict__ gamma,
-                                                         int act, float slope, float* dgamma, float* dbeta,
-                                                         int accumulate, float* __restrict__ dz) {
-  const int C4 = C >> 2;
-  const int c = (threadIdx.x % C4) * 4;
-  f32x4 sc, sf, mean, inv, k0, k1, k2;
-#pragma unroll
-  for (int e = 0; e < 4; ++e) {
-    sc[e] = ss[c + e]; sf[e] = ss[C + c + e]; mean[e] = mi[c + e]; inv[e] = mi[C + c + e];
-    k0[e] = gamma[c + e] * inv[e];
-    k1[e] = (float)(gsum[c + e] / nvox);
-    k2[e] = (float)(gsum[C + c + e] / nvox);
-    if (blockIdx.x == 0 && threadIdx.x < C4) {
-      const float db = (float)gsum[c + e], dg = (float)gsum[C + c + e];
-      if (dbeta) dbeta[c + e] = accumulate ? dbeta[c + e] + db : db;
-      if (dgamma) dgamma[c + e] = accumulate ? dgamma[c + e] + dg : dg;
-    }
-  }
-  const f32x4* z4 = reinterpret_cast<const f32x4*>(z);
-  const f32x4* d4 = reinterpret_cast<const f32x4*>(dy);
-  f32x4* o4 = reinterpret_cast<f32x4*>(dz);
-  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (long long)gridDim.x * blockDim.x) {
-    const f32x4 zz = z4[i], dd = d4[i];
-    f32x4 o;
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const float g = dd[e] * act_grad(zz[e] * sc[e] + sf[e], act, slope);
-      const float xh = (zz[e] - mean[e]) * inv[e];
-      o[e] = k0[e] * (g - k1[e] - xh * k2[e]);
-    }
-    o4[i] = o;
+__global__ __launch_bounds__(256) void bn_bwd_finalize_slab_kernel(const float* __restrict__ part, int nslots, int C,
+                                                                   double nvox, const float* __restrict__ gamma,
+                                                                   const float* __restrict__ mi, float* dgamma,
+                                                                   float* dbeta, float* coef, int accumulate) {
+  const int c = blockIdx.x;
+  double s0, s1;
+  slab_sums(part, nslots, C, c, &s0, &s1);
+  if (threadIdx.x == 0) {
+    if (dbeta) dbeta[c] = accumulate ? dbeta[c] + (float)s0 : (float)s0;
+    if (dgamma) dgamma[c] = accumulate ? dgamma[c] + (float)s1 : (float)s1;
+    coef[c] = gamma[c] * mi[C + c];
+    coef[C + c] = (float)(s0 / nvox);
+    coef[2 * C + c] = (float)(s1 / nvox);
   }
 }
 
@@ -348,35 +346,35 @@ extern "C" int cgan3d_bn_apply(const float* z, int64_t nvox, int32_t c, const fl
   return CGAN3D_OK;
 }
 
-extern "C" int cgan3d_bn_apply_acc(const float* z, int64_t nvox, int32_t c, const double* bn_sum, const float* gamma,
-                                   const float* beta, float* running_mean, float* running_var,
-                                   int64_t* num_batches_tracked, float momentum, float eps, int32_t act, float slope,
-                                   const float* residual, float* y, float* scale_shift, float* mean_invstd,
-                                   void* stream) {
-  CG_CHECK_ARG(z && bn_sum && gamma && beta && y && scale_shift && mean_invstd, "cgan3d_bn_apply_acc: null pointer");
-  CG_CHECK_ARG(nvox > 0 && c > 0 && c % 4 == 0 && 256 % (c / 4) == 0,
-               "cgan3d_bn_apply_acc: channels must be a multiple of 4 dividing 1024");
-  const long long n4 = (long long)nvox * c / 4;
-  int blocks = (int)std::min<long long>((n4 + 255) / 256, 4096);
-  hipLaunchKernelGGL(bn_apply_acc_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, z, n4, c, bn_sum,
-                     (double)nvox, gamma, beta, running_mean, running_var, (long long*)num_batches_tracked, momentum,
-                     eps, act, slope, residual, y, scale_shift, mean_invstd);
-  CG_LAUNCH_CHECK("bn_apply_acc_kernel");
+extern "C" int cgan3d_bn_finalize_slab(const float* part, int32_t nslots, int32_t c, int64_t nvox, const float* gamma,
+                                       const float* beta, float* running_mean, float* running_var,
+                                       int64_t* num_batches_tracked, float momentum, float eps, float* scale_shift,
+                                       float* mean_invstd, void* stream) {
+  CG_CHECK_ARG(part && gamma && beta && scale_shift && mean_invstd, "cgan3d_bn_finalize_slab: null pointer");
+  CG_CHECK_ARG(nslots > 0 && c > 0 && c <= 1024 && nvox > 0, "cgan3d_bn_finalize_slab: bad sizes");
+  hipLaunchKernelGGL(bn_finalize_slab_kernel, dim3(c), dim3(256), 0, (hipStream_t)stream, part, nslots, c, (double)nvox,
+                     gamma, beta, running_mean, running_var, (long long*)num_batches_tracked, momentum, eps,
+                     scale_shift, mean_invstd);
+  CG_LAUNCH_CHECK("bn_finalize_slab_kernel");
   return CGAN3D_OK;
 }
 
-extern "C" int cgan3d_bn_backward_acc(const float* dy, const float* z, int64_t nvox, int32_t c, const double* bn_gsum,
-                                      const float* scale_shift, const float* mean_invstd, const float* gamma,
-                                      int32_t act, float slope, float* dgamma, float* dbeta, float* dz,
-                                      int32_t accumulate, void* stream) {
-  CG_CHECK_ARG(dy && z && bn_gsum && scale_shift && mean_invstd && gamma && dz, "cgan3d_bn_backward_acc: null pointer");
-  CG_CHECK_ARG(nvox > 1 && c > 0 && c % 4 == 0 && 256 % (c / 4) == 0,
-               "cgan3d_bn_backward_acc: channels must be a multiple of 4 dividing 1024");
+extern "C" int cgan3d_bn_backward_slab(const float* dy, const float* z, int64_t nvox, int32_t c, const float* part,
+                                       int32_t nslots, const float* scale_shift, const float* mean_invstd,
+                                       const float* gamma, int32_t act, float slope, float* dgamma, float* dbeta,
+                                       float* dz, int32_t accumulate, float* ws, void* stream) {
+  CG_CHECK_ARG(dy && z && part && scale_shift && mean_invstd && gamma && dz && ws, "cgan3d_bn_backward_slab: null pointer");
+  CG_CHECK_ARG(nvox > 1 && nslots > 0 && c >= 4 && c <= 256 && 256 % c == 0,
+               "cgan3d_bn_backward_slab: channels must divide 256 and be >= 4");
+  hipStream_t s = (hipStream_t)stream;
+  hipLaunchKernelGGL(bn_bwd_finalize_slab_kernel, dim3(c), dim3(256), 0, s, part, nslots, c, (double)nvox, gamma,
+                     mean_invstd, dgamma, dbeta, ws, accumulate);
+  CG_LAUNCH_CHECK("bn_bwd_finalize_slab_kernel");
   const long long n4 = (long long)nvox * c / 4;
-  int blocks = (int)std::min<long long>((n4 + 255) / 256, 4096);
-  hipLaunchKernelGGL(bn_bwd_acc_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, dy, z, n4, c, bn_gsum,
-                     (double)nvox, scale_shift, mean_invstd, gamma, act, slope, dgamma, dbeta, accumulate, dz);
-  CG_LAUNCH_CHECK("bn_bwd_acc_kernel");
+  const int blocks = (int)std::min<long long>((n4 + 255) / 256, 4096);
+  hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(blocks), dim3(256), 0, s, dy, z, n4, c, scale_shift, mean_invstd, act,
+                     slope, ws, dz);
+  CG_LAUNCH_CHECK("bn_bwd_apply_kernel");
   return CGAN3D_OK;
 }
 

@@ -76,8 +76,9 @@ struct Epi {
   float* stats;
   int act;
   float slope;
-  double* bn_sum;
-  double* bn_gsum;
+  float* bn_part;
+  int bn_mode;
+  int bn_slots;
   const float* bn_z;
   const float* bn_ss;
   const float* bn_mi;
@@ -92,9 +93,9 @@ __device__ __forceinline__ float act_grad(float pre, int act, float slope) {
 }
 
 // The fused BatchNorm statistic pair of an epilogue value v at output element o, channel c (C
-// channels): (v, v^2) for bn_sum, (g, g*xhat) of the layer whose dL/dy is v for bn_gsum.
+// channels): (v, v^2) in mode 1, (g, g*xhat) of the layer whose dL/dy is v in mode 2.
 __device__ __forceinline__ void bn_pair(const Epi& e, float v, long long o, int c, int C, float* p1, float* p2) {
-  if (e.bn_sum) {
+  if (e.bn_mode == 1) {
     *p1 += v;
     *p2 += v * v;
   } else {
@@ -115,7 +116,7 @@ void k7m_wgrad_launch(const cgan3d_conv_geom* g, bool wide_in, long long wc, con
 long long k7_n2w_blocks(const cgan3d_conv_geom* g);
 long long k7m_n2w_blocks(const cgan3d_conv_geom* g);
 void k7m_n2w_launch(const cgan3d_conv_geom* g, int P, int reflect, int flip, long long wc, const float* x,
-                    const float* w, float* y, float* stats, double* bn_sum, hipStream_t s);
+                    const float* w, float* y, float* stats, float* bn_part, hipStream_t s);
 void k7m_w2n_launch(const cgan3d_conv_geom* g, int P, int reflect, long long wc, const float* x, const float* w,
                     float* y, const Epi& e, hipStream_t s);
 // implicit-GEMM forward / input-grad (conv_gemm.hip)
@@ -134,5 +135,17 @@ long long halo_mblocks(const cgan3d_conv_geom* g);
 int halo_launch(const cgan3d_conv_geom* g, const float* x, const float* w, float* y, const Epi& e, hipStream_t st);
 int halo_pack(const cgan3d_conv_geom* g, const float* w, void* wp, hipStream_t st);
 int gemm_launch(const cgan3d_conv_geom* g, const float* x, const float* w, float* y, const Epi& e, hipStream_t st);
+
+// mode-2 pair from a prefetched z
+__device__ __forceinline__ void bn_pair_z(const Epi& e, float v, float z, int c, int C, float* p1, float* p2) {
+  const float gg = v * act_grad(z * e.bn_ss[c] + e.bn_ss[C + c], e.bn_act, e.bn_slope);
+  *p1 += gg;
+  *p2 += gg * (z - e.bn_mi[c]) * e.bn_mi[C + c];
+}
+
+// slab slot b, channel c, pair member q of a fused BatchNorm slab
+__device__ __forceinline__ float* bn_slot(const Epi& e, int q, int C, int c, int b) {
+  return e.bn_part + ((long long)q * C + c) * e.bn_slots + b;
+}
 
 }  // namespace cg

@@ -404,10 +404,17 @@ static Epi to_epi(const cgan3d_epilogue* ep) {
   if (ep) {
     e.bias = ep->bias; e.residual = ep->residual; e.mask_src = ep->mask_src; e.minuend = ep->minuend;
     e.out2 = ep->out2; e.stats = ep->stats; e.act = ep->act; e.slope = ep->slope;
-    e.bn_sum = ep->bn_sum; e.bn_gsum = ep->bn_gsum; e.bn_z = ep->bn_z; e.bn_ss = ep->bn_ss; e.bn_mi = ep->bn_mi;
+    e.bn_part = ep->bn_mode ? ep->bn_part : nullptr; e.bn_mode = ep->bn_part ? ep->bn_mode : 0;
+    e.bn_slots = ep->bn_slots; e.bn_z = ep->bn_z; e.bn_ss = ep->bn_ss; e.bn_mi = ep->bn_mi;
     e.bn_act = ep->bn_act; e.bn_slope = ep->bn_slope;
   }
   return e;
+}
+
+extern "C" int64_t cgan3d_conv3d_bn_slots(const cgan3d_conv_geom* g) {
+  if (!g || g->cout == 1) return 0;
+  const int64_t f = cgan3d_conv3d_stats_floats(g);
+  return f > 0 ? f / (2 * g->cout + 1) : 0;
 }
 
 extern "C" int64_t cgan3d_conv3d_stats_floats(const cgan3d_conv_geom* g) {
@@ -426,9 +433,14 @@ extern "C" int cgan3d_conv3d_fwd(const cgan3d_conv_geom* g, const float* x, cons
   CG_CHECK_ARG(x && w && y, "cgan3d_conv3d_fwd: null pointer");
   Epi e = to_epi(ep);
   CG_CHECK_ARG(!(e.out2 && (!e.minuend || g->cout != 1)), "cgan3d_conv3d_fwd: out2 needs minuend and cout==1");
-  CG_CHECK_ARG(!(e.bn_sum && e.bn_gsum), "cgan3d_conv3d_fwd: bn_sum and bn_gsum are exclusive");
-  CG_CHECK_ARG(!e.bn_gsum || (e.bn_z && e.bn_ss && e.bn_mi), "cgan3d_conv3d_fwd: bn_gsum needs bn_z, bn_ss, bn_mi");
-  CG_CHECK_ARG(!((e.bn_sum || e.bn_gsum) && g->cout == 1), "cgan3d_conv3d_fwd: fused BatchNorm statistics need cout > 1");
+  CG_CHECK_ARG(e.bn_mode >= 0 && e.bn_mode <= 2, "cgan3d_conv3d_fwd: bn_mode must be 0, 1 or 2");
+  CG_CHECK_ARG(e.bn_mode != 2 || (e.bn_z && e.bn_ss && e.bn_mi), "cgan3d_conv3d_fwd: bn_mode 2 needs bn_z, bn_ss, bn_mi");
+  if (e.bn_mode) {
+    const long long slots = cgan3d_conv3d_bn_slots(g);
+    CG_CHECK_ARG(slots > 0 && slots == e.bn_slots, "cgan3d_conv3d_fwd: bn_slots %d, the launch has %lld", e.bn_slots,
+                 slots);
+    CG_CHECK_ARG(!(e.bn_mode == 2 && g->k == 7 && g->cin == 1), "cgan3d_conv3d_fwd: no bn_mode 2 on the k7 path");
+  }
   hipStream_t s = (hipStream_t)stream;
   CG_CHECK_ARG(!g->w_packed || (g->cout > 1 && !(g->k == 7 && g->stride == 1 && g->cin == 1)),
                "cgan3d_conv3d_fwd: packed weights only for the implicit-GEMM path");

@@ -301,6 +301,18 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(GemmArgs a, const float*
     rowo[j] = row_out[wm * 16 + 4 * g + j];
     rowv[j] = rowo[j] >= 0;
   }
+  // residual / BatchNorm-input operands: every load issued before the first use
+  float resv[NBW][4], zv[NBW][4];
+#pragma unroll
+  for (int nb = 0; nb < NBW; ++nb) {
+    const int c = co0 + (wn * NBW + nb) * 16 + r16;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const long long o = (rowv[j] && c < a.cout) ? (long long)rowo[j] * a.cout + c : 0;
+      resv[nb][j] = ep.residual ? ep.residual[o] : 0.f;
+      zv[nb][j] = ep.bn_mode == 2 ? ep.bn_z[o] : 0.f;
+    }
+  }
 #pragma unroll
   for (int nb = 0; nb < NBW; ++nb) {
     const int c = co0 + (wn * NBW + nb) * 16 + r16;
@@ -315,13 +327,13 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(GemmArgs a, const float*
       if (rowv[j] && cv) {
         const long long o = (long long)rowo[j] * a.cout + c;
         if (ep.mask_src) v = ep.mask_src[o] > 0.f ? v : v * ep.slope;
-        if (ep.residual) v += ep.residual[o];
+        v += resv[nb][j];
         y[o] = v;
       }
       vals[nb][j] = (rowv[j] && cv) ? v : 0.f;
     }
   }
-  if (ep.stats) {
+  if (ep.stats || ep.bn_mode == 1) {  // (sum, M2 about the block mean, count): block-major or slab
     __syncthreads();
     float* red = reinterpret_cast<float*>(As);  // [WM][BN]  (<= 4*64 floats)
     __shared__ float bmean[64];
@@ -340,7 +352,10 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(GemmArgs a, const float*
       float S = 0.f;
       for (int q = 0; q < WM; ++q) S += red[q * BN + tid];
       bmean[tid] = cntv ? S / cntv : 0.f;
-      if (co0 + tid < a.cout) ep.stats[sbase + co0 + tid] = S;
+      if (co0 + tid < a.cout) {
+        if (ep.stats) ep.stats[sbase + co0 + tid] = S;
+        else *bn_slot(ep, 0, a.cout, co0 + tid, blockIdx.x) = S;
+      }
     }
     __syncthreads();
 #pragma unroll
@@ -361,12 +376,17 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(GemmArgs a, const float*
     if (tid < BN) {
       float M2 = 0.f;
       for (int q = 0; q < WM; ++q) M2 += red[q * BN + tid];
-      if (co0 + tid < a.cout) ep.stats[sbase + a.cout + co0 + tid] = M2;
+      if (co0 + tid < a.cout) {
+        if (ep.stats) ep.stats[sbase + a.cout + co0 + tid] = M2;
+        else *bn_slot(ep, 1, a.cout, co0 + tid, blockIdx.x) = M2;
+      }
     }
-    if (tid == 0 && blockIdx.y == 0) ep.stats[sbase + 2 * a.cout] = (float)cntv;
+    if (tid == 0 && blockIdx.y == 0) {
+      if (ep.stats) ep.stats[sbase + 2 * a.cout] = (float)cntv;
+      else *bn_slot(ep, 2, a.cout, 0, blockIdx.x) = (float)cntv;
+    }
   }
-  if (ep.bn_sum || ep.bn_gsum) {  // fused BatchNorm statistics: fp64 atomics per block and channel
-    double* acc64 = ep.bn_sum ? ep.bn_sum : ep.bn_gsum;
+  if (ep.bn_mode == 2) {  // fused BatchNorm backward statistics: this block's slot of the slab
     float p1[NBW], p2[NBW];
 #pragma unroll
     for (int nb = 0; nb < NBW; ++nb) {
@@ -376,7 +396,7 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(GemmArgs a, const float*
       if (c < a.cout) {
 #pragma unroll
         for (int j = 0; j < 4; ++j)
-          if (rowv[j]) bn_pair(ep, vals[nb][j], (long long)rowo[j] * a.cout + c, c, a.cout, &p1[nb], &p2[nb]);
+          if (rowv[j]) bn_pair_z(ep, vals[nb][j], zv[nb][j], c, a.cout, &p1[nb], &p2[nb]);
       }
       p1[nb] += __shfl_xor(p1[nb], 16, 64);
       p1[nb] += __shfl_xor(p1[nb], 32, 64);
@@ -396,8 +416,8 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(GemmArgs a, const float*
     if (tid < BN && co0 + tid < a.cout) {
       float S1 = 0.f, S2 = 0.f;
       for (int q = 0; q < WM; ++q) { S1 += red[q * BN + tid]; S2 += red[(WM + q) * BN + tid]; }
-      atomicAdd(acc64 + co0 + tid, (double)S1);
-      atomicAdd(acc64 + a.cout + co0 + tid, (double)S2);
+      *bn_slot(ep, 0, a.cout, co0 + tid, blockIdx.x) = S1;
+      *bn_slot(ep, 1, a.cout, co0 + tid, blockIdx.x) = S2;
     }
   }
 }

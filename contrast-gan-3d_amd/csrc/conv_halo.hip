@@ -203,6 +203,18 @@ __global__ __launch_bounds__(256) void conv_halo_kernel(HaloArgs a, const float*
     rowo[jj] = row_out[wave * 16 + 4 * g + jj];
     rowv[jj] = rowo[jj] >= 0;
   }
+  // residual / BatchNorm-input operands: every load issued before the first use
+  float resv[NT][4], zv[NT][4];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    const int c = co0 + t * 16 + r16;
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj) {
+      const long long o = (rowv[jj] && c < a.cout) ? (long long)rowo[jj] * a.cout + c : 0;
+      resv[t][jj] = ep.residual ? ep.residual[o] : 0.f;
+      zv[t][jj] = ep.bn_mode == 2 ? ep.bn_z[o] : 0.f;
+    }
+  }
 #pragma unroll
   for (int t = 0; t < NT; ++t) {
     const int c = co0 + t * 16 + r16;
@@ -216,13 +228,13 @@ __global__ __launch_bounds__(256) void conv_halo_kernel(HaloArgs a, const float*
       if (rowv[jj] && cv) {
         const long long o = (long long)rowo[jj] * a.cout + c;
         if (ep.mask_src) v = ep.mask_src[o] > 0.f ? v : v * ep.slope;
-        if (ep.residual) v += ep.residual[o];
+        v += resv[t][jj];
         y[o] = v;
       }
       vals[t][jj] = (rowv[jj] && cv) ? v : 0.f;
     }
   }
-  if (ep.stats) {
+  if (ep.stats || ep.bn_mode == 1) {  // (sum, M2 about the block mean, count): block-major or slab
     __syncthreads();
     float* red = reinterpret_cast<float*>(smem);  // [4 waves][BN]
     __shared__ float bmean[64];
@@ -240,7 +252,10 @@ __global__ __launch_bounds__(256) void conv_halo_kernel(HaloArgs a, const float*
     if (tid < BN) {
       const float S = red[tid] + red[BN + tid] + red[2 * BN + tid] + red[3 * BN + tid];
       bmean[tid] = cntv ? S / cntv : 0.f;
-      if (co0 + tid < a.cout) ep.stats[sbase + co0 + tid] = S;
+      if (co0 + tid < a.cout) {
+        if (ep.stats) ep.stats[sbase + co0 + tid] = S;
+        else *bn_slot(ep, 0, a.cout, co0 + tid, blockIdx.x) = S;
+      }
     }
     __syncthreads();
 #pragma unroll
@@ -260,12 +275,17 @@ __global__ __launch_bounds__(256) void conv_halo_kernel(HaloArgs a, const float*
     __syncthreads();
     if (tid < BN) {
       const float M2 = red[tid] + red[BN + tid] + red[2 * BN + tid] + red[3 * BN + tid];
-      if (co0 + tid < a.cout) ep.stats[sbase + a.cout + co0 + tid] = M2;
+      if (co0 + tid < a.cout) {
+        if (ep.stats) ep.stats[sbase + a.cout + co0 + tid] = M2;
+        else *bn_slot(ep, 1, a.cout, co0 + tid, blockIdx.x) = M2;
+      }
     }
-    if (tid == 0 && blockIdx.y == 0) ep.stats[sbase + 2 * a.cout] = (float)cntv;
+    if (tid == 0 && blockIdx.y == 0) {
+      if (ep.stats) ep.stats[sbase + 2 * a.cout] = (float)cntv;
+      else *bn_slot(ep, 2, a.cout, 0, blockIdx.x) = (float)cntv;
+    }
   }
-  if (ep.bn_sum || ep.bn_gsum) {  // fused BatchNorm statistics: fp64 atomics per block and channel
-    double* acc64 = ep.bn_sum ? ep.bn_sum : ep.bn_gsum;
+  if (ep.bn_mode == 2) {  // fused BatchNorm backward statistics: this block's slot of the slab
     float p1[NT], p2[NT];
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
@@ -275,7 +295,7 @@ __global__ __launch_bounds__(256) void conv_halo_kernel(HaloArgs a, const float*
       if (c < a.cout) {
 #pragma unroll
         for (int jj = 0; jj < 4; ++jj)
-          if (rowv[jj]) bn_pair(ep, vals[t][jj], (long long)rowo[jj] * a.cout + c, c, a.cout, &p1[t], &p2[t]);
+          if (rowv[jj]) bn_pair_z(ep, vals[t][jj], zv[t][jj], c, a.cout, &p1[t], &p2[t]);
       }
       p1[t] += __shfl_xor(p1[t], 16, 64);
       p1[t] += __shfl_xor(p1[t], 32, 64);
@@ -293,9 +313,9 @@ __global__ __launch_bounds__(256) void conv_halo_kernel(HaloArgs a, const float*
     }
     __syncthreads();
     if (tid < BN && co0 + tid < a.cout) {
-      atomicAdd(acc64 + co0 + tid, (double)(red[tid] + red[BN + tid] + red[2 * BN + tid] + red[3 * BN + tid]));
-      atomicAdd(acc64 + a.cout + co0 + tid,
-                (double)(red[4 * BN + tid] + red[5 * BN + tid] + red[6 * BN + tid] + red[7 * BN + tid]));
+      *bn_slot(ep, 0, a.cout, co0 + tid, blockIdx.x) = red[tid] + red[BN + tid] + red[2 * BN + tid] + red[3 * BN + tid];
+      *bn_slot(ep, 1, a.cout, co0 + tid, blockIdx.x) =
+          red[4 * BN + tid] + red[5 * BN + tid] + red[6 * BN + tid] + red[7 * BN + tid];
     }
   }
 }

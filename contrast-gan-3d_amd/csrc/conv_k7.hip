@@ -52,7 +52,7 @@ __device__ __forceinline__ void k7_row(const float* xs, float (&xr)[10]) {
 // ------------------------------------------------------------------------------------------
 template <int C>
 __global__ __launch_bounds__(256) void k7_n2w_kernel(K7Args a, const float* __restrict__ x, const float* __restrict__ w,
-                                                     float* __restrict__ y, float* stats, double* bn_sum) {
+                                                     float* __restrict__ y, float* stats, float* bn_part) {
   __shared__ __attribute__((aligned(16))) float xs[HALO];
   __shared__ __attribute__((aligned(16))) float ws[KT7 * C];  // [t][c]
   const int tid = threadIdx.x;
@@ -102,7 +102,7 @@ __global__ __launch_bounds__(256) void k7_n2w_kernel(K7Args a, const float* __re
             f32x4{acc[4 * c4][j], acc[4 * c4 + 1][j], acc[4 * c4 + 2][j], acc[4 * c4 + 3][j]};
     }
   }
-  if (stats) {  // per-block BatchNorm partials (sum, M2, count), same layout as conv.hip
+  if (stats || bn_part) {  // per-block BatchNorm partials (sum, M2, count): block-major, or slab
     __syncthreads();
     float* red = xs;  // [256][C] fits in the halo buffer (C <= 16)
     __shared__ float bmean[C];
@@ -123,7 +123,8 @@ __global__ __launch_bounds__(256) void k7_n2w_kernel(K7Args a, const float* __re
       double S = 0.0;
       for (int k = 0; k < 256; ++k) S += red[k * C + tid];
       bmean[tid] = (float)(S / cnt);
-      stats[(long long)blockIdx.x * (2 * C + 1) + tid] = (float)S;
+      if (stats) stats[(long long)blockIdx.x * (2 * C + 1) + tid] = (float)S;
+      else bn_part[(long long)tid * gridDim.x + blockIdx.x] = (float)S;
     }
     __syncthreads();
 #pragma unroll
@@ -141,29 +142,12 @@ __global__ __launch_bounds__(256) void k7_n2w_kernel(K7Args a, const float* __re
     if (tid < C) {
       double Q = 0.0;
       for (int k = 0; k < 256; ++k) Q += red[k * C + tid];
-      stats[(long long)blockIdx.x * (2 * C + 1) + C + tid] = (float)Q;
+      if (stats) stats[(long long)blockIdx.x * (2 * C + 1) + C + tid] = (float)Q;
+      else bn_part[(long long)(C + tid) * gridDim.x + blockIdx.x] = (float)Q;
     }
-    if (tid == 0) stats[(long long)blockIdx.x * (2 * C + 1) + 2 * C] = (float)cnt;
-  }
-  if (bn_sum) {  // fused statistics: fp64 atomics of the block's (sum, sum of squares)
-    __syncthreads();
-    float* red = xs;  // [256][C]
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {
-#pragma unroll
-      for (int c = 0; c < C; ++c) {
-        float s = 0.f;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) s += valid[j] ? (q ? acc[c][j] * acc[c][j] : acc[c][j]) : 0.f;
-        red[tid * C + c] = s;
-      }
-      __syncthreads();
-      if (tid < C) {
-        double S = 0.0;
-        for (int k = 0; k < 256; ++k) S += red[k * C + tid];
-        atomicAdd(bn_sum + q * C + tid, S);
-      }
-      __syncthreads();
+    if (tid == 0) {
+      if (stats) stats[(long long)blockIdx.x * (2 * C + 1) + 2 * C] = (float)cnt;
+      else bn_part[(long long)2 * C * gridDim.x + blockIdx.x] = (float)cnt;
     }
   }
 }
@@ -360,19 +344,21 @@ long long k7_n2w_blocks(const cgan3d_conv_geom* g) {
 int k7_try_fwd(const cgan3d_conv_geom* g, const float* x, const float* w, float* y, const Epi& e,
                hipStream_t s) {
   if (g->k != 7 || g->stride != 1) return 0;
-  if (g->cin == 1 && k7_wide_ok(g->cout) && !e.bias && !e.residual && !e.mask_src && !e.out2 && !e.bn_gsum &&
+  if (g->cin == 1 && k7_wide_ok(g->cout) && !e.bias && !e.residual && !e.mask_src && !e.out2 && e.bn_mode != 2 &&
       e.act == CGAN3D_ACT_NONE) {
     if (k7m_ok(g, g->cout)) {
-      if (!g->transposed) k7m_n2w_launch(g, g->pad, g->reflect, 0, g->w_sb, x, w, y, e.stats, e.bn_sum, s);
-      else k7m_n2w_launch(g, g->k - 1 - g->pad, 0, 1, g->w_sb, x, w, y, e.stats, e.bn_sum, s);
+      float* bp = e.bn_mode == 1 ? e.bn_part : nullptr;
+      if (!g->transposed) k7m_n2w_launch(g, g->pad, g->reflect, 0, g->w_sb, x, w, y, e.stats, bp, s);
+      else k7m_n2w_launch(g, g->k - 1 - g->pad, 0, 1, g->w_sb, x, w, y, e.stats, bp, s);
       return 1;
     }
     K7Args a;
     if (!g->transposed) a = k7_args(g, g->pad, g->reflect, 0, g->w_sb);
     else a = k7_args(g, g->k - 1 - g->pad, 0, 1, g->w_sb);  // input-grad: flipped taps, zero pad
+    float* bp = e.bn_mode == 1 ? e.bn_part : nullptr;
     if (g->cout == 16)
-      hipLaunchKernelGGL((k7_n2w_kernel<16>), dim3(k7_blocks(a)), dim3(256), 0, s, a, x, w, y, e.stats, e.bn_sum);
-    else hipLaunchKernelGGL((k7_n2w_kernel<8>), dim3(k7_blocks(a)), dim3(256), 0, s, a, x, w, y, e.stats, e.bn_sum);
+      hipLaunchKernelGGL((k7_n2w_kernel<16>), dim3(k7_blocks(a)), dim3(256), 0, s, a, x, w, y, e.stats, bp);
+    else hipLaunchKernelGGL((k7_n2w_kernel<8>), dim3(k7_blocks(a)), dim3(256), 0, s, a, x, w, y, e.stats, bp);
     return 1;
   }
   if (g->cout == 1 && k7_wide_ok(g->cin) && !g->transposed && !e.residual && !e.mask_src && !e.stats &&

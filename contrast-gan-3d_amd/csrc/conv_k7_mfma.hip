@@ -57,7 +57,7 @@ constexpr int N_X = N_ROWS * N_HW, N_X_PER = (N_X + 255) / 256;
 
 __global__ __launch_bounds__(256, 2) void k7m_n2w_kernel(K7Args a, const float* __restrict__ x,
                                                          const float* __restrict__ w, float* __restrict__ y,
-                                                         float* stats, double* bn_sum, int tiles_per_block, int ntiles) {
+                                                         float* stats, float* bn_part, int tiles_per_block, int ntiles) {
   constexpr int C = 16;
   __shared__ __attribute__((aligned(16))) __bf16 us[N_ROWS * N_TW * 8];  // [row][ow][8 taps]
   __shared__ __attribute__((aligned(16))) __bf16 xs[N_ROWS * N_HWP];     // [row][24]
@@ -117,7 +117,6 @@ __global__ __launch_bounds__(256, 2) void k7m_n2w_kernel(K7Args a, const float* 
   };
   // running BatchNorm statistics of this block (threads tid < 16, channel tid): Chan merge per tile
   float run_n = 0.f, run_mean = 0.f, run_m2 = 0.f;
-  float bs1 = 0.f, bs2 = 0.f;  // fused statistics: this lane's (sum, sum of squares) of channel r16
   const int t0 = blockIdx.x * tiles_per_block, t1 = min(ntiles, t0 + tiles_per_block);
   if (t0 < t1 && !(a.dbg & 4)) load(t0);
   for (int tile = t0; tile < t1; ++tile) {
@@ -174,13 +173,11 @@ __global__ __launch_bounds__(256, 2) void k7m_n2w_kernel(K7Args a, const float* 
         if (od < a.do_ && oh < a.ho && ow < a.wo) {
           if (!(a.dbg & 8)) y[((((n * a.do_ + od) * a.ho + oh) * a.wo + ow) * C) + r16] = acc[r][jj];
           s1 += acc[r][jj];
-          bs2 += acc[r][jj] * acc[r][jj];
           ++cntl;
         }
       }
     }
-    bs1 += s1;
-    if (stats) {  // tile (sum, M2 about the tile mean), merged into the block's running statistics
+    if (stats || bn_part) {  // tile (sum, M2 about the tile mean), merged into the block's running statistics
       const int vd = min(N_TD, a.do_ - d0), vh = min(N_TH, a.ho - h0), vw = min(N_TW, a.wo - w0);
       const float tn = (float)(vd * vh * vw);
       s1 += __shfl_xor(s1, 16, 64);
@@ -214,25 +211,16 @@ __global__ __launch_bounds__(256, 2) void k7m_n2w_kernel(K7Args a, const float* 
     }
     (void)cntl;
   }
-  if (bn_sum) {  // fused statistics: fp64 atomics of the block's (sum, sum of squares)
-    bs1 += __shfl_xor(bs1, 16, 64);
-    bs1 += __shfl_xor(bs1, 32, 64);
-    bs2 += __shfl_xor(bs2, 16, 64);
-    bs2 += __shfl_xor(bs2, 32, 64);
-    __syncthreads();
-    __shared__ float red2[4][C];
-    if (g == 0) { red[wave][r16] = bs1; red2[wave][r16] = bs2; }
-    __syncthreads();
-    if (tid < C) {
-      atomicAdd(bn_sum + tid, (double)(red[0][tid] + red[1][tid] + red[2][tid] + red[3][tid]));
-      atomicAdd(bn_sum + C + tid, (double)(red2[0][tid] + red2[1][tid] + red2[2][tid] + red2[3][tid]));
-    }
-  }
   if (stats && tid < C) {  // BatchNorm partials (sum, M2, count) per block, layout of conv.hip
     const long long sb = (long long)blockIdx.x * (2 * C + 1);
     stats[sb + tid] = run_mean * run_n;
     stats[sb + C + tid] = run_m2;
     if (tid == 0) stats[sb + 2 * C] = run_n;
+  }
+  if (bn_part && tid < C) {  // the same partials into slot blockIdx.x of the channel-major slab
+    bn_part[(long long)tid * gridDim.x + blockIdx.x] = run_mean * run_n;
+    bn_part[(long long)(C + tid) * gridDim.x + blockIdx.x] = run_m2;
+    if (tid == 0) bn_part[(long long)2 * C * gridDim.x + blockIdx.x] = run_n;
   }
 }
 
@@ -602,11 +590,11 @@ long long k7m_n2w_blocks(const cgan3d_conv_geom* g) {
 }
 
 void k7m_n2w_launch(const cgan3d_conv_geom* g, int P, int reflect, int flip, long long wc, const float* x,
-                    const float* w, float* y, float* stats, double* bn_sum, hipStream_t s) {
+                    const float* w, float* y, float* stats, float* bn_part, hipStream_t s) {
   const K7Args a = k7m_args(g, P, reflect, flip, wc, N_TD, N_TH, N_TW);
   int grid, per, nt;
   k7m_n2w_split(a, &grid, &per, &nt);
-  hipLaunchKernelGGL(k7m_n2w_kernel, dim3(grid), dim3(256), 0, s, a, x, w, y, stats, bn_sum, per, nt);
+  hipLaunchKernelGGL(k7m_n2w_kernel, dim3(grid), dim3(256), 0, s, a, x, w, y, stats, bn_part, per, nt);
 }
 
 void k7m_w2n_launch(const cgan3d_conv_geom* g, int P, int reflect, long long wc, const float* x, const float* w,

@@ -116,8 +116,8 @@ __global__ __launch_bounds__(256) void reflect_fold_bn_kernel(const float* __res
     for (int k = tid; k < 256; k += C4) { s0 += r0[k]; s1 += r1[k]; }
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
-      atomicAdd(ep.bn_gsum + 4 * tid + e, (double)s0[e]);
-      atomicAdd(ep.bn_gsum + C + 4 * tid + e, (double)s1[e]);
+      *bn_slot(ep, 0, C, 4 * tid + e, blockIdx.x) = s0[e];
+      *bn_slot(ep, 1, C, 4 * tid + e, blockIdx.x) = s1[e];
     }
   }
 }
@@ -193,19 +193,26 @@ extern "C" int cgan3d_reflect_fold(const float* padded, float* out, int32_t n, i
   return CGAN3D_OK;
 }
 
+extern "C" int32_t cgan3d_reflect_fold_slots(int32_t n, int32_t d, int32_t h, int32_t w, int32_t c) {
+  const long long total = (long long)n * d * h * w * c;
+  return (int32_t)std::max<long long>(1, std::min<long long>((total / 4 + 255) / 256, 4096));
+}
+
 extern "C" int cgan3d_reflect_fold_ex(const float* padded, float* out, int32_t n, int32_t d, int32_t h, int32_t w,
                                       int32_t c, int32_t pad, const cgan3d_epilogue* ep, void* stream) {
-  if (!ep || !ep->bn_gsum) return cgan3d_reflect_fold(padded, out, n, d, h, w, c, pad, stream);
-  CG_CHECK_ARG(padded && out && ep->bn_z && ep->bn_ss && ep->bn_mi, "cgan3d_reflect_fold_ex: null pointer");
+  if (!ep || !ep->bn_mode) return cgan3d_reflect_fold(padded, out, n, d, h, w, c, pad, stream);
+  CG_CHECK_ARG(ep->bn_mode == 2, "cgan3d_reflect_fold_ex: only bn_mode 2");
+  CG_CHECK_ARG(padded && out && ep->bn_part && ep->bn_z && ep->bn_ss && ep->bn_mi, "cgan3d_reflect_fold_ex: null pointer");
   CG_CHECK_ARG(n > 0 && d > 2 * pad && h > 2 * pad && w > 2 * pad && pad >= 0,
                "cgan3d_reflect_fold_ex: dims must exceed 2*pad");
   CG_CHECK_ARG(c >= 4 && c % 4 == 0 && 256 % (c / 4) == 0, "cgan3d_reflect_fold_ex: channels must be 4k dividing 1024");
   const long long total = (long long)n * d * h * w * c;
   CG_CHECK_ARG(total < (1LL << 31), "cgan3d_reflect_fold_ex: volume too large");
+  const int blocks = cgan3d_reflect_fold_slots(n, d, h, w, c);
+  CG_CHECK_ARG(ep->bn_slots == blocks, "cgan3d_reflect_fold_ex: bn_slots %d, the launch has %d", ep->bn_slots, blocks);
   Epi e{};
-  e.bn_gsum = ep->bn_gsum; e.bn_z = ep->bn_z; e.bn_ss = ep->bn_ss; e.bn_mi = ep->bn_mi;
-  e.bn_act = ep->bn_act; e.bn_slope = ep->bn_slope;
-  const int blocks = (int)std::min<long long>((total / 4 + 255) / 256, 2048);
+  e.bn_part = ep->bn_part; e.bn_mode = 2; e.bn_slots = blocks; e.bn_z = ep->bn_z; e.bn_ss = ep->bn_ss;
+  e.bn_mi = ep->bn_mi; e.bn_act = ep->bn_act; e.bn_slope = ep->bn_slope;
   hipLaunchKernelGGL(reflect_fold_bn_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, padded, out, n, d, h, w, c,
                      pad, e);
   CG_LAUNCH_CHECK("reflect_fold_bn_kernel");

@@ -70,13 +70,15 @@ typedef struct cgan3d_conv_geom {
  * stats != NULL: per-block BatchNorm partials (sum, M2, count) of v, consumed by
  * cgan3d_bn_finalize; size cgan3d_conv3d_stats_floats().
  * Fused BatchNorm statistics (forward and input-grad kernels of the k7 / halo / implicit-GEMM
- * paths, and cgan3d_reflect_fold_ex), accumulated with fp64 atomics into caller-zeroed buffers:
- *  bn_sum  != NULL: bn_sum[c] += sum v, bn_sum[cout + c] += sum v^2  (the BatchNorm input z = v;
- *                   consumed by cgan3d_bn_apply_acc);
- *  bn_gsum != NULL: v is dL/dy of a BatchNorm layer y = act(z * scale + shift) whose input z has
- *                   the layout of this output: with g = v * act'(z*scale + shift) and
- *                   xhat = (z - mean) * invstd, bn_gsum[c] += sum g, bn_gsum[cout + c] += sum g*xhat
- *                   (consumed by cgan3d_bn_backward_acc). */
+ * paths, and cgan3d_reflect_fold_ex): each block b of the launch writes its per-channel partial
+ * pair into a channel-major slab bn_part[(q * cout + c) * bn_slots + b] (q = 0, 1; no atomics),
+ * bn_slots = cgan3d_conv3d_bn_slots() / cgan3d_reflect_fold_slots():
+ *  bn_mode 1: v is the BatchNorm input z: rows sum v (c), M2 of v about the block mean (cout + c)
+ *             and the block's voxel count (row 2*cout): (2*cout + 1) * bn_slots floats
+ *             (cgan3d_bn_finalize_slab, Chan's combine);
+ *  bn_mode 2: v is dL/dy of a BatchNorm layer y = act(z * scale + shift) whose input z has the
+ *             layout of this output: (sum g, sum g*xhat) with g = v * act'(z*scale + shift),
+ *             xhat = (z - mean) * invstd (cgan3d_bn_backward_finalize_slab). */
 typedef struct cgan3d_epilogue {
   const float* bias;
   const float* residual;
@@ -86,12 +88,13 @@ typedef struct cgan3d_epilogue {
   float* stats;
   int32_t act;
   float slope;
-  double* bn_sum;
-  double* bn_gsum;
-  const float* bn_z;           /* bn_gsum: the BatchNorm input z */
-  const float* bn_ss;          /* bn_gsum: [scale | shift] (cgan3d_bn_apply_acc) */
-  const float* bn_mi;          /* bn_gsum: [mean | invstd] */
-  int32_t bn_act;              /* bn_gsum: the activation after the BatchNorm */
+  float* bn_part;
+  int32_t bn_mode;             /* 0 off, 1 forward statistics, 2 backward statistics */
+  int32_t bn_slots;            /* slot stride of bn_part (must equal the launch's slot count) */
+  const float* bn_z;           /* mode 2: the BatchNorm input z */
+  const float* bn_ss;          /* mode 2: [scale | shift] */
+  const float* bn_mi;          /* mode 2: [mean | invstd] */
+  int32_t bn_act;              /* mode 2: the activation after the BatchNorm */
   float bn_slope;
 } cgan3d_epilogue;
 
@@ -139,21 +142,23 @@ int cgan3d_bn_finalize(const float* stats, int64_t nblk, int32_t c, const float*
                        float* scale_shift, float* mean_invstd, void* stream);
 int cgan3d_bn_apply(const float* z, int64_t nvox, int32_t c, const float* scale_shift,
                     int32_t act, float slope, const float* residual, float* y, void* stream);
-/* Fused-statistics forward: scale/shift from bn_sum (fp64 [sum | sum of squares] over nvox
- * voxels, filled by the producing conv's epilogue), y = act(z*scale + shift) (+ residual); also
- * writes scale_shift, mean_invstd and the running statistics (biased variance to normalise,
- * unbiased into running_var, momentum as torch). */
-int cgan3d_bn_apply_acc(const float* z, int64_t nvox, int32_t c, const double* bn_sum, const float* gamma,
-                        const float* beta, float* running_mean, float* running_var,
-                        int64_t* num_batches_tracked, float momentum, float eps, int32_t act, float slope,
-                        const float* residual, float* y, float* scale_shift, float* mean_invstd,
-                        void* stream);
-/* Fused-statistics backward: dz from dy, z and bn_gsum (fp64 [sum g | sum g*xhat], filled by the
- * epilogue that produced dy); dgamma = sum g*xhat, dbeta = sum g (+= when accumulate). */
-int cgan3d_bn_backward_acc(const float* dy, const float* z, int64_t nvox, int32_t c, const double* bn_gsum,
-                           const float* scale_shift, const float* mean_invstd, const float* gamma,
-                           int32_t act, float slope, float* dgamma, float* dbeta, float* dz,
-                           int32_t accumulate, void* stream);
+/* Slots of a launch's fused BatchNorm slab (cgan3d_epilogue bn_part); 0 when the geometry's
+ * kernel has no fused statistics. */
+int64_t cgan3d_conv3d_bn_slots(const cgan3d_conv_geom* g);
+/* Forward statistics from a bn_mode-1 slab of nslots slots over nvox voxels (fp64 Chan combine):
+ * scale_shift, mean_invstd and the running statistics (biased variance to normalise, unbiased
+ * into running_var, torch momentum), for cgan3d_bn_apply. */
+int cgan3d_bn_finalize_slab(const float* part, int32_t nslots, int32_t c, int64_t nvox, const float* gamma,
+                            const float* beta, float* running_mean, float* running_var,
+                            int64_t* num_batches_tracked, float momentum, float eps, float* scale_shift,
+                            float* mean_invstd, void* stream);
+/* Backward from a bn_mode-2 slab (filled by the kernel that produced dy): dgamma = sum g*xhat,
+ * dbeta = sum g (+= when accumulate), then dz = gamma*invstd*(g - mean g - xhat*mean(g*xhat)).
+ * ws: 3*c floats. */
+int cgan3d_bn_backward_slab(const float* dy, const float* z, int64_t nvox, int32_t c, const float* part,
+                            int32_t nslots, const float* scale_shift, const float* mean_invstd,
+                            const float* gamma, int32_t act, float slope, float* dgamma, float* dbeta,
+                            float* dz, int32_t accumulate, float* ws, void* stream);
 int64_t cgan3d_bn_backward_ws_floats(int64_t nvox, int32_t c);
 /* accumulate != 0: dgamma/dbeta += this batch's gradients (a module called on several batches in
  * one step, e.g. the BatchNorm critic on the real and the fake batch, Trainer.py:119-121). */
@@ -168,7 +173,9 @@ int cgan3d_channel_sum(const float* x, int64_t nvox, int32_t c, float* out, floa
                        void* stream);
 int cgan3d_reflect_fold(const float* padded, float* out, int32_t n, int32_t d, int32_t h,
                         int32_t w, int32_t c, int32_t pad, void* stream);
-/* reflect_fold with the epilogue's bn_gsum statistics of its output (other fields ignored) */
+/* reflect_fold with the epilogue's bn_mode-2 statistics of its output (other fields ignored);
+ * slots of its slab: cgan3d_reflect_fold_slots() */
+int32_t cgan3d_reflect_fold_slots(int32_t n, int32_t d, int32_t h, int32_t w, int32_t c);
 int cgan3d_reflect_fold_ex(const float* padded, float* out, int32_t n, int32_t d, int32_t h,
                            int32_t w, int32_t c, int32_t pad, const cgan3d_epilogue* ep, void* stream);
 int cgan3d_gp_interpolate(const float* real, const float* fake, const float* eps, float* out,

@@ -1,8 +1,8 @@
-"""Fused BatchNorm statistics (include/cgan3d.h cgan3d_epilogue bn_sum / bn_gsum,
-cgan3d_bn_apply_acc, cgan3d_bn_backward_acc, cgan3d_reflect_fold_ex).
+"""Fused BatchNorm statistics (include/cgan3d.h cgan3d_epilogue bn_part / bn_mode,
+cgan3d_bn_finalize_slab, cgan3d_bn_backward_slab, cgan3d_reflect_fold_ex).
 
-The per-channel sums accumulated by each producing kernel's epilogue are checked against the same
-sums of that kernel's own output (float64, 1e-4: fp32 partials, fp64 atomics); the BatchNorm
+The per-block partial pairs each producing kernel writes into its slab are summed and checked
+against the same sums of that kernel's own output (float64, 1e-4: fp32 partials); the BatchNorm
 forward / backward built on them against torch autograd (float64) within 1e-3, as the two-pass
 path in test_gpu_ops.test_batchnorm_train_forward_backward (model/blocks.py:26-27,45-53).
 """
@@ -64,9 +64,19 @@ def test_fused_forward_statistics(name, prec, cin, cout, k, s, p, reflect, sp, m
         assert (geo.w_packed == 2) == name.startswith("halo"), "unexpected kernel choice"
     x = _cl(torch.randn(n, cin, *sp, generator=g))
     y = torch.empty(n, *dout, cout, device="cuda")
-    acc = torch.zeros(2 * cout, device="cuda", dtype=torch.float64)
-    ops.conv(geo, x, w, y, ops.epilogue(bn_sum=acc))
-    assert_close(acc.cpu().numpy(), _pairs(y, cout).numpy(), 1e-4, f"{name} bn_sum")
+    slots = ops.bn_slots(geo)
+    part = torch.full(((2 * cout + 1) * slots,), float("nan"), device="cuda")  # every slot must be written
+    ops.conv(geo, x, w, y, ops.epilogue(bn_part=part, bn_mode=1, bn_slots=slots))
+    sl = part.double().cpu().view(2 * cout + 1, slots)
+    cnt = sl[2 * cout]
+    tot = cnt.sum()
+    yk = y.double().cpu().reshape(-1, cout)
+    assert int(tot) == yk.shape[0]
+    mean = sl[:cout].sum(1) / tot
+    bm = sl[:cout] / cnt.clamp(min=1)
+    m2 = sl[cout:2 * cout].sum(1) + (cnt * (bm - mean[:, None]) ** 2).sum(1)
+    assert_close(mean.numpy(), yk.mean(0).numpy(), 1e-4, f"{name} slab mean")
+    assert_close((m2 / tot).numpy(), yk.var(0, unbiased=False).numpy(), 1e-4, f"{name} slab var")
 
 
 @pytest.mark.parametrize("name,prec,cin,cout,k,s,p,sp", [
@@ -102,10 +112,13 @@ def test_fused_backward_statistics(name, prec, cin, cout, k, s, p, sp, monkeypat
     ss = torch.cat([torch.rand(cout, generator=g) + 0.5, torch.randn(cout, generator=g) * 0.2]).cuda()
     mi = torch.cat([torch.randn(cout, generator=g) * 0.1, torch.rand(cout, generator=g) + 0.5]).cuda()
     res = torch.randn(n, *dout, cout, generator=g).cuda()
-    acc = torch.zeros(2 * cout, device="cuda", dtype=torch.float64)
-    ep = ops.epilogue(residual=res, bn_gsum=acc, bn_z=z, bn_ss=ss, bn_mi=mi, bn_act=L.ACT_RELU)
+    slots = ops.bn_slots(geo)
+    part = torch.full((2 * cout * slots,), float("nan"), device="cuda")
+    ep = ops.epilogue(residual=res, bn_part=part, bn_mode=2, bn_slots=slots, bn_z=z, bn_ss=ss, bn_mi=mi,
+                      bn_act=L.ACT_RELU)
     ops.conv(geo, _cl(gin), wp, out, ep)
-    assert_close(acc.cpu().numpy(), _pairs(out, cout, z, ss, mi, L.ACT_RELU).numpy(), 1e-4, f"{name} bn_gsum")
+    got = part.double().cpu().view(2 * cout, slots).sum(1)
+    assert_close(got.numpy(), _pairs(out, cout, z, ss, mi, L.ACT_RELU).numpy(), 1e-4, f"{name} backward slab")
 
 
 @pytest.mark.parametrize("c,act", [(16, 1), (64, 0)])
@@ -132,23 +145,28 @@ def test_fused_batchnorm_vs_torch(c, act):
     nvox = n * sp[0] * sp[1] * sp[2]
     geo = ops.conv_fwd_geom(n, sp, sp, 8, c, 3, 1, 1)
     zd = torch.empty(n, *sp, c, device="cuda")
-    acc = torch.zeros(2, 2 * c, device="cuda", dtype=torch.float64)
-    ops.conv(geo, _cl(x), w.float().cuda(), zd, ops.epilogue(bn_sum=acc[0]))
+    sf = ops.bn_slots(geo)
+    pf = torch.empty((2 * c + 1) * sf, device="cuda")
+    ops.conv(geo, _cl(x), w.float().cuda(), zd, ops.epilogue(bn_part=pf, bn_mode=1, bn_slots=sf))
     ss, mi = torch.empty(2 * c, device="cuda"), torch.empty(2 * c, device="cuda")
     rmd, rvd = torch.zeros(c, device="cuda"), torch.ones(c, device="cuda")
     nbt = torch.zeros((), dtype=torch.int64, device="cuda")
     gmd, btd = gamma.float().cuda(), beta.float().cuda()
+    ops.bn_finalize_slab(pf, sf, c, nvox, gmd, btd, rmd, rvd, nbt, ss, mi)
     yd = torch.empty_like(zd)
-    ops.bn_apply_acc(zd, nvox, c, acc[0], gmd, btd, rmd, rvd, nbt, act, yd, ss, mi)
+    ops.bn_apply(zd, nvox, c, ss, act, yd)
     assert_close(_ncdhw(yd).numpy(), y.detach().numpy(), 1e-3, "fused bn fwd")
     assert_close(rmd.cpu().numpy(), rm.numpy(), 1e-3, "running_mean")
     assert_close(rvd.cpu().numpy(), rv.numpy(), 1e-3, "running_var")
     assert int(nbt.item()) == 1
     dyd = torch.empty_like(zd)
-    ep = ops.epilogue(bn_gsum=acc[1], bn_z=zd, bn_ss=ss, bn_mi=mi, bn_act=act)
+    sb = ops.reflect_fold_slots(n, sp, c)
+    pb = torch.empty(2 * c * sb, device="cuda")
+    ep = ops.epilogue(bn_part=pb, bn_mode=2, bn_slots=sb, bn_z=zd, bn_ss=ss, bn_mi=mi, bn_act=act)
     ops.reflect_fold(_cl(gpad), dyd, n, sp, c, P, ep=ep)
     dzd, dgd, dbd = torch.empty_like(zd), torch.empty(c, device="cuda"), torch.empty(c, device="cuda")
-    ops.bn_backward_acc(dyd, zd, nvox, c, acc[1], ss, mi, gmd, act, dgd, dbd, dzd)
+    ws = torch.empty(3 * c, device="cuda")
+    ops.bn_backward_slab(dyd, zd, nvox, c, pb, sb, ss, mi, gmd, act, dgd, dbd, dzd, ws)
     assert_close(_ncdhw(dzd).numpy(), dz.numpy(), 1e-3, "fused bn dz")
     assert_close(dgd.double().cpu().numpy(), dgm.numpy(), 1e-3, "fused bn dgamma")
     assert_close(dbd.double().cpu().numpy(), dbt.numpy(), 1e-3, "fused bn dbeta")
