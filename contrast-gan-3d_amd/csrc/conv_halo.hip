@@ -22,6 +22,7 @@
 namespace cg {
 
 typedef __bf16 bf16x8_h __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4_h __attribute__((ext_vector_type(4)));
 
 struct HaloArgs {
   int n, di, hi, wi, do_, ho, wo, cin, cout, k, s, p, transposed;
@@ -31,9 +32,12 @@ struct HaloArgs {
   int ez, ey, ex;             // halo extents
   int halo_bytes;
   int bn;                     // output channels per block
+  int dbg;                    // kernel-phase switches for timing experiments (cgan3d_set_tuning key 8)
 };
 
 constexpr int HT = 4;  // tile edge (4 x 4 x 4 = 64 output voxels)
+
+static int g_halo_dbg = 0;
 
 struct ClassTaps {
   int f, st, n;   // first tap, step, count
@@ -56,6 +60,142 @@ __host__ __device__ inline ClassTaps class_info(int r, int k, int s, int p, int 
 // halo extent along one dim for a 4-wide tile
 __host__ __device__ inline int halo_extent(const ClassTaps& c, int s, int transposed) {
   return transposed ? HT + c.omax - c.omin : (HT - 1) * s + c.omax + 1;
+}
+
+// Epilogue of the halo-tiled kernels: lane holds tile rows wave*16 + 4g + jj (row_out: output
+// voxel of each of the 64 tile rows, -1 outside) for channel co0 + t*16 + r16; bias, activation,
+// mask, residual, store, BatchNorm statistics (block-major partials, or slab modes 1 / 2).
+// smemf: >= 8 * 16 * NT floats of LDS the caller no longer needs.
+template <int NT>
+__device__ __forceinline__ void halo_epilogue(const HaloArgs& a, f32x4 (&acc)[NT], const int* row_out, int co0,
+                                              float* y, const Epi& ep, float* smemf) {
+  constexpr int BN = 16 * NT;
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int g = lane >> 4, r16 = lane & 15;
+  // ---- epilogue: lane holds tile rows wave*16 + 4g + jj for channel co0 + t*16 + r16
+  float vals[NT][4];
+  bool rowv[4];
+  int rowo[4];
+#pragma unroll
+  for (int jj = 0; jj < 4; ++jj) {
+    rowo[jj] = row_out[wave * 16 + 4 * g + jj];
+    rowv[jj] = rowo[jj] >= 0;
+  }
+  // residual / BatchNorm-input operands: every load issued before the first use
+  float resv[NT][4], zv[NT][4];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    const int c = co0 + t * 16 + r16;
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj) {
+      const long long o = (rowv[jj] && c < a.cout) ? (long long)rowo[jj] * a.cout + c : 0;
+      resv[t][jj] = ep.residual ? ep.residual[o] : 0.f;
+      zv[t][jj] = ep.bn_mode == 2 ? ep.bn_z[o] : 0.f;
+    }
+  }
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    const int c = co0 + t * 16 + r16;
+    const bool cv = c < a.cout;
+    const float b = (ep.bias && cv) ? ep.bias[c] : 0.f;
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj) {
+      float v = acc[t][jj] + b;
+      if (ep.act == CGAN3D_ACT_RELU) v = fmaxf(v, 0.f);
+      else if (ep.act == CGAN3D_ACT_LRELU) v = v > 0.f ? v : v * ep.slope;
+      if (rowv[jj] && cv) {
+        const long long o = (long long)rowo[jj] * a.cout + c;
+        if (ep.mask_src) v = ep.mask_src[o] > 0.f ? v : v * ep.slope;
+        v += resv[t][jj];
+        y[o] = v;
+      }
+      vals[t][jj] = (rowv[jj] && cv) ? v : 0.f;
+    }
+  }
+  if (ep.stats || ep.bn_mode == 1) {  // (sum, M2 about the block mean, count): block-major or slab
+    __syncthreads();
+    float* red = smemf;  // [4 waves][BN]
+    __shared__ float bmean[64];
+    int cntv = 0;
+    for (int r = 0; r < 64; ++r) cntv += row_out[r] >= 0;
+    const long long sbase = (long long)blockIdx.x * (2 * a.cout + 1);
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      float sum = vals[t][0] + vals[t][1] + vals[t][2] + vals[t][3];
+      sum += __shfl_xor(sum, 16, 64);
+      sum += __shfl_xor(sum, 32, 64);
+      if (g == 0) red[wave * BN + t * 16 + r16] = sum;
+    }
+    __syncthreads();
+    if (tid < BN) {
+      const float S = red[tid] + red[BN + tid] + red[2 * BN + tid] + red[3 * BN + tid];
+      bmean[tid] = cntv ? S / cntv : 0.f;
+      if (co0 + tid < a.cout) {
+        if (ep.stats) ep.stats[sbase + co0 + tid] = S;
+        else *bn_slot(ep, 0, a.cout, co0 + tid, blockIdx.x) = S;
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      const int cl = t * 16 + r16;
+      const float m = bmean[cl];
+      float q = 0.f;
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj) {
+        const float d = (rowv[jj] && co0 + cl < a.cout) ? vals[t][jj] - m : 0.f;
+        q += d * d;
+      }
+      q += __shfl_xor(q, 16, 64);
+      q += __shfl_xor(q, 32, 64);
+      if (g == 0) red[wave * BN + cl] = q;
+    }
+    __syncthreads();
+    if (tid < BN) {
+      const float M2 = red[tid] + red[BN + tid] + red[2 * BN + tid] + red[3 * BN + tid];
+      if (co0 + tid < a.cout) {
+        if (ep.stats) ep.stats[sbase + a.cout + co0 + tid] = M2;
+        else *bn_slot(ep, 1, a.cout, co0 + tid, blockIdx.x) = M2;
+      }
+    }
+    if (tid == 0 && blockIdx.y == 0) {
+      if (ep.stats) ep.stats[sbase + 2 * a.cout] = (float)cntv;
+      else *bn_slot(ep, 2, a.cout, 0, blockIdx.x) = (float)cntv;
+    }
+  }
+  if (ep.bn_mode == 2) {  // fused BatchNorm backward statistics: this block's slot of the slab
+    float p1[NT], p2[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      const int c = co0 + t * 16 + r16;
+      p1[t] = 0.f;
+      p2[t] = 0.f;
+      if (c < a.cout) {
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj)
+          if (rowv[jj]) bn_pair_z(ep, vals[t][jj], zv[t][jj], c, a.cout, &p1[t], &p2[t]);
+      }
+      p1[t] += __shfl_xor(p1[t], 16, 64);
+      p1[t] += __shfl_xor(p1[t], 32, 64);
+      p2[t] += __shfl_xor(p2[t], 16, 64);
+      p2[t] += __shfl_xor(p2[t], 32, 64);
+    }
+    __syncthreads();
+    float* red = smemf;  // [2][4 waves][BN]
+    if (g == 0) {
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        red[wave * BN + t * 16 + r16] = p1[t];
+        red[(4 + wave) * BN + t * 16 + r16] = p2[t];
+      }
+    }
+    __syncthreads();
+    if (tid < BN && co0 + tid < a.cout) {
+      *bn_slot(ep, 0, a.cout, co0 + tid, blockIdx.x) = red[tid] + red[BN + tid] + red[2 * BN + tid] + red[3 * BN + tid];
+      *bn_slot(ep, 1, a.cout, co0 + tid, blockIdx.x) =
+          red[4 * BN + tid] + red[5 * BN + tid] + red[6 * BN + tid] + red[7 * BN + tid];
+    }
+  }
 }
 
 template <int CIN, int NT>  // NT = BN/16 output-channel tiles per wave
@@ -194,130 +334,147 @@ __global__ __launch_bounds__(256) void conv_halo_kernel(HaloArgs a, const float*
     __builtin_amdgcn_s_barrier();
   }
 
-  // ---- epilogue: lane holds tile rows wave*16 + 4g + jj for channel co0 + t*16 + r16
-  float vals[NT][4];
-  bool rowv[4];
-  int rowo[4];
-#pragma unroll
-  for (int jj = 0; jj < 4; ++jj) {
-    rowo[jj] = row_out[wave * 16 + 4 * g + jj];
-    rowv[jj] = rowo[jj] >= 0;
+  halo_epilogue<NT>(a, acc, row_out, co0, y, ep, reinterpret_cast<float*>(smem));
+}
+
+// ---- ResNet-block convs (k3 s1 p1, 64 -> 64) and their input-grads: one 4x4x4 output tile x
+// all 64 output channels per block, the 27 taps split over the 4 waves (K split), so each tap's
+// work is 4 M tiles x 4 N tiles x 2 K steps = 32 MFMAs per wave between no barriers at all:
+//  * the input halo (6 x 6 x 6 voxels, x padded to 8) is staged once, bf16, 192-byte voxel rows
+//    with 16-byte granules XOR-swizzled by (2 * row) & 7 — conflict-free A reads for every tap and
+//    M tile (ds_read_b128 lane groups, MI355X_MICROARCH.md LDS table; found by exhaustive search);
+//  * B fragments come straight from the packed weights in L2 (format 2), the next tap's eight in
+//    flight during the current tap's MFMAs;
+//  * the four waves' partial tiles are combined once through LDS (wave w keeps M tile w) and the
+//    shared halo epilogue writes the tile.
+constexpr int K3_HX = 8, K3_HY = 6, K3_HZ = 6, K3_VROW = 96;  // halo dims (x padded), elements per voxel row
+
+template <bool TR, int NT>  // NT: 16-channel output tiles per block (blockIdx.y picks the channel block)
+__global__ __launch_bounds__(256, 2) void conv_k3_kernel(HaloArgs a, const float* __restrict__ x,
+                                                         const __bf16* __restrict__ wpk, float* y, Epi ep) {
+  constexpr int CIN = 64, COUT = 64, KS = 2;
+  const int co0 = blockIdx.y * 16 * NT;
+  constexpr int HALO_BYTES = K3_HZ * K3_HY * K3_HX * K3_VROW * 2;  // 55296
+  static_assert(HALO_BYTES >= 3 * 4 * NT * 256 * 4, "reduction buffer aliases the halo");
+  __shared__ __attribute__((aligned(16))) unsigned char smem[HALO_BYTES];
+  __shared__ int row_out[64];
+  __bf16* halo = reinterpret_cast<__bf16*>(smem);
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int g = lane >> 4, r16 = lane & 15;
+  const int tiles = a.td * a.th * a.tw;
+  int bid = blockIdx.x;
+  const int nb = bid / tiles;
+  bid -= nb * tiles;
+  const int tz = bid / (a.th * a.tw), ty = (bid / a.tw) % a.th, tx = bid % a.tw;
+  const int oz = tz * HT - 1, oy = ty * HT - 1, ox = tx * HT - 1;  // halo origin (pad 1 either way)
+  if (tid < 64) {
+    const int jz = tz * HT + (tid >> 4), jy = ty * HT + ((tid >> 2) & 3), jx = tx * HT + (tid & 3);
+    row_out[tid] = (jz < a.do_ && jy < a.ho && jx < a.wo) ? ((nb * a.do_ + jz) * a.ho + jy) * a.wo + jx : -1;
   }
-  // residual / BatchNorm-input operands: every load issued before the first use
-  float resv[NT][4], zv[NT][4];
+  // B fragments of one tap: N tile nt, K step ks -> lane (channel nt*16 + r16, granule ks*4 + g);
+  // taps t, t+4 and t+8 in registers: two taps' loads in flight during a tap's MFMAs
+  bf16x8_h bq[3][NT][KS];
+  auto loadb = [&](int t, bf16x8_h (&b)[NT][KS]) {
 #pragma unroll
-  for (int t = 0; t < NT; ++t) {
-    const int c = co0 + t * 16 + r16;
+    for (int nt = 0; nt < NT; ++nt) {
+      const int col = co0 + nt * 16 + r16;
 #pragma unroll
-    for (int jj = 0; jj < 4; ++jj) {
-      const long long o = (rowv[jj] && c < a.cout) ? (long long)rowo[jj] * a.cout + c : 0;
-      resv[t][jj] = ep.residual ? ep.residual[o] : 0.f;
-      zv[t][jj] = ep.bn_mode == 2 ? ep.bn_z[o] : 0.f;
+      for (int ks = 0; ks < KS; ++ks)
+        b[nt][ks] = *reinterpret_cast<const bf16x8_h*>(wpk + ((long long)t * COUT + col) * CIN +
+                                                      8 * ((ks * 4 + g) ^ (col & 7)));
     }
+  };
+  if (!(a.dbg & 4)) {
+    loadb(wave, bq[0]);
+    loadb(wave + 4, bq[1]);
   }
+  // ---- halo: fp32 NDHWC -> bf16 LDS, voxel (hz, hy, hx) row (hz*6 + hy)*8 + hx, granule swizzle;
+  // every load of the thread issued before the first conversion
+  constexpr int ST = K3_HZ * K3_HY * 6 * 16, ST_PER = (ST + 255) / 256;
+  if (!(a.dbg & 1)) {
+    f32x4 sv[ST_PER];
 #pragma unroll
-  for (int t = 0; t < NT; ++t) {
-    const int c = co0 + t * 16 + r16;
-    const bool cv = c < a.cout;
-    const float b = (ep.bias && cv) ? ep.bias[c] : 0.f;
+    for (int k = 0; k < ST_PER; ++k) {
+      const int i = tid + 256 * k;
+      const int c4 = i & 15, v = i >> 4;
+      const int hx = v % 6, hy = (v / 6) % 6, hz = v / 36;
+      const int iz = oz + hz, iy = oy + hy, ix = ox + hx;
+      const bool ok = i < ST && (unsigned)iz < (unsigned)a.di && (unsigned)iy < (unsigned)a.hi &&
+                      (unsigned)ix < (unsigned)a.wi;
+      sv[k] = *reinterpret_cast<const f32x4*>(
+          x + (ok ? (((long long)(nb * a.di + iz) * a.hi + iy) * a.wi + ix) * CIN + 4 * c4 : 0));
+      if (!ok) sv[k] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
 #pragma unroll
-    for (int jj = 0; jj < 4; ++jj) {
-      float v = acc[t][jj] + b;
-      if (ep.act == CGAN3D_ACT_RELU) v = fmaxf(v, 0.f);
-      else if (ep.act == CGAN3D_ACT_LRELU) v = v > 0.f ? v : v * ep.slope;
-      if (rowv[jj] && cv) {
-        const long long o = (long long)rowo[jj] * a.cout + c;
-        if (ep.mask_src) v = ep.mask_src[o] > 0.f ? v : v * ep.slope;
-        v += resv[t][jj];
-        y[o] = v;
-      }
-      vals[t][jj] = (rowv[jj] && cv) ? v : 0.f;
-    }
-  }
-  if (ep.stats || ep.bn_mode == 1) {  // (sum, M2 about the block mean, count): block-major or slab
-    __syncthreads();
-    float* red = reinterpret_cast<float*>(smem);  // [4 waves][BN]
-    __shared__ float bmean[64];
-    int cntv = 0;
-    for (int r = 0; r < 64; ++r) cntv += row_out[r] >= 0;
-    const long long sbase = (long long)blockIdx.x * (2 * a.cout + 1);
-#pragma unroll
-    for (int t = 0; t < NT; ++t) {
-      float sum = vals[t][0] + vals[t][1] + vals[t][2] + vals[t][3];
-      sum += __shfl_xor(sum, 16, 64);
-      sum += __shfl_xor(sum, 32, 64);
-      if (g == 0) red[wave * BN + t * 16 + r16] = sum;
-    }
-    __syncthreads();
-    if (tid < BN) {
-      const float S = red[tid] + red[BN + tid] + red[2 * BN + tid] + red[3 * BN + tid];
-      bmean[tid] = cntv ? S / cntv : 0.f;
-      if (co0 + tid < a.cout) {
-        if (ep.stats) ep.stats[sbase + co0 + tid] = S;
-        else *bn_slot(ep, 0, a.cout, co0 + tid, blockIdx.x) = S;
-      }
-    }
-    __syncthreads();
-#pragma unroll
-    for (int t = 0; t < NT; ++t) {
-      const int cl = t * 16 + r16;
-      const float m = bmean[cl];
-      float q = 0.f;
-#pragma unroll
-      for (int jj = 0; jj < 4; ++jj) {
-        const float d = (rowv[jj] && co0 + cl < a.cout) ? vals[t][jj] - m : 0.f;
-        q += d * d;
-      }
-      q += __shfl_xor(q, 16, 64);
-      q += __shfl_xor(q, 32, 64);
-      if (g == 0) red[wave * BN + cl] = q;
-    }
-    __syncthreads();
-    if (tid < BN) {
-      const float M2 = red[tid] + red[BN + tid] + red[2 * BN + tid] + red[3 * BN + tid];
-      if (co0 + tid < a.cout) {
-        if (ep.stats) ep.stats[sbase + a.cout + co0 + tid] = M2;
-        else *bn_slot(ep, 1, a.cout, co0 + tid, blockIdx.x) = M2;
-      }
-    }
-    if (tid == 0 && blockIdx.y == 0) {
-      if (ep.stats) ep.stats[sbase + 2 * a.cout] = (float)cntv;
-      else *bn_slot(ep, 2, a.cout, 0, blockIdx.x) = (float)cntv;
+    for (int k = 0; k < ST_PER; ++k) {
+      const int i = tid + 256 * k;
+      if (i >= ST) break;
+      const int c4 = i & 15, v = i >> 4;
+      const int hx = v % 6, hy = (v / 6) % 6, hz = v / 36;
+      const int row = hz * K3_HY + hy, vv = row * K3_HX + hx;
+      const int pg = (c4 >> 1) ^ ((row * 2) & 7);
+      bf16x4_h u;
+      u[0] = (__bf16)sv[k][0]; u[1] = (__bf16)sv[k][1]; u[2] = (__bf16)sv[k][2]; u[3] = (__bf16)sv[k][3];
+      *reinterpret_cast<bf16x4_h*>(halo + vv * K3_VROW + pg * 8 + 4 * (c4 & 1)) = u;
     }
   }
-  if (ep.bn_mode == 2) {  // fused BatchNorm backward statistics: this block's slot of the slab
-    float p1[NT], p2[NT];
+  __syncthreads();
+
+  f32x4 acc[4][NT];  // [M tile = tile z slice][N tile]
 #pragma unroll
-    for (int t = 0; t < NT; ++t) {
-      const int c = co0 + t * 16 + r16;
-      p1[t] = 0.f;
-      p2[t] = 0.f;
-      if (c < a.cout) {
+  for (int m = 0; m < 4; ++m)
 #pragma unroll
-        for (int jj = 0; jj < 4; ++jj)
-          if (rowv[jj]) bn_pair_z(ep, vals[t][jj], zv[t][jj], c, a.cout, &p1[t], &p2[t]);
-      }
-      p1[t] += __shfl_xor(p1[t], 16, 64);
-      p1[t] += __shfl_xor(p1[t], 32, 64);
-      p2[t] += __shfl_xor(p2[t], 16, 64);
-      p2[t] += __shfl_xor(p2[t], 32, 64);
-    }
-    __syncthreads();
-    float* red = reinterpret_cast<float*>(smem);  // [2][4 waves][BN]
-    if (g == 0) {
+    for (int nt = 0; nt < NT; ++nt) acc[m][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int ly = r16 >> 2, lx = r16 & 3;  // this lane's A row (y, x) inside an M tile
+  if (!(a.dbg & 2))
 #pragma unroll
-      for (int t = 0; t < NT; ++t) {
-        red[wave * BN + t * 16 + r16] = p1[t];
-        red[(4 + wave) * BN + t * 16 + r16] = p2[t];
-      }
-    }
-    __syncthreads();
-    if (tid < BN && co0 + tid < a.cout) {
-      *bn_slot(ep, 0, a.cout, co0 + tid, blockIdx.x) = red[tid] + red[BN + tid] + red[2 * BN + tid] + red[3 * BN + tid];
-      *bn_slot(ep, 1, a.cout, co0 + tid, blockIdx.x) =
-          red[4 * BN + tid] + red[5 * BN + tid] + red[6 * BN + tid] + red[7 * BN + tid];
+  for (int j = 0; j < 7; ++j) {  // taps t = wave + 4j (< 27); ring slot j % 3
+    const int t = wave + 4 * j;
+    if (t >= 27) break;  // wave-uniform
+    if (t + 8 < 27 && !(a.dbg & 4)) loadb(t + 8, bq[(j + 2) % 3]);
+    const int td = t / 9, th = (t / 3) % 3, tw = t % 3;
+    const int dz = TR ? 2 - td : td, dy = TR ? 2 - th : th, dx = TR ? 2 - tw : tw;
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+      const int row = (m + dz) * K3_HY + ly + dy;
+      const __bf16* arow = halo + (row * K3_HX + lx + dx) * K3_VROW;
+      const int sw = (row * 2) & 7;
+      bf16x8_h av[KS];
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) av[ks] = *reinterpret_cast<const bf16x8_h*>(arow + 8 * ((ks * 4 + g) ^ sw));
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt)
+          acc[m][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[ks], bq[j % 3][nt][ks], acc[m][nt], 0, 0, 0);
     }
   }
+  // ---- combine the waves' K partials: wave w keeps M tile w, ships the other three
+  __syncthreads();  // halo reads done: the buffer becomes the reduction area [m][slot][nt][256]
+  float* red = reinterpret_cast<float*>(smem);
+#pragma unroll
+  for (int m = 0; m < 4; ++m) {
+    if (m == wave) continue;  // wave-uniform
+    const int slot = wave < m ? wave : wave - 1;
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt)
+      *reinterpret_cast<f32x4*>(red + (((m * 3 + slot) * NT + nt) * 256) + lane * 4) = acc[m][nt];
+  }
+  __syncthreads();
+  f32x4 mine[NT];
+#pragma unroll
+  for (int nt = 0; nt < NT; ++nt) {
+    mine[nt] = acc[0][nt];
+#pragma unroll
+    for (int m = 1; m < 4; ++m)
+      if (m == wave) mine[nt] = acc[m][nt];
+#pragma unroll
+    for (int slot = 0; slot < 3; ++slot)
+      mine[nt] += *reinterpret_cast<const f32x4*>(red + (((wave * 3 + slot) * NT + nt) * 256) + lane * 4);
+  }
+  __syncthreads();  // reduction area free for the epilogue's scratch
+  if (a.dbg & 8) { if (mine[0][0] == 1.2345f) y[0] = 0.f; return; }
+  halo_epilogue<NT>(a, mine, row_out, co0, y, ep, red);
 }
 
 // bf16 [tap][b][a] with 16-byte granules of a XOR-swizzled by (b mod granules-per-row)
@@ -341,6 +498,7 @@ void halo_set_min_blocks(int v) { g_halo_min_blocks = v; }
 static bool halo_setup(const cgan3d_conv_geom* g, HaloArgs* a) {
   if (g->prec != CGAN3D_PREC_BF16 || g->reflect) return false;
   if (!(g->cin == 32 || g->cin == 64) || g->cout % 16 || g->k > 4 || g->stride < 1 || g->stride > 2) return false;
+  a->dbg = g_halo_dbg;
   a->n = g->n; a->di = g->di; a->hi = g->hi; a->wi = g->wi; a->do_ = g->do_; a->ho = g->ho; a->wo = g->wo;
   a->cin = g->cin; a->cout = g->cout; a->k = g->k; a->s = g->stride; a->p = g->pad; a->transposed = g->transposed;
   if (g->transposed && g->stride > 1) {
@@ -372,6 +530,17 @@ static bool halo_setup(const cgan3d_conv_geom* g, HaloArgs* a) {
   return true;
 }
 
+static int g_k3_tile = 1;  // cgan3d_set_tuning key 3: 0 keeps the ResNet convs on conv_halo_kernel
+
+void halo_set_dbg(int v) { g_halo_dbg = v; }
+
+void k3_tile_set(int v) { g_k3_tile = v; }
+
+// k3 s1 p1 64 -> 64, forward or input-grad (the input-grad of a stride-1 conv is a stride-1 conv)
+static bool k3_tile_ok(const cgan3d_conv_geom* g) {
+  return g_k3_tile && g->cin == 64 && g->cout == 64 && g->k == 3 && g->stride == 1 && g->pad == 1 && !g->reflect;
+}
+
 bool halo_ok(const cgan3d_conv_geom* g) {
   HaloArgs a;
   return g->w_packed == 2 && halo_setup(g, &a);
@@ -393,6 +562,20 @@ int halo_launch(const cgan3d_conv_geom* g, const float* x, const float* w, float
   if (!halo_setup(g, &a)) {
     set_error("conv_halo: geometry not supported");
     return CGAN3D_EINVAL;
+  }
+  if (k3_tile_ok(g)) {  // ResNet-block shape: whole-tile K-split kernel
+    const long long tiles = (long long)a.n * a.td * a.th * a.tw;
+    const bool split = tiles < g_halo_min_blocks;  // small grids: two 32-channel blocks per tile
+    const dim3 grid1((unsigned)tiles, split ? 2 : 1);
+    const __bf16* wp = reinterpret_cast<const __bf16*>(w);
+    if (split) {
+      if (g->transposed) hipLaunchKernelGGL((conv_k3_kernel<true, 2>), grid1, dim3(256), 0, st, a, x, wp, y, e);
+      else hipLaunchKernelGGL((conv_k3_kernel<false, 2>), grid1, dim3(256), 0, st, a, x, wp, y, e);
+    } else {
+      if (g->transposed) hipLaunchKernelGGL((conv_k3_kernel<true, 4>), grid1, dim3(256), 0, st, a, x, wp, y, e);
+      else hipLaunchKernelGGL((conv_k3_kernel<false, 4>), grid1, dim3(256), 0, st, a, x, wp, y, e);
+    }
+    return CGAN3D_OK;
   }
   dim3 grid((unsigned)(a.nclass * a.n * a.td * a.th * a.tw), g->cout / a.bn);
   const size_t lds = 3 * (size_t)a.bn * g->cin * 2 + a.halo_bytes;
