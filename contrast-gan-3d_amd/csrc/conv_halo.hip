@@ -541,23 +541,22 @@ static bool k3_tile_ok(const cgan3d_conv_geom* g) {
   return g_k3_tile && g->cin == 64 && g->cout == 64 && g->k == 3 && g->stride == 1 && g->pad == 1 && !g->reflect;
 }
 
-bool halo_ok(const cgan3d_conv_geom* g) {
-  HaloArgs a;
-  return g->w_packed == 2 && halo_setup(g, &a);
-}
-
 bool halo_format_ok(const cgan3d_conv_geom* g) {
   HaloArgs a;
-  return halo_setup(g, &a);
+  return s2_kind(g) || halo_setup(g, &a);
 }
 
+bool halo_ok(const cgan3d_conv_geom* g) { return g->w_packed == 2 && halo_format_ok(g); }
+
 long long halo_mblocks(const cgan3d_conv_geom* g) {
+  if (s2_kind(g)) return s2_blocks(g);
   HaloArgs a;
   if (!halo_setup(g, &a)) return 0;
   return (long long)a.nclass * a.n * a.td * a.th * a.tw;
 }
 
 int halo_launch(const cgan3d_conv_geom* g, const float* x, const float* w, float* y, const Epi& e, hipStream_t st) {
+  if (s2_kind(g)) return s2_launch(g, x, reinterpret_cast<const __bf16*>(w), y, e, st);  // conv_s2.hip
   HaloArgs a;
   if (!halo_setup(g, &a)) {
     set_error("conv_halo: geometry not supported");

@@ -1,0 +1,436 @@
+// Stride-2 convolutions between the generator's 16- and 32-channel levels, bf16 MFMA (gfx950).
+//
+// Four launches per step share two shapes (model/generator.py:40-47,61-77; blocks.py:23-38):
+//  * S2F, Conv3d k3 s2 p1, 16 -> 32 channels (gathered 2S^3 -> aligned S^3): the first
+//    downsampling conv forward and the input-grad of the last ConvTranspose3d;
+//  * S2T, the transposed mapping, 32 gathered -> 16 channels on the 2x grid: the last
+//    ConvTranspose3d forward (output_padding 1) and the first downsampling conv's input-grad.
+// conv_halo_kernel does not take them (16-channel K or N side), and the implicit-GEMM kernel
+// re-gathers every tap through L1 (110-127 us per launch at 64^3, B=4).  Both kernels here are
+// built to be HBM-bound: one block stages its input halo once (fp32 NDHWC -> bf16 LDS), holds
+// all of its weight fragments in registers (loaded from L2 before the staging), and writes a
+// 128-voxel (S2F) or 1024-voxel (S2T, all 8 parity classes of a tile) output block.
+//
+// LDS layouts are bank-conflict-free for the MFMA A reads (ds_read_b128 lane groups of
+// MI355X_MICROARCH.md §LDS; the swizzles were found by exhaustive search over every tap offset):
+//  * S2F: an M tile is 16 consecutive outputs along x; tap (td,th,tw) reads input x = 2x + tw,
+//    so the halo keeps each (z, y) input row split by x parity — sub-row [parity][x/2][16 ch],
+//    32-byte voxels — and a lane group reads 16 consecutive voxels of one sub-row.  One K step of
+//    v_mfma_f32_16x16x32_bf16 covers two taps (16 channels each; g>>1 selects the tap).
+//  * S2T: an M tile is 16 consecutive class voxels along x; rows [z][y][17 x][32 ch], 64-byte
+//    voxels with granule g stored at g ^ ((x >> 1) & 2).
+#include "common.h"
+
+namespace cg {
+
+typedef __bf16 bf16x8_s __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4_s __attribute__((ext_vector_type(4)));
+
+struct S2Args {
+  int n, di, hi, wi, do_, ho, wo;
+  int cd, ch, cw;  // output grid (S2F) or class grid (S2T)
+  int td, th, tw;  // tiles per dim
+  int dbg;         // phase switches for timing experiments (cgan3d_set_tuning key 5): 1 no halo
+                   // loads, 2 no MFMA, 4 no output stores, 8 no weight loads
+};
+
+// per-channel sum over the block: v[nt] (this lane's partial for channel nt*16 + r16) summed over
+// the four row groups and the four waves; every lane receives its channels' block totals
+template <int NT>
+__device__ __forceinline__ void block_chan_sum(float (&v)[NT], float* red) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4, r16 = lane & 15;
+#pragma unroll
+  for (int nt = 0; nt < NT; ++nt) {
+    v[nt] += __shfl_xor(v[nt], 16, 64);
+    v[nt] += __shfl_xor(v[nt], 32, 64);
+  }
+  __syncthreads();  // red is free
+  if (g == 0) {
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) red[wave * NT * 16 + nt * 16 + r16] = v[nt];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int nt = 0; nt < NT; ++nt) {
+    const int c = nt * 16 + r16;
+    v[nt] = red[c] + red[NT * 16 + c] + red[2 * NT * 16 + c] + red[3 * NT * 16 + c];
+  }
+}
+
+__device__ __forceinline__ float s2_act(float v, const Epi& ep) {
+  if (ep.act == CGAN3D_ACT_RELU) return fmaxf(v, 0.f);
+  if (ep.act == CGAN3D_ACT_LRELU) return v > 0.f ? v : v * ep.slope;
+  return v;
+}
+
+// Block statistics of the fused BatchNorm slab (include/cgan3d.h): mode 1 (sum, M2 about the block
+// mean, count), mode 2 (sum g, sum g*xhat).  vals / zv: [U][NT][4] per lane, ok: [U][4] row validity.
+template <int U, int NT>
+__device__ __forceinline__ void s2_bn_slab(const Epi& ep, int C, const float (&vals)[U][NT][4], const float (&zv)[U][NT][4],
+                                           const bool (&ok)[U][4], int cnt, float* red) {
+  const int tid = threadIdx.x, r16 = tid & 15;
+  if (ep.bn_mode == 1) {
+    float s[NT];
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) {
+      s[nt] = 0.f;
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) s[nt] += ok[u][j] ? vals[u][nt][j] : 0.f;
+    }
+    block_chan_sum<NT>(s, red);
+    float q[NT];
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) {
+      const float m = cnt ? s[nt] / cnt : 0.f;
+      q[nt] = 0.f;
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const float d = ok[u][j] ? vals[u][nt][j] - m : 0.f;
+          q[nt] += d * d;
+        }
+    }
+    block_chan_sum<NT>(q, red);
+    if (tid < 16) {
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) {
+        *bn_slot(ep, 0, C, nt * 16 + r16, blockIdx.x) = s[nt];
+        *bn_slot(ep, 1, C, nt * 16 + r16, blockIdx.x) = q[nt];
+      }
+      if (tid == 0) *bn_slot(ep, 2, C, 0, blockIdx.x) = (float)cnt;
+    }
+  } else if (ep.bn_mode == 2) {
+    float p1[NT], p2[NT];
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) {
+      p1[nt] = 0.f;
+      p2[nt] = 0.f;
+      const int c = nt * 16 + r16;
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          if (ok[u][j]) bn_pair_z(ep, vals[u][nt][j], zv[u][nt][j], c, C, &p1[nt], &p2[nt]);
+    }
+    block_chan_sum<NT>(p1, red);
+    block_chan_sum<NT>(p2, red);
+    if (tid < 16) {
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) {
+        *bn_slot(ep, 0, C, nt * 16 + r16, blockIdx.x) = p1[nt];
+        *bn_slot(ep, 1, C, nt * 16 + r16, blockIdx.x) = p2[nt];
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// S2F: Conv3d k3 s2 p1, 16 -> 32.  Block = 16 (x) x 4 (y) x 2 (z) outputs; wave w = output row y,
+// both z slices (2 M tiles) x 2 N tiles; K = 27 taps x 16 channels in 14 steps of two taps.
+constexpr int F_HX = 33, F_HY = 9, F_HZ = 5, F_SX = 17;
+constexpr int F_HALO = F_HZ * F_HY * 2 * F_SX * 16;  // bf16 elements (48960 bytes)
+
+__global__ __launch_bounds__(256) void conv_s2f_kernel(S2Args a, const float* __restrict__ x,
+                                                       const __bf16* __restrict__ wpk, float* y, Epi ep) {
+  constexpr int CI = 16, CO = 32, KSTEPS = 14;
+  __shared__ __attribute__((aligned(16))) __bf16 halo[F_HALO];
+  __shared__ float red[4 * CO];
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int g = lane >> 4, r16 = lane & 15;
+  const int tiles = a.td * a.th * a.tw;
+  int bid = blockIdx.x;
+  const int nb = bid / tiles;
+  bid -= nb * tiles;
+  const int Z0 = (bid / (a.th * a.tw)) * 2, Y0 = ((bid / a.tw) % a.th) * 4, X0 = (bid % a.tw) * 16;
+
+  // weight fragments of every K step: lane (channel nt*16 + r16, tap 2s + (g>>1), granule g&1)
+  bf16x8_s bq[KSTEPS][2];
+#pragma unroll
+  for (int s = 0; s < KSTEPS; ++s) {
+    const int t = 2 * s + (g >> 1);
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt) {
+      const int co = nt * 16 + r16;
+      const int tt = t < 27 ? t : 26;
+      bq[s][nt] = (a.dbg & 8) ? bf16x8_s{} : *reinterpret_cast<const bf16x8_s*>(wpk + ((long long)tt * CO + co) * CI + 8 * ((g & 1) ^ (co & 1)));
+      if (t >= 27) bq[s][nt] = bf16x8_s{};
+    }
+  }
+
+  // halo: input (2*Z0-1 .. +5, 2*Y0-1 .. +9, 2*X0-1 .. +33) -> [hz][hy][x parity][x/2][16] bf16
+  {
+    const int iz0 = 2 * Z0 - 1, iy0 = 2 * Y0 - 1, ix0 = 2 * X0 - 1;
+    constexpr int NV4 = F_HZ * F_HY * F_HX * 4, PER = (NV4 + 255) / 256, BATCH = 8;
+#pragma unroll
+    for (int k0 = 0; k0 < PER; k0 += BATCH) {
+      f32x4 sv[BATCH];
+#pragma unroll
+      for (int k = 0; k < BATCH; ++k) {
+        const int i = tid + 256 * (k0 + k);
+        const int c4 = i & 3, v = i >> 2;
+        const int hx = v % F_HX, r = v / F_HX;
+        const int hy = r % F_HY, hz = r / F_HY;
+        const int iz = iz0 + hz, iy = iy0 + hy, ix = ix0 + hx;
+        const bool ok = !(a.dbg & 1) && k0 + k < PER && i < NV4 && (unsigned)iz < (unsigned)a.di && (unsigned)iy < (unsigned)a.hi &&
+                        (unsigned)ix < (unsigned)a.wi;
+        sv[k] = *reinterpret_cast<const f32x4*>(
+            x + (ok ? ((((long long)nb * a.di + iz) * a.hi + iy) * a.wi + ix) * CI + 4 * c4 : 0));
+        if (!ok) sv[k] = f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+#pragma unroll
+      for (int k = 0; k < BATCH; ++k) {
+        const int i = tid + 256 * (k0 + k);
+        if (k0 + k >= PER || i >= NV4) break;
+        const int c4 = i & 3, v = i >> 2;
+        const int hx = v % F_HX, r = v / F_HX;
+        const int row = r * 2 + (hx & 1);
+        bf16x4_s u;
+        u[0] = (__bf16)sv[k][0]; u[1] = (__bf16)sv[k][1]; u[2] = (__bf16)sv[k][2]; u[3] = (__bf16)sv[k][3];
+        *reinterpret_cast<bf16x4_s*>(halo + (row * F_SX + (hx >> 1)) * CI + 4 * c4) = u;
+      }
+    }
+  }
+  __syncthreads();
+
+  f32x4 acc[2][2];
+#pragma unroll
+  for (int zz = 0; zz < 2; ++zz)
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt) acc[zz][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  if (!(a.dbg & 2))
+#pragma unroll
+  for (int s = 0; s < KSTEPS; ++s) {
+    int t = 2 * s + (g >> 1);
+    t = t < 27 ? t : 26;  // the padding tap reads valid data against zero weights
+    const int td = t / 9, th = (t / 3) % 3, tw = t % 3;
+#pragma unroll
+    for (int zz = 0; zz < 2; ++zz) {
+      const int row = ((2 * zz + td) * F_HY + 2 * wave + th) * 2 + (tw & 1);
+      const bf16x8_s av =
+          *reinterpret_cast<const bf16x8_s*>(halo + (row * F_SX + r16 + (tw >> 1)) * CI + 8 * (g & 1));
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt)
+        acc[zz][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, bq[s][nt], acc[zz][nt], 0, 0, 0);
+    }
+  }
+
+  // ---- epilogue: lane holds outputs x = X0 + 4g + j, y = Y0 + wave, z = Z0 + zz, channel nt*16 + r16
+  float vals[2][2][4], zv[2][2][4];
+  bool ok[2][4];
+  const int oy = Y0 + wave;
+#pragma unroll
+  for (int zz = 0; zz < 2; ++zz) {
+    const int oz = Z0 + zz;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int ox = X0 + 4 * g + j;
+      ok[zz][j] = oz < a.cd && oy < a.ch && ox < a.cw;
+      const long long o = ok[zz][j] ? (((long long)nb * a.cd + oz) * a.ch + oy) * a.cw + ox : 0;
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt) {
+        const int c = nt * 16 + r16;
+        zv[zz][nt][j] = ep.bn_mode == 2 ? ep.bn_z[o * CO + c] : 0.f;
+        float v = acc[zz][nt][j] + (ep.bias ? ep.bias[c] : 0.f);
+        v = s2_act(v, ep);
+        if (ok[zz][j] && (!(a.dbg & 4) || v == 1.2345f)) y[o * CO + c] = v;
+        vals[zz][nt][j] = v;
+      }
+    }
+  }
+  if (ep.bn_mode) {
+    const int cnt = max(0, min(2, a.cd - Z0)) * max(0, min(4, a.ch - Y0)) * max(0, min(16, a.cw - X0));
+    s2_bn_slab<2, 2>(ep, CO, vals, zv, ok, cnt, red);
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// S2T: transposed k3 s2 p1 (output = 2 x gathered grid), 32 gathered -> 16 channels.  Block = a
+// 16 x 4 x 2 tile of class coordinates j, all 8 parity classes r (output 2j + r): wave w = class
+// row y, both z slices x 8 classes = 16 M tiles, one N tile; 27 taps, K = 32 channels each.
+// Class r, per dim: r = 0 -> tap 1 at gathered j; r = 1 -> tap 0 at j + 1 and tap 2 at j.
+constexpr int T_HX = 17, T_HY = 5, T_HZ = 3;
+constexpr int T_HALO = T_HZ * T_HY * T_HX * 32;  // bf16 elements (16320 bytes)
+
+template <int R>
+struct S2Taps;  // per-dim taps of parity class R: (tap, gathered offset)
+template <>
+struct S2Taps<0> {
+  static constexpr int n = 1;
+  static constexpr int t[2] = {1, 1};
+  static constexpr int off[2] = {0, 0};
+};
+template <>
+struct S2Taps<1> {
+  static constexpr int n = 2;
+  static constexpr int t[2] = {0, 2};
+  static constexpr int off[2] = {1, 0};
+};
+
+template <int RZ, int RY, int RX>
+__device__ __forceinline__ void s2t_class(const __bf16* halo, const bf16x8_s (&bq)[27], f32x4 (&acc)[2], int wave,
+                                          int g, int r16) {
+  using TZ = S2Taps<RZ>;
+  using TY = S2Taps<RY>;
+  using TX = S2Taps<RX>;
+#pragma unroll
+  for (int a = 0; a < TZ::n; ++a)
+#pragma unroll
+    for (int b = 0; b < TY::n; ++b)
+#pragma unroll
+      for (int c = 0; c < TX::n; ++c) {
+        const int t = TZ::t[a] * 9 + TY::t[b] * 3 + TX::t[c];
+        const int hx = r16 + TX::off[c];
+#pragma unroll
+        for (int zz = 0; zz < 2; ++zz) {
+          const int row = (zz + TZ::off[a]) * T_HY + wave + TY::off[b];
+          const bf16x8_s av =
+              *reinterpret_cast<const bf16x8_s*>(halo + (row * T_HX + hx) * 32 + 8 * (g ^ ((hx >> 1) & 2)));
+          acc[zz] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, bq[t], acc[zz], 0, 0, 0);
+        }
+      }
+}
+
+__global__ __launch_bounds__(256) void conv_s2t_kernel(S2Args a, const float* __restrict__ x,
+                                                       const __bf16* __restrict__ wpk, float* y, Epi ep) {
+  constexpr int CI = 32, CO = 16;
+  __shared__ __attribute__((aligned(16))) __bf16 halo[T_HALO];
+  __shared__ float red[4 * CO];
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int g = lane >> 4, r16 = lane & 15;
+  const int tiles = a.td * a.th * a.tw;
+  int bid = blockIdx.x;
+  const int nb = bid / tiles;
+  bid -= nb * tiles;
+  const int Z0 = (bid / (a.th * a.tw)) * 2, Y0 = ((bid / a.tw) % a.th) * 4, X0 = (bid % a.tw) * 16;
+
+  bf16x8_s bq[27];  // lane (channel r16, granule g) of every tap
+#pragma unroll
+  for (int t = 0; t < 27; ++t)
+    bq[t] = (a.dbg & 8) ? bf16x8_s{} : *reinterpret_cast<const bf16x8_s*>(wpk + ((long long)t * CO + r16) * CI + 8 * (g ^ (r16 & 3)));
+
+  {  // halo: gathered (Z0 .. +3, Y0 .. +5, X0 .. +17) -> [hz][hy][hx][32] bf16, granule swizzle
+    constexpr int NV4 = T_HZ * T_HY * T_HX * 8, PER = (NV4 + 255) / 256;
+    f32x4 sv[PER];
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+      const int i = tid + 256 * k;
+      const int c4 = i & 7, v = i >> 3;
+      const int hx = v % T_HX, r = v / T_HX;
+      const int hy = r % T_HY, hz = r / T_HY;
+      const int iz = Z0 + hz, iy = Y0 + hy, ix = X0 + hx;
+      const bool ok = !(a.dbg & 1) && i < NV4 && iz < a.di && iy < a.hi && ix < a.wi;
+      sv[k] = *reinterpret_cast<const f32x4*>(
+          x + (ok ? ((((long long)nb * a.di + iz) * a.hi + iy) * a.wi + ix) * CI + 4 * c4 : 0));
+      if (!ok) sv[k] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+      const int i = tid + 256 * k;
+      if (i >= NV4) break;
+      const int c4 = i & 7, v = i >> 3;
+      const int hx = v % T_HX;
+      bf16x4_s u;
+      u[0] = (__bf16)sv[k][0]; u[1] = (__bf16)sv[k][1]; u[2] = (__bf16)sv[k][2]; u[3] = (__bf16)sv[k][3];
+      *reinterpret_cast<bf16x4_s*>(halo + v * 32 + 8 * ((c4 >> 1) ^ ((hx >> 1) & 2)) + 4 * (c4 & 1)) = u;
+    }
+  }
+  __syncthreads();
+
+  f32x4 acc[8][2];
+#pragma unroll
+  for (int c = 0; c < 8; ++c) acc[c][0] = acc[c][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+  if (!(a.dbg & 2)) {
+  s2t_class<0, 0, 0>(halo, bq, acc[0], wave, g, r16);
+  s2t_class<0, 0, 1>(halo, bq, acc[1], wave, g, r16);
+  s2t_class<0, 1, 0>(halo, bq, acc[2], wave, g, r16);
+  s2t_class<0, 1, 1>(halo, bq, acc[3], wave, g, r16);
+  s2t_class<1, 0, 0>(halo, bq, acc[4], wave, g, r16);
+  s2t_class<1, 0, 1>(halo, bq, acc[5], wave, g, r16);
+  s2t_class<1, 1, 0>(halo, bq, acc[6], wave, g, r16);
+  s2t_class<1, 1, 1>(halo, bq, acc[7], wave, g, r16);
+  }
+
+  // ---- epilogue: class c = (rz, ry, rx), slice zz, row j -> output (2(Z0+zz)+rz, 2(Y0+w)+ry, 2(X0+4g+j)+rx)
+  float vals[16][1][4], zv[16][1][4];
+  bool ok[16][4];
+  const int jy = Y0 + wave;
+  const float bias = ep.bias ? ep.bias[r16] : 0.f;
+#pragma unroll
+  for (int c = 0; c < 8; ++c) {
+    const int rz = c >> 2, ry = (c >> 1) & 1, rx = c & 1;
+#pragma unroll
+    for (int zz = 0; zz < 2; ++zz) {
+      const int jz = Z0 + zz;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int jx = X0 + 4 * g + j;
+        const bool v_ok = jz < a.cd && jy < a.ch && jx < a.cw;
+        ok[c * 2 + zz][j] = v_ok;
+        const long long o =
+            v_ok ? (((long long)nb * a.do_ + 2 * jz + rz) * a.ho + 2 * jy + ry) * a.wo + 2 * jx + rx : 0;
+        zv[c * 2 + zz][0][j] = ep.bn_mode == 2 ? ep.bn_z[o * CO + r16] : 0.f;
+        const float v = s2_act(acc[c][zz][j] + bias, ep);
+        if (v_ok && (!(a.dbg & 4) || v == 1.2345f)) y[o * CO + r16] = v;
+        vals[c * 2 + zz][0][j] = v;
+      }
+    }
+  }
+  if (ep.bn_mode) {
+    const int cnt = 8 * max(0, min(2, a.cd - Z0)) * max(0, min(4, a.ch - Y0)) * max(0, min(16, a.cw - X0));
+    s2_bn_slab<16, 1>(ep, CO, vals, zv, ok, cnt, red);
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+static int g_s2 = 1;  // cgan3d_set_tuning key 4: 0 keeps these shapes on the implicit-GEMM kernel
+static int g_s2_dbg = 0;  // key 5
+
+void s2_set(int v) { g_s2 = v; }
+void s2_set_dbg(int v) { g_s2_dbg = v; }
+
+// 1: S2F, 2: S2T, 0: neither
+int s2_kind(const cgan3d_conv_geom* g) {
+  if (!g_s2 || g->prec != CGAN3D_PREC_BF16 || g->reflect || g->k != 3 || g->stride != 2 || g->pad != 1) return 0;
+  if (!g->transposed && g->cin == 16 && g->cout == 32 && g->do_ == (g->di - 1) / 2 + 1 &&
+      g->ho == (g->hi - 1) / 2 + 1 && g->wo == (g->wi - 1) / 2 + 1)
+    return 1;
+  if (g->transposed && g->cin == 32 && g->cout == 16 && g->do_ == 2 * g->di && g->ho == 2 * g->hi &&
+      g->wo == 2 * g->wi)
+    return 2;
+  return 0;
+}
+
+static S2Args s2_args(const cgan3d_conv_geom* g, int kind) {
+  S2Args a;
+  a.n = g->n; a.di = g->di; a.hi = g->hi; a.wi = g->wi; a.do_ = g->do_; a.ho = g->ho; a.wo = g->wo;
+  if (kind == 1) { a.cd = g->do_; a.ch = g->ho; a.cw = g->wo; }
+  else { a.cd = g->di; a.ch = g->hi; a.cw = g->wi; }
+  a.td = (a.cd + 1) / 2; a.th = (a.ch + 3) / 4; a.tw = (a.cw + 15) / 16;
+  a.dbg = g_s2_dbg;
+  return a;
+}
+
+long long s2_blocks(const cgan3d_conv_geom* g) {
+  const int kind = s2_kind(g);
+  if (!kind) return 0;
+  S2Args a = s2_args(g, kind);
+  return (long long)a.n * a.td * a.th * a.tw;
+}
+
+int s2_launch(const cgan3d_conv_geom* g, const float* x, const __bf16* wp, float* y, const Epi& e, hipStream_t st) {
+  const int kind = s2_kind(g);
+  if (!kind || e.residual || e.mask_src || e.stats || e.minuend || e.out2) {
+    set_error("conv_s2: geometry or epilogue not supported (residual/mask/stats/out2)");
+    return CGAN3D_EINVAL;
+  }
+  S2Args a = s2_args(g, kind);
+  const dim3 grid((unsigned)((long long)a.n * a.td * a.th * a.tw));
+  if (kind == 1) hipLaunchKernelGGL(conv_s2f_kernel, grid, dim3(256), 0, st, a, x, wp, y, e);
+  else hipLaunchKernelGGL(conv_s2t_kernel, grid, dim3(256), 0, st, a, x, wp, y, e);
+  return CGAN3D_OK;
+}
+
+}  // namespace cg

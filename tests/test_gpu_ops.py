@@ -397,3 +397,86 @@ def test_wgrad_bf16_conv_transpose():
     dwo = torch.empty(w.shape, device="cuda")
     ops.wgrad(gw, _cl(gy), _cl(x), dwo, ws)
     assert_close(dwo.double().cpu().numpy(), dw.numpy(), 2e-2, "bf16 convT wgrad")
+
+
+S2_CASES = [
+    # role, spatial of the 16-channel (fine) grid
+    ("down_fwd", (10, 12, 36)),    # Conv3d 16 -> 32 k3 s2 p1 forward (S2F)
+    ("down_fwd", (11, 9, 17)),     # odd fine grid: partial tiles on every axis
+    ("up_dgrad", (10, 12, 36)),    # ConvTranspose3d 32 -> 16 input-grad = stride-2 conv (S2F)
+    ("up_fwd", (10, 12, 36)),      # ConvTranspose3d 32 -> 16 forward, output_padding 1 (S2T)
+    ("down_dgrad", (10, 12, 36)),  # Conv3d 16 -> 32 input-grad = transposed mapping (S2T)
+    ("up_fwd", (6, 10, 34)),
+]
+
+
+@pytest.mark.parametrize("role,fine", S2_CASES)
+def test_conv_s2_bf16(role, fine):
+    """Stride-2 16 <-> 32-channel kernels (conv_s2.hip) in all four generator roles: output against
+    torch float64 within 2e-2 (bf16 operands, fp32 accumulation), bias + ReLU epilogue, and both
+    fused BatchNorm slab modes against the kernel's own output (1e-4)."""
+    from cgan3d_amd import ops, _lib as L
+    n, k, s, p = 2, 3, 2, 1
+    fine = tuple(fine)
+    coarse = tuple((d - 1) // 2 + 1 for d in fine)
+    if role.startswith("up"):  # the ConvTranspose's coarse grid must map onto exactly 2x
+        fine = tuple(2 * d for d in coarse)
+    g = torch.Generator().manual_seed(3 + len(role) + fine[2])
+    if role == "down_fwd":       # x16 (fine) -> y32 (coarse)
+        w = torch.randn(32, 16, k, k, k, generator=g, dtype=torch.float64) / np.sqrt(16 * 27)
+        x = torch.randn(n, 16, *fine, generator=g, dtype=torch.float64)
+        ref = F.conv3d(x, w, stride=s, padding=p)
+        geo0 = ops.conv_fwd_geom(n, fine, coarse, 16, 32, k, s, p)
+    elif role == "down_dgrad":   # dz32 (coarse) -> dx16 (fine)
+        w = torch.randn(32, 16, k, k, k, generator=g, dtype=torch.float64) / np.sqrt(32 * 27)
+        x = torch.randn(n, 32, *coarse, generator=g, dtype=torch.float64)
+        ref = torch.nn.grad.conv3d_input((n, 16, *fine), w, x, stride=s, padding=p)
+        geo0 = ops.conv_dgrad_geom(n, fine, coarse, 16, 32, k, s, p)
+    elif role == "up_fwd":       # ConvTranspose3d(32 -> 16): x32 (coarse) -> y16 (fine)
+        w = torch.randn(32, 16, k, k, k, generator=g, dtype=torch.float64) / np.sqrt(32 * 27)
+        x = torch.randn(n, 32, *coarse, generator=g, dtype=torch.float64)
+        ref = F.conv_transpose3d(x, w, stride=s, padding=p, output_padding=1)
+        geo0 = ops.convt_fwd_geom(n, coarse, fine, 32, 16, k, s, p)
+    else:                        # up_dgrad: dy16 (fine) -> dx32 (coarse)
+        w = torch.randn(32, 16, k, k, k, generator=g, dtype=torch.float64) / np.sqrt(16 * 27)
+        x = torch.randn(n, 16, *fine, generator=g, dtype=torch.float64)
+        ref = F.conv3d(x, w, stride=s, padding=p)
+        geo0 = ops.convt_dgrad_geom(n, coarse, fine, 32, 16, k, s, p)
+    cout = ref.shape[1]
+    bias = torch.randn(cout, generator=g, dtype=torch.float64) * 0.1
+    ps = ops.PackSet(torch.device("cuda"))
+    geo, wp = ps.add(geo0, w.float().cuda(), L.PREC_BF16)
+    ps.pack()
+    assert geo.w_packed == 2, "expected the halo-format (conv_s2) kernel"
+    dout = tuple(ref.shape[2:])
+    y = torch.empty(n, *dout, cout, device="cuda")
+    slots = ops.bn_slots(geo)
+    part = torch.full(((2 * cout + 1) * slots,), float("nan"), device="cuda")
+    ops.conv(geo, _cl(x), wp, y, ops.epilogue(bias=bias.float().cuda(), act=L.ACT_RELU, bn_part=part, bn_mode=1,
+                                              bn_slots=slots))
+    assert_close(_ncdhw(y).numpy(), torch.relu(ref + bias.view(1, -1, 1, 1, 1)).numpy(), 2e-2, f"{role} out")
+    sl = part.double().cpu().view(2 * cout + 1, slots)
+    cnt = sl[2 * cout]
+    tot = cnt.sum()
+    yk = y.double().cpu().reshape(-1, cout)
+    assert int(tot) == yk.shape[0]
+    mean = sl[:cout].sum(1) / tot
+    bm = sl[:cout] / cnt.clamp(min=1)
+    m2 = sl[cout:2 * cout].sum(1) + (cnt * (bm - mean[:, None]) ** 2).sum(1)
+    assert_close(mean.numpy(), yk.mean(0).numpy(), 1e-4, f"{role} slab mean")
+    assert_close((m2 / tot).numpy(), yk.var(0, unbiased=False).numpy(), 1e-4, f"{role} slab var")
+    # mode 2: (sum g, sum g*xhat) of a BatchNorm + ReLU layer whose input z has this output's shape
+    z = torch.randn(n, *dout, cout, generator=g).cuda()
+    ss = torch.cat([torch.rand(cout, generator=g) + 0.5, torch.randn(cout, generator=g) * 0.2]).cuda()
+    mi = torch.cat([torch.randn(cout, generator=g) * 0.1, torch.rand(cout, generator=g) + 0.5]).cuda()
+    part2 = torch.full((2 * cout * slots,), float("nan"), device="cuda")
+    y2 = torch.empty_like(y)
+    ops.conv(geo, _cl(x), wp, y2, ops.epilogue(bn_part=part2, bn_mode=2, bn_slots=slots, bn_z=z, bn_ss=ss, bn_mi=mi,
+                                               bn_act=L.ACT_RELU))
+    o = y2.double().cpu().reshape(-1, cout)
+    zz = z.double().cpu().reshape(-1, cout)
+    ssd, mid = ss.double().cpu(), mi.double().cpu()
+    gg = o * ((zz * ssd[:cout] + ssd[cout:]) > 0).double()
+    want = torch.cat([gg.sum(0), (gg * (zz - mid[:cout]) * mid[cout:]).sum(0)])
+    got = part2.double().cpu().view(2 * cout, slots).sum(1)
+    assert_close(got.numpy(), want.numpy(), 1e-4, f"{role} mode-2 slab")

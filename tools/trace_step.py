@@ -1,4 +1,4 @@
-"""Per-step view of a rocprofv3 kernel trace (``--kernel-trace --output-format csv``).
+"""Per-step view of a rocprofv3 kernel trace (``--kernel-trace``; CSV or the SQLite ``*_results.db``).
 
     python tools/trace_step.py gpurun_out/prof/run_kernel_trace.csv [--steps 20] [--drop-last 10] [--list]
 
@@ -12,6 +12,17 @@ import collections
 import csv
 
 
+def load_rows(path):
+    """Kernel-trace rows from a rocprofv3 CSV or its default SQLite output (``*_results.db``)."""
+    if not path.endswith(".db"):
+        return list(csv.DictReader(open(path)))
+    import sqlite3
+    c = sqlite3.connect(path)
+    q = "select name, start, end, queue_id, grid_x, workgroup_x from kernels"
+    return [{"Kernel_Name": n, "Start_Timestamp": s, "End_Timestamp": e, "Queue_Id": qid, "Grid_Size_X": gx,
+             "Workgroup_Size_X": wx} for n, s, e, qid, gx, wx in c.execute(q)]
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("trace")
@@ -20,7 +31,7 @@ def main():
     ap.add_argument("--drop-last", type=int, default=10, help="trailing steps to skip (bench.py's roofline steps)")
     ap.add_argument("--top", type=int, default=40)
     a = ap.parse_args()
-    rows = sorted(csv.DictReader(open(a.trace)), key=lambda r: int(r["Start_Timestamp"]))
+    rows = sorted(load_rows(a.trace), key=lambda r: int(r["Start_Timestamp"]))
     adam = [i for i, r in enumerate(rows) if r["Kernel_Name"].startswith("cg::adam_kernel")]
     ends = adam[1::2]  # two Adam launches per step: critic, then generator
     if a.drop_last:
