@@ -49,7 +49,7 @@ def conv_flops(n, dout, cin, cout, k):
 # (HBM bytes per launch from rocprofv3 FETCH_SIZE / WRITE_SIZE passes, profiles/)
 ROOFLINES = {
     "halo_res": ("ResNet-block Conv3d 64->64 k3 s1 at (S/4)^3, forward + input-grad "
-                 "(bf16: conv_halo_kernel; f32: conv_gemm_kernel)",
+                 "(bf16: conv_k3_kernel; f32: conv_gemm_kernel)",
                  "conv", lambda g: g.cin == 64 and g.cout == 64 and g.k == 3 and g.stride == 1,
                  "profiles/r01_pmc_conv_halo_64_4.json"),
     "k7_w2n": ("k7m_w2n_kernel: generator last Conv3d 16->1 k7 (+bias, tanh, opt_hat) forward",
@@ -109,9 +109,10 @@ def main():
     ap.add_argument("--precision", choices=["f32", "bf16"], default="bf16",
                     help="MFMA operand precision of the convolutions (accumulation is f32)")
     ap.add_argument("--roofline", choices=sorted(ROOFLINES), default="halo_res")
-    ap.add_argument("--graph", action="store_true",
-                    help="replay the step as one captured HIP graph (default: eager launches, which let the "
-                         "weight-gradient side stream run concurrently on its own hardware queue)")
+    ap.add_argument("--mode", choices=["plan", "eager", "graph"], default="plan",
+                    help="plan (default): the step recorded once as a launch plan (cgan3d_plan_*) and re-issued "
+                         "from C++ each step, two streams kept; eager: the Python wrappers launch every kernel; "
+                         "graph: one captured HIP graph per step (1 GPU only)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -141,7 +142,7 @@ def main():
     d = pcg64_init_(PatchGANDiscriminator(1, 8, 3, negative_slope=0.2, norm_layer=nn.Identity), 1).to(dev)
     eng = StepEngine(g, d, g.config, d.config, B, B, (S, S, S), g_hyper=(1e-4, 0.0, 0.9, 1e-8),
                      d_hyper=(1e-4, 0.0, 0.9, 1e-8), device=dev, precision=args.precision)
-    use_graph = args.graph and world == 1
+    mode = "eager" if (args.mode == "graph" and world > 1) else args.mode
     batches = []
     for j in range(2):
         opt, _ = synth_patches(B, S, 1000 * rank + 10 * j)
@@ -172,19 +173,27 @@ def main():
         eng.load_inputs(*batches[i % len(batches)])
         eng.replay()
 
+    def plan_step(i):
+        eng.load_inputs(*batches[i % len(batches)])
+        eng.run_plan()
+
     for i in range(args.warmup):
         one_step(i, False)
-    if use_graph:
+    if mode == "graph":
         torch.cuda.synchronize()
         eng.capture()  # records one step; replays below run the whole step as one graph launch
+    elif mode == "plan":
+        eng.record()  # records one step's launches (nothing runs); run_plan() re-issues them
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(args.steps):
-        if use_graph:
+        if mode == "graph":
             graph_step(i)
+        elif mode == "plan":
+            plan_step(i)
         else:
             one_step(i, False)
     torch.cuda.synchronize()
@@ -220,7 +229,7 @@ def main():
         "data": "synthetic",
         "config": {"workload": f"{S}^3 patches, {B} OPT + {B} LOW/HIGH per GPU, full G+D step (WGAN-GP conf)",
                    "global_batch": world * B, "patch": S, "parallelism": f"dp{world}",
-                   "hip_graph": use_graph},
+                   "launch_mode": mode},
         "roofline": {"kernel": roof_desc, "bound": "mfma", "achieved": round(achieved, 3), "peak": peak,
                      "unit": "TFLOP/s", "frac": round(achieved / peak, 4),
                      "traffic": pmc_traffic(roof_pmc, S, B, args.precision), "traffic_source": roof_pmc,

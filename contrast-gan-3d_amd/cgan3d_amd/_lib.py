@@ -80,6 +80,12 @@ _SIGS = {
     "cgan3d_generator_output_grad": ([_P, _P, _P, _P, _P, _I64, _F, _F, _F, _F, _P, _P, _P, _P], _I32),
     "cgan3d_adam_tick": ([_P, _P], _I32),
     "cgan3d_adam": ([_P, _P, _P, _P, _I64, _P, _P], _I32),
+    "cgan3d_plan_begin": ([], _I32),
+    "cgan3d_plan_end": ([C.POINTER(C.c_void_p)], _I32),
+    "cgan3d_plan_size": ([_P], _I64),
+    "cgan3d_plan_run": ([_P], _I32),
+    "cgan3d_plan_destroy": ([_P], _I32),
+    "cgan3d_stream_wait": ([_P, _P], _I32),
 }
 
 _lib = None

@@ -199,7 +199,7 @@ class GeneratorPlan:
         """Enqueue ``fn``'s launches on the side stream after everything enqueued so far."""
         if self.side is None:
             return fn()
-        self.side.wait_stream(torch.cuda.current_stream(self.device))
+        ops.stream_wait(self.side, torch.cuda.current_stream(self.device))
         with torch.cuda.stream(self.side):
             fn()
 
@@ -293,7 +293,7 @@ class GeneratorPlan:
             ep.residual = res
             ops.conv(self.geo_dgrad[i], self.dz[i], self.wd[i], self.dy[i - 1], ep)
         if self.side is not None:  # the weight gradients are complete before anything reads them
-            torch.cuda.current_stream(self.device).wait_stream(self.side)
+            ops.stream_wait(torch.cuda.current_stream(self.device), self.side)
 
 
 def _running_scale_shift(P, nb, ss):
@@ -623,11 +623,14 @@ class StepEngine:
         if self.world == 1:
             return
         dist = torch.distributed
-        if dist.get_backend(self.pg) == "nccl":
-            dist.all_reduce(flat_grad, op=dist.ReduceOp.AVG, group=self.pg)
-        else:
-            dist.all_reduce(flat_grad, op=dist.ReduceOp.SUM, group=self.pg)
-            flat_grad.mul_(1.0 / self.world)
+
+        def reduce():
+            if dist.get_backend(self.pg) == "nccl":
+                dist.all_reduce(flat_grad, op=dist.ReduceOp.AVG, group=self.pg)
+            else:
+                dist.all_reduce(flat_grad, op=dist.ReduceOp.SUM, group=self.pg)
+                flat_grad.mul_(1.0 / self.world)
+        ops.plan_host(reduce)  # inside a recorded plan: runs between its C segments
 
     def capture(self, do_critic: bool = True, do_generator: bool = True):
         """Record one whole step (~200 launches) as a HIP graph; ``replay()`` then costs one launch.
@@ -649,6 +652,25 @@ class StepEngine:
 
     def replay(self):
         self.graph.replay()
+        return self.losses
+
+    def record(self, do_critic: bool = True, do_generator: bool = True) -> "ops.Plan":
+        """Record one step as a launch plan (cgan3d_plan_*): ``run_plan()`` then re-issues its
+        ~200 launches from C++ on the same two streams, without the Python wrappers' per-launch
+        cost.  Nothing is executed while recording.  Collectives (world > 1) stay host callables
+        between the plan's C segments.  Same validity rules as ``capture``; the plan runs on the
+        streams current at recording time."""
+        ops.plan_begin()
+        try:
+            self.step(do_critic, do_generator)
+        except BaseException:
+            ops.plan_abort()
+            raise
+        self.plan = ops.plan_end()
+        return self.plan
+
+    def run_plan(self):
+        self.plan.run()
         return self.losses
 
     def step(self, do_critic: bool = True, do_generator: bool = True):

@@ -233,6 +233,91 @@ def _launch(name, *args):
     return getattr(L.lib(), name)(*args, L.stream())
 
 
+def stream_wait(waiter, signaler):
+    """``waiter`` (torch stream) waits for the work enqueued so far on ``signaler`` — recorded
+    when inside a plan, unlike torch's ``Stream.wait_stream``."""
+    if DRY_RUN or waiter is None or signaler is None:
+        return
+    check(L.lib().cgan3d_stream_wait(waiter.cuda_stream, signaler.cuda_stream), "stream_wait")
+
+
+class Plan:
+    """A recorded step: C-side launch plans (cgan3d_plan_*, include/cgan3d.h) interleaved with host
+    callables that cannot be recorded (RCCL collectives).  ``run()`` re-issues it."""
+
+    def __init__(self):
+        self.items = []
+        self.launches = 0
+
+    def run(self):
+        lib = L.lib()
+        for it in self.items:
+            if isinstance(it, int):
+                check(lib.cgan3d_plan_run(it), "plan_run")
+            else:
+                it()
+
+    def __del__(self):
+        if L._lib is not None:
+            for it in self.items:
+                if isinstance(it, int):
+                    L._lib.cgan3d_plan_destroy(it)
+        self.items = []
+
+
+_RECORDING: Optional[Plan] = None
+
+
+def recording() -> bool:
+    return _RECORDING is not None
+
+
+def plan_begin() -> Plan:
+    global _RECORDING
+    if _RECORDING is not None:
+        raise RuntimeError("plan_begin: already recording")
+    check(L.lib().cgan3d_plan_begin(), "plan_begin")
+    _RECORDING = Plan()
+    return _RECORDING
+
+
+def _plan_close():
+    h = ctypes.c_void_p()
+    check(L.lib().cgan3d_plan_end(ctypes.byref(h)), "plan_end")
+    _RECORDING.launches += int(L.lib().cgan3d_plan_size(h))
+    _RECORDING.items.append(h.value)
+
+
+def plan_host(fn):
+    """While recording: close the current C plan, append host callable ``fn``, open a new plan.
+    Otherwise: call ``fn`` now."""
+    if _RECORDING is None:
+        return fn()
+    _plan_close()
+    _RECORDING.items.append(fn)
+    check(L.lib().cgan3d_plan_begin(), "plan_begin")
+
+
+def plan_end() -> Plan:
+    global _RECORDING
+    if _RECORDING is None:
+        raise RuntimeError("plan_end: not recording")
+    _plan_close()
+    p, _RECORDING = _RECORDING, None
+    return p
+
+
+def plan_abort():
+    """Drop a recording (after an exception while recording)."""
+    global _RECORDING
+    if _RECORDING is None:
+        return
+    try:
+        _plan_close()
+    finally:
+        _RECORDING = None
+
+
 # bench.py's roofline timer: LAUNCH_HOOK(role, geometry) returns (start, end, reps) — two
 # torch.cuda.Event recorded on the launch stream around ``reps`` back-to-back repeats of that
 # launch (idempotent: same operands, same outputs) — or None.

@@ -326,7 +326,7 @@ extern "C" int cgan3d_bn_finalize(const float* stats, int64_t nblk, int32_t c, c
                                   float momentum, float eps, float* scale_shift, float* mean_invstd, void* stream) {
   CG_CHECK_ARG(stats && gamma && beta && scale_shift && mean_invstd, "cgan3d_bn_finalize: null pointer");
   CG_CHECK_ARG(nblk > 0 && c > 0 && c <= 1024, "cgan3d_bn_finalize: bad sizes");
-  hipLaunchKernelGGL(bn_finalize_kernel, dim3(c), dim3(256), 0, (hipStream_t)stream, stats, (long long)nblk, c, gamma,
+  ::cg::launch(bn_finalize_kernel, dim3(c), dim3(256), 0, (hipStream_t)stream, stats, (long long)nblk, c, gamma,
                      beta, running_mean, running_var, (long long*)num_batches_tracked, momentum, eps, scale_shift,
                      mean_invstd);
   CG_LAUNCH_CHECK("bn_finalize_kernel");
@@ -340,7 +340,7 @@ extern "C" int cgan3d_bn_apply(const float* z, int64_t nvox, int32_t c, const fl
                "cgan3d_bn_apply: channels must be a multiple of 4 dividing 1024");
   const long long n4 = (long long)nvox * c / 4;
   int blocks = (int)std::min<long long>((n4 + 255) / 256, 4096);
-  hipLaunchKernelGGL(bn_apply_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, z, n4, c, scale_shift, act,
+  ::cg::launch(bn_apply_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, z, n4, c, scale_shift, act,
                      slope, residual, y);
   CG_LAUNCH_CHECK("bn_apply_kernel");
   return CGAN3D_OK;
@@ -352,7 +352,7 @@ extern "C" int cgan3d_bn_finalize_slab(const float* part, int32_t nslots, int32_
                                        float* mean_invstd, void* stream) {
   CG_CHECK_ARG(part && gamma && beta && scale_shift && mean_invstd, "cgan3d_bn_finalize_slab: null pointer");
   CG_CHECK_ARG(nslots > 0 && c > 0 && c <= 1024 && nvox > 0, "cgan3d_bn_finalize_slab: bad sizes");
-  hipLaunchKernelGGL(bn_finalize_slab_kernel, dim3(c), dim3(256), 0, (hipStream_t)stream, part, nslots, c, (double)nvox,
+  ::cg::launch(bn_finalize_slab_kernel, dim3(c), dim3(256), 0, (hipStream_t)stream, part, nslots, c, (double)nvox,
                      gamma, beta, running_mean, running_var, (long long*)num_batches_tracked, momentum, eps,
                      scale_shift, mean_invstd);
   CG_LAUNCH_CHECK("bn_finalize_slab_kernel");
@@ -367,12 +367,12 @@ extern "C" int cgan3d_bn_backward_slab(const float* dy, const float* z, int64_t 
   CG_CHECK_ARG(nvox > 1 && nslots > 0 && c >= 4 && c <= 256 && 256 % c == 0,
                "cgan3d_bn_backward_slab: channels must divide 256 and be >= 4");
   hipStream_t s = (hipStream_t)stream;
-  hipLaunchKernelGGL(bn_bwd_finalize_slab_kernel, dim3(c), dim3(256), 0, s, part, nslots, c, (double)nvox, gamma,
+  ::cg::launch(bn_bwd_finalize_slab_kernel, dim3(c), dim3(256), 0, s, part, nslots, c, (double)nvox, gamma,
                      mean_invstd, dgamma, dbeta, ws, accumulate);
   CG_LAUNCH_CHECK("bn_bwd_finalize_slab_kernel");
   const long long n4 = (long long)nvox * c / 4;
   const int blocks = (int)std::min<long long>((n4 + 255) / 256, 4096);
-  hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(blocks), dim3(256), 0, s, dy, z, n4, c, scale_shift, mean_invstd, act,
+  ::cg::launch(bn_bwd_apply_kernel, dim3(blocks), dim3(256), 0, s, dy, z, n4, c, scale_shift, mean_invstd, act,
                      slope, ws, dz);
   CG_LAUNCH_CHECK("bn_bwd_apply_kernel");
   return CGAN3D_OK;
@@ -393,14 +393,14 @@ extern "C" int cgan3d_bn_backward(const float* dy, const float* z, int64_t nvox,
   const int nblk = reduce_blocks(total);
   float* part = ws;
   float* coef = ws + (long long)nblk * 2 * c;
-  hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(nblk), dim3(256), 0, s, dy, z, n4, c, scale_shift, mean_invstd,
+  ::cg::launch(bn_bwd_reduce_kernel, dim3(nblk), dim3(256), 0, s, dy, z, n4, c, scale_shift, mean_invstd,
                      act, slope, part);
   CG_LAUNCH_CHECK("bn_bwd_reduce_kernel");
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(c), dim3(256), 0, s, part, nblk, c, (long long)nvox, gamma,
+  ::cg::launch(bn_bwd_finalize_kernel, dim3(c), dim3(256), 0, s, part, nblk, c, (long long)nvox, gamma,
                      mean_invstd, dgamma, dbeta, coef, accumulate);
   CG_LAUNCH_CHECK("bn_bwd_finalize_kernel");
   int blocks = (int)std::min<long long>((n4 + 255) / 256, 4096);
-  hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(blocks), dim3(256), 0, s, dy, z, n4, c, scale_shift, mean_invstd,
+  ::cg::launch(bn_bwd_apply_kernel, dim3(blocks), dim3(256), 0, s, dy, z, n4, c, scale_shift, mean_invstd,
                      act, slope, coef, dz);
   CG_LAUNCH_CHECK("bn_bwd_apply_kernel");
   return CGAN3D_OK;
@@ -416,9 +416,9 @@ extern "C" int cgan3d_channel_sum(const float* x, int64_t nvox, int32_t c, float
   hipStream_t s = (hipStream_t)stream;
   const long long total = (long long)nvox * c;
   const int nblk = reduce_blocks(total);
-  hipLaunchKernelGGL(channel_sum_kernel, dim3(nblk), dim3(256), 0, s, x, total, c, ws);
+  ::cg::launch(channel_sum_kernel, dim3(nblk), dim3(256), 0, s, x, total, c, ws);
   CG_LAUNCH_CHECK("channel_sum_kernel");
-  hipLaunchKernelGGL(channel_sum_finalize_kernel, dim3(c), dim3(256), 0, s, ws, nblk, c, out);
+  ::cg::launch(channel_sum_finalize_kernel, dim3(c), dim3(256), 0, s, ws, nblk, c, out);
   CG_LAUNCH_CHECK("channel_sum_finalize_kernel");
   return CGAN3D_OK;
 }

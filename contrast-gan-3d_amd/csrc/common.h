@@ -3,7 +3,10 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <functional>
+#include <tuple>
 #include <type_traits>
+#include <vector>
 #include <cstdarg>
 #include <cstdint>
 #include <cstdio>
@@ -11,6 +14,38 @@
 #include "../../include/cgan3d.h"
 
 namespace cg {
+
+// ---- launch plans (cgan3d_plan_*, plan.hip): while a plan is being recorded on this host thread,
+// every launch / memset / cross-stream wait the entry points issue is appended to it (kernel
+// arguments copied by value) instead of being enqueued; cgan3d_plan_run re-issues the whole
+// sequence from C++ on the recorded streams — the step's ~200 launches without the Python
+// wrappers' per-launch cost, and with the side-stream concurrency a replayed hipGraph loses.
+struct Plan {
+  std::vector<std::function<hipError_t()>> ops;
+  std::vector<hipEvent_t> events;  // owned (cross-stream waits)
+};
+extern thread_local Plan* g_rec;
+
+template <typename... KArgs, typename... Args>
+inline void launch(void (*k)(KArgs...), dim3 grid, dim3 block, size_t lds, hipStream_t st, Args... args) {
+  if (g_rec == nullptr) {
+    hipLaunchKernelGGL(k, grid, block, lds, st, args...);
+    return;
+  }
+  std::tuple<std::decay_t<KArgs>...> t(static_cast<std::decay_t<KArgs>>(args)...);
+  g_rec->ops.emplace_back([k, grid, block, lds, st, t]() mutable {
+    return std::apply([&](auto&... a) {
+      void* argv[] = {static_cast<void*>(&a)...};
+      return hipLaunchKernel(reinterpret_cast<const void*>(k), grid, block, argv, lds, st);
+    }, t);
+  });
+}
+
+inline hipError_t memset_async(void* p, int v, size_t bytes, hipStream_t st) {
+  if (g_rec == nullptr) return hipMemsetAsync(p, v, bytes, st);
+  g_rec->ops.emplace_back([=]() { return hipMemsetAsync(p, v, bytes, st); });
+  return hipSuccess;
+}
 
 // Workgroup barrier for LDS hand-offs that leaves outstanding global loads in flight: hipcc's
 // __syncthreads() waits vmcnt(0) first, which serialises a register-prefetch pipeline on the

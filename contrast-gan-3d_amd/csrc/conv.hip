@@ -455,11 +455,11 @@ extern "C" int cgan3d_conv3d_fwd(const cgan3d_conv_geom* g, const float* x, cons
     size_t lds = (size_t)g->k * g->k * g->k * g->cin * sizeof(float);
     CG_CHECK_ARG(lds <= 64 * 1024, "cgan3d_conv3d_fwd: cout==1 weights exceed LDS");
     if (!g->transposed && g->cin % 4 == 0 && a.class_vox <= 16384) {  // few outputs, long reductions
-      hipLaunchKernelGGL(conv_cout1_wave_kernel, dim3(cg::ceil_div(a.class_vox, 4)), dim3(256), lds, s, a, x, w, y, e);
+      ::cg::launch(conv_cout1_wave_kernel, dim3(cg::ceil_div(a.class_vox, 4)), dim3(256), lds, s, a, x, w, y, e);
       CG_LAUNCH_CHECK("conv_cout1_wave_kernel");
       return CGAN3D_OK;
     }
-    hipLaunchKernelGGL(conv_cout1_kernel, dim3(a.nclass * a.tiles_per_class), dim3(256), lds, s, a, x, w, y, e);
+    ::cg::launch(conv_cout1_kernel, dim3(a.nclass * a.tiles_per_class), dim3(256), lds, s, a, x, w, y, e);
     CG_LAUNCH_CHECK("conv_cout1_kernel");
     return CGAN3D_OK;
   }
@@ -505,7 +505,7 @@ extern "C" int cgan3d_conv3d_wgrad(const cgan3d_conv_geom* g, const float* gathe
   const long long R = (long long)T * g->cin;
   const long long V = (long long)g->n * g->do_ * g->ho * g->wo;
   if (g->k == 7 && g->stride == 1 && (g->cin == 1 || g->cout == 1)) {
-    if (!accumulate && hipMemsetAsync(dw, 0, R * g->cout * sizeof(float), s) != hipSuccess) {
+    if (!accumulate && ::cg::memset_async(dw, 0, R * g->cout * sizeof(float), s) != hipSuccess) {
       set_error("cgan3d_conv3d_wgrad: memset failed");
       return CGAN3D_EHIP;
     }
@@ -516,7 +516,7 @@ extern "C" int cgan3d_conv3d_wgrad(const cgan3d_conv_geom* g, const float* gathe
     CG_CHECK_ARG(!accumulate, "cgan3d_conv3d_wgrad: internal dispatch error");
   }
   if (wgrad_c1_ok(g)) {  // single-channel input: straight into dW, no workspace
-    if (!accumulate && hipMemsetAsync(dw, 0, R * g->cout * sizeof(float), s) != hipSuccess) {
+    if (!accumulate && ::cg::memset_async(dw, 0, R * g->cout * sizeof(float), s) != hipSuccess) {
       set_error("cgan3d_conv3d_wgrad: memset failed");
       return CGAN3D_EHIP;
     }
@@ -524,7 +524,7 @@ extern "C" int cgan3d_conv3d_wgrad(const cgan3d_conv_geom* g, const float* gathe
     CG_LAUNCH_CHECK("conv_wgrad_c1_kernel");
     return CGAN3D_OK;
   }
-  if (hipMemsetAsync(ws, 0, R * g->cout * sizeof(float), s) != hipSuccess) {
+  if (::cg::memset_async(ws, 0, R * g->cout * sizeof(float), s) != hipSuccess) {
     set_error("cgan3d_conv3d_wgrad: memset failed");
     return CGAN3D_EHIP;
   }
@@ -537,7 +537,7 @@ extern "C" int cgan3d_conv3d_wgrad(const cgan3d_conv_geom* g, const float* gathe
     if (vpb < 64) vpb = 64;
     vpb = (vpb + 63) / 64 * 64;
     dim3 grid(cg::ceil_div(V, vpb), gy);
-    hipLaunchKernelGGL((conv_wgrad_cout1_kernel<1>), grid, dim3(256), 0, s, a, gathered, aligned, ws, vpb);
+    ::cg::launch((conv_wgrad_cout1_kernel<1>), grid, dim3(256), 0, s, a, gathered, aligned, ws, vpb);
     CG_LAUNCH_CHECK("conv_wgrad_cout1_kernel");
   } else if (wgrad_bf16_ok(g)) {
     int rc = wgrad_bf16_launch(g, gathered, aligned, ws, s);
@@ -549,7 +549,7 @@ extern "C" int cgan3d_conv3d_wgrad(const cgan3d_conv_geom* g, const float* gathe
     dim3 grid(gxb, cg::ceil_div(V, vpb));
     const int nb = (g->cout + 15) / 16;
     const bool v4 = (g->cin % 4) == 0;
-#define CG_LAUNCH_WG(VV, N) hipLaunchKernelGGL((conv_wgrad_kernel<VV, N>), grid, dim3(256), 0, s, a, gathered, aligned, ws, vpb)
+#define CG_LAUNCH_WG(VV, N) ::cg::launch((conv_wgrad_kernel<VV, N>), grid, dim3(256), 0, s, a, gathered, aligned, ws, vpb)
     if (v4) {
       if (nb == 1) CG_LAUNCH_WG(4, 1); else if (nb == 2) CG_LAUNCH_WG(4, 2); else if (nb == 3) CG_LAUNCH_WG(4, 3); else CG_LAUNCH_WG(4, 4);
     } else {
@@ -559,7 +559,7 @@ extern "C" int cgan3d_conv3d_wgrad(const cgan3d_conv_geom* g, const float* gathe
     CG_LAUNCH_CHECK("conv_wgrad_kernel");
   }
   const long long total = R * g->cout;
-  hipLaunchKernelGGL(wgrad_unpack_kernel, dim3(cg::ceil_div(total, 256)), dim3(256), 0, s, ws, dw, T, g->cin, g->cout,
+  ::cg::launch(wgrad_unpack_kernel, dim3(cg::ceil_div(total, 256)), dim3(256), 0, s, ws, dw, T, g->cin, g->cout,
                      (long long)g->w_sa, (long long)g->w_sb, accumulate);
   CG_LAUNCH_CHECK("wgrad_unpack_kernel");
   return CGAN3D_OK;

@@ -475,7 +475,7 @@ int gemm_launch(const cgan3d_conv_geom* g, const float* x, const float* w, float
   dim3 grid(a.nclass * a.tiles_per_class, c.gy);
   const bool v4 = g->cin % 4 == 0;
   const int prec = g->prec;
-#define CG_GL(P, V, W, N) hipLaunchKernelGGL((conv_gemm_kernel<P, V, W, N>), grid, dim3(256), 0, st, a, x, w, y, e)
+#define CG_GL(P, V, W, N) ::cg::launch((conv_gemm_kernel<P, V, W, N>), grid, dim3(256), 0, st, a, x, w, y, e)
 #define CG_GL_NB(P, V)                                    \
   do {                                                    \
     if (c.wm == 2) CG_GL(P, V, 2, 1);                     \
@@ -514,7 +514,7 @@ extern "C" int cgan3d_pack_weights(const cgan3d_conv_geom* g, const float* w, fl
   const int T = g->k * g->k * g->k, ldb = (g->cout + 3) / 4 * 4;
   const long long total = (long long)T * g->cin * ldb;
   int blocks = (int)std::min<long long>((total + 255) / 256, 2048);
-  hipLaunchKernelGGL(pack_weights_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, w, wp, T, g->cin, g->cout,
+  ::cg::launch(pack_weights_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, w, wp, T, g->cin, g->cout,
                      ldb, (long long)g->w_sa, (long long)g->w_sb, total);
   CG_LAUNCH_CHECK("pack_weights_kernel");
   return CGAN3D_OK;
@@ -523,7 +523,7 @@ extern "C" int cgan3d_pack_weights(const cgan3d_conv_geom* g, const float* w, fl
 extern "C" int cgan3d_pack_weights_multi(const cgan3d_pack_desc* descs, int32_t n, int64_t max_total, void* stream) {
   CG_CHECK_ARG(descs && n > 0 && n <= 65535 && max_total > 0, "cgan3d_pack_weights_multi: bad args");
   int bx = (int)std::min<long long>((max_total + 255) / 256, 256);
-  hipLaunchKernelGGL(pack_multi_kernel, dim3(bx, n), dim3(256), 0, (hipStream_t)stream, descs);
+  ::cg::launch(pack_multi_kernel, dim3(bx, n), dim3(256), 0, (hipStream_t)stream, descs);
   CG_LAUNCH_CHECK("pack_multi_kernel");
   return CGAN3D_OK;
 }

@@ -568,18 +568,18 @@ int halo_launch(const cgan3d_conv_geom* g, const float* x, const float* w, float
     const dim3 grid1((unsigned)tiles, split ? 2 : 1);
     const __bf16* wp = reinterpret_cast<const __bf16*>(w);
     if (split) {
-      if (g->transposed) hipLaunchKernelGGL((conv_k3_kernel<true, 2>), grid1, dim3(256), 0, st, a, x, wp, y, e);
-      else hipLaunchKernelGGL((conv_k3_kernel<false, 2>), grid1, dim3(256), 0, st, a, x, wp, y, e);
+      if (g->transposed) ::cg::launch((conv_k3_kernel<true, 2>), grid1, dim3(256), 0, st, a, x, wp, y, e);
+      else ::cg::launch((conv_k3_kernel<false, 2>), grid1, dim3(256), 0, st, a, x, wp, y, e);
     } else {
-      if (g->transposed) hipLaunchKernelGGL((conv_k3_kernel<true, 4>), grid1, dim3(256), 0, st, a, x, wp, y, e);
-      else hipLaunchKernelGGL((conv_k3_kernel<false, 4>), grid1, dim3(256), 0, st, a, x, wp, y, e);
+      if (g->transposed) ::cg::launch((conv_k3_kernel<true, 4>), grid1, dim3(256), 0, st, a, x, wp, y, e);
+      else ::cg::launch((conv_k3_kernel<false, 4>), grid1, dim3(256), 0, st, a, x, wp, y, e);
     }
     return CGAN3D_OK;
   }
   dim3 grid((unsigned)(a.nclass * a.n * a.td * a.th * a.tw), g->cout / a.bn);
   const size_t lds = 3 * (size_t)a.bn * g->cin * 2 + a.halo_bytes;
   const __bf16* wp = reinterpret_cast<const __bf16*>(w);
-#define CG_HL(CI, NT) hipLaunchKernelGGL((conv_halo_kernel<CI, NT>), grid, dim3(256), lds, st, a, x, wp, y, e)
+#define CG_HL(CI, NT) ::cg::launch((conv_halo_kernel<CI, NT>), grid, dim3(256), lds, st, a, x, wp, y, e)
   if (g->cin == 64) {
     if (a.bn == 64) CG_HL(64, 4); else if (a.bn == 32) CG_HL(64, 2); else return CGAN3D_EINVAL;
   } else {
@@ -593,7 +593,7 @@ int halo_pack(const cgan3d_conv_geom* g, const float* w, void* wp, hipStream_t s
   const int T = g->k * g->k * g->k;
   const long long total = (long long)T * g->cout * g->cin;
   int blocks = (int)std::min<long long>((total + 255) / 256, 2048);
-  hipLaunchKernelGGL(pack_halo_kernel, dim3(blocks), dim3(256), 0, st, w, reinterpret_cast<__bf16*>(wp), T, g->cin,
+  ::cg::launch(pack_halo_kernel, dim3(blocks), dim3(256), 0, st, w, reinterpret_cast<__bf16*>(wp), T, g->cin,
                      g->cout, (long long)g->w_sa, (long long)g->w_sb);
   return CGAN3D_OK;
 }

@@ -357,8 +357,8 @@ int k7_try_fwd(const cgan3d_conv_geom* g, const float* x, const float* w, float*
     else a = k7_args(g, g->k - 1 - g->pad, 0, 1, g->w_sb);  // input-grad: flipped taps, zero pad
     float* bp = e.bn_mode == 1 ? e.bn_part : nullptr;
     if (g->cout == 16)
-      hipLaunchKernelGGL((k7_n2w_kernel<16>), dim3(k7_blocks(a)), dim3(256), 0, s, a, x, w, y, e.stats, bp);
-    else hipLaunchKernelGGL((k7_n2w_kernel<8>), dim3(k7_blocks(a)), dim3(256), 0, s, a, x, w, y, e.stats, bp);
+      ::cg::launch((k7_n2w_kernel<16>), dim3(k7_blocks(a)), dim3(256), 0, s, a, x, w, y, e.stats, bp);
+    else ::cg::launch((k7_n2w_kernel<8>), dim3(k7_blocks(a)), dim3(256), 0, s, a, x, w, y, e.stats, bp);
     return 1;
   }
   if (g->cout == 1 && k7_wide_ok(g->cin) && !g->transposed && !e.residual && !e.mask_src && !e.stats &&
@@ -369,10 +369,10 @@ int k7_try_fwd(const cgan3d_conv_geom* g, const float* x, const float* w, float*
     }
     K7Args a = k7_args(g, g->pad, g->reflect, 0, g->w_sa);
     if (g->cin == 16)
-      hipLaunchKernelGGL((k7_w2n_kernel<16, 2>), dim3(k7_blocks(a)), dim3(256), 0, s, a, x, w, y, e.bias, e.act,
+      ::cg::launch((k7_w2n_kernel<16, 2>), dim3(k7_blocks(a)), dim3(256), 0, s, a, x, w, y, e.bias, e.act,
                          e.minuend, e.out2);
     else
-      hipLaunchKernelGGL((k7_w2n_kernel<8, 2>), dim3(k7_blocks(a)), dim3(256), 0, s, a, x, w, y, e.bias, e.act,
+      ::cg::launch((k7_w2n_kernel<8, 2>), dim3(k7_blocks(a)), dim3(256), 0, s, a, x, w, y, e.bias, e.act,
                          e.minuend, e.out2);
     return 1;
   }
@@ -393,15 +393,15 @@ int k7_try_wgrad(const cgan3d_conv_geom* g, const float* x, const float* go, flo
   if (g->cout == 1 && k7_wide_ok(g->cin)) {
     K7Args a = k7_args(g, g->pad, g->reflect, 0, g->w_sa);
     const int C = g->cin;
-    if (C == 16) hipLaunchKernelGGL((k7_wg_w2n_kernel<16, 2>), dim3(k7_blocks(a) * 8), dim3(256), 0, s, a, x, go, dw);
-    else hipLaunchKernelGGL((k7_wg_w2n_kernel<8, 2>), dim3(k7_blocks(a) * 4), dim3(256), 0, s, a, x, go, dw);
+    if (C == 16) ::cg::launch((k7_wg_w2n_kernel<16, 2>), dim3(k7_blocks(a) * 8), dim3(256), 0, s, a, x, go, dw);
+    else ::cg::launch((k7_wg_w2n_kernel<8, 2>), dim3(k7_blocks(a) * 4), dim3(256), 0, s, a, x, go, dw);
     return 1;
   }
   if (g->cin == 1 && k7_wide_ok(g->cout)) {
     K7Args a = k7_args(g, g->pad, g->reflect, 0, g->w_sb);
     const int C = g->cout;
-    if (C == 16) hipLaunchKernelGGL((k7_wg_n2w_kernel<16, 2>), dim3(k7_blocks(a) * 8), dim3(256), 0, s, a, x, go, dw);
-    else hipLaunchKernelGGL((k7_wg_n2w_kernel<8, 2>), dim3(k7_blocks(a) * 4), dim3(256), 0, s, a, x, go, dw);
+    if (C == 16) ::cg::launch((k7_wg_n2w_kernel<16, 2>), dim3(k7_blocks(a) * 8), dim3(256), 0, s, a, x, go, dw);
+    else ::cg::launch((k7_wg_n2w_kernel<8, 2>), dim3(k7_blocks(a) * 4), dim3(256), 0, s, a, x, go, dw);
     return 1;
   }
   return 0;

@@ -594,7 +594,7 @@ void k7m_n2w_launch(const cgan3d_conv_geom* g, int P, int reflect, int flip, lon
   const K7Args a = k7m_args(g, P, reflect, flip, wc, N_TD, N_TH, N_TW);
   int grid, per, nt;
   k7m_n2w_split(a, &grid, &per, &nt);
-  hipLaunchKernelGGL(k7m_n2w_kernel, dim3(grid), dim3(256), 0, s, a, x, w, y, stats, bn_part, per, nt);
+  ::cg::launch(k7m_n2w_kernel, dim3(grid), dim3(256), 0, s, a, x, w, y, stats, bn_part, per, nt);
 }
 
 void k7m_w2n_launch(const cgan3d_conv_geom* g, int P, int reflect, long long wc, const float* x, const float* w,
@@ -602,7 +602,7 @@ void k7m_w2n_launch(const cgan3d_conv_geom* g, int P, int reflect, long long wc,
   const K7Args a = k7m_args(g, P, reflect, 0, wc, W_TD, W_TH, W_TW);
   int grid, per, nt;
   k7m_n2w_split(a, &grid, &per, &nt);
-  hipLaunchKernelGGL(k7m_w2n_kernel, dim3(grid), dim3(256), 0, s, a, x, w, y, e.bias, e.act, e.minuend, e.out2, per,
+  ::cg::launch(k7m_w2n_kernel, dim3(grid), dim3(256), 0, s, a, x, w, y, e.bias, e.act, e.minuend, e.out2, per,
                      nt);
 }
 
@@ -619,10 +619,10 @@ void k7m_wgrad_launch(const cgan3d_conv_geom* g, bool wide_in, long long wc, con
   const K7Args a = k7m_args(g, g->pad, g->reflect, 0, wc, G_TD, G_TH, G_TW);
   int grid, per, ntiles;
   k7m_wg_split(g, wide_in, &grid, &per, &ntiles);
-  if (wide_in) hipLaunchKernelGGL(k7m_wg_kernel<1>, dim3(grid), dim3(256), 0, s, a, x, go, ws, per, ntiles);
-  else hipLaunchKernelGGL(k7m_wg_kernel<0>, dim3(grid), dim3(256), 0, s, a, x, go, ws, per, ntiles);
+  if (wide_in) ::cg::launch(k7m_wg_kernel<1>, dim3(grid), dim3(256), 0, s, a, x, go, ws, per, ntiles);
+  else ::cg::launch(k7m_wg_kernel<0>, dim3(grid), dim3(256), 0, s, a, x, go, ws, per, ntiles);
   const int rows_per = 32;
-  hipLaunchKernelGGL(k7m_colsum_kernel, dim3((G_COLS + 255) / 256, (grid + rows_per - 1) / rows_per), dim3(256), 0, s,
+  ::cg::launch(k7m_colsum_kernel, dim3((G_COLS + 255) / 256, (grid + rows_per - 1) / rows_per), dim3(256), 0, s,
                      ws, grid, rows_per, dw, wc);
 }
 

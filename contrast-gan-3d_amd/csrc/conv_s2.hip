@@ -428,8 +428,8 @@ int s2_launch(const cgan3d_conv_geom* g, const float* x, const __bf16* wp, float
   }
   S2Args a = s2_args(g, kind);
   const dim3 grid((unsigned)((long long)a.n * a.td * a.th * a.tw));
-  if (kind == 1) hipLaunchKernelGGL(conv_s2f_kernel, grid, dim3(256), 0, st, a, x, wp, y, e);
-  else hipLaunchKernelGGL(conv_s2t_kernel, grid, dim3(256), 0, st, a, x, wp, y, e);
+  if (kind == 1) ::cg::launch(conv_s2f_kernel, grid, dim3(256), 0, st, a, x, wp, y, e);
+  else ::cg::launch(conv_s2t_kernel, grid, dim3(256), 0, st, a, x, wp, y, e);
   return CGAN3D_OK;
 }
 

@@ -226,7 +226,7 @@ int wgrad_c1_launch(const cgan3d_conv_geom* g, const float* gathered, const floa
   a.vpb = (a.V + blocks - 1) / blocks;
   a.vpb = (a.vpb + 3) / 4 * 4;
   dim3 grid((unsigned)((a.V + a.vpb - 1) / a.vpb));
-#define CG_WC1(C) hipLaunchKernelGGL((conv_wgrad_c1_kernel<C>), grid, dim3(256), 0, st, a, gathered, aligned, dw, (long long)g->w_sb)
+#define CG_WC1(C) ::cg::launch((conv_wgrad_c1_kernel<C>), grid, dim3(256), 0, st, a, gathered, aligned, dw, (long long)g->w_sb)
   if (g->cout == 4) CG_WC1(4); else if (g->cout == 8) CG_WC1(8); else CG_WC1(16);
 #undef CG_WC1
   return CGAN3D_OK;
@@ -258,7 +258,7 @@ int wgrad_bf16_launch(const cgan3d_conv_geom* g, const float* gathered, const fl
   a.vpb = (vpb + WG_KV - 1) / WG_KV * WG_KV;
   dim3 grid(gx, (unsigned)((a.V + a.vpb - 1) / a.vpb));
   const int nb = (g->cout + 15) / 16;
-#define CG_WGB(N, R8) hipLaunchKernelGGL((conv_wgrad_bf16_kernel<N, R8>), grid, dim3(256), 0, st, a, gathered, aligned, dwp)
+#define CG_WGB(N, R8) ::cg::launch((conv_wgrad_bf16_kernel<N, R8>), grid, dim3(256), 0, st, a, gathered, aligned, dwp)
   if (g->wo % 8 == 0) {  // chunks are 64-voxel aligned: 8 | W keeps each thread's 8 voxels in one row
     if (nb == 1) CG_WGB(1, true); else if (nb == 2) CG_WGB(2, true); else if (nb == 3) CG_WGB(3, true); else CG_WGB(4, true);
   } else {

@@ -28,10 +28,10 @@ extern "C" int cgan3d_unpack_patches(const void* src, int32_t src_dtype, int64_t
   CG_CHECK_ARG(src_dtype == 0 || src_dtype == 1, "cgan3d_unpack_patches: src_dtype must be 0 (int16) or 1 (float32)");
   int blocks = (int)std::min<long long>((nvox + 255) / 256, 8192);
   if (src_dtype == 0)
-    hipLaunchKernelGGL(unpack_patches_kernel<int16_t>, dim3(blocks), dim3(256), 0, (hipStream_t)stream,
+    ::cg::launch(unpack_patches_kernel<int16_t>, dim3(blocks), dim3(256), 0, (hipStream_t)stream,
                        static_cast<const int16_t*>(src), (long long)nvox, shift, factor, data, seg);
   else
-    hipLaunchKernelGGL(unpack_patches_kernel<float>, dim3(blocks), dim3(256), 0, (hipStream_t)stream,
+    ::cg::launch(unpack_patches_kernel<float>, dim3(blocks), dim3(256), 0, (hipStream_t)stream,
                        static_cast<const float*>(src), (long long)nvox, shift, factor, data, seg);
   CG_LAUNCH_CHECK("unpack_patches_kernel");
   return CGAN3D_OK;

@@ -221,7 +221,7 @@ extern "C" int cgan3d_critic_logits_grad(const float* logits, int32_t n_real, in
                                          void* stream) {
   CG_CHECK_ARG(logits && dlogits && losses, "cgan3d_critic_logits_grad: null pointer");
   CG_CHECK_ARG(n_real > 0 && n_fake > 0 && n_gp >= 0 && per_sample > 0, "cgan3d_critic_logits_grad: bad sizes");
-  hipLaunchKernelGGL(critic_logits_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, logits, n_real, n_fake, n_gp,
+  ::cg::launch(critic_logits_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, logits, n_real, n_fake, n_gp,
                      per_sample, gan_w, dlogits, losses);
   CG_LAUNCH_CHECK("critic_logits_kernel");
   return CGAN3D_OK;
@@ -230,7 +230,7 @@ extern "C" int cgan3d_critic_logits_grad(const float* logits, int32_t n_real, in
 extern "C" int cgan3d_generator_logits_grad(const float* logits, int32_t n, float gan_w, float* dlogits, float* losses,
                                             void* stream) {
   CG_CHECK_ARG(logits && dlogits && losses && n > 0, "cgan3d_generator_logits_grad: bad args");
-  hipLaunchKernelGGL(gen_logits_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, logits, n, gan_w, dlogits, losses);
+  ::cg::launch(gen_logits_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, logits, n, gan_w, dlogits, losses);
   CG_LAUNCH_CHECK("gen_logits_kernel");
   return CGAN3D_OK;
 }
@@ -244,13 +244,13 @@ extern "C" int cgan3d_gradient_penalty(const float* grad, int32_t b, int64_t per
   if (chunks > 64) chunks = 64;
   float* part = ws;
   float* coef = ws + (long long)b * chunks;
-  hipLaunchKernelGGL(sumsq_kernel, dim3(chunks, b), dim3(256), 0, s, grad, (long long)per_sample, chunks, part);
+  ::cg::launch(sumsq_kernel, dim3(chunks, b), dim3(256), 0, s, grad, (long long)per_sample, chunks, part);
   CG_LAUNCH_CHECK("sumsq_kernel");
-  hipLaunchKernelGGL(gp_finalize_kernel, dim3(1), dim3(256), 0, s, part, b, chunks, lambda_, coef, losses);
+  ::cg::launch(gp_finalize_kernel, dim3(1), dim3(256), 0, s, part, b, chunks, lambda_, coef, losses);
   CG_LAUNCH_CHECK("gp_finalize_kernel");
   const long long total = (long long)b * per_sample;
   int blocks = (int)std::min<long long>((total + 255) / 256, 4096);
-  hipLaunchKernelGGL(scale_rows_kernel, dim3(blocks), dim3(256), 0, s, grad, (long long)per_sample, total, coef,
+  ::cg::launch(scale_rows_kernel, dim3(blocks), dim3(256), 0, s, grad, (long long)per_sample, total, coef,
                      gamma_out);
   CG_LAUNCH_CHECK("scale_rows_kernel");
   return CGAN3D_OK;
@@ -267,16 +267,16 @@ extern "C" int cgan3d_generator_output_grad(const float* opt_hat, const float* s
   double* part = reinterpret_cast<double*>(ws);
   double* stat = part + 512 * 4;
   const int nblk = red_blocks(n);
-  hipLaunchKernelGGL(gen_pass1_kernel, dim3(nblk), dim3(256), 0, s, opt_hat, subopt, mask, (long long)n, lo, hi, part);
+  ::cg::launch(gen_pass1_kernel, dim3(nblk), dim3(256), 0, s, opt_hat, subopt, mask, (long long)n, lo, hi, part);
   CG_LAUNCH_CHECK("gen_pass1_kernel");
-  hipLaunchKernelGGL(gen_fin1_kernel, dim3(1), dim3(256), 0, s, part, nblk, (long long)n, stat);
+  ::cg::launch(gen_fin1_kernel, dim3(1), dim3(256), 0, s, part, nblk, (long long)n, stat);
   CG_LAUNCH_CHECK("gen_fin1_kernel");
-  hipLaunchKernelGGL(gen_pass2_kernel, dim3(nblk), dim3(256), 0, s, opt_hat, subopt, (long long)n, stat, part);
+  ::cg::launch(gen_pass2_kernel, dim3(nblk), dim3(256), 0, s, opt_hat, subopt, (long long)n, stat, part);
   CG_LAUNCH_CHECK("gen_pass2_kernel");
-  hipLaunchKernelGGL(gen_fin2_kernel, dim3(1), dim3(256), 0, s, part, nblk, (long long)n, sim_w, hu_w, stat, losses);
+  ::cg::launch(gen_fin2_kernel, dim3(1), dim3(256), 0, s, part, nblk, (long long)n, sim_w, hu_w, stat, losses);
   CG_LAUNCH_CHECK("gen_fin2_kernel");
   int blocks = (int)std::min<long long>((n + 255) / 256, 4096);
-  hipLaunchKernelGGL(gen_grad_kernel, dim3(blocks), dim3(256), 0, s, opt_hat, subopt, att, mask, d_critic,
+  ::cg::launch(gen_grad_kernel, dim3(blocks), dim3(256), 0, s, opt_hat, subopt, att, mask, d_critic,
                      (long long)n, lo, hi, stat, dz_last);
   CG_LAUNCH_CHECK("gen_grad_kernel");
   return CGAN3D_OK;

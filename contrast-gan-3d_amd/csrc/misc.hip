@@ -148,7 +148,7 @@ using namespace cg;
 extern "C" int cgan3d_tanh_backward(const float* y, const float* dy, float* dz, int64_t n, void* stream) {
   CG_CHECK_ARG(y && dy && dz && n > 0, "cgan3d_tanh_backward: bad args");
   int blocks = (int)std::min<long long>((n + 255) / 256, 4096);
-  hipLaunchKernelGGL(tanh_bwd_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, y, dy, dz, (long long)n);
+  ::cg::launch(tanh_bwd_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, y, dy, dz, (long long)n);
   CG_LAUNCH_CHECK("tanh_bwd_kernel");
   return CGAN3D_OK;
 }
@@ -158,7 +158,7 @@ extern "C" const char* cgan3d_get_last_error(void) { return g_err; }
 
 extern "C" int cgan3d_adam_tick(float* hyper, void* stream) {
   CG_CHECK_ARG(hyper, "cgan3d_adam_tick: null pointer");
-  hipLaunchKernelGGL(adam_tick_kernel, dim3(1), dim3(1), 0, (hipStream_t)stream, hyper);
+  ::cg::launch(adam_tick_kernel, dim3(1), dim3(1), 0, (hipStream_t)stream, hyper);
   CG_LAUNCH_CHECK("adam_tick_kernel");
   return CGAN3D_OK;
 }
@@ -168,7 +168,7 @@ extern "C" int cgan3d_adam(float* param, const float* grad, float* exp_avg, floa
   CG_CHECK_ARG(param && grad && exp_avg && exp_avg_sq && hyper, "cgan3d_adam: null pointer");
   CG_CHECK_ARG(n > 0, "cgan3d_adam: n must be positive");
   int blocks = (int)std::min<long long>((n + 255) / 256, 2048);
-  hipLaunchKernelGGL(adam_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, param, grad, exp_avg, exp_avg_sq,
+  ::cg::launch(adam_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, param, grad, exp_avg, exp_avg_sq,
                      (long long)n, hyper);
   CG_LAUNCH_CHECK("adam_kernel");
   return CGAN3D_OK;
@@ -184,10 +184,10 @@ extern "C" int cgan3d_reflect_fold(const float* padded, float* out, int32_t n, i
   const bool v4 = c % 4 == 0;
   int blocks = (int)std::min<long long>((total / (v4 ? 4 : 1) + 255) / 256, 8192);
   if (v4)
-    hipLaunchKernelGGL(reflect_fold_kernel<4>, dim3(blocks), dim3(256), 0, (hipStream_t)stream, padded, out, n, d, h, w,
+    ::cg::launch(reflect_fold_kernel<4>, dim3(blocks), dim3(256), 0, (hipStream_t)stream, padded, out, n, d, h, w,
                        c, pad);
   else
-    hipLaunchKernelGGL(reflect_fold_kernel<1>, dim3(blocks), dim3(256), 0, (hipStream_t)stream, padded, out, n, d, h, w,
+    ::cg::launch(reflect_fold_kernel<1>, dim3(blocks), dim3(256), 0, (hipStream_t)stream, padded, out, n, d, h, w,
                        c, pad);
   CG_LAUNCH_CHECK("reflect_fold_kernel");
   return CGAN3D_OK;
@@ -213,7 +213,7 @@ extern "C" int cgan3d_reflect_fold_ex(const float* padded, float* out, int32_t n
   Epi e{};
   e.bn_part = ep->bn_part; e.bn_mode = 2; e.bn_slots = blocks; e.bn_z = ep->bn_z; e.bn_ss = ep->bn_ss;
   e.bn_mi = ep->bn_mi; e.bn_act = ep->bn_act; e.bn_slope = ep->bn_slope;
-  hipLaunchKernelGGL(reflect_fold_bn_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, padded, out, n, d, h, w, c,
+  ::cg::launch(reflect_fold_bn_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, padded, out, n, d, h, w, c,
                      pad, e);
   CG_LAUNCH_CHECK("reflect_fold_bn_kernel");
   return CGAN3D_OK;
@@ -224,7 +224,7 @@ extern "C" int cgan3d_gp_interpolate(const float* real, const float* fake, const
   CG_CHECK_ARG(real && fake && eps && out && b > 0 && per_sample > 0, "cgan3d_gp_interpolate: bad args");
   const long long total = (long long)b * per_sample;
   int blocks = (int)std::min<long long>((total + 255) / 256, 4096);
-  hipLaunchKernelGGL(interp_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, real, fake, eps, out,
+  ::cg::launch(interp_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, real, fake, eps, out,
                      (long long)per_sample, total);
   CG_LAUNCH_CHECK("interp_kernel");
   return CGAN3D_OK;

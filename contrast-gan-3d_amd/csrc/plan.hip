@@ -1,0 +1,99 @@
+// Launch plans: record a sequence of the library's launches once, re-issue it from C++.
+//
+// The step engine (cgan3d_amd/engine.py) issues ~200 launches per G+D step through the ctypes
+// wrappers; their host cost (~10 us each: operand checks, argument marshalling) exceeded the GPU
+// time of the step.  A plan records what the entry points would enqueue — kernel launches with
+// their by-value arguments, workspace memsets, cross-stream waits — and cgan3d_plan_run re-issues
+// them in order on the recorded streams, so the whole step costs one ctypes call plus one
+// hipLaunchKernel per kernel.  Unlike a replayed hipGraph the two-stream structure (weight
+// gradients beside the input-gradient chain) is kept exactly as in eager mode.
+//
+// Contract (as for hipGraph capture): every buffer and device scalar a recorded launch touches
+// must stay allocated and keep its address; values may change between runs.
+#include "common.h"
+
+namespace cg {
+
+thread_local Plan* g_rec = nullptr;
+
+static hipEvent_t g_eager_events[64];
+static int g_eager_next = -1;
+
+}  // namespace cg
+
+using namespace cg;
+
+extern "C" int cgan3d_plan_begin(void) {
+  CG_CHECK_ARG(g_rec == nullptr, "cgan3d_plan_begin: a plan is already being recorded on this thread");
+  g_rec = new Plan();
+  return CGAN3D_OK;
+}
+
+extern "C" int cgan3d_plan_end(void** plan) {
+  CG_CHECK_ARG(g_rec != nullptr, "cgan3d_plan_end: no plan is being recorded");
+  CG_CHECK_ARG(plan != nullptr, "cgan3d_plan_end: null output");
+  *plan = g_rec;
+  g_rec = nullptr;
+  return CGAN3D_OK;
+}
+
+extern "C" int64_t cgan3d_plan_size(void* plan) {
+  return plan ? (int64_t)static_cast<Plan*>(plan)->ops.size() : 0;
+}
+
+extern "C" int cgan3d_plan_run(void* plan) {
+  CG_CHECK_ARG(plan != nullptr, "cgan3d_plan_run: null plan");
+  CG_CHECK_ARG(g_rec == nullptr, "cgan3d_plan_run: cannot run a plan while recording");
+  Plan* p = static_cast<Plan*>(plan);
+  for (size_t i = 0; i < p->ops.size(); ++i) {
+    const hipError_t e = p->ops[i]();
+    if (e != hipSuccess) {
+      set_error("cgan3d_plan_run: op %zu of %zu failed: %s", i, p->ops.size(), hipGetErrorString(e));
+      return CGAN3D_EHIP;
+    }
+  }
+  return CGAN3D_OK;
+}
+
+extern "C" int cgan3d_plan_destroy(void* plan) {
+  if (plan == nullptr) return CGAN3D_OK;
+  Plan* p = static_cast<Plan*>(plan);
+  for (hipEvent_t e : p->events) (void)hipEventDestroy(e);
+  delete p;
+  return CGAN3D_OK;
+}
+
+// `waiter` waits for everything enqueued so far on `signaler` (torch's Stream.wait_stream).
+extern "C" int cgan3d_stream_wait(void* waiter, void* signaler) {
+  hipStream_t w = static_cast<hipStream_t>(waiter), s = static_cast<hipStream_t>(signaler);
+  if (w == s) return CGAN3D_OK;
+  hipEvent_t ev;
+  if (g_rec != nullptr) {
+    if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) {
+      set_error("cgan3d_stream_wait: hipEventCreate failed");
+      return CGAN3D_EHIP;
+    }
+    g_rec->events.push_back(ev);
+    g_rec->ops.emplace_back([ev, w, s]() {
+      hipError_t e = hipEventRecord(ev, s);
+      return e != hipSuccess ? e : hipStreamWaitEvent(w, ev, 0);
+    });
+    return CGAN3D_OK;
+  }
+  // eager: a small ring (an event may be re-recorded once the wait on it has been enqueued)
+  if (g_eager_next < 0) {
+    for (auto& e : g_eager_events)
+      if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) {
+        set_error("cgan3d_stream_wait: hipEventCreate failed");
+        return CGAN3D_EHIP;
+      }
+    g_eager_next = 0;
+  }
+  ev = g_eager_events[g_eager_next];
+  g_eager_next = (g_eager_next + 1) % 64;
+  if (hipEventRecord(ev, s) != hipSuccess || hipStreamWaitEvent(w, ev, 0) != hipSuccess) {
+    set_error("cgan3d_stream_wait: event record/wait failed");
+    return CGAN3D_EHIP;
+  }
+  return CGAN3D_OK;
+}

@@ -210,6 +210,21 @@ int cgan3d_adam_tick(float* hyper, void* stream);
 int cgan3d_adam(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, int64_t n,
                 const float* hyper, void* stream);
 
+/* --- launch plans (the step engine's replacement for a replayed hipGraph; Trainer.py:163-203 is
+ * the sequence recorded) ---
+ * Between cgan3d_plan_begin and cgan3d_plan_end every entry point called on this host thread
+ * RECORDS what it would enqueue (kernel launches with by-value arguments, workspace memsets,
+ * cgan3d_stream_wait) instead of enqueuing it; operand checks still run at record time.
+ * cgan3d_plan_run re-issues the recorded sequence on the recorded streams (one host call for a
+ * whole step).  Every buffer a recorded launch touches must keep its address while the plan lives. */
+int cgan3d_plan_begin(void);
+int cgan3d_plan_end(void** plan);
+int64_t cgan3d_plan_size(void* plan);
+int cgan3d_plan_run(void* plan);
+int cgan3d_plan_destroy(void* plan);
+/* `waiter` waits for all work enqueued so far on `signaler` (recorded when inside a plan). */
+int cgan3d_stream_wait(void* waiter, void* signaler);
+
 #ifdef __cplusplus
 }
 #endif

@@ -201,3 +201,37 @@ def test_step_matches_oracle_64(S, b):
             for k, p in zip(opt_.arena.names, opt_.arena.params):
                 st.exp_avg[k] = opt_.state[p]["exp_avg"].detach().cpu().double()
                 st.exp_avg_sq[k] = opt_.state[p]["exp_avg_sq"].detach().cpu().double()
+
+
+@pytest.mark.parametrize("prec", ["f32", "bf16"])
+def test_plan_replay_matches_eager(prec):
+    """A recorded launch plan (engine.record / run_plan, cgan3d_plan_*) replays the same step as
+    the eager launches: three steps each way from identical weights, new inputs before each."""
+    from cgan3d_amd.data.synthetic import synth_patches
+    from cgan3d_amd.engine import StepEngine
+    g_args = dict(n_resnet_blocks=2, n_updownsample_blocks=2, init_channels_out=16)
+    S, b = 32, 2
+    engs = []
+    for _ in range(2):
+        g, d = _models(g_args)
+        engs.append((StepEngine(g, d, g.config, d.config, b, b, (S, S, S), precision=prec), g, d))
+    batches = []
+    for j in range(3):
+        opt, _ = synth_patches(b, S, 100 + j)
+        sub, seg = synth_patches(b, S, 200 + j)
+        batches.append((torch.from_numpy(opt).cuda(), torch.from_numpy(sub).cuda(), torch.from_numpy(seg).cuda(),
+                        torch.full((b,), 0.3 + 0.1 * j, device="cuda")))
+    eager, planned = engs[0][0], engs[1][0]
+    plan = planned.record()
+    assert plan.launches > 100
+    for bt in batches:
+        eager.load_inputs(*bt)
+        eager.step()
+        planned.load_inputs(*bt)
+        planned.run_plan()
+        # (bf16: atomics order moves the small W-distance losses by ~1e-6 absolute)
+        np.testing.assert_allclose(planned.losses.cpu().numpy(), eager.losses.cpu().numpy(), rtol=1e-4, atol=2e-5)
+    # weight-gradient atomics may add in another order: gradients to 1e-3 of their largest entry
+    for a1, a2 in ((eager.g_arena, planned.g_arena), (eager.d_arena, planned.d_arena)):
+        g1, g2 = a1.grad.cpu().numpy(), a2.grad.cpu().numpy()
+        assert np.abs(g1 - g2).max() <= 1e-3 * np.abs(g1).max()
