@@ -158,6 +158,11 @@ void k7m_w2n_launch(const cgan3d_conv_geom* g, int P, int reflect, long long wc,
 int gemm_blocks(const cgan3d_conv_geom* g, long long* mblocks);
 bool wgrad_bf16_ok(const cgan3d_conv_geom* g);
 bool wgrad_c1_ok(const cgan3d_conv_geom* g);
+bool wgrad_k3_ok(const cgan3d_conv_geom* g);
+long long wgrad_k3_ws_floats(const cgan3d_conv_geom* g);
+void wgrad_k3_set_chunks(int v);
+int wgrad_k3_launch(const cgan3d_conv_geom* g, const float* gathered, const float* aligned, float* dw, int accumulate,
+                    float* ws, hipStream_t st);
 int wgrad_c1_launch(const cgan3d_conv_geom* g, const float* gathered, const float* aligned, float* dw, hipStream_t st);
 void wgrad_bf16_set_blocks(int v);
 void halo_set_min_blocks(int v);

@@ -488,7 +488,8 @@ static long long wgrad_vpb(long long V, int gx_blocks) {
 
 extern "C" int64_t cgan3d_conv3d_wgrad_ws_floats(const cgan3d_conv_geom* g) {
   if (!g) return -1;
-  return std::max<int64_t>((int64_t)g->k * g->k * g->k * g->cin * g->cout, k7_wgrad_ws_floats(g));
+  return std::max<int64_t>(std::max<int64_t>((int64_t)g->k * g->k * g->k * g->cin * g->cout, k7_wgrad_ws_floats(g)),
+                           wgrad_k3_ws_floats(g));
 }
 
 extern "C" int cgan3d_conv3d_wgrad(const cgan3d_conv_geom* g, const float* gathered, const float* aligned, float* dw,
@@ -522,6 +523,12 @@ extern "C" int cgan3d_conv3d_wgrad(const cgan3d_conv_geom* g, const float* gathe
     }
     wgrad_c1_launch(g, gathered, aligned, dw, s);
     CG_LAUNCH_CHECK("conv_wgrad_c1_kernel");
+    return CGAN3D_OK;
+  }
+  if (wgrad_k3_ok(g)) {  // ResNet-block shape: per-block partials + reduce, no memset
+    int rc = wgrad_k3_launch(g, gathered, aligned, dw, accumulate, ws, s);
+    if (rc) return rc;
+    CG_LAUNCH_CHECK("wgrad_k3_kernel");
     return CGAN3D_OK;
   }
   if (::cg::memset_async(ws, 0, R * g->cout * sizeof(float), s) != hipSuccess) {

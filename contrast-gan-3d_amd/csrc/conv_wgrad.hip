@@ -18,6 +18,7 @@
 namespace cg {
 
 typedef __bf16 bf16x8_w __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4_w __attribute__((ext_vector_type(4)));
 
 struct WgArgs {
   int n, di, hi, wi, do_, ho, wo, cin, cout, k, s, p, reflect;
@@ -266,6 +267,233 @@ int wgrad_bf16_launch(const cgan3d_conv_geom* g, const float* gathered, const fl
     else CG_WGB(4, false);
   }
 #undef CG_WGB
+  return CGAN3D_OK;
+}
+
+
+// ---- ResNet-block weight gradient (k3 s1 p1, 64 -> 64, bf16 MFMA), SURVEY.md §8 a2/a5:
+// dW[t][a][b] = sum_o X(o + t - 1)[a] * dZ(o)[b].  Block = (tap plane td, chunk p of the output
+// voxels); wave w owns input channels 16w..16w+15 x all 64 output channels x the 9 taps of the
+// plane (36 accumulator tiles).  K = output voxels in units of 4 (y) x 8 (x) = 32, two units per
+// LDS stage.  Both operands stay NDHWC ([voxel][channel] bf16 rows of 128 B) in LDS and are read
+// as MFMA fragments with ds_read_b64_tr_b16 (lane i of a 16-lane group receives channel i of 4
+// voxel rows, whatever those rows' addresses): the tap shift is just another row address, so the
+// X halo is staged once per unit and serves all 9 taps.  16-channel chunks of a row are XOR-
+// swizzled by ((x >> 1) + 2y) & 3: the 8 rows a 32-lane half reads (4 consecutive x, 2 y) land
+// on 8 distinct 8-bank groups, for every tap.  Per-block partials go to ws[p][t][b][a] (plain
+// stores), wgrad_k3_reduce_kernel sums them into dW's layout.
+namespace wk3 {
+constexpr int EX = 10, EY = 6;                  // X halo of one unit: 6 (y) x 10 (x) voxels
+constexpr int XROWS = 2 * EX * EY, ZROWS = 2 * 32;  // rows per stage (two units)
+constexpr int STAGE_BYTES = (XROWS + ZROWS) * 128;
+__device__ __forceinline__ int swz(int x, int y) { return ((x >> 1) + 2 * y) & 3; }
+}  // namespace wk3
+
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef short s16x8 __attribute__((ext_vector_type(8)));
+
+__device__ __forceinline__ bf16x8_w tr_pair(const unsigned char* lds, int off0, int off1) {
+  const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(lds + off0));
+  const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(lds + off1));
+  const s16x8 v = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+  return __builtin_bit_cast(bf16x8_w, v);
+}
+
+struct Wk3Args {
+  int n, d, h, w;
+  int units;      // n * d * (h/4) * (w/8)
+  int upb;        // units per block (even)
+};
+
+__global__ __launch_bounds__(512, 2) void wgrad_k3_kernel(Wk3Args a, const float* __restrict__ x,
+                                                          const float* __restrict__ dz, float* __restrict__ ws) {
+  // 8 waves: wave w owns input channels 16*(w & 3) .. +15 and output-channel tiles 2*(w >> 2), +1
+  // (18 accumulator tiles); 2 waves per SIMD interleave their MFMAs with the other's loads
+  using namespace wk3;
+  __shared__ __attribute__((aligned(16))) unsigned char smem[2 * STAGE_BYTES];
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int at = wave & 3, bh = wave >> 2;
+  const int td = blockIdx.y, p = blockIdx.x;
+  const int u0 = p * a.upb;
+  const int yb_n = a.h >> 2, xb_n = a.w >> 3;
+  const long long plane = (long long)a.h * a.w;
+
+  // per-thread staging slots (fixed over the stages): X halo quads k < 4 (rows (tid>>4) + 32k of the
+  // stage's 120), dZ quads k < 2 (rows (tid>>4) + 32k of 64); q4 = channel quad
+  const int q4 = tid & 15, rbase = tid >> 4;
+  // block-uniform decode of a unit: voxel index of its (z, 4*yb, 8*xb) corner, and its z, yb, xb
+  struct Unit { long long corner; int z, yb, xb; bool ok; };
+  auto unit = [&](int uu) {
+    Unit r;
+    r.ok = uu < u0 + a.upb && uu < a.units;
+    const int xb = uu % xb_n, q = uu / xb_n, yb = q % yb_n, zq = q / yb_n;
+    r.z = zq % a.d;
+    r.yb = yb; r.xb = xb;
+    r.corner = (long long)zq * plane + (long long)(yb * 4) * a.w + xb * 8;  // zq = nb * d + z
+    return r;
+  };
+  f32x4 sx[4], sz[2];
+  auto load = [&](int s) {
+    const Unit U0 = unit(u0 + 2 * s), U1 = unit(u0 + 2 * s + 1);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int row = rbase + 32 * k;  // < 128; rows >= 120 idle
+      const int u = row >= EX * EY, r = row - u * EX * EY;
+      const int hy = r / EX, hx = r - hy * EX;
+      const Unit V = u ? U1 : U0;
+      const int iz = V.z + td - 1, iy = V.yb * 4 + hy - 1, ix = V.xb * 8 + hx - 1;
+      const bool ok = row < XROWS && V.ok && (unsigned)iz < (unsigned)a.d && (unsigned)iy < (unsigned)a.h &&
+                      (unsigned)ix < (unsigned)a.w;
+      const long long off = V.corner + (long long)(td - 1) * plane + (long long)(hy - 1) * a.w + (hx - 1);
+      sx[k] = ok ? *reinterpret_cast<const f32x4*>(x + off * 64 + 4 * q4) : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int row = rbase + 32 * k;  // < 64
+      const int u = row >> 5, r = row & 31;
+      const Unit V = u ? U1 : U0;
+      const long long off = V.corner + (long long)(r >> 3) * a.w + (r & 7);
+      sz[k] = V.ok ? *reinterpret_cast<const f32x4*>(dz + off * 64 + 4 * q4) : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+  };
+  auto store = [&](int buf) {
+    unsigned char* base = smem + buf * STAGE_BYTES;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int row = rbase + 32 * k;
+      if (row >= XROWS) break;
+      const int r = row >= EX * EY ? row - EX * EY : row;
+      const int hy = r / EX, hx = r - hy * EX;
+      bf16x4_w v;
+      v[0] = (__bf16)sx[k][0]; v[1] = (__bf16)sx[k][1]; v[2] = (__bf16)sx[k][2]; v[3] = (__bf16)sx[k][3];
+      *reinterpret_cast<bf16x4_w*>(base + row * 128 + (((q4 >> 2) ^ swz(hx, hy)) * 32) + (q4 & 3) * 8) = v;
+    }
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int row = rbase + 32 * k;
+      const int r = row & 31;
+      bf16x4_w v;
+      v[0] = (__bf16)sz[k][0]; v[1] = (__bf16)sz[k][1]; v[2] = (__bf16)sz[k][2]; v[3] = (__bf16)sz[k][3];
+      *reinterpret_cast<bf16x4_w*>(base + (XROWS + row) * 128 + (((q4 >> 2) ^ swz(r & 7, r >> 3)) * 32) + (q4 & 3) * 8) = v;
+    }
+  };
+
+  f32x4 acc[9][2];
+#pragma unroll
+  for (int t = 0; t < 9; ++t)
+#pragma unroll
+    for (int bt = 0; bt < 2; ++bt) acc[t][bt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int g = lane >> 4, q = (lane & 15) >> 2, pp = lane & 3;
+  // per-lane LDS byte offsets of the fragment reads (unit 0; unit 1 adds a constant)
+  int boff[2][2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int bt = 2 * bh + j;
+    boff[j][0] = (XROWS + g * 8 + q) * 128 + ((bt ^ swz(q, g)) * 32) + pp * 8;
+    boff[j][1] = (XROWS + g * 8 + q + 4) * 128 + ((bt ^ swz(q + 4, g)) * 32) + pp * 8;
+  }
+  const int nstages = a.upb / 2;
+  load(0);
+  for (int s = 0; s < nstages; ++s) {
+    const int buf = s & 1;
+    store(buf);
+    lds_barrier();
+    if (s + 1 < nstages) load(s + 1);
+    const unsigned char* base = smem + buf * STAGE_BYTES;
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      bf16x8_w bfr[2];
+#pragma unroll
+      for (int j = 0; j < 2; ++j) bfr[j] = tr_pair(base + u * 32 * 128, boff[j][0], boff[j][1]);
+#pragma unroll
+      for (int th = 0; th < 3; ++th)
+#pragma unroll
+        for (int tw = 0; tw < 3; ++tw) {
+          const int hy = g + th, hx0 = q + tw, hx1 = q + 4 + tw;
+          const int r0 = u * (EX * EY) + hy * EX + hx0, r1 = r0 + 4;
+          const bf16x8_w afr = tr_pair(base, r0 * 128 + ((at ^ swz(hx0, hy)) * 32) + pp * 8,
+                                       r1 * 128 + ((at ^ swz(hx1, hy)) * 32) + pp * 8);
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+            acc[th * 3 + tw][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afr, bfr[j], acc[th * 3 + tw][j], 0, 0, 0);
+        }
+    }
+    // no trailing barrier: the next iteration stores into the other buffer, last read one stage
+    // earlier, before every wave passed this iteration's barrier
+  }
+  // partials: lane holds a = 16*at + 4g + jj (jj = 0..3), b = 16*bt + (lane & 15)
+  const int bl = lane & 15;
+#pragma unroll
+  for (int t = 0; t < 9; ++t)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int tap = td * 9 + t, bt = 2 * bh + j;
+      *reinterpret_cast<f32x4*>(ws + ((((long long)p * 27 + tap) * 64 + bt * 16 + bl) * 64 + 16 * at + 4 * g)) =
+          acc[t][j];
+    }
+}
+
+// dW[b * w_sb + a * w_sa + t] (+)= sum_p ws[p][t][b][a]; block = (b, 16 input channels)
+__global__ __launch_bounds__(448) void wgrad_k3_reduce_kernel(const float* __restrict__ ws, int P, float* dw,
+                                                              long long w_sa, long long w_sb, int accumulate) {
+  __shared__ float tile[16][28];
+  const int b = blockIdx.x, a0 = blockIdx.y * 16, tid = threadIdx.x;
+  if (tid < 432) {
+    const int t = tid >> 4, al = tid & 15;
+    const float* src = ws + ((long long)t * 64 + b) * 64 + a0 + al;
+    constexpr long long PS = 27 * 4096;
+    float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};  // 8 independent loads in flight
+    int p = 0;
+    for (; p + 8 <= P; p += 8)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s[j] += src[(p + j) * PS];
+    for (; p < P; ++p) s[0] += src[p * PS];
+    tile[al][t] = ((s[0] + s[1]) + (s[2] + s[3])) + ((s[4] + s[5]) + (s[6] + s[7]));
+  }
+  __syncthreads();
+  if (tid < 432) {
+    const int al = tid / 27, t = tid - al * 27;
+    float* o = dw + (long long)b * w_sb + (long long)(a0 + al) * w_sa + t;
+    *o = accumulate ? *o + tile[al][t] : tile[al][t];
+  }
+}
+
+static int g_wk3_P = 64;  // cgan3d_set_tuning key 9: voxel chunks (blocks per tap plane); 0 = off
+
+void wgrad_k3_set_chunks(int v) { g_wk3_P = v; }
+
+bool wgrad_k3_ok(const cgan3d_conv_geom* g) {
+  return g_wk3_P > 0 && g->prec == CGAN3D_PREC_BF16 && !g->transposed && !g->reflect && g->k == 3 && g->stride == 1 && g->pad == 1 &&
+         g->cin == 64 && g->cout == 64 && g->di == g->do_ && g->hi == g->ho && g->wi == g->wo && g->ho % 4 == 0 &&
+         g->wo % 8 == 0;
+}
+
+static void wgrad_k3_geometry(const cgan3d_conv_geom* g, Wk3Args* a, int* P) {
+  a->n = g->n; a->d = g->do_; a->h = g->ho; a->w = g->wo;
+  a->units = g->n * g->do_ * (g->ho / 4) * (g->wo / 8);
+  int p = std::max(1, std::min(g_wk3_P, (a->units + 1) / 2));
+  int upb = (a->units + p - 1) / p;
+  upb = (upb + 1) / 2 * 2;
+  *P = (a->units + upb - 1) / upb;
+  a->upb = upb;
+}
+
+long long wgrad_k3_ws_floats(const cgan3d_conv_geom* g) {
+  if (!wgrad_k3_ok(g)) return 0;
+  Wk3Args a;
+  int P;
+  wgrad_k3_geometry(g, &a, &P);
+  return (long long)P * 27 * 64 * 64;
+}
+
+int wgrad_k3_launch(const cgan3d_conv_geom* g, const float* gathered, const float* aligned, float* dw, int accumulate,
+                    float* ws, hipStream_t st) {
+  Wk3Args a;
+  int P;
+  wgrad_k3_geometry(g, &a, &P);
+  ::cg::launch(wgrad_k3_kernel, dim3(P, 3), dim3(512), 0, st, a, gathered, aligned, ws);
+  ::cg::launch(wgrad_k3_reduce_kernel, dim3(64, 4), dim3(448), 0, st, (const float*)ws, P, dw, (long long)g->w_sa,
+               (long long)g->w_sb, accumulate);
   return CGAN3D_OK;
 }
 

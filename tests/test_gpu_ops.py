@@ -355,7 +355,9 @@ def test_k7_bf16_mfma(sp):
 
 WGRAD_BF16_CASES = [
     # cin, cout, k, s, p, reflect, spatial (module input)
-    (64, 64, 3, 1, 1, False, (8, 10, 12)),   # ResNet block
+    (64, 64, 3, 1, 1, False, (8, 10, 12)),   # ResNet block (H % 4 != 0: generic kernel)
+    (64, 64, 3, 1, 1, False, (16, 16, 16)),  # ResNet block at 64^3 patches: wgrad_k3_kernel
+    (64, 64, 3, 1, 1, False, (5, 4, 8)),     # wgrad_k3_kernel, odd unit count, one unit per row
     (16, 32, 3, 2, 1, False, (12, 16, 20)),  # downsampling
     (8, 16, 4, 2, 1, False, (16, 16, 16)),   # critic middle
     (32, 64, 4, 2, 1, False, (8, 8, 8)),
@@ -381,6 +383,8 @@ def test_wgrad_bf16(cin, cout, k, s, p, reflect, sp):
     dwo = torch.empty(w.shape, device="cuda")
     ops.wgrad(gw, _cl(x), _cl(gy), dwo, ws)
     assert_close(dwo.double().cpu().numpy(), dw.numpy(), 2e-2, "bf16 wgrad")
+    ops.wgrad(gw, _cl(x), _cl(gy), dwo, ws, accumulate=True)
+    assert_close(dwo.double().cpu().numpy(), 2 * dw.numpy(), 2e-2, "bf16 wgrad accumulate")
 
 
 def test_wgrad_bf16_conv_transpose():

@@ -38,7 +38,8 @@ def _cases(B=4, S=64):
     def wgrad_case(geo, din, dout):
         x, go = t(B, *din, geo.cin), t(B, *dout, geo.cout)
         dw = torch.empty(geo.cout, geo.cin, geo.k, geo.k, geo.k, device=dev)
-        ws = torch.empty(ops.wgrad_ws_floats(geo), device=dev)
+        # room for any chunk count a --tune 9=... sweep asks for (wgrad_k3_kernel partials)
+        ws = torch.empty(max(ops.wgrad_ws_floats(geo), 256 * 27 * 4096 if geo.cin == geo.cout == 64 else 0), device=dev)
         flops = 2.0 * B * dout[0] * dout[1] * dout[2] * geo.cin * geo.cout * geo.k**3
         return (lambda: ops.wgrad(geo, x, go, dw, ws)), flops
 
