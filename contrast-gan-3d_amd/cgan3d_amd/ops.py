@@ -40,6 +40,8 @@ def uses_gemm(g: ConvGeom) -> bool:
     packed weights and run in bf16); k7 single-channel and cout == 1 launches use direct kernels."""
     if g.cout < 2:
         return False
+    if g.cin == 1 and g.cout == 8 and g.k == 4 and g.stride == 2 and g.pad == 1 and not g.transposed:
+        return False  # critic first layer: conv_c1.hip reads torch-layout weights
     return not (g.k == 7 and g.stride == 1 and g.cin == 1 and g.cout in (8, 16))
 
 

@@ -159,6 +159,14 @@ int gemm_blocks(const cgan3d_conv_geom* g, long long* mblocks);
 bool wgrad_bf16_ok(const cgan3d_conv_geom* g);
 bool wgrad_c1_ok(const cgan3d_conv_geom* g);
 bool wgrad_k3_ok(const cgan3d_conv_geom* g);
+// critic first layer, single channel (conv_c1.hip)
+bool c1_fwd_ok(const cgan3d_conv_geom* g);
+bool c1_dgrad_ok(const cgan3d_conv_geom* g);
+bool c1_wgrad_ok(const cgan3d_conv_geom* g);
+int c1_fwd_launch(const cgan3d_conv_geom* g, const float* x, const float* w, float* y, const Epi& e, hipStream_t st);
+int c1_dgrad_launch(const cgan3d_conv_geom* g, const float* dz, const float* w, float* dx, const Epi& e,
+                    hipStream_t st);
+int c1_wgrad_launch(const cgan3d_conv_geom* g, const float* x, const float* dz, float* dw, hipStream_t st);
 long long wgrad_k3_ws_floats(const cgan3d_conv_geom* g);
 void wgrad_k3_set_chunks(int v);
 int wgrad_k3_launch(const cgan3d_conv_geom* g, const float* gathered, const float* aligned, float* dw, int accumulate,

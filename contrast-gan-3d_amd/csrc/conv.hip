@@ -444,6 +444,13 @@ extern "C" int cgan3d_conv3d_fwd(const cgan3d_conv_geom* g, const float* x, cons
   hipStream_t s = (hipStream_t)stream;
   CG_CHECK_ARG(!g->w_packed || (g->cout > 1 && !(g->k == 7 && g->stride == 1 && g->cin == 1)),
                "cgan3d_conv3d_fwd: packed weights only for the implicit-GEMM path");
+  if (c1_fwd_ok(g) || c1_dgrad_ok(g)) {  // critic first layer (conv_c1.hip)
+    CG_CHECK_ARG(!e.bn_mode, "cgan3d_conv3d_fwd: no BatchNorm statistics on the single-channel critic layer");
+    const int rc = g->transposed ? c1_dgrad_launch(g, x, w, y, e, s) : c1_fwd_launch(g, x, w, y, e, s);
+    if (rc) return rc;
+    CG_LAUNCH_CHECK("conv_c1");
+    return CGAN3D_OK;
+  }
   if (k7_try_fwd(g, x, w, y, e, s)) {
     CG_LAUNCH_CHECK("k7 conv");
     return CGAN3D_OK;
@@ -515,6 +522,16 @@ extern "C" int cgan3d_conv3d_wgrad(const cgan3d_conv_geom* g, const float* gathe
       return CGAN3D_OK;
     }
     CG_CHECK_ARG(!accumulate, "cgan3d_conv3d_wgrad: internal dispatch error");
+  }
+  if (c1_wgrad_ok(g)) {  // critic first layer: LDS-window kernel, atomics straight into dW
+    if (!accumulate && ::cg::memset_async(dw, 0, R * g->cout * sizeof(float), s) != hipSuccess) {
+      set_error("cgan3d_conv3d_wgrad: memset failed");
+      return CGAN3D_EHIP;
+    }
+    const int rc = c1_wgrad_launch(g, gathered, aligned, dw, s);
+    if (rc) return rc;
+    CG_LAUNCH_CHECK("c1_wgrad_kernel");
+    return CGAN3D_OK;
   }
   if (wgrad_c1_ok(g)) {  // single-channel input: straight into dW, no workspace
     if (!accumulate && ::cg::memset_async(dw, 0, R * g->cout * sizeof(float), s) != hipSuccess) {

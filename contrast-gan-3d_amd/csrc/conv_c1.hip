@@ -1,0 +1,238 @@
+// The critic's single-channel first layer (model/discriminator.py:24-39: Conv3d 1 -> 8, k4 s2 p1,
+// bias, LeakyReLU 0.2) in its three roles — forward (also the gradient-penalty forward-mode
+// chain, mask epilogue), input-grad (ConvTranspose-shaped, 8 -> 1, only for the interpolated
+// samples whose dD/dx the penalty needs) and weight-grad.  One input channel means no channel
+// contraction to put on MFMA: these are exact fp32 FMA kernels that read each input voxel once
+// through an LDS window and are bound by HBM/L2 traffic (12 x 64^3 inputs per step), not by the
+// ~0.4 GFLOP they do.  Tiles: 2 x 8 x 16 output voxels (z, y, x), one per thread.
+#include "common.h"
+
+namespace cg {
+
+struct C1Args {
+  int n, di, hi, wi, do_, ho, wo;  // gathered (stride-2 input) dims, output dims (fwd roles)
+  int tz, ty, tx;                  // tiles per dim
+  long long w_sa, w_sb;            // weight strides (input-channel side, output-channel side)
+  int tiles_per_block;             // wgrad
+};
+
+namespace c1 {
+constexpr int TZ = 2, TY = 8, TX = 16;                 // output tile
+constexpr int WZ = 2 * TZ + 2, WY = 2 * TY + 2, WX = 2 * TX + 2;  // k4 s2 p1 input window (6 x 18 x 34)
+constexpr int RS = 36, PS = 656;                        // LDS row / plane strides (floats): 36 = 4 mod 32,
+                                                        // 656 = 16 mod 32 (conflict-free tap-lane reads)
+constexpr int WIN = WZ * PS;
+}  // namespace c1
+
+// stage the k4 s2 p1 input window of output tile (n, oz0, oy0, ox0) into xs (zero outside)
+__device__ __forceinline__ void c1_stage_window(const C1Args& a, const float* __restrict__ x, int nb, int oz0, int oy0,
+                                                int ox0, float* xs) {
+  using namespace c1;
+  const int iz0 = 2 * oz0 - 1, iy0 = 2 * oy0 - 1, ix0 = 2 * ox0 - 1;
+  for (int i = threadIdx.x; i < WZ * WY * WX; i += 256) {
+    const int hx = i % WX, r = i / WX, hy = r % WY, hz = r / WY;
+    const int iz = iz0 + hz, iy = iy0 + hy, ix = ix0 + hx;
+    float v = 0.f;
+    if ((unsigned)iz < (unsigned)a.di && (unsigned)iy < (unsigned)a.hi && (unsigned)ix < (unsigned)a.wi)
+      v = x[(((long long)nb * a.di + iz) * a.hi + iy) * a.wi + ix];
+    xs[hz * PS + hy * RS + hx] = v;
+  }
+}
+
+__device__ __forceinline__ void c1_tile(const C1Args& a, int t, int* nb, int* oz0, int* oy0, int* ox0) {
+  const int tx = t % a.tx, r = t / a.tx, ty = r % a.ty, r2 = r / a.ty, tz = r2 % a.tz;
+  *nb = r2 / a.tz;
+  *oz0 = tz * c1::TZ; *oy0 = ty * c1::TY; *ox0 = tx * c1::TX;
+}
+
+// y[o][b] = epi(sum_t x[2o - 1 + t] * w[b][t]), 8 output channels
+__global__ __launch_bounds__(256) void c1_fwd_kernel(C1Args a, const float* __restrict__ x, const float* __restrict__ w,
+                                                     float* y, Epi ep) {
+  using namespace c1;
+  __shared__ __attribute__((aligned(16))) float xs[WIN];
+  int nb, oz0, oy0, ox0;
+  c1_tile(a, blockIdx.x, &nb, &oz0, &oy0, &ox0);
+  c1_stage_window(a, x, nb, oz0, oy0, ox0, xs);
+  __syncthreads();
+  const int tid = threadIdx.x, lz = tid >> 7, ly = (tid >> 4) & 7, lx = tid & 15;
+  float acc[8];
+#pragma unroll
+  for (int b = 0; b < 8; ++b) acc[b] = 0.f;
+#pragma unroll
+  for (int td = 0; td < 4; ++td)
+#pragma unroll
+    for (int th = 0; th < 4; ++th)
+#pragma unroll
+      for (int tw = 0; tw < 4; tw += 2) {
+        const float2 v = *reinterpret_cast<const float2*>(xs + (2 * lz + td) * PS + (2 * ly + th) * RS + 2 * lx + tw);
+        const int t = (td * 4 + th) * 4 + tw;
+#pragma unroll
+        for (int b = 0; b < 8; ++b) {  // block-uniform weight reads: scalar loads
+          acc[b] = fmaf(v.x, w[b * a.w_sb + t], acc[b]);
+          acc[b] = fmaf(v.y, w[b * a.w_sb + t + 1], acc[b]);
+        }
+      }
+  const int oz = oz0 + lz, oy = oy0 + ly, ox = ox0 + lx;
+  if (oz >= a.do_ || oy >= a.ho || ox >= a.wo) return;
+  const long long o = (((long long)nb * a.do_ + oz) * a.ho + oy) * a.wo + ox;
+  float v[8];
+  f32x4 m0 = {1.f, 1.f, 1.f, 1.f}, m1 = m0;
+  if (ep.mask_src) {
+    m0 = *reinterpret_cast<const f32x4*>(ep.mask_src + o * 8);
+    m1 = *reinterpret_cast<const f32x4*>(ep.mask_src + o * 8 + 4);
+  }
+#pragma unroll
+  for (int b = 0; b < 8; ++b) {
+    float t = acc[b] + (ep.bias ? ep.bias[b] : 0.f);
+    if (ep.act == CGAN3D_ACT_RELU) t = fmaxf(t, 0.f);
+    else if (ep.act == CGAN3D_ACT_LRELU) t = t > 0.f ? t : t * ep.slope;
+    const float m = b < 4 ? m0[b & 3] : m1[b & 3];
+    if (ep.mask_src) t = m > 0.f ? t : t * ep.slope;
+    v[b] = t;
+  }
+  *reinterpret_cast<f32x4*>(y + o * 8) = f32x4{v[0], v[1], v[2], v[3]};
+  *reinterpret_cast<f32x4*>(y + o * 8 + 4) = f32x4{v[4], v[5], v[6], v[7]};
+}
+
+// input-grad: dx[i] = sum_{t, o : i = 2o - 1 + t} sum_c dz[o][c] * w[c][t]  (i on the fine grid)
+// a.di.. = coarse (dz) dims, a.do_.. = fine (dx) dims; tile = 2 x 8 x 16 fine voxels
+__global__ __launch_bounds__(256) void c1_dgrad_kernel(C1Args a, const float* __restrict__ dz,
+                                                       const float* __restrict__ w, float* dx) {
+  constexpr int GZ = c1::TZ / 2 + 2, GY = c1::TY / 2 + 2, GX = c1::TX / 2 + 2;  // coarse window 3 x 6 x 10
+  __shared__ __attribute__((aligned(16))) float gs[GZ * GY * GX * 8];
+  __shared__ __attribute__((aligned(16))) float ws[64 * 8];  // [tap][c]
+  int nb, oz0, oy0, ox0;
+  c1_tile(a, blockIdx.x, &nb, &oz0, &oy0, &ox0);
+  const int tid = threadIdx.x;
+  for (int i = tid; i < 512; i += 256) ws[i] = w[(i & 7) * a.w_sa + (i >> 3)];
+  const int cz0 = oz0 / 2 - 1, cy0 = oy0 / 2 - 1, cx0 = ox0 / 2 - 1;
+  for (int i = tid; i < GZ * GY * GX * 2; i += 256) {  // float4 halves of 8-channel voxels
+    const int h = i & 1, v = i >> 1;
+    const int gx = v % GX, r = v / GX, gy = r % GY, gz = r / GY;
+    const int cz = cz0 + gz, cy = cy0 + gy, cx = cx0 + gx;
+    f32x4 val = {0.f, 0.f, 0.f, 0.f};
+    if ((unsigned)cz < (unsigned)a.di && (unsigned)cy < (unsigned)a.hi && (unsigned)cx < (unsigned)a.wi)
+      val = *reinterpret_cast<const f32x4*>(dz + ((((long long)nb * a.di + cz) * a.hi + cy) * a.wi + cx) * 8 + 4 * h);
+    *reinterpret_cast<f32x4*>(gs + v * 8 + 4 * h) = val;
+  }
+  __syncthreads();
+  const int lz = tid >> 7, ly = (tid >> 4) & 7, lx = tid & 15;
+  const int oz = oz0 + lz, oy = oy0 + ly, ox = ox0 + lx;
+  // per dim: taps t = ((o + 1) & 1) + 2j, coarse o' = (o + 1 - t) / 2, local = o' - c0
+  float acc = 0.f;
+#pragma unroll
+  for (int jz = 0; jz < 2; ++jz)
+#pragma unroll
+    for (int jy = 0; jy < 2; ++jy)
+#pragma unroll
+      for (int jx = 0; jx < 2; ++jx) {
+        const int tz = ((oz + 1) & 1) + 2 * jz, ty = ((oy + 1) & 1) + 2 * jy, tx = ((ox + 1) & 1) + 2 * jx;
+        const int gz = (oz + 1 - tz) / 2 - cz0, gy = (oy + 1 - ty) / 2 - cy0, gx = (ox + 1 - tx) / 2 - cx0;
+        const float* gv = gs + ((gz * GY + gy) * GX + gx) * 8;
+        const float* wv = ws + ((tz * 4 + ty) * 4 + tx) * 8;
+        const f32x4 g0 = *reinterpret_cast<const f32x4*>(gv), g1 = *reinterpret_cast<const f32x4*>(gv + 4);
+        const f32x4 w0 = *reinterpret_cast<const f32x4*>(wv), w1 = *reinterpret_cast<const f32x4*>(wv + 4);
+#pragma unroll
+        for (int c = 0; c < 4; ++c) acc = fmaf(g0[c], w0[c], acc);
+#pragma unroll
+        for (int c = 0; c < 4; ++c) acc = fmaf(g1[c], w1[c], acc);
+      }
+  if (oz < a.do_ && oy < a.ho && ox < a.wo) dx[(((long long)nb * a.do_ + oz) * a.ho + oy) * a.wo + ox] = acc;
+}
+
+// weight-grad: dw[b][t] += sum_{n,o} x[2o - 1 + t] * dz[o][b]; lane = tap, 4 waves split a tile's
+// voxels; tiles_per_block tiles per block, one atomic add per (b, t) per block
+__global__ __launch_bounds__(256) void c1_wgrad_kernel(C1Args a, const float* __restrict__ x,
+                                                       const float* __restrict__ dz, float* dw, int ntiles) {
+  using namespace c1;
+  __shared__ __attribute__((aligned(16))) float xs[WIN];
+  __shared__ __attribute__((aligned(16))) float gs[TZ * TY * TX * 8];
+  __shared__ float red[4][8][65];
+  const int tid = threadIdx.x, t = tid & 63, vg = tid >> 6;
+  const int td = t >> 4, th = (t >> 2) & 3, tw = t & 3;
+  float acc[8];
+#pragma unroll
+  for (int b = 0; b < 8; ++b) acc[b] = 0.f;
+  for (int k = 0; k < a.tiles_per_block; ++k) {
+    const int tile = blockIdx.x * a.tiles_per_block + k;
+    if (tile >= ntiles) break;  // block-uniform
+    int nb, oz0, oy0, ox0;
+    c1_tile(a, tile, &nb, &oz0, &oy0, &ox0);
+    __syncthreads();  // previous tile's reads done
+    c1_stage_window(a, x, nb, oz0, oy0, ox0, xs);
+    for (int i = tid; i < TZ * TY * TX * 2; i += 256) {
+      const int h = i & 1, v = i >> 1;
+      const int oz = oz0 + (v >> 7), oy = oy0 + ((v >> 4) & 7), ox = ox0 + (v & 15);
+      f32x4 val = {0.f, 0.f, 0.f, 0.f};
+      if (oz < a.do_ && oy < a.ho && ox < a.wo)
+        val = *reinterpret_cast<const f32x4*>(dz + ((((long long)nb * a.do_ + oz) * a.ho + oy) * a.wo + ox) * 8 + 4 * h);
+      *reinterpret_cast<f32x4*>(gs + v * 8 + 4 * h) = val;
+    }
+    __syncthreads();
+    for (int v = vg * 64; v < vg * 64 + 64; ++v) {
+      const int lz = v >> 7, ly = (v >> 4) & 7, lx = v & 15;
+      const float xv = xs[(2 * lz + td) * PS + (2 * ly + th) * RS + 2 * lx + tw];
+      const f32x4 g0 = *reinterpret_cast<const f32x4*>(gs + v * 8), g1 = *reinterpret_cast<const f32x4*>(gs + v * 8 + 4);
+#pragma unroll
+      for (int b = 0; b < 4; ++b) acc[b] = fmaf(xv, g0[b], acc[b]);
+#pragma unroll
+      for (int b = 0; b < 4; ++b) acc[4 + b] = fmaf(xv, g1[b], acc[4 + b]);
+    }
+  }
+#pragma unroll
+  for (int b = 0; b < 8; ++b) red[vg][b][t] = acc[b];
+  __syncthreads();
+  for (int i = tid; i < 512; i += 256) {
+    const int b = i >> 6, tt = i & 63;
+    const float s = red[0][b][tt] + red[1][b][tt] + red[2][b][tt] + red[3][b][tt];
+    atomicAdd(dw + b * a.w_sb + tt, s);
+  }
+}
+
+// roles this file takes (geometries as built by cgan3d_amd/ops.py)
+bool c1_fwd_ok(const cgan3d_conv_geom* g) {
+  return !g->transposed && !g->reflect && g->cin == 1 && g->cout == 8 && g->k == 4 && g->stride == 2 && g->pad == 1 &&
+         g->w_packed == 0;
+}
+bool c1_dgrad_ok(const cgan3d_conv_geom* g) {
+  return g->transposed && !g->reflect && g->cin == 8 && g->cout == 1 && g->k == 4 && g->stride == 2 && g->pad == 1 &&
+         g->w_packed == 0 && g->do_ % 2 == 0 && g->ho % 2 == 0 && g->wo % 2 == 0;
+}
+bool c1_wgrad_ok(const cgan3d_conv_geom* g) { return c1_fwd_ok(g); }
+
+static C1Args c1_args(const cgan3d_conv_geom* g) {
+  C1Args a;
+  a.n = g->n; a.di = g->di; a.hi = g->hi; a.wi = g->wi; a.do_ = g->do_; a.ho = g->ho; a.wo = g->wo;
+  a.tz = ceil_div(g->do_, c1::TZ); a.ty = ceil_div(g->ho, c1::TY); a.tx = ceil_div(g->wo, c1::TX);
+  a.w_sa = g->w_sa; a.w_sb = g->w_sb;
+  a.tiles_per_block = 1;
+  return a;
+}
+
+int c1_fwd_launch(const cgan3d_conv_geom* g, const float* x, const float* w, float* y, const Epi& e, hipStream_t st) {
+  CG_CHECK_ARG(!e.residual && !e.minuend && !e.out2 && !e.stats && !e.bn_mode,
+               "conv c1: only bias / activation / mask epilogues");
+  C1Args a = c1_args(g);
+  ::cg::launch(c1_fwd_kernel, dim3(a.n * a.tz * a.ty * a.tx), dim3(256), 0, st, a, x, w, y, e);
+  return CGAN3D_OK;
+}
+
+int c1_dgrad_launch(const cgan3d_conv_geom* g, const float* dz, const float* w, float* dx, const Epi& e,
+                    hipStream_t st) {
+  CG_CHECK_ARG(!e.bias && !e.residual && !e.mask_src && !e.minuend && !e.out2 && !e.stats && !e.bn_mode &&
+                   e.act == CGAN3D_ACT_NONE,
+               "conv c1 input-grad: no epilogue");
+  C1Args a = c1_args(g);
+  ::cg::launch(c1_dgrad_kernel, dim3(a.n * a.tz * a.ty * a.tx), dim3(256), 0, st, a, dz, w, dx);
+  return CGAN3D_OK;
+}
+
+int c1_wgrad_launch(const cgan3d_conv_geom* g, const float* x, const float* dz, float* dw, hipStream_t st) {
+  C1Args a = c1_args(g);
+  const int ntiles = a.n * a.tz * a.ty * a.tx;
+  a.tiles_per_block = ntiles >= 1024 ? 4 : (ntiles >= 512 ? 2 : 1);
+  ::cg::launch(c1_wgrad_kernel, dim3(ceil_div(ntiles, a.tiles_per_block)), dim3(256), 0, st, a, x, dz, dw, ntiles);
+  return CGAN3D_OK;
+}
+
+}  // namespace cg

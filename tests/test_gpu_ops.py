@@ -21,7 +21,8 @@ CONV_CASES = [
     (8, 1, 7, 1, 3, True, (8, 8, 8)),
     (16, 32, 3, 2, 1, False, (12, 16, 20)),  # downsampling
     (64, 64, 3, 1, 1, False, (6, 8, 10)),    # resnet block
-    (1, 8, 4, 2, 1, False, (16, 16, 16)),    # critic first
+    (1, 8, 4, 2, 1, False, (16, 16, 16)),    # critic first (conv_c1.hip)
+    (1, 8, 4, 2, 1, False, (10, 12, 36)),    # critic first, partial 2 x 8 x 16 tiles
     (8, 16, 4, 2, 1, False, (16, 16, 16)),   # critic middle
     (64, 1, 4, 1, 1, False, (4, 4, 4)),      # critic last
     (12, 20, 3, 1, 1, False, (5, 6, 7)),     # odd channel counts (generic path)
