@@ -54,6 +54,7 @@ _SIGS = {
     "cgan3d_conv3d_fwd": ([_P, _P, _P, _P, _P, _P], _I32),
     "cgan3d_packed_weight_floats": ([_P], _I64),
     "cgan3d_halo_eligible": ([_P], _I32),
+    "cgan3d_packed_format": ([_P], _I32),
     "cgan3d_pack_weights": ([_P, _P, _P, _P], _I32),
     "cgan3d_pack_weights_multi": ([_P, _I32, _I64, _P], _I32),
     "cgan3d_conv3d_wgrad_ws_floats": ([_P], _I64),

@@ -54,14 +54,23 @@ def halo_eligible(g: ConvGeom) -> bool:
     return bool(L.load().cgan3d_halo_eligible(ctypes.byref(g)))
 
 
+# conv_sk.hip takes the critic's k4 convs in bf16 (format 3); CGAN3D_NO_SK=1 keeps them on the
+# halo / implicit-GEMM kernels (A/B measurements)
+SK = os.environ.get("CGAN3D_NO_SK", "0") != "1"
+
+
 def with_packing(g: ConvGeom, prec: int = L.PREC_F32) -> ConvGeom:
-    """Copy of ``g`` that reads packed weights (cgan3d_pack_weights) and runs in ``prec``:
-    format 2 (halo kernel, bf16 [tap][b][a]) where eligible, else format 1 ([tap][a][b] f32)."""
+    """Copy of ``g`` that reads packed weights (cgan3d_pack_weights) and runs in ``prec``: in bf16
+    format 3 (K-split small-grid kernel, bf16 [b][tap][a]) or 2 (halo kernel, bf16 [tap][b][a])
+    where eligible (cgan3d_packed_format), else format 1 ([tap][a][b] f32)."""
     h = ConvGeom()
     ctypes.pointer(h)[0] = g
     h.w_packed, h.prec = 1, prec
-    if prec == L.PREC_BF16 and HALO and halo_eligible(h):
-        h.w_packed = 2
+    if prec == L.PREC_BF16 and HALO:
+        f = int(L.load().cgan3d_packed_format(ctypes.byref(h)))
+        if f == 3 and not SK:
+            f = 2 if halo_eligible(h) else 1
+        h.w_packed = f
     return h
 
 
@@ -76,7 +85,7 @@ def with_prec(g: ConvGeom, prec: int) -> ConvGeom:
 
 def packed_elements(g: ConvGeom) -> int:
     """Elements (f32 or bf16) the pack kernel writes for ``g``."""
-    if g.w_packed == 2:
+    if g.w_packed in (2, 3):
         return g.k**3 * g.cin * g.cout
     return g.k**3 * g.cin * ((g.cout + 3) // 4 * 4)
 

@@ -159,6 +159,11 @@ int gemm_blocks(const cgan3d_conv_geom* g, long long* mblocks);
 bool wgrad_bf16_ok(const cgan3d_conv_geom* g);
 bool wgrad_c1_ok(const cgan3d_conv_geom* g);
 bool wgrad_k3_ok(const cgan3d_conv_geom* g);
+// critic middle layers, K split over waves (conv_sk.hip): packed weights format 3
+bool sk_format_ok(const cgan3d_conv_geom* g);
+bool sk_ok(const cgan3d_conv_geom* g);
+long long sk_blocks(const cgan3d_conv_geom* g);
+int sk_launch(const cgan3d_conv_geom* g, const float* x, const __bf16* wp, float* y, const Epi& e, hipStream_t st);
 // critic first layer, single channel (conv_c1.hip)
 bool c1_fwd_ok(const cgan3d_conv_geom* g);
 bool c1_dgrad_ok(const cgan3d_conv_geom* g);

@@ -97,9 +97,16 @@ __global__ __launch_bounds__(256) void conv_cout1_wave_kernel(ConvArgs a, const 
                                                               const float* __restrict__ w, float* y, Epi ep) {
   extern __shared__ __attribute__((aligned(16))) float Ws[];  // [T][cin]
   const int T = a.k * a.k * a.k;
-  for (int i = threadIdx.x; i < T * a.cin; i += blockDim.x) {
-    int t = i / a.cin, ci = i - t * a.cin;
-    Ws[i] = w[(long long)ci * a.sa + t];
+  for (int i0 = threadIdx.x; i0 < T * a.cin; i0 += 8 * blockDim.x) {  // 8 loads in flight per thread
+    float v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int i = i0 + u * blockDim.x, t = i / a.cin, ci = i - t * a.cin;
+      v[u] = i < T * a.cin ? w[(long long)ci * a.sa + t] : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+      if (i0 + u * blockDim.x < T * a.cin) Ws[i0 + u * blockDim.x] = v[u];
   }
   __syncthreads();
   const int lane = threadIdx.x & 63;
@@ -111,6 +118,7 @@ __global__ __launch_bounds__(256) void conv_cout1_wave_kernel(ConvArgs a, const 
   const int bd = od * a.s - a.p, bh = oh * a.s - a.p, bw = ow * a.s - a.p;
   const int C4 = a.cin >> 2, R4 = T * C4;
   float acc = 0.f;
+#pragma unroll 4
   for (int r4 = lane; r4 < R4; r4 += 64) {
     const int t = r4 / C4, c = (r4 - t * C4) * 4;
     const int td = t / (a.k * a.k), th = (t / a.k) % a.k, tw = t % a.k;
@@ -420,6 +428,7 @@ extern "C" int64_t cgan3d_conv3d_bn_slots(const cgan3d_conv_geom* g) {
 extern "C" int64_t cgan3d_conv3d_stats_floats(const cgan3d_conv_geom* g) {
   if (!g) return -1;
   if (long long kb = k7_n2w_blocks(g)) return (int64_t)kb * (2 * g->cout + 1);
+  if (sk_ok(g)) return (int64_t)sk_blocks(g) * (2 * g->cout + 1);
   if (halo_ok(g)) return (int64_t)halo_mblocks(g) * (2 * g->cout + 1);
   long long mb = 0;
   if (gemm_blocks(g, &mb)) return -1;
@@ -468,6 +477,13 @@ extern "C" int cgan3d_conv3d_fwd(const cgan3d_conv_geom* g, const float* x, cons
     }
     ::cg::launch(conv_cout1_kernel, dim3(a.nclass * a.tiles_per_class), dim3(256), lds, s, a, x, w, y, e);
     CG_LAUNCH_CHECK("conv_cout1_kernel");
+    return CGAN3D_OK;
+  }
+  if (g->w_packed == 3) {
+    CG_CHECK_ARG(sk_ok(g), "cgan3d_conv3d_fwd: w_packed 3 on a geometry conv_sk does not take");
+    int rc = sk_launch(g, x, reinterpret_cast<const __bf16*>(w), y, e, s);
+    if (rc) return rc;
+    CG_LAUNCH_CHECK("conv_sk_kernel");
     return CGAN3D_OK;
   }
   if (g->w_packed == 2) {

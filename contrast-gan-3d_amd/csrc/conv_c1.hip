@@ -24,20 +24,32 @@ constexpr int RS = 36, PS = 656;                        // LDS row / plane strid
 constexpr int WIN = WZ * PS;
 }  // namespace c1
 
-// stage the k4 s2 p1 input window of output tile (n, oz0, oy0, ox0) into xs (zero outside)
+// stage the k4 s2 p1 input window of output tile (n, oz0, oy0, ox0) into xs (zero outside); every
+// load of the thread is issued before the first LDS store
 __device__ __forceinline__ void c1_stage_window(const C1Args& a, const float* __restrict__ x, int nb, int oz0, int oy0,
                                                 int ox0, float* xs) {
   using namespace c1;
+  constexpr int N = WZ * WY * WX, PER = (N + 255) / 256;
   const int iz0 = 2 * oz0 - 1, iy0 = 2 * oy0 - 1, ix0 = 2 * ox0 - 1;
-  for (int i = threadIdx.x; i < WZ * WY * WX; i += 256) {
+  float v[PER];
+#pragma unroll
+  for (int k = 0; k < PER; ++k) {
+    const int i = threadIdx.x + 256 * k;
     const int hx = i % WX, r = i / WX, hy = r % WY, hz = r / WY;
     const int iz = iz0 + hz, iy = iy0 + hy, ix = ix0 + hx;
-    float v = 0.f;
-    if ((unsigned)iz < (unsigned)a.di && (unsigned)iy < (unsigned)a.hi && (unsigned)ix < (unsigned)a.wi)
-      v = x[(((long long)nb * a.di + iz) * a.hi + iy) * a.wi + ix];
-    xs[hz * PS + hy * RS + hx] = v;
+    const bool ok = i < N && (unsigned)iz < (unsigned)a.di && (unsigned)iy < (unsigned)a.hi && (unsigned)ix < (unsigned)a.wi;
+    v[k] = ok ? x[(((long long)nb * a.di + iz) * a.hi + iy) * a.wi + ix] : 0.f;
+  }
+#pragma unroll
+  for (int k = 0; k < PER; ++k) {
+    const int i = threadIdx.x + 256 * k;
+    if (i >= N) break;
+    const int hx = i % WX, r = i / WX, hy = r % WY, hz = r / WY;
+    xs[hz * PS + hy * RS + hx] = v[k];
   }
 }
+
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 __device__ __forceinline__ void c1_tile(const C1Args& a, int t, int* nb, int* oz0, int* oy0, int* ox0) {
   const int tx = t % a.tx, r = t / a.tx, ty = r % a.ty, r2 = r / a.ty, tz = r2 % a.tz;
@@ -50,27 +62,32 @@ __global__ __launch_bounds__(256) void c1_fwd_kernel(C1Args a, const float* __re
                                                      float* y, Epi ep) {
   using namespace c1;
   __shared__ __attribute__((aligned(16))) float xs[WIN];
+  __shared__ __attribute__((aligned(16))) float wsh[64 * 8];  // [tap][b]
   int nb, oz0, oy0, ox0;
   c1_tile(a, blockIdx.x, &nb, &oz0, &oy0, &ox0);
+  const int tid = threadIdx.x;
+  for (int i = tid; i < 512; i += 256) wsh[i] = w[(i & 7) * a.w_sb + (i >> 3)];
   c1_stage_window(a, x, nb, oz0, oy0, ox0, xs);
   __syncthreads();
-  const int tid = threadIdx.x, lz = tid >> 7, ly = (tid >> 4) & 7, lx = tid & 15;
-  float acc[8];
+  const int lz = tid >> 7, ly = (tid >> 4) & 7, lx = tid & 15;
+  f32x2 acc[4];  // channel pairs (2j, 2j + 1): packed fp32 FMA
 #pragma unroll
-  for (int b = 0; b < 8; ++b) acc[b] = 0.f;
-#pragma unroll
-  for (int td = 0; td < 4; ++td)
-#pragma unroll
-    for (int th = 0; th < 4; ++th)
+  for (int j = 0; j < 4; ++j) acc[j] = f32x2{0.f, 0.f};
+  // (td, th) rolled: unrolled, the compiler hoists all 128 weight reads into registers and spills
+#pragma unroll 1
+  for (int tdh = 0; tdh < 16; ++tdh)
 #pragma unroll
       for (int tw = 0; tw < 4; tw += 2) {
+        const int td = tdh >> 2, th = tdh & 3;
         const float2 v = *reinterpret_cast<const float2*>(xs + (2 * lz + td) * PS + (2 * ly + th) * RS + 2 * lx + tw);
-        const int t = (td * 4 + th) * 4 + tw;
-#pragma unroll
-        for (int b = 0; b < 8; ++b) {  // block-uniform weight reads: scalar loads
-          acc[b] = fmaf(v.x, w[b * a.w_sb + t], acc[b]);
-          acc[b] = fmaf(v.y, w[b * a.w_sb + t + 1], acc[b]);
-        }
+        const int t = tdh * 4 + tw;
+        const f32x4* wt = reinterpret_cast<const f32x4*>(wsh + t * 8);  // broadcast reads
+        const f32x4 w0 = wt[0], w1 = wt[1], w2 = wt[2], w3 = wt[3];
+        const f32x2 vx = {v.x, v.x}, vy = {v.y, v.y};
+        acc[0] += vx * f32x2{w0[0], w0[1]} + vy * f32x2{w2[0], w2[1]};
+        acc[1] += vx * f32x2{w0[2], w0[3]} + vy * f32x2{w2[2], w2[3]};
+        acc[2] += vx * f32x2{w1[0], w1[1]} + vy * f32x2{w3[0], w3[1]};
+        acc[3] += vx * f32x2{w1[2], w1[3]} + vy * f32x2{w3[2], w3[3]};
       }
   const int oz = oz0 + lz, oy = oy0 + ly, ox = ox0 + lx;
   if (oz >= a.do_ || oy >= a.ho || ox >= a.wo) return;
@@ -83,7 +100,7 @@ __global__ __launch_bounds__(256) void c1_fwd_kernel(C1Args a, const float* __re
   }
 #pragma unroll
   for (int b = 0; b < 8; ++b) {
-    float t = acc[b] + (ep.bias ? ep.bias[b] : 0.f);
+    float t = acc[b >> 1][b & 1] + (ep.bias ? ep.bias[b] : 0.f);
     if (ep.act == CGAN3D_ACT_RELU) t = fmaxf(t, 0.f);
     else if (ep.act == CGAN3D_ACT_LRELU) t = t > 0.f ? t : t * ep.slope;
     const float m = b < 4 ? m0[b & 3] : m1[b & 3];
@@ -104,17 +121,26 @@ __global__ __launch_bounds__(256) void c1_dgrad_kernel(C1Args a, const float* __
   int nb, oz0, oy0, ox0;
   c1_tile(a, blockIdx.x, &nb, &oz0, &oy0, &ox0);
   const int tid = threadIdx.x;
-  for (int i = tid; i < 512; i += 256) ws[i] = w[(i & 7) * a.w_sa + (i >> 3)];
   const int cz0 = oz0 / 2 - 1, cy0 = oy0 / 2 - 1, cx0 = ox0 / 2 - 1;
-  for (int i = tid; i < GZ * GY * GX * 2; i += 256) {  // float4 halves of 8-channel voxels
-    const int h = i & 1, v = i >> 1;
+  // every global load of the thread (2 weights, <= 3 float4 halves of 8-channel voxels) in flight
+  // before the first LDS store
+  constexpr int NG = GZ * GY * GX * 2, PER = (NG + 255) / 256;
+  const float w0 = w[(tid & 7) * a.w_sa + (tid >> 3)], w1 = w[(tid & 7) * a.w_sa + ((tid + 256) >> 3)];
+  f32x4 gv[PER];
+#pragma unroll
+  for (int k = 0; k < PER; ++k) {
+    const int i = tid + 256 * k, h = i & 1, v = i >> 1;
     const int gx = v % GX, r = v / GX, gy = r % GY, gz = r / GY;
     const int cz = cz0 + gz, cy = cy0 + gy, cx = cx0 + gx;
-    f32x4 val = {0.f, 0.f, 0.f, 0.f};
-    if ((unsigned)cz < (unsigned)a.di && (unsigned)cy < (unsigned)a.hi && (unsigned)cx < (unsigned)a.wi)
-      val = *reinterpret_cast<const f32x4*>(dz + ((((long long)nb * a.di + cz) * a.hi + cy) * a.wi + cx) * 8 + 4 * h);
-    *reinterpret_cast<f32x4*>(gs + v * 8 + 4 * h) = val;
+    gv[k] = (i < NG && (unsigned)cz < (unsigned)a.di && (unsigned)cy < (unsigned)a.hi && (unsigned)cx < (unsigned)a.wi)
+                ? *reinterpret_cast<const f32x4*>(dz + ((((long long)nb * a.di + cz) * a.hi + cy) * a.wi + cx) * 8 + 4 * h)
+                : f32x4{0.f, 0.f, 0.f, 0.f};
   }
+  ws[tid] = w0;
+  ws[tid + 256] = w1;
+#pragma unroll
+  for (int k = 0; k < PER; ++k)
+    if (tid + 256 * k < NG) *reinterpret_cast<f32x4*>(gs + (tid + 256 * k) * 4) = gv[k];
   __syncthreads();
   const int lz = tid >> 7, ly = (tid >> 4) & 7, lx = tid & 15;
   const int oz = oz0 + lz, oy = oy0 + ly, ox = ox0 + lx;
@@ -148,39 +174,72 @@ __global__ __launch_bounds__(256) void c1_wgrad_kernel(C1Args a, const float* __
   __shared__ __attribute__((aligned(16))) float xs[WIN];
   __shared__ __attribute__((aligned(16))) float gs[TZ * TY * TX * 8];
   __shared__ float red[4][8][65];
+  constexpr int N = WZ * WY * WX, PER = (N + 255) / 256;
   const int tid = threadIdx.x, t = tid & 63, vg = tid >> 6;
   const int td = t >> 4, th = (t >> 2) & 3, tw = t & 3;
-  float acc[8];
-#pragma unroll
-  for (int b = 0; b < 8; ++b) acc[b] = 0.f;
-  for (int k = 0; k < a.tiles_per_block; ++k) {
-    const int tile = blockIdx.x * a.tiles_per_block + k;
-    if (tile >= ntiles) break;  // block-uniform
+  // next tile's window + dz held in registers while the current tile is reduced (the staging
+  // latency of tile k+1 hides behind tile k's FMAs; one atomic per (b, t) per block at the end:
+  // every block adds into the same 512 words, so fewer, longer blocks)
+  float xv_n[PER];
+  f32x4 gv_n[2];
+  auto load = [&](int tile) {
     int nb, oz0, oy0, ox0;
     c1_tile(a, tile, &nb, &oz0, &oy0, &ox0);
-    __syncthreads();  // previous tile's reads done
-    c1_stage_window(a, x, nb, oz0, oy0, ox0, xs);
-    for (int i = tid; i < TZ * TY * TX * 2; i += 256) {
-      const int h = i & 1, v = i >> 1;
-      const int oz = oz0 + (v >> 7), oy = oy0 + ((v >> 4) & 7), ox = ox0 + (v & 15);
-      f32x4 val = {0.f, 0.f, 0.f, 0.f};
-      if (oz < a.do_ && oy < a.ho && ox < a.wo)
-        val = *reinterpret_cast<const f32x4*>(dz + ((((long long)nb * a.do_ + oz) * a.ho + oy) * a.wo + ox) * 8 + 4 * h);
-      *reinterpret_cast<f32x4*>(gs + v * 8 + 4 * h) = val;
+    const int iz0 = 2 * oz0 - 1, iy0 = 2 * oy0 - 1, ix0 = 2 * ox0 - 1;
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+      const int i = tid + 256 * k;
+      const int hx = i % WX, r = i / WX, hy = r % WY, hz = r / WY;
+      const int iz = iz0 + hz, iy = iy0 + hy, ix = ix0 + hx;
+      const bool ok = i < N && (unsigned)iz < (unsigned)a.di && (unsigned)iy < (unsigned)a.hi && (unsigned)ix < (unsigned)a.wi;
+      xv_n[k] = ok ? x[(((long long)nb * a.di + iz) * a.hi + iy) * a.wi + ix] : 0.f;
     }
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int i = tid + 256 * k, h = i & 1, v = i >> 1;
+      const int oz = oz0 + (v >> 7), oy = oy0 + ((v >> 4) & 7), ox = ox0 + (v & 15);
+      gv_n[k] = (oz < a.do_ && oy < a.ho && ox < a.wo)
+                    ? *reinterpret_cast<const f32x4*>(dz + ((((long long)nb * a.do_ + oz) * a.ho + oy) * a.wo + ox) * 8 + 4 * h)
+                    : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+  };
+  auto store = [&]() {
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+      const int i = tid + 256 * k;
+      if (i >= N) break;
+      const int hx = i % WX, r = i / WX, hy = r % WY, hz = r / WY;
+      xs[hz * PS + hy * RS + hx] = xv_n[k];
+    }
+#pragma unroll
+    for (int k = 0; k < 2; ++k) *reinterpret_cast<f32x4*>(gs + (tid + 256 * k) * 4) = gv_n[k];
+  };
+  f32x2 acc[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) acc[j] = f32x2{0.f, 0.f};
+  const int t0 = blockIdx.x * a.tiles_per_block;
+  const int t1 = min(t0 + a.tiles_per_block, ntiles);
+  if (t0 < t1) load(t0);
+  for (int tile = t0; tile < t1; ++tile) {
+    __syncthreads();  // previous tile's LDS reads done
+    store();
     __syncthreads();
+    if (tile + 1 < t1) load(tile + 1);
+    // one wave per SIMD: unrolled so that several voxels' LDS reads are in flight at once
+#pragma unroll 8
     for (int v = vg * 64; v < vg * 64 + 64; ++v) {
       const int lz = v >> 7, ly = (v >> 4) & 7, lx = v & 15;
       const float xv = xs[(2 * lz + td) * PS + (2 * ly + th) * RS + 2 * lx + tw];
       const f32x4 g0 = *reinterpret_cast<const f32x4*>(gs + v * 8), g1 = *reinterpret_cast<const f32x4*>(gs + v * 8 + 4);
-#pragma unroll
-      for (int b = 0; b < 4; ++b) acc[b] = fmaf(xv, g0[b], acc[b]);
-#pragma unroll
-      for (int b = 0; b < 4; ++b) acc[4 + b] = fmaf(xv, g1[b], acc[4 + b]);
+      const f32x2 x2 = {xv, xv};
+      acc[0] += x2 * f32x2{g0[0], g0[1]};
+      acc[1] += x2 * f32x2{g0[2], g0[3]};
+      acc[2] += x2 * f32x2{g1[0], g1[1]};
+      acc[3] += x2 * f32x2{g1[2], g1[3]};
     }
   }
 #pragma unroll
-  for (int b = 0; b < 8; ++b) red[vg][b][t] = acc[b];
+  for (int b = 0; b < 8; ++b) red[vg][b][t] = acc[b >> 1][b & 1];
   __syncthreads();
   for (int i = tid; i < 512; i += 256) {
     const int b = i >> 6, tt = i & 63;
@@ -230,7 +289,7 @@ int c1_dgrad_launch(const cgan3d_conv_geom* g, const float* dz, const float* w, 
 int c1_wgrad_launch(const cgan3d_conv_geom* g, const float* x, const float* dz, float* dw, hipStream_t st) {
   C1Args a = c1_args(g);
   const int ntiles = a.n * a.tz * a.ty * a.tx;
-  a.tiles_per_block = ntiles >= 1024 ? 4 : (ntiles >= 512 ? 2 : 1);
+  a.tiles_per_block = std::max(1, std::min(8, ntiles / 256));  // <= ~256 blocks adding into dW
   ::cg::launch(c1_wgrad_kernel, dim3(ceil_div(ntiles, a.tiles_per_block)), dim3(256), 0, st, a, x, dz, dw, ntiles);
   return CGAN3D_OK;
 }

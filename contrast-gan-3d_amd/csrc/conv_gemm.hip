@@ -436,6 +436,17 @@ __global__ __launch_bounds__(256) void pack_weights_kernel(const float* __restri
 
 __global__ __launch_bounds__(256) void pack_multi_kernel(const cgan3d_pack_desc* __restrict__ descs) {
   const cgan3d_pack_desc d = descs[blockIdx.y];
+  if (d.format == 3) {  // conv_sk bf16 [b][tap][a]
+    __bf16* wp = reinterpret_cast<__bf16*>(d.wp);
+    const long long total = (long long)d.taps * d.cout * d.cin;
+    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long long)gridDim.x * blockDim.x) {
+      const int ai = (int)(i % d.cin);
+      const long long r = i / d.cin;
+      const int t = (int)(r % d.taps), b = (int)(r / d.taps);
+      wp[i] = (__bf16)d.w[ai * d.sa + b * d.sb + t];
+    }
+    return;
+  }
   if (d.format == 2) {  // halo bf16 [tap][b][a], granules of a swizzled by b
     __bf16* wp = reinterpret_cast<__bf16*>(d.wp);
     const long long total = (long long)d.taps * d.cout * d.cin;
@@ -499,12 +510,13 @@ using namespace cg;
 
 extern "C" int64_t cgan3d_packed_weight_floats(const cgan3d_conv_geom* g) {
   if (!g) return -1;
-  if (g->w_packed == 2) return ((int64_t)g->k * g->k * g->k * g->cin * g->cout + 1) / 2;  // bf16
+  if (g->w_packed == 2 || g->w_packed == 3) return ((int64_t)g->k * g->k * g->k * g->cin * g->cout + 1) / 2;  // bf16
   return (int64_t)g->k * g->k * g->k * g->cin * ((g->cout + 3) / 4 * 4);
 }
 
 extern "C" int cgan3d_pack_weights(const cgan3d_conv_geom* g, const float* w, float* wp, void* stream) {
   CG_CHECK_ARG(g && w && wp, "cgan3d_pack_weights: null pointer");
+  CG_CHECK_ARG(g->w_packed != 3, "cgan3d_pack_weights: format 3 is packed by cgan3d_pack_weights_multi");
   if (g->w_packed == 2) {
     CG_CHECK_ARG(halo_format_ok(g), "cgan3d_pack_weights: geometry not halo-eligible");
     halo_pack(g, w, wp, (hipStream_t)stream);
@@ -529,6 +541,13 @@ extern "C" int cgan3d_pack_weights_multi(const cgan3d_pack_desc* descs, int32_t 
 }
 
 extern "C" int32_t cgan3d_halo_eligible(const cgan3d_conv_geom* g) { return g && halo_format_ok(g) ? 1 : 0; }
+
+extern "C" int32_t cgan3d_packed_format(const cgan3d_conv_geom* g) {
+  if (!g) return 0;
+  if (sk_format_ok(g)) return 3;
+  if (g->prec == CGAN3D_PREC_BF16 && halo_format_ok(g)) return 2;
+  return 1;
+}
 
 extern "C" int cgan3d_set_tuning(int32_t key, int32_t value) {
   if (key == 0) { g_small_tile_below = value; return CGAN3D_OK; }

@@ -1,0 +1,246 @@
+// Small-grid convolutions on bf16 MFMA with the K dimension split over the waves: the critic's
+// middle layers (model/discriminator.py:42-68, Conv3d k4 s2 p1, 8 -> 16 -> 32 -> 64 channels) in
+// their forward, input-grad (ConvTranspose-shaped, stride-2 parity classes) and gradient-penalty
+// forward-mode roles.  At 64^3 patches these layers have 768 - 49k output voxels but 512 - 2048
+// reduction terms each, so a block per 64-voxel tile walking all taps in series (conv_halo,
+// conv_gemm) leaves most CUs idle and every block latency-bound.  Here:
+//
+//  * M tile = 16 output voxels of one parity class; K = class taps x cin, ordered (tap, channel);
+//  * MT = 1: the four waves take K-steps w, w + 4, ... of the same 16 x (16 NT) tile and are summed
+//    once through LDS (4x the blocks of a 64-row tiling); MT = 4: each wave its own 16 rows, all K
+//    (short K, many rows);
+//  * operands straight from L2, no LDS staging: A = 8 consecutive K = 8 channels of one gathered
+//    voxel (two float4, converted to bf16), B = packed weights format 3, bf16 [b][tap][a], one
+//    16-byte load per fragment; the next K-step's loads are in flight during the current MFMAs;
+//  * epilogue: bias / activation / LeakyReLU-mask / residual, per-block BatchNorm statistics
+//    (sum, M2, count) for the BatchNorm critic of the weight-clip configuration.
+#include "common.h"
+
+namespace cg {
+
+typedef __bf16 bf16x8_k __attribute__((ext_vector_type(8)));
+
+struct SkArgs {
+  int n, di, hi, wi, do_, ho, wo, cin, cout, k, s, p, transposed;
+  int nclass, cd, ch, cw;  // parity-class grid (transposed stride 2) or the output grid
+  int mblocks;             // blocks per class
+  int ktot;                // k^3 * cin: packed weight row length
+};
+
+__device__ __forceinline__ void sk_class(int r, int k, int s, int p, int transposed, int* f, int* st, int* cnt) {
+  if (transposed) {
+    *f = (r + p) % s; *st = s; *cnt = *f < k ? (k - *f + s - 1) / s : 0;
+  } else {
+    *f = 0; *st = 1; *cnt = k;
+  }
+}
+
+template <int MT, int NT>
+__global__ __launch_bounds__(256) void conv_sk_kernel(SkArgs a, const float* __restrict__ x,
+                                                      const __bf16* __restrict__ wp, float* y, Epi ep) {
+  __shared__ int tq[3][64];
+  __shared__ int tlin[64];
+  __shared__ int rowo[16 * MT];
+  __shared__ int rowb[3][16 * MT];  // gathered-grid base coordinate per row (gathered = base + tq)
+  __shared__ int rown[16 * MT];
+  __shared__ __attribute__((aligned(16))) f32x4 red[3][NT][64];
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int cls = blockIdx.x / a.mblocks, mb = blockIdx.x - cls * a.mblocks;
+  const int s = a.s;
+  int r3[3] = {0, 0, 0};
+  if (a.transposed) { r3[0] = cls / (s * s); r3[1] = (cls / s) % s; r3[2] = cls % s; }
+  int fz, sz, nz, fy, sy, ny, fx, sx, nx;
+  sk_class(r3[0], a.k, s, a.p, a.transposed, &fz, &sz, &nz);
+  sk_class(r3[1], a.k, s, a.p, a.transposed, &fy, &sy, &ny);
+  sk_class(r3[2], a.k, s, a.p, a.transposed, &fx, &sx, &nx);
+  const int ntap = nz * ny * nx;
+  if (tid < ntap) {
+    const int mw = tid % nx, mh = (tid / nx) % ny, md = tid / (nx * ny);
+    const int t0 = fz + sz * md, t1 = fy + sy * mh, t2 = fx + sx * mw;
+    if (a.transposed) {  // o = j*s + r, i = j + (r + p - t)/s
+      tq[0][tid] = (r3[0] + a.p - t0) / s; tq[1][tid] = (r3[1] + a.p - t1) / s; tq[2][tid] = (r3[2] + a.p - t2) / s;
+    } else {
+      tq[0][tid] = t0; tq[1][tid] = t1; tq[2][tid] = t2;
+    }
+    tlin[tid] = (t0 * a.k + t1) * a.k + t2;
+  }
+  if (tid < 16 * MT) {
+    const long long m = (long long)mb * 16 * MT + tid;
+    const long long cvox = (long long)a.n * a.cd * a.ch * a.cw;
+    int jx = (int)(m % a.cw);
+    long long q = m / a.cw;
+    const int jy = (int)(q % a.ch);
+    q /= a.ch;
+    const int jz = (int)(q % a.cd), nb = (int)(q / a.cd);
+    const bool ok = m < cvox;
+    int od = jz, oh = jy, ow = jx;
+    if (a.transposed) {
+      od = jz * s + r3[0]; oh = jy * s + r3[1]; ow = jx * s + r3[2];
+      rowb[0][tid] = jz; rowb[1][tid] = jy; rowb[2][tid] = jx;
+    } else {
+      rowb[0][tid] = jz * s - a.p; rowb[1][tid] = jy * s - a.p; rowb[2][tid] = jx * s - a.p;
+    }
+    rowo[tid] = ok ? ((nb * a.do_ + od) * a.ho + oh) * a.wo + ow : -1;
+    rown[tid] = nb;
+  }
+  __syncthreads();
+
+  const int g = lane >> 4, r16 = lane & 15;
+  const int mt = MT == 1 ? 0 : wave;
+  const int row = mt * 16 + r16;
+  const bool rok = rowo[row] >= 0;
+  const int bz = rowb[0][row], by = rowb[1][row], bx = rowb[2][row], nb = rown[row];
+  const int KS = ntap * a.cin / 32;
+  const int ks0 = MT == 1 ? wave : 0, kstep = MT == 1 ? 4 : 1;
+
+  f32x4 acc[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  f32x4 xa0, xa1;        // next A: 8 fp32 channels
+  bf16x8_k bb[NT];       // next B fragments
+  auto load = [&](int ks) {
+    const int k0 = ks * 32 + 8 * g;
+    const int j = k0 / a.cin, a0 = k0 - j * a.cin;
+    const int iz = bz + tq[0][j], iy = by + tq[1][j], ix = bx + tq[2][j];
+    const bool ok = rok && (unsigned)iz < (unsigned)a.di && (unsigned)iy < (unsigned)a.hi && (unsigned)ix < (unsigned)a.wi;
+    const float* src = x + (ok ? (((long long)(nb * a.di + iz) * a.hi + iy) * a.wi + ix) * a.cin + a0 : 0);
+    xa0 = ok ? *reinterpret_cast<const f32x4*>(src) : f32x4{0.f, 0.f, 0.f, 0.f};
+    xa1 = ok ? *reinterpret_cast<const f32x4*>(src + 4) : f32x4{0.f, 0.f, 0.f, 0.f};
+    const int wk = tlin[j] * a.cin + a0;
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      const int col = t * 16 + r16;
+      bb[t] = col < a.cout ? *reinterpret_cast<const bf16x8_k*>(wp + (long long)col * a.ktot + wk)
+                           : bf16x8_k{0, 0, 0, 0, 0, 0, 0, 0};
+    }
+  };
+  if (ks0 < KS) load(ks0);
+  for (int ks = ks0; ks < KS; ks += kstep) {
+    bf16x8_k av;
+    av[0] = (__bf16)xa0[0]; av[1] = (__bf16)xa0[1]; av[2] = (__bf16)xa0[2]; av[3] = (__bf16)xa0[3];
+    av[4] = (__bf16)xa1[0]; av[5] = (__bf16)xa1[1]; av[6] = (__bf16)xa1[2]; av[7] = (__bf16)xa1[3];
+    bf16x8_k bv[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) bv[t] = bb[t];
+    if (ks + kstep < KS) load(ks + kstep);
+#pragma unroll
+    for (int t = 0; t < NT; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, bv[t], acc[t], 0, 0, 0);
+  }
+  if (MT == 1) {  // combine the waves' K partials in wave 0
+    if (wave > 0) {
+#pragma unroll
+      for (int t = 0; t < NT; ++t) red[wave - 1][t][lane] = acc[t];
+    }
+    __syncthreads();
+    if (wave > 0) return;
+#pragma unroll
+    for (int t = 0; t < NT; ++t) acc[t] += red[0][t][lane] + red[1][t][lane] + red[2][t][lane];
+  }
+  // epilogue: lane holds rows mt*16 + 4g + jj, channel t*16 + r16
+  float vals[NT][4];
+  int ro[4];
+#pragma unroll
+  for (int jj = 0; jj < 4; ++jj) ro[jj] = rowo[mt * 16 + 4 * g + jj];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    const int c = t * 16 + r16;
+    const bool cv = c < a.cout;
+    const float b = (ep.bias && cv) ? ep.bias[c] : 0.f;
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj) {
+      float v = acc[t][jj] + b;
+      if (ep.act == CGAN3D_ACT_RELU) v = fmaxf(v, 0.f);
+      else if (ep.act == CGAN3D_ACT_LRELU) v = v > 0.f ? v : v * ep.slope;
+      const bool ok = cv && ro[jj] >= 0;
+      if (ok) {
+        const long long o = (long long)ro[jj] * a.cout + c;
+        if (ep.mask_src) v = ep.mask_src[o] > 0.f ? v : v * ep.slope;
+        if (ep.residual) v += ep.residual[o];
+        y[o] = v;
+      }
+      vals[t][jj] = ok ? v : 0.f;
+    }
+  }
+  if (ep.stats) {  // block-major (sum, M2 about the block mean, count), MT == 1: this wave's 16 rows
+    int cnt = 0;
+    for (int r = 0; r < 16; ++r) cnt += rowo[mt * 16 + r] >= 0;
+    const long long sb = (long long)blockIdx.x * (2 * a.cout + 1);
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      const int c = t * 16 + r16;
+      float S = vals[t][0] + vals[t][1] + vals[t][2] + vals[t][3];
+      S += __shfl_xor(S, 16, 64);
+      S += __shfl_xor(S, 32, 64);
+      const float mean = cnt ? S / cnt : 0.f;
+      float q = 0.f;
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj) {
+        const float d = ro[jj] >= 0 ? vals[t][jj] - mean : 0.f;
+        q += d * d;
+      }
+      q += __shfl_xor(q, 16, 64);
+      q += __shfl_xor(q, 32, 64);
+      if (g == 0 && c < a.cout) {
+        ep.stats[sb + c] = S;
+        ep.stats[sb + a.cout + c] = q;
+      }
+    }
+    if (lane == 0) ep.stats[sb + 2 * a.cout] = (float)cnt;
+  }
+}
+
+// geometry (ignoring the weight format): the critic's k4 convs, bf16
+bool sk_format_ok(const cgan3d_conv_geom* g) {
+  if (g->prec != CGAN3D_PREC_BF16 || g->reflect || g->k != 4 || g->cin % 8 || g->cout % 8 || g->cout > 64) return false;
+  if (g->transposed && g->stride > 1 && (g->do_ % g->stride || g->ho % g->stride || g->wo % g->stride)) return false;
+  // every parity class's K (taps x cin) a multiple of 32
+  const int kd = g->transposed ? (g->k + g->stride - 1) / g->stride : g->k;  // taps per dim (k % s == 0 here)
+  if (g->transposed && g->k % g->stride) return false;
+  return (kd * kd * kd * g->cin) % 32 == 0;
+}
+
+bool sk_ok(const cgan3d_conv_geom* g) { return g->w_packed == 3 && sk_format_ok(g); }
+
+static SkArgs sk_args(const cgan3d_conv_geom* g, int* mt) {
+  SkArgs a;
+  a.n = g->n; a.di = g->di; a.hi = g->hi; a.wi = g->wi; a.do_ = g->do_; a.ho = g->ho; a.wo = g->wo;
+  a.cin = g->cin; a.cout = g->cout; a.k = g->k; a.s = g->stride; a.p = g->pad; a.transposed = g->transposed;
+  if (g->transposed && g->stride > 1) {
+    a.nclass = g->stride * g->stride * g->stride;
+    a.cd = g->do_ / g->stride; a.ch = g->ho / g->stride; a.cw = g->wo / g->stride;
+  } else {
+    a.nclass = 1; a.cd = g->do_; a.ch = g->ho; a.cw = g->wo;
+  }
+  const int kd = g->transposed ? g->k / g->stride : g->k;
+  const int ks = kd * kd * kd * g->cin / 32;
+  *mt = ks >= 8 ? 1 : 4;  // long K: split over the waves; short K: one 16-row tile per wave
+  const long long cvox = (long long)a.n * a.cd * a.ch * a.cw;
+  a.mblocks = (int)((cvox + 16 * *mt - 1) / (16 * *mt));
+  a.ktot = g->k * g->k * g->k * g->cin;
+  return a;
+}
+
+long long sk_blocks(const cgan3d_conv_geom* g) {
+  int mt;
+  SkArgs a = sk_args(g, &mt);
+  return (long long)a.nclass * a.mblocks;
+}
+
+int sk_launch(const cgan3d_conv_geom* g, const float* x, const __bf16* wp, float* y, const Epi& e, hipStream_t st) {
+  CG_CHECK_ARG(!e.out2 && !e.minuend && !e.bn_mode, "conv_sk: no out2 / BatchNorm-slab epilogue");
+  int mt;
+  SkArgs a = sk_args(g, &mt);
+  CG_CHECK_ARG(!e.stats || mt == 1, "conv_sk: statistics epilogue only on the K-split tiling");
+  const int nt = (g->cout + 15) / 16;
+  const dim3 grid((unsigned)(a.nclass * a.mblocks));
+#define CG_SK(M, N) ::cg::launch((conv_sk_kernel<M, N>), grid, dim3(256), 0, st, a, x, wp, y, e)
+  if (mt == 1) {
+    if (nt == 1) CG_SK(1, 1); else if (nt == 2) CG_SK(1, 2); else if (nt == 3) CG_SK(1, 3); else CG_SK(1, 4);
+  } else {
+    if (nt == 1) CG_SK(4, 1); else if (nt == 2) CG_SK(4, 2); else if (nt == 3) CG_SK(4, 3); else CG_SK(4, 4);
+  }
+#undef CG_SK
+  return CGAN3D_OK;
+}
+
+}  // namespace cg

@@ -53,7 +53,9 @@ typedef struct cgan3d_conv_geom {
   int32_t w_packed;  /* 1: w is cgan3d_pack_weights() output [tap][a][b] f32, b contiguous;
                       * 2: halo format, bf16 [tap][b][a] with 16-byte granules of a XOR-swizzled
                       *    by (b mod a/8) — prec BF16, cin 32|64, cout%16==0, no reflect, k<=4,
-                      *    stride<=2 (cgan3d_halo_eligible) */
+                      *    stride<=2 (cgan3d_halo_eligible);
+                      * 3: small-grid K-split format, bf16 [b][tap][a] — prec BF16, k 4, cin%8==0,
+                      *    cout%8==0 (the critic's middle layers; cgan3d_packed_format) */
   int32_t prec;      /* CGAN3D_PREC_F32 (exact f32 MFMA) or CGAN3D_PREC_BF16 (bf16 MFMA, f32 accumulate) */
 } cgan3d_conv_geom;
 
@@ -115,6 +117,8 @@ int64_t cgan3d_conv3d_stats_floats(const cgan3d_conv_geom* g);
 int64_t cgan3d_packed_weight_floats(const cgan3d_conv_geom* g);
 /* 1 when the geometry (ignoring w_packed) can run the halo-tiled bf16 kernel (w_packed = 2). */
 int32_t cgan3d_halo_eligible(const cgan3d_conv_geom* g);
+/* The packed weight format the fastest kernel for this geometry reads (3, 2 or 1; see w_packed). */
+int32_t cgan3d_packed_format(const cgan3d_conv_geom* g);
 int cgan3d_pack_weights(const cgan3d_conv_geom* g, const float* w, float* wp, void* stream);
 /* Many packs in one launch: `descs` is a DEVICE array of n descriptors (built once; the pointers
  * are stable), `max_total` the largest element count (taps*cin*ldb or taps*cin*cout) among them. */
@@ -123,7 +127,8 @@ typedef struct cgan3d_pack_desc {
   float* wp;
   int64_t sa, sb;
   int32_t taps, cin, cout, ldb;
-  int32_t format;  /* w_packed value: 1 f32 [tap][a][b] (ldb-padded), 2 halo bf16 [tap][b][a] */
+  int32_t format;  /* w_packed value: 1 f32 [tap][a][b] (ldb-padded), 2 halo bf16 [tap][b][a],
+                    * 3 K-split bf16 [b][tap][a] */
   int32_t reserved;
 } cgan3d_pack_desc;
 int cgan3d_pack_weights_multi(const cgan3d_pack_desc* descs, int32_t n, int64_t max_total, void* stream);

@@ -189,7 +189,8 @@ def test_conv_gemm_packed(cin, cout, k, s, p, sp, prec, monkeypatch):
     ps = ops.PackSet(torch.device("cuda"))
     gf, wf = ps.add(ops.conv_fwd_geom(n, din, dout, cin, cout, k, s, p), wd, pc)
     ps.pack()
-    assert gf.w_packed == 1
+    # the critic's single-channel first layer reads torch-layout weights (conv_c1.hip)
+    assert gf.w_packed == (0 if (cin == 1 and k == 4) else 1)
     yo = torch.empty(n, *dout, cout, device="cuda")
     ops.conv(gf, _cl(x), wf, yo)
     assert_close(_ncdhw(yo).numpy(), y.numpy(), tol, f"{prec} fwd")
@@ -272,7 +273,8 @@ def test_conv_halo_bf16(transposed, cin, cout, k, s, p, sp):
     gf, wf = ps.add(gf0, wd, L.PREC_BF16)
     gd, wdp = ps.add(gd0, wd, L.PREC_BF16)
     ps.pack()
-    assert gf.w_packed == 2 and gd.w_packed == 2, "expected the halo kernel for both launches"
+    # the critic's k4 geometries go to the K-split kernel (format 3, conv_sk.hip), the rest to the halo kernel
+    assert gf.w_packed in (2, 3) and gd.w_packed in (2, 3), "expected the halo / K-split kernels"
     yo = torch.empty(n, *dout, cout, device="cuda")
     stats = torch.empty(ops.stats_floats(gf), device="cuda")
     ops.conv(gf, _cl(x), wf, yo, ops.epilogue(act=L.ACT_RELU, residual=_cl(res), stats=stats))
@@ -485,3 +487,63 @@ def test_conv_s2_bf16(role, fine):
     want = torch.cat([gg.sum(0), (gg * (zz - mid[:cout]) * mid[cout:]).sum(0)])
     got = part2.double().cpu().view(2 * cout, slots).sum(1)
     assert_close(got.numpy(), want.numpy(), 1e-4, f"{role} mode-2 slab")
+
+
+SK_CASES = [
+    # cin, cout, spatial (module input): the critic's middle layers, k4 s2 p1 (conv_sk.hip)
+    (8, 16, (16, 16, 16)),
+    (16, 32, (8, 8, 8)),
+    (32, 64, (8, 8, 8)),
+    (8, 16, (10, 12, 14)),  # partial 16-row tiles
+]
+
+
+@pytest.mark.parametrize("cin,cout,sp", SK_CASES)
+def test_conv_sk_bf16(cin, cout, sp):
+    """K-split small-grid bf16 kernel in the critic's three roles, against torch float64 within
+    2e-2: forward with bias + LeakyReLU + BatchNorm statistics (weight-clip critic), the gradient
+    penalty's forward-mode launch (mask = the output's previous contents, in place) and the
+    input-grad with the layer below's LeakyReLU mask (discriminator.py:24-80)."""
+    from cgan3d_amd import ops, _lib as L
+    k, s, p, slope = 4, 2, 1, 0.2
+    g = torch.Generator().manual_seed(21 + cin + cout + sp[0])
+    n = 3
+    x = torch.randn(n, cin, *sp, generator=g, dtype=torch.float64)
+    w = torch.randn(cout, cin, k, k, k, generator=g, dtype=torch.float64) / np.sqrt(cin * k**3)
+    b = torch.randn(cout, generator=g, dtype=torch.float64) * 0.1
+    z = F.conv3d(x, w, b, stride=s, padding=p)
+    yref = F.leaky_relu(z, slope)
+    din, dout = tuple(sp), tuple(z.shape[2:])
+    below = torch.randn(x.shape, generator=g, dtype=torch.float64)  # activations of the layer below
+    gy = torch.randn(z.shape, generator=g, dtype=torch.float64)
+    dx = torch.nn.grad.conv3d_input(x.shape, w, gy, stride=s, padding=p)
+    dxref = torch.where(below > 0, dx, dx * slope)
+    wd = w.float().cuda()
+    ps = ops.PackSet(torch.device("cuda"))
+    gf, wf = ps.add(ops.conv_fwd_geom(n, din, dout, cin, cout, k, s, p), wd, L.PREC_BF16)
+    gd, wdp = ps.add(ops.conv_dgrad_geom(n, din, dout, cin, cout, k, s, p), wd, L.PREC_BF16)
+    ps.pack()
+    assert gf.w_packed == 3 and gd.w_packed == 3
+    yo = torch.empty(n, *dout, cout, device="cuda")
+    stats = torch.empty(ops.stats_floats(gf), device="cuda")
+    ops.conv(gf, _cl(x), wf, yo, ops.epilogue(bias=b.float().cuda(), act=L.ACT_LRELU, slope=slope, stats=stats))
+    assert_close(_ncdhw(yo).numpy(), yref.numpy(), 2e-2, "sk fwd")
+    st = stats.double().cpu().view(-1, 2 * cout + 1)
+    cnt = st[:, 2 * cout]
+    tot = cnt.sum()
+    mean = st[:, :cout].sum(0) / tot
+    bm = st[:, :cout] / cnt.clamp(min=1)[:, None]
+    m2 = st[:, cout:2 * cout].sum(0) + (cnt[:, None] * (bm - mean) ** 2).sum(0)
+    yk = yo.double().cpu().view(-1, cout)
+    assert int(tot) == yk.shape[0]
+    assert_close(mean.numpy(), yk.mean(0).numpy(), 1e-4, "sk stats mean")
+    assert_close((m2 / tot).numpy(), yk.var(0, unbiased=False).numpy(), 1e-4, "sk stats var")
+    # gradient-penalty forward mode: nu = mask(y > 0) * conv(x) without bias, written over y
+    nu = yo.clone()
+    ops.conv(gf, _cl(x), wf, nu, ops.epilogue(mask_src=nu, slope=slope))
+    zf = F.conv3d(x, w, stride=s, padding=p)
+    nuref = torch.where(_ncdhw(yo) > 0, zf, zf * slope)
+    assert_close(_ncdhw(nu).numpy(), nuref.numpy(), 2e-2, "sk forward-mode")
+    dxo = torch.empty(n, *din, cin, device="cuda")
+    ops.conv(gd, _cl(gy), wdp, dxo, ops.epilogue(mask_src=_cl(below), slope=slope))
+    assert_close(_ncdhw(dxo).numpy(), dxref.numpy(), 2e-2, "sk dgrad")
