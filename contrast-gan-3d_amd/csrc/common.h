@@ -174,6 +174,11 @@ int c1_dgrad_launch(const cgan3d_conv_geom* g, const float* dz, const float* w, 
 int c1_wgrad_launch(const cgan3d_conv_geom* g, const float* x, const float* dz, float* dw, hipStream_t st);
 long long wgrad_k3_ws_floats(const cgan3d_conv_geom* g);
 void wgrad_k3_set_chunks(int v);
+bool wgrad_s2_ok(const cgan3d_conv_geom* g);
+long long wgrad_s2_ws_floats(const cgan3d_conv_geom* g);
+void wgrad_s2_set_blocks(int v);
+int wgrad_s2_launch(const cgan3d_conv_geom* g, const float* gathered, const float* aligned, float* dw, int accumulate,
+                    float* ws, hipStream_t st);
 int wgrad_k3_launch(const cgan3d_conv_geom* g, const float* gathered, const float* aligned, float* dw, int accumulate,
                     float* ws, hipStream_t st);
 int wgrad_c1_launch(const cgan3d_conv_geom* g, const float* gathered, const float* aligned, float* dw, hipStream_t st);

@@ -512,7 +512,7 @@ static long long wgrad_vpb(long long V, int gx_blocks) {
 extern "C" int64_t cgan3d_conv3d_wgrad_ws_floats(const cgan3d_conv_geom* g) {
   if (!g) return -1;
   return std::max<int64_t>(std::max<int64_t>((int64_t)g->k * g->k * g->k * g->cin * g->cout, k7_wgrad_ws_floats(g)),
-                           wgrad_k3_ws_floats(g));
+                           std::max<int64_t>(wgrad_k3_ws_floats(g), wgrad_s2_ws_floats(g)));
 }
 
 extern "C" int cgan3d_conv3d_wgrad(const cgan3d_conv_geom* g, const float* gathered, const float* aligned, float* dw,
@@ -556,6 +556,12 @@ extern "C" int cgan3d_conv3d_wgrad(const cgan3d_conv_geom* g, const float* gathe
     }
     wgrad_c1_launch(g, gathered, aligned, dw, s);
     CG_LAUNCH_CHECK("conv_wgrad_c1_kernel");
+    return CGAN3D_OK;
+  }
+  if (wgrad_s2_ok(g)) {  // stride-2 16 <-> 32 levels: per-block partials + reduce, no memset
+    int rc = wgrad_s2_launch(g, gathered, aligned, dw, accumulate, ws, s);
+    if (rc) return rc;
+    CG_LAUNCH_CHECK("wgrad_s2_kernel");
     return CGAN3D_OK;
   }
   if (wgrad_k3_ok(g)) {  // ResNet-block shape: per-block partials + reduce, no memset

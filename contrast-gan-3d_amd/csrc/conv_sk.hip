@@ -96,35 +96,47 @@ __global__ __launch_bounds__(256) void conv_sk_kernel(SkArgs a, const float* __r
   f32x4 acc[NT];
 #pragma unroll
   for (int t = 0; t < NT; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-  f32x4 xa0, xa1;        // next A: 8 fp32 channels
-  bf16x8_k bb[NT];       // next B fragments
-  auto load = [&](int ks) {
+  // PF K-steps of operands in flight per wave (a ring of register slots; slot indices are
+  // compile-time after unrolling): the chain is latency-bound, not MFMA-bound
+  constexpr int PF = 4;
+  f32x4 xa0[PF], xa1[PF];  // A: 8 fp32 channels of one gathered voxel
+  bf16x8_k bb[PF][NT];     // B fragments
+  auto load = [&](int ks, int sl) {
     const int k0 = ks * 32 + 8 * g;
     const int j = k0 / a.cin, a0 = k0 - j * a.cin;
     const int iz = bz + tq[0][j], iy = by + tq[1][j], ix = bx + tq[2][j];
     const bool ok = rok && (unsigned)iz < (unsigned)a.di && (unsigned)iy < (unsigned)a.hi && (unsigned)ix < (unsigned)a.wi;
     const float* src = x + (ok ? (((long long)(nb * a.di + iz) * a.hi + iy) * a.wi + ix) * a.cin + a0 : 0);
-    xa0 = ok ? *reinterpret_cast<const f32x4*>(src) : f32x4{0.f, 0.f, 0.f, 0.f};
-    xa1 = ok ? *reinterpret_cast<const f32x4*>(src + 4) : f32x4{0.f, 0.f, 0.f, 0.f};
+    xa0[sl] = ok ? *reinterpret_cast<const f32x4*>(src) : f32x4{0.f, 0.f, 0.f, 0.f};
+    xa1[sl] = ok ? *reinterpret_cast<const f32x4*>(src + 4) : f32x4{0.f, 0.f, 0.f, 0.f};
     const int wk = tlin[j] * a.cin + a0;
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
       const int col = t * 16 + r16;
-      bb[t] = col < a.cout ? *reinterpret_cast<const bf16x8_k*>(wp + (long long)col * a.ktot + wk)
-                           : bf16x8_k{0, 0, 0, 0, 0, 0, 0, 0};
+      bb[sl][t] = col < a.cout ? *reinterpret_cast<const bf16x8_k*>(wp + (long long)col * a.ktot + wk)
+                               : bf16x8_k{0, 0, 0, 0, 0, 0, 0, 0};
     }
   };
-  if (ks0 < KS) load(ks0);
-  for (int ks = ks0; ks < KS; ks += kstep) {
-    bf16x8_k av;
-    av[0] = (__bf16)xa0[0]; av[1] = (__bf16)xa0[1]; av[2] = (__bf16)xa0[2]; av[3] = (__bf16)xa0[3];
-    av[4] = (__bf16)xa1[0]; av[5] = (__bf16)xa1[1]; av[6] = (__bf16)xa1[2]; av[7] = (__bf16)xa1[3];
-    bf16x8_k bv[NT];
+  const int nk = ks0 < KS ? (KS - ks0 + kstep - 1) / kstep : 0;  // this wave's K-steps
 #pragma unroll
-    for (int t = 0; t < NT; ++t) bv[t] = bb[t];
-    if (ks + kstep < KS) load(ks + kstep);
+  for (int i = 0; i < PF; ++i)
+    if (i < nk) load(ks0 + i * kstep, i);
+  for (int q0 = 0; q0 < nk; q0 += PF) {
 #pragma unroll
-    for (int t = 0; t < NT; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, bv[t], acc[t], 0, 0, 0);
+    for (int i = 0; i < PF; ++i) {
+      const int q = q0 + i;
+      if (q < nk) {
+        bf16x8_k av;
+        av[0] = (__bf16)xa0[i][0]; av[1] = (__bf16)xa0[i][1]; av[2] = (__bf16)xa0[i][2]; av[3] = (__bf16)xa0[i][3];
+        av[4] = (__bf16)xa1[i][0]; av[5] = (__bf16)xa1[i][1]; av[6] = (__bf16)xa1[i][2]; av[7] = (__bf16)xa1[i][3];
+        bf16x8_k bv[NT];
+#pragma unroll
+        for (int t = 0; t < NT; ++t) bv[t] = bb[i][t];
+        if (q + PF < nk) load(ks0 + (q + PF) * kstep, i);
+#pragma unroll
+        for (int t = 0; t < NT; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, bv[t], acc[t], 0, 0, 0);
+      }
+    }
   }
   if (MT == 1) {  // combine the waves' K partials in wave 0
     if (wave > 0) {

@@ -433,15 +433,16 @@ __global__ __launch_bounds__(512, 2) void wgrad_k3_kernel(Wk3Args a, const float
     }
 }
 
-// dW[b * w_sb + a * w_sa + t] (+)= sum_p ws[p][t][b][a]; block = (b, 16 input channels)
-__global__ __launch_bounds__(448) void wgrad_k3_reduce_kernel(const float* __restrict__ ws, int P, float* dw,
-                                                              long long w_sa, long long w_sb, int accumulate) {
+// dW[b * w_sb + a * w_sa + t] (+)= sum_p ws[p][t][b][a] (27 taps, A gathered x B aligned channels);
+// block = (b, 16 gathered channels)
+__global__ __launch_bounds__(448) void wgrad_k3_reduce_kernel(const float* __restrict__ ws, int P, int A, int B,
+                                                              float* dw, long long w_sa, long long w_sb, int accumulate) {
   __shared__ float tile[16][28];
   const int b = blockIdx.x, a0 = blockIdx.y * 16, tid = threadIdx.x;
   if (tid < 432) {
     const int t = tid >> 4, al = tid & 15;
-    const float* src = ws + ((long long)t * 64 + b) * 64 + a0 + al;
-    constexpr long long PS = 27 * 4096;
+    const float* src = ws + ((long long)t * B + b) * A + a0 + al;
+    const long long PS = 27LL * A * B;
     float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};  // 8 independent loads in flight
     int p = 0;
     for (; p + 8 <= P; p += 8)
@@ -455,6 +456,115 @@ __global__ __launch_bounds__(448) void wgrad_k3_reduce_kernel(const float* __res
     const int al = tid / 27, t = tid - al * 27;
     float* o = dw + (long long)b * w_sb + (long long)(a0 + al) * w_sa + t;
     *o = accumulate ? *o + tile[al][t] : tile[al][t];
+  }
+}
+
+// ---- stride-2 weight gradient between the generator's 16- and 32-channel levels (bf16 MFMA):
+// the first downsampling Conv3d 16 -> 32 (generator.py:40-47) and, operands swapped, the last
+// ConvTranspose3d 32 -> 16 (generator.py:61-77; its output-grad is the gathered operand), both
+// dW[t][a][b] = sum_o X(2o - 1 + t)[a] * dZ(o)[b] with X 16 channels on the 2x grid.  At 64^3 the
+// gathered operand is 67 MB: a block stages a slab (one output plane, 4 rows, 32 columns) of both
+// operands once — X's 3 x 9 x 65 window serves all 27 taps — and reads MFMA fragments with
+// ds_read_b64_tr_b16 (any tap shift is a row address).  Layouts: X rows of 32 B (16 channels),
+// one pad voxel per 16 along x (the two 16-lane groups of a read 17 voxels apart: disjoint banks);
+// dZ rows of 64 B with the 16-channel halves swapped on odd 8-column groups.  Waves: tap group
+// (w & 3, taps t = w & 3 + 4i) x output-channel tile (w >> 2).  The next slab's loads are in
+// registers during the current slab's MFMAs.  Per-block partials -> wgrad_k3_reduce_kernel.
+namespace ws2 {
+constexpr int XW = 65, XRS = 70, XPS = 9 * XRS;  // window columns; padded row / plane strides (voxels)
+constexpr int XBYTES = 3 * XPS * 32, ZBYTES = 4 * 32 * 64;
+constexpr int NX = 3 * 9 * XW * 4, NXT = (NX + 511) / 512;  // X float4 items per slab, per thread
+__device__ __forceinline__ int xcol(int c) { return c + (c >> 4); }
+}  // namespace ws2
+
+struct Ws2Args {
+  int n, di, hi, wi, do_, ho, wo;
+  int slabs, spb;  // slabs in all, per block
+};
+
+__global__ __launch_bounds__(512) void wgrad_s2_kernel(Ws2Args a, const float* __restrict__ x,
+                                                       const float* __restrict__ dz, float* __restrict__ ws) {
+  using namespace ws2;
+  __shared__ __attribute__((aligned(16))) unsigned char smem[XBYTES + ZBYTES];
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int tg = wave & 3, bt = wave >> 2;
+  const int p = blockIdx.x;
+  const int s0 = p * a.spb, s1 = min(s0 + a.spb, a.slabs);
+  const int yg_n = a.ho >> 2, xc_n = a.wo >> 5;
+  f32x4 rx[NXT], rz[2];
+  auto load = [&](int sl) {
+    const int xc = sl % xc_n, q1 = sl / xc_n, yg = q1 % yg_n, zq = q1 / yg_n;  // zq = nb * do + oz
+    const int oz = zq % a.do_, nb = zq / a.do_;
+    const int iz0 = 2 * oz - 1, iy0 = 8 * yg - 1, ix0 = 64 * xc - 1;
+#pragma unroll
+    for (int k = 0; k < NXT; ++k) {
+      const int i = tid + 512 * k, q4 = i & 3, v = i >> 2;
+      const int c = v % XW, r = (v / XW) % 9, pl = v / (9 * XW);
+      const int iz = iz0 + pl, iy = iy0 + r, ix = ix0 + c;
+      const bool ok = i < NX && (unsigned)iz < (unsigned)a.di && (unsigned)iy < (unsigned)a.hi && (unsigned)ix < (unsigned)a.wi;
+      rx[k] = ok ? *reinterpret_cast<const f32x4*>(x + ((((long long)nb * a.di + iz) * a.hi + iy) * a.wi + ix) * 16 + 4 * q4)
+                 : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int i = tid + 512 * k, q8 = i & 7, v = i >> 3;  // v = u * 32 + ox
+      const int oy = 4 * yg + (v >> 5), ox = 32 * xc + (v & 31);
+      rz[k] = *reinterpret_cast<const f32x4*>(dz + ((((long long)nb * a.do_ + oz) * a.ho + oy) * a.wo + ox) * 32 + 4 * q8);
+    }
+  };
+  auto store = [&]() {
+#pragma unroll
+    for (int k = 0; k < NXT; ++k) {
+      const int i = tid + 512 * k, q4 = i & 3, v = i >> 2;
+      if (i >= NX) break;
+      const int c = v % XW, r = (v / XW) % 9, pl = v / (9 * XW);
+      bf16x4_w h;
+      h[0] = (__bf16)rx[k][0]; h[1] = (__bf16)rx[k][1]; h[2] = (__bf16)rx[k][2]; h[3] = (__bf16)rx[k][3];
+      *reinterpret_cast<bf16x4_w*>(smem + (pl * XPS + r * XRS + xcol(c)) * 32 + q4 * 8) = h;
+    }
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int i = tid + 512 * k, q8 = i & 7, v = i >> 3, ox = v & 31;
+      const int ph = (q8 >> 2) ^ ((ox >> 3) & 1);
+      bf16x4_w h;
+      h[0] = (__bf16)rz[k][0]; h[1] = (__bf16)rz[k][1]; h[2] = (__bf16)rz[k][2]; h[3] = (__bf16)rz[k][3];
+      *reinterpret_cast<bf16x4_w*>(smem + XBYTES + v * 64 + ph * 32 + (q8 & 3) * 8) = h;
+    }
+  };
+  constexpr int NTAP = 7;  // taps tg, tg + 4, ... (< 27)
+  f32x4 acc[NTAP];
+#pragma unroll
+  for (int i = 0; i < NTAP; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int g = lane >> 4, q = (lane & 15) >> 2, pp = lane & 3;
+  if (s0 < s1) load(s0);
+  for (int sl = s0; sl < s1; ++sl) {
+    __syncthreads();  // the previous slab's fragment reads are done
+    store();
+    __syncthreads();
+    if (sl + 1 < s1) load(sl + 1);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int ox0 = 8 * g + q, ox1 = ox0 + 4;
+      const bf16x8_w bfr = tr_pair(smem + XBYTES, (u * 32 + ox0) * 64 + ((bt ^ ((ox0 >> 3) & 1)) * 32) + pp * 8,
+                                   (u * 32 + ox1) * 64 + ((bt ^ ((ox1 >> 3) & 1)) * 32) + pp * 8);
+#pragma unroll
+      for (int i = 0; i < NTAP; ++i) {
+        const int t = tg + 4 * i;
+        if (t < 27) {  // wave-uniform
+          const int td = t / 9, th = (t / 3) % 3, tw = t % 3;
+          const int rb = td * XPS + (2 * u + th) * XRS;
+          const bf16x8_w afr = tr_pair(smem, (rb + xcol(2 * ox0 + tw)) * 32 + pp * 8, (rb + xcol(2 * ox1 + tw)) * 32 + pp * 8);
+          acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afr, bfr, acc[i], 0, 0, 0);
+        }
+      }
+    }
+  }
+  // partials ws[p][t][b][a]: lane holds a = 4g + jj, b = 16 bt + (lane & 15)
+  const int bl = lane & 15;
+#pragma unroll
+  for (int i = 0; i < NTAP; ++i) {
+    const int t = tg + 4 * i;
+    if (t < 27) *reinterpret_cast<f32x4*>(ws + ((((long long)p * 27 + t) * 32 + bt * 16 + bl) * 16 + 4 * g)) = acc[i];
   }
 }
 
@@ -492,8 +602,45 @@ int wgrad_k3_launch(const cgan3d_conv_geom* g, const float* gathered, const floa
   int P;
   wgrad_k3_geometry(g, &a, &P);
   ::cg::launch(wgrad_k3_kernel, dim3(P, 3), dim3(512), 0, st, a, gathered, aligned, ws);
-  ::cg::launch(wgrad_k3_reduce_kernel, dim3(64, 4), dim3(448), 0, st, (const float*)ws, P, dw, (long long)g->w_sa,
+  ::cg::launch(wgrad_k3_reduce_kernel, dim3(64, 4), dim3(448), 0, st, (const float*)ws, P, 64, 64, dw, (long long)g->w_sa,
                (long long)g->w_sb, accumulate);
+  return CGAN3D_OK;
+}
+
+static int g_ws2_P = 128;  // cgan3d_set_tuning key 10: blocks of wgrad_s2_kernel; 0 = off
+
+void wgrad_s2_set_blocks(int v) { g_ws2_P = v; }
+
+bool wgrad_s2_ok(const cgan3d_conv_geom* g) {
+  return g_ws2_P > 0 && g->prec == CGAN3D_PREC_BF16 && !g->transposed && !g->reflect && g->k == 3 && g->stride == 2 &&
+         g->pad == 1 && g->cin == 16 && g->cout == 32 && g->ho % 4 == 0 && g->wo % 32 == 0 &&
+         (long long)2 * g->do_ - 1 <= g->di && (long long)2 * g->ho - 1 <= g->hi && (long long)2 * g->wo - 1 <= g->wi;
+}
+
+static void wgrad_s2_geometry(const cgan3d_conv_geom* g, Ws2Args* a, int* P) {
+  a->n = g->n; a->di = g->di; a->hi = g->hi; a->wi = g->wi; a->do_ = g->do_; a->ho = g->ho; a->wo = g->wo;
+  a->slabs = g->n * g->do_ * (g->ho / 4) * (g->wo / 32);
+  const int p = std::max(1, std::min(g_ws2_P, a->slabs));
+  a->spb = (a->slabs + p - 1) / p;
+  *P = (a->slabs + a->spb - 1) / a->spb;
+}
+
+long long wgrad_s2_ws_floats(const cgan3d_conv_geom* g) {
+  if (!wgrad_s2_ok(g)) return 0;
+  Ws2Args a;
+  int P;
+  wgrad_s2_geometry(g, &a, &P);
+  return (long long)P * 27 * 16 * 32;
+}
+
+int wgrad_s2_launch(const cgan3d_conv_geom* g, const float* gathered, const float* aligned, float* dw, int accumulate,
+                    float* ws, hipStream_t st) {
+  Ws2Args a;
+  int P;
+  wgrad_s2_geometry(g, &a, &P);
+  ::cg::launch(wgrad_s2_kernel, dim3(P), dim3(512), 0, st, a, gathered, aligned, ws);
+  ::cg::launch(wgrad_k3_reduce_kernel, dim3(32, 1), dim3(448), 0, st, (const float*)ws, P, 16, 32, dw,
+               (long long)g->w_sa, (long long)g->w_sb, accumulate);
   return CGAN3D_OK;
 }
 

@@ -362,6 +362,7 @@ WGRAD_BF16_CASES = [
     (64, 64, 3, 1, 1, False, (16, 16, 16)),  # ResNet block at 64^3 patches: wgrad_k3_kernel
     (64, 64, 3, 1, 1, False, (5, 4, 8)),     # wgrad_k3_kernel, odd unit count, one unit per row
     (16, 32, 3, 2, 1, False, (12, 16, 20)),  # downsampling
+    (16, 32, 3, 2, 1, False, (8, 16, 64)),   # downsampling 16 -> 32: wgrad_s2_kernel (4 x 8 x 32 outputs)
     (8, 16, 4, 2, 1, False, (16, 16, 16)),   # critic middle
     (32, 64, 4, 2, 1, False, (8, 8, 8)),
     (12, 20, 3, 1, 1, True, (5, 6, 7)),      # odd channel counts, reflect
@@ -390,10 +391,13 @@ def test_wgrad_bf16(cin, cout, k, s, p, reflect, sp):
     assert_close(dwo.double().cpu().numpy(), 2 * dw.numpy(), 2e-2, "bf16 wgrad accumulate")
 
 
-def test_wgrad_bf16_conv_transpose():
+@pytest.mark.parametrize("cin,cout,sp", [(64, 32, (4, 6, 8)), (32, 16, (4, 8, 32))])
+def test_wgrad_bf16_conv_transpose(cin, cout, sp):
+    """ConvTranspose3d weight gradient (operands swapped); 32 -> 16 at (4, 8, 32) takes
+    wgrad_s2_kernel (the last upsampling layer's shape)."""
     from cgan3d_amd import ops, _lib as L
-    g = torch.Generator().manual_seed(9)
-    n, cin, cout, k, s, p, sp = 2, 64, 32, 3, 2, 1, (4, 6, 8)
+    g = torch.Generator().manual_seed(9 + cin)
+    n, k, s, p = 2, 3, 2, 1
     x = torch.randn(n, cin, *sp, generator=g, dtype=torch.float64)
     w = (torch.randn(cin, cout, k, k, k, generator=g, dtype=torch.float64) / np.sqrt(cout * k**3)).requires_grad_()
     y = F.conv_transpose3d(x, w, stride=s, padding=p, output_padding=1)
