@@ -283,8 +283,9 @@ int wgrad_bf16_launch(const cgan3d_conv_geom* g, const float* gathered, const fl
 // on 8 distinct 8-bank groups, for every tap.  Per-block partials go to ws[p][t][b][a] (plain
 // stores), wgrad_k3_reduce_kernel sums them into dW's layout.
 namespace wk3 {
-constexpr int EX = 10, EY = 6;                  // X halo of one unit: 6 (y) x 10 (x) voxels
-constexpr int XROWS = 2 * EX * EY, ZROWS = 2 * 32;  // rows per stage (two units)
+constexpr int UPS = 4;                          // units per LDS stage
+constexpr int EX = 10, EY = 4;                  // X rows of one unit for one th: 4 (y) x 10 (x) voxels
+constexpr int XROWS = UPS * EX * EY, ZROWS = UPS * 32;  // rows per stage
 constexpr int STAGE_BYTES = (XROWS + ZROWS) * 128;
 __device__ __forceinline__ int swz(int x, int y) { return ((x >> 1) + 2 * y) & 3; }
 }  // namespace wk3
@@ -307,21 +308,18 @@ struct Wk3Args {
 
 __global__ __launch_bounds__(512, 2) void wgrad_k3_kernel(Wk3Args a, const float* __restrict__ x,
                                                           const float* __restrict__ dz, float* __restrict__ ws) {
-  // 8 waves: wave w owns input channels 16*(w & 3) .. +15 and output-channel tiles 2*(w >> 2), +1
-  // (18 accumulator tiles); 2 waves per SIMD interleave their MFMAs with the other's loads
+  // block = (voxel chunk p, tap row tdh = (td, th)): the 3 taps tw of that row x 64 x 64; 8 waves:
+  // wave w owns input channels 16*(w & 3) .. +15 and output-channel tiles 2*(w >> 2), +1.  Nine
+  // tap rows instead of one chunk per block keeps the split-K partials (P x |dW|) small.
   using namespace wk3;
   __shared__ __attribute__((aligned(16))) unsigned char smem[2 * STAGE_BYTES];
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int at = wave & 3, bh = wave >> 2;
-  const int td = blockIdx.y, p = blockIdx.x;
+  const int tdh = blockIdx.y, td = tdh / 3, th = tdh % 3, p = blockIdx.x;
   const int u0 = p * a.upb;
   const int yb_n = a.h >> 2, xb_n = a.w >> 3;
   const long long plane = (long long)a.h * a.w;
-
-  // per-thread staging slots (fixed over the stages): X halo quads k < 4 (rows (tid>>4) + 32k of the
-  // stage's 120), dZ quads k < 2 (rows (tid>>4) + 32k of 64); q4 = channel quad
   const int q4 = tid & 15, rbase = tid >> 4;
-  // block-uniform decode of a unit: voxel index of its (z, 4*yb, 8*xb) corner, and its z, yb, xb
   struct Unit { long long corner; int z, yb, xb; bool ok; };
   auto unit = [&](int uu) {
     Unit r;
@@ -332,59 +330,58 @@ __global__ __launch_bounds__(512, 2) void wgrad_k3_kernel(Wk3Args a, const float
     r.corner = (long long)zq * plane + (long long)(yb * 4) * a.w + xb * 8;  // zq = nb * d + z
     return r;
   };
-  f32x4 sx[4], sz[2];
-  auto load = [&](int s) {
-    const Unit U0 = unit(u0 + 2 * s), U1 = unit(u0 + 2 * s + 1);
+  constexpr int NXK = XROWS * 16 / 512, NZK = ZROWS * 16 / 512;  // 5, 4 float4 per thread
+  f32x4 sx[2][NXK], sz[2][NZK];  // two stages of loads in flight (register slots)
+  auto load = [&](int s, int sl) {
+    const Unit U0 = unit(u0 + UPS * s), U1 = unit(u0 + UPS * s + 1), U2 = unit(u0 + UPS * s + 2),
+               U3 = unit(u0 + UPS * s + 3);
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const int row = rbase + 32 * k;  // < 128; rows >= 120 idle
-      const int u = row >= EX * EY, r = row - u * EX * EY;
+    for (int k = 0; k < NXK; ++k) {
+      const int row = rbase + 32 * k;
+      const int u = row / (EX * EY), r = row - u * EX * EY;
       const int hy = r / EX, hx = r - hy * EX;
-      const Unit V = u ? U1 : U0;
-      const int iz = V.z + td - 1, iy = V.yb * 4 + hy - 1, ix = V.xb * 8 + hx - 1;
-      const bool ok = row < XROWS && V.ok && (unsigned)iz < (unsigned)a.d && (unsigned)iy < (unsigned)a.h &&
-                      (unsigned)ix < (unsigned)a.w;
-      const long long off = V.corner + (long long)(td - 1) * plane + (long long)(hy - 1) * a.w + (hx - 1);
-      sx[k] = ok ? *reinterpret_cast<const f32x4*>(x + off * 64 + 4 * q4) : f32x4{0.f, 0.f, 0.f, 0.f};
+      const Unit V = u == 0 ? U0 : (u == 1 ? U1 : (u == 2 ? U2 : U3));
+      const int iz = V.z + td - 1, iy = V.yb * 4 + hy + th - 1, ix = V.xb * 8 + hx - 1;
+      const bool ok = V.ok && (unsigned)iz < (unsigned)a.d && (unsigned)iy < (unsigned)a.h && (unsigned)ix < (unsigned)a.w;
+      const long long off = V.corner + (long long)(td - 1) * plane + (long long)(hy + th - 1) * a.w + (hx - 1);
+      sx[sl][k] = ok ? *reinterpret_cast<const f32x4*>(x + off * 64 + 4 * q4) : f32x4{0.f, 0.f, 0.f, 0.f};
     }
 #pragma unroll
-    for (int k = 0; k < 2; ++k) {
-      const int row = rbase + 32 * k;  // < 64
+    for (int k = 0; k < NZK; ++k) {
+      const int row = rbase + 32 * k;
       const int u = row >> 5, r = row & 31;
-      const Unit V = u ? U1 : U0;
+      const Unit V = u == 0 ? U0 : (u == 1 ? U1 : (u == 2 ? U2 : U3));
       const long long off = V.corner + (long long)(r >> 3) * a.w + (r & 7);
-      sz[k] = V.ok ? *reinterpret_cast<const f32x4*>(dz + off * 64 + 4 * q4) : f32x4{0.f, 0.f, 0.f, 0.f};
+      sz[sl][k] = V.ok ? *reinterpret_cast<const f32x4*>(dz + off * 64 + 4 * q4) : f32x4{0.f, 0.f, 0.f, 0.f};
     }
   };
-  auto store = [&](int buf) {
+  auto store = [&](int buf, int sl) {
     unsigned char* base = smem + buf * STAGE_BYTES;
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
+    for (int k = 0; k < NXK; ++k) {
       const int row = rbase + 32 * k;
-      if (row >= XROWS) break;
-      const int r = row >= EX * EY ? row - EX * EY : row;
+      const int r = row % (EX * EY);
       const int hy = r / EX, hx = r - hy * EX;
       bf16x4_w v;
-      v[0] = (__bf16)sx[k][0]; v[1] = (__bf16)sx[k][1]; v[2] = (__bf16)sx[k][2]; v[3] = (__bf16)sx[k][3];
+      v[0] = (__bf16)sx[sl][k][0]; v[1] = (__bf16)sx[sl][k][1]; v[2] = (__bf16)sx[sl][k][2]; v[3] = (__bf16)sx[sl][k][3];
       *reinterpret_cast<bf16x4_w*>(base + row * 128 + (((q4 >> 2) ^ swz(hx, hy)) * 32) + (q4 & 3) * 8) = v;
     }
 #pragma unroll
-    for (int k = 0; k < 2; ++k) {
+    for (int k = 0; k < NZK; ++k) {
       const int row = rbase + 32 * k;
       const int r = row & 31;
       bf16x4_w v;
-      v[0] = (__bf16)sz[k][0]; v[1] = (__bf16)sz[k][1]; v[2] = (__bf16)sz[k][2]; v[3] = (__bf16)sz[k][3];
+      v[0] = (__bf16)sz[sl][k][0]; v[1] = (__bf16)sz[sl][k][1]; v[2] = (__bf16)sz[sl][k][2]; v[3] = (__bf16)sz[sl][k][3];
       *reinterpret_cast<bf16x4_w*>(base + (XROWS + row) * 128 + (((q4 >> 2) ^ swz(r & 7, r >> 3)) * 32) + (q4 & 3) * 8) = v;
     }
   };
 
-  f32x4 acc[9][2];
+  f32x4 acc[3][2];
 #pragma unroll
-  for (int t = 0; t < 9; ++t)
+  for (int t = 0; t < 3; ++t)
 #pragma unroll
     for (int bt = 0; bt < 2; ++bt) acc[t][bt] = f32x4{0.f, 0.f, 0.f, 0.f};
   const int g = lane >> 4, q = (lane & 15) >> 2, pp = lane & 3;
-  // per-lane LDS byte offsets of the fragment reads (unit 0; unit 1 adds a constant)
   int boff[2][2];
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
@@ -392,44 +389,45 @@ __global__ __launch_bounds__(512, 2) void wgrad_k3_kernel(Wk3Args a, const float
     boff[j][0] = (XROWS + g * 8 + q) * 128 + ((bt ^ swz(q, g)) * 32) + pp * 8;
     boff[j][1] = (XROWS + g * 8 + q + 4) * 128 + ((bt ^ swz(q + 4, g)) * 32) + pp * 8;
   }
-  const int nstages = a.upb / 2;
-  load(0);
-  for (int s = 0; s < nstages; ++s) {
-    const int buf = s & 1;
-    store(buf);
+  const int nstages = a.upb / UPS;
+  auto stage = [&](int s, int sl) {  // sl == s & 1 (compile-time after the unroll below)
+    store(sl, sl);
     lds_barrier();
-    if (s + 1 < nstages) load(s + 1);
-    const unsigned char* base = smem + buf * STAGE_BYTES;
+    if (s + 2 < nstages) load(s + 2, sl);
+    const unsigned char* base = smem + sl * STAGE_BYTES;
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
+    for (int u = 0; u < UPS; ++u) {
       bf16x8_w bfr[2];
 #pragma unroll
       for (int j = 0; j < 2; ++j) bfr[j] = tr_pair(base + u * 32 * 128, boff[j][0], boff[j][1]);
 #pragma unroll
-      for (int th = 0; th < 3; ++th)
+      for (int tw = 0; tw < 3; ++tw) {
+        const int hy = g, hx0 = q + tw, hx1 = q + 4 + tw;
+        const int r0 = u * (EX * EY) + hy * EX + hx0, r1 = r0 + 4;
+        const bf16x8_w afr = tr_pair(base, r0 * 128 + ((at ^ swz(hx0, hy)) * 32) + pp * 8,
+                                     r1 * 128 + ((at ^ swz(hx1, hy)) * 32) + pp * 8);
 #pragma unroll
-        for (int tw = 0; tw < 3; ++tw) {
-          const int hy = g + th, hx0 = q + tw, hx1 = q + 4 + tw;
-          const int r0 = u * (EX * EY) + hy * EX + hx0, r1 = r0 + 4;
-          const bf16x8_w afr = tr_pair(base, r0 * 128 + ((at ^ swz(hx0, hy)) * 32) + pp * 8,
-                                       r1 * 128 + ((at ^ swz(hx1, hy)) * 32) + pp * 8);
-#pragma unroll
-          for (int j = 0; j < 2; ++j)
-            acc[th * 3 + tw][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afr, bfr[j], acc[th * 3 + tw][j], 0, 0, 0);
-        }
+        for (int j = 0; j < 2; ++j) acc[tw][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afr, bfr[j], acc[tw][j], 0, 0, 0);
+      }
     }
-    // no trailing barrier: the next iteration stores into the other buffer, last read one stage
-    // earlier, before every wave passed this iteration's barrier
+    // no trailing barrier: the next stage stores into the other LDS buffer, last read one stage
+    // earlier, before every wave passed this stage's barrier
+  };
+  if (nstages > 0) load(0, 0);
+  if (nstages > 1) load(1, 1);
+  for (int s = 0; s < nstages; s += 2) {
+    stage(s, 0);
+    if (s + 1 < nstages) stage(s + 1, 1);
   }
   // partials: lane holds a = 16*at + 4g + jj (jj = 0..3), b = 16*bt + (lane & 15)
   const int bl = lane & 15;
 #pragma unroll
-  for (int t = 0; t < 9; ++t)
+  for (int tw = 0; tw < 3; ++tw)
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
-      const int tap = td * 9 + t, bt = 2 * bh + j;
+      const int tap = tdh * 3 + tw, bt = 2 * bh + j;
       *reinterpret_cast<f32x4*>(ws + ((((long long)p * 27 + tap) * 64 + bt * 16 + bl) * 64 + 16 * at + 4 * g)) =
-          acc[t][j];
+          acc[tw][j];
     }
 }
 
@@ -568,7 +566,7 @@ __global__ __launch_bounds__(512) void wgrad_s2_kernel(Ws2Args a, const float* _
   }
 }
 
-static int g_wk3_P = 64;  // cgan3d_set_tuning key 9: voxel chunks (blocks per tap plane); 0 = off
+static int g_wk3_P = 28;  // cgan3d_set_tuning key 9: voxel chunks (blocks per tap plane); 0 = off
 
 void wgrad_k3_set_chunks(int v) { g_wk3_P = v; }
 
@@ -581,9 +579,9 @@ bool wgrad_k3_ok(const cgan3d_conv_geom* g) {
 static void wgrad_k3_geometry(const cgan3d_conv_geom* g, Wk3Args* a, int* P) {
   a->n = g->n; a->d = g->do_; a->h = g->ho; a->w = g->wo;
   a->units = g->n * g->do_ * (g->ho / 4) * (g->wo / 8);
-  int p = std::max(1, std::min(g_wk3_P, (a->units + 1) / 2));
+  int p = std::max(1, std::min(g_wk3_P, (a->units + wk3::UPS - 1) / wk3::UPS));
   int upb = (a->units + p - 1) / p;
-  upb = (upb + 1) / 2 * 2;
+  upb = (upb + wk3::UPS - 1) / wk3::UPS * wk3::UPS;
   *P = (a->units + upb - 1) / upb;
   a->upb = upb;
 }
@@ -601,7 +599,7 @@ int wgrad_k3_launch(const cgan3d_conv_geom* g, const float* gathered, const floa
   Wk3Args a;
   int P;
   wgrad_k3_geometry(g, &a, &P);
-  ::cg::launch(wgrad_k3_kernel, dim3(P, 3), dim3(512), 0, st, a, gathered, aligned, ws);
+  ::cg::launch(wgrad_k3_kernel, dim3(P, 9), dim3(512), 0, st, a, gathered, aligned, ws);
   ::cg::launch(wgrad_k3_reduce_kernel, dim3(64, 4), dim3(448), 0, st, (const float*)ws, P, 64, 64, dw, (long long)g->w_sa,
                (long long)g->w_sb, accumulate);
   return CGAN3D_OK;

@@ -78,7 +78,9 @@ __global__ __launch_bounds__(256) void reflect_fold_kernel(const float* __restri
 }
 
 // reflect_fold + the fused BatchNorm backward statistics of its output (cgan3d_epilogue bn_gsum):
-// V = 4 channels per thread, fixed for the whole grid-stride loop (256 % (C/4) == 0)
+// V = 4 channels per thread, fixed for the whole grid-stride loop (256 % (C/4) == 0), so the
+// channels' scale / shift / mean / invstd live in registers; z is read as float4; two items per
+// iteration keep more loads in flight (HBM-bound: padded dL/dy in, dL/dy + z through)
 __global__ __launch_bounds__(256) void reflect_fold_bn_kernel(const float* __restrict__ pad_in, float* __restrict__ out,
                                                               int N, int D, int H, int W, int C, int P, Epi ep) {
   __shared__ f32x4 r0[256], r1[256];
@@ -86,14 +88,22 @@ __global__ __launch_bounds__(256) void reflect_fold_bn_kernel(const float* __res
   const int total = N * D * H * W * C4;
   const int Dp = D + 2 * P, Hp = H + 2 * P, Wp = W + 2 * P;
   const int c0 = (tid % C4) * 4;
+  f32x4 sc, sf, mu, iv;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    sc[e] = ep.bn_ss[c0 + e]; sf[e] = ep.bn_ss[C + c0 + e]; mu[e] = ep.bn_mi[c0 + e]; iv[e] = ep.bn_mi[C + c0 + e];
+  }
   f32x4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = {0.f, 0.f, 0.f, 0.f};
-  for (int i = blockIdx.x * blockDim.x + tid; i < total; i += gridDim.x * blockDim.x) {
+  const int stride = gridDim.x * blockDim.x;
+#pragma unroll 2
+  for (int i = blockIdx.x * blockDim.x + tid; i < total; i += stride) {
     int t = i / C4;
     const int w = t % W; t /= W;
     const int h = t % H; t /= H;
     const int d = t % D, n = t / D;
     int qd[2], qh[2], qw[2];
     const int nd = fold_src(d, D, P, qd), nh = fold_src(h, H, P, qh), nw = fold_src(w, W, P, qw);
+    const f32x4 z = reinterpret_cast<const f32x4*>(ep.bn_z)[i];
     f32x4 s = {0.f, 0.f, 0.f, 0.f};
     for (int a = 0; a < nd; ++a)
       for (int b = 0; b < nh; ++b)
@@ -102,10 +112,9 @@ __global__ __launch_bounds__(256) void reflect_fold_bn_kernel(const float* __res
     reinterpret_cast<f32x4*>(out)[i] = s;
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
-      float p1 = 0.f, p2 = 0.f;
-      bn_pair(ep, s[e], (long long)i * 4 + e, c0 + e, C, &p1, &p2);
-      a0[e] += p1;
-      a1[e] += p2;
+      const float gg = s[e] * act_grad(z[e] * sc[e] + sf[e], ep.bn_act, ep.bn_slope);
+      a0[e] += gg;
+      a1[e] += gg * (z[e] - mu[e]) * iv[e];
     }
   }
   r0[tid] = a0;
