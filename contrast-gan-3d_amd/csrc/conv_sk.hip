@@ -173,10 +173,11 @@ __global__ __launch_bounds__(256) void conv_sk_kernel(SkArgs a, const float* __r
       vals[t][jj] = ok ? v : 0.f;
     }
   }
-  if (ep.stats) {  // block-major (sum, M2 about the block mean, count), MT == 1: this wave's 16 rows
+  if (ep.stats) {  // (sum, M2 about the row mean, count) of this wave's 16 rows: one stats row per
+                   // block (MT == 1) or per wave (MT == 4)
     int cnt = 0;
     for (int r = 0; r < 16; ++r) cnt += rowo[mt * 16 + r] >= 0;
-    const long long sb = (long long)blockIdx.x * (2 * a.cout + 1);
+    const long long sb = ((long long)blockIdx.x * MT + mt) * (2 * a.cout + 1);
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
       const int c = t * 16 + r16;
@@ -225,24 +226,24 @@ static SkArgs sk_args(const cgan3d_conv_geom* g, int* mt) {
   }
   const int kd = g->transposed ? g->k / g->stride : g->k;
   const int ks = kd * kd * kd * g->cin / 32;
-  *mt = ks >= 8 ? 1 : 4;  // long K: split over the waves; short K: one 16-row tile per wave
   const long long cvox = (long long)a.n * a.cd * a.ch * a.cw;
+  // long K on a small grid: split K over the waves; short K or many rows: one 16-row tile per wave
+  *mt = (ks >= 8 && (long long)a.nclass * ((cvox + 15) / 16) < 1024) ? 1 : 4;
   a.mblocks = (int)((cvox + 16 * *mt - 1) / (16 * *mt));
   a.ktot = g->k * g->k * g->k * g->cin;
   return a;
 }
 
-long long sk_blocks(const cgan3d_conv_geom* g) {
+long long sk_blocks(const cgan3d_conv_geom* g) {  // rows of the statistics epilogue
   int mt;
   SkArgs a = sk_args(g, &mt);
-  return (long long)a.nclass * a.mblocks;
+  return (long long)a.nclass * a.mblocks * mt;
 }
 
 int sk_launch(const cgan3d_conv_geom* g, const float* x, const __bf16* wp, float* y, const Epi& e, hipStream_t st) {
   CG_CHECK_ARG(!e.out2 && !e.minuend && !e.bn_mode, "conv_sk: no out2 / BatchNorm-slab epilogue");
   int mt;
   SkArgs a = sk_args(g, &mt);
-  CG_CHECK_ARG(!e.stats || mt == 1, "conv_sk: statistics epilogue only on the K-split tiling");
   const int nt = (g->cout + 15) / 16;
   const dim3 grid((unsigned)(a.nclass * a.mblocks));
 #define CG_SK(M, N) ::cg::launch((conv_sk_kernel<M, N>), grid, dim3(256), 0, st, a, x, wp, y, e)

@@ -499,6 +499,7 @@ SK_CASES = [
     (16, 32, (8, 8, 8)),
     (32, 64, (8, 8, 8)),
     (8, 16, (10, 12, 14)),  # partial 16-row tiles
+    (8, 16, (32, 32, 48)),  # >= 1024 row tiles: one tile per wave (statistics rows per wave)
 ]
 
 

@@ -65,7 +65,12 @@ def test_step_matches_reference_fixture(golden, tag):
                 if key in f and key.replace("/grad/", "/grad64/") in f:
                     assert_parity(gv.cpu().numpy(), f[key], f[key.replace("/grad/", "/grad64/")], key, atol=atol)
                 elif key in f:
-                    assert_close(gv.cpu().numpy(), f[key], 1e-3, key, atol=atol)
+                    # no fp64 yardstick: 1e-3 on the first iteration; afterwards the parameters
+                    # entering the iteration may already differ by Adam's 2 lr on elements whose
+                    # gradient is below fp32 noise (see _assert_adam_final: atomic summation order
+                    # flips the sign of such steps), which moves the BatchNorm-amplified generator
+                    # gradients by up to ~0.5 %: 1e-2 there
+                    assert_close(gv.cpu().numpy(), f[key], 1e-3 if it == 0 else 1e-2, key, atol=atol)
     for net, mod in (("G", g), ("D", d)):
         sd = mod.state_dict()
         for k in f:
