@@ -63,6 +63,8 @@ _SIGS = {
     "cgan3d_bn_apply": ([_P, _I64, _I32, _P, _I32, _F, _P, _P, _P], _I32),
     "cgan3d_conv3d_bn_slots": ([_P], _I64),
     "cgan3d_bn_finalize_slab": ([_P, _I32, _I32, _I64, _P, _P, _P, _P, _P, _F, _F, _P, _P, _P], _I32),
+    "cgan3d_bn_apply_slab": ([_P, _I32, _I32, _I64, _P, _P, _P, _P, _P, _F, _F, _P, _P, _P, _I32, _F, _P, _P, _P],
+                             _I32),
     "cgan3d_bn_backward_slab": ([_P, _P, _I64, _I32, _P, _I32, _P, _P, _P, _I32, _F, _P, _P, _P, _I32, _P, _P], _I32),
     "cgan3d_bn_backward_ws_floats": ([_I64, _I32], _I64),
     "cgan3d_bn_backward": ([_P, _P, _I64, _I32, _P, _P, _P, _I32, _F, _P, _P, _P, _I32, _P, _P], _I32),

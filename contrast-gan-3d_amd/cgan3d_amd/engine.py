@@ -225,13 +225,13 @@ class GeneratorPlan:
             if training:
                 ep = ops.epilogue(bn_part=self.part_f[i], bn_mode=1, bn_slots=self.slots_f[i])
                 ops.conv(self.geo_fwd[i], h, self.wf[i], self.z[i], ep)
-                ops.bn_finalize_slab(self.part_f[i], self.slots_f[i], ly.cout, nvox, P[f"{nb}.weight"],
-                                     P[f"{nb}.bias"], P[f"{nb}.running_mean"], P[f"{nb}.running_var"],
-                                     P[f"{nb}.num_batches_tracked"], self.ss[i], self.mi[i])
+                ops.bn_apply_slab(self.part_f[i], self.slots_f[i], ly.cout, nvox, P[f"{nb}.weight"], P[f"{nb}.bias"],
+                                  P[f"{nb}.running_mean"], P[f"{nb}.running_var"], P[f"{nb}.num_batches_tracked"],
+                                  self.ss[i], self.mi[i], self.z[i], ly.act, self.y[i], residual=res)
             else:
                 ops.conv(self.geo_fwd[i], h, self.wf[i], self.z[i])
                 self._eval_scale_shift(P, nb, i)
-            ops.bn_apply(self.z[i], nvox, ly.cout, self.ss[i], ly.act, self.y[i], residual=res)
+                ops.bn_apply(self.z[i], nvox, ly.cout, self.ss[i], ly.act, self.y[i], residual=res)
             h = self.y[i]
         la = self.last
         ep = ops.epilogue(bias=P["model.last_conv.bias"], act=L.ACT_TANH,

@@ -421,7 +421,7 @@ def reflect_fold_slots(n, dims: Sequence[int], c) -> int:
 
 
 def bn_finalize_slab(part, nslots, c, nvox, gamma, beta, rmean, rvar, nbt, scale_shift, mean_invstd, momentum=0.1,
-                     eps=1e-5):
+                     eps=1e-5, _checks_only=False):
     """BatchNorm forward statistics from a mode-1 slab (the producing conv's per-block partials)."""
     _need(part, (2 * c + 1) * nslots, "bn_finalize_slab part", exact=False)
     for t, nm in ((gamma, "gamma"), (beta, "beta")):
@@ -433,8 +433,24 @@ def bn_finalize_slab(part, nslots, c, nvox, gamma, beta, rmean, rvar, nbt, scale
         _need(nbt, 1, "bn_finalize_slab num_batches_tracked", dtype=torch.int64)
     _need(scale_shift, 2 * c, "bn_finalize_slab scale_shift")
     _need(mean_invstd, 2 * c, "bn_finalize_slab mean_invstd")
+    if _checks_only:
+        return
     check(_launch("cgan3d_bn_finalize_slab", ptr(part), nslots, c, nvox, ptr(gamma), ptr(beta), ptr(rmean), ptr(rvar),
                   ptr(nbt), momentum, eps, ptr(scale_shift), ptr(mean_invstd)), "bn_finalize_slab")
+
+
+def bn_apply_slab(part, nslots, c, nvox, gamma, beta, rmean, rvar, nbt, scale_shift, mean_invstd, z, act, y,
+                  residual=None, slope=0.0, momentum=0.1, eps=1e-5):
+    """``bn_finalize_slab`` + ``bn_apply`` (one launch when the slab is small)."""
+    bn_finalize_slab(part, nslots, c, nvox, gamma, beta, rmean, rvar, nbt, scale_shift, mean_invstd, momentum, eps,
+                     _checks_only=True)
+    _need(z, nvox * c, "bn_apply_slab z")
+    _need(y, nvox * c, "bn_apply_slab y")
+    if residual is not None:
+        _need(residual, nvox * c, "bn_apply_slab residual")
+    check(_launch("cgan3d_bn_apply_slab", ptr(part), nslots, c, nvox, ptr(gamma), ptr(beta), ptr(rmean), ptr(rvar),
+                  ptr(nbt), momentum, eps, ptr(scale_shift), ptr(mean_invstd), ptr(z), act, float(slope),
+                  ptr(residual), ptr(y)), "bn_apply_slab")
 
 
 def bn_backward_slab(dy, z, nvox, c, part, nslots, scale_shift, mean_invstd, gamma, act, dgamma, dbeta, dz, ws,

@@ -310,6 +310,152 @@ __global__ __launch_bounds__(256) void channel_sum_finalize_kernel(const float* 
   if (tid == 0) out[c] = (float)(red[0] + red[1] + red[2] + red[3]);
 }
 
+// ---- finalize fused into the elementwise pass (small slabs): every block combines the whole slab
+// itself (G = 256 / C threads per channel, Chan in fp64, group shuffles), block 0 publishes the
+// statistics / running buffers / parameter gradients; no separate finalize launch.  Only for small
+// slabs (<= 24 KB per block, e.g. 32^3 patches): at 64^3 the 16^3 x 64-channel layers' 196 KB slab
+// read by every block made the fused launch slower than finalize + apply.
+__device__ __forceinline__ void slab_chan(const float* __restrict__ part, int nslots, int C, int c, int j, int G,
+                                          double* n, double* m, double* q) {
+  const float* rs = part + (long long)c * nslots;
+  const float* rq = part + (long long)(C + c) * nslots;
+  const float* rn = part + (long long)2 * C * nslots;
+  double nn = 0.0, mm = 0.0, qq = 0.0;
+  for (int b0 = j; b0 < nslots; b0 += 4 * G) {
+    float sv[4], qv[4], nv[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int b = b0 + k * G, bb = b < nslots ? b : 0;
+      sv[k] = rs[bb]; qv[k] = rq[bb]; nv[k] = b < nslots ? rn[bb] : 0.f;
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      if (nv[k] > 0.f) chan_merge(nn, mm, qq, nv[k], (double)sv[k] / nv[k], qv[k]);
+  }
+  for (int off = G >> 1; off > 0; off >>= 1) {
+    const double nb = __shfl_xor(nn, off, 64), mb = __shfl_xor(mm, off, 64), qb = __shfl_xor(qq, off, 64);
+    chan_merge(nn, mm, qq, nb, mb, qb);
+  }
+  *n = nn; *m = mm; *q = qq;
+}
+
+__global__ __launch_bounds__(256) void bn_apply_slab_kernel(const float* __restrict__ part, int nslots, int C,
+                                                            double nvox, const float* gamma, const float* beta,
+                                                            float* rmean, float* rvar, long long* nbt, float momentum,
+                                                            float eps, float* scale_shift, float* mean_invstd,
+                                                            const float* __restrict__ z, long long n4, int act,
+                                                            float slope, const float* __restrict__ res,
+                                                            float* __restrict__ y) {
+  __shared__ float ssh[2 * 256];
+  const int tid = threadIdx.x, G = 256 / C, c = tid / G, j = tid - c * G;
+  double n, m, q;
+  slab_chan(part, nslots, C, c, j, G, &n, &m, &q);
+  if (j == 0) {
+    const double mean = m, var = q / n;
+    const double invstd = 1.0 / sqrt(var + (double)eps);
+    const double sc = (double)gamma[c] * invstd;
+    ssh[c] = (float)sc;
+    ssh[C + c] = (float)((double)beta[c] - mean * sc);
+    if (blockIdx.x == 0) {
+      scale_shift[c] = ssh[c];
+      scale_shift[C + c] = ssh[C + c];
+      mean_invstd[c] = (float)mean;
+      mean_invstd[C + c] = (float)invstd;
+      if (rmean) rmean[c] = (float)((1.0 - momentum) * rmean[c] + momentum * mean);
+      if (rvar) rvar[c] = (float)((1.0 - momentum) * rvar[c] + momentum * var * nvox / (nvox > 1 ? nvox - 1 : 1));
+      if (nbt && c == 0) *nbt += 1;
+    }
+  }
+  __syncthreads();
+  const int C4 = C >> 2, cc = (tid % C4) * 4;
+  f32x4 sc4, sf4;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) { sc4[e] = ssh[cc + e]; sf4[e] = ssh[C + cc + e]; }
+  const f32x4* z4 = reinterpret_cast<const f32x4*>(z);
+  const f32x4* r4 = reinterpret_cast<const f32x4*>(res);
+  f32x4* y4 = reinterpret_cast<f32x4*>(y);
+  for (long long i = (long long)blockIdx.x * blockDim.x + tid; i < n4; i += (long long)gridDim.x * blockDim.x) {
+    f32x4 v = z4[i];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[e] = act_f(v[e] * sc4[e] + sf4[e], act, slope);
+    if (res) v += r4[i];
+    y4[i] = v;
+  }
+}
+
+__global__ __launch_bounds__(256) void bn_bwd_apply_slab_kernel(const float* __restrict__ part, int nslots, int C,
+                                                                double nvox, const float* __restrict__ gamma,
+                                                                const float* __restrict__ mi, float* dgamma,
+                                                                float* dbeta, int accumulate,
+                                                                const float* __restrict__ dy,
+                                                                const float* __restrict__ z, long long n4,
+                                                                const float* __restrict__ ss, int act, float slope,
+                                                                float* __restrict__ dz) {
+  __shared__ float co[3 * 256];
+  const int tid = threadIdx.x, G = 256 / C, c = tid / G, j = tid - c * G;
+  {
+    const float* r0 = part + (long long)c * nslots;
+    const float* r1 = part + (long long)(C + c) * nslots;
+    double a0 = 0.0, a1 = 0.0;
+    for (int b0 = j; b0 < nslots; b0 += 4 * G) {
+      float v0[4], v1[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int b = b0 + k * G, bb = b < nslots ? b : 0;
+        v0[k] = b < nslots ? r0[bb] : 0.f;
+        v1[k] = b < nslots ? r1[bb] : 0.f;
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) { a0 += v0[k]; a1 += v1[k]; }
+    }
+    for (int off = G >> 1; off > 0; off >>= 1) {
+      a0 += __shfl_xor(a0, off, 64);
+      a1 += __shfl_xor(a1, off, 64);
+    }
+    if (j == 0) {
+      co[c] = gamma[c] * mi[C + c];
+      co[C + c] = (float)(a0 / nvox);
+      co[2 * C + c] = (float)(a1 / nvox);
+      if (blockIdx.x == 0) {
+        if (dbeta) dbeta[c] = accumulate ? dbeta[c] + (float)a0 : (float)a0;
+        if (dgamma) dgamma[c] = accumulate ? dgamma[c] + (float)a1 : (float)a1;
+      }
+    }
+  }
+  __syncthreads();
+  const int C4 = C >> 2, cc = (tid % C4) * 4;
+  f32x4 sc, sf, mean, inv, k0, k1, k2;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    sc[e] = ss[cc + e]; sf[e] = ss[C + cc + e]; mean[e] = mi[cc + e]; inv[e] = mi[C + cc + e];
+    k0[e] = co[cc + e]; k1[e] = co[C + cc + e]; k2[e] = co[2 * C + cc + e];
+  }
+  const f32x4* z4 = reinterpret_cast<const f32x4*>(z);
+  const f32x4* d4 = reinterpret_cast<const f32x4*>(dy);
+  f32x4* o4 = reinterpret_cast<f32x4*>(dz);
+  for (long long i = (long long)blockIdx.x * blockDim.x + tid; i < n4; i += (long long)gridDim.x * blockDim.x) {
+    const f32x4 zz = z4[i], dd = d4[i];
+    f32x4 o;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float g = dd[e] * act_grad(zz[e] * sc[e] + sf[e], act, slope);
+      const float xh = (zz[e] - mean[e]) * inv[e];
+      o[e] = k0[e] * (g - k1[e] - xh * k2[e]);
+    }
+    o4[i] = o;
+  }
+}
+
+// blocks of the fused finalize + elementwise launch, or 0 when the slab is too large to be read by
+// every block (then: separate finalize launch)
+static int slab_fused_blocks(int nslots, int C, int rows, long long n4) {
+  if (C < 4 || C > 256 || 256 % C) return 0;
+  long long b = (n4 + 256 * 16 - 1) / (256 * 16);  // ~16 float4 per thread
+  b = std::max(1LL, std::min(b, 256LL));
+  const long long per_block = (long long)nslots * C * rows * 4;  // read by every block, latency-bound:
+  return per_block <= 24 * 1024 && per_block * b <= (16LL << 20) ? (int)b : 0;  // measured: 196 KB/block is 3x slower
+}
+
 static int reduce_blocks(long long total) {
   long long b = (total + 256 * 8 - 1) / (256 * 8);
   if (b > 1024) b = 1024;
@@ -367,6 +513,13 @@ extern "C" int cgan3d_bn_backward_slab(const float* dy, const float* z, int64_t 
   CG_CHECK_ARG(nvox > 1 && nslots > 0 && c >= 4 && c <= 256 && 256 % c == 0,
                "cgan3d_bn_backward_slab: channels must divide 256 and be >= 4");
   hipStream_t s = (hipStream_t)stream;
+  if (const int fb = slab_fused_blocks(nslots, c, 2, (long long)nvox * c / 4)) {
+    ::cg::launch(bn_bwd_apply_slab_kernel, dim3(fb), dim3(256), 0, s, part, nslots, c, (double)nvox, gamma,
+                 mean_invstd, dgamma, dbeta, (int)accumulate, dy, z, (long long)nvox * c / 4, scale_shift, act, slope,
+                 dz);
+    CG_LAUNCH_CHECK("bn_bwd_apply_slab_kernel");
+    return CGAN3D_OK;
+  }
   ::cg::launch(bn_bwd_finalize_slab_kernel, dim3(c), dim3(256), 0, s, part, nslots, c, (double)nvox, gamma,
                      mean_invstd, dgamma, dbeta, ws, accumulate);
   CG_LAUNCH_CHECK("bn_bwd_finalize_slab_kernel");
@@ -421,4 +574,25 @@ extern "C" int cgan3d_channel_sum(const float* x, int64_t nvox, int32_t c, float
   ::cg::launch(channel_sum_finalize_kernel, dim3(c), dim3(256), 0, s, ws, nblk, c, out);
   CG_LAUNCH_CHECK("channel_sum_finalize_kernel");
   return CGAN3D_OK;
+}
+
+extern "C" int cgan3d_bn_apply_slab(const float* part, int32_t nslots, int32_t c, int64_t nvox, const float* gamma,
+                                    const float* beta, float* running_mean, float* running_var,
+                                    int64_t* num_batches_tracked, float momentum, float eps, float* scale_shift,
+                                    float* mean_invstd, const float* z, int32_t act, float slope,
+                                    const float* residual, float* y, void* stream) {
+  CG_CHECK_ARG(part && gamma && beta && scale_shift && mean_invstd && z && y, "cgan3d_bn_apply_slab: null pointer");
+  CG_CHECK_ARG(nslots > 0 && nvox > 0 && c >= 4 && c % 4 == 0 && 256 % c == 0,
+               "cgan3d_bn_apply_slab: channels must be a multiple of 4 dividing 256");
+  const long long n4 = (long long)nvox * c / 4;
+  if (const int fb = slab_fused_blocks(nslots, c, 3, n4)) {
+    ::cg::launch(bn_apply_slab_kernel, dim3(fb), dim3(256), 0, (hipStream_t)stream, part, nslots, c, (double)nvox,
+                 gamma, beta, running_mean, running_var, (long long*)num_batches_tracked, momentum, eps, scale_shift,
+                 mean_invstd, z, n4, act, slope, residual, y);
+    CG_LAUNCH_CHECK("bn_apply_slab_kernel");
+    return CGAN3D_OK;
+  }
+  int rc = cgan3d_bn_finalize_slab(part, nslots, c, nvox, gamma, beta, running_mean, running_var, num_batches_tracked,
+                                   momentum, eps, scale_shift, mean_invstd, stream);
+  return rc ? rc : cgan3d_bn_apply(z, nvox, c, scale_shift, act, slope, residual, y, stream);
 }

@@ -160,6 +160,13 @@ int cgan3d_bn_finalize_slab(const float* part, int32_t nslots, int32_t c, int64_
 /* Backward from a bn_mode-2 slab (filled by the kernel that produced dy): dgamma = sum g*xhat,
  * dbeta = sum g (+= when accumulate), then dz = gamma*invstd*(g - mean g - xhat*mean(g*xhat)).
  * ws: 3*c floats. */
+/* cgan3d_bn_finalize_slab followed by cgan3d_bn_apply, as ONE launch when the slab is small
+ * (every block combines the statistics itself; block 0 writes scale_shift / mean_invstd and the
+ * running buffers) — blocks.py:26-27,45 BatchNorm3d train forward + activation (+ residual). */
+int cgan3d_bn_apply_slab(const float* part, int32_t nslots, int32_t c, int64_t nvox, const float* gamma,
+                         const float* beta, float* running_mean, float* running_var, int64_t* num_batches_tracked,
+                         float momentum, float eps, float* scale_shift, float* mean_invstd, const float* z,
+                         int32_t act, float slope, const float* residual, float* y, void* stream);
 int cgan3d_bn_backward_slab(const float* dy, const float* z, int64_t nvox, int32_t c, const float* part,
                             int32_t nslots, const float* scale_shift, const float* mean_invstd,
                             const float* gamma, int32_t act, float slope, float* dgamma, float* dbeta,
