@@ -113,6 +113,10 @@ def load(path: os.PathLike | str | None = None) -> C.CDLL:
         fn.restype = res
     if path is None:
         _lib = lib
+        # CGAN3D_TUNE="key=value,key=value": cgan3d_set_tuning before anything is built (sweeps)
+        for kv in filter(None, os.environ.get("CGAN3D_TUNE", "").split(",")):
+            k, v = kv.split("=")
+            check(lib.cgan3d_set_tuning(int(k), int(v)), f"set_tuning {kv}")
     return lib
 
 

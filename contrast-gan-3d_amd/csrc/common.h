@@ -186,6 +186,7 @@ void wgrad_bf16_set_blocks(int v);
 void halo_set_min_blocks(int v);
 void k7m_set_dbg(int v);
 void k3_tile_set(int v);
+void k3_split_set(int v);
 void halo_set_dbg(int v);
 int wgrad_bf16_launch(const cgan3d_conv_geom* g, const float* gathered, const float* aligned, float* dwp,
                       hipStream_t st);

@@ -531,6 +531,9 @@ static bool halo_setup(const cgan3d_conv_geom* g, HaloArgs* a) {
 }
 
 static int g_k3_tile = 1;  // cgan3d_set_tuning key 3: 0 keeps the ResNet convs on conv_halo_kernel
+static int g_k3_split = 0;  // cgan3d_set_tuning key 12: output-channel blocks per tile (0 auto, 1, 2, 4)
+
+void k3_split_set(int v) { g_k3_split = (v == 1 || v == 2 || v == 4) ? v : 0; }
 
 void halo_set_dbg(int v) { g_halo_dbg = v; }
 
@@ -564,16 +567,16 @@ int halo_launch(const cgan3d_conv_geom* g, const float* x, const float* w, float
   }
   if (k3_tile_ok(g)) {  // ResNet-block shape: whole-tile K-split kernel
     const long long tiles = (long long)a.n * a.td * a.th * a.tw;
-    const bool split = tiles < g_halo_min_blocks;  // small grids: two 32-channel blocks per tile
-    const dim3 grid1((unsigned)tiles, split ? 2 : 1);
+    // small grids: the 64 output channels split over 2 (or, tuning key 12, 4) blocks per tile
+    const int split = g_k3_split ? g_k3_split : (tiles < g_halo_min_blocks ? 2 : 1);
+    const dim3 grid1((unsigned)tiles, split);
     const __bf16* wp = reinterpret_cast<const __bf16*>(w);
-    if (split) {
-      if (g->transposed) ::cg::launch((conv_k3_kernel<true, 2>), grid1, dim3(256), 0, st, a, x, wp, y, e);
-      else ::cg::launch((conv_k3_kernel<false, 2>), grid1, dim3(256), 0, st, a, x, wp, y, e);
-    } else {
-      if (g->transposed) ::cg::launch((conv_k3_kernel<true, 4>), grid1, dim3(256), 0, st, a, x, wp, y, e);
-      else ::cg::launch((conv_k3_kernel<false, 4>), grid1, dim3(256), 0, st, a, x, wp, y, e);
-    }
+#define CG_K3(N) (g->transposed ? ::cg::launch((conv_k3_kernel<true, N>), grid1, dim3(256), 0, st, a, x, wp, y, e) \
+                                : ::cg::launch((conv_k3_kernel<false, N>), grid1, dim3(256), 0, st, a, x, wp, y, e))
+    if (split == 4) CG_K3(1);
+    else if (split == 2) CG_K3(2);
+    else CG_K3(4);
+#undef CG_K3
     return CGAN3D_OK;
   }
   dim3 grid((unsigned)(a.nclass * a.n * a.td * a.th * a.tw), g->cout / a.bn);
