@@ -42,7 +42,8 @@ class Epilogue(C.Structure):
                 ("minuend", C.c_void_p), ("out2", C.c_void_p), ("stats", C.c_void_p),
                 ("act", C.c_int32), ("slope", C.c_float),
                 ("bn_part", C.c_void_p), ("bn_mode", C.c_int32), ("bn_slots", C.c_int32), ("bn_z", C.c_void_p),
-                ("bn_ss", C.c_void_p), ("bn_mi", C.c_void_p), ("bn_act", C.c_int32), ("bn_slope", C.c_float)]
+                ("bn_ss", C.c_void_p), ("bn_mi", C.c_void_p), ("bn_act", C.c_int32), ("bn_slope", C.c_float),
+                ("x_bf16", C.c_void_p)]
 
 
 _P, _I32, _I64, _F = C.c_void_p, C.c_int32, C.c_int64, C.c_float
@@ -60,12 +61,13 @@ _SIGS = {
     "cgan3d_conv3d_wgrad_ws_floats": ([_P], _I64),
     "cgan3d_conv3d_wgrad": ([_P, _P, _P, _P, _I32, _P, _P], _I32),
     "cgan3d_bn_finalize": ([_P, _I64, _I32, _P, _P, _P, _P, _P, _F, _F, _P, _P, _P], _I32),
-    "cgan3d_bn_apply": ([_P, _I64, _I32, _P, _I32, _F, _P, _P, _P], _I32),
+    "cgan3d_bn_apply": ([_P, _I64, _I32, _P, _I32, _F, _P, _P, _P, _P], _I32),
     "cgan3d_conv3d_bn_slots": ([_P], _I64),
     "cgan3d_bn_finalize_slab": ([_P, _I32, _I32, _I64, _P, _P, _P, _P, _P, _F, _F, _P, _P, _P], _I32),
-    "cgan3d_bn_apply_slab": ([_P, _I32, _I32, _I64, _P, _P, _P, _P, _P, _F, _F, _P, _P, _P, _I32, _F, _P, _P, _P],
-                             _I32),
-    "cgan3d_bn_backward_slab": ([_P, _P, _I64, _I32, _P, _I32, _P, _P, _P, _I32, _F, _P, _P, _P, _I32, _P, _P], _I32),
+    "cgan3d_bn_apply_slab": ([_P, _I32, _I32, _I64, _P, _P, _P, _P, _P, _F, _F, _P, _P, _P, _I32, _F, _P, _P, _P,
+                              _P], _I32),
+    "cgan3d_bn_backward_slab": ([_P, _P, _I64, _I32, _P, _I32, _P, _P, _P, _I32, _F, _P, _P, _P, _I32, _P, _P, _P],
+                                _I32),
     "cgan3d_bn_backward_ws_floats": ([_I64, _I32], _I64),
     "cgan3d_bn_backward": ([_P, _P, _I64, _I32, _P, _P, _P, _I32, _F, _P, _P, _P, _I32, _P, _P], _I32),
     "cgan3d_channel_sum_ws_floats": ([_I64, _I32], _I64),

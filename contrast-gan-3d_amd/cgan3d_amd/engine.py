@@ -186,6 +186,18 @@ class GeneratorPlan:
         self.dpad = buf(pd, la.cin)
         ws = max(ws, ops.wgrad_ws_floats(self.geo_last_wgrad), ops.channel_sum_ws_floats(n * la.dout[0] * la.dout[1] * la.dout[2], 1))
         self.ws = torch.empty(ws, device=device)
+        # bf16 shadows of the ResNet-block conv inputs (forward: the previous BatchNorm's output;
+        # input-grad: the layer's own BatchNorm input-grad), written by the BatchNorm pass that
+        # produces the fp32 tensor: the ResNet-block kernel stages its halo from half the bytes
+        # with no conversion (bf16 mode only: the kernel converts to bf16 anyway)
+        self.y16, self.dz16 = [None] * len(layers), [None] * len(layers)
+        if prec == L.PREC_BF16 and not os.environ.get("CGAN3D_NO_SHADOW"):
+            for i, ly in enumerate(layers):
+                if ly.kind == "conv" and (ly.k, ly.s, ly.p, ly.cin, ly.cout, ly.reflect) == (3, 1, 1, 64, 64, False):
+                    if i > 0:
+                        self.y16[i - 1] = torch.empty((n, *layers[i - 1].dout, ly.cin), device=device,
+                                                      dtype=torch.bfloat16)
+                    self.dz16[i] = torch.empty((n, *ly.dout, ly.cout), device=device, dtype=torch.bfloat16)
         # weight gradients run on a side stream, beside the input-gradient chain (each wgrad only
         # needs its layer's dz and input, both final when it is enqueued); own workspace
         wsw = max([ops.wgrad_ws_floats(gw) for gw in self.geo_wgrad] + [ops.wgrad_ws_floats(self.geo_last_wgrad)])
@@ -222,16 +234,17 @@ class GeneratorPlan:
             nb = f"{ly.name}.normalization"
             nvox = self.n * ly.dout[0] * ly.dout[1] * ly.dout[2]
             res = h_res if ly.residual else None
+            h16 = self.y16[i - 1] if i > 0 else None
             if training:
-                ep = ops.epilogue(bn_part=self.part_f[i], bn_mode=1, bn_slots=self.slots_f[i])
+                ep = ops.epilogue(bn_part=self.part_f[i], bn_mode=1, bn_slots=self.slots_f[i], x_bf16=h16)
                 ops.conv(self.geo_fwd[i], h, self.wf[i], self.z[i], ep)
                 ops.bn_apply_slab(self.part_f[i], self.slots_f[i], ly.cout, nvox, P[f"{nb}.weight"], P[f"{nb}.bias"],
                                   P[f"{nb}.running_mean"], P[f"{nb}.running_var"], P[f"{nb}.num_batches_tracked"],
-                                  self.ss[i], self.mi[i], self.z[i], ly.act, self.y[i], residual=res)
+                                  self.ss[i], self.mi[i], self.z[i], ly.act, self.y[i], residual=res, y16=self.y16[i])
             else:
-                ops.conv(self.geo_fwd[i], h, self.wf[i], self.z[i])
+                ops.conv(self.geo_fwd[i], h, self.wf[i], self.z[i], ops.epilogue(x_bf16=h16))
                 self._eval_scale_shift(P, nb, i)
-                ops.bn_apply(self.z[i], nvox, ly.cout, self.ss[i], ly.act, self.y[i], residual=res)
+                ops.bn_apply(self.z[i], nvox, ly.cout, self.ss[i], ly.act, self.y[i], residual=res, y16=self.y16[i])
             h = self.y[i]
         la = self.last
         ep = ops.epilogue(bias=P["model.last_conv.bias"], act=L.ACT_TANH,
@@ -273,7 +286,7 @@ class GeneratorPlan:
             if BN_FUSED_BWD:
                 ops.bn_backward_slab(self.dy[i], self.z[i], nvox, ly.cout, self.part_b[i], self.slots_b[i],
                                      self.ss[i], self.mi[i], P[f"{nb}.weight"], ly.act, G[f"{nb}.weight"],
-                                     G[f"{nb}.bias"], self.dz[i], self.ws)
+                                     G[f"{nb}.bias"], self.dz[i], self.ws, dz16=self.dz16[i])
             else:
                 ops.bn_backward(self.dy[i], self.z[i], nvox, ly.cout, self.ss[i], self.mi[i], P[f"{nb}.weight"],
                                 ly.act, G[f"{nb}.weight"], G[f"{nb}.bias"], self.dz[i], self.ws)
@@ -291,6 +304,7 @@ class GeneratorPlan:
             res = self.dy[i + 1] if ly.name.endswith("block0") else None
             ep = self._bn_grad_epi(i - 1)
             ep.residual = res
+            ep.x_bf16 = self.dz16[i] if BN_FUSED_BWD else None  # only the slab backward writes it
             ops.conv(self.geo_dgrad[i], self.dz[i], self.wd[i], self.dy[i - 1], ep)
         if self.side is not None:  # the weight gradients are complete before anything reads them
             ops.stream_wait(torch.cuda.current_stream(self.device), self.side)

@@ -182,8 +182,9 @@ class Epi:
 
     def __init__(self, bias=None, residual=None, mask_src=None, minuend=None, out2=None, stats=None,
                  act=L.ACT_NONE, slope=0.0, bn_part=None, bn_mode=0, bn_slots=0, bn_z=None, bn_ss=None,
-                 bn_mi=None, bn_act=L.ACT_NONE, bn_slope=0.0):
+                 bn_mi=None, bn_act=L.ACT_NONE, bn_slope=0.0, x_bf16=None):
         self.bias, self.residual, self.mask_src = bias, residual, mask_src
+        self.x_bf16 = x_bf16  # bf16 copy of the conv input (ResNet-block kernel halo source)
         self.minuend, self.out2, self.stats = minuend, out2, stats
         self.act, self.slope = act, float(slope)
         # fused BatchNorm statistics slab (per-block partial pairs): see include/cgan3d.h
@@ -207,6 +208,7 @@ class Epi:
         e.act, e.slope = self.act, self.slope
         e.bn_part, e.bn_mode, e.bn_slots, e.bn_z = ptr(self.bn_part), self.bn_mode, self.bn_slots, ptr(self.bn_z)
         e.bn_ss, e.bn_mi, e.bn_act, e.bn_slope = ptr(self.bn_ss), ptr(self.bn_mi), self.bn_act, self.bn_slope
+        e.x_bf16 = ptr(self.x_bf16)
         return e
 
 
@@ -370,6 +372,8 @@ def conv(g: ConvGeom, x: torch.Tensor, w: torch.Tensor, y: torch.Tensor, ep: Opt
                 _need(getattr(ep, nm), ny, f"conv {nm}")
         if ep.stats is not None:
             _need(ep.stats, stats_floats(g), "conv stats", exact=False)
+        if ep.x_bf16 is not None:
+            _need(ep.x_bf16, _vox_in(g) * g.cin, "conv x_bf16", dtype=torch.bfloat16)
         ep.check_bn(ny, g.cout, "conv")
     check(_timed("conv", g, "cgan3d_conv3d_fwd", ctypes.byref(g), ptr(x), ptr(w), ptr(y),
                  ctypes.byref(ep.c()) if ep is not None else None), "conv3d_fwd")
@@ -401,14 +405,20 @@ def bn_finalize(stats, nblk, c, gamma, beta, rmean, rvar, nbt, scale_shift, mean
                   momentum, eps, ptr(scale_shift), ptr(mean_invstd)), "bn_finalize")
 
 
-def bn_apply(z, nvox, c, scale_shift, act, y, residual=None, slope=0.0):
+def _need16(t, n, what):
+    if t is not None:
+        _need(t, n, what, dtype=torch.bfloat16)
+    return ptr(t)
+
+
+def bn_apply(z, nvox, c, scale_shift, act, y, residual=None, slope=0.0, y16=None):
     _need(z, nvox * c, "bn_apply z")
     _need(y, nvox * c, "bn_apply y")
     _need(scale_shift, 2 * c, "bn_apply scale_shift")
     if residual is not None:
         _need(residual, nvox * c, "bn_apply residual")
-    check(_launch("cgan3d_bn_apply", ptr(z), nvox, c, ptr(scale_shift), act, slope, ptr(residual), ptr(y)),
-          "bn_apply")
+    check(_launch("cgan3d_bn_apply", ptr(z), nvox, c, ptr(scale_shift), act, slope, ptr(residual), ptr(y),
+                  _need16(y16, nvox * c, "bn_apply y16")), "bn_apply")
 
 
 def bn_slots(g: ConvGeom) -> int:
@@ -440,7 +450,7 @@ def bn_finalize_slab(part, nslots, c, nvox, gamma, beta, rmean, rvar, nbt, scale
 
 
 def bn_apply_slab(part, nslots, c, nvox, gamma, beta, rmean, rvar, nbt, scale_shift, mean_invstd, z, act, y,
-                  residual=None, slope=0.0, momentum=0.1, eps=1e-5):
+                  residual=None, slope=0.0, momentum=0.1, eps=1e-5, y16=None):
     """``bn_finalize_slab`` + ``bn_apply`` (one launch when the slab is small)."""
     bn_finalize_slab(part, nslots, c, nvox, gamma, beta, rmean, rvar, nbt, scale_shift, mean_invstd, momentum, eps,
                      _checks_only=True)
@@ -450,11 +460,11 @@ def bn_apply_slab(part, nslots, c, nvox, gamma, beta, rmean, rvar, nbt, scale_sh
         _need(residual, nvox * c, "bn_apply_slab residual")
     check(_launch("cgan3d_bn_apply_slab", ptr(part), nslots, c, nvox, ptr(gamma), ptr(beta), ptr(rmean), ptr(rvar),
                   ptr(nbt), momentum, eps, ptr(scale_shift), ptr(mean_invstd), ptr(z), act, float(slope),
-                  ptr(residual), ptr(y)), "bn_apply_slab")
+                  ptr(residual), ptr(y), _need16(y16, nvox * c, "bn_apply_slab y16")), "bn_apply_slab")
 
 
 def bn_backward_slab(dy, z, nvox, c, part, nslots, scale_shift, mean_invstd, gamma, act, dgamma, dbeta, dz, ws,
-                     slope=0.0, accumulate=False):
+                     slope=0.0, accumulate=False, dz16=None):
     """BatchNorm backward from a mode-2 slab (written by the kernel that produced dy)."""
     for t, nm in ((dy, "dy"), (z, "z"), (dz, "dz")):
         _need(t, nvox * c, f"bn_backward_slab {nm}")
@@ -466,7 +476,7 @@ def bn_backward_slab(dy, z, nvox, c, part, nslots, scale_shift, mean_invstd, gam
     _need(ws, 3 * c, "bn_backward_slab ws", exact=False)
     check(_launch("cgan3d_bn_backward_slab", ptr(dy), ptr(z), nvox, c, ptr(part), nslots, ptr(scale_shift),
                   ptr(mean_invstd), ptr(gamma), act, slope, ptr(dgamma), ptr(dbeta), ptr(dz), int(accumulate),
-                  ptr(ws)), "bn_backward_slab")
+                  ptr(ws), _need16(dz16, nvox * c, "bn_backward_slab dz16")), "bn_backward_slab")
 
 
 def bn_backward_ws_floats(nvox, c) -> int:

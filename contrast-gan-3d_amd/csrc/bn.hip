@@ -74,12 +74,22 @@ __device__ __forceinline__ float act_f(float v, int act, float slope) {
   return v;
 }
 
+// optional bf16 shadow of an output (read by the ResNet-block conv's halo staging)
+typedef __bf16 bf16x4_n __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ void store16(__bf16* o16, long long i, f32x4 v) {
+  bf16x4_n h;
+  h[0] = (__bf16)v[0]; h[1] = (__bf16)v[1]; h[2] = (__bf16)v[2]; h[3] = (__bf16)v[3];
+  reinterpret_cast<bf16x4_n*>(o16)[i] = h;
+}
+
 // y = act(z*scale + shift) (+ residual); C % 4 == 0, float4 vectorised grid-stride.  With
 // 256 % (C/4) == 0 the grid stride is a multiple of C/4, so a thread keeps its 4 channels (and
 // their scale/shift in registers) for the whole loop.
 __global__ __launch_bounds__(256) void bn_apply_kernel(const float* __restrict__ z, long long n4, int C,
                                                        const float* __restrict__ ss, int act, float slope,
-                                                       const float* __restrict__ res, float* __restrict__ y) {
+                                                       const float* __restrict__ res, float* __restrict__ y,
+                                                       __bf16* __restrict__ y16) {
   const int C4 = C >> 2;
   const int c = (threadIdx.x % C4) * 4;
   f32x4 sc, sf;
@@ -94,6 +104,7 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const float* __restrict__
     for (int e = 0; e < 4; ++e) v[e] = act_f(v[e] * sc[e] + sf[e], act, slope);
     if (res) v += r4[i];
     y4[i] = v;
+    if (y16) store16(y16, i, v);
   }
 }
 
@@ -166,7 +177,8 @@ __global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(const float* __res
 __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const float* __restrict__ dy, const float* __restrict__ z,
                                                            long long n4, int C, const float* __restrict__ ss,
                                                            const float* __restrict__ mi, int act, float slope,
-                                                           const float* __restrict__ coef, float* dz) {
+                                                           const float* __restrict__ coef, float* dz,
+                                                           __bf16* __restrict__ dz16) {
   const int C4 = C >> 2;
   const int c = (threadIdx.x % C4) * 4;
   f32x4 sc, sf, mean, inv, k0, k1, k2;
@@ -188,6 +200,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const float* __restri
       o[e] = k0[e] * (g - k1[e] - xh * k2[e]);
     }
     o4[i] = o;
+    if (dz16) store16(dz16, i, o);
   }
 }
 
@@ -345,7 +358,7 @@ __global__ __launch_bounds__(256) void bn_apply_slab_kernel(const float* __restr
                                                             float eps, float* scale_shift, float* mean_invstd,
                                                             const float* __restrict__ z, long long n4, int act,
                                                             float slope, const float* __restrict__ res,
-                                                            float* __restrict__ y) {
+                                                            float* __restrict__ y, __bf16* __restrict__ y16) {
   __shared__ float ssh[2 * 256];
   const int tid = threadIdx.x, G = 256 / C, c = tid / G, j = tid - c * G;
   double n, m, q;
@@ -380,6 +393,7 @@ __global__ __launch_bounds__(256) void bn_apply_slab_kernel(const float* __restr
     for (int e = 0; e < 4; ++e) v[e] = act_f(v[e] * sc4[e] + sf4[e], act, slope);
     if (res) v += r4[i];
     y4[i] = v;
+    if (y16) store16(y16, i, v);
   }
 }
 
@@ -390,7 +404,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_slab_kernel(const float* __r
                                                                 const float* __restrict__ dy,
                                                                 const float* __restrict__ z, long long n4,
                                                                 const float* __restrict__ ss, int act, float slope,
-                                                                float* __restrict__ dz) {
+                                                                float* __restrict__ dz, __bf16* __restrict__ dz16) {
   __shared__ float co[3 * 256];
   const int tid = threadIdx.x, G = 256 / C, c = tid / G, j = tid - c * G;
   {
@@ -443,6 +457,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_slab_kernel(const float* __r
       o[e] = k0[e] * (g - k1[e] - xh * k2[e]);
     }
     o4[i] = o;
+    if (dz16) store16(dz16, i, o);
   }
 }
 
@@ -480,14 +495,14 @@ extern "C" int cgan3d_bn_finalize(const float* stats, int64_t nblk, int32_t c, c
 }
 
 extern "C" int cgan3d_bn_apply(const float* z, int64_t nvox, int32_t c, const float* scale_shift, int32_t act,
-                               float slope, const float* residual, float* y, void* stream) {
+                               float slope, const float* residual, float* y, void* y_bf16, void* stream) {
   CG_CHECK_ARG(z && scale_shift && y, "cgan3d_bn_apply: null pointer");
   CG_CHECK_ARG(nvox > 0 && c > 0 && c % 4 == 0 && 256 % (c / 4) == 0,
                "cgan3d_bn_apply: channels must be a multiple of 4 dividing 1024");
   const long long n4 = (long long)nvox * c / 4;
   int blocks = (int)std::min<long long>((n4 + 255) / 256, 4096);
   ::cg::launch(bn_apply_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, z, n4, c, scale_shift, act,
-                     slope, residual, y);
+                     slope, residual, y, reinterpret_cast<__bf16*>(y_bf16));
   CG_LAUNCH_CHECK("bn_apply_kernel");
   return CGAN3D_OK;
 }
@@ -508,7 +523,7 @@ extern "C" int cgan3d_bn_finalize_slab(const float* part, int32_t nslots, int32_
 extern "C" int cgan3d_bn_backward_slab(const float* dy, const float* z, int64_t nvox, int32_t c, const float* part,
                                        int32_t nslots, const float* scale_shift, const float* mean_invstd,
                                        const float* gamma, int32_t act, float slope, float* dgamma, float* dbeta,
-                                       float* dz, int32_t accumulate, float* ws, void* stream) {
+                                       float* dz, int32_t accumulate, float* ws, void* dz_bf16, void* stream) {
   CG_CHECK_ARG(dy && z && part && scale_shift && mean_invstd && gamma && dz && ws, "cgan3d_bn_backward_slab: null pointer");
   CG_CHECK_ARG(nvox > 1 && nslots > 0 && c >= 4 && c <= 256 && 256 % c == 0,
                "cgan3d_bn_backward_slab: channels must divide 256 and be >= 4");
@@ -516,7 +531,7 @@ extern "C" int cgan3d_bn_backward_slab(const float* dy, const float* z, int64_t 
   if (const int fb = slab_fused_blocks(nslots, c, 2, (long long)nvox * c / 4)) {
     ::cg::launch(bn_bwd_apply_slab_kernel, dim3(fb), dim3(256), 0, s, part, nslots, c, (double)nvox, gamma,
                  mean_invstd, dgamma, dbeta, (int)accumulate, dy, z, (long long)nvox * c / 4, scale_shift, act, slope,
-                 dz);
+                 dz, reinterpret_cast<__bf16*>(dz_bf16));
     CG_LAUNCH_CHECK("bn_bwd_apply_slab_kernel");
     return CGAN3D_OK;
   }
@@ -526,7 +541,7 @@ extern "C" int cgan3d_bn_backward_slab(const float* dy, const float* z, int64_t 
   const long long n4 = (long long)nvox * c / 4;
   const int blocks = (int)std::min<long long>((n4 + 255) / 256, 4096);
   ::cg::launch(bn_bwd_apply_kernel, dim3(blocks), dim3(256), 0, s, dy, z, n4, c, scale_shift, mean_invstd, act,
-                     slope, ws, dz);
+                     slope, ws, dz, reinterpret_cast<__bf16*>(dz_bf16));
   CG_LAUNCH_CHECK("bn_bwd_apply_kernel");
   return CGAN3D_OK;
 }
@@ -554,7 +569,7 @@ extern "C" int cgan3d_bn_backward(const float* dy, const float* z, int64_t nvox,
   CG_LAUNCH_CHECK("bn_bwd_finalize_kernel");
   int blocks = (int)std::min<long long>((n4 + 255) / 256, 4096);
   ::cg::launch(bn_bwd_apply_kernel, dim3(blocks), dim3(256), 0, s, dy, z, n4, c, scale_shift, mean_invstd,
-                     act, slope, coef, dz);
+                     act, slope, coef, dz, nullptr);
   CG_LAUNCH_CHECK("bn_bwd_apply_kernel");
   return CGAN3D_OK;
 }
@@ -580,7 +595,7 @@ extern "C" int cgan3d_bn_apply_slab(const float* part, int32_t nslots, int32_t c
                                     const float* beta, float* running_mean, float* running_var,
                                     int64_t* num_batches_tracked, float momentum, float eps, float* scale_shift,
                                     float* mean_invstd, const float* z, int32_t act, float slope,
-                                    const float* residual, float* y, void* stream) {
+                                    const float* residual, float* y, void* y_bf16, void* stream) {
   CG_CHECK_ARG(part && gamma && beta && scale_shift && mean_invstd && z && y, "cgan3d_bn_apply_slab: null pointer");
   CG_CHECK_ARG(nslots > 0 && nvox > 0 && c >= 4 && c % 4 == 0 && 256 % c == 0,
                "cgan3d_bn_apply_slab: channels must be a multiple of 4 dividing 256");
@@ -588,11 +603,11 @@ extern "C" int cgan3d_bn_apply_slab(const float* part, int32_t nslots, int32_t c
   if (const int fb = slab_fused_blocks(nslots, c, 3, n4)) {
     ::cg::launch(bn_apply_slab_kernel, dim3(fb), dim3(256), 0, (hipStream_t)stream, part, nslots, c, (double)nvox,
                  gamma, beta, running_mean, running_var, (long long*)num_batches_tracked, momentum, eps, scale_shift,
-                 mean_invstd, z, n4, act, slope, residual, y);
+                 mean_invstd, z, n4, act, slope, residual, y, reinterpret_cast<__bf16*>(y_bf16));
     CG_LAUNCH_CHECK("bn_apply_slab_kernel");
     return CGAN3D_OK;
   }
   int rc = cgan3d_bn_finalize_slab(part, nslots, c, nvox, gamma, beta, running_mean, running_var, num_batches_tracked,
                                    momentum, eps, scale_shift, mean_invstd, stream);
-  return rc ? rc : cgan3d_bn_apply(z, nvox, c, scale_shift, act, slope, residual, y, stream);
+  return rc ? rc : cgan3d_bn_apply(z, nvox, c, scale_shift, act, slope, residual, y, y_bf16, stream);
 }

@@ -119,6 +119,7 @@ struct Epi {
   const float* bn_mi;
   int bn_act;
   float bn_slope;
+  const __bf16* x16;  // optional bf16 shadow of the conv input
 };
 
 __device__ __forceinline__ float act_grad(float pre, int act, float slope) {

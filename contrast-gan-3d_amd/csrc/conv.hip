@@ -415,6 +415,7 @@ static Epi to_epi(const cgan3d_epilogue* ep) {
     e.bn_part = ep->bn_mode ? ep->bn_part : nullptr; e.bn_mode = ep->bn_part ? ep->bn_mode : 0;
     e.bn_slots = ep->bn_slots; e.bn_z = ep->bn_z; e.bn_ss = ep->bn_ss; e.bn_mi = ep->bn_mi;
     e.bn_act = ep->bn_act; e.bn_slope = ep->bn_slope;
+    e.x16 = reinterpret_cast<const __bf16*>(ep->x_bf16);
   }
   return e;
 }

@@ -391,7 +391,31 @@ __global__ __launch_bounds__(256, 2) void conv_k3_kernel(HaloArgs a, const float
   // ---- halo: fp32 NDHWC -> bf16 LDS, voxel (hz, hy, hx) row (hz*6 + hy)*8 + hx, granule swizzle;
   // every load of the thread issued before the first conversion
   constexpr int ST = K3_HZ * K3_HY * 6 * 16, ST_PER = (ST + 255) / 256;
-  if (!(a.dbg & 1)) {
+  if (ep.x16 && !(a.dbg & 1)) {  // bf16 shadow of the input: 16-byte granules copied as they are
+    constexpr int SB = K3_HZ * K3_HY * 6 * 8, SB_PER = (SB + 255) / 256;
+    bf16x8_h sb[SB_PER];
+#pragma unroll
+    for (int k = 0; k < SB_PER; ++k) {
+      const int i = tid + 256 * k;
+      const int g8 = i & 7, v = i >> 3;
+      const int hx = v % 6, hy = (v / 6) % 6, hz = v / 36;
+      const int iz = oz + hz, iy = oy + hy, ix = ox + hx;
+      const bool ok = i < SB && (unsigned)iz < (unsigned)a.di && (unsigned)iy < (unsigned)a.hi &&
+                      (unsigned)ix < (unsigned)a.wi;
+      sb[k] = *reinterpret_cast<const bf16x8_h*>(
+          ep.x16 + (ok ? (((long long)(nb * a.di + iz) * a.hi + iy) * a.wi + ix) * CIN + 8 * g8 : 0));
+      if (!ok) sb[k] = bf16x8_h{};
+    }
+#pragma unroll
+    for (int k = 0; k < SB_PER; ++k) {
+      const int i = tid + 256 * k;
+      if (i >= SB) break;
+      const int g8 = i & 7, v = i >> 3;
+      const int hx = v % 6, hy = (v / 6) % 6, hz = v / 36;
+      const int row = hz * K3_HY + hy, vv = row * K3_HX + hx;
+      *reinterpret_cast<bf16x8_h*>(halo + vv * K3_VROW + (g8 ^ ((row * 2) & 7)) * 8) = sb[k];
+    }
+  } else if (!(a.dbg & 1)) {
     f32x4 sv[ST_PER];
 #pragma unroll
     for (int k = 0; k < ST_PER; ++k) {

@@ -98,6 +98,8 @@ typedef struct cgan3d_epilogue {
   const float* bn_mi;          /* mode 2: [mean | invstd] */
   int32_t bn_act;              /* mode 2: the activation after the BatchNorm */
   float bn_slope;
+  const void* x_bf16;          /* optional bf16 copy of the input x (same layout): the ResNet-block
+                                * kernel stages its halo from it (half the bytes, no conversion) */
 } cgan3d_epilogue;
 
 const char* cgan3d_version(void);
@@ -145,8 +147,10 @@ int cgan3d_bn_finalize(const float* stats, int64_t nblk, int32_t c, const float*
                        const float* beta, float* running_mean, float* running_var,
                        int64_t* num_batches_tracked, float momentum, float eps,
                        float* scale_shift, float* mean_invstd, void* stream);
+/* y_bf16 (optional, NULL = none): a bf16 copy of y written by the same pass (the input of the
+ * next ResNet-block conv, cgan3d_epilogue.x_bf16). */
 int cgan3d_bn_apply(const float* z, int64_t nvox, int32_t c, const float* scale_shift,
-                    int32_t act, float slope, const float* residual, float* y, void* stream);
+                    int32_t act, float slope, const float* residual, float* y, void* y_bf16, void* stream);
 /* Slots of a launch's fused BatchNorm slab (cgan3d_epilogue bn_part); 0 when the geometry's
  * kernel has no fused statistics. */
 int64_t cgan3d_conv3d_bn_slots(const cgan3d_conv_geom* g);
@@ -166,11 +170,13 @@ int cgan3d_bn_finalize_slab(const float* part, int32_t nslots, int32_t c, int64_
 int cgan3d_bn_apply_slab(const float* part, int32_t nslots, int32_t c, int64_t nvox, const float* gamma,
                          const float* beta, float* running_mean, float* running_var, int64_t* num_batches_tracked,
                          float momentum, float eps, float* scale_shift, float* mean_invstd, const float* z,
-                         int32_t act, float slope, const float* residual, float* y, void* stream);
+                         int32_t act, float slope, const float* residual, float* y, void* y_bf16,
+                         void* stream);
+/* dz_bf16 (optional): bf16 copy of dz, as y_bf16 above (input of a ResNet-block input-grad). */
 int cgan3d_bn_backward_slab(const float* dy, const float* z, int64_t nvox, int32_t c, const float* part,
                             int32_t nslots, const float* scale_shift, const float* mean_invstd,
                             const float* gamma, int32_t act, float slope, float* dgamma, float* dbeta,
-                            float* dz, int32_t accumulate, float* ws, void* stream);
+                            float* dz, int32_t accumulate, float* ws, void* dz_bf16, void* stream);
 int64_t cgan3d_bn_backward_ws_floats(int64_t nvox, int32_t c);
 /* accumulate != 0: dgamma/dbeta += this batch's gradients (a module called on several batches in
  * one step, e.g. the BatchNorm critic on the real and the fake batch, Trainer.py:119-121). */

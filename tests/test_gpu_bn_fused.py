@@ -166,7 +166,9 @@ def test_fused_batchnorm_vs_torch(c, act):
     ops.reflect_fold(_cl(gpad), dyd, n, sp, c, P, ep=ep)
     dzd, dgd, dbd = torch.empty_like(zd), torch.empty(c, device="cuda"), torch.empty(c, device="cuda")
     ws = torch.empty(3 * c, device="cuda")
-    ops.bn_backward_slab(dyd, zd, nvox, c, pb, sb, ss, mi, gmd, act, dgd, dbd, dzd, ws)
+    dz16 = torch.empty(zd.shape, device="cuda", dtype=torch.bfloat16)
+    ops.bn_backward_slab(dyd, zd, nvox, c, pb, sb, ss, mi, gmd, act, dgd, dbd, dzd, ws, dz16=dz16)
     assert_close(_ncdhw(dzd).numpy(), dz.numpy(), 1e-3, "fused bn dz")
+    assert torch.equal(dz16, dzd.bfloat16()), "bf16 shadow of the BN input-grad"
     assert_close(dgd.double().cpu().numpy(), dgm.numpy(), 1e-3, "fused bn dgamma")
     assert_close(dbd.double().cpu().numpy(), dbt.numpy(), 1e-3, "fused bn dbeta")

@@ -136,8 +136,10 @@ def test_batchnorm_train_forward_backward(c):
     ops.bn_finalize(stats, stats.numel() // (2 * c + 1), c, gmd, btd, rmd, rvd, nbt, ss, mi)
     nvox = n * sp[0] * sp[1] * sp[2]
     yd = torch.empty_like(zd)
-    ops.bn_apply(zd, nvox, c, ss, L.ACT_RELU, yd)
+    y16 = torch.empty(zd.shape, device="cuda", dtype=torch.bfloat16)
+    ops.bn_apply(zd, nvox, c, ss, L.ACT_RELU, yd, y16=y16)
     assert_close(_ncdhw(yd).numpy(), y.detach().numpy(), 1e-3, "bn fwd")
+    assert torch.equal(y16, yd.bfloat16()), "bf16 shadow of the BN output"
     assert_close(rmd.cpu().numpy(), rm.numpy(), 1e-3, "running_mean")
     assert_close(rvd.cpu().numpy(), rv.numpy(), 1e-3, "running_var")
     assert int(nbt.item()) == 1
@@ -293,6 +295,17 @@ def test_conv_halo_bf16(transposed, cin, cout, k, s, p, sp):
     dxo = torch.empty(n, *din, cin, device="cuda")
     ops.conv(gd, _cl(gy), wdp, dxo)
     assert_close(_ncdhw(dxo).numpy(), dx.numpy(), 2e-2, "halo dgrad")
+    if (transposed, cin, cout, k, s) == (False, 64, 64, 3, 1):
+        # ResNet-block kernel staging its halo from a bf16 shadow of the input: the same bf16
+        # operands (round-to-nearest-even either way), so bit-identical outputs and statistics
+        yo16, st16 = torch.empty_like(yo), torch.empty_like(stats)
+        ops.conv(gf, _cl(x), wf, yo16, ops.epilogue(act=L.ACT_RELU, residual=_cl(res), stats=st16,
+                                                    x_bf16=_cl(x).bfloat16()))
+        assert torch.equal(yo16, yo), "bf16-shadow forward differs"
+        assert torch.equal(st16, stats), "bf16-shadow statistics differ"
+        dxo16 = torch.empty_like(dxo)
+        ops.conv(gd, _cl(gy), wdp, dxo16, ops.epilogue(x_bf16=_cl(gy).bfloat16()))
+        assert torch.equal(dxo16, dxo), "bf16-shadow input-grad differs"
 
 
 @pytest.mark.parametrize("sp", [(12, 20, 36), (16, 16, 16)])
