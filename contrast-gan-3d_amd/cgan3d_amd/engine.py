@@ -198,6 +198,8 @@ class GeneratorPlan:
                         self.y16[i - 1] = torch.empty((n, *layers[i - 1].dout, ly.cin), device=device,
                                                       dtype=torch.bfloat16)
                     self.dz16[i] = torch.empty((n, *ly.dout, ly.cout), device=device, dtype=torch.bfloat16)
+            # ... and of the last conv's input (its 16 -> 1 k7 kernel stages a halo of it per tile)
+            self.y16[-1] = torch.empty((n, *layers[-1].dout, layers[-1].cout), device=device, dtype=torch.bfloat16)
         # weight gradients run on a side stream, beside the input-gradient chain (each wgrad only
         # needs its layer's dz and input, both final when it is enqueued); own workspace
         wsw = max([ops.wgrad_ws_floats(gw) for gw in self.geo_wgrad] + [ops.wgrad_ws_floats(self.geo_last_wgrad)])
@@ -248,7 +250,7 @@ class GeneratorPlan:
             h = self.y[i]
         la = self.last
         ep = ops.epilogue(bias=P["model.last_conv.bias"], act=L.ACT_TANH,
-                          minuend=x if opt_hat_out is not None else None, out2=opt_hat_out)
+                          minuend=x if opt_hat_out is not None else None, out2=opt_hat_out, x_bf16=self.y16[-1])
         ops.conv(self.geo_last_fwd, h, P["model.last_conv.weight"], self.att, ep)
         return self.att
 

@@ -227,13 +227,17 @@ __global__ __launch_bounds__(256, 2) void k7m_n2w_kernel(K7Args a, const float* 
 // ---- w2n tile: 4 (d) x 4 (h) x 16 (w) outputs; the 4 waves split the 100 input rows; the 16
 // channels are staged in two halves of 8 (one 16-byte vector per halo voxel).  Persistent blocks:
 // the weight table is staged once per block and each half's halo is loaded into registers while
-// the previous half's MFMAs run.
+// the previous half's MFMAs run.  X16: the halo comes from a bf16 shadow of x (cgan3d_epilogue
+// x_bf16; one 16-byte granule per voxel and half, copied as it is) instead of fp32 x.
 constexpr int W_TD = 4, W_TH = 4, W_TW = 16;
 constexpr int W_HD = W_TD + 6, W_HH = W_TH + 6, W_HW = 24, W_HWU = W_TW + 6;
 constexpr int W_ROWS = W_HD * W_HH;  // 100
 constexpr int W_F4 = W_ROWS * W_HWU * 2, W_F4_PER = (W_F4 + 255) / 256;  // float4 per half
+constexpr int W_G16 = W_ROWS * W_HWU, W_G16_PER = (W_G16 + 255) / 256;   // bf16 granules per half
 
+template <bool X16>
 __global__ __launch_bounds__(256, 2) void k7m_w2n_kernel(K7Args a, const float* __restrict__ x,
+                                                         const __bf16* __restrict__ x16,
                                                          const float* __restrict__ w, float* __restrict__ y,
                                                          const float* __restrict__ bias, int act,
                                                          const float* __restrict__ minuend, float* __restrict__ out2,
@@ -257,13 +261,15 @@ __global__ __launch_bounds__(256, 2) void k7m_w2n_kernel(K7Args a, const float* 
     const int r = i / ((W_HW - W_HWU) * 8), j = i % ((W_HW - W_HWU) * 8);
     hs[(r * W_HW + W_HWU) * 8 + j] = (__bf16)0.f;
   }
-  int hc[W_F4_PER];  // this thread's staged float4s: packed (hd, hh, hw, q), -1 past the halo
+  constexpr int NPER = X16 ? W_G16_PER : W_F4_PER, NTOT = X16 ? W_G16 : W_F4;
+  int hc[NPER];  // this thread's staged vectors: packed (hd, hh, hw, q), -1 past the halo
 #pragma unroll
-  for (int k = 0; k < W_F4_PER; ++k) {
-    const int i = tid + 256 * k, q = i & 1, v = i >> 1, hw = v % W_HWU, r = v / W_HWU;
-    hc[k] = i < W_F4 ? ((r / W_HH) | ((r % W_HH) << 8) | (hw << 16) | (q << 24)) : -1;
+  for (int k = 0; k < NPER; ++k) {
+    const int i = tid + 256 * k, q = X16 ? 0 : i & 1, v = X16 ? i : i >> 1, hw = v % W_HWU, r = v / W_HWU;
+    hc[k] = i < NTOT ? ((r / W_HH) | ((r % W_HH) << 8) | (hw << 16) | (q << 24)) : -1;
   }
-  f32x4 xv[W_F4_PER];
+  f32x4 xv[X16 ? 1 : W_F4_PER];
+  bf16x8_k xb[X16 ? W_G16_PER : 1];
   auto tile_origin = [&](int tile, int* n, int* d0, int* h0, int* w0) {
     int r = tile;
     const int tw_ = r % a.tiles_w; r /= a.tiles_w;
@@ -275,23 +281,34 @@ __global__ __launch_bounds__(256, 2) void k7m_w2n_kernel(K7Args a, const float* 
     int n, d0, h0, w0;
     tile_origin(tile, &n, &d0, &h0, &w0);
     const f32x4* xp = reinterpret_cast<const f32x4*>(x);
+    const bf16x8_k* xq = reinterpret_cast<const bf16x8_k*>(x16);
 #pragma unroll
-    for (int k = 0; k < W_F4_PER; ++k) {
+    for (int k = 0; k < NPER; ++k) {
       const int c = hc[k];
       const int id = k7_src(d0 + (c & 255) - a.P, a.di, a.reflect),
                 ih = k7_src(h0 + ((c >> 8) & 255) - a.P, a.hi, a.reflect),
                 iw = k7_src(w0 + ((c >> 16) & 255) - a.P, a.wi, a.reflect);
       const bool ok = c >= 0 && (id | ih | iw) >= 0;
-      xv[k] = xp[ok ? (((n * a.di + id) * a.hi + ih) * a.wi + iw) * (C / 4) + half * 2 + (c >> 24) : 0];
-      if (!ok) xv[k] = f32x4{0.f, 0.f, 0.f, 0.f};
+      const int vox = ((n * a.di + id) * a.hi + ih) * a.wi + iw;
+      if constexpr (X16) {
+        xb[k] = xq[ok ? vox * 2 + half : 0];
+        if (!ok) xb[k] = bf16x8_k{};
+      } else {
+        xv[k] = xp[ok ? vox * (C / 4) + half * 2 + (c >> 24) : 0];
+        if (!ok) xv[k] = f32x4{0.f, 0.f, 0.f, 0.f};
+      }
     }
   };
   auto store = [&]() {
 #pragma unroll
-    for (int k = 0; k < W_F4_PER; ++k) {
+    for (int k = 0; k < NPER; ++k) {
       const int c = hc[k];
       if (c < 0) continue;
       const int row = (c & 255) * W_HH + ((c >> 8) & 255);
+      if constexpr (X16) {
+        *reinterpret_cast<bf16x8_k*>(hs + (row * W_HW + ((c >> 16) & 255)) * 8) = xb[k];
+        continue;
+      }
       bf16x4_k u;
       u[0] = (__bf16)xv[k][0]; u[1] = (__bf16)xv[k][1]; u[2] = (__bf16)xv[k][2]; u[3] = (__bf16)xv[k][3];
       *reinterpret_cast<bf16x4_k*>(hs + (row * W_HW + ((c >> 16) & 255)) * 8 + 4 * (c >> 24)) = u;
@@ -602,8 +619,12 @@ void k7m_w2n_launch(const cgan3d_conv_geom* g, int P, int reflect, long long wc,
   const K7Args a = k7m_args(g, P, reflect, 0, wc, W_TD, W_TH, W_TW);
   int grid, per, nt;
   k7m_n2w_split(a, &grid, &per, &nt);
-  ::cg::launch(k7m_w2n_kernel, dim3(grid), dim3(256), 0, s, a, x, w, y, e.bias, e.act, e.minuend, e.out2, per,
-                     nt);
+  if (e.x16)
+    ::cg::launch(k7m_w2n_kernel<true>, dim3(grid), dim3(256), 0, s, a, x, e.x16, w, y, e.bias, e.act, e.minuend,
+                 e.out2, per, nt);
+  else
+    ::cg::launch(k7m_w2n_kernel<false>, dim3(grid), dim3(256), 0, s, a, x, e.x16, w, y, e.bias, e.act, e.minuend,
+                 e.out2, per, nt);
 }
 
 long long k7m_wgrad_ws_floats(const cgan3d_conv_geom* g) {

@@ -350,6 +350,12 @@ def test_k7_bf16_mfma(sp):
              ops.epilogue(bias=bl.float().cuda(), act=L.ACT_TANH, minuend=mn, out2=o2))
     assert_close(_ncdhw(att).numpy(), yl.detach().numpy(), 2e-2, "k7 w2n fwd")
     assert_close(_ncdhw(o2).numpy(), (x1 - yl).detach().numpy(), 2e-2, "k7 w2n out2")
+    # the same launch staging from a bf16 shadow of x (the same bf16 operands): bit-identical
+    att16, o216 = torch.empty_like(att), torch.empty_like(o2)
+    ops.conv(geo, _cl(x16), wl.detach().float().cuda(), att16,
+             ops.epilogue(bias=bl.float().cuda(), act=L.ACT_TANH, minuend=mn, out2=o216,
+                          x_bf16=_cl(x16).bfloat16()))
+    assert torch.equal(att16, att) and torch.equal(o216, o2), "k7 w2n bf16-shadow output differs"
     # weight grads
     for name, gw, gath, alig, ref, w in (
             ("k7 wg n2w", ops.conv_wgrad_geom(n, dims, dims, 1, 16, k, 1, p, True), _cl(x1), _cl(gf), dwf, wf),
