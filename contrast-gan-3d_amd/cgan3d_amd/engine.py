@@ -186,20 +186,29 @@ class GeneratorPlan:
         self.dpad = buf(pd, la.cin)
         ws = max(ws, ops.wgrad_ws_floats(self.geo_last_wgrad), ops.channel_sum_ws_floats(n * la.dout[0] * la.dout[1] * la.dout[2], 1))
         self.ws = torch.empty(ws, device=device)
-        # bf16 shadows of the ResNet-block conv inputs (forward: the previous BatchNorm's output;
-        # input-grad: the layer's own BatchNorm input-grad), written by the BatchNorm pass that
-        # produces the fp32 tensor: the ResNet-block kernel stages its halo from half the bytes
-        # with no conversion (bf16 mode only: the kernel converts to bf16 anyway)
+        # bf16 shadows of conv inputs (forward: the previous BatchNorm's output; input-grad: the
+        # layer's own BatchNorm input-grad), written by the BatchNorm pass that produces the fp32
+        # tensor: the halo-staging kernels (ResNet-block conv_k3, the last k7 conv) copy their halo
+        # from half the bytes with no conversion.  bf16 mode only (those kernels round to bf16
+        # anyway): results are bit-identical with or without.  The stride-2 S2F / S2T kernels take
+        # shadows too (tests/test_gpu_ops.py) but are not given any: measured at 64^3, the extra
+        # shadow writes in the BatchNorm passes cost what S2F saves, and S2T is bound by its output.
+        shadow_kinds = {("conv", 3, 1, 64, 64)}
         self.y16, self.dz16 = [None] * len(layers), [None] * len(layers)
+
+        def bf(dd, c):
+            return torch.empty((n, *dd, c), device=device, dtype=torch.bfloat16)
+
         if prec == L.PREC_BF16 and not os.environ.get("CGAN3D_NO_SHADOW"):
             for i, ly in enumerate(layers):
-                if ly.kind == "conv" and (ly.k, ly.s, ly.p, ly.cin, ly.cout, ly.reflect) == (3, 1, 1, 64, 64, False):
-                    if i > 0:
-                        self.y16[i - 1] = torch.empty((n, *layers[i - 1].dout, ly.cin), device=device,
-                                                      dtype=torch.bfloat16)
-                    self.dz16[i] = torch.empty((n, *ly.dout, ly.cout), device=device, dtype=torch.bfloat16)
+                if (ly.kind, ly.k, ly.s, ly.cin, ly.cout) not in shadow_kinds or ly.reflect:
+                    continue
+                if i > 0 and self.geo_fwd[i].w_packed == 2:
+                    self.y16[i - 1] = bf(layers[i - 1].dout, ly.cin)
+                if self.geo_dgrad[i].w_packed == 2:
+                    self.dz16[i] = bf(ly.dout, ly.cout)
             # ... and of the last conv's input (its 16 -> 1 k7 kernel stages a halo of it per tile)
-            self.y16[-1] = torch.empty((n, *layers[-1].dout, layers[-1].cout), device=device, dtype=torch.bfloat16)
+            self.y16[-1] = bf(layers[-1].dout, layers[-1].cout)
         # weight gradients run on a side stream, beside the input-gradient chain (each wgrad only
         # needs its layer's dz and input, both final when it is enqueued); own workspace
         wsw = max([ops.wgrad_ws_floats(gw) for gw in self.geo_wgrad] + [ops.wgrad_ws_floats(self.geo_last_wgrad)])

@@ -161,7 +161,33 @@ __global__ __launch_bounds__(256) void conv_s2f_kernel(S2Args a, const float* __
   }
 
   // halo: input (2*Z0-1 .. +5, 2*Y0-1 .. +9, 2*X0-1 .. +33) -> [hz][hy][x parity][x/2][16] bf16
-  {
+  if (ep.x16) {  // from the bf16 shadow of the input: 16-byte granules (8 channels) copied as they are
+    const int iz0 = 2 * Z0 - 1, iy0 = 2 * Y0 - 1, ix0 = 2 * X0 - 1;
+    constexpr int NG = F_HZ * F_HY * F_HX * 2, PG = (NG + 255) / 256;
+    const bf16x8_s* xq = reinterpret_cast<const bf16x8_s*>(ep.x16);
+    bf16x8_s sb[PG];
+#pragma unroll
+    for (int k = 0; k < PG; ++k) {
+      const int i = tid + 256 * k;
+      const int q = i & 1, v = i >> 1;
+      const int hx = v % F_HX, r = v / F_HX;
+      const int hy = r % F_HY, hz = r / F_HY;
+      const int iz = iz0 + hz, iy = iy0 + hy, ix = ix0 + hx;
+      const bool ok = !(a.dbg & 1) && i < NG && (unsigned)iz < (unsigned)a.di && (unsigned)iy < (unsigned)a.hi &&
+                      (unsigned)ix < (unsigned)a.wi;
+      sb[k] = xq[ok ? ((((long long)nb * a.di + iz) * a.hi + iy) * a.wi + ix) * 2 + q : 0];
+      if (!ok) sb[k] = bf16x8_s{};
+    }
+#pragma unroll
+    for (int k = 0; k < PG; ++k) {
+      const int i = tid + 256 * k;
+      if (i >= NG) break;
+      const int q = i & 1, v = i >> 1;
+      const int hx = v % F_HX, r = v / F_HX;
+      const int row = r * 2 + (hx & 1);
+      *reinterpret_cast<bf16x8_s*>(halo + (row * F_SX + (hx >> 1)) * CI + 8 * q) = sb[k];
+    }
+  } else {
     const int iz0 = 2 * Z0 - 1, iy0 = 2 * Y0 - 1, ix0 = 2 * X0 - 1;
     constexpr int NV4 = F_HZ * F_HY * F_HX * 4, PER = (NV4 + 255) / 256, BATCH = 8;
 #pragma unroll
@@ -311,7 +337,30 @@ __global__ __launch_bounds__(256) void conv_s2t_kernel(S2Args a, const float* __
   for (int t = 0; t < 27; ++t)
     bq[t] = (a.dbg & 8) ? bf16x8_s{} : *reinterpret_cast<const bf16x8_s*>(wpk + ((long long)t * CO + r16) * CI + 8 * (g ^ (r16 & 3)));
 
-  {  // halo: gathered (Z0 .. +3, Y0 .. +5, X0 .. +17) -> [hz][hy][hx][32] bf16, granule swizzle
+  if (ep.x16) {  // the same halo from the bf16 shadow of the input, 16-byte granules as they are
+    constexpr int NG = T_HZ * T_HY * T_HX * 4, PG = (NG + 255) / 256;
+    const bf16x8_s* xq = reinterpret_cast<const bf16x8_s*>(ep.x16);
+    bf16x8_s sb[PG];
+#pragma unroll
+    for (int k = 0; k < PG; ++k) {
+      const int i = tid + 256 * k;
+      const int q = i & 3, v = i >> 2;
+      const int hx = v % T_HX, r = v / T_HX;
+      const int hy = r % T_HY, hz = r / T_HY;
+      const int iz = Z0 + hz, iy = Y0 + hy, ix = X0 + hx;
+      const bool ok = !(a.dbg & 1) && i < NG && iz < a.di && iy < a.hi && ix < a.wi;
+      sb[k] = xq[ok ? ((((long long)nb * a.di + iz) * a.hi + iy) * a.wi + ix) * 4 + q : 0];
+      if (!ok) sb[k] = bf16x8_s{};
+    }
+#pragma unroll
+    for (int k = 0; k < PG; ++k) {
+      const int i = tid + 256 * k;
+      if (i >= NG) break;
+      const int q = i & 3, v = i >> 2;
+      const int hx = v % T_HX;
+      *reinterpret_cast<bf16x8_s*>(halo + v * 32 + 8 * (q ^ ((hx >> 1) & 2))) = sb[k];
+    }
+  } else {  // halo: gathered (Z0 .. +3, Y0 .. +5, X0 .. +17) -> [hz][hy][hx][32] bf16, granule swizzle
     constexpr int NV4 = T_HZ * T_HY * T_HX * 8, PER = (NV4 + 255) / 256;
     f32x4 sv[PER];
 #pragma unroll

@@ -485,6 +485,12 @@ def test_conv_s2_bf16(role, fine):
     ops.conv(geo, _cl(x), wp, y, ops.epilogue(bias=bias.float().cuda(), act=L.ACT_RELU, bn_part=part, bn_mode=1,
                                               bn_slots=slots))
     assert_close(_ncdhw(y).numpy(), torch.relu(ref + bias.view(1, -1, 1, 1, 1)).numpy(), 2e-2, f"{role} out")
+    # staging from a bf16 shadow of the input (the same bf16 operands): bit-identical output and slab
+    y16, part16 = torch.empty_like(y), torch.full_like(part, float("nan"))
+    ops.conv(geo, _cl(x), wp, y16, ops.epilogue(bias=bias.float().cuda(), act=L.ACT_RELU, bn_part=part16, bn_mode=1,
+                                                bn_slots=slots, x_bf16=_cl(x).bfloat16()))
+    assert torch.equal(y16, y) and torch.equal(part16.nan_to_num(), part.nan_to_num()), \
+        f"{role}: bf16-shadow result differs"
     sl = part.double().cpu().view(2 * cout + 1, slots)
     cnt = sl[2 * cout]
     tot = cnt.sum()
