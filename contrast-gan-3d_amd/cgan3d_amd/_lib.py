@@ -60,6 +60,7 @@ _SIGS = {
     "cgan3d_pack_weights_multi": ([_P, _I32, _I64, _P], _I32),
     "cgan3d_conv3d_wgrad_ws_floats": ([_P], _I64),
     "cgan3d_conv3d_wgrad": ([_P, _P, _P, _P, _I32, _P, _P], _I32),
+    "cgan3d_conv3d_wgrad_ex": ([_P, _P, _P, _P, _I32, _P, _P, _P, _P], _I32),
     "cgan3d_bn_finalize": ([_P, _I64, _I32, _P, _P, _P, _P, _P, _F, _F, _P, _P, _P], _I32),
     "cgan3d_bn_apply": ([_P, _I64, _I32, _P, _I32, _F, _P, _P, _P, _P], _I32),
     "cgan3d_conv3d_bn_slots": ([_P], _I64),

@@ -306,9 +306,12 @@ class GeneratorPlan:
             if ly.kind == "convt":  # ConvTranspose3d: the output-grad is the gathered operand
                 self._on_side(lambda g=self.geo_wgrad[i], a=self.dz[i], b=xin, w=G[wname]:
                               ops.wgrad(g, a, b, w, self.ws_side))
-            else:
-                self._on_side(lambda g=self.geo_wgrad[i], a=xin, b=self.dz[i], w=G[wname]:
-                              ops.wgrad(g, a, b, w, self.ws_side))
+            else:  # ResNet layers: both operands' bf16 shadows (when present) feed the weight grad
+                x16 = self.y16[i - 1] if i > 0 else None
+                d16 = self.dz16[i] if BN_FUSED_BWD else None
+                self._on_side(lambda g=self.geo_wgrad[i], a=xin, b=self.dz[i], w=G[wname], a16=x16, b16=d16:
+                              ops.wgrad(g, a, b, w, self.ws_side, gathered16=a16 if b16 is not None else None,
+                                        aligned16=b16 if a16 is not None else None))
             if i == 0:
                 break
             # input-grad; a ResNet block0 also receives the skip gradient dL/dh_{r+1}

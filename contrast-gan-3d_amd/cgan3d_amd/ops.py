@@ -383,15 +383,17 @@ def wgrad_ws_floats(g: ConvGeom) -> int:
     return int(L.load().cgan3d_conv3d_wgrad_ws_floats(ctypes.byref(g)))
 
 
-def wgrad(g: ConvGeom, gathered, aligned, dw, ws, accumulate=False):
+def wgrad(g: ConvGeom, gathered, aligned, dw, ws, accumulate=False, gathered16=None, aligned16=None):
+    """Weight gradient; ``gathered16`` / ``aligned16``: optional bf16 shadows of the operands."""
     _need(gathered, _vox_in(g) * g.cin, "wgrad gathered")
     _need(aligned, _vox_out(g) * g.cout, "wgrad aligned")
     _need(dw, g.cin * g.cout * g.k**3, "wgrad dw")
     if _w_extent(g) > dw.numel():
         raise ValueError("wgrad: weight strides exceed dw")
     _need(ws, wgrad_ws_floats(g), "wgrad ws", exact=False)
-    check(_timed("wgrad", g, "cgan3d_conv3d_wgrad", ctypes.byref(g), ptr(gathered), ptr(aligned), ptr(dw),
-                 int(accumulate), ptr(ws)), "conv3d_wgrad")
+    check(_timed("wgrad", g, "cgan3d_conv3d_wgrad_ex", ctypes.byref(g), ptr(gathered), ptr(aligned), ptr(dw),
+                 int(accumulate), ptr(ws), _need16(gathered16, _vox_in(g) * g.cin, "wgrad gathered16"),
+                 _need16(aligned16, _vox_out(g) * g.cout, "wgrad aligned16")), "conv3d_wgrad")
 
 
 def bn_finalize(stats, nblk, c, gamma, beta, rmean, rvar, nbt, scale_shift, mean_invstd, momentum=0.1, eps=1e-5):

@@ -180,7 +180,8 @@ long long wgrad_s2_ws_floats(const cgan3d_conv_geom* g);
 void wgrad_s2_set_blocks(int v);
 int wgrad_s2_launch(const cgan3d_conv_geom* g, const float* gathered, const float* aligned, float* dw, int accumulate,
                     float* ws, hipStream_t st);
-int wgrad_k3_launch(const cgan3d_conv_geom* g, const float* gathered, const float* aligned, float* dw, int accumulate,
+int wgrad_k3_launch(const cgan3d_conv_geom* g, const float* gathered, const float* aligned, const __bf16* g16,
+                    const __bf16* a16, float* dw, int accumulate,
                     float* ws, hipStream_t st);
 int wgrad_c1_launch(const cgan3d_conv_geom* g, const float* gathered, const float* aligned, float* dw, hipStream_t st);
 void wgrad_bf16_set_blocks(int v);

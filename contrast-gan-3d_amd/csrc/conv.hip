@@ -518,6 +518,12 @@ extern "C" int64_t cgan3d_conv3d_wgrad_ws_floats(const cgan3d_conv_geom* g) {
 
 extern "C" int cgan3d_conv3d_wgrad(const cgan3d_conv_geom* g, const float* gathered, const float* aligned, float* dw,
                                    int32_t accumulate, float* ws, void* stream) {
+  return cgan3d_conv3d_wgrad_ex(g, gathered, aligned, dw, accumulate, ws, nullptr, nullptr, stream);
+}
+
+extern "C" int cgan3d_conv3d_wgrad_ex(const cgan3d_conv_geom* g, const float* gathered, const float* aligned, float* dw,
+                                      int32_t accumulate, float* ws, const void* gathered_bf16,
+                                      const void* aligned_bf16, void* stream) {
   int st = validate(g, "cgan3d_conv3d_wgrad");
   if (st) return st;
   CG_CHECK_ARG(!g->transposed, "cgan3d_conv3d_wgrad: use the forward mapping (see header)");
@@ -566,7 +572,8 @@ extern "C" int cgan3d_conv3d_wgrad(const cgan3d_conv_geom* g, const float* gathe
     return CGAN3D_OK;
   }
   if (wgrad_k3_ok(g)) {  // ResNet-block shape: per-block partials + reduce, no memset
-    int rc = wgrad_k3_launch(g, gathered, aligned, dw, accumulate, ws, s);
+    int rc = wgrad_k3_launch(g, gathered, aligned, reinterpret_cast<const __bf16*>(gathered_bf16),
+                             reinterpret_cast<const __bf16*>(aligned_bf16), dw, accumulate, ws, s);
     if (rc) return rc;
     CG_LAUNCH_CHECK("wgrad_k3_kernel");
     return CGAN3D_OK;

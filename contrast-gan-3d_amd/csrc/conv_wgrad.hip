@@ -281,7 +281,9 @@ int wgrad_bf16_launch(const cgan3d_conv_geom* g, const float* gathered, const fl
 // X halo is staged once per unit and serves all 9 taps.  16-channel chunks of a row are XOR-
 // swizzled by ((x >> 1) + 2y) & 3: the 8 rows a 32-lane half reads (4 consecutive x, 2 y) land
 // on 8 distinct 8-bank groups, for every tap.  Per-block partials go to ws[p][t][b][a] (plain
-// stores), wgrad_k3_reduce_kernel sums them into dW's layout.
+// stores), wgrad_k3_reduce_kernel sums them into dW's layout.  B16: both operands come from their
+// bf16 shadows (8-byte loads of the same 4 channels, stored as they are: half the bytes, no
+// conversion, bit-identical partials).
 namespace wk3 {
 constexpr int UPS = 4;                          // units per LDS stage
 constexpr int EX = 10, EY = 4;                  // X rows of one unit for one th: 4 (y) x 10 (x) voxels
@@ -306,8 +308,10 @@ struct Wk3Args {
   int upb;        // units per block (even)
 };
 
+template <bool B16>
 __global__ __launch_bounds__(512, 2) void wgrad_k3_kernel(Wk3Args a, const float* __restrict__ x,
-                                                          const float* __restrict__ dz, float* __restrict__ ws) {
+                                                          const float* __restrict__ dz, const __bf16* __restrict__ x16,
+                                                          const __bf16* __restrict__ dz16, float* __restrict__ ws) {
   // block = (voxel chunk p, tap row tdh = (td, th)): the 3 taps tw of that row x 64 x 64; 8 waves:
   // wave w owns input channels 16*(w & 3) .. +15 and output-channel tiles 2*(w >> 2), +1.  Nine
   // tap rows instead of one chunk per block keeps the split-K partials (P x |dW|) small.
@@ -331,7 +335,8 @@ __global__ __launch_bounds__(512, 2) void wgrad_k3_kernel(Wk3Args a, const float
     return r;
   };
   constexpr int NXK = XROWS * 16 / 512, NZK = ZROWS * 16 / 512;  // 5, 4 float4 per thread
-  f32x4 sx[2][NXK], sz[2][NZK];  // two stages of loads in flight (register slots)
+  using SV = std::conditional_t<B16, bf16x4_w, f32x4>;
+  SV sx[2][NXK], sz[2][NZK];  // two stages of loads in flight (register slots)
   auto load = [&](int s, int sl) {
     const Unit U0 = unit(u0 + UPS * s), U1 = unit(u0 + UPS * s + 1), U2 = unit(u0 + UPS * s + 2),
                U3 = unit(u0 + UPS * s + 3);
@@ -344,7 +349,8 @@ __global__ __launch_bounds__(512, 2) void wgrad_k3_kernel(Wk3Args a, const float
       const int iz = V.z + td - 1, iy = V.yb * 4 + hy + th - 1, ix = V.xb * 8 + hx - 1;
       const bool ok = V.ok && (unsigned)iz < (unsigned)a.d && (unsigned)iy < (unsigned)a.h && (unsigned)ix < (unsigned)a.w;
       const long long off = V.corner + (long long)(td - 1) * plane + (long long)(hy + th - 1) * a.w + (hx - 1);
-      sx[sl][k] = ok ? *reinterpret_cast<const f32x4*>(x + off * 64 + 4 * q4) : f32x4{0.f, 0.f, 0.f, 0.f};
+      if constexpr (B16) sx[sl][k] = ok ? *reinterpret_cast<const bf16x4_w*>(x16 + off * 64 + 4 * q4) : bf16x4_w{};
+      else sx[sl][k] = ok ? *reinterpret_cast<const f32x4*>(x + off * 64 + 4 * q4) : f32x4{0.f, 0.f, 0.f, 0.f};
     }
 #pragma unroll
     for (int k = 0; k < NZK; ++k) {
@@ -352,7 +358,8 @@ __global__ __launch_bounds__(512, 2) void wgrad_k3_kernel(Wk3Args a, const float
       const int u = row >> 5, r = row & 31;
       const Unit V = u == 0 ? U0 : (u == 1 ? U1 : (u == 2 ? U2 : U3));
       const long long off = V.corner + (long long)(r >> 3) * a.w + (r & 7);
-      sz[sl][k] = V.ok ? *reinterpret_cast<const f32x4*>(dz + off * 64 + 4 * q4) : f32x4{0.f, 0.f, 0.f, 0.f};
+      if constexpr (B16) sz[sl][k] = V.ok ? *reinterpret_cast<const bf16x4_w*>(dz16 + off * 64 + 4 * q4) : bf16x4_w{};
+      else sz[sl][k] = V.ok ? *reinterpret_cast<const f32x4*>(dz + off * 64 + 4 * q4) : f32x4{0.f, 0.f, 0.f, 0.f};
     }
   };
   auto store = [&](int buf, int sl) {
@@ -363,7 +370,8 @@ __global__ __launch_bounds__(512, 2) void wgrad_k3_kernel(Wk3Args a, const float
       const int r = row % (EX * EY);
       const int hy = r / EX, hx = r - hy * EX;
       bf16x4_w v;
-      v[0] = (__bf16)sx[sl][k][0]; v[1] = (__bf16)sx[sl][k][1]; v[2] = (__bf16)sx[sl][k][2]; v[3] = (__bf16)sx[sl][k][3];
+      if constexpr (B16) v = sx[sl][k];
+      else { v[0] = (__bf16)sx[sl][k][0]; v[1] = (__bf16)sx[sl][k][1]; v[2] = (__bf16)sx[sl][k][2]; v[3] = (__bf16)sx[sl][k][3]; }
       *reinterpret_cast<bf16x4_w*>(base + row * 128 + (((q4 >> 2) ^ swz(hx, hy)) * 32) + (q4 & 3) * 8) = v;
     }
 #pragma unroll
@@ -371,7 +379,8 @@ __global__ __launch_bounds__(512, 2) void wgrad_k3_kernel(Wk3Args a, const float
       const int row = rbase + 32 * k;
       const int r = row & 31;
       bf16x4_w v;
-      v[0] = (__bf16)sz[sl][k][0]; v[1] = (__bf16)sz[sl][k][1]; v[2] = (__bf16)sz[sl][k][2]; v[3] = (__bf16)sz[sl][k][3];
+      if constexpr (B16) v = sz[sl][k];
+      else { v[0] = (__bf16)sz[sl][k][0]; v[1] = (__bf16)sz[sl][k][1]; v[2] = (__bf16)sz[sl][k][2]; v[3] = (__bf16)sz[sl][k][3]; }
       *reinterpret_cast<bf16x4_w*>(base + (XROWS + row) * 128 + (((q4 >> 2) ^ swz(r & 7, r >> 3)) * 32) + (q4 & 3) * 8) = v;
     }
   };
@@ -594,12 +603,15 @@ long long wgrad_k3_ws_floats(const cgan3d_conv_geom* g) {
   return (long long)P * 27 * 64 * 64;
 }
 
-int wgrad_k3_launch(const cgan3d_conv_geom* g, const float* gathered, const float* aligned, float* dw, int accumulate,
-                    float* ws, hipStream_t st) {
+int wgrad_k3_launch(const cgan3d_conv_geom* g, const float* gathered, const float* aligned, const __bf16* g16,
+                    const __bf16* a16, float* dw, int accumulate, float* ws, hipStream_t st) {
   Wk3Args a;
   int P;
   wgrad_k3_geometry(g, &a, &P);
-  ::cg::launch(wgrad_k3_kernel, dim3(P, 9), dim3(512), 0, st, a, gathered, aligned, ws);
+  if (g16 && a16)
+    ::cg::launch(wgrad_k3_kernel<true>, dim3(P, 9), dim3(512), 0, st, a, gathered, aligned, g16, a16, ws);
+  else
+    ::cg::launch(wgrad_k3_kernel<false>, dim3(P, 9), dim3(512), 0, st, a, gathered, aligned, g16, a16, ws);
   ::cg::launch(wgrad_k3_reduce_kernel, dim3(64, 4), dim3(448), 0, st, (const float*)ws, P, 64, 64, dw, (long long)g->w_sa,
                (long long)g->w_sb, accumulate);
   return CGAN3D_OK;

@@ -141,6 +141,11 @@ int cgan3d_conv3d_fwd(const cgan3d_conv_geom* g, const float* x, const float* w,
 int64_t cgan3d_conv3d_wgrad_ws_floats(const cgan3d_conv_geom* g);
 int cgan3d_conv3d_wgrad(const cgan3d_conv_geom* g, const float* gathered, const float* aligned,
                         float* dw, int32_t accumulate, float* ws, void* stream);
+/* The same with optional bf16 shadows of both operands (same layouts, NULL = none): the ResNet-
+ * block weight-grad kernel then stages them as they are (bit-identical: it rounds to bf16 anyway). */
+int cgan3d_conv3d_wgrad_ex(const cgan3d_conv_geom* g, const float* gathered, const float* aligned,
+                           float* dw, int32_t accumulate, float* ws, const void* gathered_bf16,
+                           const void* aligned_bf16, void* stream);
 
 /* --- BatchNorm3d, training mode (model/blocks.py:26-27,45; torch.nn.BatchNorm3d) --- */
 int cgan3d_bn_finalize(const float* stats, int64_t nblk, int32_t c, const float* gamma,
