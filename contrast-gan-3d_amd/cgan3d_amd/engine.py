@@ -188,12 +188,11 @@ class GeneratorPlan:
         self.ws = torch.empty(ws, device=device)
         # bf16 shadows of conv inputs (forward: the previous BatchNorm's output; input-grad: the
         # layer's own BatchNorm input-grad), written by the BatchNorm pass that produces the fp32
-        # tensor: the halo-staging kernels (ResNet-block conv_k3, the last k7 conv) copy their halo
-        # from half the bytes with no conversion.  bf16 mode only (those kernels round to bf16
-        # anyway): results are bit-identical with or without.  The stride-2 S2F / S2T kernels take
-        # shadows too (tests/test_gpu_ops.py) but are not given any: measured at 64^3, the extra
-        # shadow writes in the BatchNorm passes cost what S2F saves, and S2T is bound by its output.
-        shadow_kinds = {("conv", 3, 1, 64, 64)}
+        # tensor: the halo-staging kernels (ResNet-block conv_k3, the stride-2 S2F / S2T kernels,
+        # the last k7 conv) copy their halo from half the bytes with no conversion, and the
+        # ResNet / stride-2 weight grads read both operands from them.  bf16 mode only (those
+        # kernels round to bf16 anyway): results are bit-identical with or without.
+        shadow_kinds = {("conv", 3, 1, 64, 64), ("conv", 3, 2, 16, 32), ("convt", 3, 2, 32, 16)}
         self.y16, self.dz16 = [None] * len(layers), [None] * len(layers)
 
         def bf(dd, c):
@@ -303,15 +302,17 @@ class GeneratorPlan:
                                 ly.act, G[f"{nb}.weight"], G[f"{nb}.bias"], self.dz[i], self.ws)
             xin = self.y[i - 1] if i > 0 else x
             wname = f"{ly.name}.conv.weight"
+            # both operands' bf16 shadows, when the layer has them, feed the weight grad
+            x16 = self.y16[i - 1] if i > 0 else None
+            d16 = self.dz16[i] if BN_FUSED_BWD else None
+            if x16 is None or d16 is None:
+                x16 = d16 = None
             if ly.kind == "convt":  # ConvTranspose3d: the output-grad is the gathered operand
-                self._on_side(lambda g=self.geo_wgrad[i], a=self.dz[i], b=xin, w=G[wname]:
-                              ops.wgrad(g, a, b, w, self.ws_side))
-            else:  # ResNet layers: both operands' bf16 shadows (when present) feed the weight grad
-                x16 = self.y16[i - 1] if i > 0 else None
-                d16 = self.dz16[i] if BN_FUSED_BWD else None
+                self._on_side(lambda g=self.geo_wgrad[i], a=self.dz[i], b=xin, w=G[wname], a16=d16, b16=x16:
+                              ops.wgrad(g, a, b, w, self.ws_side, gathered16=a16, aligned16=b16))
+            else:
                 self._on_side(lambda g=self.geo_wgrad[i], a=xin, b=self.dz[i], w=G[wname], a16=x16, b16=d16:
-                              ops.wgrad(g, a, b, w, self.ws_side, gathered16=a16 if b16 is not None else None,
-                                        aligned16=b16 if a16 is not None else None))
+                              ops.wgrad(g, a, b, w, self.ws_side, gathered16=a16, aligned16=b16))
             if i == 0:
                 break
             # input-grad; a ResNet block0 also receives the skip gradient dL/dh_{r+1}

@@ -178,8 +178,8 @@ void wgrad_k3_set_chunks(int v);
 bool wgrad_s2_ok(const cgan3d_conv_geom* g);
 long long wgrad_s2_ws_floats(const cgan3d_conv_geom* g);
 void wgrad_s2_set_blocks(int v);
-int wgrad_s2_launch(const cgan3d_conv_geom* g, const float* gathered, const float* aligned, float* dw, int accumulate,
-                    float* ws, hipStream_t st);
+int wgrad_s2_launch(const cgan3d_conv_geom* g, const float* gathered, const float* aligned, const __bf16* g16,
+                    const __bf16* a16, float* dw, int accumulate, float* ws, hipStream_t st);
 int wgrad_k3_launch(const cgan3d_conv_geom* g, const float* gathered, const float* aligned, const __bf16* g16,
                     const __bf16* a16, float* dw, int accumulate,
                     float* ws, hipStream_t st);

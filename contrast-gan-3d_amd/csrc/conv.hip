@@ -566,7 +566,8 @@ extern "C" int cgan3d_conv3d_wgrad_ex(const cgan3d_conv_geom* g, const float* ga
     return CGAN3D_OK;
   }
   if (wgrad_s2_ok(g)) {  // stride-2 16 <-> 32 levels: per-block partials + reduce, no memset
-    int rc = wgrad_s2_launch(g, gathered, aligned, dw, accumulate, ws, s);
+    int rc = wgrad_s2_launch(g, gathered, aligned, reinterpret_cast<const __bf16*>(gathered_bf16),
+                             reinterpret_cast<const __bf16*>(aligned_bf16), dw, accumulate, ws, s);
     if (rc) return rc;
     CG_LAUNCH_CHECK("wgrad_s2_kernel");
     return CGAN3D_OK;

@@ -489,8 +489,10 @@ struct Ws2Args {
   int slabs, spb;  // slabs in all, per block
 };
 
+template <bool B16>  // both operands from bf16 shadows (as wgrad_k3_kernel)
 __global__ __launch_bounds__(512) void wgrad_s2_kernel(Ws2Args a, const float* __restrict__ x,
-                                                       const float* __restrict__ dz, float* __restrict__ ws) {
+                                                       const float* __restrict__ dz, const __bf16* __restrict__ x16,
+                                                       const __bf16* __restrict__ dz16, float* __restrict__ ws) {
   using namespace ws2;
   __shared__ __attribute__((aligned(16))) unsigned char smem[XBYTES + ZBYTES];
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -498,7 +500,8 @@ __global__ __launch_bounds__(512) void wgrad_s2_kernel(Ws2Args a, const float* _
   const int p = blockIdx.x;
   const int s0 = p * a.spb, s1 = min(s0 + a.spb, a.slabs);
   const int yg_n = a.ho >> 2, xc_n = a.wo >> 5;
-  f32x4 rx[NXT], rz[2];
+  using SV = std::conditional_t<B16, bf16x4_w, f32x4>;
+  SV rx[NXT], rz[2];
   auto load = [&](int sl) {
     const int xc = sl % xc_n, q1 = sl / xc_n, yg = q1 % yg_n, zq = q1 / yg_n;  // zq = nb * do + oz
     const int oz = zq % a.do_, nb = zq / a.do_;
@@ -509,14 +512,17 @@ __global__ __launch_bounds__(512) void wgrad_s2_kernel(Ws2Args a, const float* _
       const int c = v % XW, r = (v / XW) % 9, pl = v / (9 * XW);
       const int iz = iz0 + pl, iy = iy0 + r, ix = ix0 + c;
       const bool ok = i < NX && (unsigned)iz < (unsigned)a.di && (unsigned)iy < (unsigned)a.hi && (unsigned)ix < (unsigned)a.wi;
-      rx[k] = ok ? *reinterpret_cast<const f32x4*>(x + ((((long long)nb * a.di + iz) * a.hi + iy) * a.wi + ix) * 16 + 4 * q4)
-                 : f32x4{0.f, 0.f, 0.f, 0.f};
+      const long long o = ((((long long)nb * a.di + iz) * a.hi + iy) * a.wi + ix) * 16 + 4 * q4;
+      if constexpr (B16) rx[k] = ok ? *reinterpret_cast<const bf16x4_w*>(x16 + o) : bf16x4_w{};
+      else rx[k] = ok ? *reinterpret_cast<const f32x4*>(x + o) : f32x4{0.f, 0.f, 0.f, 0.f};
     }
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
       const int i = tid + 512 * k, q8 = i & 7, v = i >> 3;  // v = u * 32 + ox
       const int oy = 4 * yg + (v >> 5), ox = 32 * xc + (v & 31);
-      rz[k] = *reinterpret_cast<const f32x4*>(dz + ((((long long)nb * a.do_ + oz) * a.ho + oy) * a.wo + ox) * 32 + 4 * q8);
+      const long long o = ((((long long)nb * a.do_ + oz) * a.ho + oy) * a.wo + ox) * 32 + 4 * q8;
+      if constexpr (B16) rz[k] = *reinterpret_cast<const bf16x4_w*>(dz16 + o);
+      else rz[k] = *reinterpret_cast<const f32x4*>(dz + o);
     }
   };
   auto store = [&]() {
@@ -526,7 +532,8 @@ __global__ __launch_bounds__(512) void wgrad_s2_kernel(Ws2Args a, const float* _
       if (i >= NX) break;
       const int c = v % XW, r = (v / XW) % 9, pl = v / (9 * XW);
       bf16x4_w h;
-      h[0] = (__bf16)rx[k][0]; h[1] = (__bf16)rx[k][1]; h[2] = (__bf16)rx[k][2]; h[3] = (__bf16)rx[k][3];
+      if constexpr (B16) h = rx[k];
+      else { h[0] = (__bf16)rx[k][0]; h[1] = (__bf16)rx[k][1]; h[2] = (__bf16)rx[k][2]; h[3] = (__bf16)rx[k][3]; }
       *reinterpret_cast<bf16x4_w*>(smem + (pl * XPS + r * XRS + xcol(c)) * 32 + q4 * 8) = h;
     }
 #pragma unroll
@@ -534,7 +541,8 @@ __global__ __launch_bounds__(512) void wgrad_s2_kernel(Ws2Args a, const float* _
       const int i = tid + 512 * k, q8 = i & 7, v = i >> 3, ox = v & 31;
       const int ph = (q8 >> 2) ^ ((ox >> 3) & 1);
       bf16x4_w h;
-      h[0] = (__bf16)rz[k][0]; h[1] = (__bf16)rz[k][1]; h[2] = (__bf16)rz[k][2]; h[3] = (__bf16)rz[k][3];
+      if constexpr (B16) h = rz[k];
+      else { h[0] = (__bf16)rz[k][0]; h[1] = (__bf16)rz[k][1]; h[2] = (__bf16)rz[k][2]; h[3] = (__bf16)rz[k][3]; }
       *reinterpret_cast<bf16x4_w*>(smem + XBYTES + v * 64 + ph * 32 + (q8 & 3) * 8) = h;
     }
   };
@@ -643,12 +651,13 @@ long long wgrad_s2_ws_floats(const cgan3d_conv_geom* g) {
   return (long long)P * 27 * 16 * 32;
 }
 
-int wgrad_s2_launch(const cgan3d_conv_geom* g, const float* gathered, const float* aligned, float* dw, int accumulate,
-                    float* ws, hipStream_t st) {
+int wgrad_s2_launch(const cgan3d_conv_geom* g, const float* gathered, const float* aligned, const __bf16* g16,
+                    const __bf16* a16, float* dw, int accumulate, float* ws, hipStream_t st) {
   Ws2Args a;
   int P;
   wgrad_s2_geometry(g, &a, &P);
-  ::cg::launch(wgrad_s2_kernel, dim3(P), dim3(512), 0, st, a, gathered, aligned, ws);
+  if (g16 && a16) ::cg::launch(wgrad_s2_kernel<true>, dim3(P), dim3(512), 0, st, a, gathered, aligned, g16, a16, ws);
+  else ::cg::launch(wgrad_s2_kernel<false>, dim3(P), dim3(512), 0, st, a, gathered, aligned, g16, a16, ws);
   ::cg::launch(wgrad_k3_reduce_kernel, dim3(32, 1), dim3(448), 0, st, (const float*)ws, P, 16, 32, dw,
                (long long)g->w_sa, (long long)g->w_sb, accumulate);
   return CGAN3D_OK;

@@ -406,9 +406,9 @@ def test_wgrad_bf16(cin, cout, k, s, p, reflect, sp):
     dwo = torch.empty(w.shape, device="cuda")
     ops.wgrad(gw, _cl(x), _cl(gy), dwo, ws)
     assert_close(dwo.double().cpu().numpy(), dw.numpy(), 2e-2, "bf16 wgrad")
-    if (cin, cout, k, s) == (64, 64, 3, 1) and sp[1] % 4 == 0 and sp[2] % 8 == 0:
-        # wgrad_k3_kernel (the generic kernel ignores shadows and sums with atomics, so no
-        # bitwise comparison there): both operands from bf16 shadows, bit-identical partials
+    if ((cin, cout, k, s) == (64, 64, 3, 1) and sp[1] % 4 == 0 and sp[2] % 8 == 0) or tuple(sp) == (8, 16, 64):
+        # wgrad_k3_kernel / wgrad_s2_kernel (the generic kernel ignores shadows and sums with
+        # atomics, so no bitwise comparison there): both operands from bf16 shadows, bit-identical
         dw16 = torch.empty_like(dwo)
         ops.wgrad(gw, _cl(x), _cl(gy), dw16, ws, gathered16=_cl(x).bfloat16(), aligned16=_cl(gy).bfloat16())
         assert torch.equal(dw16, dwo), "bf16-shadow weight grad differs"
@@ -433,6 +433,10 @@ def test_wgrad_bf16_conv_transpose(cin, cout, sp):
     dwo = torch.empty(w.shape, device="cuda")
     ops.wgrad(gw, _cl(gy), _cl(x), dwo, ws)
     assert_close(dwo.double().cpu().numpy(), dw.numpy(), 2e-2, "bf16 convT wgrad")
+    if cin == 32:  # wgrad_s2_kernel from both operands' bf16 shadows: bit-identical
+        dw16 = torch.empty_like(dwo)
+        ops.wgrad(gw, _cl(gy), _cl(x), dw16, ws, gathered16=_cl(gy).bfloat16(), aligned16=_cl(x).bfloat16())
+        assert torch.equal(dw16, dwo), "bf16-shadow convT weight grad differs"
 
 
 S2_CASES = [
