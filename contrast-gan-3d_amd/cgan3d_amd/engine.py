@@ -188,11 +188,12 @@ class GeneratorPlan:
         self.ws = torch.empty(ws, device=device)
         # bf16 shadows of conv inputs (forward: the previous BatchNorm's output; input-grad: the
         # layer's own BatchNorm input-grad), written by the BatchNorm pass that produces the fp32
-        # tensor: the halo-staging kernels (ResNet-block conv_k3, the stride-2 S2F / S2T kernels,
-        # the last k7 conv) copy their halo from half the bytes with no conversion, and the
+        # tensor: the halo-staging kernels (ResNet-block conv_k3, the stride-2 S2F / S2T and
+        # 32 <-> 64 halo kernels, the last k7 conv) copy their halo from half the bytes with no conversion, and the
         # ResNet / stride-2 weight grads read both operands from them.  bf16 mode only (those
         # kernels round to bf16 anyway): results are bit-identical with or without.
-        shadow_kinds = {("conv", 3, 1, 64, 64), ("conv", 3, 2, 16, 32), ("convt", 3, 2, 32, 16)}
+        shadow_kinds = {("conv", 3, 1, 64, 64), ("conv", 3, 2, 16, 32), ("convt", 3, 2, 32, 16),
+                        ("conv", 3, 2, 32, 64), ("convt", 3, 2, 64, 32)}
         self.y16, self.dz16 = [None] * len(layers), [None] * len(layers)
 
         def bf(dd, c):

@@ -275,8 +275,22 @@ __global__ __launch_bounds__(256) void conv_halo_kernel(HaloArgs a, const float*
   if (ntap > 0) issue(0);
   if (ntap > 1) issue(1);
 
-  // ---- halo: fp32 NDHWC -> bf16 LDS (zero outside the gathered volume)
-  {
+  // ---- halo: fp32 NDHWC -> bf16 LDS (zero outside the gathered volume); with a bf16 shadow of
+  // x (ep.x16) 16-byte granules are copied as they are
+  if (ep.x16) {
+    const int nvox = a.ez * a.ey * a.ex;
+    constexpr int C8 = CIN / 8;
+    for (int i = tid; i < nvox * C8; i += 256) {
+      const int v = i / C8, c8 = i - v * C8;
+      const int hx = v % a.ex, hy = (v / a.ex) % a.ey, hz = v / (a.ex * a.ey);
+      const int iz = oz + hz, iy = oy + hy, ix = ox + hx;
+      bf16x8_h val = {};
+      if (iz >= 0 && iz < a.di && iy >= 0 && iy < a.hi && ix >= 0 && ix < a.wi)
+        val = *reinterpret_cast<const bf16x8_h*>(ep.x16 + (((long long)(nb * a.di + iz) * a.hi + iy) * a.wi + ix) * CIN +
+                                                 8 * c8);
+      *reinterpret_cast<bf16x8_h*>(halo + v * ROW + 8 * c8) = val;
+    }
+  } else {
     const int nvox = a.ez * a.ey * a.ex;
     constexpr int C4 = CIN / 4;
     for (int i = tid; i < nvox * C4; i += 256) {
