@@ -240,3 +240,33 @@ def test_plan_replay_matches_eager(prec):
     for a1, a2 in ((eager.g_arena, planned.g_arena), (eager.d_arena, planned.d_arena)):
         g1, g2 = a1.grad.cpu().numpy(), a2.grad.cpu().numpy()
         assert np.abs(g1 - g2).max() <= 1e-3 * np.abs(g1).max()
+
+
+def test_bf16_shadows_match_fp32_staging(monkeypatch):
+    """The bf16 input shadows (BatchNorm passes writing bf16 copies that the halo / weight-grad
+    kernels stage from) change no arithmetic: a 64^3 bf16 step with them matches the step without
+    (CGAN3D_NO_SHADOW=1) up to the atomics order of the generic weight-grad kernels."""
+    from cgan3d_amd.data.synthetic import synth_patches
+    from cgan3d_amd.engine import StepEngine
+    g_args = dict(n_resnet_blocks=2, n_updownsample_blocks=2, init_channels_out=16)
+    S, b = 64, 1
+    engs = []
+    for off in (False, True):
+        if off:
+            monkeypatch.setenv("CGAN3D_NO_SHADOW", "1")
+        g, d = _models(g_args)
+        engs.append(StepEngine(g, d, g.config, d.config, b, b, (S, S, S), precision="bf16"))
+    with_s, without = engs
+    assert sum(t is not None for t in with_s.G.y16 + with_s.G.dz16) >= 8
+    assert all(t is None for t in without.G.y16 + without.G.dz16)
+    opt, _ = synth_patches(b, S, 7)
+    sub, seg = synth_patches(b, S, 8)
+    bt = (torch.from_numpy(opt).cuda(), torch.from_numpy(sub).cuda(), torch.from_numpy(seg).cuda(),
+          torch.full((b,), 0.4, device="cuda"))
+    for e in engs:
+        e.load_inputs(*bt)
+        e.step()
+    np.testing.assert_allclose(with_s.losses.cpu().numpy(), without.losses.cpu().numpy(), rtol=1e-4, atol=2e-5)
+    for a1, a2 in ((with_s.g_arena, without.g_arena), (with_s.d_arena, without.d_arena)):
+        g1, g2 = a1.grad.cpu().numpy(), a2.grad.cpu().numpy()
+        assert np.abs(g1 - g2).max() <= 1e-3 * np.abs(g1).max()
