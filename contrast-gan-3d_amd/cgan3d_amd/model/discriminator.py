@@ -65,9 +65,21 @@ class PatchGANDiscriminator(nn.Module):
     def _tensors(self):
         return dict(self.state_dict(keep_vars=True))  # parameters and BatchNorm buffers
 
-    def plan_for(self, n, dims):
+    def plan_for(self, n, dims, fresh: bool = False):
+        """The critic plan for an ``n``-sample batch of ``dims`` patches: cached per shape (buffers
+        are allocated once; the packed weight copies are refreshed on every call, the weights may
+        have changed).  ``fresh`` plans own their buffers until the caller drops them (the autograd
+        paths keep activations for their backward)."""
         from ..engine import CriticPlan
-        return CriticPlan(self.config, n, tuple(dims), self.model.first.conv.weight.device, self._tensors())
+        dev = self.model.first.conv.weight.device
+        key = (n, tuple(dims), dev, tuple(p.data_ptr() for p in self.parameters()))
+        if fresh:
+            return CriticPlan(self.config, n, tuple(dims), dev, self._tensors())
+        if getattr(self, "_plan", None) is None or self._plan[0] != key:
+            self._plan = (key, CriticPlan(self.config, n, tuple(dims), dev, self._tensors()))
+        else:
+            self._plan[1].pack()
+        return self._plan[1]
 
     def forward(self, x: Tensor) -> Tensor:
         if self._unsupported:
@@ -88,7 +100,7 @@ class _CriticFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, module, *params):
         n, _, *dims = x.shape
-        plan = module.plan_for(n, dims)
+        plan = module.plan_for(n, dims, fresh=True)  # activations live until backward
         xc = x.detach().float().contiguous().view(n, *dims, 1)
         logits = plan.forward(module._tensors(), xc, 0, n, training=module.training)
         ctx.plan, ctx.module, ctx.xc, ctx.needs_x = plan, module, xc, x.requires_grad

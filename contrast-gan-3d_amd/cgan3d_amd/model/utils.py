@@ -38,7 +38,7 @@ class _GradientPenaltyFn(torch.autograd.Function):
     def forward(ctx, real, fake, eps, critic, lambda_, *params):
         from .. import ops
         n, _, *dims = real.shape
-        plan = critic.plan_for(n, dims)
+        plan = critic.plan_for(n, dims, fresh=True)  # kept until backward
         P = critic._tensors()
         V = dims[0] * dims[1] * dims[2]
         x = torch.empty((n, *dims, 1), device=real.device)

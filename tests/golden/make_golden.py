@@ -16,8 +16,9 @@ Fixtures (all fp32, CPU, torch as installed here — recorded in each file's ``t
   d_fwd_*.npz     PatchGANDiscriminator forward (GP conf: Identity norm; BN conf)
   losses.npz      ZNCCLoss / HULoss / WassersteinLoss values and input gradients
   gp.npz          wgan_gradient_penalty value + critic parameter gradients (eps injected)
-  step_*.npz      Trainer.train_step over 3 iterations (GP conf and weight-clip conf):
-                  losses, gradients seen by each optimizer step, final params & buffers
+  step_*.npz      Trainer.train_step over 1-3 iterations (GP conf and weight-clip conf):
+                  losses, gradients seen by each optimizer step, final params & buffers; per
+                  iteration the entering state and a float64 re-run of that iteration
 """
 from __future__ import annotations
 
@@ -182,12 +183,9 @@ class _NullLogger:
         pass
 
 
-def train_steps(tag, g_args, gp: bool, S, b_opt, b_low, b_high, iters, seed, save_final_g=True,
-                dtype=torch.float32, save=True):
-    """Trainer.train_step (Trainer.py:163-203) with train_{critic,generator}_every = 1.
-
-    ``dtype=torch.float64`` runs the reference itself in double precision (modules ``.double()``,
-    inputs in double): the exact-arithmetic yardstick for the parity tests."""
+def _make_trainer(g_args, gp: bool, S, b_low, b_high, iters, dtype):
+    """A reference Trainer for the fixture runs; ``dtype=torch.float64`` converts the modules, the
+    optimisers and the HU constants to double (the exact-arithmetic yardstick)."""
     d_extra = dict(norm_layer=torch.nn.Identity) if gp else {}
     lr, betas = (1e-4, (0.0, 0.9)) if gp else (2e-4, (0.5, 0.999))
     lo, hi = scaled_hu_bounds()
@@ -210,22 +208,95 @@ def train_steps(tag, g_args, gp: bool, S, b_opt, b_low, b_high, iters, seed, sav
         tr.optimizer_D = partial(torch.optim.Adam, lr=lr, betas=betas)(tr.critic.parameters())
         tr.loss_HU.min_HU = tr.loss_HU.min_HU.to(dtype)  # loss.py:51-56 constants
         tr.loss_HU.max_HU = tr.loss_HU.max_HU.to(dtype)
-    out = {}
-    grads = {"G": [], "D": []}
-
-    def snap(opt, model, key):
-        orig = opt.step
-
-        def step(*a, **k):
-            grads[key].append({n: p.grad.detach().clone().numpy() for n, p in model.named_parameters()
-                               if p.grad is not None})
-            return orig(*a, **k)
-        opt.step = step
-
-    snap(tr.optimizer_G, tr.generator, "G")
-    snap(tr.optimizer_D, tr.critic, "D")
     tr.generator.train()
     tr.critic.train()
+    return tr, lr, betas
+
+
+def _snapshot(tr):
+    """Everything the next iteration depends on: both state_dicts (parameters + BatchNorm buffers)
+    and both Adam states (deep copies)."""
+    import copy
+    return {"G": copy.deepcopy(tr.generator.state_dict()), "D": copy.deepcopy(tr.critic.state_dict()),
+            "optG": copy.deepcopy(tr.optimizer_G.state_dict()), "optD": copy.deepcopy(tr.optimizer_D.state_dict())}
+
+
+def _restore(tr, snap):
+    tr.generator.load_state_dict(snap["G"])
+    tr.critic.load_state_dict(snap["D"])
+    tr.optimizer_G.load_state_dict(snap["optG"])  # moments cast to the parameters' dtype by torch
+    tr.optimizer_D.load_state_dict(snap["optD"])
+
+
+def _state_arrays(tr, snap, it):
+    """Fixture entries of the state entering iteration ``it``: the GPU test loads it, so every
+    iteration's gradients are checked from the reference's own state (not from a state the device
+    reached by itself, which differs by Adam's sign flips of sub-noise gradient elements)."""
+    out = {}
+    for net, mod, optk in (("G", tr.generator, "optG"), ("D", tr.critic, "optD")):
+        for k, v in snap[net].items():
+            out[f"it{it}/state/{net}/{k}"] = v.detach().cpu().numpy().copy()
+        st = snap[optk]["state"]
+        for idx, (n, _) in enumerate(mod.named_parameters()):
+            if idx in st:
+                out[f"it{it}/adam/{net}/{n}/exp_avg"] = st[idx]["exp_avg"].detach().cpu().numpy().copy()
+                out[f"it{it}/adam/{net}/{n}/exp_avg_sq"] = st[idx]["exp_avg_sq"].detach().cpu().numpy().copy()
+                out[f"it{it}/adam/{net}/step"] = np.float32(float(st[idx]["step"]))
+    return out
+
+
+def _run_iteration(tr, gp, inputs, it, dtype):
+    """One Trainer.train_step on ``inputs``; returns (logged losses, {"G": grads, "D": grads}) with
+    the gradients each optimiser step consumed."""
+    opt, low, low_seg, high, high_seg, eps = inputs
+    grads = {}
+
+    def snap(optim, model, key):
+        orig = optim.step
+
+        def step(*a, **k):
+            grads[key] = {n: p.grad.detach().clone().numpy() for n, p in model.named_parameters()
+                          if p.grad is not None}
+            return orig(*a, **k)
+        optim.step = step
+        return orig
+
+    og = snap(tr.optimizer_G, tr.generator, "G")
+    od = snap(tr.optimizer_D, tr.critic, "D")
+    patches = [{"data": torch.from_numpy(opt).to(dtype)},
+               {"data": torch.from_numpy(low).to(dtype), "seg": torch.from_numpy(low_seg)},
+               {"data": torch.from_numpy(high).to(dtype), "seg": torch.from_numpy(high_seg)}]
+    logged = {}
+    orig_c, orig_g = tr.train_critic, tr.train_generator
+
+    def tc(*a, **k):
+        r = orig_c(*a, **k)
+        logged.update(r)
+        return r
+
+    def tg(*a, **k):
+        r = orig_g(*a, **k)
+        logged.update(r)
+        return r
+    tr.train_critic, tr.train_generator = tc, tg
+    ctx = injected_rand([torch.from_numpy(eps).to(dtype)]) if gp else contextlib.nullcontext()
+    with ctx:
+        tr.train_step(patches, it)
+    tr.train_critic, tr.train_generator = orig_c, orig_g
+    tr.optimizer_G.step, tr.optimizer_D.step = og, od
+    return {k: v.detach().numpy() for k, v in logged.items()}, grads
+
+
+def train_steps(tag, g_args, gp: bool, S, b_opt, b_low, b_high, iters, seed, save_final_g=True):
+    """Trainer.train_step (Trainer.py:163-203) with train_{critic,generator}_every = 1, ``iters``
+    iterations in float32 (the reference's precision).
+
+    For every iteration the fixture also holds the state entering it (``it{k}/state``,
+    ``it{k}/adam``, k > 0) and the same iteration re-run in float64 from that state
+    (``it{k}/grad64``, ``it{k}/loss64``): the exact-arithmetic yardstick the GPU test holds each
+    iteration to."""
+    tr, lr, betas = _make_trainer(g_args, gp, S, b_low, b_high, iters, torch.float32)
+    out = {}
     rngs = np.random.Generator(np.random.PCG64(seed + 100))
     for it in range(iters):
         opt, _ = synth_patches(b_opt, S, seed + 10 * it)
@@ -233,54 +304,35 @@ def train_steps(tag, g_args, gp: bool, S, b_opt, b_low, b_high, iters, seed, sav
         high, high_seg = synth_patches(b_high, S, seed + 10 * it + 2)
         low = low - 0.3  # hypo-enhanced (LOW) / hyper-enhanced (HIGH) flavour
         high = high + 0.3
-        eps = torch.from_numpy(rngs.random((min(b_opt, b_low + b_high), 1, 1, 1, 1)).astype(np.float32))
-        patches = [{"data": torch.from_numpy(opt).to(dtype)},
-                   {"data": torch.from_numpy(low).to(dtype), "seg": torch.from_numpy(low_seg)},
-                   {"data": torch.from_numpy(high).to(dtype), "seg": torch.from_numpy(high_seg)}]
-        eps = eps.to(dtype)
-        logged = {}
-        orig_c, orig_g = tr.train_critic, tr.train_generator
-
-        def tc(*a, **k):
-            r = orig_c(*a, **k)
-            logged.update(r)
-            return r
-
-        def tg(*a, **k):
-            r = orig_g(*a, **k)
-            logged.update(r)
-            return r
-        tr.train_critic, tr.train_generator = tc, tg
-        ctx = injected_rand([eps]) if gp else contextlib.nullcontext()
-        with ctx:
-            tr.train_step(patches, it)
-        tr.train_critic, tr.train_generator = orig_c, orig_g
+        eps = rngs.random((min(b_opt, b_low + b_high), 1, 1, 1, 1)).astype(np.float32)
+        inputs = (opt, low, low_seg, high, high_seg, eps)
+        snap = _snapshot(tr)
+        if it > 0:
+            out.update(_state_arrays(tr, snap, it))
+        losses, grads = _run_iteration(tr, gp, inputs, it, torch.float32)
+        # the same iteration in float64 from the same state
+        tr64, _, _ = _make_trainer(g_args, gp, S, b_low, b_high, iters, torch.float64)
+        _restore(tr64, snap)
+        losses64, grads64 = _run_iteration(tr64, gp, inputs, it, torch.float64)
         out[f"it{it}/opt"] = opt
         out[f"it{it}/low"] = low
         out[f"it{it}/high"] = high
         out[f"it{it}/low_seg"] = low_seg
         out[f"it{it}/high_seg"] = high_seg
-        out[f"it{it}/eps"] = eps.numpy()
-        for k, v in logged.items():
-            out[f"it{it}/loss/{k}"] = v.detach().numpy()
-    for key in ("G", "D"):
-        for it, gdict in enumerate(grads[key]):
-            for n, g in gdict.items():
+        out[f"it{it}/eps"] = eps
+        for k, v in losses.items():
+            out[f"it{it}/loss/{k}"] = v
+            out[f"it{it}/loss64/{k}"] = np.asarray(losses64[k], dtype=np.float32)
+        for key in ("G", "D"):
+            for n, g in grads[key].items():
                 out[f"it{it}/grad/{key}/{n}"] = g
+                out[f"it{it}/grad64/{key}/{n}"] = np.asarray(grads64[key][n], dtype=np.float32)
     if save_final_g:
         out.update(sd_np(tr.generator, "final/G/"))
     out.update(sd_np(tr.critic, "final/D/"))
     meta = dict(S=S, b_opt=b_opt, b_low=b_low, b_high=b_high, iters=iters, gp=int(gp), lr=lr,
-                beta1=betas[0], beta2=betas[1], **{f"g_{k}": v for k, v in g_args.items()})
-    if not save:
-        return out
-    if dtype == torch.float32:
-        # iteration 0 once more in float64 (identical start state): the exact-arithmetic yardstick
-        o64 = train_steps(tag, g_args, gp, S, b_opt, b_low, b_high, 1, seed, dtype=torch.float64, save=False)
-        for k, v in o64.items():
-            if k.startswith("it0/grad/") or k.startswith("it0/loss/"):
-                out[k.replace("it0/grad/", "it0/grad64/").replace("it0/loss/", "it0/loss64/")] = \
-                    np.asarray(v, dtype=np.float32)
+                beta1=betas[0], beta2=betas[1], teacher_forced=1,
+                **{f"g_{k}": v for k, v in g_args.items()})
     np.savez_compressed(HERE / f"step_{tag}.npz", torch_version=torch.__version__,
                         meta=np.array(repr(meta)), **out)
 

@@ -108,3 +108,39 @@ def test_train_step(golden, tag):
         assert [k.split("/", 2)[2] for k in keys] == list(p.keys())  # same state_dict layout & order
         for k in keys:
             assert_close(p[k.split("/", 2)[2]].numpy(), f[k], 1e-3, k)
+
+
+@pytest.mark.parametrize("tag", ["gp_small", "clip_small"])
+def test_teacher_forced_fixture_state_is_consistent(golden, tag):
+    """The per-iteration fixture entries the GPU test is held to: from the stored state entering
+    iteration k (parameters, BatchNorm buffers, Adam moments), the oracle in float64 reproduces the
+    reference's float64 gradients of that iteration (it{k}/grad64)."""
+    f = golden(f"step_{tag}")
+    meta = ast.literal_eval(str(f["meta"]))
+    gen = R.GenConfig(meta["g_n_resnet_blocks"], meta["g_n_updownsample_blocks"], meta["g_init_channels_out"])
+    gp = bool(meta["gp"])
+    crit = R.CriticConfig(norm="identity" if gp else "batch")
+    cfg = R.StepConfig(gen=gen, critic=crit, gp_weight=10.0 if gp else None, weight_clip=None if gp else 0.01)
+    it = meta["iters"] - 1
+    pars = {}
+    for net in ("G", "D"):
+        pars[net] = {k.split("/", 3)[3]: torch.from_numpy(f[k].copy()) for k in f if k.startswith(f"it{it}/state/{net}/")}
+        pars[net] = {k: v.double() if v.is_floating_point() else v for k, v in pars[net].items()}
+    opts = {}
+    for net in ("G", "D"):
+        st = R.AdamState(meta["lr"], meta["beta1"], meta["beta2"], step=int(f[f"it{it}/adam/{net}/step"]))
+        for k in R.trainable(pars[net]):
+            st.exp_avg[k] = torch.from_numpy(f[f"it{it}/adam/{net}/{k}/exp_avg"]).double()
+            st.exp_avg_sq[k] = torch.from_numpy(f[f"it{it}/adam/{net}/{k}/exp_avg_sq"]).double()
+        opts[net] = st
+    opt = torch.from_numpy(f[f"it{it}/opt"]).double()
+    sub = torch.from_numpy(np.concatenate([f[f"it{it}/low"], f[f"it{it}/high"]])).double()
+    mask = torch.from_numpy(np.concatenate([f[f"it{it}/low_seg"], f[f"it{it}/high_seg"]]))
+    rec = {}
+    logs = R.train_step(pars["G"], pars["D"], opts["G"], opts["D"], opt, sub, mask,
+                        torch.from_numpy(f[f"it{it}/eps"]).double(), cfg, record=rec)
+    for k, v in logs.items():
+        assert_close(v, f[f"it{it}/loss64/{k}"], 1e-5, f"it{it} loss64 {k}")
+    for net in ("G", "D"):
+        for k, g in rec[net].items():
+            assert_close(g.numpy(), f[f"it{it}/grad64/{net}/{k}"], 1e-4, f"it{it} grad64 {net} {k}", atol=1e-9)
