@@ -81,7 +81,9 @@ def test_generator_autograd_backward_matches_oracle():
     from cgan3d_amd.data.synthetic import synth_patches
     from cgan3d_amd.model.generator import ResnetGenerator
     from cgan3d_amd.model.init import pcg64_init_
-    g_args = dict(n_resnet_blocks=2, n_updownsample_blocks=2, init_channels_out=16)
+    # (the 16-channel generator at 32^3 B=2 is ill-conditioned under this random loss: the reference's own
+    # float32 weight gradients deviate from float64 by ~1e-2 there; this width is conditioned to ~5e-6)
+    g_args = dict(n_resnet_blocks=1, n_updownsample_blocks=2, init_channels_out=8)
     g = pcg64_init_(ResnetGenerator(**g_args), 0).cuda().train()
     par = _oracle_params(g)
     x, _ = synth_patches(2, 32, 5)
