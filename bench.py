@@ -11,9 +11,12 @@ value = all ranks' patches / max-over-ranks wall time of the K timed steps.  Inp
 HBM when the timed region starts (a device-to-device copy into the engine's slots is inside it).
 
 Extra JSON fields: ``roofline`` for the dominant kernel (HIP events around each of its launches
-over eager steps run after the timed region, on the launch stream; algorithmic FLOPs from the
-launch geometry, 2 * out-voxels * Cout * Cin * k^3) and ``cpu_baseline`` (the oracle — torch fp32
-on the host cores — on a bounded sample, rank 0 only, N=1 only).
+in place inside eager steps run after the timed region, on the launch stream; algorithmic FLOPs
+from the launch geometry, 2 * out-voxels * Cout * Cin * k^3; ``warm_cache`` the same launches
+repeated back to back; ``step`` the whole step against the MFMA and HBM peaks),
+``reference_schedule`` (patches/s when the generator trains every 5th iteration, as the
+reference's basic_conf does) and ``cpu_baseline`` (the oracle — torch fp32 on the host cores — on
+a bounded sample, rank 0 only, N=1 only).
 
 Precision: ``--precision bf16`` (default; BASELINE.json's metric is quoted in bf16) runs every
 convolution on bf16 MFMA operands with fp32 accumulation, BatchNorm / losses / Adam in fp32;
@@ -155,13 +158,18 @@ def main():
     ev = []  # (start, end, algorithmic flops) per timed launch
 
     reps = 8
+    timing = {"reps": reps}
 
     def hook(role, geo):
         if role != roof_role or not roof_match(geo):
             return None
         e = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
         ev.append((*e, conv_flops(geo.n, (geo.do_, geo.ho, geo.wo), geo.cin, geo.cout, geo.k)))
-        return (*e, reps)
+        if timing["reps"] == 0:
+            # in-step: a spin kernel ahead of the bracket keeps the queue busy while the host
+            # enqueues start event, launch and end event, so the bracket holds only the launch
+            torch.cuda._sleep(200000)
+        return (*e, timing["reps"])
 
     def one_step(i, timed):
         eng.load_inputs(*batches[i % len(batches)])
@@ -208,18 +216,55 @@ def main():
         one_step(i, True)
     torch.cuda.synchronize()
     kern = [(a.elapsed_time(b) / reps, f) for a, b, f in ev]
+    # the same launches timed in place inside the step (cold-ish caches, no repeats): the in-step
+    # rate, which a plan-mode rocprofv3 kernel trace of the bench reproduces
+    ev.clear()
+    timing["reps"] = 0
+    for i in range(min(args.steps, 10)):
+        one_step(i, True)
+    torch.cuda.synchronize()
+    kern_in = [(a.elapsed_time(b), f) for a, b, f in ev]
+    # the reference's schedule (basic_conf.py:24, Trainer.py:174-184): the critic trains every
+    # iteration, the generator every 5th; every iteration runs the generator forward on its batch
+    ref_sched = None
+    if mode == "plan" and world == 1:
+        crit_plan = eng.record(do_critic=True, do_generator=False)
+        full_plan = eng.record()
+        for i in range(5):
+            (full_plan if i % 5 == 0 else crit_plan).run()
+        torch.cuda.synchronize()
+        n_it = 5 * max(1, args.steps // 5)
+        t1 = time.perf_counter()
+        for i in range(n_it):
+            eng.load_inputs(*batches[i % len(batches)])
+            (full_plan if i % 5 == 0 else crit_plan).run()
+        torch.cuda.synchronize()
+        el_ref = time.perf_counter() - t1
+        ref_sched = {"value": round(B * n_it / el_ref, 3), "unit": "patches/s", "iterations": n_it,
+                     "ms_per_iteration": round(el_ref / n_it * 1e3, 3),
+                     "schedule": "critic every iteration, generator every 5th (basic_conf.py:24); "
+                                 "generator forward every iteration"}
     if dist:
         t = torch.tensor([el], device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
     losses = eng.losses.cpu().numpy()
     assert np.isfinite(losses).all(), f"non-finite losses {losses}"
-    kern_ms = float(np.mean([t for t, _ in kern]))
-    roof_flops = float(np.mean([f for _, f in kern]))
+    kern_ms = float(np.mean([t for t, _ in kern_in]))
+    warm_ms = float(np.mean([t for t, _ in kern]))
+    roof_flops = float(np.mean([f for _, f in kern_in]))
     achieved = roof_flops / (kern_ms * 1e-3) / 1e12
     peak = BF16_PEAK_TFLOPS if args.precision == "bf16" else F32_PEAK_TFLOPS
     ms = el / args.steps * 1e3
     value = world * B * args.steps / el
+    # whole-step roofline: the reference step's algorithmic work per subopt patch (BASELINE.md §2,
+    # torch.utils.flop_counter on the reference, GP conf, useful work: 46.48 GFLOP at 64^3) and
+    # its compulsory HBM bytes in bf16 (SURVEY.md §8d model: ~180 MB at 64^3), both scaling with
+    # the voxel count, times this GPU's B patches, over the measured step time
+    scale = (S / 64.0) ** 3
+    step_flops, step_bytes = 46.48e9 * scale * B, 180e6 * scale * B
+    step_tflops = step_flops / (ms * 1e-3) / 1e12
+    step_gbs = step_bytes / (ms * 1e-3) / 1e9
     out = {
         "metric": "3D patches/sec (G+D train step), 64³ bf16, at 1/2/4/8 MI355X",
         "value": round(value, 3), "unit": "patches/s", "n_gpus": world, "steps": args.steps,
@@ -233,9 +278,21 @@ def main():
         "roofline": {"kernel": roof_desc, "bound": "mfma", "achieved": round(achieved, 3), "peak": peak,
                      "unit": "TFLOP/s", "frac": round(achieved / peak, 4),
                      "traffic": pmc_traffic(roof_pmc, S, B, args.precision), "traffic_source": roof_pmc,
-                     "avg_launch_ms": round(kern_ms, 4), "flops_per_launch": roof_flops, "launches_timed": len(kern),
-                     "timing": f"HIP events around {reps} back-to-back repeats of each launch, eager steps"},
+                     "avg_launch_ms": round(kern_ms, 4), "flops_per_launch": roof_flops, "launches_timed": len(kern_in),
+                     "timing": "HIP events around each launch in place inside eager steps (in-step caches)",
+                     "warm_cache": {"avg_launch_ms": round(warm_ms, 4),
+                                    "achieved": round(roof_flops / (warm_ms * 1e-3) / 1e12, 3),
+                                    "timing": f"{reps} back-to-back repeats of each launch on its own operands "
+                                              f"(inputs warm in L2 / MALL): a best case"},
+                     "step": {"bound": "mfma", "achieved": round(step_tflops, 3), "peak": peak, "unit": "TFLOP/s",
+                              "frac": round(step_tflops / peak, 4), "flops_per_step": step_flops,
+                              "hbm_achieved_gbs": round(step_gbs, 1), "hbm_peak_gbs": HBM_PEAK_GBS,
+                              "hbm_frac": round(step_gbs / HBM_PEAK_GBS, 4), "bytes_per_step": step_bytes,
+                              "source": "46.48 GFLOP and ~180 MB per 64^3 subopt patch (BASELINE.md §2, "
+                                        "SURVEY.md §8d), x B, / ms_per_step"}},
     }
+    if ref_sched is not None:
+        out["reference_schedule"] = ref_sched
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(S, args.cpu_seconds, g_args)
     if rank == 0:

@@ -333,7 +333,8 @@ def plan_abort():
 
 # bench.py's roofline timer: LAUNCH_HOOK(role, geometry) returns (start, end, reps) — two
 # torch.cuda.Event recorded on the launch stream around ``reps`` back-to-back repeats of that
-# launch (idempotent: same operands, same outputs) — or None.
+# launch (idempotent: same operands, same outputs), or around the step's own launch when reps is
+# 0 — or None.
 LAUNCH_HOOK = None
 
 
@@ -341,6 +342,11 @@ def _timed(role, g, name, *args):
     ev = LAUNCH_HOOK(role, g) if LAUNCH_HOOK is not None else None
     if ev is None:
         return _launch(name, *args)
+    if ev[2] == 0:  # the step's own launch, in place (in-step timing)
+        ev[0].record()
+        rc = _launch(name, *args)
+        ev[1].record()
+        return rc
     rc = _launch(name, *args)  # the step's own launch; then the timed repeats
     ev[0].record()
     for _ in range(ev[2]):

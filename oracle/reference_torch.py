@@ -104,6 +104,47 @@ def critic_param_shapes(cfg: CriticConfig) -> "Dict[str, tuple]":
     return shp
 
 
+# ----------------------------------------------------------------------------- bf16 yardstick
+# BF16_OPERANDS (tests only): every generator conv and the critic's middle convs take their
+# operands rounded to bf16 (round-to-nearest-even) — forward (input, weight), input-grad (the
+# incoming gradient, weight) and weight-grad (input, incoming gradient) — with exact accumulation,
+# which is what a bf16 MFMA path with fp32 accumulation does.  Run in float64 it measures how far
+# a bf16-operand reference lands from the exact step: the yardstick for the device's bf16 path
+# (tests/test_gpu_configs.py).  The critic's first (1 -> 8) and last (64 -> 1) layers stay exact,
+# as the device runs them in fp32.
+BF16_OPERANDS = False
+
+
+def _bf16(t: Tensor) -> Tensor:
+    """t rounded to bf16 in the forward pass, identity gradient (straight-through)."""
+    return t + (t.to(torch.bfloat16).to(t.dtype) - t).detach()
+
+
+class _GradToBf16(torch.autograd.Function):
+    """Identity forward; the incoming gradient is rounded to bf16 (differentiable, so the
+    gradient penalty's double backward sees the same rounding)."""
+
+    @staticmethod
+    def forward(ctx, t):
+        return t.view_as(t)
+
+    @staticmethod
+    def backward(ctx, g):
+        return _bf16(g)
+
+
+def _conv3d(x: Tensor, w: Tensor, b: Optional[Tensor] = None, rounded: bool = True, **kw) -> Tensor:
+    if not (BF16_OPERANDS and rounded):
+        return F.conv3d(x, w, b, **kw)
+    return _GradToBf16.apply(F.conv3d(_bf16(x), _bf16(w), b, **kw))
+
+
+def _conv_transpose3d(x: Tensor, w: Tensor, **kw) -> Tensor:
+    if not BF16_OPERANDS:
+        return F.conv_transpose3d(x, w, **kw)
+    return _GradToBf16.apply(F.conv_transpose3d(_bf16(x), _bf16(w), **kw))
+
+
 # ----------------------------------------------------------------------------- layers
 def batch_norm(x: Tensor, p: Dict[str, Tensor], prefix: str, training: bool, momentum=0.1, eps=1e-5):
     """nn.BatchNorm3d (blocks.py:26-27,45): batch stats over N·D·H·W in train mode."""
@@ -127,39 +168,40 @@ def batch_norm(x: Tensor, p: Dict[str, Tensor], prefix: str, training: bool, mom
 def generator_forward(p: Dict[str, Tensor], x: Tensor, cfg: GenConfig, training=True) -> Tensor:
     """ResnetGenerator.forward (generator.py:89-90)."""
     h = F.pad(x, (3,) * 6, mode="reflect")  # padding_mode="reflect", padding=3 (generator.py:19-23)
-    h = F.relu(batch_norm(F.conv3d(h, p["model.first.conv.weight"]), p, "model.first.normalization", training))
+    h = F.relu(batch_norm(_conv3d(h, p["model.first.conv.weight"]), p, "model.first.normalization", training))
     for i in range(cfg.n_updownsample_blocks):
         pre = f"model.downsampling.{i}"
-        h = F.conv3d(h, p[f"{pre}.conv.weight"], stride=2, padding=1)
+        h = _conv3d(h, p[f"{pre}.conv.weight"], stride=2, padding=1)
         h = F.relu(batch_norm(h, p, f"{pre}.normalization", training))
     for r in range(cfg.n_resnet_blocks):  # ResNetBlock.forward: x + block1(block0(x)) (blocks.py:87-88)
         pre = f"model.resnet_backbone.{r}"
-        t = F.conv3d(h, p[f"{pre}.block0.conv.weight"], padding=1)
+        t = _conv3d(h, p[f"{pre}.block0.conv.weight"], padding=1)
         t = batch_norm(t, p, f"{pre}.block0.normalization", training)  # activation Identity
-        t = F.conv3d(t, p[f"{pre}.block1.conv.weight"], padding=1)
+        t = _conv3d(t, p[f"{pre}.block1.conv.weight"], padding=1)
         t = F.relu(batch_norm(t, p, f"{pre}.block1.normalization", training))
         h = h + t
     for j in range(cfg.n_updownsample_blocks):
         pre = f"model.upsampling.{j}"
-        h = F.conv_transpose3d(h, p[f"{pre}.conv.weight"], stride=2, padding=1, output_padding=1)
+        h = _conv_transpose3d(h, p[f"{pre}.conv.weight"], stride=2, padding=1, output_padding=1)
         h = F.relu(batch_norm(h, p, f"{pre}.normalization", training))
     h = F.pad(h, (3,) * 6, mode="reflect")
-    h = F.conv3d(h, p["model.last_conv.weight"], p["model.last_conv.bias"])
+    h = _conv3d(h, p["model.last_conv.weight"], p["model.last_conv.bias"])
     return torch.tanh(h)
 
 
 def critic_forward(p: Dict[str, Tensor], x: Tensor, cfg: CriticConfig, training=True) -> Tensor:
     """PatchGANDiscriminator.forward (discriminator.py:83-84)."""
     s = cfg.negative_slope
-    h = F.leaky_relu(F.conv3d(x, p["model.first.conv.weight"], p["model.first.conv.bias"], stride=2, padding=1), s)
+    h = F.leaky_relu(_conv3d(x, p["model.first.conv.weight"], p["model.first.conv.bias"], rounded=False, stride=2,
+                             padding=1), s)
     for n in range(cfg.discriminator_depth):
         pre = f"model.middle.{n}"
         if cfg.norm == "identity":
-            h = F.conv3d(h, p[f"{pre}.conv.weight"], p[f"{pre}.conv.bias"], stride=2, padding=1)
+            h = _conv3d(h, p[f"{pre}.conv.weight"], p[f"{pre}.conv.bias"], stride=2, padding=1)
         else:
-            h = batch_norm(F.conv3d(h, p[f"{pre}.conv.weight"], stride=2, padding=1), p, f"{pre}.normalization", training)
+            h = batch_norm(_conv3d(h, p[f"{pre}.conv.weight"], stride=2, padding=1), p, f"{pre}.normalization", training)
         h = F.leaky_relu(h, s)
-    return F.conv3d(h, p["model.last.weight"], p["model.last.bias"], stride=1, padding=1)
+    return _conv3d(h, p["model.last.weight"], p["model.last.bias"], rounded=False, stride=1, padding=1)
 
 
 # ----------------------------------------------------------------------------- losses
