@@ -100,6 +100,83 @@ def cpu_baseline(size, seconds, g_args):
                       f"{el:.1f}s after 1 warm-up step"}
 
 
+class _NullLogger:
+    """logger_interface stand-in: the reference's wandb logger is out of scope."""
+
+    class logger:  # noqa: N801
+        @staticmethod
+        def log_loss(*a, **k):
+            pass
+
+    def __call__(self, *a, **k):
+        pass
+
+    def end_hook(self):
+        pass
+
+
+def bench_trainer(args, S, B, dev, world, rank, dist, batches):
+    """Trainer.train_step (cgan3d_amd.trainer.Trainer, constructed as train.py:154-176 does with the
+    GP conf's partials) on device-resident [OPT, LOW, HIGH] patch dicts; the generator trains every
+    iteration, as in the engine bench."""
+    from functools import partial
+    from torch import nn
+    from cgan3d_amd.model.discriminator import PatchGANDiscriminator
+    from cgan3d_amd.model.generator import ResnetGenerator
+    from cgan3d_amd.model.loss import HULoss
+    from cgan3d_amd.trainer.Trainer import Trainer
+    tr = Trainer(args.warmup + args.steps, 1, None, 1, 1, 10**9, 10**9,
+                 partial(ResnetGenerator, 4, 2, 16),
+                 partial(PatchGANDiscriminator, channels_in=1, init_channels_out=8, discriminator_depth=3,
+                         negative_slope=0.2, norm_layer=nn.Identity),
+                 partial(torch.optim.Adam, lr=1e-4, betas=(0.0, 0.9)), partial(torch.optim.Adam, lr=1e-4, betas=(0.0, 0.9)),
+                 HULoss(112.0 / 600.0, 212.0 / 600.0), _NullLogger(), dev, checkpoint_dir=None, checkpoint_every=None,
+                 precision=args.precision)
+    h = B // 2
+    pl = []
+    for opt, sub, seg, _ in batches:
+        pl.append([{"data": opt, "seg": torch.zeros_like(opt, dtype=torch.bool)},
+                   {"data": sub[:h], "seg": seg[:h]}, {"data": sub[h:], "seg": seg[h:]}])
+    it = 0
+    for _ in range(max(args.warmup, 3)):  # first: eager; second: the plan is recorded and run
+        tr.train_step(pl[it % len(pl)], it)
+        it += 1
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        tr.train_step(pl[it % len(pl)], it)
+        it += 1
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    if dist:
+        t = torch.tensor([el], device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    losses = tr.engine.losses.cpu().numpy()
+    assert np.isfinite(losses).all(), f"non-finite losses {losses}"
+    ms = el / args.steps * 1e3
+    out = {
+        "metric": "3D patches/sec (G+D train step), 64³ bf16, at 1/2/4/8 MI355X",
+        "value": round(world * B * args.steps / el, 3), "unit": "patches/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": args.precision, "data": "synthetic",
+        "config": {"workload": f"{S}^3 patches, {B} OPT + {B} LOW/HIGH per GPU, Trainer.train_step (WGAN-GP conf)",
+                   "global_batch": world * B, "patch": S, "parallelism": f"dp{world}",
+                   "launch_mode": "trainer (launch plans recorded by Trainer.train_step)",
+                   "plans": sum(p is not None for p in tr._plans.values())},
+    }
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if dist:
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -112,6 +189,9 @@ def main():
     ap.add_argument("--precision", choices=["f32", "bf16"], default="bf16",
                     help="MFMA operand precision of the convolutions (accumulation is f32)")
     ap.add_argument("--roofline", choices=sorted(ROOFLINES), default="halo_res")
+    ap.add_argument("--via-trainer", action="store_true",
+                    help="time the drop-in Trainer.train_step (the path train.py drives: plans recorded and "
+                         "replayed by the Trainer itself) on device-resident patch batches, instead of the engine")
     ap.add_argument("--mode", choices=["plan", "eager", "graph"], default="plan",
                     help="plan (default): the step recorded once as a launch plan (cgan3d_plan_*) and re-issued "
                          "from C++ each step, two streams kept; eager: the Python wrappers launch every kernel; "
@@ -152,6 +232,9 @@ def main():
         sub, seg = synth_patches(B, S, 1000 * rank + 10 * j + 1)
         batches.append((torch.from_numpy(opt).to(dev), torch.from_numpy(sub).to(dev),
                         torch.from_numpy(seg).to(dev), torch.rand(B, device=dev)))
+
+    if args.via_trainer:
+        return bench_trainer(args, S, B, dev, world, rank, dist, batches)
 
     from cgan3d_amd import ops
     roof_desc, roof_role, roof_match, roof_pmc = ROOFLINES[args.roofline]

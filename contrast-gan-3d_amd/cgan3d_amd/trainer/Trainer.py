@@ -16,6 +16,7 @@ Differences from the reference, all deliberate and documented in DESIGN.md:
 """
 from __future__ import annotations
 
+import os
 from functools import partial
 from pathlib import Path
 from typing import Dict, List, Optional, Union
@@ -80,6 +81,9 @@ class Trainer:
         self.loss_HU = hu_loss_instance
         self.logger_interface = logger_interface
         self.engine: Optional[StepEngine] = None
+        # launch plans per (engine, do_critic, do_generator) (_replay); CGAN3D_TRAINER_PLANS=0: eager
+        self.use_plans = os.environ.get("CGAN3D_TRAINER_PLANS", "1") == "1"
+        self._plans: Dict[tuple, object] = {}
 
         self.iteration = 0
         self.checkpoint_every = checkpoint_every
@@ -99,6 +103,7 @@ class Trainer:
                                      gan_w=self.gan_loss_w, sim_w=self.sim_loss_w, hu_w=self.hu_loss_w,
                                      device=self.device, g_optim=self.optimizer_G, d_optim=self.optimizer_D,
                                      precision=self.precision, weight_clip=self.weight_clip)
+            self._plans.clear()  # plans refer to the old engine's buffers
         return self.engine
 
     def _losses(self, keys) -> Dict[str, Tensor]:
@@ -139,12 +144,19 @@ class Trainer:
             eng.mask.view(-1)[ml:].copy_(high["seg"].reshape(-1), non_blocking=True)
         # eps ~ U[0,1) per interpolated sample, drawn on the device (model/utils.py:26)
         eng.eps.uniform_(0.0, 1.0)
-        eng.generator_forward()
+        do_c = iteration % self.train_critic_every == 0
         log_dict = {}
-        if iteration % self.train_critic_every == 0:
-            log_dict = self.train_critic(None, None, do_g)
-        if do_g:
-            log_dict |= self.train_generator(None, None, None)
+        if self._replay(eng, do_c, do_g):
+            if do_c:
+                log_dict = self._losses(["D"])
+            if do_g:
+                log_dict |= self._losses(["G", "G-full", "sim", "HU"])
+        else:
+            eng.generator_forward()
+            if do_c:
+                log_dict = self.train_critic(None, None, do_g)
+            if do_g:
+                log_dict |= self.train_generator(None, None, None)
 
         if iteration % self.log_every == 0:
             self.logger_interface.logger.log_loss({k: v.mean() for k, v in log_dict.items()}, iteration, "train")
@@ -156,6 +168,39 @@ class Trainer:
             self.logger_interface(patches, [None, opt_hat[:cut], opt_hat[cut:]], [None, att[:cut], att[cut:]],
                                   _scan_types(), iteration, "train", self.train_log_sample_size)
         return log_dict
+
+    def _replay(self, eng: StepEngine, do_c: bool, do_g: bool) -> bool:
+        """Run this iteration's generator forward + updates from a recorded launch plan
+        (engine.record / run_plan, cgan3d_plan_*): one plan per (engine, schedule) combination,
+        recorded on the combination's second iteration (the first runs eagerly: kernel code objects
+        load lazily) and re-issued from C++ afterwards.  Learning rates reach the plan through the
+        optimisers' device scalars (sync_hyper), the LR schedulers step on the host as in the eager
+        path.  Returns False when the eager path must run (first sighting, debug mode, no plans)."""
+        if not self.use_plans or self.debug:
+            return False
+        key = (id(eng), do_c, do_g)
+        plan = self._plans.get(key)
+        if plan is None:
+            if key not in self._plans:
+                self._plans[key] = None  # seen once: eager this time, record next time
+                return False
+            host = (self.optimizer_D._host_step, self.optimizer_G._host_step)
+            plan = self._plans[key] = eng.record(do_c, do_g)
+            assert (self.optimizer_D._host_step, self.optimizer_G._host_step) == host
+        if do_c:
+            self.optimizer_D.sync_hyper()
+        if do_g:
+            self.optimizer_G.sync_hyper()
+        plan.run()
+        if do_c:
+            self.optimizer_D.note_step()
+            if self.lr_scheduler_D is not None:
+                self.lr_scheduler_D.step()
+        if do_g:
+            self.optimizer_G.note_step()
+            if self.lr_scheduler_G is not None:
+                self.lr_scheduler_G.step()
+        return True
 
     def fit(self, train_loaders, val_loaders, profiler=None):
         self.generator.train()

@@ -63,6 +63,11 @@ class FusedAdam(torch.optim.Optimizer):
         ops.adam_tick(self.hyper)
         a = self.arena
         ops.adam(a.flat, a.grad, a.exp_avg, a.exp_avg_sq, self.hyper)
+        if not ops.recording():  # a recorded plan counts its steps when it runs (note_step)
+            self._host_step += 1
+
+    def note_step(self):
+        """Count one update issued by a replayed launch plan (the device counter ticks itself)."""
         self._host_step += 1
 
     @torch.no_grad()

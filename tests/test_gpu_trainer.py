@@ -31,14 +31,14 @@ class _LoggerInterface:
         pass
 
 
-def _trainer(ckpt_dir, precision="f32", clip=False):
+def _trainer(ckpt_dir, precision="f32", clip=False, gen_every=1):
     from cgan3d_amd.model.discriminator import PatchGANDiscriminator
     from cgan3d_amd.model.generator import ResnetGenerator
     from cgan3d_amd.model.loss import HULoss
     from cgan3d_amd.trainer.Trainer import Trainer
     torch.manual_seed(0)
     return Trainer(
-        3, 1, 2, 1, 1, 1, 1000,
+        3, 1, 2, gen_every, 1, 1, 1000,
         partial(ResnetGenerator, 2, 2, 8),
         partial(PatchGANDiscriminator, channels_in=1, init_channels_out=8, discriminator_depth=3,
                 negative_slope=0.2, **({} if clip else dict(norm_layer=nn.Identity))),
@@ -117,3 +117,70 @@ def test_fit_with_patch_loaders(tmp_path):
     assert "validation" in modes
     assert all(np.isfinite(v) for _, _, d in tr.logger_interface.logger.losses for v in d.values())
     assert (tmp_path / "ck" / "3.pt").exists()
+
+
+def _sync_state(dst, src):
+    """Give trainer ``dst`` the full training state of ``src``: weights, BatchNorm buffers, both
+    Adam states (moments and device step counters), then refresh the packed weight copies."""
+    dst.generator.load_state_dict(src.generator.state_dict())
+    dst.critic.load_state_dict(src.critic.state_dict())
+    dst.optimizer_G.load_state_dict(src.optimizer_G.state_dict())
+    dst.optimizer_D.load_state_dict(src.optimizer_D.state_dict())
+    dst.engine.G.pack()
+    dst.engine.D.pack()
+
+
+@pytest.mark.parametrize("precision", ["f32", "bf16"])
+def test_trainer_plan_replay_matches_eager(tmp_path, precision, monkeypatch):
+    """Trainer.train_step replays recorded launch plans (one per batch shape and schedule; the
+    generator trains every 2nd iteration here, so both schedules are recorded and replayed) and
+    computes what the eager Trainer computes: after warm-up both trainers are put in the same state,
+    then a replayed critic-only iteration and a replayed full iteration are compared with the eager
+    ones (losses, every gradient tensor, the updated weights)."""
+    trs = []
+    for plans in (False, True):
+        monkeypatch.setenv("CGAN3D_TRAINER_PLANS", "1" if plans else "0")
+        tr = _trainer(tmp_path / f"p{int(plans)}", precision, gen_every=2)
+        assert tr.use_plans == plans
+        trs.append(tr)
+    eager, planned = trs
+    batches = [_patches(np.random.default_rng(10 + it)) for it in range(7)]
+    for tr in trs:
+        for it in range(5):  # planned: eager, eager, record + run, record + run, replay
+            torch.cuda.manual_seed(100 + it)  # the GP eps draw
+            tr.train_step(batches[it], it)
+    assert len([p for p in planned._plans.values() if p is not None]) == 2
+    assert planned.optimizer_D._host_step == eager.optimizer_D._host_step == 5
+    assert planned.optimizer_G._host_step == eager.optimizer_G._host_step == 3
+    for it in (5, 6):  # critic-only (replayed), full step (replayed)
+        _sync_state(planned, eager)
+        for tr in trs:
+            torch.cuda.manual_seed(100 + it)
+            tr.train_step(batches[it], it)
+        torch.cuda.synchronize()
+        (_, ie, de), (_, ip, dp) = eager.logger_interface.logger.losses[-1], planned.logger_interface.logger.losses[-1]
+        assert ie == ip == it and sorted(de) == sorted(dp)
+        for k in de:  # weight-gradient atomics may add in another order
+            assert abs(de[k] - dp[k]) <= 1e-5 * max(abs(de[k]), 1e-2), (it, k, de[k], dp[k])
+        arenas = [(eager.engine.d_arena, planned.engine.d_arena)]
+        if it % 2 == 0:
+            arenas.append((eager.engine.g_arena, planned.engine.g_arena))
+        # the full iteration's generator gradients go through the critic just updated, whose Adam
+        # step may flip noise-level elements (below); in bf16 such an element can round its conv
+        # operand the other way, and the generator's BatchNorm backward amplifies that (see
+        # test_gpu_configs.py): 5e-3 of the tensor's max there, 1e-4 everywhere else
+        for net, (ae, ap) in zip("DG", arenas):
+            tol = 5e-3 if (net == "G" and precision == "bf16") else 1e-4
+            for k in ae.gviews:
+                ge, gp = ae.gviews[k].cpu().numpy(), ap.gviews[k].cpu().numpy()
+                assert np.abs(ge - gp).max() <= tol * max(np.abs(ge).max(), 1e-12), (it, k)
+        for a, b in ((eager.generator, planned.generator), (eager.critic, planned.critic)):
+            for (k, va), (_, vb) in zip(a.state_dict().items(), b.state_dict().items()):
+                va, vb = va.float().cpu().numpy(), vb.float().cpu().numpy()
+                # Adam's normalised step may flip sign where a gradient element is rounding noise
+                d = np.abs(va - vb)
+                off = d > 1e-5 * max(np.abs(va).max(), 1e-3)
+                assert d.max() <= 2 * 1e-4 / np.sqrt(1 - 0.9) * 1.001 and off.mean() <= 0.01, (
+                    it, k, float(d.max()), float(off.mean()))
+    assert planned.optimizer_D._host_step == eager.optimizer_D._host_step == 7
+    assert planned.optimizer_G._host_step == eager.optimizer_G._host_step == 4
