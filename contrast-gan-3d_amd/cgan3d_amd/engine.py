@@ -28,7 +28,7 @@ from __future__ import annotations
 
 import os
 from dataclasses import dataclass
-from typing import Dict, List, Optional, Sequence, Tuple
+from typing import Callable, Dict, List, Optional, Sequence, Tuple
 
 import torch
 
@@ -41,6 +41,10 @@ Dims = Tuple[int, int, int]
 # step time at 64^3 B=4 under launch plans, 13 fewer launches), or CGAN3D_BN_FUSED_BWD=0 for a
 # separate reduction pass over (dy, z)
 BN_FUSED_BWD = os.environ.get("CGAN3D_BN_FUSED_BWD", "1") == "1"
+# data parallelism: generator gradient bucket size (all-reduce started per bucket during the backward)
+# (measured on one GPU over a one-rank RCCL group: each extra bucket ~15 us of step time, so the
+# default makes ~2-3 buckets of the 4.1 MB arena: 2.21 ms/step at 1 MB, 2.16 with 2 buckets)
+G_BUCKET_BYTES = int(os.environ.get("CGAN3D_G_BUCKET_BYTES", str(2 << 20)))
 
 
 def _half(d: Dims) -> Dims:
@@ -280,7 +284,11 @@ class GeneratorPlan:
             self.ss[i][c:].copy_(P[f"{nb}.bias"] - P[f"{nb}.running_mean"] * sc)
 
     # -- backward from dz_last = dL/d(pre-tanh) ; writes parameter grads into G (grad views)
-    def backward(self, P: Dict[str, torch.Tensor], G: Dict[str, torch.Tensor], x: torch.Tensor):
+    def backward(self, P: Dict[str, torch.Tensor], G: Dict[str, torch.Tensor], x: torch.Tensor,
+                 grads_enqueued: Optional[Callable[[int], None]] = None):
+        """``grads_enqueued(i)`` (optional) is called once every launch producing layer i's
+        parameter gradients is enqueued (i = len(layers) for the last conv, which goes first; then
+        len(layers) - 1 down to 0): the data-parallel engine starts bucket all-reduces there."""
         la = self.last
         n = self.n
         u = self.y[-1]
@@ -288,6 +296,8 @@ class GeneratorPlan:
                                         self.ws_side))
         nvl = n * la.dout[0] * la.dout[1] * la.dout[2]
         ops.channel_sum(self.dz_last, nvl, 1, G["model.last_conv.bias"], self.ws)
+        if grads_enqueued is not None:
+            grads_enqueued(len(self.layers))
         ops.conv(self.geo_last_dgrad, self.dz_last, P["model.last_conv.weight"], self.dpad)
         ops.reflect_fold(self.dpad, self.dy[-1], n, la.din, la.cin, la.p, ep=self._bn_grad_epi(len(self.layers) - 1))
         for i in range(len(self.layers) - 1, -1, -1):
@@ -314,6 +324,8 @@ class GeneratorPlan:
             else:
                 self._on_side(lambda g=self.geo_wgrad[i], a=xin, b=self.dz[i], w=G[wname], a16=x16, b16=d16:
                               ops.wgrad(g, a, b, w, self.ws_side, gathered16=a16, aligned16=b16))
+            if grads_enqueued is not None:
+                grads_enqueued(i)
             if i == 0:
                 break
             # input-grad; a ResNet block0 also receives the skip gradient dL/dh_{r+1}
@@ -602,6 +614,9 @@ class StepEngine:
         self.world = 1
         if process_group is not None or (torch.distributed.is_available() and torch.distributed.is_initialized()):
             self.world = torch.distributed.get_world_size(process_group)
+        # data-parallel collectives on; CGAN3D_FORCE_DP=1 also at world size 1 (exercises the RCCL
+        # path, buckets and streams on a single GPU: tools/dist_nccl1_check.py)
+        self.dp = self.world > 1 or (os.environ.get("CGAN3D_FORCE_DP") == "1" and torch.distributed.is_initialized())
         self.g_arena, self.d_arena = g_optim.arena, d_optim.arena
         self.gP = dict(self.g_arena.views)
         self.gP.update({k: v for k, v in generator.state_dict(keep_vars=True).items() if k not in self.gP})
@@ -620,8 +635,72 @@ class StepEngine:
         self.dcrit = torch.empty((b_sub, *dims, 1), device=device)       # dL_G/d opt_hat via the critic
         self.losses = torch.zeros(8, device=device)
         self.loss_ws = torch.empty(ops.loss_ws_floats(), device=device)
+        self._pending = []  # in-flight bucket all-reduces of the generator gradients
+        self.g_buckets = self._make_g_buckets(G_BUCKET_BYTES) if self.dp else []
+        on_gpu = torch.device(device).type == "cuda"
+        self.comm = torch.cuda.Stream(device=device) if (self.dp and on_gpu) else None
         if self.world > 1:
             self.broadcast_state()
+
+    def _make_g_buckets(self, bucket_bytes: int):
+        """Generator gradient buckets for data parallelism: the backward produces parameter
+        gradients from the last layer to the first, i.e. from the end of the flat arena (forward
+        order) toward its start, so a bucket is a contiguous arena slice closed at a layer boundary
+        once it holds >= ``bucket_bytes``; the first three layers (the last gradients produced, on
+        the critical path to Adam) form their own small final bucket.  Returns
+        [(layer stage that closes the bucket, lo, hi)] in backward order."""
+        ar = self.g_arena
+        span, off = {}, 0
+        for n, p in zip(ar.names, ar.params):
+            span[n] = (off, off + p.numel())
+            off += p.numel()
+        nl = len(self.G.layers)
+        stages = [(nl, [k for k in span if k.startswith("model.last_conv.")])]
+        for i in range(nl - 1, -1, -1):
+            stages.append((i, [k for k in span if k.startswith(self.G.layers[i].name + ".")]))
+        buckets, hi, acc = [], ar.numel, 0
+        for stage, names in stages:
+            lo = min(span[k][0] for k in names)
+            assert max(span[k][1] for k in names) == hi - acc, "generator arena is not in layer order"
+            acc = hi - lo
+            if stage == 3 or (acc * 4 >= bucket_bytes and stage > 3) or stage == 0:
+                buckets.append((stage, lo, hi))
+                hi, acc = lo, 0
+        assert hi == 0 and acc == 0
+        return buckets
+
+    def _bucket_ready(self, stage: int):
+        """GeneratorPlan.backward callback: start the all-reduce of a bucket whose gradients are all
+        enqueued (a host callable inside a recorded plan: ops.plan_host)."""
+        for st, lo, hi in self.g_buckets:
+            if st == stage:
+                ops.plan_host(lambda lo=lo, hi=hi: self._start_allreduce(self.g_arena.grad[lo:hi]))
+
+    def _start_allreduce(self, grad: torch.Tensor):
+        """Mean over ranks of ``grad``, started now and overlapped with whatever is enqueued next:
+        RCCL on a communication stream ordered after the main and side streams' work so far (both
+        produce gradients); ``_finish_allreduce`` makes the main stream wait before Adam.  gloo
+        (CPU tensors): synchronous."""
+        dist = torch.distributed
+        if dist.get_backend(self.pg) != "nccl":
+            if self.G.side is not None:  # gloo over GPU tensors orders only after the current stream
+                torch.cuda.current_stream(self.device).wait_stream(self.G.side)
+            dist.all_reduce(grad, op=dist.ReduceOp.SUM, group=self.pg)
+            grad.mul_(1.0 / self.world)
+            return
+        cur = torch.cuda.current_stream(self.device)
+        self.comm.wait_stream(cur)
+        if self.G.side is not None:
+            self.comm.wait_stream(self.G.side)
+        with torch.cuda.stream(self.comm):
+            self._pending.append(dist.all_reduce(grad, op=dist.ReduceOp.AVG, group=self.pg, async_op=True))
+
+    def _finish_allreduce(self):
+        def wait():
+            for w in self._pending:
+                w.wait()  # the current stream waits for the collective
+            self._pending.clear()
+        ops.plan_host(wait)
 
     def broadcast_state(self, src: int = 0):
         """Start every rank from rank ``src``'s weights, BatchNorm buffers and Adam moments (what
@@ -636,6 +715,28 @@ class StepEngine:
                     dist.broadcast(v.data, src, group=self.pg)
         self.G.pack()
         self.D.pack()
+
+    def sync_bn_buffers(self, src: int = 0):
+        """BatchNorm running statistics of rank ``src`` on every rank (one coalesced broadcast).
+
+        Policy under data parallelism: every rank normalises with its own batch statistics and
+        updates its own running buffers (as DistributedDataParallel does between its per-forward
+        buffer broadcasts); rank ``src``'s buffers evolve exactly as DDP's rank 0 buffers do, since
+        they only ever see that rank's batches.  The running buffers are read only by eval-mode
+        forwards (Trainer.validate) and checkpoints (written by rank 0), so the Trainer calls this
+        before both instead of broadcasting every step."""
+        if self.world == 1:
+            return
+        bufs = [v for P in (self.gP, self.dP) for k, v in P.items() if k.endswith(("running_mean", "running_var"))]
+        if not bufs:
+            return
+        flat = torch.cat([b.detach().reshape(-1) for b in bufs])
+        torch.distributed.broadcast(flat, src, group=self.pg)
+        off = 0
+        with torch.no_grad():
+            for b in bufs:
+                b.copy_(flat[off:off + b.numel()].view_as(b))
+                off += b.numel()
 
     @property
     def opt_hat(self):
@@ -691,14 +792,17 @@ class StepEngine:
         D.input_grad(self.dP, 0, bs, self.dcrit, 0, bs)
         ops.generator_output_grad(self.opt_hat, self.subopt, self.G.att, self.mask, self.dcrit, bs * V, self.lo,
                                   self.hi, self.sim_w, self.hu_w, self.G.dz_last, self.losses, self.loss_ws)
-        self.G.backward(self.gP, self.gG, self.subopt)
-        self._allreduce(self.g_arena.grad)
+        if self.dp:  # bucketed, overlapped with the rest of the backward
+            self.G.backward(self.gP, self.gG, self.subopt, grads_enqueued=self._bucket_ready)
+            self._finish_allreduce()
+        else:
+            self.G.backward(self.gP, self.gG, self.subopt)
         self.g_optim.launch()
         self.G.pack()
 
     def _allreduce(self, flat_grad: torch.Tensor):
         """Mean of the per-rank gradients (RCCL over xGMI with the nccl backend; gloo on CPU)."""
-        if self.world == 1:
+        if not self.dp:
             return
         dist = torch.distributed
 

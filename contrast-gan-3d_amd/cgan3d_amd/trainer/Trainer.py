@@ -226,6 +226,8 @@ class Trainer:
     @torch.no_grad()
     def validate(self, val_loaders, train_iteration: int):
         """Eval-mode pass (Trainer.py:247-308): running-stat BN, no gradients."""
+        if self.engine is not None:
+            self.engine.sync_bn_buffers()  # data parallelism: rank 0's running statistics (engine docstring)
         self.critic.eval()
         self.generator.eval()
         z = torch.zeros(4, dtype=torch.float32, device=self.device)
@@ -265,6 +267,8 @@ class Trainer:
                 "lr_scheduler_D"]
 
     def save_checkpoint(self, iteration: int):
+        if self.engine is not None:
+            self.engine.sync_bn_buffers()
         state = {"iteration": iteration}
         for attr in self.model_torch_attrs:
             el = getattr(self, attr, None)

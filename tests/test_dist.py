@@ -32,7 +32,7 @@ def _worker(rank, world, port, q):
         from cgan3d_amd.model.discriminator import PatchGANDiscriminator
         from cgan3d_amd.model.generator import ResnetGenerator
         torch.manual_seed(100 + rank)  # different initial weights per rank: the engine must broadcast
-        g = ResnetGenerator(1, 2, 8)
+        g = ResnetGenerator(2, 2, 8)
         d = PatchGANDiscriminator(**D_ARGS, norm_layer=nn.Identity)
         ops.DRY_RUN = True
         eng = StepEngine(g, d, g.config, d.config, 1, 1, (32, 32, 32), g_hyper=(1e-4, 0.0, 0.9, 1e-8),
@@ -49,7 +49,25 @@ def _worker(rank, world, port, q):
             eng._allreduce(ar.grad)
             want = torch.arange(ar.grad.numel(), dtype=torch.float32) * (sum(range(1, world + 1)) / world)
             assert torch.allclose(ar.grad, want), "gradient arena is not the mean over ranks"
-        eng.step()  # full step with the collectives in place
+        # generator buckets: contiguous slices that tile the arena exactly once, closed in backward
+        # order (stages descending), the first three layers in the small final bucket
+        bk = eng.g_buckets
+        assert len(bk) >= 2 and [st for st, _, _ in bk] == sorted((st for st, _, _ in bk), reverse=True)
+        assert bk[0][2] == eng.g_arena.numel and bk[-1][1] == 0 and bk[-1][0] == 0
+        assert all(bk[j][1] == bk[j + 1][2] for j in range(len(bk) - 1))
+        # a full step with the collectives in place (kernels are no-ops here): the bucketed
+        # all-reduces leave the mean over ranks in the generator arena, the critic's in its arena
+        for ar in (eng.g_arena, eng.d_arena):
+            ar.grad.copy_(torch.arange(ar.grad.numel(), dtype=torch.float32) * (rank + 1))
+        eng.step()
+        for ar in (eng.g_arena, eng.d_arena):
+            want = torch.arange(ar.grad.numel(), dtype=torch.float32) * (sum(range(1, world + 1)) / world)
+            assert torch.allclose(ar.grad, want), "step did not leave the mean gradient"
+        # BatchNorm running buffers: rank 0's on every rank after sync_bn_buffers
+        rm = eng.gP["model.first.normalization.running_mean"]
+        rm.fill_(float(rank + 1))
+        eng.sync_bn_buffers()
+        assert torch.all(rm == 1.0), "running buffers not synchronised from rank 0"
         q.put((rank, "ok"))
     except Exception as e:  # surfaced by the parent
         q.put((rank, repr(e)))

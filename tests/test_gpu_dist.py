@@ -21,3 +21,13 @@ def test_two_rank_plan_step():
     out = r.stdout + r.stderr
     assert r.returncode == 0, out[-4000:]
     assert "rank 0: ok" in out and "rank 1: ok" in out, out[-4000:]
+
+
+def test_rccl_bucketed_path_one_rank():
+    """The RCCL path itself (bucketed async all-reduces on a communication stream, inside a launch
+    plan) on a one-rank nccl group: tools/dist_nccl1_check.py (the mean over one rank is exact)."""
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT="29533")
+    r = subprocess.run([sys.executable, str(REPO / "tools" / "dist_nccl1_check.py")], cwd=REPO, env=env,
+                       capture_output=True, text=True, timeout=110)
+    out = r.stdout + r.stderr
+    assert r.returncode == 0 and "path ok" in out, out[-4000:]

@@ -20,6 +20,12 @@ def main():
     from cgan3d_amd.model.discriminator import PatchGANDiscriminator
     from cgan3d_amd.model.generator import ResnetGenerator
     from cgan3d_amd.model.init import pcg64_init_
+    import os
+    if os.environ.get("CGAN3D_FORCE_DP") == "1":  # the data-parallel path over a one-rank RCCL group
+        import torch.distributed as dist
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29543")
+        dist.init_process_group("nccl", device_id=torch.device("cuda", 0), rank=0, world_size=1)
     S, B = 64, 4
     prec = sys.argv[1] if len(sys.argv) > 1 else "bf16"
     g = pcg64_init_(ResnetGenerator(4, 2, 16), 0).cuda()
