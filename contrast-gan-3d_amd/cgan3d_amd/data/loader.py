@@ -20,8 +20,10 @@ Per batch:
   read on the host and copied over PCIe.  A returned batch's tensors live in a ring slot and are
   overwritten ``depth`` batches later (the Trainer consumes each batch within its step).
 
-Spatial augmentation (``SpatialTransform_2``: elastic deformation, scaling, rotation with
-per-sample probabilities, ``basic_conf.py:88-106``) is not applied.
+* spatial augmentation (optional ``transform``, ``data/augment.py``: batchgenerators'
+  ``SpatialTransform_2`` as ``basic_conf.py:87-113`` configures it): the per-sample parameters
+  are drawn on the host with the crop boxes, the elastic noise fields by the host worker, and
+  ``cgan3d_spatial_augment`` resamples the unpacked batch on the loader stream.
 """
 from __future__ import annotations
 
@@ -73,7 +75,7 @@ def read_crop(vol: np.ndarray, patch: Sequence[int], box, out: np.ndarray):
 class PatchLoader:
     def __init__(self, data: List[str], patch_shape: Sequence[int], batch_size: int, rng: np.random.Generator,
                  scaler=None, infinite: bool = True, shuffle: bool = True, device=None, depth: int = 3,
-                 num_threads: int = 4, seed_for_shuffle: Optional[int] = None):
+                 num_threads: int = 4, seed_for_shuffle: Optional[int] = None, transform=None):
         if len(patch_shape) != 3:
             raise NotImplementedError("PatchLoader: 3-D patches (the 2-D slice sampler is SURVEY.md §8f row 4)")
         self.paths = [str(p) for p in data]
@@ -96,6 +98,13 @@ class PatchLoader:
         self._seg = [torch.empty((batch_size, 1, *self.patch), dtype=torch.bool, device=self.device)
                      for _ in range(self.depth)]
         self._copied = [None] * self.depth  # HIP event: slot's H2D copy finished (host slot reusable)
+        self.transform = transform
+        if transform is not None:  # unpack into staging buffers, augment into the returned ones
+            if tuple(transform.patch_size) != self.patch:
+                raise ValueError(f"PatchLoader: transform patch {transform.patch_size} != loader patch {self.patch}")
+            self._pre_data = [torch.empty_like(t) for t in self._data]
+            self._pre_seg = [torch.empty_like(t) for t in self._seg]
+            self._aug_ws = torch.empty(ops.augment_ws_floats(batch_size, self.patch, batch_size), device=self.device)
         self._stream = torch.cuda.Stream(device=self.device)
         self._threads, self._pool = num_threads, None
         self._lock = threading.Lock()
@@ -128,16 +137,22 @@ class PatchLoader:
                 idx.append(self._order[self._pos])
                 self._pos += 1
             boxes = [crop_box(self._volume(self.paths[i]).shape[:3], self.patch, self.rng) for i in idx]
-            return list(zip(idx, boxes))
+            aug = None
+            if self.transform is not None:  # drawn here, under the lock, from the loader's generator
+                aug = self.transform.draw(self.rng, self.batch_size)
+            return list(zip(idx, boxes)), aug
 
     def _fill(self, slot: int, picks):
         ev = self._copied[slot]
         if ev is not None:
             ev.synchronize()  # the previous H2D copy out of this pinned slot has finished
         host = self._host[slot].numpy()
+        picks, aug = picks
         for b, (i, box) in enumerate(picks):
             read_crop(self._volume(self.paths[i]), self.patch, box, host[b])
-        return picks
+        if aug is not None:  # small parameter / noise tensors, pinned by this worker for the async copy
+            aug = tuple(None if a is None else torch.from_numpy(a).pin_memory() for a in aug)
+        return picks, aug
 
     def _submit(self):
         picks = self._indices()
@@ -176,7 +191,7 @@ class PatchLoader:
         fut = self._pending.pop(slot, None)
         if fut is None:
             raise StopIteration
-        picks = fut.result()
+        picks, aug = fut.result()
         self._consume = (slot + 1) % self.depth
         cur = torch.cuda.current_stream(self.device)
         # work enqueued so far (the consumers of the batch that last used this slot) precedes the copy
@@ -186,7 +201,15 @@ class PatchLoader:
             ev = torch.cuda.Event()
             ev.record(self._stream)
             self._copied[slot] = ev
-            ops.unpack_patches(self._raw[slot], self._data[slot], self._seg[slot], self.shift, self.factor)
+            if aug is None:
+                ops.unpack_patches(self._raw[slot], self._data[slot], self._seg[slot], self.shift, self.factor)
+            else:
+                ops.unpack_patches(self._raw[slot], self._pre_data[slot], self._pre_seg[slot], self.shift,
+                                   self.factor)
+                prm, noise, gauss = (None if a is None else a.to(self.device, non_blocking=True) for a in aug)
+                self.transform.apply(self._pre_data[slot], self._pre_seg[slot], prm, noise, gauss, self._data[slot],
+                                     self._seg[slot], ws=self._aug_ws)
+                self._aug_keep = aug  # pinned sources alive until the next batch's copies are queued
         cur.wait_stream(self._stream)
         names = [Path(self.paths[i]).name for i, _ in picks]
         return {"data": self._data[slot], "seg": self._seg[slot], "name": names,

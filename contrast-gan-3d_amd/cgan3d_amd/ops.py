@@ -612,3 +612,30 @@ def unpack_patches(src: torch.Tensor, data: torch.Tensor, seg: torch.Tensor, shi
         raise TypeError("unpack_patches: seg must be bool or uint8")
     check(_launch("cgan3d_unpack_patches", ptr(src), 0 if src.dtype == torch.int16 else 1, nvox, float(shift),
                   float(factor), ptr(data), ptr(seg)), "unpack_patches")
+
+
+def augment_ws_floats(n: int, dims, n_elastic: int) -> int:
+    return int(L.lib().cgan3d_augment_ws_floats(n, *dims, n_elastic))
+
+
+def spatial_augment(data: torch.Tensor, seg: torch.Tensor, params: torch.Tensor, noise: Optional[torch.Tensor],
+                    gauss: Optional[torch.Tensor], n_elastic: int, data_out: torch.Tensor, seg_out: torch.Tensor,
+                    ws: torch.Tensor):
+    """SpatialTransform_2 on a patch batch (cgan3d_spatial_augment): data [n, 1?, a0, a1, a2] float32,
+    seg of the same shape (bool / uint8), per-sample params [n, 16]; out of place."""
+    n, dims = data.shape[0], tuple(data.shape[-3:])
+    vox = dims[0] * dims[1] * dims[2]
+    _need(data, n * vox, "spatial_augment data")
+    _need(data_out, n * vox, "spatial_augment data_out")
+    for t, nm in ((seg, "seg"), (seg_out, "seg_out")):
+        if t.dtype not in (torch.bool, torch.uint8):
+            raise TypeError(f"spatial_augment: {nm} must be bool or uint8")
+        _need(t, n * vox, f"spatial_augment {nm}", dtype=t.dtype)
+    _need(params, n * 16, "spatial_augment params")
+    if n_elastic:
+        _need(noise, n_elastic * 3 * vox, "spatial_augment noise", exact=False)
+        _need(gauss, n_elastic * 3 * max(dims), "spatial_augment gauss", exact=False)
+    _need(ws, augment_ws_floats(n, dims, n_elastic), "spatial_augment ws", exact=False)
+    check(_launch("cgan3d_spatial_augment", ptr(data), ptr(seg), n, *dims, ptr(params),
+                  ptr(noise) if n_elastic else None, n_elastic, ptr(gauss) if n_elastic else None, ptr(data_out),
+                  ptr(seg_out), ptr(ws)), "spatial_augment")

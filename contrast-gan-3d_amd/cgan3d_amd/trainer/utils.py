@@ -10,6 +10,7 @@ from typing import Dict, List, Optional, Tuple, Union
 
 import numpy as np
 
+from ..data.augment import SpatialTransform_2
 from ..data.loader import PatchLoader
 
 DEFAULT_SEED = 42  # contrast_gan_3D/constants.py
@@ -30,15 +31,33 @@ def create_dataloaders(train_fold, val_fold, train_patch_size, val_patch_size, t
     """Returns ({label: PatchLoader} for training, {label: PatchLoader} for validation).
 
     ``augmenter_class`` is accepted for signature compatibility and ignored (the loader is its
-    own prefetching pipeline).  ``train_transform`` (SpatialTransform_2) is not applied yet: a
-    warning says so."""
-    if train_transform is not None:
-        warnings.warn("create_dataloaders: spatial augmentation (train_transform) is not applied by PatchLoader")
+    own prefetching pipeline).  ``train_transform`` (the reference conf's factory of a
+    batchgenerators ``Compose([SpatialTransform_2(...), NumpyToTensor, ...])``, or a
+    :class:`cgan3d_amd.data.augment.SpatialTransform_2`) becomes the training loaders' GPU spatial
+    augmentation; the tensor conversions are what the loader does anyway."""
+    spatial = spatial_transform_from(train_transform)
 
-    def build(fold, patch, sizes, workers):
+    def build(fold, patch, sizes, workers, tf):
         return {label: PatchLoader(paths, patch, sizes[label], rng, scaler=scaler, shuffle=True, device=device,
-                                   num_threads=max(1, workers), seed_for_shuffle=seed)
+                                   num_threads=max(1, workers), seed_for_shuffle=seed, transform=tf)
                 for label, paths in divide_scans_in_fold(fold).items()}
 
-    return (build(train_fold, train_patch_size, train_batch_sizes, num_workers[0]),
-            build(val_fold, val_patch_size, val_batch_sizes, num_workers[1]))
+    return (build(train_fold, train_patch_size, train_batch_sizes, num_workers[0], spatial),
+            build(val_fold, val_patch_size, val_batch_sizes, num_workers[1], None))
+
+
+def spatial_transform_from(train_transform) -> Optional[SpatialTransform_2]:
+    """The SpatialTransform_2 inside the reference conf's ``train_transform`` (basic_conf.py:107-113):
+    a factory returning a batchgenerators Compose, a Compose, a transform, or None."""
+    if train_transform is None:
+        return None
+    t = train_transform
+    if callable(t) and not hasattr(t, "transforms") and type(t).__name__ != "SpatialTransform_2":
+        t = t()
+    for c in getattr(t, "transforms", [t]):
+        if isinstance(c, SpatialTransform_2):
+            return c
+        if type(c).__name__ == "SpatialTransform_2":  # batchgenerators' own instance: its attributes
+            return SpatialTransform_2.from_transform(c)
+    warnings.warn("create_dataloaders: train_transform holds no SpatialTransform_2; no augmentation applied")
+    return None

@@ -211,6 +211,20 @@ int cgan3d_tanh_backward(const float* y, const float* dy, float* dz, int64_t n, 
  *     seg = label != 0 --- */
 int cgan3d_unpack_patches(const void* src, int32_t src_dtype, int64_t nvox, float shift, float factor,
                           float* data, uint8_t* seg, void* stream);
+/* --- spatial augmentation (experiments/basic_conf.py:87-113: batchgenerators SpatialTransform_2,
+ * augment_spatial_2 with random_crop=False; replaces the augmenter's per-sample numpy/scipy work).
+ * data/seg: [n][a0][a1][a2] (C = 1), out of place into data_out/seg_out.  params (device, n x 16
+ * floats per sample): A[9] row-major (rotation x scale applied to the zero-centred grid), ctr[3]
+ * (patch centre, a/2 - 0.5), field slot (>= 0: elastic sample index into noise; -1: none;
+ * -2: no transform drawn, copy), mag[3] (elastic magnitude + 1e-8 per axis).  noise (device,
+ * n_elastic x 3 x a0*a1*a2): uniform [-1, 1) fields; gauss (device, n_elastic x 3 axes x
+ * max(a0, a1, a2)): circular Gaussian kernels (the inverse DFT of scipy.ndimage.fourier_gaussian's
+ * response).  data: cubic B-spline, mode 'nearest' (scipy.ndimage.map_coordinates order 3);
+ * seg: nearest neighbour, 0 outside the patch (order 0, mode 'constant'). */
+int64_t cgan3d_augment_ws_floats(int32_t n, int32_t a0, int32_t a1, int32_t a2, int32_t n_elastic);
+int cgan3d_spatial_augment(const float* data, const uint8_t* seg, int32_t n, int32_t a0, int32_t a1, int32_t a2,
+                           const float* params, const float* noise, int32_t n_elastic, const float* gauss,
+                           float* data_out, uint8_t* seg_out, float* ws, void* stream);
 
 /* --- losses (model/loss.py:11-80, model/utils.py:12-41, Trainer.py:119-154) ---
  * losses[] slots: 0 D total, 1 W_D, 2 GP, 3 G (adversarial), 4 sim (ZNCC), 5 HU, 6 G-full. */

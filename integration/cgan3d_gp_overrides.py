@@ -5,8 +5,10 @@
 
 ``train.py`` does ``globals().update(vars(<this module>))`` before it builds the Trainer
 (train.py:106-107, 154-176), so every name defined here replaces the experiment's: the model
-factories, the HU loss class and the ``Trainer`` class itself.  The optimizer partials, LR
-schedulers, batch sizes, data loaders and logger of the experiment are left untouched.
+factories, the HU loss class, the ``Trainer`` class itself and ``train_u`` (whose
+``create_dataloaders`` then builds the pinned-host -> HBM PatchLoaders with the GPU spatial
+augmentation of the experiment's ``train_transform``).  The optimizer partials, LR schedulers,
+batch sizes, transform parameters and logger of the experiment are left untouched.
 """
 import sys
 from functools import partial
@@ -34,3 +36,21 @@ gp_weight = 10
 
 # "f32" reproduces the reference's arithmetic; "bf16" runs the convolutions on bf16 MFMA
 Trainer = partial(_HipTrainer, precision="f32")
+
+
+class _TrainUtilsShim:
+    """Stand-in for train.py's module global ``train_u`` (``from contrast_gan_3D.trainer import
+    utils as train_u``, train.py:18): ``create_dataloaders`` (train.py:131) builds the pinned-host ->
+    HBM PatchLoaders with the GPU spatial augmentation; every other attribute (config_from_globals,
+    global_overrides, ...) is the reference module's own."""
+
+    def __init__(self):
+        from cgan3d_amd.trainer import utils as _ours
+        self.create_dataloaders = _ours.create_dataloaders
+
+    def __getattr__(self, name):
+        from contrast_gan_3D.trainer import utils as _ref
+        return getattr(_ref, name)
+
+
+train_u = _TrainUtilsShim()
