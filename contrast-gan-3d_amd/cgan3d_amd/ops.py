@@ -639,3 +639,21 @@ def spatial_augment(data: torch.Tensor, seg: torch.Tensor, params: torch.Tensor,
     check(_launch("cgan3d_spatial_augment", ptr(data), ptr(seg), n, *dims, ptr(params),
                   ptr(noise) if n_elastic else None, n_elastic, ptr(gauss) if n_elastic else None, ptr(data_out),
                   ptr(seg_out), ptr(ws)), "spatial_augment")
+
+
+def patch_accumulate(patches: torch.Tensor, origins: torch.Tensor, out: torch.Tensor, weight: torch.Tensor):
+    """out[origin + patch] += patch, weight[...] += 1 for a batch [b, 1?, p0, p1, p2] (origins [b, 3] int32)."""
+    b, pd = patches.shape[0], tuple(patches.shape[-3:])
+    sd = tuple(out.shape[-3:])
+    _need(patches, b * pd[0] * pd[1] * pd[2], "patch_accumulate patches")
+    _need(origins, 3 * b, "patch_accumulate origins", dtype=torch.int32)
+    _need(out, sd[0] * sd[1] * sd[2], "patch_accumulate out")
+    _need(weight, sd[0] * sd[1] * sd[2], "patch_accumulate weight")
+    check(_launch("cgan3d_patch_accumulate", ptr(patches), b, *pd, ptr(origins), ptr(out), ptr(weight), *sd),
+          "patch_accumulate")
+
+
+def patch_normalize(out: torch.Tensor, weight: torch.Tensor):
+    _need(weight, out.numel(), "patch_normalize weight")
+    _need(out, out.numel(), "patch_normalize out")
+    check(_launch("cgan3d_patch_normalize", ptr(out), ptr(weight), out.numel()), "patch_normalize")

@@ -36,3 +36,51 @@ extern "C" int cgan3d_unpack_patches(const void* src, int32_t src_dtype, int64_t
   CG_LAUNCH_CHECK("unpack_patches_kernel");
   return CGAN3D_OK;
 }
+
+// ---- whole-scan inference (eval/CCTAContrastCorrector.py, reference eval/CCTAContrastCorrector.py:
+// 60-81, patchly GridSampler + Aggregator): overlapping grid patches of the corrected scan are
+// averaged.  out / weight accumulate every patch (fp32 atomics: the squeezed last patch of a dim
+// overlaps its neighbour within one batch); cgan3d_patch_normalize divides.
+namespace cg {
+
+__global__ __launch_bounds__(256) void patch_accumulate_kernel(const float* __restrict__ patch, int b, int p0, int p1,
+                                                               int p2, const int* __restrict__ org, float* out,
+                                                               float* weight, int s0, int s1, int s2) {
+  const long long pv = (long long)p0 * p1 * p2, tot = pv * b;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < tot; i += (long long)gridDim.x * blockDim.x) {
+    const int k = (int)(i / pv);
+    const long long v = i - (long long)k * pv;
+    const int x2 = (int)(v % p2), x1 = (int)((v / p2) % p1), x0 = (int)(v / ((long long)p1 * p2));
+    const long long o = ((long long)(org[3 * k] + x0) * s1 + (org[3 * k + 1] + x1)) * s2 + (org[3 * k + 2] + x2);
+    atomicAdd(out + o, patch[i]);
+    atomicAdd(weight + o, 1.f);
+  }
+}
+
+__global__ __launch_bounds__(256) void patch_normalize_kernel(float* out, const float* __restrict__ weight, long long n) {
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x)
+    out[i] = out[i] / weight[i];
+}
+
+}  // namespace cg
+
+extern "C" int cgan3d_patch_accumulate(const float* patch, int32_t b, int32_t p0, int32_t p1, int32_t p2,
+                                       const int32_t* origins, float* out, float* weight, int32_t s0, int32_t s1,
+                                       int32_t s2, void* stream) {
+  CG_CHECK_ARG(patch && origins && out && weight && b > 0 && p0 > 0 && p1 > 0 && p2 > 0 && p0 <= s0 && p1 <= s1 &&
+               p2 <= s2, "cgan3d_patch_accumulate: bad args");
+  const long long tot = (long long)b * p0 * p1 * p2;
+  ::cg::launch(patch_accumulate_kernel, dim3((int)std::min<long long>((tot + 255) / 256, 16384)), dim3(256), 0,
+               (hipStream_t)stream, patch, (int)b, (int)p0, (int)p1, (int)p2, (const int*)origins, out, weight,
+               (int)s0, (int)s1, (int)s2);
+  CG_LAUNCH_CHECK("patch_accumulate_kernel");
+  return CGAN3D_OK;
+}
+
+extern "C" int cgan3d_patch_normalize(float* out, const float* weight, int64_t n, void* stream) {
+  CG_CHECK_ARG(out && weight && n > 0, "cgan3d_patch_normalize: bad args");
+  ::cg::launch(patch_normalize_kernel, dim3((int)std::min<long long>((n + 255) / 256, 16384)), dim3(256), 0,
+               (hipStream_t)stream, out, weight, (long long)n);
+  CG_LAUNCH_CHECK("patch_normalize_kernel");
+  return CGAN3D_OK;
+}

@@ -221,6 +221,13 @@ int cgan3d_unpack_patches(const void* src, int32_t src_dtype, int64_t nvox, floa
  * max(a0, a1, a2)): circular Gaussian kernels (the inverse DFT of scipy.ndimage.fourier_gaussian's
  * response).  data: cubic B-spline, mode 'nearest' (scipy.ndimage.map_coordinates order 3);
  * seg: nearest neighbour, 0 outside the patch (order 0, mode 'constant'). */
+/* --- whole-scan inference (eval/CCTAContrastCorrector.py:60-81, patchly GridSampler + Aggregator
+ * with averaging): add b patches [b][p0][p1][p2] at origins (b x 3 int32, device) into out[s0][s1][s2]
+ * and 1 into weight (both zeroed by the caller); cgan3d_patch_normalize: out /= weight. */
+int cgan3d_patch_accumulate(const float* patch, int32_t b, int32_t p0, int32_t p1, int32_t p2,
+                            const int32_t* origins, float* out, float* weight, int32_t s0, int32_t s1, int32_t s2,
+                            void* stream);
+int cgan3d_patch_normalize(float* out, const float* weight, int64_t n, void* stream);
 int64_t cgan3d_augment_ws_floats(int32_t n, int32_t a0, int32_t a1, int32_t a2, int32_t n_elastic);
 int cgan3d_spatial_augment(const float* data, const uint8_t* seg, int32_t n, int32_t a0, int32_t a1, int32_t a2,
                            const float* params, const float* noise, int32_t n_elastic, const float* gauss,
