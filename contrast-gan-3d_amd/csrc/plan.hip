@@ -19,6 +19,17 @@ thread_local Plan* g_rec = nullptr;
 static hipEvent_t g_eager_events[64];
 static int g_eager_next = -1;
 
+// Cross-stream waits join two streams of one device, so the event's release only has to reach
+// device scope: hipEventDisableSystemFence skips the system-scope cache write-back a default event
+// record issues (CGAN3D_EVENT_SYSTEM_FENCE=1 restores it for A/B runs).
+static unsigned event_flags() {
+  static const unsigned f = [] {
+    const char* v = getenv("CGAN3D_EVENT_SYSTEM_FENCE");
+    return hipEventDisableTiming | ((v && v[0] == '1') ? 0u : (unsigned)hipEventDisableSystemFence);
+  }();
+  return f;
+}
+
 }  // namespace cg
 
 using namespace cg;
@@ -69,7 +80,7 @@ extern "C" int cgan3d_stream_wait(void* waiter, void* signaler) {
   if (w == s) return CGAN3D_OK;
   hipEvent_t ev;
   if (g_rec != nullptr) {
-    if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) {
+    if (hipEventCreateWithFlags(&ev, event_flags()) != hipSuccess) {
       set_error("cgan3d_stream_wait: hipEventCreate failed");
       return CGAN3D_EHIP;
     }
@@ -83,7 +94,7 @@ extern "C" int cgan3d_stream_wait(void* waiter, void* signaler) {
   // eager: a small ring (an event may be re-recorded once the wait on it has been enqueued)
   if (g_eager_next < 0) {
     for (auto& e : g_eager_events)
-      if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) {
+      if (hipEventCreateWithFlags(&e, event_flags()) != hipSuccess) {
         set_error("cgan3d_stream_wait: hipEventCreate failed");
         return CGAN3D_EHIP;
       }

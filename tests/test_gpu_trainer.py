@@ -160,8 +160,11 @@ def test_trainer_plan_replay_matches_eager(tmp_path, precision, monkeypatch):
         torch.cuda.synchronize()
         (_, ie, de), (_, ip, dp) = eager.logger_interface.logger.losses[-1], planned.logger_interface.logger.losses[-1]
         assert ie == ip == it and sorted(de) == sorted(dp)
-        for k in de:  # weight-gradient atomics may add in another order
-            assert abs(de[k] - dp[k]) <= 1e-5 * max(abs(de[k]), 1e-2), (it, k, de[k], dp[k])
+        for k in de:  # weight-gradient atomics may add in another order; the full iteration's
+            # generator losses go through the critic just updated (bf16: its operands may round the
+            # other way where an Adam step flipped a noise-level element, see below)
+            ltol = 1e-4 if (precision == "bf16" and it % 2 == 0 and k != "D") else 1e-5
+            assert abs(de[k] - dp[k]) <= ltol * max(abs(de[k]), 1e-2), (it, k, de[k], dp[k])
         arenas = [(eager.engine.d_arena, planned.engine.d_arena)]
         if it % 2 == 0:
             arenas.append((eager.engine.g_arena, planned.engine.g_arena))
