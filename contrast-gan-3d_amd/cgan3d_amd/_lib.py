@@ -16,6 +16,7 @@ import torch  # noqa: F401  (must be imported first: see module docstring)
 LIB_PATH = Path(__file__).resolve().parent / "libcgan3d.so"
 
 ACT_NONE, ACT_RELU, ACT_LRELU, ACT_TANH = 0, 1, 2, 3
+WGRAD_ACCUMULATE, WGRAD_WS_CLEAN = 1, 2  # cgan3d_conv3d_wgrad_ex flag word
 # device loss slots written by the loss kernels (include/cgan3d.h)
 L_D, L_WD, L_GP, L_G, L_SIM, L_HU, L_GFULL = range(7)
 
@@ -33,6 +34,20 @@ class PackDesc(C.Structure):
                 ("taps", C.c_int32), ("cin", C.c_int32), ("cout", C.c_int32), ("ldb", C.c_int32),
                 ("format", C.c_int32), ("reserved", C.c_int32)]
 
+
+class CsumDesc(C.Structure):
+    _fields_ = [("x", C.c_void_p), ("out", C.c_void_p), ("ws", C.c_void_p), ("nvox", C.c_int64), ("c", C.c_int32),
+                ("accumulate", C.c_int32)]
+
+
+class LnArgs(C.Structure):
+    _fields_ = [("n", C.c_int32), ("mode", C.c_int32), ("L", C.c_int64), ("slope", C.c_float), ("eps", C.c_float),
+                ("z", C.c_void_p), ("da", C.c_void_p), ("zdot", C.c_void_p), ("adot", C.c_void_p),
+                ("abar", C.c_void_p), ("p_stats", C.c_void_p), ("p_bwd", C.c_void_p), ("p_jvp", C.c_void_p),
+                ("p_sig", C.c_void_p), ("p_adj", C.c_void_p)]
+
+
+LN_STATS, LN_BWD, LN_JVP, LN_SIG, LN_ADJ = range(5)
 
 PREC_F32, PREC_BF16 = 0, 1
 
@@ -73,6 +88,7 @@ _SIGS = {
     "cgan3d_bn_backward": ([_P, _P, _I64, _I32, _P, _P, _P, _I32, _F, _P, _P, _P, _I32, _P, _P], _I32),
     "cgan3d_channel_sum_ws_floats": ([_I64, _I32], _I64),
     "cgan3d_channel_sum": ([_P, _I64, _I32, _P, _P, _P], _I32),
+    "cgan3d_channel_sum_multi": ([_P, _I32, _I32, _P], _I32),
     "cgan3d_reflect_fold": ([_P, _P, _I32, _I32, _I32, _I32, _I32, _I32, _P], _I32),
     "cgan3d_reflect_fold_slots": ([_I32, _I32, _I32, _I32, _I32], _I32),
     "cgan3d_reflect_fold_ex": ([_P, _P, _I32, _I32, _I32, _I32, _I32, _I32, _P, _P], _I32),
@@ -90,6 +106,11 @@ _SIGS = {
     "cgan3d_generator_output_grad": ([_P, _P, _P, _P, _P, _I64, _F, _F, _F, _F, _P, _P, _P, _P], _I32),
     "cgan3d_adam_tick": ([_P, _P], _I32),
     "cgan3d_adam": ([_P, _P, _P, _P, _I64, _P, _P], _I32),
+    "cgan3d_zero": ([_P, _I64, _P], _I32),
+    "cgan3d_ln_partial_doubles": ([_I32, _I64], _I64),
+    "cgan3d_ln_reduce": ([_P, _P, _P], _I32),
+    "cgan3d_ln_apply": ([_P, _P, _P], _I32),
+    "cgan3d_conv3d_wgrad_ws_mode": ([_P], _I32),
     "cgan3d_plan_begin": ([], _I32),
     "cgan3d_plan_end": ([C.POINTER(C.c_void_p)], _I32),
     "cgan3d_plan_size": ([_P], _I64),

@@ -217,6 +217,9 @@ class GeneratorPlan:
         # needs its layer's dz and input, both final when it is enqueued); own workspace
         wsw = max([ops.wgrad_ws_floats(gw) for gw in self.geo_wgrad] + [ops.wgrad_ws_floats(self.geo_last_wgrad)])
         self.ws_side = torch.empty(wsw, device=device)
+        # all-zero workspace of the weight grads that sum into theirs by atomics (CGAN3D_WGRAD_WS_CLEAN:
+        # each leaves it zeroed, so no memset per layer); they all run on the side stream, in turn
+        self.ws_clean = torch.zeros(wsw, device=device)
         # (CGAN3D_NO_SIDE_STREAM=1 serialises them, so a kernel trace shows unshared durations)
         on_gpu = torch.device(device).type == "cuda" and not os.environ.get("CGAN3D_NO_SIDE_STREAM")
         self.side = torch.cuda.Stream(device=device) if on_gpu else None
@@ -284,16 +287,24 @@ class GeneratorPlan:
             self.ss[i][c:].copy_(P[f"{nb}.bias"] - P[f"{nb}.running_mean"] * sc)
 
     # -- backward from dz_last = dL/d(pre-tanh) ; writes parameter grads into G (grad views)
+    def _wgrad(self, g, a, b, dw, zeroed: bool, **kw):
+        """Weight gradient on the side stream's workspaces: into a pre-zeroed gradient arena
+        (``zeroed``) every layer accumulates, and the atomic-workspace geometries take the clean one."""
+        if zeroed and ops.wgrad_ws_atomic(g):
+            return ops.wgrad(g, a, b, dw, self.ws_clean, accumulate=True, ws_clean=True, **kw)
+        return ops.wgrad(g, a, b, dw, self.ws_side, accumulate=zeroed, **kw)
+
     def backward(self, P: Dict[str, torch.Tensor], G: Dict[str, torch.Tensor], x: torch.Tensor,
-                 grads_enqueued: Optional[Callable[[int], None]] = None):
+                 grads_enqueued: Optional[Callable[[int], None]] = None, zeroed: bool = False):
         """``grads_enqueued(i)`` (optional) is called once every launch producing layer i's
         parameter gradients is enqueued (i = len(layers) for the last conv, which goes first; then
-        len(layers) - 1 down to 0): the data-parallel engine starts bucket all-reduces there."""
+        len(layers) - 1 down to 0): the data-parallel engine starts bucket all-reduces there.
+        ``zeroed``: the gradient views in G were zeroed (one memset of the arena) after the last
+        reader, so weight gradients are added into them without a memset per layer."""
         la = self.last
         n = self.n
         u = self.y[-1]
-        self._on_side(lambda: ops.wgrad(self.geo_last_wgrad, u, self.dz_last, G["model.last_conv.weight"],
-                                        self.ws_side))
+        self._on_side(lambda: self._wgrad(self.geo_last_wgrad, u, self.dz_last, G["model.last_conv.weight"], zeroed))
         nvl = n * la.dout[0] * la.dout[1] * la.dout[2]
         ops.channel_sum(self.dz_last, nvl, 1, G["model.last_conv.bias"], self.ws)
         if grads_enqueued is not None:
@@ -320,10 +331,10 @@ class GeneratorPlan:
                 x16 = d16 = None
             if ly.kind == "convt":  # ConvTranspose3d: the output-grad is the gathered operand
                 self._on_side(lambda g=self.geo_wgrad[i], a=self.dz[i], b=xin, w=G[wname], a16=d16, b16=x16:
-                              ops.wgrad(g, a, b, w, self.ws_side, gathered16=a16, aligned16=b16))
+                              self._wgrad(g, a, b, w, zeroed, gathered16=a16, aligned16=b16))
             else:
                 self._on_side(lambda g=self.geo_wgrad[i], a=xin, b=self.dz[i], w=G[wname], a16=x16, b16=d16:
-                              ops.wgrad(g, a, b, w, self.ws_side, gathered16=a16, aligned16=b16))
+                              self._wgrad(g, a, b, w, zeroed, gathered16=a16, aligned16=b16))
             if grads_enqueued is not None:
                 grads_enqueued(i)
             if i == 0:
@@ -394,6 +405,11 @@ class CriticPlan:
         self.bn = cfg.norm == "batch"
         # BatchNorm layers: the middle convs of the BN critic (no conv bias, blocks.py:34)
         self.is_bn = [self.bn and ly.name.startswith("model.middle.") for ly in ls]
+        # LayerNorm layers: the middle convs of the gp_layernorm conf's critic (no conv bias; per-sample
+        # normalisation over (C, D, H, W), no affine parameters: gp_layernorm.py:9-11)
+        self.ln = cfg.norm == "layer"
+        self.is_ln = [self.ln and ly.name.startswith("model.middle.") for ly in ls]
+        self.biased = [not (self.is_bn[i] or self.is_ln[i]) for i in range(len(ls))]
         self.logit_ps = dn[0] * dn[1] * dn[2]
         self.a = [torch.empty((nmax, *ly.dout, ly.cout), device=device) for ly in ls]   # activations (last = logits)
         self.dz = [torch.empty((nmax, *ly.dout, ly.cout), device=device) for ly in ls]  # dL/dz (last = dlogits)
@@ -404,6 +420,7 @@ class CriticPlan:
             ws = max(ws, ops.wgrad_ws_floats(g), ops.channel_sum_ws_floats(nv, ly.cout),
                      ops.bn_backward_ws_floats(nv, ly.cout))
         self.ws = torch.empty(ws, device=device)
+        self.ws_clean = torch.zeros(ws, device=device)  # see GeneratorPlan.ws_clean
         # CGAN3D_CRITIC_SIDE=1: GP-configuration weight / bias gradients on a side stream beside the
         # penalty's forward-mode chain (own workspace).  Off by default: measured 2.7 % slower per
         # step at 64^3 B=4 (the chain's kernels are short and lose CUs to the gradient launches)
@@ -418,6 +435,22 @@ class CriticPlan:
             self.ss = [[torch.empty(2 * ly.cout, device=device) for ly in ls] for _ in range(2)]
             self.mi = [[torch.empty(2 * ly.cout, device=device) for ly in ls] for _ in range(2)]
             self.bn_scratch = [torch.empty(2 * ly.cout, device=device) for ly in ls]  # discarded dgamma/dbeta
+        if self.ln:
+            # conv outputs z, dL/da, and per-sample partial sums (ops.ln_*) of every LayerNorm layer;
+            # the penalty's tangent (zdot, adot) and primal-adjoint (abar, zbar) chains over the
+            # interpolation rows (at most nmax), and the penalty direction gamma
+            vol = [ly.dout[0] * ly.dout[1] * ly.dout[2] * ly.cout for ly in ls]
+            self.L = vol
+            self.z = [torch.empty_like(self.a[i]) if b else None for i, b in enumerate(self.is_ln)]
+            self.dy = [torch.empty_like(self.a[i]) if b else None for i, b in enumerate(self.is_ln)]
+            npart = [ops.ln_partial_doubles(nmax, v) for v in vol]
+            self.lnp = {k: [torch.empty(npart[i], device=device, dtype=torch.float64) if b else None
+                            for i, b in enumerate(self.is_ln)] for k in ("stats", "bwd", "jvp", "sig", "adj")}
+            self.zdot = [torch.empty_like(self.a[i]) if b else None for i, b in enumerate(self.is_ln)]
+            self.adot = [torch.empty_like(self.a[i]) for i in range(len(ls) - 1)]
+            self.abar = [torch.empty_like(self.a[i]) for i in range(len(ls) - 1)]
+            self.zbar = [torch.empty_like(self.a[i]) for i in range(len(ls) - 1)]
+            self.gam = torch.empty((nmax, *dims, cfg.channels_in), device=device)
         # packed weight copies per (layer, role); the packed layout does not depend on batch/dims
         self.packs = ops.PackSet(device)
         self.wf, self.wd = [], []
@@ -467,6 +500,12 @@ class CriticPlan:
                     _running_scale_shift(P, nb, ss)
                 nvox = n * ly.dout[0] * ly.dout[1] * ly.dout[2]
                 ops.bn_apply(z, nvox, ly.cout, ss, L.ACT_LRELU, out, slope=self.slope)
+            elif self.is_ln[i]:
+                z = self._sl(self.z[i], off, n)
+                ops.conv(g, h, w, z)
+                ps = self._lp("stats", i, off)
+                ops.ln_reduce(L.LN_STATS, n, self.L[i], self.slope, ps, z=z, p_stats=ps)
+                ops.ln_apply(L.LN_STATS, n, self.L[i], self.slope, out, z=z, p_stats=ps)
             else:
                 last = i == len(self.layers) - 1
                 ep = ops.epilogue(bias=P[f"{ly.name}.bias"], act=L.ACT_NONE if last else L.ACT_LRELU,
@@ -474,6 +513,12 @@ class CriticPlan:
                 ops.conv(g, h, w, out, ep)
             h = out
         return self._sl(self.a[-1], off, n)
+
+    def _lp(self, kind: str, i: int, off: int):
+        """LayerNorm layer i's partial sums of ``kind`` from sample ``off`` on."""
+        t = self.lnp[kind][i]
+        k = t.numel() // self.nmax
+        return t[off * k:]
 
     def input_grad(self, P, off: int, n: int, dx_out: torch.Tensor, dx_off: int, dx_n: int, bn_pass: int = 0,
                    G=None, bn_accumulate: bool = False):
@@ -497,6 +542,14 @@ class CriticPlan:
                                 self.mi[bn_pass][i - 1], P[f"{nb}.weight"], L.ACT_LRELU, dg, db,
                                 self._sl(self.dz[i - 1], off, n), self.ws, slope=self.slope,
                                 accumulate=bn_accumulate and G is not None)
+            elif self.is_ln[i - 1]:  # dL/da -> LayerNorm + LeakyReLU backward -> dL/dz
+                da, z = self._sl(self.dy[i - 1], off, n), self._sl(self.z[i - 1], off, n)
+                ops.conv(g, self._sl(self.dz[i], off, n), w, da)
+                ps, pb = self._lp("stats", i - 1, off), self._lp("bwd", i - 1, off)
+                Li = self.L[i - 1]
+                ops.ln_reduce(L.LN_BWD, n, Li, self.slope, pb, z=z, da=da, p_stats=ps)
+                ops.ln_apply(L.LN_BWD, n, Li, self.slope, self._sl(self.dz[i - 1], off, n), z=z, da=da, p_stats=ps,
+                             p_bwd=pb)
             else:
                 ops.conv(g, self._sl(self.dz[i], off, n), w, self._sl(self.dz[i - 1], off, n),
                          ops.epilogue(mask_src=self._sl(self.a[i - 1], off, n), slope=self.slope))
@@ -529,25 +582,25 @@ class CriticPlan:
         if self.side is not None:
             ops.stream_wait(torch.cuda.current_stream(self.device), self.side)
 
+    def _wgrad(self, g, a, b, dw, ws, zeroed: bool):
+        if zeroed and ops.wgrad_ws_atomic(g):
+            return ops.wgrad(g, a, b, dw, self.ws_clean, accumulate=True, ws_clean=True)
+        return ops.wgrad(g, a, b, dw, ws, accumulate=zeroed)
+
     def gp_grads_overlapped(self, P, G, x_all: torch.Tensor, gamma: torch.Tensor, off: int, n: int, n_all: int,
-                            n_bias: int):
+                            n_bias: int, zeroed: bool = False):
         """``gp_forward_mode`` + ``weight_grads`` with the gradient launches on the side stream:
         the bias sums as soon as the input-grad chain is done, dW_l as soon as nu_{l-1} (the
         forward-mode output it gathers) is written; the forward-mode chain stays on the main
         stream.  Call ``join_side`` before anything reads the gradients or reuses a / dz."""
         ws = self.ws_side
 
-        def biases():
-            for i, ly in enumerate(self.layers):
-                if not self.is_bn[i]:
-                    nv = n_bias * ly.dout[0] * ly.dout[1] * ly.dout[2]
-                    ops.channel_sum(self.dz[i][:n_bias], nv, ly.cout, G[f"{ly.name}.bias"], ws)
-        self._on_side(biases)
+        self._on_side(lambda: self._bias_sums(G, n_bias, side=True).run())
 
         def wgrad(i, prev):
             ly = self.layers[i]
             g = ops.with_prec(ops.conv_wgrad_geom(n_all, ly.din, ly.dout, ly.cin, ly.cout, ly.k, ly.s, ly.p), self.prec)
-            ops.wgrad(g, prev, self.dz[i][:n_all], G[f"{ly.name}.weight"], ws)
+            self._wgrad(g, prev, self.dz[i][:n_all], G[f"{ly.name}.weight"], ws, zeroed)
         self._on_side(lambda: wgrad(0, x_all))  # x_all's interpolation rows hold gamma = nu_0
         h = gamma
         for i, ly in enumerate(self.layers[:-1]):
@@ -558,16 +611,94 @@ class CriticPlan:
             h = out
             self._on_side(lambda i=i: wgrad(i + 1, self.a[i][:n_all]))  # a_i now holds nu_i in its interp rows
 
-    def weight_grads(self, P, G, x_all: torch.Tensor, n_all: int, n_bias: int):
+    def _bias_sums(self, G, n_bias: int, side: bool = False) -> "ops.ChannelSumSet":
+        """db_l = sum of dz_l over the first n_bias samples, every biased layer in two launches
+        (built once per (n_bias, stream role); the gradient views and dz buffers keep their addresses)."""
+        key = (n_bias, side, id(G))
+        cache = self.__dict__.setdefault("_csum", {})
+        if key not in cache:
+            items = [(self.dz[i], n_bias * ly.dout[0] * ly.dout[1] * ly.dout[2], ly.cout, G[f"{ly.name}.bias"], False)
+                     for i, ly in enumerate(self.layers) if self.biased[i]]
+            cache[key] = ops.ChannelSumSet(self.device, items)
+        return cache[key]
+
+    def weight_grads(self, P, G, x_all: torch.Tensor, n_all: int, n_bias: int, zeroed: bool = False):
         """dW_l = wgrad(a_{l-1}, dz_l) over n_all samples; db_l = sum dz_l over the first n_bias."""
         prev = x_all
         for i, ly in enumerate(self.layers):
             g = ops.with_prec(ops.conv_wgrad_geom(n_all, ly.din, ly.dout, ly.cin, ly.cout, ly.k, ly.s, ly.p), self.prec)
-            ops.wgrad(g, prev, self.dz[i][:n_all], G[f"{ly.name}.weight"], self.ws)
-            if not self.is_bn[i]:
-                nv = n_bias * ly.dout[0] * ly.dout[1] * ly.dout[2]
-                ops.channel_sum(self.dz[i][:n_bias], nv, ly.cout, G[f"{ly.name}.bias"], self.ws)
+            self._wgrad(g, prev, self.dz[i][:n_all], G[f"{ly.name}.weight"], self.ws, zeroed)
             prev = self.a[i][:n_all]
+        self._bias_sums(G, n_bias).run()
+
+    def gp_grads_ln(self, P, G, x_all: torch.Tensor, gamma: torch.Tensor, off: int, n: int):
+        """Critic gradients of the LayerNorm critic with the gradient penalty (gp_layernorm conf),
+        into a zeroed arena G.  Rows [0, off) are the real / fake samples of the Wasserstein loss,
+        rows [off, off + n) the interpolation, whose dz chain (input_grad) carries dSum(D)/dx;
+        ``gamma`` = dGP/dg.  The penalty's parameter gradient is d/dtheta of the directional
+        derivative s = <dD/dx, gamma> (model/utils.py:34-41 differentiated): a tangent forward
+        along gamma (LayerNorm linearised at the interpolation's statistics), whose adjoint is the
+        existing dz chain, plus the primal adjoint the LayerNorm tangent injects at every middle
+        layer (ln.hip header), propagated down through the primal convs.  Weight gradients:
+        wgrad(a_{l-1}, dz_l) over real/fake + wgrad(adot_{l-1}, dz_l) + wgrad(a_{l-1}, zbar_l) over
+        the interpolation; the first bias also receives sum zbar_0."""
+        nl = len(self.layers)
+        sl = self.slope
+        sl_ = lambda t: t[off:off + n]  # noqa: E731
+        geo = lambda i, m, role: self._geo(getattr(ops, role)(m, self.layers[i].din, self.layers[i].dout,  # noqa: E731
+                                                               self.layers[i].cin, self.layers[i].cout, 4,
+                                                               self.layers[i].s, 1),
+                                           self.wf[i] if role == "conv_fwd_geom" else self.wd[i])
+        wt = lambda i, role: ((self.wf[i] if role == "fwd" else self.wd[i]) if (  # noqa: E731
+            self.wf[i] if role == "fwd" else self.wd[i]) is not None else P[f"{self.layers[i].name}.weight"])
+        # 1. tangent forward along gamma
+        for i in range(nl - 1):
+            src = gamma if i == 0 else self.adot[i - 1][:n]
+            if self.is_ln[i]:
+                zd, z, da = self.zdot[i][:n], sl_(self.z[i]), sl_(self.dy[i])
+                ops.conv(geo(i, n, "conv_fwd_geom"), src, wt(i, "fwd"), zd)
+                ps, pj, pg = self._lp("stats", i, off), self._lp("jvp", i, 0), self._lp("sig", i, 0)
+                ops.ln_reduce(L.LN_JVP, n, self.L[i], sl, pj, z=z, zdot=zd, p_stats=ps)
+                ops.ln_apply(L.LN_JVP, n, self.L[i], sl, self.adot[i][:n], z=z, zdot=zd, p_stats=ps, p_jvp=pj)
+                ops.ln_reduce(L.LN_SIG, n, self.L[i], sl, pg, z=z, da=da, adot=self.adot[i][:n], p_stats=ps)
+            else:
+                ops.conv(geo(i, n, "conv_fwd_geom"), src, wt(i, "fwd"), self.adot[i][:n],
+                         ops.epilogue(mask_src=sl_(self.a[i]), slope=sl))
+        # 2. primal adjoint, top LayerNorm layer down (nothing reaches the top one from above)
+        for i in range(nl - 2, -1, -1):
+            if i < nl - 2:
+                ab = self.abar[i][:n] if self.is_ln[i] else self.zbar[i][:n]
+                ep = None if self.is_ln[i] else ops.epilogue(mask_src=sl_(self.a[i]), slope=sl)
+                ops.conv(geo(i + 1, n, "conv_dgrad_geom"), self.zbar[i + 1][:n], wt(i + 1, "dgrad"), ab, ep)
+            else:
+                ab = None
+            if self.is_ln[i]:
+                z, da, zd = sl_(self.z[i]), sl_(self.dy[i]), self.zdot[i][:n]
+                ps, pb = self._lp("stats", i, off), self._lp("bwd", i, off)
+                pj, pg, pa = self._lp("jvp", i, 0), self._lp("sig", i, 0), self._lp("adj", i, 0)
+                kw = dict(z=z, da=da, zdot=zd, abar=ab, p_stats=ps, p_bwd=pb, p_jvp=pj)
+                ops.ln_reduce(L.LN_ADJ, n, self.L[i], sl, pa, **kw)
+                ops.ln_apply(L.LN_ADJ, n, self.L[i], sl, self.zbar[i][:n], p_sig=pg, p_adj=pa, **kw)
+            elif ab is None:
+                raise NotImplementedError("LayerNorm critic: the layer below the last conv must be a LayerNorm block")
+        # 3. weight gradients (accumulated) and biases
+        for i, ly in enumerate(self.layers):
+            wg = lambda m: ops.with_prec(ops.conv_wgrad_geom(m, ly.din, ly.dout, ly.cin, ly.cout, ly.k, ly.s, ly.p),  # noqa
+                                         self.prec)
+            dw = G[f"{ly.name}.weight"]
+            prev = x_all if i == 0 else self.a[i - 1]
+            self._wgrad(wg(off), prev[:off], self.dz[i][:off], dw, self.ws, True)
+            self._wgrad(wg(n), gamma if i == 0 else self.adot[i - 1][:n], sl_(self.dz[i]), dw, self.ws, True)
+            if i < nl - 1:
+                self._wgrad(wg(n), sl_(prev), self.zbar[i][:n], dw, self.ws, True)
+        self._bias_sums(G, off).run()
+        key = ("zbar0", n, id(G))
+        cache = self.__dict__.setdefault("_csum", {})
+        if key not in cache:
+            ly = self.layers[0]
+            cache[key] = ops.ChannelSumSet(self.device, [(self.zbar[0], n * ly.dout[0] * ly.dout[1] * ly.dout[2],
+                                                          ly.cout, G[f"{ly.name}.bias"], True)])
+        cache[key].run()
 
 
 # ----------------------------------------------------------------------------------------------
@@ -581,14 +712,15 @@ class StepEngine:
                  weight_clip: Optional[float] = None):
         if b_opt != b_sub:
             raise NotImplementedError("StepEngine: the GP path assumes |OPT| == |LOW|+|HIGH| (basic_conf.py:74-79)")
-        if d_cfg.norm not in ("identity", "batch"):
-            raise NotImplementedError(f"StepEngine: critic norm {d_cfg.norm!r} (LayerNorm critic: SURVEY.md §8f row 4)")
+        if d_cfg.norm not in ("identity", "batch", "layer"):
+            raise NotImplementedError(f"StepEngine: critic norm {d_cfg.norm!r}")
         # gradient penalty unless weight clipping (Trainer.py:122-131): the GP conf (Identity-norm
-        # critic) or the weight-clip conf (BatchNorm critic, basic_conf.py:37,60-66)
+        # critic), the gp_layernorm conf (LayerNorm critic, gp_layernorm.py:9-11) or the weight-clip
+        # conf (BatchNorm critic, basic_conf.py:37,60-66)
         self.use_gp = weight_clip is None
-        if self.use_gp and d_cfg.norm != "identity":
+        if self.use_gp and d_cfg.norm == "batch":
             raise NotImplementedError("gradient penalty through a BatchNorm critic needs BatchNorm double backward "
-                                      "(SURVEY.md §8f row 4)")
+                                      "(no reference configuration uses it: SURVEY.md §8f row 4)")
         device = device or torch.device("cuda", torch.cuda.current_device())
         self.device = device
         self.dims = tuple(dims)
@@ -762,9 +894,19 @@ class StepEngine:
         D.forward(self.dP, self.xc, 0, nall)
         ops.critic_logits_grad(D.a[-1], bo, bs, bg, D.logit_ps, self.gan_w, D.dz[-1], self.losses)
         D.input_grad(self.dP, 0, nall, self.gbuf, bo + bs, bg)
+        if D.ln:  # LayerNorm critic: the interpolation stays in xc (its primal adjoint needs it)
+            gamma = D.gam[:bg]
+            ops.gradient_penalty(self.gbuf, bg, V, self.gp_weight, gamma, self.losses, self.loss_ws)
+            ops.zero(self.d_arena.grad)  # optimizer_D.zero_grad (Trainer.py:109)
+            D.gp_grads_ln(self.dP, self.dG, self.xc, gamma, bo + bs, bg)
+            self._allreduce(self.d_arena.grad)
+            self.d_optim.launch()
+            self.D.pack()
+            return
         gamma = self.xc[bo + bs:]
         ops.gradient_penalty(self.gbuf, bg, V, self.gp_weight, gamma, self.losses, self.loss_ws)
-        D.gp_grads_overlapped(self.dP, self.dG, self.xc, gamma, bo + bs, bg, nall, bo + bs)
+        ops.zero(self.d_arena.grad)  # optimizer_D.zero_grad (Trainer.py:109): every layer then accumulates
+        D.gp_grads_overlapped(self.dP, self.dG, self.xc, gamma, bo + bs, bg, nall, bo + bs, zeroed=True)
         D.join_side()
         self._allreduce(self.d_arena.grad)  # on the critical path: the G update uses the new critic
         self.d_optim.launch()
@@ -778,9 +920,10 @@ class StepEngine:
         D.forward(self.dP, self.xc[:bo], 0, bo, bn_pass=0)
         D.forward(self.dP, self.opt_hat, bo, bs, bn_pass=1)
         ops.critic_logits_grad(D.a[-1], bo, bs, 0, D.logit_ps, self.gan_w, D.dz[-1], self.losses)
+        ops.zero(self.d_arena.grad)  # optimizer_D.zero_grad (Trainer.py:109)
         D.input_grad(self.dP, 0, bo, self.gbuf, 0, 0, bn_pass=0, G=self.dG)
         D.input_grad(self.dP, bo, bs, self.gbuf, 0, 0, bn_pass=1, G=self.dG, bn_accumulate=True)
-        D.weight_grads(self.dP, self.dG, self.xc[:bo + bs], bo + bs, bo + bs)
+        D.weight_grads(self.dP, self.dG, self.xc[:bo + bs], bo + bs, bo + bs, zeroed=True)
         self._allreduce(self.d_arena.grad)
         self.d_optim.launch()
         self.D.pack()
@@ -792,11 +935,12 @@ class StepEngine:
         D.input_grad(self.dP, 0, bs, self.dcrit, 0, bs)
         ops.generator_output_grad(self.opt_hat, self.subopt, self.G.att, self.mask, self.dcrit, bs * V, self.lo,
                                   self.hi, self.sim_w, self.hu_w, self.G.dz_last, self.losses, self.loss_ws)
+        ops.zero(self.g_arena.grad)  # optimizer_G.zero_grad (Trainer.py:146): every layer then accumulates
         if self.dp:  # bucketed, overlapped with the rest of the backward
-            self.G.backward(self.gP, self.gG, self.subopt, grads_enqueued=self._bucket_ready)
+            self.G.backward(self.gP, self.gG, self.subopt, grads_enqueued=self._bucket_ready, zeroed=True)
             self._finish_allreduce()
         else:
-            self.G.backward(self.gP, self.gG, self.subopt)
+            self.G.backward(self.gP, self.gG, self.subopt, zeroed=True)
         self.g_optim.launch()
         self.G.pack()
 

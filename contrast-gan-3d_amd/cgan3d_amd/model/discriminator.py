@@ -6,7 +6,9 @@ same ``state_dict``.  The hot-path configuration is the gradient-penalty critic
 bias + LeakyReLU(0.2) fused in the conv epilogue, last k4 s1 p1 conv to one channel.  Under
 autograd ``backward`` runs the critic input-grad chain (LeakyReLU masks fused into the
 input-grad conv epilogues) and the weight-grad kernels.  The GP's double backward is done by the
-Trainer's step engine (``cgan3d_amd.engine``), not through autograd.
+Trainer's step engine (``cgan3d_amd.engine``), not through autograd.  Also built: the weight-clip
+conf's BatchNorm critic and the gp_layernorm conf's LayerNorm critic (``norm_layer=nn.LayerNorm``,
+``patch_size=(1, *patch)``, ``elementwise_affine=False``: ``experiments/gp_layernorm.py:9-11``).
 """
 from __future__ import annotations
 
@@ -36,13 +38,17 @@ class PatchGANDiscriminator(nn.Module):
         super().__init__()
         stride = 2
         slope = kwargs.get("negative_slope", 0.01)
-        norm = {None: "batch", nn.BatchNorm3d: "batch", nn.BatchNorm2d: "batch", nn.Identity: "identity"}.get(
-            norm_layer, "other")
+        norm = {None: "batch", nn.BatchNorm3d: "batch", nn.BatchNorm2d: "batch", nn.Identity: "identity",
+                nn.LayerNorm: "layer"}.get(norm_layer, "other")
         self.config = CriticConfig(channels_in, init_channels_out, discriminator_depth, slope, norm)
         self._unsupported = None
-        if is_2D or kernel_size != 4 or padding != 1 or norm not in ("identity", "batch"):
-            self._unsupported = ("the HIP critic implements the 3-D k4 p1 critic with Identity norm (GP conf) or "
-                                 "BatchNorm (weight-clip conf); LayerNorm/2-D critics are SURVEY.md §8f row 4")
+        if is_2D or kernel_size != 4 or padding != 1 or norm not in ("identity", "batch", "layer"):
+            self._unsupported = ("the HIP critic implements the 3-D k4 p1 critic with Identity norm (GP conf), "
+                                 "BatchNorm (weight-clip conf) or LayerNorm (gp_layernorm conf); 2-D critics are "
+                                 "SURVEY.md §8f row 4")
+        elif norm == "layer" and kwargs.get("elementwise_affine", True):
+            self._unsupported = ("the HIP LayerNorm critic implements the gp_layernorm conf's LayerNorm without "
+                                 "affine parameters (gp_layernorm.py:9-11: elementwise_affine=False)")
         model = [("first", ConvBlock(is_2D, channels_in, init_channels_out, kernel_size, stride=stride,
                                      padding=padding, norm_layer=nn.Identity, activation_fn=nn.LeakyReLU, **kwargs))]
         middle = []
@@ -58,9 +64,26 @@ class PatchGANDiscriminator(nn.Module):
             middle.append(ConvBlock(is_2D, in_, out_, kernel_size, stride=stride, padding=padding,
                                     norm_layer=norm_layer, activation_fn=nn.LeakyReLU, **kwargs))
         model.append(("middle", nn.Sequential(*middle)))
+        if norm == "layer" and self._unsupported is None and any(
+                len(m.normalization.normalized_shape) != 4 for m in middle):
+            self._unsupported = ("the HIP LayerNorm critic normalises each sample over (C, D, H, W): pass "
+                                 "patch_size=(1, D, H, W) as gp_layernorm.py:9-11 does")
         model.append(("last", (nn.Conv2d if is_2D else nn.Conv3d)(out_, 1, kernel_size=kernel_size, stride=1,
                                                                    padding=padding)))
         self.model = nn.Sequential(OrderedDict(model))
+
+    def _check_layernorm_shape(self, dims):
+        """nn.LayerNorm's normalized_shape is fixed at construction (the patch size): reject
+        other patch sizes as torch would."""
+        if self.config.norm != "layer":
+            return
+        d = [(x + 2 - 4) // 2 + 1 for x in dims]  # the first k4 s2 p1 conv
+        for m in self.model.middle:
+            d = [(x + 2 - 4) // 2 + 1 for x in d]
+            want = (m.conv.out_channels, *d)
+            if tuple(m.normalization.normalized_shape) != want:
+                raise RuntimeError(f"LayerNorm normalized_shape {tuple(m.normalization.normalized_shape)} does not "
+                                   f"match the block output {want} (patch size {tuple(dims)})")
 
     def _tensors(self):
         return dict(self.state_dict(keep_vars=True))  # parameters and BatchNorm buffers
@@ -90,6 +113,7 @@ class PatchGANDiscriminator(nn.Module):
         if torch.is_grad_enabled() and (x.requires_grad or any(p.requires_grad for p in params)):
             return _CriticFn.apply(x, self, *params)
         n, _, *dims = x.shape
+        self._check_layernorm_shape(dims)
         plan = self.plan_for(n, dims)
         logits = plan.forward(self._tensors(), x.detach().float().contiguous().view(n, *dims, 1), 0, n,
                               training=self.training)
@@ -100,6 +124,7 @@ class _CriticFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, module, *params):
         n, _, *dims = x.shape
+        module._check_layernorm_shape(dims)
         plan = module.plan_for(n, dims, fresh=True)  # activations live until backward
         xc = x.detach().float().contiguous().view(n, *dims, 1)
         logits = plan.forward(module._tensors(), xc, 0, n, training=module.training)

@@ -389,16 +389,35 @@ def wgrad_ws_floats(g: ConvGeom) -> int:
     return int(L.load().cgan3d_conv3d_wgrad_ws_floats(ctypes.byref(g)))
 
 
-def wgrad(g: ConvGeom, gathered, aligned, dw, ws, accumulate=False, gathered16=None, aligned16=None):
-    """Weight gradient; ``gathered16`` / ``aligned16``: optional bf16 shadows of the operands."""
+def wgrad_ws_atomic(g: ConvGeom) -> bool:
+    """True if the weight gradient of ``g`` sums into its workspace by atomics (it may then take a
+    clean workspace: ``wgrad(..., ws_clean=True)``)."""
+    r = int(L.load().cgan3d_conv3d_wgrad_ws_mode(ctypes.byref(g)))
+    if r < 0:
+        raise ValueError("wgrad_ws_atomic: invalid geometry")
+    return bool(r)
+
+
+def zero(t: torch.Tensor):
+    """Zero a contiguous device tensor (a memset recorded in launch plans)."""
+    if not t.is_contiguous():
+        raise ValueError("zero: tensor must be contiguous")
+    check(_launch("cgan3d_zero", ptr(t), t.numel() * t.element_size()), "zero")
+
+
+def wgrad(g: ConvGeom, gathered, aligned, dw, ws, accumulate=False, gathered16=None, aligned16=None,
+          ws_clean=False):
+    """Weight gradient; ``gathered16`` / ``aligned16``: optional bf16 shadows of the operands.
+    ``ws_clean``: ``ws`` is all-zero and is left all-zero (geometries with ``wgrad_ws_atomic``)."""
     _need(gathered, _vox_in(g) * g.cin, "wgrad gathered")
     _need(aligned, _vox_out(g) * g.cout, "wgrad aligned")
     _need(dw, g.cin * g.cout * g.k**3, "wgrad dw")
     if _w_extent(g) > dw.numel():
         raise ValueError("wgrad: weight strides exceed dw")
     _need(ws, wgrad_ws_floats(g), "wgrad ws", exact=False)
+    flags = (L.WGRAD_ACCUMULATE if accumulate else 0) | (L.WGRAD_WS_CLEAN if ws_clean else 0)
     check(_timed("wgrad", g, "cgan3d_conv3d_wgrad_ex", ctypes.byref(g), ptr(gathered), ptr(aligned), ptr(dw),
-                 int(accumulate), ptr(ws), _need16(gathered16, _vox_in(g) * g.cin, "wgrad gathered16"),
+                 flags, ptr(ws), _need16(gathered16, _vox_in(g) * g.cin, "wgrad gathered16"),
                  _need16(aligned16, _vox_out(g) * g.cout, "wgrad aligned16")), "conv3d_wgrad")
 
 
@@ -513,6 +532,66 @@ def channel_sum(x, nvox, c, out, ws):
     _need(out, c, "channel_sum out")
     _need(ws, channel_sum_ws_floats(nvox, c), "channel_sum ws", exact=False)
     check(_launch("cgan3d_channel_sum", ptr(x), nvox, c, ptr(out), ptr(ws)), "channel_sum")
+
+
+class ChannelSumSet:
+    """Per-channel sums of several tensors in two launches (cgan3d_channel_sum_multi): the critic's
+    bias gradients.  Built once per (tensors, sizes); the descriptors live on the device."""
+
+    def __init__(self, device, items, nblk: int = 64):
+        """items: [(x, nvox, c, out, accumulate)]; every x / out keeps its address."""
+        self.nblk, self.keep = nblk, []
+        descs = []
+        for x, nvox, c, out, acc in items:
+            if c <= 0 or 256 % c:
+                raise ValueError(f"ChannelSumSet: channels {c} must divide 256")
+            _need(x, nvox * c, "channel_sum_multi x", exact=False)
+            _need(out, c, "channel_sum_multi out")
+            ws = torch.empty(nblk * c, device=device, dtype=torch.float64)
+            d = L.CsumDesc()
+            d.x, d.out, d.ws, d.nvox, d.c, d.accumulate = ptr(x), ptr(out), ptr(ws), nvox, c, int(acc)
+            descs.append(d)
+            self.keep += [x, out, ws]
+        self.n = len(descs)
+        raw = b"".join(bytes(d) for d in descs)
+        self.dev = torch.frombuffer(bytearray(raw), dtype=torch.uint8).to(device)
+
+    def run(self):
+        check(_launch("cgan3d_channel_sum_multi", ptr(self.dev), self.n, self.nblk), "channel_sum_multi")
+
+
+def ln_partial_doubles(n: int, L_: int) -> int:
+    return int(L.load().cgan3d_ln_partial_doubles(n, L_))
+
+
+def _ln_args(mode, n, L_, slope, z, p_stats, da=None, zdot=None, adot=None, abar=None, p_bwd=None, p_jvp=None,
+             p_sig=None, p_adj=None):
+    for t, nm in ((z, "z"), (da, "da"), (zdot, "zdot"), (adot, "adot"), (abar, "abar")):
+        if t is not None:
+            _need(t, n * L_, f"ln {nm}", exact=False)
+    npart = ln_partial_doubles(n, L_)
+    for t, nm in ((p_stats, "p_stats"), (p_bwd, "p_bwd"), (p_jvp, "p_jvp"), (p_sig, "p_sig"), (p_adj, "p_adj")):
+        if t is not None:
+            _need(t, npart, f"ln {nm}", dtype=torch.float64, exact=False)
+    a = L.LnArgs()
+    a.n, a.mode, a.L, a.slope, a.eps = n, mode, L_, slope, 1e-5
+    a.z, a.da, a.zdot, a.adot, a.abar = ptr(z), ptr(da), ptr(zdot), ptr(adot), ptr(abar)
+    a.p_stats, a.p_bwd, a.p_jvp, a.p_sig, a.p_adj = ptr(p_stats), ptr(p_bwd), ptr(p_jvp), ptr(p_sig), ptr(p_adj)
+    return a
+
+
+def ln_reduce(mode, n, L_, slope, part, **kw):
+    """Per-sample partial sums of a LayerNorm mode (cgan3d_ln_reduce; modes L.LN_*)."""
+    a = _ln_args(mode, n, L_, slope, **kw)
+    _need(part, ln_partial_doubles(n, L_), "ln_reduce part", dtype=torch.float64, exact=False)
+    check(_launch("cgan3d_ln_reduce", ctypes.byref(a), ptr(part)), "ln_reduce")
+
+
+def ln_apply(mode, n, L_, slope, out, **kw):
+    """Elementwise LayerNorm pass of a mode from its partials (cgan3d_ln_apply)."""
+    a = _ln_args(mode, n, L_, slope, **kw)
+    _need(out, n * L_, "ln_apply out", exact=False)
+    check(_launch("cgan3d_ln_apply", ctypes.byref(a), ptr(out)), "ln_apply")
 
 
 def reflect_fold(padded, out, n, dims: Sequence[int], c, pad, ep: Optional[Epi] = None):

@@ -323,6 +323,40 @@ __global__ __launch_bounds__(256) void channel_sum_finalize_kernel(const float* 
   if (tid == 0) out[c] = (float)(red[0] + red[1] + red[2] + red[3]);
 }
 
+// ---- several channel sums in two launches (the critic's bias gradients, one tensor per layer):
+// grid (nblk, n) of fp64 partial sums into each descriptor's workspace, then one block per
+// descriptor combines its nblk partials per channel (wave per channel).  fp64 throughout: a bias
+// gradient is often a near-cancelling sum (the critic's last bias: -1/n per real logit, +1/n per
+// fake one, exactly 0 in real arithmetic).
+__global__ __launch_bounds__(256) void channel_sum_multi_kernel(const cgan3d_csum_desc* __restrict__ descs) {
+  __shared__ double r0[256];
+  const cgan3d_csum_desc e = descs[blockIdx.y];
+  const int tid = threadIdx.x, C = e.c;
+  const long long total = (long long)e.nvox * C;
+  double a0 = 0.0;
+  for (long long i = (long long)blockIdx.x * blockDim.x + tid; i < total; i += (long long)gridDim.x * blockDim.x)
+    a0 += (double)e.x[i];
+  r0[tid] = a0;
+  __syncthreads();
+  for (int w = 128; w >= C; w >>= 1) {  // tree over the 256 / C threads of each channel
+    if (tid < w) r0[tid] += r0[tid + w];
+    __syncthreads();
+  }
+  if (tid < C) e.ws[(long long)blockIdx.x * C + tid] = r0[tid];
+}
+
+__global__ __launch_bounds__(256) void channel_sum_multi_finalize_kernel(const cgan3d_csum_desc* __restrict__ descs,
+                                                                         int nblk) {
+  const cgan3d_csum_desc e = descs[blockIdx.x];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  for (int c = wave; c < e.c; c += 4) {
+    double s = 0.0;
+    for (int b = lane; b < nblk; b += 64) s += e.ws[(long long)b * e.c + c];
+    s = wave_sum_d(s);
+    if (lane == 0) e.out[c] = e.accumulate ? e.out[c] + (float)s : (float)s;
+  }
+}
+
 // ---- finalize fused into the elementwise pass (small slabs): every block combines the whole slab
 // itself (G = 256 / C threads per channel, Chan in fp64, group shuffles), block 0 publishes the
 // statistics / running buffers / parameter gradients; no separate finalize launch.  Only for small
@@ -610,4 +644,15 @@ extern "C" int cgan3d_bn_apply_slab(const float* part, int32_t nslots, int32_t c
   int rc = cgan3d_bn_finalize_slab(part, nslots, c, nvox, gamma, beta, running_mean, running_var, num_batches_tracked,
                                    momentum, eps, scale_shift, mean_invstd, stream);
   return rc ? rc : cgan3d_bn_apply(z, nvox, c, scale_shift, act, slope, residual, y, y_bf16, stream);
+}
+
+extern "C" int cgan3d_channel_sum_multi(const cgan3d_csum_desc* descs, int32_t n, int32_t nblk, void* stream) {
+  CG_CHECK_ARG(descs && n > 0 && n <= 65535 && nblk > 0 && nblk <= 4096,
+               "cgan3d_channel_sum_multi: need a device descriptor array, 0 < n <= 65535, 0 < nblk <= 4096");
+  hipStream_t s = (hipStream_t)stream;
+  ::cg::launch(channel_sum_multi_kernel, dim3(nblk, n), dim3(256), 0, s, descs);
+  CG_LAUNCH_CHECK("channel_sum_multi_kernel");
+  ::cg::launch(channel_sum_multi_finalize_kernel, dim3(n), dim3(256), 0, s, descs, (int)nblk);
+  CG_LAUNCH_CHECK("channel_sum_multi_finalize_kernel");
+  return CGAN3D_OK;
 }

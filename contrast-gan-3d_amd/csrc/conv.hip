@@ -391,16 +391,18 @@ __global__ __launch_bounds__(256) void conv_wgrad_cout1_kernel(ConvArgs a, const
   }
 }
 
-// dw[a*sa + b*sb + t] (+)= dwp[(t*cin + a)*cout + b]
-__global__ void wgrad_unpack_kernel(const float* __restrict__ dwp, float* dw, int T, int cin, int cout, long long sa,
-                                    long long sb, int accumulate) {
+// dw[a*sa + b*sb + t] (+)= dwp[(t*cin + a)*cout + b]; clean: dwp is left zeroed for its next user
+__global__ void wgrad_unpack_kernel(float* __restrict__ dwp, float* dw, int T, int cin, int cout, long long sa,
+                                    long long sb, int accumulate, int clean) {
   long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   long long total = (long long)T * cin * cout;
   if (i >= total) return;
   int b = (int)(i % cout); long long r = i / cout;
   int ca = (int)(r % cin); int t = (int)(r / cin);
   float* d = dw + ca * sa + b * sb + t;
-  *d = accumulate ? *d + dwp[i] : dwp[i];
+  const float v = dwp[i];
+  *d = accumulate ? *d + v : v;
+  if (clean) dwp[i] = 0.f;
 }
 
 }  // namespace cg
@@ -521,11 +523,28 @@ extern "C" int cgan3d_conv3d_wgrad(const cgan3d_conv_geom* g, const float* gathe
   return cgan3d_conv3d_wgrad_ex(g, gathered, aligned, dw, accumulate, ws, nullptr, nullptr, stream);
 }
 
+// 1 if the weight gradient of `g` sums into the workspace by atomics (then zeroed by a memset,
+// or kept clean under CGAN3D_WGRAD_WS_CLEAN), 0 if it needs no zeroed workspace
+static int wgrad_ws_atomic(const cgan3d_conv_geom* g) {
+  return !k7_wgrad_handles(g) && !c1_wgrad_ok(g) && !wgrad_c1_ok(g) && !wgrad_s2_ok(g) && !wgrad_k3_ok(g);
+}
+
+extern "C" int cgan3d_conv3d_wgrad_ws_mode(const cgan3d_conv_geom* g) {
+  if (validate(g, "cgan3d_conv3d_wgrad_ws_mode")) return -1;
+  return wgrad_ws_atomic(g);
+}
+
 extern "C" int cgan3d_conv3d_wgrad_ex(const cgan3d_conv_geom* g, const float* gathered, const float* aligned, float* dw,
                                       int32_t accumulate, float* ws, const void* gathered_bf16,
                                       const void* aligned_bf16, void* stream) {
   int st = validate(g, "cgan3d_conv3d_wgrad");
   if (st) return st;
+  CG_CHECK_ARG((accumulate & ~3) == 0, "cgan3d_conv3d_wgrad: flags are CGAN3D_WGRAD_ACCUMULATE | CGAN3D_WGRAD_WS_CLEAN");
+  const bool ws_clean = (accumulate & CGAN3D_WGRAD_WS_CLEAN) != 0;
+  accumulate &= CGAN3D_WGRAD_ACCUMULATE;
+  CG_CHECK_ARG(!ws_clean || wgrad_ws_atomic(g),
+               "cgan3d_conv3d_wgrad: CGAN3D_WGRAD_WS_CLEAN on a geometry whose workspace is not atomic "
+               "(cgan3d_conv3d_wgrad_ws_mode() == 0)");
   CG_CHECK_ARG(!g->transposed, "cgan3d_conv3d_wgrad: use the forward mapping (see header)");
   CG_CHECK_ARG(gathered && aligned && dw && ws, "cgan3d_conv3d_wgrad: null pointer");
   CG_CHECK_ARG(g->cout == 1 || g->cout % 4 == 0, "cgan3d_conv3d_wgrad: cout must be 1 or a multiple of 4");
@@ -579,7 +598,7 @@ extern "C" int cgan3d_conv3d_wgrad_ex(const cgan3d_conv_geom* g, const float* ga
     CG_LAUNCH_CHECK("wgrad_k3_kernel");
     return CGAN3D_OK;
   }
-  if (::cg::memset_async(ws, 0, R * g->cout * sizeof(float), s) != hipSuccess) {
+  if (!ws_clean && ::cg::memset_async(ws, 0, R * g->cout * sizeof(float), s) != hipSuccess) {
     set_error("cgan3d_conv3d_wgrad: memset failed");
     return CGAN3D_EHIP;
   }
@@ -615,7 +634,7 @@ extern "C" int cgan3d_conv3d_wgrad_ex(const cgan3d_conv_geom* g, const float* ga
   }
   const long long total = R * g->cout;
   ::cg::launch(wgrad_unpack_kernel, dim3(cg::ceil_div(total, 256)), dim3(256), 0, s, ws, dw, T, g->cin, g->cout,
-                     (long long)g->w_sa, (long long)g->w_sb, accumulate);
+                     (long long)g->w_sa, (long long)g->w_sb, accumulate, (int)ws_clean);
   CG_LAUNCH_CHECK("wgrad_unpack_kernel");
   return CGAN3D_OK;
 }

@@ -379,6 +379,13 @@ int k7_try_fwd(const cgan3d_conv_geom* g, const float* x, const float* w, float*
   return 0;
 }
 
+// 1 if k7_try_wgrad handles the geometry (same conditions)
+int k7_wgrad_handles(const cgan3d_conv_geom* g) {
+  if (g->k != 7 || g->stride != 1 || g->transposed) return 0;
+  return (g->cout == 1 && (k7m_ok(g, g->cin) || k7_wide_ok(g->cin))) ||
+         (g->cin == 1 && (k7m_ok(g, g->cout) || k7_wide_ok(g->cout)));
+}
+
 // Weight-grad launch (dw zeroed by the caller unless accumulating); returns 1 if handled.
 int k7_try_wgrad(const cgan3d_conv_geom* g, const float* x, const float* go, float* dw, float* ws, hipStream_t s) {
   if (g->k != 7 || g->stride != 1 || g->transposed) return 0;

@@ -73,9 +73,13 @@ __global__ __launch_bounds__(256) void sumsq_kernel(const float* __restrict__ g,
   if (threadIdx.x == 0) part[(long long)b * chunks + blockIdx.x] = (float)s;
 }
 
-__global__ void gp_finalize_kernel(const float* __restrict__ part, int B, int chunks, float lambda_, float* coef,
-                                   float* losses) {
+// Finalize folded into the scaling pass: every block combines the B x chunks partial sums itself
+// (same order in every block, so every block holds the same coefficients); block 0 writes the loss.
+__global__ __launch_bounds__(256) void gp_scale_kernel(const float* __restrict__ part, int B, int chunks,
+                                                       float lambda_, float* losses, const float* __restrict__ g,
+                                                       long long ps, long long total, float* out) {
   __shared__ double red[4];
+  __shared__ float coef[1024];
   double acc = 0.0;
   for (int b = threadIdx.x; b < B; b += blockDim.x) {
     double ss = 0.0;
@@ -85,16 +89,12 @@ __global__ void gp_finalize_kernel(const float* __restrict__ part, int B, int ch
     // d/dg_b of lambda*mean((||g_b||-1)^2) = lambda * 2/B * (||g_b||-1) * g_b/||g_b||  (0 at ||g_b||=0)
     coef[b] = nrm > 0.0 ? (float)(lambda_ * 2.0 / B * (nrm - 1.0) / nrm) : 0.f;
   }
-  acc = block_sum_d(acc, red);
-  if (threadIdx.x == 0) {
+  acc = block_sum_d(acc, red);  // (its barriers also publish coef)
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
     const float gp = (float)(lambda_ * acc / B);
     losses[L_GP] = gp;
     losses[L_D] = losses[L_WD] + gp;
   }
-}
-
-__global__ __launch_bounds__(256) void scale_rows_kernel(const float* __restrict__ g, long long ps, long long total,
-                                                         const float* __restrict__ coef, float* out) {
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long long)gridDim.x * blockDim.x)
     out[i] = coef[i / ps] * g[i];
 }
@@ -123,24 +123,26 @@ __global__ __launch_bounds__(256) void gen_pass1_kernel(const float* __restrict_
   }
 }
 
-// means -> stat[0..3] = s_mean, t_mean, mask_sum, hu_sum
-__global__ __launch_bounds__(256) void gen_fin1_kernel(const double* __restrict__ part, int nblk, long long n,
-                                                       double* stat) {
-  __shared__ double red[4];
-  double a[4] = {0, 0, 0, 0};
+// the nblk x 4 partials of a pass combined in a fixed order (identical in every block that calls it)
+__device__ __forceinline__ void gen_combine(const double* __restrict__ part, int nblk, double* red, double (&a)[4]) {
+  for (int q = 0; q < 4; ++q) a[q] = 0.0;
   for (int b = threadIdx.x; b < nblk; b += blockDim.x)
     for (int q = 0; q < 4; ++q) a[q] += part[b * 4 + q];
   for (int q = 0; q < 4; ++q) a[q] = block_sum_d(a[q], red);
-  if (threadIdx.x == 0) {
-    stat[0] = a[0] / (double)n; stat[1] = a[1] / (double)n; stat[2] = a[2]; stat[3] = a[3];
-  }
 }
 
-// pass 2: sum (s-sm)(t-tm), (s-sm)^2, (t-tm)^2, (t-tm)
+// pass 2 (pass 1's finalize folded in: every block combines pass 1's partials; block 0 publishes
+// stat[0..3] = s_mean, t_mean, mask_sum, hu_sum): sum (s-sm)(t-tm), (s-sm)^2, (t-tm)^2, (t-tm)
 __global__ __launch_bounds__(256) void gen_pass2_kernel(const float* __restrict__ s, const float* __restrict__ t,
-                                                        long long n, const double* __restrict__ stat, double* part) {
+                                                        long long n, const double* __restrict__ part1, int nblk1,
+                                                        double* stat, double* part) {
   __shared__ double red[4];
-  const float sm = (float)stat[0], tm = (float)stat[1];
+  double f[4];
+  gen_combine(part1, nblk1, red, f);
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    stat[0] = f[0] / (double)n; stat[1] = f[1] / (double)n; stat[2] = f[2]; stat[3] = f[3];
+  }
+  const float sm = (float)(f[0] / (double)n), tm = (float)(f[1] / (double)n);
   double a0 = 0, a1 = 0, a2 = 0, a3 = 0;
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
     const float u = s[i] - sm, w = t[i] - tm;
@@ -156,39 +158,33 @@ __global__ __launch_bounds__(256) void gen_pass2_kernel(const float* __restrict_
   }
 }
 
-// losses + gradient coefficients: stat[4..] = A (w coef), Bc (u coef), w_mean, hu_scale
-__global__ __launch_bounds__(256) void gen_fin2_kernel(const double* __restrict__ part, int nblk, long long n,
-                                                       float sim_w, float hu_w, double* stat, float* losses) {
+// dz_last = d(opt_hat)/d(z) chain: opt_hat = subopt - tanh(z)  =>  dz = -dL/dopt_hat * (1 - att^2).
+// Pass 2's finalize folded in: every block combines its partials into the losses and the gradient
+// coefficients A (w coef), Bc (u coef), w_mean, hu_scale; block 0 writes the losses.
+__global__ __launch_bounds__(256) void gen_grad_kernel(const float* __restrict__ s, const float* __restrict__ t,
+                                                       const float* __restrict__ att, const uint8_t* __restrict__ m,
+                                                       const float* __restrict__ dcrit, long long n, float lo, float hi,
+                                                       const double* __restrict__ stat, const double* __restrict__ part2,
+                                                       int nblk2, float sim_w, float hu_w, float* losses, float* dz) {
   __shared__ double red[4];
-  double a[4] = {0, 0, 0, 0};
-  for (int b = threadIdx.x; b < nblk; b += blockDim.x)
-    for (int q = 0; q < 4; ++q) a[q] += part[b * 4 + q];
-  for (int q = 0; q < 4; ++q) a[q] = block_sum_d(a[q], red);
-  if (threadIdx.x != 0) return;
+  double a[4];
+  gen_combine(part2, nblk2, red, a);
   const double suw = a[0], suu = a[1], sww = a[2], sw = a[3];
   const double nn = (double)n;
   const double cc = suw / nn;
   const double ss = sqrt(suu / (nn - 1.0)), st = sqrt(sww / (nn - 1.0));  // torch.std (unbiased)
   const double D = ss * st + 1e-8;
-  const double zncc = -cc / D;
-  const double hu = stat[3] / (stat[2] + 1e-8);
   // dL/ds_j = -(1/D) (w_j - mean w)/n  +  cc*st/D^2 * 2/(n-1) * (s_j - s_mean)/(2 ss + 1e-6)
-  stat[4] = sim_w * (-1.0 / (D * nn));
-  stat[5] = sim_w * (cc * st / (D * D)) * (2.0 / (nn - 1.0)) / (2.0 * ss + 1e-6);
-  stat[6] = sw / nn;
-  stat[7] = hu_w * 2.0 / (stat[2] + 1e-8);
-  losses[L_SIM] = (float)(sim_w * zncc);
-  losses[L_HU] = (float)(hu_w * hu);
-  losses[L_GFULL] = losses[L_G] + (float)(sim_w * zncc) + (float)(hu_w * hu);
-}
-
-// dz_last = d(opt_hat)/d(z) chain: opt_hat = subopt - tanh(z)  =>  dz = -dL/dopt_hat * (1 - att^2)
-__global__ __launch_bounds__(256) void gen_grad_kernel(const float* __restrict__ s, const float* __restrict__ t,
-                                                       const float* __restrict__ att, const uint8_t* __restrict__ m,
-                                                       const float* __restrict__ dcrit, long long n, float lo, float hi,
-                                                       const double* __restrict__ stat, float* dz) {
+  const float A = (float)(sim_w * (-1.0 / (D * nn)));
+  const float Bc = (float)(sim_w * (cc * st / (D * D)) * (2.0 / (nn - 1.0)) / (2.0 * ss + 1e-6));
+  const float wm = (float)(sw / nn), hs = (float)(hu_w * 2.0 / (stat[2] + 1e-8));
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    const double zncc = -cc / D, hu = stat[3] / (stat[2] + 1e-8);
+    losses[L_SIM] = (float)(sim_w * zncc);
+    losses[L_HU] = (float)(hu_w * hu);
+    losses[L_GFULL] = losses[L_G] + (float)(sim_w * zncc) + (float)(hu_w * hu);
+  }
   const float sm = (float)stat[0], tm = (float)stat[1];
-  const float A = (float)stat[4], Bc = (float)stat[5], wm = (float)stat[6], hs = (float)stat[7];
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
     const float x = s[i];
     float g = A * ((t[i] - tm) - wm) + Bc * (x - sm);
@@ -211,9 +207,9 @@ static int red_blocks(long long n) {
 using namespace cg;
 
 extern "C" int64_t cgan3d_loss_ws_floats(int64_t n) {
-  // generator losses: (512 x 4 partials + 8 stats) doubles; GP: b x (<=64 chunks + 1) floats, b <= 1024
+  // generator losses: (2 x 512 x 4 partials + 8 stats) doubles; GP: b x (<=64 chunks) floats, b <= 1024
   (void)n;
-  return 2 * (512 * 4 + 8) + 65 * 1024;
+  return 2 * (2 * 512 * 4 + 8) + 65 * 1024;
 }
 
 extern "C" int cgan3d_critic_logits_grad(const float* logits, int32_t n_real, int32_t n_fake, int32_t n_gp,
@@ -243,16 +239,13 @@ extern "C" int cgan3d_gradient_penalty(const float* grad, int32_t b, int64_t per
   int chunks = (int)((per_sample + 8191) / 8192);
   if (chunks > 64) chunks = 64;
   float* part = ws;
-  float* coef = ws + (long long)b * chunks;
   ::cg::launch(sumsq_kernel, dim3(chunks, b), dim3(256), 0, s, grad, (long long)per_sample, chunks, part);
   CG_LAUNCH_CHECK("sumsq_kernel");
-  ::cg::launch(gp_finalize_kernel, dim3(1), dim3(256), 0, s, part, b, chunks, lambda_, coef, losses);
-  CG_LAUNCH_CHECK("gp_finalize_kernel");
   const long long total = (long long)b * per_sample;
-  int blocks = (int)std::min<long long>((total + 255) / 256, 4096);
-  ::cg::launch(scale_rows_kernel, dim3(blocks), dim3(256), 0, s, grad, (long long)per_sample, total, coef,
-                     gamma_out);
-  CG_LAUNCH_CHECK("scale_rows_kernel");
+  int blocks = (int)std::min<long long>((total + 255) / 256, 1024);
+  ::cg::launch(gp_scale_kernel, dim3(blocks), dim3(256), 0, s, part, b, chunks, lambda_, losses, grad,
+               (long long)per_sample, total, gamma_out);
+  CG_LAUNCH_CHECK("gp_scale_kernel");
   return CGAN3D_OK;
 }
 
@@ -264,20 +257,17 @@ extern "C" int cgan3d_generator_output_grad(const float* opt_hat, const float* s
   CG_CHECK_ARG(n > 1, "cgan3d_generator_output_grad: need n > 1");
   CG_CHECK_ARG(((uintptr_t)ws & 7) == 0, "cgan3d_generator_output_grad: workspace must be 8-byte aligned");
   hipStream_t s = (hipStream_t)stream;
-  double* part = reinterpret_cast<double*>(ws);
-  double* stat = part + 512 * 4;
+  double* part1 = reinterpret_cast<double*>(ws);
+  double* part2 = part1 + 512 * 4;
+  double* stat = part2 + 512 * 4;
   const int nblk = red_blocks(n);
-  ::cg::launch(gen_pass1_kernel, dim3(nblk), dim3(256), 0, s, opt_hat, subopt, mask, (long long)n, lo, hi, part);
+  ::cg::launch(gen_pass1_kernel, dim3(nblk), dim3(256), 0, s, opt_hat, subopt, mask, (long long)n, lo, hi, part1);
   CG_LAUNCH_CHECK("gen_pass1_kernel");
-  ::cg::launch(gen_fin1_kernel, dim3(1), dim3(256), 0, s, part, nblk, (long long)n, stat);
-  CG_LAUNCH_CHECK("gen_fin1_kernel");
-  ::cg::launch(gen_pass2_kernel, dim3(nblk), dim3(256), 0, s, opt_hat, subopt, (long long)n, stat, part);
+  ::cg::launch(gen_pass2_kernel, dim3(nblk), dim3(256), 0, s, opt_hat, subopt, (long long)n, part1, nblk, stat, part2);
   CG_LAUNCH_CHECK("gen_pass2_kernel");
-  ::cg::launch(gen_fin2_kernel, dim3(1), dim3(256), 0, s, part, nblk, (long long)n, sim_w, hu_w, stat, losses);
-  CG_LAUNCH_CHECK("gen_fin2_kernel");
-  int blocks = (int)std::min<long long>((n + 255) / 256, 4096);
+  int blocks = (int)std::min<long long>((n + 255) / 256, 512);
   ::cg::launch(gen_grad_kernel, dim3(blocks), dim3(256), 0, s, opt_hat, subopt, att, mask, d_critic,
-                     (long long)n, lo, hi, stat, dz_last);
+                     (long long)n, lo, hi, stat, part2, nblk, sim_w, hu_w, losses, dz_last);
   CG_LAUNCH_CHECK("gen_grad_kernel");
   return CGAN3D_OK;
 }

@@ -238,3 +238,13 @@ extern "C" int cgan3d_gp_interpolate(const float* real, const float* fake, const
   CG_LAUNCH_CHECK("interp_kernel");
   return CGAN3D_OK;
 }
+
+// Zero `bytes` bytes at p (a gradient arena before an update): a memset recorded in launch plans.
+extern "C" int cgan3d_zero(void* p, int64_t bytes, void* stream) {
+  CG_CHECK_ARG(p && bytes > 0, "cgan3d_zero: bad args");
+  if (::cg::memset_async(p, 0, (size_t)bytes, (hipStream_t)stream) != hipSuccess) {
+    set_error("cgan3d_zero: memset failed");
+    return CGAN3D_EHIP;
+  }
+  return CGAN3D_OK;
+}

@@ -143,6 +143,16 @@ int cgan3d_conv3d_wgrad(const cgan3d_conv_geom* g, const float* gathered, const 
                         float* dw, int32_t accumulate, float* ws, void* stream);
 /* The same with optional bf16 shadows of both operands (same layouts, NULL = none): the ResNet-
  * block weight-grad kernel then stages them as they are (bit-identical: it rounds to bf16 anyway). */
+/* `accumulate` of the weight-gradient entry points is a flag word: CGAN3D_WGRAD_ACCUMULATE adds
+ * into dw instead of overwriting it (a caller that zeroes a whole gradient arena once per update
+ * passes it for every layer, so no per-layer memset of dw is issued); CGAN3D_WGRAD_WS_CLEAN promises
+ * that ws is all-zero on entry and asks that the kernels that sum into ws by atomics leave it
+ * all-zero again (no per-layer memset of ws; the workspace must then be used by clean calls only). */
+#define CGAN3D_WGRAD_ACCUMULATE 1
+#define CGAN3D_WGRAD_WS_CLEAN 2
+/* 1 if the weight gradient of `g` sums into its workspace by atomics (the geometries that may take
+ * CGAN3D_WGRAD_WS_CLEAN), 0 if not, -1 on an invalid geometry. */
+int cgan3d_conv3d_wgrad_ws_mode(const cgan3d_conv_geom* g);
 int cgan3d_conv3d_wgrad_ex(const cgan3d_conv_geom* g, const float* gathered, const float* aligned,
                            float* dw, int32_t accumulate, float* ws, const void* gathered_bf16,
                            const void* aligned_bf16, void* stream);
@@ -191,6 +201,19 @@ int cgan3d_bn_backward(const float* dy, const float* z, int64_t nvox, int32_t c,
                        int32_t accumulate, float* ws, void* stream);
 
 /* --- reductions / elementwise --- */
+/* Several channel sums in two launches (the critic's bias gradients, Trainer.py:133 backward of
+ * model/discriminator.py's conv biases): `descs` is a DEVICE array of n descriptors (stable
+ * pointers, built once), each summing x[nvox][c] per channel into out[c] (+= when accumulate)
+ * through its own workspace of nblk * c doubles; c must divide 256.  Sums in fp64. */
+typedef struct cgan3d_csum_desc {
+  const float* x;
+  float* out;
+  double* ws;
+  int64_t nvox;
+  int32_t c;
+  int32_t accumulate;
+} cgan3d_csum_desc;
+int cgan3d_channel_sum_multi(const cgan3d_csum_desc* descs, int32_t n, int32_t nblk, void* stream);
 int64_t cgan3d_channel_sum_ws_floats(int64_t nvox, int32_t c);
 int cgan3d_channel_sum(const float* x, int64_t nvox, int32_t c, float* out, float* ws,
                        void* stream);
@@ -251,6 +274,38 @@ int cgan3d_generator_output_grad(const float* opt_hat, const float* subopt, cons
 /* --- optimiser (torch.optim.Adam, experiments/basic_conf.py:55,67) ---
  * hyper (device): [lr, beta1, beta2, eps, step, weight_clip]; cgan3d_adam_tick increments step. */
 int cgan3d_adam_tick(float* hyper, void* stream);
+/* Zero `bytes` bytes of device memory (recorded in launch plans): the engine zeroes a network's
+ * whole gradient arena once per update and then accumulates every layer's weight gradient
+ * (CGAN3D_WGRAD_ACCUMULATE) — Trainer.py:109,146 optimizer.zero_grad. */
+int cgan3d_zero(void* p, int64_t bytes, void* stream);
+
+/* LayerNorm critic (experiments/gp_layernorm.py:9-11, model/blocks.py:40-45): per-sample
+ * normalisation over (C, D, H, W) — one contiguous run of L floats per sample in NDHWC — without
+ * affine parameters, then LeakyReLU; plus the forward-mode tangent and the adjoint it injects,
+ * which the gradient penalty's double backward (model/utils.py:34-39) differentiates through.
+ * cgan3d_ln_reduce writes per-sample partial sums (cgan3d_ln_partial_doubles doubles) of the
+ * mode's quantities; cgan3d_ln_apply combines them per sample and runs the elementwise pass.
+ * Formulas: csrc/ln.hip header.  All tensor pointers start at the slice's first sample. */
+#define CGAN3D_LN_STATS 0 /* reduce: sum z, z^2            apply: a = lrelu(x^)                */
+#define CGAN3D_LN_BWD 1   /* reduce: sum rho, rho x^        apply: dz (LayerNorm + lrelu backward) */
+#define CGAN3D_LN_JVP 2   /* reduce: sum zdot, zdot x^      apply: adot (tangent)               */
+#define CGAN3D_LN_SIG 3   /* reduce: sum da * adot          (no apply)                          */
+#define CGAN3D_LN_ADJ 4   /* reduce: sum xbar, xbar x^      apply: zbar (primal adjoint)        */
+typedef struct cgan3d_ln_args {
+  int32_t n;        /* samples */
+  int32_t mode;
+  int64_t L;        /* elements per sample */
+  float slope, eps; /* LeakyReLU slope, LayerNorm eps (1e-5) */
+  const float* z;   /* conv output (pre-norm) [n][L] */
+  const float* da;  /* dL/d(activation) [n][L] (BWD, SIG, ADJ) */
+  const float* zdot;  /* tangent conv output (JVP, ADJ) */
+  const float* adot;  /* tangent activation (SIG) */
+  const float* abar;  /* primal adjoint of the activation (ADJ; NULL = 0) */
+  const double* p_stats, *p_bwd, *p_jvp, *p_sig, *p_adj; /* partials of the modes */
+} cgan3d_ln_args;
+int64_t cgan3d_ln_partial_doubles(int32_t n, int64_t L);
+int cgan3d_ln_reduce(const cgan3d_ln_args* args, double* partials, void* stream);
+int cgan3d_ln_apply(const cgan3d_ln_args* args, float* out, void* stream);
 int cgan3d_adam(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, int64_t n,
                 const float* hyper, void* stream);
 

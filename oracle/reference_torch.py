@@ -48,7 +48,7 @@ class CriticConfig:
     init_channels_out: int = 8
     discriminator_depth: int = 3
     negative_slope: float = 0.2
-    norm: str = "identity"  # "identity" (GP conf) or "batch" (basic conf)
+    norm: str = "identity"  # "identity" (GP conf), "batch" (basic conf) or "layer" (gp_layernorm conf)
 
 
 def gen_param_shapes(cfg: GenConfig) -> "Dict[str, tuple]":
@@ -94,6 +94,8 @@ def critic_param_shapes(cfg: CriticConfig) -> "Dict[str, tuple]":
         shp[f"model.middle.{n}.conv.weight"] = (out_, in_, 4, 4, 4)
         if cfg.norm == "identity":
             shp[f"model.middle.{n}.conv.bias"] = (out_,)
+        elif cfg.norm == "layer":
+            pass  # conv without bias (blocks.py:34), LayerNorm without affine parameters (gp_layernorm.py:9-11)
         else:
             p = f"model.middle.{n}.normalization"
             shp[f"{p}.weight"], shp[f"{p}.bias"] = (out_,), (out_,)
@@ -198,6 +200,9 @@ def critic_forward(p: Dict[str, Tensor], x: Tensor, cfg: CriticConfig, training=
         pre = f"model.middle.{n}"
         if cfg.norm == "identity":
             h = _conv3d(h, p[f"{pre}.conv.weight"], p[f"{pre}.conv.bias"], stride=2, padding=1)
+        elif cfg.norm == "layer":  # LayerNorm over (C, D, H, W) per sample (blocks.py:40-45, gp_layernorm.py:9-11)
+            h = _conv3d(h, p[f"{pre}.conv.weight"], stride=2, padding=1)
+            h = F.layer_norm(h, h.shape[1:], eps=1e-5)
         else:
             h = batch_norm(_conv3d(h, p[f"{pre}.conv.weight"], stride=2, padding=1), p, f"{pre}.normalization", training)
         h = F.leaky_relu(h, s)

@@ -16,7 +16,8 @@ Fixtures (all fp32, CPU, torch as installed here — recorded in each file's ``t
   d_fwd_*.npz     PatchGANDiscriminator forward (GP conf: Identity norm; BN conf)
   losses.npz      ZNCCLoss / HULoss / WassersteinLoss values and input gradients
   gp.npz          wgan_gradient_penalty value + critic parameter gradients (eps injected)
-  step_*.npz      Trainer.train_step over 1-3 iterations (GP conf and weight-clip conf):
+  step_*.npz      Trainer.train_step over 1-3 iterations (GP conf, weight-clip conf, and the
+                  gp_layernorm conf's LayerNorm critic with the GP):
                   losses, gradients seen by each optimizer step, final params & buffers; per
                   iteration the entering state and a float64 re-run of that iteration
 """
@@ -183,10 +184,14 @@ class _NullLogger:
         pass
 
 
-def _make_trainer(g_args, gp: bool, S, b_low, b_high, iters, dtype):
+def _make_trainer(g_args, gp: bool, S, b_low, b_high, iters, dtype, critic_norm="identity"):
     """A reference Trainer for the fixture runs; ``dtype=torch.float64`` converts the modules, the
-    optimisers and the HU constants to double (the exact-arithmetic yardstick)."""
+    optimisers and the HU constants to double (the exact-arithmetic yardstick).  ``critic_norm``
+    "layer": the gp_layernorm conf's critic (experiments/gp_layernorm.py:9-11: LayerNorm over
+    (C, D, H, W) of every middle block, no affine parameters)."""
     d_extra = dict(norm_layer=torch.nn.Identity) if gp else {}
+    if critic_norm == "layer":
+        d_extra = dict(norm_layer=torch.nn.LayerNorm, patch_size=(1, S, S, S), elementwise_affine=False)
     lr, betas = (1e-4, (0.0, 0.9)) if gp else (2e-4, (0.5, 0.999))
     lo, hi = scaled_hu_bounds()
     tr = Trainer(
@@ -287,7 +292,8 @@ def _run_iteration(tr, gp, inputs, it, dtype):
     return {k: v.detach().numpy() for k, v in logged.items()}, grads
 
 
-def train_steps(tag, g_args, gp: bool, S, b_opt, b_low, b_high, iters, seed, save_final_g=True):
+def train_steps(tag, g_args, gp: bool, S, b_opt, b_low, b_high, iters, seed, save_final_g=True,
+                critic_norm="identity"):
     """Trainer.train_step (Trainer.py:163-203) with train_{critic,generator}_every = 1, ``iters``
     iterations in float32 (the reference's precision).
 
@@ -295,7 +301,7 @@ def train_steps(tag, g_args, gp: bool, S, b_opt, b_low, b_high, iters, seed, sav
     ``it{k}/adam``, k > 0) and the same iteration re-run in float64 from that state
     (``it{k}/grad64``, ``it{k}/loss64``): the exact-arithmetic yardstick the GPU test holds each
     iteration to."""
-    tr, lr, betas = _make_trainer(g_args, gp, S, b_low, b_high, iters, torch.float32)
+    tr, lr, betas = _make_trainer(g_args, gp, S, b_low, b_high, iters, torch.float32, critic_norm)
     out = {}
     rngs = np.random.Generator(np.random.PCG64(seed + 100))
     for it in range(iters):
@@ -311,7 +317,7 @@ def train_steps(tag, g_args, gp: bool, S, b_opt, b_low, b_high, iters, seed, sav
             out.update(_state_arrays(tr, snap, it))
         losses, grads = _run_iteration(tr, gp, inputs, it, torch.float32)
         # the same iteration in float64 from the same state
-        tr64, _, _ = _make_trainer(g_args, gp, S, b_low, b_high, iters, torch.float64)
+        tr64, _, _ = _make_trainer(g_args, gp, S, b_low, b_high, iters, torch.float64, critic_norm)
         _restore(tr64, snap)
         losses64, grads64 = _run_iteration(tr64, gp, inputs, it, torch.float64)
         out[f"it{it}/opt"] = opt
@@ -330,7 +336,7 @@ def train_steps(tag, g_args, gp: bool, S, b_opt, b_low, b_high, iters, seed, sav
     if save_final_g:
         out.update(sd_np(tr.generator, "final/G/"))
     out.update(sd_np(tr.critic, "final/D/"))
-    meta = dict(S=S, b_opt=b_opt, b_low=b_low, b_high=b_high, iters=iters, gp=int(gp), lr=lr,
+    meta = dict(S=S, b_opt=b_opt, b_low=b_low, b_high=b_high, iters=iters, gp=int(gp), lr=lr, critic_norm=critic_norm,
                 beta1=betas[0], beta2=betas[1], teacher_forced=1,
                 **{f"g_{k}": v for k, v in g_args.items()})
     np.savez_compressed(HERE / f"step_{tag}.npz", torch_version=torch.__version__,
@@ -340,6 +346,12 @@ def train_steps(tag, g_args, gp: bool, S, b_opt, b_low, b_high, iters, seed, sav
 if __name__ == "__main__":
     torch.set_num_threads(8)
     torch.use_deterministic_algorithms(True)
+    only = sys.argv[1:]  # optional fixture tags to (re)generate, e.g. gp_layernorm
+    if only:
+        if "gp_layernorm" in only:
+            train_steps("gp_layernorm", G_SMALL, True, S=32, b_opt=2, b_low=1, b_high=1, iters=2, seed=800,
+                        critic_norm="layer")
+        sys.exit(0)
     gen_forward(32, 2, seed=1234)
     disc_forward(32, 3, seed=1234)
     losses(32, 2, seed=77)
@@ -349,5 +361,8 @@ if __name__ == "__main__":
     train_steps("gp_full", G_ARGS, True, S=32, b_opt=2, b_low=1, b_high=1, iters=1, seed=600,
                 save_final_g=False)
     train_steps("clip_small", G_SMALL, False, S=32, b_opt=2, b_low=1, b_high=1, iters=2, seed=700)
+    # gp_layernorm conf (experiments/gp_layernorm.py): LayerNorm critic with the gradient penalty
+    train_steps("gp_layernorm", G_SMALL, True, S=32, b_opt=2, b_low=1, b_high=1, iters=2, seed=800,
+                critic_norm="layer")
     for f in sorted(HERE.glob("*.npz")):
         print(f.name, f.stat().st_size)

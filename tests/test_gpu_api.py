@@ -105,15 +105,19 @@ def test_generator_autograd_backward_matches_oracle():
                       f"dG/d{k}")
 
 
-def test_critic_autograd_backward_matches_oracle():
-    """PatchGANDiscriminator (GP conf) as a plain module: input and parameter gradients of
-    sum(D(x) * r) against the oracle's autograd in float64."""
+@pytest.mark.parametrize("norm", ["identity", "layer"])
+def test_critic_autograd_backward_matches_oracle(norm):
+    """PatchGANDiscriminator (GP conf; gp_layernorm conf's LayerNorm critic) as a plain module:
+    input and parameter gradients of sum(D(x) * r) against the oracle's autograd in float64."""
     from torch import nn
     from oracle import reference_torch as R
     from cgan3d_amd.data.synthetic import synth_patches
     from cgan3d_amd.model.discriminator import PatchGANDiscriminator
     from cgan3d_amd.model.init import pcg64_init_
-    d = pcg64_init_(PatchGANDiscriminator(**D_ARGS, norm_layer=nn.Identity), 1).cuda()
+    kw = dict(norm_layer=nn.Identity)
+    if norm == "layer":  # experiments/gp_layernorm.py:9-11
+        kw = dict(norm_layer=nn.LayerNorm, patch_size=(1, 32, 32, 32), elementwise_affine=False)
+    d = pcg64_init_(PatchGANDiscriminator(**D_ARGS, **kw), 1).cuda()
     par = _oracle_params(d)
     x, _ = synth_patches(3, 32, 7)
     xd = torch.from_numpy(x).cuda().requires_grad_()
@@ -124,7 +128,7 @@ def test_critic_autograd_backward_matches_oracle():
     for k in keys:
         par[k].requires_grad_(True)
     xr = torch.from_numpy(x).double().requires_grad_()
-    yr = R.critic_forward(par, xr, R.CriticConfig())
+    yr = R.critic_forward(par, xr, R.CriticConfig(norm=norm))
     assert_close(y.detach().cpu().numpy(), yr.detach().numpy(), 1e-3, "D(x)")
     grads = torch.autograd.grad((yr * torch.from_numpy(r).double()).sum(), [xr] + [par[k] for k in keys])
     assert_close(xd.grad.cpu().numpy(), grads[0].numpy(), 1e-3, "dD/dx")

@@ -16,13 +16,15 @@ pytestmark = pytest.mark.gpu
 D_ARGS = dict(channels_in=1, init_channels_out=8, discriminator_depth=3, negative_slope=0.2)
 
 
-def _models(g_args, critic_bn=False):
+def _models(g_args, critic_bn=False, ln_patch=None):
     from torch import nn
     from cgan3d_amd.model.discriminator import PatchGANDiscriminator
     from cgan3d_amd.model.generator import ResnetGenerator
     from cgan3d_amd.model.init import pcg64_init_
     g = pcg64_init_(ResnetGenerator(**g_args), 0).cuda()
     norm = {} if critic_bn else dict(norm_layer=nn.Identity)  # BatchNorm critic: basic_conf.py:60-66
+    if ln_patch is not None:  # LayerNorm critic: experiments/gp_layernorm.py:9-11
+        norm = dict(norm_layer=nn.LayerNorm, patch_size=(1, *ln_patch), elementwise_affine=False)
     d = pcg64_init_(PatchGANDiscriminator(**D_ARGS, **norm), 1).cuda()
     return g, d
 
@@ -49,9 +51,10 @@ def _load_fixture_state(eng, g, d, f, it):
     eng.D.pack()
 
 
-@pytest.mark.parametrize("tag", ["gp_small", "gp_full", "clip_small"])
+@pytest.mark.parametrize("tag", ["gp_small", "gp_full", "clip_small", "gp_layernorm"])
 def test_step_matches_reference_fixture(golden, tag):
-    """Trainer.train_step of the reference (GP conf; weight-clip conf with the BatchNorm critic)
+    """Trainer.train_step of the reference (GP conf; weight-clip conf with the BatchNorm critic;
+    gp_layernorm conf with the LayerNorm critic and the penalty's double backward through it)
     against the device step: losses, every gradient, final parameters and BN buffers.
 
     Every iteration starts from the reference's own state entering it (fixture ``it{k}/state``) and
@@ -65,7 +68,8 @@ def test_step_matches_reference_fixture(golden, tag):
                   init_channels_out=meta["g_init_channels_out"])
     S, b = meta["S"], meta["b_opt"]
     gp = bool(meta["gp"])
-    g, d = _models(g_args, critic_bn=not gp)
+    ln = meta.get("critic_norm") == "layer"
+    g, d = _models(g_args, critic_bn=not gp, ln_patch=(S, S, S) if ln else None)
     eng = _engine(g, d, b, S, meta["lr"], meta["beta1"], meta["beta2"], weight_clip=None if gp else 0.01)
     names = {"L_D": 0, "D": 0, "G": 3, "sim": 4, "HU": 5, "G-full": 6}
     for it in range(meta["iters"]):

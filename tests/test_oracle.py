@@ -77,13 +77,17 @@ def test_gradient_penalty(golden):
     assert float(f["fake_grad_absmax"]) == 0.0  # the G path of the GP is dead
 
 
-@pytest.mark.parametrize("tag", ["gp_small", "gp_full", "clip_small"])
+def _critic_norm(meta):
+    return meta.get("critic_norm", "identity") if meta["gp"] else "batch"
+
+
+@pytest.mark.parametrize("tag", ["gp_small", "gp_full", "clip_small", "gp_layernorm"])
 def test_train_step(golden, tag):
     f = golden(f"step_{tag}")
     meta = ast.literal_eval(str(f["meta"]))
     gen = R.GenConfig(meta["g_n_resnet_blocks"], meta["g_n_updownsample_blocks"], meta["g_init_channels_out"])
     gp = bool(meta["gp"])
-    crit = R.CriticConfig(norm="identity" if gp else "batch")
+    crit = R.CriticConfig(norm=_critic_norm(meta))
     cfg = R.StepConfig(gen=gen, critic=crit, gp_weight=10.0 if gp else None,
                        weight_clip=None if gp else 0.01)
     gpar, dpar = params(R.gen_param_shapes(gen), 0), params(R.critic_param_shapes(crit), 1)
@@ -110,7 +114,7 @@ def test_train_step(golden, tag):
             assert_close(p[k.split("/", 2)[2]].numpy(), f[k], 1e-3, k)
 
 
-@pytest.mark.parametrize("tag", ["gp_small", "clip_small"])
+@pytest.mark.parametrize("tag", ["gp_small", "clip_small", "gp_layernorm"])
 def test_teacher_forced_fixture_state_is_consistent(golden, tag):
     """The per-iteration fixture entries the GPU test is held to: from the stored state entering
     iteration k (parameters, BatchNorm buffers, Adam moments), the oracle in float64 reproduces the
@@ -119,7 +123,7 @@ def test_teacher_forced_fixture_state_is_consistent(golden, tag):
     meta = ast.literal_eval(str(f["meta"]))
     gen = R.GenConfig(meta["g_n_resnet_blocks"], meta["g_n_updownsample_blocks"], meta["g_init_channels_out"])
     gp = bool(meta["gp"])
-    crit = R.CriticConfig(norm="identity" if gp else "batch")
+    crit = R.CriticConfig(norm=_critic_norm(meta))
     cfg = R.StepConfig(gen=gen, critic=crit, gp_weight=10.0 if gp else None, weight_clip=None if gp else 0.01)
     it = meta["iters"] - 1
     pars = {}
