@@ -41,6 +41,8 @@ Dims = Tuple[int, int, int]
 # step time at 64^3 B=4 under launch plans, 13 fewer launches), or CGAN3D_BN_FUSED_BWD=0 for a
 # separate reduction pass over (dy, z)
 BN_FUSED_BWD = os.environ.get("CGAN3D_BN_FUSED_BWD", "1") == "1"
+# weight grads of consecutive ResNet-block layers per cross-stream wait (GeneratorPlan.backward)
+WGRAD_GROUP = max(1, int(os.environ.get("CGAN3D_WGRAD_GROUP", "2")))
 # data parallelism: generator gradient bucket size (all-reduce started per bucket during the backward)
 # (measured on one GPU over a one-rank RCCL group: each extra bucket ~15 us of step time, so the
 # default makes ~2-3 buckets of the 4.1 MB arena: 2.21 ms/step at 1 MB, 2.16 with 2 buckets)
@@ -305,6 +307,15 @@ class GeneratorPlan:
         n = self.n
         u = self.y[-1]
         self._on_side(lambda: self._wgrad(self.geo_last_wgrad, u, self.dz_last, G["model.last_conv.weight"], zeroed))
+        pending = []  # (layer, weight-grad launcher) not yet handed to the side stream
+
+        def flush():
+            fns = [f for _, f in pending]
+            self._on_side(lambda: [f() for f in fns])
+            if grads_enqueued is not None:
+                for j, _ in pending:
+                    grads_enqueued(j)
+            pending.clear()
         nvl = n * la.dout[0] * la.dout[1] * la.dout[2]
         ops.channel_sum(self.dz_last, nvl, 1, G["model.last_conv.bias"], self.ws)
         if grads_enqueued is not None:
@@ -330,13 +341,17 @@ class GeneratorPlan:
             if x16 is None or d16 is None:
                 x16 = d16 = None
             if ly.kind == "convt":  # ConvTranspose3d: the output-grad is the gathered operand
-                self._on_side(lambda g=self.geo_wgrad[i], a=self.dz[i], b=xin, w=G[wname], a16=d16, b16=x16:
-                              self._wgrad(g, a, b, w, zeroed, gathered16=a16, aligned16=b16))
+                pending.append((i, lambda g=self.geo_wgrad[i], a=self.dz[i], b=xin, w=G[wname], a16=d16, b16=x16:
+                                self._wgrad(g, a, b, w, zeroed, gathered16=a16, aligned16=b16)))
             else:
-                self._on_side(lambda g=self.geo_wgrad[i], a=xin, b=self.dz[i], w=G[wname], a16=x16, b16=d16:
-                              self._wgrad(g, a, b, w, zeroed, gathered16=a16, aligned16=b16))
-            if grads_enqueued is not None:
-                grads_enqueued(i)
+                pending.append((i, lambda g=self.geo_wgrad[i], a=xin, b=self.dz[i], w=G[wname], a16=x16, b16=d16:
+                                self._wgrad(g, a, b, w, zeroed, gathered16=a16, aligned16=b16)))
+            # consecutive ResNet-block layers hand their weight grads to the side stream in groups
+            # of WGRAD_GROUP: one cross-stream wait per group (an event record costs the main stream
+            # ~4 us, tools/launch_micro.hip) at the price of starting a wgrad one layer later
+            if i == 0 or len(pending) >= WGRAD_GROUP or not (
+                    "resnet_backbone" in ly.name and "resnet_backbone" in self.layers[i - 1].name):
+                flush()
             if i == 0:
                 break
             # input-grad; a ResNet block0 also receives the skip gradient dL/dh_{r+1}

@@ -538,8 +538,12 @@ class ChannelSumSet:
     """Per-channel sums of several tensors in two launches (cgan3d_channel_sum_multi): the critic's
     bias gradients.  Built once per (tensors, sizes); the descriptors live on the device."""
 
-    def __init__(self, device, items, nblk: int = 64):
-        """items: [(x, nvox, c, out, accumulate)]; every x / out keeps its address."""
+    def __init__(self, device, items, nblk: int = 0):
+        """items: [(x, nvox, c, out, accumulate)]; every x / out keeps its address.  ``nblk``
+        (partial sums per tensor): by default ~16 float4-rows of work per thread of the largest."""
+        if nblk <= 0:
+            big = max(nvox * c for _, nvox, c, _, _ in items)
+            nblk = max(1, min(1024, -(-big // (256 * 16))))
         self.nblk, self.keep = nblk, []
         descs = []
         for x, nvox, c, out, acc in items:

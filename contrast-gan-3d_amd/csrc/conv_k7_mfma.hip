@@ -245,7 +245,7 @@ __global__ __launch_bounds__(256, 2) void k7m_w2n_kernel(K7Args a, const float* 
   constexpr int C = 16;
   __shared__ __attribute__((aligned(16))) __bf16 hs[W_ROWS * W_HW * 8];  // [row][iw][8 channels]
   constexpr int WP = 8 * C + 8;  // (td, th) block of the weight table, padded
-  __shared__ __attribute__((aligned(16))) __bf16 wt[49 * WP];           // [td*7+th][tw8][c]
+  __shared__ __attribute__((aligned(16))) __bf16 wt[50 * WP];           // [td*7+th][tw8][c]; row 49 = 0
   __shared__ float red[4][256];
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int g = lane >> 4, r16 = lane & 15;
@@ -257,6 +257,7 @@ __global__ __launch_bounds__(256, 2) void k7m_w2n_kernel(K7Args a, const float* 
         return tw < K7 ? (long long)c * a.wc + p * K7 + tw : -1;
       },
       [&](int i, float v) { wt[(i >> 7) * WP + (i & 127)] = (__bf16)v; });
+  for (int i = tid; i < WP; i += 256) wt[49 * WP + i] = (__bf16)0.f;  // off-band rows read this zero block
   for (int i = tid; i < W_ROWS * (W_HW - W_HWU) * 8; i += 256) {  // pad columns 22, 23: read with zero weights
     const int r = i / ((W_HW - W_HWU) * 8), j = i % ((W_HW - W_HWU) * 8);
     hs[(r * W_HW + W_HWU) * 8 + j] = (__bf16)0.f;
@@ -328,23 +329,42 @@ __global__ __launch_bounds__(256, 2) void k7m_w2n_kernel(K7Args a, const float* 
       else if (half == 0) load(tile, 1);
       else if (tile + 1 < t1) load(tile + 1, 0);
       __syncthreads();
-      if (!(a.dbg & 1))
-#pragma unroll 5
-      for (int prl = 0; prl < 25; ++prl) {
-        const int pr = wave * 25 + prl;
-        const int id = pr / W_HH, ih = pr - id * W_HH;
-        const int td = id - odl, th = ih - ohl;
-        const bool band = td >= 0 && td < K7 && th >= 0 && th < K7;
-        const __bf16* wrow = wt + (band ? td * K7 + th : 0) * WP + half * 8;
-        const __bf16* hrow = hs + (pr * W_HW + r16) * 8;
+      if (!(a.dbg & 1)) {
+        // software-pipelined: row prl + 1's four fragments are read from LDS while row prl's two
+        // MFMAs run (the LDS latency is otherwise exposed on every row)
+        bf16x8_k av[2][2], bv[2][2];
+        auto fetch = [&](int prl, bf16x8_k (&ar)[2], bf16x8_k (&br)[2]) {
+          const int pr = wave * 25 + prl;
+          const int id = pr / W_HH, ih = pr - id * W_HH;
+          const int td = id - odl, th = ih - ohl;
+          const bool band = td >= 0 && td < K7 && th >= 0 && th < K7;
+          const __bf16* wrow = wt + (band ? td * K7 + th : 49) * WP + half * 8;
+          const __bf16* hrow = hs + (pr * W_HW + r16) * 8;
 #pragma unroll
-        for (int sq = 0; sq < 2; ++sq) {
-          const int tw = 4 * sq + g;
-          const bf16x8_k av = *reinterpret_cast<const bf16x8_k*>(hrow + tw * 8);
-          bf16x8_k bv = *reinterpret_cast<const bf16x8_k*>(wrow + tw * C);
-          if (!band) bv = bf16x8_k{};
-          acc[sq] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, bv, acc[sq], 0, 0, 0);
+          for (int sq = 0; sq < 2; ++sq) {
+            const int tw = 4 * sq + g;
+            ar[sq] = *reinterpret_cast<const bf16x8_k*>(hrow + tw * 8);
+            br[sq] = *reinterpret_cast<const bf16x8_k*>(wrow + tw * C);
+          }
+        };
+        auto mma = [&](const bf16x8_k (&ar)[2], const bf16x8_k (&br)[2]) {
+#pragma unroll
+          for (int sq = 0; sq < 2; ++sq)
+            acc[sq] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ar[sq], br[sq], acc[sq], 0, 0, 0);
+        };
+        fetch(0, av[0], bv[0]);
+#pragma unroll 1
+        for (int prl = 0; prl < 24; prl += 2) {  // ping-pong buffers (compile-time indices)
+          fetch(prl + 1, av[1], bv[1]);
+          __builtin_amdgcn_sched_barrier(0);
+          mma(av[0], bv[0]);
+          __builtin_amdgcn_sched_barrier(0);
+          fetch(prl + 2, av[0], bv[0]);
+          __builtin_amdgcn_sched_barrier(0);
+          mma(av[1], bv[1]);
+          __builtin_amdgcn_sched_barrier(0);
         }
+        mma(av[0], bv[0]);
       }
     }
     acc[0] += acc[1];
@@ -366,6 +386,175 @@ __global__ __launch_bounds__(256, 2) void k7m_w2n_kernel(K7Args a, const float* 
       }
     }
   }
+}
+
+// ---- streamed-plane w2n (16 -> 1 from the bf16 shadow, the generator's last conv): the
+// contraction is split as  out[d][h][w] = sum_td P[d + td - 3][h][w][td]  with
+//   P[q][h][w][td] = sum_{th, tw, c} X[q][h + th - 3][w + tw - 3][c] * W[c][td][th][tw]
+// a GEMM per (input plane q, output row h): M = 16 w, N = td (7 of 16 columns), K = (th, tw, c)
+// = 7 x (8 tw x 16 c) = 28 K-steps.  The A fragment of a K-step is 8 consecutive channels of one
+// staged voxel (16 bytes straight from the plane staged in LDS: no unfolding), the 28 B
+// fragments (the weights) stay in registers for the whole launch, and each A fragment (staged
+// row r, tw pair) feeds the MFMAs of every output row h with th = r - h in range (112 MFMAs per
+// plane and wave, no off-band work).  A block streams the TDc + 6 input planes of a chunk of TDc
+// output planes through a ring of 4 LDS buffers filled by LDS-DMA (global_load_lds, 16 bytes per
+// lane, no staging registers) three planes ahead, together with the minuend rows of the output
+// plane each step finishes; lane (g, td) adds its P values into a per-wave ring of the 7 output
+// planes still open (td selects the plane: no two lanes of an instruction touch one address),
+// and a plane is finished (bias, tanh, opt_hat) once its last input plane has been added.
+__device__ u32x4 k7s_zero;  // zero-initialised device global: the source of out-of-volume granules
+
+namespace k7s {
+constexpr int SH = 4;                    // output rows per block
+constexpr int WB = 64;                   // output columns per block (4 waves x 16)
+constexpr int ROWS = SH + 6, COLS = WB + 7;  // 70 halo columns + one zero column (read by tw = 7)
+constexpr int RB = COLS * 32;            // staged row bytes (16 bf16 channels per voxel)
+constexpr int GRAN = ROWS * COLS * 2;    // 16-byte granules of a plane
+constexpr int GPT = (GRAN + 255) / 256;  // LDS-DMA instructions per wave per plane
+constexpr int MOFF = GPT * 256 * 16;     // minuend granules after the plane (4 waves x 64 lanes;
+constexpr int BUF = MOFF + 4 * 64 * 16;  // 16 of them used) — bytes per ring buffer
+constexpr int NBUF = 4;                  // planes in flight: 3 ahead of the one computed (5: same time)
+constexpr int PER_STEP = GPT + 1;        // LDS-DMA instructions per wave per step
+}  // namespace k7s
+
+__global__ __launch_bounds__(256, 1) void k7s_w2n_kernel(K7Args a, const __bf16* __restrict__ x16,
+                                                         const float* __restrict__ w, float* __restrict__ y,
+                                                         const float* __restrict__ bias, int act,
+                                                         const float* __restrict__ minuend, float* __restrict__ out2,
+                                                         int tdc) {
+  using namespace k7s;
+  extern __shared__ __attribute__((aligned(16))) unsigned char k7s_lds[];
+  unsigned char* bufs = k7s_lds;                                         // [NBUF][BUF]
+  float(*ring)[8][SH][16] = reinterpret_cast<float(*)[8][SH][16]>(k7s_lds + NBUF * BUF);  // per wave
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int g = lane >> 4, r16 = lane & 15;
+  int bid = blockIdx.x;  // (an XCD-grouped tile order measured the same: tools/k7s_probe.py)
+  const int tw_n = a.tiles_w, th_n = a.tiles_h, td_n = a.tiles_d;
+  const int wt_ = bid % tw_n; bid /= tw_n;
+  const int ht_ = bid % th_n; bid /= th_n;
+  const int dt_ = bid % td_n;
+  const int n = bid / td_n;
+  const int d0 = dt_ * tdc, h0 = ht_ * SH, w0 = wt_ * WB;
+  // weights: B fragment (th, j) of lane (g, td = r16): W[c0 .. c0+7][td][th][tw], tw = 2j + (g >> 1)
+  bf16x8_k bw[7][4];
+  {  // branch-free (clamped addresses, then a select): every load of the thread in flight at once
+    const int td = r16, c0 = 8 * (g & 1);
+#pragma unroll
+    for (int th = 0; th < 7; ++th)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int tw = 2 * j + (g >> 1);
+        const bool ok = td < 7 && tw < 7;
+        const long long base = ok ? (td * 7 + th) * 7 + tw : 0;
+        float f[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) f[e] = w[(long long)(c0 + e) * a.wc + base];
+        bf16x8_k v;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = (__bf16)(ok ? f[e] : 0.f);
+        bw[th][j] = v;
+      }
+  }
+  // this lane's plane granules (lane-linear LDS image: granule i of the plane at byte 16 i, i = k *
+  // 256 + wave * 64 + lane): the (h, w) part of the source offset, -1 = zero (past a partial tile,
+  // the tw = 7 pad column, or past the plane's 1420 granules).  Reflect padding (the launcher's
+  // condition): every plane index is in range.
+  int hw[GPT];
+#pragma unroll
+  for (int k = 0; k < GPT; ++k) {
+    const int i = k * 256 + wave * 64 + lane;
+    const int q = i & 1, u = (i >> 1) % COLS, r = (i >> 1) / COLS;
+    const int ih = k7_src(h0 - a.P + r, a.hi, 1);
+    const int iw = u < WB + 6 ? k7_src(w0 - a.P + u, a.wi, 1) : -1;
+    hw[k] = (i < GRAN && (ih | iw) >= 0) ? (ih * a.wi + iw) * 2 + q : -1;
+  }
+  const int nplanes = tdc + 6;
+  const u32x4* xg = reinterpret_cast<const u32x4*>(x16);
+  const float* mbase = out2 ? minuend : y;  // any valid address when there is no minuend
+  // plane s (and the minuend rows of output plane s - 6) into buffer s % NBUF; always PER_STEP
+  // instructions per wave (dummy sources past the chunk) so the vmcnt waits below are exact
+  auto issue = [&](int s) {
+    const int sp = s < nplanes ? s : nplanes - 1;
+    const int id = k7_src(d0 - a.P + sp, a.di, 1);
+    const u32x4* src = xg + (long long)(n * a.di + id) * a.hi * a.wi * 2;
+    unsigned char* dst = bufs + (s % NBUF) * BUF;
+#pragma unroll
+    for (int k = 0; k < GPT; ++k)
+      __builtin_amdgcn_global_load_lds((const void*)(hw[k] >= 0 ? src + hw[k] : &k7s_zero),
+                                       (__attribute__((address_space(3))) void*)(dst + (k * 256 + wave * 64) * 16),
+                                       16, 0, 0);
+    // minuend granule lane (16 per wave: row lane / 4, 4 floats); W % 4 == 0 (launcher)
+    const int df = s - 6, od = d0 + df, oh = h0 + (lane >> 2) % SH, ow = w0 + wave * 16 + 4 * (lane & 3);
+    const bool mok = lane < 16 && out2 && df >= 0 && df < tdc && od < a.do_ && oh < a.ho && ow < a.wo;
+    const float* ms = mok ? mbase + (((long long)n * a.do_ + od) * a.ho + oh) * a.wo + ow
+                          : reinterpret_cast<const float*>(&k7s_zero);
+    __builtin_amdgcn_global_load_lds((const void*)ms,
+                                     (__attribute__((address_space(3))) void*)(dst + MOFF + wave * 64 * 16), 16, 0, 0);
+  };
+  const float b0 = bias ? bias[0] : 0.f;
+  for (int s = 0; s < NBUF - 1; ++s) issue(s);
+  for (int s = 0; s < nplanes; ++s) {
+    // plane s and its minuend rows are in: all but the two later batches retired (in order; the
+    // output stores issued since only make the wait longer), then a barrier so every wave's DMA is
+    // visible to every wave and every wave has finished reading the buffer refilled next
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER_STEP * (NBUF - 2)) : "memory");
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    issue(s + NBUF - 1);  // NBUF - 1 planes ahead, into the buffer of plane s - 1 (dummies past the chunk)
+    const unsigned char* pb = bufs + (s % NBUF) * BUF + (wave * 16 + r16) * 32 + 16 * (g & 1);
+    f32x4 acc[SH];
+#pragma unroll
+    for (int h = 0; h < SH; ++h) acc[h] = f32x4{0.f, 0.f, 0.f, 0.f};
+    // row r + 1's four A fragments are read while row r's MFMAs run
+    bf16x8_k av[2][4];
+    auto fetch = [&](int r, bf16x8_k (&o)[4]) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) o[j] = *reinterpret_cast<const bf16x8_k*>(pb + r * RB + (2 * j + (g >> 1)) * 32);
+    };
+    if (!(a.dbg & 4)) fetch(0, av[0]);
+#pragma unroll
+    for (int r = 0; r < ROWS; ++r) {
+      if (r + 1 < ROWS && !(a.dbg & 4)) fetch(r + 1, av[(r + 1) & 1]);
+      __builtin_amdgcn_sched_barrier(0);
+      if (!(a.dbg & 1))
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int h = 0; h < SH; ++h) {
+          const int th = r - h;
+          if (th >= 0 && th < 7)
+            acc[h] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[r & 1][j], bw[th][j], acc[h], 0, 0, 0);
+        }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    // lane (g, td) holds P[s][h][w = 4g + jj][td]: output plane dl = s - td of this block
+    const int dl = s - r16;
+    if (!(a.dbg & 2) && r16 < 7 && dl >= 0 && dl < tdc) {
+      float* rs = &ring[wave][dl & 7][0][0];
+#pragma unroll
+      for (int h = 0; h < SH; ++h)
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) {
+          float* o = rs + h * 16 + 4 * g + jj;
+          *o = r16 == 0 ? acc[h][jj] : *o + acc[h][jj];
+        }
+    }
+    const int df = s - 6;  // output plane complete after this input plane
+    const int fh = lane >> 4, fwl = lane & 15;
+    const int od = d0 + df, oh = h0 + fh, ow = w0 + wave * 16 + fwl;
+    if (df >= 0 && df < tdc && od < a.do_ && oh < a.ho && ow < a.wo) {
+      float v = ring[wave][df & 7][fh][fwl] + b0;
+      if (act == CGAN3D_ACT_TANH) v = tanhf(v);
+      const long long o = (((long long)n * a.do_ + od) * a.ho + oh) * a.wo + ow;
+      y[o] = v;
+      if (out2) {
+        const float* mrow = reinterpret_cast<const float*>(bufs + (s % NBUF) * BUF + MOFF + wave * 64 * 16);
+        out2[o] = mrow[fh * 16 + fwl] - v;
+      }
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the trailing dummy DMAs land before the block exits
 }
 
 // ---- weight gradients.  Both roles are  dW[c][t] = sum_v X16[v][c] * X1[v + t']  with one
@@ -614,8 +803,31 @@ void k7m_n2w_launch(const cgan3d_conv_geom* g, int P, int reflect, int flip, lon
   ::cg::launch(k7m_n2w_kernel, dim3(grid), dim3(256), 0, s, a, x, w, y, stats, bn_part, per, nt);
 }
 
+static int g_k7s = 0;  // cgan3d_set_tuning key 13: output planes per streamed-w2n block (0 auto, -1 off)
+void k7s_set(int v) { g_k7s = v; }
+
 void k7m_w2n_launch(const cgan3d_conv_geom* g, int P, int reflect, long long wc, const float* x, const float* w,
                     float* y, const Epi& e, hipStream_t s) {
+  if (e.x16 && g_k7s >= 0 && reflect && g->di == g->do_ && g->hi == g->ho && g->wi == g->wo && P == 3 &&
+      std::min(g->di, std::min(g->hi, g->wi)) >= 4 && g->wo % 4 == 0) {
+    // streamed-plane kernel: output-plane chunks of 16 planes, or 8 when 16 leaves CUs idle.  At 64^3
+    // B=4 (tools/k7s_probe.py): 77-80 us against 82-84 for k7m_w2n_kernel; bound by the per-CU rate
+    // of the LDS-DMA plane stream (the halo re-reads: 3.8x the input bytes), not by the MFMAs
+    K7Args a = k7m_args(g, P, reflect, 0, wc, 1, k7s::SH, k7s::WB);
+    int tdc = g_k7s > 0 ? g_k7s : 16;
+    auto blocks = [&](int t) { return (long long)g->n * ((g->do_ + t - 1) / t) * a.tiles_h * a.tiles_w; };
+    if (g_k7s == 0 && blocks(16) < 256) tdc = 8;
+    a.tiles_d = (g->do_ + tdc - 1) / tdc;
+    const size_t lds = (size_t)k7s::NBUF * k7s::BUF + 4 * 8 * k7s::SH * 16 * sizeof(float);
+    static bool attr = false;  // > 64 KB of dynamic LDS must be allowed explicitly
+    if (!attr) {
+      attr = hipFuncSetAttribute((const void*)k7s_w2n_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                 (int)lds) == hipSuccess;
+    }
+    ::cg::launch(k7s_w2n_kernel, dim3((unsigned)blocks(tdc)), dim3(256), lds, s, a, e.x16, w, y, e.bias, e.act,
+                 e.minuend, e.out2, tdc);
+    return;
+  }
   const K7Args a = k7m_args(g, P, reflect, 0, wc, W_TD, W_TH, W_TW);
   int grid, per, nt;
   k7m_n2w_split(a, &grid, &per, &nt);

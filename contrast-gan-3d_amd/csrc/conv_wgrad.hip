@@ -450,12 +450,16 @@ __global__ __launch_bounds__(448) void wgrad_k3_reduce_kernel(const float* __res
     const int t = tid >> 4, al = tid & 15;
     const float* src = ws + ((long long)t * B + b) * A + a0 + al;
     const long long PS = 27LL * A * B;
-    float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};  // 8 independent loads in flight
-    int p = 0;
-    for (; p + 8 <= P; p += 8)
+    float s[16];  // 16 independent loads in flight (the reduce is latency-bound: few blocks, long P)
 #pragma unroll
-      for (int j = 0; j < 8; ++j) s[j] += src[(p + j) * PS];
+    for (int j = 0; j < 16; ++j) s[j] = 0.f;
+    int p = 0;
+    for (; p + 16 <= P; p += 16)
+#pragma unroll
+      for (int j = 0; j < 16; ++j) s[j] += src[(p + j) * PS];
     for (; p < P; ++p) s[0] += src[p * PS];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) s[j] += s[j + 8];
     tile[al][t] = ((s[0] + s[1]) + (s[2] + s[3])) + ((s[4] + s[5]) + (s[6] + s[7]));
   }
   __syncthreads();

@@ -308,7 +308,7 @@ def test_conv_halo_bf16(transposed, cin, cout, k, s, p, sp):
         assert torch.equal(dxo16, dxo), "bf16-shadow input-grad differs"
 
 
-@pytest.mark.parametrize("sp", [(12, 20, 36), (16, 16, 16)])
+@pytest.mark.parametrize("sp", [(12, 20, 36), (16, 16, 16), (20, 9, 72)])
 def test_k7_bf16_mfma(sp):
     """bf16 MFMA variants of the generator's k7 convs (conv_k7_mfma.hip), all four roles plus the
     last conv's input-grad, against torch float64 within 2e-2 (bf16 operands, f32 accumulate); the
@@ -350,12 +350,16 @@ def test_k7_bf16_mfma(sp):
              ops.epilogue(bias=bl.float().cuda(), act=L.ACT_TANH, minuend=mn, out2=o2))
     assert_close(_ncdhw(att).numpy(), yl.detach().numpy(), 2e-2, "k7 w2n fwd")
     assert_close(_ncdhw(o2).numpy(), (x1 - yl).detach().numpy(), 2e-2, "k7 w2n out2")
-    # the same launch staging from a bf16 shadow of x (the same bf16 operands): bit-identical
+    # from a bf16 shadow of x the streamed-plane kernel runs (k7s_w2n_kernel: the same bf16
+    # operands, another fp32 summation order): against float64 at the bf16 bar, and against the
+    # fp32-staging kernel within fp32 reassociation noise (bf16 products summed exactly in fp32)
     att16, o216 = torch.empty_like(att), torch.empty_like(o2)
     ops.conv(geo, _cl(x16), wl.detach().float().cuda(), att16,
              ops.epilogue(bias=bl.float().cuda(), act=L.ACT_TANH, minuend=mn, out2=o216,
                           x_bf16=_cl(x16).bfloat16()))
-    assert torch.equal(att16, att) and torch.equal(o216, o2), "k7 w2n bf16-shadow output differs"
+    assert_close(_ncdhw(att16).numpy(), yl.detach().numpy(), 2e-2, "k7s w2n fwd")
+    assert_close(_ncdhw(o216).numpy(), (x1 - yl).detach().numpy(), 2e-2, "k7s w2n out2")
+    assert float((att16 - att).abs().max()) <= 1e-5, "k7s w2n vs k7m w2n (same bf16 operands)"
     # weight grads
     for name, gw, gath, alig, ref, w in (
             ("k7 wg n2w", ops.conv_wgrad_geom(n, dims, dims, 1, 16, k, 1, p, True), _cl(x1), _cl(gf), dwf, wf),
