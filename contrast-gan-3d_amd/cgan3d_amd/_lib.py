@@ -88,7 +88,7 @@ _SIGS = {
     "cgan3d_bn_backward": ([_P, _P, _I64, _I32, _P, _P, _P, _I32, _F, _P, _P, _P, _I32, _P, _P], _I32),
     "cgan3d_channel_sum_ws_floats": ([_I64, _I32], _I64),
     "cgan3d_channel_sum": ([_P, _I64, _I32, _P, _P, _P], _I32),
-    "cgan3d_channel_sum_multi": ([_P, _I32, _I32, _P], _I32),
+    "cgan3d_channel_sum_multi": ([_P, _I32, _I32, _I32, _P], _I32),
     "cgan3d_reflect_fold": ([_P, _P, _I32, _I32, _I32, _I32, _I32, _I32, _P], _I32),
     "cgan3d_reflect_fold_slots": ([_I32, _I32, _I32, _I32, _I32], _I32),
     "cgan3d_reflect_fold_ex": ([_P, _P, _I32, _I32, _I32, _I32, _I32, _I32, _P, _P], _I32),

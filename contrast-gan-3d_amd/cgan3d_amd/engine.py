@@ -71,7 +71,10 @@ class Arena:
             self.params.append(p)
         total = sum(p.numel() for p in self.params)
         self.flat = torch.empty(total, device=device, dtype=torch.float32)
-        self.grad = torch.zeros(total, device=device, dtype=torch.float32)
+        # grad storage padded to whole 64-byte lines: the per-update memset of the arena
+        # (ops.zero(grad_padded)) is then one fill with no unaligned tail
+        self.grad_padded = torch.zeros((total + 15) // 16 * 16, device=device, dtype=torch.float32)
+        self.grad = self.grad_padded[:total]
         self.exp_avg = torch.zeros(total, device=device, dtype=torch.float32)
         self.exp_avg_sq = torch.zeros(total, device=device, dtype=torch.float32)
         self.views, self.gviews = {}, {}
@@ -222,6 +225,7 @@ class GeneratorPlan:
         # all-zero workspace of the weight grads that sum into theirs by atomics (CGAN3D_WGRAD_WS_CLEAN:
         # each leaves it zeroed, so no memset per layer); they all run on the side stream, in turn
         self.ws_clean = torch.zeros(wsw, device=device)
+        self._csum = {}  # bias-sum launch sets (ops.ChannelSumSet) per gradient dict
         # (CGAN3D_NO_SIDE_STREAM=1 serialises them, so a kernel trace shows unshared durations)
         on_gpu = torch.device(device).type == "cuda" and not os.environ.get("CGAN3D_NO_SIDE_STREAM")
         self.side = torch.cuda.Stream(device=device) if on_gpu else None
@@ -317,7 +321,10 @@ class GeneratorPlan:
                     grads_enqueued(j)
             pending.clear()
         nvl = n * la.dout[0] * la.dout[1] * la.dout[2]
-        ops.channel_sum(self.dz_last, nvl, 1, G["model.last_conv.bias"], self.ws)
+        key = (id(G), "last_bias")
+        if key not in self._csum:
+            self._csum[key] = ops.ChannelSumSet(self.device, [(self.dz_last, nvl, 1, G["model.last_conv.bias"], False)])
+        self._csum[key].run()
         if grads_enqueued is not None:
             grads_enqueued(len(self.layers))
         ops.conv(self.geo_last_dgrad, self.dz_last, P["model.last_conv.weight"], self.dpad)
@@ -912,7 +919,7 @@ class StepEngine:
         if D.ln:  # LayerNorm critic: the interpolation stays in xc (its primal adjoint needs it)
             gamma = D.gam[:bg]
             ops.gradient_penalty(self.gbuf, bg, V, self.gp_weight, gamma, self.losses, self.loss_ws)
-            ops.zero(self.d_arena.grad)  # optimizer_D.zero_grad (Trainer.py:109)
+            ops.zero(self.d_arena.grad_padded)  # optimizer_D.zero_grad (Trainer.py:109)
             D.gp_grads_ln(self.dP, self.dG, self.xc, gamma, bo + bs, bg)
             self._allreduce(self.d_arena.grad)
             self.d_optim.launch()
@@ -920,7 +927,7 @@ class StepEngine:
             return
         gamma = self.xc[bo + bs:]
         ops.gradient_penalty(self.gbuf, bg, V, self.gp_weight, gamma, self.losses, self.loss_ws)
-        ops.zero(self.d_arena.grad)  # optimizer_D.zero_grad (Trainer.py:109): every layer then accumulates
+        ops.zero(self.d_arena.grad_padded)  # optimizer_D.zero_grad (Trainer.py:109): every layer then accumulates
         D.gp_grads_overlapped(self.dP, self.dG, self.xc, gamma, bo + bs, bg, nall, bo + bs, zeroed=True)
         D.join_side()
         self._allreduce(self.d_arena.grad)  # on the critical path: the G update uses the new critic
@@ -935,7 +942,7 @@ class StepEngine:
         D.forward(self.dP, self.xc[:bo], 0, bo, bn_pass=0)
         D.forward(self.dP, self.opt_hat, bo, bs, bn_pass=1)
         ops.critic_logits_grad(D.a[-1], bo, bs, 0, D.logit_ps, self.gan_w, D.dz[-1], self.losses)
-        ops.zero(self.d_arena.grad)  # optimizer_D.zero_grad (Trainer.py:109)
+        ops.zero(self.d_arena.grad_padded)  # optimizer_D.zero_grad (Trainer.py:109)
         D.input_grad(self.dP, 0, bo, self.gbuf, 0, 0, bn_pass=0, G=self.dG)
         D.input_grad(self.dP, bo, bs, self.gbuf, 0, 0, bn_pass=1, G=self.dG, bn_accumulate=True)
         D.weight_grads(self.dP, self.dG, self.xc[:bo + bs], bo + bs, bo + bs, zeroed=True)
@@ -950,7 +957,7 @@ class StepEngine:
         D.input_grad(self.dP, 0, bs, self.dcrit, 0, bs)
         ops.generator_output_grad(self.opt_hat, self.subopt, self.G.att, self.mask, self.dcrit, bs * V, self.lo,
                                   self.hi, self.sim_w, self.hu_w, self.G.dz_last, self.losses, self.loss_ws)
-        ops.zero(self.g_arena.grad)  # optimizer_G.zero_grad (Trainer.py:146): every layer then accumulates
+        ops.zero(self.g_arena.grad_padded)  # optimizer_G.zero_grad (Trainer.py:146): every layer then accumulates
         if self.dp:  # bucketed, overlapped with the rest of the backward
             self.G.backward(self.gP, self.gG, self.subopt, grads_enqueued=self._bucket_ready, zeroed=True)
             self._finish_allreduce()

@@ -557,11 +557,12 @@ class ChannelSumSet:
             descs.append(d)
             self.keep += [x, out, ws]
         self.n = len(descs)
+        self.cmax = max(c for _, _, c, _, _ in items)
         raw = b"".join(bytes(d) for d in descs)
         self.dev = torch.frombuffer(bytearray(raw), dtype=torch.uint8).to(device)
 
     def run(self):
-        check(_launch("cgan3d_channel_sum_multi", ptr(self.dev), self.n, self.nblk), "channel_sum_multi")
+        check(_launch("cgan3d_channel_sum_multi", ptr(self.dev), self.n, self.nblk, self.cmax), "channel_sum_multi")
 
 
 def ln_partial_doubles(n: int, L_: int) -> int:

@@ -345,15 +345,21 @@ __global__ __launch_bounds__(256) void channel_sum_multi_kernel(const cgan3d_csu
   if (tid < C) e.ws[(long long)blockIdx.x * C + tid] = r0[tid];
 }
 
+// block (channel, descriptor): 256 threads over the nblk partials, fp64 tree
 __global__ __launch_bounds__(256) void channel_sum_multi_finalize_kernel(const cgan3d_csum_desc* __restrict__ descs,
                                                                          int nblk) {
-  const cgan3d_csum_desc e = descs[blockIdx.x];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  for (int c = wave; c < e.c; c += 4) {
-    double s = 0.0;
-    for (int b = lane; b < nblk; b += 64) s += e.ws[(long long)b * e.c + c];
-    s = wave_sum_d(s);
-    if (lane == 0) e.out[c] = e.accumulate ? e.out[c] + (float)s : (float)s;
+  __shared__ double red[4];
+  const cgan3d_csum_desc e = descs[blockIdx.y];
+  const int c = blockIdx.x, tid = threadIdx.x;
+  if (c >= e.c) return;
+  double s = 0.0;
+  for (int b = tid; b < nblk; b += 256) s += e.ws[(long long)b * e.c + c];
+  s = wave_sum_d(s);
+  if ((tid & 63) == 0) red[tid >> 6] = s;
+  __syncthreads();
+  if (tid == 0) {
+    const double t = (red[0] + red[1]) + (red[2] + red[3]);
+    e.out[c] = e.accumulate ? e.out[c] + (float)t : (float)t;
   }
 }
 
@@ -646,13 +652,15 @@ extern "C" int cgan3d_bn_apply_slab(const float* part, int32_t nslots, int32_t c
   return rc ? rc : cgan3d_bn_apply(z, nvox, c, scale_shift, act, slope, residual, y, y_bf16, stream);
 }
 
-extern "C" int cgan3d_channel_sum_multi(const cgan3d_csum_desc* descs, int32_t n, int32_t nblk, void* stream) {
-  CG_CHECK_ARG(descs && n > 0 && n <= 65535 && nblk > 0 && nblk <= 4096,
-               "cgan3d_channel_sum_multi: need a device descriptor array, 0 < n <= 65535, 0 < nblk <= 4096");
+extern "C" int cgan3d_channel_sum_multi(const cgan3d_csum_desc* descs, int32_t n, int32_t nblk, int32_t cmax,
+                                        void* stream) {
+  CG_CHECK_ARG(descs && n > 0 && n <= 65535 && nblk > 0 && nblk <= 4096 && cmax > 0 && cmax <= 256,
+               "cgan3d_channel_sum_multi: need a device descriptor array, 0 < n <= 65535, 0 < nblk <= 4096, "
+               "0 < cmax <= 256 (the largest channel count)");
   hipStream_t s = (hipStream_t)stream;
   ::cg::launch(channel_sum_multi_kernel, dim3(nblk, n), dim3(256), 0, s, descs);
   CG_LAUNCH_CHECK("channel_sum_multi_kernel");
-  ::cg::launch(channel_sum_multi_finalize_kernel, dim3(n), dim3(256), 0, s, descs, (int)nblk);
+  ::cg::launch(channel_sum_multi_finalize_kernel, dim3(cmax, n), dim3(256), 0, s, descs, (int)nblk);
   CG_LAUNCH_CHECK("channel_sum_multi_finalize_kernel");
   return CGAN3D_OK;
 }

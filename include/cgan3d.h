@@ -204,7 +204,7 @@ int cgan3d_bn_backward(const float* dy, const float* z, int64_t nvox, int32_t c,
 /* Several channel sums in two launches (the critic's bias gradients, Trainer.py:133 backward of
  * model/discriminator.py's conv biases): `descs` is a DEVICE array of n descriptors (stable
  * pointers, built once), each summing x[nvox][c] per channel into out[c] (+= when accumulate)
- * through its own workspace of nblk * c doubles; c must divide 256.  Sums in fp64. */
+ * through its own workspace of nblk * c doubles; c must divide 256 and be <= cmax.  Sums in fp64. */
 typedef struct cgan3d_csum_desc {
   const float* x;
   float* out;
@@ -213,7 +213,7 @@ typedef struct cgan3d_csum_desc {
   int32_t c;
   int32_t accumulate;
 } cgan3d_csum_desc;
-int cgan3d_channel_sum_multi(const cgan3d_csum_desc* descs, int32_t n, int32_t nblk, void* stream);
+int cgan3d_channel_sum_multi(const cgan3d_csum_desc* descs, int32_t n, int32_t nblk, int32_t cmax, void* stream);
 int64_t cgan3d_channel_sum_ws_floats(int64_t nvox, int32_t c);
 int cgan3d_channel_sum(const float* x, int64_t nvox, int32_t c, float* out, float* ws,
                        void* stream);
