@@ -441,32 +441,36 @@ __global__ __launch_bounds__(512, 2) void wgrad_k3_kernel(Wk3Args a, const float
 }
 
 // dW[b * w_sb + a * w_sa + t] (+)= sum_p ws[p][t][b][a] (27 taps, A gathered x B aligned channels);
-// block = (b, 16 gathered channels)
-__global__ __launch_bounds__(448) void wgrad_k3_reduce_kernel(const float* __restrict__ ws, int P, int A, int B,
+// block = (b, 16 gathered channels, 9 taps); its 576 threads are (tap, channel, quarter of the P
+// partials): each sums a quarter with 16 loads in flight, the quarters are combined in a fixed order
+// (deterministic), one write per weight.  (Latency-bound: 3x the blocks and 4x the loads in flight
+// of one thread per weight.)
+__global__ __launch_bounds__(576) void wgrad_k3_reduce_kernel(const float* __restrict__ ws, int P, int A, int B,
                                                               float* dw, long long w_sa, long long w_sb, int accumulate) {
-  __shared__ float tile[16][28];
-  const int b = blockIdx.x, a0 = blockIdx.y * 16, tid = threadIdx.x;
-  if (tid < 432) {
-    const int t = tid >> 4, al = tid & 15;
-    const float* src = ws + ((long long)t * B + b) * A + a0 + al;
-    const long long PS = 27LL * A * B;
-    float s[16];  // 16 independent loads in flight (the reduce is latency-bound: few blocks, long P)
+  __shared__ float part[4][9][16];
+  const int b = blockIdx.x, a0 = blockIdx.y * 16, t0 = blockIdx.z * 9, tid = threadIdx.x;
+  const int qt = tid / 144, r = tid - qt * 144, tl = r >> 4, al = r & 15;
+  const int t = t0 + tl;
+  const float* src = ws + ((long long)t * B + b) * A + a0 + al;
+  const long long PS = 27LL * A * B;
+  const int pq = (P + 3) / 4, p0 = qt * pq, p1 = min(P, p0 + pq);
+  float s[16];
 #pragma unroll
-    for (int j = 0; j < 16; ++j) s[j] = 0.f;
-    int p = 0;
-    for (; p + 16 <= P; p += 16)
+  for (int j = 0; j < 16; ++j) s[j] = 0.f;
+  int p = p0;
+  for (; p + 16 <= p1; p += 16)
 #pragma unroll
-      for (int j = 0; j < 16; ++j) s[j] += src[(p + j) * PS];
-    for (; p < P; ++p) s[0] += src[p * PS];
+    for (int j = 0; j < 16; ++j) s[j] += src[(p + j) * PS];
+  for (; p < p1; ++p) s[0] += src[p * PS];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) s[j] += s[j + 8];
-    tile[al][t] = ((s[0] + s[1]) + (s[2] + s[3])) + ((s[4] + s[5]) + (s[6] + s[7]));
-  }
+  for (int j = 0; j < 8; ++j) s[j] += s[j + 8];
+  part[qt][tl][al] = ((s[0] + s[1]) + (s[2] + s[3])) + ((s[4] + s[5]) + (s[6] + s[7]));
   __syncthreads();
-  if (tid < 432) {
-    const int al = tid / 27, t = tid - al * 27;
-    float* o = dw + (long long)b * w_sb + (long long)(a0 + al) * w_sa + t;
-    *o = accumulate ? *o + tile[al][t] : tile[al][t];
+  if (tid < 144) {
+    const int tt = tid / 16, aa = tid & 15;  // (the write pattern: consecutive threads, consecutive a)
+    const float v = (part[0][tt][aa] + part[1][tt][aa]) + (part[2][tt][aa] + part[3][tt][aa]);
+    float* o = dw + (long long)b * w_sb + (long long)(a0 + aa) * w_sa + t0 + tt;
+    *o = accumulate ? *o + v : v;
   }
 }
 
@@ -624,7 +628,7 @@ int wgrad_k3_launch(const cgan3d_conv_geom* g, const float* gathered, const floa
     ::cg::launch(wgrad_k3_kernel<true>, dim3(P, 9), dim3(512), 0, st, a, gathered, aligned, g16, a16, ws);
   else
     ::cg::launch(wgrad_k3_kernel<false>, dim3(P, 9), dim3(512), 0, st, a, gathered, aligned, g16, a16, ws);
-  ::cg::launch(wgrad_k3_reduce_kernel, dim3(64, 4), dim3(448), 0, st, (const float*)ws, P, 64, 64, dw, (long long)g->w_sa,
+  ::cg::launch(wgrad_k3_reduce_kernel, dim3(64, 4, 3), dim3(576), 0, st, (const float*)ws, P, 64, 64, dw, (long long)g->w_sa,
                (long long)g->w_sb, accumulate);
   return CGAN3D_OK;
 }
@@ -662,7 +666,7 @@ int wgrad_s2_launch(const cgan3d_conv_geom* g, const float* gathered, const floa
   wgrad_s2_geometry(g, &a, &P);
   if (g16 && a16) ::cg::launch(wgrad_s2_kernel<true>, dim3(P), dim3(512), 0, st, a, gathered, aligned, g16, a16, ws);
   else ::cg::launch(wgrad_s2_kernel<false>, dim3(P), dim3(512), 0, st, a, gathered, aligned, g16, a16, ws);
-  ::cg::launch(wgrad_k3_reduce_kernel, dim3(32, 1), dim3(448), 0, st, (const float*)ws, P, 16, 32, dw,
+  ::cg::launch(wgrad_k3_reduce_kernel, dim3(32, 1, 3), dim3(576), 0, st, (const float*)ws, P, 16, 32, dw,
                (long long)g->w_sa, (long long)g->w_sb, accumulate);
   return CGAN3D_OK;
 }
