@@ -75,6 +75,7 @@ _SIGS = {
     "cgan3d_pack_weights_multi": ([_P, _I32, _I64, _P], _I32),
     "cgan3d_conv3d_wgrad_ws_floats": ([_P], _I64),
     "cgan3d_conv3d_wgrad": ([_P, _P, _P, _P, _I32, _P, _P], _I32),
+    "cgan3d_conv3d_shadow_only": ([_P, _I32], _I32),
     "cgan3d_conv3d_wgrad_ex": ([_P, _P, _P, _P, _I32, _P, _P, _P, _P], _I32),
     "cgan3d_bn_finalize": ([_P, _I64, _I32, _P, _P, _P, _P, _P, _F, _F, _P, _P, _P], _I32),
     "cgan3d_bn_apply": ([_P, _I64, _I32, _P, _I32, _F, _P, _P, _P, _P], _I32),
@@ -106,6 +107,7 @@ _SIGS = {
     "cgan3d_generator_output_grad": ([_P, _P, _P, _P, _P, _I64, _F, _F, _F, _F, _P, _P, _P, _P], _I32),
     "cgan3d_adam_tick": ([_P, _P], _I32),
     "cgan3d_adam": ([_P, _P, _P, _P, _I64, _P, _P], _I32),
+    "cgan3d_adam_pack": ([_P, _P, _P, _P, _I64, _P, _P, _I32, _P, _P], _I32),
     "cgan3d_zero": ([_P, _I64, _P], _I32),
     "cgan3d_ln_partial_doubles": ([_I32, _I64], _I64),
     "cgan3d_ln_reduce": ([_P, _P, _P], _I32),

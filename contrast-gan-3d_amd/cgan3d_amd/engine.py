@@ -41,6 +41,7 @@ Dims = Tuple[int, int, int]
 # step time at 64^3 B=4 under launch plans, 13 fewer launches), or CGAN3D_BN_FUSED_BWD=0 for a
 # separate reduction pass over (dy, z)
 BN_FUSED_BWD = os.environ.get("CGAN3D_BN_FUSED_BWD", "1") == "1"
+UNFUSED_ADAM = os.environ.get("CGAN3D_UNFUSED_ADAM") == "1"
 # weight grads of consecutive ResNet-block layers per cross-stream wait (GeneratorPlan.backward)
 WGRAD_GROUP = max(1, int(os.environ.get("CGAN3D_WGRAD_GROUP", "2")))
 # data parallelism: generator gradient bucket size (all-reduce started per bucket during the backward)
@@ -218,6 +219,25 @@ class GeneratorPlan:
                     self.dz16[i] = bf(ly.dout, ly.cout)
             # ... and of the last conv's input (its 16 -> 1 k7 kernel stages a halo of it per tile)
             self.y16[-1] = bf(layers[-1].dout, layers[-1].cout)
+            # ... and of the first layer's input-grad (its k7 weight grad's 16-channel operand)
+            if BN_FUSED_BWD and ops.shadow_only(self.geo_wgrad[0], 1):
+                self.dz16[0] = bf(layers[0].dout, layers[0].cout)
+        # fp32 tensors that only shadow-reading kernels consume are not written at all (bf16 mode):
+        # at 64^3 the 16-channel outputs / input-grads of the first and last BatchNorm layers, 67 MB
+        # each; the tensors stay allocated (same plan addresses), their contents undefined
+        self.y_dead, self.dz_dead = [False] * len(layers), [False] * len(layers)
+        if not os.environ.get("CGAN3D_KEEP_FP32"):
+            for i, ly in enumerate(layers):
+                if self.y16[i] is not None:
+                    if i == len(layers) - 1:
+                        self.y_dead[i] = ops.shadow_only(self.geo_last_fwd, 0) and ops.shadow_only(
+                            self.geo_last_wgrad, 1)
+                    elif not layers[i + 1].name.endswith("block0") and self.dz16[i + 1] is not None:
+                        self.y_dead[i] = (ops.shadow_only(self.geo_fwd[i + 1], 0)
+                                          and ops.shadow_only(self.geo_wgrad[i + 1], 1))
+                if self.dz16[i] is not None and BN_FUSED_BWD:
+                    reads_ok = i == 0 or (self.y16[i - 1] is not None and ops.shadow_only(self.geo_dgrad[i], 0))
+                    self.dz_dead[i] = reads_ok and ops.shadow_only(self.geo_wgrad[i], 1)
         # weight gradients run on a side stream, beside the input-gradient chain (each wgrad only
         # needs its layer's dz and input, both final when it is enqueued); own workspace
         wsw = max([ops.wgrad_ws_floats(gw) for gw in self.geo_wgrad] + [ops.wgrad_ws_floats(self.geo_last_wgrad)])
@@ -264,7 +284,8 @@ class GeneratorPlan:
                 ops.conv(self.geo_fwd[i], h, self.wf[i], self.z[i], ep)
                 ops.bn_apply_slab(self.part_f[i], self.slots_f[i], ly.cout, nvox, P[f"{nb}.weight"], P[f"{nb}.bias"],
                                   P[f"{nb}.running_mean"], P[f"{nb}.running_var"], P[f"{nb}.num_batches_tracked"],
-                                  self.ss[i], self.mi[i], self.z[i], ly.act, self.y[i], residual=res, y16=self.y16[i])
+                                  self.ss[i], self.mi[i], self.z[i], ly.act, None if self.y_dead[i] else self.y[i],
+                                  residual=res, y16=self.y16[i])
             else:
                 ops.conv(self.geo_fwd[i], h, self.wf[i], self.z[i], ops.epilogue(x_bf16=h16))
                 self._eval_scale_shift(P, nb, i)
@@ -310,7 +331,8 @@ class GeneratorPlan:
         la = self.last
         n = self.n
         u = self.y[-1]
-        self._on_side(lambda: self._wgrad(self.geo_last_wgrad, u, self.dz_last, G["model.last_conv.weight"], zeroed))
+        self._on_side(lambda: self._wgrad(self.geo_last_wgrad, u, self.dz_last, G["model.last_conv.weight"], zeroed,
+                                          gathered16=self.y16[-1] if self.y_dead[-1] else None))
         pending = []  # (layer, weight-grad launcher) not yet handed to the side stream
 
         def flush():
@@ -336,7 +358,8 @@ class GeneratorPlan:
             if BN_FUSED_BWD:
                 ops.bn_backward_slab(self.dy[i], self.z[i], nvox, ly.cout, self.part_b[i], self.slots_b[i],
                                      self.ss[i], self.mi[i], P[f"{nb}.weight"], ly.act, G[f"{nb}.weight"],
-                                     G[f"{nb}.bias"], self.dz[i], self.ws, dz16=self.dz16[i])
+                                     G[f"{nb}.bias"], None if self.dz_dead[i] else self.dz[i], self.ws,
+                                     dz16=self.dz16[i])
             else:
                 ops.bn_backward(self.dy[i], self.z[i], nvox, ly.cout, self.ss[i], self.mi[i], P[f"{nb}.weight"],
                                 ly.act, G[f"{nb}.weight"], G[f"{nb}.bias"], self.dz[i], self.ws)
@@ -345,7 +368,9 @@ class GeneratorPlan:
             # both operands' bf16 shadows, when the layer has them, feed the weight grad
             x16 = self.y16[i - 1] if i > 0 else None
             d16 = self.dz16[i] if BN_FUSED_BWD else None
-            if x16 is None or d16 is None:
+            if i == 0 and self.dz_dead[0]:  # k7 first conv: only its 16-channel operand has a shadow
+                x16 = None
+            elif x16 is None or d16 is None:
                 x16 = d16 = None
             if ly.kind == "convt":  # ConvTranspose3d: the output-grad is the gathered operand
                 pending.append((i, lambda g=self.geo_wgrad[i], a=self.dz[i], b=xin, w=G[wname], a16=d16, b16=x16:
@@ -922,8 +947,7 @@ class StepEngine:
             ops.zero(self.d_arena.grad_padded)  # optimizer_D.zero_grad (Trainer.py:109)
             D.gp_grads_ln(self.dP, self.dG, self.xc, gamma, bo + bs, bg)
             self._allreduce(self.d_arena.grad)
-            self.d_optim.launch()
-            self.D.pack()
+            self._optim_step(self.d_optim, self.D)
             return
         gamma = self.xc[bo + bs:]
         ops.gradient_penalty(self.gbuf, bg, V, self.gp_weight, gamma, self.losses, self.loss_ws)
@@ -931,8 +955,7 @@ class StepEngine:
         D.gp_grads_overlapped(self.dP, self.dG, self.xc, gamma, bo + bs, bg, nall, bo + bs, zeroed=True)
         D.join_side()
         self._allreduce(self.d_arena.grad)  # on the critical path: the G update uses the new critic
-        self.d_optim.launch()
-        self.D.pack()
+        self._optim_step(self.d_optim, self.D)
 
     def _critic_update_clip(self):
         """Weight-clip conf (basic_conf.py:37,60-66): BatchNorm critic run on the real and on the
@@ -947,8 +970,7 @@ class StepEngine:
         D.input_grad(self.dP, bo, bs, self.gbuf, 0, 0, bn_pass=1, G=self.dG, bn_accumulate=True)
         D.weight_grads(self.dP, self.dG, self.xc[:bo + bs], bo + bs, bo + bs, zeroed=True)
         self._allreduce(self.d_arena.grad)
-        self.d_optim.launch()
-        self.D.pack()
+        self._optim_step(self.d_optim, self.D)
 
     def generator_update(self):
         D, bs, V = self.D, self.b_sub, self.vox
@@ -963,8 +985,17 @@ class StepEngine:
             self._finish_allreduce()
         else:
             self.G.backward(self.gP, self.gG, self.subopt, zeroed=True)
-        self.g_optim.launch()
-        self.G.pack()
+        self._optim_step(self.g_optim, self.G)
+
+    @staticmethod
+    def _optim_step(optim, plan):
+        """optimizer.step() (Trainer.py:135,158) and the plan's packed weight copies, as one launch
+        (CGAN3D_UNFUSED_ADAM=1: separate tick / Adam / repack launches, the A/B baseline)."""
+        if UNFUSED_ADAM:
+            optim.launch()
+            plan.pack()
+        else:
+            optim.launch(packs=plan.packs)
 
     def _allreduce(self, flat_grad: torch.Tensor):
         """Mean of the per-rank gradients (RCCL over xGMI with the nccl backend; gloo on CPU)."""

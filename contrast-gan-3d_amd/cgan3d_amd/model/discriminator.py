@@ -5,8 +5,10 @@ same ``state_dict``.  The hot-path configuration is the gradient-penalty critic
 (``norm_layer=nn.Identity``, ``experiments/gradient_penalty_conf.py:14``): k4 s2 p1 convs with
 bias + LeakyReLU(0.2) fused in the conv epilogue, last k4 s1 p1 conv to one channel.  Under
 autograd ``backward`` runs the critic input-grad chain (LeakyReLU masks fused into the
-input-grad conv epilogues) and the weight-grad kernels.  The GP's double backward is done by the
-Trainer's step engine (``cgan3d_amd.engine``), not through autograd.  Also built: the weight-clip
+input-grad conv epilogues) and the weight-grad kernels.  The GP's double backward runs fused in
+the Trainer's step engine (``cgan3d_amd.engine``); for the Identity-norm critic it is also
+available through autograd (``torch.autograd.grad(..., create_graph=True)`` then ``backward``, as
+the reference's ``wgan_gradient_penalty`` does, model/utils.py:34-41) via ``_CriticInputGradFn``.  Also built: the weight-clip
 conf's BatchNorm critic and the gp_layernorm conf's LayerNorm critic (``norm_layer=nn.LayerNorm``,
 ``patch_size=(1, *patch)``, ``elementwise_affine=False``: ``experiments/gp_layernorm.py:9-11``).
 """
@@ -133,19 +135,74 @@ class _CriticFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, grad_out):
-        if torch.is_grad_enabled():
-            raise NotImplementedError("create_graph through the HIP critic: the gradient penalty's double backward "
-                                      "runs in the Trainer step engine (cgan3d_amd.engine.StepEngine)")
+        create_graph = torch.is_grad_enabled()  # autograd.grad(..., create_graph=True): model/utils.py:34-39
         plan, module, xc = ctx.plan, ctx.module, ctx.xc
+        if create_graph and (plan.bn or plan.ln):
+            raise NotImplementedError("create_graph through the HIP critic is built for the GP conf's Identity-norm "
+                                      "critic; the LayerNorm critic's penalty runs in the Trainer step engine "
+                                      "(cgan3d_amd.engine.StepEngine)")
         n = xc.shape[0]
-        plan.dz[-1].view(-1).copy_(grad_out.reshape(-1))
-        dx = torch.empty_like(xc) if ctx.needs_x else None
         names = [nm for nm, _ in module.named_parameters()]
-        grads = {nm: torch.zeros_like(p) for nm, p in module.named_parameters()}
-        if plan.bn and not module.training:
-            raise NotImplementedError("backward through the eval-mode BatchNorm critic")
-        plan.input_grad(module._tensors(), 0, n, dx if dx is not None else xc, 0, n if dx is not None else 0,
-                        G=grads)
-        plan.weight_grads(module._tensors(), grads, xc, n, n)
+        with torch.no_grad():
+            plan.dz[-1].view(-1).copy_(grad_out.reshape(-1))
+            dx = torch.empty_like(xc) if ctx.needs_x else None
+            grads = {nm: torch.zeros_like(p) for nm, p in module.named_parameters()}
+            if plan.bn and not module.training:
+                raise NotImplementedError("backward through the eval-mode BatchNorm critic")
+            plan.input_grad(module._tensors(), 0, n, dx if dx is not None else xc, 0, n if dx is not None else 0,
+                            G=grads)
+            plan.weight_grads(module._tensors(), grads, xc, n, n)
         dxo = dx.view(n, 1, *xc.shape[1:4]) if dx is not None else None
+        if create_graph and dxo is not None:
+            # dx as a differentiable function of the parameters (and of grad_out): the penalty's
+            # double backward, _CriticInputGradFn.backward
+            dxo = _CriticInputGradFn.apply(dxo, grad_out, _PlanRef(plan, module), *module.parameters())
         return (dxo, None, *[grads[nm] for nm in names])
+
+
+class _PlanRef:
+    """Carries a fresh CriticPlan (activations, masks and the dz chain of one forward / backward)
+    into the second-order Function without making it an autograd input."""
+
+    def __init__(self, plan, module):
+        self.plan, self.module = plan, module
+
+
+class _CriticInputGradFn(torch.autograd.Function):
+    """dx = dD/dx . grad_out of the Identity-norm critic (convs + LeakyReLU, gradient_penalty_conf.py:14),
+    differentiable w.r.t. the parameters and grad_out: what ``torch.autograd.grad(critic(x), x,
+    create_graph=True)`` provides the reference's wgan_gradient_penalty (model/utils.py:34-41).
+
+    For s = <dx, gamma>: ds/dW_l = wgrad(nu_{l-1}, dz_l) with the forward-mode tangent
+    nu_0 = gamma, nu_l = m_l * conv_l(nu_{l-1}) along the fixed LeakyReLU masks m_l and dz_l the
+    first backward's chain; ds/db_l = 0; ds/dgrad_out = conv_last(nu_{L-1}); ds/dx = 0 (the masks
+    are piecewise constant in x).  The same chain as the Trainer's fused penalty (engine.py)."""
+
+    @staticmethod
+    def forward(ctx, dx, grad_out, ref, *params):
+        ctx.ref = ref
+        ctx.go_shape = grad_out.shape
+        return dx.view_as(dx)
+
+    @staticmethod
+    def backward(ctx, gamma):
+        plan, module = ctx.ref.plan, ctx.ref.module
+        ctx.ref = None  # the plan's activations are overwritten below: one double backward per forward
+        n = gamma.shape[0]
+        names = [nm for nm, _ in module.named_parameters()]
+        with torch.no_grad():
+            P = module._tensors()
+            g = gamma.detach().float().contiguous().view(n, *plan.dims, 1)
+            plan.gp_forward_mode(P, g, 0, n)  # nu_l over a_l (the masks are consumed as it goes)
+            grads = {nm: torch.zeros_like(p) for nm, p in module.named_parameters()}
+            sink = {nm: torch.zeros_like(p) for nm, p in module.named_parameters() if nm.endswith("bias")}
+            plan.weight_grads(P, {**grads, **sink}, g, n, n)
+            d_go = None
+            if ctx.needs_input_grad[1]:  # J gamma: the last conv (no bias) over nu_{L-1}
+                ly = plan.layers[-1]
+                geo = plan._geo(ops.conv_fwd_geom(n, ly.din, ly.dout, ly.cin, ly.cout, ly.k, ly.s, ly.p), plan.wf[-1])
+                w = plan.wf[-1] if plan.wf[-1] is not None else P[f"{ly.name}.weight"]
+                out = torch.empty((n, *ly.dout, 1), device=gamma.device)
+                ops.conv(geo, plan.a[-2][:n], w, out)
+                d_go = out.view(ctx.go_shape)
+        return (None, d_go, None, *[grads[nm] for nm in names])

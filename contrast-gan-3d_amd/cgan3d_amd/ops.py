@@ -134,13 +134,16 @@ class PackSet:
         self.dev = None
         return gp, wp
 
-    def pack(self):
-        if not self.descs:
-            return
+    def device_descs(self) -> torch.Tensor:
         if self.dev is None:
             raw = b"".join(bytes(d[0]) for d in self.descs)
             self.dev = torch.frombuffer(bytearray(raw), dtype=torch.uint8).to(self.device)
-        pack_weights_multi(self.dev, len(self.descs), self.max_total)
+        return self.dev
+
+    def pack(self):
+        if not self.descs:
+            return
+        pack_weights_multi(self.device_descs(), len(self.descs), self.max_total)
 
 
 # --- geometry per role ------------------------------------------------------------------------
@@ -405,6 +408,12 @@ def zero(t: torch.Tensor):
     check(_launch("cgan3d_zero", ptr(t), t.numel() * t.element_size()), "zero")
 
 
+def shadow_only(g: ConvGeom, role: int) -> bool:
+    """True if, given bf16 shadows, the kernel ``g`` dispatches to reads only them (role 0: conv
+    input via ``epilogue(x_bf16=...)``; role 1: weight-gradient operands) — cgan3d_conv3d_shadow_only."""
+    return bool(L.load().cgan3d_conv3d_shadow_only(ctypes.byref(g), int(role)))
+
+
 def wgrad(g: ConvGeom, gathered, aligned, dw, ws, accumulate=False, gathered16=None, aligned16=None,
           ws_clean=False):
     """Weight gradient; ``gathered16`` / ``aligned16``: optional bf16 shadows of the operands.
@@ -476,13 +485,28 @@ def bn_finalize_slab(part, nslots, c, nvox, gamma, beta, rmean, rvar, nbt, scale
                   ptr(nbt), momentum, eps, ptr(scale_shift), ptr(mean_invstd)), "bn_finalize_slab")
 
 
+def _need_ticket(t, what):
+    if t.dtype != torch.int32 or t.numel() < 2 or not t.is_contiguous():
+        raise ValueError(f"{what}: ticket must be >= 2 contiguous int32 words (zeroed once)")
+    if t.device.type != "cuda" and not DRY_RUN:
+        raise ValueError(f"{what}: ticket must be a device tensor")
+
+
+def tickets(n: int, device) -> torch.Tensor:
+    """``n`` launch tickets (2 zeroed int32 words each, left zeroed by every launch); ``tickets(n)[i]``."""
+    return torch.zeros((n, 2), dtype=torch.int32, device=device)
+
+
 def bn_apply_slab(part, nslots, c, nvox, gamma, beta, rmean, rvar, nbt, scale_shift, mean_invstd, z, act, y,
                   residual=None, slope=0.0, momentum=0.1, eps=1e-5, y16=None):
     """``bn_finalize_slab`` + ``bn_apply`` (one launch when the slab is small)."""
     bn_finalize_slab(part, nslots, c, nvox, gamma, beta, rmean, rvar, nbt, scale_shift, mean_invstd, momentum, eps,
                      _checks_only=True)
     _need(z, nvox * c, "bn_apply_slab z")
-    _need(y, nvox * c, "bn_apply_slab y")
+    if y is None and y16 is None:
+        raise ValueError("bn_apply_slab: y may be None only when y16 is given")
+    if y is not None:
+        _need(y, nvox * c, "bn_apply_slab y")
     if residual is not None:
         _need(residual, nvox * c, "bn_apply_slab residual")
     check(_launch("cgan3d_bn_apply_slab", ptr(part), nslots, c, nvox, ptr(gamma), ptr(beta), ptr(rmean), ptr(rvar),
@@ -493,8 +517,11 @@ def bn_apply_slab(part, nslots, c, nvox, gamma, beta, rmean, rvar, nbt, scale_sh
 def bn_backward_slab(dy, z, nvox, c, part, nslots, scale_shift, mean_invstd, gamma, act, dgamma, dbeta, dz, ws,
                      slope=0.0, accumulate=False, dz16=None):
     """BatchNorm backward from a mode-2 slab (written by the kernel that produced dy)."""
+    if dz is None and dz16 is None:
+        raise ValueError("bn_backward_slab: dz may be None only when dz16 is given")
     for t, nm in ((dy, "dy"), (z, "z"), (dz, "dz")):
-        _need(t, nvox * c, f"bn_backward_slab {nm}")
+        if t is not None:
+            _need(t, nvox * c, f"bn_backward_slab {nm}")
     _need(part, 2 * c * nslots, "bn_backward_slab part", exact=False)
     for t, nm in ((scale_shift, "scale_shift"), (mean_invstd, "mean_invstd")):
         _need(t, 2 * c, f"bn_backward_slab {nm}")
@@ -681,6 +708,24 @@ def adam(param, grad, exp_avg, exp_avg_sq, hyper):
     _need(hyper, 6, "adam hyper")
     check(_launch("cgan3d_adam", ptr(param), ptr(grad), ptr(exp_avg), ptr(exp_avg_sq), param.numel(), ptr(hyper)),
           "adam")
+
+
+def adam_pack(param, grad, exp_avg, exp_avg_sq, hyper, ticket, packs: Optional["PackSet"] = None):
+    """``adam_tick`` + ``adam`` + ``packs.pack()`` as one launch (cgan3d_adam_pack); every packed
+    copy's source weight must be a contiguous view into ``param``."""
+    for t, nm in ((grad, "grad"), (exp_avg, "exp_avg"), (exp_avg_sq, "exp_avg_sq")):
+        _need(t, param.numel(), f"adam_pack {nm}")
+    _need(hyper, 6, "adam_pack hyper")
+    _need_ticket(ticket, "adam_pack")
+    nd = 0
+    if packs is not None and packs.descs:
+        lo, hi = param.data_ptr(), param.data_ptr() + 4 * param.numel()
+        for _, _, w in packs.descs:
+            if not (w.is_contiguous() and lo <= w.data_ptr() and w.data_ptr() + 4 * w.numel() <= hi):
+                raise ValueError("adam_pack: a packed weight is not a contiguous view into the parameter arena")
+        nd = len(packs.descs)
+    check(_launch("cgan3d_adam_pack", ptr(param), ptr(grad), ptr(exp_avg), ptr(exp_avg_sq), param.numel(), ptr(hyper),
+                  ptr(packs.device_descs()) if nd else None, nd, ptr(ticket)), "adam_pack")
 
 
 def unpack_patches(src: torch.Tensor, data: torch.Tensor, seg: torch.Tensor, shift: float, factor: float):

@@ -40,6 +40,7 @@ class FusedAdam(torch.optim.Optimizer):
         # device-resident [lr, beta1, beta2, eps, step, clip] so a captured step replays correctly
         self.hyper = torch.tensor([lr, betas[0], betas[1], eps, 0.0, weight_clip or 0.0], device=dev,
                                   dtype=torch.float32)
+        self.ticket = ops.tickets(1, dev)[0]  # launch ticket of the fused update + repack
         self._host_step = 0
         self._host_lr = lr
         for p, name in zip(arena.params, arena.names):
@@ -58,11 +59,16 @@ class FusedAdam(torch.optim.Optimizer):
             self.hyper[0].fill_(lr)
             self._host_lr = lr
 
-    def launch(self):
-        """Enqueue one update (step counter advanced on the device); no host sync."""
-        ops.adam_tick(self.hyper)
+    def launch(self, packs=None):
+        """Enqueue one update (step counter advanced on the device); no host sync.  With
+        ``packs`` (an ops.PackSet over this arena's weights) the packed copies are refreshed in
+        the same launch (cgan3d_adam_pack: every updated parameter also written packed)."""
         a = self.arena
-        ops.adam(a.flat, a.grad, a.exp_avg, a.exp_avg_sq, self.hyper)
+        if packs is not None:
+            ops.adam_pack(a.flat, a.grad, a.exp_avg, a.exp_avg_sq, self.hyper, self.ticket, packs)
+        else:
+            ops.adam_tick(self.hyper)
+            ops.adam(a.flat, a.grad, a.exp_avg, a.exp_avg_sq, self.hyper)
         if not ops.recording():  # a recorded plan counts its steps when it runs (note_step)
             self._host_step += 1
 

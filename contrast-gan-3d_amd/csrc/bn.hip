@@ -103,7 +103,7 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const float* __restrict__
 #pragma unroll
     for (int e = 0; e < 4; ++e) v[e] = act_f(v[e] * sc[e] + sf[e], act, slope);
     if (res) v += r4[i];
-    y4[i] = v;
+    if (y) y4[i] = v;  // (null: only the bf16 copy is read downstream)
     if (y16) store16(y16, i, v);
   }
 }
@@ -199,7 +199,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const float* __restri
       const float xh = (zz[e] - mean[e]) * inv[e];
       o[e] = k0[e] * (g - k1[e] - xh * k2[e]);
     }
-    o4[i] = o;
+    if (dz) o4[i] = o;
     if (dz16) store16(dz16, i, o);
   }
 }
@@ -234,14 +234,13 @@ __device__ __forceinline__ void slab_sums(const float* __restrict__ part, int ns
 }
 
 // forward slab rows: sum (c), M2 about the block mean (C + c), block count (2C); Chan's combine
-// in fp64, read coalesced (one block per channel, threads striding the slots)
-__global__ __launch_bounds__(256) void bn_finalize_slab_kernel(const float* __restrict__ part, int nslots, int C,
-                                                               double nvox, const float* gamma, const float* beta,
-                                                               float* rmean, float* rvar, long long* nbt,
-                                                               float momentum, float eps, float* scale_shift,
-                                                               float* mean_invstd) {
+// in fp64, read coalesced (one block per channel, threads striding the slots).
+__device__ __forceinline__ void finalize_slab_channel(int c, const float* __restrict__ part, int nslots, int C,
+                                                      double nvox, const float* gamma, const float* beta,
+                                                      float* rmean, float* rvar, long long* nbt, float momentum,
+                                                      float eps, float* scale_shift, float* mean_invstd) {
   __shared__ double red[3][4];
-  const int c = blockIdx.x, tid = threadIdx.x;
+  const int tid = threadIdx.x;
   const float* rs = part + (long long)c * nslots;
   const float* rq = part + (long long)(C + c) * nslots;
   const float* rn = part + (long long)2 * C * nslots;
@@ -277,6 +276,15 @@ __global__ __launch_bounds__(256) void bn_finalize_slab_kernel(const float* __re
     if (rvar) rvar[c] = (float)((1.0 - momentum) * rvar[c] + momentum * var * nvox / (nvox > 1 ? nvox - 1 : 1));
     if (nbt && c == 0) *nbt += 1;
   }
+}
+
+__global__ __launch_bounds__(256) void bn_finalize_slab_kernel(const float* __restrict__ part, int nslots, int C,
+                                                               double nvox, const float* gamma, const float* beta,
+                                                               float* rmean, float* rvar, long long* nbt,
+                                                               float momentum, float eps, float* scale_shift,
+                                                               float* mean_invstd) {
+  finalize_slab_channel(blockIdx.x, part, nslots, C, nvox, gamma, beta, rmean, rvar, nbt, momentum, eps, scale_shift,
+                        mean_invstd);
 }
 
 __global__ __launch_bounds__(256) void bn_bwd_finalize_slab_kernel(const float* __restrict__ part, int nslots, int C,
@@ -432,7 +440,7 @@ __global__ __launch_bounds__(256) void bn_apply_slab_kernel(const float* __restr
 #pragma unroll
     for (int e = 0; e < 4; ++e) v[e] = act_f(v[e] * sc4[e] + sf4[e], act, slope);
     if (res) v += r4[i];
-    y4[i] = v;
+    if (y) y4[i] = v;  // (null: only the bf16 copy is read downstream)
     if (y16) store16(y16, i, v);
   }
 }
@@ -496,7 +504,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_slab_kernel(const float* __r
       const float xh = (zz[e] - mean[e]) * inv[e];
       o[e] = k0[e] * (g - k1[e] - xh * k2[e]);
     }
-    o4[i] = o;
+    if (dz) o4[i] = o;
     if (dz16) store16(dz16, i, o);
   }
 }
@@ -536,7 +544,7 @@ extern "C" int cgan3d_bn_finalize(const float* stats, int64_t nblk, int32_t c, c
 
 extern "C" int cgan3d_bn_apply(const float* z, int64_t nvox, int32_t c, const float* scale_shift, int32_t act,
                                float slope, const float* residual, float* y, void* y_bf16, void* stream) {
-  CG_CHECK_ARG(z && scale_shift && y, "cgan3d_bn_apply: null pointer");
+  CG_CHECK_ARG(z && scale_shift && (y || y_bf16), "cgan3d_bn_apply: null pointer");
   CG_CHECK_ARG(nvox > 0 && c > 0 && c % 4 == 0 && 256 % (c / 4) == 0,
                "cgan3d_bn_apply: channels must be a multiple of 4 dividing 1024");
   const long long n4 = (long long)nvox * c / 4;
@@ -564,7 +572,8 @@ extern "C" int cgan3d_bn_backward_slab(const float* dy, const float* z, int64_t 
                                        int32_t nslots, const float* scale_shift, const float* mean_invstd,
                                        const float* gamma, int32_t act, float slope, float* dgamma, float* dbeta,
                                        float* dz, int32_t accumulate, float* ws, void* dz_bf16, void* stream) {
-  CG_CHECK_ARG(dy && z && part && scale_shift && mean_invstd && gamma && dz && ws, "cgan3d_bn_backward_slab: null pointer");
+  CG_CHECK_ARG(dy && z && part && scale_shift && mean_invstd && gamma && (dz || dz_bf16) && ws,
+               "cgan3d_bn_backward_slab: null pointer");
   CG_CHECK_ARG(nvox > 1 && nslots > 0 && c >= 4 && c <= 256 && 256 % c == 0,
                "cgan3d_bn_backward_slab: channels must divide 256 and be >= 4");
   hipStream_t s = (hipStream_t)stream;
@@ -636,7 +645,8 @@ extern "C" int cgan3d_bn_apply_slab(const float* part, int32_t nslots, int32_t c
                                     int64_t* num_batches_tracked, float momentum, float eps, float* scale_shift,
                                     float* mean_invstd, const float* z, int32_t act, float slope,
                                     const float* residual, float* y, void* y_bf16, void* stream) {
-  CG_CHECK_ARG(part && gamma && beta && scale_shift && mean_invstd && z && y, "cgan3d_bn_apply_slab: null pointer");
+  CG_CHECK_ARG(part && gamma && beta && scale_shift && mean_invstd && z && (y || y_bf16),
+               "cgan3d_bn_apply_slab: null pointer");
   CG_CHECK_ARG(nslots > 0 && nvox > 0 && c >= 4 && c % 4 == 0 && 256 % c == 0,
                "cgan3d_bn_apply_slab: channels must be a multiple of 4 dividing 256");
   const long long n4 = (long long)nvox * c / 4;
@@ -664,3 +674,4 @@ extern "C" int cgan3d_channel_sum_multi(const cgan3d_csum_desc* descs, int32_t n
   CG_LAUNCH_CHECK("channel_sum_multi_finalize_kernel");
   return CGAN3D_OK;
 }
+

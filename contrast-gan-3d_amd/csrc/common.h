@@ -147,11 +147,14 @@ __device__ __forceinline__ void bn_pair(const Epi& e, float v, long long o, int 
 int k7_try_fwd(const cgan3d_conv_geom* g, const float* x, const float* w, float* y, const Epi& e, hipStream_t s);
 void k7s_set(int v);
 int k7_wgrad_handles(const cgan3d_conv_geom* g);
-int k7_try_wgrad(const cgan3d_conv_geom* g, const float* x, const float* go, float* dw, float* ws, hipStream_t s);
+int k7m_wgrad_taken(const cgan3d_conv_geom* g);
+int k7m_w2n_taken(const cgan3d_conv_geom* g);
+int k7_try_wgrad(const cgan3d_conv_geom* g, const float* x, const float* go, float* dw, float* ws, hipStream_t s,
+                 const __bf16* wide16 = nullptr);
 long long k7_wgrad_ws_floats(const cgan3d_conv_geom* g);
 long long k7m_wgrad_ws_floats(const cgan3d_conv_geom* g);
 void k7m_wgrad_launch(const cgan3d_conv_geom* g, bool wide_in, long long wc, const float* x, const float* go, float* dw,
-                      float* ws, hipStream_t s);
+                      float* ws, hipStream_t s, const __bf16* wide16 = nullptr);
 long long k7_n2w_blocks(const cgan3d_conv_geom* g);
 long long k7m_n2w_blocks(const cgan3d_conv_geom* g);
 void k7m_n2w_launch(const cgan3d_conv_geom* g, int P, int reflect, int flip, long long wc, const float* x,
@@ -213,6 +216,56 @@ __device__ __forceinline__ void bn_pair_z(const Epi& e, float v, float z, int c,
   const float gg = v * act_grad(z * e.bn_ss[c] + e.bn_ss[C + c], e.bn_act, e.bn_slope);
   *p1 += gg;
   *p2 += gg * (z - e.bn_mi[c]) * e.bn_mi[C + c];
+}
+
+// ---- launch tickets: "last block out" of a launch, without any waiting.  Two uint32 words, zeroed
+// once by the caller; each block takes a ticket when it is done and the last one (true in its
+// thread 0) re-zeroes them.  Relaxed agent-scope atomics: no cache writeback / invalidate.  (A
+// phase gate on top of this — later blocks spinning until earlier ones publish — measured 1.3-5x
+// slower than two launches for BatchNorm finalize + apply)
+__device__ __forceinline__ bool last_block_out(unsigned* ticket) {
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned nblk = gridDim.x * gridDim.y * gridDim.z;
+    if (__hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nblk - 1) {
+      __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return true;
+    }
+  }
+  return false;
+}
+
+// torch.optim.Adam single-element update (no weight decay / amsgrad / maximize) at the 1-based
+// `step`, then the optional WGAN weight clip (Trainer.py:136-138).  hyper = [lr, beta1, beta2, eps,
+// step, clip]; shared by adam_kernel and the fused update + repack launch.
+struct AdamK {
+  float lr, b2, eps, clip, bc2s, wgt, step_size;
+};
+__device__ __forceinline__ AdamK adam_k(const float* hyper, float step) {
+#pragma clang fp contract(off)
+  AdamK k;
+  const float b1 = hyper[1];
+  k.lr = hyper[0]; k.b2 = hyper[2]; k.eps = hyper[3]; k.clip = hyper[5];
+  k.bc2s = sqrtf(1.f - powf(k.b2, step));
+  k.wgt = 1.f - b1;
+  k.step_size = k.lr / (1.f - powf(b1, step));
+  return k;
+}
+__device__ __forceinline__ float adam_elem(const AdamK& k, float* __restrict__ p, const float* __restrict__ g,
+                                          float* __restrict__ m, float* __restrict__ v, long long i) {
+#pragma clang fp contract(off)  // the same roundings in every kernel that inlines it (no FMA choices)
+  const float gi = g[i];
+  float mi = m[i];
+  // torch lerp: weight < 0.5 ? self + w*(end-self) : end - (end-self)*(1-w)
+  mi = k.wgt < 0.5f ? mi + k.wgt * (gi - mi) : gi - (gi - mi) * (1.f - k.wgt);
+  const float vi = v[i] * k.b2 + (1.f - k.b2) * gi * gi;
+  m[i] = mi;
+  v[i] = vi;
+  const float denom = sqrtf(vi) / k.bc2s + k.eps;
+  float pi = p[i] - k.step_size * (mi / denom);
+  if (k.clip > 0.f) pi = fminf(fmaxf(pi, -k.clip), k.clip);
+  p[i] = pi;
+  return pi;
 }
 
 // slab slot b, channel c, pair member q of a fused BatchNorm slab

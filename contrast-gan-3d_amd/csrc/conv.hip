@@ -534,6 +534,16 @@ extern "C" int cgan3d_conv3d_wgrad_ws_mode(const cgan3d_conv_geom* g) {
   return wgrad_ws_atomic(g);
 }
 
+extern "C" int32_t cgan3d_conv3d_shadow_only(const cgan3d_conv_geom* g, int32_t role) {
+  if (!g || validate(g, "cgan3d_conv3d_shadow_only")) return 0;
+  if (role == 0)  // stride-2 16 <-> 32 kernels (conv_s2.hip), the 16 -> 1 k7 forward (conv_k7_mfma.hip)
+    return (g->w_packed == 2 && s2_kind(g) != 0) || k7m_w2n_taken(g) ? 1 : 0;
+  if (role != 1 || g->transposed) return 0;
+  if (g->k == 7 && g->stride == 1 && (g->cin == 1 || g->cout == 1)) return k7m_wgrad_taken(g);
+  if (c1_wgrad_ok(g) || wgrad_c1_ok(g)) return 0;
+  return wgrad_s2_ok(g) || wgrad_k3_ok(g) ? 1 : 0;
+}
+
 extern "C" int cgan3d_conv3d_wgrad_ex(const cgan3d_conv_geom* g, const float* gathered, const float* aligned, float* dw,
                                       int32_t accumulate, float* ws, const void* gathered_bf16,
                                       const void* aligned_bf16, void* stream) {
@@ -559,7 +569,9 @@ extern "C" int cgan3d_conv3d_wgrad_ex(const cgan3d_conv_geom* g, const float* ga
       set_error("cgan3d_conv3d_wgrad: memset failed");
       return CGAN3D_EHIP;
     }
-    if (k7_try_wgrad(g, gathered, aligned, dw, ws, s)) {
+    // the 16-channel side may come from its bf16 shadow (gathered for a 16 -> 1 conv, aligned for 1 -> 16)
+    const __bf16* w16 = reinterpret_cast<const __bf16*>(g->cout == 1 ? gathered_bf16 : aligned_bf16);
+    if (k7_try_wgrad(g, gathered, aligned, dw, ws, s, w16)) {
       CG_LAUNCH_CHECK("k7 wgrad");
       return CGAN3D_OK;
     }

@@ -434,12 +434,13 @@ __global__ __launch_bounds__(256) void pack_weights_kernel(const float* __restri
   }
 }
 
-__global__ __launch_bounds__(256) void pack_multi_kernel(const cgan3d_pack_desc* __restrict__ descs) {
-  const cgan3d_pack_desc d = descs[blockIdx.y];
+// one packed copy (descriptor d), this block being block bx of nbx working on it
+__device__ __forceinline__ void pack_one(const cgan3d_pack_desc& d, long long bx, long long nbx) {
+  const long long s0 = bx * blockDim.x + threadIdx.x, st = nbx * blockDim.x;
   if (d.format == 3) {  // conv_sk bf16 [b][tap][a]
     __bf16* wp = reinterpret_cast<__bf16*>(d.wp);
     const long long total = (long long)d.taps * d.cout * d.cin;
-    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long long)gridDim.x * blockDim.x) {
+    for (long long i = s0; i < total; i += st) {
       const int ai = (int)(i % d.cin);
       const long long r = i / d.cin;
       const int t = (int)(r % d.taps), b = (int)(r / d.taps);
@@ -451,7 +452,7 @@ __global__ __launch_bounds__(256) void pack_multi_kernel(const cgan3d_pack_desc*
     __bf16* wp = reinterpret_cast<__bf16*>(d.wp);
     const long long total = (long long)d.taps * d.cout * d.cin;
     const int ng = d.cin / 8;
-    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long long)gridDim.x * blockDim.x) {
+    for (long long i = s0; i < total; i += st) {
       const int ai = (int)(i % d.cin);
       const long long r = i / d.cin;
       const int b = (int)(r % d.cout), t = (int)(r / d.cout);
@@ -460,12 +461,64 @@ __global__ __launch_bounds__(256) void pack_multi_kernel(const cgan3d_pack_desc*
     return;
   }
   const long long total = (long long)d.taps * d.cin * d.ldb;
-  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long long)gridDim.x * blockDim.x) {
+  for (long long i = s0; i < total; i += st) {
     const int b = (int)(i % d.ldb);
     const long long r = i / d.ldb;
     const int ai = (int)(r % d.cin), t = (int)(r / d.cin);
     d.wp[i] = b < d.cout ? d.w[ai * d.sa + b * d.sb + t] : 0.f;
   }
+}
+
+__global__ __launch_bounds__(256) void pack_multi_kernel(const cgan3d_pack_desc* __restrict__ descs) {
+  pack_one(descs[blockIdx.y], blockIdx.x, gridDim.x);
+}
+
+// element `off` of a contiguous weight (taps innermost; the smaller of the sa / sb strides is the
+// inner channel index) written into descriptor d's packed copy: the inverse of pack_one's gather
+__device__ __forceinline__ void pack_elem(const cgan3d_pack_desc& d, int off, float val) {
+  const int taps = d.taps, t = off % taps, r = off / taps;
+  int ai, b;
+  if (d.sa <= d.sb) {
+    ai = r % d.cin;
+    b = r / d.cin;
+  } else {
+    b = r % d.cout;
+    ai = r / d.cout;
+  }
+  if (d.format == 3) {
+    reinterpret_cast<__bf16*>(d.wp)[(b * taps + t) * d.cin + ai] = (__bf16)val;
+  } else if (d.format == 2) {
+    const int ng = d.cin / 8;
+    reinterpret_cast<__bf16*>(d.wp)[(t * d.cout + b) * d.cin + ((ai / 8) ^ (b & (ng - 1))) * 8 + (ai & 7)] =
+        (__bf16)val;
+  } else {
+    d.wp[(t * d.cin + ai) * d.ldb + b] = val;
+  }
+}
+
+// One optimiser step of a network in one launch: Adam over the arena at step hyper[4] + 1, each
+// updated parameter also written into every packed copy of its weight, and the last block out
+// advances hyper[4] (every block read the old step before taking its ticket).  Replaces
+// adam_tick_kernel -> adam_kernel -> pack_multi_kernel with the same bits.  A block works on 256
+// consecutive parameters at a time and scans the descriptors once per chunk (uniform, scalar), so
+// a thread only decodes the one or two packed positions of its own element.
+__global__ __launch_bounds__(256) void adam_pack_kernel(float* __restrict__ p, const float* __restrict__ g,
+                                                        float* __restrict__ m, float* __restrict__ v, long long n,
+                                                        float* hyper, const cgan3d_pack_desc* __restrict__ descs,
+                                                        int ndesc, unsigned* ticket) {
+  const AdamK k = adam_k(hyper, hyper[4] + 1.f);
+  for (long long base = (long long)blockIdx.x * 256; base < n; base += (long long)gridDim.x * 256) {
+    const long long i = base + threadIdx.x;
+    const bool live = i < n;
+    const float pi = live ? adam_elem(k, p, g, m, v, i) : 0.f;
+    for (int j = 0; j < ndesc; ++j) {
+      const cgan3d_pack_desc d = descs[j];
+      const long long lo = d.w - p, hi = lo + (long long)d.taps * d.cin * d.cout;
+      if (hi <= base || lo >= base + 256) continue;  // uniform: this chunk holds none of it
+      if (live && i >= lo && i < hi) pack_elem(d, (int)(i - lo), pi);
+    }
+  }
+  if (last_block_out(ticket)) hyper[4] += 1.f;
 }
 
 int gemm_blocks(const cgan3d_conv_geom* g, long long* mblocks) {
@@ -564,4 +617,16 @@ extern "C" int cgan3d_set_tuning(int32_t key, int32_t value) {
   if (key == 13) { k7s_set(value); return CGAN3D_OK; }
   set_error("cgan3d_set_tuning: unknown key %d", key);
   return CGAN3D_EINVAL;
+}
+
+extern "C" int cgan3d_adam_pack(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, int64_t n,
+                                float* hyper, const cgan3d_pack_desc* descs, int32_t ndesc, uint32_t* ticket,
+                                void* stream) {
+  CG_CHECK_ARG(param && grad && exp_avg && exp_avg_sq && hyper && ticket, "cgan3d_adam_pack: null pointer");
+  CG_CHECK_ARG(n > 0 && ndesc >= 0 && ndesc <= 256 && (ndesc == 0 || descs), "cgan3d_adam_pack: bad sizes");
+  const int blocks = (int)std::min<long long>((n + 255) / 256, 1024);
+  ::cg::launch(adam_pack_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, param, grad, exp_avg, exp_avg_sq,
+               (long long)n, hyper, descs, (int)ndesc, (unsigned*)ticket);
+  CG_LAUNCH_CHECK("adam_pack_kernel");
+  return CGAN3D_OK;
 }

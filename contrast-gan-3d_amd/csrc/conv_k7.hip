@@ -379,6 +379,19 @@ int k7_try_fwd(const cgan3d_conv_geom* g, const float* x, const float* w, float*
   return 0;
 }
 
+// 1 if the forward of a 16 -> 1 k7 conv takes a bf16 MFMA kernel (k7s_w2n / k7m_w2n): given the bf16
+// shadow of its input it reads only that
+int k7m_w2n_taken(const cgan3d_conv_geom* g) {
+  return g->k == 7 && g->stride == 1 && !g->transposed && g->cout == 1 && k7m_ok(g, g->cin);
+}
+
+// 1 if k7_try_wgrad takes a bf16 MFMA kernel (k7m_wg_kernel) for the geometry: it then reads the
+// multi-channel operand from its bf16 shadow alone when one is given
+int k7m_wgrad_taken(const cgan3d_conv_geom* g) {
+  if (g->k != 7 || g->stride != 1 || g->transposed) return 0;
+  return (g->cout == 1 && k7m_ok(g, g->cin)) || (g->cin == 1 && k7m_ok(g, g->cout));
+}
+
 // 1 if k7_try_wgrad handles the geometry (same conditions)
 int k7_wgrad_handles(const cgan3d_conv_geom* g) {
   if (g->k != 7 || g->stride != 1 || g->transposed) return 0;
@@ -387,14 +400,17 @@ int k7_wgrad_handles(const cgan3d_conv_geom* g) {
 }
 
 // Weight-grad launch (dw zeroed by the caller unless accumulating); returns 1 if handled.
-int k7_try_wgrad(const cgan3d_conv_geom* g, const float* x, const float* go, float* dw, float* ws, hipStream_t s) {
+// wide16: optional bf16 shadow of the multi-channel operand (read instead of its fp32 tensor by
+// the MFMA kernel, which rounds it to bf16 anyway: same bits)
+int k7_try_wgrad(const cgan3d_conv_geom* g, const float* x, const float* go, float* dw, float* ws, hipStream_t s,
+                 const __bf16* wide16) {
   if (g->k != 7 || g->stride != 1 || g->transposed) return 0;
   if (g->cout == 1 && k7m_ok(g, g->cin)) {
-    k7m_wgrad_launch(g, true, g->w_sa, x, go, dw, ws, s);
+    k7m_wgrad_launch(g, true, g->w_sa, x, go, dw, ws, s, g->prec == CGAN3D_PREC_BF16 ? wide16 : nullptr);
     return 1;
   }
   if (g->cin == 1 && k7m_ok(g, g->cout)) {
-    k7m_wgrad_launch(g, false, g->w_sb, x, go, dw, ws, s);
+    k7m_wgrad_launch(g, false, g->w_sb, x, go, dw, ws, s, g->prec == CGAN3D_PREC_BF16 ? wide16 : nullptr);
     return 1;
   }
   if (g->cout == 1 && k7_wide_ok(g->cin)) {

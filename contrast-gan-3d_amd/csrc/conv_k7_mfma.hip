@@ -583,7 +583,8 @@ constexpr int G_X1_PER = (G_X1 + 255) / 256;
 template <int MODE>
 __global__ __launch_bounds__(256, 2) void k7m_wg_kernel(K7Args a, const float* __restrict__ x,
                                                         const float* __restrict__ go, float* __restrict__ part,
-                                                        int tiles_per_block, int ntiles) {
+                                                        int tiles_per_block, int ntiles,
+                                                        const __bf16* __restrict__ x16src) {
   constexpr int SX_BYTES = G_ROWS_IN * 8 * G_SXW * 2;    // 53760
   constexpr int AS_BYTES = G_VOX * 16 * 2;               // 16384: [octet][c][8]
   __shared__ __attribute__((aligned(16))) unsigned char lds[SX_BYTES + AS_BYTES + G_ROWS_IN * G_HWP * 2];
@@ -625,12 +626,19 @@ __global__ __launch_bounds__(256, 2) void k7m_wg_kernel(K7Args a, const float* _
         rowbase = (vd < gd && vh < gh) ? ((n * a.do_ + vd) * a.ho + vh) * a.wo : -1;
       }
       const f32x4* p = reinterpret_cast<const f32x4*>(MODE ? x : go);
+      const bf16x4_k* p16 = reinterpret_cast<const bf16x4_k*>(x16src);  // bf16 shadow of the same tensor
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
         const int vw = wl + e;
         const int iw = MODE ? k7_src(vw - a.P, a.wi, a.reflect) : (vw < gw ? vw : -1);
         const bool ok = rowbase >= 0 && vw < gw && iw >= 0;
-        xa[e] = p[ok ? (rowbase + iw) * 4 + c4 : 0];
+        const int idx = ok ? (rowbase + iw) * 4 + c4 : 0;
+        if (p16) {  // exact: bf16 -> fp32 here, back to the same bf16 in store()
+          const bf16x4_k h = p16[idx];
+          xa[e] = f32x4{(float)h[0], (float)h[1], (float)h[2], (float)h[3]};
+        } else {
+          xa[e] = p[idx];
+        }
         if (!ok) xa[e] = f32x4{0.f, 0.f, 0.f, 0.f};
       }
     }
@@ -848,12 +856,12 @@ long long k7m_wgrad_ws_floats(const cgan3d_conv_geom* g) {
 
 // weight grad of a k7 conv with one single-channel side; dw already zeroed (or accumulating)
 void k7m_wgrad_launch(const cgan3d_conv_geom* g, bool wide_in, long long wc, const float* x, const float* go, float* dw,
-                      float* ws, hipStream_t s) {
+                      float* ws, hipStream_t s, const __bf16* wide16) {
   const K7Args a = k7m_args(g, g->pad, g->reflect, 0, wc, G_TD, G_TH, G_TW);
   int grid, per, ntiles;
   k7m_wg_split(g, wide_in, &grid, &per, &ntiles);
-  if (wide_in) ::cg::launch(k7m_wg_kernel<1>, dim3(grid), dim3(256), 0, s, a, x, go, ws, per, ntiles);
-  else ::cg::launch(k7m_wg_kernel<0>, dim3(grid), dim3(256), 0, s, a, x, go, ws, per, ntiles);
+  if (wide_in) ::cg::launch(k7m_wg_kernel<1>, dim3(grid), dim3(256), 0, s, a, x, go, ws, per, ntiles, wide16);
+  else ::cg::launch(k7m_wg_kernel<0>, dim3(grid), dim3(256), 0, s, a, x, go, ws, per, ntiles, wide16);
   const int rows_per = 32;
   ::cg::launch(k7m_colsum_kernel, dim3((G_COLS + 255) / 256, (grid + rows_per - 1) / rows_per), dim3(256), 0, s,
                      ws, grid, rows_per, dw, wc);

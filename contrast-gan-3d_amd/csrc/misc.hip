@@ -15,29 +15,13 @@ void set_error(const char* fmt, ...) {
   va_end(ap);
 }
 
-// torch.optim.Adam single-tensor update (no weight decay / amsgrad / maximize), followed by the
-// optional WGAN weight clip of Trainer.py:136-138.  hyper = [lr, beta1, beta2, eps, step, clip].
+// torch.optim.Adam over a flat arena at step hyper[4] (advanced beforehand by adam_tick_kernel).
 __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, const float* __restrict__ g,
                                                    float* __restrict__ m, float* __restrict__ v, long long n,
                                                    const float* __restrict__ hyper) {
-  const float lr = hyper[0], b1 = hyper[1], b2 = hyper[2], eps = hyper[3], step = hyper[4], clip = hyper[5];
-  const float bc1 = 1.f - powf(b1, step);
-  const float bc2s = sqrtf(1.f - powf(b2, step));
-  const float wgt = 1.f - b1;
-  const float step_size = lr / bc1;
-  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
-    const float gi = g[i];
-    float mi = m[i];
-    // torch lerp: weight < 0.5 ? self + w*(end-self) : end - (end-self)*(1-w)
-    mi = wgt < 0.5f ? mi + wgt * (gi - mi) : gi - (gi - mi) * (1.f - wgt);
-    const float vi = v[i] * b2 + (1.f - b2) * gi * gi;
-    m[i] = mi;
-    v[i] = vi;
-    const float denom = sqrtf(vi) / bc2s + eps;
-    float pi = p[i] - step_size * (mi / denom);
-    if (clip > 0.f) pi = fminf(fmaxf(pi, -clip), clip);
-    p[i] = pi;
-  }
+  const AdamK k = adam_k(hyper, hyper[4]);
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x)
+    adam_elem(k, p, g, m, v, i);
 }
 
 __global__ void adam_tick_kernel(float* hyper) { hyper[4] += 1.f; }

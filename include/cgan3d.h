@@ -134,6 +134,13 @@ typedef struct cgan3d_pack_desc {
   int32_t reserved;
 } cgan3d_pack_desc;
 int cgan3d_pack_weights_multi(const cgan3d_pack_desc* descs, int32_t n, int64_t max_total, void* stream);
+/* One optimiser step in one launch (optimizer.step(), Trainer.py:135,158): cgan3d_adam_tick +
+ * cgan3d_adam over the arena + cgan3d_pack_weights_multi over `descs` (ndesc may be 0), same bits:
+ * each updated parameter is also written into every packed copy whose source weight holds it
+ * (descriptor weights must be contiguous views into `param`).  `ticket`: two uint32 words, zeroed
+ * once by the caller and left zeroed (the last block out advances the step counter). */
+int cgan3d_adam_pack(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, int64_t n, float* hyper,
+                     const cgan3d_pack_desc* descs, int32_t ndesc, uint32_t* ticket, void* stream);
 int cgan3d_conv3d_fwd(const cgan3d_conv_geom* g, const float* x, const float* w, float* y,
                       const cgan3d_epilogue* ep, void* stream);
 /* weight gradient: dw[a*w_sa + b*w_sb + t] (+)= sum_o G_gathered(o,t,a) * O(o,b) with the
@@ -153,6 +160,12 @@ int cgan3d_conv3d_wgrad(const cgan3d_conv_geom* g, const float* gathered, const 
 /* 1 if the weight gradient of `g` sums into its workspace by atomics (the geometries that may take
  * CGAN3D_WGRAD_WS_CLEAN), 0 if not, -1 on an invalid geometry. */
 int cgan3d_conv3d_wgrad_ws_mode(const cgan3d_conv_geom* g);
+/* 1 when the kernel this geometry dispatches to reads ONLY the bf16 shadows of its operands once
+ * they are given, so the caller may leave their fp32 tensors unwritten: role 0 = cgan3d_conv3d_fwd
+ * with cgan3d_epilogue.x_bf16 (the stride-2 16 <-> 32 kernels, the 16 -> 1 k7 conv), role 1 = cgan3d_conv3d_wgrad_ex
+ * with both shadows (ResNet / stride-2 kernels) or, for a k7 conv with a single-channel side, the
+ * multi-channel operand's shadow (the bf16 MFMA kernel).  0 otherwise. */
+int32_t cgan3d_conv3d_shadow_only(const cgan3d_conv_geom* g, int32_t role);
 int cgan3d_conv3d_wgrad_ex(const cgan3d_conv_geom* g, const float* gathered, const float* aligned,
                            float* dw, int32_t accumulate, float* ws, const void* gathered_bf16,
                            const void* aligned_bf16, void* stream);
@@ -163,7 +176,8 @@ int cgan3d_bn_finalize(const float* stats, int64_t nblk, int32_t c, const float*
                        int64_t* num_batches_tracked, float momentum, float eps,
                        float* scale_shift, float* mean_invstd, void* stream);
 /* y_bf16 (optional, NULL = none): a bf16 copy of y written by the same pass (the input of the
- * next ResNet-block conv, cgan3d_epilogue.x_bf16). */
+ * next ResNet-block conv, cgan3d_epilogue.x_bf16).  y may be NULL when y_bf16 is given (every
+ * reader of the output takes the bf16 copy); the same holds for cgan3d_bn_apply_slab. */
 int cgan3d_bn_apply(const float* z, int64_t nvox, int32_t c, const float* scale_shift,
                     int32_t act, float slope, const float* residual, float* y, void* y_bf16, void* stream);
 /* Slots of a launch's fused BatchNorm slab (cgan3d_epilogue bn_part); 0 when the geometry's
@@ -187,12 +201,14 @@ int cgan3d_bn_apply_slab(const float* part, int32_t nslots, int32_t c, int64_t n
                          float momentum, float eps, float* scale_shift, float* mean_invstd, const float* z,
                          int32_t act, float slope, const float* residual, float* y, void* y_bf16,
                          void* stream);
-/* dz_bf16 (optional): bf16 copy of dz, as y_bf16 above (input of a ResNet-block input-grad). */
+/* dz_bf16 (optional): bf16 copy of dz, as y_bf16 above (input of a ResNet-block input-grad);
+ * dz may then be NULL. */
 int cgan3d_bn_backward_slab(const float* dy, const float* z, int64_t nvox, int32_t c, const float* part,
                             int32_t nslots, const float* scale_shift, const float* mean_invstd,
                             const float* gamma, int32_t act, float slope, float* dgamma, float* dbeta,
                             float* dz, int32_t accumulate, float* ws, void* dz_bf16, void* stream);
 int64_t cgan3d_bn_backward_ws_floats(int64_t nvox, int32_t c);
+
 /* accumulate != 0: dgamma/dbeta += this batch's gradients (a module called on several batches in
  * one step, e.g. the BatchNorm critic on the real and the fake batch, Trainer.py:119-121). */
 int cgan3d_bn_backward(const float* dy, const float* z, int64_t nvox, int32_t c,

@@ -136,6 +136,43 @@ def test_critic_autograd_backward_matches_oracle(norm):
         assert_close(p.grad.cpu().numpy(), gr.numpy(), 1e-3, f"dD/d{k}")
 
 
+def test_reference_style_gradient_penalty_double_backward():
+    """The reference's own penalty code path over the HIP critic (model/utils.py:26-41: interpolate,
+    torch.autograd.grad(D(x_hat), x_hat, ones, create_graph=True), lambda * mean((||g|| - 1)^2),
+    then backward): critic parameter gradients against the same code over the oracle's float64
+    critic.  Biases get no penalty gradient (exactly 0 in real arithmetic, atol 1e-9)."""
+    from torch import nn
+    from oracle import reference_torch as R
+    from cgan3d_amd.data.synthetic import synth_patches
+    from cgan3d_amd.model.discriminator import PatchGANDiscriminator
+    from cgan3d_amd.model.init import pcg64_init_
+
+    def penalty(critic_fn, real, fake, eps):
+        xh = (eps * real + (1 - eps) * fake).requires_grad_(True)
+        out = critic_fn(xh)
+        g = torch.autograd.grad(outputs=out, inputs=xh, grad_outputs=torch.ones_like(out), create_graph=True,
+                                retain_graph=True)[0]
+        return 10.0 * ((g.flatten(1).norm(2, dim=1) - 1) ** 2).mean()
+
+    d = pcg64_init_(PatchGANDiscriminator(**D_ARGS, norm_layer=nn.Identity), 1).cuda()
+    par = _oracle_params(d)
+    real, _ = synth_patches(2, 32, 21)
+    fake, _ = synth_patches(2, 32, 22)
+    eps = np.array([0.3, 0.8], dtype=np.float32).reshape(2, 1, 1, 1, 1)
+    gp = penalty(d, *(torch.from_numpy(a).cuda() for a in (real, fake, eps)))
+    gp.backward()
+    keys = [k for k, _ in d.named_parameters()]
+    for k in keys:
+        par[k].requires_grad_(True)
+    gpr = penalty(lambda x: R.critic_forward(par, x, R.CriticConfig(norm="identity")),
+                  *(torch.from_numpy(a).double() for a in (real, fake, eps)))
+    grads = torch.autograd.grad(gpr, [par[k] for k in keys], allow_unused=True)  # (the last bias is unused)
+    grads = [torch.zeros_like(par[k]) if gr is None else gr for k, gr in zip(keys, grads)]
+    assert_close(float(gp.detach()), float(gpr.detach()), 1e-3, "GP value")
+    for (k, p), gr in zip(d.named_parameters(), grads):
+        assert_close(p.grad.cpu().numpy(), gr.numpy(), 1e-3, f"dGP/d{k}", atol=1e-9 if k.endswith("bias") else 0.0)
+
+
 def _random_running_stats(module, rng):
     with torch.no_grad():
         for k, b in module.named_buffers():

@@ -172,3 +172,4 @@ def test_fused_batchnorm_vs_torch(c, act):
     assert torch.equal(dz16, dzd.bfloat16()), "bf16 shadow of the BN input-grad"
     assert_close(dgd.double().cpu().numpy(), dgm.numpy(), 1e-3, "fused bn dgamma")
     assert_close(dbd.double().cpu().numpy(), dbt.numpy(), 1e-3, "fused bn dbeta")
+

@@ -591,3 +591,51 @@ def test_conv_sk_bf16(cin, cout, sp):
     dxo = torch.empty(n, *din, cin, device="cuda")
     ops.conv(gd, _cl(gy), wdp, dxo, ops.epilogue(mask_src=_cl(below), slope=slope))
     assert_close(_ncdhw(dxo).numpy(), dxref.numpy(), 2e-2, "sk dgrad")
+
+
+def test_adam_pack_matches_separate_launches():
+    """cgan3d_adam_pack (step tick + Adam + repack of every packed format in one launch) leaves
+    the same bits as cgan3d_adam_tick -> cgan3d_adam -> cgan3d_pack_weights_multi, over three
+    steps through one ticket (which must stay zeroed)."""
+    from torch import nn
+    from cgan3d_amd import ops, _lib as L
+    from cgan3d_amd.engine import Arena
+    from cgan3d_amd.trainer.optim import FusedAdam
+    torch.manual_seed(3)
+    n = 2
+    layers = [(16, 32, 3, 2, 1, (16, 16, 16), (8, 8, 8)),    # halo / stride-2 family (bf16 format 2)
+              (64, 64, 3, 1, 1, (8, 8, 8), (8, 8, 8)),       # ResNet block (format 2)
+              (8, 16, 4, 2, 1, (16, 16, 16), (8, 8, 8)),     # critic middle (format 3)
+              (12, 20, 3, 1, 1, (5, 6, 7), (5, 6, 7))]       # generic (f32 format 1)
+    mod = nn.Module()
+    for i, (ci, co, k, s, p, di, do) in enumerate(layers):
+        mod.register_parameter(f"w{i}", nn.Parameter(torch.randn(co, ci, k, k, k) * 0.1))
+    mod.register_parameter("b", nn.Parameter(torch.randn(100)))
+    runs = []
+    for fused in (False, True):
+        m2 = nn.Module()
+        for k_, v in mod.named_parameters():
+            m2.register_parameter(k_, nn.Parameter(v.detach().clone().cuda()))
+        ar = Arena(m2, torch.device("cuda"))
+        opt = FusedAdam(ar, 1e-3, (0.0, 0.9), 1e-8)
+        ps = ops.PackSet(torch.device("cuda"))
+        outs = []
+        for i, (ci, co, k, s, p, di, do) in enumerate(layers):
+            pc = L.PREC_BF16 if i < 3 else L.PREC_F32
+            _, wp = ps.add(ops.conv_fwd_geom(n, di, do, ci, co, k, s, p), ar.views[f"w{i}"], pc)
+            outs.append(wp)
+        assert len(ps.descs) == 4
+        g = torch.Generator(device="cuda").manual_seed(11)
+        for _ in range(3):
+            ar.grad.copy_(torch.randn(ar.numel, device="cuda", generator=g))
+            if fused:
+                opt.launch(packs=ps)
+            else:
+                opt.launch()
+                ps.pack()
+            assert torch.equal(opt.ticket.cpu(), torch.zeros(2, dtype=torch.int32))
+        runs.append([ar.flat.clone(), ar.exp_avg.clone(), ar.exp_avg_sq.clone(), opt.hyper.clone()]
+                    + [o.clone() for o in outs])
+    assert float(runs[1][3][4]) == 3.0
+    for j, (a, b) in enumerate(zip(*runs)):
+        assert torch.equal(a, b), f"output {j}"

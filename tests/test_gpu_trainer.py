@@ -172,18 +172,31 @@ def test_trainer_plan_replay_matches_eager(tmp_path, precision, monkeypatch):
         # step may flip noise-level elements (below); in bf16 such an element can round its conv
         # operand the other way, and the generator's BatchNorm backward amplifies that (see
         # test_gpu_configs.py): 5e-3 of the tensor's max there, 1e-4 everywhere else
+        # (bf16 G: relative to the tensor's max, floored at 1 % of the network's largest gradient —
+        # a tensor whose gradients are all near the noise floor, e.g. a first-layer BatchNorm bias at
+        # 1e-3, carries those flips at full relative size)
         for net, (ae, ap) in zip("DG", arenas):
-            tol = 5e-3 if (net == "G" and precision == "bf16") else 1e-4
+            bf16_g = net == "G" and precision == "bf16"
+            tol = 5e-3 if bf16_g else 1e-4
+            floor = 1e-2 * float(ae.grad.abs().max()) if bf16_g else 1e-12
             for k in ae.gviews:
                 ge, gp = ae.gviews[k].cpu().numpy(), ap.gviews[k].cpu().numpy()
-                assert np.abs(ge - gp).max() <= tol * max(np.abs(ge).max(), 1e-12), (it, k)
-        for a, b in ((eager.generator, planned.generator), (eager.critic, planned.critic)):
+                assert np.abs(ge - gp).max() <= tol * max(np.abs(ge).max(), floor), (it, k)
+        max_step = 2 * 1e-4 / np.sqrt(1 - 0.9) * 1.001  # two opposite Adam steps (lr 1e-4, beta2 0.9)
+        for net, a, b in (("G", eager.generator, planned.generator), ("D", eager.critic, planned.critic)):
             for (k, va), (_, vb) in zip(a.state_dict().items(), b.state_dict().items()):
                 va, vb = va.float().cpu().numpy(), vb.float().cpu().numpy()
                 # Adam's normalised step may flip sign where a gradient element is rounding noise
                 d = np.abs(va - vb)
-                off = d > 1e-5 * max(np.abs(va).max(), 1e-3)
-                assert d.max() <= 2 * 1e-4 / np.sqrt(1 - 0.9) * 1.001 and off.mean() <= 0.01, (
+                # "moved" = by more than 1e-5 of the tensor's scale and 1e-3 of lr (a tensor that holds
+                # only a few Adam steps, like a BatchNorm bias at ~4e-4, is otherwise judged at 1e-8);
+                # bf16 generator after a full iteration: by more than the 5e-3 gradient tolerance above
+                # carries into a step, 5e-3 of max_step
+                thr = max(1e-5 * max(np.abs(va).max(), 1e-3), 1e-7)
+                if net == "G" and precision == "bf16" and it % 2 == 0:
+                    thr = max(thr, 5e-3 * max_step)
+                off = d > thr
+                assert d.max() <= max_step and off.mean() <= 0.01, (
                     it, k, float(d.max()), float(off.mean()))
     assert planned.optimizer_D._host_step == eager.optimizer_D._host_step == 7
     assert planned.optimizer_G._host_step == eager.optimizer_G._host_step == 4
