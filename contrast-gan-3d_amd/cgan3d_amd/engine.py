@@ -41,7 +41,6 @@ Dims = Tuple[int, int, int]
 # step time at 64^3 B=4 under launch plans, 13 fewer launches), or CGAN3D_BN_FUSED_BWD=0 for a
 # separate reduction pass over (dy, z)
 BN_FUSED_BWD = os.environ.get("CGAN3D_BN_FUSED_BWD", "1") == "1"
-UNFUSED_ADAM = os.environ.get("CGAN3D_UNFUSED_ADAM") == "1"
 # weight grads of consecutive ResNet-block layers per cross-stream wait (GeneratorPlan.backward)
 WGRAD_GROUP = max(1, int(os.environ.get("CGAN3D_WGRAD_GROUP", "2")))
 # data parallelism: generator gradient bucket size (all-reduce started per bucket during the backward)
@@ -989,13 +988,10 @@ class StepEngine:
 
     @staticmethod
     def _optim_step(optim, plan):
-        """optimizer.step() (Trainer.py:135,158) and the plan's packed weight copies, as one launch
-        (CGAN3D_UNFUSED_ADAM=1: separate tick / Adam / repack launches, the A/B baseline)."""
-        if UNFUSED_ADAM:
-            optim.launch()
-            plan.pack()
-        else:
-            optim.launch(packs=plan.packs)
+        """optimizer.step() (Trainer.py:135,158): Adam with the step tick in one launch, then the
+        plan's packed weight copies (one coalesced repack launch)."""
+        optim.launch()
+        plan.pack()
 
     def _allreduce(self, flat_grad: torch.Tensor):
         """Mean of the per-rank gradients (RCCL over xGMI with the nccl backend; gloo on CPU)."""

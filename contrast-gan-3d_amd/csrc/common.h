@@ -210,6 +210,9 @@ void s2_set(int v);
 void s2_set_dbg(int v);
 int halo_pack(const cgan3d_conv_geom* g, const float* w, void* wp, hipStream_t st);
 int gemm_launch(const cgan3d_conv_geom* g, const float* x, const float* w, float* y, const Epi& e, hipStream_t st);
+// Adam over a flat arena (+ optional repack of packed weight copies, step tick) — conv_gemm.hip
+void adam_launch(float* p, const float* g, float* m, float* v, long long n, float* hyper,
+                 const cgan3d_pack_desc* descs, int ndesc, int tick, unsigned* ticket, hipStream_t st);
 
 // mode-2 pair from a prefetched z
 __device__ __forceinline__ void bn_pair_z(const Epi& e, float v, float z, int c, int C, float* p1, float* p2) {
@@ -242,7 +245,6 @@ struct AdamK {
   float lr, b2, eps, clip, bc2s, wgt, step_size;
 };
 __device__ __forceinline__ AdamK adam_k(const float* hyper, float step) {
-#pragma clang fp contract(off)
   AdamK k;
   const float b1 = hyper[1];
   k.lr = hyper[0]; k.b2 = hyper[2]; k.eps = hyper[3]; k.clip = hyper[5];
@@ -253,7 +255,6 @@ __device__ __forceinline__ AdamK adam_k(const float* hyper, float step) {
 }
 __device__ __forceinline__ float adam_elem(const AdamK& k, float* __restrict__ p, const float* __restrict__ g,
                                           float* __restrict__ m, float* __restrict__ v, long long i) {
-#pragma clang fp contract(off)  // the same roundings in every kernel that inlines it (no FMA choices)
   const float gi = g[i];
   float mi = m[i];
   // torch lerp: weight < 0.5 ? self + w*(end-self) : end - (end-self)*(1-w)

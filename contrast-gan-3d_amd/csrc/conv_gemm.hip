@@ -496,17 +496,17 @@ __device__ __forceinline__ void pack_elem(const cgan3d_pack_desc& d, int off, fl
   }
 }
 
-// One optimiser step of a network in one launch: Adam over the arena at step hyper[4] + 1, each
-// updated parameter also written into every packed copy of its weight, and the last block out
-// advances hyper[4] (every block read the old step before taking its ticket).  Replaces
-// adam_tick_kernel -> adam_kernel -> pack_multi_kernel with the same bits.  A block works on 256
-// consecutive parameters at a time and scans the descriptors once per chunk (uniform, scalar), so
-// a thread only decodes the one or two packed positions of its own element.
+// Adam over the arena at step hyper[4] (+ 1 with `tick`), each updated parameter also written
+// into every packed copy of its weight (ndesc > 0), and with `tick` the last block out advances
+// hyper[4] (every block read the old step before taking its ticket).  One optimiser step of a
+// network is then one launch instead of adam_tick_kernel -> Adam -> pack_multi_kernel, same bits.
+// A block works on 256 consecutive parameters at a time and scans the descriptors once per chunk
+// (uniform, scalar), so a thread only decodes the one or two packed positions of its own element.
 __global__ __launch_bounds__(256) void adam_pack_kernel(float* __restrict__ p, const float* __restrict__ g,
                                                         float* __restrict__ m, float* __restrict__ v, long long n,
                                                         float* hyper, const cgan3d_pack_desc* __restrict__ descs,
-                                                        int ndesc, unsigned* ticket) {
-  const AdamK k = adam_k(hyper, hyper[4] + 1.f);
+                                                        int ndesc, int tick, unsigned* ticket) {
+  const AdamK k = adam_k(hyper, tick ? hyper[4] + 1.f : hyper[4]);
   for (long long base = (long long)blockIdx.x * 256; base < n; base += (long long)gridDim.x * 256) {
     const long long i = base + threadIdx.x;
     const bool live = i < n;
@@ -518,7 +518,13 @@ __global__ __launch_bounds__(256) void adam_pack_kernel(float* __restrict__ p, c
       if (live && i >= lo && i < hi) pack_elem(d, (int)(i - lo), pi);
     }
   }
-  if (last_block_out(ticket)) hyper[4] += 1.f;
+  if (tick && last_block_out(ticket)) hyper[4] += 1.f;
+}
+
+void adam_launch(float* p, const float* g, float* m, float* v, long long n, float* hyper,
+                 const cgan3d_pack_desc* descs, int ndesc, int tick, unsigned* ticket, hipStream_t st) {
+  const int blocks = (int)std::min<long long>((n + 255) / 256, 1024);
+  ::cg::launch(adam_pack_kernel, dim3(blocks), dim3(256), 0, st, p, g, m, v, n, hyper, descs, ndesc, tick, ticket);
 }
 
 int gemm_blocks(const cgan3d_conv_geom* g, long long* mblocks) {
@@ -624,9 +630,8 @@ extern "C" int cgan3d_adam_pack(float* param, const float* grad, float* exp_avg,
                                 void* stream) {
   CG_CHECK_ARG(param && grad && exp_avg && exp_avg_sq && hyper && ticket, "cgan3d_adam_pack: null pointer");
   CG_CHECK_ARG(n > 0 && ndesc >= 0 && ndesc <= 256 && (ndesc == 0 || descs), "cgan3d_adam_pack: bad sizes");
-  const int blocks = (int)std::min<long long>((n + 255) / 256, 1024);
-  ::cg::launch(adam_pack_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, param, grad, exp_avg, exp_avg_sq,
-               (long long)n, hyper, descs, (int)ndesc, (unsigned*)ticket);
+  adam_launch(param, grad, exp_avg, exp_avg_sq, (long long)n, hyper, descs, (int)ndesc, 1, (unsigned*)ticket,
+              (hipStream_t)stream);
   CG_LAUNCH_CHECK("adam_pack_kernel");
   return CGAN3D_OK;
 }

@@ -402,27 +402,31 @@ __global__ __launch_bounds__(256) void conv_s2t_kernel(S2Args a, const float* __
   s2t_class<1, 1, 1>(halo, bq, acc[7], wave, g, r16);
   }
 
-  // ---- epilogue: class c = (rz, ry, rx), slice zz, row j -> output (2(Z0+zz)+rz, 2(Y0+w)+ry, 2(X0+4g+j)+rx)
+  // ---- epilogue: class c = (rz, ry, rx), slice zz, row j -> output (2(Z0+zz)+rz, 2(Y0+w)+ry, 2(X0+4g+j)+rx).
+  // Rows j of one (class, slice) are 2 voxels apart: one 32-bit element offset per (class, slice),
+  // the rows at immediate offsets (the per-element 64-bit index math was most of the kernel's VALU)
   float vals[16][1][4], zv[16][1][4];
   bool ok[16][4];
   const int jy = Y0 + wave;
   const float bias = ep.bias ? ep.bias[r16] : 0.f;
+  // element offsets of this launch fit 32 bits (s2_launch checks it)
+  const int xrow = 2 * (X0 + 4 * g);
 #pragma unroll
   for (int c = 0; c < 8; ++c) {
     const int rz = c >> 2, ry = (c >> 1) & 1, rx = c & 1;
 #pragma unroll
     for (int zz = 0; zz < 2; ++zz) {
       const int jz = Z0 + zz;
+      const bool zy_ok = jz < a.cd && jy < a.ch;
+      const int o0 = ((((nb * a.do_ + 2 * jz + rz) * a.ho + 2 * jy + ry) * a.wo + xrow + rx) * CO) + r16;
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        const int jx = X0 + 4 * g + j;
-        const bool v_ok = jz < a.cd && jy < a.ch && jx < a.cw;
+        const bool v_ok = zy_ok && X0 + 4 * g + j < a.cw;
         ok[c * 2 + zz][j] = v_ok;
-        const long long o =
-            v_ok ? (((long long)nb * a.do_ + 2 * jz + rz) * a.ho + 2 * jy + ry) * a.wo + 2 * jx + rx : 0;
-        zv[c * 2 + zz][0][j] = ep.bn_mode == 2 ? ep.bn_z[o * CO + r16] : 0.f;
+        const int o = v_ok ? o0 + 2 * j * CO : 0;
+        zv[c * 2 + zz][0][j] = ep.bn_mode == 2 ? ep.bn_z[o] : 0.f;
         const float v = s2_act(acc[c][zz][j] + bias, ep);
-        if (v_ok && (!(a.dbg & 4) || v == 1.2345f)) y[o * CO + r16] = v;
+        if (v_ok && (!(a.dbg & 4) || v == 1.2345f)) y[o] = v;
         vals[c * 2 + zz][0][j] = v;
       }
     }
@@ -476,6 +480,10 @@ int s2_launch(const cgan3d_conv_geom* g, const float* x, const __bf16* wp, float
     return CGAN3D_EINVAL;
   }
   S2Args a = s2_args(g, kind);
+  if ((long long)g->n * g->do_ * g->ho * g->wo * g->cout >= (1LL << 31)) {  // 32-bit output offsets
+    set_error("conv_s2: output too large for 32-bit element offsets");
+    return CGAN3D_EINVAL;
+  }
   const dim3 grid((unsigned)((long long)a.n * a.td * a.th * a.tw));
   if (kind == 1) ::cg::launch(conv_s2f_kernel, grid, dim3(256), 0, st, a, x, wp, y, e);
   else ::cg::launch(conv_s2t_kernel, grid, dim3(256), 0, st, a, x, wp, y, e);

@@ -15,15 +15,6 @@ void set_error(const char* fmt, ...) {
   va_end(ap);
 }
 
-// torch.optim.Adam over a flat arena at step hyper[4] (advanced beforehand by adam_tick_kernel).
-__global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, const float* __restrict__ g,
-                                                   float* __restrict__ m, float* __restrict__ v, long long n,
-                                                   const float* __restrict__ hyper) {
-  const AdamK k = adam_k(hyper, hyper[4]);
-  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x)
-    adam_elem(k, p, g, m, v, i);
-}
-
 __global__ void adam_tick_kernel(float* hyper) { hyper[4] += 1.f; }
 
 // out[i] = sum of padded[q] over the reflect-pad preimages q of interior voxel i
@@ -160,10 +151,11 @@ extern "C" int cgan3d_adam(float* param, const float* grad, float* exp_avg, floa
                            const float* hyper, void* stream) {
   CG_CHECK_ARG(param && grad && exp_avg && exp_avg_sq && hyper, "cgan3d_adam: null pointer");
   CG_CHECK_ARG(n > 0, "cgan3d_adam: n must be positive");
-  int blocks = (int)std::min<long long>((n + 255) / 256, 2048);
-  ::cg::launch(adam_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, param, grad, exp_avg, exp_avg_sq,
-                     (long long)n, hyper);
-  CG_LAUNCH_CHECK("adam_kernel");
+  // torch.optim.Adam at step hyper[4] (advanced beforehand by cgan3d_adam_tick): the Adam phase
+  // of adam_pack_kernel (conv_gemm.hip) with no packed copies and no tick
+  adam_launch(param, grad, exp_avg, exp_avg_sq, (long long)n, const_cast<float*>(hyper), nullptr, 0, 0, nullptr,
+              (hipStream_t)stream);
+  CG_LAUNCH_CHECK("adam_pack_kernel");
   return CGAN3D_OK;
 }
 

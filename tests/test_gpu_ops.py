@@ -631,7 +631,8 @@ def test_adam_pack_matches_separate_launches():
             if fused:
                 opt.launch(packs=ps)
             else:
-                opt.launch()
+                ops.adam_tick(opt.hyper)
+                ops.adam(ar.flat, ar.grad, ar.exp_avg, ar.exp_avg_sq, opt.hyper)
                 ps.pack()
             assert torch.equal(opt.ticket.cpu(), torch.zeros(2, dtype=torch.int32))
         runs.append([ar.flat.clone(), ar.exp_avg.clone(), ar.exp_avg_sq.clone(), opt.hyper.clone()]
