@@ -97,16 +97,20 @@ __global__ __launch_bounds__(256) void conv_cout1_wave_kernel(ConvArgs a, const 
                                                               const float* __restrict__ w, float* y, Epi ep) {
   extern __shared__ __attribute__((aligned(16))) float Ws[];  // [T][cin]
   const int T = a.k * a.k * a.k;
-  for (int i0 = threadIdx.x; i0 < T * a.cin; i0 += 8 * blockDim.x) {  // 8 loads in flight per thread
+  // weights staged in source order (ci major, taps contiguous when sa == T: coalesced), 8 loads in
+  // flight per thread, transposed into [t][cin] on the LDS side
+  for (int i0 = threadIdx.x; i0 < T * a.cin; i0 += 8 * blockDim.x) {
     float v[8];
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
-      const int i = i0 + u * blockDim.x, t = i / a.cin, ci = i - t * a.cin;
+      const int i = i0 + u * blockDim.x, ci = i / T, t = i - ci * T;
       v[u] = i < T * a.cin ? w[(long long)ci * a.sa + t] : 0.f;
     }
 #pragma unroll
-    for (int u = 0; u < 8; ++u)
-      if (i0 + u * blockDim.x < T * a.cin) Ws[i0 + u * blockDim.x] = v[u];
+    for (int u = 0; u < 8; ++u) {
+      const int i = i0 + u * blockDim.x, ci = i / T, t = i - ci * T;
+      if (i < T * a.cin) Ws[t * a.cin + ci] = v[u];
+    }
   }
   __syncthreads();
   const int lane = threadIdx.x & 63;
@@ -619,9 +623,12 @@ extern "C" int cgan3d_conv3d_wgrad_ex(const cgan3d_conv_geom* g, const float* ga
     const long long R4 = R / 4;
     // one float4 of (tap, channel) accumulators per thread; r4 chunks over blockIdx.y, voxels over x
     const int gy = cg::ceil_div(R4, 256);
+    // voxels per block: >= 8 so that a few hundred outputs (the critic's last layer: 12 x 27) still
+    // spread over ~160 blocks — each block's voxel loop is a chain of dependent L2 round trips
+    // (64 voxels per block: 25.7 us at 64^3 B=4; rocprof, profiles/r02_*)
     long long vpb = (V * gy + 1023) / 1024;
-    if (vpb < 64) vpb = 64;
-    vpb = (vpb + 63) / 64 * 64;
+    if (vpb < 8) vpb = 8;
+    vpb = (vpb + 7) / 8 * 8;
     dim3 grid(cg::ceil_div(V, vpb), gy);
     ::cg::launch((conv_wgrad_cout1_kernel<1>), grid, dim3(256), 0, s, a, gathered, aligned, ws, vpb);
     CG_LAUNCH_CHECK("conv_wgrad_cout1_kernel");

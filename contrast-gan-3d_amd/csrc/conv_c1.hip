@@ -289,7 +289,8 @@ int c1_dgrad_launch(const cgan3d_conv_geom* g, const float* dz, const float* w, 
 int c1_wgrad_launch(const cgan3d_conv_geom* g, const float* x, const float* dz, float* dw, hipStream_t st) {
   C1Args a = c1_args(g);
   const int ntiles = a.n * a.tz * a.ty * a.tx;
-  a.tiles_per_block = std::max(1, std::min(8, ntiles / 256));  // <= ~256 blocks adding into dW
+  // <= ~256 blocks adding into dW (measured: 1024 blocks of one tile each, 36 -> 47 us at 64^3 B=4)
+  a.tiles_per_block = std::max(1, std::min(8, ntiles / 256));
   ::cg::launch(c1_wgrad_kernel, dim3(ceil_div(ntiles, a.tiles_per_block)), dim3(256), 0, st, a, x, dz, dw, ntiles);
   return CGAN3D_OK;
 }
