@@ -58,7 +58,7 @@ class Epilogue(C.Structure):
                 ("act", C.c_int32), ("slope", C.c_float),
                 ("bn_part", C.c_void_p), ("bn_mode", C.c_int32), ("bn_slots", C.c_int32), ("bn_z", C.c_void_p),
                 ("bn_ss", C.c_void_p), ("bn_mi", C.c_void_p), ("bn_act", C.c_int32), ("bn_slope", C.c_float),
-                ("x_bf16", C.c_void_p)]
+                ("x_bf16", C.c_void_p), ("bn_fold", C.c_int32)]
 
 
 _P, _I32, _I64, _F = C.c_void_p, C.c_int32, C.c_int64, C.c_float
@@ -76,6 +76,7 @@ _SIGS = {
     "cgan3d_conv3d_wgrad_ws_floats": ([_P], _I64),
     "cgan3d_conv3d_wgrad": ([_P, _P, _P, _P, _I32, _P, _P], _I32),
     "cgan3d_conv3d_shadow_only": ([_P, _I32], _I32),
+    "cgan3d_conv3d_bn_fold_ok": ([_P], _I32),
     "cgan3d_conv3d_wgrad_ex": ([_P, _P, _P, _P, _I32, _P, _P, _P, _P], _I32),
     "cgan3d_bn_finalize": ([_P, _I64, _I32, _P, _P, _P, _P, _P, _F, _F, _P, _P, _P], _I32),
     "cgan3d_bn_apply": ([_P, _I64, _I32, _P, _I32, _F, _P, _P, _P, _P], _I32),
@@ -86,6 +87,8 @@ _SIGS = {
     "cgan3d_bn_backward_slab": ([_P, _P, _I64, _I32, _P, _I32, _P, _P, _P, _I32, _F, _P, _P, _P, _I32, _P, _P, _P],
                                 _I32),
     "cgan3d_bn_backward_ws_floats": ([_I64, _I32], _I64),
+    "cgan3d_bn_backward_slab_fold": ([_P, _P, _I32, _I32, _I32, _I32, _I32, _I32, _P, _I32, _P, _P, _P, _I32, _F, _P,
+                                      _P, _P, _I32, _P, _P, _P], _I32),
     "cgan3d_bn_backward": ([_P, _P, _I64, _I32, _P, _P, _P, _I32, _F, _P, _P, _P, _I32, _P, _P], _I32),
     "cgan3d_channel_sum_ws_floats": ([_I64, _I32], _I64),
     "cgan3d_channel_sum": ([_P, _I64, _I32, _P, _P, _P], _I32),

@@ -190,6 +190,14 @@ class GeneratorPlan:
         self.slots_b = [ops.bn_slots(self.geo_dgrad[i + 1]) for i in range(len(layers) - 1)]
         self.slots_b.append(ops.reflect_fold_slots(n, la.din, la.cin))
         self.part_b = [torch.empty(2 * ly.cout * sl, device=device) for ly, sl in zip(layers, self.slots_b)]
+        # bf16: the last BatchNorm layer's backward statistics come from the last conv's input-grad
+        # launch itself (folded over the reflect pad) and its elementwise pass folds the padded grid
+        # on the fly — no reflect-fold pass and no fp32 dL/dy of that layer (cgan3d_epilogue.bn_fold)
+        self.fold_bn = (BN_FUSED_BWD and not os.environ.get("CGAN3D_NO_BN_FOLD")
+                        and ops.bn_fold_ok(self.geo_last_dgrad))
+        if self.fold_bn:
+            self.slots_b[-1] = ops.bn_slots(self.geo_last_dgrad)
+            self.part_b[-1] = torch.empty(2 * layers[-1].cout * self.slots_b[-1], device=device)
         self.att = buf(la.dout, 1)
         self.dz_last = buf(la.dout, 1)
         self.dpad = buf(pd, la.cin)
@@ -348,13 +356,24 @@ class GeneratorPlan:
         self._csum[key].run()
         if grads_enqueued is not None:
             grads_enqueued(len(self.layers))
-        ops.conv(self.geo_last_dgrad, self.dz_last, P["model.last_conv.weight"], self.dpad)
-        ops.reflect_fold(self.dpad, self.dy[-1], n, la.din, la.cin, la.p, ep=self._bn_grad_epi(len(self.layers) - 1))
+        if self.fold_bn:
+            ep = self._bn_grad_epi(len(self.layers) - 1)
+            ep.bn_fold = la.p
+            ops.conv(self.geo_last_dgrad, self.dz_last, P["model.last_conv.weight"], self.dpad, ep)
+        else:
+            ops.conv(self.geo_last_dgrad, self.dz_last, P["model.last_conv.weight"], self.dpad)
+            ops.reflect_fold(self.dpad, self.dy[-1], n, la.din, la.cin, la.p,
+                             ep=self._bn_grad_epi(len(self.layers) - 1))
         for i in range(len(self.layers) - 1, -1, -1):
             ly = self.layers[i]
             nb = f"{ly.name}.normalization"
             nvox = n * ly.dout[0] * ly.dout[1] * ly.dout[2]
-            if BN_FUSED_BWD:
+            if BN_FUSED_BWD and self.fold_bn and i == len(self.layers) - 1:
+                ops.bn_backward_slab_fold(self.dpad, self.z[i], n, ly.dout, ly.cout, la.p, self.part_b[i],
+                                          self.slots_b[i], self.ss[i], self.mi[i], P[f"{nb}.weight"], ly.act,
+                                          G[f"{nb}.weight"], G[f"{nb}.bias"], None if self.dz_dead[i] else self.dz[i],
+                                          self.ws, dz16=self.dz16[i])
+            elif BN_FUSED_BWD:
                 ops.bn_backward_slab(self.dy[i], self.z[i], nvox, ly.cout, self.part_b[i], self.slots_b[i],
                                      self.ss[i], self.mi[i], P[f"{nb}.weight"], ly.act, G[f"{nb}.weight"],
                                      G[f"{nb}.bias"], None if self.dz_dead[i] else self.dz[i], self.ws,

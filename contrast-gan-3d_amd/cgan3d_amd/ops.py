@@ -185,7 +185,7 @@ class Epi:
 
     def __init__(self, bias=None, residual=None, mask_src=None, minuend=None, out2=None, stats=None,
                  act=L.ACT_NONE, slope=0.0, bn_part=None, bn_mode=0, bn_slots=0, bn_z=None, bn_ss=None,
-                 bn_mi=None, bn_act=L.ACT_NONE, bn_slope=0.0, x_bf16=None):
+                 bn_mi=None, bn_act=L.ACT_NONE, bn_slope=0.0, x_bf16=None, bn_fold=0):
         self.bias, self.residual, self.mask_src = bias, residual, mask_src
         self.x_bf16 = x_bf16  # bf16 copy of the conv input (ResNet-block kernel halo source)
         self.minuend, self.out2, self.stats = minuend, out2, stats
@@ -194,13 +194,14 @@ class Epi:
         self.bn_part, self.bn_mode, self.bn_slots = bn_part, int(bn_mode), int(bn_slots)
         self.bn_z, self.bn_ss, self.bn_mi = bn_z, bn_ss, bn_mi
         self.bn_act, self.bn_slope = bn_act, float(bn_slope)
+        self.bn_fold = int(bn_fold)  # mode 2 over a reflect-padded k7 input-grad grid (include/cgan3d.h)
 
-    def check_bn(self, nout, c, what):
+    def check_bn(self, nout, c, what, nz=None):
         if not self.bn_mode:
             return
         _need(self.bn_part, (2 * c + (self.bn_mode == 1)) * self.bn_slots, f"{what} bn_part", exact=False)
         if self.bn_mode == 2:
-            _need(self.bn_z, nout, f"{what} bn_z")
+            _need(self.bn_z, nout if nz is None else nz, f"{what} bn_z")
             _need(self.bn_ss, 2 * c, f"{what} bn_ss")
             _need(self.bn_mi, 2 * c, f"{what} bn_mi")
 
@@ -212,6 +213,7 @@ class Epi:
         e.bn_part, e.bn_mode, e.bn_slots, e.bn_z = ptr(self.bn_part), self.bn_mode, self.bn_slots, ptr(self.bn_z)
         e.bn_ss, e.bn_mi, e.bn_act, e.bn_slope = ptr(self.bn_ss), ptr(self.bn_mi), self.bn_act, self.bn_slope
         e.x_bf16 = ptr(self.x_bf16)
+        e.bn_fold = self.bn_fold
         return e
 
 
@@ -383,7 +385,9 @@ def conv(g: ConvGeom, x: torch.Tensor, w: torch.Tensor, y: torch.Tensor, ep: Opt
             _need(ep.stats, stats_floats(g), "conv stats", exact=False)
         if ep.x_bf16 is not None:
             _need(ep.x_bf16, _vox_in(g) * g.cin, "conv x_bf16", dtype=torch.bfloat16)
-        ep.check_bn(ny, g.cout, "conv")
+        f = ep.bn_fold
+        nz = None if not f else g.n * (g.do_ - 2 * f) * (g.ho - 2 * f) * (g.wo - 2 * f) * g.cout
+        ep.check_bn(ny, g.cout, "conv", nz)
     check(_timed("conv", g, "cgan3d_conv3d_fwd", ctypes.byref(g), ptr(x), ptr(w), ptr(y),
                  ctypes.byref(ep.c()) if ep is not None else None), "conv3d_fwd")
 
@@ -412,6 +416,11 @@ def shadow_only(g: ConvGeom, role: int) -> bool:
     """True if, given bf16 shadows, the kernel ``g`` dispatches to reads only them (role 0: conv
     input via ``epilogue(x_bf16=...)``; role 1: weight-gradient operands) — cgan3d_conv3d_shadow_only."""
     return bool(L.load().cgan3d_conv3d_shadow_only(ctypes.byref(g), int(role)))
+
+
+def bn_fold_ok(g: ConvGeom) -> bool:
+    """True if ``g``'s launch takes ``epilogue(bn_fold=...)`` (cgan3d_conv3d_bn_fold_ok)."""
+    return bool(L.load().cgan3d_conv3d_bn_fold_ok(ctypes.byref(g)))
 
 
 def wgrad(g: ConvGeom, gathered, aligned, dw, ws, accumulate=False, gathered16=None, aligned16=None,
@@ -531,6 +540,29 @@ def bn_backward_slab(dy, z, nvox, c, part, nslots, scale_shift, mean_invstd, gam
     check(_launch("cgan3d_bn_backward_slab", ptr(dy), ptr(z), nvox, c, ptr(part), nslots, ptr(scale_shift),
                   ptr(mean_invstd), ptr(gamma), act, slope, ptr(dgamma), ptr(dbeta), ptr(dz), int(accumulate),
                   ptr(ws), _need16(dz16, nvox * c, "bn_backward_slab dz16")), "bn_backward_slab")
+
+
+def bn_backward_slab_fold(padded, z, n, dims: Sequence[int], c, pad, part, nslots, scale_shift, mean_invstd, gamma,
+                          act, dgamma, dbeta, dz, ws, slope=0.0, accumulate=False, dz16=None):
+    """``bn_backward_slab`` with dy = reflect_fold(padded) folded on the fly (cgan3d_bn_backward_slab_fold)."""
+    d, h, w = dims
+    nvox = n * d * h * w
+    _need(padded, n * (d + 2 * pad) * (h + 2 * pad) * (w + 2 * pad) * c, "bn_backward_slab_fold padded")
+    if dz is None and dz16 is None:
+        raise ValueError("bn_backward_slab_fold: dz may be None only when dz16 is given")
+    for t, nm in ((z, "z"), (dz, "dz")):
+        if t is not None:
+            _need(t, nvox * c, f"bn_backward_slab_fold {nm}")
+    _need(part, 2 * c * nslots, "bn_backward_slab_fold part", exact=False)
+    for t, nm in ((scale_shift, "scale_shift"), (mean_invstd, "mean_invstd")):
+        _need(t, 2 * c, f"bn_backward_slab_fold {nm}")
+    for t, nm in ((gamma, "gamma"), (dgamma, "dgamma"), (dbeta, "dbeta")):
+        _need(t, c, f"bn_backward_slab_fold {nm}")
+    _need(ws, 3 * c, "bn_backward_slab_fold ws", exact=False)
+    check(_launch("cgan3d_bn_backward_slab_fold", ptr(padded), ptr(z), n, d, h, w, c, pad, ptr(part), nslots,
+                  ptr(scale_shift), ptr(mean_invstd), ptr(gamma), act, float(slope), ptr(dgamma), ptr(dbeta), ptr(dz),
+                  int(accumulate), ptr(ws), _need16(dz16, nvox * c, "bn_backward_slab_fold dz16")),
+          "bn_backward_slab_fold")
 
 
 def bn_backward_ws_floats(nvox, c) -> int:

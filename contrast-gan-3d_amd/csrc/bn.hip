@@ -204,6 +204,56 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const float* __restri
   }
 }
 
+// bn_bwd_apply_kernel with dy = reflect_fold(padded) gathered on the fly: per voxel the 1..8
+// padded sources that mirror onto it (fold_src), float4 of channels per thread, channels fixed per
+// thread (256 % (C/4) == 0); the bf16 copy (and the fp32 dz when asked) as bn_bwd_apply_kernel.
+__global__ __launch_bounds__(256) void bn_bwd_apply_fold_kernel(const float* __restrict__ padded,
+                                                                const float* __restrict__ z, int n, int D, int H, int W,
+                                                                int P, int C, const float* __restrict__ ss,
+                                                                const float* __restrict__ mi, int act, float slope,
+                                                                const float* __restrict__ coef, float* dz,
+                                                                __bf16* __restrict__ dz16) {
+  const int C4 = C >> 2;
+  const int c = (threadIdx.x % C4) * 4;
+  f32x4 sc, sf, mean, inv, k0, k1, k2;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    sc[e] = ss[c + e]; sf[e] = ss[C + c + e]; mean[e] = mi[c + e]; inv[e] = mi[C + c + e];
+    k0[e] = coef[c + e]; k1[e] = coef[C + c + e]; k2[e] = coef[2 * C + c + e];
+  }
+  const int Dp = D + 2 * P, Hp = H + 2 * P, Wp = W + 2 * P;
+  const long long n4 = (long long)n * D * H * W * C4;
+  const f32x4* z4 = reinterpret_cast<const f32x4*>(z);
+  const f32x4* p4 = reinterpret_cast<const f32x4*>(padded);
+  f32x4* o4 = reinterpret_cast<f32x4*>(dz);
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (long long)gridDim.x * blockDim.x) {
+    long long v = i / C4;
+    const int c4 = (int)(i - v * C4);
+    const int w = (int)(v % W); v /= W;
+    const int h = (int)(v % H); v /= H;
+    const int d = (int)(v % D), nb = (int)(v / D);
+    int qd[2], qh[2], qw[2];
+    const int nd = fold_src(d, D, P, qd), nh = fold_src(h, H, P, qh), nw = fold_src(w, W, P, qw);
+    const f32x4 zz = z4[i];
+    f32x4 dd = p4[(((long long)(nb * Dp + qd[0]) * Hp + qh[0]) * Wp + qw[0]) * C4 + c4];
+    if (nd * nh * nw > 1) {  // boundary voxel: its mirrored sources
+      for (int a = 0; a < nd; ++a)
+        for (int b = 0; b < nh; ++b)
+          for (int e = 0; e < nw; ++e)
+            if (a | b | e) dd += p4[(((long long)(nb * Dp + qd[a]) * Hp + qh[b]) * Wp + qw[e]) * C4 + c4];
+    }
+    f32x4 o;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float g = dd[e] * act_grad(zz[e] * sc[e] + sf[e], act, slope);
+      const float xh = (zz[e] - mean[e]) * inv[e];
+      o[e] = k0[e] * (g - k1[e] - xh * k2[e]);
+    }
+    if (dz) o4[i] = o;
+    if (dz16) store16(dz16, i, o);
+  }
+}
+
 // ---- fused-statistics path: per-block partials written by the producing kernel's epilogue into
 // a channel-major slab part[(q * C + c) * nslots + b] (no atomics); one block per channel reads its
 // contiguous rows (coalesced) and combines them in fp64.
@@ -675,3 +725,27 @@ extern "C" int cgan3d_channel_sum_multi(const cgan3d_csum_desc* descs, int32_t n
   return CGAN3D_OK;
 }
 
+
+extern "C" int cgan3d_bn_backward_slab_fold(const float* padded, const float* z, int32_t n, int32_t d, int32_t h,
+                                            int32_t w, int32_t c, int32_t pad, const float* part, int32_t nslots,
+                                            const float* scale_shift, const float* mean_invstd, const float* gamma,
+                                            int32_t act, float slope, float* dgamma, float* dbeta, float* dz,
+                                            int32_t accumulate, float* ws, void* dz_bf16, void* stream) {
+  CG_CHECK_ARG(padded && z && part && scale_shift && mean_invstd && gamma && (dz || dz_bf16) && ws,
+               "cgan3d_bn_backward_slab_fold: null pointer");
+  CG_CHECK_ARG(n > 0 && nslots > 0 && c >= 4 && c <= 256 && 256 % c == 0 && pad >= 0 && d > 2 * pad && h > 2 * pad &&
+                   w > 2 * pad,
+               "cgan3d_bn_backward_slab_fold: channels must divide 256 (>= 4), dims must exceed 2*pad");
+  const long long nvox = (long long)n * d * h * w;
+  CG_CHECK_ARG(nvox > 1, "cgan3d_bn_backward_slab_fold: need more than one voxel");
+  hipStream_t s = (hipStream_t)stream;
+  ::cg::launch(bn_bwd_finalize_slab_kernel, dim3(c), dim3(256), 0, s, part, nslots, c, (double)nvox, gamma,
+               mean_invstd, dgamma, dbeta, ws, accumulate);
+  CG_LAUNCH_CHECK("bn_bwd_finalize_slab_kernel");
+  const long long n4 = nvox * c / 4;
+  const int blocks = (int)std::min<long long>((n4 + 255) / 256, 4096);
+  ::cg::launch(bn_bwd_apply_fold_kernel, dim3(blocks), dim3(256), 0, s, padded, z, n, d, h, w, pad, c, scale_shift,
+               mean_invstd, act, slope, ws, dz, reinterpret_cast<__bf16*>(dz_bf16));
+  CG_LAUNCH_CHECK("bn_bwd_apply_fold_kernel");
+  return CGAN3D_OK;
+}

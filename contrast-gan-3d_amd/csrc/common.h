@@ -121,6 +121,7 @@ struct Epi {
   int bn_act;
   float bn_slope;
   const __bf16* x16;  // optional bf16 shadow of the conv input
+  int bn_fold;        // mode 2 over a reflect-padded k7 input-grad grid (cgan3d_epilogue.bn_fold)
 };
 
 __device__ __forceinline__ float act_grad(float pre, int act, float slope) {
@@ -149,6 +150,7 @@ void k7s_set(int v);
 int k7_wgrad_handles(const cgan3d_conv_geom* g);
 int k7m_wgrad_taken(const cgan3d_conv_geom* g);
 int k7m_w2n_taken(const cgan3d_conv_geom* g);
+int k7m_fold_ok(const cgan3d_conv_geom* g);
 int k7_try_wgrad(const cgan3d_conv_geom* g, const float* x, const float* go, float* dw, float* ws, hipStream_t s,
                  const __bf16* wide16 = nullptr);
 long long k7_wgrad_ws_floats(const cgan3d_conv_geom* g);
@@ -158,7 +160,7 @@ void k7m_wgrad_launch(const cgan3d_conv_geom* g, bool wide_in, long long wc, con
 long long k7_n2w_blocks(const cgan3d_conv_geom* g);
 long long k7m_n2w_blocks(const cgan3d_conv_geom* g);
 void k7m_n2w_launch(const cgan3d_conv_geom* g, int P, int reflect, int flip, long long wc, const float* x,
-                    const float* w, float* y, float* stats, float* bn_part, hipStream_t s);
+                    const float* w, float* y, float* stats, float* bn_part, hipStream_t s, const Epi* fold = nullptr);
 void k7m_w2n_launch(const cgan3d_conv_geom* g, int P, int reflect, long long wc, const float* x, const float* w,
                     float* y, const Epi& e, hipStream_t s);
 // implicit-GEMM forward / input-grad (conv_gemm.hip)
@@ -267,6 +269,15 @@ __device__ __forceinline__ float adam_elem(const AdamK& k, float* __restrict__ p
   if (k.clip > 0.f) pi = fminf(fmaxf(pi, -k.clip), k.clip);
   p[i] = pi;
   return pi;
+}
+
+// out[i] = sum of padded[q] over the reflect-pad preimages q of interior voxel i
+__device__ __forceinline__ int fold_src(int d, int D, int P, int* q) {  // padded rows mirroring onto d
+  int n = 0;
+  q[n++] = d + P;
+  if (d >= 1 && d <= P) q[n++] = P - d;
+  else if (d <= D - 2 && d >= D - 1 - P) q[n++] = 2 * (D - 1) - d + P;
+  return n;
 }
 
 // slab slot b, channel c, pair member q of a fused BatchNorm slab

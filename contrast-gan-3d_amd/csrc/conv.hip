@@ -422,6 +422,7 @@ static Epi to_epi(const cgan3d_epilogue* ep) {
     e.bn_slots = ep->bn_slots; e.bn_z = ep->bn_z; e.bn_ss = ep->bn_ss; e.bn_mi = ep->bn_mi;
     e.bn_act = ep->bn_act; e.bn_slope = ep->bn_slope;
     e.x16 = reinterpret_cast<const __bf16*>(ep->x_bf16);
+    e.bn_fold = ep->bn_fold;
   }
   return e;
 }
@@ -455,7 +456,11 @@ extern "C" int cgan3d_conv3d_fwd(const cgan3d_conv_geom* g, const float* x, cons
     const long long slots = cgan3d_conv3d_bn_slots(g);
     CG_CHECK_ARG(slots > 0 && slots == e.bn_slots, "cgan3d_conv3d_fwd: bn_slots %d, the launch has %lld", e.bn_slots,
                  slots);
-    CG_CHECK_ARG(!(e.bn_mode == 2 && g->k == 7 && g->cin == 1), "cgan3d_conv3d_fwd: no bn_mode 2 on the k7 path");
+    CG_CHECK_ARG(!(e.bn_mode == 2 && g->k == 7 && g->cin == 1) || (e.bn_fold > 0 && k7m_fold_ok(g)),
+                 "cgan3d_conv3d_fwd: bn_mode 2 on the k7 path only folded (bn_fold) on the bf16 input-grad kernel");
+    CG_CHECK_ARG(e.bn_fold == 0 || (e.bn_mode == 2 && k7m_fold_ok(g) && g->do_ > 4 * e.bn_fold &&
+                                    g->ho > 4 * e.bn_fold && g->wo > 4 * e.bn_fold),
+                 "cgan3d_conv3d_fwd: bn_fold needs bn_mode 2 on a k7 bf16 input-grad geometry");
   }
   hipStream_t s = (hipStream_t)stream;
   CG_CHECK_ARG(!g->w_packed || (g->cout > 1 && !(g->k == 7 && g->stride == 1 && g->cin == 1)),
@@ -536,6 +541,10 @@ static int wgrad_ws_atomic(const cgan3d_conv_geom* g) {
 extern "C" int cgan3d_conv3d_wgrad_ws_mode(const cgan3d_conv_geom* g) {
   if (validate(g, "cgan3d_conv3d_wgrad_ws_mode")) return -1;
   return wgrad_ws_atomic(g);
+}
+
+extern "C" int32_t cgan3d_conv3d_bn_fold_ok(const cgan3d_conv_geom* g) {
+  return g && !validate(g, "cgan3d_conv3d_bn_fold_ok") && k7m_fold_ok(g) ? 1 : 0;
 }
 
 extern "C" int32_t cgan3d_conv3d_shadow_only(const cgan3d_conv_geom* g, int32_t role) {

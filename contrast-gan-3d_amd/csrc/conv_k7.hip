@@ -344,12 +344,13 @@ long long k7_n2w_blocks(const cgan3d_conv_geom* g) {
 int k7_try_fwd(const cgan3d_conv_geom* g, const float* x, const float* w, float* y, const Epi& e,
                hipStream_t s) {
   if (g->k != 7 || g->stride != 1) return 0;
-  if (g->cin == 1 && k7_wide_ok(g->cout) && !e.bias && !e.residual && !e.mask_src && !e.out2 && e.bn_mode != 2 &&
-      e.act == CGAN3D_ACT_NONE) {
+  const bool fold = e.bn_mode == 2 && e.bn_fold > 0;  // folded mode-2 statistics (k7m input-grad only)
+  if (g->cin == 1 && k7_wide_ok(g->cout) && !e.bias && !e.residual && !e.mask_src && !e.out2 &&
+      (e.bn_mode != 2 || (fold && g->transposed && k7m_ok(g, g->cout))) && e.act == CGAN3D_ACT_NONE) {
     if (k7m_ok(g, g->cout)) {
       float* bp = e.bn_mode == 1 ? e.bn_part : nullptr;
       if (!g->transposed) k7m_n2w_launch(g, g->pad, g->reflect, 0, g->w_sb, x, w, y, e.stats, bp, s);
-      else k7m_n2w_launch(g, g->k - 1 - g->pad, 0, 1, g->w_sb, x, w, y, e.stats, bp, s);
+      else k7m_n2w_launch(g, g->k - 1 - g->pad, 0, 1, g->w_sb, x, w, y, e.stats, bp, s, fold ? &e : nullptr);
       return 1;
     }
     K7Args a;
@@ -383,6 +384,11 @@ int k7_try_fwd(const cgan3d_conv_geom* g, const float* x, const float* w, float*
 // shadow of its input it reads only that
 int k7m_w2n_taken(const cgan3d_conv_geom* g) {
   return g->k == 7 && g->stride == 1 && !g->transposed && g->cout == 1 && k7m_ok(g, g->cin);
+}
+
+// 1 if the geometry's forward takes the k7m n2w kernel as an input-grad (folded mode-2 statistics)
+int k7m_fold_ok(const cgan3d_conv_geom* g) {
+  return g->k == 7 && g->stride == 1 && g->transposed && g->cin == 1 && k7m_ok(g, g->cout);
 }
 
 // 1 if k7_try_wgrad takes a bf16 MFMA kernel (k7m_wg_kernel) for the geometry: it then reads the

@@ -55,9 +55,24 @@ constexpr int N_ROWS = N_HD * N_HH;
 constexpr int N_PAIRS = 52;                                 // 49 (td, th) pairs padded to 13 K-steps
 constexpr int N_X = N_ROWS * N_HW, N_X_PER = (N_X + 255) / 256;
 
+// mode-2 BatchNorm statistics of the reflect-folded output (cgan3d_epilogue.bn_fold): the input-grad
+// of the generator's last conv lands on the padded grid, dy = fold(out) on the unpadded one, and
+// sum_v dy(v) a(v) = sum_q out(q) a(refl(q - P)) for the pair weights a = act' (1, xhat) — so the
+// statistics come straight from this kernel's outputs and z at the reflected voxel (no fold pass)
+struct K7Fold {
+  const float* z;   // BatchNorm input on the unpadded grid [n][zd][zh][zw][16]
+  const float* ss;  // [scale | shift]
+  const float* mi;  // [mean | invstd]
+  float* part;      // mode-2 slab, slot = block
+  int act;
+  float slope;
+  int P, zd, zh, zw;
+};
+
 __global__ __launch_bounds__(256, 2) void k7m_n2w_kernel(K7Args a, const float* __restrict__ x,
                                                          const float* __restrict__ w, float* __restrict__ y,
-                                                         float* stats, float* bn_part, int tiles_per_block, int ntiles) {
+                                                         float* stats, float* bn_part, int tiles_per_block, int ntiles,
+                                                         K7Fold fb) {
   constexpr int C = 16;
   __shared__ __attribute__((aligned(16))) __bf16 us[N_ROWS * N_TW * 8];  // [row][ow][8 taps]
   __shared__ __attribute__((aligned(16))) __bf16 xs[N_ROWS * N_HWP];     // [row][24]
@@ -117,6 +132,11 @@ __global__ __launch_bounds__(256, 2) void k7m_n2w_kernel(K7Args a, const float* 
   };
   // running BatchNorm statistics of this block (threads tid < 16, channel tid): Chan merge per tile
   float run_n = 0.f, run_mean = 0.f, run_m2 = 0.f;
+  // folded mode-2 pairs of this lane's channel r16, summed over its outputs of every tile
+  float fp1 = 0.f, fp2 = 0.f, fsc = 0.f, fsh = 0.f, fmean = 0.f, finv = 0.f;
+  if (fb.z) {
+    fsc = fb.ss[r16]; fsh = fb.ss[C + r16]; fmean = fb.mi[r16]; finv = fb.mi[C + r16];
+  }
   const int t0 = blockIdx.x * tiles_per_block, t1 = min(ntiles, t0 + tiles_per_block);
   if (t0 < t1 && !(a.dbg & 4)) load(t0);
   for (int tile = t0; tile < t1; ++tile) {
@@ -177,6 +197,31 @@ __global__ __launch_bounds__(256, 2) void k7m_n2w_kernel(K7Args a, const float* 
         }
       }
     }
+    if (fb.z) {  // every z of the tile's outputs loaded before the first is used
+      const int vd = reflect_idx(od - fb.P, fb.zd);
+      float zv[N_TH][4];
+#pragma unroll
+      for (int r = 0; r < N_TH; ++r) {
+        const int vh = reflect_idx(h0 + r - fb.P, fb.zh);
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) {
+          const int ow = w0 + 4 * g + jj, vw = reflect_idx(ow - fb.P, fb.zw);
+          const bool ok = od < a.do_ && h0 + r < a.ho && ow < a.wo;
+          zv[r][jj] = fb.z[ok ? (((n * fb.zd + vd) * fb.zh + vh) * fb.zw + vw) * C + r16 : 0];
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < N_TH; ++r)
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) {
+          const int ow = w0 + 4 * g + jj;
+          if (od < a.do_ && h0 + r < a.ho && ow < a.wo) {
+            const float gg = acc[r][jj] * act_grad(zv[r][jj] * fsc + fsh, fb.act, fb.slope);
+            fp1 += gg;
+            fp2 += gg * (zv[r][jj] - fmean) * finv;
+          }
+        }
+    }
     if (stats || bn_part) {  // tile (sum, M2 about the tile mean), merged into the block's running statistics
       const int vd = min(N_TD, a.do_ - d0), vh = min(N_TH, a.ho - h0), vw = min(N_TW, a.wo - w0);
       const float tn = (float)(vd * vh * vw);
@@ -221,6 +266,21 @@ __global__ __launch_bounds__(256, 2) void k7m_n2w_kernel(K7Args a, const float* 
     bn_part[(long long)tid * gridDim.x + blockIdx.x] = run_mean * run_n;
     bn_part[(long long)(C + tid) * gridDim.x + blockIdx.x] = run_m2;
     if (tid == 0) bn_part[(long long)2 * C * gridDim.x + blockIdx.x] = run_n;
+  }
+  if (fb.z) {  // folded mode-2 pairs: lanes g -> shuffles, waves -> LDS, into slot blockIdx.x
+    fp1 += __shfl_xor(fp1, 16, 64);
+    fp1 += __shfl_xor(fp1, 32, 64);
+    fp2 += __shfl_xor(fp2, 16, 64);
+    fp2 += __shfl_xor(fp2, 32, 64);
+    __syncthreads();
+    if (g == 0) red[wave][r16] = fp1;
+    __syncthreads();
+    if (tid < C) fb.part[(long long)tid * gridDim.x + blockIdx.x] = red[0][tid] + red[1][tid] + red[2][tid] + red[3][tid];
+    __syncthreads();
+    if (g == 0) red[wave][r16] = fp2;
+    __syncthreads();
+    if (tid < C)
+      fb.part[(long long)(C + tid) * gridDim.x + blockIdx.x] = red[0][tid] + red[1][tid] + red[2][tid] + red[3][tid];
   }
 }
 
@@ -804,11 +864,17 @@ long long k7m_n2w_blocks(const cgan3d_conv_geom* g) {
 }
 
 void k7m_n2w_launch(const cgan3d_conv_geom* g, int P, int reflect, int flip, long long wc, const float* x,
-                    const float* w, float* y, float* stats, float* bn_part, hipStream_t s) {
+                    const float* w, float* y, float* stats, float* bn_part, hipStream_t s, const Epi* fold) {
   const K7Args a = k7m_args(g, P, reflect, flip, wc, N_TD, N_TH, N_TW);
   int grid, per, nt;
   k7m_n2w_split(a, &grid, &per, &nt);
-  ::cg::launch(k7m_n2w_kernel, dim3(grid), dim3(256), 0, s, a, x, w, y, stats, bn_part, per, nt);
+  K7Fold fb{};
+  if (fold) {
+    const int f = fold->bn_fold;
+    fb = K7Fold{fold->bn_z, fold->bn_ss, fold->bn_mi, fold->bn_part, fold->bn_act, fold->bn_slope, f,
+                g->do_ - 2 * f, g->ho - 2 * f, g->wo - 2 * f};
+  }
+  ::cg::launch(k7m_n2w_kernel, dim3(grid), dim3(256), 0, s, a, x, w, y, stats, bn_part, per, nt, fb);
 }
 
 static int g_k7s = 0;  // cgan3d_set_tuning key 13: output planes per streamed-w2n block (0 auto, -1 off)

@@ -17,14 +17,6 @@ void set_error(const char* fmt, ...) {
 
 __global__ void adam_tick_kernel(float* hyper) { hyper[4] += 1.f; }
 
-// out[i] = sum of padded[q] over the reflect-pad preimages q of interior voxel i
-__device__ __forceinline__ int fold_src(int d, int D, int P, int* q) {  // padded rows mirroring onto d
-  int n = 0;
-  q[n++] = d + P;
-  if (d >= 1 && d <= P) q[n++] = P - d;
-  else if (d <= D - 2 && d >= D - 1 - P) q[n++] = 2 * (D - 1) - d + P;
-  return n;
-}
 
 // one thread per (voxel, V channels); 32-bit index math (element count < 2^31)
 template <int V>

@@ -100,6 +100,10 @@ typedef struct cgan3d_epilogue {
   float bn_slope;
   const void* x_bf16;          /* optional bf16 copy of the input x (same layout): the ResNet-block
                                 * kernel stages its halo from it (half the bytes, no conversion) */
+  int32_t bn_fold;             /* mode 2 on the padded output grid of a k7 input-grad (the last
+                                * conv's, generator.py:78-84): the statistics are those of the
+                                * reflect-folded tensor (pad bn_fold), bn_z lives on the unpadded
+                                * grid; see cgan3d_bn_backward_slab_fold.  0 otherwise. */
 } cgan3d_epilogue;
 
 const char* cgan3d_version(void);
@@ -166,6 +170,8 @@ int cgan3d_conv3d_wgrad_ws_mode(const cgan3d_conv_geom* g);
  * with both shadows (ResNet / stride-2 kernels) or, for a k7 conv with a single-channel side, the
  * multi-channel operand's shadow (the bf16 MFMA kernel).  0 otherwise. */
 int32_t cgan3d_conv3d_shadow_only(const cgan3d_conv_geom* g, int32_t role);
+/* 1 when the geometry's launch accepts cgan3d_epilogue.bn_fold (the bf16 k7 input-grad kernel). */
+int32_t cgan3d_conv3d_bn_fold_ok(const cgan3d_conv_geom* g);
 int cgan3d_conv3d_wgrad_ex(const cgan3d_conv_geom* g, const float* gathered, const float* aligned,
                            float* dw, int32_t accumulate, float* ws, const void* gathered_bf16,
                            const void* aligned_bf16, void* stream);
@@ -208,6 +214,15 @@ int cgan3d_bn_backward_slab(const float* dy, const float* z, int64_t nvox, int32
                             const float* gamma, int32_t act, float slope, float* dgamma, float* dbeta,
                             float* dz, int32_t accumulate, float* ws, void* dz_bf16, void* stream);
 int64_t cgan3d_bn_backward_ws_floats(int64_t nvox, int32_t c);
+/* cgan3d_bn_backward_slab whose dy is the reflect fold (pad `pad`, torch "reflect") of `padded`
+ * ([n][d+2pad][h+2pad][w+2pad][c]), folded on the fly — the input-grad of the generator's last conv
+ * (generator.py:78-84) without materialising dy; the slab comes from that conv's launch with
+ * cgan3d_epilogue.bn_fold = pad.  dz may be NULL when dz_bf16 is given. */
+int cgan3d_bn_backward_slab_fold(const float* padded, const float* z, int32_t n, int32_t d, int32_t h, int32_t w,
+                                 int32_t c, int32_t pad, const float* part, int32_t nslots, const float* scale_shift,
+                                 const float* mean_invstd, const float* gamma, int32_t act, float slope,
+                                 float* dgamma, float* dbeta, float* dz, int32_t accumulate, float* ws,
+                                 void* dz_bf16, void* stream);
 
 /* accumulate != 0: dgamma/dbeta += this batch's gradients (a module called on several batches in
  * one step, e.g. the BatchNorm critic on the real and the fake batch, Trainer.py:119-121). */
