@@ -80,7 +80,7 @@ __global__ __launch_bounds__(256, 2) void k7m_n2w_kernel(K7Args a, const float* 
   __shared__ float red[4][C];
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int g = lane >> 4, r16 = lane & 15;
-  k7m_stage<(N_PAIRS * C * 8 + 255) / 256>(
+  if (!(a.dbg & 16)) k7m_stage<(N_PAIRS * C * 8 + 255) / 256>(
       w, N_PAIRS * C * 8,
       [&](int i) -> long long {
         const int tw = i & 7, c = (i >> 3) & 15, p = i >> 7;
@@ -94,6 +94,7 @@ __global__ __launch_bounds__(256, 2) void k7m_n2w_kernel(K7Args a, const float* 
     xs[r * N_HWP + N_HW + 1] = (__bf16)0.f;
   }
   __syncthreads();
+  if (a.dbg & 32) return;
   bf16x8_k bv[N_PAIRS / 4];  // K-step ks: pair 4ks + g, tw 0..7, channel r16
 #pragma unroll
   for (int ks = 0; ks < N_PAIRS / 4; ++ks) bv[ks] = *reinterpret_cast<const bf16x8_k*>(wt + ((4 * ks + g) * C + r16) * 8);

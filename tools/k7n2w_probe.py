@@ -1,7 +1,7 @@
 """Time the generator's first conv (1 -> 16 k7 reflect, mode-1 BatchNorm statistics) and the last
 conv's input-grad (1 -> 16 over the reflect-padded grid, with and without the folded mode-2
 statistics) at 64^3 B=4 alone, under k7m debug switches (cgan3d_set_tuning key 11): 1 no unfold,
-2 no MFMA, 4 no halo loads, 8 no output stores."""
+2 no MFMA, 4 no halo loads, 8 no output stores, 16 no weight staging, 32 exit after it."""
 import sys
 from pathlib import Path
 
@@ -45,7 +45,7 @@ def main():
     mi = torch.rand(2 * C, device="cuda") + 0.5
     ep2 = ops.epilogue(bn_part=part2, bn_mode=2, bn_slots=sl2, bn_z=z, bn_ss=ss, bn_mi=mi, bn_act=L.ACT_RELU,
                        bn_fold=P)
-    for dbg in (0, 1, 2, 4, 8, 15):
+    for dbg in (0, 1, 2, 4, 8, 15, 16, 31, 32):
         L.check(lib.cgan3d_set_tuning(11, dbg), "dbg")
         t1 = timeit(lambda: ops.conv(fwd, x, w, y, ep1))
         t2 = timeit(lambda: ops.conv(dg, g, wl, dpad, ep2))
