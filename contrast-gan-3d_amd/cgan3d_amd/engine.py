@@ -43,6 +43,10 @@ Dims = Tuple[int, int, int]
 BN_FUSED_BWD = os.environ.get("CGAN3D_BN_FUSED_BWD", "1") == "1"
 # weight grads of consecutive ResNet-block layers per cross-stream wait (GeneratorPlan.backward)
 WGRAD_GROUP = max(1, int(os.environ.get("CGAN3D_WGRAD_GROUP", "2")))
+# the generator's first WGRAD_TAIL_MAIN layers (the end of its backward) compute their weight grads
+# on the main stream: nothing is left there to overlap them with, and on the side stream they cost
+# two cross-stream hand-offs and share the chip with the stride-2 input-grad
+WGRAD_TAIL_MAIN = max(0, int(os.environ.get("CGAN3D_WGRAD_TAIL_MAIN", "2")))
 # data parallelism: generator gradient bucket size (all-reduce started per bucket during the backward)
 # (measured on one GPU over a one-rank RCCL group: each extra bucket ~15 us of step time, so the
 # default makes ~2-3 buckets of the 4.1 MB arena: 2.21 ms/step at 1 MB, 2.16 with 2 buckets)
@@ -321,9 +325,12 @@ class GeneratorPlan:
             self.ss[i][c:].copy_(P[f"{nb}.bias"] - P[f"{nb}.running_mean"] * sc)
 
     # -- backward from dz_last = dL/d(pre-tanh) ; writes parameter grads into G (grad views)
-    def _wgrad(self, g, a, b, dw, zeroed: bool, **kw):
+    def _wgrad(self, g, a, b, dw, zeroed: bool, main: bool = False, **kw):
         """Weight gradient on the side stream's workspaces: into a pre-zeroed gradient arena
-        (``zeroed``) every layer accumulates, and the atomic-workspace geometries take the clean one."""
+        (``zeroed``) every layer accumulates, and the atomic-workspace geometries take the clean one.
+        ``main``: launched on the main stream instead, with the main stream's workspace."""
+        if main:
+            return ops.wgrad(g, a, b, dw, self.ws, accumulate=zeroed, **kw)
         if zeroed and ops.wgrad_ws_atomic(g):
             return ops.wgrad(g, a, b, dw, self.ws_clean, accumulate=True, ws_clean=True, **kw)
         return ops.wgrad(g, a, b, dw, self.ws_side, accumulate=zeroed, **kw)
@@ -390,17 +397,30 @@ class GeneratorPlan:
                 x16 = None
             elif x16 is None or d16 is None:
                 x16 = d16 = None
+            main = i < WGRAD_TAIL_MAIN and self.side is not None
             if ly.kind == "convt":  # ConvTranspose3d: the output-grad is the gathered operand
-                pending.append((i, lambda g=self.geo_wgrad[i], a=self.dz[i], b=xin, w=G[wname], a16=d16, b16=x16:
-                                self._wgrad(g, a, b, w, zeroed, gathered16=a16, aligned16=b16)))
+                fn = (lambda g=self.geo_wgrad[i], a=self.dz[i], b=xin, w=G[wname], a16=d16, b16=x16, m=main:
+                      self._wgrad(g, a, b, w, zeroed, main=m, gathered16=a16, aligned16=b16))
             else:
-                pending.append((i, lambda g=self.geo_wgrad[i], a=xin, b=self.dz[i], w=G[wname], a16=x16, b16=d16:
-                                self._wgrad(g, a, b, w, zeroed, gathered16=a16, aligned16=b16)))
+                fn = (lambda g=self.geo_wgrad[i], a=xin, b=self.dz[i], w=G[wname], a16=x16, b16=d16, m=main:
+                      self._wgrad(g, a, b, w, zeroed, main=m, gathered16=a16, aligned16=b16))
+            if main:
+                if pending:
+                    flush()
+                fn()
+                if grads_enqueued is not None:
+                    grads_enqueued(i)
+                if i == 0:
+                    break
+                pending_done = True
+            else:
+                pending.append((i, fn))
+                pending_done = False
             # consecutive ResNet-block layers hand their weight grads to the side stream in groups
             # of WGRAD_GROUP: one cross-stream wait per group (an event record costs the main stream
             # ~4 us, tools/launch_micro.hip) at the price of starting a wgrad one layer later
-            if i == 0 or len(pending) >= WGRAD_GROUP or not (
-                    "resnet_backbone" in ly.name and "resnet_backbone" in self.layers[i - 1].name):
+            if not pending_done and (i == 0 or len(pending) >= WGRAD_GROUP or not (
+                    "resnet_backbone" in ly.name and "resnet_backbone" in self.layers[i - 1].name)):
                 flush()
             if i == 0:
                 break
