@@ -112,6 +112,7 @@ _SIGS = {
     "cgan3d_adam": ([_P, _P, _P, _P, _I64, _P, _P], _I32),
     "cgan3d_adam_pack": ([_P, _P, _P, _P, _I64, _P, _P, _I32, _P, _P], _I32),
     "cgan3d_zero": ([_P, _I64, _P], _I32),
+    "cgan3d_copy_multi": ([_P, _P, _P, _I32, _P], _I32),
     "cgan3d_ln_partial_doubles": ([_I32, _I64], _I64),
     "cgan3d_ln_reduce": ([_P, _P, _P], _I32),
     "cgan3d_ln_apply": ([_P, _P, _P], _I32),

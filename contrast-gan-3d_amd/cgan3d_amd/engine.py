@@ -960,7 +960,17 @@ class StepEngine:
         return self.xc[self.b_opt:self.b_opt + self.b_sub]
 
     def load_inputs(self, opt: torch.Tensor, subopt: torch.Tensor, mask: torch.Tensor, eps: torch.Tensor):
-        """Copy a batch (NCDHW with C=1 == NDHWC) into the engine's resident input slots."""
+        """Copy a batch (NCDHW with C=1 == NDHWC) into the engine's resident input slots: one
+        launch when the operands allow a plain byte copy (fp32 patches and weights, a bool / uint8
+        mask, 16-byte aligned), else one torch copy each."""
+        ins = (opt, subopt, mask, eps)
+        slots = (self.xc[:self.b_opt], self.subopt, self.mask, self.eps)
+        if (all(t.is_cuda and t.is_contiguous() and t.data_ptr() % 16 == 0 and t.numel() == s.numel()
+                for t, s in zip(ins, slots)) and opt.dtype == subopt.dtype == eps.dtype == torch.float32
+                and mask.dtype in (torch.bool, torch.uint8) and not ops.DRY_RUN and not ops.recording()
+                and not os.environ.get("CGAN3D_TORCH_LOAD")):
+            ops.copy_multi(list(zip(ins, slots)))  # a bool mask's bytes are its 0 / 1 uint8 values
+            return
         self.xc[:self.b_opt].view(-1).copy_(opt.reshape(-1), non_blocking=True)
         self.subopt.view(-1).copy_(subopt.reshape(-1), non_blocking=True)
         self.mask.view(-1).copy_(mask.reshape(-1), non_blocking=True)

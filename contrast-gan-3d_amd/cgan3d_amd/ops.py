@@ -412,6 +412,24 @@ def zero(t: torch.Tensor):
     check(_launch("cgan3d_zero", ptr(t), t.numel() * t.element_size()), "zero")
 
 
+def copy_multi(pairs):
+    """``dst.copy_(src)`` for each (src, dst) pair of contiguous device tensors with the same byte
+    size, in one launch (include/cgan3d.h cgan3d_copy_multi; at most 8 pairs, no dtype conversion:
+    the bytes are copied)."""
+    if not 0 < len(pairs) <= 8:
+        raise ValueError("copy_multi: 1..8 pairs")
+    for s, d in pairs:
+        if not (s.is_contiguous() and d.is_contiguous()):
+            raise ValueError("copy_multi: operands must be contiguous")
+        if s.numel() * s.element_size() != d.numel() * d.element_size():
+            raise ValueError("copy_multi: byte sizes differ")
+    n = len(pairs)
+    src = (ctypes.c_void_p * n)(*[s.data_ptr() for s, _ in pairs])
+    dst = (ctypes.c_void_p * n)(*[d.data_ptr() for _, d in pairs])
+    nb = (ctypes.c_int64 * n)(*[s.numel() * s.element_size() for s, _ in pairs])
+    check(_launch("cgan3d_copy_multi", src, dst, nb, n), "copy_multi")
+
+
 def shadow_only(g: ConvGeom, role: int) -> bool:
     """True if, given bf16 shadows, the kernel ``g`` dispatches to reads only them (role 0: conv
     input via ``epilogue(x_bf16=...)``; role 1: weight-gradient operands) — cgan3d_conv3d_shadow_only."""

@@ -207,6 +207,57 @@ extern "C" int cgan3d_gp_interpolate(const float* real, const float* fake, const
   return CGAN3D_OK;
 }
 
+// Several device-to-device copies in one launch (a batch into the engine's input slots: the
+// OPT / subopt patches, the segmentation mask, the GP interpolation weights).  Work unit = one
+// 16-byte vector of a segment; a segment's tail (bytes % 16, or all of it when src/dst are not
+// 16-byte aligned) is the extra last unit, copied bytewise by its thread.
+namespace cg {
+constexpr int COPY_SEGS = 8;
+struct CopySegs {
+  const unsigned char* src[COPY_SEGS];
+  unsigned char* dst[COPY_SEGS];
+  long long bytes[COPY_SEGS], n16[COPY_SEGS], start[COPY_SEGS + 1];
+  int n;
+};
+
+__global__ __launch_bounds__(256) void copy_multi_kernel(CopySegs c) {
+  const long long total = c.start[c.n];
+  for (long long u = (long long)blockIdx.x * 256 + threadIdx.x; u < total; u += (long long)gridDim.x * 256) {
+    int s = 0;
+    while (s + 1 < c.n && u >= c.start[s + 1]) ++s;
+    const long long k = u - c.start[s];
+    if (k < c.n16[s]) {
+      reinterpret_cast<uint4*>(c.dst[s])[k] = reinterpret_cast<const uint4*>(c.src[s])[k];
+    } else {
+      for (long long b = c.n16[s] * 16; b < c.bytes[s]; ++b) c.dst[s][b] = c.src[s][b];
+    }
+  }
+}
+}  // namespace cg
+
+extern "C" int cgan3d_copy_multi(const void* const* src, void* const* dst, const int64_t* bytes, int32_t n,
+                                 void* stream) {
+  CG_CHECK_ARG(src && dst && bytes && n > 0 && n <= ::cg::COPY_SEGS, "cgan3d_copy_multi: bad args");
+  ::cg::CopySegs c{};
+  c.n = n;
+  c.start[0] = 0;
+  for (int s = 0; s < n; ++s) {
+    CG_CHECK_ARG(src[s] && dst[s] && bytes[s] >= 0, "cgan3d_copy_multi: bad segment");
+    c.src[s] = static_cast<const unsigned char*>(src[s]);
+    c.dst[s] = static_cast<unsigned char*>(dst[s]);
+    c.bytes[s] = bytes[s];
+    const bool aligned = !(reinterpret_cast<uintptr_t>(src[s]) & 15) && !(reinterpret_cast<uintptr_t>(dst[s]) & 15);
+    c.n16[s] = aligned ? bytes[s] / 16 : 0;
+    CG_CHECK_ARG(bytes[s] - c.n16[s] * 16 <= 4096, "cgan3d_copy_multi: unaligned segment over 4 KB");
+    c.start[s + 1] = c.start[s] + c.n16[s] + (bytes[s] > c.n16[s] * 16 ? 1 : 0);
+  }
+  const long long total = c.start[n];
+  if (total == 0) return CGAN3D_OK;
+  const unsigned blocks = (unsigned)std::min<long long>((total + 255) / 256, 2048);
+  ::cg::launch(::cg::copy_multi_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, c);
+  return CGAN3D_OK;
+}
+
 // Zero `bytes` bytes at p (a gradient arena before an update): a memset recorded in launch plans.
 extern "C" int cgan3d_zero(void* p, int64_t bytes, void* stream) {
   CG_CHECK_ARG(p && bytes > 0, "cgan3d_zero: bad args");

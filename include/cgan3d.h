@@ -309,6 +309,10 @@ int cgan3d_adam_tick(float* hyper, void* stream);
  * whole gradient arena once per update and then accumulates every layer's weight gradient
  * (CGAN3D_WGRAD_ACCUMULATE) — Trainer.py:109,146 optimizer.zero_grad. */
 int cgan3d_zero(void* p, int64_t bytes, void* stream);
+/* n <= 8 device-to-device copies of bytes[i] bytes from src[i] to dst[i] in one launch (host
+ * arrays; a batch into the step's input slots).  Segments whose src or dst is not 16-byte aligned
+ * are copied bytewise and limited to 4 KB (CGAN3D_EINVAL beyond). */
+int cgan3d_copy_multi(const void* const* src, void* const* dst, const int64_t* bytes, int32_t n, void* stream);
 
 /* LayerNorm critic (experiments/gp_layernorm.py:9-11, model/blocks.py:40-45): per-sample
  * normalisation over (C, D, H, W) — one contiguous run of L floats per sample in NDHWC — without

@@ -640,3 +640,41 @@ def test_adam_pack_matches_separate_launches():
     assert float(runs[1][3][4]) == 3.0
     for j, (a, b) in enumerate(zip(*runs)):
         assert torch.equal(a, b), f"output {j}"
+
+
+def test_copy_multi_and_batch_load():
+    """cgan3d_copy_multi: vector body, byte tails, an unaligned small segment, a bool mask copied into
+    uint8 bytes; and StepEngine.load_inputs' one-launch path fills the slots like torch copies."""
+    from cgan3d_amd import ops
+    g = torch.Generator(device="cpu").manual_seed(5)
+    a = torch.randn(1000003, generator=g).cuda()
+    b = torch.randint(0, 2, (777,), generator=g).bool().cuda()
+    base = torch.randn(64, generator=g).cuda()
+    c = base[1:6]  # 4-byte aligned only: bytewise segment
+    da, db, dc = torch.empty_like(a), torch.empty(777, dtype=torch.uint8, device="cuda"), torch.empty(5, device="cuda")
+    ops.copy_multi([(a, da), (b, db), (c, dc)])
+    torch.cuda.synchronize()
+    assert torch.equal(da, a) and torch.equal(db, b.to(torch.uint8)) and torch.equal(dc, c)
+    with pytest.raises(ValueError):
+        ops.copy_multi([(a, db)])
+    # the engine's batch load: one launch for a bool mask, the torch copies for a float one
+    from cgan3d_amd.data.synthetic import synth_patches
+    from cgan3d_amd.engine import StepEngine
+    from cgan3d_amd.model.discriminator import PatchGANDiscriminator
+    from cgan3d_amd.model.generator import ResnetGenerator
+    from torch import nn
+    S, n = 32, 2
+    opt, _ = synth_patches(n, S, 3)
+    sub, seg = synth_patches(n, S, 4)
+    gm = ResnetGenerator(4, 2, 16).cuda()
+    dm = PatchGANDiscriminator(1, 8, 3, negative_slope=0.2, norm_layer=nn.Identity).cuda()
+    eng = StepEngine(gm, dm, gm.config, dm.config, n, n, (S, S, S))
+    eps = torch.rand(n, device="cuda")
+    for m in (torch.from_numpy(seg).cuda(), torch.from_numpy(seg).cuda().float()):
+        eng.xc.zero_(), eng.subopt.zero_(), eng.mask.zero_(), eng.eps.zero_()
+        eng.load_inputs(torch.from_numpy(opt).cuda(), torch.from_numpy(sub).cuda(), m, eps)
+        torch.cuda.synchronize()
+        assert torch.equal(eng.xc[:n].cpu().reshape(-1), torch.from_numpy(opt).reshape(-1))
+        assert torch.equal(eng.subopt.cpu().reshape(-1), torch.from_numpy(sub).reshape(-1))
+        assert torch.equal(eng.mask.cpu().reshape(-1), torch.from_numpy(seg).reshape(-1).to(torch.uint8))
+        assert torch.equal(eng.eps.cpu(), eps.cpu())
