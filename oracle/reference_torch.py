@@ -135,10 +135,26 @@ class _GradToBf16(torch.autograd.Function):
         return _bf16(g)
 
 
+_COLS_MAX = 1 << 30
+
+
+def _conv3d_cpu(x: Tensor, w: Tensor, b: Optional[Tensor], **kw) -> Tensor:
+    """F.conv3d; on the CPU a stride-1 unpadded conv whose unfolded operand (Cin k^3 x output
+    voxels) would pass 2^30 elements — the generator's 16 -> 1 k7 conv at 128^3 is 11.5 G, a 92 GB
+    float64 buffer past int32 indexing — runs over slabs of output depth instead (same sums)."""
+    k = w.shape[2]
+    do = x.shape[2] - k + 1
+    cols = w.shape[1] * k ** 3 * x.shape[0] * do * (x.shape[3] - k + 1) * (x.shape[4] - k + 1)
+    if kw or x.is_cuda or cols <= _COLS_MAX:
+        return F.conv3d(x, w, b, **kw)
+    per = max(1, do * _COLS_MAX // cols)
+    return torch.cat([F.conv3d(x[:, :, d0:min(do, d0 + per) + k - 1], w, b) for d0 in range(0, do, per)], dim=2)
+
+
 def _conv3d(x: Tensor, w: Tensor, b: Optional[Tensor] = None, rounded: bool = True, **kw) -> Tensor:
     if not (BF16_OPERANDS and rounded):
-        return F.conv3d(x, w, b, **kw)
-    return _GradToBf16.apply(F.conv3d(_bf16(x), _bf16(w), b, **kw))
+        return _conv3d_cpu(x, w, b, **kw)
+    return _GradToBf16.apply(_conv3d_cpu(_bf16(x), _bf16(w), b, **kw))
 
 
 def _conv_transpose3d(x: Tensor, w: Tensor, **kw) -> Tensor:
