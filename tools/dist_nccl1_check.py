@@ -2,7 +2,10 @@
 runs the bucketed generator all-reduces (communication stream ordered after the main and side
 streams, async RCCL all-reduce per bucket from plan host callables, wait before Adam) and the
 critic all-reduce.  Over one rank the mean is the identity, so three plan-replayed steps must match
-an engine without collectives (up to weight-gradient atomics order).
+an engine without collectives (up to weight-gradient atomics order).  Each compared step starts
+from the same state (the reference engine's weights, Adam moments and BatchNorm buffers copied in
+place): with beta1 = 0 Adam turns a last-bit gradient difference into a whole step of the other
+sign, so free-running replicas drift apart over a few steps whatever the collectives do.
 
     python tools/dist_nccl1_check.py
 """
@@ -16,6 +19,20 @@ sys.path.insert(0, str(REPO / "contrast-gan-3d_amd"))
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 from torch import nn  # noqa: E402
+
+
+def sync_state(src, dst):
+    """src's trained state into dst's resident buffers, in place (recorded plans keep addresses)."""
+    with torch.no_grad():
+        for a, b in ((src.g_arena, dst.g_arena), (src.d_arena, dst.d_arena)):
+            for t1, t2 in ((a.flat, b.flat), (a.exp_avg, b.exp_avg), (a.exp_avg_sq, b.exp_avg_sq)):
+                t2.copy_(t1)
+        for P1, P2 in ((src.gP, dst.gP), (src.dP, dst.dP)):
+            for k, v in P1.items():
+                if k.endswith(("running_mean", "running_var", "num_batches_tracked")):
+                    P2[k].copy_(v)
+    dst.G.pack()
+    dst.D.pack()
 
 
 def main():
@@ -49,6 +66,7 @@ def main():
     hosts = sum(1 for it in plans[0].items if not isinstance(it, int))
     assert hosts == len(dp.g_buckets) + 2, hosts
     for _ in range(3):
+        sync_state(ref, dp)
         for e in engs:
             e.load_inputs(*inputs)
             e.run_plan()
