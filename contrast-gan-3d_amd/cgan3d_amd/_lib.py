@@ -16,7 +16,7 @@ import torch  # noqa: F401  (must be imported first: see module docstring)
 LIB_PATH = Path(__file__).resolve().parent / "libcgan3d.so"
 
 ACT_NONE, ACT_RELU, ACT_LRELU, ACT_TANH = 0, 1, 2, 3
-WGRAD_ACCUMULATE, WGRAD_WS_CLEAN = 1, 2  # cgan3d_conv3d_wgrad_ex flag word
+WGRAD_ACCUMULATE, WGRAD_WS_CLEAN, WGRAD_DEFER_UNPACK = 1, 2, 4  # cgan3d_conv3d_wgrad_ex flag word
 # device loss slots written by the loss kernels (include/cgan3d.h)
 L_D, L_WD, L_GP, L_G, L_SIM, L_HU, L_GFULL = range(7)
 
@@ -27,6 +27,11 @@ class ConvGeom(C.Structure):
                 ("cin", C.c_int32), ("cout", C.c_int32), ("k", C.c_int32), ("stride", C.c_int32),
                 ("pad", C.c_int32), ("transposed", C.c_int32), ("reflect", C.c_int32),
                 ("w_sa", C.c_int64), ("w_sb", C.c_int64), ("w_packed", C.c_int32), ("prec", C.c_int32)]
+
+
+class UnpackDesc(C.Structure):
+    _fields_ = [("ws", C.c_void_p), ("dw", C.c_void_p), ("sa", C.c_int64), ("sb", C.c_int64),
+                ("taps", C.c_int32), ("cin", C.c_int32), ("cout", C.c_int32), ("accumulate", C.c_int32)]
 
 
 class PackDesc(C.Structure):
@@ -113,6 +118,7 @@ _SIGS = {
     "cgan3d_adam_pack": ([_P, _P, _P, _P, _I64, _P, _P, _I32, _P, _P], _I32),
     "cgan3d_zero": ([_P, _I64, _P], _I32),
     "cgan3d_copy_multi": ([_P, _P, _P, _I32, _P], _I32),
+    "cgan3d_wgrad_unpack_multi": ([_P, _I32, _I64, _P], _I32),
     "cgan3d_ln_partial_doubles": ([_I32, _I64], _I64),
     "cgan3d_ln_reduce": ([_P, _P, _P], _I32),
     "cgan3d_ln_apply": ([_P, _P, _P], _I32),

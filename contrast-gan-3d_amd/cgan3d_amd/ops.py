@@ -442,16 +442,20 @@ def bn_fold_ok(g: ConvGeom) -> bool:
 
 
 def wgrad(g: ConvGeom, gathered, aligned, dw, ws, accumulate=False, gathered16=None, aligned16=None,
-          ws_clean=False):
+          ws_clean=False, defer_unpack=False):
     """Weight gradient; ``gathered16`` / ``aligned16``: optional bf16 shadows of the operands.
-    ``ws_clean``: ``ws`` is all-zero and is left all-zero (geometries with ``wgrad_ws_atomic``)."""
+    ``ws_clean``: ``ws`` is all-zero and is left all-zero (geometries with ``wgrad_ws_atomic``).
+    ``defer_unpack`` (with ``ws_clean``): the result stays in ``ws`` until an ``UnpackSet`` run."""
+    if defer_unpack and not ws_clean:
+        raise ValueError("wgrad: defer_unpack needs ws_clean")
     _need(gathered, _vox_in(g) * g.cin, "wgrad gathered")
     _need(aligned, _vox_out(g) * g.cout, "wgrad aligned")
     _need(dw, g.cin * g.cout * g.k**3, "wgrad dw")
     if _w_extent(g) > dw.numel():
         raise ValueError("wgrad: weight strides exceed dw")
     _need(ws, wgrad_ws_floats(g), "wgrad ws", exact=False)
-    flags = (L.WGRAD_ACCUMULATE if accumulate else 0) | (L.WGRAD_WS_CLEAN if ws_clean else 0)
+    flags = ((L.WGRAD_ACCUMULATE if accumulate else 0) | (L.WGRAD_WS_CLEAN if ws_clean else 0)
+             | (L.WGRAD_DEFER_UNPACK if defer_unpack else 0))
     check(_timed("wgrad", g, "cgan3d_conv3d_wgrad_ex", ctypes.byref(g), ptr(gathered), ptr(aligned), ptr(dw),
                  flags, ptr(ws), _need16(gathered16, _vox_in(g) * g.cin, "wgrad gathered16"),
                  _need16(aligned16, _vox_out(g) * g.cout, "wgrad aligned16")), "conv3d_wgrad")
@@ -609,6 +613,31 @@ def channel_sum(x, nvox, c, out, ws):
     _need(out, c, "channel_sum out")
     _need(ws, channel_sum_ws_floats(nvox, c), "channel_sum ws", exact=False)
     check(_launch("cgan3d_channel_sum", ptr(x), nvox, c, ptr(out), ptr(ws)), "channel_sum")
+
+
+class UnpackSet:
+    """Several deferred weight gradients (``wgrad(..., defer_unpack=True)``) moved from their packed
+    workspaces into dW in one launch (cgan3d_wgrad_unpack_multi), the workspaces re-zeroed.  Built
+    once per (workspaces, gradient views); the descriptors live on the device."""
+
+    def __init__(self, device, items):
+        """items: [(geometry, ws, dw, accumulate)]; every ws / dw keeps its address."""
+        descs, self.keep = [], []
+        for g, ws, dw, acc in items:
+            t = g.k ** 3
+            _need(ws, t * g.cin * g.cout, "UnpackSet ws", exact=False)
+            _need(dw, g.cin * g.cout * t, "UnpackSet dw")
+            d = L.UnpackDesc()
+            d.ws, d.dw, d.sa, d.sb = ptr(ws), ptr(dw), g.w_sa, g.w_sb
+            d.taps, d.cin, d.cout, d.accumulate = t, g.cin, g.cout, int(acc)
+            descs.append(d)
+            self.keep += [ws, dw]
+        self.n = len(descs)
+        self.max_total = max(g.k ** 3 * g.cin * g.cout for g, _, _, _ in items)
+        self.dev = torch.frombuffer(bytearray(b"".join(bytes(d) for d in descs)), dtype=torch.uint8).to(device)
+
+    def run(self):
+        check(_launch("cgan3d_wgrad_unpack_multi", ptr(self.dev), self.n, self.max_total), "wgrad_unpack_multi")
 
 
 class ChannelSumSet:

@@ -409,6 +409,21 @@ __global__ void wgrad_unpack_kernel(float* __restrict__ dwp, float* dw, int T, i
   if (clean) dwp[i] = 0.f;
 }
 
+// the same for several weight gradients in one launch (blockIdx.y = descriptor); always clean
+__global__ __launch_bounds__(256) void wgrad_unpack_multi_kernel(const cgan3d_unpack_desc* __restrict__ descs) {
+  const cgan3d_unpack_desc d = descs[blockIdx.y];
+  const long long total = (long long)d.taps * d.cin * d.cout;
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long long)gridDim.x * 256) {
+    const int b = (int)(i % d.cout);
+    const long long r = i / d.cout;
+    const int ca = (int)(r % d.cin), t = (int)(r / d.cin);
+    float* o = d.dw + ca * d.sa + b * d.sb + t;
+    const float v = d.ws[i];
+    *o = d.accumulate ? *o + v : v;
+    d.ws[i] = 0.f;
+  }
+}
+
 }  // namespace cg
 
 using namespace cg;
@@ -562,8 +577,14 @@ extern "C" int cgan3d_conv3d_wgrad_ex(const cgan3d_conv_geom* g, const float* ga
                                       const void* aligned_bf16, void* stream) {
   int st = validate(g, "cgan3d_conv3d_wgrad");
   if (st) return st;
-  CG_CHECK_ARG((accumulate & ~3) == 0, "cgan3d_conv3d_wgrad: flags are CGAN3D_WGRAD_ACCUMULATE | CGAN3D_WGRAD_WS_CLEAN");
+  CG_CHECK_ARG((accumulate & ~7) == 0,
+               "cgan3d_conv3d_wgrad: flags are CGAN3D_WGRAD_ACCUMULATE | CGAN3D_WGRAD_WS_CLEAN | "
+               "CGAN3D_WGRAD_DEFER_UNPACK");
   const bool ws_clean = (accumulate & CGAN3D_WGRAD_WS_CLEAN) != 0;
+  const bool defer = (accumulate & CGAN3D_WGRAD_DEFER_UNPACK) != 0;
+  CG_CHECK_ARG(!defer || (ws_clean && wgrad_ws_atomic(g)),
+               "cgan3d_conv3d_wgrad: CGAN3D_WGRAD_DEFER_UNPACK needs CGAN3D_WGRAD_WS_CLEAN on an atomic-workspace "
+               "geometry");
   accumulate &= CGAN3D_WGRAD_ACCUMULATE;
   CG_CHECK_ARG(!ws_clean || wgrad_ws_atomic(g),
                "cgan3d_conv3d_wgrad: CGAN3D_WGRAD_WS_CLEAN on a geometry whose workspace is not atomic "
@@ -660,9 +681,19 @@ extern "C" int cgan3d_conv3d_wgrad_ex(const cgan3d_conv_geom* g, const float* ga
 #undef CG_LAUNCH_WG
     CG_LAUNCH_CHECK("conv_wgrad_kernel");
   }
+  if (defer) return CGAN3D_OK;  // the caller's cgan3d_wgrad_unpack_multi moves it into dw
   const long long total = R * g->cout;
   ::cg::launch(wgrad_unpack_kernel, dim3(cg::ceil_div(total, 256)), dim3(256), 0, s, ws, dw, T, g->cin, g->cout,
                      (long long)g->w_sa, (long long)g->w_sb, accumulate, (int)ws_clean);
   CG_LAUNCH_CHECK("wgrad_unpack_kernel");
+  return CGAN3D_OK;
+}
+
+extern "C" int cgan3d_wgrad_unpack_multi(const cgan3d_unpack_desc* descs, int32_t n, int64_t max_total, void* stream) {
+  CG_CHECK_ARG(descs && n > 0 && n <= 65535 && max_total > 0,
+               "cgan3d_wgrad_unpack_multi: need a device descriptor array, 0 < n <= 65535, max_total > 0");
+  const unsigned bx = (unsigned)std::min<long long>((max_total + 255) / 256, 1024);
+  ::cg::launch(wgrad_unpack_multi_kernel, dim3(bx, n), dim3(256), 0, (hipStream_t)stream, descs);
+  CG_LAUNCH_CHECK("wgrad_unpack_multi_kernel");
   return CGAN3D_OK;
 }

@@ -161,6 +161,18 @@ int cgan3d_conv3d_wgrad(const cgan3d_conv_geom* g, const float* gathered, const 
  * all-zero again (no per-layer memset of ws; the workspace must then be used by clean calls only). */
 #define CGAN3D_WGRAD_ACCUMULATE 1
 #define CGAN3D_WGRAD_WS_CLEAN 2
+/* with CGAN3D_WGRAD_WS_CLEAN on an atomic-workspace geometry: leave the result in the packed
+ * workspace ([tap][a][b]); the caller later moves it into dw, and re-zeroes the workspace, with
+ * cgan3d_wgrad_unpack_multi — one launch for a whole network's weight gradients */
+#define CGAN3D_WGRAD_DEFER_UNPACK 4
+typedef struct cgan3d_unpack_desc {
+  float* ws;     /* packed [tap][a][b] workspace of one deferred weight gradient (left zeroed) */
+  float* dw;     /* dw[a*sa + b*sb + tap] (+)= ws[(tap*cin + a)*cout + b] */
+  int64_t sa, sb;
+  int32_t taps, cin, cout, accumulate;
+} cgan3d_unpack_desc;
+/* `descs`: a DEVICE array of n descriptors; max_total = the largest taps*cin*cout among them */
+int cgan3d_wgrad_unpack_multi(const cgan3d_unpack_desc* descs, int32_t n, int64_t max_total, void* stream);
 /* 1 if the weight gradient of `g` sums into its workspace by atomics (the geometries that may take
  * CGAN3D_WGRAD_WS_CLEAN), 0 if not, -1 on an invalid geometry. */
 int cgan3d_conv3d_wgrad_ws_mode(const cgan3d_conv_geom* g);
