@@ -36,6 +36,9 @@ from pathlib import Path
 # with HIP's default of 4 some of them share an in-order hardware queue, where one stream's
 # cross-stream wait blocks the other's kernels (measured on one GPU, one-rank RCCL path: 2.56 ms/step
 # at 4 queues, 2.21 at 8, 2.21 at 16; 2.06 without collectives at either setting)
+# (the package raises it the same way at import, cgan3d_amd/__init__.py, so the Trainer path gets
+# the same queues; the setting in force is reported in the JSON line as config.hw_queues)
+HW_QUEUES_ENV = os.environ.get("GPU_MAX_HW_QUEUES")
 if int(os.environ.get("GPU_MAX_HW_QUEUES", "4")) < 8:
     os.environ["GPU_MAX_HW_QUEUES"] = "8"
 
@@ -188,8 +191,8 @@ def bench_trainer(args, S, B, dev, world, rank, dist, batches):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--size", type=int, default=64)
     ap.add_argument("--batch", type=int, default=4)
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
@@ -293,7 +296,11 @@ def main():
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
+    # per-step boundaries: an event on the main stream after each step (every step ends with the
+    # main stream waiting for the side stream), read after the timed region -> median step time
+    marks = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
     t0 = time.perf_counter()
+    marks[0].record()
     for i in range(args.steps):
         if mode == "graph":
             graph_step(i)
@@ -301,11 +308,13 @@ def main():
             plan_step(i)
         else:
             one_step(i, False)
+        marks[i + 1].record()
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
+    step_ms = np.array([marks[i].elapsed_time(marks[i + 1]) for i in range(args.steps)])
     # the roofline kernel's launch time: after the timed region, eager steps in which each of its
     # launches is followed by `reps` back-to-back repeats between two HIP events on its stream
     # (repeats keep the queue full, so host launch gaps stay out of the measurement)
@@ -371,7 +380,11 @@ def main():
         "data": "synthetic",
         "config": {"workload": f"{S}^3 patches, {B} OPT + {B} LOW/HIGH per GPU, full G+D step (WGAN-GP conf)",
                    "global_batch": world * B, "patch": S, "parallelism": f"dp{world}",
-                   "launch_mode": mode},
+                   "launch_mode": mode, "hw_queues": int(os.environ["GPU_MAX_HW_QUEUES"]),
+                   "hw_queues_env": HW_QUEUES_ENV},
+        "step_ms": {"median": round(float(np.median(step_ms)), 4), "p10": round(float(np.percentile(step_ms, 10)), 4),
+                    "p90": round(float(np.percentile(step_ms, 90)), 4), "steps": int(args.steps),
+                    "timing": "HIP events on the main stream between consecutive timed steps"},
         "roofline": {"kernel": roof_desc, "bound": "mfma", "achieved": round(achieved, 3), "peak": peak,
                      "unit": "TFLOP/s", "frac": round(achieved / peak, 4),
                      "traffic": pmc_traffic(roof_pmc, S, B, args.precision), "traffic_source": roof_pmc,

@@ -114,7 +114,9 @@ class SpatialTransform_2:  # noqa: N801 (batchgenerators' name)
             slot, mags, modified = -1, np.zeros(3), False
             dec = {}
             decisions.append(dec)
-            if self.do_elastic_deform and rng.uniform() < self.p_el_per_sample:
+            # augment_spatial_2 evaluates `uniform() < p_el_per_sample and do_elastic_deform`: the
+            # draw happens even with elastic deformation off, which keeps the later draws in place
+            if rng.uniform() < self.p_el_per_sample and self.do_elastic_deform:
                 def_scale = _uniform(rng, *self.deformation_scale)
                 sig = [def_scale * p for p in ps]
                 mags = np.array([_uniform(rng, sg / 8.0, sg / 2.0) for sg in sig])

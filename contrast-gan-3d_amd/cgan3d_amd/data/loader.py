@@ -22,8 +22,10 @@ Per batch:
 
 * spatial augmentation (optional ``transform``, ``data/augment.py``: batchgenerators'
   ``SpatialTransform_2`` as ``basic_conf.py:87-113`` configures it): the per-sample parameters
-  are drawn on the host with the crop boxes, the elastic noise fields by the host worker, and
-  ``cgan3d_spatial_augment`` resamples the unpacked batch on the loader stream.
+  and the elastic noise fields are drawn on the host with the crop boxes, under the loader's lock
+  from its one generator (a single random stream, as batchgenerators draws per batch); the host
+  worker pins them for the async copy, and ``cgan3d_spatial_augment`` resamples the unpacked batch
+  on the loader stream.
 """
 from __future__ import annotations
 

@@ -3,8 +3,15 @@
 
 ``correct_scan_3D`` (reference :60-81) tiles the scan with patchly's ``GridSampler`` (step = patch,
 squeeze mode: the last patch of a dim is moved back to end at the border, overlapping its
-neighbour), runs ``patch - G(patch)`` on scaled patches in eval mode, and averages overlapping
-outputs with patchly's ``Aggregator``.  patchly is a dependency of the reference outside its tree
+neighbour), runs ``patch - G(patch)`` on scaled patches, and averages overlapping outputs with
+patchly's ``Aggregator``.
+
+BatchNorm mode.  The reference never calls ``model.eval()`` (reference :33-38): its generator stays in
+train mode, so every batch of tiles is normalised with ITS OWN batch statistics and every batch
+updates the running buffers (momentum 0.1) — the output of a tile depends on the other tiles of its
+batch.  This is the default here too (same C-order batching of the grid, same ``batch_size``).
+``eval_mode=True`` is a build-only option (not in the reference): running statistics, batch
+independent, buffers untouched.  patchly is a dependency of the reference outside its tree
 (not installed here); its grid and averaging are restated here: ``grid_origins`` on the host, the
 patch accumulation and the average in HIP (``cgan3d_patch_accumulate`` / ``cgan3d_patch_normalize``),
 the generator on the HIP kernels.  The 2-D path (``correct_scan_2D``) belongs to the 2-D variants
@@ -47,13 +54,17 @@ class CCTAContrastCorrector:
     inference_patch_size: Optional[Sequence[int]] = None
     checkpoint_path: Optional[Path] = None
     upsampler: Callable[[Tensor], Tensor] = field(init=False, default=None)
+    eval_mode: bool = False  # build-only option: eval-mode BatchNorm (see the module docstring)
 
     def __post_init__(self):
         self.model: nn.Module = self.model()
         if self.checkpoint_path is not None:
             self.load_model(self.checkpoint_path)
         self.device = torch.device(self.device)
-        self.model = self.model.to(self.device).eval()
+        # the reference leaves the module in its default train mode (reference :33-38)
+        self.model = self.model.to(self.device)
+        if self.eval_mode:
+            self.model.eval()
         if self.inference_patch_size is None or len(self.inference_patch_size) < 3:
             raise NotImplementedError("CCTAContrastCorrector: the 2-D path is SURVEY.md §8f row 4")
         self.inference_patch_size = tuple(int(p) for p in self.inference_patch_size)

@@ -44,22 +44,6 @@ class _LossFn(torch.autograd.Function):
         return g * grad, None, None
 
 
-class StableStd(torch.autograd.Function):
-    """``torch.std`` with the reference's gradient ``2/(n-1) * g/(2 std + 1e-6) * (x - mean)``."""
-
-    @staticmethod
-    def forward(ctx, tensor: Tensor) -> Tensor:
-        ctx.tensor = tensor.detach()
-        res = torch.std(tensor).detach()
-        ctx.result = res
-        return res
-
-    @staticmethod
-    def backward(ctx, grad_output: Tensor) -> Tensor:
-        t = ctx.tensor
-        return (2.0 / (t.numel() - 1.0)) * (grad_output / (ctx.result * 2 + 1e-6)) * (t - t.mean())
-
-
 class ZNCCLoss(nn.Module):
     """``-cc / (std_s * std_t + 1e-8)`` over the whole batch tensor (loss.py:32-41)."""
 

@@ -255,6 +255,7 @@ extern "C" int cgan3d_copy_multi(const void* const* src, void* const* dst, const
   if (total == 0) return CGAN3D_OK;
   const unsigned blocks = (unsigned)std::min<long long>((total + 255) / 256, 2048);
   ::cg::launch(::cg::copy_multi_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, c);
+  CG_LAUNCH_CHECK("copy_multi_kernel");
   return CGAN3D_OK;
 }
 

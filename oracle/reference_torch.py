@@ -138,11 +138,42 @@ class _GradToBf16(torch.autograd.Function):
 _COLS_MAX = 1 << 30
 
 
-def _conv3d_cpu(x: Tensor, w: Tensor, b: Optional[Tensor], **kw) -> Tensor:
-    """F.conv3d; on the CPU a stride-1 unpadded conv whose unfolded operand (Cin k^3 x output
-    voxels) would pass 2^30 elements — the generator's 16 -> 1 k7 conv at 128^3 is 11.5 G, a 92 GB
-    float64 buffer past int32 indexing — runs over slabs of output depth instead (same sums)."""
+def _conv3d_fft(x: Tensor, w: Tensor) -> Tensor:
+    """Valid (unpadded, stride-1) cross-correlation through a float64 FFT: the circular
+    convolution of x with the flipped kernel over the input's own extent equals the valid
+    correlation at indices k-1 .. D-1 (no wrap reaches them).  Differentiable (torch.fft)."""
+    k = w.shape[2:]
+    s = x.shape[2:]
+    X = torch.fft.rfftn(x, s=s, dim=(2, 3, 4))
+    Wf = torch.fft.rfftn(torch.flip(w, dims=(2, 3, 4)), s=s, dim=(2, 3, 4))
+    Y = torch.einsum("ncdhw,ocdhw->nodhw", X, Wf)
+    y = torch.fft.irfftn(Y, s=s, dim=(2, 3, 4))
+    return y[:, :, k[0] - 1:, k[1] - 1:, k[2] - 1:]
+
+
+def _conv3d_unfold(x: Tensor, w: Tensor, stride: int = 1, padding: int = 0) -> Tensor:
+    """Cross-correlation as one GEMM over windows (Tensor.unfold views + einsum): the backward is
+    an unfold adjoint plus GEMMs, ~15x faster than the CPU's float64 slow_conv3d backward."""
+    if padding:
+        x = F.pad(x, (padding,) * 6)
     k = w.shape[2]
+    u = x.unfold(2, k, stride).unfold(3, k, stride).unfold(4, k, stride)  # [n, c, do, ho, wo, k, k, k]
+    return torch.einsum("ncdhwijk,ocijk->nodhw", u, w)
+
+
+def _conv3d_cpu(x: Tensor, w: Tensor, b: Optional[Tensor], **kw) -> Tensor:
+    """F.conv3d.  float64 on the CPU (the exact-arithmetic stand-in, where torch's only kernel is
+    the unfold-based slow_conv3d at a few GFLOP/s): the generator's k7 convs through an FFT, the
+    k3 / k4 convs as one windowed GEMM — the same sums to float64 rounding.  Otherwise a stride-1
+    unpadded conv whose unfolded operand (Cin k^3 x output voxels) would pass 2^30 elements runs
+    over slabs of output depth (same sums)."""
+    k = w.shape[2]
+    if x.dtype == torch.float64 and not x.is_cuda:
+        if k >= 7 and not kw:
+            y = _conv3d_fft(x, w)
+        else:
+            y = _conv3d_unfold(x, w, kw.get("stride", 1), kw.get("padding", 0))
+        return y if b is None else y + b.view(1, -1, 1, 1, 1)
     do = x.shape[2] - k + 1
     cols = w.shape[1] * k ** 3 * x.shape[0] * do * (x.shape[3] - k + 1) * (x.shape[4] - k + 1)
     if kw or x.is_cuda or cols <= _COLS_MAX:

@@ -41,15 +41,17 @@ def rel_errors(actual, ref):
     return float(np.abs(a - e).max()) / emax, float(np.linalg.norm(a - e)) / enrm
 
 
-def run_vs_oracle(S, b, iters, precision="f32", g_args=None, with_fp32=True, threads=None, yard="fp32"):
+def run_vs_oracle(S, b, iters, precision="f32", g_args=None, with_fp32=True, threads=None, yard="fp32", exact=True):
     """Yield, per iteration, ``(it, losses, ref32, ref64, grads, rec32, rec64, params)``:
     device losses (engine slot layout), the oracle's float32 / float64 losses, the device gradient
     arenas {net: {name: ndarray}}, the oracle's float32 / float64 gradient records, and
-    ``params`` = {net: (before, device_after, oracle64_after, grads64)} for the post-Adam comparison.
+    ``params`` = {net: (before, device_after, oracle64_after, grads64, yard_after)} for the post-Adam
+    comparison (``yard_after``: the float32 / bf16-operand yardstick run's own post-Adam parameters).
     ``with_fp32=False`` skips the float32 oracle (``ref32`` / ``rec32`` are then None).
     ``yard="bf16"``: the yardstick run (``ref32`` / ``rec32``) is the oracle in float64 with every
     bf16-MFMA convolution's operands rounded to bf16 (``reference_torch.BF16_OPERANDS``) instead of
-    the float32 oracle."""
+    the float32 oracle.  ``exact=False`` skips the exact float64 run (``ref64`` / ``rec64`` and the
+    oracle's post-Adam parameters are then None)."""
     from oracle import reference_torch as R
     from cgan3d_amd.engine import StepEngine
     if threads:
@@ -100,18 +102,22 @@ def run_vs_oracle(S, b, iters, precision="f32", g_args=None, with_fp32=True, thr
                                      after_critic=use_device_critic)
             finally:
                 R.BF16_OPERANDS = False
+        yard_after = {"G": {k: v.detach().clone() for k, v in g32.items()}, "D": dict(d_oracle_after)} if with_fp32 else None
         d_oracle_after.clear()
-        rec64 = {}
-        ref64 = R.train_step(gpar, dpar, gopt, dopt, torch.from_numpy(opt).double(), torch.from_numpy(sub).double(),
-                             torch.from_numpy(seg), torch.from_numpy(eps).double(), cfg, record=rec64,
-                             after_critic=use_device_critic)
+        rec64 = ref64 = None
+        if exact:
+            rec64 = {}
+            ref64 = R.train_step(gpar, dpar, gopt, dopt, torch.from_numpy(opt).double(), torch.from_numpy(sub).double(),
+                                 torch.from_numpy(seg), torch.from_numpy(eps).double(), cfg, record=rec64,
+                                 after_critic=use_device_critic)
         losses = eng.losses.cpu().numpy()
         grads = {net: {k: gv.cpu().numpy() for k, gv in arena.gviews.items()}
                  for net, arena in (("G", eng.g_arena), ("D", eng.d_arena))}
         after = {"G": {k: v.detach().cpu().clone() for k, v in g.state_dict().items()},
                  "D": d_after}
         oracle_after = {"G": {k: v.detach().clone() for k, v in gpar.items()}, "D": dict(d_oracle_after)}
-        params = {net: (before[net], after[net], oracle_after[net], rec64[net]) for net in ("G", "D")}
+        params = {net: (before[net], after[net], oracle_after[net] if exact else None, rec64[net] if exact else None,
+                        yard_after[net] if with_fp32 else None) for net in ("G", "D")}
         yield it, losses, ref32, ref64, grads, rec32, rec64, params
         # the next iteration starts from the device's state (params, BN buffers, Adam moments)
         for k, v in g.state_dict().items():

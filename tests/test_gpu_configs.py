@@ -1,29 +1,35 @@
 """Every single-GPU configuration of BASELINE.json on the HIP path, against the CPU oracle.
 
 * configs[1] — 64^3, batch 4 (+4 subopt), bf16, the full 4-block generator + GP critic: the
-  benchmarked step itself, one step against the float64 oracle with the bf16 bar below.
+  benchmarked step itself, one step against its own yardstick (below) and reported against the
+  exact float64 step.
 * configs[2] — 128^3, batch 1, fp32: one step against the float64 oracle at north_star's 1e-3
   (conftest.assert_parity, the reference's own float32 deviation as the yardstick, ceiling 5e-3).
 * configs[4] — 128^3 bf16 with the gradient penalty (global batch 16 over 8 GPUs, 2 per GPU): one
-  step at batch 1 against the float64 oracle with the bf16 bar (the two float64 oracle runs at
-  128^3 bound the check to batch 1 on the box's CPU share; the batch dimension of every kernel is
-  exercised at batch 4 by the 64^3 test).
+  step at batch 1 against its own yardstick (the batch dimension of every kernel is exercised at
+  batch 4 by the 64^3 test).
 
-The bf16 bar (stated here).  Every convolution rounds both operands to bf16 (8-bit mantissa,
-unit roundoff 2^-9 ~ 2e-3) and accumulates in fp32; the per-op tests hold one bf16 conv to 2e-2
-of its max (test_gpu_ops.py).  Through a whole step the generator's BatchNorm backward amplifies
-that rounding: dL/dz = gamma*invstd*(g - mean g - xhat*mean(g*xhat)) nearly cancels, so the
-deep layers' weight gradients of ANY bf16-operand implementation sit 10-20 % (relative L2) from
-the exact ones.  The yardstick is therefore the oracle itself run in float64 with every such
-convolution's operands rounded to bf16 (``reference_torch.BF16_OPERANDS``): per tensor, the
-device's error against the float64 step must be within max(3e-2, 2x that reference's own
-deviation) in relative L2 and within max(1e-1, 4x its largest element's deviation, 2x its L2
-deviation) in max-abs, hard ceiling 0.3 relative L2; losses within 2e-2 of float64.  Tensors
-that are exactly zero in real arithmetic (the critic's last bias) are held to 1e-3 of the
-network's largest gradient.  Post-Adam parameters: every element whose float64 gradient is above
-twice the bf16-operand reference's gradient noise (and above 5e-2 of the tensor's largest) takes
-an Adam step of the same sign as the oracle's (Adam's first steps are ~lr*sign(g)/sqrt(1-beta2),
-so the sign is what the update carries).
+The bf16 yardstick (stated here).  The device's bf16 path rounds both operands of every generator
+convolution and of the critic's middle convolutions to bf16 (round-to-nearest-even) and
+accumulates in fp32; everything else runs in fp32.  The oracle run in float64 with exactly those
+roundings (``reference_torch.BF16_OPERANDS``) computes the same function up to the device's fp32
+accumulation order, so the device is compared with it DIRECTLY:
+
+* every gradient tensor: relative L2 error <= 1e-2 (BF16_L2) and max-abs error <= 5e-2 of the
+  tensor's largest element (BF16_MAX: single elements move further than the norm where an fp32
+  summation difference carries an operand across a bf16 rounding boundary and the generator's
+  BatchNorm backward amplifies it);
+* tensors exactly zero in real arithmetic (the critic's last bias): within 1e-3 of the network's
+  largest gradient;
+* losses: within 1e-3 relative (floor 1e-2 absolute scale for the small Wasserstein terms);
+* post-Adam parameters: every element whose yardstick gradient is above twice the device's
+  gradient deviation on that tensor (and above 5e-2 of the tensor's largest) takes an Adam step of
+  the same sign as the yardstick's (Adam's first steps are ~lr*sign(g)/sqrt(1-beta2)).
+
+Against the EXACT float64 step the bf16 path is 10-20 % off in relative L2 on the deep generator
+layers (the BatchNorm backward amplifies the 2^-9 operand rounding of ANY bf16-operand
+implementation); the 64^3 test reports that (gpurun_out/bf16_vs_oracle_64_b4.json, with the
+yardstick's own deviation beside it) and bounds it by 0.3 as a sanity ceiling only.
 """
 import json
 import os
@@ -37,7 +43,7 @@ from oracle_step import LOSS_SLOTS, rel_errors, run_vs_oracle
 
 pytestmark = pytest.mark.gpu
 
-BF16_L2, BF16_MAX, BF16_LOSS, BF16_CEIL = 3e-2, 1e-1, 2e-2, 0.3
+BF16_L2, BF16_MAX, BF16_LOSS, EXACT_CEIL = 1e-2, 5e-2, 1e-3, 0.3
 # exactly zero in real arithmetic: a conv bias feeding BatchNorm has zero gradient, and the critic's
 # last bias gradient is d/db [mean D(fake) - mean D(real)] = 0 (+ the penalty's, also 0)
 ZERO_GRADS = ("model.last.bias",)
@@ -49,57 +55,68 @@ def _dump(name, rec):
         (out / f"{name}.json").write_text(json.dumps(rec, indent=1))
 
 
-def _bf16_check(S, b, tag):
-    report = {"S": S, "b": b, "tensors": {}, "losses": {}, "adam": {}}
+def _bf16_check(S, b, tag, exact):
+    report = {"S": S, "b": b, "bars": {"l2": BF16_L2, "max": BF16_MAX, "loss": BF16_LOSS}, "tensors": {},
+              "losses": {}, "adam": {}}
     fails = []
-    for it, losses, refbf, ref64, grads, recbf, rec64, params in run_vs_oracle(S, b, 1, "bf16", yard="bf16"):
+    for it, losses, refbf, ref64, grads, recbf, rec64, params in run_vs_oracle(S, b, 1, "bf16", yard="bf16",
+                                                                                exact=exact):
         for k, slot in LOSS_SLOTS:
-            err = abs(float(losses[slot]) - ref64[k]) / max(abs(ref64[k]), 1e-3)
-            report["losses"][k] = [err, abs(refbf[k] - ref64[k]) / max(abs(ref64[k]), 1e-3)]
+            err = abs(float(losses[slot]) - refbf[k]) / max(abs(refbf[k]), 1e-2)
+            report["losses"][k] = {"vs_yard": err}
+            if exact:
+                report["losses"][k]["vs_exact"] = abs(float(losses[slot]) - ref64[k]) / max(abs(ref64[k]), 1e-3)
             if err > BF16_LOSS:
-                fails.append(f"loss {k}: rel err {err:.3e}")
+                fails.append(f"loss {k}: rel err {err:.3e} vs the bf16-operand oracle")
         for net in ("G", "D"):
             netmax = max(float(np.abs(g).max()) for g in grads[net].values())
             for k, gv in grads[net].items():
-                e = rec64[net][k].numpy()
-                if k in ZERO_GRADS or float(np.abs(e).max()) == 0.0:
+                y = recbf[net][k].numpy()
+                if k in ZERO_GRADS:
                     err = float(np.abs(gv).max()) / netmax
                     report["tensors"][f"{net}/{k}"] = {"zero_grad_abs_over_net_max": err}
                     if err > 1e-3:
                         fails.append(f"{net}/{k}: zero gradient off by {err:.3e} of the net's max")
                     continue
-                mx, l2 = rel_errors(gv, e)
-                ymx, yl2 = rel_errors(recbf[net][k].numpy(), e)  # the bf16-operand reference's own deviation
-                tol_l2 = min(max(BF16_L2, 2.0 * yl2), BF16_CEIL)
-                tol_mx = min(max(BF16_MAX, 4.0 * ymx, 2.0 * yl2), 2 * BF16_CEIL)
-                report["tensors"][f"{net}/{k}"] = {"max": mx, "l2": l2, "yard_max": ymx, "yard_l2": yl2}
-                if l2 > tol_l2 or mx > tol_mx:
-                    fails.append(f"grad {net}/{k}: rel max {mx:.3e} (tol {tol_mx:.2e}) L2 {l2:.3e} (tol {tol_l2:.2e})")
-            before, dev_after, ora_after, g64 = params[net]
-            for k, g in g64.items():
-                g = g.numpy()
-                noise = float(np.abs(recbf[net][k].numpy() - g).max())  # bf16-operand gradient noise
-                big = np.abs(g) > max(2.0 * noise, 5e-2 * float(np.abs(g).max()))
-                d_dev = (dev_after[k].numpy().astype(np.float64) - before[k].numpy())
-                d_ora = (ora_after[k].numpy() - before[k].numpy().astype(np.float64))
-                flips = int((np.sign(d_dev[big]) != np.sign(d_ora[big])).sum())
-                report["adam"][f"{net}/{k}"] = [flips, int(big.sum()), int(g.size)]
+                mx, l2 = rel_errors(gv, y)
+                rec = {"max": mx, "l2": l2}
+                if exact:
+                    e = rec64[net][k].numpy()
+                    rec["exact_max"], rec["exact_l2"] = rel_errors(gv, e)
+                    rec["yard_exact_max"], rec["yard_exact_l2"] = rel_errors(y, e)
+                    if rec["exact_l2"] > EXACT_CEIL:
+                        fails.append(f"grad {net}/{k}: {rec['exact_l2']:.3e} relative L2 from the exact step")
+                report["tensors"][f"{net}/{k}"] = rec
+                if l2 > BF16_L2 or mx > BF16_MAX:
+                    fails.append(f"grad {net}/{k}: vs the bf16-operand oracle rel max {mx:.3e} (bar {BF16_MAX}) "
+                                 f"L2 {l2:.3e} (bar {BF16_L2})")
+            before, dev_after, _, _, yard_after = params[net]
+            for k in grads[net]:
+                if k in ZERO_GRADS:
+                    continue
+                gy = recbf[net][k].numpy()
+                noise = float(np.abs(grads[net][k] - gy).max())  # the device's gradient deviation on this tensor
+                big = np.abs(gy) > max(2.0 * noise, 5e-2 * float(np.abs(gy).max()))
+                d_dev = dev_after[k].numpy().astype(np.float64) - before[k].numpy()
+                d_yard = yard_after[k].numpy() - before[k].numpy().astype(np.float64)
+                flips = int((np.sign(d_dev[big]) != np.sign(d_yard[big])).sum())
+                report["adam"][f"{net}/{k}"] = [flips, int(big.sum()), int(gy.size)]
                 if flips:
                     fails.append(f"adam {net}/{k}: {flips} of {int(big.sum())} elements with gradients above the "
-                                 f"bf16 noise stepped the wrong way")
+                                 f"device's deviation stepped the other way")
     _dump(f"bf16_vs_oracle_{tag}", report)
     assert not fails, "; ".join(fails[:12])
 
 
 def test_bf16_step_64_b4_matches_oracle():
     """BASELINE.json configs[1]: the benchmarked step (64^3, 4 + 4 patches, 4 ResNet blocks, bf16)."""
-    _bf16_check(64, 4, "64_b4")
+    _bf16_check(64, 4, "64_b4", exact=True)
 
 
 @pytest.mark.timeout(240)
 def test_bf16_step_128_matches_oracle():
     """BASELINE.json configs[4]: 128^3, bf16, gradient penalty (batch 1 + 1, see above)."""
-    _bf16_check(128, 1, "128_b1")
+    _bf16_check(128, 1, "128_b1", exact=False)
 
 
 @pytest.mark.timeout(240)

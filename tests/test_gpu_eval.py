@@ -1,45 +1,72 @@
 """Whole-scan inference (eval/CCTAContrastCorrector.py, reference eval/CCTAContrastCorrector.py:
-60-81): the HIP corrector against the oracle generator (eval mode, float64) tiled and averaged by
-a numpy restatement of patchly's squeeze-mode GridSampler + averaging Aggregator (patchly is not
-installed: grid and averaging unpinned by the reference itself)."""
+60-81): the HIP corrector against the oracle generator (float64) tiled and averaged by a numpy
+restatement of patchly's squeeze-mode GridSampler + averaging Aggregator (patchly is not
+installed: grid order and averaging unpinned by the reference itself).
+
+Default: the reference's semantics — the generator stays in train mode (the reference never calls
+``.eval()``, :33-38), so each DataLoader batch of tiles (C-order grid, ``batch_size`` per batch) is
+normalised with its own BatchNorm statistics and updates the running buffers.  The build-only
+``eval_mode=True`` option runs eval-mode BatchNorm (running statistics)."""
 import numpy as np
 import pytest
 import torch
 
 pytestmark = pytest.mark.gpu
 
+G_ARGS = dict(n_resnet_blocks=1, n_updownsample_blocks=2, init_channels_out=8)
 
-def test_corrector_matches_oracle():
-    from functools import partial
-    from oracle import reference_torch as R
-    from cgan3d_amd.eval.CCTAContrastCorrector import CCTAContrastCorrector, _FactorZeroCenterScaler, grid_origins
+
+def _generator():
     from cgan3d_amd.model.generator import ResnetGenerator
     from cgan3d_amd.model.init import pcg64_init_
-    g_args = dict(n_resnet_blocks=1, n_updownsample_blocks=2, init_channels_out=8)
-    gen = pcg64_init_(ResnetGenerator(**g_args), 5)
-    with torch.no_grad():  # non-trivial running statistics for eval mode
+    gen = pcg64_init_(ResnetGenerator(**G_ARGS), 5)
+    with torch.no_grad():  # non-trivial running statistics
         for k, v in gen.state_dict().items():
             if k.endswith("running_mean"):
                 v.uniform_(-0.2, 0.2)
             elif k.endswith("running_var"):
                 v.uniform_(0.5, 1.5)
-    sd = {k: v.detach().clone() for k, v in gen.state_dict().items()}
-    sc = _FactorZeroCenterScaler(238, 600)
-    corr = CCTAContrastCorrector(lambda: gen, sc, torch.device("cuda"), inference_patch_size=(32, 32, 32))
-    rng = np.random.default_rng(0)
-    scan = (rng.standard_normal((40, 36, 48)) * 200 + 200).astype(np.float32)
-    got = corr(scan, batch_size=3).numpy()
-    # restatement: every grid patch through the float64 oracle, averaged where patches overlap
-    p64 = {k: v.double() if v.is_floating_point() else v for k, v in sd.items()}
+    return gen
+
+
+def _oracle(scan, sd, batch_size, training, ps=(32, 32, 32)):
+    """patch - G(patch) per C-order batch of grid tiles through the float64 oracle, averaged."""
+    from oracle import reference_torch as R
+    from cgan3d_amd.eval.CCTAContrastCorrector import grid_origins
+    p64 = {k: v.double() if v.is_floating_point() else v.clone() for k, v in sd.items()}
     acc = np.zeros(scan.shape)
     cnt = np.zeros(scan.shape)
-    for o in grid_origins(scan.shape, (32, 32, 32)):
-        sl = tuple(slice(a, a + 32) for a in o)
-        x = torch.from_numpy(((scan[sl] - 238) / 600).astype(np.float64))[None, None]
-        y = (x - R.generator_forward(p64, x, R.GenConfig(**g_args), training=False))[0, 0].numpy()
-        acc[sl] += y
-        cnt[sl] += 1
-    want = acc / cnt * 600 + 238
+    orgs = grid_origins(scan.shape, ps)
+    for b0 in range(0, len(orgs), batch_size):
+        chunk = orgs[b0:b0 + batch_size]
+        sls = [tuple(slice(a, a + p) for a, p in zip(o, ps)) for o in chunk]
+        x = torch.from_numpy(np.stack([((scan[sl] - 238) / 600).astype(np.float64) for sl in sls]))[:, None]
+        y = (x - R.generator_forward(p64, x, R.GenConfig(**G_ARGS), training=training))[:, 0].numpy()
+        for sl, yi in zip(sls, y):
+            acc[sl] += yi
+            cnt[sl] += 1
+    return acc / cnt * 600 + 238, p64
+
+
+@pytest.mark.parametrize("eval_mode", [False, True])
+def test_corrector_matches_oracle(eval_mode):
+    from cgan3d_amd.eval.CCTAContrastCorrector import CCTAContrastCorrector, _FactorZeroCenterScaler
+    gen = _generator()
+    sd = {k: v.detach().clone() for k, v in gen.state_dict().items()}
+    corr = CCTAContrastCorrector(lambda: gen, _FactorZeroCenterScaler(238, 600), torch.device("cuda"),
+                                 inference_patch_size=(32, 32, 32), eval_mode=eval_mode)
+    assert corr.model.training == (not eval_mode)
+    rng = np.random.default_rng(0)
+    scan = (rng.standard_normal((40, 36, 48)) * 200 + 200).astype(np.float32)
+    got = corr(scan, batch_size=3).numpy()  # 8 tiles: batches of 3, 3, 2
+    want, p64 = _oracle(scan, sd, 3, training=not eval_mode)
     assert got.shape == scan.shape
     err = np.abs(got - want).max() / np.abs(want).max()
-    assert err <= 1e-5, err
+    assert err <= 1e-4, err
+    # train mode: the running buffers advanced once per batch, as in the reference
+    for k, v in gen.state_dict().items():
+        if k.endswith(("running_mean", "running_var")):
+            a, e = v.cpu().numpy(), p64[k].numpy()
+            assert np.abs(a - e).max() <= 1e-4 * max(np.abs(e).max(), 1.0), k
+        elif k.endswith("num_batches_tracked"):
+            assert int(v) == int(sd[k]) + (0 if eval_mode else 3), k

@@ -74,6 +74,7 @@ def test_step_matches_reference_fixture(golden, tag):
     names = {"L_D": 0, "D": 0, "G": 3, "sim": 4, "HU": 5, "G-full": 6}
     for it in range(meta["iters"]):
         if it > 0:
+            _assert_carried_state(eng, g, d, f, it, meta["lr"], meta["beta1"], meta["beta2"])
             _load_fixture_state(eng, g, d, f, it)
         sub = np.concatenate([f[f"it{it}/low"], f[f"it{it}/high"]])
         mask = np.concatenate([f[f"it{it}/low_seg"], f[f"it{it}/high_seg"]])
@@ -98,6 +99,50 @@ def test_step_matches_reference_fixture(golden, tag):
                 name = k.split("/", 2)[2]
                 gk = f"it{last}/grad64/{net}/{name}"
                 _assert_adam_final(sd[name].cpu().numpy(), f[k], [f[gk]] if gk in f else [], meta["lr"], k)
+
+
+def _assert_carried_state(eng, g, d, f, it, lr, b1, b2):
+    """What the device carries out of iteration it-1 (which started from the reference's state)
+    against the reference's own state entering iteration it, BEFORE the fixture overwrites it: the
+    Adam step counter exactly (advanced inside adam_pack by its last block), num_batches_tracked
+    exactly, the BatchNorm running buffers and both Adam moments at 1e-3 (max-abs and L2 of the
+    tensor's scale; exp_avg_sq squares the gradient, so 2e-3), the parameters as after any Adam step
+    (_assert_adam_final: sub-noise gradients may flip their normalised step).  This covers the state
+    the step keeps between iterations: the tick, gradient arenas zeroed once per update, self-cleaning
+    workspaces, deferred weight-gradient unpacks."""
+    for net, mod, opt in (("G", g, eng.g_optim), ("D", d, eng.d_optim)):
+        assert int(opt.hyper[4].item()) == int(f[f"it{it}/adam/{net}/step"]), f"it{it} {net}: Adam step counter"
+        sd = mod.state_dict()
+        for name, v in sd.items():
+            key = f"it{it}/state/{net}/{name}"
+            if key not in f:
+                continue
+            a = v.detach().cpu().numpy()
+            if name.endswith("num_batches_tracked"):
+                assert int(a) == int(f[key]), f"{key}: {int(a)} != {int(f[key])}"
+            elif name.endswith(("running_mean", "running_var")):
+                assert_close(a, f[key], 1e-3, f"carried {key}")
+            else:
+                gk = f"it{it - 1}/grad64/{net}/{name}"
+                _assert_adam_final(a, f[key], [f[gk]] if gk in f else [], lr, f"carried {key}")
+        for name, p in zip(opt.arena.names, opt.arena.params):
+            for mom, rt in (("exp_avg", 1e-3), ("exp_avg_sq", 2e-3)):
+                key = f"it{it}/adam/{net}/{name}/{mom}"
+                e = f[key]
+                if not np.abs(e).max() > 0:
+                    continue
+                gk = f"it{it - 1}/grad64/{net}/{name}"
+                atol = 1e-7 if name == "model.last.bias" else 0.0  # its gradient is 0 in real arithmetic
+                a = opt.state[p][mom].detach().cpu().numpy()
+                if gk in f and name != "model.last.bias":
+                    # the moments' float64 counterpart: the same update with the float64 gradient
+                    # (the moments entering it-1 are the reference's own), so the bar is the
+                    # gradients' own (conftest.assert_parity, the reference's float32 deviation)
+                    g64, g32 = f[gk], f[gk.replace("/grad64/", "/grad/")]
+                    m64 = e + ((1 - b1) * (g64 - g32) if mom == "exp_avg" else (1 - b2) * (g64 * g64 - g32 * g32))
+                    assert_parity(a, e, m64, f"carried {key}", rtol=rt)
+                else:
+                    assert_close(a, e, rt, f"carried {key}", atol=atol)
 
 
 def _assert_adam_final(actual, expected, grads, lr, name):
