@@ -26,7 +26,8 @@ class ConvGeom(C.Structure):
                 ("do_", C.c_int32), ("ho", C.c_int32), ("wo", C.c_int32),
                 ("cin", C.c_int32), ("cout", C.c_int32), ("k", C.c_int32), ("stride", C.c_int32),
                 ("pad", C.c_int32), ("transposed", C.c_int32), ("reflect", C.c_int32),
-                ("w_sa", C.c_int64), ("w_sb", C.c_int64), ("w_packed", C.c_int32), ("prec", C.c_int32)]
+                ("w_sa", C.c_int64), ("w_sb", C.c_int64), ("w_packed", C.c_int32), ("prec", C.c_int32),
+                ("planar", C.c_int32)]
 
 
 class UnpackDesc(C.Structure):
@@ -101,6 +102,7 @@ _SIGS = {
     "cgan3d_reflect_fold": ([_P, _P, _I32, _I32, _I32, _I32, _I32, _I32, _P], _I32),
     "cgan3d_reflect_fold_slots": ([_I32, _I32, _I32, _I32, _I32], _I32),
     "cgan3d_reflect_fold_ex": ([_P, _P, _I32, _I32, _I32, _I32, _I32, _I32, _P, _P], _I32),
+    "cgan3d_reflect_fold2d": ([_P, _P, _I32, _I32, _I32, _I32, _I32, _P, _P], _I32),
     "cgan3d_gp_interpolate": ([_P, _P, _P, _P, _I32, _I64, _P], _I32),
     "cgan3d_tanh_backward": ([_P, _P, _P, _I64, _P], _I32),
     "cgan3d_unpack_patches": ([_P, _I32, _I64, _F, _F, _P, _P, _P], _I32),

@@ -57,8 +57,23 @@ def _half(d: Dims) -> Dims:
     return tuple((x + 2 * 1 - 3) // 2 + 1 for x in d)
 
 
-def _conv_out(d: Dims, k, s, p) -> Dims:
+def _conv_out(d: Dims, k, s, p, planar: bool = False) -> Dims:
+    """Output dims of a conv; ``planar`` (the 2-D variants on dims (1, H, W)): depth passes through."""
+    if planar:
+        return (1,) + tuple((x + 2 * p - k) // s + 1 for x in d[1:])
     return tuple((x + 2 * p - k) // s + 1 for x in d)
+
+
+def _planar_dims(dims, planar: bool) -> Dims:
+    """(H, W) or (1, H, W) -> (1, H, W) for the 2-D variants; 3-D dims unchanged."""
+    dims = tuple(int(x) for x in dims)
+    if planar and len(dims) == 2:
+        return (1,) + dims
+    if planar and dims[0] != 1:
+        raise ValueError(f"2-D variant: dims must be (H, W) or (1, H, W), got {dims}")
+    if len(dims) != 3:
+        raise ValueError(f"dims must have three entries, got {dims}")
+    return dims
 
 
 class Arena:
@@ -123,13 +138,18 @@ class GeneratorPlan:
 
     def __init__(self, cfg, n: int, dims: Dims, device, P: Dict[str, torch.Tensor], prec: int = L.PREC_F32):
         c0 = cfg.init_channels_out
+        # the 2-D variants (experiments/conf_2D.py, is_2D): planar geometries on dims (1, H, W), f32
+        self.planar = pl = bool(getattr(cfg, "is_2D", False))
+        if pl and prec != L.PREC_F32:
+            raise NotImplementedError("the 2-D variants run the exact-f32 path (precision='f32')")
+        dims = _planar_dims(dims, pl)
         self.n, self.dims, self.device = n, tuple(dims), device
         self.packs = ops.PackSet(device)  # packed [tap][cin][cout] weight copies, refreshed per update
         layers: List[_GLayer] = [_GLayer("conv", "model.first", 7, 1, 3, True, 1, c0, dims, dims)]
         d = tuple(dims)
         for i in range(cfg.n_updownsample_blocks):
             ci = c0 * 2**i
-            dn = _conv_out(d, 3, 2, 1)
+            dn = _conv_out(d, 3, 2, 1, pl)
             layers.append(_GLayer("conv", f"model.downsampling.{i}", 3, 2, 1, False, ci, 2 * ci, d, dn))
             d = dn
         cr = c0 * 2**cfg.n_updownsample_blocks
@@ -140,7 +160,7 @@ class GeneratorPlan:
                                   residual=True))
         for j, i in enumerate(range(cfg.n_updownsample_blocks, 0, -1)):
             ci = c0 * 2**i
-            up = tuple(2 * x for x in d)  # k3 s2 p1 output_padding 1
+            up = tuple(x if (pl and a == 0) else 2 * x for a, x in enumerate(d))  # k3 s2 p1 output_padding 1
             layers.append(_GLayer("convt", f"model.upsampling.{j}", 3, 2, 1, False, ci, ci // 2, d, up))
             d = up
         assert d == tuple(dims), f"generator output dims {d} != input dims {dims} (need dims % 4 == 0)"
@@ -157,13 +177,13 @@ class GeneratorPlan:
         ws = 0
         for ly in layers:
             if ly.kind == "conv":
-                gf = ops.conv_fwd_geom(n, ly.din, ly.dout, ly.cin, ly.cout, ly.k, ly.s, ly.p, ly.reflect)
-                gd = ops.conv_dgrad_geom(n, ly.din, ly.dout, ly.cin, ly.cout, ly.k, ly.s, ly.p)
-                gw = ops.conv_wgrad_geom(n, ly.din, ly.dout, ly.cin, ly.cout, ly.k, ly.s, ly.p, ly.reflect)
+                gf = ops.conv_fwd_geom(n, ly.din, ly.dout, ly.cin, ly.cout, ly.k, ly.s, ly.p, ly.reflect, planar=pl)
+                gd = ops.conv_dgrad_geom(n, ly.din, ly.dout, ly.cin, ly.cout, ly.k, ly.s, ly.p, planar=pl)
+                gw = ops.conv_wgrad_geom(n, ly.din, ly.dout, ly.cin, ly.cout, ly.k, ly.s, ly.p, ly.reflect, planar=pl)
             else:
-                gf = ops.convt_fwd_geom(n, ly.din, ly.dout, ly.cin, ly.cout, ly.k, ly.s, ly.p)
-                gd = ops.convt_dgrad_geom(n, ly.din, ly.dout, ly.cin, ly.cout, ly.k, ly.s, ly.p)
-                gw = ops.convt_wgrad_geom(n, ly.din, ly.dout, ly.cin, ly.cout, ly.k, ly.s, ly.p)
+                gf = ops.convt_fwd_geom(n, ly.din, ly.dout, ly.cin, ly.cout, ly.k, ly.s, ly.p, planar=pl)
+                gd = ops.convt_dgrad_geom(n, ly.din, ly.dout, ly.cin, ly.cout, ly.k, ly.s, ly.p, planar=pl)
+                gw = ops.convt_wgrad_geom(n, ly.din, ly.dout, ly.cin, ly.cout, ly.k, ly.s, ly.p, planar=pl)
             gw = ops.with_prec(gw, prec)
             wt = P[f"{ly.name}.conv.weight"]
             gf, wf = self.packs.add(gf, wt, prec)
@@ -184,11 +204,13 @@ class GeneratorPlan:
             nvox = n * ly.dout[0] * ly.dout[1] * ly.dout[2]
             ws = max(ws, ops.wgrad_ws_floats(gw), ops.bn_backward_ws_floats(nvox, ly.cout))
         la = self.last
-        pd = tuple(x + 2 * la.p for x in la.din)
-        self.geo_last_fwd = ops.with_prec(ops.conv_fwd_geom(n, la.din, la.dout, la.cin, 1, la.k, 1, la.p, True), prec)
-        self.geo_last_wgrad = ops.with_prec(ops.conv_wgrad_geom(n, la.din, la.dout, la.cin, 1, la.k, 1, la.p, True),
-                                            prec)
-        self.geo_last_dgrad = ops.with_prec(ops.conv_dgrad_geom(n, pd, la.dout, la.cin, 1, la.k, 1, 0), prec)  # padded grid
+        pd = tuple(x if (pl and a == 0) else x + 2 * la.p for a, x in enumerate(la.din))
+        self.geo_last_fwd = ops.with_prec(ops.conv_fwd_geom(n, la.din, la.dout, la.cin, 1, la.k, 1, la.p, True,
+                                                            planar=pl), prec)
+        self.geo_last_wgrad = ops.with_prec(ops.conv_wgrad_geom(n, la.din, la.dout, la.cin, 1, la.k, 1, la.p, True,
+                                                                planar=pl), prec)
+        self.geo_last_dgrad = ops.with_prec(ops.conv_dgrad_geom(n, pd, la.dout, la.cin, 1, la.k, 1, 0, planar=pl),
+                                            prec)  # padded grid
         # backward slabs: layer i's dL/dy comes from layer i+1's input-grad launch, the last one's
         # from the reflect fold of the last conv's input-grad
         self.slots_b = [ops.bn_slots(self.geo_dgrad[i + 1]) for i in range(len(layers) - 1)]
@@ -370,7 +392,7 @@ class GeneratorPlan:
         else:
             ops.conv(self.geo_last_dgrad, self.dz_last, P["model.last_conv.weight"], self.dpad)
             ops.reflect_fold(self.dpad, self.dy[-1], n, la.din, la.cin, la.p,
-                             ep=self._bn_grad_epi(len(self.layers) - 1))
+                             ep=self._bn_grad_epi(len(self.layers) - 1), planar=self.planar)
         for i in range(len(self.layers) - 1, -1, -1):
             ly = self.layers[i]
             nb = f"{ly.name}.normalization"
@@ -468,22 +490,26 @@ class CriticPlan:
     statistics for its backward."""
 
     def __init__(self, cfg, nmax: int, dims: Dims, device, P: Dict[str, torch.Tensor], prec: int = L.PREC_F32):
+        self.pl = pl = bool(getattr(cfg, "is_2D", False))  # the 2-D variants: planar geometries, f32
+        if pl and prec != L.PREC_F32:
+            raise NotImplementedError("the 2-D variants run the exact-f32 path (precision='f32')")
+        dims = _planar_dims(dims, pl)
         self.cfg, self.nmax, self.dims, self.device = cfg, nmax, tuple(dims), device
         self.prec = prec
         c0, s = cfg.init_channels_out, cfg.negative_slope
         self.slope = s
         d = tuple(dims)
         ls = []
-        dn = _conv_out(d, 4, 2, 1)
+        dn = _conv_out(d, 4, 2, 1, pl)
         ls.append(_DLayer("model.first.conv", 4, 2, 1, cfg.channels_in, c0, d, dn))
         d = dn
         out_ = c0
         for m in range(cfg.discriminator_depth):
             in_, out_ = min(2**m, 8) * c0, min(2 ** (m + 1), 8) * c0
-            dn = _conv_out(d, 4, 2, 1)
+            dn = _conv_out(d, 4, 2, 1, pl)
             ls.append(_DLayer(f"model.middle.{m}.conv", 4, 2, 1, in_, out_, d, dn))
             d = dn
-        dn = _conv_out(d, 4, 1, 1)
+        dn = _conv_out(d, 4, 1, 1, pl)
         assert min(dn) > 0, f"patch {dims} too small for the critic"
         ls.append(_DLayer("model.last", 4, 1, 1, out_, 1, d, dn))
         self.layers = ls
@@ -500,7 +526,7 @@ class CriticPlan:
         self.dz = [torch.empty((nmax, *ly.dout, ly.cout), device=device) for ly in ls]  # dL/dz (last = dlogits)
         ws = 0
         for ly in ls:
-            g = ops.conv_wgrad_geom(nmax, ly.din, ly.dout, ly.cin, ly.cout, ly.k, ly.s, ly.p)
+            g = ops.conv_wgrad_geom(nmax, ly.din, ly.dout, ly.cin, ly.cout, ly.k, ly.s, ly.p, planar=self.pl)
             nv = nmax * ly.dout[0] * ly.dout[1] * ly.dout[2]
             ws = max(ws, ops.wgrad_ws_floats(g), ops.channel_sum_ws_floats(nv, ly.cout),
                      ops.bn_backward_ws_floats(nv, ly.cout))
@@ -543,16 +569,21 @@ class CriticPlan:
         # packed weight copies per (layer, role); the packed layout does not depend on batch/dims
         self.packs = ops.PackSet(device)
         self.wf, self.wd = [], []
-        for ly in ls:
+        # the last layer (64 -> 1) stays exact fp32 in every role, as the first does: its forward and
+        # weight grad are the fp32 VALU cout == 1 kernels, and its input-grad (1 -> 64, the start of
+        # every critic backward) takes the fp32 implicit GEMM — rounding the dlogits and its weights
+        # to bf16 there would perturb the whole input-gradient chain feeding the generator
+        self.prec_d = [L.PREC_F32 if i == len(ls) - 1 else prec for i in range(len(ls))]
+        for i, ly in enumerate(ls):
             w = P[f"{ly.name}.weight"]
-            gf, wf = self.packs.add(ops.conv_fwd_geom(nmax, ly.din, ly.dout, ly.cin, ly.cout, ly.k, ly.s, ly.p), w, prec)
-            gd, wd = self.packs.add(ops.conv_dgrad_geom(nmax, ly.din, ly.dout, ly.cin, ly.cout, ly.k, ly.s, ly.p), w,
-                                    prec)
+            gf, wf = self.packs.add(ops.conv_fwd_geom(nmax, ly.din, ly.dout, ly.cin, ly.cout, ly.k, ly.s, ly.p, planar=self.pl), w, prec)
+            gd, wd = self.packs.add(ops.conv_dgrad_geom(nmax, ly.din, ly.dout, ly.cin, ly.cout, ly.k, ly.s, ly.p, planar=self.pl), w,
+                                    self.prec_d[i])
             self.wf.append(wf if gf.w_packed else None)
             self.wd.append(wd if gd.w_packed else None)
         for i, ly in enumerate(ls):
             if self.is_bn[i]:
-                gs = self._geo(ops.conv_fwd_geom(nmax, ly.din, ly.dout, ly.cin, ly.cout, ly.k, ly.s, ly.p), self.wf[i])
+                gs = self._geo(ops.conv_fwd_geom(nmax, ly.din, ly.dout, ly.cin, ly.cout, ly.k, ly.s, ly.p, planar=self.pl), self.wf[i])
                 self.stats[i] = torch.empty(ops.stats_floats(gs), device=device)
         self.pack()
 
@@ -560,8 +591,8 @@ class CriticPlan:
         """Refresh the packed weight copies (one launch); call after every weight update."""
         self.packs.pack()
 
-    def _geo(self, g, packed):
-        return ops.with_packing(g, self.prec) if packed is not None else g
+    def _geo(self, g, packed, prec=None):
+        return ops.with_packing(g, self.prec if prec is None else prec) if packed is not None else g
 
     def _sl(self, t, off, n):
         return t[off:off + n]
@@ -572,7 +603,7 @@ class CriticPlan:
         updated; eval: running statistics) and keep scale/shift in slot ``bn_pass``."""
         h = x
         for i, ly in enumerate(self.layers):
-            g = self._geo(ops.conv_fwd_geom(n, ly.din, ly.dout, ly.cin, ly.cout, ly.k, ly.s, ly.p), self.wf[i])
+            g = self._geo(ops.conv_fwd_geom(n, ly.din, ly.dout, ly.cin, ly.cout, ly.k, ly.s, ly.p, planar=self.pl), self.wf[i])
             w = self.wf[i] if self.wf[i] is not None else P[f"{ly.name}.weight"]
             out = self._sl(self.a[i], off, n)
             if self.is_bn[i]:
@@ -617,7 +648,8 @@ class CriticPlan:
         (added when ``bn_accumulate``) or are discarded when ``G`` is None."""
         for i in range(len(self.layers) - 1, 0, -1):
             ly = self.layers[i]
-            g = self._geo(ops.conv_dgrad_geom(n, ly.din, ly.dout, ly.cin, ly.cout, ly.k, ly.s, ly.p), self.wd[i])
+            g = self._geo(ops.conv_dgrad_geom(n, ly.din, ly.dout, ly.cin, ly.cout, ly.k, ly.s, ly.p, planar=self.pl), self.wd[i],
+                          self.prec_d[i])
             w = self.wd[i] if self.wd[i] is not None else P[f"{ly.name}.weight"]
             if self.is_bn[i - 1]:  # dL/da -> BatchNorm + LeakyReLU backward -> dL/dz
                 lp = self.layers[i - 1]
@@ -644,7 +676,7 @@ class CriticPlan:
                          ops.epilogue(mask_src=self._sl(self.a[i - 1], off, n), slope=self.slope))
         ly = self.layers[0]
         if dx_n > 0:
-            g = self._geo(ops.conv_dgrad_geom(dx_n, ly.din, ly.dout, ly.cin, ly.cout, ly.k, ly.s, ly.p), self.wd[0])
+            g = self._geo(ops.conv_dgrad_geom(dx_n, ly.din, ly.dout, ly.cin, ly.cout, ly.k, ly.s, ly.p, planar=self.pl), self.wd[0])
             w = self.wd[0] if self.wd[0] is not None else P[f"{ly.name}.weight"]
             ops.conv(g, self._sl(self.dz[0], dx_off, dx_n), w, dx_out)
 
@@ -653,7 +685,7 @@ class CriticPlan:
         a_l[off:off+n] (after the masks there have been consumed)."""
         h = gamma
         for i, ly in enumerate(self.layers[:-1]):
-            g = self._geo(ops.conv_fwd_geom(n, ly.din, ly.dout, ly.cin, ly.cout, ly.k, ly.s, ly.p), self.wf[i])
+            g = self._geo(ops.conv_fwd_geom(n, ly.din, ly.dout, ly.cin, ly.cout, ly.k, ly.s, ly.p, planar=self.pl), self.wf[i])
             out = self._sl(self.a[i], off, n)
             w = self.wf[i] if self.wf[i] is not None else P[f"{ly.name}.weight"]
             ops.conv(g, h, w, out, ops.epilogue(mask_src=out, slope=self.slope))
@@ -708,12 +740,12 @@ class CriticPlan:
 
         def wgrad(i, prev):
             ly = self.layers[i]
-            g = ops.with_prec(ops.conv_wgrad_geom(n_all, ly.din, ly.dout, ly.cin, ly.cout, ly.k, ly.s, ly.p), self.prec)
+            g = ops.with_prec(ops.conv_wgrad_geom(n_all, ly.din, ly.dout, ly.cin, ly.cout, ly.k, ly.s, ly.p, planar=self.pl), self.prec)
             self._wgrad(g, prev, self.dz[i][:n_all], G[f"{ly.name}.weight"], ws, zeroed, layer=i)
         self._on_side(lambda: wgrad(0, x_all))  # x_all's interpolation rows hold gamma = nu_0
         h = gamma
         for i, ly in enumerate(self.layers[:-1]):
-            g = self._geo(ops.conv_fwd_geom(n, ly.din, ly.dout, ly.cin, ly.cout, ly.k, ly.s, ly.p), self.wf[i])
+            g = self._geo(ops.conv_fwd_geom(n, ly.din, ly.dout, ly.cin, ly.cout, ly.k, ly.s, ly.p, planar=self.pl), self.wf[i])
             out = self._sl(self.a[i], off, n)
             w = self.wf[i] if self.wf[i] is not None else P[f"{ly.name}.weight"]
             ops.conv(g, h, w, out, ops.epilogue(mask_src=out, slope=self.slope))
@@ -736,7 +768,7 @@ class CriticPlan:
         """dW_l = wgrad(a_{l-1}, dz_l) over n_all samples; db_l = sum dz_l over the first n_bias."""
         prev = x_all
         for i, ly in enumerate(self.layers):
-            g = ops.with_prec(ops.conv_wgrad_geom(n_all, ly.din, ly.dout, ly.cin, ly.cout, ly.k, ly.s, ly.p), self.prec)
+            g = ops.with_prec(ops.conv_wgrad_geom(n_all, ly.din, ly.dout, ly.cin, ly.cout, ly.k, ly.s, ly.p, planar=self.pl), self.prec)
             self._wgrad(g, prev, self.dz[i][:n_all], G[f"{ly.name}.weight"], self.ws, zeroed, layer=i)
             prev = self.a[i][:n_all]
         self._flush_unpack()
@@ -794,7 +826,7 @@ class CriticPlan:
                 raise NotImplementedError("LayerNorm critic: the layer below the last conv must be a LayerNorm block")
         # 3. weight gradients (accumulated) and biases
         for i, ly in enumerate(self.layers):
-            wg = lambda m: ops.with_prec(ops.conv_wgrad_geom(m, ly.din, ly.dout, ly.cin, ly.cout, ly.k, ly.s, ly.p),  # noqa
+            wg = lambda m: ops.with_prec(ops.conv_wgrad_geom(m, ly.din, ly.dout, ly.cin, ly.cout, ly.k, ly.s, ly.p, planar=self.pl),  # noqa
                                          self.prec)
             dw = G[f"{ly.name}.weight"]
             prev = x_all if i == 0 else self.a[i - 1]
@@ -834,6 +866,11 @@ class StepEngine:
                                       "(no reference configuration uses it: SURVEY.md §8f row 4)")
         device = device or torch.device("cuda", torch.cuda.current_device())
         self.device = device
+        # the 2-D variants (experiments/conf_2D.py): patches [N, 1, H, W] as planar (1, H, W) grids
+        self.planar = bool(getattr(g_cfg, "is_2D", False))
+        if self.planar != bool(getattr(d_cfg, "is_2D", False)):
+            raise ValueError("StepEngine: generator and critic must both be 2-D or both 3-D")
+        dims = _planar_dims(dims, self.planar)
         self.dims = tuple(dims)
         self.b_opt, self.b_sub, self.b_gp = b_opt, b_sub, min(b_opt, b_sub)
         self.vox = dims[0] * dims[1] * dims[2]

@@ -55,31 +55,38 @@ class ConvBlock(nn.Module):
 
     # -- standalone HIP forward (channels-first API tensors) -------------------------------
     def forward(self, x: Tensor) -> Tensor:
-        if self.is_2D:
-            raise NotImplementedError("2-D variants are outside this build's hot path (SURVEY.md §8f row 4)")
         if torch.is_grad_enabled() and (x.requires_grad or any(p.requires_grad for p in self.parameters())):
             raise NotImplementedError("ConvBlock.forward with autograd: use ResnetGenerator / "
                                       "PatchGANDiscriminator or the Trainer step engine")
         conv = self.conv
-        n, cin, *din = x.shape
+        pl = self.is_2D  # 2-D variants: planar geometries on (1, H, W) grids
+        if x.dim() != (4 if pl else 5):
+            raise ValueError(f"ConvBlock expects [N, C, {'H, W' if pl else 'D, H, W'}], got {tuple(x.shape)}")
+        n, cin, *sp = x.shape
+        din = (1, *sp) if pl else tuple(sp)
         k, s, p = conv.kernel_size[0], conv.stride[0], conv.padding[0]
-        xc = x.permute(0, 2, 3, 4, 1).contiguous()
+        xc = x.movedim(1, -1).contiguous()
         reflect = conv.padding_mode == "reflect"
-        if isinstance(conv, nn.ConvTranspose3d):
+        keep = lambda a, v: v if not (pl and a == 0) else 1  # noqa: E731 (depth passes through in 2-D)
+        if isinstance(conv, (nn.ConvTranspose3d, nn.ConvTranspose2d)):
             op = conv.output_padding[0]
-            dout = tuple((d - 1) * s - 2 * p + k + op for d in din)
-            g = ops.convt_fwd_geom(n, tuple(din), dout, cin, conv.out_channels, k, s, p)
+            dout = tuple(keep(a, (d - 1) * s - 2 * p + k + op) for a, d in enumerate(din))
+            g = ops.convt_fwd_geom(n, din, dout, cin, conv.out_channels, k, s, p, planar=pl)
         else:
-            dout = tuple((d + 2 * p - k) // s + 1 for d in din)
-            g = ops.conv_fwd_geom(n, tuple(din), dout, cin, conv.out_channels, k, s, p, reflect)
+            dout = tuple(keep(a, (d + 2 * p - k) // s + 1) for a, d in enumerate(din))
+            g = ops.conv_fwd_geom(n, din, dout, cin, conv.out_channels, k, s, p, reflect, planar=pl)
         cout = conv.out_channels
         z = torch.empty((n, *dout, cout), device=x.device)
         act, slope = _act_code(self.activation_fn)
         norm = self.normalization
+        out_shape = (n, cout, *(dout[1:] if pl else dout))
+
+        def channels_first(t):
+            return t.view(n, *(dout[1:] if pl else dout), cout).movedim(-1, 1).contiguous()
         if isinstance(norm, nn.Identity):
             ops.conv(g, xc, conv.weight, z, ops.epilogue(bias=conv.bias, act=act, slope=slope))
-            return z.permute(0, 4, 1, 2, 3).contiguous()
-        if not isinstance(norm, nn.BatchNorm3d):
+            return channels_first(z)
+        if not isinstance(norm, (nn.BatchNorm3d, nn.BatchNorm2d)):
             raise NotImplementedError("LayerNorm critic (gp_layernorm.py) is outside this build's hot path")
         nvox = n * dout[0] * dout[1] * dout[2]
         ss = torch.empty(2 * cout, device=x.device)
@@ -96,7 +103,8 @@ class ConvBlock(nn.Module):
             ss[cout:] = norm.bias - norm.running_mean * ss[:cout]
         y = torch.empty_like(z)
         ops.bn_apply(z, nvox, cout, ss, act, y, slope=slope)
-        return y.permute(0, 4, 1, 2, 3).contiguous()
+        assert channels_first(y).shape == out_shape
+        return channels_first(y)
 
 
 class ResNetBlock(nn.Module):

@@ -32,6 +32,7 @@ class CriticConfig:
     discriminator_depth: int = 3
     negative_slope: float = 0.2
     norm: str = "identity"
+    is_2D: bool = False  # the 2-D variants (experiments/conf_2D.py): planar kernels, f32
 
 
 class PatchGANDiscriminator(nn.Module):
@@ -42,12 +43,12 @@ class PatchGANDiscriminator(nn.Module):
         slope = kwargs.get("negative_slope", 0.01)
         norm = {None: "batch", nn.BatchNorm3d: "batch", nn.BatchNorm2d: "batch", nn.Identity: "identity",
                 nn.LayerNorm: "layer"}.get(norm_layer, "other")
-        self.config = CriticConfig(channels_in, init_channels_out, discriminator_depth, slope, norm)
+        self.config = CriticConfig(channels_in, init_channels_out, discriminator_depth, slope, norm, bool(is_2D))
+        self.is_2D = is_2D
         self._unsupported = None
-        if is_2D or kernel_size != 4 or padding != 1 or norm not in ("identity", "batch", "layer"):
-            self._unsupported = ("the HIP critic implements the 3-D k4 p1 critic with Identity norm (GP conf), "
-                                 "BatchNorm (weight-clip conf) or LayerNorm (gp_layernorm conf); 2-D critics are "
-                                 "SURVEY.md §8f row 4")
+        if kernel_size != 4 or padding != 1 or norm not in ("identity", "batch", "layer") or (is_2D and norm == "layer"):
+            self._unsupported = ("the HIP critic implements the k4 p1 critic with Identity norm (GP conf), "
+                                 "BatchNorm (weight-clip conf, 3-D and conf_2D) or LayerNorm (gp_layernorm conf, 3-D)")
         elif norm == "layer" and kwargs.get("elementwise_affine", True):
             self._unsupported = ("the HIP LayerNorm critic implements the gp_layernorm conf's LayerNorm without "
                                  "affine parameters (gp_layernorm.py:9-11: elementwise_affine=False)")
@@ -109,8 +110,9 @@ class PatchGANDiscriminator(nn.Module):
     def forward(self, x: Tensor) -> Tensor:
         if self._unsupported:
             raise NotImplementedError(self._unsupported)
-        if x.dim() != 5 or x.shape[1] != self.config.channels_in or self.config.channels_in != 1:
-            raise ValueError(f"PatchGANDiscriminator expects [N,1,D,H,W], got {tuple(x.shape)}")
+        if x.dim() != (4 if self.is_2D else 5) or x.shape[1] != self.config.channels_in or self.config.channels_in != 1:
+            raise ValueError(f"PatchGANDiscriminator expects [N,1,{'H,W' if self.is_2D else 'D,H,W'}], "
+                             f"got {tuple(x.shape)}")
         params = list(self.parameters())
         if torch.is_grad_enabled() and (x.requires_grad or any(p.requires_grad for p in params)):
             return _CriticFn.apply(x, self, *params)
@@ -119,7 +121,7 @@ class PatchGANDiscriminator(nn.Module):
         plan = self.plan_for(n, dims)
         logits = plan.forward(self._tensors(), x.detach().float().contiguous().view(n, *dims, 1), 0, n,
                               training=self.training)
-        return logits.clone().view(n, 1, *logits.shape[1:4])
+        return logits.clone().view(n, 1, *logits.shape[(2 if self.is_2D else 1):4])
 
 
 class _CriticFn(torch.autograd.Function):
@@ -131,7 +133,8 @@ class _CriticFn(torch.autograd.Function):
         xc = x.detach().float().contiguous().view(n, *dims, 1)
         logits = plan.forward(module._tensors(), xc, 0, n, training=module.training)
         ctx.plan, ctx.module, ctx.xc, ctx.needs_x = plan, module, xc, x.requires_grad
-        return logits.clone().view(n, 1, *logits.shape[1:4])
+        ctx.x_shape = x.shape
+        return logits.clone().view(n, 1, *logits.shape[(2 if module.is_2D else 1):4])
 
     @staticmethod
     def backward(ctx, grad_out):
@@ -152,7 +155,7 @@ class _CriticFn(torch.autograd.Function):
             plan.input_grad(module._tensors(), 0, n, dx if dx is not None else xc, 0, n if dx is not None else 0,
                             G=grads)
             plan.weight_grads(module._tensors(), grads, xc, n, n)
-        dxo = dx.view(n, 1, *xc.shape[1:4]) if dx is not None else None
+        dxo = dx.view(ctx.x_shape) if dx is not None else None
         if create_graph and dxo is not None:
             # dx as a differentiable function of the parameters (and of grad_out): the penalty's
             # double backward, _CriticInputGradFn.backward
@@ -200,7 +203,8 @@ class _CriticInputGradFn(torch.autograd.Function):
             d_go = None
             if ctx.needs_input_grad[1]:  # J gamma: the last conv (no bias) over nu_{L-1}
                 ly = plan.layers[-1]
-                geo = plan._geo(ops.conv_fwd_geom(n, ly.din, ly.dout, ly.cin, ly.cout, ly.k, ly.s, ly.p), plan.wf[-1])
+                geo = plan._geo(ops.conv_fwd_geom(n, ly.din, ly.dout, ly.cin, ly.cout, ly.k, ly.s, ly.p, planar=plan.pl),
+                                plan.wf[-1])
                 w = plan.wf[-1] if plan.wf[-1] is not None else P[f"{ly.name}.weight"]
                 out = torch.empty((n, *ly.dout, 1), device=gamma.device)
                 ops.conv(geo, plan.a[-2][:n], w, out)

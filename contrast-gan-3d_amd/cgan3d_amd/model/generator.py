@@ -25,6 +25,7 @@ class GenConfig:
     n_resnet_blocks: int = 4
     n_updownsample_blocks: int = 2
     init_channels_out: int = 16
+    is_2D: bool = False  # the 2-D variants (experiments/conf_2D.py): planar kernels, f32
 
 
 class ResnetGenerator(nn.Module):
@@ -32,10 +33,10 @@ class ResnetGenerator(nn.Module):
                  is_2D: bool = False, resnet_dropout_prob: float = 0.0, resnet_padding_mode: str = "zeros"):
         assert n_resnet_blocks > 0
         super().__init__()
-        self.config = GenConfig(n_resnet_blocks, n_updownsample_blocks, init_channels_out)
+        self.config = GenConfig(n_resnet_blocks, n_updownsample_blocks, init_channels_out, bool(is_2D))
         self.is_2D = is_2D
-        if is_2D or resnet_dropout_prob > 0 or resnet_padding_mode != "zeros":
-            self._unsupported = "2-D / dropout / non-zero resnet padding variants are outside the hot path"
+        if resnet_dropout_prob > 0 or resnet_padding_mode != "zeros":
+            self._unsupported = "dropout / non-zero resnet padding variants are not used by any reference config"
         else:
             self._unsupported = None
         common = {"kernel_size": 7, "padding_mode": "reflect", "padding": 3}
@@ -79,8 +80,8 @@ class ResnetGenerator(nn.Module):
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         if self._unsupported:
             raise NotImplementedError(self._unsupported)
-        if x.dim() != 5 or x.shape[1] != 1:
-            raise ValueError(f"ResnetGenerator expects [N,1,D,H,W], got {tuple(x.shape)}")
+        if x.dim() != (4 if self.is_2D else 5) or x.shape[1] != 1:
+            raise ValueError(f"ResnetGenerator expects [N,1,{'H,W' if self.is_2D else 'D,H,W'}], got {tuple(x.shape)}")
         params = [p for p in self.parameters()]
         if torch.is_grad_enabled() and any(p.requires_grad for p in params):
             return _GeneratorFn.apply(x, self, *params)

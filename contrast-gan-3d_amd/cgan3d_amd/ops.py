@@ -23,7 +23,7 @@ from ._lib import ConvGeom, Epilogue, PackDesc, check, ptr
 DRY_RUN = False
 
 
-def _geom(n, di, do, cin, cout, k, s, p, transposed, reflect, sa, sb) -> ConvGeom:
+def _geom(n, di, do, cin, cout, k, s, p, transposed, reflect, sa, sb, planar=False) -> ConvGeom:
     g = ConvGeom()
     g.n = n
     g.di, g.hi, g.wi = di
@@ -32,7 +32,13 @@ def _geom(n, di, do, cin, cout, k, s, p, transposed, reflect, sa, sb) -> ConvGeo
     g.transposed, g.reflect = int(transposed), int(reflect)
     g.w_sa, g.w_sb = sa, sb
     g.w_packed, g.prec = 0, L.PREC_F32
+    g.planar = int(planar)
     return g
+
+
+def taps(g) -> int:
+    """Kernel taps of a geometry: k^3, or k^2 for the 2-D variants (``planar``)."""
+    return g.k ** 2 if g.planar else g.k ** 3
 
 
 def uses_gemm(g: ConvGeom) -> bool:
@@ -40,6 +46,8 @@ def uses_gemm(g: ConvGeom) -> bool:
     packed weights and run in bf16); k7 single-channel and cout == 1 launches use direct kernels."""
     if g.cout < 2:
         return False
+    if g.planar:  # 2-D variants: every cout >= 2 role on the implicit GEMM
+        return True
     if g.cin == 1 and g.cout == 8 and g.k == 4 and g.stride == 2 and g.pad == 1 and not g.transposed:
         return False  # critic first layer: conv_c1.hip reads torch-layout weights
     return not (g.k == 7 and g.stride == 1 and g.cin == 1 and g.cout in (8, 16))
@@ -86,8 +94,8 @@ def with_prec(g: ConvGeom, prec: int) -> ConvGeom:
 def packed_elements(g: ConvGeom) -> int:
     """Elements (f32 or bf16) the pack kernel writes for ``g``."""
     if g.w_packed in (2, 3):
-        return g.k**3 * g.cin * g.cout
-    return g.k**3 * g.cin * ((g.cout + 3) // 4 * 4)
+        return taps(g) * g.cin * g.cout
+    return taps(g) * g.cin * ((g.cout + 3) // 4 * 4)
 
 
 def packed_weight_floats(g: ConvGeom) -> int:
@@ -99,7 +107,7 @@ def pack_desc(g: ConvGeom, w: torch.Tensor, wp: torch.Tensor) -> PackDesc:
     _need(wp, packed_weight_floats(g), "pack wp")
     d = PackDesc()
     d.w, d.wp, d.sa, d.sb = ptr(w), ptr(wp), g.w_sa, g.w_sb
-    d.taps, d.cin, d.cout, d.ldb = g.k**3, g.cin, g.cout, (g.cout + 3) // 4 * 4
+    d.taps, d.cin, d.cout, d.ldb = taps(g), g.cin, g.cout, (g.cout + 3) // 4 * 4
     d.format = g.w_packed
     return d
 
@@ -147,37 +155,38 @@ class PackSet:
 
 
 # --- geometry per role ------------------------------------------------------------------------
-# Conv3d(cin -> cout), weight [cout, cin, k,k,k]; din = input dims, dout = output dims
-def conv_fwd_geom(n, din, dout, cin, cout, k, s, p, reflect=False):
-    t = k**3
-    return _geom(n, din, dout, cin, cout, k, s, p, 0, reflect, t, cin * t)
+# Conv3d(cin -> cout), weight [cout, cin, k,k,k]; din = input dims, dout = output dims.
+# planar=True: the 2-D variants (Conv2d / ConvTranspose2d, weights [., ., k, k]) on dims (1, H, W)
+def conv_fwd_geom(n, din, dout, cin, cout, k, s, p, reflect=False, planar=False):
+    t = k**2 if planar else k**3
+    return _geom(n, din, dout, cin, cout, k, s, p, 0, reflect, t, cin * t, planar)
 
 
-def conv_dgrad_geom(n, din, dout, cin, cout, k, s, p):
-    t = k**3
-    return _geom(n, dout, din, cout, cin, k, s, p, 1, 0, cin * t, t)
+def conv_dgrad_geom(n, din, dout, cin, cout, k, s, p, planar=False):
+    t = k**2 if planar else k**3
+    return _geom(n, dout, din, cout, cin, k, s, p, 1, 0, cin * t, t, planar)
 
 
-def conv_wgrad_geom(n, din, dout, cin, cout, k, s, p, reflect=False):
-    t = k**3
-    return _geom(n, din, dout, cin, cout, k, s, p, 0, reflect, t, cin * t)
+def conv_wgrad_geom(n, din, dout, cin, cout, k, s, p, reflect=False, planar=False):
+    t = k**2 if planar else k**3
+    return _geom(n, din, dout, cin, cout, k, s, p, 0, reflect, t, cin * t, planar)
 
 
 # ConvTranspose3d(cin -> cout), weight [cin, cout, k,k,k]; din = input dims, dout = output dims
-def convt_fwd_geom(n, din, dout, cin, cout, k, s, p):
-    t = k**3
-    return _geom(n, din, dout, cin, cout, k, s, p, 1, 0, cout * t, t)
+def convt_fwd_geom(n, din, dout, cin, cout, k, s, p, planar=False):
+    t = k**2 if planar else k**3
+    return _geom(n, din, dout, cin, cout, k, s, p, 1, 0, cout * t, t, planar)
 
 
-def convt_dgrad_geom(n, din, dout, cin, cout, k, s, p):
-    t = k**3
-    return _geom(n, dout, din, cout, cin, k, s, p, 0, 0, t, cout * t)
+def convt_dgrad_geom(n, din, dout, cin, cout, k, s, p, planar=False):
+    t = k**2 if planar else k**3
+    return _geom(n, dout, din, cout, cin, k, s, p, 0, 0, t, cout * t, planar)
 
 
-def convt_wgrad_geom(n, din, dout, cin, cout, k, s, p):
+def convt_wgrad_geom(n, din, dout, cin, cout, k, s, p, planar=False):
     """gathered operand = the ConvTranspose output-grad; aligned operand = its input."""
-    t = k**3
-    return _geom(n, dout, din, cout, cin, k, s, p, 0, 0, t, cout * t)
+    t = k**2 if planar else k**3
+    return _geom(n, dout, din, cout, cin, k, s, p, 0, 0, t, cout * t, planar)
 
 
 class Epi:
@@ -242,7 +251,7 @@ def _vox_out(g):
 
 
 def _w_extent(g):
-    return (g.cin - 1) * g.w_sa + (g.cout - 1) * g.w_sb + g.k**3
+    return (g.cin - 1) * g.w_sa + (g.cout - 1) * g.w_sb + taps(g)
 
 
 def _launch(name, *args):
@@ -450,7 +459,7 @@ def wgrad(g: ConvGeom, gathered, aligned, dw, ws, accumulate=False, gathered16=N
         raise ValueError("wgrad: defer_unpack needs ws_clean")
     _need(gathered, _vox_in(g) * g.cin, "wgrad gathered")
     _need(aligned, _vox_out(g) * g.cout, "wgrad aligned")
-    _need(dw, g.cin * g.cout * g.k**3, "wgrad dw")
+    _need(dw, g.cin * g.cout * taps(g), "wgrad dw")
     if _w_extent(g) > dw.numel():
         raise ValueError("wgrad: weight strides exceed dw")
     _need(ws, wgrad_ws_floats(g), "wgrad ws", exact=False)
@@ -624,7 +633,7 @@ class UnpackSet:
         """items: [(geometry, ws, dw, accumulate)]; every ws / dw keeps its address."""
         descs, self.keep = [], []
         for g, ws, dw, acc in items:
-            t = g.k ** 3
+            t = taps(g)
             _need(ws, t * g.cin * g.cout, "UnpackSet ws", exact=False)
             _need(dw, g.cin * g.cout * t, "UnpackSet dw")
             d = L.UnpackDesc()
@@ -633,7 +642,7 @@ class UnpackSet:
             descs.append(d)
             self.keep += [ws, dw]
         self.n = len(descs)
-        self.max_total = max(g.k ** 3 * g.cin * g.cout for g, _, _, _ in items)
+        self.max_total = max(taps(g) * g.cin * g.cout for g, _, _, _ in items)
         self.dev = torch.frombuffer(bytearray(b"".join(bytes(d) for d in descs)), dtype=torch.uint8).to(device)
 
     def run(self):
@@ -705,9 +714,22 @@ def ln_apply(mode, n, L_, slope, out, **kw):
     check(_launch("cgan3d_ln_apply", ctypes.byref(a), ptr(out)), "ln_apply")
 
 
-def reflect_fold(padded, out, n, dims: Sequence[int], c, pad, ep: Optional[Epi] = None):
-    """Adjoint of reflection padding; ``ep.bn_gsum`` adds the fused BatchNorm backward statistics."""
+def reflect_fold(padded, out, n, dims: Sequence[int], c, pad, ep: Optional[Epi] = None, planar: bool = False):
+    """Adjoint of reflection padding; ``ep.bn_gsum`` adds the fused BatchNorm backward statistics.
+    ``planar``: dims (1, H, W) of the 2-D variants, padded in H and W only."""
     d, h, w = dims
+    if planar:
+        if d != 1:
+            raise ValueError("reflect_fold: planar dims must be (1, H, W)")
+        _need(padded, n * (h + 2 * pad) * (w + 2 * pad) * c, "reflect_fold2d padded")
+        _need(out, n * h * w * c, "reflect_fold2d out")
+        if ep is not None and ep.bn_mode:
+            if ep.bn_slots != reflect_fold_slots(n, dims, c):
+                raise ValueError("reflect_fold: bn_slots != reflect_fold_slots()")
+            ep.check_bn(n * h * w * c, c, "reflect_fold2d")
+        check(_launch("cgan3d_reflect_fold2d", ptr(padded), ptr(out), n, h, w, c, pad,
+                      ctypes.byref(ep.c()) if ep is not None else None), "reflect_fold2d")
+        return
     _need(padded, n * (d + 2 * pad) * (h + 2 * pad) * (w + 2 * pad) * c, "reflect_fold padded")
     _need(out, n * d * h * w * c, "reflect_fold out")
     if ep is None:

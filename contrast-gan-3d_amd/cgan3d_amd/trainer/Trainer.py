@@ -26,7 +26,7 @@ import torch
 from torch import Tensor, nn
 
 from .. import _lib as L
-from ..engine import Arena, StepEngine
+from ..engine import Arena, StepEngine, _planar_dims
 from ..model.loss import WassersteinLoss, ZNCCLoss
 from .optim import FusedAdam, adam_hyper_from_partial
 
@@ -96,6 +96,7 @@ class Trainer:
     # ------------------------------------------------------------------------------------------
     def _engine_for(self, b_opt: int, b_sub: int, dims) -> StepEngine:
         e = self.engine
+        dims = _planar_dims(dims, bool(getattr(self.generator.config, "is_2D", False)))  # 2-D: (1, H, W)
         if e is None or (e.b_opt, e.b_sub, e.dims) != (b_opt, b_sub, tuple(dims)):
             lo, hi = _hu_bounds(self.loss_HU)
             self.engine = StepEngine(self.generator, self.critic, self.generator.config, self.critic.config, b_opt,

@@ -102,6 +102,13 @@ __device__ __forceinline__ int reflect_idx(int i, int n) {
 
 inline int ceil_div(long long a, long long b) { return (int)((a + b - 1) / b); }
 
+// taps of a geometry's kernel: k^3, or k^2 for the 2-D variants (cgan3d_conv_geom.planar)
+inline int geom_taps(const cgan3d_conv_geom* g) { return g->planar ? g->k * g->k : g->k * g->k * g->k; }
+// depth-axis kernel extent / stride / pad: the 2-D variants pass depth through (1, 1, 0)
+inline int geom_kd(const cgan3d_conv_geom* g) { return g->planar ? 1 : g->k; }
+inline int geom_sd(const cgan3d_conv_geom* g) { return g->planar ? 1 : g->stride; }
+inline int geom_pd(const cgan3d_conv_geom* g) { return g->planar ? 0 : g->pad; }
+
 // device-side view of cgan3d_epilogue
 struct Epi {
   const float* bias;

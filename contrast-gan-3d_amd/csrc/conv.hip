@@ -17,6 +17,7 @@ namespace cg {
 
 struct ConvArgs {
   int n, di, hi, wi, do_, ho, wo, cin, cout, k, s, p, transposed, reflect;
+  int kd, sd, pd;          // depth-axis kernel / stride / pad: (k, s, p), or (1, 1, 0) for planar (2-D)
   long long sa, sb;
   int cd, ch, cw;          // grid walked by the tiles: output grid, or one parity class
   long long class_vox;     // voxels per class (or all output voxels)
@@ -29,10 +30,11 @@ static bool make_args(const cgan3d_conv_geom* g, ConvArgs* a, int bm) {
   a->do_ = g->do_; a->ho = g->ho; a->wo = g->wo; a->cin = g->cin; a->cout = g->cout;
   a->k = g->k; a->s = g->stride; a->p = g->pad; a->transposed = g->transposed; a->reflect = g->reflect;
   a->sa = g->w_sa; a->sb = g->w_sb;
+  a->kd = geom_kd(g); a->sd = geom_sd(g); a->pd = geom_pd(g);
   if (g->transposed && g->stride > 1) {
-    if (g->do_ % g->stride || g->ho % g->stride || g->wo % g->stride) return false;
-    a->cd = g->do_ / g->stride; a->ch = g->ho / g->stride; a->cw = g->wo / g->stride;
-    a->nclass = g->stride * g->stride * g->stride;
+    if (g->do_ % a->sd || g->ho % g->stride || g->wo % g->stride) return false;
+    a->cd = g->do_ / a->sd; a->ch = g->ho / g->stride; a->cw = g->wo / g->stride;
+    a->nclass = a->sd * g->stride * g->stride;
   } else {
     a->cd = g->do_; a->ch = g->ho; a->cw = g->wo; a->nclass = 1;
   }
@@ -45,14 +47,16 @@ static int validate(const cgan3d_conv_geom* g, const char* who) {
   CG_CHECK_ARG(g != nullptr, "%s: null geometry", who);
   CG_CHECK_ARG(g->n > 0 && g->di > 0 && g->hi > 0 && g->wi > 0 && g->do_ > 0 && g->ho > 0 && g->wo > 0,
                "%s: non-positive dims", who);
-  CG_CHECK_ARG(g->cin > 0 && g->cout > 0 && g->cout <= 64, "%s: channels cin=%d cout=%d (cout<=64)", who,
-               g->cin, g->cout);
+  CG_CHECK_ARG(g->cin > 0 && g->cout > 0 && (g->cout <= 64 || g->planar), "%s: channels cin=%d cout=%d (cout<=64)",
+               who, g->cin, g->cout);
+  CG_CHECK_ARG(!g->planar || (g->di == 1 && g->do_ == 1 && g->prec == CGAN3D_PREC_F32 && g->w_packed <= 1),
+               "%s: planar (2-D) geometries have di == do_ == 1 and run in f32 with w_packed 0 or 1", who);
   CG_CHECK_ARG(g->k > 0 && g->k <= 7 && g->stride >= 1 && g->stride <= 2 && g->pad >= 0 && g->pad < g->k,
                "%s: kernel k=%d s=%d p=%d unsupported", who, g->k, g->stride, g->pad);
   CG_CHECK_ARG(!(g->reflect && g->transposed), "%s: reflect padding only in forward mapping", who);
-  CG_CHECK_ARG(!g->reflect || (g->pad < g->di && g->pad < g->hi && g->pad < g->wi),
+  CG_CHECK_ARG(!g->reflect || ((g->planar || g->pad < g->di) && g->pad < g->hi && g->pad < g->wi),
                "%s: reflect pad %d >= dim", who, g->pad);
-  if (!g->transposed) {
+  if (!g->transposed && !g->planar) {
     CG_CHECK_ARG((long long)(g->do_ - 1) * g->stride - g->pad + g->k - 1 < (long long)g->di + g->pad &&
                  (long long)(g->ho - 1) * g->stride - g->pad + g->k - 1 < (long long)g->hi + g->pad &&
                  (long long)(g->wo - 1) * g->stride - g->pad + g->k - 1 < (long long)g->wi + g->pad,
@@ -96,7 +100,7 @@ __device__ __forceinline__ int gcoord(int base, int off, int n, int reflect) {
 __global__ __launch_bounds__(256) void conv_cout1_wave_kernel(ConvArgs a, const float* __restrict__ x,
                                                               const float* __restrict__ w, float* y, Epi ep) {
   extern __shared__ __attribute__((aligned(16))) float Ws[];  // [T][cin]
-  const int T = a.k * a.k * a.k;
+  const int T = a.kd * a.k * a.k;
   // weights staged in source order (ci major, taps contiguous when sa == T: coalesced), 8 loads in
   // flight per thread, transposed into [t][cin] on the LDS side
   for (int i0 = threadIdx.x; i0 < T * a.cin; i0 += 8 * blockDim.x) {
@@ -119,7 +123,7 @@ __global__ __launch_bounds__(256) void conv_cout1_wave_kernel(ConvArgs a, const 
   int ow = (int)(lin % a.wo); long long tt = lin / a.wo;
   int oh = (int)(tt % a.ho); tt /= a.ho;
   int od = (int)(tt % a.do_); int nb = (int)(tt / a.do_);
-  const int bd = od * a.s - a.p, bh = oh * a.s - a.p, bw = ow * a.s - a.p;
+  const int bd = od * a.sd - a.pd, bh = oh * a.s - a.p, bw = ow * a.s - a.p;
   const int C4 = a.cin >> 2, R4 = T * C4;
   float acc = 0.f;
 #pragma unroll 4
@@ -150,7 +154,7 @@ __global__ __launch_bounds__(256) void conv_cout1_wave_kernel(ConvArgs a, const 
 __global__ __launch_bounds__(256) void conv_cout1_kernel(ConvArgs a, const float* __restrict__ x,
                                                          const float* __restrict__ w, float* y, Epi ep) {
   extern __shared__ __attribute__((aligned(16))) float Ws[];  // [T][cin]
-  const int T = a.k * a.k * a.k;
+  const int T = a.kd * a.k * a.k;
   for (int i = threadIdx.x; i < T * a.cin; i += blockDim.x) {
     int t = i / a.cin, ci = i - t * a.cin;
     Ws[i] = w[(long long)ci * a.sa + t];
@@ -164,19 +168,19 @@ __global__ __launch_bounds__(256) void conv_cout1_kernel(ConvArgs a, const float
   int rd = 0, rh = 0, rw = 0;
   if (a.transposed) { rd = cls / (s * s); rh = (cls / s) % s; rw = cls % s; }
   int fd, sd, nd, fh, sh, nh, fw, sw, nw;
-  class_taps(rd, k, s, p, a.transposed, &fd, &sd, &nd);
+  class_taps(rd, a.kd, a.sd, a.pd, a.transposed, &fd, &sd, &nd);
   class_taps(rh, k, s, p, a.transposed, &fh, &sh, &nh);
   class_taps(rw, k, s, p, a.transposed, &fw, &sw, &nw);
   int jw = (int)(lin % a.cw); long long tt = lin / a.cw;
   int jh = (int)(tt % a.ch); tt /= a.ch;
   int jd = (int)(tt % a.cd); int nb = (int)(tt / a.cd);
   int od, oh, ow, bd, bh, bw;
-  if (a.transposed) { od = jd * s + rd; oh = jh * s + rh; ow = jw * s + rw; bd = jd; bh = jh; bw = jw; }
-  else { od = jd; oh = jh; ow = jw; bd = jd * s - p; bh = jh * s - p; bw = jw * s - p; }
+  if (a.transposed) { od = jd * a.sd + rd; oh = jh * s + rh; ow = jw * s + rw; bd = jd; bh = jh; bw = jw; }
+  else { od = jd; oh = jh; ow = jw; bd = jd * a.sd - a.pd; bh = jh * s - p; bw = jw * s - p; }
   float acc = 0.f;
   for (int md = 0; md < nd; ++md) {
     const int td = fd + sd * md;
-    const int id = gcoord(bd, a.transposed ? (rd + p - td) / s : td, a.di, a.reflect);
+    const int id = gcoord(bd, a.transposed ? (rd + a.pd - td) / a.sd : td, a.di, a.reflect);
     if (id < 0) continue;
     for (int mh = 0; mh < nh; ++mh) {
       const int th = fh + sh * mh;
@@ -225,8 +229,9 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(ConvArgs a, const float
   __shared__ int vtab[5][KV];                                  // n*di, bd, bh, bw, aligned voxel
 
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int R = a.k * a.k * a.k * a.cin;
+  const int R = a.kd * a.k * a.k * a.cin;
   const int r0 = blockIdx.x * 64;
+  const int co0 = blockIdx.z * 64;  // output-channel block (cout > 64: the 2-D critic's 128 channels)
   if (tid < 64) {
     int r = r0 + tid;
     if (r < R) {
@@ -252,7 +257,7 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(ConvArgs a, const float
         int ow = (int)(lin % a.wo); long long t = lin / a.wo;
         int oh = (int)(t % a.ho); t /= a.ho;
         int od = (int)(t % a.do_); int nb = (int)(t / a.do_);
-        vtab[0][tid] = nb * a.di; vtab[1][tid] = od * a.s - a.p; vtab[2][tid] = oh * a.s - a.p;
+        vtab[0][tid] = nb * a.di; vtab[1][tid] = od * a.sd - a.pd; vtab[2][tid] = oh * a.s - a.p;
         vtab[3][tid] = ow * a.s - a.p; vtab[4][tid] = (int)lin;
       } else {
         vtab[0][tid] = -1; vtab[4][tid] = -1;
@@ -298,7 +303,8 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(ConvArgs a, const float
         const int v = (tid >> 4) + 16 * i;
         f32x4 val = {0.f, 0.f, 0.f, 0.f};
         const int ov = vtab[4][v];
-        if (ov >= 0 && 4 * c4 < a.cout) val = *reinterpret_cast<const f32x4*>(go + (long long)ov * a.cout + 4 * c4);
+        if (ov >= 0 && co0 + 4 * c4 < a.cout)
+          val = *reinterpret_cast<const f32x4*>(go + (long long)ov * a.cout + co0 + 4 * c4);
         *reinterpret_cast<f32x4*>(&Gs[v * LD + 4 * c4]) = val;
       }
     }
@@ -317,7 +323,7 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(ConvArgs a, const float
   // D[row = 4g + j][col = r16]: row -> r = r0 + 16*wave + 4g + j, col -> b = 16n + r16
 #pragma unroll
   for (int n = 0; n < NB; ++n) {
-    const int b = 16 * n + r16;
+    const int b = co0 + 16 * n + r16;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int r = r0 + 16 * wave + 4 * g + j;
@@ -335,7 +341,7 @@ __global__ __launch_bounds__(256) void conv_wgrad_cout1_kernel(ConvArgs a, const
   __shared__ int vtab[5][VB];
   __shared__ float gv[VB];
   const int tid = threadIdx.x;
-  const int R4 = a.k * a.k * a.k * a.cin / 4;
+  const int R4 = a.kd * a.k * a.k * a.cin / 4;
   int td[MAXJ], th[MAXJ], tw[MAXJ], ca[MAXJ];
   f32x4 acc[MAXJ];
 #pragma unroll
@@ -360,7 +366,7 @@ __global__ __launch_bounds__(256) void conv_wgrad_cout1_kernel(ConvArgs a, const
         int ow = (int)(lin % a.wo); long long t = lin / a.wo;
         int oh = (int)(t % a.ho); t /= a.ho;
         int od = (int)(t % a.do_); int nb = (int)(t / a.do_);
-        vtab[0][tid] = nb * a.di; vtab[1][tid] = od * a.s - a.p; vtab[2][tid] = oh * a.s - a.p;
+        vtab[0][tid] = nb * a.di; vtab[1][tid] = od * a.sd - a.pd; vtab[2][tid] = oh * a.s - a.p;
         vtab[3][tid] = ow * a.s - a.p;
         gv[tid] = go[lin];
       } else {
@@ -450,6 +456,11 @@ extern "C" int64_t cgan3d_conv3d_bn_slots(const cgan3d_conv_geom* g) {
 
 extern "C" int64_t cgan3d_conv3d_stats_floats(const cgan3d_conv_geom* g) {
   if (!g) return -1;
+  if (g->planar) {  // 2-D variants: the implicit GEMM (cout >= 2) only
+    long long mb = 0;
+    if (g->cout < 2 || gemm_blocks(g, &mb)) return g->cout < 2 ? 0 : -1;
+    return (int64_t)mb * (2 * g->cout + 1);
+  }
   if (long long kb = k7_n2w_blocks(g)) return (int64_t)kb * (2 * g->cout + 1);
   if (sk_ok(g)) return (int64_t)sk_blocks(g) * (2 * g->cout + 1);
   if (halo_ok(g)) return (int64_t)halo_mblocks(g) * (2 * g->cout + 1);
@@ -478,8 +489,16 @@ extern "C" int cgan3d_conv3d_fwd(const cgan3d_conv_geom* g, const float* x, cons
                  "cgan3d_conv3d_fwd: bn_fold needs bn_mode 2 on a k7 bf16 input-grad geometry");
   }
   hipStream_t s = (hipStream_t)stream;
-  CG_CHECK_ARG(!g->w_packed || (g->cout > 1 && !(g->k == 7 && g->stride == 1 && g->cin == 1)),
+  CG_CHECK_ARG(!g->w_packed || (g->cout > 1 && (g->planar || !(g->k == 7 && g->stride == 1 && g->cin == 1))),
                "cgan3d_conv3d_fwd: packed weights only for the implicit-GEMM path");
+  if (g->planar && g->cout > 1) {  // 2-D variants: the generic implicit GEMM for every cout >= 2 role
+    CG_CHECK_ARG(!e.out2 && !e.x16 && !e.bn_fold, "cgan3d_conv3d_fwd: planar geometry epilogue");
+    int rc = gemm_launch(g, x, w, y, e, s);
+    if (rc) return rc;
+    CG_LAUNCH_CHECK("conv_gemm_kernel");
+    return CGAN3D_OK;
+  }
+  if (g->planar) goto cout1;  // cout == 1: the VALU kernels below
   if (c1_fwd_ok(g) || c1_dgrad_ok(g)) {  // critic first layer (conv_c1.hip)
     CG_CHECK_ARG(!e.bn_mode, "cgan3d_conv3d_fwd: no BatchNorm statistics on the single-channel critic layer");
     const int rc = g->transposed ? c1_dgrad_launch(g, x, w, y, e, s) : c1_fwd_launch(g, x, w, y, e, s);
@@ -491,11 +510,12 @@ extern "C" int cgan3d_conv3d_fwd(const cgan3d_conv_geom* g, const float* x, cons
     CG_LAUNCH_CHECK("k7 conv");
     return CGAN3D_OK;
   }
+cout1:
   if (g->cout == 1) {
-    CG_CHECK_ARG(!e.stats, "cgan3d_conv3d_fwd: stats unsupported for cout==1");
+    CG_CHECK_ARG(!e.stats && !e.bn_mode, "cgan3d_conv3d_fwd: stats unsupported for cout==1");
     ConvArgs a;
     CG_CHECK_ARG(make_args(g, &a, 256), "cgan3d_conv3d_fwd: transposed output dims must divide stride");
-    size_t lds = (size_t)g->k * g->k * g->k * g->cin * sizeof(float);
+    size_t lds = (size_t)geom_taps(g) * g->cin * sizeof(float);
     CG_CHECK_ARG(lds <= 64 * 1024, "cgan3d_conv3d_fwd: cout==1 weights exceed LDS");
     if (!g->transposed && g->cin % 4 == 0 && a.class_vox <= 16384) {  // few outputs, long reductions
       ::cg::launch(conv_cout1_wave_kernel, dim3(cg::ceil_div(a.class_vox, 4)), dim3(256), lds, s, a, x, w, y, e);
@@ -538,6 +558,7 @@ static long long wgrad_vpb(long long V, int gx_blocks) {
 
 extern "C" int64_t cgan3d_conv3d_wgrad_ws_floats(const cgan3d_conv_geom* g) {
   if (!g) return -1;
+  if (g->planar) return (int64_t)geom_taps(g) * g->cin * g->cout;
   return std::max<int64_t>(std::max<int64_t>((int64_t)g->k * g->k * g->k * g->cin * g->cout, k7_wgrad_ws_floats(g)),
                            std::max<int64_t>(wgrad_k3_ws_floats(g), wgrad_s2_ws_floats(g)));
 }
@@ -550,6 +571,7 @@ extern "C" int cgan3d_conv3d_wgrad(const cgan3d_conv_geom* g, const float* gathe
 // 1 if the weight gradient of `g` sums into the workspace by atomics (then zeroed by a memset,
 // or kept clean under CGAN3D_WGRAD_WS_CLEAN), 0 if it needs no zeroed workspace
 static int wgrad_ws_atomic(const cgan3d_conv_geom* g) {
+  if (g->planar) return 1;
   return !k7_wgrad_handles(g) && !c1_wgrad_ok(g) && !wgrad_c1_ok(g) && !wgrad_s2_ok(g) && !wgrad_k3_ok(g);
 }
 
@@ -559,11 +581,11 @@ extern "C" int cgan3d_conv3d_wgrad_ws_mode(const cgan3d_conv_geom* g) {
 }
 
 extern "C" int32_t cgan3d_conv3d_bn_fold_ok(const cgan3d_conv_geom* g) {
-  return g && !validate(g, "cgan3d_conv3d_bn_fold_ok") && k7m_fold_ok(g) ? 1 : 0;
+  return g && !validate(g, "cgan3d_conv3d_bn_fold_ok") && !g->planar && k7m_fold_ok(g) ? 1 : 0;
 }
 
 extern "C" int32_t cgan3d_conv3d_shadow_only(const cgan3d_conv_geom* g, int32_t role) {
-  if (!g || validate(g, "cgan3d_conv3d_shadow_only")) return 0;
+  if (!g || validate(g, "cgan3d_conv3d_shadow_only") || g->planar) return 0;
   if (role == 0)  // stride-2 16 <-> 32 kernels (conv_s2.hip), the 16 -> 1 k7 forward (conv_k7_mfma.hip)
     return (g->w_packed == 2 && s2_kind(g) != 0) || k7m_w2n_taken(g) ? 1 : 0;
   if (role != 1 || g->transposed) return 0;
@@ -595,9 +617,10 @@ extern "C" int cgan3d_conv3d_wgrad_ex(const cgan3d_conv_geom* g, const float* ga
   hipStream_t s = (hipStream_t)stream;
   ConvArgs a;
   make_args(g, &a, 64);
-  const int T = g->k * g->k * g->k;
+  const int T = geom_taps(g);
   const long long R = (long long)T * g->cin;
   const long long V = (long long)g->n * g->do_ * g->ho * g->wo;
+  if (g->planar) goto generic;  // 2-D variants: the generic f32 weight-gradient kernels below
   if (g->k == 7 && g->stride == 1 && (g->cin == 1 || g->cout == 1)) {
     if (!accumulate && ::cg::memset_async(dw, 0, R * g->cout * sizeof(float), s) != hipSuccess) {
       set_error("cgan3d_conv3d_wgrad: memset failed");
@@ -644,6 +667,7 @@ extern "C" int cgan3d_conv3d_wgrad_ex(const cgan3d_conv_geom* g, const float* ga
     CG_LAUNCH_CHECK("wgrad_k3_kernel");
     return CGAN3D_OK;
   }
+generic:
   if (!ws_clean && ::cg::memset_async(ws, 0, R * g->cout * sizeof(float), s) != hipSuccess) {
     set_error("cgan3d_conv3d_wgrad: memset failed");
     return CGAN3D_EHIP;
@@ -662,15 +686,16 @@ extern "C" int cgan3d_conv3d_wgrad_ex(const cgan3d_conv_geom* g, const float* ga
     dim3 grid(cg::ceil_div(V, vpb), gy);
     ::cg::launch((conv_wgrad_cout1_kernel<1>), grid, dim3(256), 0, s, a, gathered, aligned, ws, vpb);
     CG_LAUNCH_CHECK("conv_wgrad_cout1_kernel");
-  } else if (wgrad_bf16_ok(g)) {
+  } else if (!g->planar && wgrad_bf16_ok(g)) {
     int rc = wgrad_bf16_launch(g, gathered, aligned, ws, s);
     if (rc) return rc;
     CG_LAUNCH_CHECK("conv_wgrad_bf16_kernel");
   } else {
     const int gxb = cg::ceil_div(R, 64);
-    long long vpb = wgrad_vpb(V, gxb);
-    dim3 grid(gxb, cg::ceil_div(V, vpb));
-    const int nb = (g->cout + 15) / 16;
+    const int gz = cg::ceil_div(g->cout, 64);  // 64-channel blocks (cout > 64: 2-D critic)
+    long long vpb = wgrad_vpb(V, gxb * gz);
+    dim3 grid(gxb, cg::ceil_div(V, vpb), gz);
+    const int nb = std::min(4, (g->cout + 15) / 16);
     const bool v4 = (g->cin % 4) == 0;
 #define CG_LAUNCH_WG(VV, N) ::cg::launch((conv_wgrad_kernel<VV, N>), grid, dim3(256), 0, s, a, gathered, aligned, ws, vpb)
     if (v4) {

@@ -22,6 +22,7 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
 struct GemmArgs {
   int n, di, hi, wi, do_, ho, wo, cin, cout, k, s, p, transposed, reflect;
+  int kd, sd, pd;  // depth-axis kernel / stride / pad: (k, s, p), or (1, 1, 0) for planar (2-D)
   long long sa, sb;
   int packed, ldb;
   int cd, ch, cw;
@@ -51,8 +52,9 @@ static GemmCfg gemm_cfg(const cgan3d_conv_geom* g) {
   const int nbt = g->cout <= 16 ? 1 : (g->cout <= 32 ? 2 : 4);
   long long cls = 1, cv;
   if (g->transposed && g->stride > 1) {
-    cls = (long long)g->stride * g->stride * g->stride;
-    cv = (long long)g->n * (g->do_ / g->stride) * (g->ho / g->stride) * (g->wo / g->stride);
+    const int sd = geom_sd(g);
+    cls = (long long)sd * g->stride * g->stride;
+    cv = (long long)g->n * (g->do_ / sd) * (g->ho / g->stride) * (g->wo / g->stride);
   } else {
     cv = (long long)g->n * g->do_ * g->ho * g->wo;
   }
@@ -60,7 +62,7 @@ static GemmCfg gemm_cfg(const cgan3d_conv_geom* g) {
   if (blocks64 < g_small_tile_below && g->cout > 16) {
     c.wm = 2; c.nbw = 1; c.bm = 32; c.bn = 32; c.gy = (g->cout + 31) / 32;
   } else {
-    c.wm = 4; c.nbw = nbt; c.bm = 64; c.bn = 16 * nbt; c.gy = 1;
+    c.wm = 4; c.nbw = nbt; c.bm = 64; c.bn = 16 * nbt; c.gy = (g->cout + c.bn - 1) / c.bn;  // > 1: cout > 64
   }
   return c;
 }
@@ -70,10 +72,11 @@ static bool gemm_args(const cgan3d_conv_geom* g, const GemmCfg& c, GemmArgs* a) 
   a->do_ = g->do_; a->ho = g->ho; a->wo = g->wo; a->cin = g->cin; a->cout = g->cout;
   a->k = g->k; a->s = g->stride; a->p = g->pad; a->transposed = g->transposed; a->reflect = g->reflect;
   a->sa = g->w_sa; a->sb = g->w_sb; a->packed = g->w_packed; a->ldb = (g->cout + 3) / 4 * 4;
+  a->kd = geom_kd(g); a->sd = geom_sd(g); a->pd = geom_pd(g);
   if (g->transposed && g->stride > 1) {
-    if (g->do_ % g->stride || g->ho % g->stride || g->wo % g->stride) return false;
-    a->cd = g->do_ / g->stride; a->ch = g->ho / g->stride; a->cw = g->wo / g->stride;
-    a->nclass = g->stride * g->stride * g->stride;
+    if (g->do_ % a->sd || g->ho % g->stride || g->wo % g->stride) return false;
+    a->cd = g->do_ / a->sd; a->ch = g->ho / g->stride; a->cw = g->wo / g->stride;
+    a->nclass = a->sd * g->stride * g->stride;
   } else {
     a->cd = g->do_; a->ch = g->ho; a->cw = g->wo; a->nclass = 1;
   }
@@ -118,13 +121,15 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(GemmArgs a, const float*
   int rd = 0, rh = 0, rw = 0;
   if (a.transposed) { rd = cls / (s * s); rh = (cls / s) % s; rw = cls % s; }
   int f[3], st[3], cnt[3];
+  const int sq[3] = {a.sd, s, s}, pq[3] = {a.pd, p, p}, kq[3] = {a.kd, k, k};
   {
     const int r3[3] = {rd, rh, rw};
     for (int q = 0; q < 3; ++q) {
       if (a.transposed) {
-        f[q] = (r3[q] + p) % s; st[q] = s; cnt[q] = f[q] < k ? (k - f[q] + s - 1) / s : 0;
+        f[q] = (r3[q] + pq[q]) % sq[q]; st[q] = sq[q];
+        cnt[q] = f[q] < kq[q] ? (kq[q] - f[q] + sq[q] - 1) / sq[q] : 0;
       } else {
-        f[q] = 0; st[q] = 1; cnt[q] = k;
+        f[q] = 0; st[q] = 1; cnt[q] = kq[q];
       }
     }
   }
@@ -134,7 +139,7 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(GemmArgs a, const float*
     const int mw = j % cnt[2], mh = (j / cnt[2]) % cnt[1], md = j / (cnt[1] * cnt[2]);
     const int td = f[0] + st[0] * md, th = f[1] + st[1] * mh, tw = f[2] + st[2] * mw;
     if (a.transposed) {
-      tap_off[0][j] = (rd + p - td) / s; tap_off[1][j] = (rh + p - th) / s; tap_off[2][j] = (rw + p - tw) / s;
+      tap_off[0][j] = (rd + a.pd - td) / a.sd; tap_off[1][j] = (rh + p - th) / s; tap_off[2][j] = (rw + p - tw) / s;
     } else {
       tap_off[0][j] = td; tap_off[1][j] = th; tap_off[2][j] = tw;
     }
@@ -149,11 +154,11 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(GemmArgs a, const float*
       const int jd = (int)(t % a.cd); const int nb = (int)(t / a.cd);
       int od, oh, ow;
       if (a.transposed) {
-        od = jd * s + rd; oh = jh * s + rh; ow = jw * s + rw;
+        od = jd * a.sd + rd; oh = jh * s + rh; ow = jw * s + rw;
         row_b[0][tid] = jd; row_b[1][tid] = jh; row_b[2][tid] = jw;
       } else {
         od = jd; oh = jh; ow = jw;
-        row_b[0][tid] = jd * s - p; row_b[1][tid] = jh * s - p; row_b[2][tid] = jw * s - p;
+        row_b[0][tid] = jd * a.sd - a.pd; row_b[1][tid] = jh * s - p; row_b[2][tid] = jw * s - p;
       }
       row_n[tid] = nb * a.di;
       row_out[tid] = ((nb * a.do_ + od) * a.ho + oh) * a.wo + ow;
@@ -569,20 +574,21 @@ using namespace cg;
 
 extern "C" int64_t cgan3d_packed_weight_floats(const cgan3d_conv_geom* g) {
   if (!g) return -1;
-  if (g->w_packed == 2 || g->w_packed == 3) return ((int64_t)g->k * g->k * g->k * g->cin * g->cout + 1) / 2;  // bf16
-  return (int64_t)g->k * g->k * g->k * g->cin * ((g->cout + 3) / 4 * 4);
+  if (g->w_packed == 2 || g->w_packed == 3) return ((int64_t)geom_taps(g) * g->cin * g->cout + 1) / 2;  // bf16
+  return (int64_t)geom_taps(g) * g->cin * ((g->cout + 3) / 4 * 4);
 }
 
 extern "C" int cgan3d_pack_weights(const cgan3d_conv_geom* g, const float* w, float* wp, void* stream) {
   CG_CHECK_ARG(g && w && wp, "cgan3d_pack_weights: null pointer");
   CG_CHECK_ARG(g->w_packed != 3, "cgan3d_pack_weights: format 3 is packed by cgan3d_pack_weights_multi");
+  CG_CHECK_ARG(!g->planar || g->w_packed == 1, "cgan3d_pack_weights: planar geometries use format 1");
   if (g->w_packed == 2) {
     CG_CHECK_ARG(halo_format_ok(g), "cgan3d_pack_weights: geometry not halo-eligible");
     halo_pack(g, w, wp, (hipStream_t)stream);
     CG_LAUNCH_CHECK("pack_halo_kernel");
     return CGAN3D_OK;
   }
-  const int T = g->k * g->k * g->k, ldb = (g->cout + 3) / 4 * 4;
+  const int T = geom_taps(g), ldb = (g->cout + 3) / 4 * 4;
   const long long total = (long long)T * g->cin * ldb;
   int blocks = (int)std::min<long long>((total + 255) / 256, 2048);
   ::cg::launch(pack_weights_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, w, wp, T, g->cin, g->cout,
@@ -599,10 +605,13 @@ extern "C" int cgan3d_pack_weights_multi(const cgan3d_pack_desc* descs, int32_t 
   return CGAN3D_OK;
 }
 
-extern "C" int32_t cgan3d_halo_eligible(const cgan3d_conv_geom* g) { return g && halo_format_ok(g) ? 1 : 0; }
+extern "C" int32_t cgan3d_halo_eligible(const cgan3d_conv_geom* g) {
+  return g && !g->planar && halo_format_ok(g) ? 1 : 0;
+}
 
 extern "C" int32_t cgan3d_packed_format(const cgan3d_conv_geom* g) {
   if (!g) return 0;
+  if (g->planar) return 1;
   if (sk_format_ok(g)) return 3;
   if (g->prec == CGAN3D_PREC_BF16 && halo_format_ok(g)) return 2;
   return 1;

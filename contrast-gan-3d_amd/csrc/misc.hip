@@ -18,14 +18,15 @@ void set_error(const char* fmt, ...) {
 __global__ void adam_tick_kernel(float* hyper) { hyper[4] += 1.f; }
 
 
-// one thread per (voxel, V channels); 32-bit index math (element count < 2^31)
+// one thread per (voxel, V channels); 32-bit index math (element count < 2^31).  PD: the depth
+// axis's pad (P, or 0 for the 2-D variants' planar grids, whose depth is not padded)
 template <int V>
 __global__ __launch_bounds__(256) void reflect_fold_kernel(const float* __restrict__ pad_in, float* __restrict__ out,
-                                                           int N, int D, int H, int W, int C, int P) {
+                                                           int N, int D, int H, int W, int C, int P, int PD) {
   typedef float fv __attribute__((ext_vector_type(V)));
   const int C4 = C / V;
   const int total = N * D * H * W * C4;
-  const int Dp = D + 2 * P, Hp = H + 2 * P, Wp = W + 2 * P;
+  const int Dp = D + 2 * PD, Hp = H + 2 * P, Wp = W + 2 * P;
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
     const int c4 = i % C4;
     int t = i / C4;
@@ -33,7 +34,7 @@ __global__ __launch_bounds__(256) void reflect_fold_kernel(const float* __restri
     const int h = t % H; t /= H;
     const int d = t % D, n = t / D;
     int qd[2], qh[2], qw[2];
-    const int nd = fold_src(d, D, P, qd), nh = fold_src(h, H, P, qh), nw = fold_src(w, W, P, qw);
+    const int nd = fold_src(d, D, PD, qd), nh = fold_src(h, H, P, qh), nw = fold_src(w, W, P, qw);
     fv s = {};
     for (int a = 0; a < nd; ++a)
       for (int b = 0; b < nh; ++b)
@@ -49,11 +50,11 @@ __global__ __launch_bounds__(256) void reflect_fold_kernel(const float* __restri
 // channels' scale / shift / mean / invstd live in registers; z is read as float4; two items per
 // iteration keep more loads in flight (HBM-bound: padded dL/dy in, dL/dy + z through)
 __global__ __launch_bounds__(256) void reflect_fold_bn_kernel(const float* __restrict__ pad_in, float* __restrict__ out,
-                                                              int N, int D, int H, int W, int C, int P, Epi ep) {
+                                                              int N, int D, int H, int W, int C, int P, int PD, Epi ep) {
   __shared__ f32x4 r0[256], r1[256];
   const int C4 = C / 4, tid = threadIdx.x;
   const int total = N * D * H * W * C4;
-  const int Dp = D + 2 * P, Hp = H + 2 * P, Wp = W + 2 * P;
+  const int Dp = D + 2 * PD, Hp = H + 2 * P, Wp = W + 2 * P;
   const int c0 = (tid % C4) * 4;
   f32x4 sc, sf, mu, iv;
 #pragma unroll
@@ -69,7 +70,7 @@ __global__ __launch_bounds__(256) void reflect_fold_bn_kernel(const float* __res
     const int h = t % H; t /= H;
     const int d = t % D, n = t / D;
     int qd[2], qh[2], qw[2];
-    const int nd = fold_src(d, D, P, qd), nh = fold_src(h, H, P, qh), nw = fold_src(w, W, P, qw);
+    const int nd = fold_src(d, D, PD, qd), nh = fold_src(h, H, P, qh), nw = fold_src(w, W, P, qw);
     const f32x4 z = reinterpret_cast<const f32x4*>(ep.bn_z)[i];
     f32x4 s = {0.f, 0.f, 0.f, 0.f};
     for (int a = 0; a < nd; ++a)
@@ -151,23 +152,28 @@ extern "C" int cgan3d_adam(float* param, const float* grad, float* exp_avg, floa
   return CGAN3D_OK;
 }
 
-extern "C" int cgan3d_reflect_fold(const float* padded, float* out, int32_t n, int32_t d, int32_t h, int32_t w,
-                                   int32_t c, int32_t pad, void* stream) {
-  CG_CHECK_ARG(padded && out, "cgan3d_reflect_fold: null pointer");
-  CG_CHECK_ARG(n > 0 && d > 2 * pad && h > 2 * pad && w > 2 * pad && c > 0 && pad >= 0,
-               "cgan3d_reflect_fold: dims must exceed 2*pad");
+static int reflect_fold_launch(const float* padded, float* out, int n, int d, int h, int w, int c, int pad, int pad_d,
+                               void* stream) {
   const long long total = (long long)n * d * h * w * c;
   CG_CHECK_ARG(total < (1LL << 31), "cgan3d_reflect_fold: volume too large");
   const bool v4 = c % 4 == 0;
   int blocks = (int)std::min<long long>((total / (v4 ? 4 : 1) + 255) / 256, 8192);
   if (v4)
     ::cg::launch(reflect_fold_kernel<4>, dim3(blocks), dim3(256), 0, (hipStream_t)stream, padded, out, n, d, h, w,
-                       c, pad);
+                       c, pad, pad_d);
   else
     ::cg::launch(reflect_fold_kernel<1>, dim3(blocks), dim3(256), 0, (hipStream_t)stream, padded, out, n, d, h, w,
-                       c, pad);
+                       c, pad, pad_d);
   CG_LAUNCH_CHECK("reflect_fold_kernel");
   return CGAN3D_OK;
+}
+
+extern "C" int cgan3d_reflect_fold(const float* padded, float* out, int32_t n, int32_t d, int32_t h, int32_t w,
+                                   int32_t c, int32_t pad, void* stream) {
+  CG_CHECK_ARG(padded && out, "cgan3d_reflect_fold: null pointer");
+  CG_CHECK_ARG(n > 0 && d > 2 * pad && h > 2 * pad && w > 2 * pad && c > 0 && pad >= 0,
+               "cgan3d_reflect_fold: dims must exceed 2*pad");
+  return reflect_fold_launch(padded, out, n, d, h, w, c, pad, pad, stream);
 }
 
 extern "C" int32_t cgan3d_reflect_fold_slots(int32_t n, int32_t d, int32_t h, int32_t w, int32_t c) {
@@ -175,13 +181,10 @@ extern "C" int32_t cgan3d_reflect_fold_slots(int32_t n, int32_t d, int32_t h, in
   return (int32_t)std::max<long long>(1, std::min<long long>((total / 4 + 255) / 256, 4096));
 }
 
-extern "C" int cgan3d_reflect_fold_ex(const float* padded, float* out, int32_t n, int32_t d, int32_t h, int32_t w,
-                                      int32_t c, int32_t pad, const cgan3d_epilogue* ep, void* stream) {
-  if (!ep || !ep->bn_mode) return cgan3d_reflect_fold(padded, out, n, d, h, w, c, pad, stream);
+static int reflect_fold_ex_launch(const float* padded, float* out, int n, int d, int h, int w, int c, int pad, int pad_d,
+                                  const cgan3d_epilogue* ep, void* stream) {
   CG_CHECK_ARG(ep->bn_mode == 2, "cgan3d_reflect_fold_ex: only bn_mode 2");
   CG_CHECK_ARG(padded && out && ep->bn_part && ep->bn_z && ep->bn_ss && ep->bn_mi, "cgan3d_reflect_fold_ex: null pointer");
-  CG_CHECK_ARG(n > 0 && d > 2 * pad && h > 2 * pad && w > 2 * pad && pad >= 0,
-               "cgan3d_reflect_fold_ex: dims must exceed 2*pad");
   CG_CHECK_ARG(c >= 4 && c % 4 == 0 && 256 % (c / 4) == 0, "cgan3d_reflect_fold_ex: channels must be 4k dividing 1024");
   const long long total = (long long)n * d * h * w * c;
   CG_CHECK_ARG(total < (1LL << 31), "cgan3d_reflect_fold_ex: volume too large");
@@ -191,9 +194,25 @@ extern "C" int cgan3d_reflect_fold_ex(const float* padded, float* out, int32_t n
   e.bn_part = ep->bn_part; e.bn_mode = 2; e.bn_slots = blocks; e.bn_z = ep->bn_z; e.bn_ss = ep->bn_ss;
   e.bn_mi = ep->bn_mi; e.bn_act = ep->bn_act; e.bn_slope = ep->bn_slope;
   ::cg::launch(reflect_fold_bn_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, padded, out, n, d, h, w, c,
-                     pad, e);
+                     pad, pad_d, e);
   CG_LAUNCH_CHECK("reflect_fold_bn_kernel");
   return CGAN3D_OK;
+}
+
+extern "C" int cgan3d_reflect_fold_ex(const float* padded, float* out, int32_t n, int32_t d, int32_t h, int32_t w,
+                                      int32_t c, int32_t pad, const cgan3d_epilogue* ep, void* stream) {
+  if (!ep || !ep->bn_mode) return cgan3d_reflect_fold(padded, out, n, d, h, w, c, pad, stream);
+  CG_CHECK_ARG(n > 0 && d > 2 * pad && h > 2 * pad && w > 2 * pad && pad >= 0,
+               "cgan3d_reflect_fold_ex: dims must exceed 2*pad");
+  return reflect_fold_ex_launch(padded, out, n, d, h, w, c, pad, pad, ep, stream);
+}
+
+extern "C" int cgan3d_reflect_fold2d(const float* padded, float* out, int32_t n, int32_t h, int32_t w, int32_t c,
+                                     int32_t pad, const cgan3d_epilogue* ep, void* stream) {
+  CG_CHECK_ARG(padded && out, "cgan3d_reflect_fold2d: null pointer");
+  CG_CHECK_ARG(n > 0 && h > 2 * pad && w > 2 * pad && c > 0 && pad >= 0, "cgan3d_reflect_fold2d: dims must exceed 2*pad");
+  if (ep && ep->bn_mode) return reflect_fold_ex_launch(padded, out, n, 1, h, w, c, pad, 0, ep, stream);
+  return reflect_fold_launch(padded, out, n, 1, h, w, c, pad, 0, stream);
 }
 
 extern "C" int cgan3d_gp_interpolate(const float* real, const float* fake, const float* eps, float* out, int32_t b,

@@ -57,6 +57,12 @@ typedef struct cgan3d_conv_geom {
                       * 3: small-grid K-split format, bf16 [b][tap][a] — prec BF16, k 4, cin%8==0,
                       *    cout%8==0 (the critic's middle layers; cgan3d_packed_format) */
   int32_t prec;      /* CGAN3D_PREC_F32 (exact f32 MFMA) or CGAN3D_PREC_BF16 (bf16 MFMA, f32 accumulate) */
+  int32_t planar;    /* 1: a 2-D convolution (nn.Conv2d / nn.ConvTranspose2d of the is_2D variants,
+                      * model/blocks.py:22-27, experiments/conf_2D.py): di == do_ == 1, the depth
+                      * axis is a pass-through (kernel 1, stride 1, pad 0, one parity class), the
+                      * kernel has k*k taps t = th*k + tw and weights are [Cout, Cin, k, k] /
+                      * [Cin, Cout, k, k].  Runs on the generic f32 paths (implicit GEMM for
+                      * cout >= 2, any cout; the VALU cout == 1 kernels), w_packed 0 or 1 */
 } cgan3d_conv_geom;
 
 #define CGAN3D_PREC_F32 0
@@ -262,6 +268,11 @@ int cgan3d_channel_sum(const float* x, int64_t nvox, int32_t c, float* out, floa
                        void* stream);
 int cgan3d_reflect_fold(const float* padded, float* out, int32_t n, int32_t d, int32_t h,
                         int32_t w, int32_t c, int32_t pad, void* stream);
+/* reflect_fold(_ex) for the 2-D variants (nn.Conv2d padding_mode="reflect", generator.py:19-23
+ * with is_2D): padded [n, h+2p, w+2p, c] -> out [n, h, w, c]; ep NULL or bn_mode 0: plain fold,
+ * bn_mode 2: as cgan3d_reflect_fold_ex (slots: cgan3d_reflect_fold_slots(n, 1, h, w, c)) */
+int cgan3d_reflect_fold2d(const float* padded, float* out, int32_t n, int32_t h, int32_t w, int32_t c,
+                          int32_t pad, const cgan3d_epilogue* ep, void* stream);
 /* reflect_fold with the epilogue's bn_mode-2 statistics of its output (other fields ignored);
  * slots of its slab: cgan3d_reflect_fold_slots() */
 int32_t cgan3d_reflect_fold_slots(int32_t n, int32_t d, int32_t h, int32_t w, int32_t c);

@@ -40,6 +40,7 @@ class GenConfig:
     n_resnet_blocks: int = 4
     n_updownsample_blocks: int = 2
     init_channels_out: int = 16
+    is_2D: bool = False  # experiments/conf_2D.py: Conv2d / ConvTranspose2d / BatchNorm2d (blocks.py:22-27)
 
 
 @dataclass
@@ -49,12 +50,14 @@ class CriticConfig:
     discriminator_depth: int = 3
     negative_slope: float = 0.2
     norm: str = "identity"  # "identity" (GP conf), "batch" (basic conf) or "layer" (gp_layernorm conf)
+    is_2D: bool = False  # experiments/conf_2D.py
 
 
 def gen_param_shapes(cfg: GenConfig) -> "Dict[str, tuple]":
     """state_dict layout of ResnetGenerator (generator.py:24-88)."""
     c0 = cfg.init_channels_out
     shp = {}
+    K3, K7 = ((3, 3), (7, 7)) if cfg.is_2D else ((3, 3, 3), (7, 7, 7))
 
     def bn(prefix, c):
         shp[f"{prefix}.normalization.weight"] = (c,)
@@ -63,22 +66,22 @@ def gen_param_shapes(cfg: GenConfig) -> "Dict[str, tuple]":
         shp[f"{prefix}.normalization.running_var"] = (c,)
         shp[f"{prefix}.normalization.num_batches_tracked"] = ()
 
-    shp["model.first.conv.weight"] = (c0, 1, 7, 7, 7)
+    shp["model.first.conv.weight"] = (c0, 1, *K7)
     bn("model.first", c0)
     for i in range(cfg.n_updownsample_blocks):
         ci = c0 * 2**i
-        shp[f"model.downsampling.{i}.conv.weight"] = (2 * ci, ci, 3, 3, 3)
+        shp[f"model.downsampling.{i}.conv.weight"] = (2 * ci, ci, *K3)
         bn(f"model.downsampling.{i}", 2 * ci)
     cr = c0 * 2**cfg.n_updownsample_blocks
     for r in range(cfg.n_resnet_blocks):
         for b in (0, 1):
-            shp[f"model.resnet_backbone.{r}.block{b}.conv.weight"] = (cr, cr, 3, 3, 3)
+            shp[f"model.resnet_backbone.{r}.block{b}.conv.weight"] = (cr, cr, *K3)
             bn(f"model.resnet_backbone.{r}.block{b}", cr)
     for j, i in enumerate(range(cfg.n_updownsample_blocks, 0, -1)):
         ci = c0 * 2**i
-        shp[f"model.upsampling.{j}.conv.weight"] = (ci, ci // 2, 3, 3, 3)  # ConvTranspose: [Cin, Cout, ...]
+        shp[f"model.upsampling.{j}.conv.weight"] = (ci, ci // 2, *K3)  # ConvTranspose: [Cin, Cout, ...]
         bn(f"model.upsampling.{j}", ci // 2)
-    shp["model.last_conv.weight"] = (1, c0, 7, 7, 7)
+    shp["model.last_conv.weight"] = (1, c0, *K7)
     shp["model.last_conv.bias"] = (1,)
     return shp
 
@@ -86,12 +89,13 @@ def gen_param_shapes(cfg: GenConfig) -> "Dict[str, tuple]":
 def critic_param_shapes(cfg: CriticConfig) -> "Dict[str, tuple]":
     """state_dict layout of PatchGANDiscriminator (discriminator.py:19-80)."""
     c0, shp = cfg.init_channels_out, {}
-    shp["model.first.conv.weight"] = (c0, cfg.channels_in, 4, 4, 4)
+    K4 = (4, 4) if cfg.is_2D else (4, 4, 4)
+    shp["model.first.conv.weight"] = (c0, cfg.channels_in, *K4)
     shp["model.first.conv.bias"] = (c0,)
     out_ = c0
     for n in range(cfg.discriminator_depth):
         in_, out_ = min(2**n, 8) * c0, min(2 ** (n + 1), 8) * c0
-        shp[f"model.middle.{n}.conv.weight"] = (out_, in_, 4, 4, 4)
+        shp[f"model.middle.{n}.conv.weight"] = (out_, in_, *K4)
         if cfg.norm == "identity":
             shp[f"model.middle.{n}.conv.bias"] = (out_,)
         elif cfg.norm == "layer":
@@ -101,7 +105,7 @@ def critic_param_shapes(cfg: CriticConfig) -> "Dict[str, tuple]":
             shp[f"{p}.weight"], shp[f"{p}.bias"] = (out_,), (out_,)
             shp[f"{p}.running_mean"], shp[f"{p}.running_var"] = (out_,), (out_,)
             shp[f"{p}.num_batches_tracked"] = ()
-    shp["model.last.weight"] = (1, out_, 4, 4, 4)
+    shp["model.last.weight"] = (1, out_, *K4)
     shp["model.last.bias"] = (1,)
     return shp
 
@@ -144,20 +148,26 @@ def _conv3d_fft(x: Tensor, w: Tensor) -> Tensor:
     correlation at indices k-1 .. D-1 (no wrap reaches them).  Differentiable (torch.fft)."""
     k = w.shape[2:]
     s = x.shape[2:]
-    X = torch.fft.rfftn(x, s=s, dim=(2, 3, 4))
-    Wf = torch.fft.rfftn(torch.flip(w, dims=(2, 3, 4)), s=s, dim=(2, 3, 4))
-    Y = torch.einsum("ncdhw,ocdhw->nodhw", X, Wf)
-    y = torch.fft.irfftn(Y, s=s, dim=(2, 3, 4))
-    return y[:, :, k[0] - 1:, k[1] - 1:, k[2] - 1:]
+    dims = tuple(range(2, x.dim()))
+    X = torch.fft.rfftn(x, s=s, dim=dims)
+    Wf = torch.fft.rfftn(torch.flip(w, dims=dims), s=s, dim=dims)
+    Y = torch.einsum("nc...,oc...->no...", X, Wf)
+    y = torch.fft.irfftn(Y, s=s, dim=dims)
+    return y[(slice(None), slice(None)) + tuple(slice(kk - 1, None) for kk in k)]
 
 
 def _conv3d_unfold(x: Tensor, w: Tensor, stride: int = 1, padding: int = 0) -> Tensor:
     """Cross-correlation as one GEMM over windows (Tensor.unfold views + einsum): the backward is
     an unfold adjoint plus GEMMs, ~15x faster than the CPU's float64 slow_conv3d backward."""
+    nd = x.dim() - 2
     if padding:
-        x = F.pad(x, (padding,) * 6)
+        x = F.pad(x, (padding,) * (2 * nd))
     k = w.shape[2]
-    u = x.unfold(2, k, stride).unfold(3, k, stride).unfold(4, k, stride)  # [n, c, do, ho, wo, k, k, k]
+    u = x
+    for a in range(2, 2 + nd):
+        u = u.unfold(a, k, stride)  # [n, c, (do,) ho, wo, (k,) k, k]
+    if nd == 2:
+        return torch.einsum("nchwjk,ocjk->nohw", u, w)
     return torch.einsum("ncdhwijk,ocijk->nodhw", u, w)
 
 
@@ -173,7 +183,9 @@ def _conv3d_cpu(x: Tensor, w: Tensor, b: Optional[Tensor], **kw) -> Tensor:
             y = _conv3d_fft(x, w)
         else:
             y = _conv3d_unfold(x, w, kw.get("stride", 1), kw.get("padding", 0))
-        return y if b is None else y + b.view(1, -1, 1, 1, 1)
+        return y if b is None else y + b.view(1, -1, *([1] * (x.dim() - 2)))
+    if x.dim() == 4:  # the 2-D variants
+        return F.conv2d(x, w, b, **kw)
     do = x.shape[2] - k + 1
     cols = w.shape[1] * k ** 3 * x.shape[0] * do * (x.shape[3] - k + 1) * (x.shape[4] - k + 1)
     if kw or x.is_cuda or cols <= _COLS_MAX:
@@ -189,34 +201,30 @@ def _conv3d(x: Tensor, w: Tensor, b: Optional[Tensor] = None, rounded: bool = Tr
 
 
 def _conv_transpose3d(x: Tensor, w: Tensor, **kw) -> Tensor:
+    f = F.conv_transpose2d if x.dim() == 4 else F.conv_transpose3d  # 2-D variants: ConvTranspose2d
     if not BF16_OPERANDS:
-        return F.conv_transpose3d(x, w, **kw)
-    return _GradToBf16.apply(F.conv_transpose3d(_bf16(x), _bf16(w), **kw))
+        return f(x, w, **kw)
+    return _GradToBf16.apply(f(_bf16(x), _bf16(w), **kw))
 
 
 # ----------------------------------------------------------------------------- layers
 def batch_norm(x: Tensor, p: Dict[str, Tensor], prefix: str, training: bool, momentum=0.1, eps=1e-5):
-    """nn.BatchNorm3d (blocks.py:26-27,45): batch stats over N·D·H·W in train mode."""
-    rm, rv = p[f"{prefix}.running_mean"], p[f"{prefix}.running_var"]
+    """nn.BatchNorm3d / nn.BatchNorm2d (blocks.py:26-27,45): in train mode batch statistics over
+    N·(D·)H·W (biased variance to normalise, unbiased for running_var, momentum 0.1), eval mode the
+    running statistics.  torch's own batch_norm, as the reference's module calls it: its fused
+    backward keeps the float32 gradients within ~1e-5 of float64, where differentiating an explicit
+    (x - mean) / sqrt(var + eps) formula in float32 drifts by ~1e-3 on ill-conditioned layers."""
     if training:
-        dims = [0, 2, 3, 4]
-        mean = x.mean(dims)
-        var_b = x.var(dims, unbiased=False)
-        n = x.numel() // x.shape[1]
         with torch.no_grad():
-            rm.mul_(1 - momentum).add_(momentum * mean.detach())
-            rv.mul_(1 - momentum).add_(momentum * var_b.detach() * n / max(n - 1, 1))
             p[f"{prefix}.num_batches_tracked"].add_(1)
-    else:
-        mean, var_b = rm, rv
-    sh = (1, -1, 1, 1, 1)
-    xhat = (x - mean.view(sh)) / torch.sqrt(var_b.view(sh) + eps)
-    return xhat * p[f"{prefix}.weight"].view(sh) + p[f"{prefix}.bias"].view(sh)
+    return F.batch_norm(x, p[f"{prefix}.running_mean"], p[f"{prefix}.running_var"], p[f"{prefix}.weight"],
+                        p[f"{prefix}.bias"], training, momentum, eps)
 
 
 def generator_forward(p: Dict[str, Tensor], x: Tensor, cfg: GenConfig, training=True) -> Tensor:
     """ResnetGenerator.forward (generator.py:89-90)."""
-    h = F.pad(x, (3,) * 6, mode="reflect")  # padding_mode="reflect", padding=3 (generator.py:19-23)
+    npad = 2 * (x.dim() - 2)
+    h = F.pad(x, (3,) * npad, mode="reflect")  # padding_mode="reflect", padding=3 (generator.py:19-23)
     h = F.relu(batch_norm(_conv3d(h, p["model.first.conv.weight"]), p, "model.first.normalization", training))
     for i in range(cfg.n_updownsample_blocks):
         pre = f"model.downsampling.{i}"
@@ -233,7 +241,7 @@ def generator_forward(p: Dict[str, Tensor], x: Tensor, cfg: GenConfig, training=
         pre = f"model.upsampling.{j}"
         h = _conv_transpose3d(h, p[f"{pre}.conv.weight"], stride=2, padding=1, output_padding=1)
         h = F.relu(batch_norm(h, p, f"{pre}.normalization", training))
-    h = F.pad(h, (3,) * 6, mode="reflect")
+    h = F.pad(h, (3,) * npad, mode="reflect")
     h = _conv3d(h, p["model.last_conv.weight"], p["model.last_conv.bias"])
     return torch.tanh(h)
 

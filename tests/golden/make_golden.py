@@ -184,24 +184,25 @@ class _NullLogger:
         pass
 
 
-def _make_trainer(g_args, gp: bool, S, b_low, b_high, iters, dtype, critic_norm="identity"):
+def _make_trainer(g_args, gp: bool, S, b_low, b_high, iters, dtype, critic_norm="identity", d_args=None):
     """A reference Trainer for the fixture runs; ``dtype=torch.float64`` converts the modules, the
     optimisers and the HU constants to double (the exact-arithmetic yardstick).  ``critic_norm``
     "layer": the gp_layernorm conf's critic (experiments/gp_layernorm.py:9-11: LayerNorm over
     (C, D, H, W) of every middle block, no affine parameters)."""
+    shape = tuple(S) if isinstance(S, (tuple, list)) else (S, S, S)
     d_extra = dict(norm_layer=torch.nn.Identity) if gp else {}
     if critic_norm == "layer":
-        d_extra = dict(norm_layer=torch.nn.LayerNorm, patch_size=(1, S, S, S), elementwise_affine=False)
+        d_extra = dict(norm_layer=torch.nn.LayerNorm, patch_size=(1, *shape), elementwise_affine=False)
     lr, betas = (1e-4, (0.0, 0.9)) if gp else (2e-4, (0.5, 0.999))
     lo, hi = scaled_hu_bounds()
     tr = Trainer(
         train_iterations=iters, val_iterations=1, validate_every=None,
         train_generator_every=1, train_critic_every=1, log_every=10**9, log_images_every=10**9,
         generator_class=partial(ResnetGenerator, **g_args),
-        critic_class=partial(PatchGANDiscriminator, **D_ARGS, **d_extra),
+        critic_class=partial(PatchGANDiscriminator, **(d_args or D_ARGS), **d_extra),
         generator_optim_class=partial(torch.optim.Adam, lr=lr, betas=betas),
         critic_optim_class=partial(torch.optim.Adam, lr=lr, betas=betas),
-        hu_loss_instance=ref_loss.HULoss(lo, hi, (b_low + b_high, 1, S, S, S)),
+        hu_loss_instance=ref_loss.HULoss(lo, hi, (b_low + b_high, 1, *shape)),
         logger_interface=_NullLogger(), device=torch.device("cpu"), checkpoint_dir=None,
         weight_clip=None if gp else 0.01, checkpoint_every=None)
     pcg64_init_(tr.generator, 0)
@@ -292,8 +293,16 @@ def _run_iteration(tr, gp, inputs, it, dtype):
     return {k: v.detach().numpy() for k, v in logged.items()}, grads
 
 
+def _patches(n, shape, seed):
+    """synth_patches of a 3-D shape, or of a 2-D (H, W) shape as [n, 1, H, W]."""
+    if len(shape) == 2:
+        x, m = synth_patches(n, (1, *shape), seed)
+        return x[:, :, 0], m[:, :, 0]
+    return synth_patches(n, shape, seed)
+
+
 def train_steps(tag, g_args, gp: bool, S, b_opt, b_low, b_high, iters, seed, save_final_g=True,
-                critic_norm="identity"):
+                critic_norm="identity", d_args=None):
     """Trainer.train_step (Trainer.py:163-203) with train_{critic,generator}_every = 1, ``iters``
     iterations in float32 (the reference's precision).
 
@@ -301,23 +310,24 @@ def train_steps(tag, g_args, gp: bool, S, b_opt, b_low, b_high, iters, seed, sav
     ``it{k}/adam``, k > 0) and the same iteration re-run in float64 from that state
     (``it{k}/grad64``, ``it{k}/loss64``): the exact-arithmetic yardstick the GPU test holds each
     iteration to."""
-    tr, lr, betas = _make_trainer(g_args, gp, S, b_low, b_high, iters, torch.float32, critic_norm)
+    shape = tuple(S) if isinstance(S, (tuple, list)) else (S, S, S)
+    tr, lr, betas = _make_trainer(g_args, gp, shape, b_low, b_high, iters, torch.float32, critic_norm, d_args)
     out = {}
     rngs = np.random.Generator(np.random.PCG64(seed + 100))
     for it in range(iters):
-        opt, _ = synth_patches(b_opt, S, seed + 10 * it)
-        low, low_seg = synth_patches(b_low, S, seed + 10 * it + 1)
-        high, high_seg = synth_patches(b_high, S, seed + 10 * it + 2)
+        opt, _ = _patches(b_opt, shape, seed + 10 * it)
+        low, low_seg = _patches(b_low, shape, seed + 10 * it + 1)
+        high, high_seg = _patches(b_high, shape, seed + 10 * it + 2)
         low = low - 0.3  # hypo-enhanced (LOW) / hyper-enhanced (HIGH) flavour
         high = high + 0.3
-        eps = rngs.random((min(b_opt, b_low + b_high), 1, 1, 1, 1)).astype(np.float32)
+        eps = rngs.random((min(b_opt, b_low + b_high),) + (1,) * (len(shape) + 1)).astype(np.float32)
         inputs = (opt, low, low_seg, high, high_seg, eps)
         snap = _snapshot(tr)
         if it > 0:
             out.update(_state_arrays(tr, snap, it))
         losses, grads = _run_iteration(tr, gp, inputs, it, torch.float32)
         # the same iteration in float64 from the same state
-        tr64, _, _ = _make_trainer(g_args, gp, S, b_low, b_high, iters, torch.float64, critic_norm)
+        tr64, _, _ = _make_trainer(g_args, gp, shape, b_low, b_high, iters, torch.float64, critic_norm, d_args)
         _restore(tr64, snap)
         losses64, grads64 = _run_iteration(tr64, gp, inputs, it, torch.float64)
         out[f"it{it}/opt"] = opt
@@ -336,11 +346,31 @@ def train_steps(tag, g_args, gp: bool, S, b_opt, b_low, b_high, iters, seed, sav
     if save_final_g:
         out.update(sd_np(tr.generator, "final/G/"))
     out.update(sd_np(tr.critic, "final/D/"))
-    meta = dict(S=S, b_opt=b_opt, b_low=b_low, b_high=b_high, iters=iters, gp=int(gp), lr=lr, critic_norm=critic_norm,
+    meta = dict(S=shape[0] if len(set(shape)) == 1 and len(shape) == 3 else None, shape=shape, b_opt=b_opt,
+                b_low=b_low, b_high=b_high, iters=iters, gp=int(gp), lr=lr, critic_norm=critic_norm,
                 beta1=betas[0], beta2=betas[1], teacher_forced=1,
+                d_init_channels_out=(d_args or D_ARGS)["init_channels_out"],
                 **{f"g_{k}": v for k, v in g_args.items()})
     np.savez_compressed(HERE / f"step_{tag}.npz", torch_version=torch.__version__,
                         meta=np.array(repr(meta)), **out)
+
+
+def clip_2d():
+    """experiments/conf_2D.py: the 2-D variants on top of basic_conf (weight clip 0.01, BatchNorm
+    critic, Adam lr 2e-4 betas (0.5, 0.999)) — generator with 6 ResNet blocks (is_2D), critic with
+    16 initial channels (16 -> 32 -> 64 -> 128), at 32 x 32 (the 2-D conf trains 128 x 128).  The
+    generator's width is halved (8 initial channels) to keep the fixture small; the full conf_2D
+    widths run against the oracle in tests/test_gpu_2d.py."""
+    g2 = dict(n_resnet_blocks=6, n_updownsample_blocks=2, init_channels_out=8, is_2D=True)
+    d2 = dict(channels_in=1, init_channels_out=16, discriminator_depth=3, negative_slope=0.2, is_2D=True)
+    train_steps("clip_2d", g2, False, S=(32, 32), b_opt=2, b_low=1, b_high=1, iters=2, seed=900, d_args=d2)
+
+
+def ln_aniso():
+    """gp_layernorm conf on an anisotropic patch (experiments/small_patch_size.py:4 trains
+    128 x 128 x 32 with it; here 32 x 40 x 48, every axis >= 32 for the critic's k4 pyramid)."""
+    train_steps("ln_aniso", G_SMALL, True, S=(32, 40, 48), b_opt=2, b_low=1, b_high=1, iters=2, seed=1000,
+                critic_norm="layer")
 
 
 if __name__ == "__main__":
@@ -351,6 +381,10 @@ if __name__ == "__main__":
         if "gp_layernorm" in only:
             train_steps("gp_layernorm", G_SMALL, True, S=32, b_opt=2, b_low=1, b_high=1, iters=2, seed=800,
                         critic_norm="layer")
+        if "clip_2d" in only:
+            clip_2d()
+        if "ln_aniso" in only:
+            ln_aniso()
         sys.exit(0)
     gen_forward(32, 2, seed=1234)
     disc_forward(32, 3, seed=1234)
@@ -364,5 +398,7 @@ if __name__ == "__main__":
     # gp_layernorm conf (experiments/gp_layernorm.py): LayerNorm critic with the gradient penalty
     train_steps("gp_layernorm", G_SMALL, True, S=32, b_opt=2, b_low=1, b_high=1, iters=2, seed=800,
                 critic_norm="layer")
+    clip_2d()
+    ln_aniso()
     for f in sorted(HERE.glob("*.npz")):
         print(f.name, f.stat().st_size)

@@ -16,7 +16,7 @@ pytestmark = pytest.mark.gpu
 D_ARGS = dict(channels_in=1, init_channels_out=8, discriminator_depth=3, negative_slope=0.2)
 
 
-def _models(g_args, critic_bn=False, ln_patch=None):
+def _models(g_args, critic_bn=False, ln_patch=None, d_args=None):
     from torch import nn
     from cgan3d_amd.model.discriminator import PatchGANDiscriminator
     from cgan3d_amd.model.generator import ResnetGenerator
@@ -25,13 +25,15 @@ def _models(g_args, critic_bn=False, ln_patch=None):
     norm = {} if critic_bn else dict(norm_layer=nn.Identity)  # BatchNorm critic: basic_conf.py:60-66
     if ln_patch is not None:  # LayerNorm critic: experiments/gp_layernorm.py:9-11
         norm = dict(norm_layer=nn.LayerNorm, patch_size=(1, *ln_patch), elementwise_affine=False)
-    d = pcg64_init_(PatchGANDiscriminator(**D_ARGS, **norm), 1).cuda()
+    d = pcg64_init_(PatchGANDiscriminator(**(d_args or D_ARGS), **norm), 1).cuda()
     return g, d
 
 
 def _engine(g, d, b, S, lr, b1, b2, weight_clip=None):
+    """``S``: an edge (cubic patch) or the patch shape ((D, H, W), or (H, W) for the 2-D variants)."""
     from cgan3d_amd.engine import StepEngine
-    return StepEngine(g, d, g.config, d.config, b, b, (S, S, S), g_hyper=(lr, b1, b2, 1e-8),
+    dims = tuple(S) if isinstance(S, (tuple, list)) else (S, S, S)
+    return StepEngine(g, d, g.config, d.config, b, b, dims, g_hyper=(lr, b1, b2, 1e-8),
                       d_hyper=(lr, b1, b2, 1e-8), weight_clip=weight_clip)
 
 
@@ -51,11 +53,13 @@ def _load_fixture_state(eng, g, d, f, it):
     eng.D.pack()
 
 
-@pytest.mark.parametrize("tag", ["gp_small", "gp_full", "clip_small", "gp_layernorm"])
+@pytest.mark.parametrize("tag", ["gp_small", "gp_full", "clip_small", "gp_layernorm", "clip_2d", "ln_aniso"])
 def test_step_matches_reference_fixture(golden, tag):
     """Trainer.train_step of the reference (GP conf; weight-clip conf with the BatchNorm critic;
-    gp_layernorm conf with the LayerNorm critic and the penalty's double backward through it)
-    against the device step: losses, every gradient, final parameters and BN buffers.
+    gp_layernorm conf with the LayerNorm critic and the penalty's double backward through it, on a
+    cubic and on an anisotropic 32 x 40 x 48 patch; conf_2D's 2-D generator and 2-D BatchNorm critic
+    with weight clipping) against the device step: losses, every gradient, final parameters and BN
+    buffers.
 
     Every iteration starts from the reference's own state entering it (fixture ``it{k}/state``) and
     is held to north_star's 1e-3 against the same iteration re-run in float64 from that state
@@ -64,13 +68,16 @@ def test_step_matches_reference_fixture(golden, tag):
     f = golden(f"step_{tag}")
     meta = ast.literal_eval(str(f["meta"]))
     assert meta.get("teacher_forced"), "regenerate the fixtures (tests/golden/make_golden.py)"
+    is2d = bool(meta.get("g_is_2D", False))
     g_args = dict(n_resnet_blocks=meta["g_n_resnet_blocks"], n_updownsample_blocks=meta["g_n_updownsample_blocks"],
-                  init_channels_out=meta["g_init_channels_out"])
-    S, b = meta["S"], meta["b_opt"]
+                  init_channels_out=meta["g_init_channels_out"], is_2D=is2d)
+    shape = tuple(meta.get("shape") or (meta["S"],) * 3)
+    b = meta["b_opt"]
     gp = bool(meta["gp"])
     ln = meta.get("critic_norm") == "layer"
-    g, d = _models(g_args, critic_bn=not gp, ln_patch=(S, S, S) if ln else None)
-    eng = _engine(g, d, b, S, meta["lr"], meta["beta1"], meta["beta2"], weight_clip=None if gp else 0.01)
+    d_args = dict(D_ARGS, init_channels_out=meta.get("d_init_channels_out", 8), is_2D=is2d)
+    g, d = _models(g_args, critic_bn=not gp, ln_patch=shape if ln else None, d_args=d_args)
+    eng = _engine(g, d, b, shape, meta["lr"], meta["beta1"], meta["beta2"], weight_clip=None if gp else 0.01)
     names = {"L_D": 0, "D": 0, "G": 3, "sim": 4, "HU": 5, "G-full": 6}
     for it in range(meta["iters"]):
         if it > 0:

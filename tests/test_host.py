@@ -43,6 +43,9 @@ def test_state_dict_layout_matches_reference():
     (dict(n_resnet_blocks=4, n_updownsample_blocks=2, init_channels_out=16), 64, 4, False),
     (dict(n_resnet_blocks=4, n_updownsample_blocks=2, init_channels_out=16), 32, 2, False),
     (dict(n_resnet_blocks=4, n_updownsample_blocks=2, init_channels_out=16), 64, 4, True),  # BN critic, clip
+    (dict(n_resnet_blocks=1, n_updownsample_blocks=2, init_channels_out=8), (32, 40, 48), 2, False),  # anisotropic
+    # experiments/conf_2D.py: 2-D generator (6 blocks) and 2-D BatchNorm critic (16 -> 128 channels), clip
+    (dict(n_resnet_blocks=6, n_updownsample_blocks=2, init_channels_out=16, is_2D=True), (128, 128), 8, True),
 ])
 def test_engine_step_dry_run_shapes(g_args, S, b, clip):
     """Every launch of a full step gets operands whose extents match the kernel's footprint."""
@@ -51,15 +54,34 @@ def test_engine_step_dry_run_shapes(g_args, S, b, clip):
     from cgan3d_amd.model.discriminator import PatchGANDiscriminator
     from cgan3d_amd.model.generator import ResnetGenerator
     g = ResnetGenerator(**g_args)
-    d = PatchGANDiscriminator(**D_ARGS, **({} if clip else dict(norm_layer=nn.Identity)))
+    is2d = g_args.get("is_2D", False)
+    d_args = dict(D_ARGS, init_channels_out=16, is_2D=True) if is2d else D_ARGS
+    d = PatchGANDiscriminator(**d_args, **({} if clip else dict(norm_layer=nn.Identity)))
+    dims = tuple(S) if isinstance(S, tuple) else (S, S, S)
     ops.DRY_RUN = True
     try:
-        eng = StepEngine(g, d, g.config, d.config, b, b, (S, S, S), g_hyper=(1e-4, 0.0, 0.9, 1e-8),
+        eng = StepEngine(g, d, g.config, d.config, b, b, dims, g_hyper=(1e-4, 0.0, 0.9, 1e-8),
                          d_hyper=(1e-4, 0.0, 0.9, 1e-8), device=torch.device("cpu"),
                          weight_clip=0.01 if clip else None)
         eng.step()
     finally:
         ops.DRY_RUN = False
+    if is2d:
+        assert eng.dims == (1, *S) and eng.G.planar and eng.D.pl
+        assert eng.D.layers[-2].cout == 128
+
+
+def test_2d_models_match_reference_layout():
+    """conf_2D's modules (is_2D): Conv2d / ConvTranspose2d / BatchNorm2d with the reference's keys."""
+    from oracle import reference_torch as R
+    from cgan3d_amd.model.discriminator import PatchGANDiscriminator
+    from cgan3d_amd.model.generator import ResnetGenerator
+    gc = R.GenConfig(6, 2, 16, is_2D=True)
+    g = ResnetGenerator(6, 2, 16, is_2D=True)
+    assert [(k, tuple(v.shape)) for k, v in g.state_dict().items()] == list(R.gen_param_shapes(gc).items())
+    d = PatchGANDiscriminator(1, 16, 3, is_2D=True, negative_slope=0.2)
+    dc = R.CriticConfig(init_channels_out=16, norm="batch", is_2D=True)
+    assert [(k, tuple(v.shape)) for k, v in d.state_dict().items()] == list(R.critic_param_shapes(dc).items())
 
 
 def test_conv_wrapper_rejects_mismatched_operand():
