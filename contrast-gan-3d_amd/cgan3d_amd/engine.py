@@ -136,7 +136,11 @@ class _GLayer:
 class GeneratorPlan:
     """Buffers + launch geometry of ResnetGenerator (model/generator.py:9-90) for a batch shape."""
 
-    def __init__(self, cfg, n: int, dims: Dims, device, P: Dict[str, torch.Tensor], prec: int = L.PREC_F32):
+    def __init__(self, cfg, n: int, dims: Dims, device, P: Dict[str, torch.Tensor], prec: int = L.PREC_F32,
+                 allow_resize: bool = False):
+        """``allow_resize`` (forward-only plans): input dims that are not multiples of 4 give an
+        output of other dims, as the reference's convolution arithmetic does (the whole-scan
+        corrector then resizes it, eval/CCTAContrastCorrector.py:42-52)."""
         c0 = cfg.init_channels_out
         # the 2-D variants (experiments/conf_2D.py, is_2D): planar geometries on dims (1, H, W), f32
         self.planar = pl = bool(getattr(cfg, "is_2D", False))
@@ -163,7 +167,9 @@ class GeneratorPlan:
             up = tuple(x if (pl and a == 0) else 2 * x for a, x in enumerate(d))  # k3 s2 p1 output_padding 1
             layers.append(_GLayer("convt", f"model.upsampling.{j}", 3, 2, 1, False, ci, ci // 2, d, up))
             d = up
-        assert d == tuple(dims), f"generator output dims {d} != input dims {dims} (need dims % 4 == 0)"
+        if not allow_resize:
+            assert d == tuple(dims), f"generator output dims {d} != input dims {dims} (need dims % 4 == 0)"
+        self.out_dims = d
         self.last = _GLayer("last", "model.last_conv", 7, 1, 3, True, c0, 1, d, d, act=L.ACT_TANH)
         self.layers = layers
 
@@ -919,6 +925,13 @@ class StepEngine:
         self.g_buckets = self._make_g_buckets(G_BUCKET_BYTES) if self.dp else []
         on_gpu = torch.device(device).type == "cuda"
         self.comm = torch.cuda.Stream(device=device) if (self.dp and on_gpu) else None
+        # RCCL from C++ (ops.NativeComm): with the nccl backend the all-reduces are C-ABI launches,
+        # recorded into the step's launch plan like kernels — one plan per step, no host callables
+        # (CGAN3D_TORCH_COMM=1: torch.distributed's collectives as host callables, for A/B runs)
+        self.native = None
+        if (self.dp and on_gpu and torch.distributed.get_backend(process_group) == "nccl"
+                and os.environ.get("CGAN3D_TORCH_COMM") != "1"):
+            self.native = ops.NativeComm(process_group, device)
         if self.world > 1:
             self.broadcast_state()
 
@@ -954,7 +967,10 @@ class StepEngine:
         enqueued (a host callable inside a recorded plan: ops.plan_host)."""
         for st, lo, hi in self.g_buckets:
             if st == stage:
-                ops.plan_host(lambda lo=lo, hi=hi: self._start_allreduce(self.g_arena.grad[lo:hi]))
+                if self.native is not None:  # recorded into the plan as it is
+                    self._start_allreduce(self.g_arena.grad[lo:hi])
+                else:
+                    ops.plan_host(lambda lo=lo, hi=hi: self._start_allreduce(self.g_arena.grad[lo:hi]))
 
     def _start_allreduce(self, grad: torch.Tensor):
         """Mean over ranks of ``grad``, started now and overlapped with whatever is enqueued next:
@@ -962,6 +978,14 @@ class StepEngine:
         produce gradients); ``_finish_allreduce`` makes the main stream wait before Adam.  gloo
         (CPU tensors): synchronous."""
         dist = torch.distributed
+        if self.native is not None:
+            cur = torch.cuda.current_stream(self.device)
+            ops.stream_wait(self.comm, cur)
+            ops.stream_wait(self.comm, self.G.side)
+            with torch.cuda.stream(self.comm):
+                self.native.allreduce_mean(grad)
+            self._pending.append(None)
+            return
         if dist.get_backend(self.pg) != "nccl":
             if self.G.side is not None:  # gloo over GPU tensors orders only after the current stream
                 torch.cuda.current_stream(self.device).wait_stream(self.G.side)
@@ -976,6 +1000,11 @@ class StepEngine:
             self._pending.append(dist.all_reduce(grad, op=dist.ReduceOp.AVG, group=self.pg, async_op=True))
 
     def _finish_allreduce(self):
+        if self.native is not None:  # the main stream waits for the communication stream
+            ops.stream_wait(torch.cuda.current_stream(self.device), self.comm)
+            self._pending.clear()
+            return
+
         def wait():
             for w in self._pending:
                 w.wait()  # the current stream waits for the collective
@@ -1108,6 +1137,9 @@ class StepEngine:
     def _allreduce(self, flat_grad: torch.Tensor):
         """Mean of the per-rank gradients (RCCL over xGMI with the nccl backend; gloo on CPU)."""
         if not self.dp:
+            return
+        if self.native is not None:  # on the main stream: the generator update needs the new critic
+            self.native.allreduce_mean(flat_grad)
             return
         dist = torch.distributed
 

@@ -14,8 +14,17 @@ batch.  This is the default here too (same C-order batching of the grid, same ``
 independent, buffers untouched.  patchly is a dependency of the reference outside its tree
 (not installed here); its grid and averaging are restated here: ``grid_origins`` on the host, the
 patch accumulation and the average in HIP (``cgan3d_patch_accumulate`` / ``cgan3d_patch_normalize``),
-the generator on the HIP kernels.  The 2-D path (``correct_scan_2D``) belongs to the 2-D variants
- and raises.
+the generator on the HIP kernels.
+
+``correct_scan_2D`` (reference :83-99): the 2-D generator (experiments/conf_2D.py) over the scan's
+axial slices (the last axis, CCTAEvalDataset2D), ``batch_size`` slices per batch, stacked back to
+the scan's shape.  When no patch size (or a 2-D one) is given the reference sets the inference
+patch size to (512, 512), as here.
+
+Upsampler (reference :42-52): when the generator's output shape for the inference patch differs
+from the patch (patch dims that are not multiples of 4: the stride-2 convs round up, the
+transposed convs double), the output is resized to the patch with nn.Upsample's default
+nearest-neighbour rule (source index floor(i * in / out)) before ``patch - G(patch)``.
 """
 from __future__ import annotations
 
@@ -46,6 +55,36 @@ def grid_origins(shape: Sequence[int], patch: Sequence[int], step: Optional[Sequ
     return list(itertools.product(*per_dim))
 
 
+def model_output_shape(model: nn.Module, patch: Sequence[int]) -> Tuple[int, ...]:
+    """Spatial output shape of the generator for ``patch`` (compute_convolution_filters_shape,
+    reference model/utils.py:70-95, through convolution_output_shape's arithmetic)."""
+    shape = tuple(int(p) for p in patch)
+    for m in model.modules():
+        if isinstance(m, (nn.ConvTranspose3d, nn.ConvTranspose2d)):
+            k, p, s, op = m.kernel_size[0], m.padding[0], m.stride[0], m.output_padding[0]
+            shape = tuple((x - 1) * s - 2 * p + k + op for x in shape)
+        elif isinstance(m, (nn.Conv3d, nn.Conv2d)):
+            k, p, s = m.kernel_size[0], m.padding[0], m.stride[0]
+            shape = tuple((x + 2 * p - k) // s + 1 for x in shape)
+    return shape
+
+
+def nearest_resize(t: Tensor, size: Sequence[int]) -> Tensor:
+    """nn.Upsample(size=size) (mode "nearest") on [N, C, *spatial]: source index floor(i * in / out)
+    per axis — an index gather."""
+    out = t
+    for a, n_out in enumerate(size):
+        ax = 2 + a
+        n_in = out.shape[ax]
+        if n_in == n_out:
+            continue
+        # float32 scale and product, as aten's nearest_neighbor_compute_source_index
+        src = np.floor(np.arange(n_out, dtype=np.float32) * np.float32(n_in / n_out)).astype(np.int64)
+        idx = torch.from_numpy(np.minimum(src, n_in - 1))
+        out = out.index_select(ax, idx.to(out.device))
+    return out
+
+
 @dataclass
 class CCTAContrastCorrector:
     model: Callable[[], nn.Module]
@@ -65,10 +104,14 @@ class CCTAContrastCorrector:
         self.model = self.model.to(self.device)
         if self.eval_mode:
             self.model.eval()
-        if self.inference_patch_size is None or len(self.inference_patch_size) < 3:
-            raise NotImplementedError("CCTAContrastCorrector: the 2-D path is SURVEY.md §8f row 4")
-        self.inference_patch_size = tuple(int(p) for p in self.inference_patch_size)
         self.correct_scan = self.correct_scan_3D
+        if self.inference_patch_size is None or len(self.inference_patch_size) < 3:
+            self.correct_scan = self.correct_scan_2D
+            self.inference_patch_size = (512, 512)
+        self.inference_patch_size = tuple(int(p) for p in self.inference_patch_size)
+        out = model_output_shape(self.model, self.inference_patch_size)
+        self.upsampler = (lambda t: t) if out == self.inference_patch_size else \
+            (lambda t, size=self.inference_patch_size: nearest_resize(t, size))
 
     def load_model(self, checkpoint_path: Union[str, Path]):
         ckpt = torch.load(checkpoint_path, map_location="cpu", weights_only=True)
@@ -91,11 +134,24 @@ class CCTAContrastCorrector:
                              for o in chunk])[:, None]
             patch = torch.from_numpy(host).pin_memory().to(self.device, non_blocking=True) if stream else \
                 torch.from_numpy(host).to(self.device)
-            corrected = patch - self.model(patch)  # CCTAEvalDataset3D item -> patch - G(patch) (:77-79)
+            corrected = patch - self.upsampler(self.model(patch))  # CCTAEvalDataset3D item -> patch - G(patch) (:77-79)
             ops.patch_accumulate(corrected.contiguous(), torch.tensor(chunk, dtype=torch.int32, device=self.device),
                                  out, weight)
         ops.patch_normalize(out, weight)
         return out
+
+    @torch.no_grad()
+    def correct_scan_2D(self, ccta: np.ndarray, batch_size: int, desc: Optional[str] = None) -> Tensor:
+        """The scan's slices along its last axis through the 2-D generator (reference :83-99):
+        output [1, *ccta.shape]."""
+        nsl = ccta.shape[-1]
+        out = torch.empty((nsl, 1, *ccta.shape[:-1]), device=self.device)
+        for i in range(0, nsl, batch_size):
+            host = np.stack([self._scale(np.ascontiguousarray(ccta[..., j])) for j in range(i, min(nsl, i + batch_size))])
+            batch = torch.from_numpy(host[:, None])
+            batch = batch.pin_memory().to(self.device, non_blocking=True) if self.device.type == "cuda" else batch
+            out[i:i + len(host)] = batch - self.upsampler(self.model(batch))
+        return out.permute(1, 2, 3, 0)
 
     @torch.no_grad()
     def __call__(self, ccta: np.ndarray, batch_size: int = 16, **kwargs) -> Tensor:
@@ -108,12 +164,17 @@ class CCTAContrastCorrector:
     @classmethod
     def from_checkpoint(cls, inference_patch_size, device, checkpoint_path, generator_class=None, scaler=None):
         """As the reference's (:124-139): the basic conf's generator (4 ResNet blocks, 2 up/down,
-        16 channels) and FactorZeroCenterScaler(238, 600) unless given."""
+        16 channels) for a 3-D patch size, conf_2D's (is_2D, 6 ResNet blocks) otherwise, and
+        FactorZeroCenterScaler(238, 600) unless given."""
         from functools import partial
         from ..model.generator import ResnetGenerator
         if generator_class is None:
-            generator_class = partial(ResnetGenerator, n_resnet_blocks=4, n_updownsample_blocks=2,
-                                      init_channels_out=16)
+            if inference_patch_size is None or len(inference_patch_size) < 3:
+                generator_class = partial(ResnetGenerator, n_resnet_blocks=6, n_updownsample_blocks=2,
+                                          init_channels_out=16, is_2D=True)
+            else:
+                generator_class = partial(ResnetGenerator, n_resnet_blocks=4, n_updownsample_blocks=2,
+                                          init_channels_out=16)
         if scaler is None:
             scaler = _FactorZeroCenterScaler(238, 600)
         return cls(generator_class, scaler, device, inference_patch_size=inference_patch_size,

@@ -71,7 +71,7 @@ class ResnetGenerator(nn.Module):
         # the plan's packed-weight descriptors hold raw parameter addresses: rebuild if they moved
         key = (n, tuple(dims), self.model.first.conv.weight.device, tuple(p.data_ptr() for p in self.parameters()))
         if fresh or self._plan is None or self._plan[0] != key:
-            plan = GeneratorPlan(self.config, n, tuple(dims), key[2], self._tensors())
+            plan = GeneratorPlan(self.config, n, tuple(dims), key[2], self._tensors(), allow_resize=not fresh)
             if fresh:
                 return plan
             self._plan = (key, plan)
@@ -90,7 +90,9 @@ class ResnetGenerator(nn.Module):
         plan.pack()  # weights may have changed since the plan was built
         xc = x.detach().float().contiguous().view(n, *dims, 1)
         plan.forward(self._tensors(), xc, training=self.training)
-        return plan.att.clone().view(n, 1, *dims)
+        # dims that are not multiples of 4 come out at other dims (the reference's conv arithmetic)
+        out = plan.out_dims[1:] if self.is_2D else plan.out_dims
+        return plan.att.clone().view(n, 1, *out)
 
 
 class _GeneratorFn(torch.autograd.Function):

@@ -268,6 +268,39 @@ def stream_wait(waiter, signaler):
     check(L.lib().cgan3d_stream_wait(waiter.cuda_stream, signaler.cuda_stream), "stream_wait")
 
 
+class NativeComm:
+    """This library's RCCL communicator over a torch.distributed process group's ranks
+    (include/cgan3d.h cgan3d_comm_*): rank 0's unique id is broadcast through ``group`` once, and
+    ``allreduce_mean`` is then a plain C-ABI launch — recorded into launch plans like a kernel."""
+
+    def __init__(self, group=None, device=None):
+        import torch.distributed as dist
+        lib = L.lib()
+        self.world, self.rank = dist.get_world_size(group), dist.get_rank(group)
+        nb = int(lib.cgan3d_comm_id_bytes())
+        uid = torch.zeros(nb, dtype=torch.uint8, device=device)
+        if self.rank == 0:
+            host = (ctypes.c_char * nb)()
+            check(lib.cgan3d_comm_unique_id(host), "comm_unique_id")
+            uid.copy_(torch.frombuffer(bytearray(host.raw), dtype=torch.uint8))
+        src = dist.get_global_rank(group, 0) if group is not None else 0
+        dist.broadcast(uid, src, group=group)
+        raw = bytes(uid.cpu().numpy().tobytes())
+        h = ctypes.c_void_p()
+        check(lib.cgan3d_comm_init(raw, self.world, self.rank, ctypes.byref(h)), "comm_init")
+        self.handle = h
+
+    def allreduce_mean(self, t: torch.Tensor):
+        """t = mean over the ranks of t (fp32, contiguous), on the current stream."""
+        _need(t, t.numel(), "allreduce_mean")
+        check(_launch("cgan3d_allreduce_mean", self.handle, ptr(t), t.numel()), "allreduce_mean")
+
+    def __del__(self):
+        if getattr(self, "handle", None) is not None and L._lib is not None:
+            L._lib.cgan3d_comm_destroy(self.handle)
+            self.handle = None
+
+
 class Plan:
     """A recorded step: C-side launch plans (cgan3d_plan_*, include/cgan3d.h) interleaved with host
     callables that cannot be recorded (RCCL collectives).  ``run()`` re-issues it."""

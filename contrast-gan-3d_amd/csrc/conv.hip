@@ -31,10 +31,10 @@ static bool make_args(const cgan3d_conv_geom* g, ConvArgs* a, int bm) {
   a->k = g->k; a->s = g->stride; a->p = g->pad; a->transposed = g->transposed; a->reflect = g->reflect;
   a->sa = g->w_sa; a->sb = g->w_sb;
   a->kd = geom_kd(g); a->sd = geom_sd(g); a->pd = geom_pd(g);
-  if (g->transposed && g->stride > 1) {
-    if (g->do_ % a->sd || g->ho % g->stride || g->wo % g->stride) return false;
-    a->cd = g->do_ / a->sd; a->ch = g->ho / g->stride; a->cw = g->wo / g->stride;
-    a->nclass = a->sd * g->stride * g->stride;
+  if (g->transposed && g->stride > 1) {  // ceil-sized parity-class grids (odd output dims masked)
+    const int s = g->stride;
+    a->cd = (g->do_ + a->sd - 1) / a->sd; a->ch = (g->ho + s - 1) / s; a->cw = (g->wo + s - 1) / s;
+    a->nclass = a->sd * s * s;
   } else {
     a->cd = g->do_; a->ch = g->ho; a->cw = g->wo; a->nclass = 1;
   }
@@ -177,6 +177,7 @@ __global__ __launch_bounds__(256) void conv_cout1_kernel(ConvArgs a, const float
   int od, oh, ow, bd, bh, bw;
   if (a.transposed) { od = jd * a.sd + rd; oh = jh * s + rh; ow = jw * s + rw; bd = jd; bh = jh; bw = jw; }
   else { od = jd; oh = jh; ow = jw; bd = jd * a.sd - a.pd; bh = jh * s - p; bw = jw * s - p; }
+  if (od >= a.do_ || oh >= a.ho || ow >= a.wo) return;  // past the end of a ceil-sized class grid
   float acc = 0.f;
   for (int md = 0; md < nd; ++md) {
     const int td = fd + sd * md;

@@ -52,9 +52,9 @@ static GemmCfg gemm_cfg(const cgan3d_conv_geom* g) {
   const int nbt = g->cout <= 16 ? 1 : (g->cout <= 32 ? 2 : 4);
   long long cls = 1, cv;
   if (g->transposed && g->stride > 1) {
-    const int sd = geom_sd(g);
-    cls = (long long)sd * g->stride * g->stride;
-    cv = (long long)g->n * (g->do_ / sd) * (g->ho / g->stride) * (g->wo / g->stride);
+    const int sd = geom_sd(g), s = g->stride;
+    cls = (long long)sd * s * s;
+    cv = (long long)g->n * ((g->do_ + sd - 1) / sd) * ((g->ho + s - 1) / s) * ((g->wo + s - 1) / s);
   } else {
     cv = (long long)g->n * g->do_ * g->ho * g->wo;
   }
@@ -74,9 +74,11 @@ static bool gemm_args(const cgan3d_conv_geom* g, const GemmCfg& c, GemmArgs* a) 
   a->sa = g->w_sa; a->sb = g->w_sb; a->packed = g->w_packed; a->ldb = (g->cout + 3) / 4 * 4;
   a->kd = geom_kd(g); a->sd = geom_sd(g); a->pd = geom_pd(g);
   if (g->transposed && g->stride > 1) {
-    if (g->do_ % a->sd || g->ho % g->stride || g->wo % g->stride) return false;
-    a->cd = g->do_ / a->sd; a->ch = g->ho / g->stride; a->cw = g->wo / g->stride;
-    a->nclass = a->sd * g->stride * g->stride;
+    // parity classes of an output grid not divisible by the stride: ceil-sized class grids, the
+    // voxels past the grid's end masked per row (a stride-2 conv's input-grad on odd dims)
+    const int s = g->stride;
+    a->cd = (g->do_ + a->sd - 1) / a->sd; a->ch = (g->ho + s - 1) / s; a->cw = (g->wo + s - 1) / s;
+    a->nclass = a->sd * s * s;
   } else {
     a->cd = g->do_; a->ch = g->ho; a->cw = g->wo; a->nclass = 1;
   }
@@ -160,8 +162,9 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(GemmArgs a, const float*
         od = jd; oh = jh; ow = jw;
         row_b[0][tid] = jd * a.sd - a.pd; row_b[1][tid] = jh * s - p; row_b[2][tid] = jw * s - p;
       }
-      row_n[tid] = nb * a.di;
-      row_out[tid] = ((nb * a.do_ + od) * a.ho + oh) * a.wo + ow;
+      const bool inside = od < a.do_ && oh < a.ho && ow < a.wo;  // ceil-sized class grids
+      row_n[tid] = inside ? nb * a.di : -1;
+      row_out[tid] = inside ? ((nb * a.do_ + od) * a.ho + oh) * a.wo + ow : -1;
     } else {
       row_n[tid] = -1; row_out[tid] = -1;
       row_b[0][tid] = row_b[1][tid] = row_b[2][tid] = 0;

@@ -62,8 +62,9 @@ def test_conf_2d_step_matches_oracle():
                        gp_weight=None, weight_clip=0.01)
     recs, refs = {}, {}
     for dt in (torch.float32, torch.float64):
-        cp = {k: v.to(dt) if v.is_floating_point() else v.clone() for k, v in gpar.items()}
-        cd = {k: v.to(dt) if v.is_floating_point() else v.clone() for k, v in dpar.items()}
+        # copies (the oracle updates its parameters and BatchNorm buffers in place)
+        cp = {k: v.to(dt, copy=True) if v.is_floating_point() else v.clone() for k, v in gpar.items()}
+        cd = {k: v.to(dt, copy=True) if v.is_floating_point() else v.clone() for k, v in dpar.items()}
         rec = {}
         refs[dt] = R.train_step(cp, cd, R.AdamState(LR, *BETAS), R.AdamState(LR, *BETAS),
                                 torch.from_numpy(opt).to(dt), torch.from_numpy(sub).to(dt), torch.from_numpy(seg),
@@ -138,3 +139,20 @@ def test_planar_conv_matches_torch_conv2d(transposed):
     y = torch.empty((n, Ho, Ho, cout), device="cuda")
     ops.conv(geo, xd, wd, y)
     assert_close(y.permute(0, 3, 1, 2).cpu().numpy(), ref.numpy(), 1e-4, "planar fwd")
+    if transposed:
+        return
+    # input-grad and weight-grad of the same Conv2d from a random output gradient
+    gy = rng.standard_normal(tuple(ref.shape)).astype(np.float32)
+    gyt = torch.from_numpy(gy).double()
+    dx_ref = torch.nn.grad.conv2d_input(xt.shape, wt, gyt, stride=s, padding=p)
+    dw_ref = torch.nn.grad.conv2d_weight(xt, wt.shape, gyt, stride=s, padding=p)
+    gyd = torch.from_numpy(gy).cuda().permute(0, 2, 3, 1).contiguous()
+    gd = ops.conv_dgrad_geom(n, (1, H, H), (1, Ho, Ho), cin, cout, k, s, p, planar=True)
+    dx = torch.empty((n, H, H, cin), device="cuda")
+    ops.conv(gd, gyd, wd, dx)
+    assert_close(dx.permute(0, 3, 1, 2).cpu().numpy(), dx_ref.numpy(), 1e-4, "planar dgrad")
+    gw = ops.conv_wgrad_geom(n, (1, H, H), (1, Ho, Ho), cin, cout, k, s, p, planar=True)
+    dw = torch.empty_like(wd)
+    ws = torch.empty(ops.wgrad_ws_floats(gw), device="cuda")
+    ops.wgrad(gw, xd, gyd, dw, ws)
+    assert_close(dw.cpu().numpy(), dw_ref.numpy(), 1e-4, "planar wgrad")

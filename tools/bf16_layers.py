@@ -151,6 +151,19 @@ def generator_layers(S=32, n=2):
             z = F.conv_transpose3d(hin, w, stride=2, padding=1, output_padding=1)
         dz = plan.z[i].cpu().numpy()
         print(f"{i} {ly.name:40s} z rel-L2 {rel(dz, z.permute(0, 2, 3, 4, 1).numpy()):.3e}")
+        # BatchNorm (+ act, + residual) applied to the device's own z: the apply pass alone
+        zt = plan.z[i].cpu().double().permute(0, 4, 1, 2, 3)
+        nb = f"{ly.name}.normalization"
+        yb = F.batch_norm(zt, None, None, W[f"{nb}.weight"], W[f"{nb}.bias"], True, 0.1, 1e-5)
+        if ly.act == L.ACT_RELU:
+            yb = F.relu(yb)
+        if ly.name.endswith("block0"):
+            res_in = prev
+        if ly.residual:
+            yb = yb + res_in
+        yl = plan.y16[i] if plan.y_dead[i] else plan.y[i]
+        print(f"   y rel-L2 {rel(yl.float().cpu().numpy(), yb.permute(0, 2, 3, 4, 1).numpy()):.3e} "
+              f"(dead fp32: {plan.y_dead[i]}, shadow: {plan.y16[i] is not None})")
         # the device's own output of the layer feeds the next
         yl = plan.y16[i] if plan.y_dead[i] else plan.y[i]
         prev = cf(yl.float())

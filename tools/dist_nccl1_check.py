@@ -1,7 +1,9 @@
 """The RCCL data-parallel path on ONE GPU: a one-rank nccl process group with CGAN3D_FORCE_DP=1
 runs the bucketed generator all-reduces (communication stream ordered after the main and side
-streams, async RCCL all-reduce per bucket from plan host callables, wait before Adam) and the
-critic all-reduce.  Over one rank the mean is the identity, so three plan-replayed steps must match
+streams, one RCCL all-reduce per bucket, wait before Adam) and the critic all-reduce — by default
+through this library's own communicator (ops.NativeComm, cgan3d_allreduce_mean: recorded into the
+launch plan, which stays one C segment), with CGAN3D_TORCH_COMM=1 through torch.distributed as
+host callables between the plan's C segments.  Over one rank the mean is the identity, so three plan-replayed steps must match
 an engine without collectives (up to weight-gradient atomics order).  Each compared step starts
 from the same state (the reference engine's weights, Adam moments and BatchNorm buffers copied in
 place): with beta1 = 0 Adam turns a last-bit gradient difference into a whole step of the other
@@ -64,7 +66,9 @@ def main():
         e.step()  # eager (code objects load lazily)
         plans.append(e.record())
     hosts = sum(1 for it in plans[0].items if not isinstance(it, int))
-    assert hosts == len(dp.g_buckets) + 2, hosts
+    native = os.environ.get("CGAN3D_TORCH_COMM") != "1"
+    assert (dp.native is not None) == native
+    assert hosts == (0 if native else len(dp.g_buckets) + 2), hosts
     for _ in range(3):
         sync_state(ref, dp)
         for e in engs:
@@ -76,7 +80,8 @@ def main():
     for a, b in ((dp.g_arena, ref.g_arena), (dp.d_arena, ref.d_arena)):
         err = float((a.grad - b.grad).abs().max()) / float(b.grad.abs().max())
         assert err <= 1e-3, f"gradients differ by {err:.2e} of the largest"
-    print(f"nccl one-rank data-parallel path ok: {len(dp.g_buckets)} buckets, {hosts} host callables", flush=True)
+    print(f"nccl one-rank data-parallel path ok ({'native RCCL' if native else 'torch.distributed'}): "
+          f"{len(dp.g_buckets)} buckets, {hosts} host callables, {len(plans[0].items)} plan segments", flush=True)
     dist.destroy_process_group()
 
 
