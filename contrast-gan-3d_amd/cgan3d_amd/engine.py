@@ -549,6 +549,14 @@ class CriticPlan:
                   and not os.environ.get("CGAN3D_NO_SIDE_STREAM"))
         self.side = torch.cuda.Stream(device=device) if on_gpu else None
         self.ws_side = torch.empty(ws, device=device) if on_gpu else self.ws
+        # without CGAN3D_CRITIC_SIDE: only the penalty update's bias sums and first-layer weight grad
+        # (c1_wgrad, ~36 us at 64^3 B=4, needs nothing the forward-mode chain produces) go to a side
+        # stream — one hand-off each way, beside the small-grid forward-mode chain
+        # (CGAN3D_CRITIC_W0_SIDE=0: all on the main stream, for A/B runs)
+        self.side0 = None
+        if (self.side is None and torch.device(device).type == "cuda" and not os.environ.get("CGAN3D_NO_SIDE_STREAM")
+                and os.environ.get("CGAN3D_CRITIC_W0_SIDE", "1") == "1"):
+            self.side0 = torch.cuda.Stream(device=device)
         if self.bn:  # conv outputs, pre-activation grads, statistics and per-pass scale/shift
             self.z = [torch.empty_like(self.a[i]) if b else None for i, b in enumerate(self.is_bn)]
             self.dy = [torch.empty_like(self.a[i]) if b else None for i, b in enumerate(self.is_bn)]
@@ -708,6 +716,8 @@ class CriticPlan:
     def join_side(self):
         if self.side is not None:
             ops.stream_wait(torch.cuda.current_stream(self.device), self.side)
+        if self.side0 is not None:
+            ops.stream_wait(torch.cuda.current_stream(self.device), self.side0)
 
     def _wgrad(self, g, a, b, dw, ws, zeroed: bool, layer: Optional[int] = None):
         """``layer``: defer the unpack of an atomic-workspace weight grad into the layer's own clean
@@ -742,13 +752,27 @@ class CriticPlan:
         stream.  Call ``join_side`` before anything reads the gradients or reuses a / dz."""
         ws = self.ws_side
 
-        self._on_side(lambda: self._bias_sums(G, n_bias, side=True).run())
-
         def wgrad(i, prev):
             ly = self.layers[i]
             g = ops.with_prec(ops.conv_wgrad_geom(n_all, ly.din, ly.dout, ly.cin, ly.cout, ly.k, ly.s, ly.p, planar=self.pl), self.prec)
             self._wgrad(g, prev, self.dz[i][:n_all], G[f"{ly.name}.weight"], ws, zeroed, layer=i)
-        self._on_side(lambda: wgrad(0, x_all))  # x_all's interpolation rows hold gamma = nu_0
+        if self.side0 is not None:  # bias sums + the first layer's weight grad beside the chain below
+            ops.stream_wait(self.side0, torch.cuda.current_stream(self.device))
+            with torch.cuda.stream(self.side0):
+                self._bias_sums(G, n_bias, side=True).run()
+                # x_all's interpolation rows hold gamma = nu_0; its own all-zero workspace, unpacked
+                # on this stream (nothing of it is deferred to the main stream's unpack launch)
+                ly = self.layers[0]
+                g = ops.with_prec(ops.conv_wgrad_geom(n_all, ly.din, ly.dout, ly.cin, ly.cout, ly.k, ly.s, ly.p,
+                                                      planar=self.pl), self.prec)
+                if getattr(self, "ws_side0", None) is None:
+                    self.ws_side0 = torch.zeros(ops.wgrad_ws_floats(g), device=self.ws.device)
+                atomic = zeroed and ops.wgrad_ws_atomic(g)
+                ops.wgrad(g, x_all, self.dz[0][:n_all], G[f"{ly.name}.weight"], self.ws_side0, accumulate=zeroed,
+                          ws_clean=atomic)
+        else:
+            self._on_side(lambda: self._bias_sums(G, n_bias, side=True).run())
+            self._on_side(lambda: wgrad(0, x_all))
         h = gamma
         for i, ly in enumerate(self.layers[:-1]):
             g = self._geo(ops.conv_fwd_geom(n, ly.din, ly.dout, ly.cin, ly.cout, ly.k, ly.s, ly.p, planar=self.pl), self.wf[i])

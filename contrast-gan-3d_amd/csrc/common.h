@@ -172,6 +172,7 @@ void k7m_w2n_launch(const cgan3d_conv_geom* g, int P, int reflect, long long wc,
                     float* y, const Epi& e, hipStream_t s);
 // implicit-GEMM forward / input-grad (conv_gemm.hip)
 int gemm_blocks(const cgan3d_conv_geom* g, long long* mblocks);
+void cout1_wave_set(int v);
 bool wgrad_bf16_ok(const cgan3d_conv_geom* g);
 bool wgrad_c1_ok(const cgan3d_conv_geom* g);
 bool wgrad_k3_ok(const cgan3d_conv_geom* g);

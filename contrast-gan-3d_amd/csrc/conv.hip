@@ -150,6 +150,78 @@ __global__ __launch_bounds__(256) void conv_cout1_wave_kernel(ConvArgs a, const 
   }
 }
 
+// The same contraction with the whole block (4 waves) on one output voxel: for the critic's last
+// layer at small batches the wave-per-voxel grid is a few dozen blocks whose lanes each walk 16
+// dependent float4 loads; here every voxel's 1024 float4 of (tap, channel) are split over 256
+// threads (4 loads each) and reduced through LDS.
+__global__ __launch_bounds__(256) void conv_cout1_block_kernel(ConvArgs a, const float* __restrict__ x,
+                                                               const float* __restrict__ w, float* y, Epi ep) {
+  extern __shared__ __attribute__((aligned(16))) float Ws[];  // [T][cin]
+  __shared__ float red[4];
+  const int T = a.kd * a.k * a.k;
+  for (int i0 = threadIdx.x; i0 < T * a.cin; i0 += 8 * blockDim.x) {
+    float v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int i = i0 + u * blockDim.x, ci = i / T, t = i - ci * T;
+      v[u] = i < T * a.cin ? w[(long long)ci * a.sa + t] : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int i = i0 + u * blockDim.x, ci = i / T, t = i - ci * T;
+      if (i < T * a.cin) Ws[t * a.cin + ci] = v[u];
+    }
+  }
+  const long long lin = blockIdx.x;
+  int ow = (int)(lin % a.wo); long long tt = lin / a.wo;
+  int oh = (int)(tt % a.ho); tt /= a.ho;
+  int od = (int)(tt % a.do_); int nb = (int)(tt / a.do_);
+  const int bd = od * a.sd - a.pd, bh = oh * a.s - a.p, bw = ow * a.s - a.p;
+  const int C4 = a.cin >> 2, R4 = T * C4;
+  // the x loads do not depend on the staged weights: issue them before the barrier
+  constexpr int MAXR = 8;  // float4 per thread (R4 <= 2048)
+  f32x4 xv[MAXR];
+  int toff[MAXR];
+#pragma unroll
+  for (int u = 0; u < MAXR; ++u) {
+    const int r4 = threadIdx.x + 256 * u;
+    xv[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+    toff[u] = -1;
+    if (r4 < R4) {
+      const int t = r4 / C4, c = (r4 - t * C4) * 4;
+      const int td = t / (a.k * a.k), th = (t / a.k) % a.k, tw = t % a.k;
+      const int id = gcoord(bd, td, a.di, a.reflect), ih = gcoord(bh, th, a.hi, a.reflect),
+                iw = gcoord(bw, tw, a.wi, a.reflect);
+      if ((id | ih | iw) >= 0) {
+        xv[u] = *reinterpret_cast<const f32x4*>(x + ((long long)((nb * a.di + id) * a.hi + ih) * a.wi + iw) * a.cin + c);
+        toff[u] = t * a.cin + c;
+      }
+    }
+  }
+  __syncthreads();
+  float acc = 0.f;
+#pragma unroll
+  for (int u = 0; u < MAXR; ++u) {
+    if (toff[u] >= 0) {
+      const f32x4 wv = *reinterpret_cast<const f32x4*>(Ws + toff[u]);
+      acc += xv[u][0] * wv[0] + xv[u][1] * wv[1] + xv[u][2] * wv[2] + xv[u][3] * wv[3];
+    }
+  }
+  acc = wave_sum(acc);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float v = red[0] + red[1] + red[2] + red[3] + (ep.bias ? ep.bias[0] : 0.f);
+    if (ep.act == CGAN3D_ACT_RELU) v = fmaxf(v, 0.f);
+    else if (ep.act == CGAN3D_ACT_LRELU) v = v > 0.f ? v : v * ep.slope;
+    else if (ep.act == CGAN3D_ACT_TANH) v = tanhf(v);
+    if (ep.mask_src) v = ep.mask_src[lin] > 0.f ? v : v * ep.slope;
+    if (ep.residual) v += ep.residual[lin];
+    y[lin] = v;
+    if (ep.out2) ep.out2[lin] = ep.minuend[lin] - v;
+  }
+}
+
 // One thread per output voxel, weights in LDS.
 __global__ __launch_bounds__(256) void conv_cout1_kernel(ConvArgs a, const float* __restrict__ x,
                                                          const float* __restrict__ w, float* y, Epi ep) {
@@ -435,6 +507,11 @@ __global__ __launch_bounds__(256) void wgrad_unpack_multi_kernel(const cgan3d_un
 
 using namespace cg;
 
+namespace cg {
+static int g_cout1_wave = 0;  // cgan3d_set_tuning key 14: 1 keeps the wave-per-voxel kernel (A/B)
+void cout1_wave_set(int v) { g_cout1_wave = v; }
+}  // namespace cg
+
 static Epi to_epi(const cgan3d_epilogue* ep) {
   Epi e{};
   if (ep) {
@@ -518,6 +595,13 @@ cout1:
     CG_CHECK_ARG(make_args(g, &a, 256), "cgan3d_conv3d_fwd: transposed output dims must divide stride");
     size_t lds = (size_t)geom_taps(g) * g->cin * sizeof(float);
     CG_CHECK_ARG(lds <= 64 * 1024, "cgan3d_conv3d_fwd: cout==1 weights exceed LDS");
+    const long long r4 = (long long)geom_taps(g) * g->cin / 4;
+    if (!g->transposed && g->cin % 4 == 0 && a.class_vox <= 4096 && r4 <= 2048 && !g_cout1_wave) {
+      // very few outputs, long reductions: a block per output voxel
+      ::cg::launch(conv_cout1_block_kernel, dim3((unsigned)a.class_vox), dim3(256), lds, s, a, x, w, y, e);
+      CG_LAUNCH_CHECK("conv_cout1_block_kernel");
+      return CGAN3D_OK;
+    }
     if (!g->transposed && g->cin % 4 == 0 && a.class_vox <= 16384) {  // few outputs, long reductions
       ::cg::launch(conv_cout1_wave_kernel, dim3(cg::ceil_div(a.class_vox, 4)), dim3(256), lds, s, a, x, w, y, e);
       CG_LAUNCH_CHECK("conv_cout1_wave_kernel");

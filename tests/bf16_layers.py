@@ -52,10 +52,12 @@ class Recorder:
         return {k: v for k, (v, _) in self.rows.items()}
 
 
-def generator_layers(eng, rec: Recorder, tol=1e-4, tol16=2e-3):
-    """The generator of a StepEngine after ``generator_forward`` + ``generator_update``."""
-    G, P = eng.G, eng.gP
-    W = {k: v.detach().cpu().double() for k, v in P.items()}
+def generator_layers(eng, rec: Recorder, weights=None, tol=1e-4, tol16=2e-3):
+    """The generator of a StepEngine after ``generator_forward`` + ``generator_update``;
+    ``weights``: the generator's parameters before that update's Adam step (the forward and
+    backward ran with them)."""
+    G = eng.G
+    W = {k: v.detach().cpu().double() for k, v in (weights or eng.gP).items()}
     grads = {k: v.detach().cpu().double() for k, v in eng.gG.items()}
     x = cf(eng.subopt)
 
