@@ -218,11 +218,16 @@ def main():
     if world > 1:
         import torch.distributed as dist
         dist.init_process_group("nccl", device_id=dev)
-    elif os.environ.get("CGAN3D_FORCE_DP") == "1":  # the data-parallel path over a one-rank RCCL group
+    elif os.environ.get("CGAN3D_FORCE_DP") in ("1", "init", "native"):
+        # "1": the data-parallel path over a one-rank RCCL group; "init" / "native" (diagnostics): the
+        # group (and a native communicator) exist but the engine runs its single-GPU step
         import torch.distributed as dist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29541")
         dist.init_process_group("nccl", device_id=dev, rank=0, world_size=1)
+        if os.environ["CGAN3D_FORCE_DP"] == "native":
+            from cgan3d_amd import ops as _ops
+            _probe_comm = _ops.NativeComm(None, dev, own=True)  # noqa: F841 (kept alive for the run)
 
     from torch import nn
     from cgan3d_amd.data.synthetic import synth_patches

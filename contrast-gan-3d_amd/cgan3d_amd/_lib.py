@@ -131,6 +131,7 @@ _SIGS = {
     "cgan3d_plan_run": ([_P], _I32),
     "cgan3d_plan_destroy": ([_P], _I32),
     "cgan3d_stream_wait": ([_P, _P], _I32),
+    "cgan3d_comm_shared_library": ([], _I32),
     "cgan3d_comm_id_bytes": ([], _I32),
     "cgan3d_comm_unique_id": ([_P], _I32),
     "cgan3d_comm_init": ([_P, _I32, _I32, C.POINTER(C.c_void_p)], _I32),

@@ -269,14 +269,28 @@ def stream_wait(waiter, signaler):
 
 
 class NativeComm:
-    """This library's RCCL communicator over a torch.distributed process group's ranks
-    (include/cgan3d.h cgan3d_comm_*): rank 0's unique id is broadcast through ``group`` once, and
-    ``allreduce_mean`` is then a plain C-ABI launch — recorded into launch plans like a kernel."""
+    """RCCL all-reduces as C-ABI launches over a torch.distributed process group's ranks
+    (include/cgan3d.h cgan3d_comm_*), recorded into launch plans like a kernel.
 
-    def __init__(self, group=None, device=None):
+    Default: the process group's own communicator (ProcessGroupNCCL._comm_ptr), driven through the
+    RCCL library torch loaded — one communicator per process.  ``own=True`` (or
+    CGAN3D_OWN_COMM=1): a communicator of this library, rank 0's unique id broadcast through
+    ``group`` once (measured: a second communicator in the process slows every kernel of a one-GPU
+    step ~2.4x, profiles/r03_dp1_probe.json)."""
+
+    def __init__(self, group=None, device=None, own=None):
         import torch.distributed as dist
         lib = L.lib()
         self.world, self.rank = dist.get_world_size(group), dist.get_rank(group)
+        self.owned = False
+        if own is None:
+            own = os.environ.get("CGAN3D_OWN_COMM") == "1"
+        if not own:
+            ptr = self._torch_comm(group, device)
+            if ptr and int(lib.cgan3d_comm_shared_library()) == 1:
+                self.handle = ctypes.c_void_p(ptr)
+                return
+        self.owned = True
         nb = int(lib.cgan3d_comm_id_bytes())
         uid = torch.zeros(nb, dtype=torch.uint8, device=device)
         if self.rank == 0:
@@ -290,13 +304,30 @@ class NativeComm:
         check(lib.cgan3d_comm_init(raw, self.world, self.rank, ctypes.byref(h)), "comm_init")
         self.handle = h
 
+    @staticmethod
+    def _torch_comm(group, device):
+        """The ncclComm_t of ``group``'s nccl backend (0 if unavailable); a first collective
+        creates it when the group was not initialised eagerly (init_process_group(device_id=))."""
+        import torch.distributed as dist
+        pg = group if group is not None else dist.distributed_c10d._get_default_group()
+        try:
+            be = pg._get_backend(torch.device(device))
+            ptr = int(be._comm_ptr())
+            if not ptr:
+                dist.all_reduce(torch.zeros(1, device=device), group=group)
+                torch.cuda.synchronize(device)
+                ptr = int(be._comm_ptr())
+            return ptr
+        except (AttributeError, RuntimeError):
+            return 0
+
     def allreduce_mean(self, t: torch.Tensor):
         """t = mean over the ranks of t (fp32, contiguous), on the current stream."""
         _need(t, t.numel(), "allreduce_mean")
         check(_launch("cgan3d_allreduce_mean", self.handle, ptr(t), t.numel()), "allreduce_mean")
 
     def __del__(self):
-        if getattr(self, "handle", None) is not None and L._lib is not None:
+        if getattr(self, "owned", False) and getattr(self, "handle", None) is not None and L._lib is not None:
             L._lib.cgan3d_comm_destroy(self.handle)
             self.handle = None
 

@@ -24,6 +24,7 @@ struct Rccl {
   ncclResult_t (*all_reduce)(const void*, void*, size_t, ncclDataType_t, ncclRedOp_t, ncclComm_t, hipStream_t) = nullptr;
   const char* (*error_string)(ncclResult_t) = nullptr;
   bool ok = false;
+  bool shared = false;  // resolved from the RCCL the process had already loaded (torch.distributed's)
 };
 
 static Rccl& rccl() {
@@ -34,6 +35,7 @@ static Rccl& rccl() {
       h = dlopen(name, RTLD_NOW | RTLD_NOLOAD);  // the one torch.distributed already uses
       if (h) break;
     }
+    x.shared = h != nullptr;
     if (!h) h = dlopen("librccl.so.1", RTLD_NOW | RTLD_LOCAL);
     if (!h) h = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_LOCAL);
     if (!h) return x;
@@ -68,6 +70,8 @@ extern "C" int cgan3d_comm_unique_id(void* out) {
   std::memcpy(out, &id, sizeof(id));
   return CGAN3D_OK;
 }
+
+extern "C" int32_t cgan3d_comm_shared_library(void) { return rccl().ok && rccl().shared ? 1 : 0; }
 
 extern "C" int cgan3d_comm_init(const void* unique_id, int32_t nranks, int32_t rank, void** comm) {
   CG_RCCL_READY("cgan3d_comm_init");

@@ -384,11 +384,14 @@ int cgan3d_stream_wait(void* waiter, void* signaler);
 
 /* ---- data-parallel gradient averaging (RCCL over xGMI), SURVEY.md §8e.  Replaces the gradient
  * all-reduce DDP would issue around optimizer_D.step() / optimizer_G.step() (Trainer.py:135,157):
- * the reference itself runs on one device.  A communicator of this library (not torch's process
- * group): rank 0 creates the unique id (cgan3d_comm_id_bytes() bytes), the caller broadcasts it,
- * every rank calls cgan3d_comm_init.  cgan3d_allreduce_mean averages n fp32 in place on `stream`
- * and is recorded into a launch plan like a kernel launch (cgan3d_plan_*), so a data-parallel
- * step replays as one plan. */
+ * the reference itself runs on one device.  `comm` is an ncclComm_t: either the caller's own
+ * (torch.distributed's, when cgan3d_comm_shared_library() == 1, i.e. the entry points resolve to
+ * the RCCL the process has already loaded — the default, one communicator per process), or one
+ * of this library's: rank 0 creates the unique id (cgan3d_comm_id_bytes() bytes), the caller
+ * broadcasts it, every rank calls cgan3d_comm_init.  cgan3d_allreduce_mean averages n fp32 in
+ * place on `stream` and is recorded into a launch plan like a kernel launch (cgan3d_plan_*), so a
+ * data-parallel step replays as one plan. */
+int32_t cgan3d_comm_shared_library(void);
 int32_t cgan3d_comm_id_bytes(void);
 int cgan3d_comm_unique_id(void* out);
 int cgan3d_comm_init(const void* unique_id, int32_t nranks, int32_t rank, void** comm);

@@ -200,3 +200,56 @@ def test_trainer_plan_replay_matches_eager(tmp_path, precision, monkeypatch):
                     it, k, float(d.max()), float(off.mean()))
     assert planned.optimizer_D._host_step == eager.optimizer_D._host_step == 7
     assert planned.optimizer_G._host_step == eager.optimizer_G._host_step == 4
+
+
+@pytest.mark.timeout(240)
+def test_validate_at_reference_val_patch_matches_oracle(tmp_path):
+    """Trainer.validate (Trainer.py:247-307) at basic_conf's validation patch, VAL_PATCH_SIZE =
+    (256, 256, 128) (constants.py:12, basic_conf.py:72): the basic_conf generator (4 ResNet blocks,
+    16 initial channels) and BatchNorm critic in eval mode with non-trivial running statistics, one
+    patch per scan type, against the float64 oracle — the D / G / sim losses at 1e-3 of the terms
+    they sum (D is a difference of critic means)."""
+    from oracle import reference_torch as R
+    from cgan3d_amd.data.synthetic import synth_patches
+    from cgan3d_amd.model.discriminator import PatchGANDiscriminator
+    from cgan3d_amd.model.generator import ResnetGenerator
+    from cgan3d_amd.model.loss import HULoss
+    from cgan3d_amd.trainer.Trainer import Trainer
+    g_args = dict(n_resnet_blocks=4, n_updownsample_blocks=2, init_channels_out=16)
+    d_args = dict(channels_in=1, init_channels_out=8, discriminator_depth=3, negative_slope=0.2)
+    torch.manual_seed(0)
+    tr = Trainer(1, 1, 1, 1, 1, 1, 1000, partial(ResnetGenerator, **g_args), partial(PatchGANDiscriminator, **d_args),
+                 partial(torch.optim.Adam, lr=2e-4, betas=(0.5, 0.999)),
+                 partial(torch.optim.Adam, lr=2e-4, betas=(0.5, 0.999)), HULoss(-0.2, 0.6), _LoggerInterface(),
+                 torch.device("cuda"), checkpoint_dir=tmp_path, checkpoint_every=None, weight_clip=0.01)
+    rng = np.random.Generator(np.random.PCG64(5))
+    with torch.no_grad():
+        for mod in (tr.generator, tr.critic):
+            for k, b in mod.named_buffers():
+                if k.endswith("running_mean"):
+                    b.copy_(torch.from_numpy(rng.normal(0.0, 0.3, b.shape).astype(np.float32)))
+                elif k.endswith("running_var"):
+                    b.copy_(torch.from_numpy(rng.uniform(0.5, 2.0, b.shape).astype(np.float32)))
+    shape = (256, 256, 128)
+    data = {st: synth_patches(1, shape, 30 + i)[0] for i, st in enumerate((0, -1, 1))}
+    loaders = {st: iter([{"data": torch.from_numpy(x)}]) for st, x in data.items()}
+    got = {k: float(v) for k, v in tr.validate(loaders, 0).items()}
+
+    def p64(mod):
+        return {k: v.detach().cpu().double() if v.is_floating_point() else v.detach().cpu().clone()
+                for k, v in mod.state_dict().items()}
+    gp, dp = p64(tr.generator), p64(tr.critic)
+    gcfg, dcfg = R.GenConfig(**{k: g_args[k] for k in ("n_resnet_blocks", "n_updownsample_blocks",
+                                                       "init_channels_out")}), R.CriticConfig(norm="batch")
+    with torch.no_grad():
+        real = float(R.critic_forward(dp, torch.from_numpy(data[0]).double(), dcfg, training=False).mean())
+        fakes, sims = [], []
+        for st in (-1, 1):
+            x = torch.from_numpy(data[st]).double()
+            xh = x - R.generator_forward(gp, x, gcfg, training=False)
+            fakes.append(float(R.critic_forward(dp, xh, dcfg, training=False).mean()))
+            sims.append(float(R.zncc_loss(xh, x)))
+    want = {"D": -real + sum(fakes), "G": -sum(fakes) / 2, "sim": sum(sims) / 2}
+    scale = {"D": max(abs(real), *map(abs, fakes)), "G": max(map(abs, fakes)), "sim": max(map(abs, sims))}
+    for k in want:
+        assert abs(got[k] - want[k]) <= 1e-3 * scale[k], (k, got[k], want[k])

@@ -1,8 +1,8 @@
 """The RCCL data-parallel path on ONE GPU: a one-rank nccl process group with CGAN3D_FORCE_DP=1
 runs the bucketed generator all-reduces (communication stream ordered after the main and side
 streams, one RCCL all-reduce per bucket, wait before Adam) and the critic all-reduce — by default
-through this library's own communicator (ops.NativeComm, cgan3d_allreduce_mean: recorded into the
-launch plan, which stays one C segment), with CGAN3D_TORCH_COMM=1 through torch.distributed as
+as C-ABI launches on the process group's communicator (ops.NativeComm, cgan3d_allreduce_mean:
+recorded into the launch plan, which stays one C segment), with CGAN3D_TORCH_COMM=1 through torch.distributed as
 host callables between the plan's C segments.  Over one rank the mean is the identity, so three plan-replayed steps must match
 an engine without collectives (up to weight-gradient atomics order).  Each compared step starts
 from the same state (the reference engine's weights, Adam moments and BatchNorm buffers copied in
