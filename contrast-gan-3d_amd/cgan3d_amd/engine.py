@@ -946,7 +946,7 @@ class StepEngine:
         self.losses = torch.zeros(8, device=device)
         self.loss_ws = torch.empty(ops.loss_ws_floats(), device=device)
         self._pending = []  # in-flight bucket all-reduces of the generator gradients
-        self.g_buckets = self._make_g_buckets(G_BUCKET_BYTES) if self.dp else []
+        self.g_buckets = self._make_g_buckets(G_BUCKET_BYTES) if (self.dp and G_BUCKET_BYTES > 0) else []
         on_gpu = torch.device(device).type == "cuda"
         self.comm = torch.cuda.Stream(device=device) if (self.dp and on_gpu) else None
         # RCCL from C++ (ops.NativeComm): with the nccl backend the all-reduces are C-ABI launches,
@@ -1144,11 +1144,13 @@ class StepEngine:
         ops.generator_output_grad(self.opt_hat, self.subopt, self.G.att, self.mask, self.dcrit, bs * V, self.lo,
                                   self.hi, self.sim_w, self.hu_w, self.G.dz_last, self.losses, self.loss_ws)
         ops.zero(self.g_arena.grad_padded)  # optimizer_G.zero_grad (Trainer.py:146): every layer then accumulates
-        if self.dp:  # bucketed, overlapped with the rest of the backward
+        if self.dp and self.g_buckets:  # bucketed, overlapped with the rest of the backward
             self.G.backward(self.gP, self.gG, self.subopt, grads_enqueued=self._bucket_ready, zeroed=True)
             self._finish_allreduce()
         else:
             self.G.backward(self.gP, self.gG, self.subopt, zeroed=True)
+            if self.dp:  # CGAN3D_G_BUCKET_BYTES=0: one all-reduce of the whole gradient (main stream)
+                self._allreduce(self.g_arena.grad)
         self._optim_step(self.g_optim, self.G)
 
     @staticmethod
