@@ -58,13 +58,24 @@ LN_STATS, LN_BWD, LN_JVP, LN_SIG, LN_ADJ = range(5)
 PREC_F32, PREC_BF16 = 0, 1
 
 
+class BnFuse(C.Structure):
+    """include/cgan3d.h cgan3d_bn_fuse: BatchNorm fused across a conv boundary."""
+    _fields_ = [("acc_out", C.c_void_p), ("acc_mode", C.c_int32), ("reps", C.c_int32), ("pre_mode", C.c_int32),
+                ("pre_act", C.c_int32), ("pre_slope", C.c_float), ("eps", C.c_float), ("momentum", C.c_float),
+                ("zero_n", C.c_int32), ("nvox", C.c_double), ("acc_in", C.c_void_p), ("z", C.c_void_p),
+                ("res", C.c_void_p), ("dy", C.c_void_p), ("gamma", C.c_void_p), ("beta", C.c_void_p),
+                ("rmean", C.c_void_p), ("rvar", C.c_void_p), ("nbt", C.c_void_p), ("ss", C.c_void_p),
+                ("mi", C.c_void_p), ("dgamma", C.c_void_p), ("dbeta", C.c_void_p), ("y", C.c_void_p),
+                ("y16", C.c_void_p), ("zero", C.c_void_p)]
+
+
 class Epilogue(C.Structure):
     _fields_ = [("bias", C.c_void_p), ("residual", C.c_void_p), ("mask_src", C.c_void_p),
                 ("minuend", C.c_void_p), ("out2", C.c_void_p), ("stats", C.c_void_p),
                 ("act", C.c_int32), ("slope", C.c_float),
                 ("bn_part", C.c_void_p), ("bn_mode", C.c_int32), ("bn_slots", C.c_int32), ("bn_z", C.c_void_p),
                 ("bn_ss", C.c_void_p), ("bn_mi", C.c_void_p), ("bn_act", C.c_int32), ("bn_slope", C.c_float),
-                ("x_bf16", C.c_void_p), ("bn_fold", C.c_int32)]
+                ("x_bf16", C.c_void_p), ("bn_fold", C.c_int32), ("fuse", C.POINTER(BnFuse))]
 
 
 _P, _I32, _I64, _F = C.c_void_p, C.c_int32, C.c_int64, C.c_float
@@ -83,6 +94,7 @@ _SIGS = {
     "cgan3d_conv3d_wgrad": ([_P, _P, _P, _P, _I32, _P, _P], _I32),
     "cgan3d_conv3d_shadow_only": ([_P, _I32], _I32),
     "cgan3d_conv3d_bn_fold_ok": ([_P], _I32),
+    "cgan3d_bn_fuse_ok": ([_P, _I32], _I32),
     "cgan3d_conv3d_wgrad_ex": ([_P, _P, _P, _P, _I32, _P, _P, _P, _P], _I32),
     "cgan3d_bn_finalize": ([_P, _I64, _I32, _P, _P, _P, _P, _P, _F, _F, _P, _P, _P], _I32),
     "cgan3d_bn_apply": ([_P, _I64, _I32, _P, _I32, _F, _P, _P, _P, _P], _I32),

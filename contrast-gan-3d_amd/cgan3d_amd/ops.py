@@ -189,12 +189,70 @@ def convt_wgrad_geom(n, din, dout, cin, cout, k, s, p, planar=False):
     return _geom(n, dout, din, cout, cin, k, s, p, 0, 0, t, cout * t, planar)
 
 
+class BnFuse:
+    """BatchNorm fused across a conv boundary (include/cgan3d.h cgan3d_bn_fuse), as tensors.
+
+    Producer half (``acc_mode`` 3 forward / 4 input-grad): the conv adds its BatchNorm statistic
+    pairs into ``acc_out`` (float64 [reps][2][cout]).  Consumer half (``pre_mode`` 1 forward / 2
+    input-grad, ResNet-block convs only): the conv computes its input from the previous layer's
+    BatchNorm (``z``, ``res`` / ``dy``, the producer's ``acc_in``) while staging and writes the
+    tensor that BatchNorm pass would have produced (``y`` fp32 / ``y16`` bf16, optional)."""
+
+    def __init__(self, acc_out=None, acc_mode=0, reps=1, pre_mode=0, pre_act=L.ACT_NONE, pre_slope=0.0, eps=1e-5,
+                 momentum=0.1, nvox=0, acc_in=None, z=None, res=None, dy=None, gamma=None, beta=None, rmean=None,
+                 rvar=None, nbt=None, ss=None, mi=None, dgamma=None, dbeta=None, y=None, y16=None, zero=None):
+        self.acc_out, self.acc_mode, self.reps = acc_out, int(acc_mode), int(reps)
+        self.pre_mode, self.pre_act, self.pre_slope = int(pre_mode), int(pre_act), float(pre_slope)
+        self.eps, self.momentum, self.nvox = float(eps), float(momentum), float(nvox)
+        self.acc_in, self.z, self.res, self.dy = acc_in, z, res, dy
+        self.gamma, self.beta, self.rmean, self.rvar, self.nbt = gamma, beta, rmean, rvar, nbt
+        self.ss, self.mi, self.dgamma, self.dbeta = ss, mi, dgamma, dbeta
+        self.y, self.y16, self.zero = y, y16, zero
+
+    def check(self, g, what):
+        if self.acc_mode:
+            _need(self.acc_out, self.reps * 2 * g.cout, f"{what} acc_out", dtype=torch.float64)
+        if self.pre_mode:
+            nin, c = _vox_in(g) * g.cin, g.cin
+            _need(self.acc_in, self.reps * 2 * c, f"{what} acc_in", dtype=torch.float64)
+            for t, nm in ((self.z, "z"), (self.res, "res"), (self.dy, "dy"), (self.y, "y")):
+                if t is not None:
+                    _need(t, nin, f"{what} {nm}")
+            if self.y16 is not None:
+                _need(self.y16, nin, f"{what} y16", dtype=torch.bfloat16)
+            for t, nm in ((self.gamma, "gamma"), (self.beta, "beta"), (self.rmean, "rmean"), (self.rvar, "rvar"),
+                          (self.dgamma, "dgamma"), (self.dbeta, "dbeta")):
+                if t is not None:
+                    _need(t, c, f"{what} {nm}")
+            for t, nm in ((self.ss, "ss"), (self.mi, "mi")):
+                _need(t, 2 * c, f"{what} {nm}")
+            if self.zero is not None:
+                _need(self.zero, self.zero.numel(), f"{what} zero", dtype=torch.float64)
+
+    def c(self) -> "L.BnFuse":
+        f = L.BnFuse()
+        f.acc_out, f.acc_mode, f.reps, f.pre_mode = ptr(self.acc_out), self.acc_mode, self.reps, self.pre_mode
+        f.pre_act, f.pre_slope, f.eps, f.momentum = self.pre_act, self.pre_slope, self.eps, self.momentum
+        f.zero_n = self.zero.numel() if self.zero is not None else 0
+        f.nvox, f.acc_in, f.z, f.res, f.dy = self.nvox, ptr(self.acc_in), ptr(self.z), ptr(self.res), ptr(self.dy)
+        f.gamma, f.beta, f.rmean, f.rvar = ptr(self.gamma), ptr(self.beta), ptr(self.rmean), ptr(self.rvar)
+        f.nbt, f.ss, f.mi, f.dgamma, f.dbeta = ptr(self.nbt), ptr(self.ss), ptr(self.mi), ptr(self.dgamma), ptr(self.dbeta)
+        f.y, f.y16, f.zero = ptr(self.y), ptr(self.y16), ptr(self.zero)
+        return f
+
+
+def bn_fuse_ok(g, consumer: bool) -> bool:
+    """True if the launch of ``g`` takes the producer (False) / consumer (True) half of BnFuse."""
+    return bool(L.load().cgan3d_bn_fuse_ok(ctypes.byref(g), int(consumer)))
+
+
 class Epi:
     """Fused-epilogue operands (include/cgan3d.h cgan3d_epilogue), kept as tensors for checks."""
 
     def __init__(self, bias=None, residual=None, mask_src=None, minuend=None, out2=None, stats=None,
                  act=L.ACT_NONE, slope=0.0, bn_part=None, bn_mode=0, bn_slots=0, bn_z=None, bn_ss=None,
-                 bn_mi=None, bn_act=L.ACT_NONE, bn_slope=0.0, x_bf16=None, bn_fold=0):
+                 bn_mi=None, bn_act=L.ACT_NONE, bn_slope=0.0, x_bf16=None, bn_fold=0, fuse=None):
+        self.fuse = fuse  # BnFuse or None
         self.bias, self.residual, self.mask_src = bias, residual, mask_src
         self.x_bf16 = x_bf16  # bf16 copy of the conv input (ResNet-block kernel halo source)
         self.minuend, self.out2, self.stats = minuend, out2, stats
@@ -223,6 +281,8 @@ class Epi:
         e.bn_ss, e.bn_mi, e.bn_act, e.bn_slope = ptr(self.bn_ss), ptr(self.bn_mi), self.bn_act, self.bn_slope
         e.x_bf16 = ptr(self.x_bf16)
         e.bn_fold = self.bn_fold
+        if self.fuse is not None:
+            e.fuse = ctypes.pointer(self.fuse.c())  # the pointer object keeps the struct alive
         return e
 
 
@@ -461,6 +521,8 @@ def conv(g: ConvGeom, x: torch.Tensor, w: torch.Tensor, y: torch.Tensor, ep: Opt
         f = ep.bn_fold
         nz = None if not f else g.n * (g.do_ - 2 * f) * (g.ho - 2 * f) * (g.wo - 2 * f) * g.cout
         ep.check_bn(ny, g.cout, "conv", nz)
+        if ep.fuse is not None:
+            ep.fuse.check(g, "conv")
     check(_timed("conv", g, "cgan3d_conv3d_fwd", ctypes.byref(g), ptr(x), ptr(w), ptr(y),
                  ctypes.byref(ep.c()) if ep is not None else None), "conv3d_fwd")
 

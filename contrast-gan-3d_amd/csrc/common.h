@@ -109,6 +109,31 @@ inline int geom_kd(const cgan3d_conv_geom* g) { return g->planar ? 1 : g->k; }
 inline int geom_sd(const cgan3d_conv_geom* g) { return g->planar ? 1 : g->stride; }
 inline int geom_pd(const cgan3d_conv_geom* g) { return g->planar ? 0 : g->pad; }
 
+// device-side view of cgan3d_bn_fuse (BatchNorm fused across a conv boundary, include/cgan3d.h)
+struct BnFuse {
+  double* acc_out;
+  int acc_mode, reps, pre_mode, pre_act;
+  float pre_slope, eps, momentum;
+  int zero_n;
+  double nvox;
+  const double* acc_in;
+  const float* z;
+  const float* res;
+  const float* dy;
+  const float* gamma;
+  const float* beta;
+  float* rmean;
+  float* rvar;
+  long long* nbt;
+  float* ss;
+  float* mi;
+  float* dgamma;
+  float* dbeta;
+  float* y;
+  __bf16* y16;
+  double* zero;
+};
+
 // device-side view of cgan3d_epilogue
 struct Epi {
   const float* bias;
@@ -129,6 +154,7 @@ struct Epi {
   float bn_slope;
   const __bf16* x16;  // optional bf16 shadow of the conv input
   int bn_fold;        // mode 2 over a reflect-padded k7 input-grad grid (cgan3d_epilogue.bn_fold)
+  BnFuse fz;          // all-zero unless cgan3d_epilogue.fuse is given
 };
 
 __device__ __forceinline__ float act_grad(float pre, int act, float slope) {
@@ -209,6 +235,7 @@ void halo_set_dbg(int v);
 int wgrad_bf16_launch(const cgan3d_conv_geom* g, const float* gathered, const float* aligned, float* dwp,
                       hipStream_t st);
 bool halo_ok(const cgan3d_conv_geom* g);         // w_packed == 2 and eligible
+bool k3_fuse_ok(const cgan3d_conv_geom* g);      // the ResNet-block kernel: consumer half of cgan3d_bn_fuse
 bool halo_format_ok(const cgan3d_conv_geom* g);  // eligible ignoring w_packed
 long long halo_mblocks(const cgan3d_conv_geom* g);
 int halo_launch(const cgan3d_conv_geom* g, const float* x, const float* w, float* y, const Epi& e, hipStream_t st);

@@ -522,8 +522,42 @@ static Epi to_epi(const cgan3d_epilogue* ep) {
     e.bn_act = ep->bn_act; e.bn_slope = ep->bn_slope;
     e.x16 = reinterpret_cast<const __bf16*>(ep->x_bf16);
     e.bn_fold = ep->bn_fold;
+    if (const cgan3d_bn_fuse* f = ep->fuse) {
+      BnFuse& z = e.fz;
+      z.acc_out = f->acc_out; z.acc_mode = f->acc_mode; z.reps = f->reps; z.pre_mode = f->pre_mode;
+      z.pre_act = f->pre_act; z.pre_slope = f->pre_slope; z.eps = f->eps; z.momentum = f->momentum;
+      z.zero_n = f->zero ? f->zero_n : 0; z.nvox = f->nvox; z.acc_in = f->acc_in; z.z = f->z; z.res = f->res;
+      z.dy = f->dy; z.gamma = f->gamma; z.beta = f->beta; z.rmean = f->rmean; z.rvar = f->rvar;
+      z.nbt = reinterpret_cast<long long*>(f->nbt); z.ss = f->ss; z.mi = f->mi; z.dgamma = f->dgamma;
+      z.dbeta = f->dbeta; z.y = f->y; z.y16 = static_cast<__bf16*>(f->y16); z.zero = f->zero;
+    }
   }
   return e;
+}
+
+extern "C" int32_t cgan3d_bn_fuse_ok(const cgan3d_conv_geom* g, int32_t consumer) {
+  if (!g || g->w_packed != 2 || !halo_ok(g) || s2_kind(g)) return 0;  // halo_epilogue kernels only
+  return consumer ? (k3_fuse_ok(g) ? 1 : 0) : 1;
+}
+
+// host checks of a cgan3d_bn_fuse against the launch it rides on
+static int check_fuse(const cgan3d_conv_geom* g, const Epi& e) {
+  const BnFuse& f = e.fz;
+  if (!f.acc_mode && !f.pre_mode) return CGAN3D_OK;
+  CG_CHECK_ARG(cgan3d_bn_fuse_ok(g, f.pre_mode != 0), "bn_fuse: geometry does not take the fused BatchNorm");
+  CG_CHECK_ARG(f.acc_mode == 0 || f.acc_mode == 3 || f.acc_mode == 4, "bn_fuse: acc_mode must be 0, 3 or 4");
+  CG_CHECK_ARG(f.pre_mode >= 0 && f.pre_mode <= 2, "bn_fuse: pre_mode must be 0, 1 or 2");
+  CG_CHECK_ARG(f.reps >= 1 && f.reps <= 64, "bn_fuse: reps must be 1..64");
+  CG_CHECK_ARG(!f.acc_mode || (f.acc_out && !e.bn_mode && !e.stats), "bn_fuse: acc_mode needs acc_out and no slab");
+  CG_CHECK_ARG(f.acc_mode != 4 || (e.bn_z && e.bn_ss && e.bn_mi), "bn_fuse: acc_mode 4 needs bn_z, bn_ss, bn_mi");
+  if (f.pre_mode) {
+    CG_CHECK_ARG(f.acc_in && f.z && f.gamma && f.ss && f.mi && f.nvox > 0, "bn_fuse: pre_mode operands missing");
+    CG_CHECK_ARG(f.pre_mode != 1 || f.beta, "bn_fuse: pre_mode 1 needs beta");
+    CG_CHECK_ARG(f.pre_mode != 2 || (f.dy && f.dgamma && f.dbeta && !f.res), "bn_fuse: pre_mode 2 needs dy, dgamma, dbeta");
+    CG_CHECK_ARG(!e.x16, "bn_fuse: pre_mode computes the input (no x_bf16)");
+    CG_CHECK_ARG(f.zero_n >= 0 && (f.zero_n == 0 || f.zero), "bn_fuse: zero_n without zero");
+  }
+  return CGAN3D_OK;
 }
 
 extern "C" int64_t cgan3d_conv3d_bn_slots(const cgan3d_conv_geom* g) {
@@ -553,6 +587,7 @@ extern "C" int cgan3d_conv3d_fwd(const cgan3d_conv_geom* g, const float* x, cons
   if (st) return st;
   CG_CHECK_ARG(x && w && y, "cgan3d_conv3d_fwd: null pointer");
   Epi e = to_epi(ep);
+  if (int rc = check_fuse(g, e)) return rc;
   CG_CHECK_ARG(!(e.out2 && (!e.minuend || g->cout != 1)), "cgan3d_conv3d_fwd: out2 needs minuend and cout==1");
   CG_CHECK_ARG(e.bn_mode >= 0 && e.bn_mode <= 2, "cgan3d_conv3d_fwd: bn_mode must be 0, 1 or 2");
   CG_CHECK_ARG(e.bn_mode != 2 || (e.bn_z && e.bn_ss && e.bn_mi), "cgan3d_conv3d_fwd: bn_mode 2 needs bn_z, bn_ss, bn_mi");

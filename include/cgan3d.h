@@ -87,6 +87,59 @@ typedef struct cgan3d_conv_geom {
  *  bn_mode 2: v is dL/dy of a BatchNorm layer y = act(z * scale + shift) whose input z has the
  *             layout of this output: (sum g, sum g*xhat) with g = v * act'(z*scale + shift),
  *             xhat = (z - mean) * invstd (cgan3d_bn_backward_finalize_slab). */
+/* BatchNorm fused across a conv boundary (bf16 generator path, ResNet chain — model/blocks.py:50-53,
+ * 85-88: conv -> BatchNorm3d -> act (+ skip) -> next conv).  Two halves, usable separately:
+ *
+ * Producer (acc_mode != 0; the halo-tiled kernels: cgan3d_halo_eligible geometries, w_packed 2):
+ * instead of a slab, every block adds its per-channel pair into fp64 accumulators
+ * acc_out[(r * 2 + q) * cout + c] (replica r = block % reps; reps * 2 * cout doubles, zero before
+ * the launch):
+ *   acc_mode 3 (forward): q = 0 sum v, q = 1 sum v^2 (v = the BatchNorm input z, this output);
+ *   acc_mode 4 (input-grad): the pair of bn_mode 2 — sum g, sum g*xhat — with bn_z / bn_ss / bn_mi /
+ *              bn_act of the epilogue.
+ * Consumer (pre_mode != 0; the ResNet-block kernel only: k3 s1 p1 64 -> 64, cgan3d_bn_fuse_ok): the
+ * conv's input x is not read; each staged input element is computed from the previous BatchNorm
+ * layer, whose statistics every block combines from acc_in (the producer's accumulator) in fp64:
+ *   pre_mode 1 (forward, the BatchNorm3d + act of model/blocks.py:53 and the skip add of :88):
+ *     x = act(z * scale + shift) (+ res), scale = gamma * invstd, shift = beta - mean * scale;
+ *     block (0, 0) writes ss = [scale | shift], mi = [mean | invstd] and updates the running
+ *     buffers (momentum, unbiased variance) and nbt, as cgan3d_bn_finalize_slab;
+ *   pre_mode 2 (input-grad, autograd of the same): x = dz = gamma * invstd * (g - mean(g) -
+ *     xhat * mean(g * xhat)), g = dy * act'(z * scale + shift), from ss / mi of the forward;
+ *     block (0, 0) adds sum g into dbeta and sum g*xhat into dgamma.
+ *   The blocks of output-channel block 0 also write the interior of their input tile (every input
+ *   voxel exactly once): y (fp32, optional) and y16 (bf16 copy, optional) — the tensors the
+ *   BatchNorm pass would have produced.  Block (0, 0) zeroes `zero_n` doubles at `zero` first (an
+ *   accumulator the stream is done with; the caller rotates them so none needs its own memset). */
+typedef struct cgan3d_bn_fuse {
+  double* acc_out;
+  int32_t acc_mode;     /* 0, 3, 4 */
+  int32_t reps;         /* replicas of acc_out / acc_in (1..64) */
+  int32_t pre_mode;     /* 0, 1, 2 */
+  int32_t pre_act;      /* CGAN3D_ACT_NONE / RELU / LRELU of the previous layer */
+  float pre_slope;
+  float eps;
+  float momentum;
+  int32_t zero_n;
+  double nvox;          /* BatchNorm reduction count (voxels per channel) */
+  const double* acc_in;
+  const float* z;       /* BatchNorm input of the previous layer (this conv's input layout) */
+  const float* res;     /* pre_mode 1: added after the activation (NULL: none) */
+  const float* dy;      /* pre_mode 2: dL/dy */
+  const float* gamma;
+  const float* beta;
+  float* rmean;
+  float* rvar;
+  int64_t* nbt;
+  float* ss;            /* pre_mode 1: written; 2: read */
+  float* mi;            /* pre_mode 1: written; 2: read */
+  float* dgamma;        /* pre_mode 2: accumulated */
+  float* dbeta;
+  float* y;             /* interior output fp32 (NULL: not written) */
+  void* y16;            /* interior output bf16 (NULL: not written) */
+  double* zero;
+} cgan3d_bn_fuse;
+
 typedef struct cgan3d_epilogue {
   const float* bias;
   const float* residual;
@@ -110,7 +163,11 @@ typedef struct cgan3d_epilogue {
                                 * conv's, generator.py:78-84): the statistics are those of the
                                 * reflect-folded tensor (pad bn_fold), bn_z lives on the unpadded
                                 * grid; see cgan3d_bn_backward_slab_fold.  0 otherwise. */
+  const cgan3d_bn_fuse* fuse;  /* NULL, or BatchNorm fused across the conv boundary (above) */
 } cgan3d_epilogue;
+
+/* 1 when the geometry's launch can take cgan3d_bn_fuse pre_mode (consumer) / acc_mode (producer). */
+int32_t cgan3d_bn_fuse_ok(const cgan3d_conv_geom* g, int32_t consumer);
 
 const char* cgan3d_version(void);
 const char* cgan3d_get_last_error(void);

@@ -71,6 +71,38 @@ def test_engine_step_dry_run_shapes(g_args, S, b, clip):
         assert eng.D.layers[-2].cout == 128
 
 
+@pytest.mark.parametrize("S,b", [(64, 4), ((64, 48, 32), 2)])
+def test_bf16_engine_fuses_resnet_chain_batchnorm(S, b):
+    """bf16 engine (dry run): the ResNet chain's BatchNorms are fused across the conv boundaries
+    (include/cgan3d.h cgan3d_bn_fuse) — forward: down1 .. rb3.b0 applied by the next ResNet conv;
+    backward: rb0.b0 .. rb3.b1 by their own input-grad conv — every launch passes the host checks,
+    and each fused consumer zeroes its predecessor's accumulator (the first the last one's)."""
+    from cgan3d_amd import ops
+    from cgan3d_amd.engine import StepEngine
+    from cgan3d_amd.model.discriminator import PatchGANDiscriminator
+    from cgan3d_amd.model.generator import ResnetGenerator
+    g = ResnetGenerator(4, 2, 16)
+    d = PatchGANDiscriminator(**D_ARGS, norm_layer=nn.Identity)
+    dims = tuple(S) if isinstance(S, tuple) else (S, S, S)
+    ops.DRY_RUN = True
+    try:
+        eng = StepEngine(g, d, g.config, d.config, b, b, dims, device=torch.device("cpu"), precision="bf16")
+        eng.step()
+    finally:
+        ops.DRY_RUN = False
+    G = eng.G
+    names = [ly.name.replace("model.", "") for ly in G.layers]
+    assert [names[j] for j in range(len(names)) if G.fz_f[j]] == \
+        ["downsampling.1"] + [f"resnet_backbone.{r}.block{k}" for r in range(4) for k in range(2)][:-1]
+    assert [names[j] for j in range(len(names)) if G.fz_b[j]] == \
+        [f"resnet_backbone.{r}.block{k}" for r in range(4) for k in range(2)]
+    fo = [j for j in range(len(names)) if G.fz_f[j]]
+    assert G.fz_zero_f[fo[0]] is G.acc_f[fo[-1]] and all(G.fz_zero_f[fo[k]] is G.acc_f[fo[k - 1]] for k in range(1, len(fo)))
+    # the fp32 tensors the fused passes leave unwritten are the ones no kernel reads
+    assert all(G.y_dead[j] for j in fo if G.layers[j].name.endswith("block0"))
+    assert all(G.dz_dead[j] for j in range(len(names)) if G.fz_b[j])
+
+
 def test_2d_models_match_reference_layout():
     """conf_2D's modules (is_2D): Conv2d / ConvTranspose2d / BatchNorm2d with the reference's keys."""
     from oracle import reference_torch as R
