@@ -59,14 +59,8 @@ PREC_F32, PREC_BF16 = 0, 1
 
 
 class BnFuse(C.Structure):
-    """include/cgan3d.h cgan3d_bn_fuse: BatchNorm fused across a conv boundary."""
-    _fields_ = [("acc_out", C.c_void_p), ("acc_mode", C.c_int32), ("reps", C.c_int32), ("pre_mode", C.c_int32),
-                ("pre_act", C.c_int32), ("pre_slope", C.c_float), ("eps", C.c_float), ("momentum", C.c_float),
-                ("zero_n", C.c_int32), ("nvox", C.c_double), ("acc_in", C.c_void_p), ("z", C.c_void_p),
-                ("res", C.c_void_p), ("dy", C.c_void_p), ("gamma", C.c_void_p), ("beta", C.c_void_p),
-                ("rmean", C.c_void_p), ("rvar", C.c_void_p), ("nbt", C.c_void_p), ("ss", C.c_void_p),
-                ("mi", C.c_void_p), ("dgamma", C.c_void_p), ("dbeta", C.c_void_p), ("y", C.c_void_p),
-                ("y16", C.c_void_p), ("zero", C.c_void_p)]
+    """include/cgan3d.h cgan3d_bn_fuse: BatchNorm statistics into fp64 accumulators."""
+    _fields_ = [("acc_out", C.c_void_p), ("acc_mode", C.c_int32), ("reps", C.c_int32)]
 
 
 class Epilogue(C.Structure):
@@ -94,7 +88,7 @@ _SIGS = {
     "cgan3d_conv3d_wgrad": ([_P, _P, _P, _P, _I32, _P, _P], _I32),
     "cgan3d_conv3d_shadow_only": ([_P, _I32], _I32),
     "cgan3d_conv3d_bn_fold_ok": ([_P], _I32),
-    "cgan3d_bn_fuse_ok": ([_P, _I32], _I32),
+    "cgan3d_bn_fuse_ok": ([_P], _I32),
     "cgan3d_conv3d_wgrad_ex": ([_P, _P, _P, _P, _I32, _P, _P, _P, _P], _I32),
     "cgan3d_bn_finalize": ([_P, _I64, _I32, _P, _P, _P, _P, _P, _F, _F, _P, _P, _P], _I32),
     "cgan3d_bn_apply": ([_P, _I64, _I32, _P, _I32, _F, _P, _P, _P, _P], _I32),
@@ -105,6 +99,12 @@ _SIGS = {
     "cgan3d_bn_backward_slab": ([_P, _P, _I64, _I32, _P, _I32, _P, _P, _P, _I32, _F, _P, _P, _P, _I32, _P, _P, _P],
                                 _I32),
     "cgan3d_bn_backward_ws_floats": ([_I64, _I32], _I64),
+    "cgan3d_bn_apply_acc": ([_P, _I32, _I32, _I64, _P, _P, _P, _P, _P, _F, _F, _P, _P, _P, _I32, _F, _P, _P, _P, _P,
+                             _I32, _P], _I32),
+    "cgan3d_bn_backward_acc_fold": ([_P, _P, _I32, _I32, _I32, _I32, _I32, _I32, _P, _I32, _P, _P, _P, _I32, _F, _P,
+                                     _P, _P, _I32, _P, _P, _I32, _P], _I32),
+    "cgan3d_bn_backward_acc": ([_P, _P, _I64, _I32, _P, _I32, _P, _P, _P, _I32, _F, _P, _P, _P, _I32, _P, _P, _I32,
+                                _P], _I32),
     "cgan3d_bn_backward_slab_fold": ([_P, _P, _I32, _I32, _I32, _I32, _I32, _I32, _P, _I32, _P, _P, _P, _I32, _F, _P,
                                       _P, _P, _I32, _P, _P, _P], _I32),
     "cgan3d_bn_backward": ([_P, _P, _I64, _I32, _P, _P, _P, _I32, _F, _P, _P, _P, _I32, _P, _P], _I32),

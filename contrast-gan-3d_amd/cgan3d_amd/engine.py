@@ -283,37 +283,31 @@ class GeneratorPlan:
                 if self.dz16[i] is not None and BN_FUSED_BWD:
                     reads_ok = i == 0 or (self.y16[i - 1] is not None and ops.shadow_only(self.geo_dgrad[i], 0))
                     self.dz_dead[i] = reads_ok and ops.shadow_only(self.geo_wgrad[i], 1)
-        # BatchNorm fused across conv boundaries (cgan3d_bn_fuse): layer j's forward BatchNorm is applied by
-        # conv j+1 while staging (fz_f[j]) and its backward by layer j's own input-grad conv (fz_b[j]),
-        # from fp64 accumulators the producing launch fills (acc_f / acc_b).  Each consumer zeroes the
-        # accumulator its predecessor in the chain read (fz_zero_*), the first the last one's.
+        # BatchNorm statistics through fp64 accumulators (cgan3d_bn_fuse acc_mode 3 / 4) wherever the
+        # producing conv can write them (halo-tiled, stride-2 and 1 -> 16 k7 kernels; bf16): the
+        # finalize is folded into the elementwise pass, one launch per layer and direction (ac_f[j]:
+        # cgan3d_bn_apply_acc; ac_b[j]: cgan3d_bn_backward_acc / _acc_fold); CGAN3D_NO_BN_FUSE=1 keeps
+        # the slab + finalize path (A/B).  Each elementwise launch zeroes the accumulator its
+        # predecessor in the same direction read, the first the last one's, so none needs a memset.
         nl = len(layers)
-        self.fz_f, self.fz_b = [False] * nl, [False] * nl
-        if (not os.environ.get("CGAN3D_NO_BN_FUSE") and prec == L.PREC_BF16 and not pl and BN_FUSED_BWD
-                and not os.environ.get("CGAN3D_KEEP_FP32")):
-            # fp32 readers of y_j left once conv j+1 computes its input itself: the skip path (y_j is
-            # the input of a ResNet block) and the weight grad of layer j+1 unless it reads the shadows
-            res_src = {j - 1 for j, ly in enumerate(layers) if ly.name.endswith("block0")}
-            for j in range(nl - 1):
-                if (layers[j].kind == "conv" and self.y16[j] is not None and self.dz16[j + 1] is not None
-                        and ops.shadow_only(self.geo_wgrad[j + 1], 1)
-                        and ops.bn_fuse_ok(self.geo_fwd[j + 1], True) and ops.bn_fuse_ok(self.geo_fwd[j], False)):
-                    self.fz_f[j] = True
-                    self.y_dead[j] = j not in res_src
-            # dz_j's readers once layer j's input-grad conv computes it itself: its weight grad only
-            for j in range(1, nl - 1):
-                if (self.dz16[j] is not None and self.y16[j - 1] is not None and ops.shadow_only(self.geo_wgrad[j], 1)
-                        and ops.bn_fuse_ok(self.geo_dgrad[j], True) and ops.bn_fuse_ok(self.geo_dgrad[j + 1], False)):
-                    self.fz_b[j] = True
-                    self.dz_dead[j] = True
+        self.ac_f, self.ac_b = [False] * nl, [False] * nl
+        if not os.environ.get("CGAN3D_NO_BN_FUSE") and prec == L.PREC_BF16 and not pl and BN_FUSED_BWD:
+            self.ac_f = [ops.bn_fuse_ok(self.geo_fwd[j]) for j in range(nl)]
+            self.ac_b = [j + 1 < nl and ops.bn_fuse_ok(self.geo_dgrad[j + 1]) for j in range(nl)]
+            self.ac_b[-1] = bool(self.fold_bn and ops.bn_fuse_ok(self.geo_last_dgrad))
+            if sum(self.ac_f) < 2:
+                self.ac_f = [False] * nl
+            if sum(self.ac_b) < 2:
+                self.ac_b = [False] * nl
+
         def accs(flags):
             return [torch.zeros(FUSE_REPS * 2 * ly.cout, device=device, dtype=torch.float64) if f else None
                     for ly, f in zip(layers, flags)]
-        self.acc_f, self.acc_b = accs(self.fz_f), accs(self.fz_b)
-        fo = [j for j in range(nl) if self.fz_f[j]]            # consumers run in this order (forward)
-        bo = [j for j in range(nl - 1, -1, -1) if self.fz_b[j]]  # (backward)
-        self.fz_zero_f = {j: self.acc_f[fo[k - 1]] for k, j in enumerate(fo)}
-        self.fz_zero_b = {j: self.acc_b[bo[k - 1]] for k, j in enumerate(bo)}
+        self.acc_f, self.acc_b = accs(self.ac_f), accs(self.ac_b)
+        fo = [j for j in range(nl) if self.ac_f[j]]              # their elementwise passes run in this order
+        bo = [j for j in range(nl - 1, -1, -1) if self.ac_b[j]]  # (backward)
+        self.acc_zero_f = {j: self.acc_f[fo[k - 1]] for k, j in enumerate(fo)}
+        self.acc_zero_b = {j: self.acc_b[bo[k - 1]] for k, j in enumerate(bo)}
         # weight gradients run on a side stream, beside the input-gradient chain (each wgrad only
         # needs its layer's dz and input, both final when it is enqueued); own workspace
         wsw = max([ops.wgrad_ws_floats(gw) for gw in self.geo_wgrad] + [ops.wgrad_ws_floats(self.geo_last_wgrad)])
@@ -340,13 +334,12 @@ class GeneratorPlan:
         self.packs.pack()
 
     # -- forward: x [n,D,H,W,1] -> att (tanh output); opt_hat_out = x - att (Trainer.py:170-171)
-    # Training-mode BatchNorm statistics are fused into the producing conv: per-block partials into a
-    # slab (bn_mode 1) that bn_apply_slab finalizes, or — across the ResNet chain (fz_f) — fp64
-    # accumulators that the next conv combines while it applies the BatchNorm to its staged input.
+    # Training-mode BatchNorm statistics are fused into the producing conv: fp64 accumulators (ac_f)
+    # or per-block partials into a slab (bn_mode 1), finalized by the elementwise launch.
     def forward(self, P: Dict[str, torch.Tensor], x: torch.Tensor, opt_hat_out: Optional[torch.Tensor] = None,
                 training: bool = True):
         h = x
-        h_res = h_prev_res = None
+        h_res = None
         for i, ly in enumerate(self.layers):
             if ly.name.endswith("block0"):
                 h_res = h
@@ -355,21 +348,21 @@ class GeneratorPlan:
             res = h_res if ly.residual else None
             h16 = self.y16[i - 1] if i > 0 else None
             if training:
-                pre = self._fuse_pre_fwd(P, i - 1, h_prev_res) if i > 0 and self.fz_f[i - 1] else None
-                if self.fz_f[i]:  # statistics into fp64 accumulators; conv i+1 applies this BatchNorm
-                    f = pre or ops.BnFuse()
-                    f.acc_out, f.acc_mode, f.reps = self.acc_f[i], 3, FUSE_REPS
-                    ep = ops.epilogue(x_bf16=None if pre else h16, fuse=f)
+                if self.ac_f[i]:  # statistics into fp64 accumulators, one finalize + apply launch
+                    ep = ops.epilogue(x_bf16=h16, fuse=ops.BnFuse(self.acc_f[i], 3, FUSE_REPS))
                 else:
-                    ep = ops.epilogue(bn_part=self.part_f[i], bn_mode=1, bn_slots=self.slots_f[i],
-                                      x_bf16=None if pre else h16, fuse=pre)
-                ops.conv(self.geo_fwd[i], self.z[i - 1] if pre else h, self.wf[i], self.z[i], ep)
-                if not self.fz_f[i]:
+                    ep = ops.epilogue(bn_part=self.part_f[i], bn_mode=1, bn_slots=self.slots_f[i], x_bf16=h16)
+                ops.conv(self.geo_fwd[i], h, self.wf[i], self.z[i], ep)
+                if self.ac_f[i]:
+                    ops.bn_apply_acc(self.acc_f[i], FUSE_REPS, ly.cout, nvox, P[f"{nb}.weight"], P[f"{nb}.bias"],
+                                     P[f"{nb}.running_mean"], P[f"{nb}.running_var"], P[f"{nb}.num_batches_tracked"],
+                                     self.ss[i], self.mi[i], self.z[i], ly.act, None if self.y_dead[i] else self.y[i],
+                                     residual=res, y16=self.y16[i], zero=self.acc_zero_f[i])
+                else:
                     ops.bn_apply_slab(self.part_f[i], self.slots_f[i], ly.cout, nvox, P[f"{nb}.weight"],
                                       P[f"{nb}.bias"], P[f"{nb}.running_mean"], P[f"{nb}.running_var"],
                                       P[f"{nb}.num_batches_tracked"], self.ss[i], self.mi[i], self.z[i], ly.act,
                                       None if self.y_dead[i] else self.y[i], residual=res, y16=self.y16[i])
-                h_prev_res = res
             else:
                 ops.conv(self.geo_fwd[i], h, self.wf[i], self.z[i], ops.epilogue(x_bf16=h16))
                 self._eval_scale_shift(P, nb, i)
@@ -381,27 +374,6 @@ class GeneratorPlan:
         ops.conv(self.geo_last_fwd, h, P["model.last_conv.weight"], self.att, ep)
         return self.att
 
-    def _fuse_pre_fwd(self, P, j: int, res) -> "ops.BnFuse":
-        """Consumer half of the fused forward BatchNorm of layer j (applied by conv j+1's staging):
-        y_j = act(BN(z_j)) (+ res) — written as y16 (and y where an fp32 reader remains)."""
-        ly = self.layers[j]
-        nb = f"{ly.name}.normalization"
-        return ops.BnFuse(pre_mode=1, pre_act=ly.act, nvox=self.n * ly.dout[0] * ly.dout[1] * ly.dout[2],
-                          reps=FUSE_REPS, acc_in=self.acc_f[j], z=self.z[j], res=res, gamma=P[f"{nb}.weight"],
-                          beta=P[f"{nb}.bias"], rmean=P[f"{nb}.running_mean"], rvar=P[f"{nb}.running_var"],
-                          nbt=P[f"{nb}.num_batches_tracked"], ss=self.ss[j], mi=self.mi[j],
-                          y=None if self.y_dead[j] else self.y[j], y16=self.y16[j], zero=self.fz_zero_f[j])
-
-    def _fuse_pre_bwd(self, P, G, i: int) -> "ops.BnFuse":
-        """Consumer half of the fused BatchNorm backward of layer i (applied by layer i's own
-        input-grad conv while staging dz_i; dz16_i written for the weight grad)."""
-        ly = self.layers[i]
-        nb = f"{ly.name}.normalization"
-        return ops.BnFuse(pre_mode=2, pre_act=ly.act, nvox=self.n * ly.dout[0] * ly.dout[1] * ly.dout[2],
-                          reps=FUSE_REPS, acc_in=self.acc_b[i], z=self.z[i], dy=self.dy[i], gamma=P[f"{nb}.weight"],
-                          ss=self.ss[i], mi=self.mi[i], dgamma=G[f"{nb}.weight"], dbeta=G[f"{nb}.bias"],
-                          y16=self.dz16[i], zero=self.fz_zero_b[i])
-
     def _bn_grad_epi(self, i, fused: bool = False):
         """Epilogue that accumulates BatchNorm layer i's backward statistics from its dL/dy (into
         the fp64 accumulator of the fused backward when ``fused``)."""
@@ -409,7 +381,7 @@ class GeneratorPlan:
             return ops.epilogue()
         if fused:
             return ops.epilogue(bn_z=self.z[i], bn_ss=self.ss[i], bn_mi=self.mi[i], bn_act=self.layers[i].act,
-                                fuse=ops.BnFuse(acc_out=self.acc_b[i], acc_mode=4, reps=FUSE_REPS))
+                                fuse=ops.BnFuse(self.acc_b[i], 4, FUSE_REPS))
         return ops.epilogue(bn_part=self.part_b[i], bn_mode=2, bn_slots=self.slots_b[i], bn_z=self.z[i],
                             bn_ss=self.ss[i], bn_mi=self.mi[i], bn_act=self.layers[i].act)
 
@@ -462,14 +434,13 @@ class GeneratorPlan:
         if grads_enqueued is not None:
             grads_enqueued(len(self.layers))
         if self.fold_bn:
-            ep = self._bn_grad_epi(len(self.layers) - 1)
+            ep = self._bn_grad_epi(len(self.layers) - 1, fused=self.ac_b[-1])
             ep.bn_fold = la.p
             ops.conv(self.geo_last_dgrad, self.dz_last, P["model.last_conv.weight"], self.dpad, ep)
         else:
             ops.conv(self.geo_last_dgrad, self.dz_last, P["model.last_conv.weight"], self.dpad)
             ops.reflect_fold(self.dpad, self.dy[-1], n, la.din, la.cin, la.p,
                              ep=self._bn_grad_epi(len(self.layers) - 1), planar=self.planar)
-        fb = zeroed and any(self.fz_b)  # fused BatchNorm backward (dgamma / dbeta added into the zeroed arena)
 
         def resnet_pair(j):  # layers j and j - 1 both in the ResNet chain
             return "resnet_backbone" in self.layers[j].name and "resnet_backbone" in self.layers[j - 1].name
@@ -477,9 +448,15 @@ class GeneratorPlan:
             ly = self.layers[i]
             nb = f"{ly.name}.normalization"
             nvox = n * ly.dout[0] * ly.dout[1] * ly.dout[2]
-            fused = fb and self.fz_b[i]
-            if fused:
-                pass  # applied by this layer's input-grad conv while staging (below)
+            if self.ac_b[i] and self.fold_bn and i == len(self.layers) - 1:
+                ops.bn_backward_acc_fold(self.dpad, self.z[i], n, ly.dout, ly.cout, la.p, self.acc_b[i], FUSE_REPS,
+                                         self.ss[i], self.mi[i], P[f"{nb}.weight"], ly.act, G[f"{nb}.weight"],
+                                         G[f"{nb}.bias"], None if self.dz_dead[i] else self.dz[i], dz16=self.dz16[i],
+                                         zero=self.acc_zero_b[i])
+            elif self.ac_b[i]:
+                ops.bn_backward_acc(self.dy[i], self.z[i], nvox, ly.cout, self.acc_b[i], FUSE_REPS, self.ss[i], self.mi[i],
+                                    P[f"{nb}.weight"], ly.act, G[f"{nb}.weight"], G[f"{nb}.bias"],
+                                    None if self.dz_dead[i] else self.dz[i], dz16=self.dz16[i], zero=self.acc_zero_b[i])
             elif BN_FUSED_BWD and self.fold_bn and i == len(self.layers) - 1:
                 ops.bn_backward_slab_fold(self.dpad, self.z[i], n, ly.dout, ly.cout, la.p, self.part_b[i],
                                           self.slots_b[i], self.ss[i], self.mi[i], P[f"{nb}.weight"], ly.act,
@@ -509,13 +486,6 @@ class GeneratorPlan:
             else:
                 fn = (lambda g=self.geo_wgrad[i], a=xin, b=self.dz[i], w=G[wname], a16=x16, b16=d16, m=main:
                       self._wgrad(g, a, b, w, zeroed, main=m, gathered16=a16, aligned16=b16))
-            if fused:
-                # the input-grad first: its staging writes dz16_i, the weight grad's operand
-                self._input_grad(P, G, i, fb)
-                pending.append((i, fn))
-                if len(pending) >= WGRAD_GROUP or not resnet_pair(i):
-                    flush()
-                continue
             if main:
                 if pending:
                     flush()
@@ -535,24 +505,16 @@ class GeneratorPlan:
                 flush()
             if i == 0:
                 break
-            self._input_grad(P, G, i, fb)
+            self._input_grad(P, G, i)
         if self.side is not None:  # the weight gradients are complete before anything reads them
             ops.stream_wait(torch.cuda.current_stream(self.device), self.side)
 
-    def _input_grad(self, P, G, i: int, fb: bool):
+    def _input_grad(self, P, G, i: int):
         """dL/dy of layer i - 1 from dz_i (a ResNet block0 also receives the skip gradient
-        dL/dh_{r+1}), with layer i - 1's BatchNorm backward statistics; under the fused backward dz_i
-        itself is computed while staging (fz_b[i])."""
+        dL/dh_{r+1}), with layer i - 1's BatchNorm backward statistics."""
         ly = self.layers[i]
-        ep = self._bn_grad_epi(i - 1, fused=fb and self.fz_b[i - 1])
+        ep = self._bn_grad_epi(i - 1, fused=self.ac_b[i - 1])
         ep.residual = self.dy[i + 1] if ly.name.endswith("block0") else None
-        if fb and self.fz_b[i]:
-            pre = self._fuse_pre_bwd(P, G, i)
-            if ep.fuse is not None:
-                pre.acc_out, pre.acc_mode, pre.reps = ep.fuse.acc_out, ep.fuse.acc_mode, ep.fuse.reps
-            ep.fuse = pre
-            ops.conv(self.geo_dgrad[i], self.dy[i], self.wd[i], self.dy[i - 1], ep)  # x: not read
-            return
         ep.x_bf16 = self.dz16[i] if BN_FUSED_BWD else None  # only the slab backward writes it
         ops.conv(self.geo_dgrad[i], self.dz[i], self.wd[i], self.dy[i - 1], ep)
 

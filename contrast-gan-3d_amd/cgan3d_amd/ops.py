@@ -190,60 +190,26 @@ def convt_wgrad_geom(n, din, dout, cin, cout, k, s, p, planar=False):
 
 
 class BnFuse:
-    """BatchNorm fused across a conv boundary (include/cgan3d.h cgan3d_bn_fuse), as tensors.
+    """BatchNorm statistics into fp64 accumulators (include/cgan3d.h cgan3d_bn_fuse): the producing
+    conv adds its statistic pairs into ``acc_out`` (float64 [reps][2][cout]) — ``acc_mode`` 3 forward
+    (sum, sum of squares), 4 input-grad (sum g, sum g*xhat, with the epilogue's bn_z / bn_ss / bn_mi)."""
 
-    Producer half (``acc_mode`` 3 forward / 4 input-grad): the conv adds its BatchNorm statistic
-    pairs into ``acc_out`` (float64 [reps][2][cout]).  Consumer half (``pre_mode`` 1 forward / 2
-    input-grad, ResNet-block convs only): the conv computes its input from the previous layer's
-    BatchNorm (``z``, ``res`` / ``dy``, the producer's ``acc_in``) while staging and writes the
-    tensor that BatchNorm pass would have produced (``y`` fp32 / ``y16`` bf16, optional)."""
-
-    def __init__(self, acc_out=None, acc_mode=0, reps=1, pre_mode=0, pre_act=L.ACT_NONE, pre_slope=0.0, eps=1e-5,
-                 momentum=0.1, nvox=0, acc_in=None, z=None, res=None, dy=None, gamma=None, beta=None, rmean=None,
-                 rvar=None, nbt=None, ss=None, mi=None, dgamma=None, dbeta=None, y=None, y16=None, zero=None):
+    def __init__(self, acc_out=None, acc_mode=0, reps=1):
         self.acc_out, self.acc_mode, self.reps = acc_out, int(acc_mode), int(reps)
-        self.pre_mode, self.pre_act, self.pre_slope = int(pre_mode), int(pre_act), float(pre_slope)
-        self.eps, self.momentum, self.nvox = float(eps), float(momentum), float(nvox)
-        self.acc_in, self.z, self.res, self.dy = acc_in, z, res, dy
-        self.gamma, self.beta, self.rmean, self.rvar, self.nbt = gamma, beta, rmean, rvar, nbt
-        self.ss, self.mi, self.dgamma, self.dbeta = ss, mi, dgamma, dbeta
-        self.y, self.y16, self.zero = y, y16, zero
 
     def check(self, g, what):
         if self.acc_mode:
             _need(self.acc_out, self.reps * 2 * g.cout, f"{what} acc_out", dtype=torch.float64)
-        if self.pre_mode:
-            nin, c = _vox_in(g) * g.cin, g.cin
-            _need(self.acc_in, self.reps * 2 * c, f"{what} acc_in", dtype=torch.float64)
-            for t, nm in ((self.z, "z"), (self.res, "res"), (self.dy, "dy"), (self.y, "y")):
-                if t is not None:
-                    _need(t, nin, f"{what} {nm}")
-            if self.y16 is not None:
-                _need(self.y16, nin, f"{what} y16", dtype=torch.bfloat16)
-            for t, nm in ((self.gamma, "gamma"), (self.beta, "beta"), (self.rmean, "rmean"), (self.rvar, "rvar"),
-                          (self.dgamma, "dgamma"), (self.dbeta, "dbeta")):
-                if t is not None:
-                    _need(t, c, f"{what} {nm}")
-            for t, nm in ((self.ss, "ss"), (self.mi, "mi")):
-                _need(t, 2 * c, f"{what} {nm}")
-            if self.zero is not None:
-                _need(self.zero, self.zero.numel(), f"{what} zero", dtype=torch.float64)
 
     def c(self) -> "L.BnFuse":
         f = L.BnFuse()
-        f.acc_out, f.acc_mode, f.reps, f.pre_mode = ptr(self.acc_out), self.acc_mode, self.reps, self.pre_mode
-        f.pre_act, f.pre_slope, f.eps, f.momentum = self.pre_act, self.pre_slope, self.eps, self.momentum
-        f.zero_n = self.zero.numel() if self.zero is not None else 0
-        f.nvox, f.acc_in, f.z, f.res, f.dy = self.nvox, ptr(self.acc_in), ptr(self.z), ptr(self.res), ptr(self.dy)
-        f.gamma, f.beta, f.rmean, f.rvar = ptr(self.gamma), ptr(self.beta), ptr(self.rmean), ptr(self.rvar)
-        f.nbt, f.ss, f.mi, f.dgamma, f.dbeta = ptr(self.nbt), ptr(self.ss), ptr(self.mi), ptr(self.dgamma), ptr(self.dbeta)
-        f.y, f.y16, f.zero = ptr(self.y), ptr(self.y16), ptr(self.zero)
+        f.acc_out, f.acc_mode, f.reps = ptr(self.acc_out), self.acc_mode, self.reps
         return f
 
 
-def bn_fuse_ok(g, consumer: bool) -> bool:
-    """True if the launch of ``g`` takes the producer (False) / consumer (True) half of BnFuse."""
-    return bool(L.load().cgan3d_bn_fuse_ok(ctypes.byref(g), int(consumer)))
+def bn_fuse_ok(g) -> bool:
+    """True if the launch of ``g`` can produce BnFuse accumulators."""
+    return bool(L.load().cgan3d_bn_fuse_ok(ctypes.byref(g)))
 
 
 class Epi:
@@ -697,6 +663,77 @@ def bn_backward_slab(dy, z, nvox, c, part, nslots, scale_shift, mean_invstd, gam
     check(_launch("cgan3d_bn_backward_slab", ptr(dy), ptr(z), nvox, c, ptr(part), nslots, ptr(scale_shift),
                   ptr(mean_invstd), ptr(gamma), act, slope, ptr(dgamma), ptr(dbeta), ptr(dz), int(accumulate),
                   ptr(ws), _need16(dz16, nvox * c, "bn_backward_slab dz16")), "bn_backward_slab")
+
+
+def bn_apply_acc(acc, reps, c, nvox, gamma, beta, rmean, rvar, nbt, scale_shift, mean_invstd, z, act, y,
+                 residual=None, slope=0.0, momentum=0.1, eps=1e-5, y16=None, zero=None):
+    """BatchNorm train forward + act (+ residual) from the producing conv's fp64 accumulators
+    (cgan3d_bn_apply_acc: finalize and elementwise pass in one launch; ``zero``: a float64 tensor
+    block 0 zeroes first)."""
+    _need(acc, reps * 2 * c, "bn_apply_acc acc", dtype=torch.float64, exact=False)
+    for t, nm in ((gamma, "gamma"), (beta, "beta")):
+        _need(t, c, f"bn_apply_acc {nm}")
+    for t, nm in ((scale_shift, "scale_shift"), (mean_invstd, "mean_invstd")):
+        _need(t, 2 * c, f"bn_apply_acc {nm}")
+    _need(z, nvox * c, "bn_apply_acc z")
+    if y is None and y16 is None:
+        raise ValueError("bn_apply_acc: y may be None only when y16 is given")
+    for t, nm in ((y, "y"), (residual, "residual")):
+        if t is not None:
+            _need(t, nvox * c, f"bn_apply_acc {nm}")
+    if zero is not None:
+        _need(zero, zero.numel(), "bn_apply_acc zero", dtype=torch.float64)
+    check(_launch("cgan3d_bn_apply_acc", ptr(acc), reps, c, nvox, ptr(gamma), ptr(beta), ptr(rmean), ptr(rvar),
+                  ptr(nbt), momentum, eps, ptr(scale_shift), ptr(mean_invstd), ptr(z), act, float(slope),
+                  ptr(residual), ptr(y), _need16(y16, nvox * c, "bn_apply_acc y16"), ptr(zero),
+                  zero.numel() if zero is not None else 0), "bn_apply_acc")
+
+
+def bn_backward_acc(dy, z, nvox, c, acc, reps, scale_shift, mean_invstd, gamma, act, dgamma, dbeta, dz, slope=0.0,
+                    accumulate=False, dz16=None, zero=None):
+    """BatchNorm backward from the fp64 accumulators the kernel that produced dy filled
+    (cgan3d_bn_backward_acc: one launch)."""
+    if dz is None and dz16 is None:
+        raise ValueError("bn_backward_acc: dz may be None only when dz16 is given")
+    for t, nm in ((dy, "dy"), (z, "z"), (dz, "dz")):
+        if t is not None:
+            _need(t, nvox * c, f"bn_backward_acc {nm}")
+    _need(acc, reps * 2 * c, "bn_backward_acc acc", dtype=torch.float64, exact=False)
+    for t, nm in ((scale_shift, "scale_shift"), (mean_invstd, "mean_invstd")):
+        _need(t, 2 * c, f"bn_backward_acc {nm}")
+    for t, nm in ((gamma, "gamma"), (dgamma, "dgamma"), (dbeta, "dbeta")):
+        _need(t, c, f"bn_backward_acc {nm}")
+    if zero is not None:
+        _need(zero, zero.numel(), "bn_backward_acc zero", dtype=torch.float64)
+    check(_launch("cgan3d_bn_backward_acc", ptr(dy), ptr(z), nvox, c, ptr(acc), reps, ptr(scale_shift),
+                  ptr(mean_invstd), ptr(gamma), act, slope, ptr(dgamma), ptr(dbeta), ptr(dz), int(accumulate),
+                  _need16(dz16, nvox * c, "bn_backward_acc dz16"), ptr(zero), zero.numel() if zero is not None else 0),
+          "bn_backward_acc")
+
+
+def bn_backward_acc_fold(padded, z, n, dims: Sequence[int], c, pad, acc, reps, scale_shift, mean_invstd, gamma,
+                         act, dgamma, dbeta, dz, slope=0.0, accumulate=False, dz16=None, zero=None):
+    """``bn_backward_slab_fold`` with the statistics from the fp64 accumulators of the last conv's
+    input-grad launch (cgan3d_bn_backward_acc_fold: one launch)."""
+    d, h, w = dims
+    nvox = n * d * h * w
+    _need(padded, n * (d + 2 * pad) * (h + 2 * pad) * (w + 2 * pad) * c, "bn_backward_acc_fold padded")
+    if dz is None and dz16 is None:
+        raise ValueError("bn_backward_acc_fold: dz may be None only when dz16 is given")
+    for t, nm in ((z, "z"), (dz, "dz")):
+        if t is not None:
+            _need(t, nvox * c, f"bn_backward_acc_fold {nm}")
+    _need(acc, reps * 2 * c, "bn_backward_acc_fold acc", dtype=torch.float64, exact=False)
+    for t, nm in ((scale_shift, "scale_shift"), (mean_invstd, "mean_invstd")):
+        _need(t, 2 * c, f"bn_backward_acc_fold {nm}")
+    for t, nm in ((gamma, "gamma"), (dgamma, "dgamma"), (dbeta, "dbeta")):
+        _need(t, c, f"bn_backward_acc_fold {nm}")
+    if zero is not None:
+        _need(zero, zero.numel(), "bn_backward_acc_fold zero", dtype=torch.float64)
+    check(_launch("cgan3d_bn_backward_acc_fold", ptr(padded), ptr(z), n, d, h, w, c, pad, ptr(acc), reps,
+                  ptr(scale_shift), ptr(mean_invstd), ptr(gamma), act, slope, ptr(dgamma), ptr(dbeta), ptr(dz),
+                  int(accumulate), _need16(dz16, nvox * c, "bn_backward_acc_fold dz16"), ptr(zero),
+                  zero.numel() if zero is not None else 0), "bn_backward_acc_fold")
 
 
 def bn_backward_slab_fold(padded, z, n, dims: Sequence[int], c, pad, part, nslots, scale_shift, mean_invstd, gamma,

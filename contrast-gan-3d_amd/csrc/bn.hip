@@ -207,12 +207,39 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const float* __restri
 // bn_bwd_apply_kernel with dy = reflect_fold(padded) gathered on the fly: per voxel the 1..8
 // padded sources that mirror onto it (fold_src), float4 of channels per thread, channels fixed per
 // thread (256 % (C/4) == 0); the bf16 copy (and the fp32 dz when asked) as bn_bwd_apply_kernel.
+__device__ __forceinline__ void acc_sums(const double* __restrict__ acc, int reps, int C, double* sums);
+
+// coef == NULL: the coefficients from fp64 accumulators (cgan3d_bn_backward_acc_fold): every block
+// combines the replicas, block 0 publishes dgamma / dbeta and zeroes `zero`
 __global__ __launch_bounds__(256) void bn_bwd_apply_fold_kernel(const float* __restrict__ padded,
                                                                 const float* __restrict__ z, int n, int D, int H, int W,
                                                                 int P, int C, const float* __restrict__ ss,
                                                                 const float* __restrict__ mi, int act, float slope,
                                                                 const float* __restrict__ coef, float* dz,
-                                                                __bf16* __restrict__ dz16) {
+                                                                __bf16* __restrict__ dz16, const double* __restrict__ acc,
+                                                                int reps, double nvox, const float* __restrict__ gamma,
+                                                                float* dgamma, float* dbeta, int accumulate,
+                                                                double* zero, int zero_n) {
+  __shared__ double sums[2 * 256];
+  __shared__ float co[3 * 256];
+  if (!coef) {
+    const int tid = threadIdx.x;
+    if (blockIdx.x == 0)
+      for (int j = tid; j < zero_n; j += blockDim.x) zero[j] = 0.0;
+    acc_sums(acc, reps, C, sums);
+    __syncthreads();
+    for (int c = tid; c < C; c += blockDim.x) {
+      co[c] = gamma[c] * mi[C + c];
+      co[C + c] = (float)(sums[c] / nvox);
+      co[2 * C + c] = (float)(sums[C + c] / nvox);
+      if (blockIdx.x == 0) {
+        if (dbeta) dbeta[c] = accumulate ? dbeta[c] + (float)sums[c] : (float)sums[c];
+        if (dgamma) dgamma[c] = accumulate ? dgamma[c] + (float)sums[C + c] : (float)sums[C + c];
+      }
+    }
+    __syncthreads();
+    coef = co;
+  }
   const int C4 = C >> 2;
   const int c = (threadIdx.x % C4) * 4;
   f32x4 sc, sf, mean, inv, k0, k1, k2;
@@ -559,6 +586,142 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_slab_kernel(const float* __r
   }
 }
 
+// ---- statistics from fp64 accumulators (cgan3d_bn_fuse acc_mode 3 / 4: the producing conv added its
+// per-block pairs into `reps` replicas acc[r][2][C]); finalize folded into the elementwise pass: every
+// block combines the replicas itself (16 KB at reps 16, C 64: all loads in flight), block 0 publishes
+// statistics / running buffers / parameter gradients and zeroes an accumulator the stream is done
+// with (the caller rotates them, so none needs a memset launch).
+__device__ __forceinline__ void acc_sums(const double* __restrict__ acc, int reps, int C, double* sums) {
+  // sums[q * C + c] = sum over replicas of acc[(r * 2 + q) * C + c]: the 256 threads split the pairs
+  // (j = q * C + c, 2C <= 128 of them) and the replicas (T = 256 / 2C threads per pair), eight loads
+  // in flight per thread — one round trip for reps <= 8T (the atomics left the values at the memory
+  // side: each round trip is long) — then the T partial sums of a pair are added through LDS
+  __shared__ double part[256];
+  const int tid = threadIdx.x, P = 2 * C, T = 256 / P, j = tid % P, h = tid / P;
+  double s = 0.0;
+  for (int r0 = h; r0 < reps; r0 += 8 * T) {
+    double v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int r = r0 + u * T;
+      v[u] = r < reps ? acc[(long long)r * P + j] : 0.0;
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) s += v[u];
+  }
+  part[tid] = s;
+  __syncthreads();
+  if (tid < P) {
+    double t = 0.0;
+    for (int k = 0; k < T; ++k) t += part[k * P + tid];
+    sums[tid] = t;
+  }
+}
+
+__global__ __launch_bounds__(256) void bn_apply_acc_kernel(const double* __restrict__ acc, int reps, int C, double nvox,
+                                                           const float* gamma, const float* beta, float* rmean,
+                                                           float* rvar, long long* nbt, float momentum, float eps,
+                                                           float* scale_shift, float* mean_invstd,
+                                                           const float* __restrict__ z, long long n4, int act,
+                                                           float slope, const float* __restrict__ res,
+                                                           float* __restrict__ y, __bf16* __restrict__ y16,
+                                                           double* zero, int zero_n) {
+  __shared__ double sums[2 * 256];
+  __shared__ float ssh[2 * 256];
+  const int tid = threadIdx.x;
+  if (blockIdx.x == 0)
+    for (int j = tid; j < zero_n; j += blockDim.x) zero[j] = 0.0;
+  acc_sums(acc, reps, C, sums);
+  __syncthreads();
+  for (int c = tid; c < C; c += blockDim.x) {
+    const double mean = sums[c] / nvox, var = fmax(sums[C + c] / nvox - mean * mean, 0.0);
+    const double invstd = 1.0 / sqrt(var + (double)eps);
+    const double sc = (double)gamma[c] * invstd;
+    ssh[c] = (float)sc;
+    ssh[C + c] = (float)((double)beta[c] - mean * sc);
+    if (blockIdx.x == 0) {
+      scale_shift[c] = ssh[c];
+      scale_shift[C + c] = ssh[C + c];
+      mean_invstd[c] = (float)mean;
+      mean_invstd[C + c] = (float)invstd;
+      if (rmean) rmean[c] = (float)((1.0 - momentum) * rmean[c] + momentum * mean);
+      if (rvar) rvar[c] = (float)((1.0 - momentum) * rvar[c] + momentum * var * nvox / (nvox > 1 ? nvox - 1 : 1));
+      if (nbt && c == 0) *nbt += 1;
+    }
+  }
+  __syncthreads();
+  const int C4 = C >> 2, cc = (tid % C4) * 4;
+  f32x4 sc4, sf4;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) { sc4[e] = ssh[cc + e]; sf4[e] = ssh[C + cc + e]; }
+  const f32x4* z4 = reinterpret_cast<const f32x4*>(z);
+  const f32x4* r4 = reinterpret_cast<const f32x4*>(res);
+  f32x4* y4 = reinterpret_cast<f32x4*>(y);
+  for (long long i = (long long)blockIdx.x * blockDim.x + tid; i < n4; i += (long long)gridDim.x * blockDim.x) {
+    f32x4 v = z4[i];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[e] = act_f(v[e] * sc4[e] + sf4[e], act, slope);
+    if (res) v += r4[i];
+    if (y) y4[i] = v;
+    if (y16) store16(y16, i, v);
+  }
+}
+
+__global__ __launch_bounds__(256) void bn_bwd_apply_acc_kernel(const double* __restrict__ acc, int reps, int C,
+                                                               double nvox, const float* __restrict__ gamma,
+                                                               const float* __restrict__ mi, float* dgamma,
+                                                               float* dbeta, int accumulate,
+                                                               const float* __restrict__ dy,
+                                                               const float* __restrict__ z, long long n4,
+                                                               const float* __restrict__ ss, int act, float slope,
+                                                               float* __restrict__ dz, __bf16* __restrict__ dz16,
+                                                               double* zero, int zero_n) {
+  __shared__ double sums[2 * 256];
+  __shared__ float co[3 * 256];
+  const int tid = threadIdx.x;
+  if (blockIdx.x == 0)
+    for (int j = tid; j < zero_n; j += blockDim.x) zero[j] = 0.0;
+  acc_sums(acc, reps, C, sums);
+  __syncthreads();
+  for (int c = tid; c < C; c += blockDim.x) {
+    co[c] = gamma[c] * mi[C + c];
+    co[C + c] = (float)(sums[c] / nvox);
+    co[2 * C + c] = (float)(sums[C + c] / nvox);
+    if (blockIdx.x == 0) {
+      if (dbeta) dbeta[c] = accumulate ? dbeta[c] + (float)sums[c] : (float)sums[c];
+      if (dgamma) dgamma[c] = accumulate ? dgamma[c] + (float)sums[C + c] : (float)sums[C + c];
+    }
+  }
+  __syncthreads();
+  const int C4 = C >> 2, cc = (tid % C4) * 4;
+  f32x4 sc, sf, mean, inv, k0, k1, k2;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    sc[e] = ss[cc + e]; sf[e] = ss[C + cc + e]; mean[e] = mi[cc + e]; inv[e] = mi[C + cc + e];
+    k0[e] = co[cc + e]; k1[e] = co[C + cc + e]; k2[e] = co[2 * C + cc + e];
+  }
+  const f32x4* z4 = reinterpret_cast<const f32x4*>(z);
+  const f32x4* d4 = reinterpret_cast<const f32x4*>(dy);
+  f32x4* o4 = reinterpret_cast<f32x4*>(dz);
+  for (long long i = (long long)blockIdx.x * blockDim.x + tid; i < n4; i += (long long)gridDim.x * blockDim.x) {
+    const f32x4 zz = z4[i], dd = d4[i];
+    f32x4 o;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float g = dd[e] * act_grad(zz[e] * sc[e] + sf[e], act, slope);
+      const float xh = (zz[e] - mean[e]) * inv[e];
+      o[e] = k0[e] * (g - k1[e] - xh * k2[e]);
+    }
+    if (dz) o4[i] = o;
+    if (dz16) store16(dz16, i, o);
+  }
+}
+
+// blocks of the accumulator passes: ~4 float4 per thread (each block reads the replicas once)
+static int acc_pass_blocks(long long n4) {
+  return (int)std::max(1LL, std::min((n4 + 1023) / 1024, 1024LL));
+}
+
 // blocks of the fused finalize + elementwise launch, or 0 when the slab is too large to be read by
 // every block (then: separate finalize launch)
 static int slab_fused_blocks(int nslots, int C, int rows, long long n4) {
@@ -745,7 +908,67 @@ extern "C" int cgan3d_bn_backward_slab_fold(const float* padded, const float* z,
   const long long n4 = nvox * c / 4;
   const int blocks = (int)std::min<long long>((n4 + 255) / 256, 4096);
   ::cg::launch(bn_bwd_apply_fold_kernel, dim3(blocks), dim3(256), 0, s, padded, z, n, d, h, w, pad, c, scale_shift,
-               mean_invstd, act, slope, ws, dz, reinterpret_cast<__bf16*>(dz_bf16));
+               mean_invstd, act, slope, (const float*)ws, dz, reinterpret_cast<__bf16*>(dz_bf16), (const double*)nullptr, 1,
+               0.0, (const float*)nullptr, (float*)nullptr, (float*)nullptr, 0, (double*)nullptr, 0);
+  CG_LAUNCH_CHECK("bn_bwd_apply_fold_kernel");
+  return CGAN3D_OK;
+}
+
+extern "C" int cgan3d_bn_apply_acc(const double* acc, int32_t reps, int32_t c, int64_t nvox, const float* gamma,
+                                   const float* beta, float* running_mean, float* running_var,
+                                   int64_t* num_batches_tracked, float momentum, float eps, float* scale_shift,
+                                   float* mean_invstd, const float* z, int32_t act, float slope, const float* residual,
+                                   float* y, void* y_bf16, double* zero, int32_t zero_n, void* stream) {
+  CG_CHECK_ARG(acc && gamma && beta && scale_shift && mean_invstd && z && (y || y_bf16),
+               "cgan3d_bn_apply_acc: null pointer");
+  CG_CHECK_ARG(reps > 0 && reps <= 64 && nvox > 0 && c >= 4 && c <= 128 && 256 % c == 0 && zero_n >= 0 &&
+                   (zero || !zero_n),
+               "cgan3d_bn_apply_acc: channels must divide 256 (4..128), reps 1..64");
+  const long long n4 = (long long)nvox * c / 4;
+  ::cg::launch(bn_apply_acc_kernel, dim3(acc_pass_blocks(n4)), dim3(256), 0, (hipStream_t)stream, acc, (int)reps, (int)c,
+               (double)nvox, gamma, beta, running_mean, running_var, (long long*)num_batches_tracked, momentum, eps,
+               scale_shift, mean_invstd, z, n4, act, slope, residual, y, reinterpret_cast<__bf16*>(y_bf16), zero,
+               (int)zero_n);
+  CG_LAUNCH_CHECK("bn_apply_acc_kernel");
+  return CGAN3D_OK;
+}
+
+extern "C" int cgan3d_bn_backward_acc(const float* dy, const float* z, int64_t nvox, int32_t c, const double* acc,
+                                      int32_t reps, const float* scale_shift, const float* mean_invstd,
+                                      const float* gamma, int32_t act, float slope, float* dgamma, float* dbeta,
+                                      float* dz, int32_t accumulate, void* dz_bf16, double* zero, int32_t zero_n,
+                                      void* stream) {
+  CG_CHECK_ARG(dy && z && acc && scale_shift && mean_invstd && gamma && (dz || dz_bf16),
+               "cgan3d_bn_backward_acc: null pointer");
+  CG_CHECK_ARG(reps > 0 && reps <= 64 && nvox > 1 && c >= 4 && c <= 128 && 256 % c == 0 && zero_n >= 0 &&
+                   (zero || !zero_n),
+               "cgan3d_bn_backward_acc: channels must divide 256 (4..128), reps 1..64");
+  const long long n4 = (long long)nvox * c / 4;
+  ::cg::launch(bn_bwd_apply_acc_kernel, dim3(acc_pass_blocks(n4)), dim3(256), 0, (hipStream_t)stream, acc, (int)reps,
+               (int)c, (double)nvox, gamma, mean_invstd, dgamma, dbeta, (int)accumulate, dy, z, n4, scale_shift, act,
+               slope, dz, reinterpret_cast<__bf16*>(dz_bf16), zero, (int)zero_n);
+  CG_LAUNCH_CHECK("bn_bwd_apply_acc_kernel");
+  return CGAN3D_OK;
+}
+
+extern "C" int cgan3d_bn_backward_acc_fold(const float* padded, const float* z, int32_t n, int32_t d, int32_t h,
+                                           int32_t w, int32_t c, int32_t pad, const double* acc, int32_t reps,
+                                           const float* scale_shift, const float* mean_invstd, const float* gamma,
+                                           int32_t act, float slope, float* dgamma, float* dbeta, float* dz,
+                                           int32_t accumulate, void* dz_bf16, double* zero, int32_t zero_n,
+                                           void* stream) {
+  CG_CHECK_ARG(padded && z && acc && scale_shift && mean_invstd && gamma && (dz || dz_bf16),
+               "cgan3d_bn_backward_acc_fold: null pointer");
+  CG_CHECK_ARG(n > 0 && reps > 0 && reps <= 64 && c >= 4 && c <= 128 && 256 % c == 0 && pad >= 0 && d > 2 * pad &&
+                   h > 2 * pad && w > 2 * pad && zero_n >= 0 && (zero || !zero_n),
+               "cgan3d_bn_backward_acc_fold: channels must divide 256 (4..128), dims must exceed 2*pad, reps 1..64");
+  const long long nvox = (long long)n * d * h * w;
+  CG_CHECK_ARG(nvox > 1, "cgan3d_bn_backward_acc_fold: need more than one voxel");
+  const long long n4 = nvox * c / 4;
+  ::cg::launch(bn_bwd_apply_fold_kernel, dim3(acc_pass_blocks(n4)), dim3(256), 0, (hipStream_t)stream, padded, z, n, d,
+               h, w, pad, c, scale_shift, mean_invstd, act, slope, (const float*)nullptr, dz,
+               reinterpret_cast<__bf16*>(dz_bf16), acc, (int)reps, (double)nvox, gamma, dgamma, dbeta, (int)accumulate,
+               zero, (int)zero_n);
   CG_LAUNCH_CHECK("bn_bwd_apply_fold_kernel");
   return CGAN3D_OK;
 }

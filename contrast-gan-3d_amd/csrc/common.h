@@ -109,29 +109,10 @@ inline int geom_kd(const cgan3d_conv_geom* g) { return g->planar ? 1 : g->k; }
 inline int geom_sd(const cgan3d_conv_geom* g) { return g->planar ? 1 : g->stride; }
 inline int geom_pd(const cgan3d_conv_geom* g) { return g->planar ? 0 : g->pad; }
 
-// device-side view of cgan3d_bn_fuse (BatchNorm fused across a conv boundary, include/cgan3d.h)
+// device-side view of cgan3d_bn_fuse (BatchNorm statistics into fp64 accumulators, include/cgan3d.h)
 struct BnFuse {
   double* acc_out;
-  int acc_mode, reps, pre_mode, pre_act;
-  float pre_slope, eps, momentum;
-  int zero_n;
-  double nvox;
-  const double* acc_in;
-  const float* z;
-  const float* res;
-  const float* dy;
-  const float* gamma;
-  const float* beta;
-  float* rmean;
-  float* rvar;
-  long long* nbt;
-  float* ss;
-  float* mi;
-  float* dgamma;
-  float* dbeta;
-  float* y;
-  __bf16* y16;
-  double* zero;
+  int acc_mode, reps;
 };
 
 // device-side view of cgan3d_epilogue
@@ -184,6 +165,7 @@ int k7_wgrad_handles(const cgan3d_conv_geom* g);
 int k7m_wgrad_taken(const cgan3d_conv_geom* g);
 int k7m_w2n_taken(const cgan3d_conv_geom* g);
 int k7m_fold_ok(const cgan3d_conv_geom* g);
+int k7m_n2w_ok(const cgan3d_conv_geom* g);
 int k7_try_wgrad(const cgan3d_conv_geom* g, const float* x, const float* go, float* dw, float* ws, hipStream_t s,
                  const __bf16* wide16 = nullptr);
 long long k7_wgrad_ws_floats(const cgan3d_conv_geom* g);
@@ -193,7 +175,8 @@ void k7m_wgrad_launch(const cgan3d_conv_geom* g, bool wide_in, long long wc, con
 long long k7_n2w_blocks(const cgan3d_conv_geom* g);
 long long k7m_n2w_blocks(const cgan3d_conv_geom* g);
 void k7m_n2w_launch(const cgan3d_conv_geom* g, int P, int reflect, int flip, long long wc, const float* x,
-                    const float* w, float* y, float* stats, float* bn_part, hipStream_t s, const Epi* fold = nullptr);
+                    const float* w, float* y, float* stats, float* bn_part, hipStream_t s, const Epi* fold = nullptr,
+                    const BnFuse* fz = nullptr);
 void k7m_w2n_launch(const cgan3d_conv_geom* g, int P, int reflect, long long wc, const float* x, const float* w,
                     float* y, const Epi& e, hipStream_t s);
 // implicit-GEMM forward / input-grad (conv_gemm.hip)
@@ -235,7 +218,6 @@ void halo_set_dbg(int v);
 int wgrad_bf16_launch(const cgan3d_conv_geom* g, const float* gathered, const float* aligned, float* dwp,
                       hipStream_t st);
 bool halo_ok(const cgan3d_conv_geom* g);         // w_packed == 2 and eligible
-bool k3_fuse_ok(const cgan3d_conv_geom* g);      // the ResNet-block kernel: consumer half of cgan3d_bn_fuse
 bool halo_format_ok(const cgan3d_conv_geom* g);  // eligible ignoring w_packed
 long long halo_mblocks(const cgan3d_conv_geom* g);
 int halo_launch(const cgan3d_conv_geom* g, const float* x, const float* w, float* y, const Epi& e, hipStream_t st);

@@ -523,40 +523,29 @@ static Epi to_epi(const cgan3d_epilogue* ep) {
     e.x16 = reinterpret_cast<const __bf16*>(ep->x_bf16);
     e.bn_fold = ep->bn_fold;
     if (const cgan3d_bn_fuse* f = ep->fuse) {
-      BnFuse& z = e.fz;
-      z.acc_out = f->acc_out; z.acc_mode = f->acc_mode; z.reps = f->reps; z.pre_mode = f->pre_mode;
-      z.pre_act = f->pre_act; z.pre_slope = f->pre_slope; z.eps = f->eps; z.momentum = f->momentum;
-      z.zero_n = f->zero ? f->zero_n : 0; z.nvox = f->nvox; z.acc_in = f->acc_in; z.z = f->z; z.res = f->res;
-      z.dy = f->dy; z.gamma = f->gamma; z.beta = f->beta; z.rmean = f->rmean; z.rvar = f->rvar;
-      z.nbt = reinterpret_cast<long long*>(f->nbt); z.ss = f->ss; z.mi = f->mi; z.dgamma = f->dgamma;
-      z.dbeta = f->dbeta; z.y = f->y; z.y16 = static_cast<__bf16*>(f->y16); z.zero = f->zero;
+      e.fz.acc_out = f->acc_out; e.fz.acc_mode = f->acc_mode; e.fz.reps = f->reps;
     }
   }
   return e;
 }
 
-extern "C" int32_t cgan3d_bn_fuse_ok(const cgan3d_conv_geom* g, int32_t consumer) {
-  if (!g || g->w_packed != 2 || !halo_ok(g) || s2_kind(g)) return 0;  // halo_epilogue kernels only
-  return consumer ? (k3_fuse_ok(g) ? 1 : 0) : 1;
+extern "C" int32_t cgan3d_bn_fuse_ok(const cgan3d_conv_geom* g) {
+  if (!g || validate(g, "cgan3d_bn_fuse_ok")) return 0;
+  // the halo-tiled family (halo_epilogue, the stride-2 16 <-> 32 kernels) and the generator's
+  // 1 -> 16 k7 MFMA kernel (first conv forward, last conv input-grad with bn_fold)
+  if (g->w_packed == 2 && halo_ok(g)) return 1;
+  return g->w_packed == 0 && k7m_n2w_ok(g) ? 1 : 0;
 }
 
 // host checks of a cgan3d_bn_fuse against the launch it rides on
 static int check_fuse(const cgan3d_conv_geom* g, const Epi& e) {
   const BnFuse& f = e.fz;
-  if (!f.acc_mode && !f.pre_mode) return CGAN3D_OK;
-  CG_CHECK_ARG(cgan3d_bn_fuse_ok(g, f.pre_mode != 0), "bn_fuse: geometry does not take the fused BatchNorm");
-  CG_CHECK_ARG(f.acc_mode == 0 || f.acc_mode == 3 || f.acc_mode == 4, "bn_fuse: acc_mode must be 0, 3 or 4");
-  CG_CHECK_ARG(f.pre_mode >= 0 && f.pre_mode <= 2, "bn_fuse: pre_mode must be 0, 1 or 2");
+  if (!f.acc_mode) return CGAN3D_OK;
+  CG_CHECK_ARG(cgan3d_bn_fuse_ok(g), "bn_fuse: geometry does not produce accumulators");
+  CG_CHECK_ARG(f.acc_mode == 3 || f.acc_mode == 4, "bn_fuse: acc_mode must be 3 or 4");
   CG_CHECK_ARG(f.reps >= 1 && f.reps <= 64, "bn_fuse: reps must be 1..64");
-  CG_CHECK_ARG(!f.acc_mode || (f.acc_out && !e.bn_mode && !e.stats), "bn_fuse: acc_mode needs acc_out and no slab");
+  CG_CHECK_ARG(f.acc_out && !e.bn_mode && !e.stats, "bn_fuse: needs acc_out and no slab");
   CG_CHECK_ARG(f.acc_mode != 4 || (e.bn_z && e.bn_ss && e.bn_mi), "bn_fuse: acc_mode 4 needs bn_z, bn_ss, bn_mi");
-  if (f.pre_mode) {
-    CG_CHECK_ARG(f.acc_in && f.z && f.gamma && f.ss && f.mi && f.nvox > 0, "bn_fuse: pre_mode operands missing");
-    CG_CHECK_ARG(f.pre_mode != 1 || f.beta, "bn_fuse: pre_mode 1 needs beta");
-    CG_CHECK_ARG(f.pre_mode != 2 || (f.dy && f.dgamma && f.dbeta && !f.res), "bn_fuse: pre_mode 2 needs dy, dgamma, dbeta");
-    CG_CHECK_ARG(!e.x16, "bn_fuse: pre_mode computes the input (no x_bf16)");
-    CG_CHECK_ARG(f.zero_n >= 0 && (f.zero_n == 0 || f.zero), "bn_fuse: zero_n without zero");
-  }
   return CGAN3D_OK;
 }
 
@@ -595,10 +584,13 @@ extern "C" int cgan3d_conv3d_fwd(const cgan3d_conv_geom* g, const float* x, cons
     const long long slots = cgan3d_conv3d_bn_slots(g);
     CG_CHECK_ARG(slots > 0 && slots == e.bn_slots, "cgan3d_conv3d_fwd: bn_slots %d, the launch has %lld", e.bn_slots,
                  slots);
-    CG_CHECK_ARG(!(e.bn_mode == 2 && g->k == 7 && g->cin == 1) || (e.bn_fold > 0 && k7m_fold_ok(g)),
+  }
+  {  // mode-2 statistics (slab or accumulators) on the k7 path: only folded, on the bf16 input-grad kernel
+    const bool m2 = e.bn_mode == 2 || e.fz.acc_mode == 4;
+    CG_CHECK_ARG(!(m2 && g->k == 7 && g->cin == 1) || (e.bn_fold > 0 && k7m_fold_ok(g)),
                  "cgan3d_conv3d_fwd: bn_mode 2 on the k7 path only folded (bn_fold) on the bf16 input-grad kernel");
-    CG_CHECK_ARG(e.bn_fold == 0 || (e.bn_mode == 2 && k7m_fold_ok(g) && g->do_ > 4 * e.bn_fold &&
-                                    g->ho > 4 * e.bn_fold && g->wo > 4 * e.bn_fold),
+    CG_CHECK_ARG(e.bn_fold == 0 || (m2 && k7m_fold_ok(g) && g->do_ > 4 * e.bn_fold && g->ho > 4 * e.bn_fold &&
+                                    g->wo > 4 * e.bn_fold),
                  "cgan3d_conv3d_fwd: bn_fold needs bn_mode 2 on a k7 bf16 input-grad geometry");
   }
   hipStream_t s = (hipStream_t)stream;

@@ -382,141 +382,7 @@ __global__ __launch_bounds__(256) void conv_halo_kernel(HaloArgs a, const float*
 //    shared halo epilogue writes the tile.
 constexpr int K3_HX = 8, K3_HY = 6, K3_HZ = 6, K3_VROW = 96;  // halo dims (x padded), elements per voxel row
 
-// Consumer half of cgan3d_bn_fuse (include/cgan3d.h): the ResNet-block conv stages the previous
-// BatchNorm layer's output (pre_mode 1) or its input-grad (pre_mode 2) itself, so that layer needs
-// no finalize and no elementwise launch:
-//  * the raw operands of the 6^3 halo (z, and the skip input / dL/dy) are loaded first, all in flight;
-//  * meanwhile every block combines the producer's fp64 accumulator replicas into the layer's
-//    per-channel coefficients (fp64), block (0, 0) publishing them and the running buffers / the
-//    gamma-beta gradients exactly once;
-//  * each element is transformed in fp32 (the arithmetic of bn_apply / bn_bwd_apply), rounded to
-//    bf16 into the halo, and the channel-block-0 blocks write their tile's interior (y / y16) — every
-//    voxel of the layer exactly once — for the weight gradients and the skip path.
-__device__ __forceinline__ float k3_act(float v, int act, float slope) {
-  if (act == CGAN3D_ACT_RELU) return fmaxf(v, 0.f);
-  if (act == CGAN3D_ACT_LRELU) return v > 0.f ? v : v * slope;
-  return v;
-}
-
-__device__ __forceinline__ void k3_pre_stage(const HaloArgs& a, const Epi& ep, int nb, int oz, int oy, int ox,
-                                             __bf16* halo) {
-  constexpr int CIN = 64;
-  constexpr int ST = K3_HZ * K3_HY * 6 * 16, ST_PER = (ST + 255) / 256;  // (voxel, 4 channels) elements
-  __shared__ double pacc[2][2][CIN];
-  __shared__ float pc[7][CIN];
-  const BnFuse& f = ep.fz;
-  const int tid = threadIdx.x;
-  const bool fwd = f.pre_mode == 1;
-  const float* second = fwd ? f.res : f.dy;  // skip input (forward) / dL/dy (input-grad)
-  // raw operands in batches of B elements per thread (the first batch in flight during the
-  // statistics): all 14 at once spill at 2 waves per SIMD; two batches of 7: 161 VGPRs
-  constexpr int B = 7, NB = (ST_PER + B - 1) / B;
-  f32x4 zr[B], sr[B];
-  auto load = [&](int b) {
-#pragma unroll
-    for (int u = 0; u < B; ++u) {
-      const int k = b * B + u;
-      const int i = tid + 256 * k;
-      const int c4 = i & 15, v = i >> 4;
-      const int hx = v % 6, hy = (v / 6) % 6, hz = v / 36;
-      const int iz = oz + hz, iy = oy + hy, ix = ox + hx;
-      const bool ok = k < ST_PER && i < ST && (unsigned)iz < (unsigned)a.di && (unsigned)iy < (unsigned)a.hi &&
-                      (unsigned)ix < (unsigned)a.wi;
-      const long long off = ok ? (((long long)(nb * a.di + iz) * a.hi + iy) * a.wi + ix) * CIN + 4 * c4 : 0;
-      zr[u] = *reinterpret_cast<const f32x4*>(f.z + off);
-      sr[u] = second ? *reinterpret_cast<const f32x4*>(second + off) : f32x4{0.f, 0.f, 0.f, 0.f};
-    }
-  };
-  load(0);
-  const bool lead = blockIdx.x == 0 && blockIdx.y == 0;
-  if (lead)
-    for (int j = tid; j < f.zero_n; j += 256) f.zero[j] = 0.0;  // an accumulator the stream is done with
-  {  // the producer's replicas, fp64: thread (half h, pair member q, channel c)
-    const int c = tid & 63, q = (tid >> 6) & 1, h = tid >> 7;
-    double s = 0.0;
-    for (int r = h; r < f.reps; r += 2) s += f.acc_in[(long long)(r * 2 + q) * CIN + c];
-    pacc[h][q][c] = s;
-  }
-  __syncthreads();
-  if (tid < CIN) {
-    const int c = tid;
-    const double S = pacc[0][0][c] + pacc[1][0][c], Q = pacc[0][1][c] + pacc[1][1][c];
-    if (fwd) {  // cgan3d_bn_finalize_slab's outputs, from (sum, sum of squares)
-      const double mean = S / f.nvox, var = fmax(Q / f.nvox - mean * mean, 0.0);
-      const double invstd = 1.0 / sqrt(var + (double)f.eps);
-      const double sc = (double)f.gamma[c] * invstd;
-      const float scf = (float)sc, shf = (float)((double)f.beta[c] - mean * sc);
-      pc[0][c] = scf;
-      pc[1][c] = shf;
-      if (lead) {
-        f.ss[c] = scf;
-        f.ss[CIN + c] = shf;
-        f.mi[c] = (float)mean;
-        f.mi[CIN + c] = (float)invstd;
-        const double m = f.momentum, n = f.nvox;
-        if (f.rmean) f.rmean[c] = (float)((1.0 - m) * f.rmean[c] + m * mean);
-        if (f.rvar) f.rvar[c] = (float)((1.0 - m) * f.rvar[c] + m * var * n / (n > 1 ? n - 1 : 1));
-        if (f.nbt && c == 0) *f.nbt += 1;
-      }
-    } else {  // cgan3d_bn_backward_finalize_slab's coefficients
-      pc[0][c] = f.ss[c];
-      pc[1][c] = f.ss[CIN + c];
-      pc[2][c] = f.mi[c];
-      pc[3][c] = f.mi[CIN + c];
-      pc[4][c] = f.gamma[c] * f.mi[CIN + c];
-      pc[5][c] = (float)(S / f.nvox);
-      pc[6][c] = (float)(Q / f.nvox);
-      if (lead) {
-        f.dbeta[c] += (float)S;
-        f.dgamma[c] += (float)Q;
-      }
-    }
-  }
-  __syncthreads();
-  const bool interior = blockIdx.y == 0;
-#pragma unroll
-  for (int b = 0; b < NB; ++b) {
-    if (b > 0) load(b);
-#pragma unroll
-    for (int u = 0; u < B; ++u) {
-      const int k = b * B + u;
-      const int i = tid + 256 * k;
-      if (k >= ST_PER || i >= ST) break;
-      const int c4 = i & 15, v = i >> 4;
-      const int hx = v % 6, hy = (v / 6) % 6, hz = v / 36;
-      const int iz = oz + hz, iy = oy + hy, ix = ox + hx;
-      const bool ok = (unsigned)iz < (unsigned)a.di && (unsigned)iy < (unsigned)a.hi && (unsigned)ix < (unsigned)a.wi;
-      f32x4 o = f32x4{0.f, 0.f, 0.f, 0.f};  // zero padding of the conv input
-      if (ok) {
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const int c = 4 * c4 + e;
-          const float zz = zr[u][e];
-          if (fwd) {
-            o[e] = k3_act(zz * pc[0][c] + pc[1][c], f.pre_act, f.pre_slope) + sr[u][e];
-          } else {
-            const float gg = sr[u][e] * act_grad(zz * pc[0][c] + pc[1][c], f.pre_act, f.pre_slope);
-            const float xh = (zz - pc[2][c]) * pc[3][c];
-            o[e] = pc[4][c] * (gg - pc[5][c] - xh * pc[6][c]);
-          }
-        }
-      }
-      bf16x4_h uu;
-      uu[0] = (__bf16)o[0]; uu[1] = (__bf16)o[1]; uu[2] = (__bf16)o[2]; uu[3] = (__bf16)o[3];
-      const int row = hz * K3_HY + hy, vv = row * K3_HX + hx;
-      const int pg = (c4 >> 1) ^ ((row * 2) & 7);
-      *reinterpret_cast<bf16x4_h*>(halo + vv * K3_VROW + pg * 8 + 4 * (c4 & 1)) = uu;
-      if (interior && ok && (unsigned)(hz - 1) < 4u && (unsigned)(hy - 1) < 4u && (unsigned)(hx - 1) < 4u) {
-        const long long off = (((long long)(nb * a.di + iz) * a.hi + iy) * a.wi + ix) * CIN + 4 * c4;
-        if (f.y) *reinterpret_cast<f32x4*>(f.y + off) = o;
-        if (f.y16) *reinterpret_cast<bf16x4_h*>(f.y16 + off) = uu;
-      }
-    }
-  }
-}
-
-template <bool TR, int NT, bool PRE>  // NT: 16-channel output tiles per block (blockIdx.y picks the channel
-                                      // block); PRE: the cgan3d_bn_fuse consumer variant (k3_pre_stage)
+template <bool TR, int NT>  // NT: 16-channel output tiles per block (blockIdx.y picks the channel block)
 __global__ __launch_bounds__(256, 2) void conv_k3_kernel(HaloArgs a, const float* __restrict__ x,
                                                          const __bf16* __restrict__ wpk, float* y, Epi ep) {
   constexpr int CIN = 64, COUT = 64, KS = 2;
@@ -558,9 +424,7 @@ __global__ __launch_bounds__(256, 2) void conv_k3_kernel(HaloArgs a, const float
   // ---- halo: fp32 NDHWC -> bf16 LDS, voxel (hz, hy, hx) row (hz*6 + hy)*8 + hx, granule swizzle;
   // every load of the thread issued before the first conversion
   constexpr int ST = K3_HZ * K3_HY * 6 * 16, ST_PER = (ST + 255) / 256;
-  if (PRE) {  // the previous BatchNorm layer applied while staging (cgan3d_bn_fuse)
-    k3_pre_stage(a, ep, nb, oz, oy, ox, halo);
-  } else if (ep.x16 && !(a.dbg & 1)) {  // bf16 shadow of the input: 16-byte granules copied as they are
+  if (ep.x16 && !(a.dbg & 1)) {  // bf16 shadow of the input: 16-byte granules copied as they are
     constexpr int SB = K3_HZ * K3_HY * 6 * 8, SB_PER = (SB + 255) / 256;
     bf16x8_h sb[SB_PER];
 #pragma unroll
@@ -737,8 +601,6 @@ static bool k3_tile_ok(const cgan3d_conv_geom* g) {
   return g_k3_tile && g->cin == 64 && g->cout == 64 && g->k == 3 && g->stride == 1 && g->pad == 1 && !g->reflect;
 }
 
-bool k3_fuse_ok(const cgan3d_conv_geom* g) { return g->w_packed == 2 && g->prec == CGAN3D_PREC_BF16 && k3_tile_ok(g); }
-
 bool halo_format_ok(const cgan3d_conv_geom* g) {
   HaloArgs a;
   return s2_kind(g) || halo_setup(g, &a);
@@ -766,14 +628,12 @@ int halo_launch(const cgan3d_conv_geom* g, const float* x, const float* w, float
     const int split = g_k3_split ? g_k3_split : (tiles < g_halo_min_blocks ? 2 : 1);
     const dim3 grid1((unsigned)tiles, split);
     const __bf16* wp = reinterpret_cast<const __bf16*>(w);
-#define CG_K3P(N, P) (g->transposed ? ::cg::launch((conv_k3_kernel<true, N, P>), grid1, dim3(256), 0, st, a, x, wp, y, e) \
-                                    : ::cg::launch((conv_k3_kernel<false, N, P>), grid1, dim3(256), 0, st, a, x, wp, y, e))
-#define CG_K3(N) (e.fz.pre_mode ? CG_K3P(N, true) : CG_K3P(N, false))
+#define CG_K3(N) (g->transposed ? ::cg::launch((conv_k3_kernel<true, N>), grid1, dim3(256), 0, st, a, x, wp, y, e) \
+                                : ::cg::launch((conv_k3_kernel<false, N>), grid1, dim3(256), 0, st, a, x, wp, y, e))
     if (split == 4) CG_K3(1);
     else if (split == 2) CG_K3(2);
     else CG_K3(4);
 #undef CG_K3
-#undef CG_K3P
     return CGAN3D_OK;
   }
   dim3 grid((unsigned)(a.nclass * a.n * a.td * a.th * a.tw), g->cout / a.bn);

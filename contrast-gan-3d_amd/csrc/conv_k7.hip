@@ -344,12 +344,14 @@ long long k7_n2w_blocks(const cgan3d_conv_geom* g) {
 int k7_try_fwd(const cgan3d_conv_geom* g, const float* x, const float* w, float* y, const Epi& e,
                hipStream_t s) {
   if (g->k != 7 || g->stride != 1) return 0;
-  const bool fold = e.bn_mode == 2 && e.bn_fold > 0;  // folded mode-2 statistics (k7m input-grad only)
+  // statistics mode: slab (bn_mode) or fp64 accumulators (cgan3d_bn_fuse acc_mode 3 / 4)
+  const int smode = e.fz.acc_mode == 3 ? 1 : e.fz.acc_mode == 4 ? 2 : e.bn_mode;
+  const bool fold = smode == 2 && e.bn_fold > 0;  // folded mode-2 statistics (k7m input-grad only)
   if (g->cin == 1 && k7_wide_ok(g->cout) && !e.bias && !e.residual && !e.mask_src && !e.out2 &&
-      (e.bn_mode != 2 || (fold && g->transposed && k7m_ok(g, g->cout))) && e.act == CGAN3D_ACT_NONE) {
+      (smode != 2 || (fold && g->transposed && k7m_ok(g, g->cout))) && e.act == CGAN3D_ACT_NONE) {
     if (k7m_ok(g, g->cout)) {
       float* bp = e.bn_mode == 1 ? e.bn_part : nullptr;
-      if (!g->transposed) k7m_n2w_launch(g, g->pad, g->reflect, 0, g->w_sb, x, w, y, e.stats, bp, s);
+      if (!g->transposed) k7m_n2w_launch(g, g->pad, g->reflect, 0, g->w_sb, x, w, y, e.stats, bp, s, nullptr, &e.fz);
       else k7m_n2w_launch(g, g->k - 1 - g->pad, 0, 1, g->w_sb, x, w, y, e.stats, bp, s, fold ? &e : nullptr);
       return 1;
     }
@@ -387,6 +389,11 @@ int k7m_w2n_taken(const cgan3d_conv_geom* g) {
 }
 
 // 1 if the geometry's forward takes the k7m n2w kernel as an input-grad (folded mode-2 statistics)
+// the 1 -> 16 MFMA kernel (k7m_n2w_kernel) takes this forward / input-grad launch
+int k7m_n2w_ok(const cgan3d_conv_geom* g) {
+  return g->k == 7 && g->stride == 1 && g->cin == 1 && k7_wide_ok(g->cout) && k7m_ok(g, g->cout);
+}
+
 int k7m_fold_ok(const cgan3d_conv_geom* g) {
   return g->k == 7 && g->stride == 1 && g->transposed && g->cin == 1 && k7m_ok(g, g->cout);
 }

@@ -64,6 +64,8 @@ struct K7Fold {
   const float* ss;  // [scale | shift]
   const float* mi;  // [mean | invstd]
   float* part;      // mode-2 slab, slot = block
+  double* acc;      // or fp64 accumulators (cgan3d_bn_fuse acc_mode 4): replica block % reps
+  int reps;
   int act;
   float slope;
   int P, zd, zh, zw;
@@ -72,7 +74,7 @@ struct K7Fold {
 __global__ __launch_bounds__(256, 2) void k7m_n2w_kernel(K7Args a, const float* __restrict__ x,
                                                          const float* __restrict__ w, float* __restrict__ y,
                                                          float* stats, float* bn_part, int tiles_per_block, int ntiles,
-                                                         K7Fold fb) {
+                                                         K7Fold fb, double* acc1, int reps1) {
   constexpr int C = 16;
   __shared__ __attribute__((aligned(16))) __bf16 us[N_ROWS * N_TW * 8];  // [row][ow][8 taps]
   __shared__ __attribute__((aligned(16))) __bf16 xs[N_ROWS * N_HWP];     // [row][24]
@@ -223,7 +225,7 @@ __global__ __launch_bounds__(256, 2) void k7m_n2w_kernel(K7Args a, const float* 
           }
         }
     }
-    if (stats || bn_part) {  // tile (sum, M2 about the tile mean), merged into the block's running statistics
+    if (stats || bn_part || acc1) {  // tile (sum, M2 about the tile mean), merged into the block's running statistics
       const int vd = min(N_TD, a.do_ - d0), vh = min(N_TH, a.ho - h0), vw = min(N_TW, a.wo - w0);
       const float tn = (float)(vd * vh * vw);
       s1 += __shfl_xor(s1, 16, 64);
@@ -263,6 +265,12 @@ __global__ __launch_bounds__(256, 2) void k7m_n2w_kernel(K7Args a, const float* 
     stats[sb + C + tid] = run_m2;
     if (tid == 0) stats[sb + 2 * C] = run_n;
   }
+  if (acc1 && tid < C && run_n > 0.f) {  // or (sum, sum of squares) into fp64 accumulators (cgan3d_bn_fuse)
+    double* r = acc1 + (long long)(blockIdx.x % reps1) * 2 * C;
+    const double S = (double)run_mean * run_n;
+    unsafeAtomicAdd(r + tid, S);
+    unsafeAtomicAdd(r + C + tid, (double)run_m2 + S * (double)run_mean);
+  }
   if (bn_part && tid < C) {  // the same partials into slot blockIdx.x of the channel-major slab
     bn_part[(long long)tid * gridDim.x + blockIdx.x] = run_mean * run_n;
     bn_part[(long long)(C + tid) * gridDim.x + blockIdx.x] = run_m2;
@@ -276,12 +284,20 @@ __global__ __launch_bounds__(256, 2) void k7m_n2w_kernel(K7Args a, const float* 
     __syncthreads();
     if (g == 0) red[wave][r16] = fp1;
     __syncthreads();
-    if (tid < C) fb.part[(long long)tid * gridDim.x + blockIdx.x] = red[0][tid] + red[1][tid] + red[2][tid] + red[3][tid];
+    double* fr = fb.acc ? fb.acc + (long long)(blockIdx.x % fb.reps) * 2 * C : nullptr;
+    if (tid < C) {
+      const float q = red[0][tid] + red[1][tid] + red[2][tid] + red[3][tid];
+      if (fr) unsafeAtomicAdd(fr + tid, (double)q);
+      else fb.part[(long long)tid * gridDim.x + blockIdx.x] = q;
+    }
     __syncthreads();
     if (g == 0) red[wave][r16] = fp2;
     __syncthreads();
-    if (tid < C)
-      fb.part[(long long)(C + tid) * gridDim.x + blockIdx.x] = red[0][tid] + red[1][tid] + red[2][tid] + red[3][tid];
+    if (tid < C) {
+      const float q = red[0][tid] + red[1][tid] + red[2][tid] + red[3][tid];
+      if (fr) unsafeAtomicAdd(fr + C + tid, (double)q);
+      else fb.part[(long long)(C + tid) * gridDim.x + blockIdx.x] = q;
+    }
   }
 }
 
@@ -865,17 +881,24 @@ long long k7m_n2w_blocks(const cgan3d_conv_geom* g) {
 }
 
 void k7m_n2w_launch(const cgan3d_conv_geom* g, int P, int reflect, int flip, long long wc, const float* x,
-                    const float* w, float* y, float* stats, float* bn_part, hipStream_t s, const Epi* fold) {
+                    const float* w, float* y, float* stats, float* bn_part, hipStream_t s, const Epi* fold,
+                    const BnFuse* fz) {
   const K7Args a = k7m_args(g, P, reflect, flip, wc, N_TD, N_TH, N_TW);
   int grid, per, nt;
   k7m_n2w_split(a, &grid, &per, &nt);
   K7Fold fb{};
+  double* acc1 = nullptr;
+  int reps1 = 1;
   if (fold) {
     const int f = fold->bn_fold;
-    fb = K7Fold{fold->bn_z, fold->bn_ss, fold->bn_mi, fold->bn_part, fold->bn_act, fold->bn_slope, f,
-                g->do_ - 2 * f, g->ho - 2 * f, g->wo - 2 * f};
+    const bool acc = fold->fz.acc_mode == 4;
+    fb = K7Fold{fold->bn_z, fold->bn_ss, fold->bn_mi, acc ? nullptr : fold->bn_part, acc ? fold->fz.acc_out : nullptr,
+                acc ? fold->fz.reps : 1, fold->bn_act, fold->bn_slope, f, g->do_ - 2 * f, g->ho - 2 * f, g->wo - 2 * f};
+  } else if (fz && fz->acc_mode == 3) {
+    acc1 = fz->acc_out;
+    reps1 = fz->reps;
   }
-  ::cg::launch(k7m_n2w_kernel, dim3(grid), dim3(256), 0, s, a, x, w, y, stats, bn_part, per, nt, fb);
+  ::cg::launch(k7m_n2w_kernel, dim3(grid), dim3(256), 0, s, a, x, w, y, stats, bn_part, per, nt, fb, acc1, reps1);
 }
 
 static int g_k7s = 0;  // cgan3d_set_tuning key 13: output planes per streamed-w2n block (0 auto, -1 off)

@@ -65,11 +65,19 @@ __device__ __forceinline__ float s2_act(float v, const Epi& ep) {
 
 // Block statistics of the fused BatchNorm slab (include/cgan3d.h): mode 1 (sum, M2 about the block
 // mean, count), mode 2 (sum g, sum g*xhat).  vals / zv: [U][NT][4] per lane, ok: [U][4] row validity.
+// fused-statistics mode of an epilogue: 1 / 2 (slab or, cgan3d_bn_fuse acc_mode 3 / 4, fp64 accumulators)
+__device__ __forceinline__ int s2_stat_mode(const Epi& ep) {
+  return ep.fz.acc_mode == 3 ? 1 : ep.fz.acc_mode == 4 ? 2 : ep.bn_mode;
+}
+
 template <int U, int NT>
 __device__ __forceinline__ void s2_bn_slab(const Epi& ep, int C, const float (&vals)[U][NT][4], const float (&zv)[U][NT][4],
                                            const bool (&ok)[U][4], int cnt, float* red) {
   const int tid = threadIdx.x, r16 = tid & 15;
-  if (ep.bn_mode == 1) {
+  const int mode = s2_stat_mode(ep);
+  // this block's replica of the accumulators (cgan3d_bn_fuse), or null: the slab
+  double* const acc = ep.fz.acc_mode ? ep.fz.acc_out + (long long)(blockIdx.x % ep.fz.reps) * 2 * C : nullptr;
+  if (mode == 1) {
     float s[NT];
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt) {
@@ -97,12 +105,19 @@ __device__ __forceinline__ void s2_bn_slab(const Epi& ep, int C, const float (&v
     if (tid < 16) {
 #pragma unroll
       for (int nt = 0; nt < NT; ++nt) {
-        *bn_slot(ep, 0, C, nt * 16 + r16, blockIdx.x) = s[nt];
-        *bn_slot(ep, 1, C, nt * 16 + r16, blockIdx.x) = q[nt];
+        if (acc) {  // (sum, sum of squares = M2 + S * mean)
+          if (cnt) {
+            unsafeAtomicAdd(acc + nt * 16 + r16, (double)s[nt]);
+            unsafeAtomicAdd(acc + C + nt * 16 + r16, (double)q[nt] + (double)s[nt] * (double)s[nt] / cnt);
+          }
+        } else {
+          *bn_slot(ep, 0, C, nt * 16 + r16, blockIdx.x) = s[nt];
+          *bn_slot(ep, 1, C, nt * 16 + r16, blockIdx.x) = q[nt];
+        }
       }
-      if (tid == 0) *bn_slot(ep, 2, C, 0, blockIdx.x) = (float)cnt;
+      if (tid == 0 && !acc) *bn_slot(ep, 2, C, 0, blockIdx.x) = (float)cnt;
     }
-  } else if (ep.bn_mode == 2) {
+  } else if (mode == 2) {
     float p1[NT], p2[NT];
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt) {
@@ -120,8 +135,13 @@ __device__ __forceinline__ void s2_bn_slab(const Epi& ep, int C, const float (&v
     if (tid < 16) {
 #pragma unroll
       for (int nt = 0; nt < NT; ++nt) {
-        *bn_slot(ep, 0, C, nt * 16 + r16, blockIdx.x) = p1[nt];
-        *bn_slot(ep, 1, C, nt * 16 + r16, blockIdx.x) = p2[nt];
+        if (acc) {
+          unsafeAtomicAdd(acc + nt * 16 + r16, (double)p1[nt]);
+          unsafeAtomicAdd(acc + C + nt * 16 + r16, (double)p2[nt]);
+        } else {
+          *bn_slot(ep, 0, C, nt * 16 + r16, blockIdx.x) = p1[nt];
+          *bn_slot(ep, 1, C, nt * 16 + r16, blockIdx.x) = p2[nt];
+        }
       }
     }
   }
@@ -258,7 +278,7 @@ __global__ __launch_bounds__(256) void conv_s2f_kernel(S2Args a, const float* __
 #pragma unroll
       for (int nt = 0; nt < 2; ++nt) {
         const int c = nt * 16 + r16;
-        zv[zz][nt][j] = ep.bn_mode == 2 ? ep.bn_z[o * CO + c] : 0.f;
+        zv[zz][nt][j] = s2_stat_mode(ep) == 2 ? ep.bn_z[o * CO + c] : 0.f;
         float v = acc[zz][nt][j] + (ep.bias ? ep.bias[c] : 0.f);
         v = s2_act(v, ep);
         if (ok[zz][j] && (!(a.dbg & 4) || v == 1.2345f)) y[o * CO + c] = v;
@@ -266,7 +286,7 @@ __global__ __launch_bounds__(256) void conv_s2f_kernel(S2Args a, const float* __
       }
     }
   }
-  if (ep.bn_mode) {
+  if (s2_stat_mode(ep)) {
     const int cnt = max(0, min(2, a.cd - Z0)) * max(0, min(4, a.ch - Y0)) * max(0, min(16, a.cw - X0));
     s2_bn_slab<2, 2>(ep, CO, vals, zv, ok, cnt, red);
   }
@@ -424,14 +444,14 @@ __global__ __launch_bounds__(256) void conv_s2t_kernel(S2Args a, const float* __
         const bool v_ok = zy_ok && X0 + 4 * g + j < a.cw;
         ok[c * 2 + zz][j] = v_ok;
         const int o = v_ok ? o0 + 2 * j * CO : 0;
-        zv[c * 2 + zz][0][j] = ep.bn_mode == 2 ? ep.bn_z[o] : 0.f;
+        zv[c * 2 + zz][0][j] = s2_stat_mode(ep) == 2 ? ep.bn_z[o] : 0.f;
         const float v = s2_act(acc[c][zz][j] + bias, ep);
         if (v_ok && (!(a.dbg & 4) || v == 1.2345f)) y[o] = v;
         vals[c * 2 + zz][0][j] = v;
       }
     }
   }
-  if (ep.bn_mode) {
+  if (s2_stat_mode(ep)) {
     const int cnt = 8 * max(0, min(2, a.cd - Z0)) * max(0, min(4, a.ch - Y0)) * max(0, min(16, a.cw - X0));
     s2_bn_slab<16, 1>(ep, CO, vals, zv, ok, cnt, red);
   }

@@ -100,98 +100,79 @@ __global__ __launch_bounds__(256) void gp_scale_kernel(const float* __restrict__
 }
 
 // --- generator losses ---------------------------------------------------------------------
-// pass 1: sum s, sum t, sum mask, sum mask*hu
+// One reduction pass: raw fp64 sums of s, t, s^2, t^2, s*t (every product of two fp32 values is exact
+// in fp64, so the centred moments E[st] - E[s]E[t] lose nothing that matters: |s|, |t| <= a few),
+// the mask count and the HU penalty sum; per-block partials part[b * 8 + q].
 __global__ __launch_bounds__(256) void gen_pass1_kernel(const float* __restrict__ s, const float* __restrict__ t,
                                                         const uint8_t* __restrict__ m, long long n, float lo, float hi,
                                                         double* part) {
   __shared__ double red[4];
-  double a0 = 0, a1 = 0, a2 = 0, a3 = 0;
+  double a[7] = {0, 0, 0, 0, 0, 0, 0};
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
-    const float x = s[i];
-    a0 += x;
-    a1 += t[i];
+    const double x = s[i], y = t[i];
+    a[0] += x;
+    a[1] += y;
+    a[2] += x * x;
+    a[3] += y * y;
+    a[4] += x * y;
     if (m[i]) {
-      const float lb = fminf(x, lo) - lo, ub = fmaxf(x, hi) - hi;
-      a2 += 1.0;
-      a3 += (double)(lb * lb + ub * ub);
+      const float xf = s[i];
+      const float lb = fminf(xf, lo) - lo, ub = fmaxf(xf, hi) - hi;
+      a[5] += 1.0;
+      a[6] += (double)(lb * lb + ub * ub);
     }
   }
-  a0 = block_sum_d(a0, red); a1 = block_sum_d(a1, red); a2 = block_sum_d(a2, red); a3 = block_sum_d(a3, red);
-  if (threadIdx.x == 0) {
-    part[blockIdx.x * 4 + 0] = a0; part[blockIdx.x * 4 + 1] = a1;
-    part[blockIdx.x * 4 + 2] = a2; part[blockIdx.x * 4 + 3] = a3;
-  }
+#pragma unroll
+  for (int q = 0; q < 7; ++q) a[q] = block_sum_d(a[q], red);
+  if (threadIdx.x == 0)
+#pragma unroll
+    for (int q = 0; q < 7; ++q) part[blockIdx.x * 8 + q] = a[q];
 }
 
-// the nblk x 4 partials of a pass combined in a fixed order (identical in every block that calls it)
-__device__ __forceinline__ void gen_combine(const double* __restrict__ part, int nblk, double* red, double (&a)[4]) {
-  for (int q = 0; q < 4; ++q) a[q] = 0.0;
+// the nblk x 8 partials combined in a fixed order (identical in every block that calls it)
+__device__ __forceinline__ void gen_combine(const double* __restrict__ part, int nblk, double* red, double (&a)[7]) {
+  for (int q = 0; q < 7; ++q) a[q] = 0.0;
   for (int b = threadIdx.x; b < nblk; b += blockDim.x)
-    for (int q = 0; q < 4; ++q) a[q] += part[b * 4 + q];
-  for (int q = 0; q < 4; ++q) a[q] = block_sum_d(a[q], red);
-}
-
-// pass 2 (pass 1's finalize folded in: every block combines pass 1's partials; block 0 publishes
-// stat[0..3] = s_mean, t_mean, mask_sum, hu_sum): sum (s-sm)(t-tm), (s-sm)^2, (t-tm)^2, (t-tm)
-__global__ __launch_bounds__(256) void gen_pass2_kernel(const float* __restrict__ s, const float* __restrict__ t,
-                                                        long long n, const double* __restrict__ part1, int nblk1,
-                                                        double* stat, double* part) {
-  __shared__ double red[4];
-  double f[4];
-  gen_combine(part1, nblk1, red, f);
-  if (blockIdx.x == 0 && threadIdx.x == 0) {
-    stat[0] = f[0] / (double)n; stat[1] = f[1] / (double)n; stat[2] = f[2]; stat[3] = f[3];
-  }
-  const float sm = (float)(f[0] / (double)n), tm = (float)(f[1] / (double)n);
-  double a0 = 0, a1 = 0, a2 = 0, a3 = 0;
-  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
-    const float u = s[i] - sm, w = t[i] - tm;
-    a0 += (double)(u * w);
-    a1 += (double)(u * u);
-    a2 += (double)(w * w);
-    a3 += (double)w;
-  }
-  a0 = block_sum_d(a0, red); a1 = block_sum_d(a1, red); a2 = block_sum_d(a2, red); a3 = block_sum_d(a3, red);
-  if (threadIdx.x == 0) {
-    part[blockIdx.x * 4 + 0] = a0; part[blockIdx.x * 4 + 1] = a1;
-    part[blockIdx.x * 4 + 2] = a2; part[blockIdx.x * 4 + 3] = a3;
-  }
+    for (int q = 0; q < 7; ++q) a[q] += part[b * 8 + q];
+  for (int q = 0; q < 7; ++q) a[q] = block_sum_d(a[q], red);
 }
 
 // dz_last = d(opt_hat)/d(z) chain: opt_hat = subopt - tanh(z)  =>  dz = -dL/dopt_hat * (1 - att^2).
-// Pass 2's finalize folded in: every block combines its partials into the losses and the gradient
-// coefficients A (w coef), Bc (u coef), w_mean, hu_scale; block 0 writes the losses.
+// The reduction's finalize folded in: every block combines the partials into the losses and the
+// gradient coefficients A (w coef), Bc (u coef), w_mean, hu_scale; block 0 writes the losses.
 __global__ __launch_bounds__(256) void gen_grad_kernel(const float* __restrict__ s, const float* __restrict__ t,
                                                        const float* __restrict__ att, const uint8_t* __restrict__ m,
                                                        const float* __restrict__ dcrit, long long n, float lo, float hi,
-                                                       const double* __restrict__ stat, const double* __restrict__ part2,
-                                                       int nblk2, float sim_w, float hu_w, float* losses, float* dz) {
+                                                       const double* __restrict__ part, int nblk, float sim_w,
+                                                       float hu_w, float* losses, float* dz) {
   __shared__ double red[4];
-  double a[4];
-  gen_combine(part2, nblk2, red, a);
-  const double suw = a[0], suu = a[1], sww = a[2], sw = a[3];
+  double a[7];
+  gen_combine(part, nblk, red, a);
   const double nn = (double)n;
+  const double smd = a[0] / nn, tmd = a[1] / nn;
+  const double suw = a[4] - nn * smd * tmd, suu = fmax(a[2] - nn * smd * smd, 0.0), sww = fmax(a[3] - nn * tmd * tmd, 0.0);
   const double cc = suw / nn;
   const double ss = sqrt(suu / (nn - 1.0)), st = sqrt(sww / (nn - 1.0));  // torch.std (unbiased)
   const double D = ss * st + 1e-8;
-  // dL/ds_j = -(1/D) (w_j - mean w)/n  +  cc*st/D^2 * 2/(n-1) * (s_j - s_mean)/(2 ss + 1e-6)
+  const float sm = (float)smd, tm = (float)tmd;
+  // dL/ds_j = -(1/D) (w_j - mean w)/n  +  cc*st/D^2 * 2/(n-1) * (s_j - s_mean)/(2 ss + 1e-6), with
+  // w_j = t_j - tm in fp32: mean w = mean t - tm exactly
   const float A = (float)(sim_w * (-1.0 / (D * nn)));
   const float Bc = (float)(sim_w * (cc * st / (D * D)) * (2.0 / (nn - 1.0)) / (2.0 * ss + 1e-6));
-  const float wm = (float)(sw / nn), hs = (float)(hu_w * 2.0 / (stat[2] + 1e-8));
+  const float wm = (float)(tmd - (double)tm), hs = (float)(hu_w * 2.0 / (a[5] + 1e-8));
   if (blockIdx.x == 0 && threadIdx.x == 0) {
-    const double zncc = -cc / D, hu = stat[3] / (stat[2] + 1e-8);
+    const double zncc = -cc / D, hu = a[6] / (a[5] + 1e-8);
     losses[L_SIM] = (float)(sim_w * zncc);
     losses[L_HU] = (float)(hu_w * hu);
     losses[L_GFULL] = losses[L_G] + (float)(sim_w * zncc) + (float)(hu_w * hu);
   }
-  const float sm = (float)stat[0], tm = (float)stat[1];
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
     const float x = s[i];
     float g = A * ((t[i] - tm) - wm) + Bc * (x - sm);
     if (m[i]) g += hs * ((fminf(x, lo) - lo) + (fmaxf(x, hi) - hi));
     if (dcrit) g += dcrit[i];
-    const float a = att[i];
-    dz[i] = -g * (1.f - a * a);
+    const float at = att[i];
+    dz[i] = -g * (1.f - at * at);
   }
 }
 
@@ -207,7 +188,7 @@ static int red_blocks(long long n) {
 using namespace cg;
 
 extern "C" int64_t cgan3d_loss_ws_floats(int64_t n) {
-  // generator losses: (2 x 512 x 4 partials + 8 stats) doubles; GP: b x (<=64 chunks) floats, b <= 1024
+  // generator losses: 512 x 8 partial doubles; GP: b x (<=64 chunks) floats, b <= 1024
   (void)n;
   return 2 * (2 * 512 * 4 + 8) + 65 * 1024;
 }
@@ -257,17 +238,13 @@ extern "C" int cgan3d_generator_output_grad(const float* opt_hat, const float* s
   CG_CHECK_ARG(n > 1, "cgan3d_generator_output_grad: need n > 1");
   CG_CHECK_ARG(((uintptr_t)ws & 7) == 0, "cgan3d_generator_output_grad: workspace must be 8-byte aligned");
   hipStream_t s = (hipStream_t)stream;
-  double* part1 = reinterpret_cast<double*>(ws);
-  double* part2 = part1 + 512 * 4;
-  double* stat = part2 + 512 * 4;
+  double* part = reinterpret_cast<double*>(ws);
   const int nblk = red_blocks(n);
-  ::cg::launch(gen_pass1_kernel, dim3(nblk), dim3(256), 0, s, opt_hat, subopt, mask, (long long)n, lo, hi, part1);
+  ::cg::launch(gen_pass1_kernel, dim3(nblk), dim3(256), 0, s, opt_hat, subopt, mask, (long long)n, lo, hi, part);
   CG_LAUNCH_CHECK("gen_pass1_kernel");
-  ::cg::launch(gen_pass2_kernel, dim3(nblk), dim3(256), 0, s, opt_hat, subopt, (long long)n, part1, nblk, stat, part2);
-  CG_LAUNCH_CHECK("gen_pass2_kernel");
   int blocks = (int)std::min<long long>((n + 255) / 256, 512);
   ::cg::launch(gen_grad_kernel, dim3(blocks), dim3(256), 0, s, opt_hat, subopt, att, mask, d_critic,
-                     (long long)n, lo, hi, stat, part2, nblk, sim_w, hu_w, losses, dz_last);
+                     (long long)n, lo, hi, part, nblk, sim_w, hu_w, losses, dz_last);
   CG_LAUNCH_CHECK("gen_grad_kernel");
   return CGAN3D_OK;
 }

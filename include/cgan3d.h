@@ -87,57 +87,20 @@ typedef struct cgan3d_conv_geom {
  *  bn_mode 2: v is dL/dy of a BatchNorm layer y = act(z * scale + shift) whose input z has the
  *             layout of this output: (sum g, sum g*xhat) with g = v * act'(z*scale + shift),
  *             xhat = (z - mean) * invstd (cgan3d_bn_backward_finalize_slab). */
-/* BatchNorm fused across a conv boundary (bf16 generator path, ResNet chain — model/blocks.py:50-53,
- * 85-88: conv -> BatchNorm3d -> act (+ skip) -> next conv).  Two halves, usable separately:
- *
- * Producer (acc_mode != 0; the halo-tiled kernels: cgan3d_halo_eligible geometries, w_packed 2):
- * instead of a slab, every block adds its per-channel pair into fp64 accumulators
- * acc_out[(r * 2 + q) * cout + c] (replica r = block % reps; reps * 2 * cout doubles, zero before
- * the launch):
+/* BatchNorm statistics into fp64 accumulators instead of a slab (bf16 generator path): every block
+ * of the producing launch adds its per-channel pair into acc_out[(r * 2 + q) * cout + c] (replica
+ * r = block % reps; reps * 2 * cout doubles, zero before the launch), consumed by
+ * cgan3d_bn_apply_acc / cgan3d_bn_backward_acc / cgan3d_bn_backward_acc_fold (finalize folded into
+ * the elementwise launch: one launch per BatchNorm layer and direction, model/blocks.py:50-53):
  *   acc_mode 3 (forward): q = 0 sum v, q = 1 sum v^2 (v = the BatchNorm input z, this output);
  *   acc_mode 4 (input-grad): the pair of bn_mode 2 — sum g, sum g*xhat — with bn_z / bn_ss / bn_mi /
- *              bn_act of the epilogue.
- * Consumer (pre_mode != 0; the ResNet-block kernel only: k3 s1 p1 64 -> 64, cgan3d_bn_fuse_ok): the
- * conv's input x is not read; each staged input element is computed from the previous BatchNorm
- * layer, whose statistics every block combines from acc_in (the producer's accumulator) in fp64:
- *   pre_mode 1 (forward, the BatchNorm3d + act of model/blocks.py:53 and the skip add of :88):
- *     x = act(z * scale + shift) (+ res), scale = gamma * invstd, shift = beta - mean * scale;
- *     block (0, 0) writes ss = [scale | shift], mi = [mean | invstd] and updates the running
- *     buffers (momentum, unbiased variance) and nbt, as cgan3d_bn_finalize_slab;
- *   pre_mode 2 (input-grad, autograd of the same): x = dz = gamma * invstd * (g - mean(g) -
- *     xhat * mean(g * xhat)), g = dy * act'(z * scale + shift), from ss / mi of the forward;
- *     block (0, 0) adds sum g into dbeta and sum g*xhat into dgamma.
- *   The blocks of output-channel block 0 also write the interior of their input tile (every input
- *   voxel exactly once): y (fp32, optional) and y16 (bf16 copy, optional) — the tensors the
- *   BatchNorm pass would have produced.  Block (0, 0) zeroes `zero_n` doubles at `zero` first (an
- *   accumulator the stream is done with; the caller rotates them so none needs its own memset). */
+ *              bn_act of the epilogue (and bn_fold on the k7 input-grad).
+ * Producers (cgan3d_bn_fuse_ok): the halo-tiled kernels (w_packed 2, incl. the stride-2 16 <-> 32
+ * ones) and the generator's 1 -> 16 k7 MFMA kernel (first conv forward, last conv input-grad). */
 typedef struct cgan3d_bn_fuse {
   double* acc_out;
-  int32_t acc_mode;     /* 0, 3, 4 */
-  int32_t reps;         /* replicas of acc_out / acc_in (1..64) */
-  int32_t pre_mode;     /* 0, 1, 2 */
-  int32_t pre_act;      /* CGAN3D_ACT_NONE / RELU / LRELU of the previous layer */
-  float pre_slope;
-  float eps;
-  float momentum;
-  int32_t zero_n;
-  double nvox;          /* BatchNorm reduction count (voxels per channel) */
-  const double* acc_in;
-  const float* z;       /* BatchNorm input of the previous layer (this conv's input layout) */
-  const float* res;     /* pre_mode 1: added after the activation (NULL: none) */
-  const float* dy;      /* pre_mode 2: dL/dy */
-  const float* gamma;
-  const float* beta;
-  float* rmean;
-  float* rvar;
-  int64_t* nbt;
-  float* ss;            /* pre_mode 1: written; 2: read */
-  float* mi;            /* pre_mode 1: written; 2: read */
-  float* dgamma;        /* pre_mode 2: accumulated */
-  float* dbeta;
-  float* y;             /* interior output fp32 (NULL: not written) */
-  void* y16;            /* interior output bf16 (NULL: not written) */
-  double* zero;
+  int32_t acc_mode;     /* 3 or 4 */
+  int32_t reps;         /* replicas of acc_out (1..64) */
 } cgan3d_bn_fuse;
 
 typedef struct cgan3d_epilogue {
@@ -163,11 +126,11 @@ typedef struct cgan3d_epilogue {
                                 * conv's, generator.py:78-84): the statistics are those of the
                                 * reflect-folded tensor (pad bn_fold), bn_z lives on the unpadded
                                 * grid; see cgan3d_bn_backward_slab_fold.  0 otherwise. */
-  const cgan3d_bn_fuse* fuse;  /* NULL, or BatchNorm fused across the conv boundary (above) */
+  const cgan3d_bn_fuse* fuse;  /* NULL, or the statistics into fp64 accumulators (above) */
 } cgan3d_epilogue;
 
-/* 1 when the geometry's launch can take cgan3d_bn_fuse pre_mode (consumer) / acc_mode (producer). */
-int32_t cgan3d_bn_fuse_ok(const cgan3d_conv_geom* g, int32_t consumer);
+/* 1 when the geometry's launch can produce cgan3d_bn_fuse accumulators. */
+int32_t cgan3d_bn_fuse_ok(const cgan3d_conv_geom* g);
 
 const char* cgan3d_version(void);
 const char* cgan3d_get_last_error(void);
@@ -298,6 +261,28 @@ int cgan3d_bn_backward_slab_fold(const float* padded, const float* z, int32_t n,
                                  const float* mean_invstd, const float* gamma, int32_t act, float slope,
                                  float* dgamma, float* dbeta, float* dz, int32_t accumulate, float* ws,
                                  void* dz_bf16, void* stream);
+/* The same two passes from fp64 accumulators (cgan3d_bn_fuse acc_mode 3 / 4 of the producing conv:
+ * acc[r][2][c], r < reps) instead of a slab, finalize folded into the elementwise launch (every
+ * block combines the replicas itself; block 0 publishes scale_shift / mean_invstd / the running
+ * buffers, or dgamma / dbeta): one launch per BatchNorm layer and direction.  Block 0 also zeroes
+ * `zero_n` doubles at `zero` (an accumulator the stream is done with; NULL / 0: none).
+ * blocks.py:26-27,45 BatchNorm3d train forward + act (+ residual), and its autograd backward. */
+int cgan3d_bn_apply_acc(const double* acc, int32_t reps, int32_t c, int64_t nvox, const float* gamma,
+                        const float* beta, float* running_mean, float* running_var, int64_t* num_batches_tracked,
+                        float momentum, float eps, float* scale_shift, float* mean_invstd, const float* z,
+                        int32_t act, float slope, const float* residual, float* y, void* y_bf16, double* zero,
+                        int32_t zero_n, void* stream);
+int cgan3d_bn_backward_acc(const float* dy, const float* z, int64_t nvox, int32_t c, const double* acc,
+                           int32_t reps, const float* scale_shift, const float* mean_invstd, const float* gamma,
+                           int32_t act, float slope, float* dgamma, float* dbeta, float* dz, int32_t accumulate,
+                           void* dz_bf16, double* zero, int32_t zero_n, void* stream);
+/* cgan3d_bn_backward_slab_fold with the statistics from accumulators (the last conv's input-grad
+ * launch with cgan3d_bn_fuse acc_mode 4 and bn_fold), one launch. */
+int cgan3d_bn_backward_acc_fold(const float* padded, const float* z, int32_t n, int32_t d, int32_t h, int32_t w,
+                                int32_t c, int32_t pad, const double* acc, int32_t reps, const float* scale_shift,
+                                const float* mean_invstd, const float* gamma, int32_t act, float slope,
+                                float* dgamma, float* dbeta, float* dz, int32_t accumulate, void* dz_bf16,
+                                double* zero, int32_t zero_n, void* stream);
 
 /* accumulate != 0: dgamma/dbeta += this batch's gradients (a module called on several batches in
  * one step, e.g. the BatchNorm critic on the real and the fake batch, Trainer.py:119-121). */
