@@ -717,9 +717,10 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_acc_kernel(const double* __r
   }
 }
 
-// blocks of the accumulator passes: ~4 float4 per thread (each block reads the replicas once)
+// blocks of the accumulator passes: ~2 float4 per thread, at most 4096 blocks (each block reads the
+// replicas once: reps x 2C doubles, 4-16 KB)
 static int acc_pass_blocks(long long n4) {
-  return (int)std::max(1LL, std::min((n4 + 1023) / 1024, 1024LL));
+  return (int)std::max(1LL, std::min((n4 + 511) / 512, 4096LL));
 }
 
 // blocks of the fused finalize + elementwise launch, or 0 when the slab is too large to be read by

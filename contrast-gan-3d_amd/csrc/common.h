@@ -272,18 +272,20 @@ __device__ __forceinline__ AdamK adam_k(const float* hyper, float step) {
   k.step_size = k.lr / (1.f - powf(b1, step));
   return k;
 }
-__device__ __forceinline__ float adam_elem(const AdamK& k, float* __restrict__ p, const float* __restrict__ g,
-                                          float* __restrict__ m, float* __restrict__ v, long long i) {
-  const float gi = g[i];
-  float mi = m[i];
+__device__ __forceinline__ void adam_vals(const AdamK& k, float gi, float& mi, float& vi, float& pi) {
   // torch lerp: weight < 0.5 ? self + w*(end-self) : end - (end-self)*(1-w)
   mi = k.wgt < 0.5f ? mi + k.wgt * (gi - mi) : gi - (gi - mi) * (1.f - k.wgt);
-  const float vi = v[i] * k.b2 + (1.f - k.b2) * gi * gi;
+  vi = vi * k.b2 + (1.f - k.b2) * gi * gi;
+  const float denom = sqrtf(vi) / k.bc2s + k.eps;
+  pi = pi - k.step_size * (mi / denom);
+  if (k.clip > 0.f) pi = fminf(fmaxf(pi, -k.clip), k.clip);
+}
+__device__ __forceinline__ float adam_elem(const AdamK& k, float* __restrict__ p, const float* __restrict__ g,
+                                          float* __restrict__ m, float* __restrict__ v, long long i) {
+  float mi = m[i], vi = v[i], pi = p[i];
+  adam_vals(k, g[i], mi, vi, pi);
   m[i] = mi;
   v[i] = vi;
-  const float denom = sqrtf(vi) / k.bc2s + k.eps;
-  float pi = p[i] - k.step_size * (mi / denom);
-  if (k.clip > 0.f) pi = fminf(fmaxf(pi, -k.clip), k.clip);
   p[i] = pi;
   return pi;
 }

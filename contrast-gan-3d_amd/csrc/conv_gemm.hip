@@ -515,6 +515,32 @@ __global__ __launch_bounds__(256) void adam_pack_kernel(float* __restrict__ p, c
                                                         float* hyper, const cgan3d_pack_desc* __restrict__ descs,
                                                         int ndesc, int tick, unsigned* ticket) {
   const AdamK k = adam_k(hyper, tick ? hyper[4] + 1.f : hyper[4]);
+  if (ndesc == 0 && !((reinterpret_cast<uintptr_t>(p) | reinterpret_cast<uintptr_t>(g) | reinterpret_cast<uintptr_t>(m) |
+                       reinterpret_cast<uintptr_t>(v)) & 15)) {
+    // no packed copies to refresh: four elements per lane (16-byte loads and stores), same arithmetic
+    const long long n4 = n >> 2;
+    f32x4* p4 = reinterpret_cast<f32x4*>(p);
+    f32x4* m4 = reinterpret_cast<f32x4*>(m);
+    f32x4* v4 = reinterpret_cast<f32x4*>(v);
+    const f32x4* g4 = reinterpret_cast<const f32x4*>(g);
+    for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n4; i += (long long)gridDim.x * 256) {
+      const f32x4 gi = g4[i];
+      f32x4 mi = m4[i], vi = v4[i], pi = p4[i];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float a = mi[e], b = vi[e], c = pi[e];
+        adam_vals(k, gi[e], a, b, c);
+        mi[e] = a; vi[e] = b; pi[e] = c;
+      }
+      m4[i] = mi;
+      v4[i] = vi;
+      p4[i] = pi;
+    }
+    for (long long i = 4 * n4 + (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long long)gridDim.x * 256)
+      adam_elem(k, p, g, m, v, i);
+    if (tick && last_block_out(ticket)) hyper[4] += 1.f;
+    return;
+  }
   for (long long base = (long long)blockIdx.x * 256; base < n; base += (long long)gridDim.x * 256) {
     const long long i = base + threadIdx.x;
     const bool live = i < n;
@@ -531,7 +557,7 @@ __global__ __launch_bounds__(256) void adam_pack_kernel(float* __restrict__ p, c
 
 void adam_launch(float* p, const float* g, float* m, float* v, long long n, float* hyper,
                  const cgan3d_pack_desc* descs, int ndesc, int tick, unsigned* ticket, hipStream_t st) {
-  const int blocks = (int)std::min<long long>((n + 255) / 256, 1024);
+  const int blocks = (int)std::min<long long>((ndesc ? n + 255 : n / 4 + 255) / 256, 1024);
   ::cg::launch(adam_pack_kernel, dim3(blocks), dim3(256), 0, st, p, g, m, v, n, hyper, descs, ndesc, tick, ticket);
 }
 

@@ -1,0 +1,11 @@
+# Quick A/B of an environment switch: default vs $AB_ENV (e.g. AB_ENV=CGAN3D_LAST_WGRAD_AFTER=1), two
+# rounds each, back to back on one box, plus a plan-mode kernel trace of the default.
+set -o pipefail
+cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out
+for k in 1 2; do
+timeout -k 10 200 python -u bench.py --no-cpu-baseline > gpurun_out/ab_def_$k.json 2> gpurun_out/ab_def_$k.err || exit $?
+env $AB_ENV timeout -k 10 200 python -u bench.py --no-cpu-baseline > gpurun_out/ab_alt_$k.json 2> gpurun_out/ab_alt_$k.err || exit $?
+done
+cd /tmp && export TMPDIR=/tmp
+rm -rf $GRAFT_REPO_ROOT/gpurun_out/tab
+timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d $GRAFT_REPO_ROOT/gpurun_out/tab -o run -- python3 $GRAFT_REPO_ROOT/bench.py --steps 20 --warmup 3 --no-cpu-baseline > $GRAFT_REPO_ROOT/gpurun_out/tab.json 2> $GRAFT_REPO_ROOT/gpurun_out/tab.err
