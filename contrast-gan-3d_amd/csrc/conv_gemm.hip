@@ -557,7 +557,10 @@ __global__ __launch_bounds__(256) void adam_pack_kernel(float* __restrict__ p, c
 
 void adam_launch(float* p, const float* g, float* m, float* v, long long n, float* hyper,
                  const cgan3d_pack_desc* descs, int ndesc, int tick, unsigned* ticket, hipStream_t st) {
-  const int blocks = (int)std::min<long long>((ndesc ? n + 255 : n / 4 + 255) / 256, 1024);
+  // vector path: ~4 float4 per thread, at most 256 blocks — the step tick's "last block out" ticket is
+  // one global atomic per block, and a thousand of them on one address took ~12 us
+  const int blocks = ndesc ? (int)std::min<long long>((n + 255) / 256, 1024)
+                           : (int)std::max<long long>(1, std::min<long long>((n / 4 + 1023) / 1024, 256));
   ::cg::launch(adam_pack_kernel, dim3(blocks), dim3(256), 0, st, p, g, m, v, n, hyper, descs, ndesc, tick, ticket);
 }
 

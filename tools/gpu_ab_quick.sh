@@ -2,6 +2,9 @@
 # rounds each, back to back on one box, plus a plan-mode kernel trace of the default.
 set -o pipefail
 cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out
+if [ -n "$AB_TESTS" ]; then
+timeout -k 10 400 python -u -m pytest -x -v --timeout 200 --timeout-method thread tests/test_gpu_step.py -k "$AB_TESTS" > gpurun_out/ab_tests.log 2>&1 || exit $?
+fi
 for k in 1 2; do
 timeout -k 10 200 python -u bench.py --no-cpu-baseline > gpurun_out/ab_def_$k.json 2> gpurun_out/ab_def_$k.err || exit $?
 env $AB_ENV timeout -k 10 200 python -u bench.py --no-cpu-baseline > gpurun_out/ab_alt_$k.json 2> gpurun_out/ab_alt_$k.err || exit $?
