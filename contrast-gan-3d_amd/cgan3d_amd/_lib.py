@@ -89,6 +89,8 @@ _SIGS = {
     "cgan3d_conv3d_shadow_only": ([_P, _I32], _I32),
     "cgan3d_conv3d_bn_fold_ok": ([_P], _I32),
     "cgan3d_bn_fuse_ok": ([_P], _I32),
+    "cgan3d_conv3d_wgrad_group_ok": ([_P], _I32),
+    "cgan3d_conv3d_wgrad_group": ([_P, _P, _P, _P, _I32, _P], _I32),
     "cgan3d_conv3d_wgrad_ex": ([_P, _P, _P, _P, _I32, _P, _P, _P, _P], _I32),
     "cgan3d_bn_finalize": ([_P, _I64, _I32, _P, _P, _P, _P, _P, _F, _F, _P, _P, _P], _I32),
     "cgan3d_bn_apply": ([_P, _I64, _I32, _P, _I32, _F, _P, _P, _P, _P], _I32),

@@ -799,6 +799,33 @@ class CriticPlan:
             return ops.wgrad(g, a, b, dw, self.ws_clean, accumulate=True, ws_clean=True)
         return ops.wgrad(g, a, b, dw, ws, accumulate=zeroed)
 
+    def _wgrad_geo(self, j: int, n_all: int):
+        ly = self.layers[j]
+        return ops.with_prec(ops.conv_wgrad_geom(n_all, ly.din, ly.dout, ly.cin, ly.cout, ly.k, ly.s, ly.p,
+                                                 planar=self.pl), self.prec)
+
+    def _groupable(self, j: int, n_all: int, zeroed: bool) -> bool:
+        """Layer j's weight grad can join one grouped launch (ops.wgrad_group): the deferred-unpack
+        path into its own clean workspace, a geometry the generic bf16 kernel takes."""
+        if not (zeroed and self.defer) or os.environ.get("CGAN3D_NO_WGRAD_GROUP"):
+            return False
+        g = self._wgrad_geo(j, n_all)
+        return ops.wgrad_ws_atomic(g) and ops.wgrad_group_ok(g)
+
+    def _wgrad_group(self, G, layers, n_all: int):
+        """The weight grads of ``layers`` (operands a_{j-1}, dz_j over n_all samples) in one launch:
+        independent small grids run side by side instead of one after another; each result waits in
+        its layer's clean workspace for the unpack launch (_flush_unpack)."""
+        items = []
+        for j in layers:
+            g = self._wgrad_geo(j, n_all)
+            wl = self.ws_layer.get(j)
+            if wl is None:
+                wl = self.ws_layer[j] = torch.zeros(ops.wgrad_ws_floats(g), device=self.ws.device)
+            items.append((g, self.a[j - 1][:n_all], self.dz[j][:n_all], wl))
+            self._deferred.append((j, g, wl, G[f"{self.layers[j].name}.weight"]))
+        ops.wgrad_group(items)
+
     def _flush_unpack(self):
         """One launch moving every deferred weight grad into dW (workspaces left zeroed)."""
         if not self._deferred:
@@ -840,13 +867,19 @@ class CriticPlan:
             self._on_side(lambda: self._bias_sums(G, n_bias, side=True).run())
             self._on_side(lambda: wgrad(0, x_all))
         h = gamma
+        group = []  # layers whose weight grads run together in one launch after the chain (_wgrad_group)
         for i, ly in enumerate(self.layers[:-1]):
             g = self._geo(ops.conv_fwd_geom(n, ly.din, ly.dout, ly.cin, ly.cout, ly.k, ly.s, ly.p, planar=self.pl), self.wf[i])
             out = self._sl(self.a[i], off, n)
             w = self.wf[i] if self.wf[i] is not None else P[f"{ly.name}.weight"]
             ops.conv(g, h, w, out, ops.epilogue(mask_src=out, slope=self.slope))
             h = out
-            self._on_side(lambda i=i: wgrad(i + 1, self.a[i][:n_all]))  # a_i now holds nu_i in its interp rows
+            if self.side is None and self._groupable(i + 1, n_all, zeroed):
+                group.append(i + 1)
+            else:
+                self._on_side(lambda i=i: wgrad(i + 1, self.a[i][:n_all]))  # a_i now holds nu_i in its interp rows
+        if group:
+            self._wgrad_group(G, group, n_all)
         self._on_side(self._flush_unpack)
 
     def _bias_sums(self, G, n_bias: int, side: bool = False) -> "ops.ChannelSumSet":

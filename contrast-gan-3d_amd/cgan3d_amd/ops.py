@@ -562,6 +562,31 @@ def wgrad(g: ConvGeom, gathered, aligned, dw, ws, accumulate=False, gathered16=N
                  _need16(aligned16, _vox_out(g) * g.cout, "wgrad aligned16")), "conv3d_wgrad")
 
 
+def wgrad_group_ok(g: ConvGeom) -> bool:
+    """True if ``g``'s weight gradient can join a ``wgrad_group`` launch."""
+    return bool(L.load().cgan3d_conv3d_wgrad_group_ok(ctypes.byref(g)))
+
+
+def wgrad_group(items):
+    """Several weight gradients in one launch (cgan3d_conv3d_wgrad_group): ``items`` = [(g, gathered,
+    aligned, ws)], each ``ws`` an all-zero workspace the result is added into, as ``wgrad(...,
+    accumulate=True, ws_clean=True, defer_unpack=True)`` — moved into dW by an ``UnpackSet`` run."""
+    if not 0 < len(items) <= 4:
+        raise ValueError("wgrad_group: 1..4 items")
+    for g, a, b, ws in items:
+        if not wgrad_group_ok(g):
+            raise ValueError("wgrad_group: geometry not eligible (cgan3d_conv3d_wgrad_group_ok)")
+        _need(a, _vox_in(g) * g.cin, "wgrad_group gathered")
+        _need(b, _vox_out(g) * g.cout, "wgrad_group aligned")
+        _need(ws, wgrad_ws_floats(g), "wgrad_group ws", exact=False)
+    n = len(items)
+    geoms = (ConvGeom * n)(*[g for g, _, _, _ in items])
+    ga = (ctypes.c_void_p * n)(*[a.data_ptr() for _, a, _, _ in items])
+    al = (ctypes.c_void_p * n)(*[b.data_ptr() for _, _, b, _ in items])
+    wss = (ctypes.c_void_p * n)(*[w.data_ptr() for _, _, _, w in items])
+    check(_launch("cgan3d_conv3d_wgrad_group", geoms, ga, al, wss, n), "wgrad_group")
+
+
 def bn_finalize(stats, nblk, c, gamma, beta, rmean, rvar, nbt, scale_shift, mean_invstd, momentum=0.1, eps=1e-5):
     _need(stats, nblk * (2 * c + 1), "bn_finalize stats", exact=False)
     for t, nm in ((gamma, "gamma"), (beta, "beta"), (rmean, "running_mean"), (rvar, "running_var")):

@@ -826,6 +826,28 @@ generic:
   return CGAN3D_OK;
 }
 
+// the weight gradient of g runs the generic bf16 kernel into an atomic workspace (the dispatch of
+// cgan3d_conv3d_wgrad_ex above reaches wgrad_bf16_launch)
+extern "C" int32_t cgan3d_conv3d_wgrad_group_ok(const cgan3d_conv_geom* g) {
+  if (!g || validate(g, "cgan3d_conv3d_wgrad_group_ok") || g->planar || g->transposed || g->cout == 1) return 0;
+  if (g->k == 7 && g->stride == 1 && (g->cin == 1 || g->cout == 1)) return 0;
+  if (c1_wgrad_ok(g) || wgrad_c1_ok(g) || wgrad_s2_ok(g) || wgrad_k3_ok(g)) return 0;
+  return wgrad_bf16_ok(g) ? 1 : 0;
+}
+
+extern "C" int cgan3d_conv3d_wgrad_group(const cgan3d_conv_geom* geoms, const float* const* gathered,
+                                         const float* const* aligned, float* const* ws, int32_t n, void* stream) {
+  CG_CHECK_ARG(geoms && gathered && aligned && ws && n > 0 && n <= 4, "cgan3d_conv3d_wgrad_group: 1..4 items");
+  for (int i = 0; i < n; ++i) {
+    CG_CHECK_ARG(cgan3d_conv3d_wgrad_group_ok(&geoms[i]), "cgan3d_conv3d_wgrad_group: item %d is not a generic bf16 "
+                 "weight gradient (cgan3d_conv3d_wgrad_group_ok)", i);
+    CG_CHECK_ARG(gathered[i] && aligned[i] && ws[i], "cgan3d_conv3d_wgrad_group: null pointer in item %d", i);
+  }
+  wgrad_bf16_group_launch(geoms, gathered, aligned, ws, n, (hipStream_t)stream);
+  CG_LAUNCH_CHECK("conv_wgrad_bf16_group_kernel");
+  return CGAN3D_OK;
+}
+
 extern "C" int cgan3d_wgrad_unpack_multi(const cgan3d_unpack_desc* descs, int32_t n, int64_t max_total, void* stream) {
   CG_CHECK_ARG(descs && n > 0 && n <= 65535 && max_total > 0,
                "cgan3d_wgrad_unpack_multi: need a device descriptor array, 0 < n <= 65535, max_total > 0");

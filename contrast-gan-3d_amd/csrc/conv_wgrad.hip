@@ -35,13 +35,12 @@ __device__ __forceinline__ int wg_coord(int i, int n, int reflect) {
 }
 
 template <int NB, bool ROW8>
-__global__ __launch_bounds__(256) void conv_wgrad_bf16_kernel(WgArgs a, const float* __restrict__ gx,
-                                                              const float* __restrict__ go, float* dwp) {
-  __shared__ __attribute__((aligned(16))) __bf16 As[64 * WG_LD];  // [row][voxel]
-  __shared__ __attribute__((aligned(16))) __bf16 Gs[64 * WG_LD];  // [b][voxel]
+__device__ __forceinline__ void wgrad_bf16_block(const WgArgs& a, const float* __restrict__ gx,
+                                                 const float* __restrict__ go, float* dwp, int bx, int by,
+                                                 __bf16* As, __bf16* Gs) {
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int r0 = blockIdx.x * 64;
-  const long long vbeg = (long long)blockIdx.y * a.vpb;
+  const int r0 = bx * 64;
+  const long long vbeg = (long long)by * a.vpb;
   const long long vend = vbeg + a.vpb < a.V ? vbeg + a.vpb : a.V;
 
   // staging role (wave-uniform): waves 0-1 gather G rows (4rq..4rq+3 = one tap, 4 channels),
@@ -150,6 +149,43 @@ __global__ __launch_bounds__(256) void conv_wgrad_bf16_kernel(WgArgs a, const fl
   }
 }
 
+template <int NB, bool ROW8>
+__global__ __launch_bounds__(256) void conv_wgrad_bf16_kernel(WgArgs a, const float* __restrict__ gx,
+                                                              const float* __restrict__ go, float* dwp) {
+  __shared__ __attribute__((aligned(16))) __bf16 As[64 * WG_LD];  // [row][voxel]
+  __shared__ __attribute__((aligned(16))) __bf16 Gs[64 * WG_LD];  // [b][voxel]
+  wgrad_bf16_block<NB, ROW8>(a, gx, go, dwp, blockIdx.x, blockIdx.y, As, Gs);
+}
+
+// ---- several of those weight gradients in one launch (cgan3d_conv3d_wgrad_group): item i owns the
+// blocks [first[i], first[i + 1]) of a 1-D grid; each block runs the single kernel's body with its
+// item's operands (the critic's middle layers after the penalty's forward-mode chain: independent
+// grids of 100-300 blocks that each leave most of the chip idle and pay a launch apiece)
+constexpr int WG_GROUP = 4;
+struct WgGroup {
+  WgArgs a[WG_GROUP];
+  const float* gx[WG_GROUP];
+  const float* go[WG_GROUP];
+  float* dwp[WG_GROUP];
+  int gxb[WG_GROUP];          // row blocks of the item (its grid's x extent)
+  int nb[WG_GROUP];           // 16-column tiles (cout / 16, rounded up)
+  int row8[WG_GROUP];         // W % 8 == 0
+  int first[WG_GROUP + 1];
+  int n;
+};
+
+__global__ __launch_bounds__(256) void conv_wgrad_bf16_group_kernel(WgGroup G) {
+  __shared__ __attribute__((aligned(16))) __bf16 As[64 * WG_LD];
+  __shared__ __attribute__((aligned(16))) __bf16 Gs[64 * WG_LD];
+  int i = 0;
+  while (i + 1 < G.n && (int)blockIdx.x >= G.first[i + 1]) ++i;
+  const int b = blockIdx.x - G.first[i], bx = b % G.gxb[i], by = b / G.gxb[i];
+#define CG_WGG(N) (G.row8[i] ? wgrad_bf16_block<N, true>(G.a[i], G.gx[i], G.go[i], G.dwp[i], bx, by, As, Gs) \
+                             : wgrad_bf16_block<N, false>(G.a[i], G.gx[i], G.go[i], G.dwp[i], bx, by, As, Gs))
+  if (G.nb[i] == 1) CG_WGG(1); else if (G.nb[i] == 2) CG_WGG(2); else if (G.nb[i] == 3) CG_WGG(3); else CG_WGG(4);
+#undef CG_WGG
+}
+
 // ---- single-channel input, few output channels (the critic's first layer, 1 -> 8, k4 s2):
 // M x N = 64 taps x 8 is too small for MFMA tiles, K = every output voxel.  A thread owns one tap
 // and all output channels; the 64 lanes of a wave are the 64 taps of ONE output voxel, so the
@@ -242,9 +278,7 @@ bool wgrad_bf16_ok(const cgan3d_conv_geom* g) {
          g->cout >= 4;
 }
 
-// adds into the packed [t][a][b] workspace dwp (zeroed by the caller)
-int wgrad_bf16_launch(const cgan3d_conv_geom* g, const float* gathered, const float* aligned, float* dwp,
-                      hipStream_t st) {
+static WgArgs wgrad_bf16_args(const cgan3d_conv_geom* g, int* gxb, int* gyb) {
   WgArgs a;
   a.n = g->n; a.di = g->di; a.hi = g->hi; a.wi = g->wi; a.do_ = g->do_; a.ho = g->ho; a.wo = g->wo;
   a.cin = g->cin; a.cout = g->cout; a.k = g->k; a.s = g->stride; a.p = g->pad; a.reflect = g->reflect;
@@ -257,7 +291,17 @@ int wgrad_bf16_launch(const cgan3d_conv_geom* g, const float* gathered, const fl
   long long vpb = (a.V + gy - 1) / gy;
   if (vpb < 4 * WG_KV) vpb = 4 * WG_KV;
   a.vpb = (vpb + WG_KV - 1) / WG_KV * WG_KV;
-  dim3 grid(gx, (unsigned)((a.V + a.vpb - 1) / a.vpb));
+  *gxb = gx;
+  *gyb = (int)((a.V + a.vpb - 1) / a.vpb);
+  return a;
+}
+
+// adds into the packed [t][a][b] workspace dwp (zeroed by the caller)
+int wgrad_bf16_launch(const cgan3d_conv_geom* g, const float* gathered, const float* aligned, float* dwp,
+                      hipStream_t st) {
+  int gxb, gyb;
+  const WgArgs a = wgrad_bf16_args(g, &gxb, &gyb);
+  dim3 grid(gxb, gyb);
   const int nb = (g->cout + 15) / 16;
 #define CG_WGB(N, R8) ::cg::launch((conv_wgrad_bf16_kernel<N, R8>), grid, dim3(256), 0, st, a, gathered, aligned, dwp)
   if (g->wo % 8 == 0) {  // chunks are 64-voxel aligned: 8 | W keeps each thread's 8 voxels in one row
@@ -270,6 +314,23 @@ int wgrad_bf16_launch(const cgan3d_conv_geom* g, const float* gathered, const fl
   return CGAN3D_OK;
 }
 
+int wgrad_bf16_group_launch(const cgan3d_conv_geom* geoms, const float* const* gathered, const float* const* aligned,
+                            float* const* ws, int n, hipStream_t st) {
+  WgGroup G{};
+  G.n = n;
+  G.first[0] = 0;
+  for (int i = 0; i < n; ++i) {
+    int gxb, gyb;
+    G.a[i] = wgrad_bf16_args(&geoms[i], &gxb, &gyb);
+    G.gx[i] = gathered[i]; G.go[i] = aligned[i]; G.dwp[i] = ws[i];
+    G.gxb[i] = gxb;
+    G.nb[i] = (geoms[i].cout + 15) / 16;
+    G.row8[i] = geoms[i].wo % 8 == 0;
+    G.first[i + 1] = G.first[i] + gxb * gyb;
+  }
+  ::cg::launch(conv_wgrad_bf16_group_kernel, dim3(G.first[n]), dim3(256), 0, st, G);
+  return CGAN3D_OK;
+}
 
 // ---- ResNet-block weight gradient (k3 s1 p1, 64 -> 64, bf16 MFMA), SURVEY.md §8 a2/a5:
 // dW[t][a][b] = sum_o X(o + t - 1)[a] * dZ(o)[b].  Block = (tap plane td, chunk p of the output

@@ -214,6 +214,16 @@ int cgan3d_conv3d_wgrad_ex(const cgan3d_conv_geom* g, const float* gathered, con
                            float* dw, int32_t accumulate, float* ws, const void* gathered_bf16,
                            const void* aligned_bf16, void* stream);
 
+/* Several independent weight gradients in ONE launch (the critic's middle layers once the penalty's
+ * forward-mode chain is done, discriminator.py:42-68: grids of 100-300 blocks that each leave most of
+ * the chip idle and pay a launch apiece): item i adds sum_o G_i(o*s - p + t, a) O_i(o, b) into its
+ * packed [t][a][b] workspace ws[i], all-zero on entry, exactly as cgan3d_conv3d_wgrad_ex with
+ * CGAN3D_WGRAD_ACCUMULATE | CGAN3D_WGRAD_WS_CLEAN | CGAN3D_WGRAD_DEFER_UNPACK would (then
+ * cgan3d_wgrad_unpack_multi).  1 <= n <= 4; every geometry cgan3d_conv3d_wgrad_group_ok. */
+int32_t cgan3d_conv3d_wgrad_group_ok(const cgan3d_conv_geom* g);
+int cgan3d_conv3d_wgrad_group(const cgan3d_conv_geom* geoms, const float* const* gathered,
+                              const float* const* aligned, float* const* ws, int32_t n, void* stream);
+
 /* --- BatchNorm3d, training mode (model/blocks.py:26-27,45; torch.nn.BatchNorm3d) --- */
 int cgan3d_bn_finalize(const float* stats, int64_t nblk, int32_t c, const float* gamma,
                        const float* beta, float* running_mean, float* running_var,
