@@ -174,16 +174,25 @@ struct WgGroup {
   int n;
 };
 
+// item I's operands indexed at compile time (a runtime index into the kernel-argument arrays makes
+// hipcc copy the whole struct to scratch)
+template <int I>
+__device__ __forceinline__ void wgrad_group_item(const WgGroup& G, __bf16* As, __bf16* Gs) {
+  const int b = blockIdx.x - G.first[I], bx = b % G.gxb[I], by = b / G.gxb[I];
+#define CG_WGG(N) (G.row8[I] ? wgrad_bf16_block<N, true>(G.a[I], G.gx[I], G.go[I], G.dwp[I], bx, by, As, Gs) \
+                             : wgrad_bf16_block<N, false>(G.a[I], G.gx[I], G.go[I], G.dwp[I], bx, by, As, Gs))
+  if (G.nb[I] == 1) CG_WGG(1); else if (G.nb[I] == 2) CG_WGG(2); else if (G.nb[I] == 3) CG_WGG(3); else CG_WGG(4);
+#undef CG_WGG
+}
+
 __global__ __launch_bounds__(256) void conv_wgrad_bf16_group_kernel(WgGroup G) {
   __shared__ __attribute__((aligned(16))) __bf16 As[64 * WG_LD];
   __shared__ __attribute__((aligned(16))) __bf16 Gs[64 * WG_LD];
-  int i = 0;
-  while (i + 1 < G.n && (int)blockIdx.x >= G.first[i + 1]) ++i;
-  const int b = blockIdx.x - G.first[i], bx = b % G.gxb[i], by = b / G.gxb[i];
-#define CG_WGG(N) (G.row8[i] ? wgrad_bf16_block<N, true>(G.a[i], G.gx[i], G.go[i], G.dwp[i], bx, by, As, Gs) \
-                             : wgrad_bf16_block<N, false>(G.a[i], G.gx[i], G.go[i], G.dwp[i], bx, by, As, Gs))
-  if (G.nb[i] == 1) CG_WGG(1); else if (G.nb[i] == 2) CG_WGG(2); else if (G.nb[i] == 3) CG_WGG(3); else CG_WGG(4);
-#undef CG_WGG
+  const int bid = blockIdx.x;
+  if (G.n > 3 && bid >= G.first[3]) wgrad_group_item<3>(G, As, Gs);
+  else if (G.n > 2 && bid >= G.first[2]) wgrad_group_item<2>(G, As, Gs);
+  else if (G.n > 1 && bid >= G.first[1]) wgrad_group_item<1>(G, As, Gs);
+  else wgrad_group_item<0>(G, As, Gs);
 }
 
 // ---- single-channel input, few output channels (the critic's first layer, 1 -> 8, k4 s2):
