@@ -468,31 +468,53 @@ __global__ __launch_bounds__(256, 2) void k7m_w2n_kernel(K7Args a, const float* 
 // ---- streamed-plane w2n (16 -> 1 from the bf16 shadow, the generator's last conv): the
 // contraction is split as  out[d][h][w] = sum_td P[d + td - 3][h][w][td]  with
 //   P[q][h][w][td] = sum_{th, tw, c} X[q][h + th - 3][w + tw - 3][c] * W[c][td][th][tw]
-// a GEMM per (input plane q, output row h): M = 16 w, N = td (7 of 16 columns), K = (th, tw, c)
-// = 7 x (8 tw x 16 c) = 28 K-steps.  The A fragment of a K-step is 8 consecutive channels of one
-// staged voxel (16 bytes straight from the plane staged in LDS: no unfolding), the 28 B
-// fragments (the weights) stay in registers for the whole launch, and each A fragment (staged
-// row r, tw pair) feeds the MFMAs of every output row h with th = r - h in range (112 MFMAs per
-// plane and wave, no off-band work).  A block streams the TDc + 6 input planes of a chunk of TDc
-// output planes through a ring of 4 LDS buffers filled by LDS-DMA (global_load_lds, 16 bytes per
-// lane, no staging registers) three planes ahead, together with the minuend rows of the output
-// plane each step finishes; lane (g, td) adds its P values into a per-wave ring of the 7 output
-// planes still open (td selects the plane: no two lanes of an instruction touch one address),
-// and a plane is finished (bias, tanh, opt_hat) once its last input plane has been added.
-__device__ u32x4 k7s_zero;  // zero-initialised device global: the source of out-of-volume granules
+// a GEMM per (input plane q, output row pair): M = 16 w, N = (h of the pair, td) = 2 x 7 of 16
+// columns, K = (th, tw, c) = 7 x (8 tw x 16 c).  The A fragment of a K-step is 8 consecutive
+// channels of one staged voxel (16 bytes straight from the plane staged in LDS: no unfolding); the
+// B fragment of staged row r and output pair (h, h + 1) holds W[.][td][r - h][.] in its first 8
+// columns and W[.][td][r - h - 1][.] in the next 8, so it depends on r - h only and the 32 of them
+// (r - h = 0..7, 4 tw pairs) stay in registers for the whole launch; every A fragment feeds the
+// MFMAs of each output pair it reaches (64 per plane and wave, none off-band).
+// A block = 16 x 16 output columns (h, w) x a chunk of TDc output planes; wave = 4 output rows.
+// It streams the TDc + 6 input planes (22 x 23 staged voxels each: the (h, w) halo re-read is
+// 1.98x, against 2.78x for a 4 x 64 tile) through a ring of 4 LDS buffers filled by LDS-DMA
+// (global_load_lds, 16 bytes per lane, no staging registers) three planes ahead, together with
+// the minuend rows of the output plane each step finishes; lane (g, h, td) adds its P values into
+// a per-wave ring of the 7 output planes still open (eight reads, then eight writes), laid out [h][w %
+// 4][w / 4][plane slot, 9 apart] so neither the adds (td picks the slot) nor the row reads of the
+// flush share a bank, and a plane is finished (bias, tanh, opt_hat) once its last input plane has
+// been added; the flush zeroes the slot for the plane 8 later.  Every store
+// instruction is issued by the whole wave (lanes past the volume write a sink), so the vmcnt wait
+// for a plane counts exactly the DMAs and stores issued after it.
+__device__ u32x4 k7s_zero;    // zero-initialised device global: the source of out-of-volume granules
+__device__ float k7s_sink[64];  // target of the stores of lanes past the volume
 
 namespace k7s {
-constexpr int SH = 4;                    // output rows per block
-constexpr int WB = 64;                   // output columns per block (4 waves x 16)
-constexpr int ROWS = SH + 6, COLS = WB + 7;  // 70 halo columns + one zero column (read by tw = 7)
+constexpr int SH = 16;                   // output rows per block (4 per wave)
+constexpr int WB = 16;                   // output columns per block (one M tile)
+constexpr int ROWS = SH + 6, COLS = WB + 7;  // 22 halo columns + one zero column (read by tw = 7)
 constexpr int RB = COLS * 32;            // staged row bytes (16 bf16 channels per voxel)
 constexpr int GRAN = ROWS * COLS * 2;    // 16-byte granules of a plane
 constexpr int GPT = (GRAN + 255) / 256;  // LDS-DMA instructions per wave per plane
 constexpr int MOFF = GPT * 256 * 16;     // minuend granules after the plane (4 waves x 64 lanes;
 constexpr int BUF = MOFF + 4 * 64 * 16;  // 16 of them used) — bytes per ring buffer
-constexpr int NBUF = 4;                  // planes in flight: 3 ahead of the one computed (5: same time)
+constexpr int NBUF = 4;                  // planes in flight: 3 ahead of the one computed
 constexpr int PER_STEP = GPT + 1;        // LDS-DMA instructions per wave per step
+constexpr int RING = 4 * 4 * 4 * 9;      // per-wave ring floats: [h][w % 4][w / 4][9]
 }  // namespace k7s
+
+template <int N>
+__device__ __forceinline__ void k7s_wait_vm(int n) {  // s_waitcnt vmcnt(n) for n in [N, N + 6]
+  switch (n - N) {
+    case 0: asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); break;
+    case 1: asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N + 1) : "memory"); break;
+    case 2: asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N + 2) : "memory"); break;
+    case 3: asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N + 3) : "memory"); break;
+    case 4: asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N + 4) : "memory"); break;
+    case 5: asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N + 5) : "memory"); break;
+    default: asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N + 6) : "memory"); break;
+  }
+}
 
 __global__ __launch_bounds__(256, 1) void k7s_w2n_kernel(K7Args a, const __bf16* __restrict__ x16,
                                                          const float* __restrict__ w, float* __restrict__ y,
@@ -501,40 +523,43 @@ __global__ __launch_bounds__(256, 1) void k7s_w2n_kernel(K7Args a, const __bf16*
                                                          int tdc) {
   using namespace k7s;
   extern __shared__ __attribute__((aligned(16))) unsigned char k7s_lds[];
-  unsigned char* bufs = k7s_lds;                                         // [NBUF][BUF]
-  float(*ring)[8][SH][16] = reinterpret_cast<float(*)[8][SH][16]>(k7s_lds + NBUF * BUF);  // per wave
+  unsigned char* bufs = k7s_lds;  // [NBUF][BUF]
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int g = lane >> 4, r16 = lane & 15;
-  int bid = blockIdx.x;  // (an XCD-grouped tile order measured the same: tools/k7s_probe.py)
-  const int tw_n = a.tiles_w, th_n = a.tiles_h, td_n = a.tiles_d;
-  const int wt_ = bid % tw_n; bid /= tw_n;
-  const int ht_ = bid % th_n; bid /= th_n;
-  const int dt_ = bid % td_n;
-  const int n = bid / td_n;
+  float* ring = reinterpret_cast<float*>(k7s_lds + NBUF * BUF) + wave * RING;
+  int bid = blockIdx.x;
+  const int wt_ = bid % a.tiles_w; bid /= a.tiles_w;
+  const int ht_ = bid % a.tiles_h; bid /= a.tiles_h;
+  const int dt_ = bid % a.tiles_d;
+  const int n = bid / a.tiles_d;
   const int d0 = dt_ * tdc, h0 = ht_ * SH, w0 = wt_ * WB;
-  // weights: B fragment (th, j) of lane (g, td = r16): W[c0 .. c0+7][td][th][tw], tw = 2j + (g >> 1)
-  bf16x8_k bw[7][4];
-  {  // branch-free (clamped addresses, then a select): every load of the thread in flight at once
-    const int td = r16, c0 = 8 * (g & 1);
+  // weights: B fragment (t0 = r - h, j) of lane (g, col = r16): column col = 8 hsel + td holds
+  // W[c0 .. c0 + 7][td][t0 - hsel][tw], tw = 2j + (g >> 1), c0 = 8 (g & 1); zero off the band.
+  // Staged once as bf16 [tap][16 channels] in the last ring buffer (first filled after the loop's
+  // first barrier): coalesced global reads, then one ds_read_b128 per fragment.
+  bf16x8_k bw[8][4];
+  {
+    __bf16* wl = reinterpret_cast<__bf16*>(bufs + (NBUF - 1) * BUF);
+    for (int i = tid; i < 16 * KT7; i += 256) {
+      const int c = i / KT7, t = i - c * KT7;
+      wl[t * 16 + c] = (__bf16)w[(long long)c * a.wc + t];
+    }
+    __syncthreads();
+    const int hsel = r16 >> 3, td = r16 & 7, c0 = 8 * (g & 1);
 #pragma unroll
-    for (int th = 0; th < 7; ++th)
+    for (int t0 = 0; t0 < 8; ++t0)
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        const int tw = 2 * j + (g >> 1);
-        const bool ok = td < 7 && tw < 7;
-        const long long base = ok ? (td * 7 + th) * 7 + tw : 0;
-        float f[8];
-#pragma unroll
-        for (int e = 0; e < 8; ++e) f[e] = w[(long long)(c0 + e) * a.wc + base];
-        bf16x8_k v;
-#pragma unroll
-        for (int e = 0; e < 8; ++e) v[e] = (__bf16)(ok ? f[e] : 0.f);
-        bw[th][j] = v;
+        const int th = t0 - hsel, tw = 2 * j + (g >> 1);
+        const bool ok = td < 7 && th >= 0 && th < 7 && tw < 7;
+        const bf16x8_k v = *reinterpret_cast<const bf16x8_k*>(wl + (ok ? (td * 7 + th) * 7 + tw : 0) * 16 + c0);
+        bw[t0][j] = ok ? v : bf16x8_k{};
       }
+    for (int i = lane; i < RING; i += 64) ring[i] = 0.f;  // slots are added into, zeroed again by the flush
   }
   // this lane's plane granules (lane-linear LDS image: granule i of the plane at byte 16 i, i = k *
   // 256 + wave * 64 + lane): the (h, w) part of the source offset, -1 = zero (past a partial tile,
-  // the tw = 7 pad column, or past the plane's 1420 granules).  Reflect padding (the launcher's
+  // the tw = 7 pad column, or past the plane's granules).  Reflect padding (the launcher's
   // condition): every plane index is in range.
   int hw[GPT];
 #pragma unroll
@@ -560,74 +585,83 @@ __global__ __launch_bounds__(256, 1) void k7s_w2n_kernel(K7Args a, const __bf16*
       __builtin_amdgcn_global_load_lds((const void*)(hw[k] >= 0 ? src + hw[k] : &k7s_zero),
                                        (__attribute__((address_space(3))) void*)(dst + (k * 256 + wave * 64) * 16),
                                        16, 0, 0);
-    // minuend granule lane (16 per wave: row lane / 4, 4 floats); W % 4 == 0 (launcher)
-    const int df = s - 6, od = d0 + df, oh = h0 + (lane >> 2) % SH, ow = w0 + wave * 16 + 4 * (lane & 3);
+    // minuend granule lane (16 per wave: row 4 wave + lane / 4, 4 floats); W % 4 == 0 (launcher)
+    const int df = s - 6, od = d0 + df, oh = h0 + 4 * wave + (lane >> 2), ow = w0 + 4 * (lane & 3);
     const bool mok = lane < 16 && out2 && df >= 0 && df < tdc && od < a.do_ && oh < a.ho && ow < a.wo;
     const float* ms = mok ? mbase + (((long long)n * a.do_ + od) * a.ho + oh) * a.wo + ow
                           : reinterpret_cast<const float*>(&k7s_zero);
     __builtin_amdgcn_global_load_lds((const void*)ms,
                                      (__attribute__((address_space(3))) void*)(dst + MOFF + wave * 64 * 16), 16, 0, 0);
   };
+  const int nst = out2 ? 2 : 1;  // store instructions per wave of a step that finishes a plane
+  auto stores_at = [&](int k) { return (k >= 6 && k - 6 < tdc) ? nst : 0; };
   const float b0 = bias ? bias[0] : 0.f;
+  const int td = r16 & 7, hsel = r16 >> 3;
   for (int s = 0; s < NBUF - 1; ++s) issue(s);
   for (int s = 0; s < nplanes; ++s) {
-    // plane s and its minuend rows are in: all but the two later batches retired (in order; the
-    // output stores issued since only make the wait longer), then a barrier so every wave's DMA is
-    // visible to every wave and every wave has finished reading the buffer refilled next
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER_STEP * (NBUF - 2)) : "memory");
+    // plane s and its minuend rows are in: everything issued after them may still be in flight
+    // (the two later DMA batches and the stores of the three steps since; in order), then a
+    // barrier so every wave's DMA is visible to every wave and every wave has finished reading the
+    // buffer refilled next
+    k7s_wait_vm<PER_STEP * (NBUF - 2)>(PER_STEP * (NBUF - 2) + stores_at(s - 3) + stores_at(s - 2) + stores_at(s - 1));
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     issue(s + NBUF - 1);  // NBUF - 1 planes ahead, into the buffer of plane s - 1 (dummies past the chunk)
-    const unsigned char* pb = bufs + (s % NBUF) * BUF + (wave * 16 + r16) * 32 + 16 * (g & 1);
-    f32x4 acc[SH];
+    const unsigned char* pb = bufs + (s % NBUF) * BUF + 4 * wave * RB + r16 * 32 + 16 * (g & 1);
+    f32x4 acc[2];
 #pragma unroll
-    for (int h = 0; h < SH; ++h) acc[h] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int hp = 0; hp < 2; ++hp) acc[hp] = f32x4{0.f, 0.f, 0.f, 0.f};
     // row r + 1's four A fragments are read while row r's MFMAs run
     bf16x8_k av[2][4];
     auto fetch = [&](int r, bf16x8_k (&o)[4]) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) o[j] = *reinterpret_cast<const bf16x8_k*>(pb + r * RB + (2 * j + (g >> 1)) * 32);
     };
-    if (!(a.dbg & 4)) fetch(0, av[0]);
+    fetch(0, av[0]);
 #pragma unroll
-    for (int r = 0; r < ROWS; ++r) {
-      if (r + 1 < ROWS && !(a.dbg & 4)) fetch(r + 1, av[(r + 1) & 1]);
+    for (int r = 0; r < 10; ++r) {
+      if (r + 1 < 10) fetch(r + 1, av[(r + 1) & 1]);
       __builtin_amdgcn_sched_barrier(0);
-      if (!(a.dbg & 1))
 #pragma unroll
       for (int j = 0; j < 4; ++j)
 #pragma unroll
-        for (int h = 0; h < SH; ++h) {
-          const int th = r - h;
-          if (th >= 0 && th < 7)
-            acc[h] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[r & 1][j], bw[th][j], acc[h], 0, 0, 0);
+        for (int hp = 0; hp < 2; ++hp) {
+          const int t0 = r - 2 * hp;
+          if (t0 >= 0 && t0 < 8)
+            acc[hp] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[r & 1][j], bw[t0][j], acc[hp], 0, 0, 0);
         }
       __builtin_amdgcn_sched_barrier(0);
     }
-    // lane (g, td) holds P[s][h][w = 4g + jj][td]: output plane dl = s - td of this block
-    const int dl = s - r16;
-    if (!(a.dbg & 2) && r16 < 7 && dl >= 0 && dl < tdc) {
-      float* rs = &ring[wave][dl & 7][0][0];
+    // lane (g, hsel, td) holds P[s][h = 2 hp + hsel][w = 4g + jj][td]: output plane dl = s - td
+    // (every read of the eight slots issued before the first write: one LDS round trip per step)
+    const int dl = s - td;
+    if (td < 7 && dl >= 0 && dl < tdc) {
+      float* rb = ring + (hsel * 16 + g) * 9 + (dl & 7);
+      float v[2][4];
 #pragma unroll
-      for (int h = 0; h < SH; ++h)
+      for (int hp = 0; hp < 2; ++hp)
 #pragma unroll
-        for (int jj = 0; jj < 4; ++jj) {
-          float* o = rs + h * 16 + 4 * g + jj;
-          *o = r16 == 0 ? acc[h][jj] : *o + acc[h][jj];
-        }
+        for (int jj = 0; jj < 4; ++jj) v[hp][jj] = rb[(hp * 32 + jj * 4) * 9];
+#pragma unroll
+      for (int hp = 0; hp < 2; ++hp)
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) rb[(hp * 32 + jj * 4) * 9] = v[hp][jj] + acc[hp][jj];
     }
     const int df = s - 6;  // output plane complete after this input plane
-    const int fh = lane >> 4, fwl = lane & 15;
-    const int od = d0 + df, oh = h0 + fh, ow = w0 + wave * 16 + fwl;
-    if (df >= 0 && df < tdc && od < a.do_ && oh < a.ho && ow < a.wo) {
-      float v = ring[wave][df & 7][fh][fwl] + b0;
+    if (df >= 0 && df < tdc) {
+      const int fh = lane >> 4, fw = lane & 15;
+      const int od = d0 + df, oh = h0 + 4 * wave + fh, ow = w0 + fw;
+      float* slot = ring + ((fh * 4 + (fw & 3)) * 4 + (fw >> 2)) * 9 + (df & 7);
+      float v = *slot + b0;
+      *slot = 0.f;
       if (act == CGAN3D_ACT_TANH) v = tanhf(v);
+      const bool ok = od < a.do_ && oh < a.ho && ow < a.wo;
       const long long o = (((long long)n * a.do_ + od) * a.ho + oh) * a.wo + ow;
-      y[o] = v;
+      *(ok ? y + o : k7s_sink + lane) = v;
       if (out2) {
         const float* mrow = reinterpret_cast<const float*>(bufs + (s % NBUF) * BUF + MOFF + wave * 64 * 16);
-        out2[o] = mrow[fh * 16 + fwl] - v;
+        *(ok ? out2 + o : k7s_sink + lane) = mrow[fh * 16 + fw] - v;
       }
     }
   }
@@ -908,15 +942,13 @@ void k7m_w2n_launch(const cgan3d_conv_geom* g, int P, int reflect, long long wc,
                     float* y, const Epi& e, hipStream_t s) {
   if (e.x16 && g_k7s >= 0 && reflect && g->di == g->do_ && g->hi == g->ho && g->wi == g->wo && P == 3 &&
       std::min(g->di, std::min(g->hi, g->wi)) >= 4 && g->wo % 4 == 0) {
-    // streamed-plane kernel: output-plane chunks of 16 planes, or 8 when 16 leaves CUs idle.  At 64^3
-    // B=4 (tools/k7s_probe.py): 77-80 us against 82-84 for k7m_w2n_kernel; bound by the per-CU rate
-    // of the LDS-DMA plane stream (the halo re-reads: 3.8x the input bytes), not by the MFMAs
+    // streamed-plane kernel: output-plane chunks of 16 planes, or 8 when 16 leaves CUs idle
     K7Args a = k7m_args(g, P, reflect, 0, wc, 1, k7s::SH, k7s::WB);
     int tdc = g_k7s > 0 ? g_k7s : 16;
     auto blocks = [&](int t) { return (long long)g->n * ((g->do_ + t - 1) / t) * a.tiles_h * a.tiles_w; };
     if (g_k7s == 0 && blocks(16) < 256) tdc = 8;
     a.tiles_d = (g->do_ + tdc - 1) / tdc;
-    const size_t lds = (size_t)k7s::NBUF * k7s::BUF + 4 * 8 * k7s::SH * 16 * sizeof(float);
+    const size_t lds = (size_t)k7s::NBUF * k7s::BUF + 4 * k7s::RING * sizeof(float);
     static bool attr = false;  // > 64 KB of dynamic LDS must be allowed explicitly
     if (!attr) {
       attr = hipFuncSetAttribute((const void*)k7s_w2n_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,

@@ -1,5 +1,6 @@
-"""Time the generator's last conv (16 -> 1 k7 reflect, bf16 shadow input) at 64^3 B=4 alone, under
-k7m debug switches (cgan3d_set_tuning key 11): 1 no MFMA, 2 no ring/flush, 4 no LDS fragment reads."""
+"""Time the generator's last conv (16 -> 1 k7 reflect, bf16 shadow input) at 64^3 B=4 alone: the
+streamed-plane kernel at each output-plane chunk (cgan3d_set_tuning key 13), then the Toeplitz
+k7m_w2n kernel (key 13 = -1)."""
 import sys
 from pathlib import Path
 
@@ -22,8 +23,7 @@ def main():
     lib = L.load()
     for knob in (13,):
         for tdc in (0, 8, 16):
-            for dbg in (0, 1, 2, 4, 7):
-                L.check(lib.cgan3d_set_tuning(11, dbg), "dbg")
+            for dbg in (0,):
                 L.check(lib.cgan3d_set_tuning(knob, tdc), "tdc")
                 ep = ops.epilogue(bias=b, act=L.ACT_TANH, minuend=mn, out2=o2, x_bf16=x16)
                 for _ in range(3):
@@ -36,7 +36,6 @@ def main():
                 e1.record()
                 torch.cuda.synchronize()
                 print(f"tdc {tdc} dbg {dbg}: {e0.elapsed_time(e1) / 20 * 1e3:.1f} us", flush=True)
-    L.check(lib.cgan3d_set_tuning(11, 0), "dbg")
     L.check(lib.cgan3d_set_tuning(13, -1), "off")
     for _ in range(3):
         ops.conv(geo, x, w, y, ops.epilogue(bias=b, act=L.ACT_TANH, minuend=mn, out2=o2, x_bf16=x16))
