@@ -475,32 +475,35 @@ __global__ __launch_bounds__(256, 2) void k7m_w2n_kernel(K7Args a, const float* 
 // columns and W[.][td][r - h - 1][.] in the next 8, so it depends on r - h only and the 32 of them
 // (r - h = 0..7, 4 tw pairs) stay in registers for the whole launch; every A fragment feeds the
 // MFMAs of each output pair it reaches (64 per plane and wave, none off-band).
-// A block = 16 x 16 output columns (h, w) x a chunk of TDc output planes; wave = 4 output rows.
-// It streams the TDc + 6 input planes (22 x 23 staged voxels each: the (h, w) halo re-read is
-// 1.98x, against 2.78x for a 4 x 64 tile) through a ring of 4 LDS buffers filled by LDS-DMA
-// (global_load_lds, 16 bytes per lane, no staging registers) three planes ahead, together with
-// the minuend rows of the output plane each step finishes; lane (g, h, td) adds its P values into
-// a per-wave ring of the 7 output planes still open (eight reads, then eight writes), laid out [h][w %
-// 4][w / 4][plane slot, 9 apart] so neither the adds (td picks the slot) nor the row reads of the
-// flush share a bank, and a plane is finished (bias, tanh, opt_hat) once its last input plane has
-// been added; the flush zeroes the slot for the plane 8 later.  Every store
-// instruction is issued by the whole wave (lanes past the volume write a sink), so the vmcnt wait
-// for a plane counts exactly the DMAs and stores issued after it.
+// A block = 16 x 16 output columns (h, w) x a chunk of TDc output planes, 8 waves: wave = (4
+// output rows, half of K = tw pairs 0-1 or 2-3), two waves per SIMD, so one wave's MFMAs run while
+// the other waits on LDS or issues its DMAs.  The block streams the TDc + 6 input planes (22 x 23
+// staged voxels each: the (h, w) halo re-read is 1.98x, against 2.78x for a 4 x 64 tile) through a
+// ring of 4 LDS buffers filled by LDS-DMA (global_load_lds, 16 bytes per lane, no staging
+// registers) three planes ahead, with the minuend rows of the output plane a step finishes; lane
+// (g, h, td) adds its P values into its wave's ring of the 7 output planes still open (eight LDS
+// reads, then eight writes), laid out [h][w % 4][w / 4][plane slot, 9 apart] so neither the adds
+// (td picks the slot) nor the row reads of the flush share a bank.  Output plane d is finished
+// (both K halves' rings summed, bias, tanh, opt_hat) at the top of step d + 7, after the barrier
+// that follows its last input plane; the flush zeroes the slots for the plane 8 later.  Every
+// store instruction is issued by the whole wave (lanes past the volume write a sink), so the vmcnt
+// wait for a plane counts exactly the DMAs and stores issued after it.
 __device__ u32x4 k7s_zero;    // zero-initialised device global: the source of out-of-volume granules
 __device__ float k7s_sink[64];  // target of the stores of lanes past the volume
 
 namespace k7s {
-constexpr int SH = 16;                   // output rows per block (4 per wave)
+constexpr int NT = 512;                  // threads per block (8 waves)
+constexpr int SH = 16;                   // output rows per block (4 per wave pair)
 constexpr int WB = 16;                   // output columns per block (one M tile)
 constexpr int ROWS = SH + 6, COLS = WB + 7;  // 22 halo columns + one zero column (read by tw = 7)
 constexpr int RB = COLS * 32;            // staged row bytes (16 bf16 channels per voxel)
 constexpr int GRAN = ROWS * COLS * 2;    // 16-byte granules of a plane
-constexpr int GPT = (GRAN + 255) / 256;  // LDS-DMA instructions per wave per plane
-constexpr int MOFF = GPT * 256 * 16;     // minuend granules after the plane (4 waves x 64 lanes;
+constexpr int GPT = (GRAN + NT - 1) / NT;  // LDS-DMA instructions per wave per plane
+constexpr int MOFF = GPT * NT * 16;      // minuend granules after the plane (waves 0-3 x 64 lanes;
 constexpr int BUF = MOFF + 4 * 64 * 16;  // 16 of them used) — bytes per ring buffer
 constexpr int NBUF = 4;                  // planes in flight: 3 ahead of the one computed
-constexpr int PER_STEP = GPT + 1;        // LDS-DMA instructions per wave per step
 constexpr int RING = 4 * 4 * 4 * 9;      // per-wave ring floats: [h][w % 4][w / 4][9]
+constexpr int FL = 7;                    // output plane s - FL is flushed at step s
 }  // namespace k7s
 
 template <int N>
@@ -516,7 +519,7 @@ __device__ __forceinline__ void k7s_wait_vm(int n) {  // s_waitcnt vmcnt(n) for 
   }
 }
 
-__global__ __launch_bounds__(256, 1) void k7s_w2n_kernel(K7Args a, const __bf16* __restrict__ x16,
+__global__ __launch_bounds__(512, 1) void k7s_w2n_kernel(K7Args a, const __bf16* __restrict__ x16,
                                                          const float* __restrict__ w, float* __restrict__ y,
                                                          const float* __restrict__ bias, int act,
                                                          const float* __restrict__ minuend, float* __restrict__ out2,
@@ -525,8 +528,10 @@ __global__ __launch_bounds__(256, 1) void k7s_w2n_kernel(K7Args a, const __bf16*
   extern __shared__ __attribute__((aligned(16))) unsigned char k7s_lds[];
   unsigned char* bufs = k7s_lds;  // [NBUF][BUF]
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int q4 = wave & 3, kh = wave >> 2;  // row quad, K half (the flushing waves are kh == 0)
   const int g = lane >> 4, r16 = lane & 15;
-  float* ring = reinterpret_cast<float*>(k7s_lds + NBUF * BUF) + wave * RING;
+  float* rings = reinterpret_cast<float*>(k7s_lds + NBUF * BUF);
+  float* ring = rings + wave * RING;
   int bid = blockIdx.x;
   const int wt_ = bid % a.tiles_w; bid /= a.tiles_w;
   const int ht_ = bid % a.tiles_h; bid /= a.tiles_h;
@@ -534,13 +539,13 @@ __global__ __launch_bounds__(256, 1) void k7s_w2n_kernel(K7Args a, const __bf16*
   const int n = bid / a.tiles_d;
   const int d0 = dt_ * tdc, h0 = ht_ * SH, w0 = wt_ * WB;
   // weights: B fragment (t0 = r - h, j) of lane (g, col = r16): column col = 8 hsel + td holds
-  // W[c0 .. c0 + 7][td][t0 - hsel][tw], tw = 2j + (g >> 1), c0 = 8 (g & 1); zero off the band.
-  // Staged once as bf16 [tap][16 channels] in the last ring buffer (first filled after the loop's
-  // first barrier): coalesced global reads, then one ds_read_b128 per fragment.
-  bf16x8_k bw[8][4];
+  // W[c0 .. c0 + 7][td][t0 - hsel][tw], tw = 2 (2 kh + j) + (g >> 1), c0 = 8 (g & 1); zero off the
+  // band.  Staged once as bf16 [tap][16 channels] in the last ring buffer (first filled after the
+  // loop's first barrier): coalesced global reads, then one ds_read_b128 per fragment.
+  bf16x8_k bw[8][2];
   {
     __bf16* wl = reinterpret_cast<__bf16*>(bufs + (NBUF - 1) * BUF);
-    for (int i = tid; i < 16 * KT7; i += 256) {
+    for (int i = tid; i < 16 * KT7; i += NT) {
       const int c = i / KT7, t = i - c * KT7;
       wl[t * 16 + c] = (__bf16)w[(long long)c * a.wc + t];
     }
@@ -549,8 +554,8 @@ __global__ __launch_bounds__(256, 1) void k7s_w2n_kernel(K7Args a, const __bf16*
 #pragma unroll
     for (int t0 = 0; t0 < 8; ++t0)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int th = t0 - hsel, tw = 2 * j + (g >> 1);
+      for (int j = 0; j < 2; ++j) {
+        const int th = t0 - hsel, tw = 2 * (2 * kh + j) + (g >> 1);
         const bool ok = td < 7 && th >= 0 && th < 7 && tw < 7;
         const bf16x8_k v = *reinterpret_cast<const bf16x8_k*>(wl + (ok ? (td * 7 + th) * 7 + tw : 0) * 16 + c0);
         bw[t0][j] = ok ? v : bf16x8_k{};
@@ -558,13 +563,13 @@ __global__ __launch_bounds__(256, 1) void k7s_w2n_kernel(K7Args a, const __bf16*
     for (int i = lane; i < RING; i += 64) ring[i] = 0.f;  // slots are added into, zeroed again by the flush
   }
   // this lane's plane granules (lane-linear LDS image: granule i of the plane at byte 16 i, i = k *
-  // 256 + wave * 64 + lane): the (h, w) part of the source offset, -1 = zero (past a partial tile,
+  // NT + wave * 64 + lane): the (h, w) part of the source offset, -1 = zero (past a partial tile,
   // the tw = 7 pad column, or past the plane's granules).  Reflect padding (the launcher's
   // condition): every plane index is in range.
   int hw[GPT];
 #pragma unroll
   for (int k = 0; k < GPT; ++k) {
-    const int i = k * 256 + wave * 64 + lane;
+    const int i = k * NT + wave * 64 + lane;
     const int q = i & 1, u = (i >> 1) % COLS, r = (i >> 1) / COLS;
     const int ih = k7_src(h0 - a.P + r, a.hi, 1);
     const int iw = u < WB + 6 ? k7_src(w0 - a.P + u, a.wi, 1) : -1;
@@ -573,8 +578,9 @@ __global__ __launch_bounds__(256, 1) void k7s_w2n_kernel(K7Args a, const __bf16*
   const int nplanes = tdc + 6;
   const u32x4* xg = reinterpret_cast<const u32x4*>(x16);
   const float* mbase = out2 ? minuend : y;  // any valid address when there is no minuend
-  // plane s (and the minuend rows of output plane s - 6) into buffer s % NBUF; always PER_STEP
-  // instructions per wave (dummy sources past the chunk) so the vmcnt waits below are exact
+  // plane s into buffer s % NBUF (GPT instructions per wave, dummy sources past the chunk) and, by
+  // the flushing waves, the minuend rows of output plane s - FL (one more): the vmcnt waits below
+  // count them exactly
   auto issue = [&](int s) {
     const int sp = s < nplanes ? s : nplanes - 1;
     const int id = k7_src(d0 - a.P + sp, a.di, 1);
@@ -583,40 +589,64 @@ __global__ __launch_bounds__(256, 1) void k7s_w2n_kernel(K7Args a, const __bf16*
 #pragma unroll
     for (int k = 0; k < GPT; ++k)
       __builtin_amdgcn_global_load_lds((const void*)(hw[k] >= 0 ? src + hw[k] : &k7s_zero),
-                                       (__attribute__((address_space(3))) void*)(dst + (k * 256 + wave * 64) * 16),
+                                       (__attribute__((address_space(3))) void*)(dst + (k * NT + wave * 64) * 16),
                                        16, 0, 0);
-    // minuend granule lane (16 per wave: row 4 wave + lane / 4, 4 floats); W % 4 == 0 (launcher)
-    const int df = s - 6, od = d0 + df, oh = h0 + 4 * wave + (lane >> 2), ow = w0 + 4 * (lane & 3);
-    const bool mok = lane < 16 && out2 && df >= 0 && df < tdc && od < a.do_ && oh < a.ho && ow < a.wo;
-    const float* ms = mok ? mbase + (((long long)n * a.do_ + od) * a.ho + oh) * a.wo + ow
-                          : reinterpret_cast<const float*>(&k7s_zero);
-    __builtin_amdgcn_global_load_lds((const void*)ms,
-                                     (__attribute__((address_space(3))) void*)(dst + MOFF + wave * 64 * 16), 16, 0, 0);
+    if (kh == 0) {  // minuend granule lane (16 per wave: row 4 q4 + lane / 4, 4 floats); W % 4 == 0 (launcher)
+      const int df = s - FL, od = d0 + df, oh = h0 + 4 * q4 + (lane >> 2), ow = w0 + 4 * (lane & 3);
+      const bool mok = lane < 16 && out2 && df >= 0 && df < tdc && od < a.do_ && oh < a.ho && ow < a.wo;
+      const float* ms = mok ? mbase + (((long long)n * a.do_ + od) * a.ho + oh) * a.wo + ow
+                            : reinterpret_cast<const float*>(&k7s_zero);
+      __builtin_amdgcn_global_load_lds((const void*)ms,
+                                       (__attribute__((address_space(3))) void*)(dst + MOFF + q4 * 64 * 16), 16, 0, 0);
+    }
   };
-  const int nst = out2 ? 2 : 1;  // store instructions per wave of a step that finishes a plane
-  auto stores_at = [&](int k) { return (k >= 6 && k - 6 < tdc) ? nst : 0; };
+  const int nst = out2 ? 2 : 1;  // store instructions of a flushing wave at a step that finishes a plane
+  auto stores_at = [&](int k) { return (k >= FL && k - FL < tdc) ? nst : 0; };
   const float b0 = bias ? bias[0] : 0.f;
   const int td = r16 & 7, hsel = r16 >> 3;
   for (int s = 0; s < NBUF - 1; ++s) issue(s);
-  for (int s = 0; s < nplanes; ++s) {
-    // plane s and its minuend rows are in: everything issued after them may still be in flight
-    // (the two later DMA batches and the stores of the three steps since; in order), then a
-    // barrier so every wave's DMA is visible to every wave and every wave has finished reading the
-    // buffer refilled next
-    k7s_wait_vm<PER_STEP * (NBUF - 2)>(PER_STEP * (NBUF - 2) + stores_at(s - 3) + stores_at(s - 2) + stores_at(s - 1));
+  for (int s = 0; s <= nplanes; ++s) {
+    // plane s (and the minuend rows it carries) are in: everything issued after them may still be
+    // in flight (the two later DMA batches and the stores of the three steps since; in order), then
+    // a barrier so every wave's DMA and ring adds are visible to every wave and every wave has
+    // finished reading the buffer refilled next
+    if (kh == 0)
+      k7s_wait_vm<(GPT + 1) * (NBUF - 2)>((GPT + 1) * (NBUF - 2) + stores_at(s - 3) + stores_at(s - 2) + stores_at(s - 1));
+    else
+      k7s_wait_vm<GPT * (NBUF - 2)>(GPT * (NBUF - 2));
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
-    issue(s + NBUF - 1);  // NBUF - 1 planes ahead, into the buffer of plane s - 1 (dummies past the chunk)
-    const unsigned char* pb = bufs + (s % NBUF) * BUF + 4 * wave * RB + r16 * 32 + 16 * (g & 1);
+    if (s < nplanes) issue(s + NBUF - 1);  // NBUF - 1 planes ahead, into the buffer of plane s - 1
+    const int df = s - FL;  // output plane whose last input plane (s - 1) both K halves have added
+    if (kh == 0 && df >= 0 && df < tdc) {
+      const int fh = lane >> 4, fw = lane & 15;
+      const int od = d0 + df, oh = h0 + 4 * q4 + fh, ow = w0 + fw;
+      const int si = ((fh * 4 + (fw & 3)) * 4 + (fw >> 2)) * 9 + (df & 7);
+      float* s0 = ring + si;
+      float* s1 = rings + (wave + 4) * RING + si;
+      float v = *s0 + *s1 + b0;
+      *s0 = 0.f;
+      *s1 = 0.f;
+      if (act == CGAN3D_ACT_TANH) v = tanhf(v);
+      const bool ok = od < a.do_ && oh < a.ho && ow < a.wo;
+      const long long o = (((long long)n * a.do_ + od) * a.ho + oh) * a.wo + ow;
+      *(ok ? y + o : k7s_sink + lane) = v;
+      if (out2) {
+        const float* mrow = reinterpret_cast<const float*>(bufs + (s % NBUF) * BUF + MOFF + q4 * 64 * 16);
+        *(ok ? out2 + o : k7s_sink + lane) = mrow[fh * 16 + fw] - v;
+      }
+    }
+    if (s == nplanes) break;
+    const unsigned char* pb = bufs + (s % NBUF) * BUF + 4 * q4 * RB + r16 * 32 + 16 * (g & 1) + 2 * kh * 64;
     f32x4 acc[2];
 #pragma unroll
     for (int hp = 0; hp < 2; ++hp) acc[hp] = f32x4{0.f, 0.f, 0.f, 0.f};
-    // row r + 1's four A fragments are read while row r's MFMAs run
-    bf16x8_k av[2][4];
-    auto fetch = [&](int r, bf16x8_k (&o)[4]) {
+    // row r + 1's two A fragments are read while row r's MFMAs run
+    bf16x8_k av[2][2];
+    auto fetch = [&](int r, bf16x8_k (&o)[2]) {
 #pragma unroll
-      for (int j = 0; j < 4; ++j) o[j] = *reinterpret_cast<const bf16x8_k*>(pb + r * RB + (2 * j + (g >> 1)) * 32);
+      for (int j = 0; j < 2; ++j) o[j] = *reinterpret_cast<const bf16x8_k*>(pb + r * RB + (2 * j + (g >> 1)) * 32);
     };
     fetch(0, av[0]);
 #pragma unroll
@@ -624,7 +654,7 @@ __global__ __launch_bounds__(256, 1) void k7s_w2n_kernel(K7Args a, const __bf16*
       if (r + 1 < 10) fetch(r + 1, av[(r + 1) & 1]);
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-      for (int j = 0; j < 4; ++j)
+      for (int j = 0; j < 2; ++j)
 #pragma unroll
         for (int hp = 0; hp < 2; ++hp) {
           const int t0 = r - 2 * hp;
@@ -633,8 +663,8 @@ __global__ __launch_bounds__(256, 1) void k7s_w2n_kernel(K7Args a, const __bf16*
         }
       __builtin_amdgcn_sched_barrier(0);
     }
-    // lane (g, hsel, td) holds P[s][h = 2 hp + hsel][w = 4g + jj][td]: output plane dl = s - td
-    // (every read of the eight slots issued before the first write: one LDS round trip per step)
+    // lane (g, hsel, td) holds this K half of P[s][h = 2 hp + hsel][w = 4g + jj][td]: output plane
+    // dl = s - td (every read of the eight slots issued before the first write)
     const int dl = s - td;
     if (td < 7 && dl >= 0 && dl < tdc) {
       float* rb = ring + (hsel * 16 + g) * 9 + (dl & 7);
@@ -647,22 +677,6 @@ __global__ __launch_bounds__(256, 1) void k7s_w2n_kernel(K7Args a, const __bf16*
       for (int hp = 0; hp < 2; ++hp)
 #pragma unroll
         for (int jj = 0; jj < 4; ++jj) rb[(hp * 32 + jj * 4) * 9] = v[hp][jj] + acc[hp][jj];
-    }
-    const int df = s - 6;  // output plane complete after this input plane
-    if (df >= 0 && df < tdc) {
-      const int fh = lane >> 4, fw = lane & 15;
-      const int od = d0 + df, oh = h0 + 4 * wave + fh, ow = w0 + fw;
-      float* slot = ring + ((fh * 4 + (fw & 3)) * 4 + (fw >> 2)) * 9 + (df & 7);
-      float v = *slot + b0;
-      *slot = 0.f;
-      if (act == CGAN3D_ACT_TANH) v = tanhf(v);
-      const bool ok = od < a.do_ && oh < a.ho && ow < a.wo;
-      const long long o = (((long long)n * a.do_ + od) * a.ho + oh) * a.wo + ow;
-      *(ok ? y + o : k7s_sink + lane) = v;
-      if (out2) {
-        const float* mrow = reinterpret_cast<const float*>(bufs + (s % NBUF) * BUF + MOFF + wave * 64 * 16);
-        *(ok ? out2 + o : k7s_sink + lane) = mrow[fh * 16 + fw] - v;
-      }
     }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the trailing dummy DMAs land before the block exits
@@ -948,13 +962,13 @@ void k7m_w2n_launch(const cgan3d_conv_geom* g, int P, int reflect, long long wc,
     auto blocks = [&](int t) { return (long long)g->n * ((g->do_ + t - 1) / t) * a.tiles_h * a.tiles_w; };
     if (g_k7s == 0 && blocks(16) < 256) tdc = 8;
     a.tiles_d = (g->do_ + tdc - 1) / tdc;
-    const size_t lds = (size_t)k7s::NBUF * k7s::BUF + 4 * k7s::RING * sizeof(float);
+    const size_t lds = (size_t)k7s::NBUF * k7s::BUF + 8 * k7s::RING * sizeof(float);
     static bool attr = false;  // > 64 KB of dynamic LDS must be allowed explicitly
     if (!attr) {
       attr = hipFuncSetAttribute((const void*)k7s_w2n_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                                  (int)lds) == hipSuccess;
     }
-    ::cg::launch(k7s_w2n_kernel, dim3((unsigned)blocks(tdc)), dim3(256), lds, s, a, e.x16, w, y, e.bias, e.act,
+    ::cg::launch(k7s_w2n_kernel, dim3((unsigned)blocks(tdc)), dim3(k7s::NT), lds, s, a, e.x16, w, y, e.bias, e.act,
                  e.minuend, e.out2, tdc);
     return;
   }
