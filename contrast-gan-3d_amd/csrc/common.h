@@ -228,7 +228,6 @@ int s2_kind(const cgan3d_conv_geom* g);
 long long s2_blocks(const cgan3d_conv_geom* g);
 int s2_launch(const cgan3d_conv_geom* g, const float* x, const __bf16* wp, float* y, const Epi& e, hipStream_t st);
 void s2_set(int v);
-void s2_set_dbg(int v);
 int halo_pack(const cgan3d_conv_geom* g, const float* w, void* wp, hipStream_t st);
 int gemm_launch(const cgan3d_conv_geom* g, const float* x, const float* w, float* y, const Epi& e, hipStream_t st);
 // Adam over a flat arena (+ optional repack of packed weight copies, step tick) — conv_gemm.hip

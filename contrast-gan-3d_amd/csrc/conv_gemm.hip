@@ -655,7 +655,6 @@ extern "C" int cgan3d_set_tuning(int32_t key, int32_t value) {
   if (key == 2) { halo_set_min_blocks(value); return CGAN3D_OK; }
   if (key == 3) { k3_tile_set(value); return CGAN3D_OK; }
   if (key == 4) { s2_set(value); return CGAN3D_OK; }
-  if (key == 5) { s2_set_dbg(value); return CGAN3D_OK; }
   if (key == 8) { halo_set_dbg(value); return CGAN3D_OK; }
   if (key == 9) { wgrad_k3_set_chunks(value); return CGAN3D_OK; }
   if (key == 10) { wgrad_s2_set_blocks(value); return CGAN3D_OK; }

@@ -19,6 +19,9 @@
 //    v_mfma_f32_16x16x32_bf16 covers two taps (16 channels each; g>>1 selects the tap).
 //  * S2T: an M tile is 16 consecutive class voxels along x; rows [z][y][17 x][32 ch], 64-byte
 //    voxels with granule g stored at g ^ ((x >> 1) & 2).
+// Both run the MFMA transposed (A = the weight fragments, B = the staged activations), so a lane
+// ends up with 4 consecutive output channels of one voxel: one 16-byte store (and, for the
+// input-grad statistics, one 16-byte z load) per voxel and lane instead of four 4-byte ones.
 #include "common.h"
 
 namespace cg {
@@ -30,31 +33,35 @@ struct S2Args {
   int n, di, hi, wi, do_, ho, wo;
   int cd, ch, cw;  // output grid (S2F) or class grid (S2T)
   int td, th, tw;  // tiles per dim
-  int dbg;         // phase switches for timing experiments (cgan3d_set_tuning key 5): 1 no halo
-                   // loads, 2 no MFMA, 4 no output stores, 8 no weight loads
 };
 
-// per-channel sum over the block: v[nt] (this lane's partial for channel nt*16 + r16) summed over
-// the four row groups and the four waves; every lane receives its channels' block totals
+// per-channel sum over the block in the transposed MFMA layout: v[nt][j] is this lane's partial
+// for channel nt*16 + 4g + j (over its voxel column r16), summed over the 16 voxel lanes and the
+// four waves; every lane receives its channels' block totals
 template <int NT>
-__device__ __forceinline__ void block_chan_sum(float (&v)[NT], float* red) {
+__device__ __forceinline__ void block_chan_sum(float (&v)[NT][4], float* red) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4, r16 = lane & 15;
 #pragma unroll
-  for (int nt = 0; nt < NT; ++nt) {
-    v[nt] += __shfl_xor(v[nt], 16, 64);
-    v[nt] += __shfl_xor(v[nt], 32, 64);
-  }
-  __syncthreads();  // red is free
-  if (g == 0) {
+  for (int nt = 0; nt < NT; ++nt)
 #pragma unroll
-    for (int nt = 0; nt < NT; ++nt) red[wave * NT * 16 + nt * 16 + r16] = v[nt];
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int m = 1; m < 16; m <<= 1) v[nt][j] += __shfl_xor(v[nt][j], m, 64);
+  __syncthreads();  // red is free
+  if (r16 == 0) {
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) red[wave * NT * 16 + nt * 16 + 4 * g + j] = v[nt][j];
   }
   __syncthreads();
 #pragma unroll
-  for (int nt = 0; nt < NT; ++nt) {
-    const int c = nt * 16 + r16;
-    v[nt] = red[c] + red[NT * 16 + c] + red[2 * NT * 16 + c] + red[3 * NT * 16 + c];
-  }
+  for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int c = nt * 16 + 4 * g + j;
+      v[nt][j] = red[c] + red[NT * 16 + c] + red[2 * NT * 16 + c] + red[3 * NT * 16 + c];
+    }
 }
 
 __device__ __forceinline__ float s2_act(float v, const Epi& ep) {
@@ -64,87 +71,106 @@ __device__ __forceinline__ float s2_act(float v, const Epi& ep) {
 }
 
 // Block statistics of the fused BatchNorm slab (include/cgan3d.h): mode 1 (sum, M2 about the block
-// mean, count), mode 2 (sum g, sum g*xhat).  vals / zv: [U][NT][4] per lane, ok: [U][4] row validity.
+// mean, count), mode 2 (sum g, sum g*xhat).  vals / zv: [U][NT] per lane = channels nt*16 + 4g +
+// 0..3 of the lane's voxel in output group u; ok[u]: that voxel is inside the volume.
 // fused-statistics mode of an epilogue: 1 / 2 (slab or, cgan3d_bn_fuse acc_mode 3 / 4, fp64 accumulators)
 __device__ __forceinline__ int s2_stat_mode(const Epi& ep) {
   return ep.fz.acc_mode == 3 ? 1 : ep.fz.acc_mode == 4 ? 2 : ep.bn_mode;
 }
+static int s2_host_stat_mode(const Epi& ep) { return ep.fz.acc_mode == 3 ? 1 : ep.fz.acc_mode == 4 ? 2 : ep.bn_mode; }
 
 template <int U, int NT>
-__device__ __forceinline__ void s2_bn_slab(const Epi& ep, int C, const float (&vals)[U][NT][4], const float (&zv)[U][NT][4],
-                                           const bool (&ok)[U][4], int cnt, float* red) {
-  const int tid = threadIdx.x, r16 = tid & 15;
+__device__ __forceinline__ void s2_bn_slab(const Epi& ep, int C, const f32x4 (&vals)[U][NT], const f32x4 (&zv)[U][NT],
+                                           const bool (&ok)[U], int cnt, float* red) {
+  const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4;
   const int mode = s2_stat_mode(ep);
+  // after the block sums, lanes 0, 16, 32, 48 of wave 0 hold channels nt*16 + 4g + j
+  const bool writer = tid < 64 && (lane & 15) == 0;
   // this block's replica of the accumulators (cgan3d_bn_fuse), or null: the slab
   double* const acc = ep.fz.acc_mode ? ep.fz.acc_out + (long long)(blockIdx.x % ep.fz.reps) * 2 * C : nullptr;
+  float s[NT][4], q[NT][4];
   if (mode == 1) {
-    float s[NT];
 #pragma unroll
-    for (int nt = 0; nt < NT; ++nt) {
-      s[nt] = 0.f;
+    for (int nt = 0; nt < NT; ++nt)
 #pragma unroll
-      for (int u = 0; u < U; ++u)
+      for (int j = 0; j < 4; ++j) {
+        s[nt][j] = 0.f;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) s[nt] += ok[u][j] ? vals[u][nt][j] : 0.f;
-    }
+        for (int u = 0; u < U; ++u) s[nt][j] += ok[u] ? vals[u][nt][j] : 0.f;
+      }
     block_chan_sum<NT>(s, red);
-    float q[NT];
 #pragma unroll
-    for (int nt = 0; nt < NT; ++nt) {
-      const float m = cnt ? s[nt] / cnt : 0.f;
-      q[nt] = 0.f;
+    for (int nt = 0; nt < NT; ++nt)
 #pragma unroll
-      for (int u = 0; u < U; ++u)
+      for (int j = 0; j < 4; ++j) {
+        const float m = cnt ? s[nt][j] / cnt : 0.f;
+        q[nt][j] = 0.f;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const float d = ok[u][j] ? vals[u][nt][j] - m : 0.f;
-          q[nt] += d * d;
-        }
-    }
-    block_chan_sum<NT>(q, red);
-    if (tid < 16) {
-#pragma unroll
-      for (int nt = 0; nt < NT; ++nt) {
-        if (acc) {  // (sum, sum of squares = M2 + S * mean)
-          if (cnt) {
-            unsafeAtomicAdd(acc + nt * 16 + r16, (double)s[nt]);
-            unsafeAtomicAdd(acc + C + nt * 16 + r16, (double)q[nt] + (double)s[nt] * (double)s[nt] / cnt);
-          }
-        } else {
-          *bn_slot(ep, 0, C, nt * 16 + r16, blockIdx.x) = s[nt];
-          *bn_slot(ep, 1, C, nt * 16 + r16, blockIdx.x) = q[nt];
+        for (int u = 0; u < U; ++u) {
+          const float d = ok[u] ? vals[u][nt][j] - m : 0.f;
+          q[nt][j] += d * d;
         }
       }
+    block_chan_sum<NT>(q, red);
+    if (writer) {
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int c = nt * 16 + 4 * g + j;
+          if (acc) {  // (sum, sum of squares = M2 + S * mean)
+            if (cnt) {
+              unsafeAtomicAdd(acc + c, (double)s[nt][j]);
+              unsafeAtomicAdd(acc + C + c, (double)q[nt][j] + (double)s[nt][j] * (double)s[nt][j] / cnt);
+            }
+          } else {
+            *bn_slot(ep, 0, C, c, blockIdx.x) = s[nt][j];
+            *bn_slot(ep, 1, C, c, blockIdx.x) = q[nt][j];
+          }
+        }
       if (tid == 0 && !acc) *bn_slot(ep, 2, C, 0, blockIdx.x) = (float)cnt;
     }
   } else if (mode == 2) {
-    float p1[NT], p2[NT];
 #pragma unroll
-    for (int nt = 0; nt < NT; ++nt) {
-      p1[nt] = 0.f;
-      p2[nt] = 0.f;
-      const int c = nt * 16 + r16;
+    for (int nt = 0; nt < NT; ++nt)
 #pragma unroll
-      for (int u = 0; u < U; ++u)
+      for (int j = 0; j < 4; ++j) {
+        const int c = nt * 16 + 4 * g + j;  // this lane's channel: its BatchNorm coefficients once
+        const float sc = ep.bn_ss[c], sh = ep.bn_ss[C + c], mu = ep.bn_mi[c], inv = ep.bn_mi[C + c];
+        s[nt][j] = 0.f;
+        q[nt][j] = 0.f;
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
-          if (ok[u][j]) bn_pair_z(ep, vals[u][nt][j], zv[u][nt][j], c, C, &p1[nt], &p2[nt]);
-    }
-    block_chan_sum<NT>(p1, red);
-    block_chan_sum<NT>(p2, red);
-    if (tid < 16) {
-#pragma unroll
-      for (int nt = 0; nt < NT; ++nt) {
-        if (acc) {
-          unsafeAtomicAdd(acc + nt * 16 + r16, (double)p1[nt]);
-          unsafeAtomicAdd(acc + C + nt * 16 + r16, (double)p2[nt]);
-        } else {
-          *bn_slot(ep, 0, C, nt * 16 + r16, blockIdx.x) = p1[nt];
-          *bn_slot(ep, 1, C, nt * 16 + r16, blockIdx.x) = p2[nt];
+        for (int u = 0; u < U; ++u) {
+          const float z = zv[u][nt][j];
+          const float gg = ok[u] ? vals[u][nt][j] * act_grad(z * sc + sh, ep.bn_act, ep.bn_slope) : 0.f;
+          s[nt][j] += gg;
+          q[nt][j] += gg * (z - mu) * inv;
         }
       }
+    block_chan_sum<NT>(s, red);
+    block_chan_sum<NT>(q, red);
+    if (writer) {
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int c = nt * 16 + 4 * g + j;
+          if (acc) {
+            unsafeAtomicAdd(acc + c, (double)s[nt][j]);
+            unsafeAtomicAdd(acc + C + c, (double)q[nt][j]);
+          } else {
+            *bn_slot(ep, 0, C, c, blockIdx.x) = s[nt][j];
+            *bn_slot(ep, 1, C, c, blockIdx.x) = q[nt][j];
+          }
+        }
     }
   }
+}
+
+__device__ __forceinline__ f32x4 s2_act4(f32x4 v, const Epi& ep) {
+#pragma unroll
+  for (int j = 0; j < 4; ++j) v[j] = s2_act(v[j], ep);
+  return v;
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -153,6 +179,7 @@ __device__ __forceinline__ void s2_bn_slab(const Epi& ep, int C, const float (&v
 constexpr int F_HX = 33, F_HY = 9, F_HZ = 5, F_SX = 17;
 constexpr int F_HALO = F_HZ * F_HY * 2 * F_SX * 16;  // bf16 elements (48960 bytes)
 
+template <int MODE>  // statistics mode s2_stat_mode(ep): 0 none, 1 forward, 2 input-grad
 __global__ __launch_bounds__(256) void conv_s2f_kernel(S2Args a, const float* __restrict__ x,
                                                        const __bf16* __restrict__ wpk, float* y, Epi ep) {
   constexpr int CI = 16, CO = 32, KSTEPS = 14;
@@ -175,7 +202,7 @@ __global__ __launch_bounds__(256) void conv_s2f_kernel(S2Args a, const float* __
     for (int nt = 0; nt < 2; ++nt) {
       const int co = nt * 16 + r16;
       const int tt = t < 27 ? t : 26;
-      bq[s][nt] = (a.dbg & 8) ? bf16x8_s{} : *reinterpret_cast<const bf16x8_s*>(wpk + ((long long)tt * CO + co) * CI + 8 * ((g & 1) ^ (co & 1)));
+      bq[s][nt] = *reinterpret_cast<const bf16x8_s*>(wpk + ((long long)tt * CO + co) * CI + 8 * ((g & 1) ^ (co & 1)));
       if (t >= 27) bq[s][nt] = bf16x8_s{};
     }
   }
@@ -193,7 +220,7 @@ __global__ __launch_bounds__(256) void conv_s2f_kernel(S2Args a, const float* __
       const int hx = v % F_HX, r = v / F_HX;
       const int hy = r % F_HY, hz = r / F_HY;
       const int iz = iz0 + hz, iy = iy0 + hy, ix = ix0 + hx;
-      const bool ok = !(a.dbg & 1) && i < NG && (unsigned)iz < (unsigned)a.di && (unsigned)iy < (unsigned)a.hi &&
+      const bool ok = i < NG && (unsigned)iz < (unsigned)a.di && (unsigned)iy < (unsigned)a.hi &&
                       (unsigned)ix < (unsigned)a.wi;
       sb[k] = xq[ok ? ((((long long)nb * a.di + iz) * a.hi + iy) * a.wi + ix) * 2 + q : 0];
       if (!ok) sb[k] = bf16x8_s{};
@@ -220,7 +247,7 @@ __global__ __launch_bounds__(256) void conv_s2f_kernel(S2Args a, const float* __
         const int hx = v % F_HX, r = v / F_HX;
         const int hy = r % F_HY, hz = r / F_HY;
         const int iz = iz0 + hz, iy = iy0 + hy, ix = ix0 + hx;
-        const bool ok = !(a.dbg & 1) && k0 + k < PER && i < NV4 && (unsigned)iz < (unsigned)a.di && (unsigned)iy < (unsigned)a.hi &&
+        const bool ok = k0 + k < PER && i < NV4 && (unsigned)iz < (unsigned)a.di && (unsigned)iy < (unsigned)a.hi &&
                         (unsigned)ix < (unsigned)a.wi;
         sv[k] = *reinterpret_cast<const f32x4*>(
             x + (ok ? ((((long long)nb * a.di + iz) * a.hi + iy) * a.wi + ix) * CI + 4 * c4 : 0));
@@ -241,12 +268,31 @@ __global__ __launch_bounds__(256) void conv_s2f_kernel(S2Args a, const float* __
   }
   __syncthreads();
 
+  // mode-2 statistics: this lane's z values (its voxel, channels nt*16 + 4g .. +3) in flight during
+  // the MFMAs
+  constexpr int mode = MODE;
+  const int oy = Y0 + wave, ox = X0 + r16;
+  long long obase[2];
+  bool ok[2];
+#pragma unroll
+  for (int zz = 0; zz < 2; ++zz) {
+    const int oz = Z0 + zz;
+    ok[zz] = oz < a.cd && oy < a.ch && ox < a.cw;
+    obase[zz] = ok[zz] ? ((((long long)nb * a.cd + oz) * a.ch + oy) * a.cw + ox) * CO + 4 * g : 0;
+  }
+  f32x4 zv[2][2];
+#pragma unroll
+  for (int zz = 0; zz < 2; ++zz)
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt)
+      zv[zz][nt] = mode == 2 ? *reinterpret_cast<const f32x4*>(ep.bn_z + obase[zz] + nt * 16) : f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // D[channel][voxel]: A = weights (lane channel r16), B = activations (lane voxel r16)
   f32x4 acc[2][2];
 #pragma unroll
   for (int zz = 0; zz < 2; ++zz)
 #pragma unroll
     for (int nt = 0; nt < 2; ++nt) acc[zz][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
-  if (!(a.dbg & 2))
 #pragma unroll
   for (int s = 0; s < KSTEPS; ++s) {
     int t = 2 * s + (g >> 1);
@@ -259,34 +305,24 @@ __global__ __launch_bounds__(256) void conv_s2f_kernel(S2Args a, const float* __
           *reinterpret_cast<const bf16x8_s*>(halo + (row * F_SX + r16 + (tw >> 1)) * CI + 8 * (g & 1));
 #pragma unroll
       for (int nt = 0; nt < 2; ++nt)
-        acc[zz][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, bq[s][nt], acc[zz][nt], 0, 0, 0);
+        acc[zz][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bq[s][nt], av, acc[zz][nt], 0, 0, 0);
     }
   }
 
-  // ---- epilogue: lane holds outputs x = X0 + 4g + j, y = Y0 + wave, z = Z0 + zz, channel nt*16 + r16
-  float vals[2][2][4], zv[2][2][4];
-  bool ok[2][4];
-  const int oy = Y0 + wave;
+  // ---- epilogue: lane holds output (x = X0 + r16, y = Y0 + wave, z = Z0 + zz), channels nt*16 + 4g .. +3
+  f32x4 vals[2][2];
 #pragma unroll
-  for (int zz = 0; zz < 2; ++zz) {
-    const int oz = Z0 + zz;
+  for (int nt = 0; nt < 2; ++nt) {
+    const int c = nt * 16 + 4 * g;
+    const f32x4 b4 = ep.bias ? f32x4{ep.bias[c], ep.bias[c + 1], ep.bias[c + 2], ep.bias[c + 3]} : f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int ox = X0 + 4 * g + j;
-      ok[zz][j] = oz < a.cd && oy < a.ch && ox < a.cw;
-      const long long o = ok[zz][j] ? (((long long)nb * a.cd + oz) * a.ch + oy) * a.cw + ox : 0;
-#pragma unroll
-      for (int nt = 0; nt < 2; ++nt) {
-        const int c = nt * 16 + r16;
-        zv[zz][nt][j] = s2_stat_mode(ep) == 2 ? ep.bn_z[o * CO + c] : 0.f;
-        float v = acc[zz][nt][j] + (ep.bias ? ep.bias[c] : 0.f);
-        v = s2_act(v, ep);
-        if (ok[zz][j] && (!(a.dbg & 4) || v == 1.2345f)) y[o * CO + c] = v;
-        vals[zz][nt][j] = v;
-      }
+    for (int zz = 0; zz < 2; ++zz) {
+      const f32x4 v = s2_act4(acc[zz][nt] + b4, ep);
+      if (ok[zz]) *reinterpret_cast<f32x4*>(y + obase[zz] + nt * 16) = v;
+      vals[zz][nt] = v;
     }
   }
-  if (s2_stat_mode(ep)) {
+  if constexpr (mode != 0) {
     const int cnt = max(0, min(2, a.cd - Z0)) * max(0, min(4, a.ch - Y0)) * max(0, min(16, a.cw - X0));
     s2_bn_slab<2, 2>(ep, CO, vals, zv, ok, cnt, red);
   }
@@ -334,11 +370,12 @@ __device__ __forceinline__ void s2t_class(const __bf16* halo, const bf16x8_s (&b
           const int row = (zz + TZ::off[a]) * T_HY + wave + TY::off[b];
           const bf16x8_s av =
               *reinterpret_cast<const bf16x8_s*>(halo + (row * T_HX + hx) * 32 + 8 * (g ^ ((hx >> 1) & 2)));
-          acc[zz] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, bq[t], acc[zz], 0, 0, 0);
+          acc[zz] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bq[t], av, acc[zz], 0, 0, 0);
         }
       }
 }
 
+template <int MODE>  // statistics mode s2_stat_mode(ep): 0 none, 1 forward, 2 input-grad
 __global__ __launch_bounds__(256) void conv_s2t_kernel(S2Args a, const float* __restrict__ x,
                                                        const __bf16* __restrict__ wpk, float* y, Epi ep) {
   constexpr int CI = 32, CO = 16;
@@ -355,7 +392,7 @@ __global__ __launch_bounds__(256) void conv_s2t_kernel(S2Args a, const float* __
   bf16x8_s bq[27];  // lane (channel r16, granule g) of every tap
 #pragma unroll
   for (int t = 0; t < 27; ++t)
-    bq[t] = (a.dbg & 8) ? bf16x8_s{} : *reinterpret_cast<const bf16x8_s*>(wpk + ((long long)t * CO + r16) * CI + 8 * (g ^ (r16 & 3)));
+    bq[t] = *reinterpret_cast<const bf16x8_s*>(wpk + ((long long)t * CO + r16) * CI + 8 * (g ^ (r16 & 3)));
 
   if (ep.x16) {  // the same halo from the bf16 shadow of the input, 16-byte granules as they are
     constexpr int NG = T_HZ * T_HY * T_HX * 4, PG = (NG + 255) / 256;
@@ -368,7 +405,7 @@ __global__ __launch_bounds__(256) void conv_s2t_kernel(S2Args a, const float* __
       const int hx = v % T_HX, r = v / T_HX;
       const int hy = r % T_HY, hz = r / T_HY;
       const int iz = Z0 + hz, iy = Y0 + hy, ix = X0 + hx;
-      const bool ok = !(a.dbg & 1) && i < NG && iz < a.di && iy < a.hi && ix < a.wi;
+      const bool ok = i < NG && iz < a.di && iy < a.hi && ix < a.wi;
       sb[k] = xq[ok ? ((((long long)nb * a.di + iz) * a.hi + iy) * a.wi + ix) * 4 + q : 0];
       if (!ok) sb[k] = bf16x8_s{};
     }
@@ -390,7 +427,7 @@ __global__ __launch_bounds__(256) void conv_s2t_kernel(S2Args a, const float* __
       const int hx = v % T_HX, r = v / T_HX;
       const int hy = r % T_HY, hz = r / T_HY;
       const int iz = Z0 + hz, iy = Y0 + hy, ix = X0 + hx;
-      const bool ok = !(a.dbg & 1) && i < NV4 && iz < a.di && iy < a.hi && ix < a.wi;
+      const bool ok = i < NV4 && iz < a.di && iy < a.hi && ix < a.wi;
       sv[k] = *reinterpret_cast<const f32x4*>(
           x + (ok ? ((((long long)nb * a.di + iz) * a.hi + iy) * a.wi + ix) * CI + 4 * c4 : 0));
       if (!ok) sv[k] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -408,10 +445,32 @@ __global__ __launch_bounds__(256) void conv_s2t_kernel(S2Args a, const float* __
   }
   __syncthreads();
 
-  f32x4 acc[8][2];
+  // class c = (rz, ry, rx), slice zz: lane's voxel = output (2(Z0+zz)+rz, 2(Y0+w)+ry, 2(X0+r16)+rx),
+  // channels 4g .. 4g+3.  Element offsets of this launch fit 32 bits (s2_launch checks it).
+  // Mode-2 statistics: the lane's 16 z granules are in flight during the MFMAs.
+  constexpr int mode = MODE;
+  const int jy = Y0 + wave, jx = X0 + r16;
+  int obase[16];
+  bool ok[16];
+#pragma unroll
+  for (int c = 0; c < 8; ++c) {
+    const int rz = c >> 2, ry = (c >> 1) & 1, rx = c & 1;
+#pragma unroll
+    for (int zz = 0; zz < 2; ++zz) {
+      const int jz = Z0 + zz;
+      const bool v_ok = jz < a.cd && jy < a.ch && jx < a.cw;
+      ok[c * 2 + zz] = v_ok;
+      obase[c * 2 + zz] = v_ok ? (((nb * a.do_ + 2 * jz + rz) * a.ho + 2 * jy + ry) * a.wo + 2 * jx + rx) * CO + 4 * g : 0;
+    }
+  }
+  f32x4 zv[16][1];
+#pragma unroll
+  for (int u = 0; u < 16; ++u)
+    zv[u][0] = mode == 2 ? *reinterpret_cast<const f32x4*>(ep.bn_z + obase[u]) : f32x4{0.f, 0.f, 0.f, 0.f};
+
+  f32x4 acc[8][2];  // D[channel][voxel]: A = weights (lane channel r16), B = activations (lane voxel r16)
 #pragma unroll
   for (int c = 0; c < 8; ++c) acc[c][0] = acc[c][1] = f32x4{0.f, 0.f, 0.f, 0.f};
-  if (!(a.dbg & 2)) {
   s2t_class<0, 0, 0>(halo, bq, acc[0], wave, g, r16);
   s2t_class<0, 0, 1>(halo, bq, acc[1], wave, g, r16);
   s2t_class<0, 1, 0>(halo, bq, acc[2], wave, g, r16);
@@ -420,38 +479,21 @@ __global__ __launch_bounds__(256) void conv_s2t_kernel(S2Args a, const float* __
   s2t_class<1, 0, 1>(halo, bq, acc[5], wave, g, r16);
   s2t_class<1, 1, 0>(halo, bq, acc[6], wave, g, r16);
   s2t_class<1, 1, 1>(halo, bq, acc[7], wave, g, r16);
-  }
 
-  // ---- epilogue: class c = (rz, ry, rx), slice zz, row j -> output (2(Z0+zz)+rz, 2(Y0+w)+ry, 2(X0+4g+j)+rx).
-  // Rows j of one (class, slice) are 2 voxels apart: one 32-bit element offset per (class, slice),
-  // the rows at immediate offsets (the per-element 64-bit index math was most of the kernel's VALU)
-  float vals[16][1][4], zv[16][1][4];
-  bool ok[16][4];
-  const int jy = Y0 + wave;
-  const float bias = ep.bias ? ep.bias[r16] : 0.f;
-  // element offsets of this launch fit 32 bits (s2_launch checks it)
-  const int xrow = 2 * (X0 + 4 * g);
+  // ---- epilogue: one 16-byte store per (class, slice)
+  f32x4 vals[16][1];
+  const f32x4 b4 = ep.bias ? f32x4{ep.bias[4 * g], ep.bias[4 * g + 1], ep.bias[4 * g + 2], ep.bias[4 * g + 3]}
+                           : f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-  for (int c = 0; c < 8; ++c) {
-    const int rz = c >> 2, ry = (c >> 1) & 1, rx = c & 1;
+  for (int c = 0; c < 8; ++c)
 #pragma unroll
     for (int zz = 0; zz < 2; ++zz) {
-      const int jz = Z0 + zz;
-      const bool zy_ok = jz < a.cd && jy < a.ch;
-      const int o0 = ((((nb * a.do_ + 2 * jz + rz) * a.ho + 2 * jy + ry) * a.wo + xrow + rx) * CO) + r16;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const bool v_ok = zy_ok && X0 + 4 * g + j < a.cw;
-        ok[c * 2 + zz][j] = v_ok;
-        const int o = v_ok ? o0 + 2 * j * CO : 0;
-        zv[c * 2 + zz][0][j] = s2_stat_mode(ep) == 2 ? ep.bn_z[o] : 0.f;
-        const float v = s2_act(acc[c][zz][j] + bias, ep);
-        if (v_ok && (!(a.dbg & 4) || v == 1.2345f)) y[o] = v;
-        vals[c * 2 + zz][0][j] = v;
-      }
+      const int u = c * 2 + zz;
+      const f32x4 v = s2_act4(acc[c][zz] + b4, ep);
+      if (ok[u]) *reinterpret_cast<f32x4*>(y + obase[u]) = v;
+      vals[u][0] = v;
     }
-  }
-  if (s2_stat_mode(ep)) {
+  if constexpr (mode != 0) {
     const int cnt = 8 * max(0, min(2, a.cd - Z0)) * max(0, min(4, a.ch - Y0)) * max(0, min(16, a.cw - X0));
     s2_bn_slab<16, 1>(ep, CO, vals, zv, ok, cnt, red);
   }
@@ -459,10 +501,8 @@ __global__ __launch_bounds__(256) void conv_s2t_kernel(S2Args a, const float* __
 
 // ------------------------------------------------------------------------------------------------
 static int g_s2 = 1;  // cgan3d_set_tuning key 4: 0 keeps these shapes on the implicit-GEMM kernel
-static int g_s2_dbg = 0;  // key 5
 
 void s2_set(int v) { g_s2 = v; }
-void s2_set_dbg(int v) { g_s2_dbg = v; }
 
 // 1: S2F, 2: S2T, 0: neither
 int s2_kind(const cgan3d_conv_geom* g) {
@@ -482,7 +522,6 @@ static S2Args s2_args(const cgan3d_conv_geom* g, int kind) {
   if (kind == 1) { a.cd = g->do_; a.ch = g->ho; a.cw = g->wo; }
   else { a.cd = g->di; a.ch = g->hi; a.cw = g->wi; }
   a.td = (a.cd + 1) / 2; a.th = (a.ch + 3) / 4; a.tw = (a.cw + 15) / 16;
-  a.dbg = g_s2_dbg;
   return a;
 }
 
@@ -505,8 +544,11 @@ int s2_launch(const cgan3d_conv_geom* g, const float* x, const __bf16* wp, float
     return CGAN3D_EINVAL;
   }
   const dim3 grid((unsigned)((long long)a.n * a.td * a.th * a.tw));
-  if (kind == 1) ::cg::launch(conv_s2f_kernel, grid, dim3(256), 0, st, a, x, wp, y, e);
-  else ::cg::launch(conv_s2t_kernel, grid, dim3(256), 0, st, a, x, wp, y, e);
+  const int mode = s2_host_stat_mode(e);
+#define CG_S2(K, M) ::cg::launch(K<M>, grid, dim3(256), 0, st, a, x, wp, y, e)
+  if (kind == 1) { if (mode == 2) CG_S2(conv_s2f_kernel, 2); else if (mode == 1) CG_S2(conv_s2f_kernel, 1); else CG_S2(conv_s2f_kernel, 0); }
+  else { if (mode == 2) CG_S2(conv_s2t_kernel, 2); else if (mode == 1) CG_S2(conv_s2t_kernel, 1); else CG_S2(conv_s2t_kernel, 0); }
+#undef CG_S2
   return CGAN3D_OK;
 }
 
