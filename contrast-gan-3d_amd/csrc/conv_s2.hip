@@ -79,92 +79,106 @@ __device__ __forceinline__ int s2_stat_mode(const Epi& ep) {
 }
 static int s2_host_stat_mode(const Epi& ep) { return ep.fz.acc_mode == 3 ? 1 : ep.fz.acc_mode == 4 ? 2 : ep.bn_mode; }
 
-template <int U, int NT>
-__device__ __forceinline__ void s2_bn_slab(const Epi& ep, int C, const f32x4 (&vals)[U][NT], const f32x4 (&zv)[U][NT],
-                                           const bool (&ok)[U], int cnt, float* red) {
+// write the block's statistic pairs (s, q) of channels nt*16 + 4g + j, summed over the block
+// first: mode 1 (sum, M2) or 2 (sum g, sum g*xhat) into slab slot `slot`, or (cgan3d_bn_fuse) into
+// replica slot % reps of the fp64 accumulators (mode 1 as (sum, sum of squares = M2 + S * mean))
+template <int NT>
+__device__ __forceinline__ void s2_stats_write(const Epi& ep, int mode, int C, float (&s)[NT][4], float (&q)[NT][4],
+                                               int cnt, int slot) {
   const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4;
-  const int mode = s2_stat_mode(ep);
   // after the block sums, lanes 0, 16, 32, 48 of wave 0 hold channels nt*16 + 4g + j
-  const bool writer = tid < 64 && (lane & 15) == 0;
-  // this block's replica of the accumulators (cgan3d_bn_fuse), or null: the slab
-  double* const acc = ep.fz.acc_mode ? ep.fz.acc_out + (long long)(blockIdx.x % ep.fz.reps) * 2 * C : nullptr;
+  if (!(tid < 64 && (lane & 15) == 0)) return;
+  double* const acc = ep.fz.acc_mode ? ep.fz.acc_out + (long long)(slot % ep.fz.reps) * 2 * C : nullptr;
+#pragma unroll
+  for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int c = nt * 16 + 4 * g + j;
+      if (acc) {
+        if (mode == 2) {
+          unsafeAtomicAdd(acc + c, (double)s[nt][j]);
+          unsafeAtomicAdd(acc + C + c, (double)q[nt][j]);
+        } else if (cnt) {
+          unsafeAtomicAdd(acc + c, (double)s[nt][j]);
+          unsafeAtomicAdd(acc + C + c, (double)q[nt][j] + (double)s[nt][j] * (double)s[nt][j] / cnt);
+        }
+      } else {
+        *bn_slot(ep, 0, C, c, slot) = s[nt][j];
+        *bn_slot(ep, 1, C, c, slot) = q[nt][j];
+      }
+    }
+  if (mode == 1 && tid == 0 && !acc) *bn_slot(ep, 2, C, 0, slot) = (float)cnt;
+}
+
+// mode 1 from the block's outputs: vals[U][NT] per lane = channels nt*16 + 4g + 0..3 of the lane's
+// voxel in output group u, ok[u] = that voxel is inside the volume; (sum, M2 about the block mean)
+template <int U, int NT>
+__device__ __forceinline__ void s2_stats_m1(const Epi& ep, int C, const f32x4 (&vals)[U][NT], const bool (&ok)[U],
+                                            int cnt, float* red, int slot) {
   float s[NT][4], q[NT][4];
-  if (mode == 1) {
 #pragma unroll
-    for (int nt = 0; nt < NT; ++nt)
+  for (int nt = 0; nt < NT; ++nt)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        s[nt][j] = 0.f;
+    for (int j = 0; j < 4; ++j) {
+      s[nt][j] = 0.f;
 #pragma unroll
-        for (int u = 0; u < U; ++u) s[nt][j] += ok[u] ? vals[u][nt][j] : 0.f;
-      }
-    block_chan_sum<NT>(s, red);
-#pragma unroll
-    for (int nt = 0; nt < NT; ++nt)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const float m = cnt ? s[nt][j] / cnt : 0.f;
-        q[nt][j] = 0.f;
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-          const float d = ok[u] ? vals[u][nt][j] - m : 0.f;
-          q[nt][j] += d * d;
-        }
-      }
-    block_chan_sum<NT>(q, red);
-    if (writer) {
-#pragma unroll
-      for (int nt = 0; nt < NT; ++nt)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int c = nt * 16 + 4 * g + j;
-          if (acc) {  // (sum, sum of squares = M2 + S * mean)
-            if (cnt) {
-              unsafeAtomicAdd(acc + c, (double)s[nt][j]);
-              unsafeAtomicAdd(acc + C + c, (double)q[nt][j] + (double)s[nt][j] * (double)s[nt][j] / cnt);
-            }
-          } else {
-            *bn_slot(ep, 0, C, c, blockIdx.x) = s[nt][j];
-            *bn_slot(ep, 1, C, c, blockIdx.x) = q[nt][j];
-          }
-        }
-      if (tid == 0 && !acc) *bn_slot(ep, 2, C, 0, blockIdx.x) = (float)cnt;
+      for (int u = 0; u < U; ++u) s[nt][j] += ok[u] ? vals[u][nt][j] : 0.f;
     }
-  } else if (mode == 2) {
+  block_chan_sum<NT>(s, red);
 #pragma unroll
-    for (int nt = 0; nt < NT; ++nt)
+  for (int nt = 0; nt < NT; ++nt)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int c = nt * 16 + 4 * g + j;  // this lane's channel: its BatchNorm coefficients once
-        const float sc = ep.bn_ss[c], sh = ep.bn_ss[C + c], mu = ep.bn_mi[c], inv = ep.bn_mi[C + c];
-        s[nt][j] = 0.f;
-        q[nt][j] = 0.f;
+    for (int j = 0; j < 4; ++j) {
+      const float m = cnt ? s[nt][j] / cnt : 0.f;
+      q[nt][j] = 0.f;
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-          const float z = zv[u][nt][j];
-          const float gg = ok[u] ? vals[u][nt][j] * act_grad(z * sc + sh, ep.bn_act, ep.bn_slope) : 0.f;
-          s[nt][j] += gg;
-          q[nt][j] += gg * (z - mu) * inv;
-        }
+      for (int u = 0; u < U; ++u) {
+        const float d = ok[u] ? vals[u][nt][j] - m : 0.f;
+        q[nt][j] += d * d;
       }
-    block_chan_sum<NT>(s, red);
-    block_chan_sum<NT>(q, red);
-    if (writer) {
-#pragma unroll
-      for (int nt = 0; nt < NT; ++nt)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int c = nt * 16 + 4 * g + j;
-          if (acc) {
-            unsafeAtomicAdd(acc + c, (double)s[nt][j]);
-            unsafeAtomicAdd(acc + C + c, (double)q[nt][j]);
-          } else {
-            *bn_slot(ep, 0, C, c, blockIdx.x) = s[nt][j];
-            *bn_slot(ep, 1, C, c, blockIdx.x) = q[nt][j];
-          }
-        }
     }
+  block_chan_sum<NT>(q, red);
+  s2_stats_write<NT>(ep, 1, C, s, q, cnt, slot);
+}
+
+// mode 2, streamed: the BatchNorm coefficients of the lane's channels, then s2_m2_add per output
+struct S2M2 {
+  float sc[4], sh[4], mu[4], inv[4];
+};
+__device__ __forceinline__ S2M2 s2_m2_coef(const Epi& ep, int C, int c0) {
+  S2M2 k;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    k.sc[j] = ep.bn_ss[c0 + j]; k.sh[j] = ep.bn_ss[C + c0 + j];
+    k.mu[j] = ep.bn_mi[c0 + j]; k.inv[j] = ep.bn_mi[C + c0 + j];
   }
+  return k;
+}
+__device__ __forceinline__ void s2_m2_add(const Epi& ep, const S2M2& k, f32x4 v, f32x4 z, bool ok, float (&s)[4],
+                                          float (&q)[4]) {
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const float gg = ok ? v[j] * act_grad(z[j] * k.sc[j] + k.sh[j], ep.bn_act, ep.bn_slope) : 0.f;
+    s[j] += gg;
+    q[j] += gg * (z[j] - k.mu[j]) * k.inv[j];
+  }
+}
+
+// lo / hi: lane r16 holds the first / second 64-byte half of line r16 (a 128-byte pair of voxels or
+// channel halves).  Rotating each by 8 lanes within the 16-lane row (DPP) gives A = lines 0..7 and
+// B = lines 8..15 whole: lane r16 of A holds half r16 >> 3 of line r16 & 7, of B of line 8 + (r16 & 7)
+__device__ __forceinline__ f32x4 s2_ror8(f32x4 v) {
+  f32x4 r;
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+    r[j] = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v[j]), 0x128, 0xf, 0xf, false));
+  return r;
+}
+__device__ __forceinline__ void s2_line_pair(f32x4 lo, f32x4 hi, int r16, f32x4& A, f32x4& B) {
+  const f32x4 lo8 = s2_ror8(lo), hi8 = s2_ror8(hi);
+  const bool first = r16 < 8;
+  A = first ? lo : hi8;
+  B = first ? lo8 : hi;
 }
 
 __device__ __forceinline__ f32x4 s2_act4(f32x4 v, const Epi& ep) {
@@ -311,20 +325,27 @@ __global__ __launch_bounds__(256) void conv_s2f_kernel(S2Args a, const float* __
 
   // ---- epilogue: lane holds output (x = X0 + r16, y = Y0 + wave, z = Z0 + zz), channels nt*16 + 4g .. +3
   f32x4 vals[2][2];
+  float s2s[2][4] = {}, s2q[2][4] = {};  // mode 2, streamed
 #pragma unroll
   for (int nt = 0; nt < 2; ++nt) {
     const int c = nt * 16 + 4 * g;
     const f32x4 b4 = ep.bias ? f32x4{ep.bias[c], ep.bias[c + 1], ep.bias[c + 2], ep.bias[c + 3]} : f32x4{0.f, 0.f, 0.f, 0.f};
+    S2M2 k2;
+    if constexpr (mode == 2) k2 = s2_m2_coef(ep, CO, c);
 #pragma unroll
     for (int zz = 0; zz < 2; ++zz) {
       const f32x4 v = s2_act4(acc[zz][nt] + b4, ep);
       if (ok[zz]) *reinterpret_cast<f32x4*>(y + obase[zz] + nt * 16) = v;
       vals[zz][nt] = v;
+      if constexpr (mode == 2) s2_m2_add(ep, k2, v, zv[zz][nt], ok[zz], s2s[nt], s2q[nt]);
     }
   }
-  if constexpr (mode != 0) {
-    const int cnt = max(0, min(2, a.cd - Z0)) * max(0, min(4, a.ch - Y0)) * max(0, min(16, a.cw - X0));
-    s2_bn_slab<2, 2>(ep, CO, vals, zv, ok, cnt, red);
+  const int cnt = max(0, min(2, a.cd - Z0)) * max(0, min(4, a.ch - Y0)) * max(0, min(16, a.cw - X0));
+  if constexpr (mode == 1) s2_stats_m1<2, 2>(ep, CO, vals, ok, cnt, red, blockIdx.x);
+  if constexpr (mode == 2) {
+    block_chan_sum<2>(s2s, red);
+    block_chan_sum<2>(s2q, red);
+    s2_stats_write<2>(ep, 2, CO, s2s, s2q, cnt, blockIdx.x);
   }
 }
 
@@ -351,9 +372,13 @@ struct S2Taps<1> {
   static constexpr int off[2] = {1, 0};
 };
 
+// weight granule (tap t, output channel co, K granule q) of the LDS copy: slot q ^ s2t_wsw(co) of
+// the (t, co) row — the 16 lanes of every ds_read_b128 lane group hit 16 distinct bank blocks
+__device__ __forceinline__ int s2t_wsw(int co) { return (co & 4) >> 1; }
+
 template <int RZ, int RY, int RX>
-__device__ __forceinline__ void s2t_class(const __bf16* halo, const bf16x8_s (&bq)[27], f32x4 (&acc)[2], int wave,
-                                          int g, int r16) {
+__device__ __forceinline__ void s2t_class(const __bf16* halo, const __bf16* wts, f32x4 (&acc)[2], int wave, int g,
+                                          int r16) {
   using TZ = S2Taps<RZ>;
   using TY = S2Taps<RY>;
   using TX = S2Taps<RX>;
@@ -365,137 +390,176 @@ __device__ __forceinline__ void s2t_class(const __bf16* halo, const bf16x8_s (&b
       for (int c = 0; c < TX::n; ++c) {
         const int t = TZ::t[a] * 9 + TY::t[b] * 3 + TX::t[c];
         const int hx = r16 + TX::off[c];
+        const bf16x8_s bw = *reinterpret_cast<const bf16x8_s*>(wts + ((t * 16 + r16) * 4 + (g ^ s2t_wsw(r16))) * 8);
 #pragma unroll
         for (int zz = 0; zz < 2; ++zz) {
           const int row = (zz + TZ::off[a]) * T_HY + wave + TY::off[b];
           const bf16x8_s av =
               *reinterpret_cast<const bf16x8_s*>(halo + (row * T_HX + hx) * 32 + 8 * (g ^ ((hx >> 1) & 2)));
-          acc[zz] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bq[t], av, acc[zz], 0, 0, 0);
+          acc[zz] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bw, av, acc[zz], 0, 0, 0);
         }
       }
 }
 
-template <int MODE>  // statistics mode s2_stat_mode(ep): 0 none, 1 forward, 2 input-grad
-__global__ __launch_bounds__(256) void conv_s2t_kernel(S2Args a, const float* __restrict__ x,
-                                                       const __bf16* __restrict__ wpk, float* y, Epi ep) {
+// Persistent: a block loops over tiles (grid = min(tiles, 2 per CU, 1 in mode 2)); the weights are staged into
+// LDS once, the next tile's halo is loaded into registers while the current tile's MFMAs and
+// epilogue run, and the mode-2 z granules of a tile are issued before its halo is staged.
+template <int MODE, bool X16>  // statistics mode s2_stat_mode(ep): 0 none, 1 forward, 2 input-grad; X16: ep.x16
+__global__ __launch_bounds__(256, MODE == 2 ? 1 : 2) void conv_s2t_kernel(S2Args a, const float* __restrict__ x,
+                                                          const __bf16* __restrict__ wpk, float* y, Epi ep, int ntiles) {
   constexpr int CI = 32, CO = 16;
   __shared__ __attribute__((aligned(16))) __bf16 halo[T_HALO];
+  __shared__ __attribute__((aligned(16))) __bf16 wts[27 * CO * CI];
   __shared__ float red[4 * CO];
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int g = lane >> 4, r16 = lane & 15;
   const int tiles = a.td * a.th * a.tw;
-  int bid = blockIdx.x;
-  const int nb = bid / tiles;
-  bid -= nb * tiles;
-  const int Z0 = (bid / (a.th * a.tw)) * 2, Y0 = ((bid / a.tw) % a.th) * 4, X0 = (bid % a.tw) * 16;
-
-  bf16x8_s bq[27];  // lane (channel r16, granule g) of every tap
-#pragma unroll
-  for (int t = 0; t < 27; ++t)
-    bq[t] = *reinterpret_cast<const bf16x8_s*>(wpk + ((long long)t * CO + r16) * CI + 8 * (g ^ (r16 & 3)));
-
-  if (ep.x16) {  // the same halo from the bf16 shadow of the input, 16-byte granules as they are
-    constexpr int NG = T_HZ * T_HY * T_HX * 4, PG = (NG + 255) / 256;
-    const bf16x8_s* xq = reinterpret_cast<const bf16x8_s*>(ep.x16);
-    bf16x8_s sb[PG];
-#pragma unroll
-    for (int k = 0; k < PG; ++k) {
-      const int i = tid + 256 * k;
-      const int q = i & 3, v = i >> 2;
-      const int hx = v % T_HX, r = v / T_HX;
-      const int hy = r % T_HY, hz = r / T_HY;
-      const int iz = Z0 + hz, iy = Y0 + hy, ix = X0 + hx;
-      const bool ok = i < NG && iz < a.di && iy < a.hi && ix < a.wi;
-      sb[k] = xq[ok ? ((((long long)nb * a.di + iz) * a.hi + iy) * a.wi + ix) * 4 + q : 0];
-      if (!ok) sb[k] = bf16x8_s{};
-    }
-#pragma unroll
-    for (int k = 0; k < PG; ++k) {
-      const int i = tid + 256 * k;
-      if (i >= NG) break;
-      const int q = i & 3, v = i >> 2;
-      const int hx = v % T_HX;
-      *reinterpret_cast<bf16x8_s*>(halo + v * 32 + 8 * (q ^ ((hx >> 1) & 2))) = sb[k];
-    }
-  } else {  // halo: gathered (Z0 .. +3, Y0 .. +5, X0 .. +17) -> [hz][hy][hx][32] bf16, granule swizzle
-    constexpr int NV4 = T_HZ * T_HY * T_HX * 8, PER = (NV4 + 255) / 256;
-    f32x4 sv[PER];
-#pragma unroll
-    for (int k = 0; k < PER; ++k) {
-      const int i = tid + 256 * k;
-      const int c4 = i & 7, v = i >> 3;
-      const int hx = v % T_HX, r = v / T_HX;
-      const int hy = r % T_HY, hz = r / T_HY;
-      const int iz = Z0 + hz, iy = Y0 + hy, ix = X0 + hx;
-      const bool ok = i < NV4 && iz < a.di && iy < a.hi && ix < a.wi;
-      sv[k] = *reinterpret_cast<const f32x4*>(
-          x + (ok ? ((((long long)nb * a.di + iz) * a.hi + iy) * a.wi + ix) * CI + 4 * c4 : 0));
-      if (!ok) sv[k] = f32x4{0.f, 0.f, 0.f, 0.f};
-    }
-#pragma unroll
-    for (int k = 0; k < PER; ++k) {
-      const int i = tid + 256 * k;
-      if (i >= NV4) break;
-      const int c4 = i & 7, v = i >> 3;
-      const int hx = v % T_HX;
-      bf16x4_s u;
-      u[0] = (__bf16)sv[k][0]; u[1] = (__bf16)sv[k][1]; u[2] = (__bf16)sv[k][2]; u[3] = (__bf16)sv[k][3];
-      *reinterpret_cast<bf16x4_s*>(halo + v * 32 + 8 * ((c4 >> 1) ^ ((hx >> 1) & 2)) + 4 * (c4 & 1)) = u;
+  {  // packed weights (granule (t*CO + co)*4 + (q ^ (co & 3)) holds K granule q) -> LDS, once
+    const bf16x8_s* src = reinterpret_cast<const bf16x8_s*>(wpk);
+    bf16x8_s* dst = reinterpret_cast<bf16x8_s*>(wts);
+    for (int i = tid; i < 27 * CO * 4; i += 256) {
+      const int q = i & 3, co = (i >> 2) & 15, t = i >> 6;
+      const int kq = q ^ s2t_wsw(co);
+      dst[i] = src[(t * CO + co) * 4 + (kq ^ (co & 3))];
     }
   }
-  __syncthreads();
-
-  // class c = (rz, ry, rx), slice zz: lane's voxel = output (2(Z0+zz)+rz, 2(Y0+w)+ry, 2(X0+r16)+rx),
-  // channels 4g .. 4g+3.  Element offsets of this launch fit 32 bits (s2_launch checks it).
-  // Mode-2 statistics: the lane's 16 z granules are in flight during the MFMAs.
-  constexpr int mode = MODE;
-  const int jy = Y0 + wave, jx = X0 + r16;
-  int obase[16];
-  bool ok[16];
+  const float4* xf = reinterpret_cast<const float4*>(x);
+  const bf16x8_s* xq = reinterpret_cast<const bf16x8_s*>(ep.x16);
+  constexpr int NG = T_HZ * T_HY * T_HX * 4, PG = (NG + 255) / 256;    // bf16 shadow granules
+  constexpr int NV4 = T_HZ * T_HY * T_HX * 8, PER = (NV4 + 255) / 256;  // fp32 float4s
+  bf16x8_s sb[X16 ? PG : 1];
+  f32x4 sv[X16 ? 1 : PER];
+  auto origin = [&](int tile, int* nb, int* Z0, int* Y0, int* X0) {
+    *nb = tile / tiles;
+    const int b = tile - *nb * tiles;
+    *Z0 = (b / (a.th * a.tw)) * 2; *Y0 = ((b / a.tw) % a.th) * 4; *X0 = (b % a.tw) * 16;
+  };
+  // halo: gathered (Z0 .. +3, Y0 .. +5, X0 .. +17) -> [hz][hy][hx][32] bf16, granule swizzle
+  auto load = [&](int tile) {
+    int nb, Z0, Y0, X0;
+    origin(tile, &nb, &Z0, &Y0, &X0);
+    if constexpr (X16) {
 #pragma unroll
-  for (int c = 0; c < 8; ++c) {
-    const int rz = c >> 2, ry = (c >> 1) & 1, rx = c & 1;
+      for (int k = 0; k < PG; ++k) {
+        const int i = tid + 256 * k;
+        const int q = i & 3, v = i >> 2;
+        const int hx = v % T_HX, r = v / T_HX;
+        const int hy = r % T_HY, hz = r / T_HY;
+        const int iz = Z0 + hz, iy = Y0 + hy, ix = X0 + hx;
+        const bool ok = i < NG && iz < a.di && iy < a.hi && ix < a.wi;
+        sb[k] = xq[ok ? ((((long long)nb * a.di + iz) * a.hi + iy) * a.wi + ix) * 4 + q : 0];
+        if (!ok) sb[k] = bf16x8_s{};
+      }
+    } else {
 #pragma unroll
-    for (int zz = 0; zz < 2; ++zz) {
-      const int jz = Z0 + zz;
-      const bool v_ok = jz < a.cd && jy < a.ch && jx < a.cw;
-      ok[c * 2 + zz] = v_ok;
-      obase[c * 2 + zz] = v_ok ? (((nb * a.do_ + 2 * jz + rz) * a.ho + 2 * jy + ry) * a.wo + 2 * jx + rx) * CO + 4 * g : 0;
+      for (int k = 0; k < PER; ++k) {
+        const int i = tid + 256 * k;
+        const int c4 = i & 7, v = i >> 3;
+        const int hx = v % T_HX, r = v / T_HX;
+        const int hy = r % T_HY, hz = r / T_HY;
+        const int iz = Z0 + hz, iy = Y0 + hy, ix = X0 + hx;
+        const bool ok = i < NV4 && iz < a.di && iy < a.hi && ix < a.wi;
+        const float4 f = xf[ok ? ((((long long)nb * a.di + iz) * a.hi + iy) * a.wi + ix) * (CI / 4) + c4 : 0];
+        sv[k] = ok ? f32x4{f.x, f.y, f.z, f.w} : f32x4{0.f, 0.f, 0.f, 0.f};
+      }
     }
-  }
-  f32x4 zv[16][1];
+  };
+  auto store = [&]() {
+    if constexpr (X16) {
 #pragma unroll
-  for (int u = 0; u < 16; ++u)
-    zv[u][0] = mode == 2 ? *reinterpret_cast<const f32x4*>(ep.bn_z + obase[u]) : f32x4{0.f, 0.f, 0.f, 0.f};
-
-  f32x4 acc[8][2];  // D[channel][voxel]: A = weights (lane channel r16), B = activations (lane voxel r16)
+      for (int k = 0; k < PG; ++k) {
+        const int i = tid + 256 * k;
+        if (i >= NG) break;
+        const int q = i & 3, v = i >> 2;
+        const int hx = v % T_HX;
+        *reinterpret_cast<bf16x8_s*>(halo + v * 32 + 8 * (q ^ ((hx >> 1) & 2))) = sb[k];
+      }
+    } else {
 #pragma unroll
-  for (int c = 0; c < 8; ++c) acc[c][0] = acc[c][1] = f32x4{0.f, 0.f, 0.f, 0.f};
-  s2t_class<0, 0, 0>(halo, bq, acc[0], wave, g, r16);
-  s2t_class<0, 0, 1>(halo, bq, acc[1], wave, g, r16);
-  s2t_class<0, 1, 0>(halo, bq, acc[2], wave, g, r16);
-  s2t_class<0, 1, 1>(halo, bq, acc[3], wave, g, r16);
-  s2t_class<1, 0, 0>(halo, bq, acc[4], wave, g, r16);
-  s2t_class<1, 0, 1>(halo, bq, acc[5], wave, g, r16);
-  s2t_class<1, 1, 0>(halo, bq, acc[6], wave, g, r16);
-  s2t_class<1, 1, 1>(halo, bq, acc[7], wave, g, r16);
-
-  // ---- epilogue: one 16-byte store per (class, slice)
-  f32x4 vals[16][1];
+      for (int k = 0; k < PER; ++k) {
+        const int i = tid + 256 * k;
+        if (i >= NV4) break;
+        const int c4 = i & 7, v = i >> 3;
+        const int hx = v % T_HX;
+        bf16x4_s u;
+        u[0] = (__bf16)sv[k][0]; u[1] = (__bf16)sv[k][1]; u[2] = (__bf16)sv[k][2]; u[3] = (__bf16)sv[k][3];
+        *reinterpret_cast<bf16x4_s*>(halo + v * 32 + 8 * ((c4 >> 1) ^ ((hx >> 1) & 2)) + 4 * (c4 & 1)) = u;
+      }
+    }
+  };
   const f32x4 b4 = ep.bias ? f32x4{ep.bias[4 * g], ep.bias[4 * g + 1], ep.bias[4 * g + 2], ep.bias[4 * g + 3]}
                            : f32x4{0.f, 0.f, 0.f, 0.f};
+  S2M2 k2;
+  if constexpr (MODE == 2) k2 = s2_m2_coef(ep, CO, 4 * g);
+  int tile = blockIdx.x;
+  if (tile < ntiles) load(tile);
+  for (; tile < ntiles; tile += gridDim.x) {
+    int nb, Z0, Y0, X0;
+    origin(tile, &nb, &Z0, &Y0, &X0);
+    // The MFMAs leave lane (g, r16) with channels 4g .. 4g+3 of class voxel jx = X0 + r16; the
+    // classes rx = 0 / 1 of one (rz, ry, slice) are the two 64-byte halves of the 128-byte voxel
+    // pairs (2jx, 2jx + 1).  The epilogue swaps halves between lanes r16 and r16 ^ 8 (DPP row
+    // rotate by 8) so each store writes whole lines: output u = ((rz * 2 + ry) * 2 + zz) * 2 + S
+    // holds class voxel jx = X0 + 8S + (r16 & 7), rx = r16 >> 3.  Element offsets of this launch
+    // fit 32 bits (s2_launch checks it).
+    const int jy = Y0 + wave;
+    int obase[16];
+    bool ok[16];
 #pragma unroll
-  for (int c = 0; c < 8; ++c)
-#pragma unroll
-    for (int zz = 0; zz < 2; ++zz) {
-      const int u = c * 2 + zz;
-      const f32x4 v = s2_act4(acc[c][zz] + b4, ep);
-      if (ok[u]) *reinterpret_cast<f32x4*>(y + obase[u]) = v;
-      vals[u][0] = v;
+    for (int u = 0; u < 16; ++u) {
+      const int S = u & 1, zz = (u >> 1) & 1, ry = (u >> 2) & 1, rz = u >> 3;
+      const int jz = Z0 + zz, jx = X0 + 8 * S + (r16 & 7), rx = r16 >> 3;
+      const bool v_ok = jz < a.cd && jy < a.ch && jx < a.cw;
+      ok[u] = v_ok;
+      obase[u] = v_ok ? (((nb * a.do_ + 2 * jz + rz) * a.ho + 2 * jy + ry) * a.wo + 2 * jx + rx) * CO + 4 * g : 0;
     }
-  if constexpr (mode != 0) {
+    f32x4 zv[MODE == 2 ? 16 : 1];  // mode 2: in flight during the staging and the MFMAs
+    if constexpr (MODE == 2) {
+#pragma unroll
+      for (int u = 0; u < 16; ++u) zv[u] = *reinterpret_cast<const f32x4*>(ep.bn_z + obase[u]);
+    }
+    __syncthreads();  // every wave done with the previous tile's halo (and the weight staging)
+    store();
+    __syncthreads();
+    if (tile + (int)gridDim.x < ntiles) load(tile + gridDim.x);  // in flight during this tile's MFMAs
+
+    f32x4 acc[8][2];  // D[channel][voxel]: A = weights (lane channel r16), B = activations (lane voxel r16)
+#pragma unroll
+    for (int c = 0; c < 8; ++c) acc[c][0] = acc[c][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+    s2t_class<0, 0, 0>(halo, wts, acc[0], wave, g, r16);
+    s2t_class<0, 0, 1>(halo, wts, acc[1], wave, g, r16);
+    s2t_class<0, 1, 0>(halo, wts, acc[2], wave, g, r16);
+    s2t_class<0, 1, 1>(halo, wts, acc[3], wave, g, r16);
+    s2t_class<1, 0, 0>(halo, wts, acc[4], wave, g, r16);
+    s2t_class<1, 0, 1>(halo, wts, acc[5], wave, g, r16);
+    s2t_class<1, 1, 0>(halo, wts, acc[6], wave, g, r16);
+    s2t_class<1, 1, 1>(halo, wts, acc[7], wave, g, r16);
+
+    // ---- epilogue: 16-byte stores of whole lines; mode 2 statistics streamed, mode 1 from the held
+    // outputs (M2 about the block mean)
+    f32x4 vals[MODE == 1 ? 16 : 1][1];
+    float s2s[1][4] = {}, s2q[1][4] = {};
+#pragma unroll
+    for (int p = 0; p < 4; ++p)  // (rz, ry): classes 2p (rx = 0) and 2p + 1 (rx = 1)
+#pragma unroll
+      for (int zz = 0; zz < 2; ++zz) {
+        f32x4 out[2];
+        s2_line_pair(s2_act4(acc[2 * p][zz] + b4, ep), s2_act4(acc[2 * p + 1][zz] + b4, ep), r16, out[0], out[1]);
+#pragma unroll
+        for (int S = 0; S < 2; ++S) {
+          const int u = (p * 2 + zz) * 2 + S;
+          if (ok[u]) *reinterpret_cast<f32x4*>(y + obase[u]) = out[S];
+          if constexpr (MODE == 1) vals[u][0] = out[S];
+          if constexpr (MODE == 2) s2_m2_add(ep, k2, out[S], zv[u], ok[u], s2s[0], s2q[0]);
+        }
+      }
     const int cnt = 8 * max(0, min(2, a.cd - Z0)) * max(0, min(4, a.ch - Y0)) * max(0, min(16, a.cw - X0));
-    s2_bn_slab<16, 1>(ep, CO, vals, zv, ok, cnt, red);
+    if constexpr (MODE == 1) s2_stats_m1<16, 1>(ep, CO, vals, ok, cnt, red, tile);
+    if constexpr (MODE == 2) {
+      block_chan_sum<1>(s2s, red);
+      block_chan_sum<1>(s2q, red);
+      s2_stats_write<1>(ep, 2, CO, s2s, s2q, cnt, tile);
+    }
   }
 }
 
@@ -543,12 +607,19 @@ int s2_launch(const cgan3d_conv_geom* g, const float* x, const __bf16* wp, float
     set_error("conv_s2: output too large for 32-bit element offsets");
     return CGAN3D_EINVAL;
   }
-  const dim3 grid((unsigned)((long long)a.n * a.td * a.th * a.tw));
+  const long long ntiles = (long long)a.n * a.td * a.th * a.tw;
+  const dim3 grid((unsigned)ntiles);
   const int mode = s2_host_stat_mode(e);
 #define CG_S2(K, M) ::cg::launch(K<M>, grid, dim3(256), 0, st, a, x, wp, y, e)
   if (kind == 1) { if (mode == 2) CG_S2(conv_s2f_kernel, 2); else if (mode == 1) CG_S2(conv_s2f_kernel, 1); else CG_S2(conv_s2f_kernel, 0); }
-  else { if (mode == 2) CG_S2(conv_s2t_kernel, 2); else if (mode == 1) CG_S2(conv_s2t_kernel, 1); else CG_S2(conv_s2t_kernel, 0); }
 #undef CG_S2
+  else {  // persistent: two blocks per CU (one with the mode-2 z granules prefetched)
+    const dim3 pgrid((unsigned)std::min<long long>(ntiles, (mode == 2 ? 1LL : 2LL) * cu_count()));
+#define CG_S2T(M, X) ::cg::launch(conv_s2t_kernel<M, X>, pgrid, dim3(256), 0, st, a, x, wp, y, e, (int)ntiles)
+    if (e.x16) { if (mode == 2) CG_S2T(2, true); else if (mode == 1) CG_S2T(1, true); else CG_S2T(0, true); }
+    else { if (mode == 2) CG_S2T(2, false); else if (mode == 1) CG_S2T(1, false); else CG_S2T(0, false); }
+#undef CG_S2T
+  }
   return CGAN3D_OK;
 }
 

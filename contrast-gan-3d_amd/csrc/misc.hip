@@ -17,6 +17,18 @@ void set_error(const char* fmt, ...) {
 
 __global__ void adam_tick_kernel(float* hyper) { hyper[4] += 1.f; }
 
+// compute units of the current device (persistent-grid sizing), looked up once per device
+int cu_count() {
+  static int cus[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+  if (!cus[dev]) {
+    int v = 0;
+    cus[dev] = hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && v > 0 ? v : 256;
+  }
+  return cus[dev];
+}
+
 
 // one thread per (voxel, V channels); 32-bit index math (element count < 2^31).  PD: the depth
 // axis's pad (P, or 0 for the 2-D variants' planar grids, whose depth is not padded)
