@@ -13,7 +13,8 @@ from pathlib import Path
 
 import torch  # noqa: F401  (must be imported first: see module docstring)
 
-LIB_PATH = Path(__file__).resolve().parent / "libcgan3d.so"
+# CGAN3D_LIB_PATH: another build of the same library (back-to-back A/B of two builds, tools/gpu_ab_lib.sh)
+LIB_PATH = Path(os.environ.get("CGAN3D_LIB_PATH") or Path(__file__).resolve().parent / "libcgan3d.so")
 
 ACT_NONE, ACT_RELU, ACT_LRELU, ACT_TANH = 0, 1, 2, 3
 WGRAD_ACCUMULATE, WGRAD_WS_CLEAN, WGRAD_DEFER_UNPACK = 1, 2, 4  # cgan3d_conv3d_wgrad_ex flag word

@@ -71,6 +71,13 @@ struct K7Fold {
   int P, zd, zh, zw;
 };
 
+// sum over the 16 lanes of a row (the voxel lanes r16 of a transposed MFMA tile)
+__device__ __forceinline__ float k7m_rowsum16(float v) {
+#pragma unroll
+  for (int m = 1; m < 16; m <<= 1) v += __shfl_xor(v, m, 64);
+  return v;
+}
+
 __global__ __launch_bounds__(256, 2) void k7m_n2w_kernel(K7Args a, const float* __restrict__ x,
                                                          const float* __restrict__ w, float* __restrict__ y,
                                                          float* stats, float* bn_part, int tiles_per_block, int ntiles,
@@ -135,10 +142,16 @@ __global__ __launch_bounds__(256, 2) void k7m_n2w_kernel(K7Args a, const float* 
   };
   // running BatchNorm statistics of this block (threads tid < 16, channel tid): Chan merge per tile
   float run_n = 0.f, run_mean = 0.f, run_m2 = 0.f;
-  // folded mode-2 pairs of this lane's channel r16, summed over its outputs of every tile
-  float fp1 = 0.f, fp2 = 0.f, fsc = 0.f, fsh = 0.f, fmean = 0.f, finv = 0.f;
+  // folded mode-2 pairs of this lane's channels 4g + jj, summed over its outputs of every tile
+  float fp1[4] = {0.f, 0.f, 0.f, 0.f}, fp2[4] = {0.f, 0.f, 0.f, 0.f};
+  float fsc[4] = {0.f, 0.f, 0.f, 0.f}, fsh[4] = {0.f, 0.f, 0.f, 0.f}, fmean[4] = {0.f, 0.f, 0.f, 0.f},
+        finv[4] = {0.f, 0.f, 0.f, 0.f};
   if (fb.z) {
-    fsc = fb.ss[r16]; fsh = fb.ss[C + r16]; fmean = fb.mi[r16]; finv = fb.mi[C + r16];
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj) {
+      const int c = 4 * g + jj;
+      fsc[jj] = fb.ss[c]; fsh[jj] = fb.ss[C + c]; fmean[jj] = fb.mi[c]; finv[jj] = fb.mi[C + c];
+    }
   }
   const int t0 = blockIdx.x * tiles_per_block, t1 = min(ntiles, t0 + tiles_per_block);
   if (t0 < t1 && !(a.dbg & 4)) load(t0);
@@ -180,84 +193,87 @@ __global__ __launch_bounds__(256, 2) void k7m_n2w_kernel(K7Args a, const float* 
       bf16x8_k av[N_TH];
 #pragma unroll
       for (int r = 0; r < N_TH; ++r) av[r] = *reinterpret_cast<const bf16x8_k*>(ub + aoff[ks] + r * N_TW * 8);
+      // transposed: D[channel][ow] (A = weights, B = the unfolded image), so a lane ends up with 4
+      // consecutive channels of one voxel: 16-byte output stores and z loads
 #pragma unroll
-      for (int r = 0; r < N_TH; ++r) acc[r] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[r], bv[ks], acc[r], 0, 0, 0);
+      for (int r = 0; r < N_TH; ++r) acc[r] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bv[ks], av[r], acc[r], 0, 0, 0);
     }
-    // lane holds out[ow = 4g + jj][c = r16] of row r (oh = h0 + r, od = d0 + wave)
-    const int od = d0 + wave;
-    float s1 = 0.f;
-    int cntl = 0;
+    // lane holds out[c = 4g + jj][ow = w0 + r16] of row r (oh = h0 + r, od = d0 + wave)
+    const int od = d0 + wave, ow = w0 + r16;
+    float s1[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int r = 0; r < N_TH; ++r) {
       const int oh = h0 + r;
+      if (od < a.do_ && oh < a.ho && ow < a.wo) {
+        if (!(a.dbg & 8))
+          *reinterpret_cast<f32x4*>(y + (((n * a.do_ + od) * a.ho + oh) * a.wo + ow) * C + 4 * g) = acc[r];
 #pragma unroll
-      for (int jj = 0; jj < 4; ++jj) {
-        const int ow = w0 + 4 * g + jj;
-        if (od < a.do_ && oh < a.ho && ow < a.wo) {
-          if (!(a.dbg & 8)) y[((((n * a.do_ + od) * a.ho + oh) * a.wo + ow) * C) + r16] = acc[r][jj];
-          s1 += acc[r][jj];
-          ++cntl;
-        }
+        for (int jj = 0; jj < 4; ++jj) s1[jj] += acc[r][jj];
       }
     }
     if (fb.z) {  // every z of the tile's outputs loaded before the first is used
-      const int vd = reflect_idx(od - fb.P, fb.zd);
-      float zv[N_TH][4];
+      const int vd = reflect_idx(od - fb.P, fb.zd), vw = reflect_idx(ow - fb.P, fb.zw);
+      f32x4 zv[N_TH];
 #pragma unroll
       for (int r = 0; r < N_TH; ++r) {
         const int vh = reflect_idx(h0 + r - fb.P, fb.zh);
-#pragma unroll
-        for (int jj = 0; jj < 4; ++jj) {
-          const int ow = w0 + 4 * g + jj, vw = reflect_idx(ow - fb.P, fb.zw);
-          const bool ok = od < a.do_ && h0 + r < a.ho && ow < a.wo;
-          zv[r][jj] = fb.z[ok ? (((n * fb.zd + vd) * fb.zh + vh) * fb.zw + vw) * C + r16 : 0];
-        }
+        const bool ok = od < a.do_ && h0 + r < a.ho && ow < a.wo;
+        zv[r] = *reinterpret_cast<const f32x4*>(fb.z + (ok ? (((n * fb.zd + vd) * fb.zh + vh) * fb.zw + vw) * C + 4 * g : 0));
       }
 #pragma unroll
       for (int r = 0; r < N_TH; ++r)
+        if (od < a.do_ && h0 + r < a.ho && ow < a.wo) {
 #pragma unroll
-        for (int jj = 0; jj < 4; ++jj) {
-          const int ow = w0 + 4 * g + jj;
-          if (od < a.do_ && h0 + r < a.ho && ow < a.wo) {
-            const float gg = acc[r][jj] * act_grad(zv[r][jj] * fsc + fsh, fb.act, fb.slope);
-            fp1 += gg;
-            fp2 += gg * (zv[r][jj] - fmean) * finv;
+          for (int jj = 0; jj < 4; ++jj) {
+            const float gg = acc[r][jj] * act_grad(zv[r][jj] * fsc[jj] + fsh[jj], fb.act, fb.slope);
+            fp1[jj] += gg;
+            fp2[jj] += gg * (zv[r][jj] - fmean[jj]) * finv[jj];
           }
         }
     }
     if (stats || bn_part || acc1) {  // tile (sum, M2 about the tile mean), merged into the block's running statistics
       const int vd = min(N_TD, a.do_ - d0), vh = min(N_TH, a.ho - h0), vw = min(N_TW, a.wo - w0);
       const float tn = (float)(vd * vh * vw);
-      s1 += __shfl_xor(s1, 16, 64);
-      s1 += __shfl_xor(s1, 32, 64);
-      if (g == 0) red[wave][r16] = s1;
+      float tmean[4], q[4];
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj) s1[jj] = k7m_rowsum16(s1[jj]);
+      if (r16 == 0) {
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) red[wave][4 * g + jj] = s1[jj];
+      }
       __syncthreads();
-      const float tmean = (red[0][r16] + red[1][r16] + red[2][r16] + red[3][r16]) / tn;
-      float q = 0.f;
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj) {
+        const int c = 4 * g + jj;
+        tmean[jj] = (red[0][c] + red[1][c] + red[2][c] + red[3][c]) / tn;
+        q[jj] = 0.f;
+      }
+      const float tmu = tid < C ? (red[0][tid] + red[1][tid] + red[2][tid] + red[3][tid]) / tn : 0.f;
 #pragma unroll
       for (int r = 0; r < N_TH; ++r) {
-        const int oh = h0 + r;
+        const bool ok = od < a.do_ && h0 + r < a.ho && ow < a.wo;
 #pragma unroll
         for (int jj = 0; jj < 4; ++jj) {
-          const int ow = w0 + 4 * g + jj;
-          const float dv = (od < a.do_ && oh < a.ho && ow < a.wo) ? acc[r][jj] - tmean : 0.f;
-          q += dv * dv;
+          const float dv = ok ? acc[r][jj] - tmean[jj] : 0.f;
+          q[jj] += dv * dv;
         }
       }
-      q += __shfl_xor(q, 16, 64);
-      q += __shfl_xor(q, 32, 64);
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj) q[jj] = k7m_rowsum16(q[jj]);
       __syncthreads();
-      if (g == 0) red[wave][r16] = q;
+      if (r16 == 0) {
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) red[wave][4 * g + jj] = q[jj];
+      }
       __syncthreads();
       if (tid < C) {
         const float tm2 = red[0][tid] + red[1][tid] + red[2][tid] + red[3][tid];
-        const float nn = run_n + tn, delta = tmean - run_mean;
+        const float nn = run_n + tn, delta = tmu - run_mean;
         run_mean += delta * (tn / nn);
         run_m2 += tm2 + delta * delta * (run_n * tn / nn);
         run_n = nn;
       }
     }
-    (void)cntl;
   }
   if (stats && tid < C) {  // BatchNorm partials (sum, M2, count) per block, layout of conv.hip
     const long long sb = (long long)blockIdx.x * (2 * C + 1);
@@ -276,13 +292,17 @@ __global__ __launch_bounds__(256, 2) void k7m_n2w_kernel(K7Args a, const float* 
     bn_part[(long long)(C + tid) * gridDim.x + blockIdx.x] = run_m2;
     if (tid == 0) bn_part[(long long)2 * C * gridDim.x + blockIdx.x] = run_n;
   }
-  if (fb.z) {  // folded mode-2 pairs: lanes g -> shuffles, waves -> LDS, into slot blockIdx.x
-    fp1 += __shfl_xor(fp1, 16, 64);
-    fp1 += __shfl_xor(fp1, 32, 64);
-    fp2 += __shfl_xor(fp2, 16, 64);
-    fp2 += __shfl_xor(fp2, 32, 64);
+  if (fb.z) {  // folded mode-2 pairs: voxel lanes -> row sums, waves -> LDS, into slot blockIdx.x
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj) {
+      fp1[jj] = k7m_rowsum16(fp1[jj]);
+      fp2[jj] = k7m_rowsum16(fp2[jj]);
+    }
     __syncthreads();
-    if (g == 0) red[wave][r16] = fp1;
+    if (r16 == 0) {
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj) red[wave][4 * g + jj] = fp1[jj];
+    }
     __syncthreads();
     double* fr = fb.acc ? fb.acc + (long long)(blockIdx.x % fb.reps) * 2 * C : nullptr;
     if (tid < C) {
@@ -291,7 +311,10 @@ __global__ __launch_bounds__(256, 2) void k7m_n2w_kernel(K7Args a, const float* 
       else fb.part[(long long)tid * gridDim.x + blockIdx.x] = q;
     }
     __syncthreads();
-    if (g == 0) red[wave][r16] = fp2;
+    if (r16 == 0) {
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj) red[wave][4 * g + jj] = fp2[jj];
+    }
     __syncthreads();
     if (tid < C) {
       const float q = red[0][tid] + red[1][tid] + red[2][tid] + red[3][tid];
