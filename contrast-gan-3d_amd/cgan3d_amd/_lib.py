@@ -16,7 +16,7 @@ import torch  # noqa: F401  (must be imported first: see module docstring)
 # CGAN3D_LIB_PATH: another build of the same library (back-to-back A/B of two builds, tools/gpu_ab_lib.sh)
 LIB_PATH = Path(os.environ.get("CGAN3D_LIB_PATH") or Path(__file__).resolve().parent / "libcgan3d.so")
 
-ACT_NONE, ACT_RELU, ACT_LRELU, ACT_TANH = 0, 1, 2, 3
+ACT_NONE, ACT_RELU, ACT_LRELU, ACT_TANH, ACT_NEG_DTANH = 0, 1, 2, 3, 4
 WGRAD_ACCUMULATE, WGRAD_WS_CLEAN, WGRAD_DEFER_UNPACK = 1, 2, 4  # cgan3d_conv3d_wgrad_ex flag word
 # device loss slots written by the loss kernels (include/cgan3d.h)
 L_D, L_WD, L_GP, L_G, L_SIM, L_HU, L_GFULL = range(7)
@@ -90,6 +90,7 @@ _SIGS = {
     "cgan3d_conv3d_shadow_only": ([_P, _I32], _I32),
     "cgan3d_conv3d_bn_fold_ok": ([_P], _I32),
     "cgan3d_bn_fuse_ok": ([_P], _I32),
+    "cgan3d_conv3d_neg_dtanh_ok": ([_P], _I32),
     "cgan3d_conv3d_wgrad_group_ok": ([_P], _I32),
     "cgan3d_conv3d_wgrad_group": ([_P, _P, _P, _P, _I32, _P], _I32),
     "cgan3d_conv3d_wgrad_ex": ([_P, _P, _P, _P, _I32, _P, _P, _P, _P], _I32),

@@ -721,7 +721,7 @@ class CriticPlan:
         return t[off * k:]
 
     def input_grad(self, P, off: int, n: int, dx_out: torch.Tensor, dx_off: int, dx_n: int, bn_pass: int = 0,
-                   G=None, bn_accumulate: bool = False):
+                   G=None, bn_accumulate: bool = False, ep0=None):
         """dz chain from dz[-1][off:off+n] (dlogits) down to dz[0]; then dD/dx for samples
         [dx_off, dx_off+dx_n) (absolute indices inside the batch) into dx_out.  BatchNorm layers
         back-propagate with the statistics of ``bn_pass``; their gamma/beta gradients go to ``G``
@@ -758,7 +758,7 @@ class CriticPlan:
         if dx_n > 0:
             g = self._geo(ops.conv_dgrad_geom(dx_n, ly.din, ly.dout, ly.cin, ly.cout, ly.k, ly.s, ly.p, planar=self.pl), self.wd[0])
             w = self.wd[0] if self.wd[0] is not None else P[f"{ly.name}.weight"]
-            ops.conv(g, self._sl(self.dz[0], dx_off, dx_n), w, dx_out)
+            ops.conv(g, self._sl(self.dz[0], dx_off, dx_n), w, dx_out, ep0)
 
     def gp_forward_mode(self, P, gamma: torch.Tensor, off: int, n: int):
         """nu_l = mask_l * conv_l(nu_{l-1}) (no bias), nu_0 = gamma, written in place over
@@ -1044,6 +1044,17 @@ class StepEngine:
         self.dcrit = torch.empty((b_sub, *dims, 1), device=device)       # dL_G/d opt_hat via the critic
         self.losses = torch.zeros(8, device=device)
         self.loss_ws = torch.empty(ops.loss_ws_floats(), device=device)
+        # The generator's similarity / HU losses and their gradient depend only on its forward, so
+        # they run on the generator's side stream beside the critic update (with the zeroing of the
+        # generator's gradient arena); the critic's first-layer input-grad of the generator update
+        # then folds its adversarial gradient through the output tanh into G.dz_last in place
+        # (CGAN3D_ACT_NEG_DTANH).  CGAN3D_NO_GLOSS_SIDE=1: everything after that input-grad (A/B).
+        g0 = self.D.layers[0]
+        self.gloss_side = (self.G.side is not None and not os.environ.get("CGAN3D_NO_GLOSS_SIDE") and
+                           ops.neg_dtanh_ok(self.D._geo(ops.conv_dgrad_geom(b_sub, g0.din, g0.dout, g0.cin, g0.cout, g0.k,
+                                                                             g0.s, g0.p, planar=self.D.pl),
+                                                        self.D.wd[0])))
+        self.loss_ws_g = torch.empty(ops.loss_ws_floats(), device=device) if self.gloss_side else self.loss_ws
         self._pending = []  # in-flight bucket all-reduces of the generator gradients
         self.g_buckets = self._make_g_buckets(G_BUCKET_BYTES) if (self.dp and G_BUCKET_BYTES > 0) else []
         on_gpu = torch.device(device).type == "cuda"
@@ -1194,6 +1205,16 @@ class StepEngine:
     # -------------------------------------------------------------------------------------------
     def generator_forward(self):
         self.G.forward(self.gP, self.subopt, opt_hat_out=self.opt_hat, training=True)
+        if self.gloss_side:
+            self.G._on_side(self._generator_loss_grad)
+
+    def _generator_loss_grad(self):
+        """ZNCC + HU losses (Trainer.py:148-157) and their gradient through the output tanh into
+        G.dz_last; optimizer_G.zero_grad (Trainer.py:146) of the gradient arena."""
+        bs, V = self.b_sub, self.vox
+        ops.generator_output_grad(self.opt_hat, self.subopt, self.G.att, self.mask, None, bs * V, self.lo, self.hi,
+                                  self.sim_w, self.hu_w, self.G.dz_last, self.losses, self.loss_ws_g)
+        ops.zero(self.g_arena.grad_padded)
 
     def critic_update(self):
         if not self.use_gp:
@@ -1237,12 +1258,18 @@ class StepEngine:
 
     def generator_update(self):
         D, bs, V = self.D, self.b_sub, self.vox
+        if self.gloss_side:  # the loss gradient and the zeroed arena (generator_forward) are in
+            ops.stream_wait(torch.cuda.current_stream(self.device), self.G.side)
         D.forward(self.dP, self.opt_hat, 0, bs)
         ops.generator_logits_grad(D.a[-1][:bs], bs * D.logit_ps, self.gan_w, D.dz[-1], self.losses)
-        D.input_grad(self.dP, 0, bs, self.dcrit, 0, bs)
-        ops.generator_output_grad(self.opt_hat, self.subopt, self.G.att, self.mask, self.dcrit, bs * V, self.lo,
-                                  self.hi, self.sim_w, self.hu_w, self.G.dz_last, self.losses, self.loss_ws)
-        ops.zero(self.g_arena.grad_padded)  # optimizer_G.zero_grad (Trainer.py:146): every layer then accumulates
+        if self.gloss_side:
+            D.input_grad(self.dP, 0, bs, self.G.dz_last, 0, bs,
+                         ep0=ops.epilogue(residual=self.G.dz_last, mask_src=self.G.att, act=L.ACT_NEG_DTANH))
+        else:
+            D.input_grad(self.dP, 0, bs, self.dcrit, 0, bs)
+            ops.generator_output_grad(self.opt_hat, self.subopt, self.G.att, self.mask, self.dcrit, bs * V, self.lo,
+                                      self.hi, self.sim_w, self.hu_w, self.G.dz_last, self.losses, self.loss_ws)
+            ops.zero(self.g_arena.grad_padded)  # optimizer_G.zero_grad (Trainer.py:146): every layer then accumulates
         if self.dp and self.g_buckets:  # bucketed, overlapped with the rest of the backward
             self.G.backward(self.gP, self.gG, self.subopt, grads_enqueued=self._bucket_ready, zeroed=True)
             self._finish_allreduce()

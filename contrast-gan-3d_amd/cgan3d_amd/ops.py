@@ -207,6 +207,11 @@ class BnFuse:
         return f
 
 
+def neg_dtanh_ok(g) -> bool:
+    """cgan3d_conv3d_neg_dtanh_ok: the input-grad geometry takes the CGAN3D_ACT_NEG_DTANH epilogue."""
+    return bool(L.load().cgan3d_conv3d_neg_dtanh_ok(ctypes.byref(g)))
+
+
 def bn_fuse_ok(g) -> bool:
     """True if the launch of ``g`` can produce BnFuse accumulators."""
     return bool(L.load().cgan3d_bn_fuse_ok(ctypes.byref(g)))

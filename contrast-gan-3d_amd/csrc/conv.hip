@@ -529,6 +529,10 @@ static Epi to_epi(const cgan3d_epilogue* ep) {
   return e;
 }
 
+extern "C" int32_t cgan3d_conv3d_neg_dtanh_ok(const cgan3d_conv_geom* g) {
+  return g && !g->planar && c1_dgrad_ok(g) ? 1 : 0;
+}
+
 extern "C" int32_t cgan3d_bn_fuse_ok(const cgan3d_conv_geom* g) {
   if (!g || validate(g, "cgan3d_bn_fuse_ok")) return 0;
   // the halo-tiled family (halo_epilogue, the stride-2 16 <-> 32 kernels) and the generator's
@@ -604,6 +608,8 @@ extern "C" int cgan3d_conv3d_fwd(const cgan3d_conv_geom* g, const float* x, cons
     return CGAN3D_OK;
   }
   if (g->planar) goto cout1;  // cout == 1: the VALU kernels below
+  CG_CHECK_ARG(e.act != CGAN3D_ACT_NEG_DTANH || (!g->planar && c1_dgrad_ok(g)),
+               "cgan3d_conv3d_fwd: CGAN3D_ACT_NEG_DTANH only on the critic's first-layer input-grad");
   if (c1_fwd_ok(g) || c1_dgrad_ok(g)) {  // critic first layer (conv_c1.hip)
     CG_CHECK_ARG(!e.bn_mode, "cgan3d_conv3d_fwd: no BatchNorm statistics on the single-channel critic layer");
     const int rc = g->transposed ? c1_dgrad_launch(g, x, w, y, e, s) : c1_fwd_launch(g, x, w, y, e, s);

@@ -113,8 +113,10 @@ __global__ __launch_bounds__(256) void c1_fwd_kernel(C1Args a, const float* __re
 
 // input-grad: dx[i] = sum_{t, o : i = 2o - 1 + t} sum_c dz[o][c] * w[c][t]  (i on the fine grid)
 // a.di.. = coarse (dz) dims, a.do_.. = fine (dx) dims; tile = 2 x 8 x 16 fine voxels
+// res / tnh (CGAN3D_ACT_NEG_DTANH): dx = res - acc * (1 - tnh^2), in place over res allowed
 __global__ __launch_bounds__(256) void c1_dgrad_kernel(C1Args a, const float* __restrict__ dz,
-                                                       const float* __restrict__ w, float* dx) {
+                                                       const float* __restrict__ w, float* dx, const float* res,
+                                                       const float* __restrict__ tnh) {
   constexpr int GZ = c1::TZ / 2 + 2, GY = c1::TY / 2 + 2, GX = c1::TX / 2 + 2;  // coarse window 3 x 6 x 10
   __shared__ __attribute__((aligned(16))) float gs[GZ * GY * GX * 8];
   __shared__ __attribute__((aligned(16))) float ws[64 * 8];  // [tap][c]
@@ -163,7 +165,14 @@ __global__ __launch_bounds__(256) void c1_dgrad_kernel(C1Args a, const float* __
 #pragma unroll
         for (int c = 0; c < 4; ++c) acc = fmaf(g1[c], w1[c], acc);
       }
-  if (oz < a.do_ && oy < a.ho && ox < a.wo) dx[(((long long)nb * a.do_ + oz) * a.ho + oy) * a.wo + ox] = acc;
+  if (oz < a.do_ && oy < a.ho && ox < a.wo) {
+    const long long o = (((long long)nb * a.do_ + oz) * a.ho + oy) * a.wo + ox;
+    if (tnh) {
+      const float t = tnh[o];
+      acc = res[o] - acc * (1.f - t * t);
+    }
+    dx[o] = acc;
+  }
 }
 
 // weight-grad: dw[b][t] += sum_{n,o} x[2o - 1 + t] * dz[o][b]; lane = tap, 4 waves split a tile's
@@ -278,11 +287,13 @@ int c1_fwd_launch(const cgan3d_conv_geom* g, const float* x, const float* w, flo
 
 int c1_dgrad_launch(const cgan3d_conv_geom* g, const float* dz, const float* w, float* dx, const Epi& e,
                     hipStream_t st) {
-  CG_CHECK_ARG(!e.bias && !e.residual && !e.mask_src && !e.minuend && !e.out2 && !e.stats && !e.bn_mode &&
-                   e.act == CGAN3D_ACT_NONE,
-               "conv c1 input-grad: no epilogue");
+  const bool fold = e.act == CGAN3D_ACT_NEG_DTANH;
+  CG_CHECK_ARG(!e.bias && !e.minuend && !e.out2 && !e.stats && !e.bn_mode &&
+                   (fold ? (e.residual && e.mask_src) : (e.act == CGAN3D_ACT_NONE && !e.residual && !e.mask_src)),
+               "conv c1 input-grad: no epilogue but CGAN3D_ACT_NEG_DTANH (residual + mask_src)");
   C1Args a = c1_args(g);
-  ::cg::launch(c1_dgrad_kernel, dim3(a.n * a.tz * a.ty * a.tx), dim3(256), 0, st, a, dz, w, dx);
+  ::cg::launch(c1_dgrad_kernel, dim3(a.n * a.tz * a.ty * a.tx), dim3(256), 0, st, a, dz, w, dx,
+               fold ? e.residual : nullptr, fold ? e.mask_src : nullptr);
   return CGAN3D_OK;
 }
 

@@ -55,7 +55,12 @@ __global__ __launch_bounds__(256) void gen_logits_kernel(const float* __restrict
   for (int i = threadIdx.x; i < n; i += blockDim.x) s += logits[i];
   s = block_sum_d(s, red);
   for (int i = threadIdx.x; i < n; i += blockDim.x) dl[i] = -gan_w / (float)n;
-  if (threadIdx.x == 0) losses[L_G] = (float)(-gan_w * s / n);
+  if (threadIdx.x == 0) {
+    losses[L_G] = (float)(-gan_w * s / n);
+    // the full generator loss, when the similarity / HU terms were computed first (beside the
+    // critic update); cgan3d_generator_output_grad writes it again when it runs after this
+    losses[L_GFULL] = losses[L_G] + losses[L_SIM] + losses[L_HU];
+  }
 }
 
 // --- gradient penalty -------------------------------------------------------------------

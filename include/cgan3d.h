@@ -72,6 +72,12 @@ typedef struct cgan3d_conv_geom {
 #define CGAN3D_ACT_RELU 1
 #define CGAN3D_ACT_LRELU 2
 #define CGAN3D_ACT_TANH 3
+/* epilogue of the critic's first-layer input-grad only (cgan3d_conv3d_neg_dtanh_ok): the generator's
+ * adversarial gradient taken through its output tanh and added to the loss part in place,
+ *   out = residual - v * (1 - mask_src^2)     (mask_src = the generator's tanh output att,
+ * opt_hat = subopt - att: generator.py:86-88; Trainer.py:148-157), so the generator's losses and
+ * their gradient can be computed beside the critic update and only this fold stays on the path. */
+#define CGAN3D_ACT_NEG_DTANH 4
 
 /* Fused epilogue: v = acc (+ bias[c]); v = act(v); v *= (mask_src > 0 ? 1 : slope) if mask_src;
  * v += residual if residual; out = v; if out2: out2 = minuend - v (cout == 1 only).
@@ -131,6 +137,9 @@ typedef struct cgan3d_epilogue {
 
 /* 1 when the geometry's launch can produce cgan3d_bn_fuse accumulators. */
 int32_t cgan3d_bn_fuse_ok(const cgan3d_conv_geom* g);
+/* 1 when the input-grad geometry takes the CGAN3D_ACT_NEG_DTANH epilogue (the critic's first layer,
+ * discriminator.py:55-60, 1 -> 8 k4 s2 p1). */
+int32_t cgan3d_conv3d_neg_dtanh_ok(const cgan3d_conv_geom* g);
 
 const char* cgan3d_version(void);
 const char* cgan3d_get_last_error(void);
