@@ -47,9 +47,6 @@ WGRAD_GROUP = max(1, int(os.environ.get("CGAN3D_WGRAD_GROUP", "2")))
 # on the main stream: nothing is left there to overlap them with, and on the side stream they cost
 # two cross-stream hand-offs and share the chip with the stride-2 input-grad
 WGRAD_TAIL_MAIN = max(0, int(os.environ.get("CGAN3D_WGRAD_TAIL_MAIN", "2")))
-# the last conv's weight grad goes to the side stream after (1) or beside (0) its input-grad: both are
-# k7 kernels that want the whole chip (A/B switch CGAN3D_LAST_WGRAD_AFTER)
-LAST_WGRAD_AFTER = os.environ.get("CGAN3D_LAST_WGRAD_AFTER", "0") == "1"
 # data parallelism: generator gradient bucket size (all-reduce started per bucket during the backward)
 # (measured on one GPU over a one-rank RCCL group: each extra bucket ~15 us of step time, so the
 # default makes ~2-3 buckets of the 4.1 MB arena: 2.21 ms/step at 1 MB, 2.16 with 2 buckets)
@@ -419,11 +416,16 @@ class GeneratorPlan:
         n = self.n
         u = self.y[-1]
 
-        def last_wgrad():
-            self._on_side(lambda: self._wgrad(self.geo_last_wgrad, u, self.dz_last, G["model.last_conv.weight"],
-                                              zeroed, gathered16=self.y16[-1] if self.y_dead[-1] else None))
-        if not LAST_WGRAD_AFTER:
-            last_wgrad()
+        nvl = n * la.dout[0] * la.dout[1] * la.dout[2]
+        key = (id(G), "last_bias")
+        if key not in self._csum:
+            self._csum[key] = ops.ChannelSumSet(self.device, [(self.dz_last, nvl, 1, G["model.last_conv.bias"], False)])
+
+        # the last conv's weight and bias grads, beside its input-grad when there is a side stream
+        # (measured: after the input-grad instead, 1.78 vs 1.76 ms/step)
+        self._on_side(lambda: (self._wgrad(self.geo_last_wgrad, u, self.dz_last, G["model.last_conv.weight"],
+                                           zeroed, gathered16=self.y16[-1] if self.y_dead[-1] else None),
+                               self._csum[key].run()))
         pending = []  # (layer, weight-grad launcher) not yet handed to the side stream
 
         def flush():
@@ -433,11 +435,6 @@ class GeneratorPlan:
                 for j, _ in pending:
                     grads_enqueued(j)
             pending.clear()
-        nvl = n * la.dout[0] * la.dout[1] * la.dout[2]
-        key = (id(G), "last_bias")
-        if key not in self._csum:
-            self._csum[key] = ops.ChannelSumSet(self.device, [(self.dz_last, nvl, 1, G["model.last_conv.bias"], False)])
-        self._csum[key].run()
         if grads_enqueued is not None:
             grads_enqueued(len(self.layers))
         if self.fold_bn:
@@ -448,8 +445,6 @@ class GeneratorPlan:
             ops.conv(self.geo_last_dgrad, self.dz_last, P["model.last_conv.weight"], self.dpad)
             ops.reflect_fold(self.dpad, self.dy[-1], n, la.din, la.cin, la.p,
                              ep=self._bn_grad_epi(len(self.layers) - 1), planar=self.planar)
-        if LAST_WGRAD_AFTER:
-            last_wgrad()
 
         def resnet_pair(j):  # layers j and j - 1 both in the ResNet chain
             return "resnet_backbone" in self.layers[j].name and "resnet_backbone" in self.layers[j - 1].name
