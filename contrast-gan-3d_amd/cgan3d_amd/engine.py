@@ -1050,6 +1050,12 @@ class StepEngine:
                                                                              g0.s, g0.p, planar=self.D.pl),
                                                         self.D.wd[0])))
         self.loss_ws_g = torch.empty(ops.loss_ws_floats(), device=device) if self.gloss_side else self.loss_ws
+        # the gradient penalty's per-sample sums of squares straight from the critic's first-layer
+        # input-grad (one float per block; CGAN3D_NO_GP_PART=1: a separate reduction pass, A/B)
+        nsq = ops.sumsq_blocks(self.D._geo(ops.conv_dgrad_geom(self.b_gp, g0.din, g0.dout, g0.cin, g0.cout, g0.k, g0.s,
+                                                               g0.p, planar=self.D.pl), self.D.wd[0]))
+        self.gp_part = (torch.empty(nsq, device=device) if nsq and self.b_gp and self.use_gp and not self.D.ln and
+                        not os.environ.get("CGAN3D_NO_GP_PART") else None)
         self._pending = []  # in-flight bucket all-reduces of the generator gradients
         self.g_buckets = self._make_g_buckets(G_BUCKET_BYTES) if (self.dp and G_BUCKET_BYTES > 0) else []
         on_gpu = torch.device(device).type == "cuda"
@@ -1219,7 +1225,8 @@ class StepEngine:
         ops.gp_interpolate(self.xc[:bg], self.xc[bo:bo + bg], self.eps, self.xc[bo + bs:], bg, V)
         D.forward(self.dP, self.xc, 0, nall)
         ops.critic_logits_grad(D.a[-1], bo, bs, bg, D.logit_ps, self.gan_w, D.dz[-1], self.losses)
-        D.input_grad(self.dP, 0, nall, self.gbuf, bo + bs, bg)
+        D.input_grad(self.dP, 0, nall, self.gbuf, bo + bs, bg,
+                     ep0=ops.epilogue(stats=self.gp_part) if self.gp_part is not None else None)
         if D.ln:  # LayerNorm critic: the interpolation stays in xc (its primal adjoint needs it)
             gamma = D.gam[:bg]
             ops.gradient_penalty(self.gbuf, bg, V, self.gp_weight, gamma, self.losses, self.loss_ws)
@@ -1229,7 +1236,11 @@ class StepEngine:
             self._optim_step(self.d_optim, self.D)
             return
         gamma = self.xc[bo + bs:]
-        ops.gradient_penalty(self.gbuf, bg, V, self.gp_weight, gamma, self.losses, self.loss_ws)
+        if self.gp_part is not None:  # the input-grad wrote the per-sample sums of squares
+            ops.gradient_penalty_part(self.gbuf, self.gp_part, bg, self.gp_part.numel() // bg, V, self.gp_weight,
+                                      gamma, self.losses)
+        else:
+            ops.gradient_penalty(self.gbuf, bg, V, self.gp_weight, gamma, self.losses, self.loss_ws)
         ops.zero(self.d_arena.grad_padded)  # optimizer_D.zero_grad (Trainer.py:109): every layer then accumulates
         D.gp_grads_overlapped(self.dP, self.dG, self.xc, gamma, bo + bs, bg, nall, bo + bs, zeroed=True)
         D.join_side()

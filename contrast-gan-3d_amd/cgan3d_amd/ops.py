@@ -485,8 +485,8 @@ def conv(g: ConvGeom, x: torch.Tensor, w: torch.Tensor, y: torch.Tensor, ep: Opt
         for nm in ("residual", "mask_src", "minuend", "out2"):
             if getattr(ep, nm) is not None:
                 _need(getattr(ep, nm), ny, f"conv {nm}")
-        if ep.stats is not None:
-            _need(ep.stats, stats_floats(g), "conv stats", exact=False)
+        if ep.stats is not None:  # the critic first-layer input-grad: per-block sums of squares
+            _need(ep.stats, sumsq_blocks(g) or stats_floats(g), "conv stats", exact=False)
         if ep.x_bf16 is not None:
             _need(ep.x_bf16, _vox_in(g) * g.cin, "conv x_bf16", dtype=torch.bfloat16)
         f = ep.bn_fold
@@ -969,6 +969,21 @@ def gradient_penalty(grad, b, per_sample, lambda_, gamma_out, losses, ws):
     _need(ws, loss_ws_floats(), "gradient_penalty ws", exact=False)
     check(_launch("cgan3d_gradient_penalty", ptr(grad), b, per_sample, lambda_, ptr(gamma_out), ptr(losses),
                   ptr(ws)), "gradient_penalty")
+
+
+def gradient_penalty_part(grad, part, b, chunks, per_sample, lambda_, gamma_out, losses):
+    """cgan3d_gradient_penalty_part: the GP from per-sample partial sums of squares part[b][chunks]."""
+    _need(grad, b * per_sample, "gradient_penalty_part grad")
+    _need(part, b * chunks, "gradient_penalty_part part", exact=False)
+    _need(gamma_out, b * per_sample, "gradient_penalty_part gamma")
+    _need(losses, 8, "losses")
+    check(_launch("cgan3d_gradient_penalty_part", ptr(grad), ptr(part), b, chunks, per_sample, lambda_,
+                  ptr(gamma_out), ptr(losses)), "gradient_penalty_part")
+
+
+def sumsq_blocks(g) -> int:
+    """cgan3d_conv3d_sumsq_blocks: per-block sum-of-squares slots of an input-grad launch (0: none)."""
+    return int(L.load().cgan3d_conv3d_sumsq_blocks(ctypes.byref(g)))
 
 
 def generator_logits_grad(logits, n, gan_w, dlogits, losses):

@@ -225,6 +225,7 @@ long long halo_mblocks(const cgan3d_conv_geom* g);
 int halo_launch(const cgan3d_conv_geom* g, const float* x, const float* w, float* y, const Epi& e, hipStream_t st);
 // stride-2 16 <-> 32-channel convs (conv_s2.hip), part of the halo (format 2) family
 int cu_count();  // compute units of the current device
+long long c1_dgrad_blocks(const cgan3d_conv_geom* g);
 int s2_kind(const cgan3d_conv_geom* g);
 long long s2_blocks(const cgan3d_conv_geom* g);
 int s2_launch(const cgan3d_conv_geom* g, const float* x, const __bf16* wp, float* y, const Epi& e, hipStream_t st);

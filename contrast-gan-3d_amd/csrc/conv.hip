@@ -529,6 +529,8 @@ static Epi to_epi(const cgan3d_epilogue* ep) {
   return e;
 }
 
+extern "C" int64_t cgan3d_conv3d_sumsq_blocks(const cgan3d_conv_geom* g) { return g ? c1_dgrad_blocks(g) : 0; }
+
 extern "C" int32_t cgan3d_conv3d_neg_dtanh_ok(const cgan3d_conv_geom* g) {
   return g && !g->planar && c1_dgrad_ok(g) ? 1 : 0;
 }
@@ -612,6 +614,7 @@ extern "C" int cgan3d_conv3d_fwd(const cgan3d_conv_geom* g, const float* x, cons
                "cgan3d_conv3d_fwd: CGAN3D_ACT_NEG_DTANH only on the critic's first-layer input-grad");
   if (c1_fwd_ok(g) || c1_dgrad_ok(g)) {  // critic first layer (conv_c1.hip)
     CG_CHECK_ARG(!e.bn_mode, "cgan3d_conv3d_fwd: no BatchNorm statistics on the single-channel critic layer");
+    CG_CHECK_ARG(!e.stats || c1_dgrad_blocks(g), "cgan3d_conv3d_fwd: stats on the critic's first layer: input-grad only");
     const int rc = g->transposed ? c1_dgrad_launch(g, x, w, y, e, s) : c1_fwd_launch(g, x, w, y, e, s);
     if (rc) return rc;
     CG_LAUNCH_CHECK("conv_c1");

@@ -113,10 +113,12 @@ __global__ __launch_bounds__(256) void c1_fwd_kernel(C1Args a, const float* __re
 
 // input-grad: dx[i] = sum_{t, o : i = 2o - 1 + t} sum_c dz[o][c] * w[c][t]  (i on the fine grid)
 // a.di.. = coarse (dz) dims, a.do_.. = fine (dx) dims; tile = 2 x 8 x 16 fine voxels
-// res / tnh (CGAN3D_ACT_NEG_DTANH): dx = res - acc * (1 - tnh^2), in place over res allowed
+// res / tnh (CGAN3D_ACT_NEG_DTANH): dx = res - acc * (1 - tnh^2), in place over res allowed.
+// sq (optional): sq[block] = sum of dx^2 over the block's outputs (the gradient penalty's per-sample
+// norms, cgan3d_gradient_penalty_part: a block never spans two samples)
 __global__ __launch_bounds__(256) void c1_dgrad_kernel(C1Args a, const float* __restrict__ dz,
                                                        const float* __restrict__ w, float* dx, const float* res,
-                                                       const float* __restrict__ tnh) {
+                                                       const float* __restrict__ tnh, float* sq) {
   constexpr int GZ = c1::TZ / 2 + 2, GY = c1::TY / 2 + 2, GX = c1::TX / 2 + 2;  // coarse window 3 x 6 x 10
   __shared__ __attribute__((aligned(16))) float gs[GZ * GY * GX * 8];
   __shared__ __attribute__((aligned(16))) float ws[64 * 8];  // [tap][c]
@@ -165,13 +167,23 @@ __global__ __launch_bounds__(256) void c1_dgrad_kernel(C1Args a, const float* __
 #pragma unroll
         for (int c = 0; c < 4; ++c) acc = fmaf(g1[c], w1[c], acc);
       }
-  if (oz < a.do_ && oy < a.ho && ox < a.wo) {
+  const bool inside = oz < a.do_ && oy < a.ho && ox < a.wo;
+  if (inside) {
     const long long o = (((long long)nb * a.do_ + oz) * a.ho + oy) * a.wo + ox;
     if (tnh) {
       const float t = tnh[o];
       acc = res[o] - acc * (1.f - t * t);
     }
     dx[o] = acc;
+  }
+  if (sq) {  // the block's sum of squares: waves by shuffles, then 4 partials through LDS (ws is free)
+    float v = inside ? acc * acc : 0.f;
+#pragma unroll
+    for (int m = 1; m < 64; m <<= 1) v += __shfl_xor(v, m, 64);
+    __syncthreads();
+    if ((tid & 63) == 0) ws[tid >> 6] = v;
+    __syncthreads();
+    if (tid == 0) sq[blockIdx.x] = (ws[0] + ws[1]) + (ws[2] + ws[3]);
   }
 }
 
@@ -268,6 +280,11 @@ bool c1_dgrad_ok(const cgan3d_conv_geom* g) {
 }
 bool c1_wgrad_ok(const cgan3d_conv_geom* g) { return c1_fwd_ok(g); }
 
+long long c1_dgrad_blocks(const cgan3d_conv_geom* g) {  // per-block sum-of-squares slots (cgan3d_conv3d_sumsq_blocks)
+  if (g->planar || !c1_dgrad_ok(g)) return 0;
+  return (long long)g->n * ceil_div(g->do_, c1::TZ) * ceil_div(g->ho, c1::TY) * ceil_div(g->wo, c1::TX);
+}
+
 static C1Args c1_args(const cgan3d_conv_geom* g) {
   C1Args a;
   a.n = g->n; a.di = g->di; a.hi = g->hi; a.wi = g->wi; a.do_ = g->do_; a.ho = g->ho; a.wo = g->wo;
@@ -288,12 +305,12 @@ int c1_fwd_launch(const cgan3d_conv_geom* g, const float* x, const float* w, flo
 int c1_dgrad_launch(const cgan3d_conv_geom* g, const float* dz, const float* w, float* dx, const Epi& e,
                     hipStream_t st) {
   const bool fold = e.act == CGAN3D_ACT_NEG_DTANH;
-  CG_CHECK_ARG(!e.bias && !e.minuend && !e.out2 && !e.stats && !e.bn_mode &&
+  CG_CHECK_ARG(!e.bias && !e.minuend && !e.out2 && !e.bn_mode &&
                    (fold ? (e.residual && e.mask_src) : (e.act == CGAN3D_ACT_NONE && !e.residual && !e.mask_src)),
                "conv c1 input-grad: no epilogue but CGAN3D_ACT_NEG_DTANH (residual + mask_src)");
   C1Args a = c1_args(g);
   ::cg::launch(c1_dgrad_kernel, dim3(a.n * a.tz * a.ty * a.tx), dim3(256), 0, st, a, dz, w, dx,
-               fold ? e.residual : nullptr, fold ? e.mask_src : nullptr);
+               fold ? e.residual : nullptr, fold ? e.mask_src : nullptr, e.stats);
   return CGAN3D_OK;
 }
 

@@ -86,13 +86,26 @@ __global__ __launch_bounds__(256) void gp_scale_kernel(const float* __restrict__
   __shared__ double red[4];
   __shared__ float coef[1024];
   double acc = 0.0;
-  for (int b = threadIdx.x; b < B; b += blockDim.x) {
-    double ss = 0.0;
-    for (int c = 0; c < chunks; ++c) ss += part[(long long)b * chunks + c];
-    const double nrm = sqrt(ss);
-    acc += (nrm - 1.0) * (nrm - 1.0);
-    // d/dg_b of lambda*mean((||g_b||-1)^2) = lambda * 2/B * (||g_b||-1) * g_b/||g_b||  (0 at ||g_b||=0)
-    coef[b] = nrm > 0.0 ? (float)(lambda_ * 2.0 / B * (nrm - 1.0) / nrm) : 0.f;
+  if (chunks >= 64) {  // many partials per sample: the block sums each sample's together
+    for (int b = 0; b < B; ++b) {
+      double ss = 0.0;
+      for (int c = threadIdx.x; c < chunks; c += blockDim.x) ss += part[(long long)b * chunks + c];
+      ss = block_sum_d(ss, red);
+      if (threadIdx.x == 0) {
+        const double nrm = sqrt(ss);
+        acc += (nrm - 1.0) * (nrm - 1.0);
+        coef[b] = nrm > 0.0 ? (float)(lambda_ * 2.0 / B * (nrm - 1.0) / nrm) : 0.f;
+      }
+    }
+  } else {
+    for (int b = threadIdx.x; b < B; b += blockDim.x) {
+      double ss = 0.0;
+      for (int c = 0; c < chunks; ++c) ss += part[(long long)b * chunks + c];
+      const double nrm = sqrt(ss);
+      acc += (nrm - 1.0) * (nrm - 1.0);
+      // d/dg_b of lambda*mean((||g_b||-1)^2) = lambda * 2/B * (||g_b||-1) * g_b/||g_b||  (0 at ||g_b||=0)
+      coef[b] = nrm > 0.0 ? (float)(lambda_ * 2.0 / B * (nrm - 1.0) / nrm) : 0.f;
+    }
   }
   acc = block_sum_d(acc, red);  // (its barriers also publish coef)
   if (blockIdx.x == 0 && threadIdx.x == 0) {
@@ -230,6 +243,20 @@ extern "C" int cgan3d_gradient_penalty(const float* grad, int32_t b, int64_t per
   const long long total = (long long)b * per_sample;
   int blocks = (int)std::min<long long>((total + 255) / 256, 1024);
   ::cg::launch(gp_scale_kernel, dim3(blocks), dim3(256), 0, s, part, b, chunks, lambda_, losses, grad,
+               (long long)per_sample, total, gamma_out);
+  CG_LAUNCH_CHECK("gp_scale_kernel");
+  return CGAN3D_OK;
+}
+
+extern "C" int cgan3d_gradient_penalty_part(const float* grad, const float* part, int32_t b, int32_t chunks,
+                                            int64_t per_sample, float lambda_, float* gamma_out, float* losses,
+                                            void* stream) {
+  CG_CHECK_ARG(grad && part && gamma_out && losses, "cgan3d_gradient_penalty_part: null pointer");
+  CG_CHECK_ARG(b > 0 && b <= 1024 && chunks > 0 && per_sample > 0, "cgan3d_gradient_penalty_part: bad sizes");
+  const long long total = (long long)b * per_sample;
+  // every block sums the b x chunks partials itself: fewer, longer blocks when there are many
+  int blocks = (int)std::min<long long>((total + 255) / 256, chunks >= 64 ? 256 : 1024);
+  ::cg::launch(gp_scale_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, part, b, chunks, lambda_, losses, grad,
                (long long)per_sample, total, gamma_out);
   CG_LAUNCH_CHECK("gp_scale_kernel");
   return CGAN3D_OK;

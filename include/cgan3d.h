@@ -140,6 +140,10 @@ int32_t cgan3d_bn_fuse_ok(const cgan3d_conv_geom* g);
 /* 1 when the input-grad geometry takes the CGAN3D_ACT_NEG_DTANH epilogue (the critic's first layer,
  * discriminator.py:55-60, 1 -> 8 k4 s2 p1). */
 int32_t cgan3d_conv3d_neg_dtanh_ok(const cgan3d_conv_geom* g);
+/* Blocks of the input-grad launch when the geometry (the critic's first layer) can write the
+ * per-block sum of squares of its output: then cgan3d_epilogue.stats = float[blocks], the blocks
+ * of sample s being [s * blocks / n, (s + 1) * blocks / n); 0 when it cannot. */
+int64_t cgan3d_conv3d_sumsq_blocks(const cgan3d_conv_geom* g);
 
 const char* cgan3d_version(void);
 const char* cgan3d_get_last_error(void);
@@ -379,6 +383,10 @@ int cgan3d_critic_logits_grad(const float* logits, int32_t n_real, int32_t n_fak
                               void* stream);
 int cgan3d_gradient_penalty(const float* grad, int32_t b, int64_t per_sample, float lambda_,
                             float* gamma_out, float* losses, float* ws, void* stream);
+/* The same from per-sample partial sums of squares already made (part[s * chunks + c], e.g. by the
+ * critic's first-layer input-grad with cgan3d_conv3d_sumsq_blocks): one scaling pass. */
+int cgan3d_gradient_penalty_part(const float* grad, const float* part, int32_t b, int32_t chunks, int64_t per_sample,
+                                 float lambda_, float* gamma_out, float* losses, void* stream);
 int cgan3d_generator_logits_grad(const float* logits, int32_t n, float gan_w, float* dlogits,
                                  float* losses, void* stream);
 int cgan3d_generator_output_grad(const float* opt_hat, const float* subopt, const float* att,
