@@ -276,6 +276,9 @@ __device__ __forceinline__ AdamK adam_k(const float* hyper, float step) {
   return k;
 }
 __device__ __forceinline__ void adam_vals(const AdamK& k, float gi, float& mi, float& vi, float& pi) {
+  // no contraction: the float4 path (cgan3d_adam) and the per-element path with packed copies
+  // (cgan3d_adam_pack) must leave the same bits whatever the compiler fuses in either context
+#pragma clang fp contract(off)
   // torch lerp: weight < 0.5 ? self + w*(end-self) : end - (end-self)*(1-w)
   mi = k.wgt < 0.5f ? mi + k.wgt * (gi - mi) : gi - (gi - mi) * (1.f - k.wgt);
   vi = vi * k.b2 + (1.f - k.b2) * gi * gi;
