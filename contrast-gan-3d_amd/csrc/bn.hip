@@ -720,7 +720,8 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_acc_kernel(const double* __r
 // blocks of the accumulator passes: ~2 float4 per thread, at most `cap` blocks — each block reads the
 // replicas once (reps x 2C doubles, 4-16 KB, values the atomics left at the memory side): measured at
 // 64^3 B=4, the 16-channel passes took 19.5 / 28 us with 4096 blocks against 13.9 / 15.4 with 1024,
-// the reflect-folded backward (a gather) 46 us with 4096 against 60 with 1024
+// the reflect-folded backward (a gather) 46 us with 4096 against 60 with 1024; the whole step with
+// 1 / 2 / 3 / 4 / 8 float4 per thread (round 3): 1.629 / 1.613 / 1.617 / 1.626 / 1.677 ms
 static int acc_pass_blocks(long long n4, long long cap = 1024) {
   return (int)std::max(1LL, std::min((n4 + 511) / 512, cap));
 }
