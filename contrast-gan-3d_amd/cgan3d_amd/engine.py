@@ -406,7 +406,8 @@ class GeneratorPlan:
         return ops.wgrad(g, a, b, dw, self.ws_side, accumulate=zeroed, **kw)
 
     def backward(self, P: Dict[str, torch.Tensor], G: Dict[str, torch.Tensor], x: torch.Tensor,
-                 grads_enqueued: Optional[Callable[[int], None]] = None, zeroed: bool = False):
+                 grads_enqueued: Optional[Callable[[int], None]] = None, zeroed: bool = False,
+                 side_first: Optional[Callable[[], None]] = None):
         """``grads_enqueued(i)`` (optional) is called once every launch producing layer i's
         parameter gradients is enqueued (i = len(layers) for the last conv, which goes first; then
         len(layers) - 1 down to 0): the data-parallel engine starts bucket all-reduces there.
@@ -423,7 +424,9 @@ class GeneratorPlan:
 
         # the last conv's weight and bias grads, beside its input-grad when there is a side stream
         # (measured: after the input-grad instead, 1.78 vs 1.76 ms/step)
-        self._on_side(lambda: (self._wgrad(self.geo_last_wgrad, u, self.dz_last, G["model.last_conv.weight"],
+        # ``side_first``: the caller's own launch for that side segment (the generator loss)
+        self._on_side(lambda: (side_first() if side_first is not None else None,
+                               self._wgrad(self.geo_last_wgrad, u, self.dz_last, G["model.last_conv.weight"],
                                            zeroed, gathered16=self.y16[-1] if self.y_dead[-1] else None),
                                self._csum[key].run()))
         pending = []  # (layer, weight-grad launcher) not yet handed to the side stream
@@ -1029,7 +1032,9 @@ class StepEngine:
         self.gG, self.dG = self.g_arena.gviews, self.d_arena.gviews
         # plans after the arenas: their packed-weight descriptors point at the arena storage
         self.G = GeneratorPlan(g_cfg, b_sub, dims, device, self.gP, prec)
-        self.D = CriticPlan(d_cfg, nmax, dims, device, self.dP, prec)
+        # critic rows [0, nmax): the critic update's batch; [nmax, nmax + b_sub): the generator
+        # update's pass over opt_hat (own rows, so both dlogits can be constant buffers, below)
+        self.D = CriticPlan(d_cfg, nmax + b_sub, dims, device, self.dP, prec)
         # critic input slots [real | fake(opt_hat) | interpolation -> gamma]
         self.xc = torch.empty((nmax, *dims, 1), device=device)
         self.subopt = torch.empty((b_sub, *dims, 1), device=device)
@@ -1056,6 +1061,14 @@ class StepEngine:
                                                                g0.p, planar=self.D.pl), self.D.wd[0]))
         self.gp_part = (torch.empty(nsq, device=device) if nsq and self.b_gp and self.use_gp and not self.D.ln and
                         not os.environ.get("CGAN3D_NO_GP_PART") else None)
+        # dL/dlogits of both critic passes are constants (Trainer.py:117-131, 150-152): written once here
+        # into their rows of D.dz[-1]; the losses come from the GP pass (critic) and from a launch
+        # beside the generator's backward (generator), so no logits launch sits on the step's path
+        self.fold_logits = (self.gp_part is not None and self.gloss_side and
+                            not os.environ.get("CGAN3D_NO_FOLD_LOGITS"))
+        self.g_off = nmax if self.fold_logits else 0  # critic rows of the generator update
+        if self.fold_logits:
+            self._write_dlogits()
         self._pending = []  # in-flight bucket all-reduces of the generator gradients
         self.g_buckets = self._make_g_buckets(G_BUCKET_BYTES) if (self.dp and G_BUCKET_BYTES > 0) else []
         on_gpu = torch.device(device).type == "cuda"
@@ -1204,6 +1217,19 @@ class StepEngine:
         self.eps.copy_(eps.reshape(-1), non_blocking=True)
 
     # -------------------------------------------------------------------------------------------
+    def _write_dlogits(self):
+        """The constant dlogits (float32 arithmetic, as critic_logits_kernel / gen_logits_kernel)."""
+        ps, bo, bs, bg = self.D.logit_ps, self.b_opt, self.b_sub, self.b_gp
+        w = torch.tensor(self.gan_w, dtype=torch.float32)
+        er, ef, eg = bo * ps, bs * ps, bg * ps
+        dl = torch.empty((self.g_off + bs) * ps, dtype=torch.float32)
+        dl[:er] = -w / torch.tensor(float(er), dtype=torch.float32)
+        dl[er:er + ef] = w / torch.tensor(float(ef), dtype=torch.float32)
+        dl[er + ef:er + ef + eg] = 1.0
+        dl[er + ef + eg:self.g_off * ps] = 0.0
+        dl[self.g_off * ps:] = -w / torch.tensor(float(ef), dtype=torch.float32)
+        self.D.dz[-1].view(-1)[:dl.numel()].copy_(dl.to(self.device))
+
     def generator_forward(self):
         self.G.forward(self.gP, self.subopt, opt_hat_out=self.opt_hat, training=True)
         if self.gloss_side:
@@ -1224,7 +1250,8 @@ class StepEngine:
         nall = bo + bs + bg
         ops.gp_interpolate(self.xc[:bg], self.xc[bo:bo + bg], self.eps, self.xc[bo + bs:], bg, V)
         D.forward(self.dP, self.xc, 0, nall)
-        ops.critic_logits_grad(D.a[-1], bo, bs, bg, D.logit_ps, self.gan_w, D.dz[-1], self.losses)
+        if not self.fold_logits:
+            ops.critic_logits_grad(D.a[-1], bo, bs, bg, D.logit_ps, self.gan_w, D.dz[-1], self.losses)
         D.input_grad(self.dP, 0, nall, self.gbuf, bo + bs, bg,
                      ep0=ops.epilogue(stats=self.gp_part) if self.gp_part is not None else None)
         if D.ln:  # LayerNorm critic: the interpolation stays in xc (its primal adjoint needs it)
@@ -1238,7 +1265,8 @@ class StepEngine:
         gamma = self.xc[bo + bs:]
         if self.gp_part is not None:  # the input-grad wrote the per-sample sums of squares
             ops.gradient_penalty_part(self.gbuf, self.gp_part, bg, self.gp_part.numel() // bg, V, self.gp_weight,
-                                      gamma, self.losses)
+                                      gamma, self.losses, logits=D.a[-1] if self.fold_logits else None, n_real=bo,
+                                      n_fake=bs, logit_ps=D.logit_ps, gan_w=self.gan_w)
         else:
             ops.gradient_penalty(self.gbuf, bg, V, self.gp_weight, gamma, self.losses, self.loss_ws)
         ops.zero(self.d_arena.grad_padded)  # optimizer_D.zero_grad (Trainer.py:109): every layer then accumulates
@@ -1266,10 +1294,12 @@ class StepEngine:
         D, bs, V = self.D, self.b_sub, self.vox
         if self.gloss_side:  # the loss gradient and the zeroed arena (generator_forward) are in
             ops.stream_wait(torch.cuda.current_stream(self.device), self.G.side)
-        D.forward(self.dP, self.opt_hat, 0, bs)
-        ops.generator_logits_grad(D.a[-1][:bs], bs * D.logit_ps, self.gan_w, D.dz[-1], self.losses)
+        go = self.g_off
+        D.forward(self.dP, self.opt_hat, go, bs)
+        if not self.fold_logits:
+            ops.generator_logits_grad(D.a[-1][:bs], bs * D.logit_ps, self.gan_w, D.dz[-1], self.losses)
         if self.gloss_side:
-            D.input_grad(self.dP, 0, bs, self.G.dz_last, 0, bs,
+            D.input_grad(self.dP, go, bs, self.G.dz_last, go, bs,
                          ep0=ops.epilogue(residual=self.G.dz_last, mask_src=self.G.att, act=L.ACT_NEG_DTANH))
         else:
             D.input_grad(self.dP, 0, bs, self.dcrit, 0, bs)
@@ -1277,13 +1307,21 @@ class StepEngine:
                                       self.hi, self.sim_w, self.hu_w, self.G.dz_last, self.losses, self.loss_ws)
             ops.zero(self.g_arena.grad_padded)  # optimizer_G.zero_grad (Trainer.py:146): every layer then accumulates
         if self.dp and self.g_buckets:  # bucketed, overlapped with the rest of the backward
-            self.G.backward(self.gP, self.gG, self.subopt, grads_enqueued=self._bucket_ready, zeroed=True)
+            self.G.backward(self.gP, self.gG, self.subopt, grads_enqueued=self._bucket_ready, zeroed=True,
+                            side_first=self._gen_logit_loss)
             self._finish_allreduce()
         else:
-            self.G.backward(self.gP, self.gG, self.subopt, zeroed=True)
+            self.G.backward(self.gP, self.gG, self.subopt, zeroed=True, side_first=self._gen_logit_loss)
             if self.dp:  # CGAN3D_G_BUCKET_BYTES=0: one all-reduce of the whole gradient (main stream)
                 self._allreduce(self.g_arena.grad)
         self._optim_step(self.g_optim, self.G)
+
+    def _gen_logit_loss(self):
+        """The generator's adversarial loss (and the full generator loss) from its critic logits, beside
+        its backward (fold_logits: the dlogits are constant)."""
+        if self.fold_logits:
+            bs, go = self.b_sub, self.g_off
+            ops.generator_logits_grad(self.D.a[-1][go:go + bs], bs * self.D.logit_ps, self.gan_w, None, self.losses)
 
     @staticmethod
     def _optim_step(optim, plan):

@@ -971,14 +971,18 @@ def gradient_penalty(grad, b, per_sample, lambda_, gamma_out, losses, ws):
                   ptr(ws)), "gradient_penalty")
 
 
-def gradient_penalty_part(grad, part, b, chunks, per_sample, lambda_, gamma_out, losses):
-    """cgan3d_gradient_penalty_part: the GP from per-sample partial sums of squares part[b][chunks]."""
+def gradient_penalty_part(grad, part, b, chunks, per_sample, lambda_, gamma_out, losses, logits=None, n_real=0,
+                          n_fake=0, logit_ps=0, gan_w=0.0):
+    """cgan3d_gradient_penalty_part: the GP from per-sample partial sums of squares part[b][chunks]
+    (and, given the critic's logits, the Wasserstein term and critic loss in the same launch)."""
     _need(grad, b * per_sample, "gradient_penalty_part grad")
     _need(part, b * chunks, "gradient_penalty_part part", exact=False)
     _need(gamma_out, b * per_sample, "gradient_penalty_part gamma")
     _need(losses, 8, "losses")
+    if logits is not None:
+        _need(logits, (n_real + n_fake) * logit_ps, "gradient_penalty_part logits", exact=False)
     check(_launch("cgan3d_gradient_penalty_part", ptr(grad), ptr(part), b, chunks, per_sample, lambda_,
-                  ptr(gamma_out), ptr(losses)), "gradient_penalty_part")
+                  ptr(gamma_out), ptr(losses), ptr(logits), n_real, n_fake, logit_ps, gan_w), "gradient_penalty_part")
 
 
 def sumsq_blocks(g) -> int:
@@ -987,8 +991,10 @@ def sumsq_blocks(g) -> int:
 
 
 def generator_logits_grad(logits, n, gan_w, dlogits, losses):
+    """dlogits None: the generator's adversarial loss only (constant dlogits kept by the caller)."""
     _need(logits, n, "generator_logits_grad logits", exact=False)
-    _need(dlogits, n, "generator_logits_grad dlogits", exact=False)
+    if dlogits is not None:
+        _need(dlogits, n, "generator_logits_grad dlogits", exact=False)
     _need(losses, 8, "losses")
     check(_launch("cgan3d_generator_logits_grad", ptr(logits), n, gan_w, ptr(dlogits), ptr(losses)),
           "generator_logits_grad")

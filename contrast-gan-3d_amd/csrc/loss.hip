@@ -54,7 +54,8 @@ __global__ __launch_bounds__(256) void gen_logits_kernel(const float* __restrict
   double s = 0.0;
   for (int i = threadIdx.x; i < n; i += blockDim.x) s += logits[i];
   s = block_sum_d(s, red);
-  for (int i = threadIdx.x; i < n; i += blockDim.x) dl[i] = -gan_w / (float)n;
+  if (dl)
+    for (int i = threadIdx.x; i < n; i += blockDim.x) dl[i] = -gan_w / (float)n;
   if (threadIdx.x == 0) {
     losses[L_G] = (float)(-gan_w * s / n);
     // the full generator loss, when the similarity / HU terms were computed first (beside the
@@ -80,9 +81,13 @@ __global__ __launch_bounds__(256) void sumsq_kernel(const float* __restrict__ g,
 
 // Finalize folded into the scaling pass: every block combines the B x chunks partial sums itself
 // (same order in every block, so every block holds the same coefficients); block 0 writes the loss.
+// lg (optional): the critic's logits [real nr x lps | fake nf x lps | ...] — block 0 also computes the
+// Wasserstein term (critic_logits_kernel's losses) so no separate launch sits on the step's path
 __global__ __launch_bounds__(256) void gp_scale_kernel(const float* __restrict__ part, int B, int chunks,
                                                        float lambda_, float* losses, const float* __restrict__ g,
-                                                       long long ps, long long total, float* out) {
+                                                       long long ps, long long total, float* out,
+                                                       const float* __restrict__ lg, int nr, int nf, int lps,
+                                                       float gan_w) {
   __shared__ double red[4];
   __shared__ float coef[1024];
   double acc = 0.0;
@@ -108,10 +113,21 @@ __global__ __launch_bounds__(256) void gp_scale_kernel(const float* __restrict__
     }
   }
   acc = block_sum_d(acc, red);  // (its barriers also publish coef)
+  float wd = 0.f;
+  if (lg && blockIdx.x == 0) {  // as critic_logits_kernel
+    const long long er = (long long)nr * lps, ef = (long long)nf * lps;
+    double sr = 0.0, sf = 0.0;
+    for (long long i = threadIdx.x; i < er; i += blockDim.x) sr += lg[i];
+    for (long long i = threadIdx.x; i < ef; i += blockDim.x) sf += lg[er + i];
+    sr = block_sum_d(sr, red);
+    sf = block_sum_d(sf, red);
+    wd = (float)(gan_w * (sf / ef - sr / er));
+  }
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     const float gp = (float)(lambda_ * acc / B);
+    if (lg) losses[L_WD] = wd;
     losses[L_GP] = gp;
-    losses[L_D] = losses[L_WD] + gp;
+    losses[L_D] = (lg ? wd : losses[L_WD]) + gp;
   }
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long long)gridDim.x * blockDim.x)
     out[i] = coef[i / ps] * g[i];
@@ -224,7 +240,7 @@ extern "C" int cgan3d_critic_logits_grad(const float* logits, int32_t n_real, in
 
 extern "C" int cgan3d_generator_logits_grad(const float* logits, int32_t n, float gan_w, float* dlogits, float* losses,
                                             void* stream) {
-  CG_CHECK_ARG(logits && dlogits && losses && n > 0, "cgan3d_generator_logits_grad: bad args");
+  CG_CHECK_ARG(logits && losses && n > 0, "cgan3d_generator_logits_grad: bad args");
   ::cg::launch(gen_logits_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, logits, n, gan_w, dlogits, losses);
   CG_LAUNCH_CHECK("gen_logits_kernel");
   return CGAN3D_OK;
@@ -243,21 +259,23 @@ extern "C" int cgan3d_gradient_penalty(const float* grad, int32_t b, int64_t per
   const long long total = (long long)b * per_sample;
   int blocks = (int)std::min<long long>((total + 255) / 256, 1024);
   ::cg::launch(gp_scale_kernel, dim3(blocks), dim3(256), 0, s, part, b, chunks, lambda_, losses, grad,
-               (long long)per_sample, total, gamma_out);
+               (long long)per_sample, total, gamma_out, (const float*)nullptr, 0, 0, 0, 0.f);
   CG_LAUNCH_CHECK("gp_scale_kernel");
   return CGAN3D_OK;
 }
 
 extern "C" int cgan3d_gradient_penalty_part(const float* grad, const float* part, int32_t b, int32_t chunks,
                                             int64_t per_sample, float lambda_, float* gamma_out, float* losses,
-                                            void* stream) {
+                                            const float* logits, int32_t n_real, int32_t n_fake, int32_t logit_ps,
+                                            float gan_w, void* stream) {
   CG_CHECK_ARG(grad && part && gamma_out && losses, "cgan3d_gradient_penalty_part: null pointer");
   CG_CHECK_ARG(b > 0 && b <= 1024 && chunks > 0 && per_sample > 0, "cgan3d_gradient_penalty_part: bad sizes");
+  CG_CHECK_ARG(!logits || (n_real > 0 && n_fake > 0 && logit_ps > 0), "cgan3d_gradient_penalty_part: bad logit sizes");
   const long long total = (long long)b * per_sample;
   // every block sums the b x chunks partials itself: fewer, longer blocks when there are many
   int blocks = (int)std::min<long long>((total + 255) / 256, chunks >= 64 ? 256 : 1024);
   ::cg::launch(gp_scale_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, part, b, chunks, lambda_, losses, grad,
-               (long long)per_sample, total, gamma_out);
+               (long long)per_sample, total, gamma_out, logits, n_real, n_fake, logit_ps, gan_w);
   CG_LAUNCH_CHECK("gp_scale_kernel");
   return CGAN3D_OK;
 }
