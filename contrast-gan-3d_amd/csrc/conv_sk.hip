@@ -35,15 +35,15 @@ __device__ __forceinline__ void sk_class(int r, int k, int s, int p, int transpo
   }
 }
 
-template <int MT, int NT>
-__global__ __launch_bounds__(256) void conv_sk_kernel(SkArgs a, const float* __restrict__ x,
-                                                      const __bf16* __restrict__ wp, float* y, Epi ep) {
+template <int MT, int NT, int W = 4>  // W: waves per block (MT == 1 splits K over them)
+__global__ __launch_bounds__(64 * W) void conv_sk_kernel(SkArgs a, const float* __restrict__ x,
+                                                         const __bf16* __restrict__ wp, float* y, Epi ep) {
   __shared__ int tq[3][64];
   __shared__ int tlin[64];
   __shared__ int rowo[16 * MT];
   __shared__ int rowb[3][16 * MT];  // gathered-grid base coordinate per row (gathered = base + tq)
   __shared__ int rown[16 * MT];
-  __shared__ __attribute__((aligned(16))) f32x4 red[3][NT][64];
+  __shared__ __attribute__((aligned(16))) f32x4 red[W - 1][NT][64];
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int cls = blockIdx.x / a.mblocks, mb = blockIdx.x - cls * a.mblocks;
   const int s = a.s;
@@ -91,7 +91,7 @@ __global__ __launch_bounds__(256) void conv_sk_kernel(SkArgs a, const float* __r
   const bool rok = rowo[row] >= 0;
   const int bz = rowb[0][row], by = rowb[1][row], bx = rowb[2][row], nb = rown[row];
   const int KS = ntap * a.cin / 32;
-  const int ks0 = MT == 1 ? wave : 0, kstep = MT == 1 ? 4 : 1;
+  const int ks0 = MT == 1 ? wave : 0, kstep = MT == 1 ? W : 1;
 
   f32x4 acc[NT];
 #pragma unroll
@@ -146,7 +146,12 @@ __global__ __launch_bounds__(256) void conv_sk_kernel(SkArgs a, const float* __r
     __syncthreads();
     if (wave > 0) return;
 #pragma unroll
-    for (int t = 0; t < NT; ++t) acc[t] += red[0][t][lane] + red[1][t][lane] + red[2][t][lane];
+    for (int t = 0; t < NT; ++t) {
+      f32x4 r = red[0][t][lane];
+#pragma unroll
+      for (int q = 1; q < W - 1; ++q) r += red[q][t][lane];
+      acc[t] += r;
+    }
   }
   // epilogue: lane holds rows mt*16 + 4g + jj, channel t*16 + r16
   float vals[NT][4];
@@ -247,12 +252,20 @@ int sk_launch(const cgan3d_conv_geom* g, const float* x, const __bf16* wp, float
   const int nt = (g->cout + 15) / 16;
   const dim3 grid((unsigned)(a.nclass * a.mblocks));
 #define CG_SK(M, N) ::cg::launch((conv_sk_kernel<M, N>), grid, dim3(256), 0, st, a, x, wp, y, e)
-  if (mt == 1) {
+#define CG_SK16(N) ::cg::launch((conv_sk_kernel<1, N, 8>), grid, dim3(512), 0, st, a, x, wp, y, e)
+  // very few row tiles with a long K (the 32 -> 64 layer at 4 samples: 16 blocks x 64 K-steps):
+  // 8 waves per block split K, half the serial K-steps per wave
+  // (A/B at 64^3 B=4: 1.602 vs 1.609 ms/step with 4 waves)
+  const bool wide = mt == 1 && grid.x < 128 && !e.stats;
+  if (wide) {
+    if (nt == 1) CG_SK16(1); else if (nt == 2) CG_SK16(2); else if (nt == 3) CG_SK16(3); else CG_SK16(4);
+  } else if (mt == 1) {
     if (nt == 1) CG_SK(1, 1); else if (nt == 2) CG_SK(1, 2); else if (nt == 3) CG_SK(1, 3); else CG_SK(1, 4);
   } else {
     if (nt == 1) CG_SK(4, 1); else if (nt == 2) CG_SK(4, 2); else if (nt == 3) CG_SK(4, 3); else CG_SK(4, 4);
   }
 #undef CG_SK
+#undef CG_SK16
   return CGAN3D_OK;
 }
 
