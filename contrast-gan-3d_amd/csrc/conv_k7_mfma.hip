@@ -21,6 +21,7 @@ namespace cg {
 typedef __bf16 bf16x8_k __attribute__((ext_vector_type(8)));
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 typedef __bf16 bf16x4_k __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x2_k __attribute__((ext_vector_type(2)));
 
 // Staging from global memory with every load of the thread in flight at once: element i < total
 // of the tile comes from src[off(i)] (off < 0: zero).  Loads use clamped addresses and no
@@ -53,7 +54,13 @@ constexpr int N_TD = 4, N_TH = 8, N_TW = 16;
 constexpr int N_HD = N_TD + 6, N_HH = N_TH + 6, N_HW = N_TW + 6, N_HWP = 24;  // x halo rows (22 used)
 constexpr int N_ROWS = N_HD * N_HH;
 constexpr int N_PAIRS = 52;                                 // 49 (td, th) pairs padded to 13 K-steps
-constexpr int N_X = N_ROWS * N_HW, N_X_PER = (N_X + 255) / 256;
+#ifndef N_US_PAD
+#define N_US_PAD 8
+#endif
+// unfolded-image row stride (bf16): 256 bytes + N_US_PAD elements — the unfold's 16-byte stores of
+// rows r .. r+3 (one ds_write lane group) land on distinct banks instead of 4-way conflicts
+constexpr int N_US = N_TW * 8 + N_US_PAD;
+constexpr int N_X = N_ROWS * N_HW / 2, N_X_PER = (N_X + 255) / 256;  // halo value pairs (w, w + 1)
 
 // mode-2 BatchNorm statistics of the reflect-folded output (cgan3d_epilogue.bn_fold): the input-grad
 // of the generator's last conv lands on the padded grid, dy = fold(out) on the unpadded one, and
@@ -83,7 +90,7 @@ __global__ __launch_bounds__(256, 2) void k7m_n2w_kernel(K7Args a, const float* 
                                                          float* stats, float* bn_part, int tiles_per_block, int ntiles,
                                                          K7Fold fb, double* acc1, int reps1) {
   constexpr int C = 16;
-  __shared__ __attribute__((aligned(16))) __bf16 us[N_ROWS * N_TW * 8];  // [row][ow][8 taps]
+  __shared__ __attribute__((aligned(16))) __bf16 us[N_ROWS * N_US];  // [row][ow][8 taps], rows N_US apart
   __shared__ __attribute__((aligned(16))) __bf16 xs[N_ROWS * N_HWP];     // [row][24]
   __shared__ __attribute__((aligned(16))) __bf16 wt[N_PAIRS * C * 8];    // [pair][c][tw8]
   __shared__ float red[4][C];
@@ -111,15 +118,15 @@ __global__ __launch_bounds__(256, 2) void k7m_n2w_kernel(K7Args a, const float* 
 #pragma unroll
   for (int ks = 0; ks < N_PAIRS / 4; ++ks) {
     const int pa = min(4 * ks + g, 48), td = pa / K7, th = pa - td * K7;
-    aoff[ks] = ((td * N_HH + th) * N_TW + r16) * 8;
+    aoff[ks] = (td * N_HH + th) * N_US + r16 * 8;
   }
-  int xc[N_X_PER];  // this thread's halo values: packed (hd, hh, hw), -1 past the halo
+  int xc[N_X_PER];  // this thread's halo pairs: packed (hd, hh, hw even), -1 past the halo
 #pragma unroll
   for (int k = 0; k < N_X_PER; ++k) {
-    const int i = tid + 256 * k, hw = i % N_HW, row = i / N_HW;
+    const int i = tid + 256 * k, hw = 2 * (i % (N_HW / 2)), row = i / (N_HW / 2);
     xc[k] = i < N_X ? ((row / N_HH) | ((row % N_HH) << 8) | (hw << 16)) : -1;
   }
-  float xb[N_X_PER];
+  float xb[N_X_PER][2];
   auto tile_origin = [&](int tile, int* n, int* d0, int* h0, int* w0) {
     int r = tile;
     const int tw_ = r % a.tiles_w; r /= a.tiles_w;
@@ -133,11 +140,14 @@ __global__ __launch_bounds__(256, 2) void k7m_n2w_kernel(K7Args a, const float* 
 #pragma unroll
     for (int k = 0; k < N_X_PER; ++k) {
       const int c = xc[k];
-      const int id = k7_src(d0 + (c & 255) - a.P, a.di, a.reflect), ih = k7_src(h0 + ((c >> 8) & 255) - a.P, a.hi, a.reflect),
-                iw = k7_src(w0 + (c >> 16) - a.P, a.wi, a.reflect);
-      const bool ok = c >= 0 && (id | ih | iw) >= 0;
-      xb[k] = x[ok ? ((n * a.di + id) * a.hi + ih) * a.wi + iw : 0];
-      if (!ok) xb[k] = 0.f;
+      const int id = k7_src(d0 + (c & 255) - a.P, a.di, a.reflect), ih = k7_src(h0 + ((c >> 8) & 255) - a.P, a.hi, a.reflect);
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        const int iw = k7_src(w0 + (c >> 16) + e - a.P, a.wi, a.reflect);
+        const bool ok = c >= 0 && (id | ih | iw) >= 0;
+        xb[k][e] = x[ok ? ((n * a.di + id) * a.hi + ih) * a.wi + iw : 0];
+        if (!ok) xb[k][e] = 0.f;
+      }
     }
   };
   // running BatchNorm statistics of this block (threads tid < 16, channel tid): Chan merge per tile
@@ -162,7 +172,12 @@ __global__ __launch_bounds__(256, 2) void k7m_n2w_kernel(K7Args a, const float* 
 #pragma unroll
     for (int k = 0; k < N_X_PER; ++k) {
       const int c = xc[k];
-      if (c >= 0) xs[((c & 255) * N_HH + ((c >> 8) & 255)) * N_HWP + (c >> 16)] = (__bf16)xb[k];
+      if (c >= 0) {  // one 4-byte LDS store per pair (two lanes never write halves of one word)
+        bf16x2_k v;
+        v[0] = (__bf16)xb[k][0];
+        v[1] = (__bf16)xb[k][1];
+        *reinterpret_cast<bf16x2_k*>(xs + ((c & 255) * N_HH + ((c >> 8) & 255)) * N_HWP + (c >> 16)) = v;
+      }
     }
     if (tile + 1 < t1 && !(a.dbg & 4)) load(tile + 1);  // in flight during this tile's MFMAs
     __syncthreads();
@@ -179,20 +194,20 @@ __global__ __launch_bounds__(256, 2) void k7m_n2w_kernel(K7Args a, const float* 
           const int m = sft / 2 + k;
           o[k] = (sft & 1) ? __builtin_amdgcn_alignbyte(wv[m + 1], wv[m], 2) : wv[m];
         }
-        *reinterpret_cast<u32x4*>(us + (r * N_TW + 8 * hf + sft) * 8) = o;
+        *reinterpret_cast<u32x4*>(us + r * N_US + (8 * hf + sft) * 8) = o;
       }
     }
     __syncthreads();
     f32x4 acc[N_TH];
 #pragma unroll
     for (int r = 0; r < N_TH; ++r) acc[r] = f32x4{0.f, 0.f, 0.f, 0.f};
-    const __bf16* ub = us + wave * N_HH * N_TW * 8;
+    const __bf16* ub = us + wave * N_HH * N_US;
 #pragma unroll
     for (int ks = 0; ks < N_PAIRS / 4; ++ks) {
       if (a.dbg & 2) break;
       bf16x8_k av[N_TH];
 #pragma unroll
-      for (int r = 0; r < N_TH; ++r) av[r] = *reinterpret_cast<const bf16x8_k*>(ub + aoff[ks] + r * N_TW * 8);
+      for (int r = 0; r < N_TH; ++r) av[r] = *reinterpret_cast<const bf16x8_k*>(ub + aoff[ks] + r * N_US);
       // transposed: D[channel][ow] (A = weights, B = the unfolded image), so a lane ends up with 4
       // consecutive channels of one voxel: 16-byte output stores and z loads
 #pragma unroll
