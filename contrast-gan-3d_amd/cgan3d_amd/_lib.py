@@ -135,6 +135,7 @@ _SIGS = {
     "cgan3d_generator_output_grad": ([_P, _P, _P, _P, _P, _I64, _F, _F, _F, _F, _P, _P, _P, _P], _I32),
     "cgan3d_adam_tick": ([_P, _P], _I32),
     "cgan3d_adam": ([_P, _P, _P, _P, _I64, _P, _P], _I32),
+    "cgan3d_adam_range": ([_P, _P, _P, _P, _I64, _P, _P], _I32),
     "cgan3d_adam_pack": ([_P, _P, _P, _P, _I64, _P, _P, _I32, _P, _P], _I32),
     "cgan3d_zero": ([_P, _I64, _P], _I32),
     "cgan3d_copy_multi": ([_P, _P, _P, _I32, _P], _I32),

@@ -155,6 +155,8 @@ class GeneratorPlan:
         dims = _planar_dims(dims, pl)
         self.n, self.dims, self.device = n, tuple(dims), device
         self.packs = ops.PackSet(device)  # packed [tap][cin][cout] weight copies, refreshed per update
+        # ... of the layers whose weight grads end the backward on the main stream (pack_tail)
+        self.packs_tail = ops.PackSet(device)
         layers: List[_GLayer] = [_GLayer("conv", "model.first", 7, 1, 3, True, 1, c0, dims, dims)]
         d = tuple(dims)
         for i in range(cfg.n_updownsample_blocks):
@@ -187,7 +189,7 @@ class GeneratorPlan:
         # fused BatchNorm statistics: per-block partial slabs written by the producing kernels
         self.slots_f, self.part_f = [], []
         ws = 0
-        for ly in layers:
+        for li, ly in enumerate(layers):
             if ly.kind == "conv":
                 gf = ops.conv_fwd_geom(n, ly.din, ly.dout, ly.cin, ly.cout, ly.k, ly.s, ly.p, ly.reflect, planar=pl)
                 gd = ops.conv_dgrad_geom(n, ly.din, ly.dout, ly.cin, ly.cout, ly.k, ly.s, ly.p, planar=pl)
@@ -198,8 +200,9 @@ class GeneratorPlan:
                 gw = ops.convt_wgrad_geom(n, ly.din, ly.dout, ly.cin, ly.cout, ly.k, ly.s, ly.p, planar=pl)
             gw = ops.with_prec(gw, prec)
             wt = P[f"{ly.name}.conv.weight"]
-            gf, wf = self.packs.add(gf, wt, prec)
-            gd, wd = self.packs.add(gd, wt, prec)
+            ps = self.packs_tail if li < WGRAD_TAIL_MAIN else self.packs
+            gf, wf = ps.add(gf, wt, prec)
+            gd, wd = ps.add(gd, wt, prec)
             self.wf.append(wf)
             self.wd.append(wd)
             self.geo_fwd.append(gf)
@@ -330,8 +333,16 @@ class GeneratorPlan:
             fn()
 
     def pack(self):
-        """Refresh the packed weight copies (one launch); call after every weight update."""
+        """Refresh the packed weight copies; call after every weight update."""
         self.packs.pack()
+        self.packs_tail.pack()
+
+    def pack_early(self):
+        """The packed copies of the layers updated ahead of the tail (StepEngine._g_early)."""
+        self.packs.pack()
+
+    def pack_tail(self):
+        self.packs_tail.pack()
 
     # -- forward: x [n,D,H,W,1] -> att (tanh output); opt_hat_out = x - att (Trainer.py:170-171)
     # Training-mode BatchNorm statistics are fused into the producing conv: fp64 accumulators (ac_f)
@@ -407,7 +418,7 @@ class GeneratorPlan:
 
     def backward(self, P: Dict[str, torch.Tensor], G: Dict[str, torch.Tensor], x: torch.Tensor,
                  grads_enqueued: Optional[Callable[[int], None]] = None, zeroed: bool = False,
-                 side_first: Optional[Callable[[], None]] = None):
+                 side_first: Optional[Callable[[], None]] = None, side_after: Optional[Callable[[], None]] = None):
         """``grads_enqueued(i)`` (optional) is called once every launch producing layer i's
         parameter gradients is enqueued (i = len(layers) for the last conv, which goes first; then
         len(layers) - 1 down to 0): the data-parallel engine starts bucket all-reduces there.
@@ -513,6 +524,11 @@ class GeneratorPlan:
             if i == 0:
                 break
             self._input_grad(P, G, i)
+            if i == WGRAD_TAIL_MAIN and side_after is not None and self.side is not None:
+                # every gradient of layers >= i is enqueued (side: weight grads; main: BatchNorm
+                # grads) and their weights' last reader, this input-grad, too: the caller's launches
+                # for those layers (their update) on the side stream, beside the main stream's tail
+                self._on_side(side_after)
         if self.side is not None:  # the weight gradients are complete before anything reads them
             ops.stream_wait(torch.cuda.current_stream(self.device), self.side)
 
@@ -1059,6 +1075,24 @@ class StepEngine:
         # input-grad (one float per block; CGAN3D_NO_GP_PART=1: a separate reduction pass, A/B)
         nsq = ops.sumsq_blocks(self.D._geo(ops.conv_dgrad_geom(self.b_gp, g0.din, g0.dout, g0.cin, g0.cout, g0.k, g0.s,
                                                                g0.p, planar=self.D.pl), self.D.wd[0]))
+        # The generator's Adam in two parts: every layer whose gradients are complete when the
+        # backward's side stream finishes its last weight grad (all but the first WGRAD_TAIL_MAIN
+        # layers) is updated and repacked on the side stream beside the main stream's tail; the
+        # tail layers' parameters (a prefix of the arena) after it, with the step tick.  Single
+        # GPU only (data parallelism all-reduces the whole gradient first).
+        self.g_split = 0
+        if self.G.side is not None and not self.dp and not os.environ.get("CGAN3D_NO_G_SPLIT_ADAM"):
+            pre = tuple(self.G.layers[li].name + "." for li in range(min(WGRAD_TAIL_MAIN, len(self.G.layers))))
+            ar, off, lo, ok = self.g_arena, 0, None, True
+            for nm, pp in zip(ar.names, ar.params):
+                tail = nm.startswith(pre) if pre else False
+                if tail and lo is not None:
+                    ok = False  # a tail parameter after an early one: not a prefix
+                if not tail and lo is None:
+                    lo = off
+                off += pp.numel()
+            if ok and lo and lo < ar.numel:
+                self.g_split = lo
         self.gp_part = (torch.empty(nsq, device=device) if nsq and self.b_gp and self.use_gp and not self.D.ln and
                         not os.environ.get("CGAN3D_NO_GP_PART") else None)
         # dL/dlogits of both critic passes are constants (Trainer.py:117-131, 150-152): written once here
@@ -1311,10 +1345,28 @@ class StepEngine:
                             side_first=self._gen_logit_loss)
             self._finish_allreduce()
         else:
-            self.G.backward(self.gP, self.gG, self.subopt, zeroed=True, side_first=self._gen_logit_loss)
+            self.G.backward(self.gP, self.gG, self.subopt, zeroed=True, side_first=self._gen_logit_loss,
+                            side_after=self._g_early if self.g_split else None)
             if self.dp:  # CGAN3D_G_BUCKET_BYTES=0: one all-reduce of the whole gradient (main stream)
                 self._allreduce(self.g_arena.grad)
-        self._optim_step(self.g_optim, self.G)
+        if self.g_split:
+            self._g_tail()
+        else:
+            self._optim_step(self.g_optim, self.G)
+
+    def _g_early(self):
+        """Adam (step + 1, no tick) and repack of the generator layers updated ahead of the tail."""
+        a, lo = self.g_arena, self.g_split
+        ops.adam_range(a.flat[lo:], a.grad[lo:], a.exp_avg[lo:], a.exp_avg_sq[lo:], self.g_optim.hyper)
+        self.G.pack_early()
+
+    def _g_tail(self):
+        """Adam of the tail layers (the arena prefix) with the step tick, then their repack."""
+        a, lo, opt = self.g_arena, self.g_split, self.g_optim
+        ops.adam_pack(a.flat[:lo], a.grad[:lo], a.exp_avg[:lo], a.exp_avg_sq[:lo], opt.hyper, opt.ticket)
+        if not ops.recording():  # a recorded plan counts its steps when it runs (note_step)
+            opt._host_step += 1
+        self.G.pack_tail()
 
     def _gen_logit_loss(self):
         """The generator's adversarial loss (and the full generator loss) from its critic logits, beside

@@ -1025,6 +1025,15 @@ def adam(param, grad, exp_avg, exp_avg_sq, hyper):
           "adam")
 
 
+def adam_range(param, grad, exp_avg, exp_avg_sq, hyper):
+    """cgan3d_adam_range: Adam over part of an arena with step + 1, the step counter left as it is."""
+    for t, nm in ((grad, "grad"), (exp_avg, "exp_avg"), (exp_avg_sq, "exp_avg_sq")):
+        _need(t, param.numel(), f"adam_range {nm}")
+    _need(hyper, 6, "adam_range hyper")
+    check(_launch("cgan3d_adam_range", ptr(param), ptr(grad), ptr(exp_avg), ptr(exp_avg_sq), param.numel(), ptr(hyper)),
+          "adam_range")
+
+
 def adam_pack(param, grad, exp_avg, exp_avg_sq, hyper, ticket, packs: Optional["PackSet"] = None):
     """``adam_tick`` + ``adam`` + ``packs.pack()`` as one launch (cgan3d_adam_pack); every packed
     copy's source weight must be a contiguous view into ``param``."""

@@ -514,6 +514,8 @@ __global__ __launch_bounds__(256) void adam_pack_kernel(float* __restrict__ p, c
                                                         float* __restrict__ m, float* __restrict__ v, long long n,
                                                         float* hyper, const cgan3d_pack_desc* __restrict__ descs,
                                                         int ndesc, int tick, unsigned* ticket) {
+  // tick 0: the step was advanced before (cgan3d_adam_tick); 1: use step + 1 and advance it here
+  // (last block out); 2: use step + 1, leave it (cgan3d_adam_range, a part updated ahead of the rest)
   const AdamK k = adam_k(hyper, tick ? hyper[4] + 1.f : hyper[4]);
   if (ndesc == 0 && !((reinterpret_cast<uintptr_t>(p) | reinterpret_cast<uintptr_t>(g) | reinterpret_cast<uintptr_t>(m) |
                        reinterpret_cast<uintptr_t>(v)) & 15)) {
@@ -538,7 +540,7 @@ __global__ __launch_bounds__(256) void adam_pack_kernel(float* __restrict__ p, c
     }
     for (long long i = 4 * n4 + (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long long)gridDim.x * 256)
       adam_elem(k, p, g, m, v, i);
-    if (tick && last_block_out(ticket)) hyper[4] += 1.f;
+    if (tick == 1 && last_block_out(ticket)) hyper[4] += 1.f;
     return;
   }
   for (long long base = (long long)blockIdx.x * 256; base < n; base += (long long)gridDim.x * 256) {
@@ -552,7 +554,7 @@ __global__ __launch_bounds__(256) void adam_pack_kernel(float* __restrict__ p, c
       if (live && i >= lo && i < hi) pack_elem(d, (int)(i - lo), pi);
     }
   }
-  if (tick && last_block_out(ticket)) hyper[4] += 1.f;
+  if (tick == 1 && last_block_out(ticket)) hyper[4] += 1.f;
 }
 
 void adam_launch(float* p, const float* g, float* m, float* v, long long n, float* hyper,
@@ -664,6 +666,16 @@ extern "C" int cgan3d_set_tuning(int32_t key, int32_t value) {
   if (key == 14) { cout1_wave_set(value); return CGAN3D_OK; }
   set_error("cgan3d_set_tuning: unknown key %d", key);
   return CGAN3D_EINVAL;
+}
+
+extern "C" int cgan3d_adam_range(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, int64_t n,
+                                 const float* hyper, void* stream) {
+  CG_CHECK_ARG(param && grad && exp_avg && exp_avg_sq && hyper, "cgan3d_adam_range: null pointer");
+  CG_CHECK_ARG(n > 0, "cgan3d_adam_range: bad size");
+  adam_launch(param, grad, exp_avg, exp_avg_sq, (long long)n, const_cast<float*>(hyper), nullptr, 0, 2, nullptr,
+              (hipStream_t)stream);
+  CG_LAUNCH_CHECK("adam_pack_kernel");
+  return CGAN3D_OK;
 }
 
 extern "C" int cgan3d_adam_pack(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, int64_t n,

@@ -25,6 +25,7 @@ struct SkArgs {
   int nclass, cd, ch, cw;  // parity-class grid (transposed stride 2) or the output grid
   int mblocks;             // blocks per class
   int ktot;                // k^3 * cin: packed weight row length
+  int cin_log2;            // cin is a power of two (sk_format_ok)
 };
 
 __device__ __forceinline__ void sk_class(int r, int k, int s, int p, int transposed, int* f, int* st, int* cnt) {
@@ -103,17 +104,18 @@ __global__ __launch_bounds__(64 * W) void conv_sk_kernel(SkArgs a, const float* 
   bf16x8_k bb[PF][NT];     // B fragments
   auto load = [&](int ks, int sl) {
     const int k0 = ks * 32 + 8 * g;
-    const int j = k0 / a.cin, a0 = k0 - j * a.cin;
+    const int j = k0 >> a.cin_log2, a0 = k0 & (a.cin - 1);
     const int iz = bz + tq[0][j], iy = by + tq[1][j], ix = bx + tq[2][j];
     const bool ok = rok && (unsigned)iz < (unsigned)a.di && (unsigned)iy < (unsigned)a.hi && (unsigned)ix < (unsigned)a.wi;
-    const float* src = x + (ok ? (((long long)(nb * a.di + iz) * a.hi + iy) * a.wi + ix) * a.cin + a0 : 0);
+    // 32-bit element offsets (sk_launch checks the sizes)
+    const float* src = x + (ok ? ((((nb * a.di + iz) * a.hi + iy) * a.wi + ix) << a.cin_log2) + a0 : 0);
     xa0[sl] = ok ? *reinterpret_cast<const f32x4*>(src) : f32x4{0.f, 0.f, 0.f, 0.f};
     xa1[sl] = ok ? *reinterpret_cast<const f32x4*>(src + 4) : f32x4{0.f, 0.f, 0.f, 0.f};
     const int wk = tlin[j] * a.cin + a0;
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
       const int col = t * 16 + r16;
-      bb[sl][t] = col < a.cout ? *reinterpret_cast<const bf16x8_k*>(wp + (long long)col * a.ktot + wk)
+      bb[sl][t] = col < a.cout ? *reinterpret_cast<const bf16x8_k*>(wp + col * a.ktot + wk)
                                : bf16x8_k{0, 0, 0, 0, 0, 0, 0, 0};
     }
   };
@@ -170,7 +172,7 @@ __global__ __launch_bounds__(64 * W) void conv_sk_kernel(SkArgs a, const float* 
       else if (ep.act == CGAN3D_ACT_LRELU) v = v > 0.f ? v : v * ep.slope;
       const bool ok = cv && ro[jj] >= 0;
       if (ok) {
-        const long long o = (long long)ro[jj] * a.cout + c;
+        const int o = ro[jj] * a.cout + c;
         if (ep.mask_src) v = ep.mask_src[o] > 0.f ? v : v * ep.slope;
         if (ep.residual) v += ep.residual[o];
         y[o] = v;
@@ -210,6 +212,10 @@ __global__ __launch_bounds__(64 * W) void conv_sk_kernel(SkArgs a, const float* 
 // geometry (ignoring the weight format): the critic's k4 convs, bf16
 bool sk_format_ok(const cgan3d_conv_geom* g) {
   if (g->prec != CGAN3D_PREC_BF16 || g->reflect || g->k != 4 || g->cin % 8 || g->cout % 8 || g->cout > 64) return false;
+  if (g->cin & (g->cin - 1)) return false;  // power of two: shift / mask index math
+  if ((long long)g->n * g->di * g->hi * g->wi * g->cin >= (1LL << 31) ||
+      (long long)g->n * g->do_ * g->ho * g->wo * g->cout >= (1LL << 31))
+    return false;  // 32-bit element offsets
   if (g->transposed && g->stride > 1 && (g->do_ % g->stride || g->ho % g->stride || g->wo % g->stride)) return false;
   // every parity class's K (taps x cin) a multiple of 32
   const int kd = g->transposed ? (g->k + g->stride - 1) / g->stride : g->k;  // taps per dim (k % s == 0 here)
@@ -236,6 +242,8 @@ static SkArgs sk_args(const cgan3d_conv_geom* g, int* mt) {
   *mt = (ks >= 8 && (long long)a.nclass * ((cvox + 15) / 16) < 1024) ? 1 : 4;
   a.mblocks = (int)((cvox + 16 * *mt - 1) / (16 * *mt));
   a.ktot = g->k * g->k * g->k * g->cin;
+  a.cin_log2 = 0;
+  while ((1 << a.cin_log2) < g->cin) ++a.cin_log2;
   return a;
 }
 

@@ -182,6 +182,11 @@ int cgan3d_pack_weights_multi(const cgan3d_pack_desc* descs, int32_t n, int64_t 
  * each updated parameter is also written into every packed copy whose source weight holds it
  * (descriptor weights must be contiguous views into `param`).  `ticket`: two uint32 words, zeroed
  * once by the caller and left zeroed (the last block out advances the step counter). */
+/* Adam over a part of an arena ahead of the rest, with the step the coming cgan3d_adam_pack of the
+ * remainder will advance to (step + 1) and without advancing it: the generator's layers whose
+ * gradients are complete early in the backward are updated beside its tail. */
+int cgan3d_adam_range(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, int64_t n,
+                      const float* hyper, void* stream);
 int cgan3d_adam_pack(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, int64_t n, float* hyper,
                      const cgan3d_pack_desc* descs, int32_t ndesc, uint32_t* ticket, void* stream);
 int cgan3d_conv3d_fwd(const cgan3d_conv_geom* g, const float* x, const float* w, float* y,
