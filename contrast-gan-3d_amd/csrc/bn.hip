@@ -207,7 +207,11 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const float* __restri
 // bn_bwd_apply_kernel with dy = reflect_fold(padded) gathered on the fly: per voxel the 1..8
 // padded sources that mirror onto it (fold_src), float4 of channels per thread, channels fixed per
 // thread (256 % (C/4) == 0); the bf16 copy (and the fp32 dz when asked) as bn_bwd_apply_kernel.
-__device__ __forceinline__ void acc_sums(const double* __restrict__ acc, int reps, int C, double* sums);
+struct NoPrefetch {
+  __device__ void operator()() const {}
+};
+template <class F>
+__device__ __forceinline__ void acc_sums(const double* __restrict__ acc, int reps, int C, double* sums, F&& prefetch);
 
 // coef == NULL: the coefficients from fp64 accumulators (cgan3d_bn_backward_acc_fold): every block
 // combines the replicas, block 0 publishes dgamma / dbeta and zeroes `zero`
@@ -226,7 +230,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_fold_kernel(const float* __r
     const int tid = threadIdx.x;
     if (blockIdx.x == 0)
       for (int j = tid; j < zero_n; j += blockDim.x) zero[j] = 0.0;
-    acc_sums(acc, reps, C, sums);
+    acc_sums(acc, reps, C, sums, NoPrefetch());
     __syncthreads();
     for (int c = tid; c < C; c += blockDim.x) {
       co[c] = gamma[c] * mi[C + c];
@@ -591,16 +595,28 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_slab_kernel(const float* __r
 // block combines the replicas itself (16 KB at reps 16, C 64: all loads in flight), block 0 publishes
 // statistics / running buffers / parameter gradients and zeroes an accumulator the stream is done
 // with (the caller rotates them, so none needs a memset launch).
-__device__ __forceinline__ void acc_sums(const double* __restrict__ acc, int reps, int C, double* sums) {
+template <class F>
+__device__ __forceinline__ void acc_sums(const double* __restrict__ acc, int reps, int C, double* sums,
+                                         F&& prefetch) {
   // sums[q * C + c] = sum over replicas of acc[(r * 2 + q) * C + c]: the 256 threads split the pairs
   // (j = q * C + c, 2C <= 128 of them) and the replicas (T = 256 / 2C threads per pair), eight loads
   // in flight per thread — one round trip for reps <= 8T (the atomics left the values at the memory
-  // side: each round trip is long) — then the T partial sums of a pair are added through LDS
+  // side: each round trip is long) — then the T partial sums of a pair are added through LDS.
+  // `prefetch` runs between issuing the first round of loads and using them: the elementwise pass
+  // issues its first loads there, so the two round trips overlap instead of adding up
   __shared__ double part[256];
   const int tid = threadIdx.x, P = 2 * C, T = 256 / P, j = tid % P, h = tid / P;
+  // unconditional loads (clamped replica, value masked after): a load under a branch gets its own
+  // wait before the branch joins, which serialised the first round trip
+  double v[8];
+#pragma unroll
+  for (int u = 0; u < 8; ++u) v[u] = acc[(long long)min(h + u * T, reps - 1) * P + j];
+  prefetch();
+  __builtin_amdgcn_sched_barrier(0);  // keep the sums below every load issued above
   double s = 0.0;
-  for (int r0 = h; r0 < reps; r0 += 8 * T) {
-    double v[8];
+#pragma unroll
+  for (int u = 0; u < 8; ++u) s += h + u * T < reps ? v[u] : 0.0;
+  for (int r0 = h + 8 * T; r0 < reps; r0 += 8 * T) {
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
       const int r = r0 + u * T;
@@ -618,6 +634,10 @@ __device__ __forceinline__ void acc_sums(const double* __restrict__ acc, int rep
   }
 }
 
+// float4 per thread loaded before the statistics are known (acc_pass_blocks sizes the grid at ~2)
+constexpr int ACC_PF = 2;
+
+template <bool RES>  // residual added: a load under `if (res)` made the compiler wait for every load in flight
 __global__ __launch_bounds__(256) void bn_apply_acc_kernel(const double* __restrict__ acc, int reps, int C, double nvox,
                                                            const float* gamma, const float* beta, float* rmean,
                                                            float* rvar, long long* nbt, float momentum, float eps,
@@ -631,7 +651,19 @@ __global__ __launch_bounds__(256) void bn_apply_acc_kernel(const double* __restr
   const int tid = threadIdx.x;
   if (blockIdx.x == 0)
     for (int j = tid; j < zero_n; j += blockDim.x) zero[j] = 0.0;
-  acc_sums(acc, reps, C, sums);
+  // the first ACC_PF float4 of this thread's elementwise range are loaded while the replicas are in flight
+  const f32x4* z4 = reinterpret_cast<const f32x4*>(z);
+  const f32x4* r4 = reinterpret_cast<const f32x4*>(res);
+  const long long i0 = (long long)blockIdx.x * blockDim.x + tid, stride = (long long)gridDim.x * blockDim.x;
+  f32x4 zp[ACC_PF], rp[ACC_PF];
+  acc_sums(acc, reps, C, sums, [&] {
+#pragma unroll
+    for (int u = 0; u < ACC_PF; ++u) {
+      const long long i = min(i0 + u * stride, n4 - 1);
+      zp[u] = z4[i];
+      if (RES) rp[u] = r4[i];
+    }
+  });
   __syncthreads();
   for (int c = tid; c < C; c += blockDim.x) {
     const double mean = sums[c] / nvox, var = fmax(sums[C + c] / nvox - mean * mean, 0.0);
@@ -654,17 +686,18 @@ __global__ __launch_bounds__(256) void bn_apply_acc_kernel(const double* __restr
   f32x4 sc4, sf4;
 #pragma unroll
   for (int e = 0; e < 4; ++e) { sc4[e] = ssh[cc + e]; sf4[e] = ssh[C + cc + e]; }
-  const f32x4* z4 = reinterpret_cast<const f32x4*>(z);
-  const f32x4* r4 = reinterpret_cast<const f32x4*>(res);
   f32x4* y4 = reinterpret_cast<f32x4*>(y);
-  for (long long i = (long long)blockIdx.x * blockDim.x + tid; i < n4; i += (long long)gridDim.x * blockDim.x) {
-    f32x4 v = z4[i];
+  auto apply = [&](long long i, f32x4 v, const f32x4& r) {
 #pragma unroll
     for (int e = 0; e < 4; ++e) v[e] = act_f(v[e] * sc4[e] + sf4[e], act, slope);
-    if (res) v += r4[i];
+    if (RES) v += r;
     if (y) y4[i] = v;
     if (y16) store16(y16, i, v);
-  }
+  };
+#pragma unroll
+  for (int u = 0; u < ACC_PF; ++u)
+    if (i0 + u * stride < n4) apply(i0 + u * stride, zp[u], rp[u]);
+  for (long long i = i0 + ACC_PF * stride; i < n4; i += stride) apply(i, z4[i], RES ? r4[i] : f32x4{});
 }
 
 __global__ __launch_bounds__(256) void bn_bwd_apply_acc_kernel(const double* __restrict__ acc, int reps, int C,
@@ -681,7 +714,18 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_acc_kernel(const double* __r
   const int tid = threadIdx.x;
   if (blockIdx.x == 0)
     for (int j = tid; j < zero_n; j += blockDim.x) zero[j] = 0.0;
-  acc_sums(acc, reps, C, sums);
+  const f32x4* z4 = reinterpret_cast<const f32x4*>(z);
+  const f32x4* d4 = reinterpret_cast<const f32x4*>(dy);
+  const long long i0 = (long long)blockIdx.x * blockDim.x + tid, stride = (long long)gridDim.x * blockDim.x;
+  f32x4 zp[ACC_PF], dp[ACC_PF];
+  acc_sums(acc, reps, C, sums, [&] {
+#pragma unroll
+    for (int u = 0; u < ACC_PF; ++u) {
+      const long long i = min(i0 + u * stride, n4 - 1);
+      zp[u] = z4[i];
+      dp[u] = d4[i];
+    }
+  });
   __syncthreads();
   for (int c = tid; c < C; c += blockDim.x) {
     co[c] = gamma[c] * mi[C + c];
@@ -700,11 +744,8 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_acc_kernel(const double* __r
     sc[e] = ss[cc + e]; sf[e] = ss[C + cc + e]; mean[e] = mi[cc + e]; inv[e] = mi[C + cc + e];
     k0[e] = co[cc + e]; k1[e] = co[C + cc + e]; k2[e] = co[2 * C + cc + e];
   }
-  const f32x4* z4 = reinterpret_cast<const f32x4*>(z);
-  const f32x4* d4 = reinterpret_cast<const f32x4*>(dy);
   f32x4* o4 = reinterpret_cast<f32x4*>(dz);
-  for (long long i = (long long)blockIdx.x * blockDim.x + tid; i < n4; i += (long long)gridDim.x * blockDim.x) {
-    const f32x4 zz = z4[i], dd = d4[i];
+  auto apply = [&](long long i, const f32x4& zz, const f32x4& dd) {
     f32x4 o;
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
@@ -714,7 +755,11 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_acc_kernel(const double* __r
     }
     if (dz) o4[i] = o;
     if (dz16) store16(dz16, i, o);
-  }
+  };
+#pragma unroll
+  for (int u = 0; u < ACC_PF; ++u)
+    if (i0 + u * stride < n4) apply(i0 + u * stride, zp[u], dp[u]);
+  for (long long i = i0 + ACC_PF * stride; i < n4; i += stride) apply(i, z4[i], d4[i]);
 }
 
 // blocks of the accumulator passes: ~2 float4 per thread, at most `cap` blocks — each block reads the
@@ -929,7 +974,8 @@ extern "C" int cgan3d_bn_apply_acc(const double* acc, int32_t reps, int32_t c, i
                    (zero || !zero_n),
                "cgan3d_bn_apply_acc: channels must divide 256 (4..128), reps 1..64");
   const long long n4 = (long long)nvox * c / 4;
-  ::cg::launch(bn_apply_acc_kernel, dim3(acc_pass_blocks(n4)), dim3(256), 0, (hipStream_t)stream, acc, (int)reps, (int)c,
+  ::cg::launch(residual ? bn_apply_acc_kernel<true> : bn_apply_acc_kernel<false>, dim3(acc_pass_blocks(n4)), dim3(256),
+               0, (hipStream_t)stream, acc, (int)reps, (int)c,
                (double)nvox, gamma, beta, running_mean, running_var, (long long*)num_batches_tracked, momentum, eps,
                scale_shift, mean_invstd, z, n4, act, slope, residual, y, reinterpret_cast<__bf16*>(y_bf16), zero,
                (int)zero_n);

@@ -44,6 +44,7 @@ def reference_check(rank, S, B):
         dist.all_reduce(t, op=dist.ReduceOp.SUM)
         flat_grad.copy_(t / dist.get_world_size())
     solo._allreduce = plain_mean
+    solo.g_split = 0  # whole-arena Adam after the wrapped backward (the split one starts inside it)
     orig_update = solo.generator_update
 
     def solo_generator_update():  # the single-rank engine skips _allreduce for G (world 1): add it

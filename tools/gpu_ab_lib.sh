@@ -3,6 +3,6 @@
 set -o pipefail
 cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out
 for k in 1 2 3; do
-timeout -k 10 200 python -u bench.py --no-cpu-baseline > gpurun_out/abl_new_$k.json 2> gpurun_out/abl_new_$k.err || exit $?
-CGAN3D_LIB_PATH=$GRAFT_REPO_ROOT/ab/libcgan3d_base.so timeout -k 10 200 python -u bench.py --no-cpu-baseline > gpurun_out/abl_base_$k.json 2> gpurun_out/abl_base_$k.err || exit $?
+timeout -k 10 200 python -u bench.py --no-cpu-baseline ${AB_ARGS} > gpurun_out/abl_new_$k.json 2> gpurun_out/abl_new_$k.err || exit $?
+CGAN3D_LIB_PATH=$GRAFT_REPO_ROOT/ab/libcgan3d_base.so timeout -k 10 200 python -u bench.py --no-cpu-baseline ${AB_ARGS} > gpurun_out/abl_base_$k.json 2> gpurun_out/abl_base_$k.err || exit $?
 done
