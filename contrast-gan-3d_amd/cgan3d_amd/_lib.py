@@ -130,7 +130,8 @@ _SIGS = {
     "cgan3d_loss_ws_floats": ([_I64], _I64),
     "cgan3d_critic_logits_grad": ([_P, _I32, _I32, _I32, _I32, _F, _P, _P, _P], _I32),
     "cgan3d_gradient_penalty": ([_P, _I32, _I64, _F, _P, _P, _P, _P], _I32),
-    "cgan3d_gradient_penalty_part": ([_P, _P, _I32, _I32, _I64, _F, _P, _P, _P, _I32, _I32, _I32, _F, _P], _I32),
+    "cgan3d_gradient_penalty_part": ([_P, _P, _I32, _I32, _I64, _F, _P, _P, _P, _I32, _I32, _I32, _F, _P, _I64, _P],
+                                     _I32),
     "cgan3d_generator_logits_grad": ([_P, _I32, _F, _P, _P, _P], _I32),
     "cgan3d_generator_output_grad": ([_P, _P, _P, _P, _P, _I64, _F, _F, _F, _F, _P, _P, _P, _P], _I32),
     "cgan3d_adam_tick": ([_P, _P], _I32),

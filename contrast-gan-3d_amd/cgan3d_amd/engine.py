@@ -1300,10 +1300,11 @@ class StepEngine:
         if self.gp_part is not None:  # the input-grad wrote the per-sample sums of squares
             ops.gradient_penalty_part(self.gbuf, self.gp_part, bg, self.gp_part.numel() // bg, V, self.gp_weight,
                                       gamma, self.losses, logits=D.a[-1] if self.fold_logits else None, n_real=bo,
-                                      n_fake=bs, logit_ps=D.logit_ps, gan_w=self.gan_w)
+                                      n_fake=bs, logit_ps=D.logit_ps, gan_w=self.gan_w,
+                                      zero=self.d_arena.grad_padded)  # optimizer_D.zero_grad (Trainer.py:109)
         else:
             ops.gradient_penalty(self.gbuf, bg, V, self.gp_weight, gamma, self.losses, self.loss_ws)
-        ops.zero(self.d_arena.grad_padded)  # optimizer_D.zero_grad (Trainer.py:109): every layer then accumulates
+            ops.zero(self.d_arena.grad_padded)  # optimizer_D.zero_grad (Trainer.py:109): every layer then accumulates
         D.gp_grads_overlapped(self.dP, self.dG, self.xc, gamma, bo + bs, bg, nall, bo + bs, zeroed=True)
         D.join_side()
         self._allreduce(self.d_arena.grad)  # on the critical path: the G update uses the new critic

@@ -972,17 +972,21 @@ def gradient_penalty(grad, b, per_sample, lambda_, gamma_out, losses, ws):
 
 
 def gradient_penalty_part(grad, part, b, chunks, per_sample, lambda_, gamma_out, losses, logits=None, n_real=0,
-                          n_fake=0, logit_ps=0, gan_w=0.0):
+                          n_fake=0, logit_ps=0, gan_w=0.0, zero=None):
     """cgan3d_gradient_penalty_part: the GP from per-sample partial sums of squares part[b][chunks]
-    (and, given the critic's logits, the Wasserstein term and critic loss in the same launch)."""
+    (and, given the critic's logits, the Wasserstein term and critic loss in the same launch;
+    given `zero`, fp32 zeros written over it by the same launch)."""
     _need(grad, b * per_sample, "gradient_penalty_part grad")
     _need(part, b * chunks, "gradient_penalty_part part", exact=False)
     _need(gamma_out, b * per_sample, "gradient_penalty_part gamma")
     _need(losses, 8, "losses")
     if logits is not None:
         _need(logits, (n_real + n_fake) * logit_ps, "gradient_penalty_part logits", exact=False)
+    if zero is not None:
+        _need(zero, zero.numel(), "gradient_penalty_part zero")
     check(_launch("cgan3d_gradient_penalty_part", ptr(grad), ptr(part), b, chunks, per_sample, lambda_,
-                  ptr(gamma_out), ptr(losses), ptr(logits), n_real, n_fake, logit_ps, gan_w), "gradient_penalty_part")
+                  ptr(gamma_out), ptr(losses), ptr(logits), n_real, n_fake, logit_ps, gan_w, ptr(zero),
+                  0 if zero is None else zero.numel()), "gradient_penalty_part")
 
 
 def sumsq_blocks(g) -> int:

@@ -211,10 +211,8 @@ int wgrad_k3_launch(const cgan3d_conv_geom* g, const float* gathered, const floa
 int wgrad_c1_launch(const cgan3d_conv_geom* g, const float* gathered, const float* aligned, float* dw, hipStream_t st);
 void wgrad_bf16_set_blocks(int v);
 void halo_set_min_blocks(int v);
-void k7m_set_dbg(int v);
 void k3_tile_set(int v);
 void k3_split_set(int v);
-void halo_set_dbg(int v);
 int wgrad_bf16_group_launch(const cgan3d_conv_geom* geoms, const float* const* gathered, const float* const* aligned,
                             float* const* ws, int n, hipStream_t st);
 int wgrad_bf16_launch(const cgan3d_conv_geom* g, const float* gathered, const float* aligned, float* dwp,

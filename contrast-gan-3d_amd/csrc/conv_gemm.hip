@@ -657,10 +657,8 @@ extern "C" int cgan3d_set_tuning(int32_t key, int32_t value) {
   if (key == 2) { halo_set_min_blocks(value); return CGAN3D_OK; }
   if (key == 3) { k3_tile_set(value); return CGAN3D_OK; }
   if (key == 4) { s2_set(value); return CGAN3D_OK; }
-  if (key == 8) { halo_set_dbg(value); return CGAN3D_OK; }
   if (key == 9) { wgrad_k3_set_chunks(value); return CGAN3D_OK; }
   if (key == 10) { wgrad_s2_set_blocks(value); return CGAN3D_OK; }
-  if (key == 11) { k7m_set_dbg(value); return CGAN3D_OK; }
   if (key == 12) { k3_split_set(value); return CGAN3D_OK; }
   if (key == 13) { k7s_set(value); return CGAN3D_OK; }
   if (key == 14) { cout1_wave_set(value); return CGAN3D_OK; }

@@ -96,7 +96,7 @@ __global__ __launch_bounds__(256, 2) void k7m_n2w_kernel(K7Args a, const float* 
   __shared__ float red[4][C];
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int g = lane >> 4, r16 = lane & 15;
-  if (!(a.dbg & 16)) k7m_stage<(N_PAIRS * C * 8 + 255) / 256>(
+  k7m_stage<(N_PAIRS * C * 8 + 255) / 256>(
       w, N_PAIRS * C * 8,
       [&](int i) -> long long {
         const int tw = i & 7, c = (i >> 3) & 15, p = i >> 7;
@@ -110,7 +110,6 @@ __global__ __launch_bounds__(256, 2) void k7m_n2w_kernel(K7Args a, const float* 
     xs[r * N_HWP + N_HW + 1] = (__bf16)0.f;
   }
   __syncthreads();
-  if (a.dbg & 32) return;
   bf16x8_k bv[N_PAIRS / 4];  // K-step ks: pair 4ks + g, tw 0..7, channel r16
 #pragma unroll
   for (int ks = 0; ks < N_PAIRS / 4; ++ks) bv[ks] = *reinterpret_cast<const bf16x8_k*>(wt + ((4 * ks + g) * C + r16) * 8);
@@ -164,7 +163,7 @@ __global__ __launch_bounds__(256, 2) void k7m_n2w_kernel(K7Args a, const float* 
     }
   }
   const int t0 = blockIdx.x * tiles_per_block, t1 = min(ntiles, t0 + tiles_per_block);
-  if (t0 < t1 && !(a.dbg & 4)) load(t0);
+  if (t0 < t1) load(t0);
   for (int tile = t0; tile < t1; ++tile) {
     int n, d0, h0, w0;
     tile_origin(tile, &n, &d0, &h0, &w0);
@@ -179,9 +178,9 @@ __global__ __launch_bounds__(256, 2) void k7m_n2w_kernel(K7Args a, const float* 
         *reinterpret_cast<bf16x2_k*>(xs + ((c & 255) * N_HH + ((c >> 8) & 255)) * N_HWP + (c >> 16)) = v;
       }
     }
-    if (tile + 1 < t1 && !(a.dbg & 4)) load(tile + 1);  // in flight during this tile's MFMAs
+    if (tile + 1 < t1) load(tile + 1);  // in flight during this tile's MFMAs
     __syncthreads();
-    if (!(a.dbg & 1)) for (int i = tid; i < N_ROWS * 2; i += 256) {  // unfold (row, half of ow): 8 shifted windows
+    for (int i = tid; i < N_ROWS * 2; i += 256) {  // unfold (row, half of ow): 8 shifted windows
       const int r = i >> 1, hf = i & 1;
       const u32x4 lo = *reinterpret_cast<const u32x4*>(xs + r * N_HWP + 8 * hf);
       const u32x4 hi = *reinterpret_cast<const u32x4*>(xs + r * N_HWP + 8 * hf + 8);
@@ -204,7 +203,6 @@ __global__ __launch_bounds__(256, 2) void k7m_n2w_kernel(K7Args a, const float* 
     const __bf16* ub = us + wave * N_HH * N_US;
 #pragma unroll
     for (int ks = 0; ks < N_PAIRS / 4; ++ks) {
-      if (a.dbg & 2) break;
       bf16x8_k av[N_TH];
 #pragma unroll
       for (int r = 0; r < N_TH; ++r) av[r] = *reinterpret_cast<const bf16x8_k*>(ub + aoff[ks] + r * N_US);
@@ -220,8 +218,7 @@ __global__ __launch_bounds__(256, 2) void k7m_n2w_kernel(K7Args a, const float* 
     for (int r = 0; r < N_TH; ++r) {
       const int oh = h0 + r;
       if (od < a.do_ && oh < a.ho && ow < a.wo) {
-        if (!(a.dbg & 8))
-          *reinterpret_cast<f32x4*>(y + (((n * a.do_ + od) * a.ho + oh) * a.wo + ow) * C + 4 * g) = acc[r];
+        *reinterpret_cast<f32x4*>(y + (((n * a.do_ + od) * a.ho + oh) * a.wo + ow) * C + 4 * g) = acc[r];
 #pragma unroll
         for (int jj = 0; jj < 4; ++jj) s1[jj] += acc[r][jj];
       }
@@ -431,7 +428,7 @@ __global__ __launch_bounds__(256, 2) void k7m_w2n_kernel(K7Args a, const float* 
     }
   };
   const int t0 = blockIdx.x * tiles_per_block, t1 = min(ntiles, t0 + tiles_per_block);
-  if (t0 < t1 && !(a.dbg & 2)) load(t0, 0);
+  if (t0 < t1) load(t0, 0);
   for (int tile = t0; tile < t1; ++tile) {
     f32x4 acc[2];  // independent accumulators: back-to-back MFMAs do not wait on each other
 #pragma unroll
@@ -439,12 +436,11 @@ __global__ __launch_bounds__(256, 2) void k7m_w2n_kernel(K7Args a, const float* 
 #pragma unroll
     for (int half = 0; half < 2; ++half) {
       __syncthreads();  // every wave done reading hs (and red) of the previous half / tile
-      if (!(a.dbg & 4)) store();
-      if (a.dbg & 2) {}
-      else if (half == 0) load(tile, 1);
+      store();
+      if (half == 0) load(tile, 1);
       else if (tile + 1 < t1) load(tile + 1, 0);
       __syncthreads();
-      if (!(a.dbg & 1)) {
+      {
         // software-pipelined: row prl + 1's four fragments are read from LDS while row prl's two
         // MFMAs run (the LDS latency is otherwise exposed on every row)
         bf16x8_k av[2][2], bv[2][2];
@@ -495,10 +491,8 @@ __global__ __launch_bounds__(256, 2) void k7m_w2n_kernel(K7Args a, const float* 
       float v = red[0][tid] + red[1][tid] + red[2][tid] + red[3][tid] + (bias ? bias[0] : 0.f);
       if (act == CGAN3D_ACT_TANH) v = tanhf(v);
       const int o = ((n * a.do_ + od) * a.ho + oh) * a.wo + ow;
-      if (!(a.dbg & 8)) {
       y[o] = v;
       if (out2) out2[o] = minuend[o] - v;
-      }
     }
   }
 }
@@ -854,13 +848,12 @@ __global__ __launch_bounds__(256, 2) void k7m_wg_kernel(K7Args a, const float* _
     boff[jl] = ((td * (G_TH + 6) + th) * 8 + (r16 & 7)) * G_SXW;
   }
   const int t0 = blockIdx.x * tiles_per_block, t1 = min(ntiles, t0 + tiles_per_block);
-  if (t0 < t1 && !(a.dbg & 4)) load(t0);
+  if (t0 < t1) load(t0);
   for (int tile = t0; tile < t1; ++tile) {
     __syncthreads();  // previous tile's reads of sx / as done
-    if (!(a.dbg & 8)) store();
-    if (tile + 1 < t1 && !(a.dbg & 4)) load(tile + 1);  // in flight during this tile's MFMAs
+    store();
+    if (tile + 1 < t1) load(tile + 1);  // in flight during this tile's MFMAs
     __syncthreads();
-    if (!(a.dbg & 1))
     for (int i = tid; i < G_ROWS_IN * 2; i += 256) {  // shifted copies of (row, half): 8 tw
       const int r = i >> 1, hf = i & 1;
       const u32x4 lo = *reinterpret_cast<const u32x4*>(xh + r * G_HWP + 8 * hf);
@@ -878,7 +871,6 @@ __global__ __launch_bounds__(256, 2) void k7m_wg_kernel(K7Args a, const float* _
       }
     }
     __syncthreads();
-    if (a.dbg & 2) continue;
     // K-step ks = 32 voxels = tile rows 2ks, 2ks+1 (16 w each); lane group g: row 2ks + (g >> 1), w 8 (g & 1)
     // K-step ks = 32 voxels = tile rows 2ks, 2ks+1; lane group g: row 2ks + (g >> 1), w 8 (g & 1).
     // Two fragment sets in registers: K-step ks + 1's reads are in flight during ks's MFMAs.
@@ -941,12 +933,9 @@ static void k7m_wg_split(const cgan3d_conv_geom* g, bool wide_in, int* grid, int
   *grid = (*ntiles + *per - 1) / *per;
 }
 
-static int g_k7m_dbg = 0;
-void k7m_set_dbg(int v) { g_k7m_dbg = v; }
 
 static K7Args k7m_args(const cgan3d_conv_geom* g, int P, int reflect, int flip, long long wc, int td, int th, int tw) {
   K7Args a;
-  a.dbg = g_k7m_dbg;
   a.n = g->n; a.di = g->di; a.hi = g->hi; a.wi = g->wi; a.do_ = g->do_; a.ho = g->ho; a.wo = g->wo;
   a.P = P; a.reflect = reflect; a.flip = flip; a.wc = wc;
   a.tiles_d = (g->do_ + td - 1) / td; a.tiles_h = (g->ho + th - 1) / th; a.tiles_w = (g->wo + tw - 1) / tw;

@@ -401,11 +401,12 @@ __device__ __forceinline__ void s2t_class(const __bf16* halo, const __bf16* wts,
       }
 }
 
-// Persistent: a block loops over tiles (grid = min(tiles, 2 per CU, 1 in mode 2)); the weights are staged into
+// Persistent: a block loops over tiles (grid = min(tiles, 2 per CU; 1 for mode 2 without the bf16
+// shadow)); the weights are staged into
 // LDS once, the next tile's halo is loaded into registers while the current tile's MFMAs and
-// epilogue run, and the mode-2 z granules of a tile are issued before its halo is staged.
+// epilogue run.
 template <int MODE, bool X16>  // statistics mode s2_stat_mode(ep): 0 none, 1 forward, 2 input-grad; X16: ep.x16
-__global__ __launch_bounds__(256, MODE == 2 ? 1 : 2) void conv_s2t_kernel(S2Args a, const float* __restrict__ x,
+__global__ __launch_bounds__(256, MODE == 2 && !X16 ? 1 : 2) void conv_s2t_kernel(S2Args a, const float* __restrict__ x,
                                                           const __bf16* __restrict__ wpk, float* y, Epi ep, int ntiles) {
   constexpr int CI = 32, CO = 16;
   __shared__ __attribute__((aligned(16))) __bf16 halo[T_HALO];
@@ -513,11 +514,6 @@ __global__ __launch_bounds__(256, MODE == 2 ? 1 : 2) void conv_s2t_kernel(S2Args
       ok[u] = v_ok;
       obase[u] = v_ok ? (((nb * a.do_ + 2 * jz + rz) * a.ho + 2 * jy + ry) * a.wo + 2 * jx + rx) * CO + 4 * g : 0;
     }
-    f32x4 zv[MODE == 2 ? 16 : 1];  // mode 2: in flight during the staging and the MFMAs
-    if constexpr (MODE == 2) {
-#pragma unroll
-      for (int u = 0; u < 16; ++u) zv[u] = *reinterpret_cast<const f32x4*>(ep.bn_z + obase[u]);
-    }
     __syncthreads();  // every wave done with the previous tile's halo (and the weight staging)
     store();
     __syncthreads();
@@ -535,12 +531,18 @@ __global__ __launch_bounds__(256, MODE == 2 ? 1 : 2) void conv_s2t_kernel(S2Args
     s2t_class<1, 1, 0>(halo, wts, acc[6], wave, g, r16);
     s2t_class<1, 1, 1>(halo, wts, acc[7], wave, g, r16);
 
-    // ---- epilogue: 16-byte stores of whole lines; mode 2 statistics streamed, mode 1 from the held
-    // outputs (M2 about the block mean)
+    // ---- epilogue: 16-byte stores of whole lines; mode 2 statistics streamed (z loaded here: the
+    // second resident block's MFMAs cover the round trip), mode 1 from the held outputs (M2 about
+    // the block mean)
     f32x4 vals[MODE == 1 ? 16 : 1][1];
     float s2s[1][4] = {}, s2q[1][4] = {};
 #pragma unroll
-    for (int p = 0; p < 4; ++p)  // (rz, ry): classes 2p (rx = 0) and 2p + 1 (rx = 1)
+    for (int p = 0; p < 4; ++p) {  // (rz, ry): classes 2p (rx = 0) and 2p + 1 (rx = 1)
+      f32x4 zv[MODE == 2 ? 4 : 1];  // outputs u = 4p .. 4p + 3
+      if constexpr (MODE == 2) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) zv[k] = *reinterpret_cast<const f32x4*>(ep.bn_z + obase[4 * p + k]);
+      }
 #pragma unroll
       for (int zz = 0; zz < 2; ++zz) {
         f32x4 out[2];
@@ -550,9 +552,10 @@ __global__ __launch_bounds__(256, MODE == 2 ? 1 : 2) void conv_s2t_kernel(S2Args
           const int u = (p * 2 + zz) * 2 + S;
           if (ok[u]) *reinterpret_cast<f32x4*>(y + obase[u]) = out[S];
           if constexpr (MODE == 1) vals[u][0] = out[S];
-          if constexpr (MODE == 2) s2_m2_add(ep, k2, out[S], zv[u], ok[u], s2s[0], s2q[0]);
+          if constexpr (MODE == 2) s2_m2_add(ep, k2, out[S], zv[u - 4 * p], ok[u], s2s[0], s2q[0]);
         }
       }
+    }
     const int cnt = 8 * max(0, min(2, a.cd - Z0)) * max(0, min(4, a.ch - Y0)) * max(0, min(16, a.cw - X0));
     if constexpr (MODE == 1) s2_stats_m1<16, 1>(ep, CO, vals, ok, cnt, red, tile);
     if constexpr (MODE == 2) {
@@ -613,8 +616,9 @@ int s2_launch(const cgan3d_conv_geom* g, const float* x, const __bf16* wp, float
 #define CG_S2(K, M) ::cg::launch(K<M>, grid, dim3(256), 0, st, a, x, wp, y, e)
   if (kind == 1) { if (mode == 2) CG_S2(conv_s2f_kernel, 2); else if (mode == 1) CG_S2(conv_s2f_kernel, 1); else CG_S2(conv_s2f_kernel, 0); }
 #undef CG_S2
-  else {  // persistent: two blocks per CU (one with the mode-2 z granules prefetched)
-    const dim3 pgrid((unsigned)std::min<long long>(ntiles, (mode == 2 ? 1LL : 2LL) * cu_count()));
+  else {  // persistent: two blocks per CU (one for mode 2 from fp32 input: its staging registers)
+    const long long per_cu = mode == 2 && !e.x16 ? 1 : 2;
+    const dim3 pgrid((unsigned)std::min<long long>(ntiles, per_cu * cu_count()));
 #define CG_S2T(M, X) ::cg::launch(conv_s2t_kernel<M, X>, pgrid, dim3(256), 0, st, a, x, wp, y, e, (int)ntiles)
     if (e.x16) { if (mode == 2) CG_S2T(2, true); else if (mode == 1) CG_S2T(1, true); else CG_S2T(0, true); }
     else { if (mode == 2) CG_S2T(2, false); else if (mode == 1) CG_S2T(1, false); else CG_S2T(0, false); }

@@ -9,11 +9,13 @@
 //  * MT = 1: the four waves take K-steps w, w + 4, ... of the same 16 x (16 NT) tile and are summed
 //    once through LDS (4x the blocks of a 64-row tiling); MT = 4: each wave its own 16 rows, all K
 //    (short K, many rows);
-//  * operands straight from L2, no LDS staging: A = 8 consecutive K = 8 channels of one gathered
-//    voxel (two float4, converted to bf16), B = packed weights format 3, bf16 [b][tap][a], one
-//    16-byte load per fragment; the next K-step's loads are in flight during the current MFMAs;
-//  * epilogue: bias / activation / LeakyReLU-mask / residual, per-block BatchNorm statistics
-//    (sum, M2, count) for the BatchNorm critic of the weight-clip configuration.
+//  * operands straight from L2, no LDS staging: activations = 8 consecutive K = 8 channels of one
+//    gathered voxel (two float4, converted to bf16), weights = packed format 3, bf16 [b][tap][a],
+//    one 16-byte load per fragment; the next K-step's loads are in flight during the current MFMAs;
+//  * MFMA transposed (A = weights, B = activations): a lane ends with 4 channels of one output
+//    voxel, so the epilogue (bias / activation / LeakyReLU-mask / residual) moves 16 bytes per
+//    lane access; per-block BatchNorm statistics (sum, M2, count) for the BatchNorm critic of the
+//    weight-clip configuration.
 #include "common.h"
 
 namespace cg {
@@ -136,7 +138,7 @@ __global__ __launch_bounds__(64 * W) void conv_sk_kernel(SkArgs a, const float* 
         for (int t = 0; t < NT; ++t) bv[t] = bb[i][t];
         if (q + PF < nk) load(ks0 + (q + PF) * kstep, i);
 #pragma unroll
-        for (int t = 0; t < NT; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, bv[t], acc[t], 0, 0, 0);
+        for (int t = 0; t < NT; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bv[t], av, acc[t], 0, 0, 0);
       }
     }
   }
@@ -155,54 +157,60 @@ __global__ __launch_bounds__(64 * W) void conv_sk_kernel(SkArgs a, const float* 
       acc[t] += r;
     }
   }
-  // epilogue: lane holds rows mt*16 + 4g + jj, channel t*16 + r16
+  // epilogue: the MFMA ran transposed (A = weights, B = activations), so lane (g, r16) holds
+  // channels t*16 + 4g .. +3 of row mt*16 + r16: one 16-byte store (and mask / residual load) per
+  // lane and N tile (cout % 8 == 0: a lane's four channels are all in range or all out)
+  const int ro = rowo[mt * 16 + r16];
   float vals[NT][4];
-  int ro[4];
-#pragma unroll
-  for (int jj = 0; jj < 4; ++jj) ro[jj] = rowo[mt * 16 + 4 * g + jj];
 #pragma unroll
   for (int t = 0; t < NT; ++t) {
-    const int c = t * 16 + r16;
-    const bool cv = c < a.cout;
-    const float b = (ep.bias && cv) ? ep.bias[c] : 0.f;
+    const int c0 = t * 16 + 4 * g;
+    const bool ok = c0 < a.cout && ro >= 0;
+    f32x4 v = acc[t];
+    if (ep.bias && c0 < a.cout) {
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj) v[jj] += ep.bias[c0 + jj];
+    }
 #pragma unroll
     for (int jj = 0; jj < 4; ++jj) {
-      float v = acc[t][jj] + b;
-      if (ep.act == CGAN3D_ACT_RELU) v = fmaxf(v, 0.f);
-      else if (ep.act == CGAN3D_ACT_LRELU) v = v > 0.f ? v : v * ep.slope;
-      const bool ok = cv && ro[jj] >= 0;
-      if (ok) {
-        const int o = ro[jj] * a.cout + c;
-        if (ep.mask_src) v = ep.mask_src[o] > 0.f ? v : v * ep.slope;
-        if (ep.residual) v += ep.residual[o];
-        y[o] = v;
-      }
-      vals[t][jj] = ok ? v : 0.f;
+      if (ep.act == CGAN3D_ACT_RELU) v[jj] = fmaxf(v[jj], 0.f);
+      else if (ep.act == CGAN3D_ACT_LRELU) v[jj] = v[jj] > 0.f ? v[jj] : v[jj] * ep.slope;
     }
+    if (ok) {
+      const int o = ro * a.cout + c0;
+      if (ep.mask_src) {
+        const f32x4 m = *reinterpret_cast<const f32x4*>(ep.mask_src + o);
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) v[jj] = m[jj] > 0.f ? v[jj] : v[jj] * ep.slope;
+      }
+      if (ep.residual) v += *reinterpret_cast<const f32x4*>(ep.residual + o);
+      *reinterpret_cast<f32x4*>(y + o) = v;
+    }
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj) vals[t][jj] = ok ? v[jj] : 0.f;
   }
   if (ep.stats) {  // (sum, M2 about the row mean, count) of this wave's 16 rows: one stats row per
-                   // block (MT == 1) or per wave (MT == 4)
+                   // block (MT == 1) or per wave (MT == 4); rows are the 16 lanes of a lane group
     int cnt = 0;
     for (int r = 0; r < 16; ++r) cnt += rowo[mt * 16 + r] >= 0;
     const long long sb = ((long long)blockIdx.x * MT + mt) * (2 * a.cout + 1);
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
-      const int c = t * 16 + r16;
-      float S = vals[t][0] + vals[t][1] + vals[t][2] + vals[t][3];
-      S += __shfl_xor(S, 16, 64);
-      S += __shfl_xor(S, 32, 64);
-      const float mean = cnt ? S / cnt : 0.f;
-      float q = 0.f;
+      const int c0 = t * 16 + 4 * g;
 #pragma unroll
       for (int jj = 0; jj < 4; ++jj) {
-        const float d = ro[jj] >= 0 ? vals[t][jj] - mean : 0.f;
-        q += d * d;
-      }
-      q += __shfl_xor(q, 16, 64);
-      q += __shfl_xor(q, 32, 64);
-      if (g == 0 && c < a.cout) {
-        ep.stats[sb + c] = S;
-        ep.stats[sb + a.cout + c] = q;
+        float S = vals[t][jj];
+#pragma unroll
+        for (int off = 8; off > 0; off >>= 1) S += __shfl_xor(S, off, 64);
+        const float mean = cnt ? S / cnt : 0.f;
+        const float d = ro >= 0 ? vals[t][jj] - mean : 0.f;
+        float q = d * d;
+#pragma unroll
+        for (int off = 8; off > 0; off >>= 1) q += __shfl_xor(q, off, 64);
+        if (r16 == 0 && c0 < a.cout) {
+          ep.stats[sb + c0 + jj] = S;
+          ep.stats[sb + a.cout + c0 + jj] = q;
+        }
       }
     }
     if (lane == 0) ep.stats[sb + 2 * a.cout] = (float)cnt;
@@ -255,6 +263,8 @@ long long sk_blocks(const cgan3d_conv_geom* g) {  // rows of the statistics epil
 
 int sk_launch(const cgan3d_conv_geom* g, const float* x, const __bf16* wp, float* y, const Epi& e, hipStream_t st) {
   CG_CHECK_ARG(!e.out2 && !e.minuend && !e.bn_mode, "conv_sk: no out2 / BatchNorm-slab epilogue");
+  CG_CHECK_ARG(!(((uintptr_t)y | (uintptr_t)e.mask_src | (uintptr_t)e.residual) & 15),
+               "conv_sk: output / mask / residual must be 16-byte aligned (float4 epilogue)");
   int mt;
   SkArgs a = sk_args(g, &mt);
   const int nt = (g->cout + 15) / 16;

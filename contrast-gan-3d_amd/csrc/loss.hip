@@ -87,9 +87,12 @@ __global__ __launch_bounds__(256) void gp_scale_kernel(const float* __restrict__
                                                        float lambda_, float* losses, const float* __restrict__ g,
                                                        long long ps, long long total, float* out,
                                                        const float* __restrict__ lg, int nr, int nf, int lps,
-                                                       float gan_w) {
+                                                       float gan_w, float* zero, long long zero_n) {
   __shared__ double red[4];
   __shared__ float coef[1024];
+  // the critic's gradient arena zeroed here (optimizer_D.zero_grad) instead of in a fill launch
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < zero_n; i += (long long)gridDim.x * blockDim.x)
+    zero[i] = 0.f;
   double acc = 0.0;
   if (chunks >= 64) {  // many partials per sample: the block sums each sample's together
     for (int b = 0; b < B; ++b) {
@@ -259,7 +262,7 @@ extern "C" int cgan3d_gradient_penalty(const float* grad, int32_t b, int64_t per
   const long long total = (long long)b * per_sample;
   int blocks = (int)std::min<long long>((total + 255) / 256, 1024);
   ::cg::launch(gp_scale_kernel, dim3(blocks), dim3(256), 0, s, part, b, chunks, lambda_, losses, grad,
-               (long long)per_sample, total, gamma_out, (const float*)nullptr, 0, 0, 0, 0.f);
+               (long long)per_sample, total, gamma_out, (const float*)nullptr, 0, 0, 0, 0.f, (float*)nullptr, 0LL);
   CG_LAUNCH_CHECK("gp_scale_kernel");
   return CGAN3D_OK;
 }
@@ -267,15 +270,16 @@ extern "C" int cgan3d_gradient_penalty(const float* grad, int32_t b, int64_t per
 extern "C" int cgan3d_gradient_penalty_part(const float* grad, const float* part, int32_t b, int32_t chunks,
                                             int64_t per_sample, float lambda_, float* gamma_out, float* losses,
                                             const float* logits, int32_t n_real, int32_t n_fake, int32_t logit_ps,
-                                            float gan_w, void* stream) {
+                                            float gan_w, float* zero, int64_t zero_n, void* stream) {
   CG_CHECK_ARG(grad && part && gamma_out && losses, "cgan3d_gradient_penalty_part: null pointer");
+  CG_CHECK_ARG(zero_n >= 0 && (zero || !zero_n), "cgan3d_gradient_penalty_part: zero range");
   CG_CHECK_ARG(b > 0 && b <= 1024 && chunks > 0 && per_sample > 0, "cgan3d_gradient_penalty_part: bad sizes");
   CG_CHECK_ARG(!logits || (n_real > 0 && n_fake > 0 && logit_ps > 0), "cgan3d_gradient_penalty_part: bad logit sizes");
   const long long total = (long long)b * per_sample;
   // every block sums the b x chunks partials itself: fewer, longer blocks when there are many
   int blocks = (int)std::min<long long>((total + 255) / 256, chunks >= 64 ? 256 : 1024);
   ::cg::launch(gp_scale_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, part, b, chunks, lambda_, losses, grad,
-               (long long)per_sample, total, gamma_out, logits, n_real, n_fake, logit_ps, gan_w);
+               (long long)per_sample, total, gamma_out, logits, n_real, n_fake, logit_ps, gan_w, zero, (long long)zero_n);
   CG_LAUNCH_CHECK("gp_scale_kernel");
   return CGAN3D_OK;
 }

@@ -392,10 +392,13 @@ int cgan3d_gradient_penalty(const float* grad, int32_t b, int64_t per_sample, fl
  * critic's first-layer input-grad with cgan3d_conv3d_sumsq_blocks): one scaling pass. */
 int cgan3d_gradient_penalty_part(const float* grad, const float* part, int32_t b, int32_t chunks, int64_t per_sample,
                                  float lambda_, float* gamma_out, float* losses, const float* logits, int32_t n_real,
-                                 int32_t n_fake, int32_t logit_ps, float gan_w, void* stream);
+                                 int32_t n_fake, int32_t logit_ps, float gan_w, float* zero, int64_t zero_n,
+                                 void* stream);
 /* logits (optional, [real n_real x logit_ps | fake n_fake x logit_ps]): the same launch also writes the
  * Wasserstein term and the critic loss (what cgan3d_critic_logits_grad's losses would be), for a
- * caller whose dlogits are constant buffers written once (so that launch is not needed at all). */
+ * caller whose dlogits are constant buffers written once (so that launch is not needed at all).
+ * zero (optional, zero_n floats): written with zeros by the same launch — the critic's gradient arena
+ * (optimizer_D.zero_grad, Trainer.py:109) without a fill launch of its own. */
 /* dlogits may be NULL: the loss only (constant dlogits kept by the caller). */
 int cgan3d_generator_logits_grad(const float* logits, int32_t n, float gan_w, float* dlogits,
                                  float* losses, void* stream);

@@ -530,6 +530,12 @@ def test_conv_s2_bf16(role, fine):
     want = torch.cat([gg.sum(0), (gg * (zz - mid[:cout]) * mid[cout:]).sum(0)])
     got = part2.double().cpu().view(2 * cout, slots).sum(1)
     assert_close(got.numpy(), want.numpy(), 1e-4, f"{role} mode-2 slab")
+    # mode 2 staged from the bf16 shadow (S2T: two resident blocks per CU instead of one): bit-identical
+    y2b, part2b = torch.empty_like(y), torch.full_like(part2, float("nan"))
+    ops.conv(geo, _cl(x), wp, y2b, ops.epilogue(bn_part=part2b, bn_mode=2, bn_slots=slots, bn_z=z, bn_ss=ss, bn_mi=mi,
+                                                bn_act=L.ACT_RELU, x_bf16=_cl(x).bfloat16()))
+    assert torch.equal(y2b, y2) and torch.equal(part2b.nan_to_num(), part2.nan_to_num()), \
+        f"{role}: bf16-shadow mode-2 result differs"
 
 
 SK_CASES = [
