@@ -257,21 +257,23 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_fold_kernel(const float* __r
   const f32x4* z4 = reinterpret_cast<const f32x4*>(z);
   const f32x4* p4 = reinterpret_cast<const f32x4*>(padded);
   f32x4* o4 = reinterpret_cast<f32x4*>(dz);
-  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (long long)gridDim.x * blockDim.x) {
-    long long v = i / C4;
-    const int c4 = (int)(i - v * C4);
-    const int w = (int)(v % W); v /= W;
-    const int h = (int)(v % H); v /= H;
-    const int d = (int)(v % D), nb = (int)(v / D);
+  // 32-bit index math: C/4 a power of two (C divides 256), the padded volume below 2^31 float4
+  // (checked by the callers); four 64-bit divides per float4 made this pass VALU-bound
+  const int c4s = __builtin_ctz(C4);
+  for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < (unsigned)n4; i += gridDim.x * blockDim.x) {
+    const unsigned v0 = i >> c4s;
+    const int c4 = (int)(i & (C4 - 1));
+    const unsigned v1 = v0 / (unsigned)W, v2 = v1 / (unsigned)H, v3 = v2 / (unsigned)D;
+    const int w = (int)(v0 - v1 * W), h = (int)(v1 - v2 * H), d = (int)(v2 - v3 * D), nb = (int)v3;
     int qd[2], qh[2], qw[2];
     const int nd = fold_src(d, D, P, qd), nh = fold_src(h, H, P, qh), nw = fold_src(w, W, P, qw);
     const f32x4 zz = z4[i];
-    f32x4 dd = p4[(((long long)(nb * Dp + qd[0]) * Hp + qh[0]) * Wp + qw[0]) * C4 + c4];
+    f32x4 dd = p4[((((nb * Dp + qd[0]) * Hp + qh[0]) * Wp + qw[0]) << c4s) + c4];
     if (nd * nh * nw > 1) {  // boundary voxel: its mirrored sources
       for (int a = 0; a < nd; ++a)
         for (int b = 0; b < nh; ++b)
           for (int e = 0; e < nw; ++e)
-            if (a | b | e) dd += p4[(((long long)(nb * Dp + qd[a]) * Hp + qh[b]) * Wp + qw[e]) * C4 + c4];
+            if (a | b | e) dd += p4[((((nb * Dp + qd[a]) * Hp + qh[b]) * Wp + qw[e]) << c4s) + c4];
     }
     f32x4 o;
 #pragma unroll
@@ -950,6 +952,8 @@ extern "C" int cgan3d_bn_backward_slab_fold(const float* padded, const float* z,
                "cgan3d_bn_backward_slab_fold: channels must divide 256 (>= 4), dims must exceed 2*pad");
   const long long nvox = (long long)n * d * h * w;
   CG_CHECK_ARG(nvox > 1, "cgan3d_bn_backward_slab_fold: need more than one voxel");
+  CG_CHECK_ARG((long long)n * (d + 2 * pad) * (h + 2 * pad) * (w + 2 * pad) * (c / 4) < (1LL << 31),
+               "cgan3d_bn_backward_slab_fold: padded volume exceeds 32-bit float4 indexing");
   hipStream_t s = (hipStream_t)stream;
   ::cg::launch(bn_bwd_finalize_slab_kernel, dim3(c), dim3(256), 0, s, part, nslots, c, (double)nvox, gamma,
                mean_invstd, dgamma, dbeta, ws, accumulate);
@@ -1014,6 +1018,8 @@ extern "C" int cgan3d_bn_backward_acc_fold(const float* padded, const float* z, 
                "cgan3d_bn_backward_acc_fold: channels must divide 256 (4..128), dims must exceed 2*pad, reps 1..64");
   const long long nvox = (long long)n * d * h * w;
   CG_CHECK_ARG(nvox > 1, "cgan3d_bn_backward_acc_fold: need more than one voxel");
+  CG_CHECK_ARG((long long)n * (d + 2 * pad) * (h + 2 * pad) * (w + 2 * pad) * (c / 4) < (1LL << 31),
+               "cgan3d_bn_backward_acc_fold: padded volume exceeds 32-bit float4 indexing");
   const long long n4 = nvox * c / 4;
   ::cg::launch(bn_bwd_apply_fold_kernel, dim3(acc_pass_blocks(n4, 4096)), dim3(256), 0, (hipStream_t)stream, padded, z, n, d,
                h, w, pad, c, scale_shift, mean_invstd, act, slope, (const float*)nullptr, dz,

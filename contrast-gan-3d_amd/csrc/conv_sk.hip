@@ -68,13 +68,15 @@ __global__ __launch_bounds__(64 * W) void conv_sk_kernel(SkArgs a, const float* 
     tlin[tid] = (t0 * a.k + t1) * a.k + t2;
   }
   if (tid < 16 * MT) {
-    const long long m = (long long)mb * 16 * MT + tid;
-    const long long cvox = (long long)a.n * a.cd * a.ch * a.cw;
-    int jx = (int)(m % a.cw);
-    long long q = m / a.cw;
-    const int jy = (int)(q % a.ch);
-    q /= a.ch;
-    const int jz = (int)(q % a.cd), nb = (int)(q / a.cd);
+    // 32-bit index math (sk_format_ok bounds every volume below 2^31 elements)
+    const unsigned m = (unsigned)mb * 16 * MT + tid;
+    const unsigned cvox = (unsigned)a.n * a.cd * a.ch * a.cw;
+    unsigned q = m / (unsigned)a.cw;
+    const int jx = (int)(m - q * a.cw);
+    unsigned q2 = q / (unsigned)a.ch;
+    const int jy = (int)(q - q2 * a.ch);
+    q = q2 / (unsigned)a.cd;
+    const int jz = (int)(q2 - q * a.cd), nb = (int)q;
     const bool ok = m < cvox;
     int od = jz, oh = jy, ow = jx;
     if (a.transposed) {
