@@ -303,6 +303,20 @@ __device__ __forceinline__ int fold_src(int d, int D, int P, int* q) {  // padde
   return n;
 }
 
+// lin -> (x, y, z, n) over extents (X, Y, Z, -): 32-bit divides whenever lin fits (a 64-bit divide
+// is ~100 VALU instructions)
+__device__ __forceinline__ void unflatten4(long long lin, int X, int Y, int Z, int& x, int& y, int& z, int& n) {
+  if (lin < (1LL << 32)) {
+    const unsigned l = (unsigned)lin, t1 = l / (unsigned)X, t2 = t1 / (unsigned)Y, t3 = t2 / (unsigned)Z;
+    x = (int)(l - t1 * X); y = (int)(t1 - t2 * Y); z = (int)(t2 - t3 * Z); n = (int)t3;
+  } else {
+    long long t = lin / X;
+    x = (int)(lin - t * X);
+    y = (int)(t % Y); t /= Y;
+    z = (int)(t % Z); n = (int)(t / Z);
+  }
+}
+
 // slab slot b, channel c, pair member q of a fused BatchNorm slab
 __device__ __forceinline__ float* bn_slot(const Epi& e, int q, int C, int c, int b) {
   return e.bn_part + ((long long)q * C + c) * e.bn_slots + b;

@@ -243,9 +243,8 @@ __global__ __launch_bounds__(256) void conv_cout1_kernel(ConvArgs a, const float
   class_taps(rd, a.kd, a.sd, a.pd, a.transposed, &fd, &sd, &nd);
   class_taps(rh, k, s, p, a.transposed, &fh, &sh, &nh);
   class_taps(rw, k, s, p, a.transposed, &fw, &sw, &nw);
-  int jw = (int)(lin % a.cw); long long tt = lin / a.cw;
-  int jh = (int)(tt % a.ch); tt /= a.ch;
-  int jd = (int)(tt % a.cd); int nb = (int)(tt / a.cd);
+  int jw, jh, jd, nb;
+  unflatten4(lin, a.cw, a.ch, a.cd, jw, jh, jd, nb);
   int od, oh, ow, bd, bh, bw;
   if (a.transposed) { od = jd * a.sd + rd; oh = jh * s + rh; ow = jw * s + rw; bd = jd; bh = jh; bw = jw; }
   else { od = jd; oh = jh; ow = jw; bd = jd * a.sd - a.pd; bh = jh * s - p; bw = jw * s - p; }
@@ -327,9 +326,8 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(ConvArgs a, const float
     if (tid < KV) {
       long long lin = vb + tid;
       if (lin < vend) {
-        int ow = (int)(lin % a.wo); long long t = lin / a.wo;
-        int oh = (int)(t % a.ho); t /= a.ho;
-        int od = (int)(t % a.do_); int nb = (int)(t / a.do_);
+        int ow, oh, od, nb;
+        unflatten4(lin, a.wo, a.ho, a.do_, ow, oh, od, nb);
         vtab[0][tid] = nb * a.di; vtab[1][tid] = od * a.sd - a.pd; vtab[2][tid] = oh * a.s - a.p;
         vtab[3][tid] = ow * a.s - a.p; vtab[4][tid] = (int)lin;
       } else {
@@ -436,9 +434,8 @@ __global__ __launch_bounds__(256) void conv_wgrad_cout1_kernel(ConvArgs a, const
     if (tid < VB) {
       long long lin = vb + tid;
       if (lin < vend) {
-        int ow = (int)(lin % a.wo); long long t = lin / a.wo;
-        int oh = (int)(t % a.ho); t /= a.ho;
-        int od = (int)(t % a.do_); int nb = (int)(t / a.do_);
+        int ow, oh, od, nb;
+        unflatten4(lin, a.wo, a.ho, a.do_, ow, oh, od, nb);
         vtab[0][tid] = nb * a.di; vtab[1][tid] = od * a.sd - a.pd; vtab[2][tid] = oh * a.s - a.p;
         vtab[3][tid] = ow * a.s - a.p;
         gv[tid] = go[lin];
@@ -477,12 +474,12 @@ __global__ __launch_bounds__(256) void conv_wgrad_cout1_kernel(ConvArgs a, const
 // dw[a*sa + b*sb + t] (+)= dwp[(t*cin + a)*cout + b]; clean: dwp is left zeroed for its next user
 __global__ void wgrad_unpack_kernel(float* __restrict__ dwp, float* dw, int T, int cin, int cout, long long sa,
                                     long long sb, int accumulate, int clean) {
-  long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  long long total = (long long)T * cin * cout;
-  if (i >= total) return;
-  int b = (int)(i % cout); long long r = i / cout;
-  int ca = (int)(r % cin); int t = (int)(r / cin);
-  float* d = dw + ca * sa + b * sb + t;
+  // 32-bit index math (weights are far below 2^31 elements)
+  const unsigned i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (unsigned)T * cin * cout) return;
+  const unsigned r = i / (unsigned)cout, t = r / (unsigned)cin;
+  const int b = (int)(i - r * cout), ca = (int)(r - t * cin);
+  float* d = dw + ca * sa + b * sb + (int)t;
   const float v = dwp[i];
   *d = accumulate ? *d + v : v;
   if (clean) dwp[i] = 0.f;
@@ -491,12 +488,11 @@ __global__ void wgrad_unpack_kernel(float* __restrict__ dwp, float* dw, int T, i
 // the same for several weight gradients in one launch (blockIdx.y = descriptor); always clean
 __global__ __launch_bounds__(256) void wgrad_unpack_multi_kernel(const cgan3d_unpack_desc* __restrict__ descs) {
   const cgan3d_unpack_desc d = descs[blockIdx.y];
-  const long long total = (long long)d.taps * d.cin * d.cout;
-  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long long)gridDim.x * 256) {
-    const int b = (int)(i % d.cout);
-    const long long r = i / d.cout;
-    const int ca = (int)(r % d.cin), t = (int)(r / d.cin);
-    float* o = d.dw + ca * d.sa + b * d.sb + t;
+  const unsigned total = (unsigned)d.taps * d.cin * d.cout;  // 32-bit index math (small weights)
+  for (unsigned i = blockIdx.x * 256 + threadIdx.x; i < total; i += gridDim.x * 256) {
+    const unsigned r = i / (unsigned)d.cout, t = r / (unsigned)d.cin;
+    const int b = (int)(i - r * d.cout), ca = (int)(r - t * d.cin);
+    float* o = d.dw + ca * d.sa + b * d.sb + (int)t;
     const float v = d.ws[i];
     *o = d.accumulate ? *o + v : v;
     d.ws[i] = 0.f;
@@ -829,6 +825,7 @@ generic:
   }
   if (defer) return CGAN3D_OK;  // the caller's cgan3d_wgrad_unpack_multi moves it into dw
   const long long total = R * g->cout;
+  CG_CHECK_ARG(total < (1LL << 31), "wgrad unpack: weight too large for 32-bit indexing");
   ::cg::launch(wgrad_unpack_kernel, dim3(cg::ceil_div(total, 256)), dim3(256), 0, s, ws, dw, T, g->cin, g->cout,
                      (long long)g->w_sa, (long long)g->w_sb, accumulate, (int)ws_clean);
   CG_LAUNCH_CHECK("wgrad_unpack_kernel");
@@ -858,8 +855,8 @@ extern "C" int cgan3d_conv3d_wgrad_group(const cgan3d_conv_geom* geoms, const fl
 }
 
 extern "C" int cgan3d_wgrad_unpack_multi(const cgan3d_unpack_desc* descs, int32_t n, int64_t max_total, void* stream) {
-  CG_CHECK_ARG(descs && n > 0 && n <= 65535 && max_total > 0,
-               "cgan3d_wgrad_unpack_multi: need a device descriptor array, 0 < n <= 65535, max_total > 0");
+  CG_CHECK_ARG(descs && n > 0 && n <= 65535 && max_total > 0 && max_total < (1LL << 31),
+               "cgan3d_wgrad_unpack_multi: need a device descriptor array, 0 < n <= 65535, 0 < max_total < 2^31");
   const unsigned bx = (unsigned)std::min<long long>((max_total + 255) / 256, 1024);
   ::cg::launch(wgrad_unpack_multi_kernel, dim3(bx, n), dim3(256), 0, (hipStream_t)stream, descs);
   CG_LAUNCH_CHECK("wgrad_unpack_multi_kernel");

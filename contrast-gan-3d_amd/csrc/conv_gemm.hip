@@ -151,9 +151,8 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(GemmArgs a, const float*
   if (tid < BM) {
     const long long lin = v0 + tid;
     if (lin < a.class_vox) {
-      const int jw = (int)(lin % a.cw); long long t = lin / a.cw;
-      const int jh = (int)(t % a.ch); t /= a.ch;
-      const int jd = (int)(t % a.cd); const int nb = (int)(t / a.cd);
+      int jw, jh, jd, nb;
+      unflatten4(lin, a.cw, a.ch, a.cd, jw, jh, jd, nb);
       int od, oh, ow;
       if (a.transposed) {
         od = jd * a.sd + rd; oh = jh * s + rh; ow = jw * s + rw;
