@@ -94,7 +94,32 @@ __global__ __launch_bounds__(256) void gp_scale_kernel(const float* __restrict__
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < zero_n; i += (long long)gridDim.x * blockDim.x)
     zero[i] = 0.f;
   double acc = 0.0;
-  if (chunks >= 64) {  // many partials per sample: the block sums each sample's together
+  if (chunks >= 64 && B <= 8) {  // many partials, few samples: every sample's sum in one pass (all
+                                  // samples' loads in flight), one block-level reduction round
+    __shared__ double wred[8][4];
+    double ss[8];
+#pragma unroll
+    for (int b = 0; b < 8; ++b) ss[b] = 0.0;
+    for (int c = threadIdx.x; c < chunks; c += blockDim.x) {
+#pragma unroll
+      for (int b = 0; b < 8; ++b)
+        if (b < B) ss[b] += part[(long long)b * chunks + c];
+    }
+#pragma unroll
+    for (int b = 0; b < 8; ++b) {
+      if (b >= B) break;
+      const double w = wave_sum_d(ss[b]);
+      if ((threadIdx.x & 63) == 0) wred[b][threadIdx.x >> 6] = w;
+    }
+    __syncthreads();
+    if (threadIdx.x < B) {
+      const int b = threadIdx.x;
+      const double t = wred[b][0] + wred[b][1] + wred[b][2] + wred[b][3];
+      const double nrm = sqrt(t);
+      acc = (nrm - 1.0) * (nrm - 1.0);
+      coef[b] = nrm > 0.0 ? (float)(lambda_ * 2.0 / B * (nrm - 1.0) / nrm) : 0.f;
+    }
+  } else if (chunks >= 64) {  // many partials per sample: the block sums each sample's together
     for (int b = 0; b < B; ++b) {
       double ss = 0.0;
       for (int c = threadIdx.x; c < chunks; c += blockDim.x) ss += part[(long long)b * chunks + c];
