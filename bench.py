@@ -36,15 +36,15 @@ from pathlib import Path
 # with HIP's default of 4 some of them share an in-order hardware queue, where one stream's
 # cross-stream wait blocks the other's kernels (measured on one GPU, one-rank RCCL path: 2.56 ms/step
 # at 4 queues, 2.21 at 8, 2.21 at 16; 2.06 without collectives at either setting)
-# (the package raises it the same way at import, cgan3d_amd/__init__.py, so the Trainer path gets
-# the same queues; the setting in force is reported in the JSON line as config.hw_queues)
+# (cgan3d_amd.configure_hw_queues, called here before torch touches the GPU; the setting in force
+# is reported in the JSON line as config.hw_queues)
 HW_QUEUES_ENV = os.environ.get("GPU_MAX_HW_QUEUES")
-if int(os.environ.get("GPU_MAX_HW_QUEUES", "4")) < 8:
-    os.environ["GPU_MAX_HW_QUEUES"] = "8"
-
 REPO = Path(__file__).resolve().parent
 sys.path.insert(0, str(REPO / "contrast-gan-3d_amd"))
 sys.path.insert(0, str(REPO))
+import cgan3d_amd  # noqa: E402
+
+cgan3d_amd.configure_hw_queues()
 
 import numpy as np  # noqa: E402
 import torch  # noqa: E402

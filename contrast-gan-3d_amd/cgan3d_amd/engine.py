@@ -37,25 +37,49 @@ from . import ops
 
 Dims = Tuple[int, int, int]
 
-# generator BatchNorm backward: statistics fused into the kernel that produces dL/dy (default: same
-# step time at 64^3 B=4 under launch plans, 13 fewer launches), or CGAN3D_BN_FUSED_BWD=0 for a
-# separate reduction pass over (dy, z)
-BN_FUSED_BWD = os.environ.get("CGAN3D_BN_FUSED_BWD", "1") == "1"
-# weight grads of consecutive ResNet-block layers per cross-stream wait (GeneratorPlan.backward)
-WGRAD_GROUP = max(1, int(os.environ.get("CGAN3D_WGRAD_GROUP", "2")))
+# Environment switches (the whole list):
+#   CGAN3D_DEBUG=flag[,flag]   comparator paths the tests run against the default (read at plan
+#                              construction): no_shadow (fp32 conv inputs, no bf16 shadows), keep_fp32
+#                              (write fp32 tensors only shadow readers consume), no_bn_fuse (BatchNorm
+#                              slabs + finalize launches instead of fp64 accumulators), no_bn_fold
+#                              (reflect-fold pass before the last BatchNorm backward), serial (no side
+#                              streams: a kernel trace then shows unshared durations)
+#   CGAN3D_FORCE_DP=1          the data-parallel path over a one-rank group (tools / tests)
+#   CGAN3D_COMM=native|torch|own   data-parallel collectives: RCCL from the launch plan on the process
+#                              group's communicator (default), torch.distributed host callables (the
+#                              fallback), or a communicator of the library's own (ops.NativeComm)
+#   CGAN3D_G_BUCKET_BYTES      generator gradient bucket size under data parallelism
+#   CGAN3D_TUNE, CGAN3D_LIB_PATH   launch-shape knobs, another build of the library (_lib.py)
+DEBUG_FLAGS = ("no_shadow", "keep_fp32", "no_bn_fuse", "no_bn_fold", "serial")
+
+
+def debug(flag: str) -> bool:
+    """True if comparator ``flag`` is set in CGAN3D_DEBUG (read when a plan is built)."""
+    assert flag in DEBUG_FLAGS, flag
+    flags = set(filter(None, os.environ.get("CGAN3D_DEBUG", "").replace(" ", "").split(",")))
+    unknown = flags - set(DEBUG_FLAGS)
+    if unknown:
+        raise ValueError(f"CGAN3D_DEBUG: unknown flags {sorted(unknown)} (known: {', '.join(DEBUG_FLAGS)})")
+    return flag in flags
+
+
+# generator BatchNorm backward: statistics fused into the kernel that produces dL/dy
+BN_FUSED_BWD = True
+# weight grads of consecutive ResNet-block layers per cross-stream wait (GeneratorPlan.backward;
+# groups of 1 or 4 measured 1.92 / 1.96 against 1.88 ms/step at 2)
+WGRAD_GROUP = 2
 # the generator's first WGRAD_TAIL_MAIN layers (the end of its backward) compute their weight grads
 # on the main stream: nothing is left there to overlap them with, and on the side stream they cost
-# two cross-stream hand-offs and share the chip with the stride-2 input-grad
-WGRAD_TAIL_MAIN = max(0, int(os.environ.get("CGAN3D_WGRAD_TAIL_MAIN", "2")))
+# two cross-stream hand-offs and share the chip with the stride-2 input-grad (DESIGN.md §5; 1 and 3
+# measured 1.895 / 1.931 against 1.880 ms/step at 2)
+WGRAD_TAIL_MAIN = 2
 # data parallelism: generator gradient bucket size (all-reduce started per bucket during the backward)
 # (measured on one GPU over a one-rank RCCL group: each extra bucket ~15 us of step time, so the
 # default makes ~2-3 buckets of the 4.1 MB arena: 2.21 ms/step at 1 MB, 2.16 with 2 buckets)
 G_BUCKET_BYTES = int(os.environ.get("CGAN3D_G_BUCKET_BYTES", str(2 << 20)))
-# BatchNorm fused across the ResNet chain's conv boundaries (include/cgan3d.h cgan3d_bn_fuse; bf16):
-# the producing conv adds its statistics into fp64 accumulators (FUSE_REPS replicas), the consuming
-# ResNet-block conv applies the BatchNorm (+ act, + skip) / its backward while staging its input — no
-# finalize and no elementwise launch for those layers (CGAN3D_NO_BN_FUSE=1 at plan construction: the
-# slab path, for A/B)
+# BatchNorm statistics through fp64 accumulators (include/cgan3d.h cgan3d_bn_fuse; bf16): the
+# producing conv adds its statistics into FUSE_REPS replicas, the layer's one elementwise launch
+# finalizes and applies them
 FUSE_REPS = 16
 
 
@@ -234,7 +258,7 @@ class GeneratorPlan:
         # bf16: the last BatchNorm layer's backward statistics come from the last conv's input-grad
         # launch itself (folded over the reflect pad) and its elementwise pass folds the padded grid
         # on the fly — no reflect-fold pass and no fp32 dL/dy of that layer (cgan3d_epilogue.bn_fold)
-        self.fold_bn = (BN_FUSED_BWD and not os.environ.get("CGAN3D_NO_BN_FOLD")
+        self.fold_bn = (BN_FUSED_BWD and not debug("no_bn_fold")
                         and ops.bn_fold_ok(self.geo_last_dgrad))
         if self.fold_bn:
             self.slots_b[-1] = ops.bn_slots(self.geo_last_dgrad)
@@ -257,7 +281,7 @@ class GeneratorPlan:
         def bf(dd, c):
             return torch.empty((n, *dd, c), device=device, dtype=torch.bfloat16)
 
-        if prec == L.PREC_BF16 and not os.environ.get("CGAN3D_NO_SHADOW"):
+        if prec == L.PREC_BF16 and not debug("no_shadow"):
             for i, ly in enumerate(layers):
                 if (ly.kind, ly.k, ly.s, ly.cin, ly.cout) not in shadow_kinds or ly.reflect:
                     continue
@@ -274,7 +298,7 @@ class GeneratorPlan:
         # at 64^3 the 16-channel outputs / input-grads of the first and last BatchNorm layers, 67 MB
         # each; the tensors stay allocated (same plan addresses), their contents undefined
         self.y_dead, self.dz_dead = [False] * len(layers), [False] * len(layers)
-        if not os.environ.get("CGAN3D_KEEP_FP32"):
+        if not debug("keep_fp32"):
             for i, ly in enumerate(layers):
                 if self.y16[i] is not None:
                     if i == len(layers) - 1:
@@ -289,12 +313,12 @@ class GeneratorPlan:
         # BatchNorm statistics through fp64 accumulators (cgan3d_bn_fuse acc_mode 3 / 4) wherever the
         # producing conv can write them (halo-tiled, stride-2 and 1 -> 16 k7 kernels; bf16): the
         # finalize is folded into the elementwise pass, one launch per layer and direction (ac_f[j]:
-        # cgan3d_bn_apply_acc; ac_b[j]: cgan3d_bn_backward_acc / _acc_fold); CGAN3D_NO_BN_FUSE=1 keeps
+        # cgan3d_bn_apply_acc; ac_b[j]: cgan3d_bn_backward_acc / _acc_fold); CGAN3D_DEBUG=no_bn_fuse keeps
         # the slab + finalize path (A/B).  Each elementwise launch zeroes the accumulator its
         # predecessor in the same direction read, the first the last one's, so none needs a memset.
         nl = len(layers)
         self.ac_f, self.ac_b = [False] * nl, [False] * nl
-        if not os.environ.get("CGAN3D_NO_BN_FUSE") and prec == L.PREC_BF16 and not pl and BN_FUSED_BWD:
+        if not debug("no_bn_fuse") and prec == L.PREC_BF16 and not pl and BN_FUSED_BWD:
             self.ac_f = [ops.bn_fuse_ok(self.geo_fwd[j]) for j in range(nl)]
             self.ac_b = [j + 1 < nl and ops.bn_fuse_ok(self.geo_dgrad[j + 1]) for j in range(nl)]
             self.ac_b[-1] = bool(self.fold_bn and ops.bn_fuse_ok(self.geo_last_dgrad))
@@ -315,12 +339,12 @@ class GeneratorPlan:
         # needs its layer's dz and input, both final when it is enqueued); own workspace
         wsw = max([ops.wgrad_ws_floats(gw) for gw in self.geo_wgrad] + [ops.wgrad_ws_floats(self.geo_last_wgrad)])
         self.ws_side = torch.empty(wsw, device=device)
-        # all-zero workspace of the weight grads that sum into theirs by atomics (CGAN3D_WGRAD_WS_CLEAN:
+        # all-zero workspace of the weight grads that sum into theirs by atomics (ops.wgrad ws_clean:
         # each leaves it zeroed, so no memset per layer); they all run on the side stream, in turn
         self.ws_clean = torch.zeros(wsw, device=device)
         self._csum = {}  # bias-sum launch sets (ops.ChannelSumSet) per gradient dict
-        # (CGAN3D_NO_SIDE_STREAM=1 serialises them, so a kernel trace shows unshared durations)
-        on_gpu = torch.device(device).type == "cuda" and not os.environ.get("CGAN3D_NO_SIDE_STREAM")
+        # (CGAN3D_DEBUG=serial serialises them, so a kernel trace shows unshared durations)
+        on_gpu = torch.device(device).type == "cuda" and not debug("serial")
         self.side = torch.cuda.Stream(device=device) if on_gpu else None
         self.pack()
 
@@ -525,9 +549,13 @@ class GeneratorPlan:
                 break
             self._input_grad(P, G, i)
             if i == WGRAD_TAIL_MAIN and side_after is not None and self.side is not None:
-                # every gradient of layers >= i is enqueued (side: weight grads; main: BatchNorm
+                # every gradient of layers >= i must be enqueued (side: weight grads; main: BatchNorm
                 # grads) and their weights' last reader, this input-grad, too: the caller's launches
-                # for those layers (their update) on the side stream, beside the main stream's tail
+                # for those layers (their update) on the side stream, beside the main stream's tail.
+                # A ResNet-chain boundary layer may still hold its weight grad back for grouping:
+                # hand it over first, or the update would read a partial gradient.
+                if pending:
+                    flush()
                 self._on_side(side_after)
         if self.side is not None:  # the weight gradients are complete before anything reads them
             ops.stream_wait(torch.cuda.current_stream(self.device), self.side)
@@ -620,22 +648,18 @@ class CriticPlan:
         self.ws_clean = torch.zeros(ws, device=device)  # see GeneratorPlan.ws_clean
         # per-layer all-zero workspaces of the weight grads whose unpack is deferred: every layer's
         # result waits in its own workspace and one launch moves them all into dW (_flush_unpack)
-        self.defer = not os.environ.get("CGAN3D_NO_DEFER_UNPACK")
+        self.defer = True
         self.ws_layer, self._deferred, self._unpack = {}, [], {}
-        # CGAN3D_CRITIC_SIDE=1: GP-configuration weight / bias gradients on a side stream beside the
-        # penalty's forward-mode chain (own workspace).  Off by default: measured 2.7 % slower per
-        # step at 64^3 B=4 (the chain's kernels are short and lose CUs to the gradient launches)
-        on_gpu = (torch.device(device).type == "cuda" and os.environ.get("CGAN3D_CRITIC_SIDE", "0") == "1"
-                  and not os.environ.get("CGAN3D_NO_SIDE_STREAM"))
-        self.side = torch.cuda.Stream(device=device) if on_gpu else None
-        self.ws_side = torch.empty(ws, device=device) if on_gpu else self.ws
-        # without CGAN3D_CRITIC_SIDE: only the penalty update's bias sums and first-layer weight grad
-        # (c1_wgrad, ~36 us at 64^3 B=4, needs nothing the forward-mode chain produces) go to a side
-        # stream — one hand-off each way, beside the small-grid forward-mode chain
-        # (CGAN3D_CRITIC_W0_SIDE=0: all on the main stream, for A/B runs)
+        # All GP-configuration weight / bias gradients on a side stream beside the penalty's
+        # forward-mode chain measured 2.7 % slower per step at 64^3 B=4 (the chain's kernels are
+        # short and lose CUs to the gradient launches): no such stream (``side`` stays None)
+        self.side = None
+        self.ws_side = self.ws
+        # only the penalty update's bias sums and first-layer weight grad (c1_wgrad, ~36 us at 64^3
+        # B=4, needs nothing the forward-mode chain produces) go to a side stream — one hand-off each
+        # way, beside the small-grid forward-mode chain
         self.side0 = None
-        if (self.side is None and torch.device(device).type == "cuda" and not os.environ.get("CGAN3D_NO_SIDE_STREAM")
-                and os.environ.get("CGAN3D_CRITIC_W0_SIDE", "1") == "1"):
+        if torch.device(device).type == "cuda" and not debug("serial"):
             self.side0 = torch.cuda.Stream(device=device)
         if self.bn:  # conv outputs, pre-activation grads, statistics and per-pass scale/shift
             self.z = [torch.empty_like(self.a[i]) if b else None for i, b in enumerate(self.is_bn)]
@@ -821,7 +845,7 @@ class CriticPlan:
     def _groupable(self, j: int, n_all: int, zeroed: bool) -> bool:
         """Layer j's weight grad can join one grouped launch (ops.wgrad_group): the deferred-unpack
         path into its own clean workspace, a geometry the generic bf16 kernel takes."""
-        if not (zeroed and self.defer) or os.environ.get("CGAN3D_NO_WGRAD_GROUP"):
+        if not (zeroed and self.defer):
             return False
         g = self._wgrad_geo(j, n_all)
         return ops.wgrad_ws_atomic(g) and ops.wgrad_group_ok(g)
@@ -892,8 +916,8 @@ class CriticPlan:
                 group.append(i + 1)
             else:
                 self._on_side(lambda i=i: wgrad(i + 1, self.a[i][:n_all]))  # a_i now holds nu_i in its interp rows
-        if group:
-            self._wgrad_group(G, group, n_all)
+        for k in range(0, len(group), 4):  # a grouped launch takes at most 4 (discriminator_depth >= 5)
+            self._wgrad_group(G, group[k:k + 4], n_all)
         self._on_side(self._flush_unpack)
 
     def _bias_sums(self, G, n_bias: int, side: bool = False) -> "ops.ChannelSumSet":
@@ -1064,15 +1088,15 @@ class StepEngine:
         # they run on the generator's side stream beside the critic update (with the zeroing of the
         # generator's gradient arena); the critic's first-layer input-grad of the generator update
         # then folds its adversarial gradient through the output tanh into G.dz_last in place
-        # (CGAN3D_ACT_NEG_DTANH).  CGAN3D_NO_GLOSS_SIDE=1: everything after that input-grad (A/B).
+        # (L.ACT_NEG_DTANH; measured 1.646 against 1.664 ms/step with everything after that input-grad).
         g0 = self.D.layers[0]
-        self.gloss_side = (self.G.side is not None and not os.environ.get("CGAN3D_NO_GLOSS_SIDE") and
+        self.gloss_side = (self.G.side is not None and
                            ops.neg_dtanh_ok(self.D._geo(ops.conv_dgrad_geom(b_sub, g0.din, g0.dout, g0.cin, g0.cout, g0.k,
                                                                              g0.s, g0.p, planar=self.D.pl),
                                                         self.D.wd[0])))
         self.loss_ws_g = torch.empty(ops.loss_ws_floats(), device=device) if self.gloss_side else self.loss_ws
         # the gradient penalty's per-sample sums of squares straight from the critic's first-layer
-        # input-grad (one float per block; CGAN3D_NO_GP_PART=1: a separate reduction pass, A/B)
+        # input-grad (one float per block; a separate reduction pass measured 1.630 against 1.622 ms/step)
         nsq = ops.sumsq_blocks(self.D._geo(ops.conv_dgrad_geom(self.b_gp, g0.din, g0.dout, g0.cin, g0.cout, g0.k, g0.s,
                                                                g0.p, planar=self.D.pl), self.D.wd[0]))
         # The generator's Adam in two parts: every layer whose gradients are complete when the
@@ -1081,7 +1105,7 @@ class StepEngine:
         # tail layers' parameters (a prefix of the arena) after it, with the step tick.  Single
         # GPU only (data parallelism all-reduces the whole gradient first).
         self.g_split = 0
-        if self.G.side is not None and not self.dp and not os.environ.get("CGAN3D_NO_G_SPLIT_ADAM"):
+        if self.G.side is not None and not self.dp:
             pre = tuple(self.G.layers[li].name + "." for li in range(min(WGRAD_TAIL_MAIN, len(self.G.layers))))
             ar, off, lo, ok = self.g_arena, 0, None, True
             for nm, pp in zip(ar.names, ar.params):
@@ -1093,26 +1117,31 @@ class StepEngine:
                 off += pp.numel()
             if ok and lo and lo < ar.numel:
                 self.g_split = lo
-        self.gp_part = (torch.empty(nsq, device=device) if nsq and self.b_gp and self.use_gp and not self.D.ln and
-                        not os.environ.get("CGAN3D_NO_GP_PART") else None)
+        self.gp_part = (torch.empty(nsq, device=device) if nsq and self.b_gp and self.use_gp and not self.D.ln
+                        else None)
         # dL/dlogits of both critic passes are constants (Trainer.py:117-131, 150-152): written once here
         # into their rows of D.dz[-1]; the losses come from the GP pass (critic) and from a launch
         # beside the generator's backward (generator), so no logits launch sits on the step's path
-        self.fold_logits = (self.gp_part is not None and self.gloss_side and
-                            not os.environ.get("CGAN3D_NO_FOLD_LOGITS"))
+        self.fold_logits = self.gp_part is not None and self.gloss_side
         self.g_off = nmax if self.fold_logits else 0  # critic rows of the generator update
         if self.fold_logits:
             self._write_dlogits()
         self._pending = []  # in-flight bucket all-reduces of the generator gradients
+        self.comm_log = None  # a list: the collective sequence is logged there (_log_comm)
         self.g_buckets = self._make_g_buckets(G_BUCKET_BYTES) if (self.dp and G_BUCKET_BYTES > 0) else []
         on_gpu = torch.device(device).type == "cuda"
         self.comm = torch.cuda.Stream(device=device) if (self.dp and on_gpu) else None
+        if self.comm is not None and int(os.environ.get("GPU_MAX_HW_QUEUES", "4")) < 8:
+            import warnings
+            warnings.warn("StepEngine: data parallelism with fewer than 8 hardware queues (GPU_MAX_HW_QUEUES): the "
+                          "communication stream shares an in-order queue (measured +16 % step time at 4); call "
+                          "cgan3d_amd.configure_hw_queues() before the first GPU use", RuntimeWarning, stacklevel=2)
         # RCCL from C++ (ops.NativeComm): with the nccl backend the all-reduces are C-ABI launches,
         # recorded into the step's launch plan like kernels — one plan per step, no host callables
-        # (CGAN3D_TORCH_COMM=1: torch.distributed's collectives as host callables, for A/B runs)
+        # (CGAN3D_COMM=torch: torch.distributed's collectives as host callables, the fallback)
         self.native = None
         if (self.dp and on_gpu and torch.distributed.get_backend(process_group) == "nccl"
-                and os.environ.get("CGAN3D_TORCH_COMM") != "1"):
+                and ops.COMM_MODE != "torch"):
             self.native = ops.NativeComm(process_group, device)
         if self.world > 1:
             self.broadcast_state()
@@ -1144,6 +1173,26 @@ class StepEngine:
         assert hi == 0 and acc == 0
         return buckets
 
+    def _cur_stream(self):
+        """The current torch stream (None on a CPU dry run)."""
+        return torch.cuda.current_stream(self.device) if torch.device(self.device).type == "cuda" else None
+
+    def _arena_span(self, grad: torch.Tensor):
+        """(network, first, last + 1) of ``grad``'s elements inside its gradient arena."""
+        for net, ar in (("G", self.g_arena), ("D", self.d_arena)):
+            lo = (grad.data_ptr() - ar.grad.data_ptr()) // 4
+            if 0 <= lo and lo + grad.numel() <= ar.numel:
+                return net, lo, lo + grad.numel()
+        return "?", 0, grad.numel()
+
+    def _log_comm(self, *event):
+        """Collective-sequence log (tests/test_dist.py): ("allreduce", stream, net, lo, hi) and
+        ("wait", waiter, signaler) in issue order, when ``comm_log`` is a list.  Every rank must issue
+        the same collectives in the same order on the shared communicator, and each collective must
+        be ordered after the previous one by a stream dependency."""
+        if self.comm_log is not None:
+            self.comm_log.append(event)
+
     def _bucket_ready(self, stage: int):
         """GeneratorPlan.backward callback: start the all-reduce of a bucket whose gradients are all
         enqueued (a host callable inside a recorded plan: ops.plan_host)."""
@@ -1161,13 +1210,17 @@ class StepEngine:
         (CPU tensors): synchronous."""
         dist = torch.distributed
         if self.native is not None:
-            cur = torch.cuda.current_stream(self.device)
-            ops.stream_wait(self.comm, cur)
-            ops.stream_wait(self.comm, self.G.side)
-            with torch.cuda.stream(self.comm):
+            ops.stream_wait(self.comm, self._cur_stream())
+            self._log_comm("wait", "comm", "main")
+            if self.G.side is not None:
+                ops.stream_wait(self.comm, self.G.side)
+                self._log_comm("wait", "comm", "side")
+            with torch.cuda.stream(self.comm):  # (None on a CPU dry run: no-op context)
+                self._log_comm("allreduce", "comm", *self._arena_span(grad))
                 self.native.allreduce_mean(grad)
             self._pending.append(None)
             return
+        self._log_comm("allreduce", "sync", *self._arena_span(grad))
         if dist.get_backend(self.pg) != "nccl":
             if self.G.side is not None:  # gloo over GPU tensors orders only after the current stream
                 torch.cuda.current_stream(self.device).wait_stream(self.G.side)
@@ -1183,7 +1236,8 @@ class StepEngine:
 
     def _finish_allreduce(self):
         if self.native is not None:  # the main stream waits for the communication stream
-            ops.stream_wait(torch.cuda.current_stream(self.device), self.comm)
+            ops.stream_wait(self._cur_stream(), self.comm)
+            self._log_comm("wait", "main", "comm")
             self._pending.clear()
             return
 
@@ -1241,8 +1295,7 @@ class StepEngine:
         slots = (self.xc[:self.b_opt], self.subopt, self.mask, self.eps)
         if (all(t.is_cuda and t.is_contiguous() and t.data_ptr() % 16 == 0 and t.numel() == s.numel()
                 for t, s in zip(ins, slots)) and opt.dtype == subopt.dtype == eps.dtype == torch.float32
-                and mask.dtype in (torch.bool, torch.uint8) and not ops.DRY_RUN and not ops.recording()
-                and not os.environ.get("CGAN3D_TORCH_LOAD")):
+                and mask.dtype in (torch.bool, torch.uint8) and not ops.DRY_RUN and not ops.recording()):
             ops.copy_multi(list(zip(ins, slots)))  # a bool mask's bytes are its 0 / 1 uint8 values
             return
         self.xc[:self.b_opt].view(-1).copy_(opt.reshape(-1), non_blocking=True)
@@ -1388,8 +1441,10 @@ class StepEngine:
         if not self.dp:
             return
         if self.native is not None:  # on the main stream: the generator update needs the new critic
+            self._log_comm("allreduce", "main", *self._arena_span(flat_grad))
             self.native.allreduce_mean(flat_grad)
             return
+        self._log_comm("allreduce", "sync", *self._arena_span(flat_grad))
         dist = torch.distributed
 
         def reduce():

@@ -119,7 +119,10 @@ class CCTAContrastCorrector:
         self.checkpoint_path = Path(checkpoint_path)
 
     def _scale(self, x: np.ndarray) -> np.ndarray:
-        return np.asarray(self.scaler(x), dtype=np.float32) if self.scaler is not None else x.astype(np.float32)
+        # float32 first, as CCTAEvalDataset2D/3D do (ccta.astype(np.float32)): an int16 scan would
+        # otherwise wrap in the scaler's shift (x - 238 below -32530) and round differently
+        x = np.asarray(x, dtype=np.float32)
+        return np.asarray(self.scaler(x), dtype=np.float32) if self.scaler is not None else x
 
     @torch.no_grad()
     def correct_scan_3D(self, ccta: np.ndarray, batch_size: int, desc: Optional[str] = None) -> Tensor:

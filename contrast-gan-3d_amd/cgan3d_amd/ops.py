@@ -53,18 +53,23 @@ def uses_gemm(g: ConvGeom) -> bool:
     return not (g.k == 7 and g.stride == 1 and g.cin == 1 and g.cout in (8, 16))
 
 
-# bf16 launches whose geometry the halo-tiled kernel takes use it (conv_halo.hip); the env switch
-# CGAN3D_NO_HALO=1 keeps them on the implicit-GEMM kernel (A/B measurements).
-HALO = os.environ.get("CGAN3D_NO_HALO", "0") != "1"
+# bf16 launches whose geometry the halo-tiled kernel takes use it (conv_halo.hip)
+HALO = True
 
 
 def halo_eligible(g: ConvGeom) -> bool:
     return bool(L.load().cgan3d_halo_eligible(ctypes.byref(g)))
 
 
-# conv_sk.hip takes the critic's k4 convs in bf16 (format 3); CGAN3D_NO_SK=1 keeps them on the
-# halo / implicit-GEMM kernels (A/B measurements)
-SK = os.environ.get("CGAN3D_NO_SK", "0") != "1"
+# conv_sk.hip takes the critic's k4 convs in bf16 (format 3)
+SK = True
+
+# data-parallel collectives (engine.StepEngine): "native" (default) RCCL from the launch plan on the
+# process group's communicator, "torch" torch.distributed host callables (the fallback), "own" a
+# communicator of this library's (NativeComm own=True)
+COMM_MODE = os.environ.get("CGAN3D_COMM", "native")
+if COMM_MODE not in ("native", "torch", "own"):
+    raise ValueError(f"CGAN3D_COMM={COMM_MODE!r}: native, torch or own")
 
 
 def with_packing(g: ConvGeom, prec: int = L.PREC_F32) -> ConvGeom:
@@ -208,7 +213,7 @@ class BnFuse:
 
 
 def neg_dtanh_ok(g) -> bool:
-    """cgan3d_conv3d_neg_dtanh_ok: the input-grad geometry takes the CGAN3D_ACT_NEG_DTANH epilogue."""
+    """cgan3d_conv3d_neg_dtanh_ok: the input-grad geometry takes the L.ACT_NEG_DTANH epilogue."""
     return bool(L.load().cgan3d_conv3d_neg_dtanh_ok(ctypes.byref(g)))
 
 
@@ -305,7 +310,7 @@ class NativeComm:
 
     Default: the process group's own communicator (ProcessGroupNCCL._comm_ptr), driven through the
     RCCL library torch loaded — one communicator per process.  ``own=True`` (or
-    CGAN3D_OWN_COMM=1): a communicator of this library, rank 0's unique id broadcast through
+    CGAN3D_COMM=own): a communicator of this library, rank 0's unique id broadcast through
     ``group`` once (measured: a second communicator in the process slows every kernel of a one-GPU
     step ~2.4x, profiles/r03_dp1_probe.json)."""
 
@@ -315,7 +320,7 @@ class NativeComm:
         self.world, self.rank = dist.get_world_size(group), dist.get_rank(group)
         self.owned = False
         if own is None:
-            own = os.environ.get("CGAN3D_OWN_COMM") == "1"
+            own = COMM_MODE == "own"
         if not own:
             ptr = self._torch_comm(group, device)
             if ptr and int(lib.cgan3d_comm_shared_library()) == 1:

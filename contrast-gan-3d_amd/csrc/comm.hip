@@ -5,8 +5,12 @@
 //
 // RCCL is the process's own: PyTorch-ROCm already loaded its librccl for torch.distributed, so the
 // entry points are resolved from the loaded library (dlopen RTLD_NOLOAD) and only fall back to
-// loading ROCm's librccl.so.1 — one RCCL per process.  The communicator is this library's
-// (ncclCommInitRank from a unique id the caller broadcasts), independent of torch's process group.
+// loading ROCm's librccl.so.1 — one RCCL per process.  The communicator a caller passes is, by
+// default, the torch process group's own (ops.NativeComm: ProcessGroupNCCL's ncclComm_t, one
+// communicator per process; a second one slowed every kernel of a one-GPU step ~2.4x); with
+// cgan3d_comm_init the library builds its own from a unique id the caller broadcasts
+// (CGAN3D_OWN_COMM=1).  On a shared communicator every rank must issue the same collectives in the
+// same order, each ordered after the previous one by stream dependencies.
 #include <dlfcn.h>
 
 #include <cstring>

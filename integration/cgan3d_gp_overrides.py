@@ -20,6 +20,12 @@ _PKG = Path(__file__).resolve().parents[1] / "contrast-gan-3d_amd"
 if str(_PKG) not in sys.path:
     sys.path.insert(0, str(_PKG))
 
+import cgan3d_amd  # noqa: E402
+
+# the step's streams each get a hardware queue (cgan3d_amd/__init__.py); train.py imports this module
+# before it touches the GPU (train.py:97-107 run before the Trainer is built)
+cgan3d_amd.configure_hw_queues()
+
 from cgan3d_amd.model.discriminator import PatchGANDiscriminator  # noqa: E402
 from cgan3d_amd.model.generator import ResnetGenerator  # noqa: E402
 from cgan3d_amd.model.loss import HULoss  # noqa: E402,F401  (train.py:166 instantiates it)

@@ -15,6 +15,12 @@ sys.path.insert(0, str(REPO))
 sys.path.insert(0, str(REPO / "contrast-gan-3d_amd"))
 GOLDEN = REPO / "tests" / "golden"
 
+import cgan3d_amd  # noqa: E402
+
+# the GPU tests run the two-stream step and data-parallel paths: the entry point's hardware-queue
+# setting (cgan3d_amd/__init__.py), before anything initialises HIP
+cgan3d_amd.configure_hw_queues()
+
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (runs the HIP kernels)")

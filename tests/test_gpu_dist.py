@@ -27,9 +27,11 @@ def test_two_rank_plan_step():
 def test_rccl_bucketed_path_one_rank(torch_comm):
     """The RCCL path itself (bucketed async all-reduces on a communication stream, inside a launch
     plan) on a one-rank nccl group: tools/dist_nccl1_check.py (the mean over one rank is exact) —
-    through the library's own RCCL communicator recorded in the plan (default), and through
-    torch.distributed host callables (CGAN3D_TORCH_COMM=1)."""
-    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT="2953" + torch_comm, CGAN3D_TORCH_COMM=torch_comm)
+    through RCCL calls recorded in the plan on the process group's own communicator (default:
+    ops.NativeComm over ProcessGroupNCCL's ncclComm_t), and through torch.distributed host callables
+    (CGAN3D_COMM=torch, the documented fallback)."""
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT="2953" + torch_comm,
+               CGAN3D_COMM="torch" if torch_comm == "1" else "native")
     r = subprocess.run([sys.executable, str(REPO / "tools" / "dist_nccl1_check.py")], cwd=REPO, env=env,
                        capture_output=True, text=True, timeout=110)
     out = r.stdout + r.stderr

@@ -353,7 +353,7 @@ SHADOW_EXACT = tuple(
 def test_bf16_shadows_match_fp32_staging(monkeypatch):
     """The bf16 input shadows (BatchNorm passes writing bf16 copies that the halo / weight-grad
     kernels stage from) change no arithmetic: a 64^3 bf16 step with them matches the step without
-    (CGAN3D_NO_SHADOW=1) up to the atomics order of the generic weight-grad kernels.  The last conv
+    (CGAN3D_DEBUG=no_shadow) up to the atomics order of the generic weight-grad kernels.  The last conv
     with a shadow takes the streamed-plane kernel (k7s_w2n_kernel: another fp32 summation order, its
     own test in test_gpu_ops.py::test_k7_bf16_mfma), so it is switched off here (tuning key 13) to
     compare like with like."""
@@ -361,7 +361,7 @@ def test_bf16_shadows_match_fp32_staging(monkeypatch):
     from cgan3d_amd.data.synthetic import synth_patches
     from cgan3d_amd.engine import StepEngine
     L.check(L.load().cgan3d_set_tuning(13, -1), "k7s off")
-    monkeypatch.setenv("CGAN3D_NO_BN_FUSE", "1")  # the fused chain needs the shadows: compared on its own below
+    monkeypatch.setenv("CGAN3D_DEBUG", "no_bn_fuse")  # the fused chain needs the shadows: compared on its own below
     try:
         _shadow_exactness(monkeypatch, synth_patches, StepEngine)
     finally:
@@ -374,7 +374,7 @@ def _shadow_exactness(monkeypatch, synth_patches, StepEngine):
     engs = []
     for off in (False, True):
         if off:
-            monkeypatch.setenv("CGAN3D_NO_SHADOW", "1")
+            monkeypatch.setenv("CGAN3D_DEBUG", "no_bn_fuse,no_shadow")
         g, d = _models(g_args)
         engs.append(StepEngine(g, d, g.config, d.config, b, b, (S, S, S), precision="bf16"))
     with_s, without = engs
@@ -406,7 +406,7 @@ def _shadow_exactness(monkeypatch, synth_patches, StepEngine):
 def test_batchnorm_accumulators_match_slab_path(monkeypatch):
     """BatchNorm statistics through fp64 accumulators filled by the producing conv (include/cgan3d.h
     cgan3d_bn_fuse), finalize folded into one elementwise launch per layer and direction, against
-    the slab + finalize + elementwise path (CGAN3D_NO_BN_FUSE=1), same 64^3 bf16 steps: losses,
+    the slab + finalize + elementwise path (CGAN3D_DEBUG=no_bn_fuse), same 64^3 bf16 steps: losses,
     running buffers, every gradient tensor within the bf16 path's 2e-2 bar (relative to its own
     largest entry) and the median tensor within 1e-3 — the two combine the statistics in another
     order (fp64 sums of squares vs Chan's fp32 merge), which moves a few operands across a bf16
@@ -418,7 +418,7 @@ def test_batchnorm_accumulators_match_slab_path(monkeypatch):
     engs = []
     for off in (False, True):
         if off:
-            monkeypatch.setenv("CGAN3D_NO_BN_FUSE", "1")
+            monkeypatch.setenv("CGAN3D_DEBUG", "no_bn_fuse")
         g, d = _models(g_args)
         engs.append(StepEngine(g, d, g.config, d.config, b, b, (S, S, S), precision="bf16"))
     fused, slab = engs
@@ -454,7 +454,7 @@ def test_batchnorm_accumulators_match_slab_path(monkeypatch):
 def test_folded_last_batchnorm_backward_matches_fold_pass(monkeypatch):
     """The last BatchNorm layer's backward without a reflect-fold pass (statistics from the last
     conv's input-grad launch, cgan3d_epilogue.bn_fold; dy folded on the fly by
-    cgan3d_bn_backward_slab_fold) against the fold pass + slab path (CGAN3D_NO_BN_FOLD=1): the same
+    cgan3d_bn_backward_slab_fold) against the fold pass + slab path (CGAN3D_DEBUG=no_bn_fold): the same
     64^3 bf16 step: every gradient tensor within the bf16 path's 2e-2 bar (relative to its own
     largest entry) and the median tensor within 1e-3.  The two sum the statistics and dy in another
     fp32 order; where that moves an input-grad element across a bf16 rounding boundary the rest of
@@ -468,7 +468,7 @@ def test_folded_last_batchnorm_backward_matches_fold_pass(monkeypatch):
     engs = []
     for off in (False, True):
         if off:
-            monkeypatch.setenv("CGAN3D_NO_BN_FOLD", "1")
+            monkeypatch.setenv("CGAN3D_DEBUG", "no_bn_fold")
         g, d = _models(g_args)
         engs.append(StepEngine(g, d, g.config, d.config, b, b, (S, S, S), precision="bf16"))
     folded, passed = engs

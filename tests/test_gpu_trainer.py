@@ -31,7 +31,7 @@ class _LoggerInterface:
         pass
 
 
-def _trainer(ckpt_dir, precision="f32", clip=False, gen_every=1):
+def _trainer(ckpt_dir, precision="f32", clip=False, gen_every=1, scheduler=None):
     from cgan3d_amd.model.discriminator import PatchGANDiscriminator
     from cgan3d_amd.model.generator import ResnetGenerator
     from cgan3d_amd.model.loss import HULoss
@@ -45,7 +45,8 @@ def _trainer(ckpt_dir, precision="f32", clip=False, gen_every=1):
         partial(torch.optim.Adam, lr=1e-4, betas=(0.0, 0.9)),
         partial(torch.optim.Adam, lr=1e-4, betas=(0.0, 0.9)),
         HULoss(-0.2, 0.6), _LoggerInterface(), torch.device("cuda"),
-        checkpoint_dir=ckpt_dir, checkpoint_every=2, precision=precision, weight_clip=0.01 if clip else None)
+        checkpoint_dir=ckpt_dir, checkpoint_every=2, precision=precision, weight_clip=0.01 if clip else None,
+        generator_lr_scheduler_class=scheduler, critic_lr_scheduler_class=scheduler)
 
 
 def _patches(rng, b=2, S=32):
@@ -200,6 +201,78 @@ def test_trainer_plan_replay_matches_eager(tmp_path, precision, monkeypatch):
                     it, k, float(d.max()), float(off.mean()))
     assert planned.optimizer_D._host_step == eager.optimizer_D._host_step == 7
     assert planned.optimizer_G._host_step == eager.optimizer_G._host_step == 4
+
+
+def _arena_state(opt):
+    a = opt.arena
+    return {k: t.detach().double().cpu().numpy().copy()
+            for k, t in (("p", a.flat), ("m", a.exp_avg), ("v", a.exp_avg_sq))}
+
+
+def _check_adam_update(before, opt, lr, what):
+    """The update the device applied equals torch.optim.Adam's (basic_conf.py:55,67; betas (0, 0.9)
+    of gradient_penalty_conf.py:9-10) at learning rate ``lr`` on the gradient it consumed (the
+    arena's gradient after the update) — float64 restatement of oracle.reference_torch.adam_step.
+    A learning rate off by the MultiStepLR factor 0.1 moves every non-zero update tenfold."""
+    a = opt.arena
+    b1, b2 = opt.param_groups[0]["betas"]
+    eps = opt.param_groups[0]["eps"]
+    step = float(opt.hyper[4].item())
+    g = a.grad.detach().double().cpu().numpy()
+    m = before["m"] + (1 - b1) * (g - before["m"])
+    v = before["v"] * b2 + (1 - b2) * g * g
+    delta = lr / (1 - b1 ** step) * m / (np.sqrt(v) / np.sqrt(1 - b2 ** step) + eps)
+    got = a.flat.detach().double().cpu().numpy()
+    want = before["p"] - delta
+    moved = np.abs(delta) > 0.5 * lr  # elements whose step is Adam's full normalised size
+    assert moved.mean() > 0.05, (what, float(moved.mean()))  # the check is not vacuous
+    ulp = np.abs(want) * 2.0 ** -23
+    err = np.abs(got - want)
+    assert (err <= 0.02 * lr + 2 * ulp).all(), (what, lr, float(err.max()), float(np.abs(delta).max()))
+    assert np.allclose(a.exp_avg.double().cpu().numpy(), m, rtol=1e-5, atol=1e-12), what
+
+
+@pytest.mark.parametrize("mode", ["replay", "resume", "stale"])
+def test_multistep_lr_reaches_replayed_plan(tmp_path, mode, monkeypatch):
+    """MultiStepLR (basic_conf.py:35-36,56-58,68: stepped after every update, Trainer.py:139-140,
+    158-159) through the drop-in Trainer's replayed launch plans: milestones [2, 4], gamma 0.1, both
+    networks, the generator every iteration.  After every iteration each network's parameters are
+    the Adam update of the gradient the device consumed at the scheduled learning rate 1e-4, 1e-5,
+    1e-6 (iterations 0-1, 2-3, 4-5) — iterations 2-5 run from a recorded plan, so the learning rate
+    must reach the plan through the optimiser's device scalar.  ``resume``: a checkpoint is saved
+    after iteration 2 (past the first milestone) and a new Trainer resumes from it, recording its own
+    plans.  ``stale``: the device learning rate is never refreshed; the check must catch it."""
+    from torch.optim.lr_scheduler import MultiStepLR
+    from cgan3d_amd.trainer.optim import FusedAdam
+    if mode == "stale":
+        monkeypatch.setattr(FusedAdam, "sync_hyper", lambda self: None)
+    sched = partial(MultiStepLR, milestones=[2, 4], gamma=0.1)
+    tr = _trainer(tmp_path, "f32", gen_every=1, scheduler=sched)
+    tr.checkpoint_every = None
+    batches = [_patches(np.random.default_rng(40 + it)) for it in range(6)]
+    failures = []
+    for it in range(6):
+        if mode == "resume" and it == 3:
+            tr.save_checkpoint(3)
+            tr = _trainer(tmp_path, "f32", gen_every=1, scheduler=sched)
+            assert tr.iteration == 3 and tr.optimizer_G._host_step == 3
+            assert tr.lr_scheduler_G.last_epoch == 3 and abs(tr.optimizer_G.param_groups[0]["lr"] - 1e-5) < 1e-12
+        before = {net: _arena_state(o) for net, o in (("D", tr.optimizer_D), ("G", tr.optimizer_G))}
+        torch.cuda.manual_seed(200 + it)
+        tr.train_step(batches[it], it)
+        torch.cuda.synchronize()
+        lr = 1e-4 * 0.1 ** sum(it >= m for m in (2, 4))
+        for net, o in (("D", tr.optimizer_D), ("G", tr.optimizer_G)):
+            try:
+                _check_adam_update(before[net], o, lr, (mode, it, net))
+            except AssertionError as e:
+                failures.append(e)
+    replayed = [p for p in tr._plans.values() if p is not None]
+    assert len(replayed) == 1  # every iteration from the second on ran the recorded plan
+    if mode == "stale":
+        assert failures, "a device learning rate that never follows the scheduler went unnoticed"
+    else:
+        assert not failures, failures[0]
 
 
 @pytest.mark.timeout(240)

@@ -2,7 +2,7 @@
 runs the bucketed generator all-reduces (communication stream ordered after the main and side
 streams, one RCCL all-reduce per bucket, wait before Adam) and the critic all-reduce — by default
 as C-ABI launches on the process group's communicator (ops.NativeComm, cgan3d_allreduce_mean:
-recorded into the launch plan, which stays one C segment), with CGAN3D_TORCH_COMM=1 through torch.distributed as
+recorded into the launch plan, which stays one C segment), with CGAN3D_COMM=torch through torch.distributed as
 host callables between the plan's C segments.  Over one rank the mean is the identity, so three plan-replayed steps must match
 an engine without collectives (up to weight-gradient atomics order).  Each compared step starts
 from the same state (the reference engine's weights, Adam moments and BatchNorm buffers copied in
@@ -17,6 +17,9 @@ from pathlib import Path
 
 REPO = Path(__file__).resolve().parents[1]
 sys.path.insert(0, str(REPO / "contrast-gan-3d_amd"))
+import cgan3d_amd  # noqa: E402
+
+cgan3d_amd.configure_hw_queues()  # before torch touches the GPU
 
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
@@ -66,7 +69,7 @@ def main():
         e.step()  # eager (code objects load lazily)
         plans.append(e.record())
     hosts = sum(1 for it in plans[0].items if not isinstance(it, int))
-    native = os.environ.get("CGAN3D_TORCH_COMM") != "1"
+    native = os.environ.get("CGAN3D_COMM", "native") != "torch"
     assert (dp.native is not None) == native
     assert hosts == (0 if native else len(dp.g_buckets) + 2), hosts
     for _ in range(3):

@@ -18,6 +18,9 @@ from pathlib import Path
 
 REPO = Path(__file__).resolve().parents[1]
 sys.path.insert(0, str(REPO / "contrast-gan-3d_amd"))
+import cgan3d_amd  # noqa: E402
+
+cgan3d_amd.configure_hw_queues()  # before torch touches the GPU
 
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402

@@ -1,5 +1,5 @@
 # Bench under several env settings, back to back on one box (VARIANTS: ';'-separated env lists,
-# "-" = defaults), e.g. VARIANTS="-;CGAN3D_KEEP_FP32=1;-;CGAN3D_KEEP_FP32=1"
+# "-" = defaults), e.g. VARIANTS="-;CGAN3D_DEBUG=keep_fp32;-;CGAN3D_DEBUG=keep_fp32"
 set -o pipefail
 cd $GRAFT_REPO_ROOT; mkdir -p gpurun_out
 IFS=';' read -ra VS <<< "${VARIANTS:--}"

@@ -1,4 +1,4 @@
-# Quick A/B of an environment switch: default vs $AB_ENV (e.g. AB_ENV=CGAN3D_NO_GLOSS_SIDE=1), two
+# Quick A/B of an environment switch: default vs $AB_ENV (e.g. AB_ENV=CGAN3D_DEBUG=no_bn_fold), two
 # rounds each, back to back on one box, plus a plan-mode kernel trace of the default.
 set -o pipefail
 cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out
