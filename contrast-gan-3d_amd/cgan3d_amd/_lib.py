@@ -127,6 +127,7 @@ _SIGS = {
     "cgan3d_patch_accumulate": ([_P, _I32, _I32, _I32, _I32, _P, _P, _P, _I32, _I32, _I32, _P], _I32),
     "cgan3d_patch_normalize": ([_P, _P, _I64, _P], _I32),
     "cgan3d_spatial_augment": ([_P, _P, _I32, _I32, _I32, _I32, _P, _P, _I32, _P, _P, _P, _P, _P], _I32),
+    "cgan3d_mirror": ([_P, _P, _I32, _I32, _I32, _I32, _P, _P, _P, _P], _I32),
     "cgan3d_loss_ws_floats": ([_I64], _I64),
     "cgan3d_critic_logits_grad": ([_P, _I32, _I32, _I32, _I32, _F, _P, _P, _P], _I32),
     "cgan3d_gradient_penalty": ([_P, _I32, _I64, _F, _P, _P, _P, _P], _I32),

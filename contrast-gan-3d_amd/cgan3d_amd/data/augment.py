@@ -82,6 +82,11 @@ class SpatialTransform_2:  # noqa: N801 (batchgenerators' name)
         if independent_scale_for_each_axis:
             raise NotImplementedError("SpatialTransform_2: one scale for all axes is supported")
         self.patch_size = tuple(int(p) for p in patch_size)
+        if len(self.patch_size) not in (2, 3):
+            raise ValueError(f"SpatialTransform_2: 2-D or 3-D patches, got {self.patch_size}")
+        if len(self.patch_size) == 2 and do_elastic_deform:
+            raise NotImplementedError("SpatialTransform_2: 2-D patches without elastic deformation "
+                                      "(experiments/conf_2D.py switches it off)")
         self.do_elastic_deform, self.deformation_scale = do_elastic_deform, tuple(deformation_scale)
         self.do_rotation = do_rotation
         self.angle_x, self.angle_y, self.angle_z = tuple(angle_x), tuple(angle_y), tuple(angle_z)
@@ -102,9 +107,16 @@ class SpatialTransform_2:  # noqa: N801 (batchgenerators' name)
         return cls(**{k: getattr(t, k) for k in names if hasattr(t, k)})
 
     # -- host: per-sample parameters ------------------------------------------------------------
+    @property
+    def kernel_dims(self):
+        """(a0, a1, a2) the kernels run on: the patch, a 2-D patch (W, H) as (1, W, H)."""
+        return self.patch_size if len(self.patch_size) == 3 else (1,) + self.patch_size
+
     def draw(self, rng: np.random.Generator, n: int):
         """Per-sample parameters [n, 16], the elastic samples' noise [n_el, 3, *patch] and Gaussian
         kernel rows [n_el, 3, max(patch)], in augment_spatial_2's order of random draws."""
+        if len(self.patch_size) == 2:
+            return self._draw_2d(rng, n)
         ps = self.patch_size
         kst = max(ps)
         prm = np.zeros((n, N_PARAMS), np.float32)
@@ -150,22 +162,110 @@ class SpatialTransform_2:  # noqa: N801 (batchgenerators' name)
         self.last_decisions = decisions  # per sample {sigmas, mags, noise, angles, scale} (tests)
         return prm, noise, gauss
 
+    def _draw_2d(self, rng: np.random.Generator, n: int):
+        """2-D patches (experiments/conf_2D.py): augment_spatial_2's draws for dim == 2 — the elastic
+        draw (its decision only: conf_2D switches the deformation off), one angle (a_x) turned by
+        rotate_coords_2d (coords' = coords^T . R, R = [[cos, -sin], [sin, cos]]), the scale — as the
+        kernels' (1, W, H) parameters: the first axis passes through."""
+        W, H = self.patch_size
+        prm = np.zeros((n, N_PARAMS), np.float32)
+        decisions = []
+        for s in range(n):
+            m = np.eye(2)
+            modified, dec = False, {}
+            decisions.append(dec)
+            rng.uniform()  # `uniform() < p_el_per_sample and do_elastic_deform`: drawn, never taken
+            if self.do_rotation and rng.uniform() < self.p_rot_per_sample:
+                a = _uniform(rng, *self.angle_x) if rng.uniform() <= self.p_rot_per_axis else 0.0
+                c, sn = np.cos(a), np.sin(a)
+                m = np.array([[c, -sn], [sn, c]]).T @ m
+                dec["angles"] = [a]
+                modified = True
+            if self.do_scale and rng.uniform() < self.p_scale_per_sample:
+                if rng.random() < 0.5 and self.scale[0] < 1:
+                    sc = _uniform(rng, self.scale[0], 1)
+                else:
+                    sc = _uniform(rng, max(self.scale[0], 1), self.scale[1])
+                m = sc * m
+                dec["scale"] = sc
+                modified = True
+            m3 = np.eye(3)
+            m3[1:, 1:] = m
+            prm[s, :9] = m3.reshape(-1)
+            prm[s, 9:12] = [0.0, W / 2.0 - 0.5, H / 2.0 - 0.5]
+            prm[s, 12] = -1 if modified else -2
+            prm[s, 13:16] = 1e-8
+        self.last_decisions = decisions
+        return prm, None, None
+
     # -- device ---------------------------------------------------------------------------------
     def apply(self, data: torch.Tensor, seg: torch.Tensor, prm, noise, gauss, data_out: torch.Tensor,
               seg_out: torch.Tensor, ws: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, torch.Tensor]:
         """Run the drawn transform on a device batch (out of place)."""
         dev = data.device
-        n, dims = data.shape[0], tuple(data.shape[-3:])
+        n, dims = data.shape[0], tuple(data.shape[-len(self.patch_size):])
         if dims != self.patch_size:
             raise ValueError(f"SpatialTransform_2: patch {dims} != patch_size {self.patch_size}")
         n_el = 0 if noise is None else int(noise.shape[0])
         t = lambda a: a if isinstance(a, torch.Tensor) else torch.from_numpy(np.ascontiguousarray(a)).to(dev)  # noqa
         if ws is None:
-            ws = torch.empty(ops.augment_ws_floats(n, dims, n_el), device=dev)
+            ws = torch.empty(ops.augment_ws_floats(n, self.kernel_dims, n_el), device=dev)
         ops.spatial_augment(data, seg, t(prm), t(noise) if n_el else None, t(gauss) if n_el else None, n_el,
-                            data_out, seg_out, ws)
+                            data_out, seg_out, ws, dims=self.kernel_dims)
         return data_out, seg_out
+
+    def run(self, params, data, seg, data_out, seg_out, ws=None):
+        """Loader interface: ``params`` = what ``draw`` returned, on the device."""
+        return self.apply(data, seg, *params, data_out, seg_out, ws=ws)
 
     def __call__(self, rng: np.random.Generator, data: torch.Tensor, seg: torch.Tensor):
         prm, noise, gauss = self.draw(rng, data.shape[0])
         return self.apply(data, seg, prm, noise, gauss, torch.empty_like(data), torch.empty_like(seg))
+
+
+class MirrorTransform:
+    """batchgenerators' MirrorTransform (same constructor), as experiments/conf_2D.py:36-43 uses it
+    after SpatialTransform_2: ``MirrorTransform(axes=(0, 1), p_per_sample=0.5)``.  Restated from the
+    package's published source (0.25; batchgenerators is not installed here): per sample, with
+    probability p_per_sample, ``augment_mirroring`` flips the sample along each spatial axis in
+    ``axes`` with probability 1/2 — one uniform draw per axis in order, axis 2 only for 3-D samples.
+    The host draws the per-sample flags from the loader's generator; ``cgan3d_mirror`` flips on
+    the GPU.  Parity: against a numpy restatement (tests/test_gpu_augment.py) — unpinned by the
+    reference, whose augmenter cannot run here."""
+
+    def __init__(self, axes=(0, 1, 2), data_key="data", label_key="seg", p_per_sample=1):
+        self.axes = tuple(int(a) for a in axes)
+        if self.axes and max(self.axes) > 2:
+            raise ValueError("MirrorTransform takes the spatial axes (0, 1, 2)")
+        self.data_key, self.label_key, self.p_per_sample = data_key, label_key, p_per_sample
+        self.patch_size = None  # set by the loader: the patch it runs on
+
+    @classmethod
+    def from_transform(cls, t) -> "MirrorTransform":
+        return cls(**{k: getattr(t, k) for k in ("axes", "data_key", "label_key", "p_per_sample") if hasattr(t, k)})
+
+    def draw(self, rng: np.random.Generator, n: int, ndim: Optional[int] = None):
+        """Per-sample flags [n] int32: bit d = flip spatial axis d (augment_mirroring's draws)."""
+        ndim = ndim if ndim is not None else len(self.patch_size)
+        flags = np.zeros(n, np.int32)
+        for s in range(n):
+            if rng.uniform() < self.p_per_sample:
+                f = 0
+                if 0 in self.axes and rng.uniform() < 0.5:
+                    f |= 1
+                if 1 in self.axes and rng.uniform() < 0.5:
+                    f |= 2
+                if 2 in self.axes and ndim == 3 and rng.uniform() < 0.5:
+                    f |= 4
+                flags[s] = f
+        return (flags,)
+
+    def run(self, params, data, seg, data_out, seg_out, ws=None):
+        """Loader interface: flip the device batch out of place by the drawn flags (device int32)."""
+        (flags,) = params
+        ps = tuple(self.patch_size)
+        dims = ps if len(ps) == 3 else (1,) + ps
+        if len(ps) == 2:  # spatial axis d of a (W, H) patch is kernel axis d + 1
+            flags = flags * 2
+        ops.mirror(data, seg, flags, data_out, seg_out, dims)
+        return data_out, seg_out

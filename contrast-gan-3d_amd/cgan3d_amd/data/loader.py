@@ -20,12 +20,20 @@ Per batch:
   read on the host and copied over PCIe.  A returned batch's tensors live in a ring slot and are
   overwritten ``depth`` batches later (the Trainer consumes each batch within its step).
 
-* spatial augmentation (optional ``transform``, ``data/augment.py``: batchgenerators'
-  ``SpatialTransform_2`` as ``basic_conf.py:87-113`` configures it): the per-sample parameters
+* augmentation (optional ``transform``, ``data/augment.py``: batchgenerators'
+  ``SpatialTransform_2`` as ``basic_conf.py:87-113`` configures it, and ``MirrorTransform`` after it
+  as ``conf_2D.py:36-43`` does — one transform or a list run in order): the per-sample parameters
   and the elastic noise fields are drawn on the host with the crop boxes, under the loader's lock
   from its one generator (a single random stream, as batchgenerators draws per batch); the host
-  worker pins them for the async copy, and ``cgan3d_spatial_augment`` resamples the unpacked batch
-  on the loader stream.
+  worker pins them for the async copy, and ``cgan3d_spatial_augment`` / ``cgan3d_mirror`` transform
+  the unpacked batch on the loader stream.
+
+2-D patches (``experiments/conf_2D.py``: a patch shape of two entries) follow
+``CCTADataLoader.get_samplable_2D`` (``CCTADataLoader.py:50-70``): with probability 1/2 a patch
+around a random centre-line point of the scan's ``<patient>_meta`` record (world -> image
+coordinates, ``utils/geometry.py:21-26``; bounds ``get_patch_bounds``, ``:114-138``, with its
+(y, x) argument order kept) in that point's slice, not cropped further; otherwise a random slice
+of the scan, padded and randomly cropped like a 3-D patch.  ``data`` is then [B, 1, W, H].
 """
 from __future__ import annotations
 
@@ -55,33 +63,112 @@ def _scaler_params(scaler) -> Tuple[float, float]:
 
 
 def crop_box(shape: Sequence[int], patch: Sequence[int], rng: np.random.Generator):
-    """Per-dim (src_lo, dst_lo, length) of CCTADataLoader.generate_one's pad-then-random-crop."""
+    """Per-dim (src_lo, dst_lo, length) of CCTADataLoader.generate_one's pad-then-random-crop:
+    batchgenerators' ``pad_nd_image`` then ``crop(crop_type="random")``, whose
+    ``get_lbs_for_random_crop`` draws ``randint(0, s - p)`` where s - p > 0 (the last offset is never
+    drawn) and takes (s - p) // 2 otherwise (no draw)."""
     box = []
     for s, p in zip(shape, patch):
         if s < p:  # pad_nd_image: centred zero padding; the padded dim equals the patch (offset 0)
             box.append((0, (p - s) // 2, s))
+        elif s > p:
+            box.append((int(rng.integers(0, s - p)), 0, p))
         else:
-            lo = int(rng.integers(0, s - p + 1))
-            box.append((lo, 0, p))
+            box.append((0, 0, p))
     return box
 
 
 def read_crop(vol: np.ndarray, patch: Sequence[int], box, out: np.ndarray):
-    """out[W,H,D,2] = zero-padded crop of vol[W,H,D,2] described by ``box``."""
+    """out[W,H,D,2] = zero-padded crop of vol[W,H,D,2] described by ``box``; a 2-D ``box`` =
+    (z, ((src_lo, dst_lo, length) in W, in H)): out[W,H,2] from slice z."""
+    if len(patch) == 2:
+        z, ((sx, dx, lx), (sy, dy, ly)) = box
+        if (dx, dy) != (0, 0) or (lx, ly) != tuple(patch):
+            out.fill(0)
+        out[dx:dx + lx, dy:dy + ly] = vol[sx:sx + lx, sy:sy + ly, z]
+        return
     (sx, dx, lx), (sy, dy, ly), (sz, dz, lz) = box
     if (dx, dy, dz) != (0, 0, 0) or (lx, ly, lz) != tuple(patch):
         out.fill(0)
     out[dx:dx + lx, dy:dy + ly, dz:dz + lz] = vol[sx:sx + lx, sy:sy + ly, sz:sz + lz]
 
 
+def load_meta(path: str) -> dict:
+    """A scan's metadata (offset, spacing, centerlines_world, name): ``<path>_meta.npz`` (numeric
+    arrays, no code), else the reference's ``<path>_meta.pkl`` (data/utils.py:48-54 writes and reads
+    it with pickle; the scan preparation of the user's own dataset)."""
+    npz = Path(path + "_meta.npz")
+    if npz.is_file():
+        with np.load(npz, allow_pickle=False) as z:
+            meta = {k: z[k] for k in z.files}
+        if "name" in meta:
+            meta["name"] = str(meta["name"])
+        return meta
+    import pickle
+    with open(path + "_meta.pkl", "rb") as f:
+        return pickle.load(f)
+
+
+def world_to_image(world, offset, spacing) -> np.ndarray:
+    """utils/geometry.py:21-26: round((world - offset) / spacing) to int (3-D coordinates)."""
+    world, offset, spacing = (np.asarray(a, dtype=np.float64) for a in (world, offset, spacing))
+    if not (world.shape == offset.shape == spacing.shape == (3,)):
+        raise ValueError("world_to_image: 3-D coordinates, offset and spacing")
+    return ((world - offset) / spacing).round().astype(int)
+
+
+def patch_bounds(target, source_shape, coords) -> np.ndarray:
+    """utils/geometry.py:131-138 get_patch_bounds (with ensure_valid_bounds, :114-128): per dim
+    [coord - half, coord + half + target % 2], shifted inside [0, size)."""
+    target = np.array(target)
+    half = np.where(target == -1, np.array(source_shape), target) // 2
+    coords = np.asarray(coords)
+    bbox = np.stack([coords - half, coords + half + target % 2], -1)
+    for i, (t, size) in enumerate(zip(target, source_shape)):
+        s, e = int(bbox[i, 0]), int(bbox[i, 1])
+        if s < 0 and e > size:
+            raise ValueError(f"patch_bounds: patch {int(t)} larger than the slice extent {size}")
+        if s < 0:
+            s, e = 0, int(t)
+        if e > size:
+            s, e = size - int(t), size
+        if s < 0:  # the reference slices a shorter patch here and fails when it assembles the batch
+            raise ValueError(f"patch_bounds: patch {int(t)} larger than the slice extent {size}")
+        bbox[i] = (s, e)
+    return bbox
+
+
+def sample_2d(shape: Sequence[int], meta: dict, patch: Sequence[int], rng: np.random.Generator):
+    """CCTADataLoader.get_samplable_2D + generate_one's pad-then-random-crop (CCTADataLoader.py:50-70,
+    88-104) for a [W,H,D,2] scan: (z, W / H boxes of read_crop), drawing from ``rng`` in the
+    reference's order: the branch, then the centre-line index or the slice, then (random slice)
+    the crop offsets."""
+    W, H, D = (int(x) for x in shape[:3])
+    if rng.random() < 0.5:  # a patch around a random centre-line point, in its slice
+        cl = np.asarray(meta["centerlines_world"])
+        i = rng.integers(0, len(cl))
+        x, y, z = world_to_image(cl[i, :3], meta["offset"], meta["spacing"])
+        bb = patch_bounds(patch, (W, H), np.array([y, x]))  # the reference's (y, x) order
+        if not -D <= z < D:
+            raise IndexError(f"sample_2d: centre-line slice {z} outside the scan's {D} slices")
+        box = tuple((int(lo), 0, int(hi - lo)) for lo, hi in bb)
+        if tuple(b[2] for b in box) != tuple(patch):
+            raise ValueError(f"sample_2d: centre-line patch {[b[2] for b in box]} != {tuple(patch)}")
+        return int(z) % D, box
+    z = int(rng.choice(D))
+    return z, tuple(crop_box((W, H), patch, rng))
+
+
 class PatchLoader:
     def __init__(self, data: List[str], patch_shape: Sequence[int], batch_size: int, rng: np.random.Generator,
                  scaler=None, infinite: bool = True, shuffle: bool = True, device=None, depth: int = 3,
                  num_threads: int = 4, seed_for_shuffle: Optional[int] = None, transform=None):
-        if len(patch_shape) != 3:
-            raise NotImplementedError("PatchLoader: 3-D patches (the 2-D slice sampler is SURVEY.md §8f row 4)")
+        if len(patch_shape) not in (2, 3):
+            raise ValueError(f"PatchLoader: 2-D or 3-D patches, got {tuple(patch_shape)}")
         self.paths = [str(p) for p in data]
         self.patch = tuple(int(p) for p in patch_shape)
+        self.planar = len(self.patch) == 2  # conf_2D: slices of the scans (sample_2d)
+        self._metas = {}
         self.batch_size, self.rng, self.infinite, self.shuffle = batch_size, rng, infinite, shuffle
         self.shift, self.factor = _scaler_params(scaler)
         self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
@@ -100,13 +187,25 @@ class PatchLoader:
         self._seg = [torch.empty((batch_size, 1, *self.patch), dtype=torch.bool, device=self.device)
                      for _ in range(self.depth)]
         self._copied = [None] * self.depth  # HIP event: slot's H2D copy finished (host slot reusable)
-        self.transform = transform
-        if transform is not None:  # unpack into staging buffers, augment into the returned ones
-            if tuple(transform.patch_size) != self.patch:
-                raise ValueError(f"PatchLoader: transform patch {transform.patch_size} != loader patch {self.patch}")
+        if transform is None:
+            self.transforms = []
+        else:
+            self.transforms = list(transform) if isinstance(transform, (list, tuple)) else [transform]
+        self.transform = self.transforms[0] if len(self.transforms) == 1 else (self.transforms or None)
+        self._aug_ws = None
+        for t in self.transforms:
+            if not hasattr(t, "run"):
+                raise TypeError(f"PatchLoader: transform {type(t).__name__} has no device implementation")
+            if getattr(t, "patch_size", None) is None:
+                t.patch_size = self.patch  # MirrorTransform: the patch it runs on
+            if tuple(t.patch_size) != self.patch:
+                raise ValueError(f"PatchLoader: transform patch {t.patch_size} != loader patch {self.patch}")
+            if hasattr(t, "kernel_dims"):  # SpatialTransform_2: resampling workspace
+                self._aug_ws = torch.empty(ops.augment_ws_floats(batch_size, t.kernel_dims, batch_size),
+                                           device=self.device)
+        if self.transforms:  # ping-pong with staging buffers so that the last transform writes the returned ones
             self._pre_data = [torch.empty_like(t) for t in self._data]
             self._pre_seg = [torch.empty_like(t) for t in self._seg]
-            self._aug_ws = torch.empty(ops.augment_ws_floats(batch_size, self.patch, batch_size), device=self.device)
         self._stream = torch.cuda.Stream(device=self.device)
         self._threads, self._pool = num_threads, None
         self._lock = threading.Lock()
@@ -125,6 +224,12 @@ class PatchLoader:
             self._vols[path] = v
         return v
 
+    def _meta(self, path: str) -> dict:
+        m = self._metas.get(path)
+        if m is None:
+            m = self._metas[path] = load_meta(path)
+        return m
+
     def _indices(self) -> Optional[List[int]]:
         with self._lock:
             idx = []
@@ -138,10 +243,14 @@ class PatchLoader:
                     self._pos = 0
                 idx.append(self._order[self._pos])
                 self._pos += 1
-            boxes = [crop_box(self._volume(self.paths[i]).shape[:3], self.patch, self.rng) for i in idx]
+            if self.planar:
+                boxes = [sample_2d(self._volume(self.paths[i]).shape, self._meta(self.paths[i]), self.patch, self.rng)
+                         for i in idx]
+            else:
+                boxes = [crop_box(self._volume(self.paths[i]).shape[:3], self.patch, self.rng) for i in idx]
             aug = None
-            if self.transform is not None:  # drawn here, under the lock, from the loader's generator
-                aug = self.transform.draw(self.rng, self.batch_size)
+            if self.transforms:  # drawn here, under the lock, from the loader's generator, in order
+                aug = [t.draw(self.rng, self.batch_size) for t in self.transforms]
             return list(zip(idx, boxes)), aug
 
     def _fill(self, slot: int, picks):
@@ -153,7 +262,8 @@ class PatchLoader:
         for b, (i, box) in enumerate(picks):
             read_crop(self._volume(self.paths[i]), self.patch, box, host[b])
         if aug is not None:  # small parameter / noise tensors, pinned by this worker for the async copy
-            aug = tuple(None if a is None else torch.from_numpy(a).pin_memory() for a in aug)
+            aug = [tuple(None if a is None else torch.from_numpy(np.ascontiguousarray(a)).pin_memory() for a in prm)
+                   for prm in aug]
         return picks, aug
 
     def _submit(self):
@@ -206,11 +316,13 @@ class PatchLoader:
             if aug is None:
                 ops.unpack_patches(self._raw[slot], self._data[slot], self._seg[slot], self.shift, self.factor)
             else:
-                ops.unpack_patches(self._raw[slot], self._pre_data[slot], self._pre_seg[slot], self.shift,
-                                   self.factor)
-                prm, noise, gauss = (None if a is None else a.to(self.device, non_blocking=True) for a in aug)
-                self.transform.apply(self._pre_data[slot], self._pre_seg[slot], prm, noise, gauss, self._data[slot],
-                                     self._seg[slot], ws=self._aug_ws)
+                bufs = [(self._data[slot], self._seg[slot]), (self._pre_data[slot], self._pre_seg[slot])]
+                k = len(self.transforms) % 2  # buffer the unpack writes: the last transform ends in _data
+                ops.unpack_patches(self._raw[slot], *bufs[k], self.shift, self.factor)
+                for t, prm in zip(self.transforms, aug):
+                    dev = tuple(None if a is None else a.to(self.device, non_blocking=True) for a in prm)
+                    t.run(dev, *bufs[k], *bufs[1 - k], ws=self._aug_ws)
+                    k = 1 - k
                 self._aug_keep = aug  # pinned sources alive until the next batch's copies are queued
         cur.wait_stream(self._stream)
         names = [Path(self.paths[i]).name for i, _ in picks]

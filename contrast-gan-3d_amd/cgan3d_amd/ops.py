@@ -1082,10 +1082,12 @@ def augment_ws_floats(n: int, dims, n_elastic: int) -> int:
 
 def spatial_augment(data: torch.Tensor, seg: torch.Tensor, params: torch.Tensor, noise: Optional[torch.Tensor],
                     gauss: Optional[torch.Tensor], n_elastic: int, data_out: torch.Tensor, seg_out: torch.Tensor,
-                    ws: torch.Tensor):
+                    ws: torch.Tensor, dims=None):
     """SpatialTransform_2 on a patch batch (cgan3d_spatial_augment): data [n, 1?, a0, a1, a2] float32,
-    seg of the same shape (bool / uint8), per-sample params [n, 16]; out of place."""
-    n, dims = data.shape[0], tuple(data.shape[-3:])
+    seg of the same shape (bool / uint8), per-sample params [n, 16]; out of place.  ``dims``: (a0, a1,
+    a2) when the trailing three dims are not the patch (a 2-D patch (W, H) runs as (1, W, H))."""
+    n = data.shape[0]
+    dims = tuple(data.shape[-3:]) if dims is None else tuple(int(d) for d in dims)
     vox = dims[0] * dims[1] * dims[2]
     _need(data, n * vox, "spatial_augment data")
     _need(data_out, n * vox, "spatial_augment data_out")
@@ -1101,6 +1103,24 @@ def spatial_augment(data: torch.Tensor, seg: torch.Tensor, params: torch.Tensor,
     check(_launch("cgan3d_spatial_augment", ptr(data), ptr(seg), n, *dims, ptr(params),
                   ptr(noise) if n_elastic else None, n_elastic, ptr(gauss) if n_elastic else None, ptr(data_out),
                   ptr(seg_out), ptr(ws)), "spatial_augment")
+
+
+def mirror(data: torch.Tensor, seg: torch.Tensor, flags: torch.Tensor, data_out: torch.Tensor,
+           seg_out: torch.Tensor, dims):
+    """MirrorTransform on a device batch (cgan3d_mirror): data / seg [n, 1?, *patch] with ``dims`` =
+    (a0, a1, a2) (a 2-D patch (W, H) as (1, W, H)), sample s flipped along a_d for every set bit d
+    of flags[s] (device int32 [n]); out of place."""
+    n = data.shape[0]
+    dims = tuple(int(d) for d in dims)
+    vox = dims[0] * dims[1] * dims[2]
+    _need(data, n * vox, "mirror data")
+    _need(data_out, n * vox, "mirror data_out")
+    for t, nm in ((seg, "seg"), (seg_out, "seg_out")):
+        if t.dtype not in (torch.bool, torch.uint8):
+            raise TypeError(f"mirror: {nm} must be bool or uint8")
+        _need(t, n * vox, f"mirror {nm}", dtype=t.dtype)
+    _need(flags, n, "mirror flags", dtype=torch.int32)
+    check(_launch("cgan3d_mirror", ptr(data), ptr(seg), n, *dims, ptr(flags), ptr(data_out), ptr(seg_out)), "mirror")
 
 
 def patch_accumulate(patches: torch.Tensor, origins: torch.Tensor, out: torch.Tensor, weight: torch.Tensor):

@@ -68,11 +68,13 @@ class FusedAdam(torch.optim.Optimizer):
         generator (37 us against 11 + 11), so the engine repacks separately."""
         a = self.arena
         ops.adam_pack(a.flat, a.grad, a.exp_avg, a.exp_avg_sq, self.hyper, self.ticket, packs)
+        self._opt_called = True  # what torch's LR schedulers check optimizer.step() for
         if not ops.recording():  # a recorded plan counts its steps when it runs (note_step)
             self._host_step += 1
 
     def note_step(self):
         """Count one update issued by a replayed launch plan (the device counter ticks itself)."""
+        self._opt_called = True
         self._host_step += 1
 
     @torch.no_grad()

@@ -181,11 +181,14 @@ __global__ __launch_bounds__(256) void aug_sample_kernel(const float* __restrict
     seg_out[i] = sv;
     // data: cubic B-spline on the padded coefficients
     const float q0 = c[0] + kAugPad, q1 = c[1] + kAugPad, q2 = c[2] + kAugPad;
-    const float f0 = floorf(q0), f1 = floorf(q1), f2 = floorf(q2);
+    const float f0 = a0 == 1 ? (float)kAugPad : floorf(q0), f1 = floorf(q1), f2 = floorf(q2);
     float w0[4], w1[4], w2[4];
     bspline3_w(q0 - f0, w0);
     bspline3_w(q1 - f1, w1);
     bspline3_w(q2 - f2, w2);
+    if (a0 == 1) {  // 2-D patches (a0 = 1, not prefiltered along it): the plane itself, weight 1
+      w0[0] = 0.f; w0[1] = 1.f; w0[2] = 0.f; w0[3] = 0.f;
+    }
     const float* cb = coeff + (long long)s * b0 * b1 * b2;
     float acc = 0.f;
 #pragma unroll
@@ -207,6 +210,26 @@ __global__ __launch_bounds__(256) void aug_sample_kernel(const float* __restrict
 
 static int aug_blocks(long long n) { return (int)std::min<long long>((n + 255) / 256, 16384); }
 
+// MirrorTransform (batchgenerators augment_mirroring): out[s][i] = x[s][i with axis d reversed for
+// every set bit d of flags[s]]; seg likewise.  Out of place.
+__global__ __launch_bounds__(256) void aug_mirror_kernel(const float* __restrict__ x, const unsigned char* __restrict__ seg,
+                                                         int n, int a0, int a1, int a2, const int* __restrict__ flags,
+                                                         float* __restrict__ out, unsigned char* __restrict__ seg_out) {
+  const long long vox = (long long)a0 * a1 * a2, tot = vox * n;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < tot; i += (long long)gridDim.x * blockDim.x) {
+    const int s = (int)(i / vox);
+    const long long v = i - (long long)s * vox;
+    int i2 = (int)(v % a2), i1 = (int)((v / a2) % a1), i0 = (int)(v / ((long long)a1 * a2));
+    const int f = flags[s];
+    if (f & 1) i0 = a0 - 1 - i0;
+    if (f & 2) i1 = a1 - 1 - i1;
+    if (f & 4) i2 = a2 - 1 - i2;
+    const long long src = (long long)s * vox + ((long long)i0 * a1 + i1) * a2 + i2;
+    out[i] = x[src];
+    seg_out[i] = seg[src];
+  }
+}
+
 }  // namespace cg
 
 using namespace cg;
@@ -221,8 +244,9 @@ extern "C" int cgan3d_spatial_augment(const float* data, const uint8_t* seg, int
                                       int32_t a2, const float* params, const float* noise, int32_t n_elastic,
                                       const float* gauss, float* data_out, uint8_t* seg_out, float* ws,
                                       void* stream) {
-  CG_CHECK_ARG(data && seg && params && data_out && seg_out && ws && n > 0 && a0 > 1 && a1 > 1 && a2 > 1,
+  CG_CHECK_ARG(data && seg && params && data_out && seg_out && ws && n > 0 && a0 >= 1 && a1 > 1 && a2 > 1,
                "cgan3d_spatial_augment: bad args");
+  CG_CHECK_ARG(a0 > 1 || n_elastic == 0, "cgan3d_spatial_augment: 2-D patches (a0 = 1) take no elastic deformation");
   CG_CHECK_ARG(n_elastic >= 0 && n_elastic <= n && (n_elastic == 0 || (noise && gauss)),
                "cgan3d_spatial_augment: elastic samples need noise and Gaussian kernels");
   CG_CHECK_ARG(data_out != data && (const void*)seg_out != (const void*)seg, "cgan3d_spatial_augment: in place");
@@ -242,8 +266,9 @@ extern "C" int cgan3d_spatial_augment(const float* data, const uint8_t* seg, int
                (long long)b2);
   ::cg::launch(aug_prefilter_kernel, dim3((unsigned)((l1 + 255) / 256)), dim3(256), 0, st, coeff, l1, b1, (long long)b2,
                (long long)b2, (long long)b1 * b2);
-  ::cg::launch(aug_prefilter_kernel, dim3((unsigned)((l0 + 255) / 256)), dim3(256), 0, st, coeff, l0, b0,
-               (long long)b1 * b2, (long long)b1 * b2, (long long)b0 * b1 * b2);
+  if (a0 > 1)  // a 2-D patch (a0 = 1) is sampled on its plane only
+    ::cg::launch(aug_prefilter_kernel, dim3((unsigned)((l0 + 255) / 256)), dim3(256), 0, st, coeff, l0, b0,
+                 (long long)b1 * b2, (long long)b1 * b2, (long long)b0 * b1 * b2);
   CG_LAUNCH_CHECK("aug_prefilter_kernel");
   if (n_elastic > 0) {  // separable circular Gaussian: noise -> fa (axis 0) -> fb (axis 1) -> fa (axis 2)
     const int kst = std::max(a0, std::max(a1, a2));
@@ -262,5 +287,17 @@ extern "C" int cgan3d_spatial_augment(const float* data, const uint8_t* seg, int
                (const unsigned char*)seg, (int)n, (int)a0, (int)a1, (int)a2, params, (const float*)fa,
                (const float*)fstats, data_out, (unsigned char*)seg_out);
   CG_LAUNCH_CHECK("aug_sample_kernel");
+  return CGAN3D_OK;
+}
+
+extern "C" int cgan3d_mirror(const float* data, const uint8_t* seg, int32_t n, int32_t a0, int32_t a1, int32_t a2,
+                             const int32_t* flags, float* data_out, uint8_t* seg_out, void* stream) {
+  CG_CHECK_ARG(data && seg && flags && data_out && seg_out && n > 0 && a0 >= 1 && a1 >= 1 && a2 >= 1,
+               "cgan3d_mirror: bad args");
+  CG_CHECK_ARG(data_out != data && (const void*)seg_out != (const void*)seg, "cgan3d_mirror: in place");
+  ::cg::launch(aug_mirror_kernel, dim3(aug_blocks((long long)n * a0 * a1 * a2)), dim3(256), 0, (hipStream_t)stream,
+               data, (const unsigned char*)seg, (int)n, (int)a0, (int)a1, (int)a2, (const int*)flags, data_out,
+               (unsigned char*)seg_out);
+  CG_LAUNCH_CHECK("aug_mirror_kernel");
   return CGAN3D_OK;
 }

@@ -379,6 +379,11 @@ int64_t cgan3d_augment_ws_floats(int32_t n, int32_t a0, int32_t a1, int32_t a2, 
 int cgan3d_spatial_augment(const float* data, const uint8_t* seg, int32_t n, int32_t a0, int32_t a1, int32_t a2,
                            const float* params, const float* noise, int32_t n_elastic, const float* gauss,
                            float* data_out, uint8_t* seg_out, float* ws, void* stream);
+/* batchgenerators MirrorTransform (experiments/conf_2D.py:36-43: axes (0, 1), p_per_sample 0.5;
+ * augment_mirroring): data/seg [n][a0][a1][a2] out of place into data_out/seg_out, sample s flipped
+ * along a_d where bit d of flags[s] (device, n int32) is set.  The host draws the flags. */
+int cgan3d_mirror(const float* data, const uint8_t* seg, int32_t n, int32_t a0, int32_t a1, int32_t a2,
+                  const int32_t* flags, float* data_out, uint8_t* seg_out, void* stream);
 
 /* --- losses (model/loss.py:11-80, model/utils.py:12-41, Trainer.py:119-154) ---
  * losses[] slots: 0 D total, 1 W_D, 2 GP, 3 G (adversarial), 4 sim (ZNCC), 5 HU, 6 G-full. */

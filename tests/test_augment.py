@@ -114,3 +114,40 @@ def test_overrides_module_swaps_the_loader_factory():
     m = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(m)
     assert m.train_u.create_dataloaders is ours.create_dataloaders
+
+
+def test_transforms_from_conf_2d_like_compose():
+    """create_dataloaders takes conf_2D's train_transform (conf_2D.py:36-43): SpatialTransform_2 then
+    MirrorTransform(axes=(0, 1), p_per_sample=0.5), NumpyToTensor dropped — in order, from
+    batchgenerators-shaped instances; the 2-D draws keep augment_spatial_2's order (one angle)."""
+    from cgan3d_amd.data.augment import MirrorTransform, SpatialTransform_2
+    from cgan3d_amd.trainer.utils import transforms_from
+    from oracle import augment_ref as A
+
+    def bg(name, **attrs):
+        cls = type(name, (), {})
+        o = cls()
+        for k, v in attrs.items():
+            setattr(o, k, v)
+        return o
+    rot = dict(angle_x=(-2 * np.pi, 2 * np.pi), angle_y=(-2 * np.pi, 2 * np.pi), angle_z=(-2 * np.pi, 2 * np.pi))
+    sp = bg("SpatialTransform_2", patch_size=(32, 32), random_crop=False, do_elastic_deform=False, do_scale=False,
+            do_rotation=True, p_rot_per_sample=0.5, order_data=3, border_mode_data="nearest", order_seg=0,
+            border_mode_seg="constant", border_cval_seg=0, **rot)
+    mi = bg("MirrorTransform", axes=(0, 1), data_key="data", label_key="seg", p_per_sample=0.5)
+
+    class Compose:
+        def __init__(self, ts):
+            self.transforms = ts
+    ts = transforms_from(Compose([sp, mi, bg("NumpyToTensor"), bg("NumpyToTensor")]))
+    assert [type(t) for t in ts] == [SpatialTransform_2, MirrorTransform]
+    assert ts[0].patch_size == (32, 32) and ts[1].axes == (0, 1) and ts[1].p_per_sample == 0.5
+    prm, noise, gauss = ts[0].draw(np.random.default_rng(4), 12)
+    want = A.spatial_2_decisions(np.random.default_rng(4).random, 12, 2, p_rot_per_sample=0.5, do_scale=False, **rot)
+    assert [d.get("angles") for d in ts[0].last_decisions] == [d.get("angles") for d in want]
+    assert noise is None and gauss is None and set(prm[:, 12]) <= {-1.0, -2.0}
+    rotated = prm[:, 12] == -1
+    assert rotated.any() and not rotated.all()
+    assert np.allclose(prm[rotated, 0], 1) and np.allclose(prm[rotated][:, [1, 2, 3, 6]], 0)
+    with pytest.raises(NotImplementedError):
+        SpatialTransform_2((16, 16), random_crop=False)  # 2-D elastic deformation (on by default)

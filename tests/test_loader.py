@@ -6,6 +6,8 @@ CCTADataLoader.generate_one (contrast_gan_3D/data/CCTADataLoader.py:88-104): pad
 CPU: the crop geometry and the host copy.  GPU: whole batches through the pinned ring, the H2D
 copy and the unpack kernel, bit-exact against numpy.
 """
+import copy
+
 import numpy as np
 import pytest
 
@@ -38,7 +40,7 @@ def test_crop_matches_pad_then_crop(shape):
 def test_crop_offsets_cover_range():
     rng = np.random.default_rng(1)
     seen = {crop_box((20, 16, 8), (16, 16, 16), rng)[0][0] for _ in range(400)}
-    assert seen == set(range(5))  # randint(0, S - P + 1): both extremes reachable
+    assert seen == set(range(4))  # get_lbs_for_random_crop: randint(0, S - P), the upper end excluded
     assert crop_box((20, 16, 8), (16, 16, 16), rng)[1:] == [(0, 0, 16), (0, 4, 8)]
 
 
@@ -110,3 +112,59 @@ def test_loader_batches_bit_exact(tmp_path, src_dtype):
             np.testing.assert_array_equal(seg[j, 0], ref[..., 1] != 0)
     assert seen == set(paths)
     loader._finish()
+
+
+def _scan_2d(rng, shape, n_cl=12):
+    """A [W, H, D, 2] int16 scan whose HU encodes the voxel coordinates, and its meta record with
+    centre-line points in world coordinates (offset, anisotropic spacing) on the label channel."""
+    W, H, D = shape
+    x, y, z = np.meshgrid(np.arange(W), np.arange(H), np.arange(D), indexing="ij")
+    hu = (x * H * D + y * D + z - 2000).astype(np.int16)
+    offset, spacing = np.array([-30.0, 12.5, 4.0]), np.array([0.4, 0.45, 0.6])
+    img = np.stack([rng.integers(0, W, n_cl), rng.integers(0, H, n_cl), rng.integers(0, D, n_cl)], -1)
+    lab = np.zeros((W, H, D), np.int16)
+    lab[img[:, 0], img[:, 1], img[:, 2]] = 1
+    world = img * spacing + offset + rng.uniform(-0.15, 0.15, img.shape) * spacing
+    meta = {"offset": offset, "spacing": spacing, "centerlines_world": np.concatenate([world, np.ones((n_cl, 1))], 1)}
+    return np.stack([hu, lab], -1), meta
+
+
+@pytest.mark.parametrize("shape,patch", [((40, 36, 7), (16, 16)), ((12, 40, 5), (16, 16)), ((16, 16, 3), (16, 16))])
+def test_sample_2d_matches_get_samplable_2d(shape, patch):
+    """conf_2D's slice sampler (CCTADataLoader.get_samplable_2D + generate_one, CCTADataLoader.py:50-104)
+    against the numpy restatement (oracle/loader_ref.py) on twin generators: the same slices, centre-line
+    patches (the reference's (y, x) bounds order kept) and pad-then-random-crop patches, draw for draw."""
+    from cgan3d_amd.data.loader import sample_2d
+    from oracle import loader_ref as R
+    rng = np.random.default_rng(5)
+    vol, meta = _scan_2d(rng, shape)
+    ours, ref = np.random.default_rng(11), np.random.default_rng(11)
+    out = np.zeros((*patch, 2), np.int16)
+    kinds = {"centre": 0, "slice": 0, "refused": 0}
+    for _ in range(60):
+        along = copy.deepcopy(ref).random() < 0.5  # the branch get_samplable_2D is about to take
+        try:
+            want, mask = R.generate_one_2d(vol, meta, patch, ref, 0.0, 1.0)
+        except (AssertionError, IndexError):  # a centre-line patch wider than the slice: the reference asserts
+            with pytest.raises(ValueError):
+                sample_2d(vol.shape, meta, patch, ours)
+            kinds["refused"] += 1
+            continue
+        z, box = sample_2d(vol.shape, meta, patch, ours)
+        read_crop(vol, patch, (z, box), out)
+        np.testing.assert_array_equal(out[..., 0].astype(np.float32), want)
+        np.testing.assert_array_equal(out[..., 1].astype(np.float32), np.asarray(mask, np.float32))
+        kinds["centre" if along else "slice"] += 1
+    assert ours.random() == ref.random()  # the generators advanced in step
+    assert kinds["slice"] > 10 and (kinds["centre"] > 10 or kinds["refused"] > 10), kinds
+
+
+def test_patch_bounds_edges():
+    from cgan3d_amd.data.loader import patch_bounds
+    from oracle import loader_ref as R
+    for coords in ([0, 0], [3, 30], [39, 35], [20, 17], [7, 8]):
+        for patch in ((16, 16), (15, 9), (40, 36)):
+            want = R.get_patch_bounds(np.array(patch), (40, 36), np.array(coords))
+            np.testing.assert_array_equal(patch_bounds(patch, (40, 36), np.array(coords)), want)
+    with pytest.raises(ValueError):
+        patch_bounds((50, 16), (40, 36), np.array([20, 10]))
