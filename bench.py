@@ -15,8 +15,11 @@ in place inside eager steps run after the timed region, on the launch stream; al
 from the launch geometry, 2 * out-voxels * Cout * Cin * k^3; ``warm_cache`` the same launches
 repeated back to back; ``step`` the whole step against the MFMA and HBM peaks),
 ``reference_schedule`` (patches/s when the generator trains every 5th iteration, as the
-reference's basic_conf does) and ``cpu_baseline`` (the oracle — torch fp32 on the host cores — on
-a bounded sample, rank 0 only, N=1 only).
+reference's basic_conf does), ``h2d`` (each batch copied from pinned host memory on a copy stream,
+overlapped with the previous step — the PatchLoader's form; ``value`` stays HBM-resident), ``f32``
+(the exact-fp32 parity path at the same workload), ``b128_f32`` (BASELINE.json configs[2]: 128^3
+B=1 fp32) and ``cpu_baseline`` (the oracle — torch fp32 on the host cores — on a bounded sample,
+rank 0 only, N=1 only).  ``--no-sub`` skips h2d / f32 / b128_f32.
 
 Precision: ``--precision bf16`` (default; BASELINE.json's metric is quoted in bf16) runs every
 convolution on bf16 MFMA operands with fp32 accumulation, BatchNorm / losses / Adam in fp32;
@@ -108,7 +111,103 @@ def cpu_baseline(size, seconds, g_args):
             break
     return {"value": round(n * b / el, 4), "unit": "patches/s", "cores": threads, "kind": "port",
             "sample": f"oracle/reference_torch.py train_step, {size}^3, batch 1+1, GP conf, fp32, {n} steps in "
-                      f"{el:.1f}s after 1 warm-up step"}
+                      f"{el:.1f}s after 1 warm-up step; patches/s per subopt patch at batch 1 stands for the GPU "
+                      f"line's batch (the CPU step's work and time grow linearly with the batch)"}
+
+
+def sub_config(S, B, precision, dev, g_args, steps=20, warmup=3):
+    """Another single-GPU configuration of the same step in this run (BASELINE.json configs[2]: 128^3
+    B=1 fp32; the exact-f32 parity path at 64^3 B=4): plan mode, ``steps`` timed steps."""
+    from torch import nn
+    from cgan3d_amd.data.synthetic import synth_patches
+    from cgan3d_amd.engine import StepEngine
+    from cgan3d_amd.model.discriminator import PatchGANDiscriminator
+    from cgan3d_amd.model.generator import ResnetGenerator
+    from cgan3d_amd.model.init import pcg64_init_
+    g = pcg64_init_(ResnetGenerator(**g_args), 0).to(dev)
+    d = pcg64_init_(PatchGANDiscriminator(1, 8, 3, negative_slope=0.2, norm_layer=nn.Identity), 1).to(dev)
+    eng = StepEngine(g, d, g.config, d.config, B, B, (S, S, S), g_hyper=(1e-4, 0.0, 0.9, 1e-8),
+                     d_hyper=(1e-4, 0.0, 0.9, 1e-8), device=dev, precision=precision)
+    opt, _ = synth_patches(B, S, 71)
+    sub, seg = synth_patches(B, S, 72)
+    batch = (torch.from_numpy(opt).to(dev), torch.from_numpy(sub).to(dev), torch.from_numpy(seg).to(dev),
+             torch.rand(B, device=dev))
+    for _ in range(warmup):
+        eng.load_inputs(*batch)
+        eng.step()
+    eng.record()
+    eng.load_inputs(*batch)
+    eng.run_plan()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        eng.load_inputs(*batch)
+        eng.run_plan()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    losses = eng.losses.cpu().numpy()
+    assert np.isfinite(losses).all(), f"non-finite losses {losses}"
+    ms = el / steps * 1e3
+    scale = (S / 64.0) ** 3
+    tflops = 46.48e9 * scale * B / (ms * 1e-3) / 1e12
+    out = {"value": round(B * steps / el, 3), "unit": "patches/s", "ms_per_step": round(ms, 3), "steps": steps,
+           "dtype": precision, "config": {"workload": f"{S}^3 patches, {B} OPT + {B} LOW/HIGH, full G+D step "
+                                                     "(WGAN-GP conf)", "patch": S, "global_batch": B},
+           "step_tflops": round(tflops, 3),
+           "step_frac": round(tflops / (BF16_PEAK_TFLOPS if precision == "bf16" else F32_PEAK_TFLOPS), 4)}
+    del eng, g, d
+    torch.cuda.empty_cache()
+    return out
+
+
+def h2d_bench(eng, S, B, dev, steps):
+    """The step with each batch coming from pinned host memory (the PatchLoader's form): batch i + 1's
+    host-to-device copy on a copy stream while step i runs, the step waiting for its own batch's copy."""
+    from cgan3d_amd.data.synthetic import synth_patches
+    host, stage = [], []
+    for j in range(2):
+        opt, _ = synth_patches(B, S, 80 + j)
+        sub, seg = synth_patches(B, S, 90 + j)
+        h = (torch.from_numpy(opt), torch.from_numpy(sub), torch.from_numpy(seg), torch.rand(B))
+        host.append(tuple(t.pin_memory() for t in h))
+        stage.append(tuple(torch.empty_like(t, device=dev) for t in h))
+    cs = torch.cuda.Stream(device=dev)
+    main = torch.cuda.current_stream(dev)
+    ready = [torch.cuda.Event() for _ in range(2)]
+    freed = [None, None]
+
+    def copy(i):
+        k = i % 2
+        if freed[k] is not None:
+            cs.wait_event(freed[k])
+        with torch.cuda.stream(cs):
+            for dst, src in zip(stage[k], host[i % 2]):
+                dst.copy_(src, non_blocking=True)
+            ready[k].record(cs)
+
+    def step(i):
+        k = i % 2
+        copy(i + 1)
+        main.wait_event(ready[k])
+        eng.load_inputs(*stage[k])
+        ev = torch.cuda.Event()
+        ev.record(main)
+        freed[k] = ev
+        eng.run_plan()
+
+    copy(0)
+    for i in range(3):
+        step(i)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(3, 3 + steps):
+        step(i)
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    mb = sum(t.numel() * t.element_size() for t in host[0]) / 1e6
+    return {"value": round(B * steps / el, 3), "unit": "patches/s", "ms_per_step": round(el / steps * 1e3, 3),
+            "steps": steps, "h2d_mb_per_step": round(mb, 2),
+            "timing": "pinned host batch -> HBM on a copy stream, overlapped with the previous step (PatchLoader form)"}
 
 
 class _NullLogger:
@@ -197,6 +296,9 @@ def main():
     ap.add_argument("--batch", type=int, default=4)
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-sub", action="store_true",
+                    help="skip the extra lines (h2d: batches from pinned host memory; f32: the exact-fp32 path; "
+                         "b128_f32: BASELINE configs[2], 128^3 B=1 fp32)")
     ap.add_argument("--precision", choices=["f32", "bf16"], default="bf16",
                     help="MFMA operand precision of the convolutions (accumulation is f32)")
     ap.add_argument("--roofline", choices=sorted(ROOFLINES), default="halo_res")
@@ -413,6 +515,15 @@ def main():
     }
     if ref_sched is not None:
         out["reference_schedule"] = ref_sched
+    if mode == "plan" and world == 1 and not args.no_sub:
+        # beside the resident number: the batch coming over PCIe from pinned host memory each step
+        out["h2d"] = h2d_bench(eng, S, B, dev, args.steps)
+        del eng
+        torch.cuda.empty_cache()
+        # the other single-GPU BASELINE configs in the same run: the exact-fp32 parity path at this
+        # workload, and configs[2] (128^3 B=1 fp32)
+        out["f32"] = sub_config(S, B, "f32", dev, g_args) if args.precision != "f32" else None
+        out["b128_f32"] = sub_config(128, 1, "f32", dev, g_args, steps=10)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(S, args.cpu_seconds, g_args)
     if rank == 0:
