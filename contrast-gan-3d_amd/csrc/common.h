@@ -217,6 +217,10 @@ int wgrad_bf16_group_launch(const cgan3d_conv_geom* geoms, const float* const* g
                             float* const* ws, int n, hipStream_t st);
 int wgrad_bf16_launch(const cgan3d_conv_geom* g, const float* gathered, const float* aligned, float* dwp,
                       hipStream_t st);
+// ResNet-block convs with every operand in LDS, 32x32x16 MFMA (conv_k3m.hip)
+bool k3m_ok(const cgan3d_conv_geom* g, const Epi& e);
+int k3m_launch(const cgan3d_conv_geom* g, const __bf16* wp, float* y, const Epi& e, hipStream_t st);
+void k3m_set(int v);
 bool halo_ok(const cgan3d_conv_geom* g);         // w_packed == 2 and eligible
 bool halo_format_ok(const cgan3d_conv_geom* g);  // eligible ignoring w_packed
 long long halo_mblocks(const cgan3d_conv_geom* g);

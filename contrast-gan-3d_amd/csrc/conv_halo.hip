@@ -613,6 +613,8 @@ int halo_launch(const cgan3d_conv_geom* g, const float* x, const float* w, float
     set_error("conv_halo: geometry not supported");
     return CGAN3D_EINVAL;
   }
+  if (k3_tile_ok(g) && k3m_ok(g, e))  // ResNet-block shape with a bf16 input: operands in LDS (conv_k3m.hip)
+    return k3m_launch(g, reinterpret_cast<const __bf16*>(w), y, e, st);
   if (k3_tile_ok(g)) {  // ResNet-block shape: whole-tile K-split kernel
     const long long tiles = (long long)a.n * a.td * a.th * a.tw;
     // small grids: the 64 output channels split over 2 (or, tuning key 12, 4) blocks per tile

@@ -1,0 +1,312 @@
+// ResNet-block convs (model/blocks.py:56-88: Conv3d 64 -> 64, k3 s1 p1) and their input-grads on
+// v_mfma_f32_32x32x16_bf16 with every operand of a block resident in LDS (round 4; the roofline
+// kernel of bench.py).
+//
+// Why this shape: at 64^3 B=4 a ResNet conv is M = 16384 voxels x N = 64 x K = 1728 — 3.6 GFLOP,
+// 1.5 us of the chip's bf16 peak — so one launch is one round of blocks, and what bounds a block is
+// how many operand bytes it must pull through its CU (tens of GB/s per CU from L2 / the Infinity
+// Cache) and how little of that overlaps its MFMAs.  A block takes a 4 x 4 x 8 output tile (128
+// voxels) x 32 output channels: 256 blocks on the 256 CUs.  Its whole working set — the 6 x 6 x 10
+// bf16 input halo (46 KB) and the 32 channels' packed weights of all 27 taps (108 KB) — is put into
+// LDS at launch by LDS-DMA (global_load_lds_dwordx4), halo first, then the weights tap by tap, every
+// wave with ~38 requests in flight; the MFMAs of a group of 3 taps start as soon as that group has
+// landed (counted vmcnt + raw s_barrier, the later groups still streaming), so the weight stream
+// hides behind the arithmetic.  157 KB per block of HBM / L2 traffic against 249 KB for the 4 x 4 x 4
+// x 64-channel tiles of conv_k3_kernel (weights re-read per 64 voxels).
+//
+// Each wave owns one 32 x 32 output tile (two z-slices of the tile x the 32 channels) over the whole
+// K = 27 x 64: 108 MFMAs, two ds_read_b128 each (A from the halo, B from the weights), no K split
+// and no cross-wave combine.  LDS images are lane-linear (DMA) with the swizzle applied to the
+// global source addresses:
+//  * halo voxel rows of 128 B, granule g at position g ^ ((hx >> 1) & 1 | (hy & 3) << 1); the A
+//    rows of a wave are permuted so that each 16-lane group of a ds_read_b128 (lanes {0-3, 12-15,
+//    20-27} and {4-11, 16-19, 28-31}, MI355X_MICROARCH.md LDS table) reads one whole 4 x 4 (x, y)
+//    plane: conflict-free for every tap shift;
+//  * weight rows (one output channel, 128 B), granule g at position g ^ ((c >> 1) & 7).
+// Epilogue as halo_epilogue: bias, activation, residual, fp32 store, BatchNorm statistics into the
+// fp64 accumulators (cgan3d_bn_fuse modes 3 and 4).  Slab statistics, masks and fp32 staging stay on
+// conv_k3_kernel (conv_halo.hip).
+#include "common.h"
+
+namespace cg {
+
+typedef __bf16 bf16x8_m __attribute__((ext_vector_type(8)));
+typedef float f32x16_m __attribute__((ext_vector_type(16)));
+
+constexpr int KM_TX = 4, KM_TY = 4, KM_TZ = 8;   // output tile
+constexpr int KM_HX = 6, KM_HY = 6, KM_HZ = 10;  // its input halo
+constexpr int KM_HROWS = KM_HX * KM_HY * KM_HZ;  // 360 voxel rows of 64 bf16
+constexpr int KM_HALO = KM_HROWS * 128;          // 46080 B
+constexpr int KM_TAPB = 32 * 128;                // one tap's weights, 32 output channels: 4 KB
+constexpr int KM_LDS = KM_HALO + 27 * KM_TAPB;   // 156672 B
+
+__device__ __attribute__((aligned(16))) unsigned char g_km_zero[16];  // source of the zero halo granules
+
+struct K3mArgs {
+  int n, d, h, w;      // volume (input = output: k3 s1 p1)
+  int tx, ty, tz;      // tiles per dim
+  int tiles, per_xcd;  // tiles; tiles per XCD share of the grid
+};
+
+__device__ __forceinline__ int km_fa(int hx, int hy) { return ((hx >> 1) & 1) | ((hy & 3) << 1); }
+__device__ __forceinline__ int km_fw(int c) { return (c >> 1) & 7; }
+
+// A row r (0..31) of a wave -> (x, y, z-slice zz): ds_read_b128 lane group {0-3, 12-15, 20-27} is
+// the zz = 0 plane, {4-11, 16-19, 28-31} the zz = 1 plane, 4 x 4 in (x, y) each
+__device__ __forceinline__ void km_row(int r, int& x, int& y, int& zz) {
+  int idx;
+  if (r < 4) { zz = 0; idx = r; }
+  else if (r < 12) { zz = 1; idx = r - 4; }
+  else if (r < 16) { zz = 0; idx = r - 8; }
+  else if (r < 20) { zz = 1; idx = r - 8; }
+  else if (r < 28) { zz = 0; idx = r - 12; }
+  else { zz = 1; idx = r - 16; }
+  x = idx & 3;
+  y = idx >> 2;
+}
+
+// One LDS-DMA request (global_load_lds_dwordx4: each lane's 16 bytes to lds_base + 16 * lane), in
+// inline asm (cdna_hip_programming.md §5.7, glds16_asm): the builtin form makes hipcc count it on
+// lgkmcnt too, which turns every counted LDS-read wait of the MFMA loop into lgkmcnt(0).  Its
+// completion is this kernel's own vmcnt waits (KM_WAIT_VM); M0 is set and restored in the statement.
+__device__ __forceinline__ void km_dma16(const void* gsrc, unsigned lds_base) {
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(gsrc), "s"(lds_base)
+               : "memory");
+}
+#define KM_WAIT_VM(N) asm volatile("s_waitcnt vmcnt(" #N ")" ::: "memory")
+
+template <bool TR>
+__global__ __launch_bounds__(256, 1) void conv_k3m_kernel(K3mArgs a, const __bf16* __restrict__ x16,
+                                                          const __bf16* __restrict__ wpk, float* __restrict__ y,
+                                                          Epi ep) {
+  __shared__ __attribute__((aligned(16))) unsigned char smem[KM_LDS];
+  using lds_t = __attribute__((address_space(3))) void*;
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  // blocks b and b + 8 share an XCD under round-robin placement (speed only, never correctness):
+  // the two channel halves of a tile and the consecutive tiles of one XCD's share read the same
+  // halo bytes through that XCD's L2
+  const int b = blockIdx.x;
+  const int half = (b >> 3) & 1;
+  const int tile = (b & 7) * a.per_xcd + (b >> 4);
+  if (tile >= a.tiles) return;  // whole block
+  int t = tile;
+  const int txi = t % a.tx;
+  t /= a.tx;
+  const int tyi = t % a.ty;
+  t /= a.ty;
+  const int tzi = t % a.tz;
+  const int nb = t / a.tz;
+  const int ox = txi * KM_TX - 1, oy = tyi * KM_TY - 1, oz = tzi * KM_TZ - 1;
+  const int co0 = half * 32;
+
+  // ---- LDS-DMA: the halo (45 wave-instructions of 8 voxel rows), then the weights tap by tap (one
+  // 8-channel quarter of every tap per wave).  Lane -> row 8i + lane / 8, position lane % 8, which
+  // holds the row's logical granule position ^ swizzle.
+  const unsigned lds0 = (unsigned)(uintptr_t)(lds_t)smem;  // LDS byte address of the operand area
+  {
+    const int p = lane & 7;
+    for (int i = wave; i < KM_HROWS / 8; i += 4) {
+      const int row = 8 * i + (lane >> 3);
+      const int hx = row % KM_HX, hy = (row / KM_HX) % KM_HY, hz = row / (KM_HX * KM_HY);
+      const int ix = ox + hx, iy = oy + hy, iz = oz + hz;
+      const bool ok = (unsigned)ix < (unsigned)a.w && (unsigned)iy < (unsigned)a.h && (unsigned)iz < (unsigned)a.d;
+      const int g = p ^ km_fa(hx, hy);
+      const void* src = ok ? (const void*)(x16 + ((((long long)nb * a.d + iz) * a.h + iy) * a.w + ix) * 64 + 8 * g)
+                           : (const void*)g_km_zero;
+      km_dma16(src, __builtin_amdgcn_readfirstlane(lds0 + i * 1024));
+    }
+    const int c = 8 * wave + (lane >> 3);  // channel row of the tap image
+    const int cout = co0 + c;
+    // packed format 2 keeps logical granule q of (tap, channel) at position q ^ (channel & 7)
+    const __bf16* src = wpk + (long long)cout * 64 + 8 * ((p ^ km_fw(c)) ^ (cout & 7));
+#pragma unroll
+    for (int tp = 0; tp < 27; ++tp)
+      km_dma16(src + (long long)tp * 64 * 64, __builtin_amdgcn_readfirstlane(lds0 + KM_HALO + tp * KM_TAPB + wave * 1024));
+  }
+
+  // ---- 27 taps x 4 K-steps of 16 channels = 108 MFMAs, in 4 groups of taps (0-2, 3-8, 9-17, 18-26)
+  // behind counted DMA waits + a barrier; inside a group the A / B fragments of the next KM_PD steps
+  // are in flight while an MFMA runs
+  const int r = lane & 31, h = lane >> 5;
+  int lx, ly, lzz;
+  km_row(r, lx, ly, lzz);
+  const int hv0 = ((2 * wave + lzz) * KM_HY + ly) * KM_HX + lx;
+  int boff[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) boff[s] = KM_HALO + r * 128 + 16 * ((2 * s + h) ^ km_fw(r));
+  f32x16_m acc;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) acc[i] = 0.f;
+  auto aoff = [&](int tp, int s) {  // byte offset of this lane's A fragment for step (tap, K-step)
+    const int td = tp / 9, th = (tp / 3) % 3, tw = tp % 3;
+    const int dz = TR ? 2 - td : td, dy = TR ? 2 - th : th, dx = TR ? 2 - tw : tw;
+    const int hv = hv0 + (dz * KM_HY + dy) * KM_HX + dx;
+    const int f = km_fa(lx + dx, ly + dy);
+    return hv * 128 + 16 * (h ^ (f & 1)) + 32 * (s ^ (f >> 1));
+  };
+  constexpr int KM_PD = 5;  // steps in flight (2 reads each: lgkmcnt <= 15)
+  bf16x8_m ra[KM_PD], rb[KM_PD];
+#pragma unroll
+  for (int grp = 0; grp < 4; ++grp) {
+    const int t0 = grp == 0 ? 0 : (grp == 1 ? 3 : (grp == 2 ? 9 : 18));
+    const int t1 = grp == 0 ? 3 : (grp == 1 ? 9 : (grp == 2 ? 18 : 27));
+    // this wave's DMAs up to the group's last tap have landed (27 - t1 younger ones in flight) ...
+    if (grp == 0) KM_WAIT_VM(24);
+    else if (grp == 1) KM_WAIT_VM(18);
+    else if (grp == 2) KM_WAIT_VM(9);
+    else KM_WAIT_VM(0);
+    __builtin_amdgcn_s_barrier();  // ... and every other wave's
+    asm volatile("" ::: "memory");
+    const int k0 = 4 * t0, k1 = 4 * t1;
+#pragma unroll
+    for (int k = k0; k < k0 + KM_PD; ++k) {
+      ra[k % KM_PD] = *reinterpret_cast<const bf16x8_m*>(smem + aoff(k >> 2, k & 3));
+      rb[k % KM_PD] = *reinterpret_cast<const bf16x8_m*>(smem + boff[k & 3] + (k >> 2) * KM_TAPB);
+    }
+#pragma unroll
+    for (int k = k0; k < k1; ++k) {
+      const bf16x8_m av = ra[k % KM_PD], bv = rb[k % KM_PD];
+      if (k + KM_PD < k1) {
+        const int kn = k + KM_PD;
+        ra[kn % KM_PD] = *reinterpret_cast<const bf16x8_m*>(smem + aoff(kn >> 2, kn & 3));
+        rb[kn % KM_PD] = *reinterpret_cast<const bf16x8_m*>(smem + boff[kn & 3] + (kn >> 2) * KM_TAPB);
+      }
+      // source order kept: the reads for step k + KM_PD go out before MFMA k (counted lgkmcnt)
+      __builtin_amdgcn_sched_barrier(0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, bv, acc, 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+
+  // ---- epilogue: lane holds rows R = (i & 3) + 8 (i >> 2) + 4 h of channel co0 + r
+  const int C = 64, c = co0 + r;
+  const float bias = ep.bias ? ep.bias[c] : 0.f;
+  long long oidx[16];
+  float vals[16];
+  int nvalid = 0;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const int R = (i & 3) + 8 * (i >> 2) + 4 * h;
+    int vx, vy, vzz;
+    km_row(R, vx, vy, vzz);
+    const int gx = txi * KM_TX + vx, gy = tyi * KM_TY + vy, gz = tzi * KM_TZ + 2 * wave + vzz;
+    const bool ok = gx < a.w && gy < a.h && gz < a.d;
+    oidx[i] = ok ? ((((long long)nb * a.d + gz) * a.h + gy) * a.w + gx) * C + c : -1;
+    nvalid += ok;
+  }
+  float resv[16], zv[16];
+  const bool mode4 = ep.fz.acc_mode == 4;
+  // residual / BatchNorm-input loads: unconditional inside uniform branches, all issued before the
+  // first use (a per-element condition makes hipcc wait for each load on its own)
+  if (ep.residual) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) resv[i] = ep.residual[oidx[i] >= 0 ? oidx[i] : c];
+  } else {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) resv[i] = 0.f;
+  }
+  if (mode4) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) zv[i] = ep.bn_z[oidx[i] >= 0 ? oidx[i] : c];
+  }
+  const int act = ep.act;
+  const float slope = ep.slope;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    float v = acc[i] + bias;
+    v = act == CGAN3D_ACT_RELU ? fmaxf(v, 0.f) : (act == CGAN3D_ACT_LRELU && v < 0.f ? v * slope : v);
+    v += resv[i];
+    vals[i] = oidx[i] >= 0 ? v : 0.f;
+  }
+#pragma unroll
+  for (int i = 0; i < 16; ++i)
+    if (oidx[i] >= 0) y[oidx[i]] = vals[i];
+  if (!ep.fz.acc_mode) return;
+  double* const facc = ep.fz.acc_out + (long long)(blockIdx.x % ep.fz.reps) * 2 * C;
+  float* red = reinterpret_cast<float*>(smem);  // [2][4 waves][32]; the operands are dead after this barrier
+  __syncthreads();
+  if (ep.fz.acc_mode == 3) {  // (sum, M2 about the block mean) -> (sum, sum of squares) in fp64
+    float s1 = 0.f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) s1 += vals[i];
+    s1 += __shfl_xor(s1, 32, 64);
+    int cnt = nvalid + __shfl_xor(nvalid, 32, 64);
+    if (h == 0) red[wave * 32 + r] = s1;
+    if (tid < 4 * 64 && lane == 0) red[256 + wave] = (float)cnt;
+    __syncthreads();
+    float S = red[r] + red[32 + r] + red[64 + r] + red[96 + r];
+    const float cn = red[256] + red[257] + red[258] + red[259];
+    const float mean = cn > 0.f ? S / cn : 0.f;
+    float q2 = 0.f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const float dv = oidx[i] >= 0 ? vals[i] - mean : 0.f;
+      q2 += dv * dv;
+    }
+    q2 += __shfl_xor(q2, 32, 64);
+    if (h == 0) red[128 + wave * 32 + r] = q2;
+    __syncthreads();
+    if (tid < 32 && cn > 0.f) {
+      const float M2 = red[128 + tid] + red[160 + tid] + red[192 + tid] + red[224 + tid];
+      unsafeAtomicAdd(facc + co0 + tid, (double)S);
+      unsafeAtomicAdd(facc + C + co0 + tid, (double)M2 + (double)S * (double)S / (double)cn);
+    }
+  } else {  // mode 4: (sum g, sum g * xhat) of the BatchNorm layer whose dL/dy this is
+    float p1 = 0.f, p2 = 0.f;
+    const float sc = ep.bn_ss[c], sh = ep.bn_ss[C + c], mu = ep.bn_mi[c], is = ep.bn_mi[C + c];
+    const int bact = ep.bn_act;
+    const float bslope = ep.bn_slope;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {  // bn_pair_z, branch-free
+      const float pre = zv[i] * sc + sh;
+      const float dg = bact == CGAN3D_ACT_RELU ? (pre > 0.f ? 1.f : 0.f)
+                                               : (bact == CGAN3D_ACT_LRELU ? (pre > 0.f ? 1.f : bslope) : 1.f);
+      const float gg = oidx[i] >= 0 ? vals[i] * dg : 0.f;
+      p1 += gg;
+      p2 += gg * (zv[i] - mu) * is;
+    }
+    p1 += __shfl_xor(p1, 32, 64);
+    p2 += __shfl_xor(p2, 32, 64);
+    if (h == 0) {
+      red[wave * 32 + r] = p1;
+      red[128 + wave * 32 + r] = p2;
+    }
+    __syncthreads();
+    if (tid < 32) {
+      unsafeAtomicAdd(facc + co0 + tid, (double)(red[tid] + red[32 + tid] + red[64 + tid] + red[96 + tid]));
+      unsafeAtomicAdd(facc + C + co0 + tid,
+                      (double)(red[128 + tid] + red[160 + tid] + red[192 + tid] + red[224 + tid]));
+    }
+  }
+}
+
+static int g_k3m = 1;  // cgan3d_set_tuning key 15: 0 keeps the ResNet convs on conv_k3_kernel (A/B)
+
+void k3m_set(int v) { g_k3m = v; }
+
+// k3 s1 p1 64 -> 64 (forward, or the input-grad: a stride-1 conv with flipped taps) with a bf16 input
+// shadow, format-2 packed weights and an epilogue this kernel has (no slabs, masks or out2)
+bool k3m_ok(const cgan3d_conv_geom* g, const Epi& e) {
+  return g_k3m && g->prec == CGAN3D_PREC_BF16 && g->w_packed == 2 && g->cin == 64 && g->cout == 64 && g->k == 3 &&
+         g->stride == 1 && g->pad == 1 && !g->reflect && !g->planar && g->di == g->do_ && g->hi == g->ho &&
+         g->wi == g->wo && e.x16 && !e.stats && !e.bn_mode && !e.mask_src && !e.minuend && !e.out2 && !e.bn_fold &&
+         (e.act == CGAN3D_ACT_NONE || e.act == CGAN3D_ACT_RELU || e.act == CGAN3D_ACT_LRELU) &&
+         (e.fz.acc_mode == 0 || e.fz.acc_mode == 3 || e.fz.acc_mode == 4);
+}
+
+int k3m_launch(const cgan3d_conv_geom* g, const __bf16* wp, float* y, const Epi& e, hipStream_t st) {
+  K3mArgs a;
+  a.n = g->n; a.d = g->do_; a.h = g->ho; a.w = g->wo;
+  a.tx = (a.w + KM_TX - 1) / KM_TX; a.ty = (a.h + KM_TY - 1) / KM_TY; a.tz = (a.d + KM_TZ - 1) / KM_TZ;
+  a.tiles = a.n * a.tx * a.ty * a.tz;
+  a.per_xcd = (a.tiles + 7) / 8;
+  const dim3 grid((unsigned)(a.per_xcd * 16));
+  if (g->transposed) ::cg::launch(conv_k3m_kernel<true>, grid, dim3(256), 0, st, a, e.x16, wp, y, e);
+  else ::cg::launch(conv_k3m_kernel<false>, grid, dim3(256), 0, st, a, e.x16, wp, y, e);
+  return CGAN3D_OK;
+}
+
+}  // namespace cg

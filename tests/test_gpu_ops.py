@@ -684,3 +684,72 @@ def test_copy_multi_and_batch_load():
         assert torch.equal(eng.subopt.cpu().reshape(-1), torch.from_numpy(sub).reshape(-1))
         assert torch.equal(eng.mask.cpu().reshape(-1), torch.from_numpy(seg).reshape(-1).to(torch.uint8))
         assert torch.equal(eng.eps.cpu(), eps.cpu())
+
+
+K3M_CASES = [(2, (16, 16, 16)), (1, (6, 8, 10)), (2, (5, 7, 9)), (1, (9, 4, 17))]
+
+
+@pytest.mark.parametrize("n,sp", K3M_CASES)
+def test_conv_k3m_bf16(n, sp):
+    """ResNet-block conv with every operand in LDS (conv_k3m.hip, 32x32x16 MFMA), as the bf16 step
+    launches it: forward from the bf16 input shadow with a ReLU + residual epilogue and BatchNorm
+    statistics into fp64 accumulators (cgan3d_bn_fuse mode 3), and the input-grad with the skip
+    gradient and the BatchNorm-backward pairs (mode 4) — against float64 sums of the same bf16
+    operands at 2e-5 (fp32 accumulation over 1728 terms), the statistics against the kernel's own
+    outputs, and against conv_k3_kernel (tuning key 15 = 0: the same products, another fp32 order).
+    Partial 4 x 4 x 8 tiles on every axis in the ragged cases."""
+    from cgan3d_amd import ops, _lib as L
+    cin = cout = 64
+    g = torch.Generator().manual_seed(5 + sp[0])
+    x = torch.randn(n, cin, *sp, generator=g, dtype=torch.float64).bfloat16().double()
+    w = (torch.randn(cout, cin, 3, 3, 3, generator=g, dtype=torch.float64) / np.sqrt(cin * 27)).float()
+    wq = w.bfloat16().double()
+    res = torch.randn(n, cout, *sp, generator=g, dtype=torch.float64).float().double()
+    gy = torch.randn(n, cout, *sp, generator=g, dtype=torch.float64).bfloat16().double()
+    skip = torch.randn(n, cin, *sp, generator=g, dtype=torch.float64).float().double()
+    yref = torch.relu(F.conv3d(x, wq, padding=1)) + res
+    dxref = torch.nn.grad.conv3d_input(x.shape, wq, gy, padding=1) + skip
+    ps = ops.PackSet(torch.device("cuda"))
+    gf, wf = ps.add(ops.conv_fwd_geom(n, sp, sp, cin, cout, 3, 1, 1), w.cuda(), L.PREC_BF16)
+    gd, wdp = ps.add(ops.conv_dgrad_geom(n, sp, sp, cin, cout, 3, 1, 1), w.cuda(), L.PREC_BF16)
+    ps.pack()
+    assert gf.w_packed == 2 and gd.w_packed == 2
+    reps = 16
+    # BatchNorm of the layer whose dL/dy the input-grad is (mode 4 pairs): its z, scale/shift, mean/invstd
+    z = torch.randn(n, cin, *sp, generator=g, dtype=torch.float64).float()
+    ss = torch.cat([torch.rand(cin, generator=g) + 0.5, torch.randn(cin, generator=g) * 0.1]).float()
+    mi = torch.cat([torch.randn(cin, generator=g) * 0.1, torch.rand(cin, generator=g) + 0.5]).float()
+    out = {}
+    for key, flag in (("k3m", 1), ("k3", 0)):
+        L.check(L.load().cgan3d_set_tuning(15, flag), "k3m switch")
+        try:
+            yo = torch.empty(n, *sp, cout, device="cuda")
+            acc3 = torch.zeros(reps * 2 * cout, device="cuda", dtype=torch.float64)
+            ops.conv(gf, _cl(x), wf, yo, ops.epilogue(act=L.ACT_RELU, residual=_cl(res), x_bf16=_cl(x).bfloat16(),
+                                                      fuse=ops.BnFuse(acc3, 3, reps)))
+            dxo = torch.empty(n, *sp, cin, device="cuda")
+            acc4 = torch.zeros(reps * 2 * cin, device="cuda", dtype=torch.float64)
+            ops.conv(gd, _cl(gy), wdp, dxo, ops.epilogue(residual=_cl(skip), x_bf16=_cl(gy).bfloat16(), bn_z=_cl(z),
+                                                         bn_ss=ss.cuda(), bn_mi=mi.cuda(), bn_act=L.ACT_RELU,
+                                                         fuse=ops.BnFuse(acc4, 4, reps)))
+            torch.cuda.synchronize()
+            out[key] = (yo.cpu(), acc3.cpu(), dxo.cpu(), acc4.cpu())
+        finally:
+            L.check(L.load().cgan3d_set_tuning(15, 1), "k3m on")
+    yo, acc3, dxo, acc4 = out["k3m"]
+    assert_close(_ncdhw(yo).numpy(), yref.numpy(), 2e-5, "k3m fwd")
+    assert_close(_ncdhw(dxo).numpy(), dxref.numpy(), 2e-5, "k3m dgrad")
+    for a, b_, nm in zip(out["k3m"], out["k3"], ("fwd", "acc3", "dgrad", "acc4")):
+        assert_close(a.double().numpy(), b_.double().numpy(), 1e-5, f"k3m vs k3 {nm}")
+    yk = yo.double().view(-1, cout)
+    a3 = acc3.view(reps, 2, cout).sum(0)
+    assert_close(a3[0].numpy(), yk.sum(0).numpy(), 1e-5, "mode-3 sum")
+    assert_close(a3[1].numpy(), (yk * yk).sum(0).numpy(), 1e-5, "mode-3 sum of squares")
+    zk = z.permute(0, 2, 3, 4, 1).reshape(-1, cin).double()
+    gk = dxo.double().view(-1, cin)
+    pre = zk * ss[:cin].double() + ss[cin:].double()
+    gg = gk * (pre > 0).double()
+    a4 = acc4.view(reps, 2, cin).sum(0)
+    assert_close(a4[0].numpy(), gg.sum(0).numpy(), 1e-5, "mode-4 sum g")
+    assert_close(a4[1].numpy(), (gg * (zk - mi[:cin].double()) * mi[cin:].double()).sum(0).numpy(), 1e-5,
+                 "mode-4 sum g xhat")
