@@ -200,6 +200,7 @@ int c1_dgrad_launch(const cgan3d_conv_geom* g, const float* dz, const float* w, 
 int c1_wgrad_launch(const cgan3d_conv_geom* g, const float* x, const float* dz, float* dw, hipStream_t st);
 long long wgrad_k3_ws_floats(const cgan3d_conv_geom* g);
 void wgrad_k3_set_chunks(int v);
+void wgrad_k3m_set(int v);
 bool wgrad_s2_ok(const cgan3d_conv_geom* g);
 long long wgrad_s2_ws_floats(const cgan3d_conv_geom* g);
 void wgrad_s2_set_blocks(int v);

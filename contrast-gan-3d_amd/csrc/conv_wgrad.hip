@@ -19,6 +19,7 @@ namespace cg {
 
 typedef __bf16 bf16x8_w __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x4_w __attribute__((ext_vector_type(4)));
+typedef float f32x16_w __attribute__((ext_vector_type(16)));
 
 struct WgArgs {
   int n, di, hi, wi, do_, ho, wo, cin, cout, k, s, p, reflect;
@@ -510,6 +511,168 @@ __global__ __launch_bounds__(512, 2) void wgrad_k3_kernel(Wk3Args a, const float
     }
 }
 
+// ---- the same weight gradient, round 4 (wgrad_k3m_kernel): the block's operand stream through
+// LDS by LDS-DMA and v_mfma_f32_32x32x16_bf16.  Same decomposition (block = voxel chunk p x tap row
+// (td, th), the 3 taps tw; per-block partials -> wgrad_reduce_lin_kernel), 4 waves: wave w owns the
+// 32 x 32 tile (input channels 32 (w & 1) .., output channels 32 (w >> 1) ..) of the 3 taps.  A
+// stage = 4 units (4 y x 8 x output voxels at one z): X rows of the tap row's window (4 y x 10 x
+// per unit: one staged window serves tw = 0, 1, 2) and dZ rows, 128 B each, DMA'd lane-linearly
+// into one of 4 ring slots three stages ahead of the MFMAs (no staging registers, no conversion,
+// no per-element index math).  MFMA operands by ds_read_b64_tr_b16 (one 16-lane group reads 4
+// voxel rows x 16 channels, lane i receiving channel i): K-step = 16 voxels = 2 y-rows x 8 x, a
+// lane's 8 K-values one y-row's x = 0..7.  Rows keep 16-byte chunk c at c ^ (4 ((r >> 1) & 1)):
+// the 4 consecutive voxel rows of a transposed read then cover all 64 banks once (conflict-free
+// for every tw shift).  Both operands from their bf16 shadows; fp32 operands stay on wgrad_k3_kernel.
+namespace wkm {
+constexpr int UPS = 4;                  // units per stage
+constexpr int XR = 40, ZR = 32;         // X / dZ rows per unit
+constexpr int XROWS = UPS * XR;         // 160
+constexpr int ZROWS = UPS * ZR;         // 128
+constexpr int SROWS = XROWS + ZROWS;    // 288 rows = 36 DMA wave-instructions per stage
+constexpr int SBYTES = SROWS * 128;     // 36864
+constexpr int NSLOT = 4;                // ring slots (3 stages in flight ahead)
+constexpr int DPW = SROWS / 8 / 4;      // DMA instructions per wave per stage (9)
+__device__ __forceinline__ int swz(int r) { return ((r >> 1) & 1) << 2; }
+}  // namespace wkm
+
+__device__ __attribute__((aligned(16))) unsigned char g_wkm_zero[16];
+
+__device__ __forceinline__ void wkm_dma16(const void* gsrc, unsigned lds_base) {
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(gsrc), "s"(lds_base)
+               : "memory");
+}
+
+__device__ __forceinline__ bf16x8_w wkm_tr(const unsigned char* lds, int off0, int off1) {
+  const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(lds + off0));
+  const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(lds + off1));
+  return __builtin_bit_cast(bf16x8_w, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+}
+
+__global__ __launch_bounds__(256, 1) void wgrad_k3m_kernel(Wk3Args a, const __bf16* __restrict__ x16,
+                                                           const __bf16* __restrict__ dz16, float* __restrict__ ws) {
+  using namespace wkm;
+  __shared__ __attribute__((aligned(16))) unsigned char smem[NSLOT * SBYTES];
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int ah = wave & 1, bh = wave >> 1;
+  const int tdh = blockIdx.y, td = tdh / 3, th = tdh % 3, p = blockIdx.x;
+  const int u0 = p * a.upb, un = min(a.upb, a.units - u0);
+  const int nst = (un + UPS - 1) / UPS;
+  const int yb_n = a.h >> 2, xb_n = a.w >> 3;
+  const long long plane = (long long)a.h * a.w;
+  const unsigned lds0 = (unsigned)(uintptr_t)(__attribute__((address_space(3))) void*)smem;
+
+  // ---- DMA of stage s into slot s % NSLOT: wave w issues instructions j = w + 4i (i < DPW); an
+  // instruction covers 8 rows, lane -> row 8j + lane / 8, 16-byte position lane % 8 (holding chunk
+  // position ^ swz(row))
+  auto issue = [&](int s) {
+    // the stage's 4 units (wave-uniform: scalar arithmetic): first voxel of the X window / dZ rows
+    long long xo[UPS], zo[UPS];
+    int zz[UPS], yy[UPS], xx[UPS];
+    bool uo[UPS];
+#pragma unroll
+    for (int u = 0; u < UPS; ++u) {
+      const int uu = u0 + UPS * s + u;
+      uo[u] = uu < u0 + un;
+      const int xb = uu % xb_n, q = uu / xb_n, yb = q % yb_n, zq = q / yb_n;
+      zz[u] = zq % a.d + td - 1;
+      yy[u] = yb * 4 + th - 1;
+      xx[u] = xb * 8 - 1;
+      xo[u] = (long long)(zq + td - 1) * plane + (long long)yy[u] * a.w + xx[u];
+      zo[u] = (long long)zq * plane + (long long)(yb * 4) * a.w + xb * 8;
+    }
+    const int pos = lane & 7, lr = lane >> 3;
+#pragma unroll
+    for (int i = 0; i < DPW; ++i) {
+      const int j = wave + 4 * i;  // instruction: 8 rows of one unit (40 and 32 are multiples of 8)
+      const void* src = g_wkm_zero;
+      if (j < XROWS / 8) {
+        const int u = j / 5, rr = (j - 5 * u) * 8 + lr, hy = rr / 10, hx = rr - 10 * hy;
+        const int chunk = pos ^ swz(8 * j + lr);
+        if (uo[u] && (unsigned)zz[u] < (unsigned)a.d && (unsigned)(yy[u] + hy) < (unsigned)a.h &&
+            (unsigned)(xx[u] + hx) < (unsigned)a.w)
+          src = x16 + ((xo[u] + (long long)hy * a.w + hx) * 64 + 8 * chunk);
+      } else {
+        const int jz = j - XROWS / 8, u = jz >> 2, rr = (jz & 3) * 8 + lr;
+        const int chunk = pos ^ swz(8 * jz + lr);
+        if (uo[u]) src = dz16 + ((zo[u] + (long long)(rr >> 3) * a.w + (rr & 7)) * 64 + 8 * chunk);
+      }
+      wkm_dma16(src, __builtin_amdgcn_readfirstlane(lds0 + (s % NSLOT) * SBYTES + j * 1024));
+    }
+  };
+
+  // ---- per-lane transposed-read offsets inside a stage (bytes): 16-lane group G = lane >> 4 reads
+  // channels 16 (G & 1) .. of its operand half; lane 4q + pp supplies row q's channels 4pp .. 4pp+3;
+  // K-step ks, lane half h (= G >> 1): y-row 2 ks + h, x = q (first read) and q + 4 (second)
+  const int G = lane >> 4, h = G >> 1, q = (lane & 15) >> 2, pp = lane & 3;
+  const int cha = 32 * ah + 16 * (G & 1) + 4 * pp;  // input channel of this lane's A read
+  const int chb = 32 * bh + 16 * (G & 1) + 4 * pp;  // output channel of its B read
+  auto roff = [&](int r, int ch) { return r * 128 + (((ch >> 3) ^ swz(r)) << 4) + (ch & 7) * 2; };
+  f32x16_w acc[3];
+#pragma unroll
+  for (int t = 0; t < 3; ++t)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc[t][i] = 0.f;
+
+  const int npre = nst < NSLOT - 1 ? nst : NSLOT - 1;
+  for (int s = 0; s < npre; ++s) issue(s);
+  for (int s = 0; s < nst; ++s) {
+    // this wave's DMAs of stage s have landed (the younger stages' DPW each still in flight) ...
+    const int ahead = min(nst - 1 - s, NSLOT - 2);
+    if (ahead >= 2) asm volatile("s_waitcnt vmcnt(18)" ::: "memory");
+    else if (ahead == 1) asm volatile("s_waitcnt vmcnt(9)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // ... every wave's, and every wave is done reading slot (s - 1) % NSLOT
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (s + NSLOT - 1 < nst) issue(s + NSLOT - 1);
+    const unsigned char* base = smem + (s % NSLOT) * SBYTES;
+    // 24 steps k = (unit u, K-step ks, tap tw) = (k / 6, (k / 3) % 2, k % 3); the A fragment of step
+    // k + PD (and the B fragment it starts) in flight while MFMA k runs (source order pinned)
+    constexpr int PD = 4, NB = 4;
+    bf16x8_w ra[PD], rb[NB];
+    auto lda = [&](int k) {
+      const int u = k / 6, ks = (k / 3) & 1, tw = k % 3, y = 2 * ks + h;
+      const int xr = u * XR + y * 10 + tw;  // X window rows of x + tw - 1
+      ra[k % PD] = wkm_tr(base, roff(xr + q, cha), roff(xr + q + 4, cha));
+    };
+    auto ldb = [&](int k) {  // the dZ fragment of steps 3 (k / 3) .. + 2
+      const int u = k / 6, ks = (k / 3) & 1, y = 2 * ks + h;
+      const int zr = XROWS + u * ZR + y * 8;  // dZ rows of y-row y, x = 0..7
+      rb[(k / 3) % NB] = wkm_tr(base, roff(zr + q, chb), roff(zr + q + 4, chb));
+    };
+#pragma unroll
+    for (int k = 0; k < PD; ++k) {
+      if (k % 3 == 0) ldb(k);
+      lda(k);
+    }
+#pragma unroll
+    for (int k = 0; k < 6 * UPS; ++k) {
+      const bf16x8_w av = ra[k % PD], bv = rb[(k / 3) % NB];
+      if (k + PD < 6 * UPS) {
+        if ((k + PD) % 3 == 0) ldb(k + PD);
+        lda(k + PD);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      acc[k % 3] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, bv, acc[k % 3], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+  // partials ws[p][tap][b][a]: lane holds a = 32 ah + (i & 3) + 8 (i >> 2) + 4 (lane >> 5), b = 32 bh + (lane & 31)
+  const int b = 32 * bh + (lane & 31), a0 = 32 * ah + 4 * (lane >> 5);
+#pragma unroll
+  for (int tw = 0; tw < 3; ++tw) {
+    float* o = ws + (((long long)p * 27 + tdh * 3 + tw) * 64 + b) * 64 + a0;
+#pragma unroll
+    for (int g4 = 0; g4 < 4; ++g4)
+      *reinterpret_cast<f32x4*>(o + 8 * g4) =
+          f32x4{acc[tw][4 * g4], acc[tw][4 * g4 + 1], acc[tw][4 * g4 + 2], acc[tw][4 * g4 + 3]};
+  }
+}
+
 // dW[b * w_sb + a * w_sa + t] (+)= sum_p ws[p][t][b][a] (27 taps, A gathered x B aligned channels),
 // read along the partials' own layout: block = 64 consecutive elements e = (t, b, a) x NC chunks of
 // the P partials (wave = chunk), so every wave load is 256 contiguous bytes; each lane sums its
@@ -670,6 +833,9 @@ __global__ __launch_bounds__(512) void wgrad_s2_kernel(Ws2Args a, const float* _
 }
 
 static int g_wk3_P = 28;  // cgan3d_set_tuning key 9: voxel chunks (blocks per tap plane); 0 = off
+static int g_wk3m = 1;    // cgan3d_set_tuning key 16: 0 keeps the bf16 ResNet weight grads on wgrad_k3_kernel (A/B)
+
+void wgrad_k3m_set(int v) { g_wk3m = v; }
 
 void wgrad_k3_set_chunks(int v) { g_wk3_P = v; }
 
@@ -702,7 +868,9 @@ int wgrad_k3_launch(const cgan3d_conv_geom* g, const float* gathered, const floa
   Wk3Args a;
   int P;
   wgrad_k3_geometry(g, &a, &P);
-  if (g16 && a16)
+  if (g16 && a16 && g_wk3m)
+    ::cg::launch(wgrad_k3m_kernel, dim3(P, 9), dim3(256), 0, st, a, g16, a16, ws);
+  else if (g16 && a16)
     ::cg::launch(wgrad_k3_kernel<true>, dim3(P, 9), dim3(512), 0, st, a, gathered, aligned, g16, a16, ws);
   else
     ::cg::launch(wgrad_k3_kernel<false>, dim3(P, 9), dim3(512), 0, st, a, gathered, aligned, g16, a16, ws);

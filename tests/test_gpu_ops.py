@@ -410,9 +410,10 @@ def test_wgrad_bf16(cin, cout, k, s, p, reflect, sp):
     dwo = torch.empty(w.shape, device="cuda")
     ops.wgrad(gw, _cl(x), _cl(gy), dwo, ws)
     assert_close(dwo.double().cpu().numpy(), dw.numpy(), 2e-2, "bf16 wgrad")
-    if ((cin, cout, k, s) == (64, 64, 3, 1) and sp[1] % 4 == 0 and sp[2] % 8 == 0) or tuple(sp) == (8, 16, 64):
-        # wgrad_k3_kernel / wgrad_s2_kernel (the generic kernel ignores shadows and sums with
-        # atomics, so no bitwise comparison there): both operands from bf16 shadows, bit-identical
+    if tuple(sp) == (8, 16, 64):
+        # wgrad_s2_kernel (the generic kernel ignores shadows and sums with atomics, so no bitwise
+        # comparison there; the ResNet shape takes wgrad_k3m_kernel from shadows: its own test below):
+        # both operands from bf16 shadows, bit-identical
         dw16 = torch.empty_like(dwo)
         ops.wgrad(gw, _cl(x), _cl(gy), dw16, ws, gathered16=_cl(x).bfloat16(), aligned16=_cl(gy).bfloat16())
         assert torch.equal(dw16, dwo), "bf16-shadow weight grad differs"
@@ -753,3 +754,38 @@ def test_conv_k3m_bf16(n, sp):
     assert_close(a4[0].numpy(), gg.sum(0).numpy(), 1e-5, "mode-4 sum g")
     assert_close(a4[1].numpy(), (gg * (zk - mi[:cin].double()) * mi[cin:].double()).sum(0).numpy(), 1e-5,
                  "mode-4 sum g xhat")
+
+
+@pytest.mark.parametrize("n,sp", [(2, (16, 16, 16)), (1, (5, 4, 8)), (2, (3, 8, 24)), (1, (7, 12, 16))])
+def test_wgrad_k3m_bf16(n, sp):
+    """ResNet-block weight gradient from the bf16 shadows (wgrad_k3m_kernel: LDS-DMA stages, 32x32x16
+    MFMA on transposed LDS reads, per-chunk partials + wgrad_reduce_lin_kernel) against float64 sums
+    of the same bf16 operands at 2e-5, against wgrad_k3_kernel (tuning key 16 = 0: the same products,
+    another fp32 order) at 1e-5, and the accumulate mode; chunks ending inside a stage and volume
+    edges on every axis in the small cases."""
+    from cgan3d_amd import ops, _lib as L
+    cin = cout = 64
+    g = torch.Generator().manual_seed(3 + sp[2])
+    x = torch.randn(n, cin, *sp, generator=g, dtype=torch.float64).bfloat16().double()
+    gy = torch.randn(n, cout, *sp, generator=g, dtype=torch.float64).bfloat16().double()
+    w = torch.zeros(cout, cin, 3, 3, 3, dtype=torch.float64, requires_grad=True)
+    y = F.conv3d(x, w, padding=1)
+    dw, = torch.autograd.grad(y, (w,), gy)
+    gw = ops.with_prec(ops.conv_wgrad_geom(n, sp, sp, cin, cout, 3, 1, 1), L.PREC_BF16)
+    ws = torch.empty(ops.wgrad_ws_floats(gw), device="cuda")
+    out = {}
+    for key, flag in (("k3m", 1), ("k3", 0)):
+        L.check(L.load().cgan3d_set_tuning(16, flag), "wk3m switch")
+        try:
+            dwo = torch.empty(w.shape, device="cuda")
+            ops.wgrad(gw, _cl(x), _cl(gy), dwo, ws, gathered16=_cl(x).bfloat16(), aligned16=_cl(gy).bfloat16())
+            torch.cuda.synchronize()
+            out[key] = dwo.cpu()
+        finally:
+            L.check(L.load().cgan3d_set_tuning(16, 1), "wk3m on")
+    assert_close(out["k3m"].double().numpy(), dw.numpy(), 2e-5, "wk3m vs fp64")
+    assert_close(out["k3m"].double().numpy(), out["k3"].double().numpy(), 1e-5, "wk3m vs wgrad_k3_kernel")
+    dwa = out["k3m"].cuda()
+    ops.wgrad(gw, _cl(x), _cl(gy), dwa, ws, accumulate=True, gathered16=_cl(x).bfloat16(),
+              aligned16=_cl(gy).bfloat16())
+    assert_close(dwa.double().cpu().numpy(), 2 * dw.numpy(), 2e-5, "wk3m accumulate")
