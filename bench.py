@@ -339,8 +339,6 @@ def main():
     from cgan3d_amd.model.init import pcg64_init_
     from cgan3d_amd import _lib
 
-    if os.environ.get("CGAN3D_SMALL_TILE_BELOW"):  # tuning sweeps
-        _lib.check(_lib.load().cgan3d_set_tuning(0, int(os.environ["CGAN3D_SMALL_TILE_BELOW"])), "set_tuning")
 
     g_args = dict(n_resnet_blocks=4, n_updownsample_blocks=2, init_channels_out=16)  # basic_conf.py:49-53
     S, B = args.size, args.batch

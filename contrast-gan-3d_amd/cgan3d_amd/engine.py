@@ -43,14 +43,16 @@ Dims = Tuple[int, int, int]
 #                              (write fp32 tensors only shadow readers consume), no_bn_fuse (BatchNorm
 #                              slabs + finalize launches instead of fp64 accumulators), no_bn_fold
 #                              (reflect-fold pass before the last BatchNorm backward), serial (no side
-#                              streams: a kernel trace then shows unshared durations)
+#                              streams: a kernel trace then shows unshared durations), system_fence
+#                              (cross-stream event records with the system-scope fence, csrc/plan.hip)
 #   CGAN3D_FORCE_DP=1          the data-parallel path over a one-rank group (tools / tests)
 #   CGAN3D_COMM=native|torch|own   data-parallel collectives: RCCL from the launch plan on the process
 #                              group's communicator (default), torch.distributed host callables (the
 #                              fallback), or a communicator of the library's own (ops.NativeComm)
 #   CGAN3D_G_BUCKET_BYTES      generator gradient bucket size under data parallelism
 #   CGAN3D_TUNE, CGAN3D_LIB_PATH   launch-shape knobs, another build of the library (_lib.py)
-DEBUG_FLAGS = ("no_shadow", "keep_fp32", "no_bn_fuse", "no_bn_fold", "serial")
+#   CGAN3D_TRAINER_PLANS=0     the drop-in Trainer issues every step eagerly (no recorded plans)
+DEBUG_FLAGS = ("no_shadow", "keep_fp32", "no_bn_fuse", "no_bn_fold", "serial", "system_fence")
 
 
 def debug(flag: str) -> bool:
@@ -1418,6 +1420,7 @@ class StepEngine:
         """Adam of the tail layers (the arena prefix) with the step tick, then their repack."""
         a, lo, opt = self.g_arena, self.g_split, self.g_optim
         ops.adam_pack(a.flat[:lo], a.grad[:lo], a.exp_avg[:lo], a.exp_avg_sq[:lo], opt.hyper, opt.ticket)
+        opt._opt_called = True  # what torch's LR schedulers check optimizer.step() for
         if not ops.recording():  # a recorded plan counts its steps when it runs (note_step)
             opt._host_step += 1
         self.G.pack_tail()

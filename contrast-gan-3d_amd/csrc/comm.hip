@@ -9,7 +9,7 @@
 // default, the torch process group's own (ops.NativeComm: ProcessGroupNCCL's ncclComm_t, one
 // communicator per process; a second one slowed every kernel of a one-GPU step ~2.4x); with
 // cgan3d_comm_init the library builds its own from a unique id the caller broadcasts
-// (CGAN3D_OWN_COMM=1).  On a shared communicator every rank must issue the same collectives in the
+// (CGAN3D_COMM=own).  On a shared communicator every rank must issue the same collectives in the
 // same order, each ordered after the previous one by stream dependencies.
 #include <dlfcn.h>
 

@@ -10,6 +10,8 @@
 //
 // Contract (as for hipGraph capture): every buffer and device scalar a recorded launch touches
 // must stay allocated and keep its address; values may change between runs.
+#include <cstring>
+
 #include "common.h"
 
 namespace cg {
@@ -21,11 +23,12 @@ static int g_eager_next = -1;
 
 // Cross-stream waits join two streams of one device, so the event's release only has to reach
 // device scope: hipEventDisableSystemFence skips the system-scope cache write-back a default event
-// record issues (CGAN3D_EVENT_SYSTEM_FENCE=1 restores it for A/B runs).
+// record issues (CGAN3D_DEBUG=system_fence restores it for A/B runs).
 static unsigned event_flags() {
   static const unsigned f = [] {
-    const char* v = getenv("CGAN3D_EVENT_SYSTEM_FENCE");
-    return hipEventDisableTiming | ((v && v[0] == '1') ? 0u : (unsigned)hipEventDisableSystemFence);
+    const char* v = getenv("CGAN3D_DEBUG");
+    const bool sys = v && strstr(v, "system_fence") != nullptr;
+    return hipEventDisableTiming | (sys ? 0u : (unsigned)hipEventDisableSystemFence);
   }();
   return f;
 }
