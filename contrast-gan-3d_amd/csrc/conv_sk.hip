@@ -38,7 +38,8 @@ __device__ __forceinline__ void sk_class(int r, int k, int s, int p, int transpo
   }
 }
 
-template <int MT, int NT, int W = 4>  // W: waves per block (MT == 1 splits K over them)
+// W: waves per block (MT == 1 splits K over them); NKC: compile-time K-steps per wave (0: runtime)
+template <int MT, int NT, int W, int NKC>
 __global__ __launch_bounds__(64 * W) void conv_sk_kernel(SkArgs a, const float* __restrict__ x,
                                                          const __bf16* __restrict__ wp, float* y, Epi ep) {
   __shared__ int tq[3][64];
@@ -101,46 +102,58 @@ __global__ __launch_bounds__(64 * W) void conv_sk_kernel(SkArgs a, const float* 
   f32x4 acc[NT];
 #pragma unroll
   for (int t = 0; t < NT; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-  // PF K-steps of operands in flight per wave (a ring of register slots; slot indices are
-  // compile-time after unrolling): the chain is latency-bound, not MFMA-bound
-  constexpr int PF = 4;
+  // K loop (round 4).  Every slot is reloaded unconditionally from a clamped, always-valid address
+  // and dead operands are zeroed by a select, so nothing in the loop branches.  NKC > 0 (the wave's
+  // K-steps fit in NKC, the launcher's choice): the loop is straight-line code with a ring of
+  // PF = min(NKC, 8) register slots, so the compiler counts the loads in flight and each MFMA waits
+  // only for its own slot (vmcnt(N)).  The round-3 loop (a runtime trip count, a branch per slot)
+  // waited for vmcnt(0) before every MFMA and again for the loop-carried register copies: one L2
+  // round trip per K-step, 17 us for the 16-block 32 -> 64 layer's 8 K-steps per wave.  NKC == 0:
+  // the runtime loop, for long K (many rows, MT == 4).
+  constexpr int PF = NKC > 0 ? (NKC < 8 ? NKC : 8) : 4;
   f32x4 xa0[PF], xa1[PF];  // A: 8 fp32 channels of one gathered voxel
   bf16x8_k bb[PF][NT];     // B fragments
-  auto load = [&](int ks, int sl) {
+  const int nk = ks0 < KS ? (KS - ks0 + kstep - 1) / kstep : 0;  // this wave's K-steps (wave-uniform)
+  auto load = [&](int q, int sl) {
+    const bool live = q < nk;
+    const int ks = ks0 + min(q, max(nk - 1, 0)) * kstep;
     const int k0 = ks * 32 + 8 * g;
     const int j = k0 >> a.cin_log2, a0 = k0 & (a.cin - 1);
     const int iz = bz + tq[0][j], iy = by + tq[1][j], ix = bx + tq[2][j];
-    const bool ok = rok && (unsigned)iz < (unsigned)a.di && (unsigned)iy < (unsigned)a.hi && (unsigned)ix < (unsigned)a.wi;
-    // 32-bit element offsets (sk_launch checks the sizes)
+    const bool ok = live && rok && (unsigned)iz < (unsigned)a.di && (unsigned)iy < (unsigned)a.hi &&
+                    (unsigned)ix < (unsigned)a.wi;
+    // 32-bit element offsets (sk_launch checks the sizes); a dead operand reads element 0
     const float* src = x + (ok ? ((((nb * a.di + iz) * a.hi + iy) * a.wi + ix) << a.cin_log2) + a0 : 0);
-    xa0[sl] = ok ? *reinterpret_cast<const f32x4*>(src) : f32x4{0.f, 0.f, 0.f, 0.f};
-    xa1[sl] = ok ? *reinterpret_cast<const f32x4*>(src + 4) : f32x4{0.f, 0.f, 0.f, 0.f};
+    const f32x4 v0 = *reinterpret_cast<const f32x4*>(src), v1 = *reinterpret_cast<const f32x4*>(src + 4);
+    const f32x4 zero = {0.f, 0.f, 0.f, 0.f};
+    xa0[sl] = ok ? v0 : zero;
+    xa1[sl] = ok ? v1 : zero;
     const int wk = tlin[j] * a.cin + a0;
 #pragma unroll
-    for (int t = 0; t < NT; ++t) {
-      const int col = t * 16 + r16;
-      bb[sl][t] = col < a.cout ? *reinterpret_cast<const bf16x8_k*>(wp + col * a.ktot + wk)
-                               : bf16x8_k{0, 0, 0, 0, 0, 0, 0, 0};
-    }
+    for (int t = 0; t < NT; ++t)  // cout % 16 == 0 (sk_format_ok): every column is in range
+      bb[sl][t] = *reinterpret_cast<const bf16x8_k*>(wp + (t * 16 + r16) * a.ktot + wk);
   };
-  const int nk = ks0 < KS ? (KS - ks0 + kstep - 1) / kstep : 0;  // this wave's K-steps
+  auto step = [&](int sl) {
+    bf16x8_k av;
+    av[0] = (__bf16)xa0[sl][0]; av[1] = (__bf16)xa0[sl][1]; av[2] = (__bf16)xa0[sl][2]; av[3] = (__bf16)xa0[sl][3];
+    av[4] = (__bf16)xa1[sl][0]; av[5] = (__bf16)xa1[sl][1]; av[6] = (__bf16)xa1[sl][2]; av[7] = (__bf16)xa1[sl][3];
 #pragma unroll
-  for (int i = 0; i < PF; ++i)
-    if (i < nk) load(ks0 + i * kstep, i);
-  for (int q0 = 0; q0 < nk; q0 += PF) {
+    for (int t = 0; t < NT; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bb[sl][t], av, acc[t], 0, 0, 0);
+  };
 #pragma unroll
-    for (int i = 0; i < PF; ++i) {
-      const int q = q0 + i;
-      if (q < nk) {
-        bf16x8_k av;
-        av[0] = (__bf16)xa0[i][0]; av[1] = (__bf16)xa0[i][1]; av[2] = (__bf16)xa0[i][2]; av[3] = (__bf16)xa0[i][3];
-        av[4] = (__bf16)xa1[i][0]; av[5] = (__bf16)xa1[i][1]; av[6] = (__bf16)xa1[i][2]; av[7] = (__bf16)xa1[i][3];
-        bf16x8_k bv[NT];
+  for (int i = 0; i < PF; ++i) load(i, i);
+  if constexpr (NKC > 0) {
 #pragma unroll
-        for (int t = 0; t < NT; ++t) bv[t] = bb[i][t];
-        if (q + PF < nk) load(ks0 + (q + PF) * kstep, i);
+    for (int q = 0; q < NKC; ++q) {
+      step(q % PF);
+      if (q + PF < NKC) load(q + PF, q % PF);  // compile-time condition
+    }
+  } else {
+    for (int q0 = 0; q0 < nk; q0 += PF) {
 #pragma unroll
-        for (int t = 0; t < NT; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bv[t], av, acc[t], 0, 0, 0);
+      for (int i = 0; i < PF; ++i) {
+        step(i);
+        load(q0 + i + PF, i);
       }
     }
   }
@@ -221,7 +234,7 @@ __global__ __launch_bounds__(64 * W) void conv_sk_kernel(SkArgs a, const float* 
 
 // geometry (ignoring the weight format): the critic's k4 convs, bf16
 bool sk_format_ok(const cgan3d_conv_geom* g) {
-  if (g->prec != CGAN3D_PREC_BF16 || g->reflect || g->k != 4 || g->cin % 8 || g->cout % 8 || g->cout > 64) return false;
+  if (g->prec != CGAN3D_PREC_BF16 || g->reflect || g->k != 4 || g->cin % 8 || g->cout % 16 || g->cout > 64) return false;
   if (g->cin & (g->cin - 1)) return false;  // power of two: shift / mask index math
   if ((long long)g->n * g->di * g->hi * g->wi * g->cin >= (1LL << 31) ||
       (long long)g->n * g->do_ * g->ho * g->wo * g->cout >= (1LL << 31))
@@ -271,21 +284,35 @@ int sk_launch(const cgan3d_conv_geom* g, const float* x, const __bf16* wp, float
   SkArgs a = sk_args(g, &mt);
   const int nt = (g->cout + 15) / 16;
   const dim3 grid((unsigned)(a.nclass * a.mblocks));
-#define CG_SK(M, N) ::cg::launch((conv_sk_kernel<M, N>), grid, dim3(256), 0, st, a, x, wp, y, e)
-#define CG_SK16(N) ::cg::launch((conv_sk_kernel<1, N, 8>), grid, dim3(512), 0, st, a, x, wp, y, e)
+  // K-steps per wave, as a compile-time trip count where it is short (every parity class has the
+  // same tap count here: k % s == 0)
+  const int kd = g->transposed ? g->k / g->stride : g->k;
+  const int KS = kd * kd * kd * g->cin / 32;
+  const bool wide = mt == 1 && grid.x < 128 && !e.stats;
+  const int w = wide ? 8 : 4;
+  const int nk = mt == 1 ? (KS + w - 1) / w : KS;
+  const int nkc = nk <= 4 ? 4 : nk <= 8 ? 8 : nk <= 16 ? 16 : 0;
+  auto go = [&](auto mt_c, auto w_c) {
+    constexpr int M = decltype(mt_c)::value, W = decltype(w_c)::value;
+    auto by_nt = [&](auto nkc_c) {
+      constexpr int K = decltype(nkc_c)::value;
+      const dim3 block(64 * W);
+      if (nt == 1) ::cg::launch((conv_sk_kernel<M, 1, W, K>), grid, block, 0, st, a, x, wp, y, e);
+      else if (nt == 2) ::cg::launch((conv_sk_kernel<M, 2, W, K>), grid, block, 0, st, a, x, wp, y, e);
+      else if (nt == 3) ::cg::launch((conv_sk_kernel<M, 3, W, K>), grid, block, 0, st, a, x, wp, y, e);
+      else ::cg::launch((conv_sk_kernel<M, 4, W, K>), grid, block, 0, st, a, x, wp, y, e);
+    };
+    if (nkc == 4) by_nt(std::integral_constant<int, 4>{});
+    else if (nkc == 8) by_nt(std::integral_constant<int, 8>{});
+    else if (nkc == 16) by_nt(std::integral_constant<int, 16>{});
+    else by_nt(std::integral_constant<int, 0>{});
+  };
   // very few row tiles with a long K (the 32 -> 64 layer at 4 samples: 16 blocks x 64 K-steps):
   // 8 waves per block split K, half the serial K-steps per wave
   // (A/B at 64^3 B=4: 1.602 vs 1.609 ms/step with 4 waves)
-  const bool wide = mt == 1 && grid.x < 128 && !e.stats;
-  if (wide) {
-    if (nt == 1) CG_SK16(1); else if (nt == 2) CG_SK16(2); else if (nt == 3) CG_SK16(3); else CG_SK16(4);
-  } else if (mt == 1) {
-    if (nt == 1) CG_SK(1, 1); else if (nt == 2) CG_SK(1, 2); else if (nt == 3) CG_SK(1, 3); else CG_SK(1, 4);
-  } else {
-    if (nt == 1) CG_SK(4, 1); else if (nt == 2) CG_SK(4, 2); else if (nt == 3) CG_SK(4, 3); else CG_SK(4, 4);
-  }
-#undef CG_SK
-#undef CG_SK16
+  if (wide) go(std::integral_constant<int, 1>{}, std::integral_constant<int, 8>{});
+  else if (mt == 1) go(std::integral_constant<int, 1>{}, std::integral_constant<int, 4>{});
+  else go(std::integral_constant<int, 4>{}, std::integral_constant<int, 4>{});
   return CGAN3D_OK;
 }
 

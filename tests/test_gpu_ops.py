@@ -546,6 +546,7 @@ SK_CASES = [
     (32, 64, (8, 8, 8)),
     (8, 16, (10, 12, 14)),  # partial 16-row tiles
     (8, 16, (32, 32, 48)),  # >= 1024 row tiles: one tile per wave (statistics rows per wave)
+    (16, 32, (32, 32, 48)),  # one tile per wave with K = 32 steps: the runtime-trip-count K loop
 ]
 
 

@@ -3,7 +3,7 @@
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
-timeout -k 10 300 python -u -m pytest tests/test_gpu_ops.py -k "k3m or halo" -q --timeout 120 --timeout-method thread > gpurun_out/k3m_ops.log 2>&1 || { echo "ops rc=$?" >> gpurun_out/k3m_ops.log; exit 1; }
+timeout -k 10 300 python -u -m pytest tests/test_gpu_ops.py -k "k3m or halo or conv_sk" -q --timeout 120 --timeout-method thread > gpurun_out/k3m_ops.log 2>&1 || { echo "ops rc=$?" >> gpurun_out/k3m_ops.log; exit 1; }
 timeout -k 10 400 python -u -m pytest tests/test_gpu_step.py tests/test_gpu_configs.py -q --timeout 200 --timeout-method thread > gpurun_out/k3m_step.log 2>&1; echo "step rc=$?" >> gpurun_out/k3m_step.log
 timeout -k 10 200 python -u bench.py --no-sub --no-cpu-baseline > gpurun_out/k3m_bench.json 2> gpurun_out/k3m_bench.err || exit $?
 cd /tmp && export TMPDIR=/tmp
