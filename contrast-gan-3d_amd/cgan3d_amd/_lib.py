@@ -70,7 +70,8 @@ class Epilogue(C.Structure):
                 ("act", C.c_int32), ("slope", C.c_float),
                 ("bn_part", C.c_void_p), ("bn_mode", C.c_int32), ("bn_slots", C.c_int32), ("bn_z", C.c_void_p),
                 ("bn_ss", C.c_void_p), ("bn_mi", C.c_void_p), ("bn_act", C.c_int32), ("bn_slope", C.c_float),
-                ("x_bf16", C.c_void_p), ("bn_fold", C.c_int32), ("fuse", C.POINTER(BnFuse))]
+                ("x_bf16", C.c_void_p), ("bn_fold", C.c_int32), ("fuse", C.POINTER(BnFuse)),
+                ("out_bf16", C.c_int32)]
 
 
 _P, _I32, _I64, _F = C.c_void_p, C.c_int32, C.c_int64, C.c_float
@@ -105,11 +106,12 @@ _SIGS = {
                                 _I32),
     "cgan3d_bn_backward_ws_floats": ([_I64, _I32], _I64),
     "cgan3d_bn_apply_acc": ([_P, _I32, _I32, _I64, _P, _P, _P, _P, _P, _F, _F, _P, _P, _P, _I32, _F, _P, _P, _P, _P,
-                             _I32, _P], _I32),
+                             _I32, _I32, _P], _I32),
     "cgan3d_bn_backward_acc_fold": ([_P, _P, _I32, _I32, _I32, _I32, _I32, _I32, _P, _I32, _P, _P, _P, _I32, _F, _P,
-                                     _P, _P, _I32, _P, _P, _I32, _P], _I32),
+                                     _P, _P, _I32, _P, _P, _I32, _I32, _P], _I32),
     "cgan3d_bn_backward_acc": ([_P, _P, _I64, _I32, _P, _I32, _P, _P, _P, _I32, _F, _P, _P, _P, _I32, _P, _P, _I32,
-                                _P], _I32),
+                                _I32, _P], _I32),
+    "cgan3d_conv3d_out_bf16_ok": ([_P], _I32),
     "cgan3d_bn_backward_slab_fold": ([_P, _P, _I32, _I32, _I32, _I32, _I32, _I32, _P, _I32, _P, _P, _P, _I32, _F, _P,
                                       _P, _P, _I32, _P, _P, _P], _I32),
     "cgan3d_bn_backward": ([_P, _P, _I64, _I32, _P, _P, _P, _I32, _F, _P, _P, _P, _I32, _P, _P], _I32),

@@ -44,7 +44,8 @@ Dims = Tuple[int, int, int]
 #                              slabs + finalize launches instead of fp64 accumulators), no_bn_fold
 #                              (reflect-fold pass before the last BatchNorm backward), serial (no side
 #                              streams: a kernel trace then shows unshared durations), system_fence
-#                              (cross-stream event records with the system-scope fence, csrc/plan.hip)
+#                              (cross-stream event records with the system-scope fence, csrc/plan.hip),
+#                              fp32_store (the 64^3 16-channel z / dy in fp32 instead of bf16)
 #   CGAN3D_FORCE_DP=1          the data-parallel path over a one-rank group (tools / tests)
 #   CGAN3D_COMM=native|torch|own   data-parallel collectives: RCCL from the launch plan on the process
 #                              group's communicator (default), torch.distributed host callables (the
@@ -52,7 +53,7 @@ Dims = Tuple[int, int, int]
 #   CGAN3D_G_BUCKET_BYTES      generator gradient bucket size under data parallelism
 #   CGAN3D_TUNE, CGAN3D_LIB_PATH   launch-shape knobs, another build of the library (_lib.py)
 #   CGAN3D_TRAINER_PLANS=0     the drop-in Trainer issues every step eagerly (no recorded plans)
-DEBUG_FLAGS = ("no_shadow", "keep_fp32", "no_bn_fuse", "no_bn_fold", "serial", "system_fence")
+DEBUG_FLAGS = ("no_shadow", "keep_fp32", "no_bn_fuse", "no_bn_fold", "serial", "system_fence", "fp32_store")
 
 
 def debug(flag: str) -> bool:
@@ -337,6 +338,25 @@ class GeneratorPlan:
         bo = [j for j in range(nl - 1, -1, -1) if self.ac_b[j]]  # (backward)
         self.acc_zero_f = {j: self.acc_f[fo[k - 1]] for k, j in enumerate(fo)}
         self.acc_zero_b = {j: self.acc_b[bo[k - 1]] for k, j in enumerate(bo)}
+        # bf16 storage of BatchNorm inputs and their gradients (round 4): a layer whose conv output z,
+        # and the dL/dy the next layer's input-grad writes, are only read by kernels that take bf16
+        # (cgan3d_conv3d_out_bf16_ok for both producers; the accumulator BatchNorm passes) keeps them in
+        # bf16 in training mode: at 64^3 the first and the last 16-channel layers (z, dy / the last
+        # conv's padded input-grad: 67-88 MB fp32 tensors read 2-3 times each).  The statistics still
+        # come from the producers' fp32 values.  zs / dys / dpads name the training-mode storage; z / dy
+        # / dpad stay fp32 (eval forward, slab paths).  CGAN3D_DEBUG=fp32_store keeps fp32 (A/B).
+        self.z16 = [False] * nl
+        if any(self.ac_f) and any(self.ac_b) and not debug("fp32_store"):
+            for j in range(nl):
+                prod = self.geo_last_dgrad if j == nl - 1 else self.geo_dgrad[j + 1]
+                # the stride-2 producers write bf16 only when they stage from their input's shadow
+                shadows = (j == 0 or self.y16[j - 1] is not None) and (j == nl - 1 or self.dz16[j + 1] is not None)
+                self.z16[j] = bool(self.ac_f[j] and self.ac_b[j] and ops.out_bf16_ok(self.geo_fwd[j])
+                                   and ops.out_bf16_ok(prod) and (j < nl - 1 or self.fold_bn) and shadows)
+        self.zs = [bf(ly.dout, ly.cout) if f else z for ly, f, z in zip(layers, self.z16, self.z)]
+        self.dys = [bf(ly.dout, ly.cout) if f and j < nl - 1 else d
+                    for j, (ly, f, d) in enumerate(zip(layers, self.z16, self.dy))]
+        self.dpads = bf(pd, la.cin) if self.z16[-1] else self.dpad
         # weight gradients run on a side stream, beside the input-gradient chain (each wgrad only
         # needs its layer's dz and input, both final when it is enqueued); own workspace
         wsw = max([ops.wgrad_ws_floats(gw) for gw in self.geo_wgrad] + [ops.wgrad_ws_floats(self.geo_last_wgrad)])
@@ -389,11 +409,11 @@ class GeneratorPlan:
                     ep = ops.epilogue(x_bf16=h16, fuse=ops.BnFuse(self.acc_f[i], 3, FUSE_REPS))
                 else:
                     ep = ops.epilogue(bn_part=self.part_f[i], bn_mode=1, bn_slots=self.slots_f[i], x_bf16=h16)
-                ops.conv(self.geo_fwd[i], h, self.wf[i], self.z[i], ep)
+                ops.conv(self.geo_fwd[i], h, self.wf[i], self.zs[i], ep)
                 if self.ac_f[i]:
                     ops.bn_apply_acc(self.acc_f[i], FUSE_REPS, ly.cout, nvox, P[f"{nb}.weight"], P[f"{nb}.bias"],
                                      P[f"{nb}.running_mean"], P[f"{nb}.running_var"], P[f"{nb}.num_batches_tracked"],
-                                     self.ss[i], self.mi[i], self.z[i], ly.act, None if self.y_dead[i] else self.y[i],
+                                     self.ss[i], self.mi[i], self.zs[i], ly.act, None if self.y_dead[i] else self.y[i],
                                      residual=res, y16=self.y16[i], zero=self.acc_zero_f[i])
                 else:
                     ops.bn_apply_slab(self.part_f[i], self.slots_f[i], ly.cout, nvox, P[f"{nb}.weight"],
@@ -417,7 +437,7 @@ class GeneratorPlan:
         if not BN_FUSED_BWD:
             return ops.epilogue()
         if fused:
-            return ops.epilogue(bn_z=self.z[i], bn_ss=self.ss[i], bn_mi=self.mi[i], bn_act=self.layers[i].act,
+            return ops.epilogue(bn_z=self.zs[i], bn_ss=self.ss[i], bn_mi=self.mi[i], bn_act=self.layers[i].act,
                                 fuse=ops.BnFuse(self.acc_b[i], 4, FUSE_REPS))
         return ops.epilogue(bn_part=self.part_b[i], bn_mode=2, bn_slots=self.slots_b[i], bn_z=self.z[i],
                             bn_ss=self.ss[i], bn_mi=self.mi[i], bn_act=self.layers[i].act)
@@ -480,7 +500,7 @@ class GeneratorPlan:
         if self.fold_bn:
             ep = self._bn_grad_epi(len(self.layers) - 1, fused=self.ac_b[-1])
             ep.bn_fold = la.p
-            ops.conv(self.geo_last_dgrad, self.dz_last, P["model.last_conv.weight"], self.dpad, ep)
+            ops.conv(self.geo_last_dgrad, self.dz_last, P["model.last_conv.weight"], self.dpads, ep)
         else:
             ops.conv(self.geo_last_dgrad, self.dz_last, P["model.last_conv.weight"], self.dpad)
             ops.reflect_fold(self.dpad, self.dy[-1], n, la.din, la.cin, la.p,
@@ -493,12 +513,12 @@ class GeneratorPlan:
             nb = f"{ly.name}.normalization"
             nvox = n * ly.dout[0] * ly.dout[1] * ly.dout[2]
             if self.ac_b[i] and self.fold_bn and i == len(self.layers) - 1:
-                ops.bn_backward_acc_fold(self.dpad, self.z[i], n, ly.dout, ly.cout, la.p, self.acc_b[i], FUSE_REPS,
+                ops.bn_backward_acc_fold(self.dpads, self.zs[i], n, ly.dout, ly.cout, la.p, self.acc_b[i], FUSE_REPS,
                                          self.ss[i], self.mi[i], P[f"{nb}.weight"], ly.act, G[f"{nb}.weight"],
                                          G[f"{nb}.bias"], None if self.dz_dead[i] else self.dz[i], dz16=self.dz16[i],
                                          zero=self.acc_zero_b[i])
             elif self.ac_b[i]:
-                ops.bn_backward_acc(self.dy[i], self.z[i], nvox, ly.cout, self.acc_b[i], FUSE_REPS, self.ss[i], self.mi[i],
+                ops.bn_backward_acc(self.dys[i], self.zs[i], nvox, ly.cout, self.acc_b[i], FUSE_REPS, self.ss[i], self.mi[i],
                                     P[f"{nb}.weight"], ly.act, G[f"{nb}.weight"], G[f"{nb}.bias"],
                                     None if self.dz_dead[i] else self.dz[i], dz16=self.dz16[i], zero=self.acc_zero_b[i])
             elif BN_FUSED_BWD and self.fold_bn and i == len(self.layers) - 1:
@@ -569,7 +589,7 @@ class GeneratorPlan:
         ep = self._bn_grad_epi(i - 1, fused=self.ac_b[i - 1])
         ep.residual = self.dy[i + 1] if ly.name.endswith("block0") else None
         ep.x_bf16 = self.dz16[i] if BN_FUSED_BWD else None  # only the slab backward writes it
-        ops.conv(self.geo_dgrad[i], self.dz[i], self.wd[i], self.dy[i - 1], ep)
+        ops.conv(self.geo_dgrad[i], self.dz[i], self.wd[i], self.dys[i - 1], ep)
 
 
 def _running_scale_shift(P, nb, ss):

@@ -212,6 +212,11 @@ class BnFuse:
         return f
 
 
+def out_bf16_ok(g) -> bool:
+    """cgan3d_conv3d_out_bf16_ok: the launch of ``g`` can write a bf16 output (and read a bf16 bn_z)."""
+    return bool(L.load().cgan3d_conv3d_out_bf16_ok(ctypes.byref(g)))
+
+
 def neg_dtanh_ok(g) -> bool:
     """cgan3d_conv3d_neg_dtanh_ok: the input-grad geometry takes the L.ACT_NEG_DTANH epilogue."""
     return bool(L.load().cgan3d_conv3d_neg_dtanh_ok(ctypes.byref(g)))
@@ -238,6 +243,7 @@ class Epi:
         self.bn_z, self.bn_ss, self.bn_mi = bn_z, bn_ss, bn_mi
         self.bn_act, self.bn_slope = bn_act, float(bn_slope)
         self.bn_fold = int(bn_fold)  # mode 2 over a reflect-padded k7 input-grad grid (include/cgan3d.h)
+        self.out_bf16 = 0  # set by conv() from the output's dtype (include/cgan3d.h out_bf16)
 
     def check_bn(self, nout, c, what, nz=None):
         if not self.bn_mode:
@@ -257,6 +263,7 @@ class Epi:
         e.bn_ss, e.bn_mi, e.bn_act, e.bn_slope = ptr(self.bn_ss), ptr(self.bn_mi), self.bn_act, self.bn_slope
         e.x_bf16 = ptr(self.x_bf16)
         e.bn_fold = self.bn_fold
+        e.out_bf16 = self.out_bf16
         if self.fuse is not None:
             e.fuse = ctypes.pointer(self.fuse.c())  # the pointer object keeps the struct alive
         return e
@@ -483,7 +490,14 @@ def conv(g: ConvGeom, x: torch.Tensor, w: torch.Tensor, y: torch.Tensor, ep: Opt
     else:
         _need(w, _w_extent(g), "conv w", exact=False)
     ny = _vox_out(g) * g.cout
-    _need(y, ny, "conv y")
+    out16 = y is not None and y.dtype == torch.bfloat16
+    if out16:  # the generator's 64^3 16-channel tensors kept in bf16 (include/cgan3d.h out_bf16)
+        if ep is None or not out_bf16_ok(g):
+            raise ValueError("conv: a bf16 output only where cgan3d_conv3d_out_bf16_ok (with an epilogue)")
+        ep.out_bf16 = 1
+    elif ep is not None:
+        ep.out_bf16 = 0
+    _need(y, ny, "conv y", dtype=y.dtype if out16 else torch.float32)
     if ep is not None:
         if ep.bias is not None:
             _need(ep.bias, g.cout, "conv bias")
@@ -499,6 +513,10 @@ def conv(g: ConvGeom, x: torch.Tensor, w: torch.Tensor, y: torch.Tensor, ep: Opt
         ep.check_bn(ny, g.cout, "conv", nz)
         if ep.fuse is not None:
             ep.fuse.check(g, "conv")
+            if ep.fuse.acc_mode == 4:  # the statistics read z at every output (folded: the unpadded grid)
+                _need(ep.bn_z, ny if nz is None else nz, "conv bn_z", dtype=y.dtype)
+        elif out16 and ep.bn_z is not None:
+            raise ValueError("conv: a bf16 output takes accumulator statistics only")
     check(_timed("conv", g, "cgan3d_conv3d_fwd", ctypes.byref(g), ptr(x), ptr(w), ptr(y),
                  ctypes.byref(ep.c()) if ep is not None else None), "conv3d_fwd")
 
@@ -710,7 +728,8 @@ def bn_apply_acc(acc, reps, c, nvox, gamma, beta, rmean, rvar, nbt, scale_shift,
         _need(t, c, f"bn_apply_acc {nm}")
     for t, nm in ((scale_shift, "scale_shift"), (mean_invstd, "mean_invstd")):
         _need(t, 2 * c, f"bn_apply_acc {nm}")
-    _need(z, nvox * c, "bn_apply_acc z")
+    z16 = z.dtype == torch.bfloat16  # z kept in bf16 by its producer (include/cgan3d.h in_bf16)
+    _need(z, nvox * c, "bn_apply_acc z", dtype=z.dtype if z16 else torch.float32)
     if y is None and y16 is None:
         raise ValueError("bn_apply_acc: y may be None only when y16 is given")
     for t, nm in ((y, "y"), (residual, "residual")):
@@ -721,7 +740,7 @@ def bn_apply_acc(acc, reps, c, nvox, gamma, beta, rmean, rvar, nbt, scale_shift,
     check(_launch("cgan3d_bn_apply_acc", ptr(acc), reps, c, nvox, ptr(gamma), ptr(beta), ptr(rmean), ptr(rvar),
                   ptr(nbt), momentum, eps, ptr(scale_shift), ptr(mean_invstd), ptr(z), act, float(slope),
                   ptr(residual), ptr(y), _need16(y16, nvox * c, "bn_apply_acc y16"), ptr(zero),
-                  zero.numel() if zero is not None else 0), "bn_apply_acc")
+                  zero.numel() if zero is not None else 0, int(z16)), "bn_apply_acc")
 
 
 def bn_backward_acc(dy, z, nvox, c, acc, reps, scale_shift, mean_invstd, gamma, act, dgamma, dbeta, dz, slope=0.0,
@@ -730,9 +749,11 @@ def bn_backward_acc(dy, z, nvox, c, acc, reps, scale_shift, mean_invstd, gamma, 
     (cgan3d_bn_backward_acc: one launch)."""
     if dz is None and dz16 is None:
         raise ValueError("bn_backward_acc: dz may be None only when dz16 is given")
-    for t, nm in ((dy, "dy"), (z, "z"), (dz, "dz")):
-        if t is not None:
-            _need(t, nvox * c, f"bn_backward_acc {nm}")
+    in16 = dy.dtype == torch.bfloat16  # dy and z kept in bf16 by their producers (include/cgan3d.h in_bf16)
+    for t, nm in ((dy, "dy"), (z, "z")):
+        _need(t, nvox * c, f"bn_backward_acc {nm}", dtype=torch.bfloat16 if in16 else torch.float32)
+    if dz is not None:
+        _need(dz, nvox * c, "bn_backward_acc dz")
     _need(acc, reps * 2 * c, "bn_backward_acc acc", dtype=torch.float64, exact=False)
     for t, nm in ((scale_shift, "scale_shift"), (mean_invstd, "mean_invstd")):
         _need(t, 2 * c, f"bn_backward_acc {nm}")
@@ -742,8 +763,8 @@ def bn_backward_acc(dy, z, nvox, c, acc, reps, scale_shift, mean_invstd, gamma, 
         _need(zero, zero.numel(), "bn_backward_acc zero", dtype=torch.float64)
     check(_launch("cgan3d_bn_backward_acc", ptr(dy), ptr(z), nvox, c, ptr(acc), reps, ptr(scale_shift),
                   ptr(mean_invstd), ptr(gamma), act, slope, ptr(dgamma), ptr(dbeta), ptr(dz), int(accumulate),
-                  _need16(dz16, nvox * c, "bn_backward_acc dz16"), ptr(zero), zero.numel() if zero is not None else 0),
-          "bn_backward_acc")
+                  _need16(dz16, nvox * c, "bn_backward_acc dz16"), ptr(zero), zero.numel() if zero is not None else 0,
+                  int(in16)), "bn_backward_acc")
 
 
 def bn_backward_acc_fold(padded, z, n, dims: Sequence[int], c, pad, acc, reps, scale_shift, mean_invstd, gamma,
@@ -752,12 +773,14 @@ def bn_backward_acc_fold(padded, z, n, dims: Sequence[int], c, pad, acc, reps, s
     input-grad launch (cgan3d_bn_backward_acc_fold: one launch)."""
     d, h, w = dims
     nvox = n * d * h * w
-    _need(padded, n * (d + 2 * pad) * (h + 2 * pad) * (w + 2 * pad) * c, "bn_backward_acc_fold padded")
+    in16 = padded.dtype == torch.bfloat16  # padded and z kept in bf16 (include/cgan3d.h in_bf16)
+    dt = torch.bfloat16 if in16 else torch.float32
+    _need(padded, n * (d + 2 * pad) * (h + 2 * pad) * (w + 2 * pad) * c, "bn_backward_acc_fold padded", dtype=dt)
     if dz is None and dz16 is None:
         raise ValueError("bn_backward_acc_fold: dz may be None only when dz16 is given")
-    for t, nm in ((z, "z"), (dz, "dz")):
-        if t is not None:
-            _need(t, nvox * c, f"bn_backward_acc_fold {nm}")
+    _need(z, nvox * c, "bn_backward_acc_fold z", dtype=dt)
+    if dz is not None:
+        _need(dz, nvox * c, "bn_backward_acc_fold dz")
     _need(acc, reps * 2 * c, "bn_backward_acc_fold acc", dtype=torch.float64, exact=False)
     for t, nm in ((scale_shift, "scale_shift"), (mean_invstd, "mean_invstd")):
         _need(t, 2 * c, f"bn_backward_acc_fold {nm}")
@@ -768,7 +791,7 @@ def bn_backward_acc_fold(padded, z, n, dims: Sequence[int], c, pad, acc, reps, s
     check(_launch("cgan3d_bn_backward_acc_fold", ptr(padded), ptr(z), n, d, h, w, c, pad, ptr(acc), reps,
                   ptr(scale_shift), ptr(mean_invstd), ptr(gamma), act, slope, ptr(dgamma), ptr(dbeta), ptr(dz),
                   int(accumulate), _need16(dz16, nvox * c, "bn_backward_acc_fold dz16"), ptr(zero),
-                  zero.numel() if zero is not None else 0), "bn_backward_acc_fold")
+                  zero.numel() if zero is not None else 0, int(in16)), "bn_backward_acc_fold")
 
 
 def bn_backward_slab_fold(padded, z, n, dims: Sequence[int], c, pad, part, nslots, scale_shift, mean_invstd, gamma,

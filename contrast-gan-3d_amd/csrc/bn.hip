@@ -83,6 +83,17 @@ __device__ __forceinline__ void store16(__bf16* o16, long long i, f32x4 v) {
   reinterpret_cast<bf16x4_n*>(o16)[i] = h;
 }
 
+// float4 i of a tensor kept in fp32 or (B16, round 4: the generator's 64^3 16-channel tensors) in bf16
+template <bool B16>
+__device__ __forceinline__ f32x4 load4(const void* __restrict__ p, long long i) {
+  if constexpr (B16) {
+    const bf16x4_n h = reinterpret_cast<const bf16x4_n*>(p)[i];
+    return f32x4{(float)h[0], (float)h[1], (float)h[2], (float)h[3]};
+  } else {
+    return reinterpret_cast<const f32x4*>(p)[i];
+  }
+}
+
 // y = act(z*scale + shift) (+ residual); C % 4 == 0, float4 vectorised grid-stride.  With
 // 256 % (C/4) == 0 the grid stride is a multiple of C/4, so a thread keeps its 4 channels (and
 // their scale/shift in registers) for the whole loop.
@@ -215,8 +226,9 @@ __device__ __forceinline__ void acc_sums(const double* __restrict__ acc, int rep
 
 // coef == NULL: the coefficients from fp64 accumulators (cgan3d_bn_backward_acc_fold): every block
 // combines the replicas, block 0 publishes dgamma / dbeta and zeroes `zero`
-__global__ __launch_bounds__(256) void bn_bwd_apply_fold_kernel(const float* __restrict__ padded,
-                                                                const float* __restrict__ z, int n, int D, int H, int W,
+template <bool B16>  // padded and z in bf16
+__global__ __launch_bounds__(256) void bn_bwd_apply_fold_kernel(const void* __restrict__ padded,
+                                                                const void* __restrict__ z, int n, int D, int H, int W,
                                                                 int P, int C, const float* __restrict__ ss,
                                                                 const float* __restrict__ mi, int act, float slope,
                                                                 const float* __restrict__ coef, float* dz,
@@ -254,8 +266,6 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_fold_kernel(const float* __r
   }
   const int Dp = D + 2 * P, Hp = H + 2 * P, Wp = W + 2 * P;
   const long long n4 = (long long)n * D * H * W * C4;
-  const f32x4* z4 = reinterpret_cast<const f32x4*>(z);
-  const f32x4* p4 = reinterpret_cast<const f32x4*>(padded);
   f32x4* o4 = reinterpret_cast<f32x4*>(dz);
   // 32-bit index math: C/4 a power of two (C divides 256), the padded volume below 2^31 float4
   // (checked by the callers); four 64-bit divides per float4 made this pass VALU-bound
@@ -267,13 +277,13 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_fold_kernel(const float* __r
     const int w = (int)(v0 - v1 * W), h = (int)(v1 - v2 * H), d = (int)(v2 - v3 * D), nb = (int)v3;
     int qd[2], qh[2], qw[2];
     const int nd = fold_src(d, D, P, qd), nh = fold_src(h, H, P, qh), nw = fold_src(w, W, P, qw);
-    const f32x4 zz = z4[i];
-    f32x4 dd = p4[((((nb * Dp + qd[0]) * Hp + qh[0]) * Wp + qw[0]) << c4s) + c4];
+    const f32x4 zz = load4<B16>(z, i);
+    f32x4 dd = load4<B16>(padded, ((((nb * Dp + qd[0]) * Hp + qh[0]) * Wp + qw[0]) << c4s) + c4);
     if (nd * nh * nw > 1) {  // boundary voxel: its mirrored sources
       for (int a = 0; a < nd; ++a)
         for (int b = 0; b < nh; ++b)
           for (int e = 0; e < nw; ++e)
-            if (a | b | e) dd += p4[((((nb * Dp + qd[a]) * Hp + qh[b]) * Wp + qw[e]) << c4s) + c4];
+            if (a | b | e) dd += load4<B16>(padded, ((((nb * Dp + qd[a]) * Hp + qh[b]) * Wp + qw[e]) << c4s) + c4);
     }
     f32x4 o;
 #pragma unroll
@@ -639,12 +649,13 @@ __device__ __forceinline__ void acc_sums(const double* __restrict__ acc, int rep
 // float4 per thread loaded before the statistics are known (acc_pass_blocks sizes the grid at ~2)
 constexpr int ACC_PF = 2;
 
-template <bool RES>  // residual added: a load under `if (res)` made the compiler wait for every load in flight
+// RES: residual added (a load under `if (res)` made the compiler wait for every load in flight); Z16: z in bf16
+template <bool RES, bool Z16>
 __global__ __launch_bounds__(256) void bn_apply_acc_kernel(const double* __restrict__ acc, int reps, int C, double nvox,
                                                            const float* gamma, const float* beta, float* rmean,
                                                            float* rvar, long long* nbt, float momentum, float eps,
                                                            float* scale_shift, float* mean_invstd,
-                                                           const float* __restrict__ z, long long n4, int act,
+                                                           const void* __restrict__ z, long long n4, int act,
                                                            float slope, const float* __restrict__ res,
                                                            float* __restrict__ y, __bf16* __restrict__ y16,
                                                            double* zero, int zero_n) {
@@ -654,7 +665,6 @@ __global__ __launch_bounds__(256) void bn_apply_acc_kernel(const double* __restr
   if (blockIdx.x == 0)
     for (int j = tid; j < zero_n; j += blockDim.x) zero[j] = 0.0;
   // the first ACC_PF float4 of this thread's elementwise range are loaded while the replicas are in flight
-  const f32x4* z4 = reinterpret_cast<const f32x4*>(z);
   const f32x4* r4 = reinterpret_cast<const f32x4*>(res);
   const long long i0 = (long long)blockIdx.x * blockDim.x + tid, stride = (long long)gridDim.x * blockDim.x;
   f32x4 zp[ACC_PF], rp[ACC_PF];
@@ -662,7 +672,7 @@ __global__ __launch_bounds__(256) void bn_apply_acc_kernel(const double* __restr
 #pragma unroll
     for (int u = 0; u < ACC_PF; ++u) {
       const long long i = min(i0 + u * stride, n4 - 1);
-      zp[u] = z4[i];
+      zp[u] = load4<Z16>(z, i);
       if (RES) rp[u] = r4[i];
     }
   });
@@ -699,15 +709,16 @@ __global__ __launch_bounds__(256) void bn_apply_acc_kernel(const double* __restr
 #pragma unroll
   for (int u = 0; u < ACC_PF; ++u)
     if (i0 + u * stride < n4) apply(i0 + u * stride, zp[u], rp[u]);
-  for (long long i = i0 + ACC_PF * stride; i < n4; i += stride) apply(i, z4[i], RES ? r4[i] : f32x4{});
+  for (long long i = i0 + ACC_PF * stride; i < n4; i += stride) apply(i, load4<Z16>(z, i), RES ? r4[i] : f32x4{});
 }
 
+template <bool B16>  // dy and z in bf16
 __global__ __launch_bounds__(256) void bn_bwd_apply_acc_kernel(const double* __restrict__ acc, int reps, int C,
                                                                double nvox, const float* __restrict__ gamma,
                                                                const float* __restrict__ mi, float* dgamma,
                                                                float* dbeta, int accumulate,
-                                                               const float* __restrict__ dy,
-                                                               const float* __restrict__ z, long long n4,
+                                                               const void* __restrict__ dy,
+                                                               const void* __restrict__ z, long long n4,
                                                                const float* __restrict__ ss, int act, float slope,
                                                                float* __restrict__ dz, __bf16* __restrict__ dz16,
                                                                double* zero, int zero_n) {
@@ -716,16 +727,14 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_acc_kernel(const double* __r
   const int tid = threadIdx.x;
   if (blockIdx.x == 0)
     for (int j = tid; j < zero_n; j += blockDim.x) zero[j] = 0.0;
-  const f32x4* z4 = reinterpret_cast<const f32x4*>(z);
-  const f32x4* d4 = reinterpret_cast<const f32x4*>(dy);
   const long long i0 = (long long)blockIdx.x * blockDim.x + tid, stride = (long long)gridDim.x * blockDim.x;
   f32x4 zp[ACC_PF], dp[ACC_PF];
   acc_sums(acc, reps, C, sums, [&] {
 #pragma unroll
     for (int u = 0; u < ACC_PF; ++u) {
       const long long i = min(i0 + u * stride, n4 - 1);
-      zp[u] = z4[i];
-      dp[u] = d4[i];
+      zp[u] = load4<B16>(z, i);
+      dp[u] = load4<B16>(dy, i);
     }
   });
   __syncthreads();
@@ -761,7 +770,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_acc_kernel(const double* __r
 #pragma unroll
   for (int u = 0; u < ACC_PF; ++u)
     if (i0 + u * stride < n4) apply(i0 + u * stride, zp[u], dp[u]);
-  for (long long i = i0 + ACC_PF * stride; i < n4; i += stride) apply(i, z4[i], d4[i]);
+  for (long long i = i0 + ACC_PF * stride; i < n4; i += stride) apply(i, load4<B16>(z, i), load4<B16>(dy, i));
 }
 
 // blocks of the accumulator passes: ~2 float4 per thread, at most `cap` blocks — each block reads the
@@ -960,7 +969,7 @@ extern "C" int cgan3d_bn_backward_slab_fold(const float* padded, const float* z,
   CG_LAUNCH_CHECK("bn_bwd_finalize_slab_kernel");
   const long long n4 = nvox * c / 4;
   const int blocks = (int)std::min<long long>((n4 + 255) / 256, 4096);
-  ::cg::launch(bn_bwd_apply_fold_kernel, dim3(blocks), dim3(256), 0, s, padded, z, n, d, h, w, pad, c, scale_shift,
+  ::cg::launch(bn_bwd_apply_fold_kernel<false>, dim3(blocks), dim3(256), 0, s, (const void*)padded, (const void*)z, n, d, h, w, pad, c, scale_shift,
                mean_invstd, act, slope, (const float*)ws, dz, reinterpret_cast<__bf16*>(dz_bf16), (const double*)nullptr, 1,
                0.0, (const float*)nullptr, (float*)nullptr, (float*)nullptr, 0, (double*)nullptr, 0);
   CG_LAUNCH_CHECK("bn_bwd_apply_fold_kernel");
@@ -970,15 +979,18 @@ extern "C" int cgan3d_bn_backward_slab_fold(const float* padded, const float* z,
 extern "C" int cgan3d_bn_apply_acc(const double* acc, int32_t reps, int32_t c, int64_t nvox, const float* gamma,
                                    const float* beta, float* running_mean, float* running_var,
                                    int64_t* num_batches_tracked, float momentum, float eps, float* scale_shift,
-                                   float* mean_invstd, const float* z, int32_t act, float slope, const float* residual,
-                                   float* y, void* y_bf16, double* zero, int32_t zero_n, void* stream) {
+                                   float* mean_invstd, const void* z, int32_t act, float slope, const float* residual,
+                                   float* y, void* y_bf16, double* zero, int32_t zero_n, int32_t in_bf16,
+                                   void* stream) {
   CG_CHECK_ARG(acc && gamma && beta && scale_shift && mean_invstd && z && (y || y_bf16),
                "cgan3d_bn_apply_acc: null pointer");
   CG_CHECK_ARG(reps > 0 && reps <= 64 && nvox > 0 && c >= 4 && c <= 128 && 256 % c == 0 && zero_n >= 0 &&
                    (zero || !zero_n),
                "cgan3d_bn_apply_acc: channels must divide 256 (4..128), reps 1..64");
   const long long n4 = (long long)nvox * c / 4;
-  ::cg::launch(residual ? bn_apply_acc_kernel<true> : bn_apply_acc_kernel<false>, dim3(acc_pass_blocks(n4)), dim3(256),
+  auto* kern = residual ? (in_bf16 ? bn_apply_acc_kernel<true, true> : bn_apply_acc_kernel<true, false>)
+                        : (in_bf16 ? bn_apply_acc_kernel<false, true> : bn_apply_acc_kernel<false, false>);
+  ::cg::launch(kern, dim3(acc_pass_blocks(n4)), dim3(256),
                0, (hipStream_t)stream, acc, (int)reps, (int)c,
                (double)nvox, gamma, beta, running_mean, running_var, (long long*)num_batches_tracked, momentum, eps,
                scale_shift, mean_invstd, z, n4, act, slope, residual, y, reinterpret_cast<__bf16*>(y_bf16), zero,
@@ -987,30 +999,31 @@ extern "C" int cgan3d_bn_apply_acc(const double* acc, int32_t reps, int32_t c, i
   return CGAN3D_OK;
 }
 
-extern "C" int cgan3d_bn_backward_acc(const float* dy, const float* z, int64_t nvox, int32_t c, const double* acc,
+extern "C" int cgan3d_bn_backward_acc(const void* dy, const void* z, int64_t nvox, int32_t c, const double* acc,
                                       int32_t reps, const float* scale_shift, const float* mean_invstd,
                                       const float* gamma, int32_t act, float slope, float* dgamma, float* dbeta,
                                       float* dz, int32_t accumulate, void* dz_bf16, double* zero, int32_t zero_n,
-                                      void* stream) {
+                                      int32_t in_bf16, void* stream) {
   CG_CHECK_ARG(dy && z && acc && scale_shift && mean_invstd && gamma && (dz || dz_bf16),
                "cgan3d_bn_backward_acc: null pointer");
   CG_CHECK_ARG(reps > 0 && reps <= 64 && nvox > 1 && c >= 4 && c <= 128 && 256 % c == 0 && zero_n >= 0 &&
                    (zero || !zero_n),
                "cgan3d_bn_backward_acc: channels must divide 256 (4..128), reps 1..64");
   const long long n4 = (long long)nvox * c / 4;
-  ::cg::launch(bn_bwd_apply_acc_kernel, dim3(acc_pass_blocks(n4)), dim3(256), 0, (hipStream_t)stream, acc, (int)reps,
+  ::cg::launch(in_bf16 ? bn_bwd_apply_acc_kernel<true> : bn_bwd_apply_acc_kernel<false>, dim3(acc_pass_blocks(n4)),
+               dim3(256), 0, (hipStream_t)stream, acc, (int)reps,
                (int)c, (double)nvox, gamma, mean_invstd, dgamma, dbeta, (int)accumulate, dy, z, n4, scale_shift, act,
                slope, dz, reinterpret_cast<__bf16*>(dz_bf16), zero, (int)zero_n);
   CG_LAUNCH_CHECK("bn_bwd_apply_acc_kernel");
   return CGAN3D_OK;
 }
 
-extern "C" int cgan3d_bn_backward_acc_fold(const float* padded, const float* z, int32_t n, int32_t d, int32_t h,
+extern "C" int cgan3d_bn_backward_acc_fold(const void* padded, const void* z, int32_t n, int32_t d, int32_t h,
                                            int32_t w, int32_t c, int32_t pad, const double* acc, int32_t reps,
                                            const float* scale_shift, const float* mean_invstd, const float* gamma,
                                            int32_t act, float slope, float* dgamma, float* dbeta, float* dz,
                                            int32_t accumulate, void* dz_bf16, double* zero, int32_t zero_n,
-                                           void* stream) {
+                                           int32_t in_bf16, void* stream) {
   CG_CHECK_ARG(padded && z && acc && scale_shift && mean_invstd && gamma && (dz || dz_bf16),
                "cgan3d_bn_backward_acc_fold: null pointer");
   CG_CHECK_ARG(n > 0 && reps > 0 && reps <= 64 && c >= 4 && c <= 128 && 256 % c == 0 && pad >= 0 && d > 2 * pad &&
@@ -1021,7 +1034,8 @@ extern "C" int cgan3d_bn_backward_acc_fold(const float* padded, const float* z, 
   CG_CHECK_ARG((long long)n * (d + 2 * pad) * (h + 2 * pad) * (w + 2 * pad) * (c / 4) < (1LL << 31),
                "cgan3d_bn_backward_acc_fold: padded volume exceeds 32-bit float4 indexing");
   const long long n4 = nvox * c / 4;
-  ::cg::launch(bn_bwd_apply_fold_kernel, dim3(acc_pass_blocks(n4, 4096)), dim3(256), 0, (hipStream_t)stream, padded, z, n, d,
+  ::cg::launch(in_bf16 ? bn_bwd_apply_fold_kernel<true> : bn_bwd_apply_fold_kernel<false>, dim3(acc_pass_blocks(n4, 4096)),
+               dim3(256), 0, (hipStream_t)stream, padded, z, n, d,
                h, w, pad, c, scale_shift, mean_invstd, act, slope, (const float*)nullptr, dz,
                reinterpret_cast<__bf16*>(dz_bf16), acc, (int)reps, (double)nvox, gamma, dgamma, dbeta, (int)accumulate,
                zero, (int)zero_n);

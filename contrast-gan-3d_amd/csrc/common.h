@@ -136,6 +136,7 @@ struct Epi {
   const __bf16* x16;  // optional bf16 shadow of the conv input
   int bn_fold;        // mode 2 over a reflect-padded k7 input-grad grid (cgan3d_epilogue.bn_fold)
   BnFuse fz;          // all-zero unless cgan3d_epilogue.fuse is given
+  int out16;          // cgan3d_epilogue.out_bf16: y and bn_z are bf16 (k7m n2w and S2T launches only)
 };
 
 __device__ __forceinline__ float act_grad(float pre, int act, float slope) {
@@ -176,7 +177,7 @@ long long k7_n2w_blocks(const cgan3d_conv_geom* g);
 long long k7m_n2w_blocks(const cgan3d_conv_geom* g);
 void k7m_n2w_launch(const cgan3d_conv_geom* g, int P, int reflect, int flip, long long wc, const float* x,
                     const float* w, float* y, float* stats, float* bn_part, hipStream_t s, const Epi* fold = nullptr,
-                    const BnFuse* fz = nullptr);
+                    const BnFuse* fz = nullptr, bool out16 = false);
 void k7m_w2n_launch(const cgan3d_conv_geom* g, int P, int reflect, long long wc, const float* x, const float* w,
                     float* y, const Epi& e, hipStream_t s);
 // implicit-GEMM forward / input-grad (conv_gemm.hip)

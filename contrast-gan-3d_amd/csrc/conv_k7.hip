@@ -351,8 +351,10 @@ int k7_try_fwd(const cgan3d_conv_geom* g, const float* x, const float* w, float*
       (smode != 2 || (fold && g->transposed && k7m_ok(g, g->cout))) && e.act == CGAN3D_ACT_NONE) {
     if (k7m_ok(g, g->cout)) {
       float* bp = e.bn_mode == 1 ? e.bn_part : nullptr;
-      if (!g->transposed) k7m_n2w_launch(g, g->pad, g->reflect, 0, g->w_sb, x, w, y, e.stats, bp, s, nullptr, &e.fz);
-      else k7m_n2w_launch(g, g->k - 1 - g->pad, 0, 1, g->w_sb, x, w, y, e.stats, bp, s, fold ? &e : nullptr);
+      if (!g->transposed)
+        k7m_n2w_launch(g, g->pad, g->reflect, 0, g->w_sb, x, w, y, e.stats, bp, s, nullptr, &e.fz, e.out16);
+      else k7m_n2w_launch(g, g->k - 1 - g->pad, 0, 1, g->w_sb, x, w, y, e.stats, bp, s, fold ? &e : nullptr, nullptr,
+                          e.out16);
       return 1;
     }
     K7Args a;

@@ -85,6 +85,9 @@ __device__ __forceinline__ float k7m_rowsum16(float v) {
   return v;
 }
 
+// B16 (round 4, cgan3d_epilogue.out_bf16): y and the fold's z are bf16 (the 64^3 16-channel tensors of
+// the generator); the statistics come from the fp32 accumulators either way
+template <bool B16>
 __global__ __launch_bounds__(256, 2) void k7m_n2w_kernel(K7Args a, const float* __restrict__ x,
                                                          const float* __restrict__ w, float* __restrict__ y,
                                                          float* stats, float* bn_part, int tiles_per_block, int ntiles,
@@ -218,7 +221,14 @@ __global__ __launch_bounds__(256, 2) void k7m_n2w_kernel(K7Args a, const float* 
     for (int r = 0; r < N_TH; ++r) {
       const int oh = h0 + r;
       if (od < a.do_ && oh < a.ho && ow < a.wo) {
-        *reinterpret_cast<f32x4*>(y + (((n * a.do_ + od) * a.ho + oh) * a.wo + ow) * C + 4 * g) = acc[r];
+        const int o = (((n * a.do_ + od) * a.ho + oh) * a.wo + ow) * C + 4 * g;
+        if constexpr (B16) {
+          bf16x4_k h;
+          h[0] = (__bf16)acc[r][0]; h[1] = (__bf16)acc[r][1]; h[2] = (__bf16)acc[r][2]; h[3] = (__bf16)acc[r][3];
+          *reinterpret_cast<bf16x4_k*>(reinterpret_cast<__bf16*>(y) + o) = h;
+        } else {
+          *reinterpret_cast<f32x4*>(y + o) = acc[r];
+        }
 #pragma unroll
         for (int jj = 0; jj < 4; ++jj) s1[jj] += acc[r][jj];
       }
@@ -230,7 +240,13 @@ __global__ __launch_bounds__(256, 2) void k7m_n2w_kernel(K7Args a, const float* 
       for (int r = 0; r < N_TH; ++r) {
         const int vh = reflect_idx(h0 + r - fb.P, fb.zh);
         const bool ok = od < a.do_ && h0 + r < a.ho && ow < a.wo;
-        zv[r] = *reinterpret_cast<const f32x4*>(fb.z + (ok ? (((n * fb.zd + vd) * fb.zh + vh) * fb.zw + vw) * C + 4 * g : 0));
+        const int zo = ok ? (((n * fb.zd + vd) * fb.zh + vh) * fb.zw + vw) * C + 4 * g : 0;
+        if constexpr (B16) {
+          const bf16x4_k h = *reinterpret_cast<const bf16x4_k*>(reinterpret_cast<const __bf16*>(fb.z) + zo);
+          zv[r] = f32x4{(float)h[0], (float)h[1], (float)h[2], (float)h[3]};
+        } else {
+          zv[r] = *reinterpret_cast<const f32x4*>(fb.z + zo);
+        }
       }
 #pragma unroll
       for (int r = 0; r < N_TH; ++r)
@@ -957,7 +973,7 @@ long long k7m_n2w_blocks(const cgan3d_conv_geom* g) {
 
 void k7m_n2w_launch(const cgan3d_conv_geom* g, int P, int reflect, int flip, long long wc, const float* x,
                     const float* w, float* y, float* stats, float* bn_part, hipStream_t s, const Epi* fold,
-                    const BnFuse* fz) {
+                    const BnFuse* fz, bool out16) {
   const K7Args a = k7m_args(g, P, reflect, flip, wc, N_TD, N_TH, N_TW);
   int grid, per, nt;
   k7m_n2w_split(a, &grid, &per, &nt);
@@ -973,7 +989,8 @@ void k7m_n2w_launch(const cgan3d_conv_geom* g, int P, int reflect, int flip, lon
     acc1 = fz->acc_out;
     reps1 = fz->reps;
   }
-  ::cg::launch(k7m_n2w_kernel, dim3(grid), dim3(256), 0, s, a, x, w, y, stats, bn_part, per, nt, fb, acc1, reps1);
+  ::cg::launch(out16 ? k7m_n2w_kernel<true> : k7m_n2w_kernel<false>, dim3(grid), dim3(256), 0, s, a, x, w, y, stats,
+               bn_part, per, nt, fb, acc1, reps1);
 }
 
 static int g_k7s = 0;  // cgan3d_set_tuning key 13: output planes per streamed-w2n block (0 auto, -1 off)

@@ -405,7 +405,9 @@ __device__ __forceinline__ void s2t_class(const __bf16* halo, const __bf16* wts,
 // shadow)); the weights are staged into
 // LDS once, the next tile's halo is loaded into registers while the current tile's MFMAs and
 // epilogue run.
-template <int MODE, bool X16>  // statistics mode s2_stat_mode(ep): 0 none, 1 forward, 2 input-grad; X16: ep.x16
+// statistics mode s2_stat_mode(ep): 0 none, 1 forward, 2 input-grad; X16: ep.x16; B16 (ep.out16, round 4):
+// the output and the mode-2 z are bf16 (the generator's 64^3 16-channel tensors)
+template <int MODE, bool X16, bool B16>
 __global__ __launch_bounds__(256, MODE == 2 && !X16 ? 1 : 2) void conv_s2t_kernel(S2Args a, const float* __restrict__ x,
                                                           const __bf16* __restrict__ wpk, float* y, Epi ep, int ntiles) {
   constexpr int CI = 32, CO = 16;
@@ -541,7 +543,14 @@ __global__ __launch_bounds__(256, MODE == 2 && !X16 ? 1 : 2) void conv_s2t_kerne
       f32x4 zv[MODE == 2 ? 4 : 1];  // outputs u = 4p .. 4p + 3
       if constexpr (MODE == 2) {
 #pragma unroll
-        for (int k = 0; k < 4; ++k) zv[k] = *reinterpret_cast<const f32x4*>(ep.bn_z + obase[4 * p + k]);
+        for (int k = 0; k < 4; ++k) {
+          if constexpr (B16) {
+            const bf16x4_s h = *reinterpret_cast<const bf16x4_s*>(reinterpret_cast<const __bf16*>(ep.bn_z) + obase[4 * p + k]);
+            zv[k] = f32x4{(float)h[0], (float)h[1], (float)h[2], (float)h[3]};
+          } else {
+            zv[k] = *reinterpret_cast<const f32x4*>(ep.bn_z + obase[4 * p + k]);
+          }
+        }
       }
 #pragma unroll
       for (int zz = 0; zz < 2; ++zz) {
@@ -550,7 +559,13 @@ __global__ __launch_bounds__(256, MODE == 2 && !X16 ? 1 : 2) void conv_s2t_kerne
 #pragma unroll
         for (int S = 0; S < 2; ++S) {
           const int u = (p * 2 + zz) * 2 + S;
-          if (ok[u]) *reinterpret_cast<f32x4*>(y + obase[u]) = out[S];
+          if constexpr (B16) {  // 8 bytes per lane (the two halves of a 64-byte voxel pair from one store)
+            bf16x4_s h;
+            h[0] = (__bf16)out[S][0]; h[1] = (__bf16)out[S][1]; h[2] = (__bf16)out[S][2]; h[3] = (__bf16)out[S][3];
+            if (ok[u]) *reinterpret_cast<bf16x4_s*>(reinterpret_cast<__bf16*>(y) + obase[u]) = h;
+          } else {
+            if (ok[u]) *reinterpret_cast<f32x4*>(y + obase[u]) = out[S];
+          }
           if constexpr (MODE == 1) vals[u][0] = out[S];
           if constexpr (MODE == 2) s2_m2_add(ep, k2, out[S], zv[u - 4 * p], ok[u], s2s[0], s2q[0]);
         }
@@ -605,6 +620,10 @@ int s2_launch(const cgan3d_conv_geom* g, const float* x, const __bf16* wp, float
     set_error("conv_s2: geometry or epilogue not supported (residual/mask/stats/out2)");
     return CGAN3D_EINVAL;
   }
+  if (e.out16 && (kind != 2 || !e.x16)) {
+    set_error("conv_s2: out_bf16 only on the S2T kernel with the bf16 input shadow");
+    return CGAN3D_EINVAL;
+  }
   S2Args a = s2_args(g, kind);
   if ((long long)g->n * g->do_ * g->ho * g->wo * g->cout >= (1LL << 31)) {  // 32-bit output offsets
     set_error("conv_s2: output too large for 32-bit element offsets");
@@ -619,9 +638,10 @@ int s2_launch(const cgan3d_conv_geom* g, const float* x, const __bf16* wp, float
   else {  // persistent: two blocks per CU (one for mode 2 from fp32 input: its staging registers)
     const long long per_cu = mode == 2 && !e.x16 ? 1 : 2;
     const dim3 pgrid((unsigned)std::min<long long>(ntiles, per_cu * cu_count()));
-#define CG_S2T(M, X) ::cg::launch(conv_s2t_kernel<M, X>, pgrid, dim3(256), 0, st, a, x, wp, y, e, (int)ntiles)
-    if (e.x16) { if (mode == 2) CG_S2T(2, true); else if (mode == 1) CG_S2T(1, true); else CG_S2T(0, true); }
-    else { if (mode == 2) CG_S2T(2, false); else if (mode == 1) CG_S2T(1, false); else CG_S2T(0, false); }
+#define CG_S2T(M, X, B) ::cg::launch(conv_s2t_kernel<M, X, B>, pgrid, dim3(256), 0, st, a, x, wp, y, e, (int)ntiles)
+    if (e.out16) { if (mode == 2) CG_S2T(2, true, true); else if (mode == 1) CG_S2T(1, true, true); else CG_S2T(0, true, true); }
+    else if (e.x16) { if (mode == 2) CG_S2T(2, true, false); else if (mode == 1) CG_S2T(1, true, false); else CG_S2T(0, true, false); }
+    else { if (mode == 2) CG_S2T(2, false, false); else if (mode == 1) CG_S2T(1, false, false); else CG_S2T(0, false, false); }
 #undef CG_S2T
   }
   return CGAN3D_OK;

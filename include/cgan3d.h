@@ -133,7 +133,17 @@ typedef struct cgan3d_epilogue {
                                 * reflect-folded tensor (pad bn_fold), bn_z lives on the unpadded
                                 * grid; see cgan3d_bn_backward_slab_fold.  0 otherwise. */
   const cgan3d_bn_fuse* fuse;  /* NULL, or the statistics into fp64 accumulators (above) */
+  int32_t out_bf16;            /* 1: the output y and bn_z are bf16 arrays (same layout, passed through
+                                * the float* / const float* slots): the generator's 64^3 16-channel
+                                * tensors kept in bf16 (round 4) — only launches with
+                                * cgan3d_conv3d_out_bf16_ok accept it, every other launch rejects it */
 } cgan3d_epilogue;
+
+/* 1 when the forward-style launch of g honours cgan3d_epilogue.out_bf16: the 1 -> 16 k7 MFMA kernel
+ * (first conv forward; last conv input-grad, its folded statistics reading a bf16 z) and the S2T
+ * kernel (ConvTranspose3d 32 -> 16 forward; the first downsampling conv's input-grad with acc_mode 4
+ * statistics reading a bf16 z). */
+int32_t cgan3d_conv3d_out_bf16_ok(const cgan3d_conv_geom* g);
 
 /* 1 when the geometry's launch can produce cgan3d_bn_fuse accumulators. */
 int32_t cgan3d_bn_fuse_ok(const cgan3d_conv_geom* g);
@@ -295,22 +305,25 @@ int cgan3d_bn_backward_slab_fold(const float* padded, const float* z, int32_t n,
  * buffers, or dgamma / dbeta): one launch per BatchNorm layer and direction.  Block 0 also zeroes
  * `zero_n` doubles at `zero` (an accumulator the stream is done with; NULL / 0: none).
  * blocks.py:26-27,45 BatchNorm3d train forward + act (+ residual), and its autograd backward. */
+/* in_bf16 (round 4): 1 when z (apply) / dy and z (backward) / padded and z (fold) are bf16 arrays
+ * (the conv that produced them had cgan3d_epilogue.out_bf16); the statistics still come from the
+ * producer's fp32 values through the accumulators. */
 int cgan3d_bn_apply_acc(const double* acc, int32_t reps, int32_t c, int64_t nvox, const float* gamma,
                         const float* beta, float* running_mean, float* running_var, int64_t* num_batches_tracked,
-                        float momentum, float eps, float* scale_shift, float* mean_invstd, const float* z,
+                        float momentum, float eps, float* scale_shift, float* mean_invstd, const void* z,
                         int32_t act, float slope, const float* residual, float* y, void* y_bf16, double* zero,
-                        int32_t zero_n, void* stream);
-int cgan3d_bn_backward_acc(const float* dy, const float* z, int64_t nvox, int32_t c, const double* acc,
+                        int32_t zero_n, int32_t in_bf16, void* stream);
+int cgan3d_bn_backward_acc(const void* dy, const void* z, int64_t nvox, int32_t c, const double* acc,
                            int32_t reps, const float* scale_shift, const float* mean_invstd, const float* gamma,
                            int32_t act, float slope, float* dgamma, float* dbeta, float* dz, int32_t accumulate,
-                           void* dz_bf16, double* zero, int32_t zero_n, void* stream);
+                           void* dz_bf16, double* zero, int32_t zero_n, int32_t in_bf16, void* stream);
 /* cgan3d_bn_backward_slab_fold with the statistics from accumulators (the last conv's input-grad
  * launch with cgan3d_bn_fuse acc_mode 4 and bn_fold), one launch. */
-int cgan3d_bn_backward_acc_fold(const float* padded, const float* z, int32_t n, int32_t d, int32_t h, int32_t w,
+int cgan3d_bn_backward_acc_fold(const void* padded, const void* z, int32_t n, int32_t d, int32_t h, int32_t w,
                                 int32_t c, int32_t pad, const double* acc, int32_t reps, const float* scale_shift,
                                 const float* mean_invstd, const float* gamma, int32_t act, float slope,
                                 float* dgamma, float* dbeta, float* dz, int32_t accumulate, void* dz_bf16,
-                                double* zero, int32_t zero_n, void* stream);
+                                double* zero, int32_t zero_n, int32_t in_bf16, void* stream);
 
 /* accumulate != 0: dgamma/dbeta += this batch's gradients (a module called on several batches in
  * one step, e.g. the BatchNorm critic on the real and the fake batch, Trainer.py:119-121). */

@@ -78,8 +78,11 @@ def generator_layers(eng, rec: Recorder, weights=None, tol=1e-4, tol16=2e-3):
             z = F.conv_transpose3d(xin, w, stride=2, padding=1, output_padding=1)
         else:
             z = conv(xin, w, stride=ly.s, padding=0 if i == 0 else ly.p)
-        rec.add(f"G fwd z {ly.name}", rel_l2(cf(G.z[i]), z), tol)
-        zd = cf(G.z[i])
+        # z kept in bf16 (the 64^3 16-channel layers, engine.zs): the restated z rounded the same way
+        z16 = G.zs[i].dtype == torch.bfloat16
+        rec.add(f"G fwd z {ly.name}" + (" (bf16)" if z16 else ""), rel_l2(cf(G.zs[i]), rnd(z) if z16 else z),
+                tol16 if z16 else tol)
+        zd = cf(G.zs[i])
         nb = f"{ly.name}.normalization"
         y = F.batch_norm(zd, None, None, W[f"{nb}.weight"], W[f"{nb}.bias"], True, 0.1, 1e-5)
         if ly.act == 1:
@@ -107,22 +110,30 @@ def generator_layers(eng, rec: Recorder, weights=None, tol=1e-4, tol16=2e-3):
     # dL/dy of the last BatchNorm layer: the last conv's input-grad folded over the reflect pad
     yl = ylast.clone().requires_grad_(True)
     xp = F.pad(yl, (3,) * 6, mode="reflect")
-    xp_r = xp + (rnd(xp) - xp).detach()
-    (dy_next,) = torch.autograd.grad(conv(xp_r, rnd(W["model.last_conv.weight"])), yl, rnd(dzl))
+    xpl = rnd(xp).detach().requires_grad_(True)  # the padded grid the device's input-grad lands on
+    (dpad,) = torch.autograd.grad(conv(xpl, rnd(W["model.last_conv.weight"])), xpl, rnd(dzl))
+    if G.dpads.dtype == torch.bfloat16:  # kept in bf16 before the fold (engine.dpads)
+        dpad = rnd(dpad)
+    (dy_next,) = torch.autograd.grad(xp, yl, dpad)  # the reflect fold
     for i in range(len(G.layers) - 1, -1, -1):
         ly = G.layers[i]
         nb = f"{ly.name}.normalization"
         dy = dy_next
         if not (G.fold_bn and i == len(G.layers) - 1):
-            rec.add(f"G bwd dy {ly.name}", rel_l2(cf(G.dy[i]), dy), tol)
+            d16 = G.dys[i].dtype == torch.bfloat16
+            rec.add(f"G bwd dy {ly.name}" + (" (bf16)" if d16 else ""), rel_l2(cf(G.dys[i]), rnd(dy) if d16 else dy),
+                    tol16 if d16 else tol)
         # BatchNorm (+ act) backward from the device's z and the restated / device dL/dy
-        zd = cf(G.z[i]).requires_grad_(True)
+        zd = cf(G.zs[i]).requires_grad_(True)
         gmm = W[f"{nb}.weight"].clone().requires_grad_(True)
         bta = W[f"{nb}.bias"].clone().requires_grad_(True)
         y = F.batch_norm(zd, None, None, gmm, bta, True, 0.1, 1e-5)
         if ly.act == 1:
             y = F.relu(y)
-        dy_in = dy if (G.fold_bn and i == len(G.layers) - 1) else cf(G.dy[i])
+        if G.fold_bn and i == len(G.layers) - 1:  # the device folds its padded input-grad on the fly
+            dy_in = dy
+        else:
+            dy_in = cf(G.dys[i])
         dz, dg, db = torch.autograd.grad(y, (zd, gmm, bta), dy_in)
         rec.add(f"G bn dgamma {ly.name}", rel_l2(grads[f"{nb}.weight"], dg), tol)
         rec.add(f"G bn dbeta {ly.name}", rel_l2(grads[f"{nb}.bias"], db), tol)

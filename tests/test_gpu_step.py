@@ -416,9 +416,8 @@ def test_batchnorm_accumulators_match_slab_path(monkeypatch):
     g_args = dict(n_resnet_blocks=4, n_updownsample_blocks=2, init_channels_out=16)
     S, b = 64, 2
     engs = []
-    for off in (False, True):
-        if off:
-            monkeypatch.setenv("CGAN3D_DEBUG", "no_bn_fuse")
+    for off in (False, True):  # both with fp32 storage: the accumulators are the difference under test
+        monkeypatch.setenv("CGAN3D_DEBUG", "no_bn_fuse,fp32_store" if off else "fp32_store")
         g, d = _models(g_args)
         engs.append(StepEngine(g, d, g.config, d.config, b, b, (S, S, S), precision="bf16"))
     fused, slab = engs
@@ -466,9 +465,8 @@ def test_folded_last_batchnorm_backward_matches_fold_pass(monkeypatch):
     g_args = dict(n_resnet_blocks=2, n_updownsample_blocks=2, init_channels_out=16)
     S, b = 64, 1
     engs = []
-    for off in (False, True):
-        if off:
-            monkeypatch.setenv("CGAN3D_DEBUG", "no_bn_fold")
+    for off in (False, True):  # both with fp32 storage: the fold is the difference under test
+        monkeypatch.setenv("CGAN3D_DEBUG", "no_bn_fold,fp32_store" if off else "fp32_store")
         g, d = _models(g_args)
         engs.append(StepEngine(g, d, g.config, d.config, b, b, (S, S, S), precision="bf16"))
     folded, passed = engs
@@ -490,3 +488,47 @@ def test_folded_last_batchnorm_backward_matches_fold_pass(monkeypatch):
     bad = {k: v for k, v in worst.items() if v > 2e-2}
     assert not bad, f"folded vs fold-pass BatchNorm backward differ: {bad}"
     assert float(np.median(list(worst.values()))) <= 1e-3, worst
+
+
+def test_bf16_storage_matches_fp32_storage(monkeypatch):
+    """The generator's 64^3 16-channel BatchNorm inputs and their gradients kept in bf16 (engine.zs /
+    dys / dpads: the first conv's z and dL/dy, the last BatchNorm layer's z and the last conv's padded
+    input-grad; the statistics still from the producers' fp32 values) against the same step with them
+    in fp32 (CGAN3D_DEBUG=fp32_store), 64^3 bf16, two steps from one state: losses, and every gradient
+    tensor within the bf16 path's 2e-2 bar relative to its own largest entry, the median tensor within
+    2e-3 (the bf16 rounding of a stored tensor is one more 2^-9 relative perturbation per element,
+    the same size as the shadows the convolutions read anyway)."""
+    from cgan3d_amd.data.synthetic import synth_patches
+    from cgan3d_amd.engine import StepEngine
+    g_args = dict(n_resnet_blocks=2, n_updownsample_blocks=2, init_channels_out=16)
+    S, b = 64, 2
+    engs = []
+    for off in (False, True):
+        monkeypatch.setenv("CGAN3D_DEBUG", "fp32_store" if off else "")
+        g, d = _models(g_args)
+        engs.append(StepEngine(g, d, g.config, d.config, b, b, (S, S, S), precision="bf16"))
+    b16, f32 = engs
+    nl = len(b16.G.layers)
+    assert b16.G.z16[0] and b16.G.z16[-1] and not any(f32.G.z16)
+    assert b16.G.zs[0].dtype == b16.G.dys[0].dtype == b16.G.dpads.dtype == torch.bfloat16
+    assert sum(b16.G.z16) == 2 and nl > 2
+    opt, _ = synth_patches(b, S, 37)
+    sub, seg = synth_patches(b, S, 38)
+    bt = (torch.from_numpy(opt).cuda(), torch.from_numpy(sub).cuda(), torch.from_numpy(seg).cuda(),
+          torch.full((b,), 0.35, device="cuda"))
+    for it in range(2):
+        if it:
+            _sync_state(f32, b16)
+        for e in engs:
+            e.load_inputs(*bt)
+            e.step()
+        np.testing.assert_allclose(b16.losses.cpu().numpy(), f32.losses.cpu().numpy(), rtol=2e-3, atol=2e-5)
+    worst = {}
+    for net, a1, a2 in (("G", b16.g_arena, f32.g_arena), ("D", b16.d_arena, f32.d_arena)):
+        for k in a1.gviews:
+            g1, g2 = a1.gviews[k].cpu().numpy(), a2.gviews[k].cpu().numpy()
+            worst[f"{net}/{k}"] = float(np.abs(g1 - g2).max() / max(np.abs(g1).max(), 1e-30))
+    _dump_json("bf16_storage_vs_fp32", worst)
+    bad = {k: v for k, v in worst.items() if v > 2e-2}
+    assert not bad, f"bf16 vs fp32 storage differ: {bad}"
+    assert float(np.median(list(worst.values()))) <= 2e-3, worst

@@ -149,10 +149,10 @@ def generator_layers(S=32, n=2):
         else:
             hin = rnd(prev)
             z = F.conv_transpose3d(hin, w, stride=2, padding=1, output_padding=1)
-        dz = plan.z[i].cpu().numpy()
+        dz = plan.zs[i].float().cpu().numpy()
         print(f"{i} {ly.name:40s} z rel-L2 {rel(dz, z.permute(0, 2, 3, 4, 1).numpy()):.3e}")
         # BatchNorm (+ act, + residual) applied to the device's own z: the apply pass alone
-        zt = plan.z[i].cpu().double().permute(0, 4, 1, 2, 3)
+        zt = plan.zs[i].cpu().double().permute(0, 4, 1, 2, 3)
         nb = f"{ly.name}.normalization"
         yb = F.batch_norm(zt, None, None, W[f"{nb}.weight"], W[f"{nb}.bias"], True, 0.1, 1e-5)
         if ly.act == L.ACT_RELU:
