@@ -159,43 +159,44 @@ __global__ __launch_bounds__(256) void conv_cout1_block_kernel(ConvArgs a, const
   extern __shared__ __attribute__((aligned(16))) float Ws[];  // [T][cin]
   __shared__ float red[4];
   const int T = a.kd * a.k * a.k;
-  for (int i0 = threadIdx.x; i0 < T * a.cin; i0 += 8 * blockDim.x) {
-    float v[8];
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int i = i0 + u * blockDim.x, ci = i / T, t = i - ci * T;
-      v[u] = i < T * a.cin ? w[(long long)ci * a.sa + t] : 0.f;
-    }
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int i = i0 + u * blockDim.x, ci = i / T, t = i - ci * T;
-      if (i < T * a.cin) Ws[t * a.cin + ci] = v[u];
-    }
-  }
+  // Every load below is unconditional from a clamped, valid address (a dead one selected to zero):
+  // a load under a branch gets a wait of its own, and the round-3 version of this kernel walked its
+  // 17 loads one round trip at a time (11.6 us for the critic's 324-voxel last layer).
   const long long lin = blockIdx.x;
   int ow = (int)(lin % a.wo); long long tt = lin / a.wo;
   int oh = (int)(tt % a.ho); tt /= a.ho;
   int od = (int)(tt % a.do_); int nb = (int)(tt / a.do_);
   const int bd = od * a.sd - a.pd, bh = oh * a.s - a.p, bw = ow * a.s - a.p;
   const int C4 = a.cin >> 2, R4 = T * C4;
-  // the x loads do not depend on the staged weights: issue them before the barrier
+  // the x loads do not depend on the staged weights: issued first, so one round trip covers both
   constexpr int MAXR = 8;  // float4 per thread (R4 <= 2048)
   f32x4 xv[MAXR];
   int toff[MAXR];
 #pragma unroll
   for (int u = 0; u < MAXR; ++u) {
     const int r4 = threadIdx.x + 256 * u;
-    xv[u] = f32x4{0.f, 0.f, 0.f, 0.f};
-    toff[u] = -1;
-    if (r4 < R4) {
-      const int t = r4 / C4, c = (r4 - t * C4) * 4;
-      const int td = t / (a.k * a.k), th = (t / a.k) % a.k, tw = t % a.k;
-      const int id = gcoord(bd, td, a.di, a.reflect), ih = gcoord(bh, th, a.hi, a.reflect),
-                iw = gcoord(bw, tw, a.wi, a.reflect);
-      if ((id | ih | iw) >= 0) {
-        xv[u] = *reinterpret_cast<const f32x4*>(x + ((long long)((nb * a.di + id) * a.hi + ih) * a.wi + iw) * a.cin + c);
-        toff[u] = t * a.cin + c;
-      }
+    const int t = min(r4, R4 - 1) / C4, c = (min(r4, R4 - 1) - t * C4) * 4;
+    const int td = t / (a.k * a.k), th = (t / a.k) % a.k, tw = t % a.k;
+    const int id = gcoord(bd, td, a.di, a.reflect), ih = gcoord(bh, th, a.hi, a.reflect),
+              iw = gcoord(bw, tw, a.wi, a.reflect);
+    const bool ok = r4 < R4 && (id | ih | iw) >= 0;
+    const f32x4 v = *reinterpret_cast<const f32x4*>(
+        x + (ok ? ((long long)((nb * a.di + id) * a.hi + ih) * a.wi + iw) * a.cin + c : 0));
+    xv[u] = ok ? v : f32x4{0.f, 0.f, 0.f, 0.f};
+    toff[u] = ok ? t * a.cin + c : -1;
+  }
+  const int TC = T * a.cin;
+  for (int i0 = threadIdx.x; i0 < TC; i0 += 8 * blockDim.x) {
+    float v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int i = min(i0 + u * (int)blockDim.x, TC - 1), ci = i / T, t = i - ci * T;
+      v[u] = w[(long long)ci * a.sa + t];
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int i = i0 + u * blockDim.x, ci = i / T, t = i - ci * T;
+      if (i < TC) Ws[t * a.cin + ci] = v[u];
     }
   }
   __syncthreads();
