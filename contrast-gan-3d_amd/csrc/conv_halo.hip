@@ -293,32 +293,66 @@ __global__ __launch_bounds__(256) void conv_halo_kernel(HaloArgs a, const float*
   if (ntap > 1) issue(1);
 
   // ---- halo: fp32 NDHWC -> bf16 LDS (zero outside the gathered volume); with a bf16 shadow of
-  // x (ep.x16) 16-byte granules are copied as they are
-  if (ep.x16) {
+  // x (ep.x16) 16-byte granules are copied as they are.  Batches of HB items per thread: every load
+  // of a batch is issued (unconditionally, from a clamped address; outside items selected to zero)
+  // before the first LDS store — round 3 stored each item right after its own load under a branch,
+  // one round trip per item (12 per thread for the 32 -> 64 layer's 9^3 x 4-granule halo).
+  {
+    constexpr int HB = 8;
     const int nvox = a.ez * a.ey * a.ex;
-    constexpr int C8 = CIN / 8;
-    for (int i = tid; i < nvox * C8; i += 256) {
-      const int v = i / C8, c8 = i - v * C8;
+    auto coords = [&](int v, int* o) -> bool {
       const int hx = v % a.ex, hy = (v / a.ex) % a.ey, hz = v / (a.ex * a.ey);
       const int iz = oz + hz, iy = oy + hy, ix = ox + hx;
-      bf16x8_h val = {};
-      if (iz >= 0 && iz < a.di && iy >= 0 && iy < a.hi && ix >= 0 && ix < a.wi)
-        val = *reinterpret_cast<const bf16x8_h*>(ep.x16 + (((long long)(nb * a.di + iz) * a.hi + iy) * a.wi + ix) * CIN +
-                                                 8 * c8);
-      *reinterpret_cast<bf16x8_h*>(halo + v * ROW + 8 * c8) = val;
-    }
-  } else {
-    const int nvox = a.ez * a.ey * a.ex;
-    constexpr int C4 = CIN / 4;
-    for (int i = tid; i < nvox * C4; i += 256) {
-      const int v = i / C4, c4 = i - v * C4;
-      const int hx = v % a.ex, hy = (v / a.ex) % a.ey, hz = v / (a.ex * a.ey);
-      const int iz = oz + hz, iy = oy + hy, ix = ox + hx;
-      f32x4 val = {0.f, 0.f, 0.f, 0.f};
-      if (iz >= 0 && iz < a.di && iy >= 0 && iy < a.hi && ix >= 0 && ix < a.wi)
-        val = *reinterpret_cast<const f32x4*>(x + (((long long)(nb * a.di + iz) * a.hi + iy) * a.wi + ix) * CIN + 4 * c4);
-      __bf16* d = halo + v * ROW + 4 * c4;
-      d[0] = (__bf16)val[0]; d[1] = (__bf16)val[1]; d[2] = (__bf16)val[2]; d[3] = (__bf16)val[3];
+      *o = ((nb * a.di + iz) * a.hi + iy) * a.wi + ix;  // 32-bit: halo_setup bounds the volume
+      return iz >= 0 && iz < a.di && iy >= 0 && iy < a.hi && ix >= 0 && ix < a.wi;
+    };
+    if (ep.x16) {
+      constexpr int C8 = CIN / 8;
+      const int total = nvox * C8;
+      for (int i0 = 0; i0 < total; i0 += 256 * HB) {
+        bf16x8_h val[HB];
+#pragma unroll
+        for (int u = 0; u < HB; ++u) {
+          const int i = i0 + u * 256 + tid, ic = min(i, total - 1);
+          const int v = ic / C8, c8 = ic - v * C8;
+          int o;
+          const bool ok = coords(v, &o) && i < total;
+          const bf16x8_h t = *reinterpret_cast<const bf16x8_h*>(ep.x16 + (ok ? (long long)o * CIN + 8 * c8 : 0));
+          val[u] = ok ? t : bf16x8_h{};
+        }
+#pragma unroll
+        for (int u = 0; u < HB; ++u) {
+          const int i = i0 + u * 256 + tid;
+          if (i < total) {
+            const int v = i / C8, c8 = i - v * C8;
+            *reinterpret_cast<bf16x8_h*>(halo + v * ROW + 8 * c8) = val[u];
+          }
+        }
+      }
+    } else {
+      constexpr int C4 = CIN / 4;
+      const int total = nvox * C4;
+      for (int i0 = 0; i0 < total; i0 += 256 * HB) {
+        f32x4 val[HB];
+#pragma unroll
+        for (int u = 0; u < HB; ++u) {
+          const int i = i0 + u * 256 + tid, ic = min(i, total - 1);
+          const int v = ic / C4, c4 = ic - v * C4;
+          int o;
+          const bool ok = coords(v, &o) && i < total;
+          const f32x4 t = *reinterpret_cast<const f32x4*>(x + (ok ? (long long)o * CIN + 4 * c4 : 0));
+          val[u] = ok ? t : f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+#pragma unroll
+        for (int u = 0; u < HB; ++u) {
+          const int i = i0 + u * 256 + tid;
+          if (i < total) {
+            const int v = i / C4, c4 = i - v * C4;
+            __bf16* d = halo + v * ROW + 4 * c4;
+            d[0] = (__bf16)val[u][0]; d[1] = (__bf16)val[u][1]; d[2] = (__bf16)val[u][2]; d[3] = (__bf16)val[u][3];
+          }
+        }
+      }
     }
   }
   // the halo stores and tap tables must be visible before the first MFMA; the weight DMAs are
@@ -549,6 +583,7 @@ void halo_set_min_blocks(int v) { g_halo_min_blocks = v; }
 static bool halo_setup(const cgan3d_conv_geom* g, HaloArgs* a) {
   if (g->prec != CGAN3D_PREC_BF16 || g->reflect) return false;
   if (!(g->cin == 32 || g->cin == 64) || g->cout % 16 || g->k > 4 || g->stride < 1 || g->stride > 2) return false;
+  if ((long long)g->n * g->di * g->hi * g->wi >= (1LL << 31)) return false;  // 32-bit voxel index (halo staging)
   a->n = g->n; a->di = g->di; a->hi = g->hi; a->wi = g->wi; a->do_ = g->do_; a->ho = g->ho; a->wo = g->wo;
   a->cin = g->cin; a->cout = g->cout; a->k = g->k; a->s = g->stride; a->p = g->pad; a->transposed = g->transposed;
   if (g->transposed && g->stride > 1) {

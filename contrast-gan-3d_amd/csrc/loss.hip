@@ -101,9 +101,13 @@ __global__ __launch_bounds__(256) void gp_scale_kernel(const float* __restrict__
 #pragma unroll
     for (int b = 0; b < 8; ++b) ss[b] = 0.0;
     for (int c = threadIdx.x; c < chunks; c += blockDim.x) {
+      // unconditional loads (a clamped sample for b >= B, masked after): a load under `if (b < B)`
+      // waited for its own round trip
+      float v[8];
 #pragma unroll
-      for (int b = 0; b < 8; ++b)
-        if (b < B) ss[b] += part[(long long)b * chunks + c];
+      for (int b = 0; b < 8; ++b) v[b] = part[(long long)min(b, B - 1) * chunks + c];
+#pragma unroll
+      for (int b = 0; b < 8; ++b) ss[b] += b < B ? (double)v[b] : 0.0;
     }
 #pragma unroll
     for (int b = 0; b < 8; ++b) {
@@ -157,8 +161,15 @@ __global__ __launch_bounds__(256) void gp_scale_kernel(const float* __restrict__
     losses[L_GP] = gp;
     losses[L_D] = (lg ? wd : losses[L_WD]) + gp;
   }
-  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long long)gridDim.x * blockDim.x)
-    out[i] = coef[i / ps] * g[i];
+  if ((ps & 3) == 0 && total < (1LL << 32) && !(((uintptr_t)g | (uintptr_t)out) & 15)) {  // float4 with 32-bit index math (no 64-bit divide per element)
+    const unsigned n4 = (unsigned)(total >> 2), ps4 = (unsigned)(ps >> 2);
+    const f32x4* g4 = reinterpret_cast<const f32x4*>(g);
+    f32x4* o4 = reinterpret_cast<f32x4*>(out);
+    for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += gridDim.x * blockDim.x) o4[i] = coef[i / ps4] * g4[i];
+  } else {
+    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long long)gridDim.x * blockDim.x)
+      out[i] = coef[i / ps] * g[i];
+  }
 }
 
 // --- generator losses ---------------------------------------------------------------------

@@ -305,7 +305,12 @@ def test_conv_halo_bf16(transposed, cin, cout, k, s, p, sp):
         assert torch.equal(st16, stats), "bf16-shadow statistics differ"
         dxo16 = torch.empty_like(dxo)
         ops.conv(gd, _cl(gy), wdp, dxo16, ops.epilogue(x_bf16=_cl(gy).bfloat16()))
-        assert torch.equal(dxo16, dxo), "bf16-shadow input-grad differs"
+        if (transposed, cin, cout, k, s, p) == (False, 64, 64, 3, 1, 1):
+            # the ResNet-block shape with a shadow and no statistics takes conv_k3m (the same bf16
+            # products summed in another fp32 order; its own test: test_conv_k3m_bf16)
+            assert_close(dxo16.cpu().double().numpy(), dxo.cpu().double().numpy(), 1e-5, "k3m vs k3 input-grad")
+        else:
+            assert torch.equal(dxo16, dxo), "bf16-shadow input-grad differs"
 
 
 @pytest.mark.parametrize("sp", [(12, 20, 36), (16, 16, 16), (20, 9, 72)])

@@ -361,11 +361,17 @@ def test_bf16_shadows_match_fp32_staging(monkeypatch):
     from cgan3d_amd.data.synthetic import synth_patches
     from cgan3d_amd.engine import StepEngine
     L.check(L.load().cgan3d_set_tuning(13, -1), "k7s off")
+    # likewise the ResNet-block kernels that only run from shadows (conv_k3m / wgrad_k3m, their own
+    # tests in test_gpu_ops.py): off, so both steps take conv_k3 / wgrad_k3
+    L.check(L.load().cgan3d_set_tuning(15, 0), "k3m off")
+    L.check(L.load().cgan3d_set_tuning(16, 0), "wgrad_k3m off")
     monkeypatch.setenv("CGAN3D_DEBUG", "no_bn_fuse")  # the fused chain needs the shadows: compared on its own below
     try:
         _shadow_exactness(monkeypatch, synth_patches, StepEngine)
     finally:
         L.check(L.load().cgan3d_set_tuning(13, 0), "k7s auto")
+        L.check(L.load().cgan3d_set_tuning(15, 1), "k3m on")
+        L.check(L.load().cgan3d_set_tuning(16, 1), "wgrad_k3m on")
 
 
 def _shadow_exactness(monkeypatch, synth_patches, StepEngine):
