@@ -130,8 +130,8 @@ __global__ __launch_bounds__(64 * W) void conv_sk_kernel(SkArgs a, const float* 
     xa1[sl] = ok ? v1 : zero;
     const int wk = tlin[j] * a.cin + a0;
 #pragma unroll
-    for (int t = 0; t < NT; ++t)  // cout % 16 == 0 (sk_format_ok): every column is in range
-      bb[sl][t] = *reinterpret_cast<const bf16x8_k*>(wp + (t * 16 + r16) * a.ktot + wk);
+    for (int t = 0; t < NT; ++t)  // columns past cout (cout = 8) read a valid row; their outputs are never stored
+      bb[sl][t] = *reinterpret_cast<const bf16x8_k*>(wp + min(t * 16 + r16, a.cout - 1) * a.ktot + wk);
   };
   auto step = [&](int sl) {
     bf16x8_k av;
@@ -234,7 +234,7 @@ __global__ __launch_bounds__(64 * W) void conv_sk_kernel(SkArgs a, const float* 
 
 // geometry (ignoring the weight format): the critic's k4 convs, bf16
 bool sk_format_ok(const cgan3d_conv_geom* g) {
-  if (g->prec != CGAN3D_PREC_BF16 || g->reflect || g->k != 4 || g->cin % 8 || g->cout % 16 || g->cout > 64) return false;
+  if (g->prec != CGAN3D_PREC_BF16 || g->reflect || g->k != 4 || g->cin % 8 || g->cout % 8 || g->cout > 64) return false;
   if (g->cin & (g->cin - 1)) return false;  // power of two: shift / mask index math
   if ((long long)g->n * g->di * g->hi * g->wi * g->cin >= (1LL << 31) ||
       (long long)g->n * g->do_ * g->ho * g->wo * g->cout >= (1LL << 31))
