@@ -139,6 +139,13 @@ struct Epi {
   int out16;          // cgan3d_epilogue.out_bf16: y and bn_z are bf16 (k7m n2w and S2T launches only)
 };
 
+// c ? v : 0 for a just-loaded v, by an integer mask: the compiler turns a select whose operand is a
+// load into a branch around the load (CodeGenPrepare), and a load under a branch gets a vmcnt(0) of
+// its own — serialising loads meant to be in flight together
+__device__ __forceinline__ float keep_if(bool c, float v) {
+  return __uint_as_float(__float_as_uint(v) & (c ? 0xffffffffu : 0u));
+}
+
 __device__ __forceinline__ float act_grad(float pre, int act, float slope) {
   if (act == CGAN3D_ACT_RELU) return pre > 0.f ? 1.f : 0.f;
   if (act == CGAN3D_ACT_LRELU) return pre > 0.f ? 1.f : slope;

@@ -175,6 +175,9 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(GemmArgs a, const float*
   f32x4 ra4[VEC == 4 ? A_SLOTS : 1];
   float ra1[VEC == 4 ? 1 : A_SLOTS];
   f32x4 rb[B_SLOTS];
+  // which loaded operands are live: applied in store_chunk, after the MFMAs the loads overlap (a mask
+  // applied right after the load would wait for it there)
+  bool oka[A_SLOTS], okb[B_SLOTS][4];
 
   auto decode = [&](int kk, int* j, int* ci) {
     if (a.cin_shift >= 0) { *j = kk >> a.cin_shift; *ci = kk & (a.cin - 1); }
@@ -189,54 +192,51 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(GemmArgs a, const float*
     if ((id | ih | iw) < 0) return -1;
     return ((long long)((nb + id) * a.hi + ih) * a.wi + iw) * a.cin + ci;
   };
+  // Every load is issued unconditionally from a clamped, valid address and a dead operand is selected
+  // to zero afterwards: loads under branches (kk < KT, the gathered voxel inside the volume, co < cout)
+  // each waited for their own round trip (round 4: 18-59 vmcnt(0) per kernel before).
   auto load_chunk = [&](int kc0) {
     if constexpr (VEC == 4) {
 #pragma unroll
       for (int i = 0; i < A_SLOTS; ++i) {
         const int sl = tid + 256 * i, r = sl >> 3, kk = kc0 + (sl & 7) * 4;
-        f32x4 v = {0.f, 0.f, 0.f, 0.f};
-        if (kk < KT) {
-          int j, ci;
-          decode(kk, &j, &ci);
-          const long long o = gather(r, j, ci);
-          if (o >= 0) v = *reinterpret_cast<const f32x4*>(x + o);
-        }
-        ra4[i] = v;
+        int j, ci;
+        decode(min(kk, KT - 1), &j, &ci);
+        const long long o = gather(r, j, ci);
+        oka[i] = kk < KT && o >= 0;
+        ra4[i] = *reinterpret_cast<const f32x4*>(x + (oka[i] ? o : 0));
       }
     } else {
 #pragma unroll
       for (int i = 0; i < A_SLOTS; ++i) {
         const int sl = tid + 256 * i, r = sl >> 5, kk = kc0 + (sl & 31);
-        float v = 0.f;
-        if (kk < KT) {
-          int j, ci;
-          decode(kk, &j, &ci);
-          const long long o = gather(r, j, ci);
-          if (o >= 0) v = x[o];
-        }
-        ra1[i] = v;
+        int j, ci;
+        decode(min(kk, KT - 1), &j, &ci);
+        const long long o = gather(r, j, ci);
+        oka[i] = kk < KT && o >= 0;
+        ra1[i] = x[oka[i] ? o : 0];
       }
     }
 #pragma unroll
     for (int i = 0; i < B_SLOTS; ++i) {
-      const int sl = tid + 256 * i;
-      f32x4 v = {0.f, 0.f, 0.f, 0.f};
-      if (sl < BN * KC / 4) {
-        const int kr = sl / (BN / 4), c4 = sl - kr * (BN / 4), kk = kc0 + kr;
-        const int co = co0 + 4 * c4;
-        if (kk < KT && co < a.cout) {
-          int j, ci;
-          decode(kk, &j, &ci);
-          if (a.packed) {
-            v = *reinterpret_cast<const f32x4*>(w + ((long long)tap_lin[j] * a.cin + ci) * a.ldb + co);
-          } else {
-            const long long base = (long long)ci * a.sa + tap_lin[j];
+      const int sl = min(tid + 256 * i, BN * KC / 4 - 1);
+      const int kr = sl / (BN / 4), c4 = sl - kr * (BN / 4), kk = kc0 + kr;
+      const int co = co0 + 4 * c4;
+      const bool live = tid + 256 * i < BN * KC / 4 && kk < KT && co < a.cout;
+      int j, ci;
+      decode(min(kk, KT - 1), &j, &ci);
+      // one code path for both weight layouts (addresses selected, not loaded values: a value merged
+      // from two branches made the compiler wait for it at the merge, before the MFMAs it should
+      // overlap): packed rows [tap][cin][ldb >= cout rounded up to 4], or torch's strided layout
+      // element (co + e) of the row at b0 + idx * bs, idx clamped into the row
+      const long long b0 = a.packed ? ((long long)tap_lin[j] * a.cin + ci) * a.ldb : (long long)ci * a.sa + tap_lin[j];
+      const long long bs = a.packed ? 1 : a.sb;
+      const int cl = a.packed ? a.ldb - 1 : a.cout - 1;
 #pragma unroll
-            for (int e = 0; e < 4; ++e) v[e] = co + e < a.cout ? w[base + (long long)(co + e) * a.sb] : 0.f;
-          }
-        }
+      for (int e = 0; e < 4; ++e) {
+        rb[i][e] = w[b0 + (long long)min(co + e, cl) * bs];
+        okb[i][e] = live && co + e < a.cout;
       }
-      rb[i] = v;
     }
   };
   auto store_chunk = [&]() {
@@ -245,13 +245,13 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(GemmArgs a, const float*
       for (int i = 0; i < A_SLOTS; ++i) {
         const int sl = tid + 256 * i, r = sl >> 3, e0 = (sl & 7) * 4;
 #pragma unroll
-        for (int e = 0; e < 4; ++e) As[r * LD + e0 + e] = (T)ra4[i][e];
+        for (int e = 0; e < 4; ++e) As[r * LD + e0 + e] = (T)keep_if(oka[i], ra4[i][e]);
       }
     } else {
 #pragma unroll
       for (int i = 0; i < A_SLOTS; ++i) {
         const int sl = tid + 256 * i;
-        As[(sl >> 5) * LD + (sl & 31)] = (T)ra1[i];
+        As[(sl >> 5) * LD + (sl & 31)] = (T)keep_if(oka[i], ra1[i]);
       }
     }
 #pragma unroll
@@ -260,7 +260,7 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(GemmArgs a, const float*
       if (sl < BN * KC / 4) {
         const int kr = sl / (BN / 4), c4 = sl - kr * (BN / 4);
 #pragma unroll
-        for (int e = 0; e < 4; ++e) Bs[(4 * c4 + e) * LD + kr] = (T)rb[i][e];
+        for (int e = 0; e < 4; ++e) Bs[(4 * c4 + e) * LD + kr] = (T)keep_if(okb[i][e], rb[i][e]);
       }
     }
   };

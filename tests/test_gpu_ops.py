@@ -747,6 +747,8 @@ def test_conv_k3m_bf16(n, sp):
     assert_close(_ncdhw(yo).numpy(), yref.numpy(), 2e-5, "k3m fwd")
     assert_close(_ncdhw(dxo).numpy(), dxref.numpy(), 2e-5, "k3m dgrad")
     for a, b_, nm in zip(out["k3m"], out["k3"], ("fwd", "acc3", "dgrad", "acc4")):
+        if nm.startswith("acc"):  # the two grids spread their blocks over the replicas differently
+            a, b_ = a.view(reps, -1).sum(0), b_.view(reps, -1).sum(0)
         assert_close(a.double().numpy(), b_.double().numpy(), 1e-5, f"k3m vs k3 {nm}")
     yk = yo.double().view(-1, cout)
     a3 = acc3.view(reps, 2, cout).sum(0)
