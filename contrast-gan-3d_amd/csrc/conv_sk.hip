@@ -112,6 +112,7 @@ __global__ __launch_bounds__(64 * W) void conv_sk_kernel(SkArgs a, const float* 
   // the runtime loop, for long K (many rows, MT == 4).
   constexpr int PF = NKC > 0 ? (NKC < 8 ? NKC : 8) : 4;
   f32x4 xa0[PF], xa1[PF];  // A: 8 fp32 channels of one gathered voxel
+  bool xok[PF];            // ... live (applied at the MFMA: a select right after the load waits for it)
   bf16x8_k bb[PF][NT];     // B fragments
   const int nk = ks0 < KS ? (KS - ks0 + kstep - 1) / kstep : 0;  // this wave's K-steps (wave-uniform)
   auto load = [&](int q, int sl) {
@@ -124,10 +125,9 @@ __global__ __launch_bounds__(64 * W) void conv_sk_kernel(SkArgs a, const float* 
                     (unsigned)ix < (unsigned)a.wi;
     // 32-bit element offsets (sk_launch checks the sizes); a dead operand reads element 0
     const float* src = x + (ok ? ((((nb * a.di + iz) * a.hi + iy) * a.wi + ix) << a.cin_log2) + a0 : 0);
-    const f32x4 v0 = *reinterpret_cast<const f32x4*>(src), v1 = *reinterpret_cast<const f32x4*>(src + 4);
-    const f32x4 zero = {0.f, 0.f, 0.f, 0.f};
-    xa0[sl] = ok ? v0 : zero;
-    xa1[sl] = ok ? v1 : zero;
+    xa0[sl] = *reinterpret_cast<const f32x4*>(src);
+    xa1[sl] = *reinterpret_cast<const f32x4*>(src + 4);
+    xok[sl] = ok;
     const int wk = tlin[j] * a.cin + a0;
 #pragma unroll
     for (int t = 0; t < NT; ++t)  // columns past cout (cout = 8) read a valid row; their outputs are never stored
@@ -135,8 +135,12 @@ __global__ __launch_bounds__(64 * W) void conv_sk_kernel(SkArgs a, const float* 
   };
   auto step = [&](int sl) {
     bf16x8_k av;
-    av[0] = (__bf16)xa0[sl][0]; av[1] = (__bf16)xa0[sl][1]; av[2] = (__bf16)xa0[sl][2]; av[3] = (__bf16)xa0[sl][3];
-    av[4] = (__bf16)xa1[sl][0]; av[5] = (__bf16)xa1[sl][1]; av[6] = (__bf16)xa1[sl][2]; av[7] = (__bf16)xa1[sl][3];
+    const bool k = xok[sl];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      av[e] = (__bf16)keep_if(k, xa0[sl][e]);
+      av[4 + e] = (__bf16)keep_if(k, xa1[sl][e]);
+    }
 #pragma unroll
     for (int t = 0; t < NT; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bb[sl][t], av, acc[t], 0, 0, 0);
   };

@@ -112,9 +112,10 @@ def generator_layers(eng, rec: Recorder, weights=None, tol=1e-4, tol16=2e-3):
     xp = F.pad(yl, (3,) * 6, mode="reflect")
     xpl = rnd(xp).detach().requires_grad_(True)  # the padded grid the device's input-grad lands on
     (dpad,) = torch.autograd.grad(conv(xpl, rnd(W["model.last_conv.weight"])), xpl, rnd(dzl))
-    if G.dpads.dtype == torch.bfloat16:  # kept in bf16 before the fold (engine.dpads)
-        dpad = rnd(dpad)
-    (dy_next,) = torch.autograd.grad(xp, yl, dpad)  # the reflect fold
+    # the reflect fold; with the padded input-grad kept in bf16 (engine.dpads) the device's statistics
+    # still come from its fp32 values (the producer's epilogue) and only the elementwise pass reads bf16
+    (dy_next,) = torch.autograd.grad(xp, yl, dpad, retain_graph=True)
+    dy_fold16 = torch.autograd.grad(xp, yl, rnd(dpad))[0] if G.dpads.dtype == torch.bfloat16 else None
     for i in range(len(G.layers) - 1, -1, -1):
         ly = G.layers[i]
         nb = f"{ly.name}.normalization"
@@ -124,17 +125,31 @@ def generator_layers(eng, rec: Recorder, weights=None, tol=1e-4, tol16=2e-3):
             rec.add(f"G bwd dy {ly.name}" + (" (bf16)" if d16 else ""), rel_l2(cf(G.dys[i]), rnd(dy) if d16 else dy),
                     tol16 if d16 else tol)
         # BatchNorm (+ act) backward from the device's z and the restated / device dL/dy
-        zd = cf(G.zs[i]).requires_grad_(True)
-        gmm = W[f"{nb}.weight"].clone().requires_grad_(True)
-        bta = W[f"{nb}.bias"].clone().requires_grad_(True)
-        y = F.batch_norm(zd, None, None, gmm, bta, True, 0.1, 1e-5)
-        if ly.act == 1:
-            y = F.relu(y)
-        if G.fold_bn and i == len(G.layers) - 1:  # the device folds its padded input-grad on the fly
-            dy_in = dy
+        last = G.fold_bn and i == len(G.layers) - 1
+        if G.z16[i]:
+            # bf16-stored layer (engine.zs / dys / dpads): the statistics pair (sum g, sum g*xhat) from
+            # the producer's fp32 dL/dy (restated: dy) and the bf16 z, the elementwise pass from the
+            # stored bf16 dL/dy, with the device's forward mean / invstd and scale / shift
+            C = ly.cout
+            zz = cf(G.zs[i])
+            mi, ssv = G.mi[i].detach().double().cpu(), G.ss[i].detach().double().cpu()
+            bc = lambda v: v.view(1, C, 1, 1, 1)  # noqa: E731
+            xh = (zz - bc(mi[:C])) * bc(mi[C:])
+            mask = ((zz * bc(ssv[:C]) + bc(ssv[C:])) > 0).double() if ly.act == 1 else torch.ones_like(zz)
+            gs = dy * mask
+            ga = (dy_fold16 if last else cf(G.dys[i])) * mask
+            nv = zz.numel() // C
+            db, dg = gs.sum((0, 2, 3, 4)), (gs * xh).sum((0, 2, 3, 4))
+            dz = bc(W[f"{nb}.weight"] * mi[C:]) * (ga - bc(db / nv) - xh * bc(dg / nv))
         else:
-            dy_in = cf(G.dys[i])
-        dz, dg, db = torch.autograd.grad(y, (zd, gmm, bta), dy_in)
+            zd = cf(G.zs[i]).requires_grad_(True)
+            gmm = W[f"{nb}.weight"].clone().requires_grad_(True)
+            bta = W[f"{nb}.bias"].clone().requires_grad_(True)
+            y = F.batch_norm(zd, None, None, gmm, bta, True, 0.1, 1e-5)
+            if ly.act == 1:
+                y = F.relu(y)
+            dy_in = dy if last else cf(G.dys[i])  # the device folds its padded input-grad on the fly
+            dz, dg, db = torch.autograd.grad(y, (zd, gmm, bta), dy_in)
         rec.add(f"G bn dgamma {ly.name}", rel_l2(grads[f"{nb}.weight"], dg), tol)
         rec.add(f"G bn dbeta {ly.name}", rel_l2(grads[f"{nb}.bias"], db), tol)
         if G.dz_dead[i]:
