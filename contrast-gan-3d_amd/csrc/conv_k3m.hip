@@ -184,18 +184,22 @@ __global__ __launch_bounds__(256, 1) void conv_k3m_kernel(K3mArgs a, const __bf1
   // ---- epilogue: lane holds rows R = (i & 3) + 8 (i >> 2) + 4 h of channel co0 + r
   const int C = 64, c = co0 + r;
   const float bias = ep.bias ? ep.bias[c] : 0.f;
-  long long oidx[16];
+  // km_row of row R = (i & 3) + 8 (i >> 2) + 4 h is x = i & 3, y = i >> 2, zz = (i >> 2 in {1, 2}) ^ h:
+  // one 32-bit voxel base per lane plus compile-time steps (k3m_ok bounds the volume below 2^31
+  // elements); round 3's per-element km_row and 64-bit index math was ~500 VALU per wave
+  int oidx[16];
   float vals[16];
   int nvalid = 0;
+  {
+    const int gx0 = txi * KM_TX, gy0 = tyi * KM_TY, gz0 = tzi * KM_TZ + 2 * wave;
+    const int vb = ((nb * a.d + gz0) * a.h + gy0) * a.w + gx0, plane = a.h * a.w;
 #pragma unroll
-  for (int i = 0; i < 16; ++i) {
-    const int R = (i & 3) + 8 * (i >> 2) + 4 * h;
-    int vx, vy, vzz;
-    km_row(R, vx, vy, vzz);
-    const int gx = txi * KM_TX + vx, gy = tyi * KM_TY + vy, gz = tzi * KM_TZ + 2 * wave + vzz;
-    const bool ok = gx < a.w && gy < a.h && gz < a.d;
-    oidx[i] = ok ? ((((long long)nb * a.d + gz) * a.h + gy) * a.w + gx) * C + c : -1;
-    nvalid += ok;
+    for (int i = 0; i < 16; ++i) {
+      const int vx = i & 3, vy = i >> 2, vzz = ((vy == 1 || vy == 2) ? 1 : 0) ^ h;
+      const bool ok = gx0 + vx < a.w && gy0 + vy < a.h && gz0 + vzz < a.d;
+      oidx[i] = ok ? (vb + vzz * plane + vy * a.w + vx) * C + c : -1;
+      nvalid += ok;
+    }
   }
   float resv[16], zv[16];
   const bool mode4 = ep.fz.acc_mode == 4;
@@ -290,7 +294,8 @@ void k3m_set(int v) { g_k3m = v; }
 // k3 s1 p1 64 -> 64 (forward, or the input-grad: a stride-1 conv with flipped taps) with a bf16 input
 // shadow, format-2 packed weights and an epilogue this kernel has (no slabs, masks or out2)
 bool k3m_ok(const cgan3d_conv_geom* g, const Epi& e) {
-  return g_k3m && g->prec == CGAN3D_PREC_BF16 && g->w_packed == 2 && g->cin == 64 && g->cout == 64 && g->k == 3 &&
+  return g_k3m && (long long)g->n * g->do_ * g->ho * g->wo * 64 < (1LL << 31) &&  // 32-bit epilogue offsets
+         g->prec == CGAN3D_PREC_BF16 && g->w_packed == 2 && g->cin == 64 && g->cout == 64 && g->k == 3 &&
          g->stride == 1 && g->pad == 1 && !g->reflect && !g->planar && g->di == g->do_ && g->hi == g->ho &&
          g->wi == g->wo && e.x16 && !e.stats && !e.bn_mode && !e.mask_src && !e.minuend && !e.out2 && !e.bn_fold &&
          (e.act == CGAN3D_ACT_NONE || e.act == CGAN3D_ACT_RELU || e.act == CGAN3D_ACT_LRELU) &&
