@@ -184,11 +184,29 @@ def load(path: os.PathLike | str | None = None) -> C.CDLL:
         fn.restype = res
     if path is None:
         _lib = lib
-        # CGAN3D_TUNE="key=value,key=value": cgan3d_set_tuning before anything is built (sweeps)
-        for kv in filter(None, os.environ.get("CGAN3D_TUNE", "").split(",")):
-            k, v = kv.split("=")
-            check(lib.cgan3d_set_tuning(int(k), int(v)), f"set_tuning {kv}")
+        # CGAN3D_TUNE="key=value,key=value": cgan3d_set_tuning before anything is built (sweeps);
+        # keys >= 100 are the host schedule's own knobs (py_tune)
+        for k, v in tune_pairs():
+            if k < 100:
+                check(lib.cgan3d_set_tuning(k, v), f"set_tuning {k}={v}")
     return lib
+
+
+def tune_pairs():
+    """(key, value) pairs of CGAN3D_TUNE."""
+    out = []
+    for kv in filter(None, os.environ.get("CGAN3D_TUNE", "").replace(" ", "").split(",")):
+        k, v = kv.split("=")
+        out.append((int(k), int(v)))
+    return out
+
+
+def py_tune(key: int, default: int) -> int:
+    """A host-schedule knob from CGAN3D_TUNE (keys >= 100; read when an engine is built)."""
+    for k, v in tune_pairs():
+        if k == key:
+            return v
+    return default
 
 
 def lib() -> C.CDLL:

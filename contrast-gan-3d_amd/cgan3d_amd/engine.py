@@ -175,6 +175,10 @@ class GeneratorPlan:
         output of other dims, as the reference's convolution arithmetic does (the whole-scan
         corrector then resizes it, eval/CCTAContrastCorrector.py:42-52)."""
         c0 = cfg.init_channels_out
+        # host-schedule knobs (CGAN3D_TUNE keys 100 / 101, sweeps): weight-grad hand-off group size,
+        # layers at the end of the backward whose weight grads stay on the main stream
+        self.wgrad_group = L.py_tune(100, WGRAD_GROUP)
+        self.wgrad_tail_main = L.py_tune(101, WGRAD_TAIL_MAIN)
         # the 2-D variants (experiments/conf_2D.py, is_2D): planar geometries on dims (1, H, W), f32
         self.planar = pl = bool(getattr(cfg, "is_2D", False))
         if pl and prec != L.PREC_F32:
@@ -227,7 +231,7 @@ class GeneratorPlan:
                 gw = ops.convt_wgrad_geom(n, ly.din, ly.dout, ly.cin, ly.cout, ly.k, ly.s, ly.p, planar=pl)
             gw = ops.with_prec(gw, prec)
             wt = P[f"{ly.name}.conv.weight"]
-            ps = self.packs_tail if li < WGRAD_TAIL_MAIN else self.packs
+            ps = self.packs_tail if li < self.wgrad_tail_main else self.packs
             gf, wf = ps.add(gf, wt, prec)
             gd, wd = ps.add(gd, wt, prec)
             self.wf.append(wf)
@@ -543,7 +547,7 @@ class GeneratorPlan:
                 x16 = None
             elif x16 is None or d16 is None:
                 x16 = d16 = None
-            main = i < WGRAD_TAIL_MAIN and self.side is not None
+            main = i < self.wgrad_tail_main and self.side is not None
             if ly.kind == "convt":  # ConvTranspose3d: the output-grad is the gathered operand
                 fn = (lambda g=self.geo_wgrad[i], a=self.dz[i], b=xin, w=G[wname], a16=d16, b16=x16, m=main:
                       self._wgrad(g, a, b, w, zeroed, main=m, gathered16=a16, aligned16=b16))
@@ -565,12 +569,12 @@ class GeneratorPlan:
             # consecutive ResNet-block layers hand their weight grads to the side stream in groups
             # of WGRAD_GROUP: one cross-stream wait per group (an event record costs the main stream
             # ~4 us, tools/launch_micro.hip) at the price of starting a wgrad one layer later
-            if not pending_done and (i == 0 or len(pending) >= WGRAD_GROUP or not resnet_pair(i)):
+            if not pending_done and (i == 0 or len(pending) >= self.wgrad_group or not resnet_pair(i)):
                 flush()
             if i == 0:
                 break
             self._input_grad(P, G, i)
-            if i == WGRAD_TAIL_MAIN and side_after is not None and self.side is not None:
+            if i == self.wgrad_tail_main and side_after is not None and self.side is not None:
                 # every gradient of layers >= i must be enqueued (side: weight grads; main: BatchNorm
                 # grads) and their weights' last reader, this input-grad, too: the caller's launches
                 # for those layers (their update) on the side stream, beside the main stream's tail.
@@ -1128,7 +1132,7 @@ class StepEngine:
         # GPU only (data parallelism all-reduces the whole gradient first).
         self.g_split = 0
         if self.G.side is not None and not self.dp:
-            pre = tuple(self.G.layers[li].name + "." for li in range(min(WGRAD_TAIL_MAIN, len(self.G.layers))))
+            pre = tuple(self.G.layers[li].name + "." for li in range(min(self.G.wgrad_tail_main, len(self.G.layers))))
             ar, off, lo, ok = self.g_arena, 0, None, True
             for nm, pp in zip(ar.names, ar.params):
                 tail = nm.startswith(pre) if pre else False
