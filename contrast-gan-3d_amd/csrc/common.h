@@ -230,6 +230,7 @@ int wgrad_bf16_launch(const cgan3d_conv_geom* g, const float* gathered, const fl
 bool k3m_ok(const cgan3d_conv_geom* g, const Epi& e);
 int k3m_launch(const cgan3d_conv_geom* g, const __bf16* wp, float* y, const Epi& e, hipStream_t st);
 void k3m_set(int v);
+void k3m_probe_set(int v);
 bool halo_ok(const cgan3d_conv_geom* g);         // w_packed == 2 and eligible
 bool halo_format_ok(const cgan3d_conv_geom* g);  // eligible ignoring w_packed
 long long halo_mblocks(const cgan3d_conv_geom* g);

@@ -663,6 +663,7 @@ extern "C" int cgan3d_set_tuning(int32_t key, int32_t value) {
   if (key == 14) { cout1_wave_set(value); return CGAN3D_OK; }
   if (key == 15) { k3m_set(value); return CGAN3D_OK; }
   if (key == 16) { wgrad_k3m_set(value); return CGAN3D_OK; }
+  if (key == 17) { k3m_probe_set(value); return CGAN3D_OK; }
   set_error("cgan3d_set_tuning: unknown key %d", key);
   return CGAN3D_EINVAL;
 }

@@ -12,3 +12,4 @@ done
 cd /tmp && export TMPDIR=/tmp
 rm -rf $R/gpurun_out/r4c_b128
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/r4c_b128 -o run -- python3 $R/bench.py --size 128 --batch 1 --precision f32 --steps 10 --warmup 2 --no-sub --no-cpu-baseline > $R/gpurun_out/r4c_b128.json 2> $R/gpurun_out/r4c_b128.err
+cd $R && timeout -k 10 200 python -u tools/bench_ops.py --case res_fwd_k3m res_dgrad_k3m res_wgrad --tune 17=0,1,2,3,4,8,12,7,15 > gpurun_out/k3m_probe.txt 2>&1
