@@ -104,21 +104,65 @@ __global__ __launch_bounds__(256, 1) void conv_k3m_kernel(K3mArgs a, const __bf1
   const int ox = txi * KM_TX - 1, oy = tyi * KM_TY - 1, oz = tzi * KM_TZ - 1;
   const int co0 = half * 32;
 
+  // ---- epilogue operands first (round 4): the output offsets of this lane's 16 voxels and the
+  // residual / BatchNorm-z loads, issued before the LDS-DMAs so the MFMA loop covers their round trip
+  // (the probe of tools/bench_ops.py: the epilogue took 3.1 / 3.9 us of a 10.6 / 11.6 us launch when
+  // they were issued after the MFMAs).  Loads are unconditional (an absent operand reads one dummy
+  // word, ignored later), so every launch issues the same 32 — all older than the DMAs, whose counted
+  // waits below therefore cover them too.
+  const int r = lane & 31, h = lane >> 5, c = co0 + r;
+  // km_row of row R = (i & 3) + 8 (i >> 2) + 4 h is x = i & 3, y = i >> 2, zz = (i >> 2 in {1, 2}) ^ h:
+  // one 32-bit voxel base per lane plus compile-time steps (k3m_ok bounds the volume below 2^31
+  // elements)
+  int oidx[16];
+  int nvalid = 0;
+  {
+    const int gx0 = txi * KM_TX, gy0 = tyi * KM_TY, gz0 = tzi * KM_TZ + 2 * wave;
+    const int vb = ((nb * a.d + gz0) * a.h + gy0) * a.w + gx0, plane = a.h * a.w;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int vx = i & 3, vy = i >> 2, vzz = ((vy == 1 || vy == 2) ? 1 : 0) ^ h;
+      const bool ok = gx0 + vx < a.w && gy0 + vy < a.h && gz0 + vzz < a.d;
+      oidx[i] = ok ? (vb + vzz * plane + vy * a.w + vx) * 64 + c : -1;
+      nvalid += ok;
+    }
+  }
+  const bool has_res = ep.residual != nullptr, mode4 = ep.fz.acc_mode == 4;
+  float resv[16], zv[16];
+  {
+    const float* rp = has_res ? ep.residual : reinterpret_cast<const float*>(g_km_zero);
+    const float* zp = mode4 ? ep.bn_z : reinterpret_cast<const float*>(g_km_zero);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      resv[i] = rp[has_res && oidx[i] >= 0 ? oidx[i] : 0];
+      zv[i] = zp[mode4 && oidx[i] >= 0 ? oidx[i] : 0];
+    }
+  }
+
   // ---- LDS-DMA: the halo (45 wave-instructions of 8 voxel rows), then the weights tap by tap (one
   // 8-channel quarter of every tap per wave).  Lane -> row 8i + lane / 8, position lane % 8, which
   // holds the row's logical granule position ^ swizzle.
   const unsigned lds0 = (unsigned)(uintptr_t)(lds_t)smem;  // LDS byte address of the operand area
   {
     const int p = lane & 7;
+    // row 8 i + lane / 8 (i = wave, wave + 4, ...): its (hx, hy, hz) stepped by 32 rows = (+2, +5, 0)
+    // with carries instead of divided out per piece; 32-bit element offsets (k3m_ok)
+    const int row0 = 8 * wave + (lane >> 3);
+    int hx = row0 % KM_HX, hy = (row0 / KM_HX) % KM_HY, hz = row0 / (KM_HX * KM_HY);
     for (int i = wave; i < ((a.probe & 1) ? 0 : KM_HROWS / 8); i += 4) {
-      const int row = 8 * i + (lane >> 3);
-      const int hx = row % KM_HX, hy = (row / KM_HX) % KM_HY, hz = row / (KM_HX * KM_HY);
       const int ix = ox + hx, iy = oy + hy, iz = oz + hz;
       const bool ok = (unsigned)ix < (unsigned)a.w && (unsigned)iy < (unsigned)a.h && (unsigned)iz < (unsigned)a.d;
       const int g = p ^ km_fa(hx, hy);
-      const void* src = ok ? (const void*)(x16 + ((((long long)nb * a.d + iz) * a.h + iy) * a.w + ix) * 64 + 8 * g)
+      const void* src = ok ? (const void*)(x16 + (((nb * a.d + iz) * a.h + iy) * a.w + ix) * 64 + 8 * g)
                            : (const void*)g_km_zero;
       km_dma16(src, __builtin_amdgcn_readfirstlane(lds0 + i * 1024));
+      hx += 2;
+      const int cx = hx >= KM_HX;
+      hx -= cx ? KM_HX : 0;
+      hy += 5 + cx;
+      const int cy = hy >= KM_HY;
+      hy -= cy ? KM_HY : 0;
+      hz += cy;
     }
     const int c = 8 * wave + (lane >> 3);  // channel row of the tap image
     const int cout = co0 + c;
@@ -134,7 +178,6 @@ __global__ __launch_bounds__(256, 1) void conv_k3m_kernel(K3mArgs a, const __bf1
   // ---- 27 taps x 4 K-steps of 16 channels = 108 MFMAs, in 4 groups of taps (0-2, 3-8, 9-17, 18-26)
   // behind counted DMA waits + a barrier; inside a group the A / B fragments of the next KM_PD steps
   // are in flight while an MFMA runs
-  const int r = lane & 31, h = lane >> 5;
   int lx, ly, lzz;
   km_row(r, lx, ly, lzz);
   const int hv0 = ((2 * wave + lzz) * KM_HY + ly) * KM_HX + lx;
@@ -190,47 +233,16 @@ __global__ __launch_bounds__(256, 1) void conv_k3m_kernel(K3mArgs a, const __bf1
     return;
   }
   // ---- epilogue: lane holds rows R = (i & 3) + 8 (i >> 2) + 4 h of channel co0 + r
-  const int C = 64, c = co0 + r;
+  const int C = 64;
   const float bias = ep.bias ? ep.bias[c] : 0.f;
-  // km_row of row R = (i & 3) + 8 (i >> 2) + 4 h is x = i & 3, y = i >> 2, zz = (i >> 2 in {1, 2}) ^ h:
-  // one 32-bit voxel base per lane plus compile-time steps (k3m_ok bounds the volume below 2^31
-  // elements); round 3's per-element km_row and 64-bit index math was ~500 VALU per wave
-  int oidx[16];
   float vals[16];
-  int nvalid = 0;
-  {
-    const int gx0 = txi * KM_TX, gy0 = tyi * KM_TY, gz0 = tzi * KM_TZ + 2 * wave;
-    const int vb = ((nb * a.d + gz0) * a.h + gy0) * a.w + gx0, plane = a.h * a.w;
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const int vx = i & 3, vy = i >> 2, vzz = ((vy == 1 || vy == 2) ? 1 : 0) ^ h;
-      const bool ok = gx0 + vx < a.w && gy0 + vy < a.h && gz0 + vzz < a.d;
-      oidx[i] = ok ? (vb + vzz * plane + vy * a.w + vx) * C + c : -1;
-      nvalid += ok;
-    }
-  }
-  float resv[16], zv[16];
-  const bool mode4 = ep.fz.acc_mode == 4;
-  // residual / BatchNorm-input loads: unconditional inside uniform branches, all issued before the
-  // first use (a per-element condition makes hipcc wait for each load on its own)
-  if (ep.residual) {
-#pragma unroll
-    for (int i = 0; i < 16; ++i) resv[i] = ep.residual[oidx[i] >= 0 ? oidx[i] : c];
-  } else {
-#pragma unroll
-    for (int i = 0; i < 16; ++i) resv[i] = 0.f;
-  }
-  if (mode4) {
-#pragma unroll
-    for (int i = 0; i < 16; ++i) zv[i] = ep.bn_z[oidx[i] >= 0 ? oidx[i] : c];
-  }
   const int act = ep.act;
   const float slope = ep.slope;
 #pragma unroll
   for (int i = 0; i < 16; ++i) {
     float v = acc[i] + bias;
     v = act == CGAN3D_ACT_RELU ? fmaxf(v, 0.f) : (act == CGAN3D_ACT_LRELU && v < 0.f ? v * slope : v);
-    v += resv[i];
+    v += has_res ? resv[i] : 0.f;
     vals[i] = oidx[i] >= 0 ? v : 0.f;
   }
 #pragma unroll
