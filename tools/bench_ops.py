@@ -62,7 +62,7 @@ def _cases(B=4, S=64):
         flops = 2.0 * n3 * dout[0] * dout[1] * dout[2] * cin * cout * 64
         return (lambda: ops.conv(geo, x, w, y)), flops
 
-    def res_k3m(dgrad):
+    def res_k3m(dgrad, reps=16, stats=True, res=True):
         """ResNet-block conv as the bf16 step issues it: bf16 shadow input, fp64 accumulator statistics
         (mode 3 forward with the residual + ReLU epilogue; mode 4 input-grad), conv_k3m_kernel"""
         geo0 = (ops.conv_dgrad_geom if dgrad else ops.conv_fwd_geom)(B, R3, R3, 64, 64, 3, 1, 1)
@@ -72,19 +72,24 @@ def _cases(B=4, S=64):
         ps.pack()
         x, y = t(B, *R3, 64), torch.empty(B, *R3, 64, device=dev)
         x16 = x.bfloat16()
-        acc = torch.zeros(16 * 2 * 64, device=dev, dtype=torch.float64)
+        acc = torch.zeros(reps * 2 * 64, device=dev, dtype=torch.float64)
+        rt = t(B, *R3, 64) if res else None
         if dgrad:
             z, ss, mi = t(B, *R3, 64), torch.rand(128, device=dev) + 0.5, torch.rand(128, device=dev) + 0.5
-            ep = ops.epilogue(x_bf16=x16, residual=t(B, *R3, 64), bn_z=z, bn_ss=ss, bn_mi=mi, bn_act=L.ACT_NONE,
-                              fuse=ops.BnFuse(acc, 4, 16))
+            ep = ops.epilogue(x_bf16=x16, residual=rt, bn_z=z if stats else None, bn_ss=ss, bn_mi=mi,
+                              bn_act=L.ACT_NONE, fuse=ops.BnFuse(acc, 4, reps) if stats else None)
         else:
-            ep = ops.epilogue(x_bf16=x16, act=L.ACT_RELU, residual=t(B, *R3, 64), fuse=ops.BnFuse(acc, 3, 16))
+            ep = ops.epilogue(x_bf16=x16, act=L.ACT_RELU, residual=rt, fuse=ops.BnFuse(acc, 3, reps) if stats else None)
         flops = 2.0 * B * r**3 * 64 * 64 * 27
         return (lambda: ops.conv(geo, x, w, y, ep)), flops
 
     return {
         "res_fwd_k3m": lambda: res_k3m(False),
         "res_dgrad_k3m": lambda: res_k3m(True),
+        "res_fwd_k3m_r64": lambda: res_k3m(False, reps=64),
+        "res_dgrad_k3m_r64": lambda: res_k3m(True, reps=64),
+        "res_fwd_k3m_nostat": lambda: res_k3m(False, stats=False),
+        "res_fwd_k3m_plain": lambda: res_k3m(False, stats=False, res=False),
         "crit_first": lambda: crit(1, 8, F3),
         "crit_m0": lambda: crit(8, 16, H3),
         "crit_m1": lambda: crit(16, 32, R3),
