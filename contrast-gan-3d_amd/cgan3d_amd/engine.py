@@ -45,7 +45,9 @@ Dims = Tuple[int, int, int]
 #                              (reflect-fold pass before the last BatchNorm backward), serial (no side
 #                              streams: a kernel trace then shows unshared durations), system_fence
 #                              (cross-stream event records with the system-scope fence, csrc/plan.hip),
-#                              fp32_store (the 64^3 16-channel z / dy in fp32 instead of bf16)
+#                              fp32_store (the 64^3 16-channel z / dy in fp32 instead of bf16),
+#                              event_record (a marker event per cross-stream wait instead of the
+#                              waited-on launch's own completion event, csrc/plan.hip)
 #   CGAN3D_FORCE_DP=1          the data-parallel path over a one-rank group (tools / tests)
 #   CGAN3D_COMM=native|torch|own   data-parallel collectives: RCCL from the launch plan on the process
 #                              group's communicator (default), torch.distributed host callables (the
@@ -53,7 +55,8 @@ Dims = Tuple[int, int, int]
 #   CGAN3D_G_BUCKET_BYTES      generator gradient bucket size under data parallelism
 #   CGAN3D_TUNE, CGAN3D_LIB_PATH   launch-shape knobs, another build of the library (_lib.py)
 #   CGAN3D_TRAINER_PLANS=0     the drop-in Trainer issues every step eagerly (no recorded plans)
-DEBUG_FLAGS = ("no_shadow", "keep_fp32", "no_bn_fuse", "no_bn_fold", "serial", "system_fence", "fp32_store")
+DEBUG_FLAGS = ("no_shadow", "keep_fp32", "no_bn_fuse", "no_bn_fold", "serial", "system_fence", "fp32_store",
+               "event_record")
 
 
 def debug(flag: str) -> bool:

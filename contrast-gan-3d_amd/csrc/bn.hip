@@ -638,7 +638,7 @@ __device__ __forceinline__ void acc_sums(const double* __restrict__ acc, int rep
     for (int u = 0; u < 8; ++u) s += v[u];
   }
   part[tid] = s;
-  __syncthreads();
+  lds_barrier();
   if (tid < P) {
     double t = 0.0;
     for (int k = 0; k < T; ++k) t += part[k * P + tid];
@@ -676,7 +676,7 @@ __global__ __launch_bounds__(256) void bn_apply_acc_kernel(const double* __restr
       if (RES) rp[u] = r4[i];
     }
   });
-  __syncthreads();
+  lds_barrier();
   for (int c = tid; c < C; c += blockDim.x) {
     const double mean = sums[c] / nvox, var = fmax(sums[C + c] / nvox - mean * mean, 0.0);
     const double invstd = 1.0 / sqrt(var + (double)eps);
@@ -693,7 +693,7 @@ __global__ __launch_bounds__(256) void bn_apply_acc_kernel(const double* __restr
       if (nbt && c == 0) *nbt += 1;
     }
   }
-  __syncthreads();
+  lds_barrier();
   const int C4 = C >> 2, cc = (tid % C4) * 4;
   f32x4 sc4, sf4;
 #pragma unroll
@@ -737,7 +737,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_acc_kernel(const double* __r
       dp[u] = load4<B16>(dy, i);
     }
   });
-  __syncthreads();
+  lds_barrier();
   for (int c = tid; c < C; c += blockDim.x) {
     co[c] = gamma[c] * mi[C + c];
     co[C + c] = (float)(sums[c] / nvox);
@@ -747,7 +747,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_acc_kernel(const double* __r
       if (dgamma) dgamma[c] = accumulate ? dgamma[c] + (float)sums[C + c] : (float)sums[C + c];
     }
   }
-  __syncthreads();
+  lds_barrier();
   const int C4 = C >> 2, cc = (tid % C4) * 4;
   f32x4 sc, sf, mean, inv, k0, k1, k2;
 #pragma unroll

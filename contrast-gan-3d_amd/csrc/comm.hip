@@ -119,7 +119,7 @@ extern "C" int cgan3d_allreduce_mean(void* comm, float* buf, int64_t n, void* st
     return hipSuccess;
   };
   if (g_rec != nullptr) {
-    g_rec->ops.emplace_back(issue);
+    g_rec->add(issue, st);
     return CGAN3D_OK;
   }
   if (issue() != hipSuccess) return CGAN3D_EHIP;

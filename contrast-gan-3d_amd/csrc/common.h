@@ -4,7 +4,9 @@
 
 #include <algorithm>
 #include <functional>
+#include <memory>
 #include <tuple>
+#include <unordered_map>
 #include <type_traits>
 #include <vector>
 #include <cstdarg>
@@ -24,6 +26,15 @@ namespace cg {
 struct Plan {
   std::vector<std::function<hipError_t()>> ops;
   std::vector<hipEvent_t> events;  // owned (cross-stream waits)
+  // Per stream, the completion-event slot of its last recorded op when that op is a kernel launch
+  // (null otherwise).  A cross-stream wait on that stream binds the event to the launch itself
+  // (hipExtLaunchKernel's stop event: the dispatch's own completion signal) instead of enqueueing
+  // a separate marker packet behind it — see cgan3d_stream_wait.
+  std::unordered_map<hipStream_t, std::shared_ptr<hipEvent_t>> tail;
+  void add(std::function<hipError_t()> op, hipStream_t st, std::shared_ptr<hipEvent_t> stop = nullptr) {
+    ops.push_back(std::move(op));
+    tail[st] = std::move(stop);
+  }
 };
 extern thread_local Plan* g_rec;
 
@@ -34,17 +45,20 @@ inline void launch(void (*k)(KArgs...), dim3 grid, dim3 block, size_t lds, hipSt
     return;
   }
   std::tuple<std::decay_t<KArgs>...> t(static_cast<std::decay_t<KArgs>>(args)...);
-  g_rec->ops.emplace_back([k, grid, block, lds, st, t]() mutable {
+  auto stop = std::make_shared<hipEvent_t>(nullptr);
+  g_rec->add([k, grid, block, lds, st, t, stop]() mutable {
     return std::apply([&](auto&... a) {
       void* argv[] = {static_cast<void*>(&a)...};
+      if (*stop != nullptr)
+        return hipExtLaunchKernel(reinterpret_cast<const void*>(k), grid, block, argv, lds, st, nullptr, *stop, 0);
       return hipLaunchKernel(reinterpret_cast<const void*>(k), grid, block, argv, lds, st);
     }, t);
-  });
+  }, st, stop);
 }
 
 inline hipError_t memset_async(void* p, int v, size_t bytes, hipStream_t st) {
   if (g_rec == nullptr) return hipMemsetAsync(p, v, bytes, st);
-  g_rec->ops.emplace_back([=]() { return hipMemsetAsync(p, v, bytes, st); });
+  g_rec->add([=]() { return hipMemsetAsync(p, v, bytes, st); }, st);
   return hipSuccess;
 }
 

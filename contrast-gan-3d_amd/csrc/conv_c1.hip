@@ -242,9 +242,9 @@ __global__ __launch_bounds__(256) void c1_wgrad_kernel(C1Args a, const float* __
   const int t1 = min(t0 + a.tiles_per_block, ntiles);
   if (t0 < t1) load(t0);
   for (int tile = t0; tile < t1; ++tile) {
-    __syncthreads();  // previous tile's LDS reads done
+    lds_barrier();  // previous tile's LDS reads done
     store();
-    __syncthreads();
+    lds_barrier();
     if (tile + 1 < t1) load(tile + 1);
     // one wave per SIMD: unrolled so that several voxels' LDS reads are in flight at once
 #pragma unroll 8

@@ -274,7 +274,7 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(GemmArgs a, const float*
   if (KT > 0) load_chunk(0);
   for (int kc0 = 0; kc0 < KT; kc0 += KC) {
     store_chunk();
-    __syncthreads();
+    lds_barrier();
     if (kc0 + KC < KT) load_chunk(kc0 + KC);  // prefetch: in flight during the MFMAs below
     if constexpr (PREC == 0) {
 #pragma unroll
@@ -296,7 +296,7 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(GemmArgs a, const float*
         acc[nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, bv, acc[nb], 0, 0, 0);
       }
     }
-    __syncthreads();
+    lds_barrier();
   }
 
   // ---- epilogue: lane holds rows wm*16 + 4g + j, column co0 + (wn*NBW + nb)*16 + r16
@@ -341,7 +341,7 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(GemmArgs a, const float*
     }
   }
   if (ep.stats || ep.bn_mode == 1) {  // (sum, M2 about the block mean, count): block-major or slab
-    __syncthreads();
+    lds_barrier();
     float* red = reinterpret_cast<float*>(As);  // [WM][BN]  (<= 4*64 floats)
     __shared__ float bmean[64];
     int cntv = 0;
@@ -354,7 +354,7 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(GemmArgs a, const float*
       sum += __shfl_xor(sum, 32, 64);
       if (g == 0) red[wm * BN + (wn * NBW + nb) * 16 + r16] = sum;
     }
-    __syncthreads();
+    lds_barrier();
     if (tid < BN) {
       float S = 0.f;
       for (int q = 0; q < WM; ++q) S += red[q * BN + tid];
@@ -364,7 +364,7 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(GemmArgs a, const float*
         else *bn_slot(ep, 0, a.cout, co0 + tid, blockIdx.x) = S;
       }
     }
-    __syncthreads();
+    lds_barrier();
 #pragma unroll
     for (int nb = 0; nb < NBW; ++nb) {
       const int cl = (wn * NBW + nb) * 16 + r16;
@@ -379,7 +379,7 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(GemmArgs a, const float*
       q += __shfl_xor(q, 32, 64);
       if (g == 0) red[wm * BN + cl] = q;
     }
-    __syncthreads();
+    lds_barrier();
     if (tid < BN) {
       float M2 = 0.f;
       for (int q = 0; q < WM; ++q) M2 += red[q * BN + tid];
@@ -410,7 +410,7 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(GemmArgs a, const float*
       p2[nb] += __shfl_xor(p2[nb], 16, 64);
       p2[nb] += __shfl_xor(p2[nb], 32, 64);
     }
-    __syncthreads();
+    lds_barrier();
     float* red = reinterpret_cast<float*>(As);  // [2][WM][BN]
     if (g == 0) {
 #pragma unroll
@@ -419,7 +419,7 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(GemmArgs a, const float*
         red[(WM + wm) * BN + (wn * NBW + nb) * 16 + r16] = p2[nb];
       }
     }
-    __syncthreads();
+    lds_barrier();
     if (tid < BN && co0 + tid < a.cout) {
       float S1 = 0.f, S2 = 0.f;
       for (int q = 0; q < WM; ++q) { S1 += red[q * BN + tid]; S2 += red[(WM + q) * BN + tid]; }

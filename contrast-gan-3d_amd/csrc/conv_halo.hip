@@ -115,7 +115,7 @@ __device__ __forceinline__ void halo_epilogue(const HaloArgs& a, f32x4 (&acc)[NT
   // replica of the fp64 accumulators this block adds into (cgan3d_bn_fuse)
   double* const facc = ep.fz.acc_mode ? ep.fz.acc_out + (long long)(blockIdx.x % ep.fz.reps) * 2 * a.cout : nullptr;
   if (ep.stats || ep.bn_mode == 1 || acc3) {  // (sum, M2 about the block mean, count): block-major or slab
-    __syncthreads();
+    lds_barrier();
     float* red = smemf;  // [4 waves][BN]
     __shared__ float bmean[64];
     int cntv = 0;
@@ -128,7 +128,7 @@ __device__ __forceinline__ void halo_epilogue(const HaloArgs& a, f32x4 (&acc)[NT
       sum += __shfl_xor(sum, 32, 64);
       if (g == 0) red[wave * BN + t * 16 + r16] = sum;
     }
-    __syncthreads();
+    lds_barrier();
     float S = 0.f;
     if (tid < BN) {
       S = red[tid] + red[BN + tid] + red[2 * BN + tid] + red[3 * BN + tid];
@@ -138,7 +138,7 @@ __device__ __forceinline__ void halo_epilogue(const HaloArgs& a, f32x4 (&acc)[NT
         else *bn_slot(ep, 0, a.cout, co0 + tid, blockIdx.x) = S;
       }
     }
-    __syncthreads();
+    lds_barrier();
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
       const int cl = t * 16 + r16;
@@ -153,7 +153,7 @@ __device__ __forceinline__ void halo_epilogue(const HaloArgs& a, f32x4 (&acc)[NT
       q += __shfl_xor(q, 32, 64);
       if (g == 0) red[wave * BN + cl] = q;
     }
-    __syncthreads();
+    lds_barrier();
     if (tid < BN) {
       const float M2 = red[tid] + red[BN + tid] + red[2 * BN + tid] + red[3 * BN + tid];
       if (co0 + tid < a.cout) {
@@ -191,7 +191,7 @@ __device__ __forceinline__ void halo_epilogue(const HaloArgs& a, f32x4 (&acc)[NT
       p2[t] += __shfl_xor(p2[t], 16, 64);
       p2[t] += __shfl_xor(p2[t], 32, 64);
     }
-    __syncthreads();
+    lds_barrier();
     float* red = smemf;  // [2][4 waves][BN]
     if (g == 0) {
 #pragma unroll
@@ -200,7 +200,7 @@ __device__ __forceinline__ void halo_epilogue(const HaloArgs& a, f32x4 (&acc)[NT
         red[(4 + wave) * BN + t * 16 + r16] = p2[t];
       }
     }
-    __syncthreads();
+    lds_barrier();
     if (tid < BN && co0 + tid < a.cout) {
       const float q0 = red[tid] + red[BN + tid] + red[2 * BN + tid] + red[3 * BN + tid];
       const float q1 = red[4 * BN + tid] + red[5 * BN + tid] + red[6 * BN + tid] + red[7 * BN + tid];

@@ -251,7 +251,9 @@ __global__ __launch_bounds__(256, 1) void conv_k3m_kernel(K3mArgs a, const __bf1
   if (!ep.fz.acc_mode) return;
   double* const facc = ep.fz.acc_out + (long long)(blockIdx.x % ep.fz.reps) * 2 * C;
   float* red = reinterpret_cast<float*>(smem);  // [2][4 waves][32]; the operands are dead after this barrier
-  __syncthreads();
+  // LDS-only barriers: the y stores above stay in flight (a __syncthreads would wait for them,
+  // putting the store latency in series with the statistics' atomics)
+  lds_barrier();
   if (ep.fz.acc_mode == 3) {  // (sum, M2 about the block mean) -> (sum, sum of squares) in fp64
     float s1 = 0.f;
 #pragma unroll
@@ -260,7 +262,7 @@ __global__ __launch_bounds__(256, 1) void conv_k3m_kernel(K3mArgs a, const __bf1
     int cnt = nvalid + __shfl_xor(nvalid, 32, 64);
     if (h == 0) red[wave * 32 + r] = s1;
     if (tid < 4 * 64 && lane == 0) red[256 + wave] = (float)cnt;
-    __syncthreads();
+    lds_barrier();
     float S = red[r] + red[32 + r] + red[64 + r] + red[96 + r];
     const float cn = red[256] + red[257] + red[258] + red[259];
     const float mean = cn > 0.f ? S / cn : 0.f;
@@ -272,7 +274,7 @@ __global__ __launch_bounds__(256, 1) void conv_k3m_kernel(K3mArgs a, const __bf1
     }
     q2 += __shfl_xor(q2, 32, 64);
     if (h == 0) red[128 + wave * 32 + r] = q2;
-    __syncthreads();
+    lds_barrier();
     if (tid < 32 && cn > 0.f) {
       const float M2 = red[128 + tid] + red[160 + tid] + red[192 + tid] + red[224 + tid];
       unsafeAtomicAdd(facc + co0 + tid, (double)S);
@@ -298,7 +300,7 @@ __global__ __launch_bounds__(256, 1) void conv_k3m_kernel(K3mArgs a, const __bf1
       red[wave * 32 + r] = p1;
       red[128 + wave * 32 + r] = p2;
     }
-    __syncthreads();
+    lds_barrier();
     if (tid < 32) {
       unsafeAtomicAdd(facc + co0 + tid, (double)(red[tid] + red[32 + tid] + red[64 + tid] + red[96 + tid]));
       unsafeAtomicAdd(facc + C + co0 + tid,

@@ -112,7 +112,7 @@ __global__ __launch_bounds__(256, 2) void k7m_n2w_kernel(K7Args a, const float* 
     xs[r * N_HWP + N_HW] = (__bf16)0.f;
     xs[r * N_HWP + N_HW + 1] = (__bf16)0.f;
   }
-  __syncthreads();
+  lds_barrier();
   bf16x8_k bv[N_PAIRS / 4];  // K-step ks: pair 4ks + g, tw 0..7, channel r16
 #pragma unroll
   for (int ks = 0; ks < N_PAIRS / 4; ++ks) bv[ks] = *reinterpret_cast<const bf16x8_k*>(wt + ((4 * ks + g) * C + r16) * 8);
@@ -170,7 +170,7 @@ __global__ __launch_bounds__(256, 2) void k7m_n2w_kernel(K7Args a, const float* 
   for (int tile = t0; tile < t1; ++tile) {
     int n, d0, h0, w0;
     tile_origin(tile, &n, &d0, &h0, &w0);
-    __syncthreads();  // previous tile's reads of us / red done
+    lds_barrier();  // previous tile's reads of us / red done
 #pragma unroll
     for (int k = 0; k < N_X_PER; ++k) {
       const int c = xc[k];
@@ -182,7 +182,7 @@ __global__ __launch_bounds__(256, 2) void k7m_n2w_kernel(K7Args a, const float* 
       }
     }
     if (tile + 1 < t1) load(tile + 1);  // in flight during this tile's MFMAs
-    __syncthreads();
+    lds_barrier();
     for (int i = tid; i < N_ROWS * 2; i += 256) {  // unfold (row, half of ow): 8 shifted windows
       const int r = i >> 1, hf = i & 1;
       const u32x4 lo = *reinterpret_cast<const u32x4*>(xs + r * N_HWP + 8 * hf);
@@ -199,7 +199,7 @@ __global__ __launch_bounds__(256, 2) void k7m_n2w_kernel(K7Args a, const float* 
         *reinterpret_cast<u32x4*>(us + r * N_US + (8 * hf + sft) * 8) = o;
       }
     }
-    __syncthreads();
+    lds_barrier();
     f32x4 acc[N_TH];
 #pragma unroll
     for (int r = 0; r < N_TH; ++r) acc[r] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -269,7 +269,7 @@ __global__ __launch_bounds__(256, 2) void k7m_n2w_kernel(K7Args a, const float* 
 #pragma unroll
         for (int jj = 0; jj < 4; ++jj) red[wave][4 * g + jj] = s1[jj];
       }
-      __syncthreads();
+      lds_barrier();
 #pragma unroll
       for (int jj = 0; jj < 4; ++jj) {
         const int c = 4 * g + jj;
@@ -288,12 +288,12 @@ __global__ __launch_bounds__(256, 2) void k7m_n2w_kernel(K7Args a, const float* 
       }
 #pragma unroll
       for (int jj = 0; jj < 4; ++jj) q[jj] = k7m_rowsum16(q[jj]);
-      __syncthreads();
+      lds_barrier();
       if (r16 == 0) {
 #pragma unroll
         for (int jj = 0; jj < 4; ++jj) red[wave][4 * g + jj] = q[jj];
       }
-      __syncthreads();
+      lds_barrier();
       if (tid < C) {
         const float tm2 = red[0][tid] + red[1][tid] + red[2][tid] + red[3][tid];
         const float nn = run_n + tn, delta = tmu - run_mean;
@@ -326,24 +326,24 @@ __global__ __launch_bounds__(256, 2) void k7m_n2w_kernel(K7Args a, const float* 
       fp1[jj] = k7m_rowsum16(fp1[jj]);
       fp2[jj] = k7m_rowsum16(fp2[jj]);
     }
-    __syncthreads();
+    lds_barrier();
     if (r16 == 0) {
 #pragma unroll
       for (int jj = 0; jj < 4; ++jj) red[wave][4 * g + jj] = fp1[jj];
     }
-    __syncthreads();
+    lds_barrier();
     double* fr = fb.acc ? fb.acc + (long long)(blockIdx.x % fb.reps) * 2 * C : nullptr;
     if (tid < C) {
       const float q = red[0][tid] + red[1][tid] + red[2][tid] + red[3][tid];
       if (fr) unsafeAtomicAdd(fr + tid, (double)q);
       else fb.part[(long long)tid * gridDim.x + blockIdx.x] = q;
     }
-    __syncthreads();
+    lds_barrier();
     if (r16 == 0) {
 #pragma unroll
       for (int jj = 0; jj < 4; ++jj) red[wave][4 * g + jj] = fp2[jj];
     }
-    __syncthreads();
+    lds_barrier();
     if (tid < C) {
       const float q = red[0][tid] + red[1][tid] + red[2][tid] + red[3][tid];
       if (fr) unsafeAtomicAdd(fr + C + tid, (double)q);
@@ -451,11 +451,11 @@ __global__ __launch_bounds__(256, 2) void k7m_w2n_kernel(K7Args a, const float* 
     for (int q = 0; q < 2; ++q) acc[q] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int half = 0; half < 2; ++half) {
-      __syncthreads();  // every wave done reading hs (and red) of the previous half / tile
+      lds_barrier();  // every wave done reading hs (and red) of the previous half / tile
       store();
       if (half == 0) load(tile, 1);
       else if (tile + 1 < t1) load(tile + 1, 0);
-      __syncthreads();
+      lds_barrier();
       {
         // software-pipelined: row prl + 1's four fragments are read from LDS while row prl's two
         // MFMAs run (the LDS latency is otherwise exposed on every row)
@@ -498,7 +498,7 @@ __global__ __launch_bounds__(256, 2) void k7m_w2n_kernel(K7Args a, const float* 
     // combine the 4 waves: lane holds out[ow = 4g + jj][(od, oh) = r16]
 #pragma unroll
     for (int jj = 0; jj < 4; ++jj) red[wave][(4 * g + jj) * 16 + r16] = acc[0][jj];
-    __syncthreads();
+    lds_barrier();
     int n, d0, h0, w0;
     tile_origin(tile, &n, &d0, &h0, &w0);
     const int m = tid >> 4, nn = tid & 15;  // ow_l = m, (odl, ohl) = nn
@@ -866,10 +866,10 @@ __global__ __launch_bounds__(256, 2) void k7m_wg_kernel(K7Args a, const float* _
   const int t0 = blockIdx.x * tiles_per_block, t1 = min(ntiles, t0 + tiles_per_block);
   if (t0 < t1) load(t0);
   for (int tile = t0; tile < t1; ++tile) {
-    __syncthreads();  // previous tile's reads of sx / as done
+    lds_barrier();  // previous tile's reads of sx / as done
     store();
     if (tile + 1 < t1) load(tile + 1);  // in flight during this tile's MFMAs
-    __syncthreads();
+    lds_barrier();
     for (int i = tid; i < G_ROWS_IN * 2; i += 256) {  // shifted copies of (row, half): 8 tw
       const int r = i >> 1, hf = i & 1;
       const u32x4 lo = *reinterpret_cast<const u32x4*>(xh + r * G_HWP + 8 * hf);
@@ -886,7 +886,7 @@ __global__ __launch_bounds__(256, 2) void k7m_wg_kernel(K7Args a, const float* _
         *reinterpret_cast<u32x4*>(sx + ((r * 8 + tw) * G_SXW + 8 * hf)) = o;
       }
     }
-    __syncthreads();
+    lds_barrier();
     // K-step ks = 32 voxels = tile rows 2ks, 2ks+1 (16 w each); lane group g: row 2ks + (g >> 1), w 8 (g & 1)
     // K-step ks = 32 voxels = tile rows 2ks, 2ks+1; lane group g: row 2ks + (g >> 1), w 8 (g & 1).
     // Two fragment sets in registers: K-step ks + 1's reads are in flight during ks's MFMAs.

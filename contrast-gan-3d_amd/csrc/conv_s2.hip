@@ -47,14 +47,14 @@ __device__ __forceinline__ void block_chan_sum(float (&v)[NT][4], float* red) {
     for (int j = 0; j < 4; ++j)
 #pragma unroll
       for (int m = 1; m < 16; m <<= 1) v[nt][j] += __shfl_xor(v[nt][j], m, 64);
-  __syncthreads();  // red is free
+  lds_barrier();  // red is free (LDS-only: outstanding output stores stay in flight)
   if (r16 == 0) {
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt)
 #pragma unroll
       for (int j = 0; j < 4; ++j) red[wave * NT * 16 + nt * 16 + 4 * g + j] = v[nt][j];
   }
-  __syncthreads();
+  lds_barrier();
 #pragma unroll
   for (int nt = 0; nt < NT; ++nt)
 #pragma unroll

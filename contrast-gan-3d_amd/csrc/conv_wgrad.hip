@@ -802,9 +802,9 @@ __global__ __launch_bounds__(512) void wgrad_s2_kernel(Ws2Args a, const float* _
   const int g = lane >> 4, q = (lane & 15) >> 2, pp = lane & 3;
   if (s0 < s1) load(s0);
   for (int sl = s0; sl < s1; ++sl) {
-    __syncthreads();  // the previous slab's fragment reads are done
+    lds_barrier();  // the previous slab's fragment reads are done
     store();
-    __syncthreads();
+    lds_barrier();
     if (sl + 1 < s1) load(sl + 1);
 #pragma unroll
     for (int u = 0; u < 4; ++u) {

@@ -33,6 +33,15 @@ static unsigned event_flags() {
   return f;
 }
 
+// CGAN3D_DEBUG=event_record: every cross-stream wait records its own marker event (A/B runs).
+static bool bind_disabled() {
+  static const bool off = [] {
+    const char* v = getenv("CGAN3D_DEBUG");
+    return v && strstr(v, "event_record") != nullptr;
+  }();
+  return off;
+}
+
 }  // namespace cg
 
 using namespace cg;
@@ -83,15 +92,30 @@ extern "C" int cgan3d_stream_wait(void* waiter, void* signaler) {
   if (w == s) return CGAN3D_OK;
   hipEvent_t ev;
   if (g_rec != nullptr) {
-    if (hipEventCreateWithFlags(&ev, event_flags()) != hipSuccess) {
-      set_error("cgan3d_stream_wait: hipEventCreate failed");
-      return CGAN3D_EHIP;
+    // Bind to the signaler's last launch when there is one: the waiter then depends on that
+    // dispatch's completion signal, and the signaler's queue carries no extra barrier packet (a
+    // hipEventRecord marker costs the signaling stream ~5 us of dispatch bubble on this pool; see
+    // DESIGN.md §5).  Anything else last on the signaler (a memset, a collective, a wait — whose
+    // dependencies must carry over transitively) keeps the recorded marker.
+    auto it = g_rec->tail.find(s);
+    std::shared_ptr<hipEvent_t> slot = (it != g_rec->tail.end() && !bind_disabled()) ? it->second : nullptr;
+    if (slot && *slot != nullptr) {
+      ev = *slot;
+    } else {
+      if (hipEventCreateWithFlags(&ev, event_flags()) != hipSuccess) {
+        set_error("cgan3d_stream_wait: hipEventCreate failed");
+        return CGAN3D_EHIP;
+      }
+      g_rec->events.push_back(ev);
+      if (slot) *slot = ev;
     }
-    g_rec->events.push_back(ev);
-    g_rec->ops.emplace_back([ev, w, s]() {
-      hipError_t e = hipEventRecord(ev, s);
-      return e != hipSuccess ? e : hipStreamWaitEvent(w, ev, 0);
-    });
+    if (slot)
+      g_rec->add([ev, w]() { return hipStreamWaitEvent(w, ev, 0); }, w);
+    else
+      g_rec->add([ev, w, s]() {
+        hipError_t e = hipEventRecord(ev, s);
+        return e != hipSuccess ? e : hipStreamWaitEvent(w, ev, 0);
+      }, w);
     return CGAN3D_OK;
   }
   // eager: a small ring (an event may be re-recorded once the wait on it has been enqueued)
