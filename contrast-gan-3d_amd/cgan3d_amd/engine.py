@@ -594,7 +594,7 @@ class GeneratorPlan:
         dL/dh_{r+1}), with layer i - 1's BatchNorm backward statistics."""
         ly = self.layers[i]
         ep = self._bn_grad_epi(i - 1, fused=self.ac_b[i - 1])
-        ep.residual = self.dy[i + 1] if ly.name.endswith("block0") else None
+        ep.residual = self.dys[i + 1] if ly.name.endswith("block0") else None  # bf16 when layer i + 1 keeps it
         ep.x_bf16 = self.dz16[i] if BN_FUSED_BWD else None  # only the slab backward writes it
         ops.conv(self.geo_dgrad[i], self.dz[i], self.wd[i], self.dys[i - 1], ep)
 

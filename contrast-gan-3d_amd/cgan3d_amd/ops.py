@@ -491,10 +491,11 @@ def conv(g: ConvGeom, x: torch.Tensor, w: torch.Tensor, y: torch.Tensor, ep: Opt
         _need(w, _w_extent(g), "conv w", exact=False)
     ny = _vox_out(g) * g.cout
     out16 = y is not None and y.dtype == torch.bfloat16
-    if out16:  # the generator's 64^3 16-channel tensors kept in bf16 (include/cgan3d.h out_bf16)
+    res16 = ep is not None and ep.residual is not None and ep.residual.dtype == torch.bfloat16
+    if out16 or res16:  # bf16 storage of BatchNorm inputs / gradients (include/cgan3d.h out_bf16)
         if ep is None or not out_bf16_ok(g):
-            raise ValueError("conv: a bf16 output only where cgan3d_conv3d_out_bf16_ok (with an epilogue)")
-        ep.out_bf16 = 1
+            raise ValueError("conv: a bf16 output / residual only where cgan3d_conv3d_out_bf16_ok (with an epilogue)")
+        ep.out_bf16 = (1 if out16 else 0) | (2 if res16 else 0)
     elif ep is not None:
         ep.out_bf16 = 0
     _need(y, ny, "conv y", dtype=y.dtype if out16 else torch.float32)
@@ -503,7 +504,7 @@ def conv(g: ConvGeom, x: torch.Tensor, w: torch.Tensor, y: torch.Tensor, ep: Opt
             _need(ep.bias, g.cout, "conv bias")
         for nm in ("residual", "mask_src", "minuend", "out2"):
             if getattr(ep, nm) is not None:
-                _need(getattr(ep, nm), ny, f"conv {nm}")
+                _need(getattr(ep, nm), ny, f"conv {nm}", dtype=torch.bfloat16 if nm == "residual" and res16 else torch.float32)
         if ep.stats is not None:  # the critic first-layer input-grad: per-block sums of squares
             _need(ep.stats, sumsq_blocks(g) or stats_floats(g), "conv stats", exact=False)
         if ep.x_bf16 is not None:

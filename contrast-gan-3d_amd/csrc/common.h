@@ -150,7 +150,8 @@ struct Epi {
   const __bf16* x16;  // optional bf16 shadow of the conv input
   int bn_fold;        // mode 2 over a reflect-padded k7 input-grad grid (cgan3d_epilogue.bn_fold)
   BnFuse fz;          // all-zero unless cgan3d_epilogue.fuse is given
-  int out16;          // cgan3d_epilogue.out_bf16: y and bn_z are bf16 (k7m n2w and S2T launches only)
+  int out16;          // cgan3d_epilogue.out_bf16 bit 0: y and bn_z are bf16 (k7m n2w, S2T, conv_k3m launches)
+  int res16;          // bit 1: the residual is bf16 (conv_k3m only)
 };
 
 // c ? v : 0 for a just-loaded v, by an integer mask: the compiler turns a select whose operand is a
@@ -242,9 +243,13 @@ int wgrad_bf16_launch(const cgan3d_conv_geom* g, const float* gathered, const fl
                       hipStream_t st);
 // ResNet-block convs with every operand in LDS, 32x32x16 MFMA (conv_k3m.hip)
 bool k3m_ok(const cgan3d_conv_geom* g, const Epi& e);
+bool k3m_geom_ok(const cgan3d_conv_geom* g);
+bool k3m_route(const cgan3d_conv_geom* g);
 int k3m_launch(const cgan3d_conv_geom* g, const __bf16* wp, float* y, const Epi& e, hipStream_t st);
 void k3m_set(int v);
 void k3m_probe_set(int v);
+void c1_groups_set(int v);
+void wgrad_k3m_probe_set(int v);
 bool halo_ok(const cgan3d_conv_geom* g);         // w_packed == 2 and eligible
 bool halo_format_ok(const cgan3d_conv_geom* g);  // eligible ignoring w_packed
 long long halo_mblocks(const cgan3d_conv_geom* g);

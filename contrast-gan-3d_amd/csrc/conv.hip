@@ -522,16 +522,18 @@ static Epi to_epi(const cgan3d_epilogue* ep) {
     if (const cgan3d_bn_fuse* f = ep->fuse) {
       e.fz.acc_out = f->acc_out; e.fz.acc_mode = f->acc_mode; e.fz.reps = f->reps;
     }
-    e.out16 = ep->out_bf16 ? 1 : 0;
+    e.out16 = ep->out_bf16 & 1;
+    e.res16 = (ep->out_bf16 >> 1) & 1;
   }
   return e;
 }
 
 // the launches that honour cgan3d_epilogue.out_bf16 (their dispatch conditions: the S2T kernel from
-// halo_launch, the 1 -> 16 k7 MFMA kernel from k7_try_fwd)
+// halo_launch, the 1 -> 16 k7 MFMA kernel from k7_try_fwd, the ResNet-block kernel conv_k3m)
 extern "C" int32_t cgan3d_conv3d_out_bf16_ok(const cgan3d_conv_geom* g) {
   if (!g || validate(g, "cgan3d_conv3d_out_bf16_ok") || g->planar) return 0;
   if (g->w_packed == 2 && s2_kind(g) == 2) return 1;
+  if (k3m_route(g)) return 1;
   return g->w_packed == 0 && k7m_n2w_ok(g) ? 1 : 0;
 }
 
@@ -589,10 +591,20 @@ extern "C" int cgan3d_conv3d_fwd(const cgan3d_conv_geom* g, const float* x, cons
   CG_CHECK_ARG(x && w && y, "cgan3d_conv3d_fwd: null pointer");
   Epi e = to_epi(ep);
   if (int rc = check_fuse(g, e)) return rc;
-  CG_CHECK_ARG(!e.out16 || cgan3d_conv3d_out_bf16_ok(g), "cgan3d_conv3d_fwd: out_bf16 not taken by this launch");
-  CG_CHECK_ARG(!e.out16 || (!e.bias && !e.residual && !e.mask_src && !e.minuend && !e.out2 && !e.stats &&
-                            !e.bn_mode && e.act == CGAN3D_ACT_NONE),
-               "cgan3d_conv3d_fwd: out_bf16 with a plain epilogue and accumulator statistics only");
+  CG_CHECK_ARG(!ep || (ep->out_bf16 >= 0 && ep->out_bf16 <= 3), "cgan3d_conv3d_fwd: out_bf16 must be 0..3");
+  CG_CHECK_ARG(!(e.out16 || e.res16) || cgan3d_conv3d_out_bf16_ok(g),
+               "cgan3d_conv3d_fwd: out_bf16 not taken by this launch");
+  if (k3m_route(g)) {  // the ResNet-block kernel: any of its epilogues, bf16 input shadow
+    CG_CHECK_ARG(!(e.out16 || e.res16) || k3m_ok(g, e),
+                 "cgan3d_conv3d_fwd: out_bf16 on the ResNet-block geometry needs the conv_k3m epilogue (x_bf16, "
+                 "fused statistics or none)");
+    CG_CHECK_ARG(!e.res16 || e.residual, "cgan3d_conv3d_fwd: out_bf16 bit 1 without a residual");
+  } else {
+    CG_CHECK_ARG(!e.res16, "cgan3d_conv3d_fwd: a bf16 residual only on the ResNet-block kernel");
+    CG_CHECK_ARG(!e.out16 || (!e.bias && !e.residual && !e.mask_src && !e.minuend && !e.out2 && !e.stats &&
+                              !e.bn_mode && e.act == CGAN3D_ACT_NONE),
+                 "cgan3d_conv3d_fwd: out_bf16 with a plain epilogue and accumulator statistics only");
+  }
   CG_CHECK_ARG(!(e.out2 && (!e.minuend || g->cout != 1)), "cgan3d_conv3d_fwd: out2 needs minuend and cout==1");
   CG_CHECK_ARG(e.bn_mode >= 0 && e.bn_mode <= 2, "cgan3d_conv3d_fwd: bn_mode must be 0, 1 or 2");
   CG_CHECK_ARG(e.bn_mode != 2 || (e.bn_z && e.bn_ss && e.bn_mi), "cgan3d_conv3d_fwd: bn_mode 2 needs bn_z, bn_ss, bn_mi");

@@ -31,25 +31,31 @@ __device__ __forceinline__ void c1_stage_window(const C1Args& a, const float* __
   using namespace c1;
   constexpr int N = WZ * WY * WX, PER = (N + 255) / 256;
   const int iz0 = 2 * oz0 - 1, iy0 = 2 * oy0 - 1, ix0 = 2 * ox0 - 1;
+  // unconditional loads (clamped index, value masked after: no branch per load), 32-bit offsets
+  // within the sample (a sample's volume is far below 2^31 voxels)
+  const float* xn = x + (long long)nb * a.di * a.hi * a.wi;
   float v[PER];
+  unsigned okm = 0;
 #pragma unroll
   for (int k = 0; k < PER; ++k) {
     const int i = threadIdx.x + 256 * k;
     const int hx = i % WX, r = i / WX, hy = r % WY, hz = r / WY;
     const int iz = iz0 + hz, iy = iy0 + hy, ix = ix0 + hx;
     const bool ok = i < N && (unsigned)iz < (unsigned)a.di && (unsigned)iy < (unsigned)a.hi && (unsigned)ix < (unsigned)a.wi;
-    v[k] = ok ? x[(((long long)nb * a.di + iz) * a.hi + iy) * a.wi + ix] : 0.f;
+    v[k] = xn[ok ? (iz * a.hi + iy) * a.wi + ix : 0];
+    okm |= ok ? 1u << k : 0u;
   }
 #pragma unroll
   for (int k = 0; k < PER; ++k) {
     const int i = threadIdx.x + 256 * k;
-    if (i >= N) break;
     const int hx = i % WX, r = i / WX, hy = r % WY, hz = r / WY;
-    xs[hz * PS + hy * RS + hx] = v[k];
+    if (k + 1 < PER || i < N) xs[hz * PS + hy * RS + hx] = keep_if((okm >> k) & 1u, v[k]);
   }
 }
 
 typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+__device__ __attribute__((aligned(16))) float g_c1_zero[8];  // source of the absent epilogue operands
 
 __device__ __forceinline__ void c1_tile(const C1Args& a, int t, int* nb, int* oz0, int* oy0, int* ox0) {
   const int tx = t % a.tx, r = t / a.tx, ty = r % a.ty, r2 = r / a.ty, tz = r2 % a.tz;
@@ -66,10 +72,28 @@ __global__ __launch_bounds__(256) void c1_fwd_kernel(C1Args a, const float* __re
   int nb, oz0, oy0, ox0;
   c1_tile(a, blockIdx.x, &nb, &oz0, &oy0, &ox0);
   const int tid = threadIdx.x;
-  for (int i = tid; i < 512; i += 256) wsh[i] = w[(i & 7) * a.w_sb + (i >> 3)];
+  // both weight loads in flight with the window's (a loop here waited for each in turn)
+  const float wv0 = w[(tid & 7) * a.w_sb + (tid >> 3)], wv1 = w[(tid & 7) * a.w_sb + ((tid + 256) >> 3)];
   c1_stage_window(a, x, nb, oz0, oy0, ox0, xs);
+  wsh[tid] = wv0;
+  wsh[tid + 256] = wv1;
   __syncthreads();
   const int lz = tid >> 7, ly = (tid >> 4) & 7, lx = tid & 15;
+  // epilogue operands before the taps (unconditional loads, absent ones from a zero dummy): bias,
+  // the LeakyReLU mask of the penalty's forward-mode chain
+  const int oz = oz0 + lz, oy = oy0 + ly, ox = ox0 + lx;
+  const bool inside = oz < a.do_ && oy < a.ho && ox < a.wo;
+  const long long o = inside ? (((long long)nb * a.do_ + oz) * a.ho + oy) * a.wo + ox : 0;
+  const bool has_bias = ep.bias != nullptr, has_mask = ep.mask_src != nullptr;
+  // integer selects, the pointers made opaque: a select between two load addresses becomes a
+  // branch around the load otherwise
+  uintptr_t ba = has_bias ? (uintptr_t)ep.bias : (uintptr_t)g_c1_zero;
+  uintptr_t ma = has_mask ? (uintptr_t)(ep.mask_src + o * 8) : (uintptr_t)g_c1_zero;
+  asm volatile("" : "+s"(ba));
+  asm volatile("" : "+v"(ma));
+  const f32x4* bp = reinterpret_cast<const f32x4*>(ba);
+  const f32x4* mp = reinterpret_cast<const f32x4*>(ma);
+  const f32x4 b0 = bp[0], b1 = bp[1], m0 = mp[0], m1 = mp[1];
   f32x2 acc[4];  // channel pairs (2j, 2j + 1): packed fp32 FMA
 #pragma unroll
   for (int j = 0; j < 4; ++j) acc[j] = f32x2{0.f, 0.f};
@@ -89,24 +113,19 @@ __global__ __launch_bounds__(256) void c1_fwd_kernel(C1Args a, const float* __re
         acc[2] += vx * f32x2{w1[0], w1[1]} + vy * f32x2{w3[0], w3[1]};
         acc[3] += vx * f32x2{w1[2], w1[3]} + vy * f32x2{w3[2], w3[3]};
       }
-  const int oz = oz0 + lz, oy = oy0 + ly, ox = ox0 + lx;
-  if (oz >= a.do_ || oy >= a.ho || ox >= a.wo) return;
-  const long long o = (((long long)nb * a.do_ + oz) * a.ho + oy) * a.wo + ox;
+  // branch-free epilogue: uniform selects
+  const bool relu = ep.act == CGAN3D_ACT_RELU, lrelu = ep.act == CGAN3D_ACT_LRELU;
+  const float slope = ep.slope;
   float v[8];
-  f32x4 m0 = {1.f, 1.f, 1.f, 1.f}, m1 = m0;
-  if (ep.mask_src) {
-    m0 = *reinterpret_cast<const f32x4*>(ep.mask_src + o * 8);
-    m1 = *reinterpret_cast<const f32x4*>(ep.mask_src + o * 8 + 4);
-  }
 #pragma unroll
   for (int b = 0; b < 8; ++b) {
-    float t = acc[b >> 1][b & 1] + (ep.bias ? ep.bias[b] : 0.f);
-    if (ep.act == CGAN3D_ACT_RELU) t = fmaxf(t, 0.f);
-    else if (ep.act == CGAN3D_ACT_LRELU) t = t > 0.f ? t : t * ep.slope;
+    float t = acc[b >> 1][b & 1] + (b < 4 ? b0[b & 3] : b1[b & 3]);
+    t = relu ? fmaxf(t, 0.f) : t;
+    t = (lrelu & (t < 0.f)) ? t * slope : t;
     const float m = b < 4 ? m0[b & 3] : m1[b & 3];
-    if (ep.mask_src) t = m > 0.f ? t : t * ep.slope;
-    v[b] = t;
+    v[b] = (has_mask & !(m > 0.f)) ? t * slope : t;
   }
+  if (!inside) return;
   *reinterpret_cast<f32x4*>(y + o * 8) = f32x4{v[0], v[1], v[2], v[3]};
   *reinterpret_cast<f32x4*>(y + o * 8 + 4) = f32x4{v[4], v[5], v[6], v[7]};
 }
@@ -187,87 +206,110 @@ __global__ __launch_bounds__(256) void c1_dgrad_kernel(C1Args a, const float* __
   }
 }
 
-// weight-grad: dw[b][t] += sum_{n,o} x[2o - 1 + t] * dz[o][b]; lane = tap, 4 waves split a tile's
-// voxels; tiles_per_block tiles per block, one atomic add per (b, t) per block
-__global__ __launch_bounds__(256) void c1_wgrad_kernel(C1Args a, const float* __restrict__ x,
-                                                       const float* __restrict__ dz, float* dw, int ntiles) {
+// weight-grad: dw[b][t] += sum_{n,o} x[2o - 1 + t] * dz[o][b]; lane = tap.  G groups of 4 waves per
+// block, each reducing its own tiles (tiles t0 + g, t0 + g + G, ...) through its own LDS window, the
+// 4 waves of a group splitting a tile's voxels; one atomic add per (b, t) per block at the end (every
+// block adds into the same 512 words, so fewer, longer blocks; the groups give each SIMD G waves to
+// hide the LDS latency of the voxel loop with).  The next tile's window + dz stay in registers while
+// the current one is reduced.
+template <int G>
+__global__ __launch_bounds__(256 * G) void c1_wgrad_kernel(C1Args a, const float* __restrict__ x,
+                                                           const float* __restrict__ dz, float* dw, int ntiles) {
   using namespace c1;
-  __shared__ __attribute__((aligned(16))) float xs[WIN];
-  __shared__ __attribute__((aligned(16))) float gs[TZ * TY * TX * 8];
-  __shared__ float red[4][8][65];
+  __shared__ __attribute__((aligned(16))) float xs_all[G][WIN];
+  __shared__ __attribute__((aligned(16))) float gs_all[G][TZ * TY * TX * 8];
+  __shared__ float red[4 * G][8][65];
   constexpr int N = WZ * WY * WX, PER = (N + 255) / 256;
-  const int tid = threadIdx.x, t = tid & 63, vg = tid >> 6;
+  const int tid = threadIdx.x & 255, grp = threadIdx.x >> 8, t = tid & 63, vg = tid >> 6;
   const int td = t >> 4, th = (t >> 2) & 3, tw = t & 3;
-  // next tile's window + dz held in registers while the current tile is reduced (the staging
-  // latency of tile k+1 hides behind tile k's FMAs; one atomic per (b, t) per block at the end:
-  // every block adds into the same 512 words, so fewer, longer blocks)
+  float* const xs = xs_all[grp];
+  float* const gs = gs_all[grp];
   float xv_n[PER];
   f32x4 gv_n[2];
+  unsigned okm = 0;  // validity of the staged values (unconditional loads, masked at the LDS store)
   auto load = [&](int tile) {
     int nb, oz0, oy0, ox0;
     c1_tile(a, tile, &nb, &oz0, &oy0, &ox0);
     const int iz0 = 2 * oz0 - 1, iy0 = 2 * oy0 - 1, ix0 = 2 * ox0 - 1;
+    const float* xn = x + (long long)nb * a.di * a.hi * a.wi;
+    const float* gn = dz + (long long)nb * a.do_ * a.ho * a.wo * 8;
+    okm = 0;
 #pragma unroll
     for (int k = 0; k < PER; ++k) {
       const int i = tid + 256 * k;
       const int hx = i % WX, r = i / WX, hy = r % WY, hz = r / WY;
       const int iz = iz0 + hz, iy = iy0 + hy, ix = ix0 + hx;
       const bool ok = i < N && (unsigned)iz < (unsigned)a.di && (unsigned)iy < (unsigned)a.hi && (unsigned)ix < (unsigned)a.wi;
-      xv_n[k] = ok ? x[(((long long)nb * a.di + iz) * a.hi + iy) * a.wi + ix] : 0.f;
+      xv_n[k] = xn[ok ? (iz * a.hi + iy) * a.wi + ix : 0];
+      okm |= ok ? 1u << k : 0u;
     }
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
       const int i = tid + 256 * k, h = i & 1, v = i >> 1;
       const int oz = oz0 + (v >> 7), oy = oy0 + ((v >> 4) & 7), ox = ox0 + (v & 15);
-      gv_n[k] = (oz < a.do_ && oy < a.ho && ox < a.wo)
-                    ? *reinterpret_cast<const f32x4*>(dz + ((((long long)nb * a.do_ + oz) * a.ho + oy) * a.wo + ox) * 8 + 4 * h)
-                    : f32x4{0.f, 0.f, 0.f, 0.f};
+      const bool ok = oz < a.do_ && oy < a.ho && ox < a.wo;
+      gv_n[k] = *reinterpret_cast<const f32x4*>(gn + (ok ? ((oz * a.ho + oy) * a.wo + ox) * 8 + 4 * h : 0));
+      okm |= ok ? 1u << (PER + k) : 0u;
     }
   };
   auto store = [&]() {
 #pragma unroll
     for (int k = 0; k < PER; ++k) {
       const int i = tid + 256 * k;
-      if (i >= N) break;
       const int hx = i % WX, r = i / WX, hy = r % WY, hz = r / WY;
-      xs[hz * PS + hy * RS + hx] = xv_n[k];
+      if (k + 1 < PER || i < N) xs[hz * PS + hy * RS + hx] = keep_if((okm >> k) & 1u, xv_n[k]);
     }
 #pragma unroll
-    for (int k = 0; k < 2; ++k) *reinterpret_cast<f32x4*>(gs + (tid + 256 * k) * 4) = gv_n[k];
+    for (int k = 0; k < 2; ++k) {
+      const bool ok = (okm >> (PER + k)) & 1u;
+      f32x4 g;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) g[e] = keep_if(ok, gv_n[k][e]);
+      *reinterpret_cast<f32x4*>(gs + (tid + 256 * k) * 4) = g;
+    }
   };
   f32x2 acc[4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) acc[j] = f32x2{0.f, 0.f};
   const int t0 = blockIdx.x * a.tiles_per_block;
   const int t1 = min(t0 + a.tiles_per_block, ntiles);
-  if (t0 < t1) load(t0);
-  for (int tile = t0; tile < t1; ++tile) {
+  const int iters = (t1 - t0 + G - 1) / G;  // block-uniform: every group meets every barrier
+  if (t0 + grp < t1) load(t0 + grp);
+  for (int it = 0; it < iters; ++it) {
+    const int tile = t0 + it * G + grp;
     lds_barrier();  // previous tile's LDS reads done
-    store();
+    if (tile < t1) store();
     lds_barrier();
-    if (tile + 1 < t1) load(tile + 1);
-    // one wave per SIMD: unrolled so that several voxels' LDS reads are in flight at once
+    if (tile + G < t1) load(tile + G);
+    if (tile < t1) {
 #pragma unroll 8
-    for (int v = vg * 64; v < vg * 64 + 64; ++v) {
-      const int lz = v >> 7, ly = (v >> 4) & 7, lx = v & 15;
-      const float xv = xs[(2 * lz + td) * PS + (2 * ly + th) * RS + 2 * lx + tw];
-      const f32x4 g0 = *reinterpret_cast<const f32x4*>(gs + v * 8), g1 = *reinterpret_cast<const f32x4*>(gs + v * 8 + 4);
-      const f32x2 x2 = {xv, xv};
-      acc[0] += x2 * f32x2{g0[0], g0[1]};
-      acc[1] += x2 * f32x2{g0[2], g0[3]};
-      acc[2] += x2 * f32x2{g1[0], g1[1]};
-      acc[3] += x2 * f32x2{g1[2], g1[3]};
+      for (int v = vg * 64; v < vg * 64 + 64; ++v) {
+        const int lz = v >> 7, ly = (v >> 4) & 7, lx = v & 15;
+        const float xv = xs[(2 * lz + td) * PS + (2 * ly + th) * RS + 2 * lx + tw];
+        const f32x4 g0 = *reinterpret_cast<const f32x4*>(gs + v * 8), g1 = *reinterpret_cast<const f32x4*>(gs + v * 8 + 4);
+        const f32x2 x2 = {xv, xv};
+        acc[0] += x2 * f32x2{g0[0], g0[1]};
+        acc[1] += x2 * f32x2{g0[2], g0[3]};
+        acc[2] += x2 * f32x2{g1[0], g1[1]};
+        acc[3] += x2 * f32x2{g1[2], g1[3]};
+      }
     }
   }
+  const int w = threadIdx.x >> 6;
 #pragma unroll
-  for (int b = 0; b < 8; ++b) red[vg][b][t] = acc[b >> 1][b & 1];
+  for (int b = 0; b < 8; ++b) red[w][b][t] = acc[b >> 1][b & 1];
   __syncthreads();
-  for (int i = tid; i < 512; i += 256) {
+  for (int i = threadIdx.x; i < 512; i += 256 * G) {
     const int b = i >> 6, tt = i & 63;
-    const float s = red[0][b][tt] + red[1][b][tt] + red[2][b][tt] + red[3][b][tt];
+    float s = 0.f;
+#pragma unroll
+    for (int k = 0; k < 4 * G; ++k) s += red[k][b][tt];
     atomicAdd(dw + b * a.w_sb + tt, s);
   }
 }
+
+static int g_c1_groups = 2;
+void c1_groups_set(int v) { g_c1_groups = v; }
 
 // roles this file takes (geometries as built by cgan3d_amd/ops.py)
 bool c1_fwd_ok(const cgan3d_conv_geom* g) {
@@ -317,9 +359,14 @@ int c1_dgrad_launch(const cgan3d_conv_geom* g, const float* dz, const float* w, 
 int c1_wgrad_launch(const cgan3d_conv_geom* g, const float* x, const float* dz, float* dw, hipStream_t st) {
   C1Args a = c1_args(g);
   const int ntiles = a.n * a.tz * a.ty * a.tx;
-  // <= ~256 blocks adding into dW (measured: 1024 blocks of one tile each, 36 -> 47 us at 64^3 B=4)
-  a.tiles_per_block = std::max(1, std::min(8, ntiles / 256));
-  ::cg::launch(c1_wgrad_kernel, dim3(ceil_div(ntiles, a.tiles_per_block)), dim3(256), 0, st, a, x, dz, dw, ntiles);
+  // <= ~256 blocks adding into dW (measured: 1024 blocks of one tile each, 36 -> 47 us at 64^3 B=4);
+  // two tile groups per block when there are tiles for both (cgan3d_set_tuning key 18: 1 forces one)
+  const int G = (g_c1_groups == 1 || ntiles < 512) ? 1 : 2;
+  a.tiles_per_block = std::max(1, std::min(8 * G, ntiles / 256));
+  if (G == 2)
+    ::cg::launch(c1_wgrad_kernel<2>, dim3(ceil_div(ntiles, a.tiles_per_block)), dim3(512), 0, st, a, x, dz, dw, ntiles);
+  else
+    ::cg::launch(c1_wgrad_kernel<1>, dim3(ceil_div(ntiles, a.tiles_per_block)), dim3(256), 0, st, a, x, dz, dw, ntiles);
   return CGAN3D_OK;
 }
 

@@ -60,6 +60,8 @@ __host__ __device__ inline int halo_extent(const ClassTaps& c, int s, int transp
   return transposed ? HT + c.omax - c.omin : (HT - 1) * s + c.omax + 1;
 }
 
+__device__ __attribute__((aligned(16))) float g_halo_zero[4];  // source of the absent epilogue operands
+
 // Epilogue of the halo-tiled kernels: lane holds tile rows wave*16 + 4g + jj (row_out: output
 // voxel of each of the 64 tile rows, -1 outside) for channel co0 + t*16 + r16; bias, activation,
 // mask, residual, store, BatchNorm statistics (block-major partials, or slab modes 1 / 2).
@@ -79,35 +81,44 @@ __device__ __forceinline__ void halo_epilogue(const HaloArgs& a, f32x4 (&acc)[NT
     rowo[jj] = row_out[wave * 16 + 4 * g + jj];
     rowv[jj] = rowo[jj] >= 0;
   }
-  // residual / BatchNorm-input operands: every load issued before the first use
+  // residual / BatchNorm-input / mask / bias operands: every load issued before the first use,
+  // unconditionally (clamped offsets, absent operands read from a zero dummy through an opaque
+  // pointer: a select between load addresses, or a load under a condition, becomes a branch with a
+  // wait of its own)
   const bool mode2 = ep.bn_mode == 2 || ep.fz.acc_mode == 4;  // (sum g, sum g*xhat): slab or accumulators
-  float resv[NT][4], zv[NT][4];
+  const bool has_res = ep.residual != nullptr, has_mask = ep.mask_src != nullptr, has_bias = ep.bias != nullptr;
+  uintptr_t pr = has_res ? (uintptr_t)ep.residual : (uintptr_t)g_halo_zero;
+  uintptr_t pz = mode2 ? (uintptr_t)ep.bn_z : (uintptr_t)g_halo_zero;
+  uintptr_t pm = has_mask ? (uintptr_t)ep.mask_src : (uintptr_t)g_halo_zero;
+  uintptr_t pb = has_bias ? (uintptr_t)ep.bias : (uintptr_t)g_halo_zero;
+  asm volatile("" : "+s"(pr), "+s"(pz), "+s"(pm), "+s"(pb));
+  float resv[NT][4], zv[NT][4], mv[NT][4], bv[NT];
 #pragma unroll
   for (int t = 0; t < NT; ++t) {
     const int c = co0 + t * 16 + r16;
+    bv[t] = reinterpret_cast<const float*>(pb)[has_bias && c < a.cout ? c : 0];
 #pragma unroll
     for (int jj = 0; jj < 4; ++jj) {
       const long long o = (rowv[jj] && c < a.cout) ? (long long)rowo[jj] * a.cout + c : 0;
-      resv[t][jj] = ep.residual ? ep.residual[o] : 0.f;
-      zv[t][jj] = mode2 ? ep.bn_z[o] : 0.f;
+      resv[t][jj] = reinterpret_cast<const float*>(pr)[has_res ? o : 0];
+      zv[t][jj] = reinterpret_cast<const float*>(pz)[mode2 ? o : 0];
+      mv[t][jj] = reinterpret_cast<const float*>(pm)[has_mask ? o : 0];
     }
   }
+  const bool relu = ep.act == CGAN3D_ACT_RELU, lrelu = ep.act == CGAN3D_ACT_LRELU;
+  const float slope = ep.slope;
 #pragma unroll
   for (int t = 0; t < NT; ++t) {
     const int c = co0 + t * 16 + r16;
     const bool cv = c < a.cout;
-    const float b = (ep.bias && cv) ? ep.bias[c] : 0.f;
 #pragma unroll
     for (int jj = 0; jj < 4; ++jj) {
-      float v = acc[t][jj] + b;
-      if (ep.act == CGAN3D_ACT_RELU) v = fmaxf(v, 0.f);
-      else if (ep.act == CGAN3D_ACT_LRELU) v = v > 0.f ? v : v * ep.slope;
-      if (rowv[jj] && cv) {
-        const long long o = (long long)rowo[jj] * a.cout + c;
-        if (ep.mask_src) v = ep.mask_src[o] > 0.f ? v : v * ep.slope;
-        v += resv[t][jj];
-        y[o] = v;
-      }
+      float v = acc[t][jj] + bv[t];
+      v = relu ? fmaxf(v, 0.f) : v;
+      v = (lrelu & !(v > 0.f)) ? v * slope : v;
+      v = (has_mask & !(mv[t][jj] > 0.f)) ? v * slope : v;
+      v += resv[t][jj];
+      if (rowv[jj] && cv) y[(long long)rowo[jj] * a.cout + c] = v;
       vals[t][jj] = (rowv[jj] && cv) ? v : 0.f;
     }
   }
@@ -118,8 +129,7 @@ __device__ __forceinline__ void halo_epilogue(const HaloArgs& a, f32x4 (&acc)[NT
     lds_barrier();
     float* red = smemf;  // [4 waves][BN]
     __shared__ float bmean[64];
-    int cntv = 0;
-    for (int r = 0; r < 64; ++r) cntv += row_out[r] >= 0;
+    const int cntv = __popcll(__ballot(row_out[lane] >= 0));  // valid tile rows (64 = one per lane)
     const long long sbase = (long long)blockIdx.x * (2 * a.cout + 1);
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
@@ -300,9 +310,13 @@ __global__ __launch_bounds__(256) void conv_halo_kernel(HaloArgs a, const float*
   {
     constexpr int HB = 8;
     const int nvox = a.ez * a.ey * a.ex;
+    // v -> (hz, hy, hx) by multiply-high with block-uniform magic numbers (exact: v * ex < 2^32):
+    // the runtime divisions were most of the kernel's VALU (SQ counters, profiles/r04_pmc_sq_step.json)
+    const unsigned mex = 0xffffffffu / (unsigned)a.ex + 1u, mey = 0xffffffffu / (unsigned)a.ey + 1u;
     auto coords = [&](int v, int* o) -> bool {
-      const int hx = v % a.ex, hy = (v / a.ex) % a.ey, hz = v / (a.ex * a.ey);
-      const int iz = oz + hz, iy = oy + hy, ix = ox + hx;
+      const unsigned q = __umulhi((unsigned)v, mex), hz = __umulhi(q, mey);
+      const int hx = v - (int)q * a.ex, hy = (int)q - (int)hz * a.ey;
+      const int iz = oz + (int)hz, iy = oy + hy, ix = ox + hx;
       *o = ((nb * a.di + iz) * a.hi + iy) * a.wi + ix;  // 32-bit: halo_setup bounds the volume
       return iz >= 0 && iz < a.di && iy >= 0 && iy < a.hi && ix >= 0 && ix < a.wi;
     };
@@ -633,6 +647,12 @@ bool halo_format_ok(const cgan3d_conv_geom* g) {
 }
 
 bool halo_ok(const cgan3d_conv_geom* g) { return g->w_packed == 2 && halo_format_ok(g); }
+
+// the geometry's launch goes to conv_k3m_kernel when its epilogue allows (k3m_ok)
+bool k3m_route(const cgan3d_conv_geom* g) {
+  HaloArgs a;
+  return g->w_packed == 2 && !s2_kind(g) && halo_setup(g, &a) && k3_tile_ok(g) && k3m_geom_ok(g);
+}
 
 long long halo_mblocks(const cgan3d_conv_geom* g) {
   if (s2_kind(g)) return s2_blocks(g);

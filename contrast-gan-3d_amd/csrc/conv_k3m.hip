@@ -80,7 +80,9 @@ __device__ __forceinline__ void km_dma16(const void* gsrc, unsigned lds_base) {
 }
 #define KM_WAIT_VM(N) asm volatile("s_waitcnt vmcnt(" #N ")" ::: "memory")
 
-template <bool TR>
+// OB (round 4, cgan3d_epilogue.out_bf16): bit 0 — y and the mode-4 bn_z are bf16; bit 1 — the
+// residual is bf16 (the ResNet chain's z / dL/dy kept in bf16, engine.zs / dys)
+template <bool TR, int OB>
 __global__ __launch_bounds__(256, 1) void conv_k3m_kernel(K3mArgs a, const __bf16* __restrict__ x16,
                                                           const __bf16* __restrict__ wpk, float* __restrict__ y,
                                                           Epi ep) {
@@ -134,8 +136,11 @@ __global__ __launch_bounds__(256, 1) void conv_k3m_kernel(K3mArgs a, const __bf1
     const float* zp = mode4 ? ep.bn_z : reinterpret_cast<const float*>(g_km_zero);
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
-      resv[i] = rp[has_res && oidx[i] >= 0 ? oidx[i] : 0];
-      zv[i] = zp[mode4 && oidx[i] >= 0 ? oidx[i] : 0];
+      const int ri = has_res && oidx[i] >= 0 ? oidx[i] : 0, zi = mode4 && oidx[i] >= 0 ? oidx[i] : 0;
+      if constexpr ((OB & 2) != 0) resv[i] = (float)reinterpret_cast<const __bf16*>(rp)[ri];
+      else resv[i] = rp[ri];
+      if constexpr ((OB & 1) != 0) zv[i] = (float)reinterpret_cast<const __bf16*>(zp)[zi];
+      else zv[i] = zp[zi];
     }
   }
 
@@ -247,7 +252,10 @@ __global__ __launch_bounds__(256, 1) void conv_k3m_kernel(K3mArgs a, const __bf1
   }
 #pragma unroll
   for (int i = 0; i < 16; ++i)
-    if (oidx[i] >= 0) y[oidx[i]] = vals[i];
+    if (oidx[i] >= 0) {
+      if constexpr ((OB & 1) != 0) reinterpret_cast<__bf16*>(y)[oidx[i]] = (__bf16)vals[i];
+      else y[oidx[i]] = vals[i];
+    }
   if (!ep.fz.acc_mode) return;
   double* const facc = ep.fz.acc_out + (long long)(blockIdx.x % ep.fz.reps) * 2 * C;
   float* red = reinterpret_cast<float*>(smem);  // [2][4 waves][32]; the operands are dead after this barrier
@@ -317,11 +325,15 @@ void k3m_probe_set(int v) { g_k3m_probe = v; }
 
 // k3 s1 p1 64 -> 64 (forward, or the input-grad: a stride-1 conv with flipped taps) with a bf16 input
 // shadow, format-2 packed weights and an epilogue this kernel has (no slabs, masks or out2)
-bool k3m_ok(const cgan3d_conv_geom* g, const Epi& e) {
+bool k3m_geom_ok(const cgan3d_conv_geom* g) {
   return g_k3m && (long long)g->n * g->do_ * g->ho * g->wo * 64 < (1LL << 31) &&  // 32-bit epilogue offsets
          g->prec == CGAN3D_PREC_BF16 && g->w_packed == 2 && g->cin == 64 && g->cout == 64 && g->k == 3 &&
          g->stride == 1 && g->pad == 1 && !g->reflect && !g->planar && g->di == g->do_ && g->hi == g->ho &&
-         g->wi == g->wo && e.x16 && !e.stats && !e.bn_mode && !e.mask_src && !e.minuend && !e.out2 && !e.bn_fold &&
+         g->wi == g->wo;
+}
+
+bool k3m_ok(const cgan3d_conv_geom* g, const Epi& e) {
+  return k3m_geom_ok(g) && e.x16 && !e.stats && !e.bn_mode && !e.mask_src && !e.minuend && !e.out2 && !e.bn_fold &&
          (e.act == CGAN3D_ACT_NONE || e.act == CGAN3D_ACT_RELU || e.act == CGAN3D_ACT_LRELU) &&
          (e.fz.acc_mode == 0 || e.fz.acc_mode == 3 || e.fz.acc_mode == 4);
 }
@@ -334,8 +346,14 @@ int k3m_launch(const cgan3d_conv_geom* g, const __bf16* wp, float* y, const Epi&
   a.per_xcd = (a.tiles + 7) / 8;
   a.probe = g_k3m_probe;
   const dim3 grid((unsigned)(a.per_xcd * 16));
-  if (g->transposed) ::cg::launch(conv_k3m_kernel<true>, grid, dim3(256), 0, st, a, e.x16, wp, y, e);
-  else ::cg::launch(conv_k3m_kernel<false>, grid, dim3(256), 0, st, a, e.x16, wp, y, e);
+  const int ob = (e.out16 ? 1 : 0) | (e.res16 ? 2 : 0);
+#define CG_K3M(TR, OB) ::cg::launch(conv_k3m_kernel<TR, OB>, grid, dim3(256), 0, st, a, e.x16, wp, y, e)
+  if (g->transposed) {
+    if (ob == 0) CG_K3M(true, 0); else if (ob == 1) CG_K3M(true, 1); else if (ob == 2) CG_K3M(true, 2); else CG_K3M(true, 3);
+  } else {
+    if (ob == 0) CG_K3M(false, 0); else if (ob == 1) CG_K3M(false, 1); else if (ob == 2) CG_K3M(false, 2); else CG_K3M(false, 3);
+  }
+#undef CG_K3M
   return CGAN3D_OK;
 }
 

@@ -133,16 +133,18 @@ typedef struct cgan3d_epilogue {
                                 * reflect-folded tensor (pad bn_fold), bn_z lives on the unpadded
                                 * grid; see cgan3d_bn_backward_slab_fold.  0 otherwise. */
   const cgan3d_bn_fuse* fuse;  /* NULL, or the statistics into fp64 accumulators (above) */
-  int32_t out_bf16;            /* 1: the output y and bn_z are bf16 arrays (same layout, passed through
-                                * the float* / const float* slots): the generator's 64^3 16-channel
-                                * tensors kept in bf16 (round 4) — only launches with
+  int32_t out_bf16;            /* bit 0 (1): the output y and bn_z are bf16 arrays (same layout, passed
+                                * through the float* / const float* slots); bit 1 (2): the residual is
+                                * bf16 (the ResNet-block kernel only): the generator's BatchNorm inputs
+                                * and their gradients kept in bf16 (round 4) — only launches with
                                 * cgan3d_conv3d_out_bf16_ok accept it, every other launch rejects it */
 } cgan3d_epilogue;
 
 /* 1 when the forward-style launch of g honours cgan3d_epilogue.out_bf16: the 1 -> 16 k7 MFMA kernel
- * (first conv forward; last conv input-grad, its folded statistics reading a bf16 z) and the S2T
+ * (first conv forward; last conv input-grad, its folded statistics reading a bf16 z), the S2T
  * kernel (ConvTranspose3d 32 -> 16 forward; the first downsampling conv's input-grad with acc_mode 4
- * statistics reading a bf16 z). */
+ * statistics reading a bf16 z) and the ResNet-block kernel (Conv3d 64 -> 64 k3 forward / input-grad
+ * with the bf16 input shadow; bit 1 there: a bf16 skip gradient as the residual). */
 int32_t cgan3d_conv3d_out_bf16_ok(const cgan3d_conv_geom* g);
 
 /* 1 when the geometry's launch can produce cgan3d_bn_fuse accumulators. */

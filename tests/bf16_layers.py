@@ -178,7 +178,7 @@ def generator_layers(eng, rec: Recorder, weights=None, tol=1e-4, tol16=2e-3):
             out = conv(xi, wr, stride=ly.s, padding=ly.p)
         (dx,) = torch.autograd.grad(out, xi, dzr)
         if ly.name.endswith("block0"):
-            dx = dx + cf(G.dy[i + 1])
+            dx = dx + cf(G.dys[i + 1])  # the skip gradient as stored (bf16 where the layer keeps it)
         dy_next = dx
 
 

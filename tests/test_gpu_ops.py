@@ -764,6 +764,57 @@ def test_conv_k3m_bf16(n, sp):
                  "mode-4 sum g xhat")
 
 
+@pytest.mark.parametrize("n,sp", [(2, (16, 16, 16)), (1, (5, 6, 9))])
+def test_conv_k3m_bf16_storage(n, sp):
+    """conv_k3m with bf16 storage (cgan3d_epilogue.out_bf16, the ResNet chain's engine.zs / dys): a
+    bf16 output and mode-4 bn_z (bit 0) and a bf16 skip gradient (bit 1) against the fp32-storage
+    launch on the same (bf16-representable) operands: the outputs are its fp32 values rounded to
+    bf16 bit for bit, the fp64 statistics equal up to summation order (they come from the fp32
+    registers either way)."""
+    from cgan3d_amd import ops, _lib as L
+    c = 64
+    g = torch.Generator().manual_seed(11 + sp[1])
+    x = torch.randn(n, c, *sp, generator=g, dtype=torch.float64).bfloat16().float()
+    w = (torch.randn(c, c, 3, 3, 3, generator=g, dtype=torch.float64) / np.sqrt(c * 27)).float()
+    skip = torch.randn(n, c, *sp, generator=g, dtype=torch.float64).bfloat16().float()
+    z = torch.randn(n, c, *sp, generator=g, dtype=torch.float64).bfloat16().float()
+    ss = torch.cat([torch.rand(c, generator=g) + 0.5, torch.randn(c, generator=g) * 0.1]).float().cuda()
+    mi = torch.cat([torch.randn(c, generator=g) * 0.1, torch.rand(c, generator=g) + 0.5]).float().cuda()
+    ps = ops.PackSet(torch.device("cuda"))
+    gf, wf = ps.add(ops.conv_fwd_geom(n, sp, sp, c, c, 3, 1, 1), w.cuda(), L.PREC_BF16)
+    gd, wdp = ps.add(ops.conv_dgrad_geom(n, sp, sp, c, c, 3, 1, 1), w.cuda(), L.PREC_BF16)
+    ps.pack()
+    assert ops.out_bf16_ok(gf) and ops.out_bf16_ok(gd)
+    reps = 16
+    xs = _cl(x).bfloat16()
+    runs = {}
+    for key, yd, zd, rd in (("fp32", torch.float32, torch.float32, torch.float32),
+                            ("bf16", torch.bfloat16, torch.bfloat16, torch.bfloat16),
+                            ("res16", torch.float32, torch.float32, torch.bfloat16)):
+        yo = torch.empty(n, *sp, c, device="cuda", dtype=yd)
+        acc3 = torch.zeros(reps * 2 * c, device="cuda", dtype=torch.float64)
+        ops.conv(gf, _cl(x), wf, yo, ops.epilogue(x_bf16=xs, fuse=ops.BnFuse(acc3, 3, reps)))
+        dxo = torch.empty(n, *sp, c, device="cuda", dtype=yd)
+        acc4 = torch.zeros(reps * 2 * c, device="cuda", dtype=torch.float64)
+        ops.conv(gd, _cl(x), wdp, dxo, ops.epilogue(residual=_cl(skip).to(rd), x_bf16=xs, bn_z=_cl(z).to(zd),
+                                                    bn_ss=ss, bn_mi=mi, bn_act=L.ACT_RELU,
+                                                    fuse=ops.BnFuse(acc4, 4, reps)))
+        torch.cuda.synchronize()
+        runs[key] = (yo.cpu(), acc3.cpu(), dxo.cpu(), acc4.cpu())
+    f, b, r = runs["fp32"], runs["bf16"], runs["res16"]
+    assert torch.equal(b[0], f[0].bfloat16()), "bf16 forward output != rounded fp32 output"
+    assert torch.equal(b[2], f[2].bfloat16()), "bf16 input-grad output != rounded fp32 output"
+    # the fp64 atomics land in launch-dependent order: equal up to fp64 summation order
+    for a_, b_, nm in ((b[1], f[1], "mode-3"), (b[3], f[3], "mode-4"), (r[3], f[3], "mode-4, bf16 residual")):
+        assert_close(a_.view(reps, -1).sum(0).numpy(), b_.view(reps, -1).sum(0).numpy(), 1e-12, f"{nm} statistics")
+    assert torch.equal(r[2], f[2]), "bf16 residual alone changed the input-grad"
+    # a bf16 residual on a geometry other than the ResNet-block kernel is refused
+    with pytest.raises(Exception):
+        g2 = ops.conv_fwd_geom(n, sp, sp, c, c, 1, 1, 0)
+        ops.conv(g2, _cl(x), w[:, :, :1, :1, :1].contiguous().cuda(), torch.empty(n, *sp, c, device="cuda"),
+                 ops.epilogue(residual=_cl(skip).bfloat16()))
+
+
 @pytest.mark.parametrize("n,sp", [(2, (16, 16, 16)), (1, (5, 4, 8)), (2, (3, 8, 24)), (1, (7, 12, 16))])
 def test_wgrad_k3m_bf16(n, sp):
     """ResNet-block weight gradient from the bf16 shadows (wgrad_k3m_kernel: LDS-DMA stages, 32x32x16

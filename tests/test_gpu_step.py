@@ -518,9 +518,10 @@ NOISE_L2_BAR, NOISE_MAX_BAR, NOISE_MEDIAN_BAR = 0.3, 0.3, 0.15
 
 
 def test_bf16_storage_matches_fp32_storage(monkeypatch):
-    """The generator's 64^3 16-channel BatchNorm inputs and their gradients kept in bf16 (engine.zs /
-    dys / dpads: the first conv's z and dL/dy, the last BatchNorm layer's z and the last conv's padded
-    input-grad; the statistics still from the producers' fp32 values) against the same step with them
+    """The generator's BatchNorm inputs and their gradients kept in bf16 (engine.zs / dys / dpads: at
+    64^3 the first conv's z and dL/dy, the last BatchNorm layer's z and the last conv's padded
+    input-grad; every ResNet layer's but the last; the statistics still from the producers' fp32
+    values) against the same step with them
     in fp32 (CGAN3D_DEBUG=fp32_store), 64^3 bf16, two steps from one state.  Rounding a stored tensor
     is one more 2^-9 relative perturbation per element — the size of the shadow rounding the
     convolutions apply anyway — and the bf16 step amplifies any perturbation layer by layer
@@ -541,7 +542,11 @@ def test_bf16_storage_matches_fp32_storage(monkeypatch):
     nl = len(b16.G.layers)
     assert b16.G.z16[0] and b16.G.z16[-1] and not any(f32.G.z16)
     assert b16.G.zs[0].dtype == b16.G.dys[0].dtype == b16.G.dpads.dtype == torch.bfloat16
-    assert sum(b16.G.z16) == 2 and nl > 2
+    # and the ResNet chain's layers but the last (conv_k3m writes / reads them in bf16; the last one's
+    # dL/dy comes from the up-sampling conv)
+    res = [j for j, ly in enumerate(b16.G.layers) if "resnet_backbone" in ly.name]
+    assert len(res) >= 2 and all(b16.G.z16[j] for j in res[:-1]) and not b16.G.z16[res[-1]]
+    assert sum(b16.G.z16) == 2 + len(res) - 1 and nl > 2
     opt, _ = synth_patches(b, S, 37)
     sub, seg = synth_patches(b, S, 38)
     bt = (torch.from_numpy(opt).cuda(), torch.from_numpy(sub).cuda(), torch.from_numpy(seg).cuda(),

@@ -62,6 +62,26 @@ def _cases(B=4, S=64):
         flops = 2.0 * n3 * dout[0] * dout[1] * dout[2] * cin * cout * 64
         return (lambda: ops.conv(geo, x, w, y)), flops
 
+    def res_wgrad_k3m():
+        """ResNet-block weight grad as the bf16 step issues it (both operands' bf16 shadows:
+        wgrad_k3m_kernel + wgrad_reduce_lin_kernel)"""
+        geo = ops.with_prec(ops.conv_wgrad_geom(B, R3, R3, 64, 64, 3, 1, 1), BF)
+        x, go = t(B, *R3, 64), t(B, *R3, 64)
+        x16, go16 = x.bfloat16(), go.bfloat16()
+        dw = torch.empty(64, 64, 3, 3, 3, device=dev)
+        ws = torch.empty(ops.wgrad_ws_floats(geo), device=dev)
+        flops = 2.0 * B * r**3 * 64 * 64 * 27
+        return (lambda: ops.wgrad(geo, x, go, dw, ws, gathered16=x16, aligned16=go16)), flops
+
+    def crit_wgrad():
+        """the critic's first layer weight-grad over the 3B critic batch (conv_c1.hip)"""
+        n3 = 3 * B
+        geo = ops.conv_wgrad_geom(n3, F3, H3, 1, 8, 4, 2, 1)
+        x, go = t(n3, *F3, 1), t(n3, *H3, 8)
+        dw = torch.empty(8, 1, 4, 4, 4, device=dev)
+        ws = torch.empty(max(ops.wgrad_ws_floats(geo), 1), device=dev)
+        return (lambda: ops.wgrad(geo, x, go, dw, ws)), 2.0 * n3 * H3[0] ** 3 * 8 * 64
+
     def res_k3m(dgrad, reps=16, stats=True, res=True):
         """ResNet-block conv as the bf16 step issues it: bf16 shadow input, fp64 accumulator statistics
         (mode 3 forward with the residual + ReLU epilogue; mode 4 input-grad), conv_k3m_kernel"""
@@ -91,6 +111,8 @@ def _cases(B=4, S=64):
         "res_fwd_k3m_nostat": lambda: res_k3m(False, stats=False),
         "res_fwd_k3m_plain": lambda: res_k3m(False, stats=False, res=False),
         "crit_first": lambda: crit(1, 8, F3),
+        "crit_first_wgrad": lambda: crit_wgrad(),
+        "res_wgrad_k3m": lambda: res_wgrad_k3m(),
         "crit_m0": lambda: crit(8, 16, H3),
         "crit_m1": lambda: crit(16, 32, R3),
         "crit_m2": lambda: crit(32, 64, (r // 2,) * 3),
