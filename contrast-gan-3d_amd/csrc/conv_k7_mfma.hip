@@ -941,11 +941,14 @@ __global__ __launch_bounds__(256) void k7m_colsum_kernel(const float* __restrict
 }
 
 // tiles of the wgrad X16 grid (output grid, or the padded input grid for the last conv)
+static int g_k7wg_blocks = 512;  // cgan3d_set_tuning key 20: most blocks of a k7 weight grad (its partial rows)
+void k7wg_blocks_set(int v) { g_k7wg_blocks = v > 0 ? v : 512; }
+
 static void k7m_wg_split(const cgan3d_conv_geom* g, bool wide_in, int* grid, int* per, int* ntiles) {
   const int gd = wide_in ? g->di + 2 * g->pad : g->do_, gh = wide_in ? g->hi + 2 * g->pad : g->ho,
             gw = wide_in ? g->wi + 2 * g->pad : g->wo;
   *ntiles = g->n * ((gd + G_TD - 1) / G_TD) * ((gh + G_TH - 1) / G_TH) * ((gw + G_TW - 1) / G_TW);
-  *per = (*ntiles + 511) / 512;
+  *per = (*ntiles + g_k7wg_blocks - 1) / g_k7wg_blocks;
   *grid = (*ntiles + *per - 1) / *per;
 }
 
@@ -960,7 +963,7 @@ static K7Args k7m_args(const cgan3d_conv_geom* g, int P, int reflect, int flip, 
 
 static void k7m_n2w_split(const K7Args& a, int* grid, int* per, int* ntiles) {
   *ntiles = a.n * a.tiles_d * a.tiles_h * a.tiles_w;
-  *per = (*ntiles + 511) / 512;
+  *per = (*ntiles + g_k7wg_blocks - 1) / g_k7wg_blocks;
   *grid = (*ntiles + *per - 1) / *per;
 }
 
