@@ -121,6 +121,8 @@ def _cases(B=4, S=64):
         "res_wgrad": lambda: wgrad_case(ops.with_prec(ops.conv_wgrad_geom(B, R3, R3, 64, 64, 3, 1, 1), BF), R3, R3),
         "down0_wgrad": lambda: wgrad_case(ops.with_prec(ops.conv_wgrad_geom(B, F3, H3, 16, 32, 3, 2, 1), BF), F3, H3),
         "down0_fwd": lambda: conv_case(ops.conv_fwd_geom(B, F3, H3, 16, 32, 3, 2, 1), 16, 32, F3, H3),
+        "up0_fwd": lambda: conv_case(ops.convt_fwd_geom(B, R3, H3, 64, 32, 3, 2, 1), 64, 32, R3, H3),
+        "down1_fwd": lambda: conv_case(ops.conv_fwd_geom(B, H3, R3, 32, 64, 3, 2, 1), 32, 64, H3, R3),
         "up1_fwd": lambda: conv_case(ops.convt_fwd_geom(B, H3, F3, 32, 16, 3, 2, 1), 32, 16, H3, F3),
         "k7_last_fwd": lambda: conv_case(ops.with_prec(ops.conv_fwd_geom(B, F3, F3, 16, 1, 7, 1, 3, True), BF), 16, 1,
                                          F3, F3, packed=False),
