@@ -92,6 +92,7 @@ _SIGS = {
     "cgan3d_conv3d_bn_fold_ok": ([_P], _I32),
     "cgan3d_bn_fuse_ok": ([_P], _I32),
     "cgan3d_conv3d_neg_dtanh_ok": ([_P], _I32),
+    "cgan3d_conv3d_cin1t": ([_P], _I32),
     "cgan3d_conv3d_sumsq_blocks": ([_P], _I64),
     "cgan3d_conv3d_wgrad_group_ok": ([_P], _I32),
     "cgan3d_conv3d_wgrad_group": ([_P, _P, _P, _P, _I32, _P], _I32),

@@ -50,6 +50,8 @@ def uses_gemm(g: ConvGeom) -> bool:
         return True
     if g.cin == 1 and g.cout == 8 and g.k == 4 and g.stride == 2 and g.pad == 1 and not g.transposed:
         return False  # critic first layer: conv_c1.hip reads torch-layout weights
+    if g.cin == 1 and g.transposed and L.load().cgan3d_conv3d_cin1t(ctypes.byref(g)):
+        return False  # the critic's last-layer input-grad: direct fp32 kernel on torch-layout weights
     return not (g.k == 7 and g.stride == 1 and g.cin == 1 and g.cout in (8, 16))
 
 

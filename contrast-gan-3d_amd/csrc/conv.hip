@@ -156,22 +156,22 @@ __global__ __launch_bounds__(256) void conv_cout1_wave_kernel(ConvArgs a, const 
 // threads (4 loads each) and reduced through LDS.
 __global__ __launch_bounds__(256) void conv_cout1_block_kernel(ConvArgs a, const float* __restrict__ x,
                                                                const float* __restrict__ w, float* y, Epi ep) {
-  extern __shared__ __attribute__((aligned(16))) float Ws[];  // [T][cin]
   __shared__ float red[4];
   const int T = a.kd * a.k * a.k;
-  // Every load below is unconditional from a clamped, valid address (a dead one selected to zero):
-  // a load under a branch gets a wait of its own, and the round-3 version of this kernel walked its
-  // 17 loads one round trip at a time (11.6 us for the critic's 324-voxel last layer).
+  // Every load below is unconditional from a clamped, valid address (a dead one masked to zero
+  // afterwards by an integer mask): a load under a branch gets a wait of its own.  Round 4: each
+  // thread reads the weights of its own (tap, 4 channels) items straight from L2, in flight with its
+  // x loads — no LDS staging pass and barrier in front of the dot product (12.8 us for the critic's
+  // 324-voxel last layer with them).
   const long long lin = blockIdx.x;
   int ow = (int)(lin % a.wo); long long tt = lin / a.wo;
   int oh = (int)(tt % a.ho); tt /= a.ho;
   int od = (int)(tt % a.do_); int nb = (int)(tt / a.do_);
   const int bd = od * a.sd - a.pd, bh = oh * a.s - a.p, bw = ow * a.s - a.p;
   const int C4 = a.cin >> 2, R4 = T * C4;
-  // the x loads do not depend on the staged weights: issued first, so one round trip covers both
   constexpr int MAXR = 8;  // float4 per thread (R4 <= 2048)
-  f32x4 xv[MAXR];
-  int toff[MAXR];
+  f32x4 xv[MAXR], wv[MAXR];
+  unsigned okm = 0;
 #pragma unroll
   for (int u = 0; u < MAXR; ++u) {
     const int r4 = threadIdx.x + 256 * u;
@@ -180,33 +180,18 @@ __global__ __launch_bounds__(256) void conv_cout1_block_kernel(ConvArgs a, const
     const int id = gcoord(bd, td, a.di, a.reflect), ih = gcoord(bh, th, a.hi, a.reflect),
               iw = gcoord(bw, tw, a.wi, a.reflect);
     const bool ok = r4 < R4 && (id | ih | iw) >= 0;
-    const f32x4 v = *reinterpret_cast<const f32x4*>(
+    xv[u] = *reinterpret_cast<const f32x4*>(
         x + (ok ? ((long long)((nb * a.di + id) * a.hi + ih) * a.wi + iw) * a.cin + c : 0));
-    xv[u] = ok ? v : f32x4{0.f, 0.f, 0.f, 0.f};
-    toff[u] = ok ? t * a.cin + c : -1;
-  }
-  const int TC = T * a.cin;
-  for (int i0 = threadIdx.x; i0 < TC; i0 += 8 * blockDim.x) {
-    float v[8];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int i = min(i0 + u * (int)blockDim.x, TC - 1), ci = i / T, t = i - ci * T;
-      v[u] = w[(long long)ci * a.sa + t];
-    }
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int i = i0 + u * blockDim.x, ci = i / T, t = i - ci * T;
-      if (i < TC) Ws[t * a.cin + ci] = v[u];
-    }
+    for (int j = 0; j < 4; ++j) wv[u][j] = w[(long long)(c + j) * a.sa + t];
+    okm |= ok ? 1u << u : 0u;
   }
-  __syncthreads();
   float acc = 0.f;
 #pragma unroll
   for (int u = 0; u < MAXR; ++u) {
-    if (toff[u] >= 0) {
-      const f32x4 wv = *reinterpret_cast<const f32x4*>(Ws + toff[u]);
-      acc += xv[u][0] * wv[0] + xv[u][1] * wv[1] + xv[u][2] * wv[2] + xv[u][3] * wv[3];
-    }
+    const bool ok = (okm >> u) & 1u;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc += keep_if(ok, xv[u][j]) * wv[u][j];
   }
   acc = wave_sum(acc);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
@@ -220,6 +205,62 @@ __global__ __launch_bounds__(256) void conv_cout1_block_kernel(ConvArgs a, const
     if (ep.residual) v += ep.residual[lin];
     y[lin] = v;
     if (ep.out2) ep.out2[lin] = ep.minuend[lin] - v;
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// cin == 1, stride-1 transposed launches (the critic's last-layer input-grad, discriminator.py:
+// Conv3d 64 -> 1 k4 s1 p1 run as 1 -> 64): exact fp32, a thread per (output voxel, channel) —
+// the 64 lanes of a wave are the 64 channels of one voxel, so the per-tap validity is wave-uniform —
+// the block's sample input and the weights staged once in LDS.  Round 4: the implicit GEMM took
+// 12.7 us for these 49k outputs (a 64-long K on 16 x 64 tiles of a mostly empty grid).
+constexpr int CIN1T_MAXV = 512, CIN1T_MAXW = 64 * 64;
+bool cin1t_ok(const cgan3d_conv_geom* g) {
+  return g->transposed && !g->planar && !g->reflect && g->stride == 1 && g->cin == 1 && g->cout >= 2 &&
+         g->cout <= 64 && g->k * g->k * g->k * g->cout <= CIN1T_MAXW && g->di * g->hi * g->wi <= CIN1T_MAXV &&
+         (long long)g->n * g->do_ * g->ho * g->wo * g->cout < (1LL << 31);
+}
+
+__global__ __launch_bounds__(256) void conv_cin1t_kernel(ConvArgs a, const float* __restrict__ x,
+                                                         const float* __restrict__ w, float* y, Epi ep,
+                                                         int blocks_per_sample) {
+  __shared__ float xs[CIN1T_MAXV];
+  __shared__ float wsm[CIN1T_MAXW];  // [t][c]
+  const int nb = blockIdx.x / blocks_per_sample, part = blockIdx.x - nb * blocks_per_sample;
+  const int T = a.k * a.k * a.k, C = a.cout;
+  const int nin = a.di * a.hi * a.wi, nout = a.do_ * a.ho * a.wo;
+  for (int i = threadIdx.x; i < nin; i += 256) xs[i] = x[(long long)nb * nin + i];
+  for (int i = threadIdx.x; i < T * C; i += 256) {
+    const int t = i / C, c = i - t * C;
+    wsm[i] = w[(long long)c * a.sb + t];
+  }
+  __syncthreads();
+  const int per = (nout * C + blocks_per_sample - 1) / blocks_per_sample;
+  const int o0 = part * per, o1 = min(nout * C, o0 + per);
+  for (int o = o0 + (int)threadIdx.x; o < o1; o += 256) {
+    const int c = o % C, v = o / C;
+    const int ow = v % a.wo, oh = (v / a.wo) % a.ho, od = v / (a.wo * a.ho);
+    float acc = 0.f;
+    for (int td = 0; td < a.k; ++td) {
+      const int id = od + a.p - td;
+      if ((unsigned)id >= (unsigned)a.di) continue;
+      for (int th = 0; th < a.k; ++th) {
+        const int ih = oh + a.p - th;
+        if ((unsigned)ih >= (unsigned)a.hi) continue;
+        for (int tw = 0; tw < a.k; ++tw) {
+          const int iw = ow + a.p - tw;
+          if ((unsigned)iw >= (unsigned)a.wi) continue;
+          acc = fmaf(xs[(id * a.hi + ih) * a.wi + iw], wsm[((td * a.k + th) * a.k + tw) * C + c], acc);
+        }
+      }
+    }
+    const long long oi = ((long long)nb * nout + v) * C + c;
+    float r = acc + (ep.bias ? ep.bias[c] : 0.f);
+    if (ep.act == CGAN3D_ACT_RELU) r = fmaxf(r, 0.f);
+    else if (ep.act == CGAN3D_ACT_LRELU) r = r > 0.f ? r : r * ep.slope;
+    if (ep.mask_src) r = ep.mask_src[oi] > 0.f ? r : r * ep.slope;
+    if (ep.residual) r += ep.residual[oi];
+    y[oi] = r;
   }
 }
 
@@ -656,7 +697,7 @@ cout1:
     const long long r4 = (long long)geom_taps(g) * g->cin / 4;
     if (!g->transposed && g->cin % 4 == 0 && a.class_vox <= 4096 && r4 <= 2048 && !g_cout1_wave) {
       // very few outputs, long reductions: a block per output voxel
-      ::cg::launch(conv_cout1_block_kernel, dim3((unsigned)a.class_vox), dim3(256), lds, s, a, x, w, y, e);
+      ::cg::launch(conv_cout1_block_kernel, dim3((unsigned)a.class_vox), dim3(256), 0, s, a, x, w, y, e);
       CG_LAUNCH_CHECK("conv_cout1_block_kernel");
       return CGAN3D_OK;
     }
@@ -684,10 +725,25 @@ cout1:
     CG_LAUNCH_CHECK("conv_halo_kernel");
     return CGAN3D_OK;
   }
+  if (!g->w_packed && cin1t_ok(g) && !g_cout1_wave) {  // the critic's last-layer input-grad
+    CG_CHECK_ARG(!e.stats && !e.bn_mode && !e.out2 && !e.minuend && !e.x16 && !e.fz.acc_mode,
+                 "cgan3d_conv3d_fwd: cin == 1 transposed launch: bias / activation / mask / residual epilogue only");
+    ConvArgs a;
+    CG_CHECK_ARG(make_args(g, &a, 256), "cgan3d_conv3d_fwd: bad transposed geometry");
+    const int nout = g->do_ * g->ho * g->wo * g->cout;
+    const int bps = std::max(1, std::min(64, (nout + 255) / 256));
+    ::cg::launch(conv_cin1t_kernel, dim3((unsigned)(g->n * bps)), dim3(256), 0, s, a, x, w, y, e, bps);
+    CG_LAUNCH_CHECK("conv_cin1t_kernel");
+    return CGAN3D_OK;
+  }
   int rc = gemm_launch(g, x, w, y, e, s);
   if (rc) return rc;
   CG_LAUNCH_CHECK("conv_gemm_kernel");
   return CGAN3D_OK;
+}
+
+extern "C" int32_t cgan3d_conv3d_cin1t(const cgan3d_conv_geom* g) {
+  return g && !validate(g, "cgan3d_conv3d_cin1t") && cin1t_ok(g) && !g_cout1_wave ? 1 : 0;
 }
 
 static long long wgrad_vpb(long long V, int gx_blocks) {

@@ -149,24 +149,41 @@ __global__ __launch_bounds__(256) void c1_dgrad_kernel(C1Args a, const float* __
   // before the first LDS store
   constexpr int NG = GZ * GY * GX * 2, PER = (NG + 255) / 256;
   const float w0 = w[(tid & 7) * a.w_sa + (tid >> 3)], w1 = w[(tid & 7) * a.w_sa + ((tid + 256) >> 3)];
+  // unconditional loads from clamped offsets, masked at the LDS store (no branch per load)
+  const float* dzn = dz + (long long)nb * a.di * a.hi * a.wi * 8;
   f32x4 gv[PER];
+  unsigned okm = 0;
 #pragma unroll
   for (int k = 0; k < PER; ++k) {
     const int i = tid + 256 * k, h = i & 1, v = i >> 1;
     const int gx = v % GX, r = v / GX, gy = r % GY, gz = r / GY;
     const int cz = cz0 + gz, cy = cy0 + gy, cx = cx0 + gx;
-    gv[k] = (i < NG && (unsigned)cz < (unsigned)a.di && (unsigned)cy < (unsigned)a.hi && (unsigned)cx < (unsigned)a.wi)
-                ? *reinterpret_cast<const f32x4*>(dz + ((((long long)nb * a.di + cz) * a.hi + cy) * a.wi + cx) * 8 + 4 * h)
-                : f32x4{0.f, 0.f, 0.f, 0.f};
+    const bool ok = i < NG && (unsigned)cz < (unsigned)a.di && (unsigned)cy < (unsigned)a.hi && (unsigned)cx < (unsigned)a.wi;
+    gv[k] = *reinterpret_cast<const f32x4*>(dzn + (ok ? ((cz * a.hi + cy) * a.wi + cx) * 8 + 4 * h : 0));
+    okm |= ok ? 1u << k : 0u;
   }
+  // the epilogue's operands (penalty fold: residual, tanh) before the taps as well
+  const int lz = tid >> 7, ly = (tid >> 4) & 7, lx = tid & 15;
+  const int oz = oz0 + lz, oy = oy0 + ly, ox = ox0 + lx;
+  const bool inside = oz < a.do_ && oy < a.ho && ox < a.wo;
+  const long long o = inside ? (((long long)nb * a.do_ + oz) * a.ho + oy) * a.wo + ox : 0;
+  const bool fold = tnh != nullptr;
+  uintptr_t pt = fold ? (uintptr_t)tnh : (uintptr_t)g_c1_zero, pr = fold ? (uintptr_t)res : (uintptr_t)g_c1_zero;
+  asm volatile("" : "+s"(pt), "+s"(pr));
+  const float tv = reinterpret_cast<const float*>(pt)[fold ? o : 0], rv = reinterpret_cast<const float*>(pr)[fold ? o : 0];
   ws[tid] = w0;
   ws[tid + 256] = w1;
 #pragma unroll
-  for (int k = 0; k < PER; ++k)
-    if (tid + 256 * k < NG) *reinterpret_cast<f32x4*>(gs + (tid + 256 * k) * 4) = gv[k];
+  for (int k = 0; k < PER; ++k) {
+    if (tid + 256 * k < NG) {
+      const bool ok = (okm >> k) & 1u;
+      f32x4 m;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) m[e] = keep_if(ok, gv[k][e]);
+      *reinterpret_cast<f32x4*>(gs + (tid + 256 * k) * 4) = m;
+    }
+  }
   __syncthreads();
-  const int lz = tid >> 7, ly = (tid >> 4) & 7, lx = tid & 15;
-  const int oz = oz0 + lz, oy = oy0 + ly, ox = ox0 + lx;
   // per dim: taps t = ((o + 1) & 1) + 2j, coarse o' = (o + 1 - t) / 2, local = o' - c0
   float acc = 0.f;
 #pragma unroll
@@ -186,15 +203,8 @@ __global__ __launch_bounds__(256) void c1_dgrad_kernel(C1Args a, const float* __
 #pragma unroll
         for (int c = 0; c < 4; ++c) acc = fmaf(g1[c], w1[c], acc);
       }
-  const bool inside = oz < a.do_ && oy < a.ho && ox < a.wo;
-  if (inside) {
-    const long long o = (((long long)nb * a.do_ + oz) * a.ho + oy) * a.wo + ox;
-    if (tnh) {
-      const float t = tnh[o];
-      acc = res[o] - acc * (1.f - t * t);
-    }
-    dx[o] = acc;
-  }
+  if (fold) acc = rv - acc * (1.f - tv * tv);
+  if (inside) dx[o] = acc;
   if (sq) {  // the block's sum of squares: waves by shuffles, then 4 partials through LDS (ws is free)
     float v = inside ? acc * acc : 0.f;
 #pragma unroll

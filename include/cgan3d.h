@@ -152,6 +152,9 @@ int32_t cgan3d_bn_fuse_ok(const cgan3d_conv_geom* g);
 /* 1 when the input-grad geometry takes the CGAN3D_ACT_NEG_DTANH epilogue (the critic's first layer,
  * discriminator.py:55-60, 1 -> 8 k4 s2 p1). */
 int32_t cgan3d_conv3d_neg_dtanh_ok(const cgan3d_conv_geom* g);
+/* 1 when the launch of g goes to the direct cin == 1 stride-1 transposed kernel (the critic's
+ * last-layer input-grad, exact fp32): it reads torch-layout weights (w_packed 0), no packed copy. */
+int32_t cgan3d_conv3d_cin1t(const cgan3d_conv_geom* g);
 /* Blocks of the input-grad launch when the geometry (the critic's first layer) can write the
  * per-block sum of squares of its output: then cgan3d_epilogue.stats = float[blocks], the blocks
  * of sample s being [s * blocks / n, (s + 1) * blocks / n); 0 when it cannot. */
