@@ -732,7 +732,20 @@ __global__ __launch_bounds__(256) void bn_apply_acc_kernel(const double* __restr
 #pragma unroll
   for (int u = 0; u < ACC_PF; ++u)
     if (i0 + u * stride < n4) apply(i0 + u * stride, zp[u], rp[u]);
-  for (long long i = i0 + ACC_PF * stride; i < n4; i += stride) apply(i, load4<Z16>(z, i), RES ? r4[i] : f32x4{});
+  // the rest (16 float4 per thread at 64^3 x 16 channels, the grid being capped at 1024 blocks) four
+  // items per trip, loads first: one round trip per four items
+  for (long long j = i0 + ACC_PF * stride; j < n4; j += 4 * stride) {
+    f32x4 zq[4], rq[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const long long i = min(j + u * stride, n4 - 1);
+      zq[u] = load4<Z16>(z, i);
+      if (RES) rq[u] = r4[i];
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      if (j + u * stride < n4) apply(j + u * stride, zq[u], RES ? rq[u] : f32x4{});
+  }
 }
 
 template <bool B16>  // dy and z in bf16
@@ -793,7 +806,18 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_acc_kernel(const double* __r
 #pragma unroll
   for (int u = 0; u < ACC_PF; ++u)
     if (i0 + u * stride < n4) apply(i0 + u * stride, zp[u], dp[u]);
-  for (long long i = i0 + ACC_PF * stride; i < n4; i += stride) apply(i, load4<B16>(z, i), load4<B16>(dy, i));
+  for (long long j = i0 + ACC_PF * stride; j < n4; j += 4 * stride) {  // four items per trip, loads first
+    f32x4 zq[4], dq[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const long long i = min(j + u * stride, n4 - 1);
+      zq[u] = load4<B16>(z, i);
+      dq[u] = load4<B16>(dy, i);
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      if (j + u * stride < n4) apply(j + u * stride, zq[u], dq[u]);
+  }
 }
 
 // blocks of the accumulator passes: ~2 float4 per thread, at most `cap` blocks — each block reads the
