@@ -251,7 +251,6 @@ void k3m_probe_set(int v);
 void c1_groups_set(int v);
 void wgrad_k3m_probe_set(int v);
 void k7wg_blocks_set(int v);
-void halo_res_set(int v);
 bool halo_ok(const cgan3d_conv_geom* g);         // w_packed == 2 and eligible
 bool halo_format_ok(const cgan3d_conv_geom* g);  // eligible ignoring w_packed
 long long halo_mblocks(const cgan3d_conv_geom* g);

@@ -667,7 +667,6 @@ extern "C" int cgan3d_set_tuning(int32_t key, int32_t value) {
   if (key == 18) { c1_groups_set(value); return CGAN3D_OK; }
   if (key == 19) { wgrad_k3m_probe_set(value); return CGAN3D_OK; }
   if (key == 20) { k7wg_blocks_set(value); return CGAN3D_OK; }
-  if (key == 21) { halo_res_set(value); return CGAN3D_OK; }
   set_error("cgan3d_set_tuning: unknown key %d", key);
   return CGAN3D_EINVAL;
 }

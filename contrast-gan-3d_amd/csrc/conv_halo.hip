@@ -32,7 +32,6 @@ struct HaloArgs {
   int ez, ey, ex;             // halo extents
   int halo_bytes;
   int bn;                     // output channels per block
-  int nres;                   // > 0: every tap's weight slab resident in LDS (nres slots), else a 3-slot ring
 };
 
 constexpr int HT = 4;  // tile edge (4 x 4 x 4 = 64 output voxels)
@@ -226,11 +225,7 @@ __device__ __forceinline__ void halo_epilogue(const HaloArgs& a, f32x4 (&acc)[NT
   }
 }
 
-// RES (round 4, HaloArgs.nres): all of the class's weight slabs are DMA'd at once into their own
-// slots (a stride-2 transposed class has at most 8 taps: 32 KB at 64 -> 32 channels) and the taps
-// run behind one wait and one barrier — with the ring, every tap cost two barriers for 2-4 MFMAs per
-// wave.
-template <int CIN, int NT, bool RES>  // NT = BN/16 output-channel tiles per wave
+template <int CIN, int NT>  // NT = BN/16 output-channel tiles per wave
 __global__ __launch_bounds__(256) void conv_halo_kernel(HaloArgs a, const float* __restrict__ x,
                                                         const __bf16* __restrict__ wpk, float* y, Epi ep) {
   constexpr int BN = 16 * NT;
@@ -240,8 +235,8 @@ __global__ __launch_bounds__(256) void conv_halo_kernel(HaloArgs a, const float*
   constexpr int DMA_PER_TAP = (SLOT * 2 + 4095) / 4096;  // global_load_lds_dwordx4 per thread per tap
   static_assert(SLOT * 2 % 1024 == 0 && DMA_PER_TAP <= 2, "slab must be 2, 4 or 8 KB");
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  __bf16* wring = reinterpret_cast<__bf16*>(smem);                                   // [3 or nres][SLOT]
-  __bf16* halo = reinterpret_cast<__bf16*>(smem + (RES ? a.nres : 3) * SLOT * 2);  // [E][ROW]
+  __bf16* wring = reinterpret_cast<__bf16*>(smem);                // [3][SLOT]
+  __bf16* halo = reinterpret_cast<__bf16*>(smem + 3 * SLOT * 2);  // [E][ROW]
   __shared__ int tq[3][64];                                        // per-tap halo offsets
   __shared__ int tlin[64];
   __shared__ int row_out[64];
@@ -293,7 +288,7 @@ __global__ __launch_bounds__(256) void conv_halo_kernel(HaloArgs a, const float*
   // ---- weight ring: slab of tap j (channels co0..co0+BN) -> slot j % 3 by LDS-DMA
   auto issue = [&](int j) {
     const __bf16* src = wpk + ((long long)tlin[j] * a.cout + co0) * CIN;
-    __bf16* dst = wring + (RES ? j : j % 3) * SLOT;
+    __bf16* dst = wring + (j % 3) * SLOT;
 #pragma unroll
     for (int q = 0; q < DMA_PER_TAP; ++q) {
       const int byte = (q * 256 + tid) * 16;
@@ -304,12 +299,8 @@ __global__ __launch_bounds__(256) void conv_halo_kernel(HaloArgs a, const float*
                                        16, 0, 0);
     }
   };
-  if constexpr (RES) {
-    for (int j = 0; j < ntap; ++j) issue(j);
-  } else {
-    if (ntap > 0) issue(0);
-    if (ntap > 1) issue(1);
-  }
+  if (ntap > 0) issue(0);
+  if (ntap > 1) issue(1);
 
   // ---- halo: fp32 NDHWC -> bf16 LDS (zero outside the gathered volume); with a bf16 shadow of
   // x (ep.x16) 16-byte granules are copied as they are.  Batches of HB items per thread: every load
@@ -390,26 +381,20 @@ __global__ __launch_bounds__(256) void conv_halo_kernel(HaloArgs a, const float*
   // this lane's output voxel (A row): z = wave, y = r16 >> 2, x = r16 & 3
   const int lane_vox = ((wave * se) * a.ey + ((r16 >> 2) * se)) * a.ex + (r16 & 3) * se;
 
-  if constexpr (RES) {  // every slab landed (this wave's DMAs), and every wave's
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-  }
   for (int j = 0; j < ntap; ++j) {
-    if constexpr (!RES) {
-      if (j + 2 < ntap) issue(j + 2);
-      // wait for tap j's DMA: leave the (up to) two younger taps in flight
-      if (j + 2 < ntap) {
-        if constexpr (DMA_PER_TAP == 1) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-      } else if (j + 1 < ntap) {
-        if constexpr (DMA_PER_TAP == 1) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-      } else {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      }
-      __builtin_amdgcn_s_barrier();
+    if (j + 2 < ntap) issue(j + 2);
+    // wait for tap j's DMA: leave the (up to) two younger taps in flight
+    if (j + 2 < ntap) {
+      if constexpr (DMA_PER_TAP == 1) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    } else if (j + 1 < ntap) {
+      if constexpr (DMA_PER_TAP == 1) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
-    const __bf16* ws = wring + (RES ? j : j % 3) * SLOT;
+    __builtin_amdgcn_s_barrier();
+    const __bf16* ws = wring + (j % 3) * SLOT;
     const int voff = (tq[0][j] * a.ey + tq[1][j]) * a.ex + tq[2][j];
     const __bf16* arow = halo + (lane_vox + voff) * ROW;
 #pragma unroll
@@ -423,13 +408,10 @@ __global__ __launch_bounds__(256) void conv_halo_kernel(HaloArgs a, const float*
         acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, bv, acc[t], 0, 0, 0);
       }
     }
-    if constexpr (!RES) {
-      // every wave has read slot j % 3 before tap j + 3 may overwrite it
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-    }
+    // every wave has read slot j % 3 before tap j + 3 may overwrite it
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
   }
-  if constexpr (RES) lds_barrier();  // the epilogue's scratch aliases the slabs
 
   halo_epilogue<NT>(a, acc, row_out, co0, y, ep, reinterpret_cast<float*>(smem));
 }
@@ -612,9 +594,6 @@ static int g_halo_min_blocks = 512;  // cgan3d_set_tuning key 2
 
 void halo_set_min_blocks(int v) { g_halo_min_blocks = v; }
 
-static int g_halo_res = 1;  // cgan3d_set_tuning key 21: 0 keeps the 3-slot weight ring everywhere (A/B), 2 widens it
-void halo_res_set(int v) { g_halo_res = v; }
-
 static bool halo_setup(const cgan3d_conv_geom* g, HaloArgs* a) {
   if (g->prec != CGAN3D_PREC_BF16 || g->reflect) return false;
   if (!(g->cin == 32 || g->cin == 64) || g->cout % 16 || g->k > 4 || g->stride < 1 || g->stride > 2) return false;
@@ -646,16 +625,6 @@ static bool halo_setup(const cgan3d_conv_geom* g, HaloArgs* a) {
   if (slot != 2048 && slot != 4096 && slot != 8192) return false;
   a->halo_bytes = ez * ey * ex * (g->cin + 8) * 2;
   if (3 * slot + a->halo_bytes > 96 * 1024) return false;
-  // resident slabs: the most taps any class has (a stride-2 transposed class: <= 2 per dim)
-  int tmax = 1;
-  for (int d = 0; d < 3; ++d) {
-    int m = 0;
-    for (int r = 0; r < (g->transposed ? g->stride : 1); ++r)
-      m = std::max(m, class_info(r, g->k, g->stride, g->pad, g->transposed).n);
-    tmax *= m;
-  }
-  // (key 21 = 2 also lets the 27 taps of a stride-2 forward in: one block per CU at 32 -> 64)
-  a->nres = (g_halo_res && tmax > 3 && tmax * slot <= (g_halo_res == 2 ? 64 : 32) * 1024) ? tmax : 0;
   if (g->k * g->k * g->k > 64) return false;
   return true;
 }
@@ -716,11 +685,9 @@ int halo_launch(const cgan3d_conv_geom* g, const float* x, const float* w, float
     return CGAN3D_OK;
   }
   dim3 grid((unsigned)(a.nclass * a.n * a.td * a.th * a.tw), g->cout / a.bn);
-  const size_t lds = (a.nres ? a.nres : 3) * (size_t)a.bn * g->cin * 2 + a.halo_bytes;
+  const size_t lds = 3 * (size_t)a.bn * g->cin * 2 + a.halo_bytes;
   const __bf16* wp = reinterpret_cast<const __bf16*>(w);
-#define CG_HL(CI, NT)                                                                                     \
-  (a.nres ? ::cg::launch((conv_halo_kernel<CI, NT, true>), grid, dim3(256), lds, st, a, x, wp, y, e)      \
-          : ::cg::launch((conv_halo_kernel<CI, NT, false>), grid, dim3(256), lds, st, a, x, wp, y, e))
+#define CG_HL(CI, NT) ::cg::launch((conv_halo_kernel<CI, NT>), grid, dim3(256), lds, st, a, x, wp, y, e)
   if (g->cin == 64) {
     if (a.bn == 64) CG_HL(64, 4); else if (a.bn == 32) CG_HL(64, 2); else return CGAN3D_EINVAL;
   } else {

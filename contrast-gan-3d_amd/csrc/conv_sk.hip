@@ -22,8 +22,6 @@ namespace cg {
 
 typedef __bf16 bf16x8_k __attribute__((ext_vector_type(8)));
 
-__device__ __attribute__((aligned(16))) float g_sk_zero[4];  // source of the absent epilogue operands
-
 struct SkArgs {
   int n, di, hi, wi, do_, ho, wo, cin, cout, k, s, p, transposed;
   int nclass, cd, ch, cw;  // parity-class grid (transposed stride 2) or the output grid
@@ -104,25 +102,6 @@ __global__ __launch_bounds__(64 * W) void conv_sk_kernel(SkArgs a, const float* 
   f32x4 acc[NT];
 #pragma unroll
   for (int t = 0; t < NT; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-  // epilogue operands (LeakyReLU mask, residual, bias) loaded ahead of the K loop, unconditionally
-  // from clamped offsets (absent operands from a zero dummy through opaque pointers), so their round
-  // trip hides behind the K-steps instead of following the cross-wave combine
-  const int ro = rowo[row];
-  const bool has_mask = ep.mask_src != nullptr, has_res = ep.residual != nullptr, has_bias = ep.bias != nullptr;
-  uintptr_t pmk = has_mask ? (uintptr_t)ep.mask_src : (uintptr_t)g_sk_zero;
-  uintptr_t prs = has_res ? (uintptr_t)ep.residual : (uintptr_t)g_sk_zero;
-  uintptr_t pbs = has_bias ? (uintptr_t)ep.bias : (uintptr_t)g_sk_zero;
-  asm volatile("" : "+s"(pmk), "+s"(prs), "+s"(pbs));
-  f32x4 mk[NT], rs[NT], bs[NT];
-#pragma unroll
-  for (int t = 0; t < NT; ++t) {
-    const int c0 = t * 16 + 4 * g;
-    const bool ok = c0 < a.cout && ro >= 0;
-    const int o = ok ? ro * a.cout + c0 : 0;
-    mk[t] = *reinterpret_cast<const f32x4*>(reinterpret_cast<const float*>(pmk) + (has_mask ? o : 0));
-    rs[t] = *reinterpret_cast<const f32x4*>(reinterpret_cast<const float*>(prs) + (has_res ? o : 0));
-    bs[t] = *reinterpret_cast<const f32x4*>(reinterpret_cast<const float*>(pbs) + (has_bias && c0 < a.cout ? c0 : 0));
-  }
   // K loop (round 4).  Every slot is reloaded unconditionally from a clamped, always-valid address
   // and dead operands are zeroed by a select, so nothing in the loop branches.  NKC > 0 (the wave's
   // K-steps fit in NKC, the launcher's choice): the loop is straight-line code with a ring of
@@ -200,22 +179,32 @@ __global__ __launch_bounds__(64 * W) void conv_sk_kernel(SkArgs a, const float* 
   // epilogue: the MFMA ran transposed (A = weights, B = activations), so lane (g, r16) holds
   // channels t*16 + 4g .. +3 of row mt*16 + r16: one 16-byte store (and mask / residual load) per
   // lane and N tile (cout % 8 == 0: a lane's four channels are all in range or all out)
+  const int ro = rowo[mt * 16 + r16];
   float vals[NT][4];
-  const bool relu = ep.act == CGAN3D_ACT_RELU, lrelu = ep.act == CGAN3D_ACT_LRELU;
-  const float slope = ep.slope;
 #pragma unroll
   for (int t = 0; t < NT; ++t) {
     const int c0 = t * 16 + 4 * g;
     const bool ok = c0 < a.cout && ro >= 0;
-    f32x4 v = acc[t] + bs[t];
+    f32x4 v = acc[t];
+    if (ep.bias && c0 < a.cout) {
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj) v[jj] += ep.bias[c0 + jj];
+    }
 #pragma unroll
     for (int jj = 0; jj < 4; ++jj) {
-      v[jj] = relu ? fmaxf(v[jj], 0.f) : v[jj];
-      v[jj] = (lrelu & !(v[jj] > 0.f)) ? v[jj] * slope : v[jj];
-      v[jj] = (has_mask & !(mk[t][jj] > 0.f)) ? v[jj] * slope : v[jj];
+      if (ep.act == CGAN3D_ACT_RELU) v[jj] = fmaxf(v[jj], 0.f);
+      else if (ep.act == CGAN3D_ACT_LRELU) v[jj] = v[jj] > 0.f ? v[jj] : v[jj] * ep.slope;
     }
-    v += rs[t];
-    if (ok) *reinterpret_cast<f32x4*>(y + ro * a.cout + c0) = v;
+    if (ok) {
+      const int o = ro * a.cout + c0;
+      if (ep.mask_src) {
+        const f32x4 m = *reinterpret_cast<const f32x4*>(ep.mask_src + o);
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) v[jj] = m[jj] > 0.f ? v[jj] : v[jj] * ep.slope;
+      }
+      if (ep.residual) v += *reinterpret_cast<const f32x4*>(ep.residual + o);
+      *reinterpret_cast<f32x4*>(y + o) = v;
+    }
 #pragma unroll
     for (int jj = 0; jj < 4; ++jj) vals[t][jj] = ok ? v[jj] : 0.f;
   }
