@@ -270,53 +270,30 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_fold_kernel(const void* __re
   // 32-bit index math: C/4 a power of two (C divides 256), the padded volume below 2^31 float4
   // (checked by the callers); four 64-bit divides per float4 made this pass VALU-bound
   const int c4s = __builtin_ctz(C4);
-  // FU items per thread per trip, every main load issued before the first use (one round trip per
-  // trip instead of per item); voxel coordinates by multiply-high with block-uniform magic numbers
-  // (exact: the unpadded volume is far below 2^32 / max(D, H, W)) instead of three divisions
-  constexpr int FU = 4;
-  const unsigned mW = 0xffffffffu / (unsigned)W + 1u, mH = 0xffffffffu / (unsigned)H + 1u,
-                 mD = 0xffffffffu / (unsigned)D + 1u;
-  const unsigned stride = gridDim.x * blockDim.x, nn4 = (unsigned)n4;
-  for (unsigned i0 = blockIdx.x * blockDim.x + threadIdx.x; i0 < nn4; i0 += FU * stride) {
-    f32x4 zz[FU], dd[FU];
-    int base[FU], qd[FU][2], qh[FU][2], qw[FU][2], nd[FU], nh[FU], nw[FU];
-#pragma unroll
-    for (int u = 0; u < FU; ++u) {
-      const unsigned i = min(i0 + u * stride, nn4 - 1);
-      const unsigned v0 = i >> c4s;
-      const int c4 = (int)(i & (C4 - 1));
-      const unsigned v1 = __umulhi(v0, mW), v2 = __umulhi(v1, mH), v3 = __umulhi(v2, mD);
-      const int w = (int)(v0 - v1 * W), h = (int)(v1 - v2 * H), d = (int)(v2 - v3 * D), nb = (int)v3;
-      nd[u] = fold_src(d, D, P, qd[u]);
-      nh[u] = fold_src(h, H, P, qh[u]);
-      nw[u] = fold_src(w, W, P, qw[u]);
-      base[u] = nb * Dp;
-      zz[u] = load4<B16>(z, i);
-      dd[u] = load4<B16>(padded, ((((base[u] + qd[u][0]) * Hp + qh[u][0]) * Wp + qw[u][0]) << c4s) + c4);
+  for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < (unsigned)n4; i += gridDim.x * blockDim.x) {
+    const unsigned v0 = i >> c4s;
+    const int c4 = (int)(i & (C4 - 1));
+    const unsigned v1 = v0 / (unsigned)W, v2 = v1 / (unsigned)H, v3 = v2 / (unsigned)D;
+    const int w = (int)(v0 - v1 * W), h = (int)(v1 - v2 * H), d = (int)(v2 - v3 * D), nb = (int)v3;
+    int qd[2], qh[2], qw[2];
+    const int nd = fold_src(d, D, P, qd), nh = fold_src(h, H, P, qh), nw = fold_src(w, W, P, qw);
+    const f32x4 zz = load4<B16>(z, i);
+    f32x4 dd = load4<B16>(padded, ((((nb * Dp + qd[0]) * Hp + qh[0]) * Wp + qw[0]) << c4s) + c4);
+    if (nd * nh * nw > 1) {  // boundary voxel: its mirrored sources
+      for (int a = 0; a < nd; ++a)
+        for (int b = 0; b < nh; ++b)
+          for (int e = 0; e < nw; ++e)
+            if (a | b | e) dd += load4<B16>(padded, ((((nb * Dp + qd[a]) * Hp + qh[b]) * Wp + qw[e]) << c4s) + c4);
     }
+    f32x4 o;
 #pragma unroll
-    for (int u = 0; u < FU; ++u) {
-      const unsigned i = i0 + u * stride;
-      if (nd[u] * nh[u] * nw[u] > 1) {  // boundary voxel: its mirrored sources
-        const int c4 = (int)(min(i, nn4 - 1) & (C4 - 1));
-        for (int a = 0; a < nd[u]; ++a)
-          for (int b = 0; b < nh[u]; ++b)
-            for (int e = 0; e < nw[u]; ++e)
-              if (a | b | e)
-                dd[u] += load4<B16>(padded, ((((base[u] + qd[u][a]) * Hp + qh[u][b]) * Wp + qw[u][e]) << c4s) + c4);
-      }
-      f32x4 o;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const float g = dd[u][e] * act_grad(zz[u][e] * sc[e] + sf[e], act, slope);
-        const float xh = (zz[u][e] - mean[e]) * inv[e];
-        o[e] = k0[e] * (g - k1[e] - xh * k2[e]);
-      }
-      if (i < nn4) {
-        if (dz) o4[i] = o;
-        if (dz16) store16(dz16, i, o);
-      }
+    for (int e = 0; e < 4; ++e) {
+      const float g = dd[e] * act_grad(zz[e] * sc[e] + sf[e], act, slope);
+      const float xh = (zz[e] - mean[e]) * inv[e];
+      o[e] = k0[e] * (g - k1[e] - xh * k2[e]);
     }
+    if (dz) o4[i] = o;
+    if (dz16) store16(dz16, i, o);
   }
 }
 
@@ -732,20 +709,7 @@ __global__ __launch_bounds__(256) void bn_apply_acc_kernel(const double* __restr
 #pragma unroll
   for (int u = 0; u < ACC_PF; ++u)
     if (i0 + u * stride < n4) apply(i0 + u * stride, zp[u], rp[u]);
-  // the rest (16 float4 per thread at 64^3 x 16 channels, the grid being capped at 1024 blocks) four
-  // items per trip, loads first: one round trip per four items
-  for (long long j = i0 + ACC_PF * stride; j < n4; j += 4 * stride) {
-    f32x4 zq[4], rq[4];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const long long i = min(j + u * stride, n4 - 1);
-      zq[u] = load4<Z16>(z, i);
-      if (RES) rq[u] = r4[i];
-    }
-#pragma unroll
-    for (int u = 0; u < 4; ++u)
-      if (j + u * stride < n4) apply(j + u * stride, zq[u], RES ? rq[u] : f32x4{});
-  }
+  for (long long i = i0 + ACC_PF * stride; i < n4; i += stride) apply(i, load4<Z16>(z, i), RES ? r4[i] : f32x4{});
 }
 
 template <bool B16>  // dy and z in bf16
@@ -806,18 +770,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_acc_kernel(const double* __r
 #pragma unroll
   for (int u = 0; u < ACC_PF; ++u)
     if (i0 + u * stride < n4) apply(i0 + u * stride, zp[u], dp[u]);
-  for (long long j = i0 + ACC_PF * stride; j < n4; j += 4 * stride) {  // four items per trip, loads first
-    f32x4 zq[4], dq[4];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const long long i = min(j + u * stride, n4 - 1);
-      zq[u] = load4<B16>(z, i);
-      dq[u] = load4<B16>(dy, i);
-    }
-#pragma unroll
-    for (int u = 0; u < 4; ++u)
-      if (j + u * stride < n4) apply(j + u * stride, zq[u], dq[u]);
-  }
+  for (long long i = i0 + ACC_PF * stride; i < n4; i += stride) apply(i, load4<B16>(z, i), load4<B16>(dy, i));
 }
 
 // blocks of the accumulator passes: ~2 float4 per thread, at most `cap` blocks — each block reads the
