@@ -4,6 +4,7 @@ set -o pipefail
 R=$GRAFT_REPO_ROOT
 cd /tmp && export TMPDIR=/tmp
 mkdir -p $R/gpurun_out
+timeout -k 10 200 python3 $R/bench.py --precision f32 --no-sub --no-cpu-baseline > $R/gpurun_out/fin_bench_f32.json 2> $R/gpurun_out/fin_bench_f32.err || exit $?
 rm -rf $R/gpurun_out/fin_trace $R/gpurun_out/fin_fetch $R/gpurun_out/fin_write $R/gpurun_out/fin_sq
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/fin_trace -o run -- python3 $R/bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-sub > $R/gpurun_out/fin_trace.json 2> $R/gpurun_out/fin_trace.err || exit $?
 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex conv_k3m_kernel --output-format csv -d $R/gpurun_out/fin_fetch -o run -- python3 $R/bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-sub --mode eager > $R/gpurun_out/fin_fetch.log 2>&1 || exit $?
