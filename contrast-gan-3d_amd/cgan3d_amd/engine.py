@@ -916,8 +916,7 @@ class CriticPlan:
             ly = self.layers[i]
             g = ops.with_prec(ops.conv_wgrad_geom(n_all, ly.din, ly.dout, ly.cin, ly.cout, ly.k, ly.s, ly.p, planar=self.pl), self.prec)
             self._wgrad(g, prev, self.dz[i][:n_all], G[f"{ly.name}.weight"], ws, zeroed, layer=i)
-
-        def side0_segment():  # bias sums + the first layer's weight grad on the second side stream
+        if self.side0 is not None:  # bias sums + the first layer's weight grad beside the chain below
             ops.stream_wait(self.side0, torch.cuda.current_stream(self.device))
             with torch.cuda.stream(self.side0):
                 self._bias_sums(G, n_bias, side=True).run()
@@ -931,12 +930,7 @@ class CriticPlan:
                 atomic = zeroed and ops.wgrad_ws_atomic(g)
                 ops.wgrad(g, x_all, self.dz[0][:n_all], G[f"{ly.name}.weight"], self.ws_side0, accumulate=zeroed,
                           ws_clean=atomic)
-        # CGAN3D_TUNE key 102 = 1: hand that segment over after the forward-mode chain instead of
-        # before it (beside the grouped weight grads rather than the chain's small-grid kernels)
-        late0 = self.side0 is not None and L.py_tune(102, 0) == 1
-        if self.side0 is not None and not late0:
-            side0_segment()
-        elif self.side0 is None:
+        else:
             self._on_side(lambda: self._bias_sums(G, n_bias, side=True).run())
             self._on_side(lambda: wgrad(0, x_all))
         h = gamma
@@ -951,8 +945,6 @@ class CriticPlan:
                 group.append(i + 1)
             else:
                 self._on_side(lambda i=i: wgrad(i + 1, self.a[i][:n_all]))  # a_i now holds nu_i in its interp rows
-        if late0:
-            side0_segment()
         for k in range(0, len(group), 4):  # a grouped launch takes at most 4 (discriminator_depth >= 5)
             self._wgrad_group(G, group[k:k + 4], n_all)
         self._on_side(self._flush_unpack)
