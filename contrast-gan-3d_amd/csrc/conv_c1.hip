@@ -372,7 +372,8 @@ int c1_wgrad_launch(const cgan3d_conv_geom* g, const float* x, const float* dz, 
   // <= ~256 blocks adding into dW (measured: 1024 blocks of one tile each, 36 -> 47 us at 64^3 B=4);
   // two tile groups per block when there are tiles for both (cgan3d_set_tuning key 18: 1 forces one)
   const int G = (g_c1_groups == 1 || ntiles < 512) ? 1 : 2;
-  a.tiles_per_block = std::max(1, std::min(8 * G, ntiles / 256));
+  // key 18 = 3: 8 tiles per block (192 blocks at 12 x 64^3), leaving CUs to the main stream's kernels
+  a.tiles_per_block = g_c1_groups == 3 ? 8 : std::max(1, std::min(8 * G, ntiles / 256));
   if (G == 2)
     ::cg::launch(c1_wgrad_kernel<2>, dim3(ceil_div(ntiles, a.tiles_per_block)), dim3(512), 0, st, a, x, dz, dw, ntiles);
   else
