@@ -318,7 +318,7 @@ __global__ __launch_bounds__(256 * G) void c1_wgrad_kernel(C1Args a, const float
   }
 }
 
-static int g_c1_groups = 2;
+static int g_c1_groups = 3;  // 3: two tile groups, 8 tiles per block (A/B: 1.447 / 1.443 / 1.455 vs 1.471 / 1.473 / 1.472 at 6)
 void c1_groups_set(int v) { g_c1_groups = v; }
 
 // roles this file takes (geometries as built by cgan3d_amd/ops.py)
