@@ -109,7 +109,16 @@ def cpu_baseline(size, seconds, g_args):
         el = time.perf_counter() - t0
         if el >= seconds or n >= 50:
             break
+    cpu_model = None
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                cpu_model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
     return {"value": round(n * b / el, 4), "unit": "patches/s", "cores": threads, "kind": "port",
+            "cpu_model": cpu_model, "torch_threads": torch.get_num_threads(),
             "sample": f"oracle/reference_torch.py train_step, {size}^3, batch 1+1, GP conf, fp32, {n} steps in "
                       f"{el:.1f}s after 1 warm-up step; patches/s per subopt patch at batch 1 stands for the GPU "
                       f"line's batch (the CPU step's work and time grow linearly with the batch)"}
@@ -522,6 +531,9 @@ def main():
         # workload, and configs[2] (128^3 B=1 fp32)
         out["f32"] = sub_config(S, B, "f32", dev, g_args) if args.precision != "f32" else None
         out["b128_f32"] = sub_config(128, 1, "f32", dev, g_args, steps=10)
+        # configs[4]'s per-GPU slice: 128^3 bf16 with the gradient penalty, 2 OPT + 2 subopt patches
+        # (global batch 16 over 8 GPUs)
+        out["b128_bf16_b2"] = sub_config(128, 2, "bf16", dev, g_args, steps=10)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(S, args.cpu_seconds, g_args)
     if rank == 0:

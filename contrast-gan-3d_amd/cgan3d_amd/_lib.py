@@ -124,6 +124,7 @@ _SIGS = {
     "cgan3d_reflect_fold_ex": ([_P, _P, _I32, _I32, _I32, _I32, _I32, _I32, _P, _P], _I32),
     "cgan3d_reflect_fold2d": ([_P, _P, _I32, _I32, _I32, _I32, _I32, _P, _P], _I32),
     "cgan3d_gp_interpolate": ([_P, _P, _P, _P, _I32, _I64, _P], _I32),
+    "cgan3d_gp_interpolate_idx": ([_P, _P, _P, _P, _P, _I32, _I64, _P], _I32),
     "cgan3d_tanh_backward": ([_P, _P, _P, _I64, _P], _I32),
     "cgan3d_unpack_patches": ([_P, _I32, _I64, _F, _F, _P, _P, _P], _I32),
     "cgan3d_augment_ws_floats": ([_I32, _I32, _I32, _I32, _I32], _I64),

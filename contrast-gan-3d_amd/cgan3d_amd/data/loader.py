@@ -93,10 +93,35 @@ def read_crop(vol: np.ndarray, patch: Sequence[int], box, out: np.ndarray):
     out[dx:dx + lx, dy:dy + ly, dz:dz + lz] = vol[sx:sx + lx, sy:sy + ly, sz:sz + lz]
 
 
+class _MetaUnpickler:
+    """Restricted unpickling of the reference's ``_meta.pkl`` records (data/utils.py:48-54: a dict of
+    numpy arrays, floats and a name): only builtin containers / scalars and numpy array / dtype /
+    scalar reconstruction resolve; any other global (arbitrary code) raises UnpicklingError."""
+
+    ALLOWED = {("builtins", n) for n in ("dict", "list", "tuple", "set", "frozenset", "str", "int", "float",
+                                          "complex", "bool", "bytes", "bytearray", "slice", "range")}
+    ALLOWED |= {(m, n) for m in ("numpy.core.multiarray", "numpy._core.multiarray")
+                for n in ("_reconstruct", "scalar")}
+    ALLOWED |= {("numpy", "ndarray"), ("numpy", "dtype"), ("collections", "OrderedDict")}
+
+    @classmethod
+    def load(cls, f):
+        import pickle
+
+        class _U(pickle.Unpickler):
+            def find_class(self, module, name):
+                if (module, name) in cls.ALLOWED or (module == "numpy" and name.endswith("DType")) or \
+                        (module == "numpy.dtypes" and name.endswith("DType")):
+                    return super().find_class(module, name)
+                raise pickle.UnpicklingError(f"_meta.pkl: global {module}.{name} is not allowed")
+        return _U(f).load()
+
+
 def load_meta(path: str) -> dict:
     """A scan's metadata (offset, spacing, centerlines_world, name): ``<path>_meta.npz`` (numeric
     arrays, no code), else the reference's ``<path>_meta.pkl`` (data/utils.py:48-54 writes and reads
-    it with pickle; the scan preparation of the user's own dataset)."""
+    it with pickle; the scan preparation of the user's own dataset) through a restricted unpickler
+    that resolves numpy arrays and builtin containers only (_MetaUnpickler)."""
     npz = Path(path + "_meta.npz")
     if npz.is_file():
         with np.load(npz, allow_pickle=False) as z:
@@ -104,9 +129,8 @@ def load_meta(path: str) -> dict:
         if "name" in meta:
             meta["name"] = str(meta["name"])
         return meta
-    import pickle
     with open(path + "_meta.pkl", "rb") as f:
-        return pickle.load(f)
+        return _MetaUnpickler.load(f)
 
 
 def world_to_image(world, offset, spacing) -> np.ndarray:

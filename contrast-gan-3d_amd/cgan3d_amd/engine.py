@@ -30,6 +30,7 @@ import os
 from dataclasses import dataclass
 from typing import Callable, Dict, List, Optional, Sequence, Tuple
 
+import numpy as np
 import torch
 
 from . import _lib as L
@@ -1049,8 +1050,6 @@ class StepEngine:
                  gp_weight: float = 10.0, hu_bounds=(112.0 / 600.0, 212.0 / 600.0), gan_w=1.0, sim_w=1.0, hu_w=1.0,
                  device=None, g_optim=None, d_optim=None, process_group=None, precision: str = "f32",
                  weight_clip: Optional[float] = None):
-        if b_opt != b_sub:
-            raise NotImplementedError("StepEngine: the GP path assumes |OPT| == |LOW|+|HIGH| (basic_conf.py:74-79)")
         if d_cfg.norm not in ("identity", "batch", "layer"):
             raise NotImplementedError(f"StepEngine: critic norm {d_cfg.norm!r}")
         # gradient penalty unless weight clipping (Trainer.py:122-131): the GP conf (Identity-norm
@@ -1109,6 +1108,12 @@ class StepEngine:
         self.subopt = torch.empty((b_sub, *dims, 1), device=device)
         self.mask = torch.empty((b_sub, *dims, 1), device=device, dtype=torch.uint8)
         self.eps = torch.empty(self.b_gp, device=device)
+        # |real| != |fake| (model/utils.py:21-25): the penalty interpolates min(|real|, |fake|) rows drawn
+        # with replacement from each batch (set_gp_indices / draw_gp_indices, before each step; the
+        # interpolation kernel reads them from this device buffer, so recorded plans follow them)
+        self.gp_idx = None
+        if b_opt != b_sub and weight_clip is None:
+            self.gp_idx = torch.cat([torch.arange(self.b_gp), torch.arange(self.b_gp)]).to(torch.int32).to(device)
         self.gbuf = torch.empty((self.b_gp, *dims, 1), device=device)    # g = dD/dx at the interpolation
         self.dcrit = torch.empty((b_sub, *dims, 1), device=device)       # dL_G/d opt_hat via the critic
         self.losses = torch.zeros(8, device=device)
@@ -1332,6 +1337,26 @@ class StepEngine:
         self.mask.view(-1).copy_(mask.reshape(-1), non_blocking=True)
         self.eps.copy_(eps.reshape(-1), non_blocking=True)
 
+    def set_gp_indices(self, real_rows, fake_rows):
+        """Rows of the real (OPT) and fake (opt_hat) batches the gradient penalty interpolates when
+        their sizes differ (model/utils.py:21-25: ``real_batch[rng.integers(len(real), size=m)]``)."""
+        if self.gp_idx is None:
+            raise ValueError("set_gp_indices: |real| == |fake|, the penalty interpolates rows 1:1")
+        r = np.asarray(real_rows, dtype=np.int64).reshape(-1)
+        f = np.asarray(fake_rows, dtype=np.int64).reshape(-1)
+        if r.size != self.b_gp or f.size != self.b_gp:
+            raise ValueError(f"set_gp_indices: {self.b_gp} rows each")
+        if r.min() < 0 or r.max() >= self.b_opt or f.min() < 0 or f.max() >= self.b_sub:
+            raise ValueError("set_gp_indices: row out of range")
+        self.gp_idx.copy_(torch.from_numpy(np.concatenate([r, f]).astype(np.int32)), non_blocking=False)
+
+    def draw_gp_indices(self, rng: np.random.Generator):
+        """The reference's draw (model/utils.py:24-25): real rows first, then fake rows."""
+        r = rng.integers(self.b_opt, size=self.b_gp)
+        f = rng.integers(self.b_sub, size=self.b_gp)
+        self.set_gp_indices(r, f)
+        return r, f
+
     # -------------------------------------------------------------------------------------------
     def _write_dlogits(self):
         """The constant dlogits (float32 arithmetic, as critic_logits_kernel / gen_logits_kernel)."""
@@ -1364,7 +1389,10 @@ class StepEngine:
             return self._critic_update_clip()
         D, bo, bs, bg, V = self.D, self.b_opt, self.b_sub, self.b_gp, self.vox
         nall = bo + bs + bg
-        ops.gp_interpolate(self.xc[:bg], self.xc[bo:bo + bg], self.eps, self.xc[bo + bs:], bg, V)
+        if self.gp_idx is None:
+            ops.gp_interpolate(self.xc[:bg], self.xc[bo:bo + bg], self.eps, self.xc[bo + bs:], bg, V)
+        else:  # |real| != |fake|: resampled rows (model/utils.py:21-25)
+            ops.gp_interpolate(self.xc[:bo], self.xc[bo:bo + bs], self.eps, self.xc[bo + bs:], bg, V, idx=self.gp_idx)
         D.forward(self.dP, self.xc, 0, nall)
         if not self.fold_logits:
             ops.critic_logits_grad(D.a[-1], bo, bs, bg, D.logit_ps, self.gan_w, D.dz[-1], self.losses)

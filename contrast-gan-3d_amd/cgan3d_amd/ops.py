@@ -321,20 +321,36 @@ class NativeComm:
     RCCL library torch loaded — one communicator per process.  ``own=True`` (or
     CGAN3D_COMM=own): a communicator of this library, rank 0's unique id broadcast through
     ``group`` once (measured: a second communicator in the process slows every kernel of a one-GPU
-    step ~2.4x, profiles/r03_dp1_probe.json)."""
+    step ~2.4x, profiles/r03_dp1_probe.json).  When the group's communicator cannot be reached (a
+    torch without ``_comm_ptr``, or another RCCL library than the one this build drives) the own
+    communicator is used, with a warning.
+
+    A group on another backend (gloo, CPU dry runs — tests/test_dist.py): the same object and call
+    sequence, the collective itself done by torch.distributed on ``group`` (``self.handle`` None)."""
 
     def __init__(self, group=None, device=None, own=None):
         import torch.distributed as dist
-        lib = L.lib()
         self.world, self.rank = dist.get_world_size(group), dist.get_rank(group)
         self.owned = False
+        self.group = group
+        self.handle = None
+        if dist.get_backend(group) != "nccl":
+            return
+        lib = L.lib()
         if own is None:
             own = COMM_MODE == "own"
         if not own:
             ptr = self._torch_comm(group, device)
-            if ptr and int(lib.cgan3d_comm_shared_library()) == 1:
+            shared = int(lib.cgan3d_comm_shared_library()) == 1
+            if ptr and shared:
                 self.handle = ctypes.c_void_p(ptr)
                 return
+            import warnings
+            why = ("ProcessGroupNCCL._comm_ptr is unavailable in this torch" if not ptr else
+                   "torch's RCCL library is not the one libcgan3d drives")
+            warnings.warn(f"NativeComm: {why}; using a communicator of this library instead (CGAN3D_COMM=own: "
+                          "one more communicator in the process, measured ~2.4x slower kernels on one GPU)",
+                          RuntimeWarning, stacklevel=2)
         self.owned = True
         nb = int(lib.cgan3d_comm_id_bytes())
         uid = torch.zeros(nb, dtype=torch.uint8, device=device)
@@ -368,6 +384,11 @@ class NativeComm:
 
     def allreduce_mean(self, t: torch.Tensor):
         """t = mean over the ranks of t (fp32, contiguous), on the current stream."""
+        if self.handle is None:  # non-RCCL group (gloo): torch.distributed does the exchange
+            import torch.distributed as dist
+            dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group)
+            t.mul_(1.0 / self.world)
+            return
         _need(t, t.numel(), "allreduce_mean")
         check(_launch("cgan3d_allreduce_mean", self.handle, ptr(t), t.numel()), "allreduce_mean")
 
@@ -966,12 +987,24 @@ def reflect_fold(padded, out, n, dims: Sequence[int], c, pad, ep: Optional[Epi] 
           "reflect_fold_ex")
 
 
-def gp_interpolate(real, fake, eps, out, b, per_sample):
-    for t, nm in ((real, "real"), (fake, "fake"), (out, "out")):
-        _need(t, b * per_sample, f"gp_interpolate {nm}")
+def gp_interpolate(real, fake, eps, out, b, per_sample, idx=None):
+    """out = eps * real + (1 - eps) * fake per sample; ``idx`` (device int32 [2 b]): rows of ``real`` /
+    ``fake`` resampled by the host when their batch sizes differ (model/utils.py:21-25)."""
+    _need(out, b * per_sample, "gp_interpolate out")
     _need(eps, b, "gp_interpolate eps")
-    check(_launch("cgan3d_gp_interpolate", ptr(real), ptr(fake), ptr(eps), ptr(out), b, per_sample),
-          "gp_interpolate")
+    if idx is None:
+        for t, nm in ((real, "real"), (fake, "fake")):
+            _need(t, b * per_sample, f"gp_interpolate {nm}")
+        check(_launch("cgan3d_gp_interpolate", ptr(real), ptr(fake), ptr(eps), ptr(out), b, per_sample),
+              "gp_interpolate")
+        return
+    if idx.dtype != torch.int32 or idx.numel() != 2 * b or not idx.is_contiguous():
+        raise ValueError("gp_interpolate: idx must be contiguous int32 [2 b]")
+    if real.numel() % per_sample or fake.numel() % per_sample:
+        raise ValueError("gp_interpolate: real / fake must hold whole samples")
+    # the rows in idx are range-checked by whoever writes them (StepEngine.set_gp_indices), on the host
+    check(_launch("cgan3d_gp_interpolate_idx", ptr(real), ptr(fake), ptr(idx), ptr(eps), ptr(out), b, per_sample),
+          "gp_interpolate_idx")
 
 
 def tanh_backward(y, dy, dz):

@@ -111,19 +111,53 @@ class Trainer:
         slots = {"D": L.L_D, "G": L.L_G, "G-full": L.L_GFULL, "sim": L.L_SIM, "HU": L.L_HU}
         return {k: self.engine.losses[slots[k]] for k in keys}
 
+    @staticmethod
+    def _same(t: Optional[Tensor], slot: Tensor) -> bool:
+        """``t`` is None (the engine's resident operand), that operand itself, or equal to it."""
+        if t is None:
+            return True
+        if t.numel() != slot.numel():
+            return False
+        if t.device == slot.device and t.data_ptr() == slot.data_ptr():
+            return True
+        return bool(torch.equal(t.detach().reshape(-1).to(slot.device, slot.dtype), slot.reshape(-1)))
+
+    def _need_engine(self, who: str) -> StepEngine:
+        if self.engine is None:
+            raise RuntimeError(f"Trainer.{who}: no step engine yet (Trainer.train_step builds it from the first batch)")
+        return self.engine
+
     def train_critic(self, real: Tensor, reconstructions: Tensor, retain_graph: bool) -> Dict[str, Tensor]:
-        """Critic update (Trainer.py:108-142) on the engine's resident batch."""
+        """Critic update (Trainer.py:108-142) on ``real`` and ``reconstructions`` (treated as data, as the
+        reference's ``reconstructions.detach()``): tensors other than the engine's resident batch are
+        copied into its slots first (same shapes required); None = the resident batch."""
+        eng = self._need_engine("train_critic")
+        for t, slot, name in ((real, eng.xc[:eng.b_opt], "real"), (reconstructions, eng.opt_hat, "reconstructions")):
+            if t is not None and not (t.device == slot.device and t.data_ptr() == slot.data_ptr()):
+                if t.numel() != slot.numel():
+                    raise ValueError(f"train_critic: {name} has {t.numel()} elements, the engine's batch "
+                                     f"{slot.numel()} (batch and patch size are fixed per engine)")
+                slot.view(-1).copy_(t.detach().reshape(-1), non_blocking=True)
         self.optimizer_D.sync_hyper()
-        self.engine.critic_update()
+        eng.critic_update()
         if self.lr_scheduler_D is not None:
             self.lr_scheduler_D.step()
         return self._losses(["D"])
 
     def train_generator(self, inputs: Tensor, reconstructions: Tensor, centerlines_masks: Tensor
                         ) -> Dict[str, Tensor]:
-        """Generator update (Trainer.py:144-161) on the engine's resident batch."""
+        """Generator update (Trainer.py:144-161).  The backward runs through the activations of the
+        engine's last generator forward, so ``reconstructions`` must be that forward's output and
+        ``inputs`` / ``centerlines_masks`` its batch (None = the resident ones); anything else raises
+        ValueError rather than silently training on another batch."""
+        eng = self._need_engine("train_generator")
+        for t, slot, name in ((inputs, eng.subopt, "inputs"), (reconstructions, eng.opt_hat, "reconstructions"),
+                              (centerlines_masks, eng.mask, "centerlines_masks")):
+            if not self._same(t, slot):
+                raise ValueError(f"train_generator: {name} is not the batch of the engine's last generator forward "
+                                 "(Trainer.train_step loads the batch and runs that forward)")
         self.optimizer_G.sync_hyper()
-        self.engine.generator_update()
+        eng.generator_update()
         if self.lr_scheduler_G is not None:
             self.lr_scheduler_G.step()
         return self._losses(["G", "G-full", "sim", "HU"])
@@ -143,6 +177,11 @@ class Trainer:
             ml = low["seg"].numel()
             eng.mask.view(-1)[:ml].copy_(low["seg"].reshape(-1), non_blocking=True)
             eng.mask.view(-1)[ml:].copy_(high["seg"].reshape(-1), non_blocking=True)
+        # |OPT| != |LOW|+|HIGH|: the penalty's rows resampled on the host (model/utils.py:21-25, rng=self.rng)
+        if eng.gp_idx is not None:
+            if self.rng is None:
+                self.rng = np.random.default_rng()
+            eng.draw_gp_indices(self.rng)
         # eps ~ U[0,1) per interpolated sample, drawn on the device (model/utils.py:26)
         eng.eps.uniform_(0.0, 1.0)
         do_c = iteration % self.train_critic_every == 0

@@ -204,7 +204,6 @@ void k7m_w2n_launch(const cgan3d_conv_geom* g, int P, int reflect, long long wc,
                     float* y, const Epi& e, hipStream_t s);
 // implicit-GEMM forward / input-grad (conv_gemm.hip)
 int gemm_blocks(const cgan3d_conv_geom* g, long long* mblocks);
-void cout1_wave_set(int v);
 bool wgrad_bf16_ok(const cgan3d_conv_geom* g);
 bool wgrad_c1_ok(const cgan3d_conv_geom* g);
 bool wgrad_k3_ok(const cgan3d_conv_geom* g);
@@ -233,10 +232,6 @@ int wgrad_k3_launch(const cgan3d_conv_geom* g, const float* gathered, const floa
                     const __bf16* a16, float* dw, int accumulate,
                     float* ws, hipStream_t st);
 int wgrad_c1_launch(const cgan3d_conv_geom* g, const float* gathered, const float* aligned, float* dw, hipStream_t st);
-void wgrad_bf16_set_blocks(int v);
-void halo_set_min_blocks(int v);
-void k3_tile_set(int v);
-void k3_split_set(int v);
 int wgrad_bf16_group_launch(const cgan3d_conv_geom* geoms, const float* const* gathered, const float* const* aligned,
                             float* const* ws, int n, hipStream_t st);
 int wgrad_bf16_launch(const cgan3d_conv_geom* g, const float* gathered, const float* aligned, float* dwp,
@@ -247,9 +242,6 @@ bool k3m_geom_ok(const cgan3d_conv_geom* g);
 bool k3m_route(const cgan3d_conv_geom* g);
 int k3m_launch(const cgan3d_conv_geom* g, const __bf16* wp, float* y, const Epi& e, hipStream_t st);
 void k3m_set(int v);
-void k3m_probe_set(int v);
-void c1_groups_set(int v);
-void wgrad_k3m_probe_set(int v);
 void k7wg_blocks_set(int v);
 bool halo_ok(const cgan3d_conv_geom* g);         // w_packed == 2 and eligible
 bool halo_format_ok(const cgan3d_conv_geom* g);  // eligible ignoring w_packed
@@ -261,7 +253,6 @@ long long c1_dgrad_blocks(const cgan3d_conv_geom* g);
 int s2_kind(const cgan3d_conv_geom* g);
 long long s2_blocks(const cgan3d_conv_geom* g);
 int s2_launch(const cgan3d_conv_geom* g, const float* x, const __bf16* wp, float* y, const Epi& e, hipStream_t st);
-void s2_set(int v);
 int halo_pack(const cgan3d_conv_geom* g, const float* w, void* wp, hipStream_t st);
 int gemm_launch(const cgan3d_conv_geom* g, const float* x, const float* w, float* y, const Epi& e, hipStream_t st);
 // Adam over a flat arena (+ optional repack of packed weight copies, step tick) — conv_gemm.hip

@@ -546,8 +546,6 @@ __global__ __launch_bounds__(256) void wgrad_unpack_multi_kernel(const cgan3d_un
 using namespace cg;
 
 namespace cg {
-static int g_cout1_wave = 0;  // cgan3d_set_tuning key 14: 1 keeps the wave-per-voxel kernel (A/B)
-void cout1_wave_set(int v) { g_cout1_wave = v; }
 }  // namespace cg
 
 static Epi to_epi(const cgan3d_epilogue* ep) {
@@ -695,7 +693,7 @@ cout1:
     size_t lds = (size_t)geom_taps(g) * g->cin * sizeof(float);
     CG_CHECK_ARG(lds <= 64 * 1024, "cgan3d_conv3d_fwd: cout==1 weights exceed LDS");
     const long long r4 = (long long)geom_taps(g) * g->cin / 4;
-    if (!g->transposed && g->cin % 4 == 0 && a.class_vox <= 4096 && r4 <= 2048 && !g_cout1_wave) {
+    if (!g->transposed && g->cin % 4 == 0 && a.class_vox <= 4096 && r4 <= 2048) {
       // very few outputs, long reductions: a block per output voxel
       ::cg::launch(conv_cout1_block_kernel, dim3((unsigned)a.class_vox), dim3(256), 0, s, a, x, w, y, e);
       CG_LAUNCH_CHECK("conv_cout1_block_kernel");
@@ -725,7 +723,7 @@ cout1:
     CG_LAUNCH_CHECK("conv_halo_kernel");
     return CGAN3D_OK;
   }
-  if (!g->w_packed && cin1t_ok(g) && !g_cout1_wave) {  // the critic's last-layer input-grad
+  if (!g->w_packed && cin1t_ok(g)) {  // the critic's last-layer input-grad
     CG_CHECK_ARG(!e.stats && !e.bn_mode && !e.out2 && !e.minuend && !e.x16 && !e.fz.acc_mode,
                  "cgan3d_conv3d_fwd: cin == 1 transposed launch: bias / activation / mask / residual epilogue only");
     ConvArgs a;
@@ -743,7 +741,7 @@ cout1:
 }
 
 extern "C" int32_t cgan3d_conv3d_cin1t(const cgan3d_conv_geom* g) {
-  return g && !validate(g, "cgan3d_conv3d_cin1t") && cin1t_ok(g) && !g_cout1_wave ? 1 : 0;
+  return g && !validate(g, "cgan3d_conv3d_cin1t") && cin1t_ok(g) ? 1 : 0;
 }
 
 static long long wgrad_vpb(long long V, int gx_blocks) {

@@ -318,8 +318,6 @@ __global__ __launch_bounds__(256 * G) void c1_wgrad_kernel(C1Args a, const float
   }
 }
 
-static int g_c1_groups = 3;  // 3: two tile groups, 8 tiles per block (A/B: 1.447 / 1.443 / 1.455 vs 1.471 / 1.473 / 1.472 at 6)
-void c1_groups_set(int v) { g_c1_groups = v; }
 
 // roles this file takes (geometries as built by cgan3d_amd/ops.py)
 bool c1_fwd_ok(const cgan3d_conv_geom* g) {
@@ -369,11 +367,12 @@ int c1_dgrad_launch(const cgan3d_conv_geom* g, const float* dz, const float* w, 
 int c1_wgrad_launch(const cgan3d_conv_geom* g, const float* x, const float* dz, float* dw, hipStream_t st) {
   C1Args a = c1_args(g);
   const int ntiles = a.n * a.tz * a.ty * a.tx;
-  // <= ~256 blocks adding into dW (measured: 1024 blocks of one tile each, 36 -> 47 us at 64^3 B=4);
-  // two tile groups per block when there are tiles for both (cgan3d_set_tuning key 18: 1 forces one)
-  const int G = (g_c1_groups == 1 || ntiles < 512) ? 1 : 2;
-  // key 18 = 3: 8 tiles per block (192 blocks at 12 x 64^3), leaving CUs to the main stream's kernels
-  a.tiles_per_block = g_c1_groups == 3 ? 8 : std::max(1, std::min(8 * G, ntiles / 256));
+  // at most ~192 blocks adding into dW (measured: 1024 blocks of one tile each, 36 -> 47 us at 64^3
+  // B=4; 192 blocks of 8 tiles at 12 x 64^3 leave CUs to the main stream's kernels: A/B 1.447 / 1.443 /
+  // 1.455 vs 1.471 / 1.473 / 1.472 ms/step at 256 blocks); two tile groups per block when there are
+  // tiles for both.  Small grids keep one tile per block (ntiles / 192 rounds to 0-1).
+  const int G = ntiles < 512 ? 1 : 2;
+  a.tiles_per_block = std::max(1, ntiles / 192);
   if (G == 2)
     ::cg::launch(c1_wgrad_kernel<2>, dim3(ceil_div(ntiles, a.tiles_per_block)), dim3(512), 0, st, a, x, dz, dw, ntiles);
   else

@@ -42,9 +42,9 @@ struct GemmCfg {
   int wm, nbw, bm, bn, gy;
 };
 
-// tuning knob (cgan3d_set_tuning key 0): grids with fewer 64-voxel tiles than this use the
-// 32 x 32 tile (more, smaller blocks: latency hiding for the 16^3-voxel ResNet layers)
-static int g_small_tile_below = 1024;
+// grids with fewer 64-voxel tiles than this use the 32 x 32 tile (more, smaller blocks: latency
+// hiding for the 16^3-voxel ResNet layers)
+constexpr int g_small_tile_below = 1024;
 
 // deterministic tile-shape choice (also sizes the BatchNorm statistics buffer)
 static GemmCfg gemm_cfg(const cgan3d_conv_geom* g) {
@@ -651,22 +651,20 @@ extern "C" int32_t cgan3d_packed_format(const cgan3d_conv_geom* g) {
 }
 
 extern "C" int cgan3d_set_tuning(int32_t key, int32_t value) {
-  if (key == 0) { g_small_tile_below = value; return CGAN3D_OK; }
-  if (key == 1) { wgrad_bf16_set_blocks(value); return CGAN3D_OK; }
-  if (key == 2) { halo_set_min_blocks(value); return CGAN3D_OK; }
-  if (key == 3) { k3_tile_set(value); return CGAN3D_OK; }
-  if (key == 4) { s2_set(value); return CGAN3D_OK; }
-  if (key == 9) { wgrad_k3_set_chunks(value); return CGAN3D_OK; }
-  if (key == 10) { wgrad_s2_set_blocks(value); return CGAN3D_OK; }
-  if (key == 12) { k3_split_set(value); return CGAN3D_OK; }
-  if (key == 13) { k7s_set(value); return CGAN3D_OK; }
-  if (key == 14) { cout1_wave_set(value); return CGAN3D_OK; }
-  if (key == 15) { k3m_set(value); return CGAN3D_OK; }
-  if (key == 16) { wgrad_k3m_set(value); return CGAN3D_OK; }
-  if (key == 17) { k3m_probe_set(value); return CGAN3D_OK; }
-  if (key == 18) { c1_groups_set(value); return CGAN3D_OK; }
-  if (key == 19) { wgrad_k3m_probe_set(value); return CGAN3D_OK; }
-  if (key == 20) { k7wg_blocks_set(value); return CGAN3D_OK; }
+  // six keys, each choosing between correct launch shapes or kernels (tests compare kernels through
+  // 13 / 15 / 16); anything else is rejected
+  switch (key) {
+    case 9: CG_CHECK_ARG(value >= 0, "cgan3d_set_tuning 9: chunks >= 0"); wgrad_k3_set_chunks(value); return CGAN3D_OK;
+    case 10: CG_CHECK_ARG(value >= 0, "cgan3d_set_tuning 10: blocks >= 0"); wgrad_s2_set_blocks(value); return CGAN3D_OK;
+    case 13:
+      CG_CHECK_ARG(value == -1 || value == 0 || value == 8 || value == 16, "cgan3d_set_tuning 13: -1, 0, 8 or 16");
+      k7s_set(value);
+      return CGAN3D_OK;
+    case 15: CG_CHECK_ARG(value == 0 || value == 1, "cgan3d_set_tuning 15: 0 or 1"); k3m_set(value); return CGAN3D_OK;
+    case 16: CG_CHECK_ARG(value == 0 || value == 1, "cgan3d_set_tuning 16: 0 or 1"); wgrad_k3m_set(value); return CGAN3D_OK;
+    case 20: CG_CHECK_ARG(value > 0, "cgan3d_set_tuning 20: blocks > 0"); k7wg_blocks_set(value); return CGAN3D_OK;
+    default: break;
+  }
   set_error("cgan3d_set_tuning: unknown key %d", key);
   return CGAN3D_EINVAL;
 }

@@ -590,9 +590,7 @@ __global__ __launch_bounds__(256) void pack_halo_kernel(const float* __restrict_
   }
 }
 
-static int g_halo_min_blocks = 512;  // cgan3d_set_tuning key 2
-
-void halo_set_min_blocks(int v) { g_halo_min_blocks = v; }
+constexpr int g_halo_min_blocks = 512;
 
 static bool halo_setup(const cgan3d_conv_geom* g, HaloArgs* a) {
   if (g->prec != CGAN3D_PREC_BF16 || g->reflect) return false;
@@ -629,16 +627,9 @@ static bool halo_setup(const cgan3d_conv_geom* g, HaloArgs* a) {
   return true;
 }
 
-static int g_k3_tile = 1;  // cgan3d_set_tuning key 3: 0 keeps the ResNet convs on conv_halo_kernel
-static int g_k3_split = 0;  // cgan3d_set_tuning key 12: output-channel blocks per tile (0 auto, 1, 2, 4)
-
-void k3_split_set(int v) { g_k3_split = (v == 1 || v == 2 || v == 4) ? v : 0; }
-
-void k3_tile_set(int v) { g_k3_tile = v; }
-
 // k3 s1 p1 64 -> 64, forward or input-grad (the input-grad of a stride-1 conv is a stride-1 conv)
 static bool k3_tile_ok(const cgan3d_conv_geom* g) {
-  return g_k3_tile && g->cin == 64 && g->cout == 64 && g->k == 3 && g->stride == 1 && g->pad == 1 && !g->reflect;
+  return g->cin == 64 && g->cout == 64 && g->k == 3 && g->stride == 1 && g->pad == 1 && !g->reflect;
 }
 
 bool halo_format_ok(const cgan3d_conv_geom* g) {
@@ -672,8 +663,8 @@ int halo_launch(const cgan3d_conv_geom* g, const float* x, const float* w, float
     return k3m_launch(g, reinterpret_cast<const __bf16*>(w), y, e, st);
   if (k3_tile_ok(g)) {  // ResNet-block shape: whole-tile K-split kernel
     const long long tiles = (long long)a.n * a.td * a.th * a.tw;
-    // small grids: the 64 output channels split over 2 (or, tuning key 12, 4) blocks per tile
-    const int split = g_k3_split ? g_k3_split : (tiles < g_halo_min_blocks ? 2 : 1);
+    // small grids: the 64 output channels split over 2 blocks per tile
+    const int split = tiles < g_halo_min_blocks ? 2 : 1;
     const dim3 grid1((unsigned)tiles, split);
     const __bf16* wp = reinterpret_cast<const __bf16*>(w);
 #define CG_K3(N) (g->transposed ? ::cg::launch((conv_k3_kernel<true, N>), grid1, dim3(256), 0, st, a, x, wp, y, e) \

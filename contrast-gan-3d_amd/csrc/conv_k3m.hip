@@ -46,8 +46,6 @@ struct K3mArgs {
   int n, d, h, w;      // volume (input = output: k3 s1 p1)
   int tx, ty, tz;      // tiles per dim
   int tiles, per_xcd;  // tiles; tiles per XCD share of the grid
-  int probe;           // timing probe (cgan3d_set_tuning key 17, tools/bench_ops.py; WRONG results when set):
-                       // bit 0 no halo DMA, 1 no weight DMA, 2 no MFMA loop, 3 no epilogue
 };
 
 __device__ __forceinline__ int km_fa(int hx, int hy) { return ((hx >> 1) & 1) | ((hy & 3) << 1); }
@@ -154,7 +152,7 @@ __global__ __launch_bounds__(256, 1) void conv_k3m_kernel(K3mArgs a, const __bf1
     // with carries instead of divided out per piece; 32-bit element offsets (k3m_ok)
     const int row0 = 8 * wave + (lane >> 3);
     int hx = row0 % KM_HX, hy = (row0 / KM_HX) % KM_HY, hz = row0 / (KM_HX * KM_HY);
-    for (int i = wave; i < ((a.probe & 1) ? 0 : KM_HROWS / 8); i += 4) {
+    for (int i = wave; i < KM_HROWS / 8; i += 4) {
       const int ix = ox + hx, iy = oy + hy, iz = oz + hz;
       const bool ok = (unsigned)ix < (unsigned)a.w && (unsigned)iy < (unsigned)a.h && (unsigned)iz < (unsigned)a.d;
       const int g = p ^ km_fa(hx, hy);
@@ -173,11 +171,9 @@ __global__ __launch_bounds__(256, 1) void conv_k3m_kernel(K3mArgs a, const __bf1
     const int cout = co0 + c;
     // packed format 2 keeps logical granule q of (tap, channel) at position q ^ (channel & 7)
     const __bf16* src = wpk + (long long)cout * 64 + 8 * ((p ^ km_fw(c)) ^ (cout & 7));
-    if (!(a.probe & 2)) {
 #pragma unroll
-      for (int tp = 0; tp < 27; ++tp)
-        km_dma16(src + (long long)tp * 64 * 64, __builtin_amdgcn_readfirstlane(lds0 + KM_HALO + tp * KM_TAPB + wave * 1024));
-    }
+    for (int tp = 0; tp < 27; ++tp)
+      km_dma16(src + (long long)tp * 64 * 64, __builtin_amdgcn_readfirstlane(lds0 + KM_HALO + tp * KM_TAPB + wave * 1024));
   }
 
   // ---- 27 taps x 4 K-steps of 16 channels = 108 MFMAs, in 4 groups of taps (0-2, 3-8, 9-17, 18-26)
@@ -202,7 +198,7 @@ __global__ __launch_bounds__(256, 1) void conv_k3m_kernel(K3mArgs a, const __bf1
   constexpr int KM_PD = 5;  // steps in flight (2 reads each: lgkmcnt <= 15)
   bf16x8_m ra[KM_PD], rb[KM_PD];
 #pragma unroll
-  for (int grp = 0; grp < ((a.probe & 4) ? 0 : 4); ++grp) {
+  for (int grp = 0; grp < 4; ++grp) {
     const int t0 = grp == 0 ? 0 : (grp == 1 ? 3 : (grp == 2 ? 9 : 18));
     const int t1 = grp == 0 ? 3 : (grp == 1 ? 9 : (grp == 2 ? 18 : 27));
     // this wave's DMAs up to the group's last tap have landed (27 - t1 younger ones in flight) ...
@@ -233,10 +229,6 @@ __global__ __launch_bounds__(256, 1) void conv_k3m_kernel(K3mArgs a, const __bf1
     }
   }
 
-  if (a.probe & 8) {
-    KM_WAIT_VM(0);
-    return;
-  }
   // ---- epilogue: lane holds rows R = (i & 3) + 8 (i >> 2) + 4 h of channel co0 + r
   const int C = 64;
   const float bias = ep.bias ? ep.bias[c] : 0.f;
@@ -318,10 +310,8 @@ __global__ __launch_bounds__(256, 1) void conv_k3m_kernel(K3mArgs a, const __bf1
 }
 
 static int g_k3m = 1;  // cgan3d_set_tuning key 15: 0 keeps the ResNet convs on conv_k3_kernel (A/B)
-static int g_k3m_probe = 0;  // key 17: K3mArgs.probe (timing experiments only)
 
 void k3m_set(int v) { g_k3m = v; }
-void k3m_probe_set(int v) { g_k3m_probe = v; }
 
 // k3 s1 p1 64 -> 64 (forward, or the input-grad: a stride-1 conv with flipped taps) with a bf16 input
 // shadow, format-2 packed weights and an epilogue this kernel has (no slabs, masks or out2)
@@ -344,7 +334,6 @@ int k3m_launch(const cgan3d_conv_geom* g, const __bf16* wp, float* y, const Epi&
   a.tx = (a.w + KM_TX - 1) / KM_TX; a.ty = (a.h + KM_TY - 1) / KM_TY; a.tz = (a.d + KM_TZ - 1) / KM_TZ;
   a.tiles = a.n * a.tx * a.ty * a.tz;
   a.per_xcd = (a.tiles + 7) / 8;
-  a.probe = g_k3m_probe;
   const dim3 grid((unsigned)(a.per_xcd * 16));
   const int ob = (e.out16 ? 1 : 0) | (e.res16 ? 2 : 0);
 #define CG_K3M(TR, OB) ::cg::launch(conv_k3m_kernel<TR, OB>, grid, dim3(256), 0, st, a, e.x16, wp, y, e)

@@ -582,13 +582,9 @@ __global__ __launch_bounds__(256, MODE == 2 && !X16 ? 1 : 2) void conv_s2t_kerne
 }
 
 // ------------------------------------------------------------------------------------------------
-static int g_s2 = 1;  // cgan3d_set_tuning key 4: 0 keeps these shapes on the implicit-GEMM kernel
-
-void s2_set(int v) { g_s2 = v; }
-
 // 1: S2F, 2: S2T, 0: neither
 int s2_kind(const cgan3d_conv_geom* g) {
-  if (!g_s2 || g->prec != CGAN3D_PREC_BF16 || g->reflect || g->k != 3 || g->stride != 2 || g->pad != 1) return 0;
+  if (g->prec != CGAN3D_PREC_BF16 || g->reflect || g->k != 3 || g->stride != 2 || g->pad != 1) return 0;
   if (!g->transposed && g->cin == 16 && g->cout == 32 && g->do_ == (g->di - 1) / 2 + 1 &&
       g->ho == (g->hi - 1) / 2 + 1 && g->wo == (g->wi - 1) / 2 + 1)
     return 1;

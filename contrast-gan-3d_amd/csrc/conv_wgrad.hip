@@ -279,9 +279,7 @@ int wgrad_c1_launch(const cgan3d_conv_geom* g, const float* gathered, const floa
   return CGAN3D_OK;
 }
 
-static int g_wgrad_blocks = 1024;  // target grid size (cgan3d_set_tuning key 1)
-
-void wgrad_bf16_set_blocks(int v) { g_wgrad_blocks = v > 0 ? v : 1024; }
+constexpr int g_wgrad_blocks = 1024;  // target grid size
 
 bool wgrad_bf16_ok(const cgan3d_conv_geom* g) {
   return g->prec == CGAN3D_PREC_BF16 && !g->transposed && g->cin % 4 == 0 && g->cout % 4 == 0 && g->cout <= 64 &&
@@ -377,8 +375,6 @@ struct Wk3Args {
   int n, d, h, w;
   int units;      // n * d * (h/4) * (w/8)
   int upb;        // units per block (even)
-  int probe;      // wgrad_k3m_kernel phase probe (cgan3d_set_tuning key 19; timing experiments only):
-                  // 1 no DMAs, 2 no LDS reads / MFMAs, 4 no partial stores, 8 return at once
 };
 
 template <bool B16>
@@ -565,13 +561,11 @@ __global__ __launch_bounds__(256, 1) void wgrad_k3m_kernel(Wk3Args a, const __bf
   const int yb_n = a.h >> 2, xb_n = a.w >> 3;
   const long long plane = (long long)a.h * a.w;
   const unsigned lds0 = (unsigned)(uintptr_t)(__attribute__((address_space(3))) void*)smem;
-  if (a.probe & 8) return;
 
   // ---- DMA of stage s into slot s % NSLOT: wave w issues instructions j = w + 4i (i < DPW); an
   // instruction covers 8 rows, lane -> row 8j + lane / 8, 16-byte position lane % 8 (holding chunk
   // position ^ swz(row))
   auto issue = [&](int s) {
-    if (a.probe & 1) return;
     // the stage's 4 units (wave-uniform: scalar arithmetic): first voxel of the X window / dZ rows
     long long xo[UPS], zo[UPS];
     int zz[UPS], yy[UPS], xx[UPS];
@@ -634,7 +628,6 @@ __global__ __launch_bounds__(256, 1) void wgrad_k3m_kernel(Wk3Args a, const __bf
     asm volatile("" ::: "memory");
     if (s + NSLOT - 1 < nst) issue(s + NSLOT - 1);
     const unsigned char* base = smem + (s % NSLOT) * SBYTES;
-    if (a.probe & 2) continue;
     // 24 steps k = (unit u, K-step ks, tap tw) = (k / 6, (k / 3) % 2, k % 3); the A fragment of step
     // k + PD (and the B fragment it starts) in flight while MFMA k runs (source order pinned)
     constexpr int PD = 4, NB = 4;
@@ -668,7 +661,6 @@ __global__ __launch_bounds__(256, 1) void wgrad_k3m_kernel(Wk3Args a, const __bf
   }
   // partials ws[p][tap][b][a]: lane holds a = 32 ah + (i & 3) + 8 (i >> 2) + 4 (lane >> 5), b = 32 bh + (lane & 31)
   const int b = 32 * bh + (lane & 31), a0 = 32 * ah + 4 * (lane >> 5);
-  if (a.probe & 4) return;
 #pragma unroll
   for (int tw = 0; tw < 3; ++tw) {
     float* o = ws + (((long long)p * 27 + tdh * 3 + tw) * 64 + b) * 64 + a0;
@@ -841,9 +833,7 @@ __global__ __launch_bounds__(512) void wgrad_s2_kernel(Ws2Args a, const float* _
 static int g_wk3_P = 28;  // cgan3d_set_tuning key 9: voxel chunks (blocks per tap plane); 0 = off
 static int g_wk3m = 1;    // cgan3d_set_tuning key 16: 0 keeps the bf16 ResNet weight grads on wgrad_k3_kernel (A/B)
 
-static int g_wk3m_probe = 0;  // key 19: Wk3Args.probe
 void wgrad_k3m_set(int v) { g_wk3m = v; }
-void wgrad_k3m_probe_set(int v) { g_wk3m_probe = v; }
 
 void wgrad_k3_set_chunks(int v) { g_wk3_P = v; }
 
@@ -861,7 +851,6 @@ static void wgrad_k3_geometry(const cgan3d_conv_geom* g, Wk3Args* a, int* P) {
   upb = (upb + wk3::UPS - 1) / wk3::UPS * wk3::UPS;
   *P = (a->units + upb - 1) / upb;
   a->upb = upb;
-  a->probe = g_wk3m_probe;
 }
 
 long long wgrad_k3_ws_floats(const cgan3d_conv_geom* g) {

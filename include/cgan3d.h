@@ -162,11 +162,12 @@ int64_t cgan3d_conv3d_sumsq_blocks(const cgan3d_conv_geom* g);
 
 const char* cgan3d_version(void);
 const char* cgan3d_get_last_error(void);
-/* Launch-shape tuning (process-wide; set before building plans: BatchNorm statistics buffers are
- * sized from the tile shape).  key 0: implicit-GEMM grids with fewer 64-voxel tiles than `value`
- * use 32x32 tiles (default 1024); key 1: target grid size of the bf16 weight-gradient kernel (default
- * 1024 blocks); key 2: the halo-tiled kernel halves its output-channel block (64 -> 32) while its grid
- * has fewer blocks than `value` (default 512). */
+/* Launch-shape / kernel choice (process-wide; set before building plans).  Six keys, every value a
+ * correct configuration (anything else: CGAN3D_EINVAL): 9 voxel chunks of the ResNet weight grad
+ * (default 28, 0 = generic kernel); 10 blocks of the stride-2 weight grad (default 128, 0 = generic);
+ * 13 output planes per streamed last-conv block (0 auto, 8, 16, -1 = Toeplitz kernel); 15 ResNet convs
+ * on conv_k3m (1, default) or conv_k3 (0); 16 ResNet weight grads on wgrad_k3m (1, default) or
+ * wgrad_k3 (0); 20 most blocks of a k7 weight grad (default 512). */
 int cgan3d_set_tuning(int32_t key, int32_t value);
 
 /* --- convolutions (model/blocks.py:29-38 Conv3d / ConvTranspose3d; generator.py:78-84 last
@@ -368,6 +369,10 @@ int cgan3d_reflect_fold_ex(const float* padded, float* out, int32_t n, int32_t d
                            int32_t w, int32_t c, int32_t pad, const cgan3d_epilogue* ep, void* stream);
 int cgan3d_gp_interpolate(const float* real, const float* fake, const float* eps, float* out,
                           int32_t b, int64_t per_sample, void* stream);
+/* The same with the reference's resampling when |real| != |fake| (model/utils.py:21-25): sample s
+ * interpolates real row idx[s] and fake row idx[b + s] (idx: device int32 [2 b], drawn by the host). */
+int cgan3d_gp_interpolate_idx(const float* real, const float* fake, const int32_t* idx, const float* eps,
+                              float* out, int32_t b, int64_t per_sample, void* stream);
 
 int cgan3d_tanh_backward(const float* y, const float* dy, float* dz, int64_t n, void* stream);
 

@@ -315,8 +315,12 @@ def wasserstein(fake: Tensor, real: Optional[Tensor] = None) -> Tensor:
     return r - real.mean() if real is not None else r
 
 
-def gradient_penalty(p, real, fake, eps, cfg: CriticConfig, lambda_=10.0):
-    """wgan_gradient_penalty (model/utils.py:12-41) with ``eps`` [B,1,1,1,1] injected."""
+def gradient_penalty(p, real, fake, eps, cfg: CriticConfig, lambda_=10.0, gp_idx=None):
+    """wgan_gradient_penalty (model/utils.py:12-41) with ``eps`` [B,1,1,1,1] injected; ``gp_idx`` =
+    (real rows, fake rows) of the resampling when |real| != |fake| (model/utils.py:21-25), injected."""
+    if gp_idx is not None:
+        real = real[torch.as_tensor(gp_idx[0], dtype=torch.long)]
+        fake = fake[torch.as_tensor(gp_idx[1], dtype=torch.long)]
     interp = eps * real + (1 - eps) * fake
     if not interp.requires_grad:
         interp.requires_grad_(True)
@@ -373,7 +377,7 @@ def trainable(p: Dict[str, Tensor]) -> List[str]:
 
 def train_step(gp_: Dict[str, Tensor], dp: Dict[str, Tensor], g_opt: AdamState, d_opt: AdamState,
                opt: Tensor, subopt: Tensor, mask: Tensor, eps: Optional[Tensor], cfg: StepConfig,
-               record: Optional[dict] = None, after_critic=None) -> Dict[str, float]:
+               record: Optional[dict] = None, after_critic=None, gp_idx=None) -> Dict[str, float]:
     """Trainer.train_step (Trainer.py:163-203) with both updates on this iteration.
 
     ``gp_``/``dp``: generator / critic state dicts (modified in place: params, BN buffers).
@@ -398,7 +402,7 @@ def train_step(gp_: Dict[str, Tensor], dp: Dict[str, Tensor], g_opt: AdamState, 
     if cfg.weight_clip is None:
         # the interpolation's gradient w.r.t. the generator is identically zero;
         # the critic-parameter gradients are what the reference computes
-        loss_d = loss_d + gradient_penalty(dp, opt, opt_hat.detach(), eps, cfg.critic, cfg.gp_weight)
+        loss_d = loss_d + gradient_penalty(dp, opt, opt_hat.detach(), eps, cfg.critic, cfg.gp_weight, gp_idx)
     d_grads = torch.autograd.grad(loss_d, [dp[k] for k in dkeys], allow_unused=True)
     d_grads = dict(zip(dkeys, d_grads))
     if record is not None:

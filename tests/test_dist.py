@@ -75,19 +75,6 @@ def _worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
-class _GlooNative:
-    """Stand-in for ops.NativeComm on CPU: the same allreduce_mean contract (mean over the ranks, in
-    place), over gloo — so the engine takes its native-RCCL code path (collectives recorded into the
-    plan on the main and communication streams) in a dry run."""
-
-    def __init__(self, world):
-        self.world = world
-
-    def allreduce_mean(self, t):
-        dist.all_reduce(t, op=dist.ReduceOp.SUM)
-        t.mul_(1.0 / self.world)
-
-
 def check_collective_order(log):
     """Every collective is ordered after every earlier one by stream dependencies (a communicator's
     collectives must run in issue order on every rank), and the main stream has joined
@@ -122,7 +109,10 @@ def _worker_sequence(rank, world, port, q):
         d = PatchGANDiscriminator(**D_ARGS, norm_layer=nn.Identity)
         ops.DRY_RUN = True
         eng = StepEngine(g, d, g.config, d.config, 1, 1, (32, 32, 32), device=torch.device("cpu"))
-        eng.native = _GlooNative(world)  # the native-RCCL code path (on the GPU: ops.NativeComm)
+        # the native-RCCL code path: ops.NativeComm over this gloo group (on the GPU the same object drives
+        # RCCL from the plan; here torch.distributed does the exchange)
+        eng.native = ops.NativeComm(None, torch.device("cpu"))
+        assert eng.native.handle is None and eng.native.world == world
         logs = []
         for it in range(2):
             eng.comm_log = []

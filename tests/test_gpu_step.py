@@ -568,3 +568,77 @@ def test_bf16_storage_matches_fp32_storage(monkeypatch):
     bad = {k: v for k, v in rep.items() if v["l2"] > NOISE_L2_BAR or v["max"] > NOISE_MAX_BAR}
     assert not bad, f"bf16 vs fp32 storage differ: {bad}"
     assert float(np.median([v["l2"] for v in rep.values()])) <= NOISE_MEDIAN_BAR, rep
+
+
+@pytest.mark.parametrize("b_opt,b_sub", [(3, 2), (2, 4)])
+def test_step_gp_resampled_batches_match_oracle(b_opt, b_sub):
+    """|OPT| != |LOW|+|HIGH| with the gradient penalty: the reference resamples min(|real|, |fake|)
+    rows of each batch with replacement (model/utils.py:21-25).  Same draw injected into both (the
+    engine's set_gp_indices / Trainer's draw_gp_indices; the oracle's gp_idx), one step in fp32 and
+    in a recorded plan with new rows on its second run, every loss and gradient against float64 at
+    north_star's 1e-3."""
+    from oracle import reference_torch as R
+    from cgan3d_amd.data.synthetic import synth_patches
+    from cgan3d_amd.engine import StepEngine
+    g_args = dict(n_resnet_blocks=1, n_updownsample_blocks=2, init_channels_out=8)
+    S = 32
+    g, d = _models(g_args)
+    dbl = lambda v: v.detach().cpu().clone().double() if v.is_floating_point() else v.detach().cpu().clone()  # noqa
+    gpar = {k: dbl(v) for k, v in g.state_dict().items()}
+    dpar = {k: dbl(v) for k, v in d.state_dict().items()}
+    eng = StepEngine(g, d, g.config, d.config, b_opt, b_sub, (S, S, S), g_hyper=(1e-4, 0.0, 0.9, 1e-8),
+                     d_hyper=(1e-4, 0.0, 0.9, 1e-8))
+    m = min(b_opt, b_sub)
+    assert eng.gp_idx is not None and eng.b_gp == m
+    cfg = R.StepConfig(gen=R.GenConfig(**g_args), critic=R.CriticConfig())
+    gopt, dopt = R.AdamState(1e-4, 0.0, 0.9), R.AdamState(1e-4, 0.0, 0.9)
+    rng = np.random.default_rng(5)
+    plan = None
+    for it in range(2):
+        opt, _ = synth_patches(b_opt, S, 40 + it)
+        sub, seg = synth_patches(b_sub, S, 50 + it)
+        eps = np.random.Generator(np.random.PCG64(60 + it)).random((m, 1, 1, 1, 1)).astype(np.float32)
+        ri, fi = eng.draw_gp_indices(rng)
+        eng.load_inputs(torch.from_numpy(opt).cuda(), torch.from_numpy(sub).cuda(), torch.from_numpy(seg).cuda(),
+                        torch.from_numpy(eps).cuda())
+        if it == 0:
+            eng.generator_forward()
+            eng.critic_update()
+            d_after = {k: v.detach().cpu().clone() for k, v in d.state_dict().items()}
+            eng.generator_update()
+        else:  # the recorded plan reads the rows from the device buffer at run time
+            snap = {k: v.detach().clone() for k, v in d.state_dict().items()}
+            plan = eng.record(do_critic=True, do_generator=False)
+            plan.run()
+            torch.cuda.synchronize()
+            d_after = {k: v.detach().cpu().clone() for k, v in d.state_dict().items()}
+        losses = eng.losses.cpu().numpy()
+
+        def use_device_critic(dp):
+            for k in dp:
+                dp[k].data.copy_(d_after[k])
+        rec = {}
+        ref = R.train_step(gpar, dpar, gopt, dopt, torch.from_numpy(opt).double(), torch.from_numpy(sub).double(),
+                           torch.from_numpy(seg), torch.from_numpy(eps).double(), cfg, record=rec,
+                           after_critic=use_device_critic, gp_idx=(ri, fi))
+        assert abs(float(losses[0]) - ref["D"]) <= 1e-3 * max(abs(ref["D"]), 1e-3), (it, losses[0], ref["D"])
+        for k, gv in eng.d_arena.gviews.items():
+            e = rec["D"][k].numpy()
+            atol = 1e-7 if k == "model.last.bias" else 0.0
+            err = float(np.abs(gv.cpu().numpy() - e).max())
+            assert err <= 1e-3 * float(np.abs(e).max()) + atol, (it, k, err)
+        if it == 0:
+            for k, slot in (("G", 3), ("sim", 4), ("HU", 5)):
+                assert abs(float(losses[slot]) - ref[k]) <= 1e-3 * max(abs(ref[k]), 1e-3), (k, losses[slot], ref[k])
+            for k, gv in eng.g_arena.gviews.items():
+                e = rec["G"][k].numpy()
+                err = float(np.linalg.norm(gv.cpu().numpy() - e)) / max(float(np.linalg.norm(e)), 1e-30)
+                assert err <= 1e-3, (k, err)
+            for k, v in g.state_dict().items():
+                gpar[k].copy_(v.detach().cpu())
+            for k, v in d.state_dict().items():
+                dpar[k].copy_(v.detach().cpu())
+            for st, opt_ in ((gopt, eng.g_optim), (dopt, eng.d_optim)):
+                for k, p in zip(opt_.arena.names, opt_.arena.params):
+                    st.exp_avg[k] = opt_.state[p]["exp_avg"].detach().cpu().double()
+                    st.exp_avg_sq[k] = opt_.state[p]["exp_avg_sq"].detach().cpu().double()

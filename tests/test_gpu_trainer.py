@@ -326,3 +326,29 @@ def test_validate_at_reference_val_patch_matches_oracle(tmp_path):
     scale = {"D": max(abs(real), *map(abs, fakes)), "G": max(map(abs, fakes)), "sim": max(map(abs, sims))}
     for k in want:
         assert abs(got[k] - want[k]) <= 1e-3 * scale[k], (k, got[k], want[k])
+
+
+def test_train_critic_generator_take_their_arguments(tmp_path):
+    """Drop-in signature fidelity (Trainer.py:108-161): train_critic computes on the tensors it is
+    given (copied into the engine's slots when they are other tensors), train_generator refuses a
+    batch that is not the one its generator forward ran on instead of silently ignoring it."""
+    rng = np.random.default_rng(3)
+    tr = _trainer(None)
+    tr.train_step(_patches(rng), 0)  # builds the engine (eager first iteration)
+    eng = tr.engine
+    pa = _patches(rng)
+    real = pa[0]["data"].cuda()
+    fake = torch.rand_like(eng.opt_hat) * 2 - 1
+    eng.generator_forward()
+    log = tr.train_critic(real, fake, True)
+    torch.cuda.synchronize()
+    assert torch.equal(eng.xc[:eng.b_opt].reshape(-1), real.reshape(-1))
+    assert torch.equal(eng.opt_hat.reshape(-1), fake.reshape(-1))
+    assert np.isfinite(float(log["D"]))
+    with pytest.raises(ValueError):
+        tr.train_generator(torch.zeros_like(eng.subopt), None, None)
+    with pytest.raises(ValueError):
+        tr.train_critic(real[:1], None, True)
+    # the resident batch (same storage or equal values) is accepted
+    log = tr.train_generator(eng.subopt.clone(), eng.opt_hat, None)
+    assert set(log) == {"G", "G-full", "sim", "HU"}

@@ -168,3 +168,29 @@ def test_patch_bounds_edges():
             np.testing.assert_array_equal(patch_bounds(patch, (40, 36), np.array(coords)), want)
     with pytest.raises(ValueError):
         patch_bounds((50, 16), (40, 36), np.array([20, 10]))
+
+
+def test_meta_pkl_restricted_unpickler(tmp_path):
+    """The reference's ``_meta.pkl`` (data/utils.py:48-54: dict of numpy arrays) loads; a pickle that
+    names any other global (code) is refused."""
+    import os
+    import pickle
+
+    import pytest
+    from cgan3d_amd.data.loader import load_meta
+    meta = {"offset": np.array([1.5, -2.0, 3.0]), "spacing": np.array([0.4, 0.4, 0.5], np.float32),
+            "centerlines_world": np.arange(12.0).reshape(3, 4), "name": "scan_0", "n": 3, "f": np.float64(2.5)}
+    with open(tmp_path / "a_meta.pkl", "wb") as f:
+        pickle.dump(meta, f)
+    got = load_meta(str(tmp_path / "a"))
+    assert set(got) == set(meta) and got["name"] == "scan_0" and got["n"] == 3 and got["f"] == 2.5
+    for k in ("offset", "spacing", "centerlines_world"):
+        assert got[k].dtype == meta[k].dtype and np.array_equal(got[k], meta[k])
+
+    class Evil:
+        def __reduce__(self):
+            return (os.system, ("true",))
+    with open(tmp_path / "b_meta.pkl", "wb") as f:
+        pickle.dump({"offset": Evil()}, f)
+    with pytest.raises(pickle.UnpicklingError):
+        load_meta(str(tmp_path / "b"))
