@@ -82,6 +82,21 @@ def pmc_traffic(path, size, batch, precision):
     return json.loads(f.read_text()).get("hbm_bytes_per_launch")
 
 
+def bn_hbm(path="profiles/r05_b128_f32_pmc.json"):
+    """The dominant BatchNorm kernel of the 128^3 B=1 f32 step (BASELINE.json configs[2], "HBM-bound,
+    rocprof GB/s vs roofline"): FETCH_SIZE / WRITE_SIZE bytes per launch over its kernel-trace duration,
+    from the committed rocprofv3 summary (tools/pmc_r5_summary.py hbm)."""
+    f = REPO / path
+    if not f.is_file():
+        return None
+    ks = [k for k in json.loads(f.read_text())["kernels"] if k["kernel"].startswith("cg::bn_") and k["trace_us"]]
+    if not ks:
+        return None
+    k = max(ks, key=lambda r: r["trace_us"] * max(r["launches_in_trace"], 1))
+    return {"kernel": k["kernel"], "bytes_per_launch": k["bytes_per_launch"], "avg_launch_us": k["trace_us"],
+            "hbm_gbs": k["gbs"], "hbm_peak_gbs": HBM_PEAK_GBS, "hbm_frac": k["hbm_frac"], "source": path}
+
+
 def cpu_baseline(size, seconds, g_args):
     """Oracle (torch fp32 CPU restatement of the reference step) on the host cores."""
     from cgan3d_amd.data.synthetic import synth_patches
@@ -308,6 +323,8 @@ def main():
     ap.add_argument("--no-sub", action="store_true",
                     help="skip the extra lines (h2d: batches from pinned host memory; f32: the exact-fp32 path; "
                          "b128_f32: BASELINE configs[2], 128^3 B=1 fp32)")
+    ap.add_argument("--sub", default="h2d,f32,b128_f32,b128_bf16_b2",
+                    help="comma list of the extra lines to run (default all; --no-sub: none)")
     ap.add_argument("--precision", choices=["f32", "bf16"], default="bf16",
                     help="MFMA operand precision of the convolutions (accumulation is f32)")
     ap.add_argument("--roofline", choices=sorted(ROOFLINES), default="halo_res")
@@ -522,18 +539,27 @@ def main():
     }
     if ref_sched is not None:
         out["reference_schedule"] = ref_sched
-    if mode == "plan" and world == 1 and not args.no_sub:
+    subs = set() if args.no_sub else set(filter(None, args.sub.split(",")))
+    if mode == "plan" and world == 1 and subs:
         # beside the resident number: the batch coming over PCIe from pinned host memory each step
-        out["h2d"] = h2d_bench(eng, S, B, dev, args.steps)
+        if "h2d" in subs:
+            out["h2d"] = h2d_bench(eng, S, B, dev, args.steps)
         del eng
         torch.cuda.empty_cache()
         # the other single-GPU BASELINE configs in the same run: the exact-fp32 parity path at this
         # workload, and configs[2] (128^3 B=1 fp32)
-        out["f32"] = sub_config(S, B, "f32", dev, g_args) if args.precision != "f32" else None
-        out["b128_f32"] = sub_config(128, 1, "f32", dev, g_args, steps=10)
+        if "f32" in subs:
+            out["f32"] = sub_config(S, B, "f32", dev, g_args) if args.precision != "f32" else None
+        if "b128_f32" in subs:
+            out["b128_f32"] = sub_config(128, 1, "f32", dev, g_args, steps=10)
+            bn = bn_hbm()
+            if bn is not None:
+                out["b128_f32"]["hbm_gbs"] = bn["hbm_gbs"]
+                out["b128_f32"]["hbm_bn_kernel"] = bn
         # configs[4]'s per-GPU slice: 128^3 bf16 with the gradient penalty, 2 OPT + 2 subopt patches
         # (global batch 16 over 8 GPUs)
-        out["b128_bf16_b2"] = sub_config(128, 2, "bf16", dev, g_args, steps=10)
+        if "b128_bf16_b2" in subs:
+            out["b128_bf16_b2"] = sub_config(128, 2, "bf16", dev, g_args, steps=10)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(S, args.cpu_seconds, g_args)
     if rank == 0:

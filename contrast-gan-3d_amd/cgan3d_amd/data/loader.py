@@ -230,6 +230,7 @@ class PatchLoader:
         if self.transforms:  # ping-pong with staging buffers so that the last transform writes the returned ones
             self._pre_data = [torch.empty_like(t) for t in self._data]
             self._pre_seg = [torch.empty_like(t) for t in self._seg]
+        ops.pooled_stream(self.device, "g_side")  # the engines' streams first: their queue mapping stays fixed
         self._stream = torch.cuda.Stream(device=self.device)
         self._threads, self._pool = num_threads, None
         self._lock = threading.Lock()

@@ -375,7 +375,7 @@ class GeneratorPlan:
         self._csum = {}  # bias-sum launch sets (ops.ChannelSumSet) per gradient dict
         # (CGAN3D_DEBUG=serial serialises them, so a kernel trace shows unshared durations)
         on_gpu = torch.device(device).type == "cuda" and not debug("serial")
-        self.side = torch.cuda.Stream(device=device) if on_gpu else None
+        self.side = ops.pooled_stream(device, "g_side") if on_gpu else None
         self.pack()
 
     def _on_side(self, fn):
@@ -690,7 +690,7 @@ class CriticPlan:
         # way, beside the small-grid forward-mode chain
         self.side0 = None
         if torch.device(device).type == "cuda" and not debug("serial"):
-            self.side0 = torch.cuda.Stream(device=device)
+            self.side0 = ops.pooled_stream(device, "d_side")
         if self.bn:  # conv outputs, pre-activation grads, statistics and per-pass scale/shift
             self.z = [torch.empty_like(self.a[i]) if b else None for i, b in enumerate(self.is_bn)]
             self.dy = [torch.empty_like(self.a[i]) if b else None for i, b in enumerate(self.is_bn)]
@@ -1164,7 +1164,7 @@ class StepEngine:
         self.comm_log = None  # a list: the collective sequence is logged there (_log_comm)
         self.g_buckets = self._make_g_buckets(G_BUCKET_BYTES) if (self.dp and G_BUCKET_BYTES > 0) else []
         on_gpu = torch.device(device).type == "cuda"
-        self.comm = torch.cuda.Stream(device=device) if (self.dp and on_gpu) else None
+        self.comm = ops.pooled_stream(device, "comm") if (self.dp and on_gpu) else None
         if self.comm is not None and int(os.environ.get("GPU_MAX_HW_QUEUES", "4")) < 8:
             import warnings
             warnings.warn("StepEngine: data parallelism with fewer than 8 hardware queues (GPU_MAX_HW_QUEUES): the "

@@ -13,7 +13,7 @@ from __future__ import annotations
 
 import ctypes
 import os
-from typing import Optional, Sequence
+from typing import Dict, Optional, Sequence
 
 import torch
 
@@ -311,6 +311,28 @@ def stream_wait(waiter, signaler):
     if DRY_RUN or waiter is None or signaler is None:
         return
     check(L.lib().cgan3d_stream_wait(waiter.cuda_stream, signaler.cuda_stream), "stream_wait")
+
+
+_STREAM_POOL: Dict[int, Dict[str, "torch.cuda.Stream"]] = {}
+POOL_ROLES = ("g_side", "d_side", "comm")
+
+
+def pooled_stream(device, role: str) -> "torch.cuda.Stream":
+    """One stream per (device, role), shared by every engine and plan of the process.
+
+    HIP hands a new stream the next hardware queue round-robin (GPU_MAX_HW_QUEUES), so engines that
+    each created their own side streams ran on different queue mappings — the same exact-f32 step
+    measured 5.2 ms/step as the first engine of a process, 8.5 as the second and 5.1 as the fourth
+    (profiles/r04_f32_sub_probe.txt).  All roles are created together on first use, so every engine
+    gets the mapping of the first; plans run in turn on one host thread, so sharing keeps their order."""
+    if role not in POOL_ROLES:
+        raise ValueError(f"pooled_stream: role {role!r} not in {POOL_ROLES}")
+    dev = torch.device(device)
+    idx = dev.index if dev.index is not None else torch.cuda.current_device()
+    pool = _STREAM_POOL.get(idx)
+    if pool is None:
+        pool = _STREAM_POOL[idx] = {r: torch.cuda.Stream(device=idx) for r in POOL_ROLES}
+    return pool[role]
 
 
 class NativeComm:

@@ -617,23 +617,35 @@ def test_step_gp_resampled_batches_match_oracle(b_opt, b_sub):
         def use_device_critic(dp):
             for k in dp:
                 dp[k].data.copy_(d_after[k])
+        # the reference's own float32 run (the yardstick of conftest.assert_parity: the generator's
+        # BatchNorm backward is ill-conditioned in fp32) on copies of the state, then float64
+        f32 = lambda v: v.float() if v.is_floating_point() else v.clone()  # noqa: E731
+        rec32 = {}
+        R.train_step({k: f32(v) for k, v in gpar.items()}, {k: f32(v) for k, v in dpar.items()},
+                     R.AdamState(1e-4, 0.0, 0.9, exp_avg={k: f32(v) for k, v in gopt.exp_avg.items()},
+                                 exp_avg_sq={k: f32(v) for k, v in gopt.exp_avg_sq.items()}, step=gopt.step),
+                     R.AdamState(1e-4, 0.0, 0.9, exp_avg={k: f32(v) for k, v in dopt.exp_avg.items()},
+                                 exp_avg_sq={k: f32(v) for k, v in dopt.exp_avg_sq.items()}, step=dopt.step),
+                     torch.from_numpy(opt), torch.from_numpy(sub), torch.from_numpy(seg), torch.from_numpy(eps), cfg,
+                     record=rec32, after_critic=use_device_critic, gp_idx=(ri, fi))
         rec = {}
         ref = R.train_step(gpar, dpar, gopt, dopt, torch.from_numpy(opt).double(), torch.from_numpy(sub).double(),
                            torch.from_numpy(seg), torch.from_numpy(eps).double(), cfg, record=rec,
                            after_critic=use_device_critic, gp_idx=(ri, fi))
         assert abs(float(losses[0]) - ref["D"]) <= 1e-3 * max(abs(ref["D"]), 1e-3), (it, losses[0], ref["D"])
         for k, gv in eng.d_arena.gviews.items():
-            e = rec["D"][k].numpy()
-            atol = 1e-7 if k == "model.last.bias" else 0.0
-            err = float(np.abs(gv.cpu().numpy() - e).max())
-            assert err <= 1e-3 * float(np.abs(e).max()) + atol, (it, k, err)
+            atol = 1e-7 if k == "model.last.bias" else 0.0  # exactly 0 in real arithmetic
+            assert_parity(gv.cpu().numpy(), rec32["D"][k].numpy(), rec["D"][k].numpy(), f"it{it} grad D {k}", atol=atol)
         if it == 0:
             for k, slot in (("G", 3), ("sim", 4), ("HU", 5)):
                 assert abs(float(losses[slot]) - ref[k]) <= 1e-3 * max(abs(ref[k]), 1e-3), (k, losses[slot], ref[k])
+            fails = []
             for k, gv in eng.g_arena.gviews.items():
-                e = rec["G"][k].numpy()
-                err = float(np.linalg.norm(gv.cpu().numpy() - e)) / max(float(np.linalg.norm(e)), 1e-30)
-                assert err <= 1e-3, (k, err)
+                try:
+                    assert_parity(gv.cpu().numpy(), rec32["G"][k].numpy(), rec["G"][k].numpy(), f"grad G {k}")
+                except AssertionError as ex:
+                    fails.append(str(ex).split("\n")[0])
+            assert not fails, "\n".join(fails)
             for k, v in g.state_dict().items():
                 gpar[k].copy_(v.detach().cpu())
             for k, v in d.state_dict().items():
