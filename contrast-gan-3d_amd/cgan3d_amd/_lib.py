@@ -17,7 +17,7 @@ import torch  # noqa: F401  (must be imported first: see module docstring)
 LIB_PATH = Path(os.environ.get("CGAN3D_LIB_PATH") or Path(__file__).resolve().parent / "libcgan3d.so")
 
 ACT_NONE, ACT_RELU, ACT_LRELU, ACT_TANH, ACT_NEG_DTANH = 0, 1, 2, 3, 4
-WGRAD_ACCUMULATE, WGRAD_WS_CLEAN, WGRAD_DEFER_UNPACK = 1, 2, 4  # cgan3d_conv3d_wgrad_ex flag word
+WGRAD_ACCUMULATE, WGRAD_WS_CLEAN, WGRAD_DEFER_UNPACK, WGRAD_DEFER_REDUCE = 1, 2, 4, 8  # cgan3d_conv3d_wgrad_ex flags
 # device loss slots written by the loss kernels (include/cgan3d.h)
 L_D, L_WD, L_GP, L_G, L_SIM, L_HU, L_GFULL = range(7)
 
@@ -64,6 +64,12 @@ class BnFuse(C.Structure):
     _fields_ = [("acc_out", C.c_void_p), ("acc_mode", C.c_int32), ("reps", C.c_int32)]
 
 
+class ReduceDesc(C.Structure):
+    """include/cgan3d.h cgan3d_reduce_desc: one deferred ResNet weight-gradient reduce."""
+    _fields_ = [("ws", C.c_void_p), ("dw", C.c_void_p), ("sa", C.c_int64), ("sb", C.c_int64),
+                ("P", C.c_int32), ("cin", C.c_int32), ("cout", C.c_int32), ("accumulate", C.c_int32)]
+
+
 class Epilogue(C.Structure):
     _fields_ = [("bias", C.c_void_p), ("residual", C.c_void_p), ("mask_src", C.c_void_p),
                 ("minuend", C.c_void_p), ("out2", C.c_void_p), ("stats", C.c_void_p),
@@ -71,7 +77,7 @@ class Epilogue(C.Structure):
                 ("bn_part", C.c_void_p), ("bn_mode", C.c_int32), ("bn_slots", C.c_int32), ("bn_z", C.c_void_p),
                 ("bn_ss", C.c_void_p), ("bn_mi", C.c_void_p), ("bn_act", C.c_int32), ("bn_slope", C.c_float),
                 ("x_bf16", C.c_void_p), ("bn_fold", C.c_int32), ("fuse", C.POINTER(BnFuse)),
-                ("out_bf16", C.c_int32)]
+                ("out_bf16", C.c_int32), ("split_ws", C.c_void_p)]
 
 
 _P, _I32, _I64, _F = C.c_void_p, C.c_int32, C.c_int64, C.c_float
@@ -125,6 +131,12 @@ _SIGS = {
     "cgan3d_reflect_fold2d": ([_P, _P, _I32, _I32, _I32, _I32, _I32, _P, _P], _I32),
     "cgan3d_gp_interpolate": ([_P, _P, _P, _P, _I32, _I64, _P], _I32),
     "cgan3d_gp_interpolate_idx": ([_P, _P, _P, _P, _P, _I32, _I64, _P], _I32),
+    "cgan3d_conv3d_split_ws_floats": ([_P], _I64),
+    "cgan3d_conv3d_wgrad_sk_ok": ([_P], _I32),
+    "cgan3d_conv3d_wgrad_partials": ([_P], _I32),
+    "cgan3d_wgrad_reduce_multi": ([_P, _I32, _P], _I32),
+    "cgan3d_conv3d_wgrad_sk_ws_floats": ([_P], _I64),
+    "cgan3d_conv3d_wgrad_sk": ([_P, _P, _P, _P, _P, _I32, _P], _I32),
     "cgan3d_tanh_backward": ([_P, _P, _P, _I64, _P], _I32),
     "cgan3d_unpack_patches": ([_P, _I32, _I64, _F, _F, _P, _P, _P], _I32),
     "cgan3d_augment_ws_floats": ([_I32, _I32, _I32, _I32, _I32], _I64),

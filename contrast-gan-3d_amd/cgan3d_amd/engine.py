@@ -48,7 +48,11 @@ Dims = Tuple[int, int, int]
 #                              (cross-stream event records with the system-scope fence, csrc/plan.hip),
 #                              fp32_store (the 64^3 16-channel z / dy in fp32 instead of bf16),
 #                              event_record (a marker event per cross-stream wait instead of the
-#                              waited-on launch's own completion event, csrc/plan.hip)
+#                              waited-on launch's own completion event, csrc/plan.hip), no_split (the
+#                              critic's 32 -> 64 layer without split-K, conv_sk.hip), own_streams (a new
+#                              side / communication stream per plan instead of ops.pooled_stream),
+#                              no_wgrad_sk (the critic's middle-layer weight grads on the generic kernel),
+#                              no_defer_reduce (one partial-reduce launch per ResNet weight grad)
 #   CGAN3D_FORCE_DP=1          the data-parallel path over a one-rank group (tools / tests)
 #   CGAN3D_COMM=native|torch|own   data-parallel collectives: RCCL from the launch plan on the process
 #                              group's communicator (default), torch.distributed host callables (the
@@ -57,7 +61,7 @@ Dims = Tuple[int, int, int]
 #   CGAN3D_TUNE, CGAN3D_LIB_PATH   launch-shape knobs, another build of the library (_lib.py)
 #   CGAN3D_TRAINER_PLANS=0     the drop-in Trainer issues every step eagerly (no recorded plans)
 DEBUG_FLAGS = ("no_shadow", "keep_fp32", "no_bn_fuse", "no_bn_fold", "serial", "system_fence", "fp32_store",
-               "event_record")
+               "event_record", "no_split", "own_streams", "no_wgrad_sk", "no_defer_reduce")
 
 
 def debug(flag: str) -> bool:
@@ -373,6 +377,8 @@ class GeneratorPlan:
         # each leaves it zeroed, so no memset per layer); they all run on the side stream, in turn
         self.ws_clean = torch.zeros(wsw, device=device)
         self._csum = {}  # bias-sum launch sets (ops.ChannelSumSet) per gradient dict
+        # ResNet weight grads whose partial reduce is deferred to one launch per backward (round 5)
+        self.ws_defer, self._deferred_red = {}, []
         # (CGAN3D_DEBUG=serial serialises them, so a kernel trace shows unshared durations)
         on_gpu = torch.device(device).type == "cuda" and not debug("serial")
         self.side = ops.pooled_stream(device, "g_side") if on_gpu else None
@@ -460,12 +466,20 @@ class GeneratorPlan:
             self.ss[i][c:].copy_(P[f"{nb}.bias"] - P[f"{nb}.running_mean"] * sc)
 
     # -- backward from dz_last = dL/d(pre-tanh) ; writes parameter grads into G (grad views)
-    def _wgrad(self, g, a, b, dw, zeroed: bool, main: bool = False, **kw):
+    def _wgrad(self, g, a, b, dw, zeroed: bool, main: bool = False, defer_layer: Optional[int] = None, **kw):
         """Weight gradient on the side stream's workspaces: into a pre-zeroed gradient arena
         (``zeroed``) every layer accumulates, and the atomic-workspace geometries take the clean one.
-        ``main``: launched on the main stream instead, with the main stream's workspace."""
+        ``main``: launched on the main stream instead, with the main stream's workspace.
+        ``defer_layer``: a partials geometry (the ResNet k3 kernel) leaves its partials in the layer's
+        own workspace; ``_reduce_deferred`` sums every such layer in one launch (round 5)."""
         if main:
             return ops.wgrad(g, a, b, dw, self.ws, accumulate=zeroed, **kw)
+        if defer_layer is not None:
+            wl = self.ws_defer.get(defer_layer)
+            if wl is None:
+                wl = self.ws_defer[defer_layer] = torch.empty(ops.wgrad_ws_floats(g), device=self.ws.device)
+            self._deferred_red.append((g, wl, dw, zeroed))
+            return ops.wgrad(g, a, b, dw, wl, accumulate=zeroed, defer_reduce=True, **kw)
         if zeroed and ops.wgrad_ws_atomic(g):
             return ops.wgrad(g, a, b, dw, self.ws_clean, accumulate=True, ws_clean=True, **kw)
         return ops.wgrad(g, a, b, dw, self.ws_side, accumulate=zeroed, **kw)
@@ -495,10 +509,19 @@ class GeneratorPlan:
                                            zeroed, gathered16=self.y16[-1] if self.y_dead[-1] else None),
                                self._csum[key].run()))
         pending = []  # (layer, weight-grad launcher) not yet handed to the side stream
+        # single GPU: the ResNet weight grads leave their partials in per-layer workspaces and the
+        # lowest ResNet layer's hand-off sums all of them in one launch (8 reduce launches -> 1;
+        # under data parallelism every bucket needs its layers' final gradients: per-layer reduce)
+        k3 = [i for i in range(len(self.layers)) if ops.wgrad_partials(self.geo_wgrad[i]) > 0]
+        defer_red = (grads_enqueued is None and self.side is not None and len(k3) > 1
+                     and not debug("no_defer_reduce"))
+        k3_last = min(k3) if defer_red else None
+        self._deferred_red = []
 
         def flush():
             fns = [f for _, f in pending]
-            self._on_side(lambda: [f() for f in fns])
+            red = k3_last is not None and any(j == k3_last for j, _ in pending)
+            self._on_side(lambda: ([f() for f in fns], self._reduce_deferred() if red else None))
             if grads_enqueued is not None:
                 for j, _ in pending:
                     grads_enqueued(j)
@@ -552,12 +575,13 @@ class GeneratorPlan:
             elif x16 is None or d16 is None:
                 x16 = d16 = None
             main = i < self.wgrad_tail_main and self.side is not None
+            dl = i if (defer_red and i in k3 and not main) else None
             if ly.kind == "convt":  # ConvTranspose3d: the output-grad is the gathered operand
-                fn = (lambda g=self.geo_wgrad[i], a=self.dz[i], b=xin, w=G[wname], a16=d16, b16=x16, m=main:
-                      self._wgrad(g, a, b, w, zeroed, main=m, gathered16=a16, aligned16=b16))
+                fn = (lambda g=self.geo_wgrad[i], a=self.dz[i], b=xin, w=G[wname], a16=d16, b16=x16, m=main, dl=dl:
+                      self._wgrad(g, a, b, w, zeroed, main=m, gathered16=a16, aligned16=b16, defer_layer=dl))
             else:
-                fn = (lambda g=self.geo_wgrad[i], a=xin, b=self.dz[i], w=G[wname], a16=x16, b16=d16, m=main:
-                      self._wgrad(g, a, b, w, zeroed, main=m, gathered16=a16, aligned16=b16))
+                fn = (lambda g=self.geo_wgrad[i], a=xin, b=self.dz[i], w=G[wname], a16=x16, b16=d16, m=main, dl=dl:
+                      self._wgrad(g, a, b, w, zeroed, main=m, gathered16=a16, aligned16=b16, defer_layer=dl))
             if main:
                 if pending:
                     flush()
@@ -589,6 +613,12 @@ class GeneratorPlan:
                 self._on_side(side_after)
         if self.side is not None:  # the weight gradients are complete before anything reads them
             ops.stream_wait(torch.cuda.current_stream(self.device), self.side)
+
+    def _reduce_deferred(self):
+        """Sum the partials of every deferred ResNet weight grad into dW (one launch, side stream)."""
+        items, self._deferred_red = self._deferred_red, []
+        for k in range(0, len(items), 16):
+            ops.reduce_multi(items[k:k + 16])
 
     def _input_grad(self, P, G, i: int):
         """dL/dy of layer i - 1 from dz_i (a ResNet block0 also receives the skip gradient
@@ -733,6 +763,18 @@ class CriticPlan:
             if self.is_bn[i]:
                 gs = self._geo(ops.conv_fwd_geom(nmax, ly.din, ly.dout, ly.cin, ly.cout, ly.k, ly.s, ly.p, planar=self.pl), self.wf[i])
                 self.stats[i] = torch.empty(ops.stats_floats(gs), device=device)
+        # all-zero workspace of the split-K forward launches (conv_sk with few row tiles and a long K:
+        # the 32 -> 64 layer), shared by every forward-style launch of this plan — they run in turn on
+        # one stream and each leaves it zeroed; sized for any batch up to nmax
+        nsw = 0
+        for i, ly in enumerate(ls):
+            if self.wf[i] is None or self.is_bn[i]:
+                continue
+            for nb in range(1, nmax + 1):
+                gs = self._geo(ops.conv_fwd_geom(nb, ly.din, ly.dout, ly.cin, ly.cout, ly.k, ly.s, ly.p, planar=self.pl),
+                               self.wf[i])
+                nsw = max(nsw, ops.split_ws_floats(gs))
+        self.split_ws = torch.zeros(nsw, device=device) if nsw and not debug("no_split") else None
         self.pack()
 
     def pack(self):
@@ -777,7 +819,7 @@ class CriticPlan:
             else:
                 last = i == len(self.layers) - 1
                 ep = ops.epilogue(bias=P[f"{ly.name}.bias"], act=L.ACT_NONE if last else L.ACT_LRELU,
-                                  slope=self.slope)
+                                  slope=self.slope, split_ws=self.split_ws)
                 ops.conv(g, h, w, out, ep)
             h = out
         return self._sl(self.a[-1], off, n)
@@ -836,7 +878,7 @@ class CriticPlan:
             g = self._geo(ops.conv_fwd_geom(n, ly.din, ly.dout, ly.cin, ly.cout, ly.k, ly.s, ly.p, planar=self.pl), self.wf[i])
             out = self._sl(self.a[i], off, n)
             w = self.wf[i] if self.wf[i] is not None else P[f"{ly.name}.weight"]
-            ops.conv(g, h, w, out, ops.epilogue(mask_src=out, slope=self.slope))
+            ops.conv(g, h, w, out, ops.epilogue(mask_src=out, slope=self.slope, split_ws=self.split_ws))
             h = out
 
     def _on_side(self, fn):
@@ -894,6 +936,19 @@ class CriticPlan:
             self._deferred.append((j, g, wl, G[f"{self.layers[j].name}.weight"]))
         ops.wgrad_group(items)
 
+    def _wgrad_sk(self, G, layers, n_all: int):
+        """The weight grads of ``layers`` (a_{j-1}, dz_j over n_all samples) on the staged-window kernel,
+        added into the zeroed gradient arena (two launches: partial tiles, then their sums)."""
+        items = []
+        for j in layers:
+            g = self._wgrad_geo(j, n_all)
+            key = ("sk_ws", j, n_all)
+            wsj = self.__dict__.setdefault("_sk_ws", {}).get(key)
+            if wsj is None:
+                wsj = self._sk_ws[key] = torch.empty(ops.wgrad_sk_ws_floats(g), device=self.ws.device)
+            items.append((g, self.a[j - 1][:n_all], self.dz[j][:n_all], wsj, G[f"{self.layers[j].name}.weight"]))
+        ops.wgrad_sk(items)
+
     def _flush_unpack(self):
         """One launch moving every deferred weight grad into dW (workspaces left zeroed)."""
         if not self._deferred:
@@ -936,16 +991,21 @@ class CriticPlan:
             self._on_side(lambda: wgrad(0, x_all))
         h = gamma
         group = []  # layers whose weight grads run together in one launch after the chain (_wgrad_group)
+        skl = []    # ... on the staged-window critic kernel (ops.wgrad_sk, round 5)
         for i, ly in enumerate(self.layers[:-1]):
             g = self._geo(ops.conv_fwd_geom(n, ly.din, ly.dout, ly.cin, ly.cout, ly.k, ly.s, ly.p, planar=self.pl), self.wf[i])
             out = self._sl(self.a[i], off, n)
             w = self.wf[i] if self.wf[i] is not None else P[f"{ly.name}.weight"]
-            ops.conv(g, h, w, out, ops.epilogue(mask_src=out, slope=self.slope))
+            ops.conv(g, h, w, out, ops.epilogue(mask_src=out, slope=self.slope, split_ws=self.split_ws))
             h = out
-            if self.side is None and self._groupable(i + 1, n_all, zeroed):
+            if self.side is None and zeroed and ops.wgrad_sk_ok(self._wgrad_geo(i + 1, n_all)) and not debug("no_wgrad_sk"):
+                skl.append(i + 1)
+            elif self.side is None and self._groupable(i + 1, n_all, zeroed):
                 group.append(i + 1)
             else:
                 self._on_side(lambda i=i: wgrad(i + 1, self.a[i][:n_all]))  # a_i now holds nu_i in its interp rows
+        for k in range(0, len(skl), 4):
+            self._wgrad_sk(G, skl[k:k + 4], n_all)
         for k in range(0, len(group), 4):  # a grouped launch takes at most 4 (discriminator_depth >= 5)
             self._wgrad_group(G, group[k:k + 4], n_all)
         self._on_side(self._flush_unpack)

@@ -234,8 +234,10 @@ class Epi:
 
     def __init__(self, bias=None, residual=None, mask_src=None, minuend=None, out2=None, stats=None,
                  act=L.ACT_NONE, slope=0.0, bn_part=None, bn_mode=0, bn_slots=0, bn_z=None, bn_ss=None,
-                 bn_mi=None, bn_act=L.ACT_NONE, bn_slope=0.0, x_bf16=None, bn_fold=0, fuse=None):
+                 bn_mi=None, bn_act=L.ACT_NONE, bn_slope=0.0, x_bf16=None, bn_fold=0, fuse=None, split_ws=None):
         self.fuse = fuse  # BnFuse or None
+        # all-zero fp32 workspace a split-K launch may use (include/cgan3d.h split_ws), or None
+        self.split_ws = split_ws
         self.bias, self.residual, self.mask_src = bias, residual, mask_src
         self.x_bf16 = x_bf16  # bf16 copy of the conv input (ResNet-block kernel halo source)
         self.minuend, self.out2, self.stats = minuend, out2, stats
@@ -266,6 +268,7 @@ class Epi:
         e.x_bf16 = ptr(self.x_bf16)
         e.bn_fold = self.bn_fold
         e.out_bf16 = self.out_bf16
+        e.split_ws = ptr(self.split_ws)
         if self.fuse is not None:
             e.fuse = ctypes.pointer(self.fuse.c())  # the pointer object keeps the struct alive
         return e
@@ -327,6 +330,8 @@ def pooled_stream(device, role: str) -> "torch.cuda.Stream":
     gets the mapping of the first; plans run in turn on one host thread, so sharing keeps their order."""
     if role not in POOL_ROLES:
         raise ValueError(f"pooled_stream: role {role!r} not in {POOL_ROLES}")
+    if "own_streams" in os.environ.get("CGAN3D_DEBUG", ""):  # A/B: a new stream per plan (rounds 1-4)
+        return torch.cuda.Stream(device=device)
     dev = torch.device(device)
     idx = dev.index if dev.index is not None else torch.cuda.current_device()
     pool = _STREAM_POOL.get(idx)
@@ -554,6 +559,12 @@ def conv(g: ConvGeom, x: torch.Tensor, w: torch.Tensor, y: torch.Tensor, ep: Opt
             _need(ep.stats, sumsq_blocks(g) or stats_floats(g), "conv stats", exact=False)
         if ep.x_bf16 is not None:
             _need(ep.x_bf16, _vox_in(g) * g.cin, "conv x_bf16", dtype=torch.bfloat16)
+        if ep.split_ws is not None:
+            nsw = split_ws_floats(g)
+            if nsw == 0:
+                ep.split_ws = None  # this launch does not split: the workspace is not passed
+            else:
+                _need(ep.split_ws, nsw, "conv split_ws", exact=False)
         f = ep.bn_fold
         nz = None if not f else g.n * (g.do_ - 2 * f) * (g.ho - 2 * f) * (g.wo - 2 * f) * g.cout
         ep.check_bn(ny, g.cout, "conv", nz)
@@ -565,6 +576,11 @@ def conv(g: ConvGeom, x: torch.Tensor, w: torch.Tensor, y: torch.Tensor, ep: Opt
             raise ValueError("conv: a bf16 output takes accumulator statistics only")
     check(_timed("conv", g, "cgan3d_conv3d_fwd", ctypes.byref(g), ptr(x), ptr(w), ptr(y),
                  ctypes.byref(ep.c()) if ep is not None else None), "conv3d_fwd")
+
+
+def split_ws_floats(g: ConvGeom) -> int:
+    """Floats of the all-zero split-K workspace a launch of ``g`` uses (0: it does not split)."""
+    return int(L.load().cgan3d_conv3d_split_ws_floats(ctypes.byref(g)))
 
 
 def wgrad_ws_floats(g: ConvGeom) -> int:
@@ -617,12 +633,16 @@ def bn_fold_ok(g: ConvGeom) -> bool:
 
 
 def wgrad(g: ConvGeom, gathered, aligned, dw, ws, accumulate=False, gathered16=None, aligned16=None,
-          ws_clean=False, defer_unpack=False):
+          ws_clean=False, defer_unpack=False, defer_reduce=False):
     """Weight gradient; ``gathered16`` / ``aligned16``: optional bf16 shadows of the operands.
     ``ws_clean``: ``ws`` is all-zero and is left all-zero (geometries with ``wgrad_ws_atomic``).
-    ``defer_unpack`` (with ``ws_clean``): the result stays in ``ws`` until an ``UnpackSet`` run."""
+    ``defer_unpack`` (with ``ws_clean``): the result stays in ``ws`` until an ``UnpackSet`` run.
+    ``defer_reduce`` (geometries with ``wgrad_partials``): the partials stay in ``ws`` until a
+    ``reduce_multi`` launch sums them into ``dw``."""
     if defer_unpack and not ws_clean:
         raise ValueError("wgrad: defer_unpack needs ws_clean")
+    if defer_reduce and wgrad_partials(g) <= 0:
+        raise ValueError("wgrad: defer_reduce on a geometry without partials")
     _need(gathered, _vox_in(g) * g.cin, "wgrad gathered")
     _need(aligned, _vox_out(g) * g.cout, "wgrad aligned")
     _need(dw, g.cin * g.cout * taps(g), "wgrad dw")
@@ -630,10 +650,32 @@ def wgrad(g: ConvGeom, gathered, aligned, dw, ws, accumulate=False, gathered16=N
         raise ValueError("wgrad: weight strides exceed dw")
     _need(ws, wgrad_ws_floats(g), "wgrad ws", exact=False)
     flags = ((L.WGRAD_ACCUMULATE if accumulate else 0) | (L.WGRAD_WS_CLEAN if ws_clean else 0)
-             | (L.WGRAD_DEFER_UNPACK if defer_unpack else 0))
+             | (L.WGRAD_DEFER_UNPACK if defer_unpack else 0) | (L.WGRAD_DEFER_REDUCE if defer_reduce else 0))
     check(_timed("wgrad", g, "cgan3d_conv3d_wgrad_ex", ctypes.byref(g), ptr(gathered), ptr(aligned), ptr(dw),
                  flags, ptr(ws), _need16(gathered16, _vox_in(g) * g.cin, "wgrad gathered16"),
                  _need16(aligned16, _vox_out(g) * g.cout, "wgrad aligned16")), "conv3d_wgrad")
+
+
+def wgrad_partials(g: ConvGeom) -> int:
+    """Per-block partial sums the weight gradient of ``g`` reduces (0: it sums another way)."""
+    return int(L.load().cgan3d_conv3d_wgrad_partials(ctypes.byref(g)))
+
+
+def reduce_multi(items):
+    """Deferred weight-gradient reduces in one launch (cgan3d_wgrad_reduce_multi): ``items`` =
+    [(g, ws, dw, accumulate)] as left by ``wgrad(..., defer_reduce=True)``."""
+    if not 0 < len(items) <= 16:
+        raise ValueError("reduce_multi: 1..16 items")
+    descs = (L.ReduceDesc * len(items))()
+    for d, (g, ws, dw, acc) in zip(descs, items):
+        P = wgrad_partials(g)
+        if P <= 0:
+            raise ValueError("reduce_multi: geometry without partials")
+        _need(ws, P * 27 * g.cin * g.cout, "reduce_multi ws", exact=False)
+        _need(dw, g.cin * g.cout * taps(g), "reduce_multi dw")
+        d.ws, d.dw, d.sa, d.sb = ptr(ws), ptr(dw), g.w_sa, g.w_sb
+        d.P, d.cin, d.cout, d.accumulate = P, g.cin, g.cout, int(acc)
+    check(_launch("cgan3d_wgrad_reduce_multi", ctypes.cast(descs, ctypes.c_void_p), len(items)), "wgrad_reduce_multi")
 
 
 def wgrad_group_ok(g: ConvGeom) -> bool:
@@ -659,6 +701,37 @@ def wgrad_group(items):
     al = (ctypes.c_void_p * n)(*[b.data_ptr() for _, _, b, _ in items])
     wss = (ctypes.c_void_p * n)(*[w.data_ptr() for _, _, _, w in items])
     check(_launch("cgan3d_conv3d_wgrad_group", geoms, ga, al, wss, n), "wgrad_group")
+
+
+def wgrad_sk_ok(g: ConvGeom) -> bool:
+    """True if ``g``'s weight gradient can run on the staged-window critic kernel (``wgrad_sk``)."""
+    return bool(L.load().cgan3d_conv3d_wgrad_sk_ok(ctypes.byref(g)))
+
+
+def wgrad_sk_ws_floats(g: ConvGeom) -> int:
+    return int(L.load().cgan3d_conv3d_wgrad_sk_ws_floats(ctypes.byref(g)))
+
+
+def wgrad_sk(items):
+    """The critic's k4 s2 middle-layer weight gradients (cgan3d_conv3d_wgrad_sk): ``items`` = [(g,
+    gathered, aligned, ws, dw)]; per-block partials into ``ws`` (any contents), then their sums ADDED
+    into ``dw`` (torch layout).  Two launches for up to four layers."""
+    if not 0 < len(items) <= 4:
+        raise ValueError("wgrad_sk: 1..4 items")
+    for g, a, b, ws, dw in items:
+        if not wgrad_sk_ok(g):
+            raise ValueError("wgrad_sk: geometry not eligible (cgan3d_conv3d_wgrad_sk_ok)")
+        _need(a, _vox_in(g) * g.cin, "wgrad_sk gathered")
+        _need(b, _vox_out(g) * g.cout, "wgrad_sk aligned")
+        _need(ws, wgrad_sk_ws_floats(g), "wgrad_sk ws", exact=False)
+        _need(dw, g.cin * g.cout * taps(g), "wgrad_sk dw")
+        for t, nm in ((a, "gathered"), (b, "aligned"), (ws, "ws")):
+            if t.data_ptr() % 16:
+                raise ValueError(f"wgrad_sk: {nm} must be 16-byte aligned")
+    n = len(items)
+    geoms = (ConvGeom * n)(*[it[0] for it in items])
+    arr = [(ctypes.c_void_p * n)(*[it[k].data_ptr() for it in items]) for k in (1, 2, 3, 4)]
+    check(_launch("cgan3d_conv3d_wgrad_sk", geoms, *arr, n), "wgrad_sk")
 
 
 def bn_finalize(stats, nblk, c, gamma, beta, rmean, rvar, nbt, scale_shift, mean_invstd, momentum=0.1, eps=1e-5):

@@ -152,6 +152,7 @@ struct Epi {
   BnFuse fz;          // all-zero unless cgan3d_epilogue.fuse is given
   int out16;          // cgan3d_epilogue.out_bf16 bit 0: y and bn_z are bf16 (k7m n2w, S2T, conv_k3m launches)
   int res16;          // bit 1: the residual is bf16 (conv_k3m only)
+  float* split_ws;    // cgan3d_epilogue.split_ws: all-zero workspace of a split-K launch (conv_sk)
 };
 
 // c ? v : 0 for a just-loaded v, by an integer mask: the compiler turns a select whose operand is a
@@ -211,6 +212,8 @@ bool wgrad_k3_ok(const cgan3d_conv_geom* g);
 bool sk_format_ok(const cgan3d_conv_geom* g);
 bool sk_ok(const cgan3d_conv_geom* g);
 long long sk_blocks(const cgan3d_conv_geom* g);
+long long sk_split_ws_floats(const cgan3d_conv_geom* g);
+void sk_nsplit_set(int v);
 int sk_launch(const cgan3d_conv_geom* g, const float* x, const __bf16* wp, float* y, const Epi& e, hipStream_t st);
 // critic first layer, single channel (conv_c1.hip)
 bool c1_fwd_ok(const cgan3d_conv_geom* g);
@@ -230,7 +233,8 @@ int wgrad_s2_launch(const cgan3d_conv_geom* g, const float* gathered, const floa
                     const __bf16* a16, float* dw, int accumulate, float* ws, hipStream_t st);
 int wgrad_k3_launch(const cgan3d_conv_geom* g, const float* gathered, const float* aligned, const __bf16* g16,
                     const __bf16* a16, float* dw, int accumulate,
-                    float* ws, hipStream_t st);
+                    float* ws, hipStream_t st, bool defer_reduce = false);
+int wgrad_k3_partials(const cgan3d_conv_geom* g);
 int wgrad_c1_launch(const cgan3d_conv_geom* g, const float* gathered, const float* aligned, float* dw, hipStream_t st);
 int wgrad_bf16_group_launch(const cgan3d_conv_geom* geoms, const float* const* gathered, const float* const* aligned,
                             float* const* ws, int n, hipStream_t st);

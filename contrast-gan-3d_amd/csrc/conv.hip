@@ -563,8 +563,14 @@ static Epi to_epi(const cgan3d_epilogue* ep) {
     }
     e.out16 = ep->out_bf16 & 1;
     e.res16 = (ep->out_bf16 >> 1) & 1;
+    e.split_ws = ep->split_ws;
   }
   return e;
+}
+
+extern "C" int64_t cgan3d_conv3d_split_ws_floats(const cgan3d_conv_geom* g) {
+  if (!g || validate(g, "cgan3d_conv3d_split_ws_floats") || g->planar || g->w_packed != 3) return 0;
+  return sk_split_ws_floats(g);
 }
 
 // the launches that honour cgan3d_epilogue.out_bf16 (their dispatch conditions: the S2T kernel from
@@ -796,11 +802,14 @@ extern "C" int cgan3d_conv3d_wgrad_ex(const cgan3d_conv_geom* g, const float* ga
                                       const void* aligned_bf16, void* stream) {
   int st = validate(g, "cgan3d_conv3d_wgrad");
   if (st) return st;
-  CG_CHECK_ARG((accumulate & ~7) == 0,
+  CG_CHECK_ARG((accumulate & ~15) == 0,
                "cgan3d_conv3d_wgrad: flags are CGAN3D_WGRAD_ACCUMULATE | CGAN3D_WGRAD_WS_CLEAN | "
-               "CGAN3D_WGRAD_DEFER_UNPACK");
+               "CGAN3D_WGRAD_DEFER_UNPACK | CGAN3D_WGRAD_DEFER_REDUCE");
   const bool ws_clean = (accumulate & CGAN3D_WGRAD_WS_CLEAN) != 0;
   const bool defer = (accumulate & CGAN3D_WGRAD_DEFER_UNPACK) != 0;
+  const bool defer_reduce = (accumulate & CGAN3D_WGRAD_DEFER_REDUCE) != 0;
+  CG_CHECK_ARG(!defer_reduce || (!g->planar && wgrad_k3_partials(g) > 0),
+               "cgan3d_conv3d_wgrad: CGAN3D_WGRAD_DEFER_REDUCE on a geometry without partials (cgan3d_conv3d_wgrad_partials)");
   CG_CHECK_ARG(!defer || (ws_clean && wgrad_ws_atomic(g)),
                "cgan3d_conv3d_wgrad: CGAN3D_WGRAD_DEFER_UNPACK needs CGAN3D_WGRAD_WS_CLEAN on an atomic-workspace "
                "geometry");
@@ -859,7 +868,7 @@ extern "C" int cgan3d_conv3d_wgrad_ex(const cgan3d_conv_geom* g, const float* ga
   }
   if (wgrad_k3_ok(g)) {  // ResNet-block shape: per-block partials + reduce, no memset
     int rc = wgrad_k3_launch(g, gathered, aligned, reinterpret_cast<const __bf16*>(gathered_bf16),
-                             reinterpret_cast<const __bf16*>(aligned_bf16), dw, accumulate, ws, s);
+                             reinterpret_cast<const __bf16*>(aligned_bf16), dw, accumulate, ws, s, defer_reduce);
     if (rc) return rc;
     CG_LAUNCH_CHECK("wgrad_k3_kernel");
     return CGAN3D_OK;

@@ -663,6 +663,7 @@ extern "C" int cgan3d_set_tuning(int32_t key, int32_t value) {
     case 15: CG_CHECK_ARG(value == 0 || value == 1, "cgan3d_set_tuning 15: 0 or 1"); k3m_set(value); return CGAN3D_OK;
     case 16: CG_CHECK_ARG(value == 0 || value == 1, "cgan3d_set_tuning 16: 0 or 1"); wgrad_k3m_set(value); return CGAN3D_OK;
     case 20: CG_CHECK_ARG(value > 0, "cgan3d_set_tuning 20: blocks > 0"); k7wg_blocks_set(value); return CGAN3D_OK;
+    case 21: CG_CHECK_ARG(value == 0 || value == 1, "cgan3d_set_tuning 21: 0 or 1"); sk_nsplit_set(value); return CGAN3D_OK;
     default: break;
   }
   set_error("cgan3d_set_tuning: unknown key %d", key);

@@ -15,7 +15,16 @@
 //  * MFMA transposed (A = weights, B = activations): a lane ends with 4 channels of one output
 //    voxel, so the epilogue (bias / activation / LeakyReLU-mask / residual) moves 16 bytes per
 //    lane access; per-block BatchNorm statistics (sum, M2, count) for the BatchNorm critic of the
-//    weight-clip configuration.
+//    weight-clip configuration;
+//  * split K across blocks (round 5, SPLIT): few row tiles with a long K (the 32 -> 64 layer: 48 tiles
+//    at 12 samples, 16 at 4, K = 2048) left each block pulling all 256 KB of weights and 128 KB of
+//    gathered activations through one CU (~15 us per launch whatever the batch).  The tile's K-steps
+//    are cut over KB blocks; each adds its partial tile into an all-zero fp32 workspace (no-return
+//    atomics at the memory side, in fragment order: every wave-instruction adds 256 contiguous bytes —
+//    lanes scattered over 16 rows ran 17x slower, MI355X_MICROARCH.md atomics table), waits for them
+//    (vmcnt) and takes a ticket; the last block of the tile reads the sums back with device-coherent
+//    loads, re-zeroes the workspace and its ticket, and runs the epilogue — one launch, no memset, no
+//    L2 writeback / invalidate (nothing but atomics and coherent loads crosses blocks).
 #include "common.h"
 
 namespace cg {
@@ -28,6 +37,8 @@ struct SkArgs {
   int mblocks;             // blocks per class
   int ktot;                // k^3 * cin: packed weight row length
   int cin_log2;            // cin is a power of two (sk_format_ok)
+  int kb;                  // SPLIT: blocks per row tile, each a contiguous range of the tile's K-steps
+  int nsplit;              // blocks per row tile, each 16 NT of the output channels (MT == 1, not SPLIT)
 };
 
 __device__ __forceinline__ void sk_class(int r, int k, int s, int p, int transposed, int* f, int* st, int* cnt) {
@@ -38,18 +49,23 @@ __device__ __forceinline__ void sk_class(int r, int k, int s, int p, int transpo
   }
 }
 
-// W: waves per block (MT == 1 splits K over them); NKC: compile-time K-steps per wave (0: runtime)
-template <int MT, int NT, int W, int NKC>
+// W: waves per block (MT == 1 splits K over them); NKC: compile-time K-steps per wave (0: runtime);
+// SPLIT (MT == 1): a.kb blocks per row tile, partial tiles summed in ep.split_ws (above)
+template <int MT, int NT, int W, int NKC, bool SPLIT>
 __global__ __launch_bounds__(64 * W) void conv_sk_kernel(SkArgs a, const float* __restrict__ x,
                                                          const __bf16* __restrict__ wp, float* y, Epi ep) {
-  __shared__ int tq[3][64];
-  __shared__ int tlin[64];
   __shared__ int rowo[16 * MT];
   __shared__ int rowb[3][16 * MT];  // gathered-grid base coordinate per row (gathered = base + tq)
   __shared__ int rown[16 * MT];
   __shared__ __attribute__((aligned(16))) f32x4 red[W - 1][NT][64];
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int cls = blockIdx.x / a.mblocks, mb = blockIdx.x - cls * a.mblocks;
+  // SPLIT: the a.kb blocks of one row tile are consecutive (their tickets complete together)
+  const int kbn = SPLIT ? a.kb : 1;
+  // N split (MT == 1): the a.nsplit blocks of a row tile take consecutive 16 NT-channel slices
+  const int nsp = (MT == 1 && !SPLIT) ? a.nsplit : 1;
+  const int bq = (int)blockIdx.x / nsp, cb = ((int)blockIdx.x - bq * nsp) * 16 * NT;
+  const int tile = SPLIT ? bq / kbn : bq, kbi = SPLIT ? bq - tile * kbn : 0;
+  const int cls = tile / a.mblocks, mb = tile - cls * a.mblocks;
   const int s = a.s;
   int r3[3] = {0, 0, 0};
   if (a.transposed) { r3[0] = cls / (s * s); r3[1] = (cls / s) % s; r3[2] = cls % s; }
@@ -58,16 +74,9 @@ __global__ __launch_bounds__(64 * W) void conv_sk_kernel(SkArgs a, const float* 
   sk_class(r3[1], a.k, s, a.p, a.transposed, &fy, &sy, &ny);
   sk_class(r3[2], a.k, s, a.p, a.transposed, &fx, &sx, &nx);
   const int ntap = nz * ny * nx;
-  if (tid < ntap) {
-    const int mw = tid % nx, mh = (tid / nx) % ny, md = tid / (nx * ny);
-    const int t0 = fz + sz * md, t1 = fy + sy * mh, t2 = fx + sx * mw;
-    if (a.transposed) {  // o = j*s + r, i = j + (r + p - t)/s
-      tq[0][tid] = (r3[0] + a.p - t0) / s; tq[1][tid] = (r3[1] + a.p - t1) / s; tq[2][tid] = (r3[2] + a.p - t2) / s;
-    } else {
-      tq[0][tid] = t0; tq[1][tid] = t1; tq[2][tid] = t2;
-    }
-    tlin[tid] = (t0 * a.k + t1) * a.k + t2;
-  }
+  (void)sz;
+  (void)sy;
+  (void)sx;
   if (tid < 16 * MT) {
     // 32-bit index math (sk_format_ok bounds every volume below 2^31 elements)
     const unsigned m = (unsigned)mb * 16 * MT + tid;
@@ -96,8 +105,18 @@ __global__ __launch_bounds__(64 * W) void conv_sk_kernel(SkArgs a, const float* 
   const int row = mt * 16 + r16;
   const bool rok = rowo[row] >= 0;
   const int bz = rowb[0][row], by = rowb[1][row], bx = rowb[2][row], nb = rown[row];
+  // tap j of the class = digits (md, mh, mw) in base 4 (forward: t = m) or 2 (transposed: t = f + s m,
+  // gathered coordinate j + (r + p - t) / s = C - m), decoded in registers (round 5: the round-4 tap
+  // tables in LDS put dependent LDS reads in front of every K-step's global loads)
+  const int lg = nz == 2 ? 1 : 2, lm = (1 << lg) - 1, sg = a.transposed ? -1 : 1, st = a.transposed ? s : 1;
+  const int Cz = bz + (a.transposed ? (r3[0] + a.p - fz) / s : 0);
+  const int Cy = by + (a.transposed ? (r3[1] + a.p - fy) / s : 0);
+  const int Cx = bx + (a.transposed ? (r3[2] + a.p - fx) / s : 0);
+  const int HW = a.hi * a.wi;
+  const int gbase = ((nb * a.di + Cz) * a.hi + Cy) * a.wi + Cx;
   const int KS = ntap * a.cin / 32;
-  const int ks0 = MT == 1 ? wave : 0, kstep = MT == 1 ? W : 1;
+  const int kbeg = SPLIT ? (KS * kbi) / kbn : 0, kend = SPLIT ? (KS * (kbi + 1)) / kbn : KS;
+  const int ks0 = kbeg + (MT == 1 ? wave : 0), kstep = MT == 1 ? W : 1;
 
   f32x4 acc[NT];
 #pragma unroll
@@ -114,24 +133,25 @@ __global__ __launch_bounds__(64 * W) void conv_sk_kernel(SkArgs a, const float* 
   f32x4 xa0[PF], xa1[PF];  // A: 8 fp32 channels of one gathered voxel
   bool xok[PF];            // ... live (applied at the MFMA: a select right after the load waits for it)
   bf16x8_k bb[PF][NT];     // B fragments
-  const int nk = ks0 < KS ? (KS - ks0 + kstep - 1) / kstep : 0;  // this wave's K-steps (wave-uniform)
+  const int nk = ks0 < kend ? (kend - ks0 + kstep - 1) / kstep : 0;  // this wave's K-steps (wave-uniform)
   auto load = [&](int q, int sl) {
     const bool live = q < nk;
     const int ks = ks0 + min(q, max(nk - 1, 0)) * kstep;
     const int k0 = ks * 32 + 8 * g;
     const int j = k0 >> a.cin_log2, a0 = k0 & (a.cin - 1);
-    const int iz = bz + tq[0][j], iy = by + tq[1][j], ix = bx + tq[2][j];
+    const int md = j >> (2 * lg), mh = (j >> lg) & lm, mw = j & lm;
+    const int iz = Cz + sg * md, iy = Cy + sg * mh, ix = Cx + sg * mw;
     const bool ok = live && rok && (unsigned)iz < (unsigned)a.di && (unsigned)iy < (unsigned)a.hi &&
                     (unsigned)ix < (unsigned)a.wi;
     // 32-bit element offsets (sk_launch checks the sizes); a dead operand reads element 0
-    const float* src = x + (ok ? ((((nb * a.di + iz) * a.hi + iy) * a.wi + ix) << a.cin_log2) + a0 : 0);
+    const float* src = x + (ok ? ((gbase + sg * (md * HW + mh * a.wi + mw)) << a.cin_log2) + a0 : 0);
     xa0[sl] = *reinterpret_cast<const f32x4*>(src);
     xa1[sl] = *reinterpret_cast<const f32x4*>(src + 4);
     xok[sl] = ok;
-    const int wk = tlin[j] * a.cin + a0;
+    const int wk = (((fz + st * md) * 4 + fy + st * mh) * 4 + fx + st * mw) * a.cin + a0;  // k == 4
 #pragma unroll
     for (int t = 0; t < NT; ++t)  // columns past cout (cout = 8) read a valid row; their outputs are never stored
-      bb[sl][t] = *reinterpret_cast<const bf16x8_k*>(wp + min(t * 16 + r16, a.cout - 1) * a.ktot + wk);
+      bb[sl][t] = *reinterpret_cast<const bf16x8_k*>(wp + min(cb + t * 16 + r16, a.cout - 1) * a.ktot + wk);
   };
   auto step = [&](int sl) {
     bf16x8_k av;
@@ -176,6 +196,33 @@ __global__ __launch_bounds__(64 * W) void conv_sk_kernel(SkArgs a, const float* 
       acc[t] += r;
     }
   }
+  if constexpr (SPLIT) {  // wave 0: this block's partial tile into the workspace, then the ticket
+    // fragment order [tile][t][jj][lane]: one wave-instruction = 64 consecutive floats
+    float* tt = ep.split_ws + (long long)tile * 16 * 16 * NT + lane;
+    unsigned* ctr = reinterpret_cast<unsigned*>(ep.split_ws + (long long)a.nclass * a.mblocks * 16 * 16 * NT);
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj)
+        __hip_atomic_fetch_add(tt + (t * 4 + jj) * 64, acc[t][jj], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // every add performed at the memory side (no-return atomics stay counted in vmcnt until then)
+    // before the ticket is taken
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    unsigned tk = 0;
+    if (lane == 0) tk = __hip_atomic_fetch_add(ctr + tile, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    tk = __shfl(tk, 0, 64);
+    if (tk != (unsigned)(kbn - 1)) return;  // not the tile's last block
+    asm volatile("" ::: "memory");
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj) {
+        float* pw = tt + (t * 4 + jj) * 64;
+        acc[t][jj] = __hip_atomic_load(pw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(pw, 0.f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // left all-zero
+      }
+    if (lane == 0) __hip_atomic_store(ctr + tile, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
   // epilogue: the MFMA ran transposed (A = weights, B = activations), so lane (g, r16) holds
   // channels t*16 + 4g .. +3 of row mt*16 + r16: one 16-byte store (and mask / residual load) per
   // lane and N tile (cout % 8 == 0: a lane's four channels are all in range or all out)
@@ -183,7 +230,7 @@ __global__ __launch_bounds__(64 * W) void conv_sk_kernel(SkArgs a, const float* 
   float vals[NT][4];
 #pragma unroll
   for (int t = 0; t < NT; ++t) {
-    const int c0 = t * 16 + 4 * g;
+    const int c0 = cb + t * 16 + 4 * g;
     const bool ok = c0 < a.cout && ro >= 0;
     f32x4 v = acc[t];
     if (ep.bias && c0 < a.cout) {
@@ -212,10 +259,10 @@ __global__ __launch_bounds__(64 * W) void conv_sk_kernel(SkArgs a, const float* 
                    // block (MT == 1) or per wave (MT == 4); rows are the 16 lanes of a lane group
     int cnt = 0;
     for (int r = 0; r < 16; ++r) cnt += rowo[mt * 16 + r] >= 0;
-    const long long sb = ((long long)blockIdx.x * MT + mt) * (2 * a.cout + 1);
+    const long long sb = ((long long)tile * MT + mt) * (2 * a.cout + 1);
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
-      const int c0 = t * 16 + 4 * g;
+      const int c0 = cb + t * 16 + 4 * g;
 #pragma unroll
       for (int jj = 0; jj < 4; ++jj) {
         float S = vals[t][jj];
@@ -239,6 +286,7 @@ __global__ __launch_bounds__(64 * W) void conv_sk_kernel(SkArgs a, const float* 
 // geometry (ignoring the weight format): the critic's k4 convs, bf16
 bool sk_format_ok(const cgan3d_conv_geom* g) {
   if (g->prec != CGAN3D_PREC_BF16 || g->reflect || g->k != 4 || g->cin % 8 || g->cout % 8 || g->cout > 64) return false;
+  if (g->stride != 1 && g->stride != 2) return false;  // taps per dim 4 or 2 (the kernel's digit decode)
   if (g->cin & (g->cin - 1)) return false;  // power of two: shift / mask index math
   if ((long long)g->n * g->di * g->hi * g->wi * g->cin >= (1LL << 31) ||
       (long long)g->n * g->do_ * g->ho * g->wo * g->cout >= (1LL << 31))
@@ -271,10 +319,36 @@ static SkArgs sk_args(const cgan3d_conv_geom* g, int* mt) {
   a.ktot = g->k * g->k * g->k * g->cin;
   a.cin_log2 = 0;
   while ((1 << a.cin_log2) < g->cin) ++a.cin_log2;
+  a.kb = 1;
+  a.nsplit = 1;
   return a;
 }
 
-long long sk_blocks(const cgan3d_conv_geom* g) {  // rows of the statistics epilogue
+// split K over blocks (SPLIT) when the row tiles alone leave most of the chip idle and K is long:
+// ~384 blocks, >= 1 K-step per wave of 4 (the launch then runs 4-wave blocks)
+static int sk_split_kb(const cgan3d_conv_geom* g, const SkArgs& a, int mt) {
+  if (mt != 1 || g->transposed) return 1;
+  const int kd = g->k;
+  const int KS = kd * kd * kd * g->cin / 32;
+  const long long tiles = (long long)a.nclass * a.mblocks;
+  if (KS < 64 || tiles >= 192) return 1;  // the 32 -> 64 layer (K = 2048); shorter K: measured slower split
+  const long long want = (384 + tiles - 1) / tiles;
+  return (int)std::max(1LL, std::min<long long>(want, KS / 4));
+}
+
+static int g_sk_nsplit = 1;  // cgan3d_set_tuning key 21 (A/B): 0 keeps the long-K layer on whole-N blocks
+void sk_nsplit_set(int v) { g_sk_nsplit = v; }
+
+long long sk_split_ws_floats(const cgan3d_conv_geom* g) {
+  if (!sk_ok(g)) return 0;
+  int mt;
+  SkArgs a = sk_args(g, &mt);
+  if (sk_split_kb(g, a, mt) <= 1) return 0;
+  const long long tiles = (long long)a.nclass * a.mblocks;
+  return tiles * 16 * 16 * ((g->cout + 15) / 16) + tiles;  // partial tiles (fragment order) + one ticket each
+}
+
+long long sk_blocks(const cgan3d_conv_geom* g) {  // rows of the statistics epilogue (per row tile)
   int mt;
   SkArgs a = sk_args(g, &mt);
   return (long long)a.nclass * a.mblocks * mt;
@@ -287,12 +361,40 @@ int sk_launch(const cgan3d_conv_geom* g, const float* x, const __bf16* wp, float
   int mt;
   SkArgs a = sk_args(g, &mt);
   const int nt = (g->cout + 15) / 16;
-  const dim3 grid((unsigned)(a.nclass * a.mblocks));
+  const int kb = e.split_ws && !e.stats ? sk_split_kb(g, a, mt) : 1;
+  CG_CHECK_ARG(!e.split_ws || kb > 1 || sk_split_ws_floats(g) == 0 || e.stats,
+               "conv_sk: split workspace given to a launch that does not split");
+  if (kb > 1) {  // SPLIT: 4-wave blocks, a contiguous K range each (sk_split_kb)
+    a.kb = kb;
+    const dim3 grid((unsigned)(a.nclass * a.mblocks * kb));
+    const int kd = g->k;
+    const int KS = kd * kd * kd * g->cin / 32;
+    const int nkw = ((KS + kb - 1) / kb + 3) / 4;  // most K-steps of a wave
+    auto by_nt = [&](auto nkc_c) {
+      constexpr int K = decltype(nkc_c)::value;
+      if (nt == 1) ::cg::launch((conv_sk_kernel<1, 1, 4, K, true>), grid, dim3(256), 0, st, a, x, wp, y, e);
+      else if (nt == 2) ::cg::launch((conv_sk_kernel<1, 2, 4, K, true>), grid, dim3(256), 0, st, a, x, wp, y, e);
+      else if (nt == 3) ::cg::launch((conv_sk_kernel<1, 3, 4, K, true>), grid, dim3(256), 0, st, a, x, wp, y, e);
+      else ::cg::launch((conv_sk_kernel<1, 4, 4, K, true>), grid, dim3(256), 0, st, a, x, wp, y, e);
+    };
+    if (nkw <= 1) by_nt(std::integral_constant<int, 1>{});
+    else if (nkw <= 2) by_nt(std::integral_constant<int, 2>{});
+    else if (nkw <= 4) by_nt(std::integral_constant<int, 4>{});
+    else by_nt(std::integral_constant<int, 8>{});
+    return CGAN3D_OK;
+  }
   // K-steps per wave, as a compile-time trip count where it is short (every parity class has the
   // same tap count here: k % s == 0)
   const int kd = g->transposed ? g->k / g->stride : g->k;
   const int KS = kd * kd * kd * g->cin / 32;
-  const bool wide = mt == 1 && grid.x < 128 && !e.stats;
+  // N split (round 5): few row tiles with a long K (the 32 -> 64 layer, K = 2048) — each block reads
+  // only its 16 output channels' weights (64 KB instead of 256 KB through one CU), nt blocks per tile
+  const long long tiles = (long long)a.nclass * a.mblocks;
+  const int ns = (g_sk_nsplit && mt == 1 && !e.stats && KS >= 64 && tiles < 192) ? nt : 1;
+  a.nsplit = ns;
+  const int ntb = nt / ns;
+  const dim3 grid((unsigned)(tiles * ns));
+  const bool wide = mt == 1 && tiles < 128 && !e.stats;
   const int w = wide ? 8 : 4;
   const int nk = mt == 1 ? (KS + w - 1) / w : KS;
   const int nkc = nk <= 4 ? 4 : nk <= 8 ? 8 : nk <= 16 ? 16 : 0;
@@ -301,10 +403,10 @@ int sk_launch(const cgan3d_conv_geom* g, const float* x, const __bf16* wp, float
     auto by_nt = [&](auto nkc_c) {
       constexpr int K = decltype(nkc_c)::value;
       const dim3 block(64 * W);
-      if (nt == 1) ::cg::launch((conv_sk_kernel<M, 1, W, K>), grid, block, 0, st, a, x, wp, y, e);
-      else if (nt == 2) ::cg::launch((conv_sk_kernel<M, 2, W, K>), grid, block, 0, st, a, x, wp, y, e);
-      else if (nt == 3) ::cg::launch((conv_sk_kernel<M, 3, W, K>), grid, block, 0, st, a, x, wp, y, e);
-      else ::cg::launch((conv_sk_kernel<M, 4, W, K>), grid, block, 0, st, a, x, wp, y, e);
+      if (ntb == 1) ::cg::launch((conv_sk_kernel<M, 1, W, K, false>), grid, block, 0, st, a, x, wp, y, e);
+      else if (ntb == 2) ::cg::launch((conv_sk_kernel<M, 2, W, K, false>), grid, block, 0, st, a, x, wp, y, e);
+      else if (ntb == 3) ::cg::launch((conv_sk_kernel<M, 3, W, K, false>), grid, block, 0, st, a, x, wp, y, e);
+      else ::cg::launch((conv_sk_kernel<M, 4, W, K, false>), grid, block, 0, st, a, x, wp, y, e);
     };
     if (nkc == 4) by_nt(std::integral_constant<int, 4>{});
     else if (nkc == 8) by_nt(std::integral_constant<int, 8>{});

@@ -861,8 +861,50 @@ long long wgrad_k3_ws_floats(const cgan3d_conv_geom* g) {
   return (long long)P * 27 * 64 * 64;
 }
 
+int wgrad_k3_partials(const cgan3d_conv_geom* g) {
+  if (!wgrad_k3_ok(g)) return 0;
+  Wk3Args a;
+  int P;
+  wgrad_k3_geometry(g, &a, &P);
+  return P;
+}
+
+// every deferred ResNet weight gradient of a backward in one launch (blockIdx.y = descriptor)
+struct ReduceMulti {
+  cgan3d_reduce_desc d[16];
+  int n;
+};
+
+__global__ __launch_bounds__(1024) void wgrad_reduce_multi_kernel(ReduceMulti R) {
+  const cgan3d_reduce_desc& d = R.d[blockIdx.y];
+  __shared__ float part[16][64];
+  const int lane = threadIdx.x & 63, c = threadIdx.x >> 6, NC = blockDim.x >> 6;
+  const int A = d.cin, B = d.cout, P = d.P;
+  const long long E = 27LL * A * B, e = (long long)blockIdx.x * 64 + lane;
+  const bool ok = e < E;
+  const int pc = (P + NC - 1) / NC, p0 = c * pc, p1 = min(P, p0 + pc);
+  float s[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) s[j] = 0.f;
+  for (int p = p0; p < p1; p += 8)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float v = d.ws[(long long)(p + j < p1 ? p + j : p0) * E + (ok ? e : 0)];
+      s[j] += p + j < p1 ? v : 0.f;
+    }
+  part[c][lane] = ((s[0] + s[1]) + (s[2] + s[3])) + ((s[4] + s[5]) + (s[6] + s[7]));
+  __syncthreads();
+  if (c == 0 && ok) {
+    float v = 0.f;
+    for (int k = 0; k < NC; ++k) v += part[k][lane];
+    const int a = (int)(e % A), r = (int)(e / A), b = r % B, t = r / B;
+    float* o = d.dw + (long long)b * d.sb + (long long)a * d.sa + t;
+    *o = d.accumulate ? *o + v : v;
+  }
+}
+
 int wgrad_k3_launch(const cgan3d_conv_geom* g, const float* gathered, const float* aligned, const __bf16* g16,
-                    const __bf16* a16, float* dw, int accumulate, float* ws, hipStream_t st) {
+                    const __bf16* a16, float* dw, int accumulate, float* ws, hipStream_t st, bool defer_reduce) {
   Wk3Args a;
   int P;
   wgrad_k3_geometry(g, &a, &P);
@@ -872,9 +914,34 @@ int wgrad_k3_launch(const cgan3d_conv_geom* g, const float* gathered, const floa
     ::cg::launch(wgrad_k3_kernel<true>, dim3(P, 9), dim3(512), 0, st, a, gathered, aligned, g16, a16, ws);
   else
     ::cg::launch(wgrad_k3_kernel<false>, dim3(P, 9), dim3(512), 0, st, a, gathered, aligned, g16, a16, ws);
-  wgrad_reduce_launch(ws, P, 64, 64, dw, (long long)g->w_sa, (long long)g->w_sb, accumulate, st);
+  if (!defer_reduce) wgrad_reduce_launch(ws, P, 64, 64, dw, (long long)g->w_sa, (long long)g->w_sb, accumulate, st);
   return CGAN3D_OK;
 }
+
+}  // namespace cg
+
+extern "C" int32_t cgan3d_conv3d_wgrad_partials(const cgan3d_conv_geom* g) { return g ? cg::wgrad_k3_partials(g) : 0; }
+
+extern "C" int cgan3d_wgrad_reduce_multi(const cgan3d_reduce_desc* descs, int32_t n, void* stream) {
+  CG_CHECK_ARG(descs && n >= 1 && n <= 16, "cgan3d_wgrad_reduce_multi: 1..16 descriptors");
+  cg::ReduceMulti R{};
+  R.n = n;
+  int pmax = 1, emax = 1;
+  for (int i = 0; i < n; ++i) {
+    const cgan3d_reduce_desc& d = descs[i];
+    CG_CHECK_ARG(d.ws && d.dw && d.P > 0 && d.cin > 0 && d.cout > 0, "cgan3d_wgrad_reduce_multi: bad descriptor %d", i);
+    R.d[i] = d;
+    pmax = std::max(pmax, (int)d.P);
+    emax = std::max(emax, 27 * d.cin * d.cout);
+  }
+  const int nc = std::max(1, std::min(16, (pmax + 7) / 8));
+  ::cg::launch(cg::wgrad_reduce_multi_kernel, dim3((unsigned)((emax + 63) / 64), (unsigned)n), dim3(64 * nc), 0,
+               (hipStream_t)stream, R);
+  CG_LAUNCH_CHECK("wgrad_reduce_multi_kernel");
+  return CGAN3D_OK;
+}
+
+namespace cg {
 
 static int g_ws2_P = 128;  // cgan3d_set_tuning key 10: blocks of wgrad_s2_kernel; 0 = off
 

@@ -138,6 +138,10 @@ typedef struct cgan3d_epilogue {
                                 * bf16 (the ResNet-block kernel only): the generator's BatchNorm inputs
                                 * and their gradients kept in bf16 (round 4) — only launches with
                                 * cgan3d_conv3d_out_bf16_ok accept it, every other launch rejects it */
+  float* split_ws;             /* NULL, or an all-zero fp32 workspace of cgan3d_conv3d_split_ws_floats(g)
+                                * floats: the launch may then split its reduction over more blocks
+                                * (partial tiles summed there; left all-zero on return).  Launches with
+                                * no split (split_ws_floats 0) ignore it. */
 } cgan3d_epilogue;
 
 /* 1 when the forward-style launch of g honours cgan3d_epilogue.out_bf16: the 1 -> 16 k7 MFMA kernel
@@ -146,6 +150,10 @@ typedef struct cgan3d_epilogue {
  * statistics reading a bf16 z) and the ResNet-block kernel (Conv3d 64 -> 64 k3 forward / input-grad
  * with the bf16 input shadow; bit 1 there: a bf16 skip gradient as the residual). */
 int32_t cgan3d_conv3d_out_bf16_ok(const cgan3d_conv_geom* g);
+
+/* fp32 floats of cgan3d_epilogue.split_ws for a launch of g that splits its reduction over blocks
+ * (the critic's k4 layers with few output rows and a long K, discriminator.py:42-68); 0 when it does not. */
+int64_t cgan3d_conv3d_split_ws_floats(const cgan3d_conv_geom* g);
 
 /* 1 when the geometry's launch can produce cgan3d_bn_fuse accumulators. */
 int32_t cgan3d_bn_fuse_ok(const cgan3d_conv_geom* g);
@@ -233,6 +241,21 @@ typedef struct cgan3d_unpack_desc {
 } cgan3d_unpack_desc;
 /* `descs`: a DEVICE array of n descriptors; max_total = the largest taps*cin*cout among them */
 int cgan3d_wgrad_unpack_multi(const cgan3d_unpack_desc* descs, int32_t n, int64_t max_total, void* stream);
+/* on a geometry whose weight gradient reduces per-block partials (cgan3d_conv3d_wgrad_partials > 0:
+ * the ResNet-block k3 kernel): leave the partials in ws and skip the reduce; the caller sums them into
+ * dw later with cgan3d_wgrad_reduce_multi — one launch for every ResNet layer of a backward (round 5) */
+#define CGAN3D_WGRAD_DEFER_REDUCE 8
+/* partial sums the weight gradient of g leaves in ws (ws[p][27][cout][cin], p < P), 0 if it sums
+ * another way */
+int32_t cgan3d_conv3d_wgrad_partials(const cgan3d_conv_geom* g);
+typedef struct cgan3d_reduce_desc {
+  const float* ws;  /* P partials [p][27][cout][cin] of one deferred weight gradient */
+  float* dw;        /* dw[a*sa + b*sb + tap] (+)= sum_p ws[p][tap][b][a] */
+  int64_t sa, sb;
+  int32_t P, cin, cout, accumulate;
+} cgan3d_reduce_desc;
+/* 1 <= n <= 16 descriptors (passed by value into the launch) */
+int cgan3d_wgrad_reduce_multi(const cgan3d_reduce_desc* descs, int32_t n, void* stream);
 /* 1 if the weight gradient of `g` sums into its workspace by atomics (the geometries that may take
  * CGAN3D_WGRAD_WS_CLEAN), 0 if not, -1 on an invalid geometry. */
 int cgan3d_conv3d_wgrad_ws_mode(const cgan3d_conv_geom* g);
@@ -255,6 +278,18 @@ int cgan3d_conv3d_wgrad_ex(const cgan3d_conv_geom* g, const float* gathered, con
  * CGAN3D_WGRAD_ACCUMULATE | CGAN3D_WGRAD_WS_CLEAN | CGAN3D_WGRAD_DEFER_UNPACK would (then
  * cgan3d_wgrad_unpack_multi).  1 <= n <= 4; every geometry cgan3d_conv3d_wgrad_group_ok. */
 int32_t cgan3d_conv3d_wgrad_group_ok(const cgan3d_conv_geom* g);
+
+/* The critic's k4 s2 p1 middle-layer weight gradients (discriminator.py:42-68, their penalty update,
+ * Trainer.py:108-142) from a staged input window per output tile (every tap a row shift inside it),
+ * bf16 MFMA, fp32 accumulation (round 5, csrc/wgrad_sk.hip): per-block partial tiles into ws[i]
+ * (cgan3d_conv3d_wgrad_sk_ws_floats(g) floats, any contents), then one reduce launch that ADDS the
+ * sums into dw[i] (torch layout, g.w_sa / g.w_sb).  1 <= n <= 4; geometries cgan3d_conv3d_wgrad_sk_ok:
+ * bf16, not transposed, (cin, cout) = (8, 16) / (16, 32) / (32, 64), input = 2 x output, output
+ * divisible by the variant's tile (4 x 8 x 8 / 4 x 4 x 8 / 4 x 4 x 4).  Two launches. */
+int32_t cgan3d_conv3d_wgrad_sk_ok(const cgan3d_conv_geom* g);
+int64_t cgan3d_conv3d_wgrad_sk_ws_floats(const cgan3d_conv_geom* g);
+int cgan3d_conv3d_wgrad_sk(const cgan3d_conv_geom* geoms, const float* const* gathered, const float* const* aligned,
+                           float* const* ws, float* const* dw, int32_t n, void* stream);
 int cgan3d_conv3d_wgrad_group(const cgan3d_conv_geom* geoms, const float* const* gathered,
                               const float* const* aligned, float* const* ws, int32_t n, void* stream);
 

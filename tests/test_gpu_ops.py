@@ -606,6 +606,87 @@ def test_conv_sk_bf16(cin, cout, sp):
     assert_close(_ncdhw(dxo).numpy(), dxref.numpy(), 2e-2, "sk dgrad")
 
 
+@pytest.mark.parametrize("n,cin,cout,sp", [(12, 32, 64, (8, 8, 8)), (4, 32, 64, (8, 8, 8)), (2, 32, 64, (8, 8, 8)),
+                                             (1, 32, 64, (8, 8, 8)), (3, 32, 64, (10, 8, 12))])
+def test_conv_sk_split_k(n, cin, cout, sp):
+    """Split-K conv_sk (round 5, cgan3d_epilogue.split_ws): the critic's 32 -> 64 layer with its K
+    (2048) cut over blocks, partial tiles summed in an all-zero workspace by
+    atomics and the tile's last block running the epilogue.  Against torch float64 within the bf16
+    bar (2e-2) and against the unsplit launch within fp32 summation-order noise (1e-5 of the output's
+    largest entry); the workspace is all-zero again after each launch (so the plan can reuse it), and
+    a second launch on the same workspace gives the same result."""
+    from cgan3d_amd import ops, _lib as L
+    k, s, p, slope = 4, 2, 1, 0.2
+    g = torch.Generator().manual_seed(5 + n + cin + sp[0])
+    x = torch.randn(n, cin, *sp, generator=g, dtype=torch.float64)
+    w = torch.randn(cout, cin, k, k, k, generator=g, dtype=torch.float64) / np.sqrt(cin * k**3)
+    b = torch.randn(cout, generator=g, dtype=torch.float64) * 0.1
+    z = F.conv3d(x, w, b, stride=s, padding=p)
+    yref = F.leaky_relu(z, slope)
+    din, dout = tuple(sp), tuple(z.shape[2:])
+    ps = ops.PackSet(torch.device("cuda"))
+    gf, wf = ps.add(ops.conv_fwd_geom(n, din, dout, cin, cout, k, s, p), w.float().cuda(), L.PREC_BF16)
+    ps.pack()
+    nsw = ops.split_ws_floats(gf)
+    assert nsw > 0, "this geometry is meant to split"
+    ws = torch.zeros(nsw, device="cuda")
+    bb = b.float().cuda()
+    y0 = torch.empty(n, *dout, cout, device="cuda")
+    ops.conv(gf, _cl(x), wf, y0, ops.epilogue(bias=bb, act=L.ACT_LRELU, slope=slope))  # unsplit
+    outs = []
+    for _ in range(2):
+        y1 = torch.full_like(y0, float("nan"))
+        ops.conv(gf, _cl(x), wf, y1, ops.epilogue(bias=bb, act=L.ACT_LRELU, slope=slope, split_ws=ws))
+        torch.cuda.synchronize()
+        assert torch.count_nonzero(ws) == 0, "split workspace not left all-zero"
+        outs.append(y1)
+    assert_close(_ncdhw(outs[0]).numpy(), yref.numpy(), 2e-2, "split fwd")
+    scale = float(y0.abs().max())
+    assert float((outs[0] - y0).abs().max()) <= 1e-5 * scale and float((outs[1] - y0).abs().max()) <= 1e-5 * scale
+    # the gradient penalty's forward-mode launch (mask = the output's previous contents, in place)
+    nu = outs[0].clone()
+    ops.conv(gf, _cl(x), wf, nu, ops.epilogue(mask_src=nu, slope=slope, split_ws=ws))
+    zf = F.conv3d(x, w, stride=s, padding=p)
+    assert_close(_ncdhw(nu).numpy(), torch.where(_ncdhw(outs[0]) > 0, zf, zf * slope).numpy(), 2e-2, "split fwd-mode")
+    assert torch.count_nonzero(ws) == 0
+
+
+@pytest.mark.parametrize("n,cin,cout,sp", [(12, 8, 16, (32, 32, 32)), (12, 16, 32, (16, 16, 16)), (12, 32, 64, (8, 8, 8)),
+                                             (3, 8, 16, (16, 32, 64)), (2, 32, 64, (16, 8, 8)), (12, 64, 1, (4, 4, 4)),
+                                             (3, 64, 1, (3, 4, 2))])
+def test_wgrad_sk_matches_float64(n, cin, cout, sp):
+    """The staged-window critic weight gradient (round 5, cgan3d_conv3d_wgrad_sk): the three middle-layer
+    variants (k4 s2, bf16 operands: against torch float64 of the bf16-rounded operands at 1e-4 relative
+    L2 — fp32 accumulation of exact bf16 products — and the unrounded ones within the bf16 bar, 2e-2)
+    and the last layer (64 -> 1 k4 s1, exact fp32: 1e-5 of float64); the result is ADDED into dW (a
+    prefilled dW keeps its contents)."""
+    from cgan3d_amd import ops, _lib as L
+    k, p = 4, 1
+    s = 1 if cout == 1 else 2
+    g = torch.Generator().manual_seed(7 + n + cin + sp[1])
+    x = torch.randn(n, cin, *sp, generator=g, dtype=torch.float64)
+    dout = tuple(d // 2 for d in sp) if s == 2 else tuple(d - 1 for d in sp)
+    dz = torch.randn(n, cout, *dout, generator=g, dtype=torch.float64)
+    geo = ops.with_prec(ops.conv_wgrad_geom(n, tuple(sp), dout, cin, cout, k, s, p), L.PREC_BF16)
+    assert ops.wgrad_sk_ok(geo)
+    ws = torch.full((ops.wgrad_sk_ws_floats(geo),), float("nan"), device="cuda")  # any contents
+    pre = torch.randn(cout, cin, k, k, k, generator=g).float().cuda()
+    dw = pre.clone()
+    ops.wgrad_sk([(geo, _cl(x), _cl(dz), ws, dw)])
+    got = (dw - pre).double().cpu()
+    want = torch.nn.grad.conv3d_weight(x, (cout, cin, k, k, k), dz, stride=s, padding=p)
+    if cout == 1:  # exact fp32 last layer (fp32 operands)
+        want32 = torch.nn.grad.conv3d_weight(x.float().double(), (cout, cin, k, k, k), dz.float().double(), stride=s,
+                                             padding=p)
+        assert float((got - want32).abs().max()) <= 1e-5 * float(want32.abs().max()) + 1e-6
+        return
+    rb = lambda t: t.float().bfloat16().double()  # noqa: E731
+    want16 = torch.nn.grad.conv3d_weight(rb(x), (cout, cin, k, k, k), rb(dz), stride=s, padding=p)
+    rel = float((got - want16).norm() / want16.norm())
+    assert rel <= 1e-4, f"vs bf16-operand float64: rel L2 {rel:.2e}"
+    assert_close(got.numpy(), want.numpy(), 2e-2, "wgrad_sk vs float64")
+
+
 def test_adam_pack_matches_separate_launches():
     """cgan3d_adam_pack (step tick + Adam + repack of every packed format in one launch) leaves
     the same bits as cgan3d_adam_tick -> cgan3d_adam -> cgan3d_pack_weights_multi, over three

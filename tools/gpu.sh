@@ -15,7 +15,7 @@
 #   configs          bench lines of the other single-GPU BASELINE configs and paths
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
-O=$R/gpurun_out
+O=${GPU_OUT:-$R/gpurun_out}
 mkdir -p $O
 export TMPDIR=/tmp
 KERNEL=${KERNEL:-.}
