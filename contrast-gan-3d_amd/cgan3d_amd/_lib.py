@@ -70,6 +70,17 @@ class ReduceDesc(C.Structure):
                 ("P", C.c_int32), ("cin", C.c_int32), ("cout", C.c_int32), ("accumulate", C.c_int32)]
 
 
+class BnPre(C.Structure):
+    """include/cgan3d.h cgan3d_bn_pre: the conv input's BatchNorm applied while the ResNet-block kernel
+    stages its halo (mode 1 forward, 2 input-grad)."""
+    _fields_ = [("mode", C.c_int32), ("z", C.c_void_p), ("acc", C.c_void_p), ("reps", C.c_int32),
+                ("nvox", C.c_int64), ("gamma", C.c_void_p), ("beta", C.c_void_p), ("running_mean", C.c_void_p),
+                ("running_var", C.c_void_p), ("num_batches_tracked", C.c_void_p), ("momentum", C.c_float),
+                ("eps", C.c_float), ("scale_shift", C.c_void_p), ("mean_invstd", C.c_void_p), ("dgamma", C.c_void_p),
+                ("dbeta", C.c_void_p), ("accumulate", C.c_int32), ("act", C.c_int32), ("slope", C.c_float),
+                ("out_bf16", C.c_void_p), ("zero", C.c_void_p), ("zero_n", C.c_int32)]
+
+
 class Epilogue(C.Structure):
     _fields_ = [("bias", C.c_void_p), ("residual", C.c_void_p), ("mask_src", C.c_void_p),
                 ("minuend", C.c_void_p), ("out2", C.c_void_p), ("stats", C.c_void_p),
@@ -77,7 +88,7 @@ class Epilogue(C.Structure):
                 ("bn_part", C.c_void_p), ("bn_mode", C.c_int32), ("bn_slots", C.c_int32), ("bn_z", C.c_void_p),
                 ("bn_ss", C.c_void_p), ("bn_mi", C.c_void_p), ("bn_act", C.c_int32), ("bn_slope", C.c_float),
                 ("x_bf16", C.c_void_p), ("bn_fold", C.c_int32), ("fuse", C.POINTER(BnFuse)),
-                ("out_bf16", C.c_int32), ("split_ws", C.c_void_p)]
+                ("out_bf16", C.c_int32), ("pre", C.POINTER(BnPre))]
 
 
 _P, _I32, _I64, _F = C.c_void_p, C.c_int32, C.c_int64, C.c_float
@@ -97,6 +108,7 @@ _SIGS = {
     "cgan3d_conv3d_shadow_only": ([_P, _I32], _I32),
     "cgan3d_conv3d_bn_fold_ok": ([_P], _I32),
     "cgan3d_bn_fuse_ok": ([_P], _I32),
+    "cgan3d_conv3d_bn_pre_ok": ([_P], _I32),
     "cgan3d_conv3d_neg_dtanh_ok": ([_P], _I32),
     "cgan3d_conv3d_cin1t": ([_P], _I32),
     "cgan3d_conv3d_sumsq_blocks": ([_P], _I64),
@@ -131,7 +143,6 @@ _SIGS = {
     "cgan3d_reflect_fold2d": ([_P, _P, _I32, _I32, _I32, _I32, _I32, _P, _P], _I32),
     "cgan3d_gp_interpolate": ([_P, _P, _P, _P, _I32, _I64, _P], _I32),
     "cgan3d_gp_interpolate_idx": ([_P, _P, _P, _P, _P, _I32, _I64, _P], _I32),
-    "cgan3d_conv3d_split_ws_floats": ([_P], _I64),
     "cgan3d_conv3d_wgrad_sk_ok": ([_P], _I32),
     "cgan3d_conv3d_wgrad_partials": ([_P], _I32),
     "cgan3d_wgrad_reduce_multi": ([_P, _I32, _P], _I32),

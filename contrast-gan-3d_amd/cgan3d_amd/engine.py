@@ -48,11 +48,12 @@ Dims = Tuple[int, int, int]
 #                              (cross-stream event records with the system-scope fence, csrc/plan.hip),
 #                              fp32_store (the 64^3 16-channel z / dy in fp32 instead of bf16),
 #                              event_record (a marker event per cross-stream wait instead of the
-#                              waited-on launch's own completion event, csrc/plan.hip), no_split (the
-#                              critic's 32 -> 64 layer without split-K, conv_sk.hip), own_streams (a new
+#                              waited-on launch's own completion event, csrc/plan.hip), own_streams (a new
 #                              side / communication stream per plan instead of ops.pooled_stream),
 #                              no_wgrad_sk (the critic's middle-layer weight grads on the generic kernel),
-#                              no_defer_reduce (one partial-reduce launch per ResNet weight grad)
+#                              no_defer_reduce (one partial-reduce launch per ResNet weight grad),
+#                              bn_pre (opt-in: the ResNet chain's BatchNorm passes folded into the next
+#                              conv's staging, cgan3d_bn_pre — measured slower)
 #   CGAN3D_FORCE_DP=1          the data-parallel path over a one-rank group (tools / tests)
 #   CGAN3D_COMM=native|torch|own   data-parallel collectives: RCCL from the launch plan on the process
 #                              group's communicator (default), torch.distributed host callables (the
@@ -61,7 +62,7 @@ Dims = Tuple[int, int, int]
 #   CGAN3D_TUNE, CGAN3D_LIB_PATH   launch-shape knobs, another build of the library (_lib.py)
 #   CGAN3D_TRAINER_PLANS=0     the drop-in Trainer issues every step eagerly (no recorded plans)
 DEBUG_FLAGS = ("no_shadow", "keep_fp32", "no_bn_fuse", "no_bn_fold", "serial", "system_fence", "fp32_store",
-               "event_record", "no_split", "own_streams", "no_wgrad_sk", "no_defer_reduce")
+               "event_record", "own_streams", "no_wgrad_sk", "no_defer_reduce", "bn_pre")
 
 
 def debug(flag: str) -> bool:
@@ -369,6 +370,22 @@ class GeneratorPlan:
         self.dys = [bf(ly.dout, ly.cout) if f and j < nl - 1 else d
                     for j, (ly, f, d) in enumerate(zip(layers, self.z16, self.dy))]
         self.dpads = bf(pd, la.cin) if self.z16[-1] else self.dpad
+        # The ResNet chain's BatchNorm passes folded into the next conv (round 5, cgan3d_bn_pre): layer
+        # j's forward pass (no residual) into layer j + 1's ResNet-block forward, which stages z_j and
+        # writes the activation's bf16 shadow; layer j's backward pass into its own input-grad conv,
+        # which stages dL/dy_j and writes dL/dz_j's shadow for the weight grad.  Needs bf16 z / dy
+        # storage, shadow-only consumers of the fp32 tensors and the ResNet-block kernel.  Off by
+        # default: the folded convs measured 17-22 us against 10.4-12.7 us plus a 5-6 us pass, 1.423 vs
+        # 1.381 ms/step (CGAN3D_DEBUG=bn_pre turns it on).
+        self.pre_f, self.pre_b = [False] * nl, [False] * nl
+        if debug("bn_pre"):
+            for j in range(nl):
+                self.pre_f[j] = bool(j + 1 < nl and self.ac_f[j] and self.z16[j] and not layers[j].residual
+                                     and self.y16[j] is not None and self.y_dead[j]
+                                     and ops.bn_pre_ok(self.geo_fwd[j + 1]))
+                self.pre_b[j] = bool(j > 0 and self.ac_b[j] and self.z16[j] and j < nl - 1
+                                     and self.dz16[j] is not None and self.dz_dead[j]
+                                     and ops.bn_pre_ok(self.geo_dgrad[j]))
         # weight gradients run on a side stream, beside the input-gradient chain (each wgrad only
         # needs its layer's dz and input, both final when it is enqueued); own workspace
         wsw = max([ops.wgrad_ws_floats(gw) for gw in self.geo_wgrad] + [ops.wgrad_ws_floats(self.geo_last_wgrad)])
@@ -423,8 +440,12 @@ class GeneratorPlan:
                     ep = ops.epilogue(x_bf16=h16, fuse=ops.BnFuse(self.acc_f[i], 3, FUSE_REPS))
                 else:
                     ep = ops.epilogue(bn_part=self.part_f[i], bn_mode=1, bn_slots=self.slots_f[i], x_bf16=h16)
+                if i > 0 and self.pre_f[i - 1]:  # the previous layer's BatchNorm applied while staging
+                    ep.x_bf16, ep.pre = self.zs[i - 1], self._pre_fwd(P, i - 1)
                 ops.conv(self.geo_fwd[i], h, self.wf[i], self.zs[i], ep)
-                if self.ac_f[i]:
+                if self.pre_f[i]:
+                    pass  # applied by layer i + 1's conv
+                elif self.ac_f[i]:
                     ops.bn_apply_acc(self.acc_f[i], FUSE_REPS, ly.cout, nvox, P[f"{nb}.weight"], P[f"{nb}.bias"],
                                      P[f"{nb}.running_mean"], P[f"{nb}.running_var"], P[f"{nb}.num_batches_tracked"],
                                      self.ss[i], self.mi[i], self.zs[i], ly.act, None if self.y_dead[i] else self.y[i],
@@ -444,6 +465,22 @@ class GeneratorPlan:
                           minuend=x if opt_hat_out is not None else None, out2=opt_hat_out, x_bf16=self.y16[-1])
         ops.conv(self.geo_last_fwd, h, P["model.last_conv.weight"], self.att, ep)
         return self.att
+
+    def _pre_fwd(self, P, j):
+        """Layer j's BatchNorm (+ act) in the next conv's staging (cgan3d_bn_pre mode 1)."""
+        ly, nb = self.layers[j], f"{self.layers[j].name}.normalization"
+        return ops.BnPre.forward(self.acc_f[j], FUSE_REPS, ly.cout, self.n * ly.dout[0] * ly.dout[1] * ly.dout[2],
+                                 P[f"{nb}.weight"], P[f"{nb}.bias"], P[f"{nb}.running_mean"], P[f"{nb}.running_var"],
+                                 P[f"{nb}.num_batches_tracked"], self.ss[j], self.mi[j], ly.act, self.y16[j],
+                                 zero=self.acc_zero_f[j])
+
+    def _pre_bwd(self, P, G, j):
+        """Layer j's BatchNorm backward in its input-grad conv's staging (cgan3d_bn_pre mode 2)."""
+        ly, nb = self.layers[j], f"{self.layers[j].name}.normalization"
+        return ops.BnPre.backward(self.zs[j], self.acc_b[j], FUSE_REPS, ly.cout,
+                                  self.n * ly.dout[0] * ly.dout[1] * ly.dout[2], self.ss[j], self.mi[j],
+                                  P[f"{nb}.weight"], ly.act, G[f"{nb}.weight"], G[f"{nb}.bias"], self.dz16[j],
+                                  zero=self.acc_zero_b[j])
 
     def _bn_grad_epi(self, i, fused: bool = False):
         """Epilogue that accumulates BatchNorm layer i's backward statistics from its dL/dy (into
@@ -543,7 +580,9 @@ class GeneratorPlan:
             ly = self.layers[i]
             nb = f"{ly.name}.normalization"
             nvox = n * ly.dout[0] * ly.dout[1] * ly.dout[2]
-            if self.ac_b[i] and self.fold_bn and i == len(self.layers) - 1:
+            if self.pre_b[i]:  # BatchNorm backward in this layer's input-grad (its wgrad reads dz16 after it)
+                self._input_grad(P, G, i)
+            elif self.ac_b[i] and self.fold_bn and i == len(self.layers) - 1:
                 ops.bn_backward_acc_fold(self.dpads, self.zs[i], n, ly.dout, ly.cout, la.p, self.acc_b[i], FUSE_REPS,
                                          self.ss[i], self.mi[i], P[f"{nb}.weight"], ly.act, G[f"{nb}.weight"],
                                          G[f"{nb}.bias"], None if self.dz_dead[i] else self.dz[i], dz16=self.dz16[i],
@@ -601,7 +640,8 @@ class GeneratorPlan:
                 flush()
             if i == 0:
                 break
-            self._input_grad(P, G, i)
+            if not self.pre_b[i]:
+                self._input_grad(P, G, i)
             if i == self.wgrad_tail_main and side_after is not None and self.side is not None:
                 # every gradient of layers >= i must be enqueued (side: weight grads; main: BatchNorm
                 # grads) and their weights' last reader, this input-grad, too: the caller's launches
@@ -627,6 +667,8 @@ class GeneratorPlan:
         ep = self._bn_grad_epi(i - 1, fused=self.ac_b[i - 1])
         ep.residual = self.dys[i + 1] if ly.name.endswith("block0") else None  # bf16 when layer i + 1 keeps it
         ep.x_bf16 = self.dz16[i] if BN_FUSED_BWD else None  # only the slab backward writes it
+        if self.pre_b[i]:  # stages dL/dy_i, maps it to dL/dz_i (and writes dz16[i]) on the way
+            ep.x_bf16, ep.pre = self.dys[i], self._pre_bwd(P, G, i)
         ops.conv(self.geo_dgrad[i], self.dz[i], self.wd[i], self.dys[i - 1], ep)
 
 
@@ -763,18 +805,6 @@ class CriticPlan:
             if self.is_bn[i]:
                 gs = self._geo(ops.conv_fwd_geom(nmax, ly.din, ly.dout, ly.cin, ly.cout, ly.k, ly.s, ly.p, planar=self.pl), self.wf[i])
                 self.stats[i] = torch.empty(ops.stats_floats(gs), device=device)
-        # all-zero workspace of the split-K forward launches (conv_sk with few row tiles and a long K:
-        # the 32 -> 64 layer), shared by every forward-style launch of this plan — they run in turn on
-        # one stream and each leaves it zeroed; sized for any batch up to nmax
-        nsw = 0
-        for i, ly in enumerate(ls):
-            if self.wf[i] is None or self.is_bn[i]:
-                continue
-            for nb in range(1, nmax + 1):
-                gs = self._geo(ops.conv_fwd_geom(nb, ly.din, ly.dout, ly.cin, ly.cout, ly.k, ly.s, ly.p, planar=self.pl),
-                               self.wf[i])
-                nsw = max(nsw, ops.split_ws_floats(gs))
-        self.split_ws = torch.zeros(nsw, device=device) if nsw and not debug("no_split") else None
         self.pack()
 
     def pack(self):
@@ -819,7 +849,7 @@ class CriticPlan:
             else:
                 last = i == len(self.layers) - 1
                 ep = ops.epilogue(bias=P[f"{ly.name}.bias"], act=L.ACT_NONE if last else L.ACT_LRELU,
-                                  slope=self.slope, split_ws=self.split_ws)
+                                  slope=self.slope)
                 ops.conv(g, h, w, out, ep)
             h = out
         return self._sl(self.a[-1], off, n)
@@ -878,7 +908,7 @@ class CriticPlan:
             g = self._geo(ops.conv_fwd_geom(n, ly.din, ly.dout, ly.cin, ly.cout, ly.k, ly.s, ly.p, planar=self.pl), self.wf[i])
             out = self._sl(self.a[i], off, n)
             w = self.wf[i] if self.wf[i] is not None else P[f"{ly.name}.weight"]
-            ops.conv(g, h, w, out, ops.epilogue(mask_src=out, slope=self.slope, split_ws=self.split_ws))
+            ops.conv(g, h, w, out, ops.epilogue(mask_src=out, slope=self.slope))
             h = out
 
     def _on_side(self, fn):
@@ -996,7 +1026,7 @@ class CriticPlan:
             g = self._geo(ops.conv_fwd_geom(n, ly.din, ly.dout, ly.cin, ly.cout, ly.k, ly.s, ly.p, planar=self.pl), self.wf[i])
             out = self._sl(self.a[i], off, n)
             w = self.wf[i] if self.wf[i] is not None else P[f"{ly.name}.weight"]
-            ops.conv(g, h, w, out, ops.epilogue(mask_src=out, slope=self.slope, split_ws=self.split_ws))
+            ops.conv(g, h, w, out, ops.epilogue(mask_src=out, slope=self.slope))
             h = out
             if self.side is None and zeroed and ops.wgrad_sk_ok(self._wgrad_geo(i + 1, n_all)) and not debug("no_wgrad_sk"):
                 skl.append(i + 1)

@@ -224,9 +224,69 @@ def neg_dtanh_ok(g) -> bool:
     return bool(L.load().cgan3d_conv3d_neg_dtanh_ok(ctypes.byref(g)))
 
 
+def bn_pre_ok(g: ConvGeom) -> bool:
+    """The launch of ``g`` can apply its input's BatchNorm while staging (cgan3d_conv3d_bn_pre_ok)."""
+    return bool(L.load().cgan3d_conv3d_bn_pre_ok(ctypes.byref(g)))
+
+
 def bn_fuse_ok(g) -> bool:
     """True if the launch of ``g`` can produce BnFuse accumulators."""
     return bool(L.load().cgan3d_bn_fuse_ok(ctypes.byref(g)))
+
+
+class BnPre:
+    """The conv input's BatchNorm applied while the ResNet-block kernel stages its halo
+    (include/cgan3d.h cgan3d_bn_pre, round 5): ``forward`` (mode 1: the launch's x_bf16 is the previous
+    layer's bf16 z) or ``backward`` (mode 2: x_bf16 is the layer's bf16 dL/dy).  Tensors are kept for
+    the checks and for the struct's lifetime."""
+
+    def __init__(self, mode, c, nvox, acc, reps, gamma, scale_shift, mean_invstd, act, out16, slope=0.0, zero=None,
+                 z=None, beta=None, rmean=None, rvar=None, nbt=None, momentum=0.1, eps=1e-5, dgamma=None, dbeta=None,
+                 accumulate=False):
+        self.mode, self.c, self.nvox, self.reps = int(mode), int(c), int(nvox), int(reps)
+        self.acc, self.gamma, self.ss, self.mi, self.act, self.out16 = acc, gamma, scale_shift, mean_invstd, act, out16
+        self.slope, self.zero, self.z, self.beta = float(slope), zero, z, beta
+        self.rmean, self.rvar, self.nbt, self.momentum, self.eps = rmean, rvar, nbt, float(momentum), float(eps)
+        self.dgamma, self.dbeta, self.accumulate = dgamma, dbeta, bool(accumulate)
+
+    @classmethod
+    def forward(cls, acc, reps, c, nvox, gamma, beta, rmean, rvar, nbt, scale_shift, mean_invstd, act, out16,
+                slope=0.0, zero=None, momentum=0.1, eps=1e-5):
+        return cls(1, c, nvox, acc, reps, gamma, scale_shift, mean_invstd, act, out16, slope, zero, beta=beta,
+                   rmean=rmean, rvar=rvar, nbt=nbt, momentum=momentum, eps=eps)
+
+    @classmethod
+    def backward(cls, z, acc, reps, c, nvox, scale_shift, mean_invstd, gamma, act, dgamma, dbeta, out16, slope=0.0,
+                 accumulate=False, zero=None):
+        return cls(2, c, nvox, acc, reps, gamma, scale_shift, mean_invstd, act, out16, slope, zero, z=z,
+                   dgamma=dgamma, dbeta=dbeta, accumulate=accumulate)
+
+    def check(self, g, x16):
+        if not int(L.load().cgan3d_conv3d_bn_pre_ok(ctypes.byref(g))):
+            raise ValueError("conv: BatchNorm prologue (pre) only on the ResNet-block kernel")
+        n = self.nvox * self.c
+        _need(x16, n, "conv pre x_bf16", dtype=torch.bfloat16)
+        _need(self.out16, n, "conv pre out16", dtype=torch.bfloat16)
+        _need(self.acc, self.reps * 2 * self.c, "conv pre acc", dtype=torch.float64, exact=False)
+        for t, nm in ((self.gamma, "gamma"),) + (((self.beta, "beta"),) if self.mode == 1 else
+                                                 ((self.dgamma, "dgamma"), (self.dbeta, "dbeta"))):
+            _need(t, self.c, f"conv pre {nm}")
+        for t, nm in ((self.ss, "scale_shift"), (self.mi, "mean_invstd")):
+            _need(t, 2 * self.c, f"conv pre {nm}")
+        if self.mode == 2:
+            _need(self.z, n, "conv pre z", dtype=torch.bfloat16)
+        if self.zero is not None:
+            _need(self.zero, self.zero.numel(), "conv pre zero", dtype=torch.float64)
+
+    def c_struct(self) -> "L.BnPre":
+        p = L.BnPre()
+        p.mode, p.z, p.acc, p.reps, p.nvox = self.mode, ptr(self.z), ptr(self.acc), self.reps, self.nvox
+        p.gamma, p.beta, p.running_mean, p.running_var = ptr(self.gamma), ptr(self.beta), ptr(self.rmean), ptr(self.rvar)
+        p.num_batches_tracked, p.momentum, p.eps = ptr(self.nbt), self.momentum, self.eps
+        p.scale_shift, p.mean_invstd, p.dgamma, p.dbeta = ptr(self.ss), ptr(self.mi), ptr(self.dgamma), ptr(self.dbeta)
+        p.accumulate, p.act, p.slope, p.out_bf16 = int(self.accumulate), int(self.act), self.slope, ptr(self.out16)
+        p.zero, p.zero_n = ptr(self.zero), self.zero.numel() if self.zero is not None else 0
+        return p
 
 
 class Epi:
@@ -234,10 +294,9 @@ class Epi:
 
     def __init__(self, bias=None, residual=None, mask_src=None, minuend=None, out2=None, stats=None,
                  act=L.ACT_NONE, slope=0.0, bn_part=None, bn_mode=0, bn_slots=0, bn_z=None, bn_ss=None,
-                 bn_mi=None, bn_act=L.ACT_NONE, bn_slope=0.0, x_bf16=None, bn_fold=0, fuse=None, split_ws=None):
+                 bn_mi=None, bn_act=L.ACT_NONE, bn_slope=0.0, x_bf16=None, bn_fold=0, fuse=None, pre=None):
         self.fuse = fuse  # BnFuse or None
-        # all-zero fp32 workspace a split-K launch may use (include/cgan3d.h split_ws), or None
-        self.split_ws = split_ws
+        self.pre = pre  # BnPre or None: the input's BatchNorm applied while staging (conv_k3m)
         self.bias, self.residual, self.mask_src = bias, residual, mask_src
         self.x_bf16 = x_bf16  # bf16 copy of the conv input (ResNet-block kernel halo source)
         self.minuend, self.out2, self.stats = minuend, out2, stats
@@ -268,9 +327,10 @@ class Epi:
         e.x_bf16 = ptr(self.x_bf16)
         e.bn_fold = self.bn_fold
         e.out_bf16 = self.out_bf16
-        e.split_ws = ptr(self.split_ws)
         if self.fuse is not None:
             e.fuse = ctypes.pointer(self.fuse.c())  # the pointer object keeps the struct alive
+        if self.pre is not None:
+            e.pre = ctypes.pointer(self.pre.c_struct())
         return e
 
 
@@ -559,12 +619,6 @@ def conv(g: ConvGeom, x: torch.Tensor, w: torch.Tensor, y: torch.Tensor, ep: Opt
             _need(ep.stats, sumsq_blocks(g) or stats_floats(g), "conv stats", exact=False)
         if ep.x_bf16 is not None:
             _need(ep.x_bf16, _vox_in(g) * g.cin, "conv x_bf16", dtype=torch.bfloat16)
-        if ep.split_ws is not None:
-            nsw = split_ws_floats(g)
-            if nsw == 0:
-                ep.split_ws = None  # this launch does not split: the workspace is not passed
-            else:
-                _need(ep.split_ws, nsw, "conv split_ws", exact=False)
         f = ep.bn_fold
         nz = None if not f else g.n * (g.do_ - 2 * f) * (g.ho - 2 * f) * (g.wo - 2 * f) * g.cout
         ep.check_bn(ny, g.cout, "conv", nz)
@@ -574,13 +628,10 @@ def conv(g: ConvGeom, x: torch.Tensor, w: torch.Tensor, y: torch.Tensor, ep: Opt
                 _need(ep.bn_z, ny if nz is None else nz, "conv bn_z", dtype=y.dtype)
         elif out16 and ep.bn_z is not None:
             raise ValueError("conv: a bf16 output takes accumulator statistics only")
+        if ep.pre is not None:
+            ep.pre.check(g, ep.x_bf16)
     check(_timed("conv", g, "cgan3d_conv3d_fwd", ctypes.byref(g), ptr(x), ptr(w), ptr(y),
                  ctypes.byref(ep.c()) if ep is not None else None), "conv3d_fwd")
-
-
-def split_ws_floats(g: ConvGeom) -> int:
-    """Floats of the all-zero split-K workspace a launch of ``g`` uses (0: it does not split)."""
-    return int(L.load().cgan3d_conv3d_split_ws_floats(ctypes.byref(g)))
 
 
 def wgrad_ws_floats(g: ConvGeom) -> int:

@@ -9,7 +9,7 @@
 // partials (conv.hip) combined here with Chan's formula in fp64, so the activation tensor is not
 // re-read for statistics.  Backward is a two-pass reduction (sum dy, sum dy*xhat per channel,
 // per-block partials -> fp64 combine) followed by one elementwise pass.
-#include "common.h"
+#include "bn_acc.h"
 
 namespace cg {
 
@@ -66,12 +66,6 @@ __global__ __launch_bounds__(256) void bn_finalize_kernel(const float* __restric
     if (rvar) rvar[c] = (float)((1.0 - momentum) * rvar[c] + momentum * var * N / (N > 1 ? N - 1 : 1));
     if (nbt && c == 0) *nbt += 1;
   }
-}
-
-__device__ __forceinline__ float act_f(float v, int act, float slope) {
-  if (act == CGAN3D_ACT_RELU) return fmaxf(v, 0.f);
-  if (act == CGAN3D_ACT_LRELU) return v > 0.f ? v : v * slope;
-  return v;
 }
 
 // optional bf16 shadow of an output (read by the ResNet-block conv's halo staging)
@@ -198,6 +192,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const float* __restri
     sc[e] = ss[c + e]; sf[e] = ss[C + c + e]; mean[e] = mi[c + e]; inv[e] = mi[C + c + e];
     k0[e] = coef[c + e]; k1[e] = coef[C + c + e]; k2[e] = coef[2 * C + c + e];
   }
+
   const f32x4* z4 = reinterpret_cast<const f32x4*>(z);
   const f32x4* d4 = reinterpret_cast<const f32x4*>(dy);
   f32x4* o4 = reinterpret_cast<f32x4*>(dz);
@@ -205,11 +200,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const float* __restri
     const f32x4 zz = z4[i], dd = d4[i];
     f32x4 o;
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const float g = dd[e] * act_grad(zz[e] * sc[e] + sf[e], act, slope);
-      const float xh = (zz[e] - mean[e]) * inv[e];
-      o[e] = k0[e] * (g - k1[e] - xh * k2[e]);
-    }
+    for (int e = 0; e < 4; ++e) o[e] = bn_bwd_map(dd[e], zz[e], sc[e], sf[e], mean[e], inv[e], k0[e], k1[e], k2[e], act, slope);
     if (dz) o4[i] = o;
     if (dz16) store16(dz16, i, o);
   }
@@ -221,8 +212,6 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const float* __restri
 struct NoPrefetch {
   __device__ void operator()() const {}
 };
-template <class F>
-__device__ __forceinline__ void acc_sums(const double* __restrict__ acc, int reps, int C, double* sums, F&& prefetch);
 
 // coef == NULL: the coefficients from fp64 accumulators (cgan3d_bn_backward_acc_fold): every block
 // combines the replicas, block 0 publishes dgamma / dbeta and zeroes `zero`
@@ -236,23 +225,17 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_fold_kernel(const void* __re
                                                                 int reps, double nvox, const float* __restrict__ gamma,
                                                                 float* dgamma, float* dbeta, int accumulate,
                                                                 double* zero, int zero_n) {
-  __shared__ double sums[2 * 256];
+  __shared__ double sums[2 * 256], part[256];
   __shared__ float co[3 * 256];
   if (!coef) {
     const int tid = threadIdx.x;
     if (blockIdx.x == 0)
       for (int j = tid; j < zero_n; j += blockDim.x) zero[j] = 0.0;
-    acc_sums(acc, reps, C, sums, NoPrefetch());
+    acc_sums(acc, reps, C, sums, part, NoPrefetch());
     __syncthreads();
-    for (int c = tid; c < C; c += blockDim.x) {
-      co[c] = gamma[c] * mi[C + c];
-      co[C + c] = (float)(sums[c] / nvox);
-      co[2 * C + c] = (float)(sums[C + c] / nvox);
-      if (blockIdx.x == 0) {
-        if (dbeta) dbeta[c] = accumulate ? dbeta[c] + (float)sums[c] : (float)sums[c];
-        if (dgamma) dgamma[c] = accumulate ? dgamma[c] + (float)sums[C + c] : (float)sums[C + c];
-      }
-    }
+    for (int c = tid; c < C; c += blockDim.x)
+      bn_acc_bwd_coeffs(sums, c, C, nvox, gamma, mi, &co[c], &co[C + c], &co[2 * C + c], blockIdx.x == 0, dgamma,
+                        dbeta, accumulate);
     __syncthreads();
     coef = co;
   }
@@ -264,6 +247,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_fold_kernel(const void* __re
     sc[e] = ss[c + e]; sf[e] = ss[C + c + e]; mean[e] = mi[c + e]; inv[e] = mi[C + c + e];
     k0[e] = coef[c + e]; k1[e] = coef[C + c + e]; k2[e] = coef[2 * C + c + e];
   }
+
   const int Dp = D + 2 * P, Hp = H + 2 * P, Wp = W + 2 * P;
   const long long n4 = (long long)n * D * H * W * C4;
   f32x4* o4 = reinterpret_cast<f32x4*>(dz);
@@ -287,11 +271,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_fold_kernel(const void* __re
     }
     f32x4 o;
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const float g = dd[e] * act_grad(zz[e] * sc[e] + sf[e], act, slope);
-      const float xh = (zz[e] - mean[e]) * inv[e];
-      o[e] = k0[e] * (g - k1[e] - xh * k2[e]);
-    }
+    for (int e = 0; e < 4; ++e) o[e] = bn_bwd_map(dd[e], zz[e], sc[e], sf[e], mean[e], inv[e], k0[e], k1[e], k2[e], act, slope);
     if (dz) o4[i] = o;
     if (dz16) store16(dz16, i, o);
   }
@@ -585,6 +565,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_slab_kernel(const float* __r
     sc[e] = ss[cc + e]; sf[e] = ss[C + cc + e]; mean[e] = mi[cc + e]; inv[e] = mi[C + cc + e];
     k0[e] = co[cc + e]; k1[e] = co[C + cc + e]; k2[e] = co[2 * C + cc + e];
   }
+
   const f32x4* z4 = reinterpret_cast<const f32x4*>(z);
   const f32x4* d4 = reinterpret_cast<const f32x4*>(dy);
   f32x4* o4 = reinterpret_cast<f32x4*>(dz);
@@ -592,11 +573,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_slab_kernel(const float* __r
     const f32x4 zz = z4[i], dd = d4[i];
     f32x4 o;
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const float g = dd[e] * act_grad(zz[e] * sc[e] + sf[e], act, slope);
-      const float xh = (zz[e] - mean[e]) * inv[e];
-      o[e] = k0[e] * (g - k1[e] - xh * k2[e]);
-    }
+    for (int e = 0; e < 4; ++e) o[e] = bn_bwd_map(dd[e], zz[e], sc[e], sf[e], mean[e], inv[e], k0[e], k1[e], k2[e], act, slope);
     if (dz) o4[i] = o;
     if (dz16) store16(dz16, i, o);
   }
@@ -607,45 +584,6 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_slab_kernel(const float* __r
 // block combines the replicas itself (16 KB at reps 16, C 64: all loads in flight), block 0 publishes
 // statistics / running buffers / parameter gradients and zeroes an accumulator the stream is done
 // with (the caller rotates them, so none needs a memset launch).
-template <class F>
-__device__ __forceinline__ void acc_sums(const double* __restrict__ acc, int reps, int C, double* sums,
-                                         F&& prefetch) {
-  // sums[q * C + c] = sum over replicas of acc[(r * 2 + q) * C + c]: the 256 threads split the pairs
-  // (j = q * C + c, 2C <= 128 of them) and the replicas (T = 256 / 2C threads per pair), eight loads
-  // in flight per thread — one round trip for reps <= 8T (the atomics left the values at the memory
-  // side: each round trip is long) — then the T partial sums of a pair are added through LDS.
-  // `prefetch` runs between issuing the first round of loads and using them: the elementwise pass
-  // issues its first loads there, so the two round trips overlap instead of adding up
-  __shared__ double part[256];
-  const int tid = threadIdx.x, P = 2 * C, T = 256 / P, j = tid % P, h = tid / P;
-  // unconditional loads (clamped replica, value masked after): a load under a branch gets its own
-  // wait before the branch joins, which serialised the first round trip
-  double v[8];
-#pragma unroll
-  for (int u = 0; u < 8; ++u) v[u] = acc[(long long)min(h + u * T, reps - 1) * P + j];
-  prefetch();
-  __builtin_amdgcn_sched_barrier(0);  // keep the sums below every load issued above
-  double s = 0.0;
-#pragma unroll
-  for (int u = 0; u < 8; ++u) s += h + u * T < reps ? v[u] : 0.0;
-  for (int r0 = h + 8 * T; r0 < reps; r0 += 8 * T) {
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int r = r0 + u * T;
-      v[u] = r < reps ? acc[(long long)r * P + j] : 0.0;
-    }
-#pragma unroll
-    for (int u = 0; u < 8; ++u) s += v[u];
-  }
-  part[tid] = s;
-  lds_barrier();
-  if (tid < P) {
-    double t = 0.0;
-    for (int k = 0; k < T; ++k) t += part[k * P + tid];
-    sums[tid] = t;
-  }
-}
-
 // float4 per thread loaded before the statistics are known (acc_pass_blocks sizes the grid at ~2)
 constexpr int ACC_PF = 2;
 
@@ -659,7 +597,7 @@ __global__ __launch_bounds__(256) void bn_apply_acc_kernel(const double* __restr
                                                            float slope, const float* __restrict__ res,
                                                            float* __restrict__ y, __bf16* __restrict__ y16,
                                                            double* zero, int zero_n) {
-  __shared__ double sums[2 * 256];
+  __shared__ double sums[2 * 256], part[256];
   __shared__ float ssh[2 * 256];
   const int tid = threadIdx.x;
   if (blockIdx.x == 0)
@@ -668,7 +606,7 @@ __global__ __launch_bounds__(256) void bn_apply_acc_kernel(const double* __restr
   const f32x4* r4 = reinterpret_cast<const f32x4*>(res);
   const long long i0 = (long long)blockIdx.x * blockDim.x + tid, stride = (long long)gridDim.x * blockDim.x;
   f32x4 zp[ACC_PF], rp[ACC_PF];
-  acc_sums(acc, reps, C, sums, [&] {
+  acc_sums(acc, reps, C, sums, part, [&] {
 #pragma unroll
     for (int u = 0; u < ACC_PF; ++u) {
       const long long i = min(i0 + u * stride, n4 - 1);
@@ -677,22 +615,9 @@ __global__ __launch_bounds__(256) void bn_apply_acc_kernel(const double* __restr
     }
   });
   lds_barrier();
-  for (int c = tid; c < C; c += blockDim.x) {
-    const double mean = sums[c] / nvox, var = fmax(sums[C + c] / nvox - mean * mean, 0.0);
-    const double invstd = 1.0 / sqrt(var + (double)eps);
-    const double sc = (double)gamma[c] * invstd;
-    ssh[c] = (float)sc;
-    ssh[C + c] = (float)((double)beta[c] - mean * sc);
-    if (blockIdx.x == 0) {
-      scale_shift[c] = ssh[c];
-      scale_shift[C + c] = ssh[C + c];
-      mean_invstd[c] = (float)mean;
-      mean_invstd[C + c] = (float)invstd;
-      if (rmean) rmean[c] = (float)((1.0 - momentum) * rmean[c] + momentum * mean);
-      if (rvar) rvar[c] = (float)((1.0 - momentum) * rvar[c] + momentum * var * nvox / (nvox > 1 ? nvox - 1 : 1));
-      if (nbt && c == 0) *nbt += 1;
-    }
-  }
+  for (int c = tid; c < C; c += blockDim.x)
+    bn_acc_fwd_coeffs(sums, c, C, nvox, gamma, beta, eps, &ssh[c], &ssh[C + c], blockIdx.x == 0, scale_shift,
+                      mean_invstd, rmean, rvar, nbt, momentum);
   lds_barrier();
   const int C4 = C >> 2, cc = (tid % C4) * 4;
   f32x4 sc4, sf4;
@@ -722,14 +647,14 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_acc_kernel(const double* __r
                                                                const float* __restrict__ ss, int act, float slope,
                                                                float* __restrict__ dz, __bf16* __restrict__ dz16,
                                                                double* zero, int zero_n) {
-  __shared__ double sums[2 * 256];
+  __shared__ double sums[2 * 256], part[256];
   __shared__ float co[3 * 256];
   const int tid = threadIdx.x;
   if (blockIdx.x == 0)
     for (int j = tid; j < zero_n; j += blockDim.x) zero[j] = 0.0;
   const long long i0 = (long long)blockIdx.x * blockDim.x + tid, stride = (long long)gridDim.x * blockDim.x;
   f32x4 zp[ACC_PF], dp[ACC_PF];
-  acc_sums(acc, reps, C, sums, [&] {
+  acc_sums(acc, reps, C, sums, part, [&] {
 #pragma unroll
     for (int u = 0; u < ACC_PF; ++u) {
       const long long i = min(i0 + u * stride, n4 - 1);
@@ -738,15 +663,9 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_acc_kernel(const double* __r
     }
   });
   lds_barrier();
-  for (int c = tid; c < C; c += blockDim.x) {
-    co[c] = gamma[c] * mi[C + c];
-    co[C + c] = (float)(sums[c] / nvox);
-    co[2 * C + c] = (float)(sums[C + c] / nvox);
-    if (blockIdx.x == 0) {
-      if (dbeta) dbeta[c] = accumulate ? dbeta[c] + (float)sums[c] : (float)sums[c];
-      if (dgamma) dgamma[c] = accumulate ? dgamma[c] + (float)sums[C + c] : (float)sums[C + c];
-    }
-  }
+  for (int c = tid; c < C; c += blockDim.x)
+    bn_acc_bwd_coeffs(sums, c, C, nvox, gamma, mi, &co[c], &co[C + c], &co[2 * C + c], blockIdx.x == 0, dgamma, dbeta,
+                      accumulate);
   lds_barrier();
   const int C4 = C >> 2, cc = (tid % C4) * 4;
   f32x4 sc, sf, mean, inv, k0, k1, k2;
@@ -755,15 +674,12 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_acc_kernel(const double* __r
     sc[e] = ss[cc + e]; sf[e] = ss[C + cc + e]; mean[e] = mi[cc + e]; inv[e] = mi[C + cc + e];
     k0[e] = co[cc + e]; k1[e] = co[C + cc + e]; k2[e] = co[2 * C + cc + e];
   }
+
   f32x4* o4 = reinterpret_cast<f32x4*>(dz);
   auto apply = [&](long long i, const f32x4& zz, const f32x4& dd) {
     f32x4 o;
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const float g = dd[e] * act_grad(zz[e] * sc[e] + sf[e], act, slope);
-      const float xh = (zz[e] - mean[e]) * inv[e];
-      o[e] = k0[e] * (g - k1[e] - xh * k2[e]);
-    }
+    for (int e = 0; e < 4; ++e) o[e] = bn_bwd_map(dd[e], zz[e], sc[e], sf[e], mean[e], inv[e], k0[e], k1[e], k2[e], act, slope);
     if (dz) o4[i] = o;
     if (dz16) store16(dz16, i, o);
   };

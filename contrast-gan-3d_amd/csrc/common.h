@@ -130,6 +130,31 @@ struct BnFuse {
 };
 
 // device-side view of cgan3d_epilogue
+// cgan3d_bn_pre (include/cgan3d.h), copied by value; mode 0: none
+struct BnPre {
+  int mode;
+  const __bf16* z;
+  const double* acc;
+  int reps;
+  double nvox;
+  const float* gamma;
+  const float* beta;
+  float* rmean;
+  float* rvar;
+  long long* nbt;
+  float momentum, eps;
+  float* ss;
+  float* mi;
+  float* dgamma;
+  float* dbeta;
+  int accumulate;
+  int act;
+  float slope;
+  __bf16* out16;
+  double* zero;
+  int zero_n;
+};
+
 struct Epi {
   const float* bias;
   const float* residual;
@@ -152,7 +177,7 @@ struct Epi {
   BnFuse fz;          // all-zero unless cgan3d_epilogue.fuse is given
   int out16;          // cgan3d_epilogue.out_bf16 bit 0: y and bn_z are bf16 (k7m n2w, S2T, conv_k3m launches)
   int res16;          // bit 1: the residual is bf16 (conv_k3m only)
-  float* split_ws;    // cgan3d_epilogue.split_ws: all-zero workspace of a split-K launch (conv_sk)
+  BnPre pre;          // the input's BatchNorm applied while staging (conv_k3m only)
 };
 
 // c ? v : 0 for a just-loaded v, by an integer mask: the compiler turns a select whose operand is a
@@ -212,8 +237,15 @@ bool wgrad_k3_ok(const cgan3d_conv_geom* g);
 bool sk_format_ok(const cgan3d_conv_geom* g);
 bool sk_ok(const cgan3d_conv_geom* g);
 long long sk_blocks(const cgan3d_conv_geom* g);
-long long sk_split_ws_floats(const cgan3d_conv_geom* g);
-void sk_nsplit_set(int v);
+// Phase probes (timing only, wrong results): kernels skip the phases set in g_probe (cgan3d_set_tuning
+// key 90).  Compiled in only with -DCGAN3D_PROBES (make PROBES=1); the product library has neither
+// the key nor the branches (CG_PROBE is constant false).
+extern int g_probe;
+#ifdef CGAN3D_PROBES
+#define CG_PROBE(p, bit) (((p) & (bit)) != 0)
+#else
+#define CG_PROBE(p, bit) false
+#endif
 int sk_launch(const cgan3d_conv_geom* g, const float* x, const __bf16* wp, float* y, const Epi& e, hipStream_t st);
 // critic first layer, single channel (conv_c1.hip)
 bool c1_fwd_ok(const cgan3d_conv_geom* g);
@@ -245,6 +277,12 @@ bool k3m_ok(const cgan3d_conv_geom* g, const Epi& e);
 bool k3m_geom_ok(const cgan3d_conv_geom* g);
 bool k3m_route(const cgan3d_conv_geom* g);
 int k3m_launch(const cgan3d_conv_geom* g, const __bf16* wp, float* y, const Epi& e, hipStream_t st);
+bool t64_geom_ok(const cgan3d_conv_geom* g);
+bool t64_ok(const cgan3d_conv_geom* g, const Epi& e);
+int t64_launch(const cgan3d_conv_geom* g, const __bf16* wp, float* y, const Epi& e, hipStream_t st);
+bool f64_geom_ok(const cgan3d_conv_geom* g);
+bool f64_ok(const cgan3d_conv_geom* g, const Epi& e);
+int f64_launch(const cgan3d_conv_geom* g, const __bf16* wp, float* y, const Epi& e, hipStream_t st);
 void k3m_set(int v);
 void k7wg_blocks_set(int v);
 bool halo_ok(const cgan3d_conv_geom* g);         // w_packed == 2 and eligible

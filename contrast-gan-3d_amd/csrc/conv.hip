@@ -563,14 +563,39 @@ static Epi to_epi(const cgan3d_epilogue* ep) {
     }
     e.out16 = ep->out_bf16 & 1;
     e.res16 = (ep->out_bf16 >> 1) & 1;
-    e.split_ws = ep->split_ws;
+    if (const cgan3d_bn_pre* p = ep->pre) {
+      BnPre& q = e.pre;
+      q.mode = p->mode; q.z = reinterpret_cast<const __bf16*>(p->z); q.acc = p->acc; q.reps = p->reps;
+      q.nvox = (double)p->nvox; q.gamma = p->gamma; q.beta = p->beta; q.rmean = p->running_mean;
+      q.rvar = p->running_var; q.nbt = (long long*)p->num_batches_tracked; q.momentum = p->momentum; q.eps = p->eps;
+      q.ss = p->scale_shift; q.mi = p->mean_invstd; q.dgamma = p->dgamma; q.dbeta = p->dbeta;
+      q.accumulate = p->accumulate; q.act = p->act; q.slope = p->slope; q.out16 = reinterpret_cast<__bf16*>(p->out_bf16);
+      q.zero = p->zero; q.zero_n = p->zero_n;
+    }
   }
   return e;
 }
 
-extern "C" int64_t cgan3d_conv3d_split_ws_floats(const cgan3d_conv_geom* g) {
-  if (!g || validate(g, "cgan3d_conv3d_split_ws_floats") || g->planar || g->w_packed != 3) return 0;
-  return sk_split_ws_floats(g);
+extern "C" int32_t cgan3d_conv3d_bn_pre_ok(const cgan3d_conv_geom* g) {
+  if (!g || validate(g, "cgan3d_conv3d_bn_pre_ok") || g->planar) return 0;
+  return k3m_route(g) ? 1 : 0;
+}
+
+// the input-BatchNorm prologue (cgan3d_bn_pre): argument checks; routes only to conv_k3m
+static int check_pre(const cgan3d_conv_geom* g, const Epi& e) {
+  const BnPre& p = e.pre;
+  if (!p.mode) return CGAN3D_OK;
+  CG_CHECK_ARG(p.mode == 1 || p.mode == 2, "cgan3d_bn_pre: mode must be 1 or 2");
+  CG_CHECK_ARG(k3m_route(g) && k3m_ok(g, e), "cgan3d_bn_pre: only the ResNet-block kernel (cgan3d_conv3d_bn_pre_ok)");
+  CG_CHECK_ARG((p.mode == 1) == !g->transposed, "cgan3d_bn_pre: mode 1 on the forward, mode 2 on the input-grad");
+  CG_CHECK_ARG(p.acc && p.reps >= 1 && p.reps <= 64 && p.nvox > 1 && p.gamma && p.ss && p.mi && p.out16 &&
+                   (p.zero || !p.zero_n) && p.zero_n >= 0,
+               "cgan3d_bn_pre: acc, reps 1..64, nvox > 1, gamma, scale_shift, mean_invstd, out_bf16 required");
+  CG_CHECK_ARG(p.mode == 2 || p.beta, "cgan3d_bn_pre: mode 1 needs beta");
+  CG_CHECK_ARG(p.mode == 1 || p.z, "cgan3d_bn_pre: mode 2 needs z");
+  CG_CHECK_ARG(p.act == CGAN3D_ACT_NONE || p.act == CGAN3D_ACT_RELU || p.act == CGAN3D_ACT_LRELU,
+               "cgan3d_bn_pre: act none, relu or leaky relu");
+  return CGAN3D_OK;
 }
 
 // the launches that honour cgan3d_epilogue.out_bf16 (their dispatch conditions: the S2T kernel from
@@ -578,7 +603,7 @@ extern "C" int64_t cgan3d_conv3d_split_ws_floats(const cgan3d_conv_geom* g) {
 extern "C" int32_t cgan3d_conv3d_out_bf16_ok(const cgan3d_conv_geom* g) {
   if (!g || validate(g, "cgan3d_conv3d_out_bf16_ok") || g->planar) return 0;
   if (g->w_packed == 2 && s2_kind(g) == 2) return 1;
-  if (k3m_route(g)) return 1;
+  if (k3m_route(g) || t64_geom_ok(g) || f64_geom_ok(g)) return 1;
   return g->w_packed == 0 && k7m_n2w_ok(g) ? 1 : 0;
 }
 
@@ -636,6 +661,7 @@ extern "C" int cgan3d_conv3d_fwd(const cgan3d_conv_geom* g, const float* x, cons
   CG_CHECK_ARG(x && w && y, "cgan3d_conv3d_fwd: null pointer");
   Epi e = to_epi(ep);
   if (int rc = check_fuse(g, e)) return rc;
+  if (int rc = check_pre(g, e)) return rc;
   CG_CHECK_ARG(!ep || (ep->out_bf16 >= 0 && ep->out_bf16 <= 3), "cgan3d_conv3d_fwd: out_bf16 must be 0..3");
   CG_CHECK_ARG(!(e.out16 || e.res16) || cgan3d_conv3d_out_bf16_ok(g),
                "cgan3d_conv3d_fwd: out_bf16 not taken by this launch");
@@ -789,8 +815,9 @@ extern "C" int32_t cgan3d_conv3d_bn_fold_ok(const cgan3d_conv_geom* g) {
 
 extern "C" int32_t cgan3d_conv3d_shadow_only(const cgan3d_conv_geom* g, int32_t role) {
   if (!g || validate(g, "cgan3d_conv3d_shadow_only") || g->planar) return 0;
-  if (role == 0)  // stride-2 16 <-> 32 kernels (conv_s2.hip), the 16 -> 1 k7 forward (conv_k7_mfma.hip)
-    return (g->w_packed == 2 && s2_kind(g) != 0) || k7m_w2n_taken(g) ? 1 : 0;
+  if (role == 0)  // stride-2 16 <-> 32 kernels (conv_s2.hip), the 16 -> 1 k7 forward (conv_k7_mfma.hip), the
+                  // ResNet-block kernel (conv_k3m.hip: its halo only ever comes from x_bf16)
+    return (g->w_packed == 2 && s2_kind(g) != 0) || k7m_w2n_taken(g) || k3m_route(g) ? 1 : 0;
   if (role != 1 || g->transposed) return 0;
   if (g->k == 7 && g->stride == 1 && (g->cin == 1 || g->cout == 1)) return k7m_wgrad_taken(g);
   if (c1_wgrad_ok(g) || wgrad_c1_ok(g)) return 0;

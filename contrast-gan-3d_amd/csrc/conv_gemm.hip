@@ -17,6 +17,8 @@
 #include "common.h"
 
 namespace cg {
+int g_probe = 0;
+
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
@@ -663,7 +665,9 @@ extern "C" int cgan3d_set_tuning(int32_t key, int32_t value) {
     case 15: CG_CHECK_ARG(value == 0 || value == 1, "cgan3d_set_tuning 15: 0 or 1"); k3m_set(value); return CGAN3D_OK;
     case 16: CG_CHECK_ARG(value == 0 || value == 1, "cgan3d_set_tuning 16: 0 or 1"); wgrad_k3m_set(value); return CGAN3D_OK;
     case 20: CG_CHECK_ARG(value > 0, "cgan3d_set_tuning 20: blocks > 0"); k7wg_blocks_set(value); return CGAN3D_OK;
-    case 21: CG_CHECK_ARG(value == 0 || value == 1, "cgan3d_set_tuning 21: 0 or 1"); sk_nsplit_set(value); return CGAN3D_OK;
+#ifdef CGAN3D_PROBES
+    case 90: g_probe = value; return CGAN3D_OK;  // phase probes (common.h CG_PROBE), timing only
+#endif
     default: break;
   }
   set_error("cgan3d_set_tuning: unknown key %d", key);

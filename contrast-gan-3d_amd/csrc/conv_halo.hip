@@ -661,6 +661,10 @@ int halo_launch(const cgan3d_conv_geom* g, const float* x, const float* w, float
   }
   if (k3_tile_ok(g) && k3m_ok(g, e))  // ResNet-block shape with a bf16 input: operands in LDS (conv_k3m.hip)
     return k3m_launch(g, reinterpret_cast<const __bf16*>(w), y, e, st);
+  if (t64_ok(g, e))  // 64 -> 32 stride-2 transposed, all parity classes per block (conv_t64.hip)
+    return t64_launch(g, reinterpret_cast<const __bf16*>(w), y, e, st);
+  if (f64_ok(g, e))  // 32 -> 64 stride-2, operands resident in LDS (conv_f64.hip)
+    return f64_launch(g, reinterpret_cast<const __bf16*>(w), y, e, st);
   if (k3_tile_ok(g)) {  // ResNet-block shape: whole-tile K-split kernel
     const long long tiles = (long long)a.n * a.td * a.th * a.tw;
     // small grids: the 64 output channels split over 2 blocks per tile

@@ -26,7 +26,7 @@
 // Epilogue as halo_epilogue: bias, activation, residual, fp32 store, BatchNorm statistics into the
 // fp64 accumulators (cgan3d_bn_fuse modes 3 and 4).  Slab statistics, masks and fp32 staging stay on
 // conv_k3_kernel (conv_halo.hip).
-#include "common.h"
+#include "bn_acc.h"
 
 namespace cg {
 
@@ -78,13 +78,25 @@ __device__ __forceinline__ void km_dma16(const void* gsrc, unsigned lds_base) {
 }
 #define KM_WAIT_VM(N) asm volatile("s_waitcnt vmcnt(" #N ")" ::: "memory")
 
+typedef __bf16 bf16x8_p __attribute__((ext_vector_type(8)));
+
 // OB (round 4, cgan3d_epilogue.out_bf16): bit 0 — y and the mode-4 bn_z are bf16; bit 1 — the
-// residual is bf16 (the ResNet chain's z / dL/dy kept in bf16, engine.zs / dys)
-template <bool TR, int OB>
+// residual is bf16 (the ResNet chain's z / dL/dy kept in bf16, engine.zs / dys).
+// PRE (round 5, cgan3d_bn_pre): 0 none; 1 the staged halo is the previous layer's z and becomes
+// act(BatchNorm(z)); 2 it is dL/dy of this layer's BatchNorm and becomes dL/dz.  Order of a PRE launch:
+// the epilogue operands and this thread's z granules (mode 2) are loaded, then the fp64 replicas, then
+// the halo and all 27 taps are DMA'd; the replica sums wait for the whole stream (one round trip for
+// the lot, the replica latency hidden under the DMAs), every block finalizes the statistics (bn_acc.h,
+// the arithmetic of the elementwise passes, so the bits agree), maps its halo in LDS (out-of-volume
+// rows stay zero: the conv pads the BatchNorm output, not its input), writes its share of the interior
+// voxels to pre.out16 (the layer's weight-grad operand) and runs the MFMA groups with no further waits.
+template <bool TR, int OB, int PRE>
 __global__ __launch_bounds__(256, 1) void conv_k3m_kernel(K3mArgs a, const __bf16* __restrict__ x16,
                                                           const __bf16* __restrict__ wpk, float* __restrict__ y,
                                                           Epi ep) {
   __shared__ __attribute__((aligned(16))) unsigned char smem[KM_LDS];
+  __shared__ double pre_sums[128], pre_part[256];
+  __shared__ __attribute__((aligned(16))) float pre_co[7 * 64];
   using lds_t = __attribute__((address_space(3))) void*;
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   // blocks b and b + 8 share an XCD under round-robin placement (speed only, never correctness):
@@ -146,7 +158,7 @@ __global__ __launch_bounds__(256, 1) void conv_k3m_kernel(K3mArgs a, const __bf1
   // 8-channel quarter of every tap per wave).  Lane -> row 8i + lane / 8, position lane % 8, which
   // holds the row's logical granule position ^ swizzle.
   const unsigned lds0 = (unsigned)(uintptr_t)(lds_t)smem;  // LDS byte address of the operand area
-  {
+  auto dma_halo = [&]() {
     const int p = lane & 7;
     // row 8 i + lane / 8 (i = wave, wave + 4, ...): its (hx, hy, hz) stepped by 32 rows = (+2, +5, 0)
     // with carries instead of divided out per piece; 32-bit element offsets (k3m_ok)
@@ -167,13 +179,98 @@ __global__ __launch_bounds__(256, 1) void conv_k3m_kernel(K3mArgs a, const __bf1
       hy -= cy ? KM_HY : 0;
       hz += cy;
     }
+  };
+  auto dma_taps = [&](int t0, int t1) {
+    const int p = lane & 7;
     const int c = 8 * wave + (lane >> 3);  // channel row of the tap image
     const int cout = co0 + c;
     // packed format 2 keeps logical granule q of (tap, channel) at position q ^ (channel & 7)
     const __bf16* src = wpk + (long long)cout * 64 + 8 * ((p ^ km_fw(c)) ^ (cout & 7));
 #pragma unroll
-    for (int tp = 0; tp < 27; ++tp)
+    for (int tp = t0; tp < t1; ++tp)
       km_dma16(src + (long long)tp * 64 * 64, __builtin_amdgcn_readfirstlane(lds0 + KM_HALO + tp * KM_TAPB + wave * 1024));
+  };
+  if constexpr (PRE == 0) {
+    dma_halo();
+    dma_taps(0, 27);
+  } else {
+    const BnPre& pr = ep.pre;
+    constexpr int C = 64;
+    // thread -> logical granule q = tid & 7 (channels 8q .. 8q + 7) of halo rows tid / 8 + 32 k
+    const int q = tid & 7, r0 = tid >> 3;
+    constexpr int NR = (KM_HROWS + 31) / 32;  // 12
+    bf16x8_p zg[PRE == 2 ? NR : 1];
+    auto row_vox = [&](int rr, int& hx, int& hy, int& hz, bool& in) {
+      hx = rr % KM_HX; hy = (rr / KM_HX) % KM_HY; hz = rr / (KM_HX * KM_HY);
+      const int ix = ox + hx, iy = oy + hy, iz = oz + hz;
+      in = rr < KM_HROWS && (unsigned)ix < (unsigned)a.w && (unsigned)iy < (unsigned)a.h && (unsigned)iz < (unsigned)a.d;
+      return in ? ((nb * a.d + iz) * a.h + iy) * a.w + ix : 0;
+    };
+    if (blockIdx.x == 0)
+      for (int j = tid; j < pr.zero_n; j += 256) pr.zero[j] = 0.0;
+    if constexpr (PRE == 2) {  // this thread's z granules, older than every DMA (see the waits below)
+#pragma unroll
+      for (int k = 0; k < NR; ++k) {
+        int hx, hy, hz;
+        bool in;
+        const int v = row_vox(r0 + 32 * k, hx, hy, hz, in);
+        zg[k] = *reinterpret_cast<const bf16x8_p*>(pr.z + (long long)v * 64 + 8 * q);
+      }
+    }
+    // the replica loads, then every DMA of the block (halo and all 27 taps) behind them: the replica
+    // sums' wait covers the whole stream (the DMAs are invisible to the compiler's counting, so it
+    // waits for them too), which is then complete for the map and for every MFMA group
+    acc_sums(pr.acc, pr.reps, C, pre_sums, pre_part, [&] {
+      dma_halo();
+      dma_taps(0, 27);
+    });
+    KM_WAIT_VM(0);  // explicit: the halo and the weights have landed (this wave's)
+    if (tid < C) {
+      if constexpr (PRE == 1)
+        bn_acc_fwd_coeffs(pre_sums, tid, C, pr.nvox, pr.gamma, pr.beta, pr.eps, &pre_co[tid], &pre_co[C + tid],
+                          blockIdx.x == 0, pr.ss, pr.mi, pr.rmean, pr.rvar, pr.nbt, pr.momentum);
+      else {
+        bn_acc_bwd_coeffs(pre_sums, tid, C, pr.nvox, pr.gamma, pr.mi, &pre_co[tid], &pre_co[C + tid],
+                          &pre_co[2 * C + tid], blockIdx.x == 0, pr.dgamma, pr.dbeta, pr.accumulate);
+        pre_co[3 * C + tid] = pr.ss[tid];
+        pre_co[4 * C + tid] = pr.ss[C + tid];
+        pre_co[5 * C + tid] = pr.mi[tid];
+        pre_co[6 * C + tid] = pr.mi[C + tid];
+      }
+    }
+    // every wave's halo landed and the coefficients are in LDS
+    lds_barrier();
+    constexpr int NCO = PRE == 1 ? 2 : 7;
+    float co[NCO][8];
+#pragma unroll
+    for (int m = 0; m < NCO; ++m)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) co[m][e] = pre_co[m * C + 8 * q + e];
+    const int pact = pr.act;
+    const float pslope = pr.slope;
+#pragma unroll
+    for (int k = 0; k < NR; ++k) {
+      const int rr = r0 + 32 * k;
+      int hx, hy, hz;
+      bool in;
+      const int v = row_vox(rr, hx, hy, hz, in);
+      if (!in) continue;  // past the halo or outside the volume: the DMA's zeros stay
+      bf16x8_p* cell = reinterpret_cast<bf16x8_p*>(smem + rr * 128 + 16 * (q ^ km_fa(hx, hy)));
+      const bf16x8_p xv = *cell;
+      bf16x8_p o;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        float f;
+        if constexpr (PRE == 1) f = act_f((float)xv[e] * co[0][e] + co[1][e], pact, pslope);
+        else f = bn_bwd_map((float)xv[e], (float)zg[k][e], co[3][e], co[4][e], co[5][e], co[6][e], co[0][e], co[1][e],
+                            co[2][e], pact, pslope);
+        o[e] = (__bf16)f;
+      }
+      *cell = o;
+      // interior voxel of this tile, the block's channel half: the weight grad's operand
+      if (hx >= 1 && hx <= KM_TX && hy >= 1 && hy <= KM_TY && hz >= 1 && hz <= KM_TZ && (q >> 2) == half)
+        *reinterpret_cast<bf16x8_p*>(pr.out16 + (long long)v * 64 + 8 * q) = o;
+    }
   }
 
   // ---- 27 taps x 4 K-steps of 16 channels = 108 MFMAs, in 4 groups of taps (0-2, 3-8, 9-17, 18-26)
@@ -202,11 +299,14 @@ __global__ __launch_bounds__(256, 1) void conv_k3m_kernel(K3mArgs a, const __bf1
     const int t0 = grp == 0 ? 0 : (grp == 1 ? 3 : (grp == 2 ? 9 : 18));
     const int t1 = grp == 0 ? 3 : (grp == 1 ? 9 : (grp == 2 ? 18 : 27));
     // this wave's DMAs up to the group's last tap have landed (27 - t1 younger ones in flight) ...
-    if (grp == 0) KM_WAIT_VM(24);
-    else if (grp == 1) KM_WAIT_VM(18);
-    else if (grp == 2) KM_WAIT_VM(9);
-    else KM_WAIT_VM(0);
-    __builtin_amdgcn_s_barrier();  // ... and every other wave's
+    // (PRE: every DMA landed before the prologue's map — no waits, only the barrier)
+    if constexpr (PRE == 0) {
+      if (grp == 0) KM_WAIT_VM(24);
+      else if (grp == 1) KM_WAIT_VM(18);
+      else if (grp == 2) KM_WAIT_VM(9);
+      else KM_WAIT_VM(0);
+    }
+    __builtin_amdgcn_s_barrier();  // ... and every other wave's (PRE: and its halo map)
     asm volatile("" ::: "memory");
     const int k0 = 4 * t0, k1 = 4 * t1;
 #pragma unroll
@@ -336,11 +436,15 @@ int k3m_launch(const cgan3d_conv_geom* g, const __bf16* wp, float* y, const Epi&
   a.per_xcd = (a.tiles + 7) / 8;
   const dim3 grid((unsigned)(a.per_xcd * 16));
   const int ob = (e.out16 ? 1 : 0) | (e.res16 ? 2 : 0);
-#define CG_K3M(TR, OB) ::cg::launch(conv_k3m_kernel<TR, OB>, grid, dim3(256), 0, st, a, e.x16, wp, y, e)
-  if (g->transposed) {
-    if (ob == 0) CG_K3M(true, 0); else if (ob == 1) CG_K3M(true, 1); else if (ob == 2) CG_K3M(true, 2); else CG_K3M(true, 3);
+#define CG_K3M(TR, OB, PRE) ::cg::launch(conv_k3m_kernel<TR, OB, PRE>, grid, dim3(256), 0, st, a, e.x16, wp, y, e)
+  if (g->transposed && e.pre.mode == 2) {
+    if (ob == 0) CG_K3M(true, 0, 2); else if (ob == 1) CG_K3M(true, 1, 2); else if (ob == 2) CG_K3M(true, 2, 2); else CG_K3M(true, 3, 2);
+  } else if (g->transposed) {
+    if (ob == 0) CG_K3M(true, 0, 0); else if (ob == 1) CG_K3M(true, 1, 0); else if (ob == 2) CG_K3M(true, 2, 0); else CG_K3M(true, 3, 0);
+  } else if (e.pre.mode == 1) {
+    if (ob == 0) CG_K3M(false, 0, 1); else if (ob == 1) CG_K3M(false, 1, 1); else if (ob == 2) CG_K3M(false, 2, 1); else CG_K3M(false, 3, 1);
   } else {
-    if (ob == 0) CG_K3M(false, 0); else if (ob == 1) CG_K3M(false, 1); else if (ob == 2) CG_K3M(false, 2); else CG_K3M(false, 3);
+    if (ob == 0) CG_K3M(false, 0, 0); else if (ob == 1) CG_K3M(false, 1, 0); else if (ob == 2) CG_K3M(false, 2, 0); else CG_K3M(false, 3, 0);
   }
 #undef CG_K3M
   return CGAN3D_OK;

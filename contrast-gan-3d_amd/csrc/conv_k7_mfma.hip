@@ -129,6 +129,15 @@ __global__ __launch_bounds__(256, 2) void k7m_n2w_kernel(K7Args a, const float* 
     xc[k] = i < N_X ? ((row / N_HH) | ((row % N_HH) << 8) | (hw << 16)) : -1;
   }
   float xb[N_X_PER][2];
+  // element offset of each of this thread's halo pairs relative to the tile's halo origin: a tile whose
+  // halo lies inside the volume (no reflect, no zero) loads from tile base + coff (round 5: the
+  // per-element reflect / range math was ~40 VALU per pair and most of a tile's VALU)
+  int coff[N_X_PER];
+#pragma unroll
+  for (int k = 0; k < N_X_PER; ++k) {
+    const int c = xc[k];
+    coff[k] = c >= 0 ? ((c & 255) * a.hi + ((c >> 8) & 255)) * a.wi + (c >> 16) : 0;
+  }
   auto tile_origin = [&](int tile, int* n, int* d0, int* h0, int* w0) {
     int r = tile;
     const int tw_ = r % a.tiles_w; r /= a.tiles_w;
@@ -139,6 +148,17 @@ __global__ __launch_bounds__(256, 2) void k7m_n2w_kernel(K7Args a, const float* 
   auto load = [&](int tile) {
     int n, d0, h0, w0;
     tile_origin(tile, &n, &d0, &h0, &w0);
+    const int hd0 = d0 - a.P, hh0 = h0 - a.P, hw0 = w0 - a.P;  // block-uniform
+    if (hd0 >= 0 && hd0 + N_HD <= a.di && hh0 >= 0 && hh0 + N_HH <= a.hi && hw0 >= 0 && hw0 + N_HW <= a.wi &&
+        !CG_PROBE(a.probe, 2)) {
+      const float* xt = x + ((n * a.di + hd0) * a.hi + hh0) * a.wi + hw0;
+#pragma unroll
+      for (int k = 0; k < N_X_PER; ++k) {
+        xb[k][0] = xt[coff[k]];
+        xb[k][1] = xt[coff[k] + 1];
+      }
+      return;
+    }
 #pragma unroll
     for (int k = 0; k < N_X_PER; ++k) {
       const int c = xc[k];
@@ -147,13 +167,20 @@ __global__ __launch_bounds__(256, 2) void k7m_n2w_kernel(K7Args a, const float* 
       for (int e = 0; e < 2; ++e) {
         const int iw = k7_src(w0 + (c >> 16) + e - a.P, a.wi, a.reflect);
         const bool ok = c >= 0 && (id | ih | iw) >= 0;
+        if (CG_PROBE(a.probe, 2)) { xb[k][e] = (float)(id + iw); continue; }
         xb[k][e] = x[ok ? ((n * a.di + id) * a.hi + ih) * a.wi + iw : 0];
         if (!ok) xb[k][e] = 0.f;
       }
     }
   };
-  // running BatchNorm statistics of this block (threads tid < 16, channel tid): Chan merge per tile
-  float run_n = 0.f, run_mean = 0.f, run_m2 = 0.f;
+  // BatchNorm statistics (round 5): each lane accumulates its outputs of channels 4g + jj over every
+  // tile as sums shifted by its first value (sum d, sum d^2, d = v - K: no cancellation while the
+  // values stay near K), merged once per block (Chan) — the round-4 per-tile mean / M2 passes cost three
+  // barriers and two cross-lane reductions per tile (7.8 of 40 us, tools/bench_ops.py probe)
+  const bool want_stats = stats || bn_part || acc1;
+  float sK[4] = {0.f, 0.f, 0.f, 0.f}, sS1[4] = {0.f, 0.f, 0.f, 0.f}, sS2[4] = {0.f, 0.f, 0.f, 0.f};
+  float sN = 0.f;
+  float run_n = 0.f, run_mean = 0.f, run_m2 = 0.f;  // the block's merged statistics (threads tid < 16)
   // folded mode-2 pairs of this lane's channels 4g + jj, summed over its outputs of every tile
   float fp1[4] = {0.f, 0.f, 0.f, 0.f}, fp2[4] = {0.f, 0.f, 0.f, 0.f};
   float fsc[4] = {0.f, 0.f, 0.f, 0.f}, fsh[4] = {0.f, 0.f, 0.f, 0.f}, fmean[4] = {0.f, 0.f, 0.f, 0.f},
@@ -183,7 +210,7 @@ __global__ __launch_bounds__(256, 2) void k7m_n2w_kernel(K7Args a, const float* 
     }
     if (tile + 1 < t1) load(tile + 1);  // in flight during this tile's MFMAs
     lds_barrier();
-    for (int i = tid; i < N_ROWS * 2; i += 256) {  // unfold (row, half of ow): 8 shifted windows
+    for (int i = tid; i < (CG_PROBE(a.probe, 4) ? 0 : N_ROWS * 2); i += 256) {  // unfold (row, half of ow): 8 shifted windows
       const int r = i >> 1, hf = i & 1;
       const u32x4 lo = *reinterpret_cast<const u32x4*>(xs + r * N_HWP + 8 * hf);
       const u32x4 hi = *reinterpret_cast<const u32x4*>(xs + r * N_HWP + 8 * hf + 8);
@@ -205,7 +232,7 @@ __global__ __launch_bounds__(256, 2) void k7m_n2w_kernel(K7Args a, const float* 
     for (int r = 0; r < N_TH; ++r) acc[r] = f32x4{0.f, 0.f, 0.f, 0.f};
     const __bf16* ub = us + wave * N_HH * N_US;
 #pragma unroll
-    for (int ks = 0; ks < N_PAIRS / 4; ++ks) {
+    for (int ks = 0; ks < (CG_PROBE(a.probe, 1) ? 0 : N_PAIRS / 4); ++ks) {
       bf16x8_k av[N_TH];
 #pragma unroll
       for (int r = 0; r < N_TH; ++r) av[r] = *reinterpret_cast<const bf16x8_k*>(ub + aoff[ks] + r * N_US);
@@ -216,11 +243,10 @@ __global__ __launch_bounds__(256, 2) void k7m_n2w_kernel(K7Args a, const float* 
     }
     // lane holds out[c = 4g + jj][ow = w0 + r16] of row r (oh = h0 + r, od = d0 + wave)
     const int od = d0 + wave, ow = w0 + r16;
-    float s1[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int r = 0; r < N_TH; ++r) {
       const int oh = h0 + r;
-      if (od < a.do_ && oh < a.ho && ow < a.wo) {
+      if (od < a.do_ && oh < a.ho && ow < a.wo && !CG_PROBE(a.probe, 8)) {
         const int o = (((n * a.do_ + od) * a.ho + oh) * a.wo + ow) * C + 4 * g;
         if constexpr (B16) {
           bf16x4_k h;
@@ -229,8 +255,6 @@ __global__ __launch_bounds__(256, 2) void k7m_n2w_kernel(K7Args a, const float* 
         } else {
           *reinterpret_cast<f32x4*>(y + o) = acc[r];
         }
-#pragma unroll
-        for (int jj = 0; jj < 4; ++jj) s1[jj] += acc[r][jj];
       }
     }
     if (fb.z) {  // every z of the tile's outputs loaded before the first is used
@@ -259,47 +283,68 @@ __global__ __launch_bounds__(256, 2) void k7m_n2w_kernel(K7Args a, const float* 
           }
         }
     }
-    if (stats || bn_part || acc1) {  // tile (sum, M2 about the tile mean), merged into the block's running statistics
-      const int vd = min(N_TD, a.do_ - d0), vh = min(N_TH, a.ho - h0), vw = min(N_TW, a.wo - w0);
-      const float tn = (float)(vd * vh * vw);
-      float tmean[4], q[4];
+    if (want_stats && !CG_PROBE(a.probe, 16)) {
+      if (tile == t0) {  // the shift: this lane's first output (row 0 of its first tile), 0 off the volume
+        const bool ok0 = od < a.do_ && h0 < a.ho && ow < a.wo;
 #pragma unroll
-      for (int jj = 0; jj < 4; ++jj) s1[jj] = k7m_rowsum16(s1[jj]);
-      if (r16 == 0) {
-#pragma unroll
-        for (int jj = 0; jj < 4; ++jj) red[wave][4 * g + jj] = s1[jj];
+        for (int jj = 0; jj < 4; ++jj) sK[jj] = ok0 ? acc[0][jj] : 0.f;
       }
-      lds_barrier();
-#pragma unroll
-      for (int jj = 0; jj < 4; ++jj) {
-        const int c = 4 * g + jj;
-        tmean[jj] = (red[0][c] + red[1][c] + red[2][c] + red[3][c]) / tn;
-        q[jj] = 0.f;
-      }
-      const float tmu = tid < C ? (red[0][tid] + red[1][tid] + red[2][tid] + red[3][tid]) / tn : 0.f;
 #pragma unroll
       for (int r = 0; r < N_TH; ++r) {
         const bool ok = od < a.do_ && h0 + r < a.ho && ow < a.wo;
+        sN += ok ? 1.f : 0.f;
 #pragma unroll
         for (int jj = 0; jj < 4; ++jj) {
-          const float dv = ok ? acc[r][jj] - tmean[jj] : 0.f;
-          q[jj] += dv * dv;
+          const float dv = ok ? acc[r][jj] - sK[jj] : 0.f;
+          sS1[jj] += dv;
+          sS2[jj] = fmaf(dv, dv, sS2[jj]);
         }
       }
+    }
+  }
+  if (want_stats) {  // lane (n, mean, M2) -> Chan merge over the 16 voxel lanes, then over the 4 waves
+    float mm[4], m2[4];
+    float nn = sN;
 #pragma unroll
-      for (int jj = 0; jj < 4; ++jj) q[jj] = k7m_rowsum16(q[jj]);
-      lds_barrier();
-      if (r16 == 0) {
+    for (int jj = 0; jj < 4; ++jj) {
+      mm[jj] = nn > 0.f ? sK[jj] + sS1[jj] / nn : 0.f;
+      m2[jj] = nn > 0.f ? fmaxf(sS2[jj] - sS1[jj] * sS1[jj] / nn, 0.f) : 0.f;
+    }
 #pragma unroll
-        for (int jj = 0; jj < 4; ++jj) red[wave][4 * g + jj] = q[jj];
+    for (int off = 1; off < 16; off <<= 1) {
+      const float no = __shfl_xor(nn, off, 64), nt = nn + no;
+      const float wo = nt > 0.f ? no / nt : 0.f, wx = nt > 0.f ? nn * no / nt : 0.f;
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj) {
+        const float mo = __shfl_xor(mm[jj], off, 64), qo = __shfl_xor(m2[jj], off, 64);
+        const float dl = mo - mm[jj];
+        mm[jj] += dl * wo;
+        m2[jj] += qo + dl * dl * wx;
       }
-      lds_barrier();
-      if (tid < C) {
-        const float tm2 = red[0][tid] + red[1][tid] + red[2][tid] + red[3][tid];
-        const float nn = run_n + tn, delta = tmu - run_mean;
-        run_mean += delta * (tn / nn);
-        run_m2 += tm2 + delta * delta * (run_n * tn / nn);
-        run_n = nn;
+      nn = nt;
+    }
+    float* rn = reinterpret_cast<float*>(us);  // [4 waves][16] x (n, mean, M2); us is dead after the last tile
+    lds_barrier();
+    if (r16 == 0) {
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj) {
+        rn[(0 * 4 + wave) * C + 4 * g + jj] = nn;
+        rn[(1 * 4 + wave) * C + 4 * g + jj] = mm[jj];
+        rn[(2 * 4 + wave) * C + 4 * g + jj] = m2[jj];
+      }
+    }
+    lds_barrier();
+    if (tid < C) {
+#pragma unroll
+      for (int w = 0; w < 4; ++w) {
+        const float no = rn[(0 * 4 + w) * C + tid], mo = rn[(1 * 4 + w) * C + tid], qo = rn[(2 * 4 + w) * C + tid];
+        const float nt = run_n + no;
+        if (no > 0.f) {
+          const float dl = mo - run_mean;
+          run_mean += dl * (no / nt);
+          run_m2 += qo + dl * dl * (run_n * no / nt);
+          run_n = nt;
+        }
       }
     }
   }
@@ -958,6 +1003,7 @@ static K7Args k7m_args(const cgan3d_conv_geom* g, int P, int reflect, int flip, 
   a.n = g->n; a.di = g->di; a.hi = g->hi; a.wi = g->wi; a.do_ = g->do_; a.ho = g->ho; a.wo = g->wo;
   a.P = P; a.reflect = reflect; a.flip = flip; a.wc = wc;
   a.tiles_d = (g->do_ + td - 1) / td; a.tiles_h = (g->ho + th - 1) / th; a.tiles_w = (g->wo + tw - 1) / tw;
+  a.probe = g_probe;
   return a;
 }
 

@@ -16,15 +16,11 @@
 //    voxel, so the epilogue (bias / activation / LeakyReLU-mask / residual) moves 16 bytes per
 //    lane access; per-block BatchNorm statistics (sum, M2, count) for the BatchNorm critic of the
 //    weight-clip configuration;
-//  * split K across blocks (round 5, SPLIT): few row tiles with a long K (the 32 -> 64 layer: 48 tiles
-//    at 12 samples, 16 at 4, K = 2048) left each block pulling all 256 KB of weights and 128 KB of
-//    gathered activations through one CU (~15 us per launch whatever the batch).  The tile's K-steps
-//    are cut over KB blocks; each adds its partial tile into an all-zero fp32 workspace (no-return
-//    atomics at the memory side, in fragment order: every wave-instruction adds 256 contiguous bytes —
-//    lanes scattered over 16 rows ran 17x slower, MI355X_MICROARCH.md atomics table), waits for them
-//    (vmcnt) and takes a ticket; the last block of the tile reads the sums back with device-coherent
-//    loads, re-zeroes the workspace and its ticket, and runs the epilogue — one launch, no memset, no
-//    L2 writeback / invalidate (nothing but atomics and coherent loads crosses blocks).
+//  * N split (round 5): few row tiles with a long K (the 32 -> 64 layer: 48 tiles at 12 samples, 16 at
+//    4, K = 2048) left each block pulling all 256 KB of weights through one CU; there every block takes
+//    one 16-channel slice of the tile (64 KB of weights), nt blocks per tile.  A split of K over blocks
+//    (no-return atomics into a zeroed workspace + a ticket, the last block running the epilogue) was
+//    built and measured slower (1.420-1.435 vs 1.402-1.405 ms/step) and removed.
 #include "common.h"
 
 namespace cg {
@@ -37,8 +33,7 @@ struct SkArgs {
   int mblocks;             // blocks per class
   int ktot;                // k^3 * cin: packed weight row length
   int cin_log2;            // cin is a power of two (sk_format_ok)
-  int kb;                  // SPLIT: blocks per row tile, each a contiguous range of the tile's K-steps
-  int nsplit;              // blocks per row tile, each 16 NT of the output channels (MT == 1, not SPLIT)
+  int nsplit;              // blocks per row tile, each 16 NT of the output channels (MT == 1)
 };
 
 __device__ __forceinline__ void sk_class(int r, int k, int s, int p, int transposed, int* f, int* st, int* cnt) {
@@ -49,9 +44,8 @@ __device__ __forceinline__ void sk_class(int r, int k, int s, int p, int transpo
   }
 }
 
-// W: waves per block (MT == 1 splits K over them); NKC: compile-time K-steps per wave (0: runtime);
-// SPLIT (MT == 1): a.kb blocks per row tile, partial tiles summed in ep.split_ws (above)
-template <int MT, int NT, int W, int NKC, bool SPLIT>
+// W: waves per block (MT == 1 splits K over them); NKC: compile-time K-steps per wave (0: runtime)
+template <int MT, int NT, int W, int NKC>
 __global__ __launch_bounds__(64 * W) void conv_sk_kernel(SkArgs a, const float* __restrict__ x,
                                                          const __bf16* __restrict__ wp, float* y, Epi ep) {
   __shared__ int rowo[16 * MT];
@@ -59,12 +53,9 @@ __global__ __launch_bounds__(64 * W) void conv_sk_kernel(SkArgs a, const float* 
   __shared__ int rown[16 * MT];
   __shared__ __attribute__((aligned(16))) f32x4 red[W - 1][NT][64];
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  // SPLIT: the a.kb blocks of one row tile are consecutive (their tickets complete together)
-  const int kbn = SPLIT ? a.kb : 1;
   // N split (MT == 1): the a.nsplit blocks of a row tile take consecutive 16 NT-channel slices
-  const int nsp = (MT == 1 && !SPLIT) ? a.nsplit : 1;
-  const int bq = (int)blockIdx.x / nsp, cb = ((int)blockIdx.x - bq * nsp) * 16 * NT;
-  const int tile = SPLIT ? bq / kbn : bq, kbi = SPLIT ? bq - tile * kbn : 0;
+  const int nsp = MT == 1 ? a.nsplit : 1;
+  const int tile = (int)blockIdx.x / nsp, cb = ((int)blockIdx.x - tile * nsp) * 16 * NT;
   const int cls = tile / a.mblocks, mb = tile - cls * a.mblocks;
   const int s = a.s;
   int r3[3] = {0, 0, 0};
@@ -115,8 +106,8 @@ __global__ __launch_bounds__(64 * W) void conv_sk_kernel(SkArgs a, const float* 
   const int HW = a.hi * a.wi;
   const int gbase = ((nb * a.di + Cz) * a.hi + Cy) * a.wi + Cx;
   const int KS = ntap * a.cin / 32;
-  const int kbeg = SPLIT ? (KS * kbi) / kbn : 0, kend = SPLIT ? (KS * (kbi + 1)) / kbn : KS;
-  const int ks0 = kbeg + (MT == 1 ? wave : 0), kstep = MT == 1 ? W : 1;
+  const int kend = KS;
+  const int ks0 = MT == 1 ? wave : 0, kstep = MT == 1 ? W : 1;
 
   f32x4 acc[NT];
 #pragma unroll
@@ -195,33 +186,6 @@ __global__ __launch_bounds__(64 * W) void conv_sk_kernel(SkArgs a, const float* 
       for (int q = 1; q < W - 1; ++q) r += red[q][t][lane];
       acc[t] += r;
     }
-  }
-  if constexpr (SPLIT) {  // wave 0: this block's partial tile into the workspace, then the ticket
-    // fragment order [tile][t][jj][lane]: one wave-instruction = 64 consecutive floats
-    float* tt = ep.split_ws + (long long)tile * 16 * 16 * NT + lane;
-    unsigned* ctr = reinterpret_cast<unsigned*>(ep.split_ws + (long long)a.nclass * a.mblocks * 16 * 16 * NT);
-#pragma unroll
-    for (int t = 0; t < NT; ++t)
-#pragma unroll
-      for (int jj = 0; jj < 4; ++jj)
-        __hip_atomic_fetch_add(tt + (t * 4 + jj) * 64, acc[t][jj], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    // every add performed at the memory side (no-return atomics stay counted in vmcnt until then)
-    // before the ticket is taken
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    unsigned tk = 0;
-    if (lane == 0) tk = __hip_atomic_fetch_add(ctr + tile, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    tk = __shfl(tk, 0, 64);
-    if (tk != (unsigned)(kbn - 1)) return;  // not the tile's last block
-    asm volatile("" ::: "memory");
-#pragma unroll
-    for (int t = 0; t < NT; ++t)
-#pragma unroll
-      for (int jj = 0; jj < 4; ++jj) {
-        float* pw = tt + (t * 4 + jj) * 64;
-        acc[t][jj] = __hip_atomic_load(pw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(pw, 0.f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // left all-zero
-      }
-    if (lane == 0) __hip_atomic_store(ctr + tile, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   // epilogue: the MFMA ran transposed (A = weights, B = activations), so lane (g, r16) holds
   // channels t*16 + 4g .. +3 of row mt*16 + r16: one 16-byte store (and mask / residual load) per
@@ -319,33 +283,8 @@ static SkArgs sk_args(const cgan3d_conv_geom* g, int* mt) {
   a.ktot = g->k * g->k * g->k * g->cin;
   a.cin_log2 = 0;
   while ((1 << a.cin_log2) < g->cin) ++a.cin_log2;
-  a.kb = 1;
   a.nsplit = 1;
   return a;
-}
-
-// split K over blocks (SPLIT) when the row tiles alone leave most of the chip idle and K is long:
-// ~384 blocks, >= 1 K-step per wave of 4 (the launch then runs 4-wave blocks)
-static int sk_split_kb(const cgan3d_conv_geom* g, const SkArgs& a, int mt) {
-  if (mt != 1 || g->transposed) return 1;
-  const int kd = g->k;
-  const int KS = kd * kd * kd * g->cin / 32;
-  const long long tiles = (long long)a.nclass * a.mblocks;
-  if (KS < 64 || tiles >= 192) return 1;  // the 32 -> 64 layer (K = 2048); shorter K: measured slower split
-  const long long want = (384 + tiles - 1) / tiles;
-  return (int)std::max(1LL, std::min<long long>(want, KS / 4));
-}
-
-static int g_sk_nsplit = 1;  // cgan3d_set_tuning key 21 (A/B): 0 keeps the long-K layer on whole-N blocks
-void sk_nsplit_set(int v) { g_sk_nsplit = v; }
-
-long long sk_split_ws_floats(const cgan3d_conv_geom* g) {
-  if (!sk_ok(g)) return 0;
-  int mt;
-  SkArgs a = sk_args(g, &mt);
-  if (sk_split_kb(g, a, mt) <= 1) return 0;
-  const long long tiles = (long long)a.nclass * a.mblocks;
-  return tiles * 16 * 16 * ((g->cout + 15) / 16) + tiles;  // partial tiles (fragment order) + one ticket each
 }
 
 long long sk_blocks(const cgan3d_conv_geom* g) {  // rows of the statistics epilogue (per row tile)
@@ -361,28 +300,6 @@ int sk_launch(const cgan3d_conv_geom* g, const float* x, const __bf16* wp, float
   int mt;
   SkArgs a = sk_args(g, &mt);
   const int nt = (g->cout + 15) / 16;
-  const int kb = e.split_ws && !e.stats ? sk_split_kb(g, a, mt) : 1;
-  CG_CHECK_ARG(!e.split_ws || kb > 1 || sk_split_ws_floats(g) == 0 || e.stats,
-               "conv_sk: split workspace given to a launch that does not split");
-  if (kb > 1) {  // SPLIT: 4-wave blocks, a contiguous K range each (sk_split_kb)
-    a.kb = kb;
-    const dim3 grid((unsigned)(a.nclass * a.mblocks * kb));
-    const int kd = g->k;
-    const int KS = kd * kd * kd * g->cin / 32;
-    const int nkw = ((KS + kb - 1) / kb + 3) / 4;  // most K-steps of a wave
-    auto by_nt = [&](auto nkc_c) {
-      constexpr int K = decltype(nkc_c)::value;
-      if (nt == 1) ::cg::launch((conv_sk_kernel<1, 1, 4, K, true>), grid, dim3(256), 0, st, a, x, wp, y, e);
-      else if (nt == 2) ::cg::launch((conv_sk_kernel<1, 2, 4, K, true>), grid, dim3(256), 0, st, a, x, wp, y, e);
-      else if (nt == 3) ::cg::launch((conv_sk_kernel<1, 3, 4, K, true>), grid, dim3(256), 0, st, a, x, wp, y, e);
-      else ::cg::launch((conv_sk_kernel<1, 4, 4, K, true>), grid, dim3(256), 0, st, a, x, wp, y, e);
-    };
-    if (nkw <= 1) by_nt(std::integral_constant<int, 1>{});
-    else if (nkw <= 2) by_nt(std::integral_constant<int, 2>{});
-    else if (nkw <= 4) by_nt(std::integral_constant<int, 4>{});
-    else by_nt(std::integral_constant<int, 8>{});
-    return CGAN3D_OK;
-  }
   // K-steps per wave, as a compile-time trip count where it is short (every parity class has the
   // same tap count here: k % s == 0)
   const int kd = g->transposed ? g->k / g->stride : g->k;
@@ -390,7 +307,7 @@ int sk_launch(const cgan3d_conv_geom* g, const float* x, const __bf16* wp, float
   // N split (round 5): few row tiles with a long K (the 32 -> 64 layer, K = 2048) — each block reads
   // only its 16 output channels' weights (64 KB instead of 256 KB through one CU), nt blocks per tile
   const long long tiles = (long long)a.nclass * a.mblocks;
-  const int ns = (g_sk_nsplit && mt == 1 && !e.stats && KS >= 64 && tiles < 192) ? nt : 1;
+  const int ns = (mt == 1 && !e.stats && KS >= 64 && tiles < 192) ? nt : 1;
   a.nsplit = ns;
   const int ntb = nt / ns;
   const dim3 grid((unsigned)(tiles * ns));
@@ -403,10 +320,10 @@ int sk_launch(const cgan3d_conv_geom* g, const float* x, const __bf16* wp, float
     auto by_nt = [&](auto nkc_c) {
       constexpr int K = decltype(nkc_c)::value;
       const dim3 block(64 * W);
-      if (ntb == 1) ::cg::launch((conv_sk_kernel<M, 1, W, K, false>), grid, block, 0, st, a, x, wp, y, e);
-      else if (ntb == 2) ::cg::launch((conv_sk_kernel<M, 2, W, K, false>), grid, block, 0, st, a, x, wp, y, e);
-      else if (ntb == 3) ::cg::launch((conv_sk_kernel<M, 3, W, K, false>), grid, block, 0, st, a, x, wp, y, e);
-      else ::cg::launch((conv_sk_kernel<M, 4, W, K, false>), grid, block, 0, st, a, x, wp, y, e);
+      if (ntb == 1) ::cg::launch((conv_sk_kernel<M, 1, W, K>), grid, block, 0, st, a, x, wp, y, e);
+      else if (ntb == 2) ::cg::launch((conv_sk_kernel<M, 2, W, K>), grid, block, 0, st, a, x, wp, y, e);
+      else if (ntb == 3) ::cg::launch((conv_sk_kernel<M, 3, W, K>), grid, block, 0, st, a, x, wp, y, e);
+      else ::cg::launch((conv_sk_kernel<M, 4, W, K>), grid, block, 0, st, a, x, wp, y, e);
     };
     if (nkc == 4) by_nt(std::integral_constant<int, 4>{});
     else if (nkc == 8) by_nt(std::integral_constant<int, 8>{});

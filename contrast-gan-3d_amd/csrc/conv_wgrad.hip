@@ -375,6 +375,7 @@ struct Wk3Args {
   int n, d, h, w;
   int units;      // n * d * (h/4) * (w/8)
   int upb;        // units per block (even)
+  int probe;      // phase probes (common.h CG_PROBE)
 };
 
 template <bool B16>
@@ -566,6 +567,7 @@ __global__ __launch_bounds__(256, 1) void wgrad_k3m_kernel(Wk3Args a, const __bf
   // instruction covers 8 rows, lane -> row 8j + lane / 8, 16-byte position lane % 8 (holding chunk
   // position ^ swz(row))
   auto issue = [&](int s) {
+    if (CG_PROBE(a.probe, 2)) return;
     // the stage's 4 units (wave-uniform: scalar arithmetic): first voxel of the X window / dZ rows
     long long xo[UPS], zo[UPS];
     int zz[UPS], yy[UPS], xx[UPS];
@@ -648,7 +650,7 @@ __global__ __launch_bounds__(256, 1) void wgrad_k3m_kernel(Wk3Args a, const __bf
       lda(k);
     }
 #pragma unroll
-    for (int k = 0; k < 6 * UPS; ++k) {
+    for (int k = 0; k < (CG_PROBE(a.probe, 1) ? 0 : 6 * UPS); ++k) {
       const bf16x8_w av = ra[k % PD], bv = rb[(k / 3) % NB];
       if (k + PD < 6 * UPS) {
         if ((k + PD) % 3 == 0) ldb(k + PD);
@@ -661,6 +663,7 @@ __global__ __launch_bounds__(256, 1) void wgrad_k3m_kernel(Wk3Args a, const __bf
   }
   // partials ws[p][tap][b][a]: lane holds a = 32 ah + (i & 3) + 8 (i >> 2) + 4 (lane >> 5), b = 32 bh + (lane & 31)
   const int b = 32 * bh + (lane & 31), a0 = 32 * ah + 4 * (lane >> 5);
+  if (CG_PROBE(a.probe, 4)) return;
 #pragma unroll
   for (int tw = 0; tw < 3; ++tw) {
     float* o = ws + (((long long)p * 27 + tdh * 3 + tw) * 64 + b) * 64 + a0;
@@ -851,6 +854,7 @@ static void wgrad_k3_geometry(const cgan3d_conv_geom* g, Wk3Args* a, int* P) {
   upb = (upb + wk3::UPS - 1) / wk3::UPS * wk3::UPS;
   *P = (a->units + upb - 1) / upb;
   a->upb = upb;
+  a->probe = g_probe;
 }
 
 long long wgrad_k3_ws_floats(const cgan3d_conv_geom* g) {

@@ -17,6 +17,7 @@ struct K7Args {
   int flip;       // use W[c, 342 - t]
   long long wc;   // weight stride of the wide channel (tap stride 1)
   int tiles_d, tiles_h, tiles_w;
+  int probe;      // phase probes (common.h CG_PROBE)
 };
 
 __device__ __forceinline__ void k7_tile(const K7Args& a, int bid, int* n, int* d0, int* h0, int* w0) {

@@ -109,6 +109,45 @@ typedef struct cgan3d_bn_fuse {
   int32_t reps;         /* replicas of acc_out (1..64) */
 } cgan3d_bn_fuse;
 
+/* BatchNorm of the conv's INPUT, applied by the ResNet-block kernel while it stages its halo (round 5:
+ * the chain's elementwise BatchNorm launches folded into the next conv; model/blocks.py:56-88).  The
+ * launch's x_bf16 is then the raw tensor of the previous BatchNorm layer and every block finalizes
+ * that layer's statistics from the fp64 replicas itself:
+ *   mode 1 (forward, cgan3d_bn_apply_acc without a residual): x_bf16 = the bf16 z, acc = its (sum,
+ *          sum of squares) replicas; the conv input is act(z * scale + shift); one block writes
+ *          scale_shift / mean_invstd / the running buffers / num_batches_tracked;
+ *   mode 2 (input-grad, cgan3d_bn_backward_acc): x_bf16 = the bf16 dL/dy of the layer, z its bf16
+ *          BatchNorm input, acc its (sum g, sum g * xhat) replicas, scale_shift / mean_invstd those of
+ *          its forward; the conv input is dL/dz; one block writes dgamma / dbeta (added when
+ *          accumulate).
+ * out_bf16 receives the applied input at every voxel (bf16, same layout): the operand the layer's
+ * weight gradient reads.  zero / zero_n: doubles zeroed by the launch (an accumulator the stream is
+ * done with, as cgan3d_bn_apply_acc).  Only launches with cgan3d_conv3d_bn_pre_ok take it. */
+typedef struct cgan3d_bn_pre {
+  int32_t mode;
+  const void* z;                /* mode 2 */
+  const double* acc;
+  int32_t reps;                 /* 1..64 */
+  int64_t nvox;
+  const float* gamma;
+  const float* beta;            /* mode 1 */
+  float* running_mean;          /* mode 1, optional */
+  float* running_var;           /* mode 1, optional */
+  int64_t* num_batches_tracked; /* mode 1, optional */
+  float momentum;
+  float eps;
+  float* scale_shift;           /* mode 1: written; mode 2: read */
+  float* mean_invstd;           /* mode 1: written; mode 2: read */
+  float* dgamma;                /* mode 2, optional */
+  float* dbeta;                 /* mode 2, optional */
+  int32_t accumulate;
+  int32_t act;
+  float slope;
+  void* out_bf16;
+  double* zero;
+  int32_t zero_n;
+} cgan3d_bn_pre;
+
 typedef struct cgan3d_epilogue {
   const float* bias;
   const float* residual;
@@ -138,22 +177,21 @@ typedef struct cgan3d_epilogue {
                                 * bf16 (the ResNet-block kernel only): the generator's BatchNorm inputs
                                 * and their gradients kept in bf16 (round 4) — only launches with
                                 * cgan3d_conv3d_out_bf16_ok accept it, every other launch rejects it */
-  float* split_ws;             /* NULL, or an all-zero fp32 workspace of cgan3d_conv3d_split_ws_floats(g)
-                                * floats: the launch may then split its reduction over more blocks
-                                * (partial tiles summed there; left all-zero on return).  Launches with
-                                * no split (split_ws_floats 0) ignore it. */
+  const cgan3d_bn_pre* pre;    /* NULL, or the input's BatchNorm applied while staging (above) */
 } cgan3d_epilogue;
+
+/* 1 when the launch of g can take cgan3d_epilogue.pre (the ResNet-block kernel: mode 1 on the forward
+ * geometry, mode 2 on the input-grad one). */
+int32_t cgan3d_conv3d_bn_pre_ok(const cgan3d_conv_geom* g);
 
 /* 1 when the forward-style launch of g honours cgan3d_epilogue.out_bf16: the 1 -> 16 k7 MFMA kernel
  * (first conv forward; last conv input-grad, its folded statistics reading a bf16 z), the S2T
  * kernel (ConvTranspose3d 32 -> 16 forward; the first downsampling conv's input-grad with acc_mode 4
- * statistics reading a bf16 z) and the ResNet-block kernel (Conv3d 64 -> 64 k3 forward / input-grad
- * with the bf16 input shadow; bit 1 there: a bf16 skip gradient as the residual). */
+ * statistics reading a bf16 z), the ResNet-block kernel (Conv3d 64 -> 64 k3 forward / input-grad
+ * with the bf16 input shadow; bit 1 there: a bf16 skip gradient as the residual) and the 64 -> 32
+ * stride-2 transposed kernel (ConvTranspose3d 64 -> 32 forward, the second downsampling conv's
+ * input-grad; round 5). */
 int32_t cgan3d_conv3d_out_bf16_ok(const cgan3d_conv_geom* g);
-
-/* fp32 floats of cgan3d_epilogue.split_ws for a launch of g that splits its reduction over blocks
- * (the critic's k4 layers with few output rows and a long K, discriminator.py:42-68); 0 when it does not. */
-int64_t cgan3d_conv3d_split_ws_floats(const cgan3d_conv_geom* g);
 
 /* 1 when the geometry's launch can produce cgan3d_bn_fuse accumulators. */
 int32_t cgan3d_bn_fuse_ok(const cgan3d_conv_geom* g);
@@ -261,7 +299,8 @@ int cgan3d_wgrad_reduce_multi(const cgan3d_reduce_desc* descs, int32_t n, void* 
 int cgan3d_conv3d_wgrad_ws_mode(const cgan3d_conv_geom* g);
 /* 1 when the kernel this geometry dispatches to reads ONLY the bf16 shadows of its operands once
  * they are given, so the caller may leave their fp32 tensors unwritten: role 0 = cgan3d_conv3d_fwd
- * with cgan3d_epilogue.x_bf16 (the stride-2 16 <-> 32 kernels, the 16 -> 1 k7 conv), role 1 = cgan3d_conv3d_wgrad_ex
+ * with cgan3d_epilogue.x_bf16 (the stride-2 16 <-> 32 kernels, the 16 -> 1 k7 conv, the ResNet-block
+ * convs), role 1 = cgan3d_conv3d_wgrad_ex
  * with both shadows (ResNet / stride-2 kernels) or, for a k7 conv with a single-channel side, the
  * multi-channel operand's shadow (the bf16 MFMA kernel).  0 otherwise. */
 int32_t cgan3d_conv3d_shadow_only(const cgan3d_conv_geom* g, int32_t role);

@@ -346,6 +346,23 @@ def test_k7_bf16_mfma(sp):
     yk = yo.double().cpu().view(-1, 16)
     assert int(st[:, 32].sum()) == yk.shape[0]
     assert_close((st[:, :16].sum(0) / yk.shape[0]).numpy(), yk.mean(0).numpy(), 1e-4, "k7 stats mean")
+    # per-block (sum, M2 about the block mean, count) merged (Chan) -> the population variance
+    cnt, S, M2 = st[:, 32], st[:, :16], st[:, 16:32]
+    live = cnt > 0
+    bm = S[live] / cnt[live, None]
+    mu = S.sum(0) / cnt.sum()
+    m2 = M2[live].sum(0) + (cnt[live, None] * (bm - mu) ** 2).sum(0)
+    assert_close((m2 / cnt.sum()).numpy(), yk.var(0, unbiased=False).numpy(), 1e-4, "k7 stats var")
+    # the same statistics into fp64 accumulators (cgan3d_bn_fuse mode 3, the bf16 step's form)
+    reps = 16
+    acc = torch.zeros(reps * 2 * 16, device="cuda", dtype=torch.float64)
+    ya = torch.empty_like(yo)
+    ops.conv(geo, _cl(x1), wf.detach().float().cuda(), ya, ops.epilogue(fuse=ops.BnFuse(acc, 3, reps)))
+    assert torch.equal(ya, yo)
+    a2 = acc.cpu().view(reps, 2, 16).sum(0)
+    N = yk.shape[0]
+    assert_close((a2[0] / N).numpy(), yk.mean(0).numpy(), 1e-4, "k7 acc mean")
+    assert_close((a2[1] / N - (a2[0] / N) ** 2).numpy(), yk.var(0, unbiased=False).numpy(), 1e-4, "k7 acc var")
     # last conv forward (bias, tanh, out2 = minuend - y)
     geo = ops.with_prec(ops.conv_fwd_geom(n, dims, dims, 16, 1, k, 1, p, True), BF)
     att = torch.empty(n, *dims, 1, device="cuda")
@@ -608,47 +625,35 @@ def test_conv_sk_bf16(cin, cout, sp):
 
 @pytest.mark.parametrize("n,cin,cout,sp", [(12, 32, 64, (8, 8, 8)), (4, 32, 64, (8, 8, 8)), (2, 32, 64, (8, 8, 8)),
                                              (1, 32, 64, (8, 8, 8)), (3, 32, 64, (10, 8, 12))])
-def test_conv_sk_split_k(n, cin, cout, sp):
-    """Split-K conv_sk (round 5, cgan3d_epilogue.split_ws): the critic's 32 -> 64 layer with its K
-    (2048) cut over blocks, partial tiles summed in an all-zero workspace by
-    atomics and the tile's last block running the epilogue.  Against torch float64 within the bf16
-    bar (2e-2) and against the unsplit launch within fp32 summation-order noise (1e-5 of the output's
-    largest entry); the workspace is all-zero again after each launch (so the plan can reuse it), and
-    a second launch on the same workspace gives the same result."""
+def test_conv_sk_n_split(n, cin, cout, sp):
+    """N-split conv_sk (round 5): the critic's 32 -> 64 layer (K = 2048, few row tiles) with every
+    block taking one 16-channel slice of its tile, in the forward (bias + LeakyReLU) and the gradient
+    penalty's forward-mode (mask in place) roles.  Against torch float64 of the bf16-rounded operands
+    at 1e-4 (fp32 accumulation of exact bf16 products) and of the unrounded ones within the bf16 bar."""
     from cgan3d_amd import ops, _lib as L
     k, s, p, slope = 4, 2, 1, 0.2
     g = torch.Generator().manual_seed(5 + n + cin + sp[0])
     x = torch.randn(n, cin, *sp, generator=g, dtype=torch.float64)
     w = torch.randn(cout, cin, k, k, k, generator=g, dtype=torch.float64) / np.sqrt(cin * k**3)
     b = torch.randn(cout, generator=g, dtype=torch.float64) * 0.1
+    rb = lambda v: v.to(torch.bfloat16).double()  # noqa: E731
     z = F.conv3d(x, w, b, stride=s, padding=p)
-    yref = F.leaky_relu(z, slope)
+    zb = F.conv3d(rb(x), rb(w), b.float().double(), stride=s, padding=p)
     din, dout = tuple(sp), tuple(z.shape[2:])
     ps = ops.PackSet(torch.device("cuda"))
     gf, wf = ps.add(ops.conv_fwd_geom(n, din, dout, cin, cout, k, s, p), w.float().cuda(), L.PREC_BF16)
     ps.pack()
-    nsw = ops.split_ws_floats(gf)
-    assert nsw > 0, "this geometry is meant to split"
-    ws = torch.zeros(nsw, device="cuda")
-    bb = b.float().cuda()
-    y0 = torch.empty(n, *dout, cout, device="cuda")
-    ops.conv(gf, _cl(x), wf, y0, ops.epilogue(bias=bb, act=L.ACT_LRELU, slope=slope))  # unsplit
-    outs = []
-    for _ in range(2):
-        y1 = torch.full_like(y0, float("nan"))
-        ops.conv(gf, _cl(x), wf, y1, ops.epilogue(bias=bb, act=L.ACT_LRELU, slope=slope, split_ws=ws))
-        torch.cuda.synchronize()
-        assert torch.count_nonzero(ws) == 0, "split workspace not left all-zero"
-        outs.append(y1)
-    assert_close(_ncdhw(outs[0]).numpy(), yref.numpy(), 2e-2, "split fwd")
-    scale = float(y0.abs().max())
-    assert float((outs[0] - y0).abs().max()) <= 1e-5 * scale and float((outs[1] - y0).abs().max()) <= 1e-5 * scale
-    # the gradient penalty's forward-mode launch (mask = the output's previous contents, in place)
-    nu = outs[0].clone()
-    ops.conv(gf, _cl(x), wf, nu, ops.epilogue(mask_src=nu, slope=slope, split_ws=ws))
-    zf = F.conv3d(x, w, stride=s, padding=p)
-    assert_close(_ncdhw(nu).numpy(), torch.where(_ncdhw(outs[0]) > 0, zf, zf * slope).numpy(), 2e-2, "split fwd-mode")
-    assert torch.count_nonzero(ws) == 0
+    y = torch.full((n, *dout, cout), float("nan"), device="cuda")
+    ops.conv(gf, _cl(x), wf, y, ops.epilogue(bias=b.float().cuda(), act=L.ACT_LRELU, slope=slope))
+    nu = y.clone()
+    ops.conv(gf, _cl(x), wf, nu, ops.epilogue(mask_src=nu, slope=slope))
+    assert_close(_ncdhw(y).numpy(), F.leaky_relu(zb, slope).numpy(), 1e-4, "n-split fwd (bf16 operands)")
+    assert_close(_ncdhw(y).numpy(), F.leaky_relu(z, slope).numpy(), 2e-2, "n-split fwd")
+    # mask from the device's own forward output (a float64 z near 0 may differ in sign from the bf16 one)
+    m = _ncdhw(y) > 0
+    zf, zfb = F.conv3d(x, w, stride=s, padding=p), F.conv3d(rb(x), rb(w), stride=s, padding=p)
+    assert_close(_ncdhw(nu).numpy(), torch.where(m, zfb, zfb * slope).numpy(), 1e-4, "n-split fwd-mode (bf16 operands)")
+    assert_close(_ncdhw(nu).numpy(), torch.where(m, zf, zf * slope).numpy(), 2e-2, "n-split fwd-mode")
 
 
 @pytest.mark.parametrize("n,cin,cout,sp", [(12, 8, 16, (32, 32, 32)), (12, 16, 32, (16, 16, 16)), (12, 32, 64, (8, 8, 8)),
@@ -845,6 +850,96 @@ def test_conv_k3m_bf16(n, sp):
                  "mode-4 sum g xhat")
 
 
+@pytest.mark.parametrize("n,sp", K3M_CASES)
+@pytest.mark.parametrize("act", ["relu", "none"])
+def test_conv_k3m_bn_prologue(n, sp, act):
+    """The ResNet chain's BatchNorm passes folded into the next conv (round 5, cgan3d_bn_pre): the
+    forward (mode 1: staged z -> act(BN(z)), statistics finalized from the fp64 replicas in every
+    block) and the input-grad (mode 2: staged dL/dy -> BatchNorm backward dL/dz) must give exactly the
+    bits of the unfused pair (cgan3d_bn_apply_acc / cgan3d_bn_backward_acc, then conv_k3m): the conv
+    output, its own accumulator statistics, the materialised operand (out_bf16, every voxel), the
+    published scale / shift / mean / invstd / running buffers / dgamma / dbeta and the zeroed
+    accumulator.  Ragged tiles on every axis in the K3M_CASES shapes."""
+    from cgan3d_amd import ops, _lib as L
+    c = 64
+    A = L.ACT_RELU if act == "relu" else L.ACT_NONE
+    g = torch.Generator().manual_seed(11 + sp[0] + n)
+    dev = torch.device("cuda")
+    nv = n * sp[0] * sp[1] * sp[2]
+    w = (torch.randn(c, c, 3, 3, 3, generator=g, dtype=torch.float64) / np.sqrt(c * 27)).float()
+    ps = ops.PackSet(dev)
+    gf, wf = ps.add(ops.conv_fwd_geom(n, sp, sp, c, c, 3, 1, 1), w.cuda(), L.PREC_BF16)
+    gd, wdp = ps.add(ops.conv_dgrad_geom(n, sp, sp, c, c, 3, 1, 1), w.cuda(), L.PREC_BF16)
+    ps.pack()
+    assert ops.bn_pre_ok(gf) and ops.bn_pre_ok(gd)
+    reps = 16
+    # z of the previous BatchNorm layer (bf16, as the chain keeps it), shifted so the mean matters
+    z16 = (torch.randn(n, *sp, c, generator=g) * 1.7 + 0.4).to(dev).bfloat16()
+    zk = z16.double().view(-1, c)
+    acc3 = torch.zeros(reps, 2, c, dtype=torch.float64, device=dev)
+    acc3[3, 0], acc3[3, 1] = zk.sum(0), (zk * zk).sum(0)  # one replica holds it all (any split sums alike)
+    acc3 = acc3.view(-1)
+    gamma = (torch.rand(c, generator=g) + 0.5).to(dev)
+    beta = (torch.randn(c, generator=g) * 0.2).to(dev)
+
+    def bufs():
+        return (torch.zeros(c, device=dev) + 0.1, torch.ones(c, device=dev) * 0.9,
+                torch.zeros((), dtype=torch.int64, device=dev))
+    # --- forward: reference pair
+    rm0, rv0, nb0 = bufs()
+    ss0, mi0 = torch.empty(2 * c, device=dev), torch.empty(2 * c, device=dev)
+    h16 = torch.empty(n, *sp, c, device=dev, dtype=torch.bfloat16)
+    zero0 = torch.ones(300, dtype=torch.float64, device=dev)
+    ops.bn_apply_acc(acc3, reps, c, nv, gamma, beta, rm0, rv0, nb0, ss0, mi0, z16, A, None, y16=h16, zero=zero0)
+    y0 = torch.empty(n, *sp, c, device=dev, dtype=torch.bfloat16)
+    accn0 = torch.zeros(reps * 2 * c, device=dev, dtype=torch.float64)
+    ops.conv(gf, h16.float(), wf, y0, ops.epilogue(x_bf16=h16, fuse=ops.BnFuse(accn0, 3, reps)))
+    # --- forward: folded
+    rm1, rv1, nb1 = bufs()
+    ss1, mi1 = torch.empty(2 * c, device=dev), torch.empty(2 * c, device=dev)
+    h16f = torch.full_like(h16, float("nan"))
+    zero1 = torch.ones(300, dtype=torch.float64, device=dev)
+    y1 = torch.empty_like(y0)
+    accn1 = torch.zeros_like(accn0)
+    pre = ops.BnPre.forward(acc3, reps, c, nv, gamma, beta, rm1, rv1, nb1, ss1, mi1, A, h16f, zero=zero1)
+    ops.conv(gf, z16.float(), wf, y1, ops.epilogue(x_bf16=z16, fuse=ops.BnFuse(accn1, 3, reps), pre=pre))
+    torch.cuda.synchronize()
+    assert torch.equal(h16f, h16), "folded forward: materialised operand"
+    assert torch.equal(y1, y0), "folded forward: conv output"
+    # fp64 atomics from many blocks: the sums agree up to their order of arrival
+    torch.testing.assert_close(accn1.view(reps, -1).sum(0), accn0.view(reps, -1).sum(0), rtol=1e-12, atol=1e-9)
+    for a_, b_, nm in ((ss1, ss0, "scale_shift"), (mi1, mi0, "mean_invstd"), (rm1, rm0, "running_mean"),
+                       (rv1, rv0, "running_var"), (nb1, nb0, "num_batches_tracked"), (zero1, zero0, "zero")):
+        assert torch.equal(a_, b_), f"folded forward: {nm}"
+    assert int(nb1) == 1 and float(zero1.abs().max()) == 0.0
+    # --- input-grad: dL/dy of this BatchNorm layer (bf16), its (sum g, sum g*xhat) replicas
+    dy16 = torch.randn(n, *sp, c, generator=g).to(dev).bfloat16()
+    sc, sh, mu, inv = ss0[:c].double(), ss0[c:].double(), mi0[:c].double(), mi0[c:].double()
+    gk = dy16.double().view(-1, c) * ((zk * sc + sh > 0).double() if act == "relu" else 1.0)
+    acc4 = torch.zeros(reps, 2, c, dtype=torch.float64, device=dev)
+    acc4[7, 0], acc4[7, 1] = gk.sum(0), (gk * (zk - mu) * inv).sum(0)
+    acc4 = acc4.view(-1)
+    skip = torch.randn(n, *sp, c, generator=g).to(dev)
+    dg0, db0 = torch.full((c,), 0.25, device=dev), torch.full((c,), -0.5, device=dev)
+    dz16 = torch.empty_like(z16)
+    zb0 = torch.ones(200, dtype=torch.float64, device=dev)
+    ops.bn_backward_acc(dy16, z16, nv, c, acc4, reps, ss0, mi0, gamma, A, dg0, db0, None, accumulate=True, dz16=dz16,
+                        zero=zb0)
+    dx0 = torch.empty(n, *sp, c, device=dev)
+    ops.conv(gd, dz16.float(), wdp, dx0, ops.epilogue(residual=skip, x_bf16=dz16))
+    dg1, db1 = torch.full((c,), 0.25, device=dev), torch.full((c,), -0.5, device=dev)
+    dz16f = torch.full_like(dz16, float("nan"))
+    zb1 = torch.ones(200, dtype=torch.float64, device=dev)
+    dx1 = torch.empty_like(dx0)
+    pre = ops.BnPre.backward(z16, acc4, reps, c, nv, ss0, mi0, gamma, A, dg1, db1, dz16f, accumulate=True, zero=zb1)
+    ops.conv(gd, dy16.float(), wdp, dx1, ops.epilogue(residual=skip, x_bf16=dy16, pre=pre))
+    torch.cuda.synchronize()
+    assert torch.equal(dz16f, dz16), "folded input-grad: materialised operand"
+    assert torch.equal(dx1, dx0), "folded input-grad: conv output"
+    for a_, b_, nm in ((dg1, dg0, "dgamma"), (db1, db0, "dbeta"), (zb1, zb0, "zero")):
+        assert torch.equal(a_, b_), f"folded input-grad: {nm}"
+
+
 @pytest.mark.parametrize("n,sp", [(2, (16, 16, 16)), (1, (5, 6, 9))])
 def test_conv_k3m_bf16_storage(n, sp):
     """conv_k3m with bf16 storage (cgan3d_epilogue.out_bf16, the ResNet chain's engine.zs / dys): a
@@ -929,3 +1024,110 @@ def test_wgrad_k3m_bf16(n, sp):
     ops.wgrad(gw, _cl(x), _cl(gy), dwa, ws, accumulate=True, gathered16=_cl(x).bfloat16(),
               aligned16=_cl(gy).bfloat16())
     assert_close(dwa.double().cpu().numpy(), 2 * dw.numpy(), 2e-5, "wk3m accumulate")
+
+
+@pytest.mark.parametrize("n,din", [(2, (16, 16, 16)), (1, (5, 6, 7)), (3, (8, 4, 12))])
+@pytest.mark.parametrize("role", ["convt_fwd", "conv_dgrad"])
+def test_conv_t64_bf16(n, din, role):
+    """The 32 <-> 64 level's stride-2 transposed conv with all eight parity classes per block (round 5,
+    conv_t64.hip): ConvTranspose3d 64 -> 32 forward (output padding 1) and the input-grad of the
+    Conv3d 32 -> 64 stride-2 (the same mapping).  Against torch float64 of the same bf16 operands at
+    2e-5 (fp32 accumulation of exact products), a bf16 output equal to the fp32 one rounded, the mode-3
+    statistics against the output's own sums and the mode-4 pairs against a float64 restatement.
+    Ragged class tiles in the second and third shapes."""
+    from cgan3d_amd import ops, _lib as L
+    g = torch.Generator().manual_seed(3 + n + din[0])
+    dout = tuple(2 * d for d in din)
+    x = torch.randn(n, 64, *din, generator=g, dtype=torch.float64).bfloat16().double()
+    if role == "convt_fwd":  # ConvTranspose3d weight [in 64, out 32, k, k, k]
+        w = (torch.randn(64, 32, 3, 3, 3, generator=g, dtype=torch.float64) / np.sqrt(64 * 8)).float()
+        yref = F.conv_transpose3d(x, w.bfloat16().double(), stride=2, padding=1, output_padding=1)
+        geo0 = ops.convt_fwd_geom(n, din, dout, 64, 32, 3, 2, 1)
+    else:  # Conv3d 32 -> 64 stride 2 (weight [64, 32, k, k, k]); its input-grad from dL/dz at din
+        w = (torch.randn(64, 32, 3, 3, 3, generator=g, dtype=torch.float64) / np.sqrt(64 * 8)).float()
+        yref = torch.nn.grad.conv3d_input((n, 32, *dout), w.bfloat16().double(), x, stride=2, padding=1)
+        geo0 = ops.conv_dgrad_geom(n, dout, din, 32, 64, 3, 2, 1)
+    ps = ops.PackSet(torch.device("cuda"))
+    geo, wp = ps.add(geo0, w.cuda(), L.PREC_BF16)
+    ps.pack()
+    assert geo.w_packed == 2 and geo.transposed and geo.cin == 64 and geo.cout == 32
+    xc, x16 = _cl(x), _cl(x).bfloat16()
+    reps = 16
+    y = torch.empty(n, *dout, 32, device="cuda")
+    acc3 = torch.zeros(reps * 2 * 32, device="cuda", dtype=torch.float64)
+    ops.conv(geo, xc, wp, y, ops.epilogue(x_bf16=x16, fuse=ops.BnFuse(acc3, 3, reps)))
+    assert_close(_ncdhw(y).numpy(), yref.numpy(), 2e-5, "t64 output")
+    yk = y.double().view(-1, 32).cpu()
+    a3 = acc3.view(reps, 2, 32).sum(0).cpu()
+    assert_close(a3[0].numpy(), yk.sum(0).numpy(), 1e-5, "t64 mode-3 sum")
+    assert_close(a3[1].numpy(), (yk * yk).sum(0).numpy(), 1e-5, "t64 mode-3 sum of squares")
+    y16 = torch.empty(n, *dout, 32, device="cuda", dtype=torch.bfloat16)
+    ops.conv(geo, xc, wp, y16, ops.epilogue(x_bf16=x16, fuse=ops.BnFuse(torch.zeros_like(acc3), 3, reps)))
+    assert torch.equal(y16, y.bfloat16()), "t64 bf16 output"
+    # mode 4: the BatchNorm-backward pairs of the layer whose dL/dy this is
+    z = torch.randn(n, *dout, 32, generator=g).cuda()
+    ss = torch.cat([torch.rand(32, generator=g) + 0.5, torch.randn(32, generator=g) * 0.1]).cuda()
+    mi = torch.cat([torch.randn(32, generator=g) * 0.1, torch.rand(32, generator=g) + 0.5]).cuda()
+    acc4 = torch.zeros_like(acc3)
+    y4 = torch.empty_like(y)
+    ops.conv(geo, xc, wp, y4, ops.epilogue(x_bf16=x16, bn_z=z, bn_ss=ss, bn_mi=mi, bn_act=L.ACT_RELU,
+                                           fuse=ops.BnFuse(acc4, 4, reps)))
+    assert torch.equal(y4, y)
+    zk, ssd, mid = z.double().view(-1, 32).cpu(), ss.double().cpu(), mi.double().cpu()
+    gg = yk * ((zk * ssd[:32] + ssd[32:]) > 0).double()
+    a4 = acc4.view(reps, 2, 32).sum(0).cpu()
+    assert_close(a4[0].numpy(), gg.sum(0).numpy(), 1e-5, "t64 mode-4 sum g")
+    assert_close(a4[1].numpy(), (gg * (zk - mid[:32]) * mid[32:]).sum(0).numpy(), 1e-5, "t64 mode-4 sum g xhat")
+
+
+@pytest.mark.parametrize("n,din", [(2, (32, 32, 32)), (1, (9, 12, 14)), (2, (17, 8, 24))])
+@pytest.mark.parametrize("role", ["conv_fwd", "convt_dgrad"])
+def test_conv_f64_bf16(n, din, role):
+    """The 32 <-> 64 level's stride-2 conv 32 -> 64 with every operand in LDS (round 5, conv_f64.hip):
+    the Conv3d forward (k3 s2 p1) and the input-grad of the ConvTranspose3d 64 -> 32 (the same
+    mapping).  Against torch float64 of the same bf16 operands at 2e-5, a bf16 output equal to the
+    fp32 one rounded, mode-3 statistics against the output's own sums and mode-4 pairs against a
+    float64 restatement.  Ragged output tiles (and odd input extents) in the last two shapes."""
+    from cgan3d_amd import ops, _lib as L
+    g = torch.Generator().manual_seed(7 + n + din[0])
+    dout = tuple((d - 1) // 2 + 1 for d in din)
+    x = torch.randn(n, 32, *din, generator=g, dtype=torch.float64).bfloat16().double()
+    if role == "conv_fwd":  # Conv3d weight [out 64, in 32, k, k, k]
+        w = (torch.randn(64, 32, 3, 3, 3, generator=g, dtype=torch.float64) / np.sqrt(32 * 27)).float()
+        yref = F.conv3d(x, w.bfloat16().double(), stride=2, padding=1)
+        geo0 = ops.conv_fwd_geom(n, din, dout, 32, 64, 3, 2, 1)
+    else:  # ConvTranspose3d 64 -> 32 (weight [in 64, out 32, k, k, k]) from dout to din; its input-grad
+        w = (torch.randn(64, 32, 3, 3, 3, generator=g, dtype=torch.float64) / np.sqrt(32 * 27)).float()
+        yref = F.conv3d(x, w.bfloat16().double(), stride=2, padding=1)  # the adjoint of conv_transpose3d
+        geo0 = ops.convt_dgrad_geom(n, dout, din, 64, 32, 3, 2, 1)
+    assert tuple(yref.shape[2:]) == dout
+    ps = ops.PackSet(torch.device("cuda"))
+    geo, wp = ps.add(geo0, w.cuda(), L.PREC_BF16)
+    ps.pack()
+    assert geo.w_packed == 2 and not geo.transposed and geo.cin == 32 and geo.cout == 64
+    xc, x16 = _cl(x), _cl(x).bfloat16()
+    reps = 16
+    y = torch.empty(n, *dout, 64, device="cuda")
+    acc3 = torch.zeros(reps * 2 * 64, device="cuda", dtype=torch.float64)
+    ops.conv(geo, xc, wp, y, ops.epilogue(x_bf16=x16, fuse=ops.BnFuse(acc3, 3, reps)))
+    assert_close(_ncdhw(y).numpy(), yref.numpy(), 2e-5, "f64 output")
+    yk = y.double().view(-1, 64).cpu()
+    a3 = acc3.view(reps, 2, 64).sum(0).cpu()
+    assert_close(a3[0].numpy(), yk.sum(0).numpy(), 1e-5, "f64 mode-3 sum")
+    assert_close(a3[1].numpy(), (yk * yk).sum(0).numpy(), 1e-5, "f64 mode-3 sum of squares")
+    y16 = torch.empty(n, *dout, 64, device="cuda", dtype=torch.bfloat16)
+    ops.conv(geo, xc, wp, y16, ops.epilogue(x_bf16=x16, fuse=ops.BnFuse(torch.zeros_like(acc3), 3, reps)))
+    assert torch.equal(y16, y.bfloat16()), "f64 bf16 output"
+    z = torch.randn(n, *dout, 64, generator=g).cuda()
+    ss = torch.cat([torch.rand(64, generator=g) + 0.5, torch.randn(64, generator=g) * 0.1]).cuda()
+    mi = torch.cat([torch.randn(64, generator=g) * 0.1, torch.rand(64, generator=g) + 0.5]).cuda()
+    acc4 = torch.zeros_like(acc3)
+    y4 = torch.empty_like(y)
+    ops.conv(geo, xc, wp, y4, ops.epilogue(x_bf16=x16, bn_z=z, bn_ss=ss, bn_mi=mi, bn_act=L.ACT_RELU,
+                                           fuse=ops.BnFuse(acc4, 4, reps)))
+    assert torch.equal(y4, y)
+    zk, ssd, mid = z.double().view(-1, 64).cpu(), ss.double().cpu(), mi.double().cpu()
+    gg = yk * ((zk * ssd[:64] + ssd[64:]) > 0).double()
+    a4 = acc4.view(reps, 2, 64).sum(0).cpu()
+    assert_close(a4[0].numpy(), gg.sum(0).numpy(), 1e-5, "f64 mode-4 sum g")
+    assert_close(a4[1].numpy(), (gg * (zk - mid[:64]) * mid[64:]).sum(0).numpy(), 1e-5, "f64 mode-4 sum g xhat")

@@ -570,6 +570,38 @@ def test_bf16_storage_matches_fp32_storage(monkeypatch):
     assert float(np.median([v["l2"] for v in rep.values()])) <= NOISE_MEDIAN_BAR, rep
 
 
+def test_bn_prologue_fold_matches_unfused_step(monkeypatch):
+    """The ResNet chain's BatchNorm passes folded into the next conv's staging (CGAN3D_DEBUG=bn_pre,
+    cgan3d_bn_pre; off by default, measured slower) against the default step: the same arithmetic
+    (test_gpu_ops.test_conv_k3m_bn_prologue pins each launch bit for bit), so one bf16 step from one
+    state agrees up to the fp64 accumulators' order of arrival — losses within 1e-5, every gradient
+    tensor within 1e-3 relative L2 (the bf16 step's own noise floor is ~0.07, test_bf16_storage_*)."""
+    from cgan3d_amd.data.synthetic import synth_patches
+    from cgan3d_amd.engine import StepEngine
+    g_args = dict(n_resnet_blocks=2, n_updownsample_blocks=2, init_channels_out=16)
+    S, b = 64, 2
+    engs = []
+    for flag in ("", "bn_pre"):
+        monkeypatch.setenv("CGAN3D_DEBUG", flag)
+        g, d = _models(g_args)
+        engs.append(StepEngine(g, d, g.config, d.config, b, b, (S, S, S), precision="bf16"))
+    base, fold = engs
+    assert not any(base.G.pre_f) and not any(base.G.pre_b)
+    assert sum(fold.G.pre_f) == 2 and sum(fold.G.pre_b) >= 3
+    opt, _ = synth_patches(b, S, 41)
+    sub, seg = synth_patches(b, S, 42)
+    bt = (torch.from_numpy(opt).cuda(), torch.from_numpy(sub).cuda(), torch.from_numpy(seg).cuda(),
+          torch.full((b,), 0.4, device="cuda"))
+    for e in engs:
+        e.load_inputs(*bt)
+        e.step()
+    np.testing.assert_allclose(fold.losses.cpu().numpy(), base.losses.cpu().numpy(), rtol=1e-5, atol=1e-7)
+    for a1, a2 in ((fold.g_arena, base.g_arena), (fold.d_arena, base.d_arena)):
+        for k in a1.gviews:
+            x, y = a1.gviews[k].cpu().double(), a2.gviews[k].cpu().double()
+            assert float((x - y).norm()) <= 1e-3 * max(float(y.norm()), 1e-30), k
+
+
 @pytest.mark.parametrize("b_opt,b_sub", [(3, 2), (2, 4)])
 def test_step_gp_resampled_batches_match_oracle(b_opt, b_sub):
     """|OPT| != |LOW|+|HIGH| with the gradient penalty: the reference resamples min(|real|, |fake|)

@@ -5,6 +5,11 @@
 Each case builds its operands once, warms up, captures 20 back-to-back launches in a HIP graph
 and times one replay between two HIP events; prints one line per (case, tuning value) with
 µs/launch and TFLOP/s (algorithmic).
+
+Phase probes (round 5; timing only, wrong results): build the probe library (make PROBES=1 in
+contrast-gan-3d_amd/csrc) and run with CGAN3D_LIB_PATH=contrast-gan-3d_amd/cgan3d_amd/probe/libcgan3d.so
+--tune 90=0,1,2,...: bit 1 skips the MFMA loop, 2 the operand loads / DMAs, 4 the unfold (k7m_n2w) or
+the partial stores (wgrad_k3m), 8 the output stores, 16 the statistics (common.h CG_PROBE).
 """
 import argparse
 import sys
@@ -103,7 +108,18 @@ def _cases(B=4, S=64):
         flops = 2.0 * B * r**3 * 64 * 64 * 27
         return (lambda: ops.conv(geo, x, w, y, ep)), flops
 
+    def k7_first_step():
+        """generator first conv (1 -> 16 k7 reflect) as the bf16 step issues it: bf16 z out, fp64
+        accumulator statistics (k7m_n2w_kernel<true>)"""
+        geo = ops.with_prec(ops.conv_fwd_geom(B, F3, F3, 1, 16, 7, 1, 3, True), BF)
+        w = t(16, 1, 7, 7, 7) * 0.05
+        x, y = t(B, *F3, 1), torch.empty(B, *F3, 16, device=dev, dtype=torch.bfloat16)
+        acc = torch.zeros(16 * 2 * 16, device=dev, dtype=torch.float64)
+        ep = ops.epilogue(fuse=ops.BnFuse(acc, 3, 16))
+        return (lambda: ops.conv(geo, x, w, y, ep)), 2.0 * B * S**3 * 16 * 343
+
     return {
+        "k7_first_step": lambda: k7_first_step(),
         "res_fwd_k3m": lambda: res_k3m(False),
         "res_dgrad_k3m": lambda: res_k3m(True),
         "res_fwd_k3m_r64": lambda: res_k3m(False, reps=64),

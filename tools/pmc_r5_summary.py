@@ -2,6 +2,7 @@
 
     python tools/pmc_r5_summary.py mfma  <pmc_dir> <trace_dir> --json profiles/r05_mfma_busy.json
     python tools/pmc_r5_summary.py hbm   <fetch_dir> <write_dir> <trace_dir> --json profiles/r05_b128_f32_pmc.json
+    python tools/pmc_r5_summary.py stall <pass_dir> [<pass_dir> ...] <trace_dir> --json profiles/r05_stalls.json
 
 mfma: SQ_VALU_MFMA_BUSY_CYCLES (cycles an MFMA occupies its SIMD, summed over SIMDs: 32 per
 v_mfma_f32_32x32x16_bf16, 16 per 16x16x32, MI355X_MICROARCH.md cycle-constants table) per dispatch
@@ -104,13 +105,52 @@ def hbm(a):
             "peak_gbs": HBM_PEAK_GBS, "kernels": out}
 
 
+def stall(a):
+    """Per-kernel instruction mix and wait fractions from several SQ passes: per dispatch medians,
+    ratios of counters in the same units (wave-cycles for SQ_WAVE_CYCLES / SQ_WAIT_* / SQ_ACTIVE_INST_*)."""
+    per = collections.defaultdict(dict)
+    for d in a.dirs[:-1]:
+        for key, cs in counters(d).items():
+            for c, v in cs.items():
+                per[key][c] = statistics.median(v)
+    dur = durations(a.dirs[-1])
+    out = []
+    for key, c in per.items():
+        g = lambda n: c.get(n, 0.0)
+        wc = g("SQ_WAVE_CYCLES")
+        mf = g("SQ_INSTS_MFMA")
+        us = statistics.mean(dur[key]) if key in dur else None
+        rec = {"kernel": key[0], "grid": key[1], "trace_us": round(us, 2) if us else None,
+               "launches_in_trace": len(dur.get(key, [])),
+               "valu_per_mfma": round(g("SQ_INSTS_VALU") / mf, 2) if mf else None,
+               "lds_per_mfma": round(g("SQ_INSTS_LDS") / mf, 2) if mf else None,
+               "vmem_rd_per_mfma": round(g("SQ_INSTS_VMEM_RD") / mf, 2) if mf else None,
+               "salu_per_mfma": round(g("SQ_INSTS_SALU") / mf, 2) if mf else None,
+               "lds_conflict_frac": round(g("SQ_LDS_BANK_CONFLICT") / g("SQ_LDS_IDX_ACTIVE"), 3) if g("SQ_LDS_IDX_ACTIVE") else None}
+        if wc:
+            for n in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_WAIT_INST_LDS", "SQ_ACTIVE_INST_VALU", "SQ_ACTIVE_INST_LDS",
+                      "SQ_ACTIVE_INST_VMEM", "SQ_ACTIVE_INST_MISC", "SQ_ACTIVE_INST_ANY"):
+                if n in c:
+                    rec[n[3:].lower() + "_frac"] = round(c[n] / wc, 3)
+        rec["raw"] = {k: c[k] for k in sorted(c)}
+        out.append(rec)
+    out.sort(key=lambda r: -(r["trace_us"] or 0) * max(r["launches_in_trace"], 1))
+    for r in out[:45]:
+        print(f"{r['kernel'][:38]:38s} g{r['grid']:8d} {r['trace_us'] or 0:6.1f}us valu/mfma {r['valu_per_mfma']} "
+              f"lds/mfma {r['lds_per_mfma']} vmem/mfma {r['vmem_rd_per_mfma']} confl {r['lds_conflict_frac']} "
+              f"wait {r.get('wait_any_frac')} winst {r.get('wait_inst_any_frac')} wlds {r.get('wait_inst_lds_frac')} "
+              f"valu {r.get('active_inst_valu_frac')} lds {r.get('active_inst_lds_frac')} vmem {r.get('active_inst_vmem_frac')}")
+    return {"source": "rocprofv3 --pmc passes (8 SQ counters each) over eager bench steps (64^3 B=4 bf16); durations: "
+                      "plan-mode kernel trace", "kernels": out}
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("what", choices=["mfma", "hbm"])
+    ap.add_argument("what", choices=["mfma", "hbm", "stall"])
     ap.add_argument("dirs", nargs="+")
     ap.add_argument("--json")
     a = ap.parse_args()
-    res = mfma(a) if a.what == "mfma" else hbm(a)
+    res = {"mfma": mfma, "hbm": hbm, "stall": stall}[a.what](a)
     if a.json:
         json.dump(res, open(a.json, "w"), indent=1)
 
