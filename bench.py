@@ -19,7 +19,8 @@ reference's basic_conf does), ``h2d`` (each batch copied from pinned host memory
 overlapped with the previous step — the PatchLoader's form; ``value`` stays HBM-resident), ``f32``
 (the exact-fp32 parity path at the same workload), ``b128_f32`` (BASELINE.json configs[2]: 128^3
 B=1 fp32) and ``cpu_baseline`` (the oracle — torch fp32 on the host cores — on a bounded sample,
-rank 0 only, N=1 only).  ``--no-sub`` skips h2d / f32 / b128_f32.
+rank 0 only, N=1 only).  ``loader`` (the drop-in Trainer fed by three PatchLoaders from int16 scans on disk, Trainer.fit's
+loop).  ``--no-sub`` skips the extra lines, ``--sub a,b`` picks some.
 
 Precision: ``--precision bf16`` (default; BASELINE.json's metric is quoted in bf16) runs every
 convolution on bf16 MFMA operands with fp32 accumulation, BatchNorm / losses / Adam in fp32;
@@ -195,7 +196,8 @@ def h2d_bench(eng, S, B, dev, steps):
         h = (torch.from_numpy(opt), torch.from_numpy(sub), torch.from_numpy(seg), torch.rand(B))
         host.append(tuple(t.pin_memory() for t in h))
         stage.append(tuple(torch.empty_like(t, device=dev) for t in h))
-    cs = torch.cuda.Stream(device=dev)
+    from cgan3d_amd import ops
+    cs = ops.pooled_stream(dev, "copy")  # the PatchLoader's copy stream (created with the engine's streams)
     main = torch.cuda.current_stream(dev)
     ready = [torch.cuda.Event() for _ in range(2)]
     freed = [None, None]
@@ -249,23 +251,80 @@ class _NullLogger:
         pass
 
 
-def bench_trainer(args, S, B, dev, world, rank, dist, batches):
-    """Trainer.train_step (cgan3d_amd.trainer.Trainer, constructed as train.py:154-176 does with the
-    GP conf's partials) on device-resident [OPT, LOW, HIGH] patch dicts; the generator trains every
-    iteration, as in the engine bench."""
+def _gp_trainer(iters, dev, precision):
+    """The drop-in Trainer as train.py:154-176 builds it with the GP conf's partials."""
     from functools import partial
     from torch import nn
     from cgan3d_amd.model.discriminator import PatchGANDiscriminator
     from cgan3d_amd.model.generator import ResnetGenerator
     from cgan3d_amd.model.loss import HULoss
     from cgan3d_amd.trainer.Trainer import Trainer
-    tr = Trainer(args.warmup + args.steps, 1, None, 1, 1, 10**9, 10**9,
-                 partial(ResnetGenerator, 4, 2, 16),
-                 partial(PatchGANDiscriminator, channels_in=1, init_channels_out=8, discriminator_depth=3,
-                         negative_slope=0.2, norm_layer=nn.Identity),
-                 partial(torch.optim.Adam, lr=1e-4, betas=(0.0, 0.9)), partial(torch.optim.Adam, lr=1e-4, betas=(0.0, 0.9)),
-                 HULoss(112.0 / 600.0, 212.0 / 600.0), _NullLogger(), dev, checkpoint_dir=None, checkpoint_every=None,
-                 precision=args.precision)
+    return Trainer(iters, 1, None, 1, 1, 10**9, 10**9,
+                   partial(ResnetGenerator, 4, 2, 16),
+                   partial(PatchGANDiscriminator, channels_in=1, init_channels_out=8, discriminator_depth=3,
+                           negative_slope=0.2, norm_layer=nn.Identity),
+                   partial(torch.optim.Adam, lr=1e-4, betas=(0.0, 0.9)), partial(torch.optim.Adam, lr=1e-4, betas=(0.0, 0.9)),
+                   HULoss(112.0 / 600.0, 212.0 / 600.0), _NullLogger(), dev, checkpoint_dir=None, checkpoint_every=None,
+                   precision=precision)
+
+
+def loader_bench(S, B, dev, steps, precision, warmup=5, workers=4):
+    """Trainer.train_step fed by create_dataloaders' PatchLoaders, the loop Trainer.fit runs
+    (Trainer.py:241-252): every iteration takes one batch per scan type (B OPT, B/2 LOW, B/2 HIGH)
+    from int16 [W,H,D,2] scans memory-mapped from disk (synthetic HU volumes written to a temporary
+    directory first), cropped by the host workers into pinned slots, copied to HBM on the copy stream
+    and unpacked / scaled there, then the step's launch plan."""
+    import shutil
+    import tempfile
+    from cgan3d_amd.data.synthetic import synth_patches
+    from cgan3d_amd.trainer.Trainer import ScanTypes
+    from cgan3d_amd.trainer.utils import create_dataloaders
+
+    class FZC:  # FactorZeroCenterScaler(238, 600) (basic_conf.py)
+        shift, factor = 238.0, 600.0
+
+    tmp = tempfile.mkdtemp(prefix="cgan3d_scans_")
+    loaders = ()
+    try:
+        fold = []
+        for i, label in enumerate((0, 0, 0, 0, -1, -1, 1, 1)):
+            vol, seg = synth_patches(1, S + 16, 500 + i)
+            hu = np.round(vol[0, 0].astype(np.float64) * 600.0 + 238.0).astype(np.int16)
+            p = f"{tmp}/scan{i}"
+            np.save(p + ".npy", np.stack([hu, seg[0, 0].astype(np.int16)], -1))
+            fold.append((p, label))
+        sizes = {0: B, -1: B // 2, 1: B - B // 2}
+        train, _ = create_dataloaders(fold, fold[:1], (S,) * 3, (S,) * 3, sizes, {0: 1}, np.random.default_rng(3),
+                                      scaler=FZC(), num_workers=(workers, 1), device=dev)
+        loaders = tuple(train.values())
+        tr = _gp_trainer(warmup + steps, dev, precision)
+        it = 0
+        for _ in range(max(warmup, 3)):  # first: eager; second: the plan is recorded and run
+            tr.train_step([next(train[st]) for st in ScanTypes], it)
+            it += 1
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            tr.train_step([next(train[st]) for st in ScanTypes], it)
+            it += 1
+        torch.cuda.synchronize()
+        el = time.perf_counter() - t0
+        mb = sum(ld._host[0].numel() * ld._host[0].element_size() for ld in loaders) / 1e6
+        return {"value": round(B * steps / el, 3), "unit": "patches/s", "ms_per_step": round(el / steps * 1e3, 3),
+                "steps": steps, "h2d_mb_per_step": round(mb, 2), "host_workers_per_loader": workers,
+                "timing": "Trainer.train_step on next() of three PatchLoaders per iteration (Trainer.fit's loop): "
+                          "int16 crops from mmap'd .npy scans, pinned slots, H2D on the copy stream, GPU unpack"}
+    finally:
+        for ld in loaders:
+            ld._finish()
+        shutil.rmtree(tmp, ignore_errors=True)
+
+
+def bench_trainer(args, S, B, dev, world, rank, dist, batches):
+    """Trainer.train_step (cgan3d_amd.trainer.Trainer, constructed as train.py:154-176 does with the
+    GP conf's partials) on device-resident [OPT, LOW, HIGH] patch dicts; the generator trains every
+    iteration, as in the engine bench."""
+    tr = _gp_trainer(args.warmup + args.steps, dev, args.precision)
     h = B // 2
     pl = []
     for opt, sub, seg, _ in batches:
@@ -323,7 +382,7 @@ def main():
     ap.add_argument("--no-sub", action="store_true",
                     help="skip the extra lines (h2d: batches from pinned host memory; f32: the exact-fp32 path; "
                          "b128_f32: BASELINE configs[2], 128^3 B=1 fp32)")
-    ap.add_argument("--sub", default="h2d,f32,b128_f32,b128_bf16_b2",
+    ap.add_argument("--sub", default="h2d,loader,f32,b128_f32,b128_bf16_b2",
                     help="comma list of the extra lines to run (default all; --no-sub: none)")
     ap.add_argument("--precision", choices=["f32", "bf16"], default="bf16",
                     help="MFMA operand precision of the convolutions (accumulation is f32)")
@@ -545,6 +604,10 @@ def main():
         if "h2d" in subs:
             out["h2d"] = h2d_bench(eng, S, B, dev, args.steps)
         del eng
+        torch.cuda.empty_cache()
+        # the drop-in Trainer fed by the PatchLoaders (the loop train.py's Trainer.fit runs)
+        if "loader" in subs:
+            out["loader"] = loader_bench(S, B, dev, args.steps, args.precision)
         torch.cuda.empty_cache()
         # the other single-GPU BASELINE configs in the same run: the exact-fp32 parity path at this
         # workload, and configs[2] (128^3 B=1 fp32)

@@ -150,6 +150,7 @@ _SIGS = {
     "cgan3d_conv3d_wgrad_sk": ([_P, _P, _P, _P, _P, _I32, _P], _I32),
     "cgan3d_tanh_backward": ([_P, _P, _P, _I64, _P], _I32),
     "cgan3d_unpack_patches": ([_P, _I32, _I64, _F, _F, _P, _P, _P], _I32),
+    "cgan3d_unpack_patches_ex": ([_P, _I32, _I64, _F, _F, _P, _P, _I32, _P], _I32),
     "cgan3d_augment_ws_floats": ([_I32, _I32, _I32, _I32, _I32], _I64),
     "cgan3d_patch_accumulate": ([_P, _I32, _I32, _I32, _I32, _P, _P, _P, _I32, _I32, _I32, _P], _I32),
     "cgan3d_patch_normalize": ([_P, _P, _I64, _P], _I32),
@@ -168,6 +169,9 @@ _SIGS = {
     "cgan3d_adam_pack": ([_P, _P, _P, _P, _I64, _P, _P, _I32, _P, _P], _I32),
     "cgan3d_zero": ([_P, _I64, _P], _I32),
     "cgan3d_copy_multi": ([_P, _P, _P, _I32, _P], _I32),
+    "cgan3d_copy_multi_ex": ([_P, _P, _P, _I32, _I32, _P], _I32),
+    "cgan3d_host_alloc": ([_I64, _P, _P], _I32),
+    "cgan3d_host_free": ([_P], _I32),
     "cgan3d_wgrad_unpack_multi": ([_P, _I32, _I64, _P], _I32),
     "cgan3d_ln_partial_doubles": ([_I32, _I64], _I64),
     "cgan3d_ln_reduce": ([_P, _P, _P], _I32),

@@ -13,12 +13,16 @@ Per batch:
   than the patch are zero-padded symmetrically (batchgenerators ``pad_nd_image``:
   below = diff // 2, above = the rest), the others are cropped at a uniformly random offset
   (``crop(..., crop_type="random")``), drawn here from the loader's ``numpy.random.Generator``;
-* one asynchronous host-to-device copy per batch runs on the loader's own HIP stream, followed
-  by ``cgan3d_unpack_patches``, which de-interleaves and scales on the GPU
-  ((HU - shift) / factor, ``FactorZeroCenterScaler``, ``data/Scaler.py:37-45``);
-* ``depth`` batches are in flight: while the trainer computes on batch j, batch j+1 is being
-  read on the host and copied over PCIe.  A returned batch's tensors live in a ring slot and are
-  overwritten ``depth`` batches later (the Trainer consumes each batch within its step).
+* the pinned slots are mapped into the device (``cgan3d_host_alloc``) and one launch of
+  ``cgan3d_unpack_patches_ex`` on the copy stream (``ops.pooled_stream(dev, "copy")``, shared by
+  the loaders of a device) reads a slot over PCIe, de-interleaves and scales it on the GPU
+  ((HU - shift) / factor, ``FactorZeroCenterScaler``, ``data/Scaler.py:37-45``) — no separate SDMA
+  copy (``zero_copy=False``: pinned slot, async copy into a device slot, then the unpack);
+* ``depth`` batches are in flight: host workers read ahead, and ``next()`` also issues the device
+  work of the following batches whose host reads are done, each ordered only after the consumers of
+  its slot's previous batch, so batch j+1 crosses PCIe while the step on batch j runs.  A returned
+  batch's tensors live in a ring slot and are overwritten ``depth`` batches later (the Trainer
+  consumes each batch within its step).
 
 * augmentation (optional ``transform``, ``data/augment.py``: batchgenerators'
   ``SpatialTransform_2`` as ``basic_conf.py:87-113`` configures it, and ``MirrorTransform`` after it
@@ -186,7 +190,8 @@ def sample_2d(shape: Sequence[int], meta: dict, patch: Sequence[int], rng: np.ra
 class PatchLoader:
     def __init__(self, data: List[str], patch_shape: Sequence[int], batch_size: int, rng: np.random.Generator,
                  scaler=None, infinite: bool = True, shuffle: bool = True, device=None, depth: int = 3,
-                 num_threads: int = 4, seed_for_shuffle: Optional[int] = None, transform=None):
+                 num_threads: int = 4, seed_for_shuffle: Optional[int] = None, transform=None,
+                 zero_copy: bool = True):
         if len(patch_shape) not in (2, 3):
             raise ValueError(f"PatchLoader: 2-D or 3-D patches, got {tuple(patch_shape)}")
         self.paths = [str(p) for p in data]
@@ -205,8 +210,18 @@ class PatchLoader:
         # which is what generate_one casts to before cropping
         self.dtype = torch.int16 if probe.dtype == np.int16 else torch.float32
         shp = (batch_size, *self.patch, 2)
-        self._host = [torch.empty(shp, dtype=self.dtype).pin_memory() for _ in range(self.depth)]
-        self._raw = [torch.empty(shp, dtype=self.dtype, device=self.device) for _ in range(self.depth)]
+        # zero_copy (round 5): the pinned slots are mapped into the device (cgan3d_host_alloc) and the
+        # unpack kernel reads them over PCIe on a few blocks — one launch per batch, no host-blocking SDMA
+        # copy (a torch non-blocking copy of a 4 MB pinned slot held the host ~0.3 ms, the step ~0.1 ms
+        # slower: tools/h2d_probe.py); False: pinned slots, SDMA copy into a device slot, then the unpack
+        self.zero_copy = bool(zero_copy)
+        if self.zero_copy:
+            self._mapped = [ops.MappedHost(shp, self.dtype) for _ in range(self.depth)]
+            self._host = [m.tensor for m in self._mapped]
+            self._raw = None
+        else:
+            self._host = [torch.empty(shp, dtype=self.dtype).pin_memory() for _ in range(self.depth)]
+            self._raw = [torch.empty(shp, dtype=self.dtype, device=self.device) for _ in range(self.depth)]
         self._data = [torch.empty((batch_size, 1, *self.patch), device=self.device) for _ in range(self.depth)]
         self._seg = [torch.empty((batch_size, 1, *self.patch), dtype=torch.bool, device=self.device)
                      for _ in range(self.depth)]
@@ -230,8 +245,9 @@ class PatchLoader:
         if self.transforms:  # ping-pong with staging buffers so that the last transform writes the returned ones
             self._pre_data = [torch.empty_like(t) for t in self._data]
             self._pre_seg = [torch.empty_like(t) for t in self._seg]
-        ops.pooled_stream(self.device, "g_side")  # the engines' streams first: their queue mapping stays fixed
-        self._stream = torch.cuda.Stream(device=self.device)
+        # one copy stream shared by every loader of the device, created with the engines' streams
+        # (ops.pooled_stream): the engines' hardware-queue mapping does not depend on how many loaders exist
+        self._stream = ops.pooled_stream(self.device, "copy")
         self._threads, self._pool = num_threads, None
         self._lock = threading.Lock()
         self._order_rng = np.random.default_rng(seed_for_shuffle)
@@ -307,7 +323,12 @@ class PatchLoader:
         if self._pool is None:
             self._pool = ThreadPoolExecutor(max_workers=self._threads)
         self._pending, self._next_slot, self._pos, self._order = {}, 0, 0, []
-        self._consume = 0
+        self._consume, self._ready, self._last = 0, {}, None
+        # every slot's device buffers are free once the work enqueued so far has run
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(self.device))
+        self._free = [ev] * self.depth
+        self._aug_keep = [None] * self.depth
         for _ in range(self.depth - 1):
             if not self._submit():
                 break
@@ -322,34 +343,62 @@ class PatchLoader:
     def __iter__(self):
         return self
 
-    def __next__(self) -> dict:
-        self._submit()  # keep depth - 1 batches ahead
-        slot = self._consume
-        fut = self._pending.pop(slot, None)
-        if fut is None:
-            raise StopIteration
-        picks, aug = fut.result()
-        self._consume = (slot + 1) % self.depth
-        cur = torch.cuda.current_stream(self.device)
-        # work enqueued so far (the consumers of the batch that last used this slot) precedes the copy
-        self._stream.wait_stream(cur)
+    def _issue(self, slot: int):
+        """Queue the slot's host-to-device copy, unpack and transforms on the copy stream, ordered
+        only after the consumers of the batch that last used the slot's device buffers."""
+        picks, aug = self._pending.pop(slot).result()
+        self._stream.wait_event(self._free[slot])
         with torch.cuda.stream(self._stream):
-            self._raw[slot].copy_(self._host[slot], non_blocking=True)
+            bufs = [(self._data[slot], self._seg[slot]), (self._pre_data[slot], self._pre_seg[slot])] \
+                if aug is not None else [(self._data[slot], self._seg[slot])]
+            k = len(self.transforms) % 2 if aug is not None else 0  # the last transform ends in _data
+            if self.zero_copy:
+                ops.unpack_patches_mapped(self._mapped[slot], *bufs[k], self.shift, self.factor)
+            else:
+                self._raw[slot].copy_(self._host[slot], non_blocking=True)
             ev = torch.cuda.Event()
             ev.record(self._stream)
-            self._copied[slot] = ev
-            if aug is None:
-                ops.unpack_patches(self._raw[slot], self._data[slot], self._seg[slot], self.shift, self.factor)
-            else:
-                bufs = [(self._data[slot], self._seg[slot]), (self._pre_data[slot], self._pre_seg[slot])]
-                k = len(self.transforms) % 2  # buffer the unpack writes: the last transform ends in _data
+            self._copied[slot] = ev  # the host slot is free once this has run
+            if not self.zero_copy:
                 ops.unpack_patches(self._raw[slot], *bufs[k], self.shift, self.factor)
+            if aug is not None:
                 for t, prm in zip(self.transforms, aug):
                     dev = tuple(None if a is None else a.to(self.device, non_blocking=True) for a in prm)
                     t.run(dev, *bufs[k], *bufs[1 - k], ws=self._aug_ws)
                     k = 1 - k
-                self._aug_keep = aug  # pinned sources alive until the next batch's copies are queued
-        cur.wait_stream(self._stream)
+                self._aug_keep[slot] = aug  # pinned sources alive until the slot is refilled
+            ready = torch.cuda.Event()
+            ready.record(self._stream)
+        self._ready[slot] = (ready, picks)
+
+    def __next__(self) -> dict:
+        cur = torch.cuda.current_stream(self.device)
+        if self._last is not None:
+            # the batch handed out last has had its consumers enqueued by now: its slot is free once
+            # they have run
+            ev = torch.cuda.Event()
+            ev.record(cur)
+            self._free[self._last] = ev
+        self._submit()  # keep depth - 1 batches ahead
+        slot = self._consume
+        if slot not in self._ready:
+            if slot not in self._pending:
+                raise StopIteration
+            self._issue(slot)
+        ready, picks = self._ready.pop(slot)
+        self._consume = (slot + 1) % self.depth
+        self._last = slot
+        # the following batches whose host reads are done go over PCIe now, while the caller's step
+        # on this batch runs (round 4 issued each copy only when its batch was asked for, behind the
+        # whole previous step)
+        nxt = self._consume
+        for _ in range(self.depth - 1):
+            fut = self._pending.get(nxt)
+            if fut is None or not fut.done():
+                break
+            self._issue(nxt)
+            nxt = (nxt + 1) % self.depth
+        cur.wait_event(ready)
         names = [Path(self.paths[i]).name for i, _ in picks]
         return {"data": self._data[slot], "seg": self._seg[slot], "name": names,
                 "path": [self.paths[i] for i, _ in picks]}

@@ -377,7 +377,7 @@ def stream_wait(waiter, signaler):
 
 
 _STREAM_POOL: Dict[int, Dict[str, "torch.cuda.Stream"]] = {}
-POOL_ROLES = ("g_side", "d_side", "comm")
+POOL_ROLES = ("g_side", "d_side", "comm", "copy")  # copy: host-to-device batches (PatchLoader)
 
 
 def pooled_stream(device, role: str) -> "torch.cuda.Stream":
@@ -1279,6 +1279,66 @@ def unpack_patches(src: torch.Tensor, data: torch.Tensor, seg: torch.Tensor, shi
         raise TypeError("unpack_patches: seg must be bool or uint8")
     check(_launch("cgan3d_unpack_patches", ptr(src), 0 if src.dtype == torch.int16 else 1, nvox, float(shift),
                   float(factor), ptr(data), ptr(seg)), "unpack_patches")
+
+
+class MappedHost:
+    """Pinned host memory mapped into the device's address space (include/cgan3d.h cgan3d_host_alloc):
+    ``tensor`` is a CPU view the host fills, ``dev`` the address kernels read it at over PCIe
+    (copy_multi_ex / unpack_patches_ex on a copy stream): a batch reaches HBM in one small launch
+    instead of a host-blocking SDMA copy (tools/h2d_probe.py)."""
+
+    def __init__(self, shape, dtype: torch.dtype):
+        numel = 1
+        for s in shape:
+            numel *= int(s)
+        item = torch.empty((), dtype=dtype).element_size()
+        self.nbytes = max(16, (numel * item + 15) // 16 * 16)
+        h, d = ctypes.c_void_p(), ctypes.c_void_p()
+        check(L.lib().cgan3d_host_alloc(self.nbytes, ctypes.byref(h), ctypes.byref(d)), "host_alloc")
+        self.host, self.dev = h.value, d.value
+        self._buf = (ctypes.c_uint8 * self.nbytes).from_address(self.host)
+        self.tensor = torch.frombuffer(self._buf, dtype=dtype, count=numel).view(tuple(int(s) for s in shape))
+        self._lib = L.lib()
+
+    def __del__(self):
+        host, self.host = getattr(self, "host", None), None
+        if host:
+            self.tensor = self._buf = None
+            self._lib.cgan3d_host_free(ctypes.c_void_p(host))
+
+
+def copy_h2d(pairs, max_blocks: int = 32):
+    """Copy each (MappedHost, contiguous device tensor of its byte size) pair on the current stream in one
+    launch of at most ``max_blocks`` workgroups reading the host memory over PCIe (cgan3d_copy_multi_ex)."""
+    if not 0 < len(pairs) <= 8:
+        raise ValueError("copy_h2d: 1..8 pairs")
+    for mh, d in pairs:
+        nb = d.numel() * d.element_size()
+        if not (d.is_cuda and d.is_contiguous()) or nb > mh.nbytes:
+            raise ValueError("copy_h2d: destination must be a contiguous device tensor within the host buffer")
+    n = len(pairs)
+    src = (ctypes.c_void_p * n)(*[mh.dev for mh, _ in pairs])
+    dst = (ctypes.c_void_p * n)(*[d.data_ptr() for _, d in pairs])
+    nb = (ctypes.c_int64 * n)(*[d.numel() * d.element_size() for _, d in pairs])
+    check(_launch("cgan3d_copy_multi_ex", src, dst, nb, n, int(max_blocks)), "copy_h2d")
+
+
+def unpack_patches_mapped(src: MappedHost, data: torch.Tensor, seg: torch.Tensor, shift: float, factor: float,
+                          max_blocks: int = 64):
+    """unpack_patches from a mapped host buffer (int16 or float32 [..., 2]) straight into the device
+    tensors: the loader's host-to-HBM step in one launch (cgan3d_unpack_patches_ex)."""
+    t = src.tensor
+    if t.dtype not in (torch.int16, torch.float32) or t.shape[-1] != 2:
+        raise TypeError("unpack_patches_mapped: src must be int16 / float32 [..., 2]")
+    nvox = t.numel() // 2
+    if not (data.is_cuda and seg.is_cuda):
+        raise ValueError("unpack_patches_mapped: data and seg must be device tensors")
+    _need(data, nvox, "unpack_patches_mapped data")
+    _need(seg, nvox, "unpack_patches_mapped seg", dtype=seg.dtype)
+    if seg.dtype not in (torch.bool, torch.uint8):
+        raise TypeError("unpack_patches_mapped: seg must be bool or uint8")
+    check(_launch("cgan3d_unpack_patches_ex", src.dev, 0 if t.dtype == torch.int16 else 1, nvox, float(shift),
+                  float(factor), ptr(data), ptr(seg), int(max_blocks)), "unpack_patches_mapped")
 
 
 def augment_ws_floats(n: int, dims, n_elastic: int) -> int:

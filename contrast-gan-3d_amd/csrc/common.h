@@ -284,6 +284,7 @@ bool f64_geom_ok(const cgan3d_conv_geom* g);
 bool f64_ok(const cgan3d_conv_geom* g, const Epi& e);
 int f64_launch(const cgan3d_conv_geom* g, const __bf16* wp, float* y, const Epi& e, hipStream_t st);
 void k3m_set(int v);
+bool k3m_enabled();  // key 15: the LDS-resident ResNet-block and 32 <-> 64 level kernels
 void k7wg_blocks_set(int v);
 bool halo_ok(const cgan3d_conv_geom* g);         // w_packed == 2 and eligible
 bool halo_format_ok(const cgan3d_conv_geom* g);  // eligible ignoring w_packed

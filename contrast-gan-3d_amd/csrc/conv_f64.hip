@@ -254,10 +254,10 @@ __global__ __launch_bounds__(256, 1) void conv_f64_kernel(F64Args a, const __bf1
 // Conv3d k3 s2 p1 32 -> 64 with the bf16 input shadow and format-2 packed weights; epilogue: output
 // (fp32 / bf16) + fp64-accumulator statistics (mode 3 / 4) or nothing
 bool f64_geom_ok(const cgan3d_conv_geom* g) {
-#if defined(CGAN3D_NO_T64) || !defined(CGAN3D_T64_VALIDATED)
-  return false;  // (pending its first GPU validation run)
+#if defined(CGAN3D_NO_T64)
+  return false;  // (A/B builds)
 #endif
-  return g->prec == CGAN3D_PREC_BF16 && g->w_packed == 2 && !g->transposed && !g->reflect && !g->planar && g->k == 3 &&
+  return k3m_enabled() && g->prec == CGAN3D_PREC_BF16 && g->w_packed == 2 && !g->transposed && !g->reflect && !g->planar && g->k == 3 &&
          g->stride == 2 && g->pad == 1 && g->cin == 32 && g->cout == 64 && g->do_ == (g->di - 1) / 2 + 1 &&
          g->ho == (g->hi - 1) / 2 + 1 && g->wo == (g->wi - 1) / 2 + 1 &&
          (long long)g->n * g->di * g->hi * g->wi * 32 < (1LL << 31) &&

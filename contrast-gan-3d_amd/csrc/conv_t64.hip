@@ -302,10 +302,10 @@ __global__ __launch_bounds__(256, 1) void conv_t64_kernel(T64Args a, const __bf1
 // ConvTranspose3d k3 s2 p1 (output padding 1) 64 -> 32 with the bf16 input shadow and format-2 packed
 // weights, epilogue: output (fp32 / bf16) + fp64-accumulator statistics (mode 3 / 4) or nothing
 bool t64_geom_ok(const cgan3d_conv_geom* g) {
-#if defined(CGAN3D_NO_T64) || !defined(CGAN3D_T64_VALIDATED)
-  return false;  // (pending its first GPU validation run)
+#if defined(CGAN3D_NO_T64)
+  return false;  // (A/B builds)
 #endif
-  return g->prec == CGAN3D_PREC_BF16 && g->w_packed == 2 && g->transposed && !g->reflect && !g->planar && g->k == 3 &&
+  return k3m_enabled() && g->prec == CGAN3D_PREC_BF16 && g->w_packed == 2 && g->transposed && !g->reflect && !g->planar && g->k == 3 &&
          g->stride == 2 && g->pad == 1 && g->cin == 64 && g->cout == 32 && g->do_ == 2 * g->di &&
          g->ho == 2 * g->hi && g->wo == 2 * g->wi && (long long)g->n * g->do_ * g->ho * g->wo * 32 < (1LL << 31);
 }

@@ -18,9 +18,66 @@ __global__ __launch_bounds__(256) void unpack_patches_kernel(const T* __restrict
   }
 }
 
+// Four voxels per thread from 16-byte loads (int16 pairs: one load; float32 pairs: two), 16-byte data
+// and 4-byte mask stores: the form for a source in mapped host memory, read over PCIe by a few blocks
+// beside the step (cgan3d_unpack_patches_ex); the voxels past the last full quad by block 0.
+template <typename T>
+__global__ __launch_bounds__(256) void unpack4_patches_kernel(const T* __restrict__ src, long long nvox, float shift,
+                                                              float factor, float* __restrict__ data,
+                                                              unsigned char* __restrict__ seg) {
+  const long long n4 = nvox >> 2;
+  for (long long q = (long long)blockIdx.x * blockDim.x + threadIdx.x; q < n4; q += (long long)gridDim.x * blockDim.x) {
+    T v[8];
+    const uint4* s4 = reinterpret_cast<const uint4*>(src);
+    if constexpr (sizeof(T) == 2) {
+      const uint4 u = s4[q];
+      __builtin_memcpy(v, &u, 16);
+    } else {
+      const uint4 u0 = s4[2 * q], u1 = s4[2 * q + 1];
+      __builtin_memcpy(v, &u0, 16);
+      __builtin_memcpy(v + 4, &u1, 16);
+    }
+    float4 d;
+    d.x = ((float)v[0] - shift) / factor;
+    d.y = ((float)v[2] - shift) / factor;
+    d.z = ((float)v[4] - shift) / factor;
+    d.w = ((float)v[6] - shift) / factor;
+    uchar4 m;
+    m.x = (float)v[1] != 0.f;
+    m.y = (float)v[3] != 0.f;
+    m.z = (float)v[5] != 0.f;
+    m.w = (float)v[7] != 0.f;
+    reinterpret_cast<float4*>(data)[q] = d;
+    reinterpret_cast<uchar4*>(seg)[q] = m;
+  }
+  if (blockIdx.x == 0)
+    for (long long v = 4 * n4 + threadIdx.x; v < nvox; v += blockDim.x) {
+      data[v] = ((float)src[2 * v] - shift) / factor;
+      seg[v] = (float)src[2 * v + 1] != 0.f;
+    }
+}
+
 }  // namespace cg
 
 using namespace cg;
+
+extern "C" int cgan3d_unpack_patches_ex(const void* src, int32_t src_dtype, int64_t nvox, float shift, float factor,
+                                        float* data, uint8_t* seg, int32_t max_blocks, void* stream) {
+  CG_CHECK_ARG(src && data && seg && nvox > 0 && factor != 0.f && max_blocks > 0, "cgan3d_unpack_patches_ex: bad args");
+  CG_CHECK_ARG(src_dtype == 0 || src_dtype == 1, "cgan3d_unpack_patches_ex: src_dtype must be 0 (int16) or 1 (float32)");
+  CG_CHECK_ARG(!(reinterpret_cast<uintptr_t>(src) & 15) && !(reinterpret_cast<uintptr_t>(data) & 15) &&
+                   !(reinterpret_cast<uintptr_t>(seg) & 3),
+               "cgan3d_unpack_patches_ex: src / data 16-byte and seg 4-byte aligned");
+  const int blocks = (int)std::max<long long>(1, std::min<long long>((nvox / 4 + 255) / 256, max_blocks));
+  if (src_dtype == 0)
+    ::cg::launch(unpack4_patches_kernel<int16_t>, dim3(blocks), dim3(256), 0, (hipStream_t)stream,
+                 static_cast<const int16_t*>(src), (long long)nvox, shift, factor, data, seg);
+  else
+    ::cg::launch(unpack4_patches_kernel<float>, dim3(blocks), dim3(256), 0, (hipStream_t)stream,
+                 static_cast<const float*>(src), (long long)nvox, shift, factor, data, seg);
+  CG_LAUNCH_CHECK("unpack4_patches_kernel");
+  return CGAN3D_OK;
+}
 
 extern "C" int cgan3d_unpack_patches(const void* src, int32_t src_dtype, int64_t nvox, float shift, float factor,
                                      float* data, uint8_t* seg, void* stream) {

@@ -283,7 +283,12 @@ __global__ __launch_bounds__(256) void copy_multi_kernel(CopySegs c) {
 
 extern "C" int cgan3d_copy_multi(const void* const* src, void* const* dst, const int64_t* bytes, int32_t n,
                                  void* stream) {
-  CG_CHECK_ARG(src && dst && bytes && n > 0 && n <= ::cg::COPY_SEGS, "cgan3d_copy_multi: bad args");
+  return cgan3d_copy_multi_ex(src, dst, bytes, n, 2048, stream);
+}
+
+extern "C" int cgan3d_copy_multi_ex(const void* const* src, void* const* dst, const int64_t* bytes, int32_t n,
+                                    int32_t max_blocks, void* stream) {
+  CG_CHECK_ARG(src && dst && bytes && n > 0 && n <= ::cg::COPY_SEGS && max_blocks > 0, "cgan3d_copy_multi: bad args");
   ::cg::CopySegs c{};
   c.n = n;
   c.start[0] = 0;
@@ -299,9 +304,37 @@ extern "C" int cgan3d_copy_multi(const void* const* src, void* const* dst, const
   }
   const long long total = c.start[n];
   if (total == 0) return CGAN3D_OK;
-  const unsigned blocks = (unsigned)std::min<long long>((total + 255) / 256, 2048);
+  const unsigned blocks = (unsigned)std::min<long long>((total + 255) / 256, max_blocks);
   ::cg::launch(::cg::copy_multi_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, c);
   CG_LAUNCH_CHECK("copy_multi_kernel");
+  return CGAN3D_OK;
+}
+
+// Pinned host memory mapped into the device's address space (hipHostMallocMapped): kernels read it
+// over PCIe through *dev, so a batch in such a buffer reaches HBM by a small copy / unpack kernel on
+// the copy stream instead of a host-blocking SDMA transfer (tools/h2d_probe.py).
+extern "C" int cgan3d_host_alloc(int64_t bytes, void** host, void** dev) {
+  CG_CHECK_ARG(bytes > 0 && host && dev, "cgan3d_host_alloc: bad args");
+  *host = nullptr;
+  *dev = nullptr;
+  if (hipHostMalloc(host, (size_t)bytes, hipHostMallocMapped) != hipSuccess || *host == nullptr) {
+    set_error("cgan3d_host_alloc: hipHostMalloc(%lld) failed", (long long)bytes);
+    return CGAN3D_EHIP;
+  }
+  if (hipHostGetDevicePointer(dev, *host, 0) != hipSuccess || *dev == nullptr) {
+    (void)hipHostFree(*host);
+    *host = nullptr;
+    set_error("cgan3d_host_alloc: no device mapping");
+    return CGAN3D_EHIP;
+  }
+  return CGAN3D_OK;
+}
+
+extern "C" int cgan3d_host_free(void* host) {
+  if (host && hipHostFree(host) != hipSuccess) {
+    set_error("cgan3d_host_free failed");
+    return CGAN3D_EHIP;
+  }
   return CGAN3D_OK;
 }
 

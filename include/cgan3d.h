@@ -212,7 +212,8 @@ const char* cgan3d_get_last_error(void);
  * correct configuration (anything else: CGAN3D_EINVAL): 9 voxel chunks of the ResNet weight grad
  * (default 28, 0 = generic kernel); 10 blocks of the stride-2 weight grad (default 128, 0 = generic);
  * 13 output planes per streamed last-conv block (0 auto, 8, 16, -1 = Toeplitz kernel); 15 ResNet convs
- * on conv_k3m (1, default) or conv_k3 (0); 16 ResNet weight grads on wgrad_k3m (1, default) or
+ * on conv_k3m and the 32 <-> 64 stride-2 pair on conv_t64 / conv_f64 (1, default) or all of them on the
+ * round-3 halo kernels conv_k3 / conv_halo (0); 16 ResNet weight grads on wgrad_k3m (1, default) or
  * wgrad_k3 (0); 20 most blocks of a k7 weight grad (default 512). */
 int cgan3d_set_tuning(int32_t key, int32_t value);
 
@@ -455,6 +456,11 @@ int cgan3d_tanh_backward(const float* y, const float* dy, float* dz, int64_t n, 
  *     seg = label != 0 --- */
 int cgan3d_unpack_patches(const void* src, int32_t src_dtype, int64_t nvox, float shift, float factor,
                           float* data, uint8_t* seg, void* stream);
+/* The same on at most max_blocks workgroups, four voxels per thread from 16-byte loads (src and data
+ * 16-byte aligned, seg 4-byte aligned): src may be mapped host memory (cgan3d_host_alloc's *dev), so
+ * the batch goes from the loader's pinned slot to its HBM tensors in this one launch. */
+int cgan3d_unpack_patches_ex(const void* src, int32_t src_dtype, int64_t nvox, float shift, float factor,
+                             float* data, uint8_t* seg, int32_t max_blocks, void* stream);
 /* --- spatial augmentation (experiments/basic_conf.py:87-113: batchgenerators SpatialTransform_2,
  * augment_spatial_2 with random_crop=False; replaces the augmenter's per-sample numpy/scipy work).
  * data/seg: [n][a0][a1][a2] (C = 1), out of place into data_out/seg_out.  params (device, n x 16
@@ -520,6 +526,15 @@ int cgan3d_zero(void* p, int64_t bytes, void* stream);
  * arrays; a batch into the step's input slots).  Segments whose src or dst is not 16-byte aligned
  * are copied bytewise and limited to 4 KB (CGAN3D_EINVAL beyond). */
 int cgan3d_copy_multi(const void* const* src, void* const* dst, const int64_t* bytes, int32_t n, void* stream);
+/* The same with at most max_blocks workgroups (a copy out of mapped host memory, cgan3d_host_alloc,
+ * running beside the step on a copy stream: a few blocks keep enough PCIe reads in flight). */
+int cgan3d_copy_multi_ex(const void* const* src, void* const* dst, const int64_t* bytes, int32_t n,
+                         int32_t max_blocks, void* stream);
+/* Pinned host memory mapped into the device address space (hipHostMallocMapped): *host for the host
+ * writer, *dev for kernels (cgan3d_copy_multi_ex, cgan3d_unpack_patches_ex).  Replaces the pinned
+ * staging + non-blocking copy of the reference's batch upload (trainer/Trainer.py:165-167,182-183). */
+int cgan3d_host_alloc(int64_t bytes, void** host, void** dev);
+int cgan3d_host_free(void* host);
 
 /* LayerNorm critic (experiments/gp_layernorm.py:9-11, model/blocks.py:40-45): per-sample
  * normalisation over (C, D, H, W) — one contiguous run of L floats per sample in NDHWC — without

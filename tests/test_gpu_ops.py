@@ -1078,6 +1078,19 @@ def test_conv_t64_bf16(n, din, role):
     a4 = acc4.view(reps, 2, 32).sum(0).cpu()
     assert_close(a4[0].numpy(), gg.sum(0).numpy(), 1e-5, "t64 mode-4 sum g")
     assert_close(a4[1].numpy(), (gg * (zk - mid[:32]) * mid[32:]).sum(0).numpy(), 1e-5, "t64 mode-4 sum g xhat")
+    # out_bf16 bit 0 with mode 4 (the step's bf16 dL/dy storage): bf16 output and bf16 z, the pairs from
+    # the fp32 values and the stored z
+    z16 = z.bfloat16()
+    acc4b = torch.zeros_like(acc3)
+    y4b = torch.empty(n, *dout, 32, device="cuda", dtype=torch.bfloat16)
+    ops.conv(geo, xc, wp, y4b, ops.epilogue(x_bf16=x16, bn_z=z16, bn_ss=ss, bn_mi=mi, bn_act=L.ACT_RELU,
+                                            fuse=ops.BnFuse(acc4b, 4, reps)))
+    assert torch.equal(y4b, y.bfloat16()), "t64 bf16 output, mode 4"
+    zb = z16.double().view(-1, 32).cpu()
+    ggb = yk * ((zb * ssd[:32] + ssd[32:]) > 0).double()
+    a4b = acc4b.view(reps, 2, 32).sum(0).cpu()
+    assert_close(a4b[0].numpy(), ggb.sum(0).numpy(), 1e-5, "t64 bf16 mode-4 sum g")
+    assert_close(a4b[1].numpy(), (ggb * (zb - mid[:32]) * mid[32:]).sum(0).numpy(), 1e-5, "t64 bf16 mode-4 sum g xhat")
 
 
 @pytest.mark.parametrize("n,din", [(2, (32, 32, 32)), (1, (9, 12, 14)), (2, (17, 8, 24))])
@@ -1131,3 +1144,16 @@ def test_conv_f64_bf16(n, din, role):
     a4 = acc4.view(reps, 2, 64).sum(0).cpu()
     assert_close(a4[0].numpy(), gg.sum(0).numpy(), 1e-5, "f64 mode-4 sum g")
     assert_close(a4[1].numpy(), (gg * (zk - mid[:64]) * mid[64:]).sum(0).numpy(), 1e-5, "f64 mode-4 sum g xhat")
+    # out_bf16 bit 0 with mode 4 (the step's bf16 dL/dy storage): bf16 output and bf16 z, the pairs from
+    # the fp32 values and the stored z
+    z16 = z.bfloat16()
+    acc4b = torch.zeros_like(acc3)
+    y4b = torch.empty(n, *dout, 64, device="cuda", dtype=torch.bfloat16)
+    ops.conv(geo, xc, wp, y4b, ops.epilogue(x_bf16=x16, bn_z=z16, bn_ss=ss, bn_mi=mi, bn_act=L.ACT_RELU,
+                                            fuse=ops.BnFuse(acc4b, 4, reps)))
+    assert torch.equal(y4b, y.bfloat16()), "f64 bf16 output, mode 4"
+    zb = z16.double().view(-1, 64).cpu()
+    ggb = yk * ((zb * ssd[:64] + ssd[64:]) > 0).double()
+    a4b = acc4b.view(reps, 2, 64).sum(0).cpu()
+    assert_close(a4b[0].numpy(), ggb.sum(0).numpy(), 1e-5, "f64 bf16 mode-4 sum g")
+    assert_close(a4b[1].numpy(), (ggb * (zb - mid[:64]) * mid[64:]).sum(0).numpy(), 1e-5, "f64 bf16 mode-4 sum g xhat")

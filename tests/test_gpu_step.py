@@ -542,11 +542,16 @@ def test_bf16_storage_matches_fp32_storage(monkeypatch):
     nl = len(b16.G.layers)
     assert b16.G.z16[0] and b16.G.z16[-1] and not any(f32.G.z16)
     assert b16.G.zs[0].dtype == b16.G.dys[0].dtype == b16.G.dpads.dtype == torch.bfloat16
-    # and the ResNet chain's layers but the last (conv_k3m writes / reads them in bf16; the last one's
-    # dL/dy comes from the up-sampling conv)
+    # and the ResNet chain's layers (conv_k3m writes / reads them in bf16); the last one's dL/dy comes
+    # from the up-sampling conv's input-grad and the second down-sampling layer's z from its forward,
+    # which write bf16 where the 32 <-> 64 level kernels take the launch (cgan3d_conv3d_out_bf16_ok)
+    from cgan3d_amd import ops
     res = [j for j, ly in enumerate(b16.G.layers) if "resnet_backbone" in ly.name]
-    assert len(res) >= 2 and all(b16.G.z16[j] for j in res[:-1]) and not b16.G.z16[res[-1]]
-    assert sum(b16.G.z16) == 2 + len(res) - 1 and nl > 2
+    s2 = ops.out_bf16_ok(b16.G.geo_dgrad[res[-1] + 1])
+    assert s2 == ops.out_bf16_ok(b16.G.geo_fwd[res[0] - 1])
+    assert len(res) >= 2 and all(b16.G.z16[j] for j in res[:-1]) and b16.G.z16[res[-1]] == s2
+    assert b16.G.z16[res[0] - 1] == s2 and nl > 2
+    assert sum(b16.G.z16) == 2 + len(res) - 1 + 2 * int(s2)
     opt, _ = synth_patches(b, S, 37)
     sub, seg = synth_patches(b, S, 38)
     bt = (torch.from_numpy(opt).cuda(), torch.from_numpy(sub).cuda(), torch.from_numpy(seg).cuda(),

@@ -69,8 +69,40 @@ def _coord_volume(shape):
 
 
 @pytest.mark.gpu
+def test_mapped_host_copy_and_unpack():
+    """Zero-copy upload (cgan3d_host_alloc + cgan3d_copy_multi_ex / cgan3d_unpack_patches_ex): a kernel
+    reading mapped pinned memory over PCIe gives the bytes of the SDMA copy, and the four-voxel unpack
+    the values of the one-voxel kernel, tails included."""
+    import torch
+    from cgan3d_amd import ops
+    g = torch.Generator().manual_seed(0)
+    for nvox in (4 * 2500 + 3, 5, 64 ** 3):
+        for dt in (torch.int16, torch.float32):
+            mh = ops.MappedHost((nvox, 2), dt)
+            src = torch.randint(-1024, 3000, (nvox, 2), generator=g).to(dt)
+            src[:, 1] = (torch.rand(nvox, generator=g) < 0.3).to(dt)
+            mh.tensor.copy_(src)
+            data, seg = torch.empty(nvox, device="cuda"), torch.empty(nvox, dtype=torch.bool, device="cuda")
+            ops.unpack_patches_mapped(mh, data, seg, 238.0, 600.0, max_blocks=8)
+            d2, s2 = torch.empty_like(data), torch.empty_like(seg)
+            ops.unpack_patches(src.cuda(), d2, s2, 238.0, 600.0)
+            torch.cuda.synchronize()
+            assert torch.equal(data, d2) and torch.equal(seg, s2), (nvox, dt)
+    for n in (1001, 4096, 3):
+        mh = ops.MappedHost((n,), torch.float32)
+        mh.tensor.copy_(torch.randn(n, generator=g))
+        mb = ops.MappedHost((n + 5,), torch.bool)
+        mb.tensor.copy_(torch.rand(n + 5, generator=g) < 0.5)
+        d, db = torch.empty(n, device="cuda"), torch.empty(n + 5, dtype=torch.bool, device="cuda")
+        ops.copy_h2d([(mh, d), (mb, db)], max_blocks=4)
+        torch.cuda.synchronize()
+        assert torch.equal(d.cpu(), mh.tensor) and torch.equal(db.cpu(), mb.tensor)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("zero_copy", [True, False])
 @pytest.mark.parametrize("src_dtype", [np.int16, np.float32])
-def test_loader_batches_bit_exact(tmp_path, src_dtype):
+def test_loader_batches_bit_exact(tmp_path, src_dtype, zero_copy):
     import torch
     from cgan3d_amd.data.loader import PatchLoader
 
@@ -88,7 +120,7 @@ def test_loader_batches_bit_exact(tmp_path, src_dtype):
         shift, factor = 238, 600
 
     loader = PatchLoader(paths, patch, batch_size=2, rng=np.random.default_rng(3), scaler=FZC(), depth=3,
-                         num_threads=2, seed_for_shuffle=5)
+                         num_threads=2, seed_for_shuffle=5, zero_copy=zero_copy)
     seen = set()
     for _ in range(7):
         b = next(loader)
