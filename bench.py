@@ -202,18 +202,23 @@ def h2d_bench(eng, S, B, dev, steps):
     ready = [torch.cuda.Event() for _ in range(2)]
     freed = [None, None]
 
-    def copy(i):
+    from concurrent.futures import ThreadPoolExecutor
+    pool = ThreadPoolExecutor(max_workers=1)
+    futs = {}
+
+    def copy(i):  # on a worker thread, as the PatchLoader issues its copies (the call holds its thread)
         k = i % 2
-        if freed[k] is not None:
-            cs.wait_event(freed[k])
-        with torch.cuda.stream(cs):
+        with torch.cuda.device(dev), torch.cuda.stream(cs):
+            if freed[k] is not None:
+                cs.wait_event(freed[k])
             for dst, src in zip(stage[k], host[i % 2]):
                 dst.copy_(src, non_blocking=True)
             ready[k].record(cs)
 
     def step(i):
         k = i % 2
-        copy(i + 1)
+        futs[i + 1] = pool.submit(copy, i + 1)
+        futs.pop(i).result()  # batch i's copy was queued during step i - 1
         main.wait_event(ready[k])
         eng.load_inputs(*stage[k])
         ev = torch.cuda.Event()
@@ -221,19 +226,23 @@ def h2d_bench(eng, S, B, dev, steps):
         freed[k] = ev
         eng.run_plan()
 
-    copy(0)
+    futs[0] = pool.submit(copy, 0)
     for i in range(3):
         step(i)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(3, 3 + steps):
         step(i)
+    host_s = time.perf_counter() - t0
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
+    futs.pop(3 + steps).result()
+    pool.shutdown()
     mb = sum(t.numel() * t.element_size() for t in host[0]) / 1e6
     return {"value": round(B * steps / el, 3), "unit": "patches/s", "ms_per_step": round(el / steps * 1e3, 3),
-            "steps": steps, "h2d_mb_per_step": round(mb, 2),
-            "timing": "pinned host batch -> HBM on a copy stream, overlapped with the previous step (PatchLoader form)"}
+            "steps": steps, "h2d_mb_per_step": round(mb, 2), "host_ms_per_step": round(host_s / steps * 1e3, 3),
+            "timing": "pinned host batch -> HBM (SDMA) on the copy stream, queued by a worker thread during the "
+                      "previous step (the PatchLoader's form)"}
 
 
 class _NullLogger:
@@ -268,7 +277,7 @@ def _gp_trainer(iters, dev, precision):
                    precision=precision)
 
 
-def loader_bench(S, B, dev, steps, precision, warmup=5, workers=4):
+def loader_bench(S, B, dev, steps, precision, warmup=5, workers=4, zero_copy=False):
     """Trainer.train_step fed by create_dataloaders' PatchLoaders, the loop Trainer.fit runs
     (Trainer.py:241-252): every iteration takes one batch per scan type (B OPT, B/2 LOW, B/2 HIGH)
     from int16 [W,H,D,2] scans memory-mapped from disk (synthetic HU volumes written to a temporary
@@ -297,6 +306,13 @@ def loader_bench(S, B, dev, steps, precision, warmup=5, workers=4):
         train, _ = create_dataloaders(fold, fold[:1], (S,) * 3, (S,) * 3, sizes, {0: 1}, np.random.default_rng(3),
                                       scaler=FZC(), num_workers=(workers, 1), device=dev)
         loaders = tuple(train.values())
+        if zero_copy:  # A/B (tools/h2d_probe.py): mapped slots read by the unpack kernel over PCIe
+            from cgan3d_amd.data.loader import PatchLoader
+            for st, ld in list(train.items()):
+                ld._finish()
+                train[st] = PatchLoader(ld.paths, ld.patch, ld.batch_size, np.random.default_rng(3 + st), scaler=FZC(),
+                                        device=dev, num_threads=workers, seed_for_shuffle=42, zero_copy=True)
+            loaders = tuple(train.values())
         tr = _gp_trainer(warmup + steps, dev, precision)
         it = 0
         for _ in range(max(warmup, 3)):  # first: eager; second: the plan is recorded and run
@@ -307,13 +323,16 @@ def loader_bench(S, B, dev, steps, precision, warmup=5, workers=4):
         for _ in range(steps):
             tr.train_step([next(train[st]) for st in ScanTypes], it)
             it += 1
+        host = time.perf_counter() - t0  # the host's share: ~el when the loop is host-bound
         torch.cuda.synchronize()
         el = time.perf_counter() - t0
         mb = sum(ld._host[0].numel() * ld._host[0].element_size() for ld in loaders) / 1e6
         return {"value": round(B * steps / el, 3), "unit": "patches/s", "ms_per_step": round(el / steps * 1e3, 3),
-                "steps": steps, "h2d_mb_per_step": round(mb, 2), "host_workers_per_loader": workers,
+                "steps": steps, "h2d_mb_per_step": round(mb, 2), "host_ms_per_step": round(host / steps * 1e3, 3), "host_workers_per_loader": workers,
+                "host_ms_per_step": round(host / steps * 1e3, 3), "zero_copy": zero_copy,
                 "timing": "Trainer.train_step on next() of three PatchLoaders per iteration (Trainer.fit's loop): "
-                          "int16 crops from mmap'd .npy scans, pinned slots, H2D on the copy stream, GPU unpack"}
+                          "int16 crops from mmap'd .npy scans into pinned slots by host workers, which also queue "
+                          "the H2D copies on the copy stream; GPU unpack"}
     finally:
         for ld in loaders:
             ld._finish()

@@ -13,11 +13,12 @@ Per batch:
   than the patch are zero-padded symmetrically (batchgenerators ``pad_nd_image``:
   below = diff // 2, above = the rest), the others are cropped at a uniformly random offset
   (``crop(..., crop_type="random")``), drawn here from the loader's ``numpy.random.Generator``;
-* the pinned slots are mapped into the device (``cgan3d_host_alloc``) and one launch of
-  ``cgan3d_unpack_patches_ex`` on the copy stream (``ops.pooled_stream(dev, "copy")``, shared by
-  the loaders of a device) reads a slot over PCIe, de-interleaves and scales it on the GPU
-  ((HU - shift) / factor, ``FactorZeroCenterScaler``, ``data/Scaler.py:37-45``) — no separate SDMA
-  copy (``zero_copy=False``: pinned slot, async copy into a device slot, then the unpack);
+* the worker that filled a slot also queues its asynchronous host-to-device (SDMA) copy on the copy
+  stream (``ops.pooled_stream(dev, "copy")``, shared by the loaders of a device), so the transfer's
+  host-side cost stays off the trainer's thread; ``cgan3d_unpack_patches`` then de-interleaves and
+  scales the batch on the GPU ((HU - shift) / factor, ``FactorZeroCenterScaler``,
+  ``data/Scaler.py:37-45``).  ``zero_copy=True``: the slots are mapped into the device
+  (``cgan3d_host_alloc``) and one ``cgan3d_unpack_patches_ex`` launch reads them over PCIe instead;
 * ``depth`` batches are in flight: host workers read ahead, and ``next()`` also issues the device
   work of the following batches whose host reads are done, each ordered only after the consumers of
   its slot's previous batch, so batch j+1 crosses PCIe while the step on batch j runs.  A returned
@@ -191,7 +192,7 @@ class PatchLoader:
     def __init__(self, data: List[str], patch_shape: Sequence[int], batch_size: int, rng: np.random.Generator,
                  scaler=None, infinite: bool = True, shuffle: bool = True, device=None, depth: int = 3,
                  num_threads: int = 4, seed_for_shuffle: Optional[int] = None, transform=None,
-                 zero_copy: bool = True):
+                 zero_copy: bool = False):
         if len(patch_shape) not in (2, 3):
             raise ValueError(f"PatchLoader: 2-D or 3-D patches, got {tuple(patch_shape)}")
         self.paths = [str(p) for p in data]
@@ -210,10 +211,11 @@ class PatchLoader:
         # which is what generate_one casts to before cropping
         self.dtype = torch.int16 if probe.dtype == np.int16 else torch.float32
         shp = (batch_size, *self.patch, 2)
-        # zero_copy (round 5): the pinned slots are mapped into the device (cgan3d_host_alloc) and the
-        # unpack kernel reads them over PCIe on a few blocks — one launch per batch, no host-blocking SDMA
-        # copy (a torch non-blocking copy of a 4 MB pinned slot held the host ~0.3 ms, the step ~0.1 ms
-        # slower: tools/h2d_probe.py); False: pinned slots, SDMA copy into a device slot, then the unpack
+        # zero_copy (round 5, off by default): the pinned slots are mapped into the device
+        # (cgan3d_host_alloc) and the unpack kernel reads them over PCIe on a few blocks — one launch per
+        # batch, no SDMA copy — but those blocks hold CUs for the transfer: the Trainer + loader step
+        # measured 1.53 ms against 1.43 with the SDMA copies issued from the worker threads
+        # (tools/h2d_probe.py); default: pinned slots, SDMA copy into a device slot, then the unpack
         self.zero_copy = bool(zero_copy)
         if self.zero_copy:
             self._mapped = [ops.MappedHost(shp, self.dtype) for _ in range(self.depth)]
@@ -294,7 +296,7 @@ class PatchLoader:
                 aug = [t.draw(self.rng, self.batch_size) for t in self.transforms]
             return list(zip(idx, boxes)), aug
 
-    def _fill(self, slot: int, picks):
+    def _fill(self, slot: int, picks, free):
         ev = self._copied[slot]
         if ev is not None:
             ev.synchronize()  # the previous H2D copy out of this pinned slot has finished
@@ -305,6 +307,18 @@ class PatchLoader:
         if aug is not None:  # small parameter / noise tensors, pinned by this worker for the async copy
             aug = [tuple(None if a is None else torch.from_numpy(np.ascontiguousarray(a)).pin_memory() for a in prm)
                    for prm in aug]
+        if not self.zero_copy:
+            # the SDMA copy is issued here, by the worker: a non-blocking copy of a pinned slot holds the
+            # calling thread for about the transfer time (~0.3 ms per 4 MB, tools/h2d_probe.py), which on
+            # the trainer's thread delayed the next step's launches.  Ordered after the consumers of the
+            # slot's previous batch (``free``); the unpack the trainer's thread issues later on the same
+            # stream follows it.
+            with torch.cuda.device(self.device), torch.cuda.stream(self._stream):
+                self._stream.wait_event(free)
+                self._raw[slot].copy_(self._host[slot], non_blocking=True)
+                done = torch.cuda.Event()
+                done.record(self._stream)
+                self._copied[slot] = done
         return picks, aug
 
     def _submit(self):
@@ -313,7 +327,7 @@ class PatchLoader:
             return False
         slot = self._next_slot
         self._next_slot = (slot + 1) % self.depth
-        self._pending[slot] = self._pool.submit(self._fill, slot, picks)
+        self._pending[slot] = self._pool.submit(self._fill, slot, picks, self._free[slot])
         return True
 
     def restart(self):
@@ -346,20 +360,18 @@ class PatchLoader:
     def _issue(self, slot: int):
         """Queue the slot's host-to-device copy, unpack and transforms on the copy stream, ordered
         only after the consumers of the batch that last used the slot's device buffers."""
-        picks, aug = self._pending.pop(slot).result()
-        self._stream.wait_event(self._free[slot])
+        picks, aug = self._pending.pop(slot).result()  # (SDMA: the worker has queued the copy)
         with torch.cuda.stream(self._stream):
             bufs = [(self._data[slot], self._seg[slot]), (self._pre_data[slot], self._pre_seg[slot])] \
                 if aug is not None else [(self._data[slot], self._seg[slot])]
             k = len(self.transforms) % 2 if aug is not None else 0  # the last transform ends in _data
             if self.zero_copy:
+                self._stream.wait_event(self._free[slot])
                 ops.unpack_patches_mapped(self._mapped[slot], *bufs[k], self.shift, self.factor)
+                ev = torch.cuda.Event()
+                ev.record(self._stream)
+                self._copied[slot] = ev  # the host slot is free once this has run
             else:
-                self._raw[slot].copy_(self._host[slot], non_blocking=True)
-            ev = torch.cuda.Event()
-            ev.record(self._stream)
-            self._copied[slot] = ev  # the host slot is free once this has run
-            if not self.zero_copy:
                 ops.unpack_patches(self._raw[slot], *bufs[k], self.shift, self.factor)
             if aug is not None:
                 for t, prm in zip(self.transforms, aug):

@@ -6,7 +6,7 @@
 // conv_halo_kernel ran these as one block per (parity class, 4^3 class tile): 2048 blocks of 64 output
 // voxels x 32 channels with 1-8 taps each, two barriers per tap and the BatchNorm epilogue's three —
 // 25-29 us per launch at 64 VALU per MFMA.  Here a block owns a 4^3 class tile
-// with ALL EIGHT parity classes (512 output voxels x 32 channels = 3.6 GFLOP / 256 blocks, the shape
+// with ALL EIGHT parity classes (512 output voxels x 32 channels: 1.8 GFLOP over 256 blocks at 64^3 B=4, the shape
 // of conv_k3m): the classes share one input halo (tile + 1 per axis, 5^3 voxels) and the 27 taps'
 // weights, both put into LDS once by LDS-DMA (the halo and the 27 x 4 KB of packed format-2 weights,
 // the image conv_k3m stages for one channel half), then each wave runs its share of the 16 (class,

@@ -30,14 +30,24 @@ def _cases(B=4, S=64):
     def t(*shape):
         return torch.randn(*shape, device=dev)
 
-    def conv_case(geo, cin, cout, din, dout, packed=True):
+    def conv_case(geo, cin, cout, din, dout, packed=True, step_epi=False):
+        """step_epi: the step's epilogue for the halo-level convs — bf16 input shadow, bf16 output and
+        mode-3 accumulator statistics (what routes the 32 <-> 64 pair to conv_t64 / conv_f64)"""
         w = t(cout, cin, geo.k, geo.k, geo.k) * 0.05
         if packed:
             ps = ops.PackSet(dev)
             geo, w = ps.add(geo, w, BF)
             ps.pack()
         x, y = t(B, *din, geo.cin), torch.empty(B, *dout, geo.cout, device=dev)
-        flops = 2.0 * B * dout[0] * dout[1] * dout[2] * geo.cin * geo.cout * geo.k**3
+        # transposed stride-2: each output voxel sums 27 / 8 taps on average (the input-voxel count
+        # x 27 is the algorithmic figure)
+        nv = B * din[0] * din[1] * din[2] if geo.transposed else B * dout[0] * dout[1] * dout[2]
+        flops = 2.0 * nv * geo.cin * geo.cout * geo.k**3
+        if step_epi:
+            acc = torch.zeros(16 * 2 * geo.cout, device=dev, dtype=torch.float64)
+            y16, x16 = y.bfloat16(), x.bfloat16()
+            ep = ops.epilogue(x_bf16=x16, fuse=ops.BnFuse(acc, 3, 16))
+            return (lambda: ops.conv(geo, x, w, y16, ep)), flops
         return (lambda: ops.conv(geo, x, w, y)), flops
 
     def wgrad_case(geo, din, dout):
@@ -139,6 +149,8 @@ def _cases(B=4, S=64):
         "down0_fwd": lambda: conv_case(ops.conv_fwd_geom(B, F3, H3, 16, 32, 3, 2, 1), 16, 32, F3, H3),
         "up0_fwd": lambda: conv_case(ops.convt_fwd_geom(B, R3, H3, 64, 32, 3, 2, 1), 64, 32, R3, H3),
         "down1_fwd": lambda: conv_case(ops.conv_fwd_geom(B, H3, R3, 32, 64, 3, 2, 1), 32, 64, H3, R3),
+        "up0_fwd_step": lambda: conv_case(ops.convt_fwd_geom(B, R3, H3, 64, 32, 3, 2, 1), 64, 32, R3, H3, step_epi=True),
+        "down1_fwd_step": lambda: conv_case(ops.conv_fwd_geom(B, H3, R3, 32, 64, 3, 2, 1), 32, 64, H3, R3, step_epi=True),
         "up1_fwd": lambda: conv_case(ops.convt_fwd_geom(B, H3, F3, 32, 16, 3, 2, 1), 32, 16, H3, F3),
         "k7_last_fwd": lambda: conv_case(ops.with_prec(ops.conv_fwd_geom(B, F3, F3, 16, 1, 7, 1, 3, True), BF), 16, 1,
                                          F3, F3, packed=False),

@@ -65,6 +65,9 @@ for init, b in [(8, 2), (8, 3)]:
                 vals, cnts = torch.unique(v, return_counts=True)
                 print(f"   ch{cc}: |pre|<1e-5: {near}, most repeated value {float(vals[cnts.argmax()]):.3e} x{int(cnts.max())}")
         h = F.relu(h)
+        if j == cg.n_updownsample_blocks - 1:
+            rout = h
+            rout.retain_grad()
     h = F.pad(h, (3,) * 6, mode="reflect")
     att = torch.tanh(R._conv3d(h, p["model.last_conv.weight"], p["model.last_conv.bias"]))
     oh = x - att
@@ -75,5 +78,12 @@ for init, b in [(8, 2), (8, 3)]:
     s = gb.sum(dim=(0, 2, 3, 4))
     sa = gb.abs().sum(dim=(0, 2, 3, 4))
     ref_db = p["model.upsampling.1.normalization.bias"].grad
+    # a ReLU mask flip at voxel v moves dbeta by dL/d(relu out)[v]: list the near-zero voxels' values
+    pre_all, gr = bnout.detach(), rout.grad
+    for cc in range(pre_all.shape[1]):
+        v, gv = pre_all[:, cc].flatten(), gr[:, cc].flatten()
+        idx = torch.nonzero(v.abs() < 1e-4).flatten()
+        print(f"   ch{cc}: dbeta diff {float(dev_db[cc] - ref_db[cc]):+.3e}; |pre|<1e-4 voxels (pre, dL/drelu):",
+              [(f"{float(v[i]):+.2e}", f"{float(gv[i]):+.3e}") for i in idx[:6]])
     print(init, b, "ref dbeta", s.numpy().round(8), "\n  sum|g|", sa.numpy().round(6), "\n  ratio", (s.abs() / sa).numpy(),
           "\n  dev dbeta", dev_db.numpy().round(8), "\n  rel err", ((dev_db - ref_db).abs() / ref_db.abs()).numpy(), flush=True)

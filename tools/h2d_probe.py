@@ -184,6 +184,10 @@ def main():
                          "wait_event_ms": host_cost(lambda: main_s.wait_event(ev))}
         elif name == "loader":
             out[name] = bench.loader_bench(S, B, dev, a.steps, "bf16")
+        elif name == "loader_zc":
+            out[name] = bench.loader_bench(S, B, dev, a.steps, "bf16", zero_copy=True)
+        elif name == "bench_h2d":  # bench.py's h2d sub-line (copies queued by a worker thread)
+            out[name] = bench.h2d_bench(eng, S, B, dev, a.steps)
         print(name, out[name], flush=True)
     print(json.dumps({"ms_per_step": out}), flush=True)
 
