@@ -112,13 +112,20 @@ __global__ __launch_bounds__(256, 1) void conv_f64_kernel(F64Args a, const __bf1
   {
     const int p = lane & 3;
     const int hx0 = 2 * ox0 - 1, hy0 = 2 * oy0 - 1, hz0 = 2 * oz0 - 1;
+    // image row ir = ((hz * 9 + hy) * 2 + par) * 5 + xh, decoded once and then stepped by 64 rows per
+    // iteration (= 12 x 5 + 4) with carries: the per-iteration divisions by 5 and 9 were most of the
+    // kernel's VALU (29 VALU per MFMA, profiles/r05_pmc_sq_step.json)
+    int xh, par, hy, hz;
+    {
+      const int ir0 = 16 * wave + (lane >> 2);
+      xh = ir0 % 5;
+      const int q = ir0 / 5;
+      par = q & 1;
+      hy = (q >> 1) % F64_HY;
+      hz = (q >> 1) / F64_HY;
+    }
     for (int i = wave; i < F64_HALO / 1024; i += 4) {
       const int ir = 16 * i + (lane >> 2);
-      const int xh = ir % 5;
-      int q = ir / 5;
-      const int par = q & 1;
-      q >>= 1;
-      const int hy = q % F64_HY, hz = q / F64_HY;
       const int hx = 2 * xh + par;
       const int ix = hx0 + hx, iy = hy0 + hy, iz = hz0 + hz;
       const bool ok = ir < F64_IROWS && hx < F64_HX && (unsigned)ix < (unsigned)a.wi && (unsigned)iy < (unsigned)a.hi &&
@@ -127,6 +134,15 @@ __global__ __launch_bounds__(256, 1) void conv_f64_kernel(F64Args a, const __bf1
       const void* src = ok ? (const void*)(x16 + ((long long)((nb * a.di + iz) * a.hi + iy) * a.wi + ix) * 32 + 8 * g)
                            : (const void*)g_f64_zero;
       f64_dma16(src, __builtin_amdgcn_readfirstlane(lds0 + i * 1024));
+      xh += 4;
+      const int cx = xh >= 5;
+      xh -= cx ? 5 : 0;
+      const int t2 = par + cx;  // q = (hz * 9 + hy) * 2 + par advances by 12 + cx
+      par = t2 & 1;
+      hy += 6 + (t2 >> 1);
+      const int cy = hy >= F64_HY;
+      hy -= cy ? F64_HY : 0;
+      hz += cy;
     }
     for (int j = wave; j < 54; j += 4) {
       const int tp = j >> 1, cw = 16 * (j & 1) + (lane >> 2);

@@ -27,9 +27,23 @@ namespace cg {
 
 typedef __bf16 bf16x8_k __attribute__((ext_vector_type(8)));
 
+// n / d for n < 2^31 by multiply-high (Granlund-Montgomery; mul and sh computed on the host): the row
+// setup's three runtime divisions were ~30 VALU each, in series before every block's first load
+struct SkDiv {
+  unsigned mul;
+  int sh;
+};
+__device__ __forceinline__ unsigned sk_div(unsigned n, SkDiv d) { return (__umulhi(n, d.mul) + n) >> d.sh; }
+static SkDiv sk_divisor(unsigned d) {
+  int l = 0;
+  while ((1ull << l) < d) ++l;
+  return SkDiv{(unsigned)(((1ull << 32) * ((1ull << l) - d)) / d + 1), l};
+}
+
 struct SkArgs {
   int n, di, hi, wi, do_, ho, wo, cin, cout, k, s, p, transposed;
   int nclass, cd, ch, cw;  // parity-class grid (transposed stride 2) or the output grid
+  SkDiv dcw, dch, dcd;     // their divisors
   int mblocks;             // blocks per class
   int ktot;                // k^3 * cin: packed weight row length
   int cin_log2;            // cin is a power of two (sk_format_ok)
@@ -44,8 +58,11 @@ __device__ __forceinline__ void sk_class(int r, int k, int s, int p, int transpo
   }
 }
 
-// W: waves per block (MT == 1 splits K over them); NKC: compile-time K-steps per wave (0: runtime)
-template <int MT, int NT, int W, int NKC>
+// W: waves per block (MT == 1 splits K over them); NKC: compile-time K-steps per wave (0: runtime);
+// MODE (round 5b): 1 a forward conv (4 taps per axis), 2 a stride-2 transposed one (2 taps per axis
+// and parity class), 0 anything else (runtime tap geometry) — the tap decode and the class geometry
+// then fold to shifts and constants (VALU per MFMA 43-85 in profiles/r05_pmc_sq_step.json before)
+template <int MT, int NT, int W, int NKC, int MODE>
 __global__ __launch_bounds__(64 * W) void conv_sk_kernel(SkArgs a, const float* __restrict__ x,
                                                          const __bf16* __restrict__ wp, float* y, Epi ep) {
   __shared__ int rowo[16 * MT];
@@ -57,13 +74,22 @@ __global__ __launch_bounds__(64 * W) void conv_sk_kernel(SkArgs a, const float* 
   const int nsp = MT == 1 ? a.nsplit : 1;
   const int tile = (int)blockIdx.x / nsp, cb = ((int)blockIdx.x - tile * nsp) * 16 * NT;
   const int cls = tile / a.mblocks, mb = tile - cls * a.mblocks;
-  const int s = a.s;
+  const int s = MODE == 1 ? 1 : MODE == 2 ? 2 : a.s;
+  const bool trans = MODE == 1 ? false : MODE == 2 ? true : (a.transposed != 0);
   int r3[3] = {0, 0, 0};
-  if (a.transposed) { r3[0] = cls / (s * s); r3[1] = (cls / s) % s; r3[2] = cls % s; }
+  if (MODE == 2) { r3[0] = cls >> 2; r3[1] = (cls >> 1) & 1; r3[2] = cls & 1; }
+  else if (trans) { r3[0] = cls / (s * s); r3[1] = (cls / s) % s; r3[2] = cls % s; }
   int fz, sz, nz, fy, sy, ny, fx, sx, nx;
-  sk_class(r3[0], a.k, s, a.p, a.transposed, &fz, &sz, &nz);
-  sk_class(r3[1], a.k, s, a.p, a.transposed, &fy, &sy, &ny);
-  sk_class(r3[2], a.k, s, a.p, a.transposed, &fx, &sx, &nx);
+  if (MODE == 1) {
+    fz = fy = fx = 0; sz = sy = sx = 1; nz = ny = nx = 4;
+  } else if (MODE == 2) {  // k4 s2: class bit r reads taps f, f + 2 with f = (r + p) & 1
+    fz = (r3[0] + a.p) & 1; fy = (r3[1] + a.p) & 1; fx = (r3[2] + a.p) & 1;
+    sz = sy = sx = 2; nz = ny = nx = 2;
+  } else {
+    sk_class(r3[0], a.k, s, a.p, trans, &fz, &sz, &nz);
+    sk_class(r3[1], a.k, s, a.p, trans, &fy, &sy, &ny);
+    sk_class(r3[2], a.k, s, a.p, trans, &fx, &sx, &nx);
+  }
   const int ntap = nz * ny * nx;
   (void)sz;
   (void)sy;
@@ -72,15 +98,15 @@ __global__ __launch_bounds__(64 * W) void conv_sk_kernel(SkArgs a, const float* 
     // 32-bit index math (sk_format_ok bounds every volume below 2^31 elements)
     const unsigned m = (unsigned)mb * 16 * MT + tid;
     const unsigned cvox = (unsigned)a.n * a.cd * a.ch * a.cw;
-    unsigned q = m / (unsigned)a.cw;
+    unsigned q = sk_div(m, a.dcw);
     const int jx = (int)(m - q * a.cw);
-    unsigned q2 = q / (unsigned)a.ch;
+    unsigned q2 = sk_div(q, a.dch);
     const int jy = (int)(q - q2 * a.ch);
-    q = q2 / (unsigned)a.cd;
+    q = sk_div(q2, a.dcd);
     const int jz = (int)(q2 - q * a.cd), nb = (int)q;
     const bool ok = m < cvox;
     int od = jz, oh = jy, ow = jx;
-    if (a.transposed) {
+    if (trans) {
       od = jz * s + r3[0]; oh = jy * s + r3[1]; ow = jx * s + r3[2];
       rowb[0][tid] = jz; rowb[1][tid] = jy; rowb[2][tid] = jx;
     } else {
@@ -99,10 +125,11 @@ __global__ __launch_bounds__(64 * W) void conv_sk_kernel(SkArgs a, const float* 
   // tap j of the class = digits (md, mh, mw) in base 4 (forward: t = m) or 2 (transposed: t = f + s m,
   // gathered coordinate j + (r + p - t) / s = C - m), decoded in registers (round 5: the round-4 tap
   // tables in LDS put dependent LDS reads in front of every K-step's global loads)
-  const int lg = nz == 2 ? 1 : 2, lm = (1 << lg) - 1, sg = a.transposed ? -1 : 1, st = a.transposed ? s : 1;
-  const int Cz = bz + (a.transposed ? (r3[0] + a.p - fz) / s : 0);
-  const int Cy = by + (a.transposed ? (r3[1] + a.p - fy) / s : 0);
-  const int Cx = bx + (a.transposed ? (r3[2] + a.p - fx) / s : 0);
+  const int lg = MODE == 1 ? 2 : MODE == 2 ? 1 : (nz == 2 ? 1 : 2), lm = (1 << lg) - 1, sg = trans ? -1 : 1;
+  const int st = trans ? s : 1;
+  const int Cz = bz + (MODE == 2 ? (r3[0] + a.p - fz) >> 1 : trans ? (r3[0] + a.p - fz) / s : 0);
+  const int Cy = by + (MODE == 2 ? (r3[1] + a.p - fy) >> 1 : trans ? (r3[1] + a.p - fy) / s : 0);
+  const int Cx = bx + (MODE == 2 ? (r3[2] + a.p - fx) >> 1 : trans ? (r3[2] + a.p - fx) / s : 0);
   const int HW = a.hi * a.wi;
   const int gbase = ((nb * a.di + Cz) * a.hi + Cy) * a.wi + Cx;
   const int KS = ntap * a.cin / 32;
@@ -201,10 +228,12 @@ __global__ __launch_bounds__(64 * W) void conv_sk_kernel(SkArgs a, const float* 
 #pragma unroll
       for (int jj = 0; jj < 4; ++jj) v[jj] += ep.bias[c0 + jj];
     }
+    if (ep.act == CGAN3D_ACT_RELU) {
 #pragma unroll
-    for (int jj = 0; jj < 4; ++jj) {
-      if (ep.act == CGAN3D_ACT_RELU) v[jj] = fmaxf(v[jj], 0.f);
-      else if (ep.act == CGAN3D_ACT_LRELU) v[jj] = v[jj] > 0.f ? v[jj] : v[jj] * ep.slope;
+      for (int jj = 0; jj < 4; ++jj) v[jj] = fmaxf(v[jj], 0.f);
+    } else if (ep.act == CGAN3D_ACT_LRELU) {
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj) v[jj] = v[jj] > 0.f ? v[jj] : v[jj] * ep.slope;
     }
     if (ok) {
       const int o = ro * a.cout + c0;
@@ -284,6 +313,9 @@ static SkArgs sk_args(const cgan3d_conv_geom* g, int* mt) {
   a.cin_log2 = 0;
   while ((1 << a.cin_log2) < g->cin) ++a.cin_log2;
   a.nsplit = 1;
+  a.dcw = sk_divisor((unsigned)a.cw);
+  a.dch = sk_divisor((unsigned)a.ch);
+  a.dcd = sk_divisor((unsigned)a.cd);
   return a;
 }
 
@@ -315,15 +347,22 @@ int sk_launch(const cgan3d_conv_geom* g, const float* x, const __bf16* wp, float
   const int w = wide ? 8 : 4;
   const int nk = mt == 1 ? (KS + w - 1) / w : KS;
   const int nkc = nk <= 4 ? 4 : nk <= 8 ? 8 : nk <= 16 ? 16 : 0;
+  const int mode = !g->transposed ? 1 : g->stride == 2 ? 2 : 0;
   auto go = [&](auto mt_c, auto w_c) {
     constexpr int M = decltype(mt_c)::value, W = decltype(w_c)::value;
     auto by_nt = [&](auto nkc_c) {
       constexpr int K = decltype(nkc_c)::value;
       const dim3 block(64 * W);
-      if (ntb == 1) ::cg::launch((conv_sk_kernel<M, 1, W, K>), grid, block, 0, st, a, x, wp, y, e);
-      else if (ntb == 2) ::cg::launch((conv_sk_kernel<M, 2, W, K>), grid, block, 0, st, a, x, wp, y, e);
-      else if (ntb == 3) ::cg::launch((conv_sk_kernel<M, 3, W, K>), grid, block, 0, st, a, x, wp, y, e);
-      else ::cg::launch((conv_sk_kernel<M, 4, W, K>), grid, block, 0, st, a, x, wp, y, e);
+      auto by_mode = [&](auto nt_c) {
+        constexpr int N = decltype(nt_c)::value;
+        if (mode == 1) ::cg::launch((conv_sk_kernel<M, N, W, K, 1>), grid, block, 0, st, a, x, wp, y, e);
+        else if (mode == 2) ::cg::launch((conv_sk_kernel<M, N, W, K, 2>), grid, block, 0, st, a, x, wp, y, e);
+        else ::cg::launch((conv_sk_kernel<M, N, W, K, 0>), grid, block, 0, st, a, x, wp, y, e);
+      };
+      if (ntb == 1) by_mode(std::integral_constant<int, 1>{});
+      else if (ntb == 2) by_mode(std::integral_constant<int, 2>{});
+      else if (ntb == 3) by_mode(std::integral_constant<int, 3>{});
+      else by_mode(std::integral_constant<int, 4>{});
     };
     if (nkc == 4) by_nt(std::integral_constant<int, 4>{});
     else if (nkc == 8) by_nt(std::integral_constant<int, 8>{});

@@ -130,36 +130,43 @@ __global__ __launch_bounds__(256, 1) void conv_t64_kernel(T64Args a, const __bf1
   };
   const int nitems = wave < 2 ? 3 : 5;
 
-  // ---- epilogue operands first (conv_k3m): output offsets of this lane's 16 rows per item, and the
-  // mode-4 BatchNorm z at them, loaded before the DMAs so the MFMAs cover their round trip
+  // ---- output offsets (round 5b): lane base + a per-item scalar + a per-row delta, instead of 80
+  // offsets of ~12 instructions each held in registers; row i of a lane is R = (i & 3) + 8 (i >> 2) +
+  // 4 h (the MFMA's accumulator rows), item (class r, M tile m) outputs voxel 2 j + r with j = tile
+  // origin + (lx, ly, 2 m + lzz)
   const int c = lane & 31, h = lane >> 5;
   const bool mode4 = ep.fz.acc_mode == 4;
-  int oidx[T64_ITEMS][16];
-  float zv[T64_ITEMS][16] = {};
-#pragma unroll
-  for (int k = 0; k < T64_ITEMS; ++k) {
+  const int obase = (((nb * DO + 2 * jz0) * HO + 2 * jy0) * WO + 2 * jx0) * 32 + c;
+  auto item_off = [&](int k) -> int {  // wave-uniform
     const int cls = item_cls(k), m = item_m(k);
-    const int rz = (cls >> 2) & 1, ry = (cls >> 1) & 1, rx = cls & 1;
+    return (((4 * m + ((cls >> 2) & 1)) * HO + ((cls >> 1) & 1)) * WO + (cls & 1)) * 32;
+  };
+  int drow[16];
+  unsigned vxy = 0, vz = 0;  // per row: (x, y) inside the volume; its z-slice lzz
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const int R = (i & 3) + 8 * (i >> 2) + 4 * h;
-      int lx, ly, lzz;
-      t64_row(R, lx, ly, lzz);
-      const int jx = jx0 + lx, jy = jy0 + ly, jz = jz0 + 2 * m + lzz;
-      const bool ok = k < nitems && jx < a.wi && jy < a.hi && jz < a.di;
-      const int ox = 2 * jx + rx, oy = 2 * jy + ry, oz = 2 * jz + rz;
-      oidx[k][i] = ok ? (((nb * DO + oz) * HO + oy) * WO + ox) * 32 + c : -1;
-    }
+  for (int i = 0; i < 16; ++i) {
+    int lx, ly, lzz;
+    t64_row((i & 3) + 8 * (i >> 2) + 4 * h, lx, ly, lzz);
+    drow[i] = ((2 * lzz * HO + 2 * ly) * WO + 2 * lx) * 32;
+    vxy |= (unsigned)(jx0 + lx < a.wi && jy0 + ly < a.hi) << i;
+    vz |= (unsigned)lzz << i;
   }
-  if (mode4) {  // block-uniform
+  const bool full = jx0 + 4 <= a.wi && jy0 + 4 <= a.hi && jz0 + 4 <= a.di;  // every row of every item
+  auto valid = [&](int k, int i) -> bool {
+    return k < nitems && ((vxy >> i) & 1) && jz0 + 2 * item_m(k) + (int)((vz >> i) & 1) < a.di;
+  };
+  float zv[T64_ITEMS][16];
+  if (mode4) {  // block-uniform; the z loads go out before the DMAs so the MFMAs cover their round trip
 #pragma unroll
-    for (int k = 0; k < T64_ITEMS; ++k)
+    for (int k = 0; k < T64_ITEMS; ++k) {
+      const int ok0 = obase + item_off(k);
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
-        const int zi = oidx[k][i] >= 0 ? oidx[k][i] : 0;
+        const int zi = (full ? k < nitems : valid(k, i)) ? ok0 + drow[i] : 0;
         if constexpr ((OB & 1) != 0) zv[k][i] = (float)reinterpret_cast<const __bf16*>(ep.bn_z)[zi];
         else zv[k][i] = ep.bn_z[zi];
       }
+    }
   }
 
   // ---- LDS-DMA: the halo (19 wave-instructions of 8 rows; rows past 150 and voxels outside the
@@ -221,38 +228,73 @@ __global__ __launch_bounds__(256, 1) void conv_t64_kernel(T64Args a, const __bf1
     t64_item<4, 1>(smem, acc[4], lx, ly, lzz, h, boff);
   }
 
-  // ---- epilogue: stores, then the statistics of channel c over this lane's outputs
-  float n1 = 0.f, K = 0.f, s1 = 0.f, s2 = 0.f;
-  bool first = true;
+  // ---- epilogue: stores, then the statistics of channel c over this lane's outputs.  Round 5b: the
+  // statistics mode and the BatchNorm activation are uniform branches around whole loops, and a tile
+  // inside the volume (all of them at 64^3) needs no per-element validity (VALU per MFMA 46.7 in
+  // profiles/r05_pmc_sq_step.json before)
   const int mode = ep.fz.acc_mode;
-  float sc = 0.f, sh = 0.f, mu = 0.f, is = 0.f;
-  if (mode4) { sc = ep.bn_ss[c]; sh = ep.bn_ss[32 + c]; mu = ep.bn_mi[c]; is = ep.bn_mi[32 + c]; }
-  const int bact = ep.bn_act;
-  const float bslope = ep.bn_slope;
+  float n1 = 0.f, K = 0.f, s1 = 0.f, s2 = 0.f;
+  auto store = [&](int o, float v) {
+    if constexpr ((OB & 1) != 0) reinterpret_cast<__bf16*>(y)[o] = (__bf16)v;
+    else y[o] = v;
+  };
+  if (mode == 3 && full) {  // shift = the lane's first value; n = 16 per item
+    K = acc[0][0];
 #pragma unroll
-  for (int k = 0; k < T64_ITEMS; ++k)
+    for (int k = 0; k < T64_ITEMS; ++k) {
+      if (k >= nitems) break;
+      const int ok0 = obase + item_off(k);
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const int o = oidx[k][i];
-      if (o < 0) continue;
-      const float v = acc[k][i];
-      if constexpr ((OB & 1) != 0) reinterpret_cast<__bf16*>(y)[o] = (__bf16)v;
-      else y[o] = v;
-      if (mode == 3) {
-        if (first) { K = v; first = false; }
+      for (int i = 0; i < 16; ++i) {
+        const float v = acc[k][i];
+        store(ok0 + drow[i], v);
         const float d = v - K;
         s1 += d;
         s2 = fmaf(d, d, s2);
-        n1 += 1.f;
-      } else if (mode4) {
+      }
+    }
+    n1 = 16.f * nitems;
+  } else if (mode4) {
+    const float sc = ep.bn_ss[c], sh = ep.bn_ss[32 + c], mu = ep.bn_mi[c], is = ep.bn_mi[32 + c];
+    const int bact = ep.bn_act;
+    const float bslope = ep.bn_slope;
+#pragma unroll
+    for (int k = 0; k < T64_ITEMS; ++k) {
+      if (k >= nitems) break;
+      const int ok0 = obase + item_off(k);
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        if (!full && !valid(k, i)) continue;
+        const float v = acc[k][i];
+        store(ok0 + drow[i], v);
         const float pre = zv[k][i] * sc + sh;
-        const float dg = bact == CGAN3D_ACT_RELU ? (pre > 0.f ? 1.f : 0.f)
-                                                 : (bact == CGAN3D_ACT_LRELU ? (pre > 0.f ? 1.f : bslope) : 1.f);
-        const float gg = v * dg;
+        const float gg = bact == CGAN3D_ACT_RELU ? (pre > 0.f ? v : 0.f)
+                                                 : (bact == CGAN3D_ACT_LRELU ? (pre > 0.f ? v : v * bslope) : v);
         s1 += gg;
         s2 += gg * (zv[k][i] - mu) * is;
       }
     }
+  } else {  // no statistics, or mode 3 on a ragged tile (the shift is the first valid value)
+    bool first = true;
+#pragma unroll
+    for (int k = 0; k < T64_ITEMS; ++k) {
+      if (k >= nitems) break;
+      const int ok0 = obase + item_off(k);
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        if (!full && !valid(k, i)) continue;
+        const float v = acc[k][i];
+        store(ok0 + drow[i], v);
+        if (mode == 3) {
+          if (first) { K = v; first = false; }
+          const float d = v - K;
+          s1 += d;
+          s2 = fmaf(d, d, s2);
+          n1 += 1.f;
+        }
+      }
+    }
+  }
   if (!mode) return;
   double* const facc = ep.fz.acc_out + (long long)(blockIdx.x % ep.fz.reps) * 2 * 32;
   if (mode == 3) {  // lane (n, mean, M2) -> merged with lane ^ 32 (same channel), then the 4 waves
