@@ -40,6 +40,8 @@ static SkDiv sk_divisor(unsigned d) {
   return SkDiv{(unsigned)(((1ull << 32) * ((1ull << l) - d)) / d + 1), l};
 }
 
+__device__ __attribute__((aligned(16))) float g_sk_zero[8];  // the dead operands' source
+
 struct SkArgs {
   int n, di, hi, wi, do_, ho, wo, cin, cout, k, s, p, transposed;
   int nclass, cd, ch, cw;  // parity-class grid (transposed stride 2) or the output grid
@@ -62,7 +64,9 @@ __device__ __forceinline__ void sk_class(int r, int k, int s, int p, int transpo
 // MODE (round 5b): 1 a forward conv (4 taps per axis), 2 a stride-2 transposed one (2 taps per axis
 // and parity class), 0 anything else (runtime tap geometry) — the tap decode and the class geometry
 // then fold to shifts and constants (VALU per MFMA 43-85 in profiles/r05_pmc_sq_step.json before)
-template <int MT, int NT, int W, int NKC, int MODE>
+// CL: log2 of cin as a compile-time constant (the critic's 8 - 64 channels; 0: runtime) — with the
+// tap geometry and NKC fixed, a lane's K-step offsets fold to constants plus its lane-group term
+template <int MT, int NT, int W, int NKC, int MODE, int CL>
 __global__ __launch_bounds__(64 * W) void conv_sk_kernel(SkArgs a, const float* __restrict__ x,
                                                          const __bf16* __restrict__ wp, float* y, Epi ep) {
   __shared__ int rowo[16 * MT];
@@ -74,7 +78,7 @@ __global__ __launch_bounds__(64 * W) void conv_sk_kernel(SkArgs a, const float* 
   const int nsp = MT == 1 ? a.nsplit : 1;
   const int tile = (int)blockIdx.x / nsp, cb = ((int)blockIdx.x - tile * nsp) * 16 * NT;
   const int cls = tile / a.mblocks, mb = tile - cls * a.mblocks;
-  const int s = MODE == 1 ? 1 : MODE == 2 ? 2 : a.s;
+  const int s = MODE == 2 ? 2 : a.s;  // the conv's stride (a forward conv keeps its own)
   const bool trans = MODE == 1 ? false : MODE == 2 ? true : (a.transposed != 0);
   int r3[3] = {0, 0, 0};
   if (MODE == 2) { r3[0] = cls >> 2; r3[1] = (cls >> 1) & 1; r3[2] = cls & 1; }
@@ -132,7 +136,8 @@ __global__ __launch_bounds__(64 * W) void conv_sk_kernel(SkArgs a, const float* 
   const int Cx = bx + (MODE == 2 ? (r3[2] + a.p - fx) >> 1 : trans ? (r3[2] + a.p - fx) / s : 0);
   const int HW = a.hi * a.wi;
   const int gbase = ((nb * a.di + Cz) * a.hi + Cy) * a.wi + Cx;
-  const int KS = ntap * a.cin / 32;
+  const int cl = CL > 0 ? CL : a.cin_log2, cin = 1 << cl;
+  const int KS = ntap * cin / 32;
   const int kend = KS;
   const int ks0 = MT == 1 ? wave : 0, kstep = MT == 1 ? W : 1;
 
@@ -149,35 +154,33 @@ __global__ __launch_bounds__(64 * W) void conv_sk_kernel(SkArgs a, const float* 
   // the runtime loop, for long K (many rows, MT == 4).
   constexpr int PF = NKC > 0 ? (NKC < 8 ? NKC : 8) : 4;
   f32x4 xa0[PF], xa1[PF];  // A: 8 fp32 channels of one gathered voxel
-  bool xok[PF];            // ... live (applied at the MFMA: a select right after the load waits for it)
   bf16x8_k bb[PF][NT];     // B fragments
   const int nk = ks0 < kend ? (kend - ks0 + kstep - 1) / kstep : 0;  // this wave's K-steps (wave-uniform)
   auto load = [&](int q, int sl) {
     const bool live = q < nk;
     const int ks = ks0 + min(q, max(nk - 1, 0)) * kstep;
     const int k0 = ks * 32 + 8 * g;
-    const int j = k0 >> a.cin_log2, a0 = k0 & (a.cin - 1);
+    const int j = k0 >> cl, a0 = k0 & (cin - 1);
     const int md = j >> (2 * lg), mh = (j >> lg) & lm, mw = j & lm;
     const int iz = Cz + sg * md, iy = Cy + sg * mh, ix = Cx + sg * mw;
     const bool ok = live && rok && (unsigned)iz < (unsigned)a.di && (unsigned)iy < (unsigned)a.hi &&
                     (unsigned)ix < (unsigned)a.wi;
-    // 32-bit element offsets (sk_launch checks the sizes); a dead operand reads element 0
-    const float* src = x + (ok ? ((gbase + sg * (md * HW + mh * a.wi + mw)) << a.cin_log2) + a0 : 0);
+    // 32-bit element offsets (sk_launch checks the sizes); a dead operand reads 8 zeros (round 5b: one
+    // 64-bit select per K-step instead of 8 selects on the loaded values)
+    const float* src = ok ? x + ((gbase + sg * (md * HW + mh * a.wi + mw)) << cl) + a0 : g_sk_zero;
     xa0[sl] = *reinterpret_cast<const f32x4*>(src);
     xa1[sl] = *reinterpret_cast<const f32x4*>(src + 4);
-    xok[sl] = ok;
-    const int wk = (((fz + st * md) * 4 + fy + st * mh) * 4 + fx + st * mw) * a.cin + a0;  // k == 4
+    const int wk = ((((fz + st * md) * 4 + fy + st * mh) * 4 + fx + st * mw) << cl) + a0;  // k == 4
 #pragma unroll
     for (int t = 0; t < NT; ++t)  // columns past cout (cout = 8) read a valid row; their outputs are never stored
       bb[sl][t] = *reinterpret_cast<const bf16x8_k*>(wp + min(cb + t * 16 + r16, a.cout - 1) * a.ktot + wk);
   };
   auto step = [&](int sl) {
     bf16x8_k av;
-    const bool k = xok[sl];
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
-      av[e] = (__bf16)keep_if(k, xa0[sl][e]);
-      av[4 + e] = (__bf16)keep_if(k, xa1[sl][e]);
+      av[e] = (__bf16)xa0[sl][e];
+      av[4 + e] = (__bf16)xa1[sl][e];
     }
 #pragma unroll
     for (int t = 0; t < NT; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bb[sl][t], av, acc[t], 0, 0, 0);
@@ -355,9 +358,17 @@ int sk_launch(const cgan3d_conv_geom* g, const float* x, const __bf16* wp, float
       const dim3 block(64 * W);
       auto by_mode = [&](auto nt_c) {
         constexpr int N = decltype(nt_c)::value;
-        if (mode == 1) ::cg::launch((conv_sk_kernel<M, N, W, K, 1>), grid, block, 0, st, a, x, wp, y, e);
-        else if (mode == 2) ::cg::launch((conv_sk_kernel<M, N, W, K, 2>), grid, block, 0, st, a, x, wp, y, e);
-        else ::cg::launch((conv_sk_kernel<M, N, W, K, 0>), grid, block, 0, st, a, x, wp, y, e);
+        auto by_cl = [&](auto mode_c) {
+          constexpr int MO = decltype(mode_c)::value;
+          if (a.cin_log2 == 3) ::cg::launch((conv_sk_kernel<M, N, W, K, MO, 3>), grid, block, 0, st, a, x, wp, y, e);
+          else if (a.cin_log2 == 4) ::cg::launch((conv_sk_kernel<M, N, W, K, MO, 4>), grid, block, 0, st, a, x, wp, y, e);
+          else if (a.cin_log2 == 5) ::cg::launch((conv_sk_kernel<M, N, W, K, MO, 5>), grid, block, 0, st, a, x, wp, y, e);
+          else if (a.cin_log2 == 6) ::cg::launch((conv_sk_kernel<M, N, W, K, MO, 6>), grid, block, 0, st, a, x, wp, y, e);
+          else ::cg::launch((conv_sk_kernel<M, N, W, K, MO, 0>), grid, block, 0, st, a, x, wp, y, e);
+        };
+        if (mode == 1) by_cl(std::integral_constant<int, 1>{});
+        else if (mode == 2) by_cl(std::integral_constant<int, 2>{});
+        else ::cg::launch((conv_sk_kernel<M, N, W, K, 0, 0>), grid, block, 0, st, a, x, wp, y, e);
       };
       if (ntb == 1) by_mode(std::integral_constant<int, 1>{});
       else if (ntb == 2) by_mode(std::integral_constant<int, 2>{});
