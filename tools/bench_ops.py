@@ -77,6 +77,22 @@ def _cases(B=4, S=64):
         flops = 2.0 * n3 * dout[0] * dout[1] * dout[2] * cin * cout * 64
         return (lambda: ops.conv(geo, x, w, y)), flops
 
+    def crit_dgrad(cin, cout, din):
+        """critic layer input-grad over the 3B critic batch: the transposed k4 s2 map from dL/dz at the
+        layer's output grid to dL/dx at din, with the LeakyReLU mask of the layer below"""
+        n3 = 3 * B
+        dout = tuple(d // 2 for d in din)
+        geo = ops.conv_dgrad_geom(n3, din, dout, cin, cout, 4, 2, 1)
+        w = t(cout, cin, 4, 4, 4) * 0.05
+        ps = ops.PackSet(dev)
+        geo, w = ps.add(geo, w, BF)
+        ps.pack()
+        dz, dx = t(n3, *dout, cout), torch.empty(n3, *din, cin, device=dev)
+        m = t(n3, *din, cin)
+        ep = ops.epilogue(mask_src=m, slope=0.2)
+        flops = 2.0 * n3 * dout[0] * dout[1] * dout[2] * cin * cout * 64
+        return (lambda: ops.conv(geo, dz, w, dx, ep)), flops
+
     def res_wgrad_k3m():
         """ResNet-block weight grad as the bf16 step issues it (both operands' bf16 shadows:
         wgrad_k3m_kernel + wgrad_reduce_lin_kernel)"""
@@ -143,6 +159,9 @@ def _cases(B=4, S=64):
         "crit_m1": lambda: crit(16, 32, R3),
         "crit_m2": lambda: crit(32, 64, (r // 2,) * 3),
         "crit_m2_gemm": lambda: crit(32, 64, (r // 2,) * 3, halo=False),
+        "crit_m0_dgrad": lambda: crit_dgrad(8, 16, H3),
+        "crit_m1_dgrad": lambda: crit_dgrad(16, 32, R3),
+        "crit_m2_dgrad": lambda: crit_dgrad(32, 64, (r // 2,) * 3),
         "res_fwd": lambda: conv_case(ops.conv_fwd_geom(B, R3, R3, 64, 64, 3, 1, 1), 64, 64, R3, R3),
         "res_wgrad": lambda: wgrad_case(ops.with_prec(ops.conv_wgrad_geom(B, R3, R3, 64, 64, 3, 1, 1), BF), R3, R3),
         "down0_wgrad": lambda: wgrad_case(ops.with_prec(ops.conv_wgrad_geom(B, F3, H3, 16, 32, 3, 2, 1), BF), F3, H3),
