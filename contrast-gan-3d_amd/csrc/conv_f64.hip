@@ -199,26 +199,50 @@ __global__ __launch_bounds__(256, 1) void conv_f64_kernel(F64Args a, const __bf1
   if (mode4) { sc = ep.bn_ss[co0 + c]; sh = ep.bn_ss[64 + co0 + c]; mu = ep.bn_mi[co0 + c]; is = ep.bn_mi[64 + co0 + c]; }
   const int bact = ep.bn_act;
   const float bslope = ep.bn_slope;
-#pragma unroll
-  for (int i = 0; i < 16; ++i) {
-    const int o = oidx[i];
-    if (o < 0) continue;
-    const float v = acc[i];
+  // round 5b: the statistics mode and the BatchNorm activation as uniform branches around whole loops,
+  // and a tile inside the volume (every tile at 64^3) without per-element validity
+  const bool full = ox0 + 4 <= a.wo && oy0 + 4 <= a.ho && oz0 + 8 <= a.do_;
+  auto store = [&](int o, float v) {
     if constexpr ((OB & 1) != 0) reinterpret_cast<__bf16*>(y)[o] = (__bf16)v;
     else y[o] = v;
-    if (mode == 3) {
-      if (first) { K = v; first = false; }
+  };
+  if (mode == 3 && full) {  // shift = the lane's first value
+    K = acc[0];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const float v = acc[i];
+      store(oidx[i], v);
       const float d = v - K;
       s1 += d;
       s2 = fmaf(d, d, s2);
-      n1 += 1.f;
-    } else if (mode4) {
+    }
+    n1 = 16.f;
+  } else if (mode4) {  // (invalid rows: skipped)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      if (!full && oidx[i] < 0) continue;
+      const float v = acc[i];
+      store(oidx[i], v);
       const float pre = zv[i] * sc + sh;
-      const float dg = bact == CGAN3D_ACT_RELU ? (pre > 0.f ? 1.f : 0.f)
-                                               : (bact == CGAN3D_ACT_LRELU ? (pre > 0.f ? 1.f : bslope) : 1.f);
-      const float gg = v * dg;
+      const float gg = bact == CGAN3D_ACT_RELU ? (pre > 0.f ? v : 0.f)
+                                               : (bact == CGAN3D_ACT_LRELU ? (pre > 0.f ? v : v * bslope) : v);
       s1 += gg;
       s2 += gg * (zv[i] - mu) * is;
+    }
+  } else {  // no statistics, or mode 3 on a ragged tile (the shift is the first valid value)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int o = oidx[i];
+      if (o < 0) continue;
+      const float v = acc[i];
+      store(o, v);
+      if (mode == 3) {
+        if (first) { K = v; first = false; }
+        const float d = v - K;
+        s1 += d;
+        s2 = fmaf(d, d, s2);
+        n1 += 1.f;
+      }
     }
   }
   if (!mode) return;
