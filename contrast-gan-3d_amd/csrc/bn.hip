@@ -277,6 +277,115 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_fold_kernel(const void* __re
   }
 }
 
+// bn_bwd_apply_fold_kernel<true> by rows (round 5c): block (h chunk, nb * D + d), a row of W voxels
+// x C channels read as 16-byte granules of 8 bf16 channels (RW = W C / 8 threads per row, a power of
+// two dividing 256), FOLD_U rows per thread.  No per-element divides (the grid-stride form spent 3
+// runtime divides per 8 bytes), the interior loads of all FOLD_U rows in flight while the replicas
+// are combined, and 16-byte accesses: 38.0 -> 34.2 us at 64^3 B = 4 (bench_ops bn_fold64).  Sums the mirrored sources
+// in the grid-stride kernel's order, so the two are bit-identical.
+constexpr int FOLD_U = 4;
+typedef __bf16 bf16x8_n __attribute__((ext_vector_type(8)));
+typedef unsigned u32x4_n __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ void bf8_set(float* d, u32x4_n r) {
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    d[2 * e] = __uint_as_float(r[e] << 16);
+    d[2 * e + 1] = __uint_as_float(r[e] & 0xffff0000u);
+  }
+}
+
+__device__ __forceinline__ void bf8_add(float* d, u32x4_n r) {
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    d[2 * e] += __uint_as_float(r[e] << 16);
+    d[2 * e + 1] += __uint_as_float(r[e] & 0xffff0000u);
+  }
+}
+
+__global__ __launch_bounds__(256) void bn_bwd_fold_rows_kernel(const __bf16* __restrict__ padded,
+                                                               const __bf16* __restrict__ z, int D, int H, int W,
+                                                               int P, int C, int lrw, int lc8,
+                                                               const float* __restrict__ ss,
+                                                               const float* __restrict__ mi, int act, float slope,
+                                                               float* dz, __bf16* __restrict__ dz16,
+                                                               const double* __restrict__ acc, int reps, double nvox,
+                                                               const float* __restrict__ gamma, float* dgamma,
+                                                               float* dbeta, int accumulate, double* zero,
+                                                               int zero_n) {
+  __shared__ double sums[2 * 256], part[256];
+  __shared__ float co[3 * 256];
+  const int tid = threadIdx.x;
+  const int RP = 256 >> lrw;  // rows per pass
+  const int rl = tid >> lrw, g = tid & ((1 << lrw) - 1);
+  const int w = g >> lc8, c = (g & ((1 << lc8) - 1)) * 8;
+  const int nd_ = blockIdx.y, nb = nd_ / D, d = nd_ - nb * D;
+  const int h0 = blockIdx.x * (FOLD_U * RP) + rl;
+  const int Dp = D + 2 * P, Hp = H + 2 * P, Wp = W + 2 * P;
+  const bool pub = blockIdx.x == 0 && blockIdx.y == 0;
+  if (pub)
+    for (int j = tid; j < zero_n; j += blockDim.x) zero[j] = 0.0;
+  // interior sources (the (0, 0, 0) preimage) and z of this thread's FOLD_U rows, raw bits
+  u32x4_n zr[FOLD_U], pr[FOLD_U];
+  acc_sums(acc, reps, C, sums, part, [&] {
+#pragma unroll
+    for (int u = 0; u < FOLD_U; ++u) {
+      const int h = min(h0 + u * RP, H - 1);
+      zr[u] = *reinterpret_cast<const u32x4_n*>(z + ((long long)(nd_ * H + h) * W + w) * C + c);
+      pr[u] = *reinterpret_cast<const u32x4_n*>(
+          padded + ((long long)((nb * Dp + d + P) * Hp + h + P) * Wp + w + P) * C + c);
+    }
+  });
+  lds_barrier();
+  for (int k = tid; k < C; k += blockDim.x)
+    bn_acc_bwd_coeffs(sums, k, C, nvox, gamma, mi, &co[k], &co[C + k], &co[2 * C + k], pub, dgamma, dbeta,
+                      accumulate);
+  lds_barrier();
+  float sc[8], sf[8], mean[8], inv[8], k0[8], k1[8], k2[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const int k = c + e;
+    sc[e] = ss[k]; sf[e] = ss[C + k]; mean[e] = mi[k]; inv[e] = mi[C + k];
+    k0[e] = co[k]; k1[e] = co[C + k]; k2[e] = co[2 * C + k];
+  }
+  int qd[2], qw[2];
+  const int nd = fold_src(d, D, P, qd), nw = fold_src(w, W, P, qw);
+#pragma unroll
+  for (int u = 0; u < FOLD_U; ++u) {
+    const int h = h0 + u * RP;
+    if (h >= H) break;
+    int qh[2];
+    const int nh = fold_src(h, H, P, qh);
+    float dd[8];
+    bf8_set(dd, pr[u]);
+    if (nd * nh * nw > 1) {  // boundary voxel: its mirrored sources, in bn_bwd_apply_fold_kernel's order
+      for (int a = 0; a < nd; ++a)
+        for (int b = 0; b < nh; ++b)
+          for (int e = 0; e < nw; ++e)
+            if (a | b | e)
+              bf8_add(dd, *reinterpret_cast<const u32x4_n*>(
+                              padded + ((long long)((nb * Dp + qd[a]) * Hp + qh[b]) * Wp + qw[e]) * C + c));
+    }
+    float o[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float zz = __uint_as_float((e & 1) ? (zr[u][e >> 1] & 0xffff0000u) : (zr[u][e >> 1] << 16));
+      o[e] = bn_bwd_map(dd[e], zz, sc[e], sf[e], mean[e], inv[e], k0[e], k1[e], k2[e], act, slope);
+    }
+    const long long i = ((long long)(nd_ * H + h) * W + w) * C + c;
+    if (dz) {
+      reinterpret_cast<f32x4*>(dz + i)[0] = f32x4{o[0], o[1], o[2], o[3]};
+      reinterpret_cast<f32x4*>(dz + i)[1] = f32x4{o[4], o[5], o[6], o[7]};
+    }
+    if (dz16) {
+      bf16x8_n v;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = (__bf16)o[e];
+      *reinterpret_cast<bf16x8_n*>(dz16 + i) = v;
+    }
+  }
+}
+
 // ---- fused-statistics path: per-block partials written by the producing kernel's epilogue into
 // a channel-major slab part[(q * C + c) * nslots + b] (no atomics); one block per channel reads its
 // contiguous rows (coalesced) and combines them in fp64.
@@ -950,6 +1059,17 @@ extern "C" int cgan3d_bn_backward_acc_fold(const void* padded, const void* z, in
   CG_CHECK_ARG((long long)n * (d + 2 * pad) * (h + 2 * pad) * (w + 2 * pad) * (c / 4) < (1LL << 31),
                "cgan3d_bn_backward_acc_fold: padded volume exceeds 32-bit float4 indexing");
   const long long n4 = nvox * c / 4;
+  const long long rw = (long long)w * c / 8;  // 16-byte granules per row
+  if (in_bf16 && c % 8 == 0 && rw <= 256 && (rw & (rw - 1)) == 0 && (long long)n * d <= 65535 &&
+      nvox * c < (1LL << 31)) {
+    const int lrw = __builtin_ctzll(rw), hpb = FOLD_U * (256 >> lrw);
+    ::cg::launch(bn_bwd_fold_rows_kernel, dim3((h + hpb - 1) / hpb, n * d), dim3(256), 0, (hipStream_t)stream,
+                 (const __bf16*)padded, (const __bf16*)z, d, h, w, pad, c, lrw, __builtin_ctz(c / 8), scale_shift,
+                 mean_invstd, act, slope, dz, reinterpret_cast<__bf16*>(dz_bf16), acc, (int)reps, (double)nvox, gamma,
+                 dgamma, dbeta, (int)accumulate, zero, (int)zero_n);
+    CG_LAUNCH_CHECK("bn_bwd_fold_rows_kernel");
+    return CGAN3D_OK;
+  }
   ::cg::launch(in_bf16 ? bn_bwd_apply_fold_kernel<true> : bn_bwd_apply_fold_kernel<false>, dim3(acc_pass_blocks(n4, 4096)),
                dim3(256), 0, (hipStream_t)stream, padded, z, n, d,
                h, w, pad, c, scale_shift, mean_invstd, act, slope, (const float*)nullptr, dz,

@@ -1157,3 +1157,48 @@ def test_conv_f64_bf16(n, din, role):
     a4b = acc4b.view(reps, 2, 64).sum(0).cpu()
     assert_close(a4b[0].numpy(), ggb.sum(0).numpy(), 1e-5, "f64 bf16 mode-4 sum g")
     assert_close(a4b[1].numpy(), (ggb * (zb - mid[:64]) * mid[64:]).sum(0).numpy(), 1e-5, "f64 bf16 mode-4 sum g xhat")
+
+
+@pytest.mark.parametrize("n,sp,c", [(2, (12, 16, 16), 16), (1, (10, 9, 64), 16), (2, (9, 7, 8), 32),
+                                    (2, (8, 12, 12), 16)])
+@pytest.mark.parametrize("act", ["relu", "lrelu"])
+def test_bn_backward_fold_rows(n, sp, c, act):
+    """The generator's last BatchNorm backward with the reflect-pad fold (round 5c row kernel, bf16
+    operands) gives exactly the bits of the grid-stride kernel run on the same values in fp32: dz16, dz,
+    dgamma / dbeta (accumulated) and the zeroed accumulator.  (2, (8, 12, 12), 16) has 24 granules per
+    row, not a power of two: the grid-stride fallback."""
+    from cgan3d_amd import ops, _lib as L
+    A, slope = (L.ACT_RELU, 0.0) if act == "relu" else (L.ACT_LRELU, 0.2)
+    g = torch.Generator().manual_seed(5 + sp[2] + c)
+    dev = torch.device("cuda")
+    p, reps = 3, 16
+    pad_sp = tuple(d + 2 * p for d in sp)
+    padded16 = torch.randn(n, *pad_sp, c, generator=g).to(dev).bfloat16()
+    z16 = (torch.randn(n, *sp, c, generator=g) * 1.3 + 0.2).to(dev).bfloat16()
+    acc = torch.zeros(reps, 2, c, dtype=torch.float64, device=dev)
+    acc[5, 0] = torch.randn(c, generator=g, dtype=torch.float64).to(dev) * 50
+    acc[9, 1] = torch.randn(c, generator=g, dtype=torch.float64).to(dev) * 50
+    acc = acc.view(-1)
+    ss = torch.cat([torch.rand(c, generator=g) + 0.5, torch.randn(c, generator=g) * 0.3]).to(dev)
+    mi = torch.cat([torch.randn(c, generator=g) * 0.2, torch.rand(c, generator=g) + 0.7]).to(dev)
+    gamma = (torch.rand(c, generator=g) + 0.5).to(dev)
+    out = []
+    for in16 in (True, False):
+        pd, zz = (padded16, z16) if in16 else (padded16.float(), z16.float())
+        dg, db = torch.full((c,), 0.25, device=dev), torch.full((c,), -0.5, device=dev)
+        dz = torch.full((n, *sp, c), float("nan"), device=dev)
+        dz16 = torch.full((n, *sp, c), float("nan"), device=dev, dtype=torch.bfloat16)
+        zero = torch.ones(100, dtype=torch.float64, device=dev)
+        ops.bn_backward_acc_fold(pd, zz, n, sp, c, p, acc, reps, ss, mi, gamma, A, dg, db, dz, slope=slope,
+                                 accumulate=True, dz16=dz16, zero=zero)
+        out.append((dz16, dz, dg, db, zero))
+    torch.cuda.synchronize()
+    for a_, b_, nm in zip(out[0], out[1], ("dz16", "dz", "dgamma", "dbeta", "zero")):
+        assert torch.equal(a_, b_), nm
+    assert float(out[0][4].abs().max()) == 0.0
+    # dz16-only (the step's form) matches too
+    dz16b = torch.empty_like(z16)
+    ops.bn_backward_acc_fold(padded16, z16, n, sp, c, p, acc, reps, ss, mi, gamma, A, torch.zeros(c, device=dev),
+                             torch.zeros(c, device=dev), None, slope=slope, dz16=dz16b)
+    torch.cuda.synchronize()
+    assert torch.equal(dz16b, out[0][0])

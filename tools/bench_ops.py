@@ -93,6 +93,22 @@ def _cases(B=4, S=64):
         flops = 2.0 * n3 * dout[0] * dout[1] * dout[2] * cin * cout * 64
         return (lambda: ops.conv(geo, dz, w, dx, ep)), flops
 
+    def bn_fold(fp32_dz=False):
+        """the generator's last BatchNorm backward with the reflect-pad fold (bn_bwd_apply_fold_kernel,
+        bf16 step operands: padded dL/dy and z in, dz16 out); the figure is HBM bytes (column = TB/s)"""
+        c, p = 16, 3
+        padded = t(B, *(d + 2 * p for d in F3), c).bfloat16()
+        z = t(B, *F3, c).bfloat16()
+        acc = torch.zeros(16 * 2 * c, device=dev, dtype=torch.float64)
+        acc[c:2 * c] = 1.0
+        ss, mi = torch.ones(2 * c, device=dev), torch.ones(2 * c, device=dev)
+        gamma, dg, db = torch.ones(c, device=dev), torch.zeros(c, device=dev), torch.zeros(c, device=dev)
+        dz16 = torch.empty(B, *F3, c, device=dev, dtype=torch.bfloat16)
+        dz = torch.empty(B, *F3, c, device=dev) if fp32_dz else None
+        nbytes = B * S**3 * c * (2 + 2 + 2 + (4 if fp32_dz else 0))
+        return (lambda: ops.bn_backward_acc_fold(padded, z, B, F3, c, p, acc, 16, ss, mi, gamma, 1, dg, db, dz,
+                                                 dz16=dz16)), nbytes
+
     def res_wgrad_k3m():
         """ResNet-block weight grad as the bf16 step issues it (both operands' bf16 shadows:
         wgrad_k3m_kernel + wgrad_reduce_lin_kernel)"""
@@ -159,6 +175,8 @@ def _cases(B=4, S=64):
         "crit_m1": lambda: crit(16, 32, R3),
         "crit_m2": lambda: crit(32, 64, (r // 2,) * 3),
         "crit_m2_gemm": lambda: crit(32, 64, (r // 2,) * 3, halo=False),
+        "bn_fold64": lambda: bn_fold(),
+        "bn_fold64_dz": lambda: bn_fold(True),
         "crit_m0_dgrad": lambda: crit_dgrad(8, 16, H3),
         "crit_m1_dgrad": lambda: crit_dgrad(16, 32, R3),
         "crit_m2_dgrad": lambda: crit_dgrad(32, 64, (r // 2,) * 3),
