@@ -281,7 +281,8 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_fold_kernel(const void* __re
 // x C channels read as 16-byte granules of 8 bf16 channels (RW = W C / 8 threads per row, a power of
 // two dividing 256), FOLD_U rows per thread.  No per-element divides (the grid-stride form spent 3
 // runtime divides per 8 bytes), the interior loads of all FOLD_U rows in flight while the replicas
-// are combined, and 16-byte accesses: 38.0 -> 34.2 us at 64^3 B = 4 (bench_ops bn_fold64).  Sums the mirrored sources
+// are combined, 16-byte accesses, the boundary rows' mirror loads issued together: 38.3 -> 26.6 us at 64^3 B = 4
+// (bench_ops bn_fold64; a bf16 add over the same bytes takes 15.4).  Sums the mirrored sources
 // in the grid-stride kernel's order, so the two are bit-identical.
 constexpr int FOLD_U = 4;
 typedef __bf16 bf16x8_n __attribute__((ext_vector_type(8)));
@@ -312,7 +313,7 @@ __global__ __launch_bounds__(256) void bn_bwd_fold_rows_kernel(const __bf16* __r
                                                                const double* __restrict__ acc, int reps, double nvox,
                                                                const float* __restrict__ gamma, float* dgamma,
                                                                float* dbeta, int accumulate, double* zero,
-                                                               int zero_n) {
+                                                               int zero_n, int probe) {
   __shared__ double sums[2 * 256], part[256];
   __shared__ float co[3 * 256];
   const int tid = threadIdx.x;
@@ -326,46 +327,49 @@ __global__ __launch_bounds__(256) void bn_bwd_fold_rows_kernel(const __bf16* __r
   if (pub)
     for (int j = tid; j < zero_n; j += blockDim.x) zero[j] = 0.0;
   // interior sources (the (0, 0, 0) preimage) and z of this thread's FOLD_U rows, raw bits
-  u32x4_n zr[FOLD_U], pr[FOLD_U];
-  acc_sums(acc, reps, C, sums, part, [&] {
+  // interior source, its w-mirror (per lane; the interior again where there is none) and z of this
+  // thread's FOLD_U rows, raw bits: every lane's common sources in flight before the first use — a
+  // mirror load issued inside the row loop waited for all earlier stores (vmcnt counts both) and made
+  // the pass 2x the HBM time
+  int qd[2], qw[2];
+  const int nd = fold_src(d, D, P, qd), nw = fold_src(w, W, P, qw);
+  const int wsrc = nw > 1 ? qw[1] : qw[0];
+  u32x4_n zr[FOLD_U], pr[FOLD_U], pw[FOLD_U];
+  float sc[8], sf[8], mean[8], inv[8], k0[8], k1[8], k2[8], gc, ic;
+  auto pf = [&] {  // the layer's scale / shift / mean / invstd first: loaded after the data, their wait
+#pragma unroll     // covered every row's loads
+    for (int e = 0; e < 8; ++e) {
+      const int k = c + e;
+      sc[e] = ss[k]; sf[e] = ss[C + k]; mean[e] = mi[k]; inv[e] = mi[C + k];
+    }
+    gc = gamma[min(tid, C - 1)];
+    ic = mi[C + min(tid, C - 1)];
 #pragma unroll
     for (int u = 0; u < FOLD_U; ++u) {
       const int h = min(h0 + u * RP, H - 1);
-      zr[u] = *reinterpret_cast<const u32x4_n*>(z + ((long long)(nd_ * H + h) * W + w) * C + c);
-      pr[u] = *reinterpret_cast<const u32x4_n*>(
-          padded + ((long long)((nb * Dp + d + P) * Hp + h + P) * Wp + w + P) * C + c);
+      const __bf16* prow = padded + ((long long)((nb * Dp + d + P) * Hp + h + P) * Wp) * C + c;
+      zr[u] = CG_PROBE(probe, 8) ? u32x4_n{} : *reinterpret_cast<const u32x4_n*>(z + ((long long)(nd_ * H + h) * W + w) * C + c);
+      pr[u] = CG_PROBE(probe, 2) ? u32x4_n{} : *reinterpret_cast<const u32x4_n*>(prow + (w + P) * C);
+      pw[u] = CG_PROBE(probe, 2) ? u32x4_n{} : *reinterpret_cast<const u32x4_n*>(prow + wsrc * C);
     }
-  });
+  };
+  if (CG_PROBE(probe, 1)) {
+    pf();
+    if (tid < 2 * C) sums[tid] = 1.0;
+  } else {
+    acc_sums(acc, reps, C, sums, part, pf);
+  }
   lds_barrier();
-  for (int k = tid; k < C; k += blockDim.x)
-    bn_acc_bwd_coeffs(sums, k, C, nvox, gamma, mi, &co[k], &co[C + k], &co[2 * C + k], pub, dgamma, dbeta,
-                      accumulate);
+  if (tid < C)  // C <= 128 (the launcher's check)
+    bn_acc_bwd_coeffs_pre(sums, tid, C, nvox, gc, ic, &co[tid], &co[C + tid], &co[2 * C + tid], pub, dgamma, dbeta,
+                          accumulate);
   lds_barrier();
-  float sc[8], sf[8], mean[8], inv[8], k0[8], k1[8], k2[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
     const int k = c + e;
-    sc[e] = ss[k]; sf[e] = ss[C + k]; mean[e] = mi[k]; inv[e] = mi[C + k];
     k0[e] = co[k]; k1[e] = co[C + k]; k2[e] = co[2 * C + k];
   }
-  int qd[2], qw[2];
-  const int nd = fold_src(d, D, P, qd), nw = fold_src(w, W, P, qw);
-#pragma unroll
-  for (int u = 0; u < FOLD_U; ++u) {
-    const int h = h0 + u * RP;
-    if (h >= H) break;
-    int qh[2];
-    const int nh = fold_src(h, H, P, qh);
-    float dd[8];
-    bf8_set(dd, pr[u]);
-    if (nd * nh * nw > 1) {  // boundary voxel: its mirrored sources, in bn_bwd_apply_fold_kernel's order
-      for (int a = 0; a < nd; ++a)
-        for (int b = 0; b < nh; ++b)
-          for (int e = 0; e < nw; ++e)
-            if (a | b | e)
-              bf8_add(dd, *reinterpret_cast<const u32x4_n*>(
-                              padded + ((long long)((nb * Dp + qd[a]) * Hp + qh[b]) * Wp + qw[e]) * C + c));
-    }
+  auto finish = [&](int u, int h, const float* dd) {
     float o[8];
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
@@ -373,6 +377,7 @@ __global__ __launch_bounds__(256) void bn_bwd_fold_rows_kernel(const __bf16* __r
       o[e] = bn_bwd_map(dd[e], zz, sc[e], sf[e], mean[e], inv[e], k0[e], k1[e], k2[e], act, slope);
     }
     const long long i = ((long long)(nd_ * H + h) * W + w) * C + c;
+    if (CG_PROBE(probe, 4)) return;
     if (dz) {
       reinterpret_cast<f32x4*>(dz + i)[0] = f32x4{o[0], o[1], o[2], o[3]};
       reinterpret_cast<f32x4*>(dz + i)[1] = f32x4{o[4], o[5], o[6], o[7]};
@@ -383,6 +388,46 @@ __global__ __launch_bounds__(256) void bn_bwd_fold_rows_kernel(const __bf16* __r
       for (int e = 0; e < 8; ++e) v[e] = (__bf16)o[e];
       *reinterpret_cast<bf16x8_n*>(dz16 + i) = v;
     }
+  };
+  // rows off the d / h boundary first (at most the prefetched w-mirror) ...
+#pragma unroll
+  for (int u = 0; u < FOLD_U; ++u) {
+    const int h = h0 + u * RP;
+    if (h >= H) break;
+    int qh[2];
+    if (nd * fold_src(h, H, P, qh) != 1) continue;  // (wave-uniform at RW >= 64)
+    float dd[8];
+    bf8_set(dd, pr[u]);
+    if (nw > 1) bf8_add(dd, pw[u]);
+    finish(u, h, dd);
+  }
+  // ... then the d / h boundary rows, whose further sources are loaded here (a load under the branch
+  // above made every row wait for all loads and stores in flight)
+  if (CG_PROBE(probe, 2)) return;
+#pragma unroll
+  for (int u = 0; u < FOLD_U; ++u) {
+    const int h = h0 + u * RP;
+    if (h >= H) break;
+    int qh[2];
+    const int nh = fold_src(h, H, P, qh);
+    if (nd * nh == 1) continue;
+    // all 6 further candidates loaded at once (the preimage itself where one does not exist), then the
+    // existing ones summed in (a, b, e) order: loaded one by one, each waited for the last, and the
+    // boundary blocks set the kernel's length (33.8 us at 64^3, against 15.4 for a bf16 add)
+    u32x4_n m[8];
+#pragma unroll
+    for (int j = 2; j < 8; ++j) {
+      const int a = j >> 2, b = (j >> 1) & 1, e = j & 1;
+      const int sd = a < nd ? qd[a] : qd[0], sh = b < nh ? qh[b] : qh[0], sw = e < nw ? qw[e] : qw[0];
+      m[j] = *reinterpret_cast<const u32x4_n*>(padded + ((long long)((nb * Dp + sd) * Hp + sh) * Wp + sw) * C + c);
+    }
+    m[1] = pw[u];
+    float dd[8];
+    bf8_set(dd, pr[u]);
+#pragma unroll
+    for (int j = 1; j < 8; ++j)
+      if ((j >> 2) < nd && ((j >> 1) & 1) < nh && (j & 1) < nw) bf8_add(dd, m[j]);
+    finish(u, h, dd);
   }
 }
 
@@ -1066,7 +1111,13 @@ extern "C" int cgan3d_bn_backward_acc_fold(const void* padded, const void* z, in
     ::cg::launch(bn_bwd_fold_rows_kernel, dim3((h + hpb - 1) / hpb, n * d), dim3(256), 0, (hipStream_t)stream,
                  (const __bf16*)padded, (const __bf16*)z, d, h, w, pad, c, lrw, __builtin_ctz(c / 8), scale_shift,
                  mean_invstd, act, slope, dz, reinterpret_cast<__bf16*>(dz_bf16), acc, (int)reps, (double)nvox, gamma,
-                 dgamma, dbeta, (int)accumulate, zero, (int)zero_n);
+                 dgamma, dbeta, (int)accumulate, zero, (int)zero_n,
+#ifdef CGAN3D_PROBES
+                 g_probe
+#else
+                 0
+#endif
+    );
     CG_LAUNCH_CHECK("bn_bwd_fold_rows_kernel");
     return CGAN3D_OK;
   }

@@ -55,15 +55,16 @@ __device__ __forceinline__ void acc_sums(const double* __restrict__ acc, int rep
 // Forward finalize of channel c from the (sum, sum of squares) replicas' totals: scale / shift of
 // act(z * scale + shift); `publish` (one block of the launch) writes the layer's scale / shift, mean /
 // invstd (read by the backward) and the running buffers (momentum update, unbiased variance).
-__device__ __forceinline__ void bn_acc_fwd_coeffs(const double* sums, int c, int C, double nvox, const float* gamma,
-                                                  const float* beta, float eps, float* sc_out, float* sh_out,
-                                                  bool publish, float* scale_shift, float* mean_invstd, float* rmean,
-                                                  float* rvar, long long* nbt, float momentum) {
+// gamma[c] / beta[c] loaded by the caller ahead of the replica combine (bn_acc_fwd_coeffs loads them)
+__device__ __forceinline__ void bn_acc_fwd_coeffs_pre(const double* sums, int c, int C, double nvox, float gamma_c,
+                                                      float beta_c, float eps, float* sc_out, float* sh_out,
+                                                      bool publish, float* scale_shift, float* mean_invstd, float* rmean,
+                                                      float* rvar, long long* nbt, float momentum) {
   const double mean = sums[c] / nvox, var = fmax(sums[C + c] / nvox - mean * mean, 0.0);
   const double invstd = 1.0 / sqrt(var + (double)eps);
-  const double sc = (double)gamma[c] * invstd;
+  const double sc = (double)gamma_c * invstd;
   *sc_out = (float)sc;
-  *sh_out = (float)((double)beta[c] - mean * sc);
+  *sh_out = (float)((double)beta_c - mean * sc);
   if (publish) {
     scale_shift[c] = *sc_out;
     scale_shift[C + c] = *sh_out;
@@ -75,6 +76,14 @@ __device__ __forceinline__ void bn_acc_fwd_coeffs(const double* sums, int c, int
   }
 }
 
+__device__ __forceinline__ void bn_acc_fwd_coeffs(const double* sums, int c, int C, double nvox, const float* gamma,
+                                                  const float* beta, float eps, float* sc_out, float* sh_out,
+                                                  bool publish, float* scale_shift, float* mean_invstd, float* rmean,
+                                                  float* rvar, long long* nbt, float momentum) {
+  bn_acc_fwd_coeffs_pre(sums, c, C, nvox, gamma[c], beta[c], eps, sc_out, sh_out, publish, scale_shift, mean_invstd,
+                        rmean, rvar, nbt, momentum);
+}
+
 // Backward finalize of channel c from the (sum g, sum g * xhat) totals: the coefficients of
 // bn_bwd_map (k0 = gamma * invstd, k1 = mean g, k2 = mean g * xhat); `publish` writes dbeta = sum g,
 // dgamma = sum g * xhat (added when `accumulate`).
@@ -82,6 +91,20 @@ __device__ __forceinline__ void bn_acc_bwd_coeffs(const double* sums, int c, int
                                                   const float* mi, float* k0, float* k1, float* k2, bool publish,
                                                   float* dgamma, float* dbeta, int accumulate) {
   *k0 = gamma[c] * mi[C + c];
+  *k1 = (float)(sums[c] / nvox);
+  *k2 = (float)(sums[C + c] / nvox);
+  if (publish) {
+    if (dbeta) dbeta[c] = accumulate ? dbeta[c] + (float)sums[c] : (float)sums[c];
+    if (dgamma) dgamma[c] = accumulate ? dgamma[c] + (float)sums[C + c] : (float)sums[C + c];
+  }
+}
+
+// bn_acc_bwd_coeffs with gamma[c] and invstd[c] loaded by the caller ahead of the replica combine
+// (loaded here, they were one more round trip between the block's two barriers); same arithmetic
+__device__ __forceinline__ void bn_acc_bwd_coeffs_pre(const double* sums, int c, int C, double nvox, float gamma_c,
+                                                      float invstd_c, float* k0, float* k1, float* k2, bool publish,
+                                                      float* dgamma, float* dbeta, int accumulate) {
+  *k0 = gamma_c * invstd_c;
   *k1 = (float)(sums[c] / nvox);
   *k2 = (float)(sums[C + c] / nvox);
   if (publish) {

@@ -93,20 +93,38 @@ def _cases(B=4, S=64):
         flops = 2.0 * n3 * dout[0] * dout[1] * dout[2] * cin * cout * 64
         return (lambda: ops.conv(geo, dz, w, dx, ep)), flops
 
-    def bn_fold(fp32_dz=False):
+    def ref_add3(shape):
+        """calibration: torch's bf16 add (two reads, one write) over a tensor of `shape`; figure = HBM bytes"""
+        a, b = t(*shape).bfloat16(), t(*shape).bfloat16()
+        o = torch.empty_like(a)
+        return (lambda: torch.add(a, b, out=o)), 3 * a.numel() * 2
+
+    def bn_bwd(c, sp, reps=16):
+        """a BatchNorm backward pass from the fp64 replicas (bn_bwd_apply_acc_kernel<true>: dy, z bf16 in,
+        dz16 out); figure = HBM bytes"""
+        dy, z = t(B, *sp, c).bfloat16(), t(B, *sp, c).bfloat16()
+        acc = torch.zeros(reps * 2 * c, device=dev, dtype=torch.float64)
+        ss, mi = torch.ones(2 * c, device=dev), torch.ones(2 * c, device=dev)
+        gamma, dg, db = torch.ones(c, device=dev), torch.zeros(c, device=dev), torch.zeros(c, device=dev)
+        dz16 = torch.empty_like(z)
+        nv = B * sp[0] * sp[1] * sp[2]
+        return (lambda: ops.bn_backward_acc(dy, z, nv, c, acc, reps, ss, mi, gamma, 1, dg, db, None,
+                                            dz16=dz16)), 3 * z.numel() * 2
+
+    def bn_fold(fp32_dz=False, reps=16):
         """the generator's last BatchNorm backward with the reflect-pad fold (bn_bwd_apply_fold_kernel,
         bf16 step operands: padded dL/dy and z in, dz16 out); the figure is HBM bytes (column = TB/s)"""
         c, p = 16, 3
         padded = t(B, *(d + 2 * p for d in F3), c).bfloat16()
         z = t(B, *F3, c).bfloat16()
-        acc = torch.zeros(16 * 2 * c, device=dev, dtype=torch.float64)
+        acc = torch.zeros(reps * 2 * c, device=dev, dtype=torch.float64)
         acc[c:2 * c] = 1.0
         ss, mi = torch.ones(2 * c, device=dev), torch.ones(2 * c, device=dev)
         gamma, dg, db = torch.ones(c, device=dev), torch.zeros(c, device=dev), torch.zeros(c, device=dev)
         dz16 = torch.empty(B, *F3, c, device=dev, dtype=torch.bfloat16)
         dz = torch.empty(B, *F3, c, device=dev) if fp32_dz else None
         nbytes = B * S**3 * c * (2 + 2 + 2 + (4 if fp32_dz else 0))
-        return (lambda: ops.bn_backward_acc_fold(padded, z, B, F3, c, p, acc, 16, ss, mi, gamma, 1, dg, db, dz,
+        return (lambda: ops.bn_backward_acc_fold(padded, z, B, F3, c, p, acc, reps, ss, mi, gamma, 1, dg, db, dz,
                                                  dz16=dz16)), nbytes
 
     def res_wgrad_k3m():
@@ -177,6 +195,12 @@ def _cases(B=4, S=64):
         "crit_m2_gemm": lambda: crit(32, 64, (r // 2,) * 3, halo=False),
         "bn_fold64": lambda: bn_fold(),
         "bn_fold64_dz": lambda: bn_fold(True),
+        "bn_fold64_r1": lambda: bn_fold(reps=1),
+        "ref_add3_64": lambda: ref_add3((B, S, S, S, 16)),
+        "ref_add3_16": lambda: ref_add3((B, r, r, r, 64)),
+        "bn_bwd16": lambda: bn_bwd(64, R3),
+        "bn_bwd16_r1": lambda: bn_bwd(64, R3, reps=1),
+        "bn_bwd32": lambda: bn_bwd(32, H3),
         "crit_m0_dgrad": lambda: crit_dgrad(8, 16, H3),
         "crit_m1_dgrad": lambda: crit_dgrad(16, 32, R3),
         "crit_m2_dgrad": lambda: crit_dgrad(32, 64, (r // 2,) * 3),
