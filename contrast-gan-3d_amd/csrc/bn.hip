@@ -281,10 +281,9 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_fold_kernel(const void* __re
 // x C channels read as 16-byte granules of 8 bf16 channels (RW = W C / 8 threads per row, a power of
 // two dividing 256), FOLD_U rows per thread.  No per-element divides (the grid-stride form spent 3
 // runtime divides per 8 bytes), the interior loads of all FOLD_U rows in flight while the replicas
-// are combined, 16-byte accesses, the boundary rows' mirror loads issued together: 38.3 -> 26.6 us at 64^3 B = 4
+// are combined, 16-byte accesses, the boundary rows' mirror loads issued together: 38.3 -> 25.3 us at 64^3 B = 4
 // (bench_ops bn_fold64; a bf16 add over the same bytes takes 15.4).  Sums the mirrored sources
 // in the grid-stride kernel's order, so the two are bit-identical.
-constexpr int FOLD_U = 4;
 typedef __bf16 bf16x8_n __attribute__((ext_vector_type(8)));
 typedef unsigned u32x4_n __attribute__((ext_vector_type(4)));
 
@@ -304,6 +303,7 @@ __device__ __forceinline__ void bf8_add(float* d, u32x4_n r) {
   }
 }
 
+template <int FOLD_U>
 __global__ __launch_bounds__(256) void bn_bwd_fold_rows_kernel(const __bf16* __restrict__ padded,
                                                                const __bf16* __restrict__ z, int D, int H, int W,
                                                                int P, int C, int lrw, int lc8,
@@ -313,20 +313,37 @@ __global__ __launch_bounds__(256) void bn_bwd_fold_rows_kernel(const __bf16* __r
                                                                const double* __restrict__ acc, int reps, double nvox,
                                                                const float* __restrict__ gamma, float* dgamma,
                                                                float* dbeta, int accumulate, double* zero,
-                                                               int zero_n, int probe) {
+                                                               int zero_n, unsigned pbytes, int probe) {
   __shared__ double sums[2 * 256], part[256];
-  __shared__ float co[3 * 256];
+  __shared__ float co[7 * 128];  // k0, k1, k2, scale, shift, mean, invstd (C <= 128): in LDS, not 56 VGPRs
   const int tid = threadIdx.x;
   const int RP = 256 >> lrw;  // rows per pass
   const int rl = tid >> lrw, g = tid & ((1 << lrw) - 1);
   const int w = g >> lc8, c = (g & ((1 << lc8) - 1)) * 8;
-  const int nd_ = blockIdx.y, nb = nd_ / D, d = nd_ - nb * D;
+  // planes dispatched boundary first (D >= 2P + 2): the 2P planes with a d-mirror have every row on
+  // the slower path, started first they finish under the interior planes instead of after them
+  int nb, d;
+  {
+    const int y = blockIdx.y, nbd = 2 * P, nbat = gridDim.y / D;
+    if (D < 2 * P + 2) {
+      nb = y / D; d = y - nb * D;
+    } else if (y < nbat * nbd) {
+      nb = y / nbd;
+      const int k = y - nb * nbd;
+      d = k < P ? 1 + k : D - 1 - P + (k - P);
+    } else {
+      const int y2 = y - nbat * nbd, ni = D - nbd;
+      nb = y2 / ni;
+      const int k = y2 - nb * ni;
+      d = k == 0 ? 0 : (k <= D - 2 - 2 * P ? k + P : D - 1);
+    }
+  }
+  const int nd_ = nb * D + d;
   const int h0 = blockIdx.x * (FOLD_U * RP) + rl;
   const int Dp = D + 2 * P, Hp = H + 2 * P, Wp = W + 2 * P;
   const bool pub = blockIdx.x == 0 && blockIdx.y == 0;
   if (pub)
     for (int j = tid; j < zero_n; j += blockDim.x) zero[j] = 0.0;
-  // interior sources (the (0, 0, 0) preimage) and z of this thread's FOLD_U rows, raw bits
   // interior source, its w-mirror (per lane; the interior again where there is none) and z of this
   // thread's FOLD_U rows, raw bits: every lane's common sources in flight before the first use — a
   // mirror load issued inside the row loop waited for all earlier stores (vmcnt counts both) and made
@@ -335,13 +352,15 @@ __global__ __launch_bounds__(256) void bn_bwd_fold_rows_kernel(const __bf16* __r
   const int nd = fold_src(d, D, P, qd), nw = fold_src(w, W, P, qw);
   const int wsrc = nw > 1 ? qw[1] : qw[0];
   u32x4_n zr[FOLD_U], pr[FOLD_U], pw[FOLD_U];
-  float sc[8], sf[8], mean[8], inv[8], k0[8], k1[8], k2[8], gc, ic;
+  // mirror sources through a buffer descriptor: a lane without one gets an offset past the end, which
+  // the range check drops (zeros, no memory request) — most lanes of every wave have none
+  const __amdgpu_buffer_rsrc_t prs = __builtin_amdgcn_make_buffer_rsrc((void*)padded, (short)0, (int)pbytes, 0x00020000);
+  constexpr unsigned OOB = 0xfffffff0u;
+  float tss, tmi, gc, ic;
   auto pf = [&] {  // the layer's scale / shift / mean / invstd first: loaded after the data, their wait
-#pragma unroll     // covered every row's loads
-    for (int e = 0; e < 8; ++e) {
-      const int k = c + e;
-      sc[e] = ss[k]; sf[e] = ss[C + k]; mean[e] = mi[k]; inv[e] = mi[C + k];
-    }
+                   // covered every row's loads
+    tss = ss[min(tid, 2 * C - 1)];
+    tmi = mi[min(tid, 2 * C - 1)];
     gc = gamma[min(tid, C - 1)];
     ic = mi[C + min(tid, C - 1)];
 #pragma unroll
@@ -350,7 +369,8 @@ __global__ __launch_bounds__(256) void bn_bwd_fold_rows_kernel(const __bf16* __r
       const __bf16* prow = padded + ((long long)((nb * Dp + d + P) * Hp + h + P) * Wp) * C + c;
       zr[u] = CG_PROBE(probe, 8) ? u32x4_n{} : *reinterpret_cast<const u32x4_n*>(z + ((long long)(nd_ * H + h) * W + w) * C + c);
       pr[u] = CG_PROBE(probe, 2) ? u32x4_n{} : *reinterpret_cast<const u32x4_n*>(prow + (w + P) * C);
-      pw[u] = CG_PROBE(probe, 2) ? u32x4_n{} : *reinterpret_cast<const u32x4_n*>(prow + wsrc * C);
+      const unsigned wo = 2u * (unsigned)((((nb * Dp + d + P) * Hp + h + P) * Wp + wsrc) * C + c);
+      pw[u] = CG_PROBE(probe, 2) ? u32x4_n{} : __builtin_amdgcn_raw_buffer_load_b128(prs, nw > 1 ? wo : OOB, 0, 0);
     }
   };
   if (CG_PROBE(probe, 1)) {
@@ -359,22 +379,23 @@ __global__ __launch_bounds__(256) void bn_bwd_fold_rows_kernel(const __bf16* __r
   } else {
     acc_sums(acc, reps, C, sums, part, pf);
   }
+  if (tid < 2 * C) {
+    co[3 * C + tid] = tss;
+    co[5 * C + tid] = tmi;
+  }
   lds_barrier();
   if (tid < C)  // C <= 128 (the launcher's check)
     bn_acc_bwd_coeffs_pre(sums, tid, C, nvox, gc, ic, &co[tid], &co[C + tid], &co[2 * C + tid], pub, dgamma, dbeta,
                           accumulate);
   lds_barrier();
-#pragma unroll
-  for (int e = 0; e < 8; ++e) {
-    const int k = c + e;
-    k0[e] = co[k]; k1[e] = co[C + k]; k2[e] = co[2 * C + k];
-  }
+  const float* cq = co + c;
   auto finish = [&](int u, int h, const float* dd) {
     float o[8];
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
       const float zz = __uint_as_float((e & 1) ? (zr[u][e >> 1] & 0xffff0000u) : (zr[u][e >> 1] << 16));
-      o[e] = bn_bwd_map(dd[e], zz, sc[e], sf[e], mean[e], inv[e], k0[e], k1[e], k2[e], act, slope);
+      o[e] = bn_bwd_map(dd[e], zz, cq[3 * C + e], cq[4 * C + e], cq[5 * C + e], cq[6 * C + e], cq[e], cq[C + e],
+                        cq[2 * C + e], act, slope);
     }
     const long long i = ((long long)(nd_ * H + h) * W + w) * C + c;
     if (CG_PROBE(probe, 4)) return;
@@ -419,7 +440,8 @@ __global__ __launch_bounds__(256) void bn_bwd_fold_rows_kernel(const __bf16* __r
     for (int j = 2; j < 8; ++j) {
       const int a = j >> 2, b = (j >> 1) & 1, e = j & 1;
       const int sd = a < nd ? qd[a] : qd[0], sh = b < nh ? qh[b] : qh[0], sw = e < nw ? qw[e] : qw[0];
-      m[j] = *reinterpret_cast<const u32x4_n*>(padded + ((long long)((nb * Dp + sd) * Hp + sh) * Wp + sw) * C + c);
+      const unsigned mo = 2u * (unsigned)((((nb * Dp + sd) * Hp + sh) * Wp + sw) * C + c);
+      m[j] = __builtin_amdgcn_raw_buffer_load_b128(prs, (a < nd && b < nh && e < nw) ? mo : OOB, 0, 0);
     }
     m[1] = pw[u];
     float dd[8];
@@ -1106,12 +1128,18 @@ extern "C" int cgan3d_bn_backward_acc_fold(const void* padded, const void* z, in
   const long long n4 = nvox * c / 4;
   const long long rw = (long long)w * c / 8;  // 16-byte granules per row
   if (in_bf16 && c % 8 == 0 && rw <= 256 && (rw & (rw - 1)) == 0 && (long long)n * d <= 65535 &&
-      nvox * c < (1LL << 31)) {
-    const int lrw = __builtin_ctzll(rw), hpb = FOLD_U * (256 >> lrw);
-    ::cg::launch(bn_bwd_fold_rows_kernel, dim3((h + hpb - 1) / hpb, n * d), dim3(256), 0, (hipStream_t)stream,
+      (long long)n * (d + 2 * pad) * (h + 2 * pad) * (w + 2 * pad) * c * 2 < (1LL << 31)) {
+#ifdef CGAN3D_PROBES
+    const int fu = (g_probe & 64) ? 2 : 4;
+#else
+    const int fu = 4;
+#endif
+    const int lrw = __builtin_ctzll(rw), hpb = fu * (256 >> lrw);
+    ::cg::launch(fu == 2 ? bn_bwd_fold_rows_kernel<2> : bn_bwd_fold_rows_kernel<4>, dim3((h + hpb - 1) / hpb, n * d), dim3(256), 0, (hipStream_t)stream,
                  (const __bf16*)padded, (const __bf16*)z, d, h, w, pad, c, lrw, __builtin_ctz(c / 8), scale_shift,
                  mean_invstd, act, slope, dz, reinterpret_cast<__bf16*>(dz_bf16), acc, (int)reps, (double)nvox, gamma,
                  dgamma, dbeta, (int)accumulate, zero, (int)zero_n,
+                 (unsigned)((long long)n * (d + 2 * pad) * (h + 2 * pad) * (w + 2 * pad) * c * 2),
 #ifdef CGAN3D_PROBES
                  g_probe
 #else
