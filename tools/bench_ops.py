@@ -93,6 +93,26 @@ def _cases(B=4, S=64):
         flops = 2.0 * n3 * dout[0] * dout[1] * dout[2] * cin * cout * 64
         return (lambda: ops.conv(geo, dz, w, dx, ep)), flops
 
+    def dgrad_m4(cin, cout, din, dout, bf16_out, transposed=False):
+        """a stride-2 conv's input-grad as the step issues it at the 32 <-> 64 level (conv_t64 role 2):
+        bf16 dL/dz shadow in, dL/dx out with the BatchNorm-backward statistics of the layer below
+        (mode 4: its z, scale / shift, mean / invstd) — fp32 or bf16 output and z"""
+        geo = (ops.convt_dgrad_geom if transposed else ops.conv_dgrad_geom)(B, din, dout, cin, cout, 3, 2, 1)
+        w = t(cin, cout, 3, 3, 3) * 0.05 if transposed else t(cout, cin, 3, 3, 3) * 0.05
+        ps = ops.PackSet(dev)
+        geo, w = ps.add(geo, w, BF)
+        ps.pack()
+        dz = t(B, *dout, cout)
+        dz16 = dz.bfloat16()
+        dx = torch.empty(B, *din, cin, device=dev, dtype=torch.bfloat16 if bf16_out else torch.float32)
+        z = t(B, *din, cin)
+        z = z.bfloat16() if bf16_out else z
+        acc = torch.zeros(16 * 2 * cin, device=dev, dtype=torch.float64)
+        ss, mi = torch.ones(2 * cin, device=dev), torch.ones(2 * cin, device=dev)
+        ep = ops.epilogue(x_bf16=dz16, bn_z=z, bn_ss=ss, bn_mi=mi, bn_act=L.ACT_RELU, fuse=ops.BnFuse(acc, 4, 16))
+        flops = 2.0 * B * dout[0] * dout[1] * dout[2] * cin * cout * 27
+        return (lambda: ops.conv(geo, dz, w, dx, ep)), flops
+
     def ref_add3(shape):
         """calibration: torch's bf16 add (two reads, one write) over a tensor of `shape`; figure = HBM bytes"""
         a, b = t(*shape).bfloat16(), t(*shape).bfloat16()
@@ -193,6 +213,9 @@ def _cases(B=4, S=64):
         "crit_m1": lambda: crit(16, 32, R3),
         "crit_m2": lambda: crit(32, 64, (r // 2,) * 3),
         "crit_m2_gemm": lambda: crit(32, 64, (r // 2,) * 3, halo=False),
+        "down1_dgrad_m4": lambda: dgrad_m4(32, 64, H3, R3, False),
+        "down1_dgrad_m4_bf16": lambda: dgrad_m4(32, 64, H3, R3, True),
+        "up0_dgrad_m4": lambda: dgrad_m4(64, 32, R3, H3, False, True),
         "bn_fold64": lambda: bn_fold(),
         "bn_fold64_dz": lambda: bn_fold(True),
         "bn_fold64_r1": lambda: bn_fold(reps=1),
