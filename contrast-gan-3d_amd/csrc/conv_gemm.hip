@@ -526,18 +526,31 @@ __global__ __launch_bounds__(256) void adam_pack_kernel(float* __restrict__ p, c
     f32x4* m4 = reinterpret_cast<f32x4*>(m);
     f32x4* v4 = reinterpret_cast<f32x4*>(v);
     const f32x4* g4 = reinterpret_cast<const f32x4*>(g);
-    for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n4; i += (long long)gridDim.x * 256) {
-      const f32x4 gi = g4[i];
-      f32x4 mi = m4[i], vi = v4[i], pi = p4[i];
+    // ADAM_U float4 groups of a thread loaded before the first is updated (adam_launch sizes the grid
+    // at ~4 per thread: a single group in flight per lane left each of them a full HBM latency apart)
+    constexpr int ADAM_U = 4;
+    const long long st = (long long)gridDim.x * 256;
+    for (long long i0 = (long long)blockIdx.x * 256 + threadIdx.x; i0 < n4; i0 += ADAM_U * st) {
+      f32x4 gi[ADAM_U], mi[ADAM_U], vi[ADAM_U], pi[ADAM_U];
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        float a = mi[e], b = vi[e], c = pi[e];
-        adam_vals(k, gi[e], a, b, c);
-        mi[e] = a; vi[e] = b; pi[e] = c;
+      for (int u = 0; u < ADAM_U; ++u) {
+        const long long i = min(i0 + u * st, n4 - 1);  // clamped duplicates are loaded, never stored
+        gi[u] = g4[i]; mi[u] = m4[i]; vi[u] = v4[i]; pi[u] = p4[i];
       }
-      m4[i] = mi;
-      v4[i] = vi;
-      p4[i] = pi;
+#pragma unroll
+      for (int u = 0; u < ADAM_U; ++u) {
+        const long long i = i0 + u * st;
+        if (i >= n4) break;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          float a = mi[u][e], b = vi[u][e], c = pi[u][e];
+          adam_vals(k, gi[u][e], a, b, c);
+          mi[u][e] = a; vi[u][e] = b; pi[u][e] = c;
+        }
+        m4[i] = mi[u];
+        v4[i] = vi[u];
+        p4[i] = pi[u];
+      }
     }
     for (long long i = 4 * n4 + (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long long)gridDim.x * 256)
       adam_elem(k, p, g, m, v, i);

@@ -309,9 +309,13 @@ def test_plan_replay_matches_eager(prec):
         # (bf16: atomics order moves the small W-distance losses by ~1e-6 absolute)
         np.testing.assert_allclose(planned.losses.cpu().numpy(), eager.losses.cpu().numpy(), rtol=1e-4, atol=2e-5)
         # weight-gradient atomics may add in another order: gradients to 1e-3 of their largest entry
+        # (f32).  bf16: the critic's Adam (betas (0, 0.9): an update is ~lr * sign(grad)) turns the
+        # atomics' last-bit differences of sub-noise critic gradients into whole-lr sign flips before
+        # the generator's backward reads the critic — observed up to 1.01e-3 (round 5d), bound 2e-3
+        tol = 1e-3 if prec == "f32" else 2e-3
         for a1, a2 in ((eager.g_arena, planned.g_arena), (eager.d_arena, planned.d_arena)):
             g1, g2 = a1.grad.cpu().numpy(), a2.grad.cpu().numpy()
-            assert np.abs(g1 - g2).max() <= 1e-3 * np.abs(g1).max(), f"step {j}"
+            assert np.abs(g1 - g2).max() <= tol * np.abs(g1).max(), f"step {j}"
 
 
 def _sync_state(src, dst):
