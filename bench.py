@@ -104,8 +104,16 @@ def cpu_baseline(size, seconds, g_args):
     from cgan3d_amd.model.init import pcg64_state_dict
     from oracle import reference_torch as R
 
-    threads = max(1, min(16, len(os.sched_getaffinity(0))))
+    # every core the process may run on; the cgroup CPU quota, when one is set, is
+    # reported beside it (on the GPU box the affinity mask can be wider than the CPU share)
+    threads = max(1, len(os.sched_getaffinity(0)))
     torch.set_num_threads(threads)
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        quota = None if q == "max" else round(int(q) / int(per), 2)
+    except (OSError, ValueError):
+        pass
     gcfg = R.GenConfig(**g_args)
     cfg = R.StepConfig(gen=gcfg, critic=R.CriticConfig())
     gp = {k: torch.from_numpy(v.copy()) for k, v in pcg64_state_dict(list(R.gen_param_shapes(gcfg).items()), 0).items()}
@@ -134,7 +142,7 @@ def cpu_baseline(size, seconds, g_args):
     except OSError:
         pass
     return {"value": round(n * b / el, 4), "unit": "patches/s", "cores": threads, "kind": "port",
-            "cpu_model": cpu_model, "torch_threads": torch.get_num_threads(),
+            "cpu_model": cpu_model, "torch_threads": torch.get_num_threads(), "cgroup_cpu_quota": quota,
             "sample": f"oracle/reference_torch.py train_step, {size}^3, batch 1+1, GP conf, fp32, {n} steps in "
                       f"{el:.1f}s after 1 warm-up step; patches/s per subopt patch at batch 1 stands for the GPU "
                       f"line's batch (the CPU step's work and time grow linearly with the batch)"}

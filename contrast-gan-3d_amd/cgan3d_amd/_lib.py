@@ -142,7 +142,7 @@ _SIGS = {
     "cgan3d_reflect_fold_ex": ([_P, _P, _I32, _I32, _I32, _I32, _I32, _I32, _P, _P], _I32),
     "cgan3d_reflect_fold2d": ([_P, _P, _I32, _I32, _I32, _I32, _I32, _P, _P], _I32),
     "cgan3d_gp_interpolate": ([_P, _P, _P, _P, _I32, _I64, _P], _I32),
-    "cgan3d_gp_interpolate_idx": ([_P, _P, _P, _P, _P, _I32, _I64, _P], _I32),
+    "cgan3d_gp_interpolate_idx": ([_P, _P, _P, _P, _P, _I32, _I64, _I32, _I32, _P], _I32),
     "cgan3d_conv3d_wgrad_sk_ok": ([_P], _I32),
     "cgan3d_conv3d_wgrad_partials": ([_P], _I32),
     "cgan3d_wgrad_reduce_multi": ([_P, _I32, _P], _I32),

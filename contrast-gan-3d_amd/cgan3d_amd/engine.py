@@ -549,7 +549,10 @@ class GeneratorPlan:
         # single GPU: the ResNet weight grads leave their partials in per-layer workspaces and the
         # lowest ResNet layer's hand-off sums all of them in one launch (8 reduce launches -> 1;
         # under data parallelism every bucket needs its layers' final gradients: per-layer reduce)
-        k3 = [i for i in range(len(self.layers)) if ops.wgrad_partials(self.geo_wgrad[i]) > 0]
+        # only the side-stream layers defer (layers below wgrad_tail_main run their weight grad on the
+        # main stream, reduced in place): the combined reduce rides on the lowest DEFERRED layer's flush
+        k3 = [i for i in range(len(self.layers)) if ops.wgrad_partials(self.geo_wgrad[i]) > 0
+              and not (i < self.wgrad_tail_main and self.side is not None)]
         defer_red = (grads_enqueued is None and self.side is not None and len(k3) > 1
                      and not debug("no_defer_reduce"))
         k3_last = min(k3) if defer_red else None
@@ -651,6 +654,8 @@ class GeneratorPlan:
                 if pending:
                     flush()
                 self._on_side(side_after)
+        if self._deferred_red:  # a deferred weight grad whose partials no reduce was issued for
+            raise RuntimeError(f"{len(self._deferred_red)} deferred ResNet weight-grad reduces were never issued")
         if self.side is not None:  # the weight gradients are complete before anything reads them
             ops.stream_wait(torch.cuda.current_stream(self.device), self.side)
 
@@ -1438,7 +1443,21 @@ class StepEngine:
             raise ValueError(f"set_gp_indices: {self.b_gp} rows each")
         if r.min() < 0 or r.max() >= self.b_opt or f.min() < 0 or f.max() >= self.b_sub:
             raise ValueError("set_gp_indices: row out of range")
-        self.gp_idx.copy_(torch.from_numpy(np.concatenate([r, f]).astype(np.int32)), non_blocking=False)
+        # staged in a ring of pinned buffers and copied without blocking the host (a pageable copy
+        # would wait for the previous step to finish); a slot's event guards its reuse
+        if not self.gp_idx.is_cuda:
+            self.gp_idx.copy_(torch.from_numpy(np.concatenate([r, f]).astype(np.int32)))
+            return
+        if not hasattr(self, "_gp_ring"):
+            self._gp_ring = [(torch.empty(2 * self.b_gp, dtype=torch.int32, pin_memory=True), torch.cuda.Event())
+                             for _ in range(4)]
+            self._gp_slot = 0
+        buf, ev = self._gp_ring[self._gp_slot]
+        self._gp_slot = (self._gp_slot + 1) % len(self._gp_ring)
+        ev.synchronize()  # the copy that last read this slot (four calls ago) is done
+        buf.copy_(torch.from_numpy(np.concatenate([r, f]).astype(np.int32)))
+        self.gp_idx.copy_(buf, non_blocking=True)
+        ev.record(torch.cuda.current_stream(self.gp_idx.device))
 
     def draw_gp_indices(self, rng: np.random.Generator):
         """The reference's draw (model/utils.py:24-25): real rows first, then fake rows."""
@@ -1463,6 +1482,7 @@ class StepEngine:
 
     def generator_forward(self):
         self.G.forward(self.gP, self.subopt, opt_hat_out=self.opt_hat, training=True)
+        self.opt_hat_foreign = False  # opt_hat is this forward's output again (Trainer.train_critic)
         if self.gloss_side:
             self.G._on_side(self._generator_loss_grad)
 

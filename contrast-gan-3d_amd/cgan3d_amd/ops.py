@@ -1148,9 +1148,10 @@ def gp_interpolate(real, fake, eps, out, b, per_sample, idx=None):
         raise ValueError("gp_interpolate: idx must be contiguous int32 [2 b]")
     if real.numel() % per_sample or fake.numel() % per_sample:
         raise ValueError("gp_interpolate: real / fake must hold whole samples")
-    # the rows in idx are range-checked by whoever writes them (StepEngine.set_gp_indices), on the host
-    check(_launch("cgan3d_gp_interpolate_idx", ptr(real), ptr(fake), ptr(idx), ptr(eps), ptr(out), b, per_sample),
-          "gp_interpolate_idx")
+    # the rows in idx are range-checked by whoever writes them (StepEngine.set_gp_indices), on the host,
+    # and clamped to the two batches' row counts in the kernel
+    check(_launch("cgan3d_gp_interpolate_idx", ptr(real), ptr(fake), ptr(idx), ptr(eps), ptr(out), b, per_sample,
+                  real.numel() // per_sample, fake.numel() // per_sample), "gp_interpolate_idx")
 
 
 def tanh_backward(y, dy, dz):

@@ -139,6 +139,10 @@ class Trainer:
                     raise ValueError(f"train_critic: {name} has {t.numel()} elements, the engine's batch "
                                      f"{slot.numel()} (batch and patch size are fixed per engine)")
                 slot.view(-1).copy_(t.detach().reshape(-1), non_blocking=True)
+                if name == "reconstructions":
+                    # the slot no longer holds the generator forward's output: train_generator refuses
+                    # to backprop through it until the next generator forward
+                    eng.opt_hat_foreign = True
         self.optimizer_D.sync_hyper()
         eng.critic_update()
         if self.lr_scheduler_D is not None:
@@ -152,6 +156,9 @@ class Trainer:
         ``inputs`` / ``centerlines_masks`` its batch (None = the resident ones); anything else raises
         ValueError rather than silently training on another batch."""
         eng = self._need_engine("train_generator")
+        if getattr(eng, "opt_hat_foreign", False):
+            raise ValueError("train_generator: train_critic replaced the generator output with other reconstructions "
+                             "since the last generator forward (Trainer.train_step runs that forward)")
         for t, slot, name in ((inputs, eng.subopt, "inputs"), (reconstructions, eng.opt_hat, "reconstructions"),
                               (centerlines_masks, eng.mask, "centerlines_masks")):
             if not self._same(t, slot):
@@ -194,6 +201,7 @@ class Trainer:
         eng.eps.uniform_(0.0, 1.0)
         do_c = iteration % self.train_critic_every == 0
         log_dict = {}
+        eng.opt_hat_foreign = False  # the step's own generator forward (replayed or eager) writes opt_hat
         if self._replay(eng, do_c, do_g):
             if do_c:
                 log_dict = self._losses(["D"])

@@ -113,14 +113,18 @@ __global__ __launch_bounds__(256) void reflect_fold_bn_kernel(const float* __res
 
 // interpolation = eps*real + (1-eps)*fake  (model/utils.py:27-28)
 // idx (optional, device int32 [2 b]): sample s interpolates real row idx[s] and fake row idx[b + s] —
-// the reference's resampling when |real| != |fake| (model/utils.py:21-25)
+// the reference's resampling when |real| != |fake| (model/utils.py:21-25).  The rows are clamped to
+// [0, n_real) / [0, n_fake) on the device: a bad index reads a valid row instead of past the batch
+// (the host range-checks them, StepEngine.set_gp_indices)
 __global__ __launch_bounds__(256) void interp_kernel(const float* __restrict__ real, const float* __restrict__ fake,
                                                      const float* __restrict__ eps, float* __restrict__ out,
-                                                     long long ps, long long total, const int* __restrict__ idx, int b) {
+                                                     long long ps, long long total, const int* __restrict__ idx, int b,
+                                                     int n_real, int n_fake) {
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long long)gridDim.x * blockDim.x) {
     const long long s = i / ps, v = i - s * ps;
     const float e = eps[s];
-    const long long ir = idx ? (long long)idx[s] * ps + v : i, jf = idx ? (long long)idx[b + s] * ps + v : i;
+    const long long ir = idx ? (long long)min(max(idx[s], 0), n_real - 1) * ps + v : i,
+                    jf = idx ? (long long)min(max(idx[b + s], 0), n_fake - 1) * ps + v : i;
     out[i] = e * real[ir] + (1.f - e) * fake[jf];
   }
 }
@@ -237,18 +241,20 @@ extern "C" int cgan3d_gp_interpolate(const float* real, const float* fake, const
   const long long total = (long long)b * per_sample;
   int blocks = (int)std::min<long long>((total + 255) / 256, 4096);
   ::cg::launch(interp_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, real, fake, eps, out,
-                     (long long)per_sample, total, (const int*)nullptr, (int)b);
+                     (long long)per_sample, total, (const int*)nullptr, (int)b, (int)b, (int)b);
   CG_LAUNCH_CHECK("interp_kernel");
   return CGAN3D_OK;
 }
 
 extern "C" int cgan3d_gp_interpolate_idx(const float* real, const float* fake, const int32_t* idx, const float* eps,
-                                         float* out, int32_t b, int64_t per_sample, void* stream) {
-  CG_CHECK_ARG(real && fake && idx && eps && out && b > 0 && per_sample > 0, "cgan3d_gp_interpolate_idx: bad args");
+                                         float* out, int32_t b, int64_t per_sample, int32_t n_real, int32_t n_fake,
+                                         void* stream) {
+  CG_CHECK_ARG(real && fake && idx && eps && out && b > 0 && per_sample > 0 && n_real > 0 && n_fake > 0,
+               "cgan3d_gp_interpolate_idx: bad args");
   const long long total = (long long)b * per_sample;
   int blocks = (int)std::min<long long>((total + 255) / 256, 4096);
   ::cg::launch(interp_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, real, fake, eps, out,
-                     (long long)per_sample, total, (const int*)idx, (int)b);
+                     (long long)per_sample, total, (const int*)idx, (int)b, (int)n_real, (int)n_fake);
   CG_LAUNCH_CHECK("interp_kernel");
   return CGAN3D_OK;
 }

@@ -325,7 +325,8 @@ int32_t cgan3d_conv3d_wgrad_group_ok(const cgan3d_conv_geom* g);
  * (cgan3d_conv3d_wgrad_sk_ws_floats(g) floats, any contents), then one reduce launch that ADDS the
  * sums into dw[i] (torch layout, g.w_sa / g.w_sb).  1 <= n <= 4; geometries cgan3d_conv3d_wgrad_sk_ok:
  * bf16, not transposed, (cin, cout) = (8, 16) / (16, 32) / (32, 64), input = 2 x output, output
- * divisible by the variant's tile (4 x 8 x 8 / 4 x 4 x 8 / 4 x 4 x 4).  Two launches. */
+ * divisible by the variant's tile (d x h x w: 4 x 8 x 16 for 8 -> 16, 4 x 4 x 8 for 16 -> 32, 4 x 4 x 4 for
+ * 32 -> 64).  Two launches. */
 int32_t cgan3d_conv3d_wgrad_sk_ok(const cgan3d_conv_geom* g);
 int64_t cgan3d_conv3d_wgrad_sk_ws_floats(const cgan3d_conv_geom* g);
 int cgan3d_conv3d_wgrad_sk(const cgan3d_conv_geom* geoms, const float* const* gathered, const float* const* aligned,
@@ -445,9 +446,12 @@ int cgan3d_reflect_fold_ex(const float* padded, float* out, int32_t n, int32_t d
 int cgan3d_gp_interpolate(const float* real, const float* fake, const float* eps, float* out,
                           int32_t b, int64_t per_sample, void* stream);
 /* The same with the reference's resampling when |real| != |fake| (model/utils.py:21-25): sample s
- * interpolates real row idx[s] and fake row idx[b + s] (idx: device int32 [2 b], drawn by the host). */
+ * interpolates real row idx[s] and fake row idx[b + s] (idx: device int32 [2 b], drawn by the host);
+ * real / fake hold n_real / n_fake rows and the kernel clamps every index into them (round 6: a bad
+ * index can no longer read past either batch). */
 int cgan3d_gp_interpolate_idx(const float* real, const float* fake, const int32_t* idx, const float* eps,
-                              float* out, int32_t b, int64_t per_sample, void* stream);
+                              float* out, int32_t b, int64_t per_sample, int32_t n_real, int32_t n_fake,
+                              void* stream);
 
 int cgan3d_tanh_backward(const float* y, const float* dy, float* dz, int64_t n, void* stream);
 

@@ -349,6 +349,12 @@ def test_train_critic_generator_take_their_arguments(tmp_path):
         tr.train_generator(torch.zeros_like(eng.subopt), None, None)
     with pytest.raises(ValueError):
         tr.train_critic(real[:1], None, True)
+    # train_critic replaced opt_hat with foreign reconstructions: even the slot itself (equal values)
+    # is refused until the generator forward runs again (no backprop through G.att of
+    # another forward)
+    with pytest.raises(ValueError):
+        tr.train_generator(None, eng.opt_hat, None)
+    eng.generator_forward()
     # the resident batch (same storage or equal values) is accepted
     log = tr.train_generator(eng.subopt.clone(), eng.opt_hat, None)
     assert set(log) == {"G", "G-full", "sim", "HU"}

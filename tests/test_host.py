@@ -152,3 +152,19 @@ def test_conf_overwrites_module_builds_trainer_like_train_py(tmp_path):
     from cgan3d_amd.model.utils import count_parameters
     assert count_parameters(tr.generator) == 1035297 and count_parameters(tr.critic) == 176761
     assert set(tr.optimizer_G.state_dict()["param_groups"][0]) >= {"lr", "betas", "eps"}
+
+
+def test_wgrad_sk_eligibility_follows_the_variant_tiles():
+    """cgan3d_conv3d_wgrad_sk_ok (host code, no GPU): the 8 -> 16 variant's tile is 4 x 8 x 16 (d, h, w),
+    so an output width that is a multiple of 8 but not of 16 is not eligible (include/cgan3d.h states it,
+    ADVICE r05); 16 -> 32 takes 4 x 4 x 8, 32 -> 64 takes 4 x 4 x 4."""
+    from cgan3d_amd import ops, _lib as L
+    BF = L.PREC_BF16
+
+    def ok(cin, cout, dout):
+        din = tuple(2 * d for d in dout)
+        return ops.wgrad_sk_ok(ops.with_prec(ops.conv_wgrad_geom(12, din, dout, cin, cout, 4, 2, 1), BF))
+    assert ok(8, 16, (16, 16, 16)) and ok(8, 16, (4, 8, 16))
+    assert not ok(8, 16, (16, 16, 8)) and not ok(8, 16, (8, 8, 24))
+    assert ok(16, 32, (8, 8, 8)) and not ok(16, 32, (8, 8, 4))
+    assert ok(32, 64, (4, 4, 4)) and not ok(32, 64, (4, 4, 2))
