@@ -210,6 +210,7 @@ __device__ __forceinline__ void bn_pair(const Epi& e, float v, long long o, int 
 // specialised k = 7 generator first/last conv kernels (conv_k7.hip); return 1 when they apply
 int k7_try_fwd(const cgan3d_conv_geom* g, const float* x, const float* w, float* y, const Epi& e, hipStream_t s);
 void k7s_set(int v);
+void k7p_set(int v);
 int k7_wgrad_handles(const cgan3d_conv_geom* g);
 int k7m_wgrad_taken(const cgan3d_conv_geom* g);
 int k7m_w2n_taken(const cgan3d_conv_geom* g);

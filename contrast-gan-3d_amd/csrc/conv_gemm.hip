@@ -678,6 +678,8 @@ extern "C" int cgan3d_set_tuning(int32_t key, int32_t value) {
     case 15: CG_CHECK_ARG(value == 0 || value == 1, "cgan3d_set_tuning 15: 0 or 1"); k3m_set(value); return CGAN3D_OK;
     case 16: CG_CHECK_ARG(value == 0 || value == 1, "cgan3d_set_tuning 16: 0 or 1"); wgrad_k3m_set(value); return CGAN3D_OK;
     case 20: CG_CHECK_ARG(value > 0, "cgan3d_set_tuning 20: blocks > 0"); k7wg_blocks_set(value); return CGAN3D_OK;
+    case 21:  // round 6: output planes per streamed-plane 1 -> 16 k7 block (0 auto; -1: the k7m_n2w kernel)
+      CG_CHECK_ARG(value >= -1 && value <= 64, "cgan3d_set_tuning 21: -1 .. 64"); k7p_set(value); return CGAN3D_OK;
 #ifdef CGAN3D_PROBES
     case 90: g_probe = value; return CGAN3D_OK;  // phase probes (common.h CG_PROBE), timing only
 #endif

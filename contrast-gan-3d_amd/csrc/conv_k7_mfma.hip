@@ -62,22 +62,6 @@ constexpr int N_PAIRS = 52;                                 // 49 (td, th) pairs
 constexpr int N_US = N_TW * 8 + N_US_PAD;
 constexpr int N_X = N_ROWS * N_HW / 2, N_X_PER = (N_X + 255) / 256;  // halo value pairs (w, w + 1)
 
-// mode-2 BatchNorm statistics of the reflect-folded output (cgan3d_epilogue.bn_fold): the input-grad
-// of the generator's last conv lands on the padded grid, dy = fold(out) on the unpadded one, and
-// sum_v dy(v) a(v) = sum_q out(q) a(refl(q - P)) for the pair weights a = act' (1, xhat) — so the
-// statistics come straight from this kernel's outputs and z at the reflected voxel (no fold pass)
-struct K7Fold {
-  const float* z;   // BatchNorm input on the unpadded grid [n][zd][zh][zw][16]
-  const float* ss;  // [scale | shift]
-  const float* mi;  // [mean | invstd]
-  float* part;      // mode-2 slab, slot = block
-  double* acc;      // or fp64 accumulators (cgan3d_bn_fuse acc_mode 4): replica block % reps
-  int reps;
-  int act;
-  float slope;
-  int P, zd, zh, zw;
-};
-
 // sum over the 16 lanes of a row (the voxel lanes r16 of a transposed MFMA tile)
 __device__ __forceinline__ float k7m_rowsum16(float v) {
 #pragma unroll
@@ -1038,6 +1022,9 @@ void k7m_n2w_launch(const cgan3d_conv_geom* g, int P, int reflect, int flip, lon
     acc1 = fz->acc_out;
     reps1 = fz->reps;
   }
+  // the streamed-plane kernel (conv_k7p.hip) takes the step's statistics modes (none, fp64 accumulators,
+  // folded accumulators); the slab forms stay here
+  if (!stats && !bn_part && k7p_n2w_try(g, P, reflect, flip, wc, x, w, y, fold ? &fb : nullptr, fz, out16, s)) return;
   ::cg::launch(out16 ? k7m_n2w_kernel<true> : k7m_n2w_kernel<false>, dim3(grid), dim3(256), 0, s, a, x, w, y, stats,
                bn_part, per, nt, fb, acc1, reps1);
 }
@@ -1080,12 +1067,15 @@ long long k7m_wgrad_ws_floats(const cgan3d_conv_geom* g) {
   int grid, per, nt, grid2;
   k7m_wg_split(g, true, &grid, &per, &nt);
   k7m_wg_split(g, false, &grid2, &per, &nt);
-  return (long long)std::max(grid, grid2) * G_COLS;
+  // the streamed-plane kernel's partial rows (conv_k7p.hip) share the workspace
+  const long long p1 = k7p_wg_blocks(g, true), p2 = k7p_wg_blocks(g, false);
+  return std::max<long long>(std::max(grid, grid2), std::max(p1, p2)) * G_COLS;
 }
 
 // weight grad of a k7 conv with one single-channel side; dw already zeroed (or accumulating)
 void k7m_wgrad_launch(const cgan3d_conv_geom* g, bool wide_in, long long wc, const float* x, const float* go, float* dw,
                       float* ws, hipStream_t s, const __bf16* wide16) {
+  if (k7p_wgrad_try(g, wide_in, wc, x, go, dw, ws, s, wide16)) return;
   const K7Args a = k7m_args(g, g->pad, g->reflect, 0, wc, G_TD, G_TH, G_TW);
   int grid, per, ntiles;
   k7m_wg_split(g, wide_in, &grid, &per, &ntiles);

@@ -358,7 +358,9 @@ def test_k7_bf16_mfma(sp):
     acc = torch.zeros(reps * 2 * 16, device="cuda", dtype=torch.float64)
     ya = torch.empty_like(yo)
     ops.conv(geo, _cl(x1), wf.detach().float().cuda(), ya, ops.epilogue(fuse=ops.BnFuse(acc, 3, reps)))
-    assert torch.equal(ya, yo)
+    # the accumulator form runs the streamed-plane kernel (conv_k7p.hip, round 6): the same bf16
+    # products summed in another fp32 order than the slab form's k7m_n2w kernel
+    assert float((ya - yo).abs().max()) <= 1e-5 * float(yo.abs().max()), "k7p vs k7m forward"
     a2 = acc.cpu().view(reps, 2, 16).sum(0)
     N = yk.shape[0]
     assert_close((a2[0] / N).numpy(), yk.mean(0).numpy(), 1e-4, "k7 acc mean")
@@ -399,6 +401,101 @@ def test_k7_bf16_mfma(sp):
     dxo = torch.empty(n, *dims, 16, device="cuda")
     ops.reflect_fold(dpad, dxo, n, dims, 16, p)
     assert_close(_ncdhw(dxo).numpy(), dx16.numpy(), 2e-2, "k7 n2w dgrad")
+
+
+def _k7_fold_operands(n, dims, g, z16):
+    """BatchNorm-backward operands of the layer under the last conv (its z, scale / shift, mean / invstd)
+    for the folded mode-2 statistics of the k7 input-grad"""
+    z = torch.randn(n, *dims, 16, generator=g).cuda()
+    ss = torch.cat([torch.rand(16, generator=g) + 0.5, torch.randn(16, generator=g) * 0.1]).cuda()
+    mi = torch.cat([torch.randn(16, generator=g) * 0.1, torch.rand(16, generator=g) + 0.5]).cuda()
+    return (z.bfloat16() if z16 else z), ss, mi
+
+
+@pytest.mark.parametrize("sp,tdc", [((12, 20, 36), 0), ((16, 16, 16), 5), ((20, 9, 72), 7), ((9, 33, 17), 64)])
+def test_k7p_n2w_matches_k7m(sp, tdc):
+    """The streamed-plane 1 -> 16 k7 kernel (conv_k7p.hip, round 6; cgan3d_set_tuning key 21 = output
+    planes per block) against the per-tile k7m_n2w kernel (key 21 = -1) on the same bf16 operands, in
+    every role the bf16 step gives it: the first conv's forward without statistics / with fp64
+    accumulator statistics (mode 3), fp32 and bf16 output; the last conv's input-grad onto the padded grid
+    with and without the reflect-folded mode-2 statistics (mode 4 accumulators), fp32 and bf16 z / output.
+    Outputs agree to fp32 reassociation (1e-5 of the largest), statistics to 1e-5 relative, ragged tiles
+    and chunks included; the forward also against torch float64 at the bf16 bar."""
+    from cgan3d_amd import ops, _lib as L
+    BF = L.PREC_BF16
+    lib = L.load()
+    g = torch.Generator().manual_seed(sum(sp) + tdc)
+    n, k, p = 2, 7, 3
+    x1 = torch.randn(n, 1, *sp, generator=g, dtype=torch.float64)
+    wf = torch.randn(16, 1, k, k, k, generator=g, dtype=torch.float64) / np.sqrt(k**3)
+    wl = torch.randn(1, 16, k, k, k, generator=g, dtype=torch.float64) / np.sqrt(16 * k**3)
+    gl = torch.randn(n, 1, *sp, generator=g, dtype=torch.float64)
+    gf = torch.randn(n, 16, *sp, generator=g, dtype=torch.float64)
+    x16 = torch.randn(n, 16, *sp, generator=g, dtype=torch.float64)
+    dims = tuple(sp)
+    pd = tuple(d + 2 * p for d in dims)
+    reps = 16
+
+    def run(key):
+        L.check(lib.cgan3d_set_tuning(21, key), "k7p tdc")
+        out = {}
+        geo = ops.with_prec(ops.conv_fwd_geom(n, dims, dims, 1, 16, k, 1, p, True), BF)
+        for dt in (torch.float32, torch.bfloat16):
+            y = torch.empty(n, *dims, 16, device="cuda", dtype=dt)
+            ops.conv(geo, _cl(x1), wf.float().cuda(), y, ops.epilogue())
+            out[f"fwd {dt}"] = y.float()
+            acc = torch.zeros(reps * 2 * 16, device="cuda", dtype=torch.float64)
+            y = torch.empty(n, *dims, 16, device="cuda", dtype=dt)
+            ops.conv(geo, _cl(x1), wf.float().cuda(), y, ops.epilogue(fuse=ops.BnFuse(acc, 3, reps)))
+            out[f"fwd3 {dt}"] = y.float()
+            out[f"acc3 {dt}"] = acc.view(reps, 2, 16).sum(0)
+        gd = ops.with_prec(ops.conv_dgrad_geom(n, pd, dims, 16, 1, k, 1, 0), BF)
+        for z16 in (False, True):
+            dt = torch.bfloat16 if z16 else torch.float32
+            dpad = torch.empty(n, *pd, 16, device="cuda", dtype=dt)
+            ops.conv(gd, _cl(gl), wl.float().cuda(), dpad, ops.epilogue())
+            out[f"dgrad {dt}"] = dpad.float()
+            gz = torch.Generator().manual_seed(5)
+            z, ss, mi = _k7_fold_operands(n, dims, gz, z16)
+            acc = torch.zeros(reps * 2 * 16, device="cuda", dtype=torch.float64)
+            ep = ops.epilogue(bn_z=z, bn_ss=ss, bn_mi=mi, bn_act=L.ACT_RELU, fuse=ops.BnFuse(acc, 4, reps))
+            ep.bn_fold = p
+            dpad = torch.empty(n, *pd, 16, device="cuda", dtype=dt)
+            ops.conv(gd, _cl(gl), wl.float().cuda(), dpad, ep)
+            out[f"dgrad4 {dt}"] = dpad.float()
+            out[f"acc4 {dt}"] = acc.view(reps, 2, 16).sum(0)
+        # weight grads from the 16-channel operand's bf16 shadow (the step's form: k7p_wg_kernel, round 6)
+        gw0 = ops.with_prec(ops.conv_wgrad_geom(n, dims, dims, 1, 16, k, 1, p, True), BF)
+        ws = torch.empty(ops.wgrad_ws_floats(gw0), device="cuda")
+        dw0 = torch.empty(16, 1, k, k, k, device="cuda")
+        ops.wgrad(gw0, _cl(x1), _cl(gf), dw0, ws, aligned16=_cl(gf).bfloat16())
+        out["wg first float32"] = dw0.clone()
+        gw1 = ops.with_prec(ops.conv_wgrad_geom(n, dims, dims, 16, 1, k, 1, p, True), BF)
+        ws = torch.empty(ops.wgrad_ws_floats(gw1), device="cuda")
+        dw1 = torch.empty(1, 16, k, k, k, device="cuda")
+        ops.wgrad(gw1, _cl(x16), _cl(gl), dw1, ws, gathered16=_cl(x16).bfloat16())
+        out["wg last float32"] = dw1.clone()
+        torch.cuda.synchronize()
+        return out
+
+    try:
+        new, old = run(tdc), run(-1)
+    finally:
+        L.check(lib.cgan3d_set_tuning(21, 0), "k7p auto")
+    for key in new:
+        a, b = new[key].double().cpu(), old[key].double().cpu()
+        scale = float(b.abs().max())
+        bar = 1e-5 if "acc" in key or "float32" in key else 8e-3  # bf16 outputs: one rounding step apart at most
+        assert float((a - b).abs().max()) <= bar * scale, (key, float((a - b).abs().max()), scale)
+    yf = _ref_conv(x1, wf, 1, p, True)
+    assert_close(_ncdhw(new["fwd3 torch.float32"]).numpy(), yf.numpy(), 2e-2, "k7p fwd vs float64")
+    # the weight grads against float64 autograd (bf16 operands: the bf16 bar)
+    wf_ = wf.clone().requires_grad_()
+    dwf, = torch.autograd.grad(_ref_conv(x1, wf_, 1, p, True), (wf_,), gf)
+    assert_close(new["wg first float32"].double().cpu().numpy(), dwf.numpy(), 2e-2, "k7p wg first vs float64")
+    wl_ = wl.clone().requires_grad_()
+    dwl, = torch.autograd.grad(_ref_conv(x16, wl_, 1, p, True), (wl_,), gl)
+    assert_close(new["wg last float32"].double().cpu().numpy(), dwl.numpy(), 2e-2, "k7p wg last vs float64")
 
 
 WGRAD_BF16_CASES = [

@@ -198,8 +198,37 @@ def _cases(B=4, S=64):
         ep = ops.epilogue(fuse=ops.BnFuse(acc, 3, 16))
         return (lambda: ops.conv(geo, x, w, y, ep)), 2.0 * B * S**3 * 16 * 343
 
+    def k7_last_dgrad_step():
+        """the generator last conv's input-grad as the bf16 step issues it: onto the reflect-padded grid,
+        bf16 output, the folded mode-2 statistics of the BatchNorm below from its bf16 z (fp64 accumulators)"""
+        P3_ = (S + 6,) * 3
+        geo = ops.with_prec(ops.conv_dgrad_geom(B, P3_, F3, 16, 1, 7, 1, 0), BF)
+        w = t(1, 16, 7, 7, 7) * 0.05
+        dz = t(B, *F3, 1)
+        y = torch.empty(B, *P3_, 16, device=dev, dtype=torch.bfloat16)
+        z = t(B, *F3, 16).bfloat16()
+        ss, mi = torch.ones(32, device=dev), torch.ones(32, device=dev)
+        acc = torch.zeros(16 * 2 * 16, device=dev, dtype=torch.float64)
+        ep = ops.epilogue(bn_z=z, bn_ss=ss, bn_mi=mi, bn_act=L.ACT_RELU, fuse=ops.BnFuse(acc, 4, 16))
+        ep.bn_fold = 3
+        return (lambda: ops.conv(geo, dz, w, y, ep)), 2.0 * B * S**3 * 16 * 343
+
+    def k7_wgrad_step(last):
+        """a k7 weight grad as the bf16 step issues it: the 16-channel operand from its bf16 shadow
+        (dL/dz of the first conv / the last conv's input)"""
+        cin, cout = (16, 1) if last else (1, 16)
+        geo = ops.with_prec(ops.conv_wgrad_geom(B, F3, F3, cin, cout, 7, 1, 3, True), BF)
+        x, go = t(B, *F3, cin), t(B, *F3, cout)
+        dw = torch.empty(cout, cin, 7, 7, 7, device=dev)
+        ws = torch.empty(ops.wgrad_ws_floats(geo), device=dev)
+        kw = dict(gathered16=x.bfloat16()) if last else dict(aligned16=go.bfloat16())
+        return (lambda: ops.wgrad(geo, x, go, dw, ws, **kw)), 2.0 * B * S**3 * 16 * 343
+
     return {
+        "k7_first_wgrad_step": lambda: k7_wgrad_step(False),
+        "k7_last_wgrad_step": lambda: k7_wgrad_step(True),
         "k7_first_step": lambda: k7_first_step(),
+        "k7_last_dgrad_step": lambda: k7_last_dgrad_step(),
         "res_fwd_k3m": lambda: res_k3m(False),
         "res_dgrad_k3m": lambda: res_k3m(True),
         "res_fwd_k3m_r64": lambda: res_k3m(False, reps=64),
