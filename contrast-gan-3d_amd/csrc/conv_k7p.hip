@@ -34,11 +34,18 @@ constexpr int NT = 256;              // 4 waves
 constexpr int SH = 16, WB = 16;      // output rows / columns per block (4 rows per wave)
 constexpr int ROWS = SH + 6;         // staged input rows
 constexpr int POS = 24;              // staged positions per copy row (bf16): windows start at 0, 4, .., 16
-constexpr int ROWB = 4 * POS * 2;    // staged row bytes: 4 shifted copies
+constexpr int ROWB = 4 * POS * 2;    // staged row bytes: 6 groups of 4 positions x 4 shifted copies (192:
+                                     // rows 16 dwords apart mod 32, for the weight grad's two-row lane groups)
 constexpr int PLANEB = (ROWS + 1) * ROWB;  // bytes per ring buffer: + one zero row (read by th = 7 only)
 constexpr int NBUF = 3;              // ring: the plane computed, the plane written, one free
 constexpr int TASKS = ROWS * (POS / 4);  // staging tasks per plane: (row, group of 4 positions) = 132
 constexpr int RINGB = NBUF * PLANEB > 14 * 64 * 16 ? NBUF * PLANEB : 14 * 64 * 16;  // also the weight image
+// n2w, wave-private staging (round 6b): a wave stages the 10 input rows its 4 output rows read through th <= 6
+// (row 10, read only with the zero weights of th = 7, is never staged: it keeps finite stale values), into
+// two buffers of its own — the plane loop then needs no workgroup barrier
+constexpr int WROWS = 11, WTASKS = 10 * (POS / 4), WNB = 2;
+constexpr int WPLANE = WROWS * ROWB, WREG = WNB * WPLANE;
+constexpr int NRINGB = 4 * WREG > 14 * 64 * 16 ? 4 * WREG : 14 * 64 * 16;
 }  // namespace k7p
 
 typedef __bf16 bf16x8_p __attribute__((ext_vector_type(8)));
@@ -63,7 +70,7 @@ __global__ __launch_bounds__(256, 2) void k7p_n2w_kernel(K7Args a, const float* 
   using namespace k7p;
   constexpr int C = 16;
   constexpr unsigned OOB = 0x80000000u;  // past every buffer: loads return 0, stores are dropped
-  __shared__ __attribute__((aligned(16))) unsigned char ring[RINGB];
+  __shared__ __attribute__((aligned(16))) unsigned char ring[NRINGB];
   __shared__ __attribute__((aligned(16))) float coef[4 * C];  // mode 2: scale, shift, mean, invstd
   __shared__ float red[8 * 4 * C];
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -77,14 +84,14 @@ __global__ __launch_bounds__(256, 2) void k7p_n2w_kernel(K7Args a, const float* 
   const int tdl = min(tdc, a.do_ - d0);  // output planes of this chunk
   const int nsteps = tdl + 6;            // input planes streamed
 
-  // staging task of this thread (tid < TASKS): row r, positions 4 m .. 4 m + 3 of every copy, from the
-  // eight source values x[q][h0 - P + r][w0 - 4 + 4 m + i], i = 0..7 (byte offsets inside the plane,
-  // reflect / zero padding resolved here: OOB = zero)
-  const bool stager = tid < TASKS;
-  const int tr = tid / (POS / 4), tm = tid - tr * (POS / 4);
+  // staging task of this lane (lane < WTASKS): the wave's row r (block row 4 wave + r), positions 4 m ..
+  // 4 m + 3 of every copy, from the eight source values x[q][h0 - P + 4 wave + r][w0 - P - 1 + 4 m + i],
+  // i = 0..7 (byte offsets inside the plane, reflect / zero padding resolved here: OOB = zero)
+  const bool stager = lane < WTASKS;
+  const int tr = lane / (POS / 4), tm = lane - tr * (POS / 4);
   unsigned soff[8];
   {
-    const int ih = k7_src(h0 - a.P + tr, a.hi, a.reflect);
+    const int ih = k7_src(h0 - a.P + 4 * wave + tr, a.hi, a.reflect);
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       // window position p = 4 m + i holds x[w0 - P - 1 + p] (lane w reads positions w + 1 .. w + 8)
@@ -108,11 +115,10 @@ __global__ __launch_bounds__(256, 2) void k7p_n2w_kernel(K7Args a, const float* 
                    d3 = k7p_pack(sv[6], sv[7]);
     const unsigned a01 = __builtin_amdgcn_alignbyte(d1, d0_, 2), a12 = __builtin_amdgcn_alignbyte(d2, d1, 2),
                    a23 = __builtin_amdgcn_alignbyte(d3, d2, 2);
-    unsigned char* rb = ring + (sp % NBUF) * PLANEB + tr * ROWB + tm * 8;
-    *reinterpret_cast<u32x2_p*>(rb + 0 * POS * 2) = u32x2_p{d0_, d1};
-    *reinterpret_cast<u32x2_p*>(rb + 1 * POS * 2) = u32x2_p{a01, a12};
-    *reinterpret_cast<u32x2_p*>(rb + 2 * POS * 2) = u32x2_p{d1, d2};
-    *reinterpret_cast<u32x2_p*>(rb + 3 * POS * 2) = u32x2_p{a12, a23};
+    // row layout [group k][copy c][4 positions]: a task's four copies are 32 contiguous bytes
+    unsigned char* rb = ring + wave * WREG + (sp % WNB) * WPLANE + tr * ROWB + tm * 32;
+    *reinterpret_cast<u32x4_p*>(rb) = u32x4_p{d0_, d1, a01, a12};
+    *reinterpret_cast<u32x4_p*>(rb + 16) = u32x4_p{d1, d2, a12, a23};
   };
   load(0);  // in flight during the weight staging
 
@@ -139,20 +145,20 @@ __global__ __launch_bounds__(256, 2) void k7p_n2w_kernel(K7Args a, const float* 
       for (int kk = 0; kk < 2; ++kk) wa[td][kk] = reinterpret_cast<const bf16x8_p*>(wi)[(td * 2 + kk) * 64 + lane];
     __syncthreads();  // the image is dead before the first plane is staged over it
   }
-  for (int i = tid; i < NBUF * ROWB / 4; i += NT) {  // the zero row of every buffer (never staged)
-    const int b = i / (ROWB / 4), j = i - b * (ROWB / 4);
-    reinterpret_cast<unsigned*>(ring + b * PLANEB + ROWS * ROWB)[j] = 0u;
-  }
-  store(0);
-  load(1);
+  for (int i = lane; i < WREG / 16; i += 64)  // this wave's buffers zeroed once (the unstaged row stays finite)
+    reinterpret_cast<u32x4_p*>(ring + wave * WREG)[i] = u32x4_p{0u, 0u, 0u, 0u};
   if (MODE == 2 && tid < C) {
     coef[tid] = fb.ss[tid]; coef[C + tid] = fb.ss[C + tid];
     coef[2 * C + tid] = fb.mi[tid]; coef[3 * C + tid] = fb.mi[C + tid];
   }
+  store(0);
+  load(1);
+  __syncthreads();  // coef: the last workgroup barrier before the epilogue
 
-  // this lane's fragment base (bytes): row 4 wave + g, copy c = (w + 1) & 3, position w + 1 - c
-  const int cl = (r16 + 1) & 3;
-  const int fbase = (4 * wave + g) * ROWB + cl * POS * 2 + (r16 + 1 - cl) * 2;
+  // this lane's fragment base (bytes): row 4 wave + g, window positions j = w + 1 .. w + 8 = copy j & 3 of
+  // groups j >> 2 and (j >> 2) + 1 (a 16-lane group's 8-byte reads then cover all 32 banks of each access)
+  const int jw = r16 + 1;
+  const int fbase = wave * WREG + g * ROWB + (4 * (jw >> 2) + (jw & 3)) * 8;
   f32x4 acc[4][7];
 #pragma unroll
   for (int r = 0; r < 4; ++r)
@@ -164,28 +170,28 @@ __global__ __launch_bounds__(256, 2) void k7p_n2w_kernel(K7Args a, const float* 
   const int oh0 = h0 + 4 * wave;
   const long long ybytes = (long long)a.n * a.do_ * a.ho * a.wo * C * (B16 ? 2 : 4);
   const __amdgpu_buffer_rsrc_t ys = __builtin_amdgcn_make_buffer_rsrc((void*)y, (short)0, (int)ybytes, 0x00020000);
-  unsigned yoff[4];  // byte offset of this lane's 4 channels of rows r at output plane d0 (+ plane stride per step)
-#pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const bool ok = oh0 + r < a.ho && ow < a.wo;
-    yoff[r] = ok ? (unsigned)((((long long)(n * a.do_ + d0) * a.ho + oh0 + r) * a.wo + ow) * C + 4 * g) * (B16 ? 2u : 4u)
-                 : OOB;
-  }
+  // byte offset of this lane's 4 channels of row 0 at output plane d0 (OOB past the volume's columns); rows
+  // add a uniform stride and a uniform row count bounds them (one register instead of four)
+  const unsigned ybase = ow < a.wo
+      ? (unsigned)((((long long)(n * a.do_ + d0) * a.ho + oh0) * a.wo + ow) * C + 4 * g) * (B16 ? 2u : 4u) : OOB;
+  const unsigned yrow = (unsigned)(a.wo * C * (B16 ? 2 : 4));
+  const int nrows = __builtin_amdgcn_readfirstlane(min(max(a.ho - oh0, 0), 4));
   const unsigned ypl = (unsigned)(a.ho * a.wo * C * (B16 ? 2 : 4));  // bytes per output plane
   // statistics (mode 1: per-lane sums shifted by the lane's first output; valid rows only)
   float sK[4] = {0.f, 0.f, 0.f, 0.f}, sS1[4] = {0.f, 0.f, 0.f, 0.f}, sS2[4] = {0.f, 0.f, 0.f, 0.f};
   float sN = 0.f;
   float fp1[4] = {0.f, 0.f, 0.f, 0.f}, fp2[4] = {0.f, 0.f, 0.f, 0.f};
-  int nval = 0;  // valid rows of this lane (0..4; all lanes of a full tile: 4)
-#pragma unroll
-  for (int r = 0; r < 4; ++r) nval += (oh0 + r < a.ho && ow < a.wo) ? 1 : 0;
+  const int nval = ow < a.wo ? nrows : 0;  // valid rows of this lane (0..4; all lanes of a full tile: 4)
 
   for (int s0 = 0; s0 < nsteps; s0 += 7) {
 #pragma unroll
     for (int u = 0; u < 7; ++u) {
       const int s = s0 + u;
       if (s >= nsteps) break;
-      lds_barrier();  // plane s is in LDS; every wave is past its reads of the buffer written next
+      // plane s is in this wave's LDS (its own writes, in order); no barrier.  The scheduling fence keeps
+      // the compiler from hoisting the next step's reads into this one (live ranges past 256 VGPRs)
+      asm volatile("" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
       // every step issues the same vector-memory instructions (staging loads past the chunk read an empty
       // buffer, stores of a step without a flush get OOB offsets): the compiler's vmcnt wait for the
       // staged values then skips the previous flush's stores instead of waiting for everything
@@ -206,8 +212,9 @@ __global__ __launch_bounds__(256, 2) void k7p_n2w_kernel(K7Args a, const float* 
         }
       };
       if (MODE == 2 && B16) zload();  // before the MFMAs: they cover the latency (every step: static counts)
-      const unsigned char* pb = ring + (s % NBUF) * PLANEB + fbase;
+      const unsigned char* pb = ring + (s % WNB) * WPLANE + fbase;
       const int tlo = max(0, s - (tdl - 1)), thi = min(6, s);  // td whose output plane s - td is in the chunk
+      const unsigned tmask = __builtin_amdgcn_readfirstlane(((2u << thi) - 1u) & ~((1u << tlo) - 1u));
       const int slot0 = u;  // slot of td: (u - td) mod 7
       bf16x8_p fr[4][2];  // (row, kk): x[q][row + 4 kk + g][w + 1 .. w + 8 positions]
       auto fread = [&](int r) {
@@ -215,7 +222,7 @@ __global__ __launch_bounds__(256, 2) void k7p_n2w_kernel(K7Args a, const float* 
         for (int kk = 0; kk < 2; ++kk) {
           const unsigned char* p = pb + (r + 4 * kk) * ROWB;
           const u32x2_p lo = CG_PROBE(a.probe, 4) ? u32x2_p{0x3f003f00u, 0x3f003f00u} : *reinterpret_cast<const u32x2_p*>(p),
-                        hi = CG_PROBE(a.probe, 4) ? lo : *reinterpret_cast<const u32x2_p*>(p + 8);
+                        hi = CG_PROBE(a.probe, 4) ? lo : *reinterpret_cast<const u32x2_p*>(p + 32);
           const u32x4_p q4 = {lo[0], lo[1], hi[0], hi[1]};
           fr[r][kk] = reinterpret_cast<const bf16x8_p&>(q4);
         }
@@ -234,7 +241,7 @@ __global__ __launch_bounds__(256, 2) void k7p_n2w_kernel(K7Args a, const float* 
         }
 #pragma unroll
         for (int td = 0; td < 7; ++td) {
-          if (td < tlo || td > thi || CG_PROBE(a.probe, 1)) continue;
+          if (!((tmask >> td) & 1u) || CG_PROBE(a.probe, 1)) continue;
           const int slot = (slot0 - td + 7) % 7;
 #pragma unroll
           for (int rr = 0; rr < 2; ++rr) {
@@ -252,7 +259,7 @@ __global__ __launch_bounds__(256, 2) void k7p_n2w_kernel(K7Args a, const float* 
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const f32x4 v = acc[r][f];
-          const unsigned o = (!fl || yoff[r] == OOB) ? OOB : yoff[r] + po;
+          const unsigned o = (!fl || ybase == OOB || r >= nrows) ? OOB : ybase + r * yrow + po;
           if (CG_PROBE(a.probe, 8)) {
           } else if constexpr (B16) {
             __builtin_amdgcn_raw_buffer_store_b64(u32x2_p{k7p_pack(v[0], v[1]), k7p_pack(v[2], v[3])}, ys, o, 0, 0);
@@ -407,8 +414,11 @@ __global__ __launch_bounds__(256, 2) void k7p_wg_kernel(K7Args a, const float* _
   using namespace k7g;
   constexpr int C = 16;
   constexpr unsigned OOB = 0x80000000u;
-  __shared__ __attribute__((aligned(16))) unsigned char xr[NBUF * PLANEB];  // X1 ring
-  __shared__ __attribute__((aligned(16))) unsigned char ar[NA * APL];       // A16 staging (and the reduction)
+  // wave-private staging (as k7p_n2w): per wave two X1 planes of its 10 rows (+ one never-staged row) and
+  // two A16 planes of its 4 rows; the block's bytes are then reused by the epilogue's reduction (28 KB)
+  constexpr int WAPL = 4 * AROW;                       // A16 rows of a wave: 2 KB
+  constexpr int WSZ = WNB * WPLANE + WNB * WAPL;       // per wave: 8.2 KB
+  __shared__ __attribute__((aligned(16))) unsigned char lds[4 * WSZ > 28 * 1024 ? 4 * WSZ : 28 * 1024];
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int g = lane >> 4, r16 = lane & 15;
   // grid (the A16 side) tile: a.do_ / a.ho / a.wo are the grid dims; a.di / a.hi / a.wi and a.P / a.reflect
@@ -422,12 +432,14 @@ __global__ __launch_bounds__(256, 2) void k7p_wg_kernel(K7Args a, const float* _
   const int tdl = min(tdc, a.do_ - d0);
   const int nsteps = tdl + 6;
 
-  // X1 staging (as k7p_n2w)
-  const bool stager = tid < TASKS;
-  const int tr = tid / (POS / 4), tm = tid - tr * (POS / 4);
+  unsigned char* xr = lds + wave * WSZ;                 // this wave's X1 buffers
+  unsigned char* ar = xr + WNB * WPLANE;               // and A16 buffers
+  // X1 staging (as k7p_n2w: the wave's rows 4 wave + 0..9)
+  const bool stager = lane < WTASKS;
+  const int tr = lane / (POS / 4), tm = lane - tr * (POS / 4);
   unsigned soff[8];
   {
-    const int ih = k7_src(h0 - a.P + tr, a.hi, a.reflect);
+    const int ih = k7_src(h0 - a.P + 4 * wave + tr, a.hi, a.reflect);
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       const int iw = k7_src(w0 - a.P - 1 + 4 * tm + i, a.wi, a.reflect);
@@ -449,15 +461,13 @@ __global__ __launch_bounds__(256, 2) void k7p_wg_kernel(K7Args a, const float* _
                    e3 = k7p_pack(sv[6], sv[7]);
     const unsigned a01 = __builtin_amdgcn_alignbyte(e1, e0, 2), a12 = __builtin_amdgcn_alignbyte(e2, e1, 2),
                    a23 = __builtin_amdgcn_alignbyte(e3, e2, 2);
-    unsigned char* rb = xr + (sp % NBUF) * PLANEB + tr * ROWB + tm * 8;
-    *reinterpret_cast<u32x2_p*>(rb + 0 * POS * 2) = u32x2_p{e0, e1};
-    *reinterpret_cast<u32x2_p*>(rb + 1 * POS * 2) = u32x2_p{a01, a12};
-    *reinterpret_cast<u32x2_p*>(rb + 2 * POS * 2) = u32x2_p{e1, e2};
-    *reinterpret_cast<u32x2_p*>(rb + 3 * POS * 2) = u32x2_p{a12, a23};
+    unsigned char* rb = xr + (sp % WNB) * WPLANE + tr * ROWB + tm * 32;
+    *reinterpret_cast<u32x4_p*>(rb) = u32x4_p{e0, e1, a01, a12};
+    *reinterpret_cast<u32x4_p*>(rb + 16) = u32x4_p{e1, e2, a12, a23};
   };
-  // A16 staging: thread = voxel (row tid >> 4, w tid & 15) of the plane, 32 bytes, slot w ^ 4 (w >> 3)
-  // (the two 8-voxel halves of a row land 32 banks apart for the transposed reads)
-  const int av = tid & 15, arow = tid >> 4;
+  // A16 staging: lane = voxel (the wave's row lane >> 4, w lane & 15) of the plane, 32 bytes, slot
+  // w ^ 4 (w >> 3) (the two 8-voxel halves of a row land 32 banks apart for the transposed reads)
+  const int av = lane & 15, arow = 4 * wave + (lane >> 4);
   unsigned aoff;  // byte offset of this voxel's source row position inside its source plane, OOB past the grid
   {
     const int gh = h0 + arow, gw = w0 + av;
@@ -478,14 +488,12 @@ __global__ __launch_bounds__(256, 2) void k7p_wg_kernel(K7Args a, const float* _
     av1 = __builtin_amdgcn_raw_buffer_load_b128(rs, aoff == OOB ? OOB : aoff + 16, 0, 0);
   };
   auto astore = [&](int sp) {
-    unsigned char* b = ar + (sp % NA) * APL + arow * AROW + ((av ^ ((av >> 3) << 2)) * 32);
+    unsigned char* b = ar + (sp % WNB) * WAPL + (lane >> 4) * AROW + ((av ^ ((av >> 3) << 2)) * 32);
     *reinterpret_cast<u32x4_p*>(b) = av0;
     *reinterpret_cast<u32x4_p*>(b + 16) = av1;
   };
-  for (int i = tid; i < NBUF * ROWB / 4; i += NT) {  // X1 zero rows
-    const int b = i / (ROWB / 4), j = i - b * (ROWB / 4);
-    reinterpret_cast<unsigned*>(xr + b * PLANEB + ROWS * ROWB)[j] = 0u;
-  }
+  for (int i = lane; i < WNB * WPLANE / 16; i += 64)  // the wave's X1 buffers zeroed (the unstaged row stays finite)
+    reinterpret_cast<u32x4_p*>(xr)[i] = u32x4_p{0u, 0u, 0u, 0u};
   xload(0);
   aload(0);
   xstore(0);
@@ -497,11 +505,11 @@ __global__ __launch_bounds__(256, 2) void k7p_wg_kernel(K7Args a, const float* _
   // supplies voxel (row 4 wave + 2 kq + (g >> 1), w = 8 (g & 1) + q [+ 4]) channels 4 p .. 4 p + 3
   const int aq = r16 >> 2, ap = r16 & 3;
   auto aslot = [&](int w_) { return (w_ ^ ((w_ >> 3) << 2)) * 32; };
-  const int abase0 = (4 * wave + (g >> 1)) * AROW + aslot(8 * (g & 1) + aq) + ap * 8;
-  const int abase1 = (4 * wave + (g >> 1)) * AROW + aslot(8 * (g & 1) + aq + 4) + ap * 8;
+  const int abase0 = (g >> 1) * AROW + aslot(8 * (g & 1) + aq) + ap * 8;
+  const int abase1 = (g >> 1) * AROW + aslot(8 * (g & 1) + aq + 4) + ap * 8;
   typedef short s16x4_p __attribute__((ext_vector_type(4)));
   auto afrag = [&](int buf, int kq) -> bf16x8_p {
-    const unsigned char* base = ar + buf * APL + 2 * kq * AROW;
+    const unsigned char* base = ar + buf * WAPL + 2 * kq * AROW;
     const s16x4_p lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4_p*)(base + abase0));
     const s16x4_p hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4_p*)(base + abase1));
     typedef short s16x8_p __attribute__((ext_vector_type(8)));
@@ -511,8 +519,8 @@ __global__ __launch_bounds__(256, 2) void k7p_wg_kernel(K7Args a, const float* _
   // B fragment (K-step kq, th pair tt): lane (n = (j, tw), g): X1 row 4 wave + 2 kq + (g >> 1) + 2 tt + j,
   // positions 8 (g & 1) + tw + 1 .. + 8
   const int bj = r16 >> 3, btw = r16 & 7;
-  const int bp0 = 8 * (g & 1) + btw + 1, bcl = bp0 & 3;
-  const int bbase = (4 * wave + (g >> 1) + bj) * ROWB + bcl * POS * 2 + (bp0 - bcl) * 2;
+  const int bp0 = 8 * (g & 1) + btw + 1;
+  const int bbase = ((g >> 1) + bj) * ROWB + (4 * (bp0 >> 2) + (bp0 & 3)) * 8;
 
   f32x4 acc[7][4];
 #pragma unroll
@@ -526,30 +534,33 @@ __global__ __launch_bounds__(256, 2) void k7p_wg_kernel(K7Args a, const float* _
     for (int u = 0; u < 7; ++u) {
       const int s = s0 + u;
       if (s >= nsteps) break;
-      lds_barrier();  // X1 plane s and A16 plane s are in LDS; the buffers written next are free
+      // X1 plane s and A16 plane s are in this wave's LDS (its own writes, in order): no barrier
+      asm volatile("" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
       xstore(s + 1);
       astore(s + 1);
       xload(s + 2);
       aload(s + 2);
       if (s < tdl) {  // A16 plane s: its fragments into register slot u
-        aw_[u][0] = afrag(s % NA, 0);
-        aw_[u][1] = afrag(s % NA, 1);
+        aw_[u][0] = afrag(s % WNB, 0);
+        aw_[u][1] = afrag(s % WNB, 1);
       }
-      const unsigned char* xb = xr + (s % NBUF) * PLANEB + bbase;
+      const unsigned char* xb = xr + (s % WNB) * WPLANE + bbase;
       const int tlo = max(0, s - (tdl - 1)), thi = min(6, s);  // A16 plane s - td in the chunk
+      const unsigned tmask = __builtin_amdgcn_readfirstlane(((2u << thi) - 1u) & ~((1u << tlo) - 1u));
 #pragma unroll
       for (int kq = 0; kq < 2; ++kq) {
         bf16x8_p bf[4];
 #pragma unroll
         for (int tt = 0; tt < 4; ++tt) {
           const unsigned char* p = xb + (2 * kq + 2 * tt) * ROWB;
-          const u32x2_p lo = *reinterpret_cast<const u32x2_p*>(p), hi = *reinterpret_cast<const u32x2_p*>(p + 8);
+          const u32x2_p lo = *reinterpret_cast<const u32x2_p*>(p), hi = *reinterpret_cast<const u32x2_p*>(p + 32);
           const u32x4_p q4 = {lo[0], lo[1], hi[0], hi[1]};
           bf[tt] = reinterpret_cast<const bf16x8_p&>(q4);
         }
 #pragma unroll
         for (int td = 0; td < 7; ++td) {
-          if (td < tlo || td > thi) continue;
+          if (!((tmask >> td) & 1u)) continue;
           const int slot = (u - td + 7) % 7;
 #pragma unroll
           for (int tt = 0; tt < 4; ++tt)
@@ -560,8 +571,8 @@ __global__ __launch_bounds__(256, 2) void k7p_wg_kernel(K7Args a, const float* _
   }
   // the four waves' tiles summed in LDS in wave order, then this block's partial row [c][t]
   __syncthreads();
-  float* red = reinterpret_cast<float*>(ar);  // 7 x 4 x 256 floats = 28 KB (the A16 buffers are 16 KB: use xr too)
-  float* red2 = reinterpret_cast<float*>(xr);
+  float* red = reinterpret_cast<float*>(lds);  // 7 x 4 x 256 floats = 28 KB
+  float* red2 = red + 16 * 256;
   for (int wv = 0; wv < 4; ++wv) {
     if (wave == wv) {
 #pragma unroll
