@@ -768,6 +768,9 @@ class CriticPlan:
         self.side0 = None
         if torch.device(device).type == "cuda" and not debug("serial"):
             self.side0 = ops.pooled_stream(device, "d_side")
+        # (round 6, measured and not kept: the real / fake rows' staged-window weight grads on the
+        # generator's idle side stream beside the forward-mode chain, the interpolation rows' after it:
+        # 1.281-1.286 vs 1.276-1.277 ms/step — the chain's small-grid kernels lose CUs to it)
         if self.bn:  # conv outputs, pre-activation grads, statistics and per-pass scale/shift
             self.z = [torch.empty_like(self.a[i]) if b else None for i, b in enumerate(self.is_bn)]
             self.dy = [torch.empty_like(self.a[i]) if b else None for i, b in enumerate(self.is_bn)]
@@ -971,17 +974,18 @@ class CriticPlan:
             self._deferred.append((j, g, wl, G[f"{self.layers[j].name}.weight"]))
         ops.wgrad_group(items)
 
-    def _wgrad_sk(self, G, layers, n_all: int):
-        """The weight grads of ``layers`` (a_{j-1}, dz_j over n_all samples) on the staged-window kernel,
-        added into the zeroed gradient arena (two launches: partial tiles, then their sums)."""
+    def _wgrad_sk(self, G, layers, n_all: int, r0: int = 0):
+        """The weight grads of ``layers`` (a_{j-1}, dz_j over samples r0 .. r0 + n_all) on the staged-window
+        kernel, added into the zeroed gradient arena (two launches: partial tiles, then their sums)."""
         items = []
         for j in layers:
             g = self._wgrad_geo(j, n_all)
-            key = ("sk_ws", j, n_all)
+            key = ("sk_ws", j, n_all, r0)
             wsj = self.__dict__.setdefault("_sk_ws", {}).get(key)
             if wsj is None:
                 wsj = self._sk_ws[key] = torch.empty(ops.wgrad_sk_ws_floats(g), device=self.ws.device)
-            items.append((g, self.a[j - 1][:n_all], self.dz[j][:n_all], wsj, G[f"{self.layers[j].name}.weight"]))
+            items.append((g, self.a[j - 1][r0:r0 + n_all], self.dz[j][r0:r0 + n_all], wsj,
+                          G[f"{self.layers[j].name}.weight"]))
         ops.wgrad_sk(items)
 
     def _flush_unpack(self):

@@ -430,6 +430,9 @@ def test_batchnorm_accumulators_match_slab_path(monkeypatch):
     # only): the accumulators are the difference under test, not another fp32 summation order
     # (the bf16 step amplifies any last-bit difference, see test_bf16_storage_matches_fp32_storage)
     L.check(L.load().cgan3d_set_tuning(15, 0), "k3m off")
+    # likewise the streamed-plane k7 kernels (conv_k7p.hip, round 6: they take the accumulator and
+    # shadow launches only; their own test test_gpu_ops.py::test_k7p_n2w_matches_k7m): off
+    L.check(L.load().cgan3d_set_tuning(21, -1), "k7p off")
     engs = []
     try:
         for off in (False, True):
@@ -439,6 +442,7 @@ def test_batchnorm_accumulators_match_slab_path(monkeypatch):
         _acc_vs_slab(engs, b, S)
     finally:
         L.check(L.load().cgan3d_set_tuning(15, 1), "k3m on")
+        L.check(L.load().cgan3d_set_tuning(21, 0), "k7p auto")
 
 
 def _acc_vs_slab(engs, b, S):
