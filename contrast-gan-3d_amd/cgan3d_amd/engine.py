@@ -83,8 +83,10 @@ WGRAD_GROUP = 2
 # the generator's first WGRAD_TAIL_MAIN layers (the end of its backward) compute their weight grads
 # on the main stream: nothing is left there to overlap them with, and on the side stream they cost
 # two cross-stream hand-offs and share the chip with the stride-2 input-grad (1 and 3
-# measured 1.895 / 1.931 against 1.880 ms/step at 2)
-WGRAD_TAIL_MAIN = 2
+# measured 1.895 / 1.931 against 1.880 ms/step at 2 in round 2; re-swept on the round-6 kernels, where
+# the first stride-2 layer's weight grad beside its input-grad pays: 1 measured 1.264 against 1.277
+# ms/step at 2, 0 1.29, profiles/r06_ab_knobs.txt)
+WGRAD_TAIL_MAIN = 1
 # data parallelism: generator gradient bucket size (all-reduce started per bucket during the backward)
 # (measured on one GPU over a one-rank RCCL group: each extra bucket ~15 us of step time, so the
 # default makes ~2-3 buckets of the 4.1 MB arena: 2.21 ms/step at 1 MB, 2.16 with 2 buckets)
