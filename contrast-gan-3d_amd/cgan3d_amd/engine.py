@@ -751,8 +751,9 @@ class CriticPlan:
         for ly in ls:
             g = ops.conv_wgrad_geom(nmax, ly.din, ly.dout, ly.cin, ly.cout, ly.k, ly.s, ly.p, planar=self.pl)
             nv = nmax * ly.dout[0] * ly.dout[1] * ly.dout[2]
-            ws = max(ws, ops.wgrad_ws_floats(g), ops.channel_sum_ws_floats(nv, ly.cout),
-                     ops.bn_backward_ws_floats(nv, ly.cout))
+            # (the bf16 weight grads' partial slabs: the geometry at the plan's precision sizes them)
+            ws = max(ws, ops.wgrad_ws_floats(g), ops.wgrad_ws_floats(ops.with_prec(g, prec)),
+                     ops.channel_sum_ws_floats(nv, ly.cout), ops.bn_backward_ws_floats(nv, ly.cout))
         self.ws = torch.empty(ws, device=device)
         self.ws_clean = torch.zeros(ws, device=device)  # see GeneratorPlan.ws_clean
         # per-layer all-zero workspaces of the weight grads whose unpack is deferred: every layer's

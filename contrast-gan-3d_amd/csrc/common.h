@@ -255,7 +255,8 @@ bool c1_wgrad_ok(const cgan3d_conv_geom* g);
 int c1_fwd_launch(const cgan3d_conv_geom* g, const float* x, const float* w, float* y, const Epi& e, hipStream_t st);
 int c1_dgrad_launch(const cgan3d_conv_geom* g, const float* dz, const float* w, float* dx, const Epi& e,
                     hipStream_t st);
-int c1_wgrad_launch(const cgan3d_conv_geom* g, const float* x, const float* dz, float* dw, hipStream_t st);
+int c1_wgrad_launch(const cgan3d_conv_geom* g, const float* x, const float* dz, float* dw, float* ws, hipStream_t st);
+long long c1_wgrad_ws_floats(const cgan3d_conv_geom* g);
 long long wgrad_k3_ws_floats(const cgan3d_conv_geom* g);
 void wgrad_k3_set_chunks(int v);
 void wgrad_k3m_set(int v);
@@ -271,8 +272,9 @@ int wgrad_k3_partials(const cgan3d_conv_geom* g);
 int wgrad_c1_launch(const cgan3d_conv_geom* g, const float* gathered, const float* aligned, float* dw, hipStream_t st);
 int wgrad_bf16_group_launch(const cgan3d_conv_geom* geoms, const float* const* gathered, const float* const* aligned,
                             float* const* ws, int n, hipStream_t st);
-int wgrad_bf16_launch(const cgan3d_conv_geom* g, const float* gathered, const float* aligned, float* dwp,
-                      hipStream_t st);
+int wgrad_bf16_launch(const cgan3d_conv_geom* g, const float* gathered, const float* aligned, float* dw, float* dwp,
+                      int accumulate, hipStream_t st);
+long long wgrad_bf16_ws_floats(const cgan3d_conv_geom* g);
 // ResNet-block convs with every operand in LDS, 32x32x16 MFMA (conv_k3m.hip)
 bool k3m_ok(const cgan3d_conv_geom* g, const Epi& e);
 bool k3m_geom_ok(const cgan3d_conv_geom* g);
@@ -309,6 +311,10 @@ __device__ __forceinline__ void bn_pair_z(const Epi& e, float v, float z, int c,
   *p1 += gg;
   *p2 += gg * (z - e.bn_mi[c]) * e.bn_mi[C + c];
 }
+
+// dw[c * wc + t] += sum over the nrows partial rows part[r][c * T + t] (ncols = C x T columns), summed in
+// a fixed order, one writer per element (conv_k7_mfma.hip; the k7 and critic first-layer weight grads)
+void colsum_launch(const float* part, int nrows, int ncols, int T, float* dw, long long wc, hipStream_t s);
 
 // ---- launch tickets: "last block out" of a launch, without any waiting.  Two uint32 words, zeroed
 // once by the caller; each block takes a ticket when it is done and the last one (true in its

@@ -785,11 +785,20 @@ static long long wgrad_vpb(long long V, int gx_blocks) {
   return (vpb + 63) / 64 * 64;
 }
 
+// the generic bf16 weight grad as one deterministic launch pair (wgrad_bf16_launch); the shapes the
+// dedicated kernels take are dispatched before it
+static bool wgrad_bf16d_ok(const cgan3d_conv_geom* g) {
+  return !g->planar && g->cout != 1 && wgrad_bf16_ok(g) && !(g->k == 7 && g->stride == 1 && (g->cin == 1 || g->cout == 1)) &&
+         !c1_wgrad_ok(g) && !wgrad_c1_ok(g) && !wgrad_s2_ok(g) && !wgrad_k3_ok(g);
+}
+
 extern "C" int64_t cgan3d_conv3d_wgrad_ws_floats(const cgan3d_conv_geom* g) {
   if (!g) return -1;
   if (g->planar) return (int64_t)geom_taps(g) * g->cin * g->cout;
+  if (wgrad_bf16d_ok(g)) return std::max<int64_t>(wgrad_bf16_ws_floats(g), (int64_t)g->k * g->k * g->k * g->cin * g->cout);
   return std::max<int64_t>(std::max<int64_t>((int64_t)g->k * g->k * g->k * g->cin * g->cout, k7_wgrad_ws_floats(g)),
-                           std::max<int64_t>(wgrad_k3_ws_floats(g), wgrad_s2_ws_floats(g)));
+                           std::max<int64_t>(std::max<int64_t>(wgrad_k3_ws_floats(g), wgrad_s2_ws_floats(g)),
+                                             c1_wgrad_ws_floats(g)));
 }
 
 extern "C" int cgan3d_conv3d_wgrad(const cgan3d_conv_geom* g, const float* gathered, const float* aligned, float* dw,
@@ -801,7 +810,8 @@ extern "C" int cgan3d_conv3d_wgrad(const cgan3d_conv_geom* g, const float* gathe
 // or kept clean under CGAN3D_WGRAD_WS_CLEAN), 0 if it needs no zeroed workspace
 static int wgrad_ws_atomic(const cgan3d_conv_geom* g) {
   if (g->planar) return 1;
-  return !k7_wgrad_handles(g) && !c1_wgrad_ok(g) && !wgrad_c1_ok(g) && !wgrad_s2_ok(g) && !wgrad_k3_ok(g);
+  return !k7_wgrad_handles(g) && !c1_wgrad_ok(g) && !wgrad_c1_ok(g) && !wgrad_s2_ok(g) && !wgrad_k3_ok(g) &&
+         !wgrad_bf16d_ok(g);
 }
 
 extern "C" int cgan3d_conv3d_wgrad_ws_mode(const cgan3d_conv_geom* g) {
@@ -867,12 +877,12 @@ extern "C" int cgan3d_conv3d_wgrad_ex(const cgan3d_conv_geom* g, const float* ga
     }
     CG_CHECK_ARG(!accumulate, "cgan3d_conv3d_wgrad: internal dispatch error");
   }
-  if (c1_wgrad_ok(g)) {  // critic first layer: LDS-window kernel, atomics straight into dW
+  if (c1_wgrad_ok(g)) {  // critic first layer: LDS-window kernel, per-block partials in ws, summed in order
     if (!accumulate && ::cg::memset_async(dw, 0, R * g->cout * sizeof(float), s) != hipSuccess) {
       set_error("cgan3d_conv3d_wgrad: memset failed");
       return CGAN3D_EHIP;
     }
-    const int rc = c1_wgrad_launch(g, gathered, aligned, dw, s);
+    const int rc = c1_wgrad_launch(g, gathered, aligned, dw, ws, s);
     if (rc) return rc;
     CG_LAUNCH_CHECK("c1_wgrad_kernel");
     return CGAN3D_OK;
@@ -900,6 +910,12 @@ extern "C" int cgan3d_conv3d_wgrad_ex(const cgan3d_conv_geom* g, const float* ga
     CG_LAUNCH_CHECK("wgrad_k3_kernel");
     return CGAN3D_OK;
   }
+  if (wgrad_bf16d_ok(g)) {  // other bf16 shapes: partial slabs in ws + their ordered sum into dw, no memset
+    int rc = wgrad_bf16_launch(g, gathered, aligned, dw, ws, accumulate, s);
+    if (rc) return rc;
+    CG_LAUNCH_CHECK("conv_wgrad_bf16_kernel");
+    return CGAN3D_OK;
+  }
 generic:
   if (!ws_clean && ::cg::memset_async(ws, 0, R * g->cout * sizeof(float), s) != hipSuccess) {
     set_error("cgan3d_conv3d_wgrad: memset failed");
@@ -919,10 +935,6 @@ generic:
     dim3 grid(cg::ceil_div(V, vpb), gy);
     ::cg::launch((conv_wgrad_cout1_kernel<1>), grid, dim3(256), 0, s, a, gathered, aligned, ws, vpb);
     CG_LAUNCH_CHECK("conv_wgrad_cout1_kernel");
-  } else if (!g->planar && wgrad_bf16_ok(g)) {
-    int rc = wgrad_bf16_launch(g, gathered, aligned, ws, s);
-    if (rc) return rc;
-    CG_LAUNCH_CHECK("conv_wgrad_bf16_kernel");
   } else {
     const int gxb = cg::ceil_div(R, 64);
     const int gz = cg::ceil_div(g->cout, 64);  // 64-channel blocks (cout > 64: 2-D critic)

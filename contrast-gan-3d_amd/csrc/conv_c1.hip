@@ -224,7 +224,7 @@ __global__ __launch_bounds__(256) void c1_dgrad_kernel(C1Args a, const float* __
 // the current one is reduced.
 template <int G>
 __global__ __launch_bounds__(256 * G) void c1_wgrad_kernel(C1Args a, const float* __restrict__ x,
-                                                           const float* __restrict__ dz, float* dw, int ntiles) {
+                                                           const float* __restrict__ dz, float* part, int ntiles) {
   using namespace c1;
   __shared__ __attribute__((aligned(16))) float xs_all[G][WIN];
   __shared__ __attribute__((aligned(16))) float gs_all[G][TZ * TY * TX * 8];
@@ -314,7 +314,7 @@ __global__ __launch_bounds__(256 * G) void c1_wgrad_kernel(C1Args a, const float
     float s = 0.f;
 #pragma unroll
     for (int k = 0; k < 4 * G; ++k) s += red[k][b][tt];
-    atomicAdd(dw + b * a.w_sb + tt, s);
+    part[(long long)blockIdx.x * 512 + i] = s;  // i = b * 64 + tt (colsum_kernel adds the rows in order)
   }
 }
 
@@ -364,19 +364,35 @@ int c1_dgrad_launch(const cgan3d_conv_geom* g, const float* dz, const float* w, 
   return CGAN3D_OK;
 }
 
-int c1_wgrad_launch(const cgan3d_conv_geom* g, const float* x, const float* dz, float* dw, hipStream_t st) {
+// per-block partial rows [block][8 x 64] in ws (c1_wgrad_ws_floats), summed into dW in block order by
+// colsum_kernel (round 6: the blocks' atomics into dW made the gradient order-dependent)
+static int c1_wgrad_grid(const C1Args& a0, int* tpb) {
+  const int ntiles = a0.n * a0.tz * a0.ty * a0.tx;
+  // at most ~192 blocks (measured: 1024 blocks of one tile each, 36 -> 47 us at 64^3 B=4; 192 blocks of 8
+  // tiles at 12 x 64^3 leave CUs to the main stream's kernels: A/B 1.447 / 1.443 / 1.455 vs 1.471 / 1.473 /
+  // 1.472 ms/step at 256 blocks).  Small grids keep one tile per block (ntiles / 192 rounds to 0-1).
+  *tpb = std::max(1, ntiles / 192);
+  return ceil_div(ntiles, *tpb);
+}
+
+// a bound for every batch up to g->n (the grid is not monotone in the tile count: 383 tiles take 383
+// blocks, 384 take 192), so a workspace sized at the largest batch serves the smaller ones
+long long c1_wgrad_ws_floats(const cgan3d_conv_geom* g) {
+  if (!c1_wgrad_ok(g)) return 0;
+  const C1Args a = c1_args(g);
+  return (long long)std::min(a.n * a.tz * a.ty * a.tx, 2 * 192) * 512;
+}
+
+int c1_wgrad_launch(const cgan3d_conv_geom* g, const float* x, const float* dz, float* dw, float* ws, hipStream_t st) {
   C1Args a = c1_args(g);
   const int ntiles = a.n * a.tz * a.ty * a.tx;
-  // at most ~192 blocks adding into dW (measured: 1024 blocks of one tile each, 36 -> 47 us at 64^3
-  // B=4; 192 blocks of 8 tiles at 12 x 64^3 leave CUs to the main stream's kernels: A/B 1.447 / 1.443 /
-  // 1.455 vs 1.471 / 1.473 / 1.472 ms/step at 256 blocks); two tile groups per block when there are
-  // tiles for both.  Small grids keep one tile per block (ntiles / 192 rounds to 0-1).
-  const int G = ntiles < 512 ? 1 : 2;
-  a.tiles_per_block = std::max(1, ntiles / 192);
-  if (G == 2)
-    ::cg::launch(c1_wgrad_kernel<2>, dim3(ceil_div(ntiles, a.tiles_per_block)), dim3(512), 0, st, a, x, dz, dw, ntiles);
+  const int blocks = c1_wgrad_grid(a, &a.tiles_per_block);
+  // two tile groups per block when there are tiles for both
+  if (ntiles >= 512)
+    ::cg::launch(c1_wgrad_kernel<2>, dim3(blocks), dim3(512), 0, st, a, x, dz, ws, ntiles);
   else
-    ::cg::launch(c1_wgrad_kernel<1>, dim3(ceil_div(ntiles, a.tiles_per_block)), dim3(256), 0, st, a, x, dz, dw, ntiles);
+    ::cg::launch(c1_wgrad_kernel<1>, dim3(blocks), dim3(256), 0, st, a, x, dz, ws, ntiles);
+  colsum_launch(ws, blocks, 512, 64, dw, (long long)g->w_sb, st);
   return CGAN3D_OK;
 }
 

@@ -769,7 +769,7 @@ __global__ __launch_bounds__(512, 1) void k7s_w2n_kernel(K7Args a, const __bf16*
 // voxels.  The four waves split the N tiles (no cross-wave reduction); A fragments come from the
 // X16 tile staged channel-major in LDS, B fragments from 8 shifted bf16 copies of the X1 halo.  Each
 // block loops over tiles (next tile's global loads in flight during the current tile's MFMAs) and
-// writes one partial [c][t]; k7m_colsum_kernel adds the partials into dW.
+// writes one partial [c][t]; colsum_kernel adds the partials into dW.
 constexpr int G_TD = 4, G_TH = 8, G_TW = 16, G_ROWS_IN = (G_TD + 6) * (G_TH + 6), G_VOX = G_TD * G_TH * G_TW;
 constexpr int G_NT = 25;                // N tiles: pairs (2j, 2j+1) x tw 0..7
 constexpr int G_COLS = 16 * KT7;        // partial row: [c][t]
@@ -956,17 +956,40 @@ __global__ __launch_bounds__(256, 2) void k7m_wg_kernel(K7Args a, const float* _
   }
 }
 
-// dW[c * wc + t] += sum_b part[b][c * 343 + t]; grid (cols / 256, row splits)
-__global__ __launch_bounds__(256) void k7m_colsum_kernel(const float* __restrict__ part, int nrows, int rows_per,
-                                                         float* dw, long long wc) {
-  const int col = blockIdx.x * 256 + threadIdx.x;
-  if (col >= G_COLS) return;
-  const int r0 = blockIdx.y * rows_per, r1 = min(nrows, r0 + rows_per);
-  float s = 0.f;
-#pragma unroll 8
-  for (int r = r0; r < r1; ++r) s += part[(long long)r * G_COLS + col];
-  const int c = col / KT7, t = col - c * KT7;
-  atomicAdd(dw + c * wc + t, s);
+// dW[c * wc + t] += sum_r part[r][c * T + t] over the nrows partial rows, in a fixed order (round 6:
+// the row-split atomics this replaced made the weight gradients order-dependent).  Block = 64 columns
+// x 16 row groups; group k sums rows k, k + 16, ... with 8 independent partial sums (8 loads in
+// flight), the groups are combined in group order in LDS and one thread per column adds the result
+// into dW (the only writer of that element in the launch).
+__global__ __launch_bounds__(1024) void colsum_kernel(const float* __restrict__ part, int nrows, int ncols, int T,
+                                                     float* dw, long long wc) {
+  __shared__ float red[16][64];
+  const int lane = threadIdx.x & 63, k = threadIdx.x >> 6;
+  const int col = blockIdx.x * 64 + lane;
+  const int cc = col < ncols ? col : 0;
+  float s8[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) s8[j] = 0.f;
+  for (int r0 = k; r0 < nrows; r0 += 128)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int r = r0 + 16 * j;
+      const float v = part[(long long)(r < nrows ? r : k) * ncols + cc];
+      s8[j] += r < nrows ? v : 0.f;
+    }
+  red[k][lane] = ((s8[0] + s8[1]) + (s8[2] + s8[3])) + ((s8[4] + s8[5]) + (s8[6] + s8[7]));
+  __syncthreads();
+  if (k == 0 && col < ncols) {
+    float v = 0.f;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) v += red[q][lane];
+    const int c = col / T, t = col - c * T;
+    dw[c * wc + t] += v;
+  }
+}
+
+void colsum_launch(const float* part, int nrows, int ncols, int T, float* dw, long long wc, hipStream_t s) {
+  ::cg::launch(colsum_kernel, dim3((unsigned)((ncols + 63) / 64)), dim3(1024), 0, s, part, nrows, ncols, T, dw, wc);
 }
 
 // tiles of the wgrad X16 grid (output grid, or the padded input grid for the last conv)
@@ -1081,9 +1104,7 @@ void k7m_wgrad_launch(const cgan3d_conv_geom* g, bool wide_in, long long wc, con
   k7m_wg_split(g, wide_in, &grid, &per, &ntiles);
   if (wide_in) ::cg::launch(k7m_wg_kernel<1>, dim3(grid), dim3(256), 0, s, a, x, go, ws, per, ntiles, wide16);
   else ::cg::launch(k7m_wg_kernel<0>, dim3(grid), dim3(256), 0, s, a, x, go, ws, per, ntiles, wide16);
-  const int rows_per = 32;
-  ::cg::launch(k7m_colsum_kernel, dim3((G_COLS + 255) / 256, (grid + rows_per - 1) / rows_per), dim3(256), 0, s,
-                     ws, grid, rows_per, dw, wc);
+  colsum_launch(ws, grid, G_COLS, KT7, dw, wc, s);
 }
 
 }  // namespace cg

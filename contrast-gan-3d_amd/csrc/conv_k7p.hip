@@ -399,7 +399,7 @@ __global__ __launch_bounds__(256, 2) void k7p_n2w_kernel(K7Args a, const float* 
 // seven steps they are used (the plane loop unrolled by 7, as k7p_n2w's output planes): per step and
 // K-step a wave reads one new A16 fragment and four X1 fragments for 28 MFMAs into its 28
 // accumulator tiles (td, tt).  The waves' tiles are summed in LDS in wave order (deterministic) and each
-// block writes one partial [c][343] row; k7m_colsum_kernel adds the rows into dW.
+// block writes one partial [c][343] row; colsum_kernel adds the rows into dW.
 namespace k7g {
 constexpr int AROW = 16 * 32;              // A16 staged row: 16 voxels x 32 bytes (quads 2 / 3 swapped per row)
 constexpr int APL = 16 * AROW;             // A16 plane (16 rows): 8 KB
@@ -691,9 +691,7 @@ int k7p_wgrad_try(const cgan3d_conv_geom* g, bool wide_in, long long wc, const f
   } else {
     ::cg::launch(k7p_wg_kernel<0>, dim3(blocks), dim3(k7p::NT), 0, s, a, x, wide16, g->do_, g->ho, g->wo, ws, tdc);
   }
-  const int rows_per = 32;
-  ::cg::launch(k7m_colsum_kernel, dim3((16 * KT7 + 255) / 256, (blocks + rows_per - 1) / rows_per), dim3(256), 0, s,
-               (const float*)ws, blocks, rows_per, dw, wc);
+  colsum_launch(ws, blocks, 16 * KT7, KT7, dw, wc, s);
   return 1;
 }
 

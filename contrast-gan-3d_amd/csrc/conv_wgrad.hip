@@ -35,7 +35,9 @@ __device__ __forceinline__ int wg_coord(int i, int n, int reflect) {
   return (i >= 0 && i < n) ? i : -1;
 }
 
-template <int NB, bool ROW8>
+// PART (round 6): block (bx, by) stores its sums into partial slab `by` of dwp ([slab][t][a][b], summed in
+// slab order by wgrad_reduce_ta_kernel) instead of adding them atomically (the grouped launch)
+template <int NB, bool ROW8, bool PART = false>
 __device__ __forceinline__ void wgrad_bf16_block(const WgArgs& a, const float* __restrict__ gx,
                                                  const float* __restrict__ go, float* dwp, int bx, int by,
                                                  __bf16* As, __bf16* Gs) {
@@ -145,7 +147,10 @@ __device__ __forceinline__ void wgrad_bf16_block(const WgArgs& a, const float* _
 #pragma unroll
     for (int jj = 0; jj < 4; ++jj) {
       const int r = r0 + wave * 16 + 4 * g + jj;
-      if (r < a.R) atomicAdd(dwp + (long long)r * a.cout + b, acc[nt][jj]);
+      if (r < a.R) {
+        if constexpr (PART) dwp[((long long)by * a.R + r) * a.cout + b] = acc[nt][jj];
+        else atomicAdd(dwp + (long long)r * a.cout + b, acc[nt][jj]);
+      }
     }
   }
 }
@@ -155,7 +160,38 @@ __global__ __launch_bounds__(256) void conv_wgrad_bf16_kernel(WgArgs a, const fl
                                                               const float* __restrict__ go, float* dwp) {
   __shared__ __attribute__((aligned(16))) __bf16 As[64 * WG_LD];  // [row][voxel]
   __shared__ __attribute__((aligned(16))) __bf16 Gs[64 * WG_LD];  // [b][voxel]
-  wgrad_bf16_block<NB, ROW8>(a, gx, go, dwp, blockIdx.x, blockIdx.y, As, Gs);
+  wgrad_bf16_block<NB, ROW8, true>(a, gx, go, dwp, blockIdx.x, blockIdx.y, As, Gs);
+}
+
+// dW[b * w_sb + a * w_sa + t] (+)= sum_p ws[p][t][a][b] (T taps, A gathered x B aligned channels): the
+// partial slabs of conv_wgrad_bf16_kernel, read along their layout (64 consecutive elements per block x NC
+// chunks of the P slabs, one wave per chunk, 8 loads in flight per lane), chunks combined in a fixed order
+__global__ __launch_bounds__(1024) void wgrad_reduce_ta_kernel(const float* __restrict__ ws, int P, int NC, int T,
+                                                               int A, int B, float* dw, long long w_sa, long long w_sb,
+                                                               int accumulate) {
+  __shared__ float part[16][64];
+  const int lane = threadIdx.x & 63, c = threadIdx.x >> 6;
+  const long long E = (long long)T * A * B, e = (long long)blockIdx.x * 64 + lane;
+  const bool ok = e < E;
+  const int pc = (P + NC - 1) / NC, p0 = c * pc, p1 = min(P, p0 + pc);
+  float s[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) s[j] = 0.f;
+  for (int p = p0; p < p1; p += 8)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float v = ws[(long long)(p + j < p1 ? p + j : p0) * E + (ok ? e : 0)];
+      s[j] += p + j < p1 ? v : 0.f;
+    }
+  part[c][lane] = ((s[0] + s[1]) + (s[2] + s[3])) + ((s[4] + s[5]) + (s[6] + s[7]));
+  __syncthreads();
+  if (c == 0 && ok) {
+    float v = 0.f;
+    for (int k = 0; k < NC; ++k) v += part[k][lane];
+    const int b = (int)(e % B), r = (int)(e / B), a = r % A, t = r / A;
+    float* o = dw + (long long)b * w_sb + (long long)a * w_sa + t;
+    *o = accumulate ? *o + v : v;
+  }
 }
 
 // ---- several of those weight gradients in one launch (cgan3d_conv3d_wgrad_group): item i owns the
@@ -305,8 +341,17 @@ static WgArgs wgrad_bf16_args(const cgan3d_conv_geom* g, int* gxb, int* gyb) {
 }
 
 // adds into the packed [t][a][b] workspace dwp (zeroed by the caller)
-int wgrad_bf16_launch(const cgan3d_conv_geom* g, const float* gathered, const float* aligned, float* dwp,
-                      hipStream_t st) {
+long long wgrad_bf16_ws_floats(const cgan3d_conv_geom* g) {
+  if (!wgrad_bf16_ok(g)) return 0;
+  int gxb, gyb;
+  const WgArgs a = wgrad_bf16_args(g, &gxb, &gyb);
+  return (long long)gyb * a.R * g->cout;
+}
+
+// partial slabs into ws (wgrad_bf16_ws_floats), then their ordered sum into dw (round 6: deterministic;
+// the blocks of one row chunk added into one workspace by atomics before)
+int wgrad_bf16_launch(const cgan3d_conv_geom* g, const float* gathered, const float* aligned, float* dw, float* dwp,
+                      int accumulate, hipStream_t st) {
   int gxb, gyb;
   const WgArgs a = wgrad_bf16_args(g, &gxb, &gyb);
   dim3 grid(gxb, gyb);
@@ -319,6 +364,10 @@ int wgrad_bf16_launch(const cgan3d_conv_geom* g, const float* gathered, const fl
     else CG_WGB(4, false);
   }
 #undef CG_WGB
+  const long long E = (long long)a.R * g->cout;
+  const int nc = std::max(1, std::min(16, (gyb + 7) / 8));  // ~8 slabs per lane
+  ::cg::launch(wgrad_reduce_ta_kernel, dim3((unsigned)((E + 63) / 64)), dim3(64 * nc), 0, st, dwp, gyb, nc,
+               g->k * g->k * g->k, g->cin, g->cout, dw, (long long)g->w_sa, (long long)g->w_sb, accumulate);
   return CGAN3D_OK;
 }
 

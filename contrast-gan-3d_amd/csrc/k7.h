@@ -41,11 +41,10 @@ int k7p_n2w_try(const cgan3d_conv_geom* g, int P, int reflect, int flip, long lo
                 float* y, const K7Fold* fold, const BnFuse* fz, bool out16, hipStream_t s);
 
 // streamed-plane weight gradient (conv_k7p.hip): 1 if it took the launch (k7m_wg otherwise); its
-// partial rows (blocks x 16 x 343 floats) are summed by k7m_colsum_kernel (conv_k7_mfma.hip)
+// partial rows (blocks x 16 x 343 floats) are summed by colsum_kernel (common.h colsum_launch)
 int k7p_wgrad_try(const cgan3d_conv_geom* g, bool wide_in, long long wc, const float* x, const float* go, float* dw,
                   float* ws, hipStream_t s, const __bf16* wide16);
 long long k7p_wg_blocks(const cgan3d_conv_geom* g, bool wide_in);
-__global__ void k7m_colsum_kernel(const float* __restrict__ part, int nrows, int rows_per, float* dw, long long wc);
 
 __device__ __forceinline__ void k7_tile(const K7Args& a, int bid, int* n, int* d0, int* h0, int* w0) {
   int tw = bid % a.tiles_w; bid /= a.tiles_w;
