@@ -296,7 +296,7 @@ typedef struct cgan3d_reduce_desc {
 /* 1 <= n <= 16 descriptors (passed by value into the launch) */
 int cgan3d_wgrad_reduce_multi(const cgan3d_reduce_desc* descs, int32_t n, void* stream);
 /* 1 if the weight gradient of `g` sums into its workspace by atomics (the geometries that may take
- * CGAN3D_WGRAD_WS_CLEAN), 0 if not, -1 on an invalid geometry.  Round 6: every bf16 geometry returns 0 —
+ * CGAN3D_WGRAD_WS_CLEAN), 0 if not, -1 on an invalid geometry.  Round 6: the bf16 geometries (cout 4-64) return 0 —
  * their weight gradients write per-block partials into ws and sum them into dw in a fixed order (the
  * k7 and critic first-layer kernels' partial rows, the generic bf16 kernel's partial slabs, the ResNet /
  * stride-2 kernels' partials), so the bf16 step's gradients do not depend on the order blocks finish;
