@@ -765,21 +765,32 @@ static void wgrad_reduce_launch(const float* ws, int P, int A, int B, float* dw,
                w_sa, w_sb, accumulate);
 }
 
-// ---- stride-2 weight gradient between the generator's 16- and 32-channel levels (bf16 MFMA):
-// the first downsampling Conv3d 16 -> 32 (generator.py:40-47) and, operands swapped, the last
-// ConvTranspose3d 32 -> 16 (generator.py:61-77; its output-grad is the gathered operand), both
-// dW[t][a][b] = sum_o X(2o - 1 + t)[a] * dZ(o)[b] with X 16 channels on the 2x grid.  At 64^3 the
-// gathered operand is 67 MB: a block stages a slab (one output plane, 4 rows, 32 columns) of both
-// operands once — X's 3 x 9 x 65 window serves all 27 taps — and reads MFMA fragments with
-// ds_read_b64_tr_b16 (any tap shift is a row address).  Layouts: X rows of 32 B (16 channels),
-// one pad voxel per 16 along x (the two 16-lane groups of a read 17 voxels apart: disjoint banks);
-// dZ rows of 64 B with the 16-channel halves swapped on odd 8-column groups.  Waves: tap group
-// (w & 3, taps t = w & 3 + 4i) x output-channel tile (w >> 2).  The next slab's loads are in
-// registers during the current slab's MFMAs.  Per-block partials -> wgrad_reduce_lin_kernel.
+// ---- stride-2 weight gradients of both generator levels (bf16 MFMA), from bf16 shadows or fp32
+// operands: dW[t][a][b] = sum_o X(2o - 1 + t)[a] * dZ(o)[b] with X the CI-channel operand on the 2x grid.
+//   <CI, CO> = <16, 32>: the first down-sampling Conv3d 16 -> 32 (generator.py:40-47) and, operands
+//   swapped, the last ConvTranspose3d 32 -> 16 (generator.py:61-77; its output-grad is the gathered
+//   operand);  <32, 64> (round 6): the second down-sampling conv and the first up-sampling
+//   ConvTranspose — the 32 <-> 64 level, on the generic kernel before (26-41 us per launch beside the
+//   backward at ~2.5 % MFMA busy).
+// A block stages a slab (one output plane, 4 rows, OC = 512 / CI columns) of both operands once — X's
+// 3 x 9 x (2 OC + 1) window (~60 KB either way) serves all 27 taps — and reads MFMA fragments with
+// ds_read_b64_tr_b16 (any tap shift is a row address).  Layouts, each chosen so the 32 lanes of a
+// transposed read hit distinct banks: X rows of 2 CI bytes with one pad voxel per 16 along x (lanes 8
+// output columns apart land 64 B apart) and, at CI = 32, the two 16-channel halves swapped on bit 2 of
+// the window column; dZ rows of 2 CO bytes with their 16-channel quarters permuted by bits 1 and 3 (CO
+// 64) / bit 3 (CO 32) of the column.  K-step = 32 output voxels (one row of 32, or two rows of 16).
+// Waves: tap group (w & 3: taps w & 3 + 4i) x 16-channel output tile (w >> 2; CO = 64: two blocks per slab
+// range, blockIdx.y the 32-channel half), every input channel.  The
+// next slab's 16-byte loads are in registers during the current slab's MFMAs.  Per-block partials
+// ws[p][t][b][a] -> wgrad_reduce_lin_kernel (fixed order).
 namespace ws2 {
-constexpr int XW = 65, XRS = 70, XPS = 9 * XRS;  // window columns; padded row / plane strides (voxels)
-constexpr int XBYTES = 3 * XPS * 32, ZBYTES = 4 * 32 * 64;
-constexpr int NX = 3 * 9 * XW * 4, NXT = (NX + 511) / 512;  // X float4 items per slab, per thread
+template <int CI>
+struct Geo {
+  static constexpr int OC = 512 / CI, XW = 2 * OC + 1, XRS = XW + XW / 16 + 1;  // window columns, padded row
+  static constexpr int XB = 2 * CI, XI = XB / 16, XPS = 9 * XRS;                // row bytes / items, plane stride
+  static constexpr int XBYTES = 3 * XPS * XB;
+  static constexpr int NX = 3 * 9 * XW * XI, NXT = (NX + 511) / 512;
+};
 __device__ __forceinline__ int xcol(int c) { return c + (c >> 4); }
 }  // namespace ws2
 
@@ -788,67 +799,97 @@ struct Ws2Args {
   int slabs, spb;  // slabs in all, per block
 };
 
-template <bool B16>  // both operands from bf16 shadows (as wgrad_k3_kernel)
+template <int CI, int CO, bool B16>  // B16: both operands from bf16 shadows (bit-identical: fp32 ones are rounded)
 __global__ __launch_bounds__(512) void wgrad_s2_kernel(Ws2Args a, const float* __restrict__ x,
                                                        const float* __restrict__ dz, const __bf16* __restrict__ x16,
                                                        const __bf16* __restrict__ dz16, float* __restrict__ ws) {
-  using namespace ws2;
-  __shared__ __attribute__((aligned(16))) unsigned char smem[XBYTES + ZBYTES];
+  using Gm = ws2::Geo<CI>;
+  using ws2::xcol;
+  constexpr int OC = Gm::OC, XW = Gm::XW, XRS = Gm::XRS, XPS = Gm::XPS, XB = Gm::XB, XI = Gm::XI;
+  constexpr int NX = Gm::NX, NXT = Gm::NXT;
+  constexpr int ZB = 2 * CO, ZI = ZB / 16, NZ = 4 * OC * ZI, NZT = (NZ + 511) / 512;
+  constexpr int AT = CI / 16, BTW = 1, KS = 4 * OC / 32, NTAP = 7;
+  __shared__ __attribute__((aligned(16))) unsigned char smem[Gm::XBYTES + 4 * OC * ZB];
+  unsigned char* const zs = smem + Gm::XBYTES;
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int tg = wave & 3, bt = wave >> 2;
+  // blockIdx.y: which 32 output channels (CO = 64: the two halves in two blocks, each wave one 16-channel
+  // tile — 56 accumulator registers instead of 112, which spilled)
+  const int tg = wave & 3, bh = 2 * (int)blockIdx.y + (wave >> 2);
   const int p = blockIdx.x;
   const int s0 = p * a.spb, s1 = min(s0 + a.spb, a.slabs);
-  const int yg_n = a.ho >> 2, xc_n = a.wo >> 5;
-  using SV = std::conditional_t<B16, bf16x4_w, f32x4>;
-  SV rx[NXT], rz[2];
+  const int yg_n = a.ho >> 2, xc_n = a.wo / OC;
+  bf16x8_w hx[B16 ? NXT : 1], hz[B16 ? NZT : 1];
+  f32x4 fx[B16 ? 1 : 2 * NXT], fz[B16 ? 1 : 2 * NZT];
   auto load = [&](int sl) {
     const int xc = sl % xc_n, q1 = sl / xc_n, yg = q1 % yg_n, zq = q1 / yg_n;  // zq = nb * do + oz
     const int oz = zq % a.do_, nb = zq / a.do_;
-    const int iz0 = 2 * oz - 1, iy0 = 8 * yg - 1, ix0 = 64 * xc - 1;
+    const int iz0 = 2 * oz - 1, iy0 = 8 * yg - 1, ix0 = 2 * OC * xc - 1;
 #pragma unroll
     for (int k = 0; k < NXT; ++k) {
-      const int i = tid + 512 * k, q4 = i & 3, v = i >> 2;
+      const int i = tid + 512 * k, qi = i % XI, v = i / XI;
       const int c = v % XW, r = (v / XW) % 9, pl = v / (9 * XW);
       const int iz = iz0 + pl, iy = iy0 + r, ix = ix0 + c;
       const bool ok = i < NX && (unsigned)iz < (unsigned)a.di && (unsigned)iy < (unsigned)a.hi && (unsigned)ix < (unsigned)a.wi;
-      const long long o = ((((long long)nb * a.di + iz) * a.hi + iy) * a.wi + ix) * 16 + 4 * q4;
-      if constexpr (B16) rx[k] = ok ? *reinterpret_cast<const bf16x4_w*>(x16 + o) : bf16x4_w{};
-      else rx[k] = ok ? *reinterpret_cast<const f32x4*>(x + o) : f32x4{0.f, 0.f, 0.f, 0.f};
+      const long long o = ((((long long)nb * a.di + iz) * a.hi + iy) * a.wi + ix) * CI + 8 * qi;
+      if constexpr (B16) {
+        hx[k] = ok ? *reinterpret_cast<const bf16x8_w*>(x16 + o) : bf16x8_w{};
+      } else {
+        fx[2 * k] = ok ? *reinterpret_cast<const f32x4*>(x + o) : f32x4{0.f, 0.f, 0.f, 0.f};
+        fx[2 * k + 1] = ok ? *reinterpret_cast<const f32x4*>(x + o + 4) : f32x4{0.f, 0.f, 0.f, 0.f};
+      }
     }
 #pragma unroll
-    for (int k = 0; k < 2; ++k) {
-      const int i = tid + 512 * k, q8 = i & 7, v = i >> 3;  // v = u * 32 + ox
-      const int oy = 4 * yg + (v >> 5), ox = 32 * xc + (v & 31);
-      const long long o = ((((long long)nb * a.do_ + oz) * a.ho + oy) * a.wo + ox) * 32 + 4 * q8;
-      if constexpr (B16) rz[k] = *reinterpret_cast<const bf16x4_w*>(dz16 + o);
-      else rz[k] = *reinterpret_cast<const f32x4*>(dz + o);
+    for (int k = 0; k < NZT; ++k) {
+      const int i = tid + 512 * k, qi = i % ZI, v = i / ZI;  // v = u * OC + column
+      const int oy = 4 * yg + v / OC, ox = OC * xc + v % OC;
+      const long long o = ((((long long)nb * a.do_ + oz) * a.ho + oy) * a.wo + ox) * CO + 8 * qi;
+      if constexpr (B16) {
+        hz[k] = *reinterpret_cast<const bf16x8_w*>(dz16 + o);
+      } else {
+        fz[2 * k] = *reinterpret_cast<const f32x4*>(dz + o);
+        fz[2 * k + 1] = *reinterpret_cast<const f32x4*>(dz + o + 4);
+      }
     }
+  };
+  auto cvt = [](const f32x4& lo, const f32x4& hi) {
+    bf16x8_w h;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) { h[e] = (__bf16)lo[e]; h[4 + e] = (__bf16)hi[e]; }
+    return h;
+  };
+  // byte offset of 16-channel group `at` of window column cc inside its X row / of quarter `bt` of dZ
+  // column c inside its row (the bank swizzles above)
+  auto xhalf = [](int at, int cc) { return CI == 16 ? 0 : ((at ^ ((cc >> 2) & 1)) * 32); };
+  auto zq = [](int bt, int c) {
+    return (CO == 32 ? (bt ^ ((c >> 3) & 1)) : (bt ^ (((c >> 1) & 1) | (((c >> 3) & 1) << 1)))) * 32;
   };
   auto store = [&]() {
 #pragma unroll
     for (int k = 0; k < NXT; ++k) {
-      const int i = tid + 512 * k, q4 = i & 3, v = i >> 2;
+      const int i = tid + 512 * k, qi = i % XI, v = i / XI;
       if (i >= NX) break;
       const int c = v % XW, r = (v / XW) % 9, pl = v / (9 * XW);
-      bf16x4_w h;
-      if constexpr (B16) h = rx[k];
-      else { h[0] = (__bf16)rx[k][0]; h[1] = (__bf16)rx[k][1]; h[2] = (__bf16)rx[k][2]; h[3] = (__bf16)rx[k][3]; }
-      *reinterpret_cast<bf16x4_w*>(smem + (pl * XPS + r * XRS + xcol(c)) * 32 + q4 * 8) = h;
+      bf16x8_w h;
+      if constexpr (B16) h = hx[k];
+      else h = cvt(fx[2 * k], fx[2 * k + 1]);
+      *reinterpret_cast<bf16x8_w*>(smem + (pl * XPS + r * XRS + xcol(c)) * XB + xhalf(qi >> 1, c) + (qi & 1) * 16) = h;
     }
 #pragma unroll
-    for (int k = 0; k < 2; ++k) {
-      const int i = tid + 512 * k, q8 = i & 7, v = i >> 3, ox = v & 31;
-      const int ph = (q8 >> 2) ^ ((ox >> 3) & 1);
-      bf16x4_w h;
-      if constexpr (B16) h = rz[k];
-      else { h[0] = (__bf16)rz[k][0]; h[1] = (__bf16)rz[k][1]; h[2] = (__bf16)rz[k][2]; h[3] = (__bf16)rz[k][3]; }
-      *reinterpret_cast<bf16x4_w*>(smem + XBYTES + v * 64 + ph * 32 + (q8 & 3) * 8) = h;
+    for (int k = 0; k < NZT; ++k) {
+      const int i = tid + 512 * k, qi = i % ZI, v = i / ZI, c = v % OC;
+      bf16x8_w h;
+      if constexpr (B16) h = hz[k];
+      else h = cvt(fz[2 * k], fz[2 * k + 1]);
+      *reinterpret_cast<bf16x8_w*>(zs + v * ZB + zq(qi >> 1, c) + (qi & 1) * 16) = h;
     }
   };
-  constexpr int NTAP = 7;  // taps tg, tg + 4, ... (< 27)
-  f32x4 acc[NTAP];
+  f32x4 acc[NTAP][AT][BTW];
 #pragma unroll
-  for (int i = 0; i < NTAP; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int i = 0; i < NTAP; ++i)
+#pragma unroll
+    for (int at = 0; at < AT; ++at)
+#pragma unroll
+      for (int j = 0; j < BTW; ++j) acc[i][at][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   const int g = lane >> 4, q = (lane & 15) >> 2, pp = lane & 3;
   if (s0 < s1) load(s0);
   for (int sl = s0; sl < s1; ++sl) {
@@ -857,28 +898,47 @@ __global__ __launch_bounds__(512) void wgrad_s2_kernel(Ws2Args a, const float* _
     lds_barrier();
     if (sl + 1 < s1) load(sl + 1);
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int ox0 = 8 * g + q, ox1 = ox0 + 4;
-      const bf16x8_w bfr = tr_pair(smem + XBYTES, (u * 32 + ox0) * 64 + ((bt ^ ((ox0 >> 3) & 1)) * 32) + pp * 8,
-                                   (u * 32 + ox1) * 64 + ((bt ^ ((ox1 >> 3) & 1)) * 32) + pp * 8);
+    for (int s = 0; s < KS; ++s) {
+      // this lane's two voxels of the K-step: kv0 = 8g + q and kv0 + 4 (same output row)
+      const int kv0 = 8 * g + q;
+      const int u = OC == 32 ? s : 2 * s + (kv0 >> 4);
+      const int c0 = OC == 32 ? kv0 : (kv0 & 15), c1 = c0 + 4;
+      bf16x8_w bfr[BTW];
+#pragma unroll
+      for (int j = 0; j < BTW; ++j) {
+        const int bt = bh * BTW + j;
+        bfr[j] = tr_pair(zs, (u * OC + c0) * ZB + zq(bt, c0) + pp * 8, (u * OC + c1) * ZB + zq(bt, c1) + pp * 8);
+      }
 #pragma unroll
       for (int i = 0; i < NTAP; ++i) {
         const int t = tg + 4 * i;
         if (t < 27) {  // wave-uniform
           const int td = t / 9, th = (t / 3) % 3, tw = t % 3;
           const int rb = td * XPS + (2 * u + th) * XRS;
-          const bf16x8_w afr = tr_pair(smem, (rb + xcol(2 * ox0 + tw)) * 32 + pp * 8, (rb + xcol(2 * ox1 + tw)) * 32 + pp * 8);
-          acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afr, bfr, acc[i], 0, 0, 0);
+          const int cc0 = 2 * c0 + tw, cc1 = 2 * c1 + tw;
+#pragma unroll
+          for (int at = 0; at < AT; ++at) {
+            const bf16x8_w afr = tr_pair(smem, (rb + xcol(cc0)) * XB + xhalf(at, cc0) + pp * 8,
+                                         (rb + xcol(cc1)) * XB + xhalf(at, cc1) + pp * 8);
+#pragma unroll
+            for (int j = 0; j < BTW; ++j) acc[i][at][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afr, bfr[j], acc[i][at][j], 0, 0, 0);
+          }
         }
       }
     }
   }
-  // partials ws[p][t][b][a]: lane holds a = 4g + jj, b = 16 bt + (lane & 15)
+  // partials ws[p][t][b][a]: lane holds a = 16 at + 4g + jj, b = 16 bt + (lane & 15)
   const int bl = lane & 15;
 #pragma unroll
   for (int i = 0; i < NTAP; ++i) {
     const int t = tg + 4 * i;
-    if (t < 27) *reinterpret_cast<f32x4*>(ws + ((((long long)p * 27 + t) * 32 + bt * 16 + bl) * 16 + 4 * g)) = acc[i];
+    if (t < 27)
+#pragma unroll
+      for (int at = 0; at < AT; ++at)
+#pragma unroll
+        for (int j = 0; j < BTW; ++j)
+          *reinterpret_cast<f32x4*>(ws + ((((long long)p * 27 + t) * CO + (bh * BTW + j) * 16 + bl) * CI + at * 16 + 4 * g)) =
+              acc[i][at][j];
   }
 }
 
@@ -1001,15 +1061,20 @@ static int g_ws2_P = 128;  // cgan3d_set_tuning key 10: blocks of wgrad_s2_kerne
 void wgrad_s2_set_blocks(int v) { g_ws2_P = v; }
 
 bool wgrad_s2_ok(const cgan3d_conv_geom* g) {
+  const bool c16 = g->cin == 16 && g->cout == 32, c32 = g->cin == 32 && g->cout == 64;
+  const int oc = c32 ? 16 : 32;
   return g_ws2_P > 0 && g->prec == CGAN3D_PREC_BF16 && !g->transposed && !g->reflect && g->k == 3 && g->stride == 2 &&
-         g->pad == 1 && g->cin == 16 && g->cout == 32 && g->ho % 4 == 0 && g->wo % 32 == 0 &&
+         g->pad == 1 && (c16 || c32) && g->ho % 4 == 0 && g->wo % oc == 0 &&
          (long long)2 * g->do_ - 1 <= g->di && (long long)2 * g->ho - 1 <= g->hi && (long long)2 * g->wo - 1 <= g->wi;
 }
 
 static void wgrad_s2_geometry(const cgan3d_conv_geom* g, Ws2Args* a, int* P) {
   a->n = g->n; a->di = g->di; a->hi = g->hi; a->wi = g->wi; a->do_ = g->do_; a->ho = g->ho; a->wo = g->wo;
-  a->slabs = g->n * g->do_ * (g->ho / 4) * (g->wo / 32);
-  const int p = std::max(1, std::min(g_ws2_P, a->slabs));
+  const int oc = g->cin == 32 ? 16 : 32;
+  a->slabs = g->n * g->do_ * (g->ho / 4) * (g->wo / oc);
+  // the 32 <-> 64 level: half the blocks (its partial rows are four times as long)
+  const int pmax = g->cin == 32 ? std::max(1, g_ws2_P / 2) : g_ws2_P;
+  const int p = std::max(1, std::min(pmax, a->slabs));
   a->spb = (a->slabs + p - 1) / p;
   *P = (a->slabs + a->spb - 1) / a->spb;
 }
@@ -1019,7 +1084,7 @@ long long wgrad_s2_ws_floats(const cgan3d_conv_geom* g) {
   Ws2Args a;
   int P;
   wgrad_s2_geometry(g, &a, &P);
-  return (long long)P * 27 * 16 * 32;
+  return (long long)P * 27 * g->cin * g->cout;
 }
 
 int wgrad_s2_launch(const cgan3d_conv_geom* g, const float* gathered, const float* aligned, const __bf16* g16,
@@ -1027,9 +1092,16 @@ int wgrad_s2_launch(const cgan3d_conv_geom* g, const float* gathered, const floa
   Ws2Args a;
   int P;
   wgrad_s2_geometry(g, &a, &P);
-  if (g16 && a16) ::cg::launch(wgrad_s2_kernel<true>, dim3(P), dim3(512), 0, st, a, gathered, aligned, g16, a16, ws);
-  else ::cg::launch(wgrad_s2_kernel<false>, dim3(P), dim3(512), 0, st, a, gathered, aligned, g16, a16, ws);
-  wgrad_reduce_launch(ws, P, 16, 32, dw, (long long)g->w_sa, (long long)g->w_sb, accumulate, st);
+  const bool b16 = g16 && a16;
+#define CG_WS2(CI, CO)                                                                                           \
+  (b16 ? ::cg::launch(wgrad_s2_kernel<CI, CO, true>, dim3(P, CO / 32), dim3(512), 0, st, a, gathered, aligned, g16, a16, \
+                      ws)                                                                                          \
+       : ::cg::launch(wgrad_s2_kernel<CI, CO, false>, dim3(P, CO / 32), dim3(512), 0, st, a, gathered, aligned, g16, \
+                      a16, ws))
+  if (g->cin == 32) CG_WS2(32, 64);
+  else CG_WS2(16, 32);
+#undef CG_WS2
+  wgrad_reduce_launch(ws, P, g->cin, g->cout, dw, (long long)g->w_sa, (long long)g->w_sb, accumulate, st);
   return CGAN3D_OK;
 }
 

@@ -505,6 +505,8 @@ WGRAD_BF16_CASES = [
     (64, 64, 3, 1, 1, False, (5, 4, 8)),     # wgrad_k3_kernel, odd unit count, one unit per row
     (16, 32, 3, 2, 1, False, (12, 16, 20)),  # downsampling
     (16, 32, 3, 2, 1, False, (8, 16, 64)),   # downsampling 16 -> 32: wgrad_s2_kernel (4 x 8 x 32 outputs)
+    (32, 64, 3, 2, 1, False, (8, 16, 32)),   # downsampling 32 -> 64: wgrad_s2_kernel<32, 64> (round 6)
+    (32, 64, 3, 2, 1, False, (7, 16, 32)),   # ... odd input depth (a window plane past the volume)
     (8, 16, 4, 2, 1, False, (16, 16, 16)),   # critic middle
     (32, 64, 4, 2, 1, False, (8, 8, 8)),
     (12, 20, 3, 1, 1, True, (5, 6, 7)),      # odd channel counts, reflect
@@ -529,7 +531,7 @@ def test_wgrad_bf16(cin, cout, k, s, p, reflect, sp):
     dwo = torch.empty(w.shape, device="cuda")
     ops.wgrad(gw, _cl(x), _cl(gy), dwo, ws)
     assert_close(dwo.double().cpu().numpy(), dw.numpy(), 2e-2, "bf16 wgrad")
-    if tuple(sp) == (8, 16, 64):
+    if tuple(sp) in ((8, 16, 64), (8, 16, 32), (7, 16, 32)):
         # wgrad_s2_kernel (the generic kernel ignores shadows and sums with atomics, so no bitwise
         # comparison there; the ResNet shape takes wgrad_k3m_kernel from shadows: its own test below):
         # both operands from bf16 shadows, bit-identical
@@ -540,10 +542,10 @@ def test_wgrad_bf16(cin, cout, k, s, p, reflect, sp):
     assert_close(dwo.double().cpu().numpy(), 2 * dw.numpy(), 2e-2, "bf16 wgrad accumulate")
 
 
-@pytest.mark.parametrize("cin,cout,sp", [(64, 32, (4, 6, 8)), (32, 16, (4, 8, 32))])
+@pytest.mark.parametrize("cin,cout,sp", [(64, 32, (4, 6, 8)), (32, 16, (4, 8, 32)), (64, 32, (4, 8, 16))])
 def test_wgrad_bf16_conv_transpose(cin, cout, sp):
-    """ConvTranspose3d weight gradient (operands swapped); 32 -> 16 at (4, 8, 32) takes
-    wgrad_s2_kernel (the last upsampling layer's shape)."""
+    """ConvTranspose3d weight gradient (operands swapped); 32 -> 16 at (4, 8, 32) and 64 -> 32 at
+    (4, 8, 16) take wgrad_s2_kernel (the up-sampling layers' shapes)."""
     from cgan3d_amd import ops, _lib as L
     g = torch.Generator().manual_seed(9 + cin)
     n, k, s, p = 2, 3, 2, 1
@@ -557,7 +559,7 @@ def test_wgrad_bf16_conv_transpose(cin, cout, sp):
     dwo = torch.empty(w.shape, device="cuda")
     ops.wgrad(gw, _cl(gy), _cl(x), dwo, ws)
     assert_close(dwo.double().cpu().numpy(), dw.numpy(), 2e-2, "bf16 convT wgrad")
-    if cin == 32:  # wgrad_s2_kernel from both operands' bf16 shadows: bit-identical
+    if tuple(sp) != (4, 6, 8):  # wgrad_s2_kernel from both operands' bf16 shadows: bit-identical
         dw16 = torch.empty_like(dwo)
         ops.wgrad(gw, _cl(gy), _cl(x), dw16, ws, gathered16=_cl(gy).bfloat16(), aligned16=_cl(x).bfloat16())
         assert torch.equal(dw16, dwo), "bf16-shadow convT weight grad differs"
