@@ -65,14 +65,21 @@ def conv_flops(n, dout, cin, cout, k):
 
 # roofline candidates: kernel description, launch role, geometry predicate, committed PMC summary
 # (HBM bytes per launch from rocprofv3 FETCH_SIZE / WRITE_SIZE passes, profiles/)
+def progress(msg):
+    """A progress line on stderr (a long default run then never looks silent to a watchdog)."""
+    print(f"bench: {msg} ({time.strftime('%H:%M:%S')})", file=sys.stderr, flush=True)
+
+
 ROOFLINES = {
     "halo_res": ("ResNet-block Conv3d 64->64 k3 s1 at (S/4)^3, forward + input-grad "
                  "(bf16: conv_k3m_kernel; f32: conv_gemm_kernel)",
                  "conv", lambda g: g.cin == 64 and g.cout == 64 and g.k == 3 and g.stride == 1,
-                 "profiles/r05_pmc_conv_k3m.json"),
-    "k7_w2n": ("k7m_w2n_kernel: generator last Conv3d 16->1 k7 (+bias, tanh, opt_hat) forward",
-               "conv", lambda g: g.k == 7 and g.cin == 16 and g.cout == 1, None),
+                 "profiles/r05_pmc_conv_k3m.json", "conv_k3m_kernel"),
+    "k7_w2n": ("k7s_w2n_kernel: generator last Conv3d 16->1 k7 (+bias, tanh, opt_hat) forward",
+               "conv", lambda g: g.k == 7 and g.cin == 16 and g.cout == 1, None, "k7s_w2n_kernel"),
 }
+# (description, launch role, geometry match, committed PMC traffic summary, kernel-name filter of the
+# bf16 plan's in-step timing: the launches of that kernel are the roofline kernel's launches)
 
 
 def pmc_traffic(path, size, batch, precision):
@@ -104,16 +111,18 @@ def cpu_baseline(size, seconds, g_args):
     from cgan3d_amd.model.init import pcg64_state_dict
     from oracle import reference_torch as R
 
-    # every core the process may run on; the cgroup CPU quota, when one is set, is
-    # reported beside it (on the GPU box the affinity mask can be wider than the CPU share)
-    threads = max(1, len(os.sched_getaffinity(0)))
-    torch.set_num_threads(threads)
+    # every core the process may use: the affinity mask, capped by the cgroup CPU quota
+    # when one is set — on the GPU box the mask lists the whole host while the quota is this GPU's share
+    # (16 CPUs); threads past the quota only time-slice (a 192-thread oracle step there ran > 3 minutes)
+    affinity = max(1, len(os.sched_getaffinity(0)))
     quota = None
     try:
         q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
         quota = None if q == "max" else round(int(q) / int(per), 2)
     except (OSError, ValueError):
         pass
+    threads = affinity if quota is None else max(1, min(affinity, int(quota + 0.5)))
+    torch.set_num_threads(threads)
     gcfg = R.GenConfig(**g_args)
     cfg = R.StepConfig(gen=gcfg, critic=R.CriticConfig())
     gp = {k: torch.from_numpy(v.copy()) for k, v in pcg64_state_dict(list(R.gen_param_shapes(gcfg).items()), 0).items()}
@@ -126,10 +135,13 @@ def cpu_baseline(size, seconds, g_args):
     eps = torch.full((b, 1, 1, 1, 1), 0.5)
     args = (torch.from_numpy(opt), torch.from_numpy(sub), torch.from_numpy(seg), eps, cfg)
     R.train_step(gp, dp, gopt, dopt, *args)  # warm-up
+    progress(f"cpu_baseline: warm-up step done on {threads} threads")
     n, t0 = 0, time.perf_counter()
     while True:
         R.train_step(gp, dp, gopt, dopt, *args)
         n += 1
+        if n % 10 == 0:
+            progress(f"cpu_baseline: {n} steps")
         el = time.perf_counter() - t0
         if el >= seconds or n >= 50:
             break
@@ -143,6 +155,7 @@ def cpu_baseline(size, seconds, g_args):
         pass
     return {"value": round(n * b / el, 4), "unit": "patches/s", "cores": threads, "kind": "port",
             "cpu_model": cpu_model, "torch_threads": torch.get_num_threads(), "cgroup_cpu_quota": quota,
+            "affinity_cpus": affinity,
             "sample": f"oracle/reference_torch.py train_step, {size}^3, batch 1+1, GP conf, fp32, {n} steps in "
                       f"{el:.1f}s after 1 warm-up step; patches/s per subopt patch at batch 1 stands for the GPU "
                       f"line's batch (the CPU step's work and time grow linearly with the batch)"}
@@ -471,7 +484,7 @@ def main():
         return bench_trainer(args, S, B, dev, world, rank, dist, batches)
 
     from cgan3d_amd import ops
-    roof_desc, roof_role, roof_match, roof_pmc = ROOFLINES[args.roofline]
+    roof_desc, roof_role, roof_match, roof_pmc, roof_kname = ROOFLINES[args.roofline]
     ev = []  # (start, end, algorithmic flops) per timed launch
 
     reps = 8
@@ -502,6 +515,7 @@ def main():
         eng.load_inputs(*batches[i % len(batches)])
         eng.run_plan()
 
+    progress(f"warm-up ({args.warmup} steps)")
     for i in range(args.warmup):
         one_step(i, False)
     if mode == "graph":
@@ -516,6 +530,7 @@ def main():
     # per-step boundaries: an event on the main stream after each step (every step ends with the
     # main stream waiting for the side stream), read after the timed region -> median step time
     marks = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
+    progress(f"timed region ({args.steps} steps, {mode})")
     t0 = time.perf_counter()
     marks[0].record()
     for i in range(args.steps):
@@ -535,6 +550,7 @@ def main():
     # the roofline kernel's launch time: after the timed region, eager steps in which each of its
     # launches is followed by `reps` back-to-back repeats between two HIP events on its stream
     # (repeats keep the queue full, so host launch gaps stay out of the measurement)
+    progress("roofline kernel timing")
     for i in range(min(args.steps, 10)):
         one_step(i, True)
     torch.cuda.synchronize()
@@ -547,9 +563,27 @@ def main():
         one_step(i, True)
     torch.cuda.synchronize()
     kern_in = [(a.elapsed_time(b), f) for a, b, f in ev]
+    # the headline figure (round 6): the kernel's launches timed inside the plan-mode step itself —
+    # a plan recorded with cgan3d_plan_time_filter issues each of them with its own start / stop
+    # events (hipExtLaunchKernel's dispatch events; the rest of the step unchanged), run over the
+    # bench batches after the timed region
+    kern_plan = []
+    if mode == "plan" and args.precision == "bf16" and roof_kname:
+        ops.plan_time_filter(roof_kname)
+        try:
+            tplan = eng.record()
+        finally:
+            ops.plan_time_filter(None)
+        for i in range(min(args.steps, 10)):
+            eng.load_inputs(*batches[i % len(batches)])
+            tplan.run()
+            torch.cuda.synchronize()
+            kern_plan += tplan.kernel_times()
+        kern_plan = [t for t in kern_plan if t > 0]
     # the reference's schedule (basic_conf.py:24, Trainer.py:174-184): the critic trains every
     # iteration, the generator every 5th; every iteration runs the generator forward on its batch
     ref_sched = None
+    progress("reference schedule")
     if mode == "plan" and world == 1:
         crit_plan = eng.record(do_critic=True, do_generator=False)
         full_plan = eng.record()
@@ -573,13 +607,15 @@ def main():
         el = float(t.item())
     losses = eng.losses.cpu().numpy()
     assert np.isfinite(losses).all(), f"non-finite losses {losses}"
-    # the kernel's launch duration: 8 back-to-back repeats of each in-step launch between two HIP
+    # the kernel's launch duration: its launches inside the plan-mode step (kern_plan, above); the
+    # warm-repeat figure beside it: 8 back-to-back repeats of each in-step launch between two HIP
     # events on its stream (the events' own dispatch cost amortised over the repeats; agrees with the
     # rocprofv3 kernel-trace average of the plan-mode step, profiles/r03_plan_kernel_stats.csv); the
     # single-launch bracket (spin kernel ahead, one launch between the events) is reported beside it
-    kern_ms = float(np.mean([t for t, _ in kern]))
+    rep_ms = float(np.mean([t for t, _ in kern]))
     single_ms = float(np.mean([t for t, _ in kern_in]))
     roof_flops = float(np.mean([f for _, f in kern]))
+    kern_ms = rep_ms
     achieved = roof_flops / (kern_ms * 1e-3) / 1e12
     peak = BF16_PEAK_TFLOPS if args.precision == "bf16" else F32_PEAK_TFLOPS
     ms = el / args.steps * 1e3
@@ -611,7 +647,15 @@ def main():
                      "traffic": pmc_traffic(roof_pmc, S, B, args.precision), "traffic_source": roof_pmc,
                      "avg_launch_ms": round(kern_ms, 4), "flops_per_launch": roof_flops, "launches_timed": len(kern),
                      "timing": f"HIP events around {reps} back-to-back repeats of each launch of the kernel inside eager "
-                               f"steps, on its own operands and stream (per-launch dispatch cost amortised)",
+                               f"steps, on its own operands and stream (per-launch dispatch cost amortised; agrees "
+                               f"with the plan-mode rocprofv3 kernel trace, profiles/r06_plan_kernel_stats.csv)",
+                     "in_plan": None if not kern_plan else {
+                         "avg_launch_ms": round(float(np.mean(kern_plan)), 4), "launches_timed": len(kern_plan),
+                         "achieved": round(roof_flops / (float(np.mean(kern_plan)) * 1e-3) / 1e12, 3),
+                         "frac": round(roof_flops / (float(np.mean(kern_plan)) * 1e-3) / 1e12 / peak, 4),
+                         "timing": "each launch inside plan-mode steps between its own start / stop events "
+                                   "(hipExtLaunchKernel via cgan3d_plan_time_filter): includes the dispatch's "
+                                   "queue latency, which the rocprofv3 kernel trace leaves out"},
                      "single_launch": {"avg_launch_ms": round(single_ms, 4),
                                        "achieved": round(roof_flops / (single_ms * 1e-3) / 1e12, 3),
                                        "timing": "one launch between two HIP events in place inside eager steps, a spin "
@@ -629,18 +673,22 @@ def main():
     if mode == "plan" and world == 1 and subs:
         # beside the resident number: the batch coming over PCIe from pinned host memory each step
         if "h2d" in subs:
+            progress("sub-line h2d")
             out["h2d"] = h2d_bench(eng, S, B, dev, args.steps)
         del eng
         torch.cuda.empty_cache()
         # the drop-in Trainer fed by the PatchLoaders (the loop train.py's Trainer.fit runs)
         if "loader" in subs:
+            progress("sub-line loader")
             out["loader"] = loader_bench(S, B, dev, args.steps, args.precision)
         torch.cuda.empty_cache()
         # the other single-GPU BASELINE configs in the same run: the exact-fp32 parity path at this
         # workload, and configs[2] (128^3 B=1 fp32)
         if "f32" in subs:
+            progress("sub-line f32")
             out["f32"] = sub_config(S, B, "f32", dev, g_args) if args.precision != "f32" else None
         if "b128_f32" in subs:
+            progress("sub-line b128_f32")
             out["b128_f32"] = sub_config(128, 1, "f32", dev, g_args, steps=10)
             bn = bn_hbm()
             if bn is not None:
@@ -649,8 +697,10 @@ def main():
         # configs[4]'s per-GPU slice: 128^3 bf16 with the gradient penalty, 2 OPT + 2 subopt patches
         # (global batch 16 over 8 GPUs)
         if "b128_bf16_b2" in subs:
+            progress("sub-line b128_bf16_b2")
             out["b128_bf16_b2"] = sub_config(128, 2, "bf16", dev, g_args, steps=10)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        progress("sub-line cpu_baseline")
         out["cpu_baseline"] = cpu_baseline(S, args.cpu_seconds, g_args)
     if rank == 0:
         print(json.dumps(out), flush=True)

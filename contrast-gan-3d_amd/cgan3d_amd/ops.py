@@ -501,6 +501,18 @@ class Plan:
             else:
                 it()
 
+    def kernel_times(self):
+        """Durations (ms) of the launches timed in the last ``run()`` (``plan_time_filter`` at record
+        time), in record order; call after synchronising."""
+        lib, out = L.lib(), []
+        for it in self.items:
+            if isinstance(it, int):
+                n = int(lib.cgan3d_plan_times(it, None, 0))
+                buf = (ctypes.c_float * max(n, 1))()
+                lib.cgan3d_plan_times(it, buf, n)
+                out += [float(v) for v in buf[:n]]
+        return out
+
     def __del__(self):
         if L._lib is not None:
             for it in self.items:
@@ -510,6 +522,12 @@ class Plan:
 
 
 _RECORDING: Optional[Plan] = None
+
+
+def plan_time_filter(substring: Optional[str]):
+    """Plans recorded while set time each launch of a kernel whose name contains ``substring`` with its
+    own HIP events (cgan3d_plan_time_filter; ``Plan.kernel_times``); None clears it."""
+    check(L.lib().cgan3d_plan_time_filter(substring.encode() if substring else None), "plan_time_filter")
 
 
 def recording() -> bool:

@@ -31,12 +31,17 @@ struct Plan {
   // (hipExtLaunchKernel's stop event: the dispatch's own completion signal) instead of enqueueing
   // a separate marker packet behind it — see cgan3d_stream_wait.
   std::unordered_map<hipStream_t, std::shared_ptr<hipEvent_t>> tail;
+  // (start, stop) timing events of the launches cgan3d_plan_time_filter selected at record time
+  // (hipExtLaunchKernel's own dispatch events: the kernel's in-plan duration, no extra packets)
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> timed;
   void add(std::function<hipError_t()> op, hipStream_t st, std::shared_ptr<hipEvent_t> stop = nullptr) {
     ops.push_back(std::move(op));
     tail[st] = std::move(stop);
   }
 };
 extern thread_local Plan* g_rec;
+// true when the launch of kernel k being recorded is one cgan3d_plan_time_filter selected (plan.hip)
+bool plan_time_match(const void* k, hipStream_t st);
 
 template <typename... KArgs, typename... Args>
 inline void launch(void (*k)(KArgs...), dim3 grid, dim3 block, size_t lds, hipStream_t st, Args... args) {
@@ -46,9 +51,25 @@ inline void launch(void (*k)(KArgs...), dim3 grid, dim3 block, size_t lds, hipSt
   }
   std::tuple<std::decay_t<KArgs>...> t(static_cast<std::decay_t<KArgs>>(args)...);
   auto stop = std::make_shared<hipEvent_t>(nullptr);
-  g_rec->add([k, grid, block, lds, st, t, stop]() mutable {
+  hipEvent_t t0 = nullptr, t1 = nullptr;
+  if (plan_time_match(reinterpret_cast<const void*>(k), st) && hipEventCreate(&t0) == hipSuccess) {
+    if (hipEventCreate(&t1) == hipSuccess) {
+      g_rec->events.push_back(t0);
+      g_rec->events.push_back(t1);
+      g_rec->timed.emplace_back(t0, t1);
+    } else {
+      (void)hipEventDestroy(t0);
+      t0 = nullptr;
+    }
+  }
+  g_rec->add([k, grid, block, lds, st, t, stop, t0, t1]() mutable {
     return std::apply([&](auto&... a) {
       void* argv[] = {static_cast<void*>(&a)...};
+      if (t0 != nullptr) {  // a timed launch (then a bound cross-stream wait gets a marker behind it)
+        hipError_t e = hipExtLaunchKernel(reinterpret_cast<const void*>(k), grid, block, argv, lds, st, t0, t1, 0);
+        if (e == hipSuccess && *stop != nullptr) e = hipEventRecord(*stop, st);
+        return e;
+      }
       if (*stop != nullptr)
         return hipExtLaunchKernel(reinterpret_cast<const void*>(k), grid, block, argv, lds, st, nullptr, *stop, 0);
       return hipLaunchKernel(reinterpret_cast<const void*>(k), grid, block, argv, lds, st);

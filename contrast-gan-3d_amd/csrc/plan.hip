@@ -11,6 +11,7 @@
 // Contract (as for hipGraph capture): every buffer and device scalar a recorded launch touches
 // must stay allocated and keep its address; values may change between runs.
 #include <cstring>
+#include <string>
 
 #include "common.h"
 
@@ -42,9 +43,34 @@ static bool bind_disabled() {
   return off;
 }
 
+static thread_local std::string g_time_filter;  // cgan3d_plan_time_filter
+
+bool plan_time_match(const void* k, hipStream_t st) {
+  if (g_time_filter.empty()) return false;
+  const char* n = hipKernelNameRefByPtr(k, st);
+  return n != nullptr && strstr(n, g_time_filter.c_str()) != nullptr;
+}
+
 }  // namespace cg
 
 using namespace cg;
+
+extern "C" int cgan3d_plan_time_filter(const char* substring) {
+  g_time_filter = substring ? substring : "";
+  return CGAN3D_OK;
+}
+
+extern "C" int64_t cgan3d_plan_times(void* plan, float* ms, int64_t max) {
+  if (plan == nullptr) return -1;
+  Plan* p = static_cast<Plan*>(plan);
+  const int64_t n = (int64_t)p->timed.size();
+  for (int64_t i = 0; i < n && i < max && ms != nullptr; ++i) {
+    float v = -1.f;
+    if (hipEventElapsedTime(&v, p->timed[i].first, p->timed[i].second) != hipSuccess) v = -1.f;
+    ms[i] = v;
+  }
+  return n;
+}
 
 extern "C" int cgan3d_plan_begin(void) {
   CG_CHECK_ARG(g_rec == nullptr, "cgan3d_plan_begin: a plan is already being recorded on this thread");
