@@ -74,7 +74,7 @@ ROOFLINES = {
     "halo_res": ("ResNet-block Conv3d 64->64 k3 s1 at (S/4)^3, forward + input-grad "
                  "(bf16: conv_k3m_kernel; f32: conv_gemm_kernel)",
                  "conv", lambda g: g.cin == 64 and g.cout == 64 and g.k == 3 and g.stride == 1,
-                 "profiles/r05_pmc_conv_k3m.json", "conv_k3m_kernel"),
+                 "profiles/r06_pmc_conv_k3m.json", "conv_k3m_kernel"),
     "k7_w2n": ("k7s_w2n_kernel: generator last Conv3d 16->1 k7 (+bias, tanh, opt_hat) forward",
                "conv", lambda g: g.k == 7 and g.cin == 16 and g.cout == 1, None, "k7s_w2n_kernel"),
 }
