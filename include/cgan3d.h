@@ -208,13 +208,15 @@ int64_t cgan3d_conv3d_sumsq_blocks(const cgan3d_conv_geom* g);
 
 const char* cgan3d_version(void);
 const char* cgan3d_get_last_error(void);
-/* Launch-shape / kernel choice (process-wide; set before building plans).  Six keys, every value a
+/* Launch-shape / kernel choice (process-wide; set before building plans).  Seven keys, every value a
  * correct configuration (anything else: CGAN3D_EINVAL): 9 voxel chunks of the ResNet weight grad
- * (default 28, 0 = generic kernel); 10 blocks of the stride-2 weight grad (default 128, 0 = generic);
+ * (default 28, 0 = generic kernel); 10 blocks of the stride-2 weight grads (default 128 for the 16 <-> 32
+ * level, half of it for the 32 <-> 64 level; 0 = generic);
  * 13 output planes per streamed last-conv block (0 auto, 8, 16, -1 = Toeplitz kernel); 15 ResNet convs
  * on conv_k3m and the 32 <-> 64 stride-2 pair on conv_t64 / conv_f64 (1, default) or all of them on the
  * round-3 halo kernels conv_k3 / conv_halo (0); 16 ResNet weight grads on wgrad_k3m (1, default) or
- * wgrad_k3 (0); 20 most blocks of a k7 weight grad (default 512). */
+ * wgrad_k3 (0); 20 most blocks of a k7 weight grad (default 512); 21 (round 6) output planes per
+ * streamed-plane 1 <-> 16 k7 block (0 auto, 1..64; -1 = the k7m_n2w / k7m_wg kernels). */
 int cgan3d_set_tuning(int32_t key, int32_t value);
 
 /* --- convolutions (model/blocks.py:29-38 Conv3d / ConvTranspose3d; generator.py:78-84 last
