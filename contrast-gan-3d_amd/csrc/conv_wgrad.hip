@@ -799,7 +799,11 @@ struct Ws2Args {
   int slabs, spb;  // slabs in all, per block
 };
 
-template <int CI, int CO, bool B16>  // B16: both operands from bf16 shadows (bit-identical: fp32 ones are rounded)
+// B16: both operands from bf16 shadows (bit-identical: fp32 ones are rounded); SPB > 0: every block takes
+// exactly SPB slabs (the launcher checks), so the slab loop unrolls into straight-line code and the compiler's
+// vmcnt waits before each LDS store count only the slab being stored (a loop-carried prefetch made it wait
+// for every load in flight)
+template <int CI, int CO, bool B16, int SPB = 0>
 __global__ __launch_bounds__(512) void wgrad_s2_kernel(Ws2Args a, const float* __restrict__ x,
                                                        const float* __restrict__ dz, const __bf16* __restrict__ x16,
                                                        const __bf16* __restrict__ dz16, float* __restrict__ ws) {
@@ -818,9 +822,17 @@ __global__ __launch_bounds__(512) void wgrad_s2_kernel(Ws2Args a, const float* _
   const int p = blockIdx.x;
   const int s0 = p * a.spb, s1 = min(s0 + a.spb, a.slabs);
   const int yg_n = a.ho >> 2, xc_n = a.wo / OC;
-  bf16x8_w hx[B16 ? NXT : 1], hz[B16 ? NZT : 1];
+  // two slabs in flight in registers from the bf16 shadows (round 6b; one with fp32 operands, which
+  // take twice the registers): the next-but-one slab's loads overlap the current slab's MFMAs
+  constexpr int DEPTH = B16 && CI == 16 ? 2 : 1;  // (<32, 64>: two slabs spilled)
+  bf16x8_w hx[B16 ? DEPTH : 1][B16 ? NXT : 1], hz[B16 ? DEPTH : 1][B16 ? NZT : 1];
   f32x4 fx[B16 ? 1 : 2 * NXT], fz[B16 ? 1 : 2 * NZT];
-  auto load = [&](int sl) {
+  // the window's out-of-volume items load a valid address (element 0) and are zeroed at the LDS store:
+  // a select on the loaded value right after the load would make the compiler wait for it there,
+  // which turned the prefetch into a serial load
+  unsigned okm[DEPTH];
+  auto load = [&](int sl, int rb) {
+    okm[rb] = 0u;
     const int xc = sl % xc_n, q1 = sl / xc_n, yg = q1 % yg_n, zq = q1 / yg_n;  // zq = nb * do + oz
     const int oz = zq % a.do_, nb = zq / a.do_;
     const int iz0 = 2 * oz - 1, iy0 = 8 * yg - 1, ix0 = 2 * OC * xc - 1;
@@ -830,12 +842,13 @@ __global__ __launch_bounds__(512) void wgrad_s2_kernel(Ws2Args a, const float* _
       const int c = v % XW, r = (v / XW) % 9, pl = v / (9 * XW);
       const int iz = iz0 + pl, iy = iy0 + r, ix = ix0 + c;
       const bool ok = i < NX && (unsigned)iz < (unsigned)a.di && (unsigned)iy < (unsigned)a.hi && (unsigned)ix < (unsigned)a.wi;
-      const long long o = ((((long long)nb * a.di + iz) * a.hi + iy) * a.wi + ix) * CI + 8 * qi;
+      const long long o = ok ? ((((long long)nb * a.di + iz) * a.hi + iy) * a.wi + ix) * CI + 8 * qi : 0;
+      okm[rb] |= (ok ? 1u : 0u) << k;
       if constexpr (B16) {
-        hx[k] = ok ? *reinterpret_cast<const bf16x8_w*>(x16 + o) : bf16x8_w{};
+        hx[rb][k] = *reinterpret_cast<const bf16x8_w*>(x16 + o);
       } else {
-        fx[2 * k] = ok ? *reinterpret_cast<const f32x4*>(x + o) : f32x4{0.f, 0.f, 0.f, 0.f};
-        fx[2 * k + 1] = ok ? *reinterpret_cast<const f32x4*>(x + o + 4) : f32x4{0.f, 0.f, 0.f, 0.f};
+        fx[2 * k] = *reinterpret_cast<const f32x4*>(x + o);
+        fx[2 * k + 1] = *reinterpret_cast<const f32x4*>(x + o + 4);
       }
     }
 #pragma unroll
@@ -844,7 +857,7 @@ __global__ __launch_bounds__(512) void wgrad_s2_kernel(Ws2Args a, const float* _
       const int oy = 4 * yg + v / OC, ox = OC * xc + v % OC;
       const long long o = ((((long long)nb * a.do_ + oz) * a.ho + oy) * a.wo + ox) * CO + 8 * qi;
       if constexpr (B16) {
-        hz[k] = *reinterpret_cast<const bf16x8_w*>(dz16 + o);
+        hz[rb][k] = *reinterpret_cast<const bf16x8_w*>(dz16 + o);
       } else {
         fz[2 * k] = *reinterpret_cast<const f32x4*>(dz + o);
         fz[2 * k + 1] = *reinterpret_cast<const f32x4*>(dz + o + 4);
@@ -863,22 +876,23 @@ __global__ __launch_bounds__(512) void wgrad_s2_kernel(Ws2Args a, const float* _
   auto zq = [](int bt, int c) {
     return (CO == 32 ? (bt ^ ((c >> 3) & 1)) : (bt ^ (((c >> 1) & 1) | (((c >> 3) & 1) << 1)))) * 32;
   };
-  auto store = [&]() {
+  auto store = [&](int rb) {
 #pragma unroll
     for (int k = 0; k < NXT; ++k) {
       const int i = tid + 512 * k, qi = i % XI, v = i / XI;
       if (i >= NX) break;
       const int c = v % XW, r = (v / XW) % 9, pl = v / (9 * XW);
       bf16x8_w h;
-      if constexpr (B16) h = hx[k];
+      if constexpr (B16) h = hx[rb][k];
       else h = cvt(fx[2 * k], fx[2 * k + 1]);
+      if (!((okm[rb] >> k) & 1u)) h = bf16x8_w{};
       *reinterpret_cast<bf16x8_w*>(smem + (pl * XPS + r * XRS + xcol(c)) * XB + xhalf(qi >> 1, c) + (qi & 1) * 16) = h;
     }
 #pragma unroll
     for (int k = 0; k < NZT; ++k) {
       const int i = tid + 512 * k, qi = i % ZI, v = i / ZI, c = v % OC;
       bf16x8_w h;
-      if constexpr (B16) h = hz[k];
+      if constexpr (B16) h = hz[rb][k];
       else h = cvt(fz[2 * k], fz[2 * k + 1]);
       *reinterpret_cast<bf16x8_w*>(zs + v * ZB + zq(qi >> 1, c) + (qi & 1) * 16) = h;
     }
@@ -891,12 +905,7 @@ __global__ __launch_bounds__(512) void wgrad_s2_kernel(Ws2Args a, const float* _
 #pragma unroll
       for (int j = 0; j < BTW; ++j) acc[i][at][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   const int g = lane >> 4, q = (lane & 15) >> 2, pp = lane & 3;
-  if (s0 < s1) load(s0);
-  for (int sl = s0; sl < s1; ++sl) {
-    lds_barrier();  // the previous slab's fragment reads are done
-    store();
-    lds_barrier();
-    if (sl + 1 < s1) load(sl + 1);
+  auto mfmas = [&]() {
 #pragma unroll
     for (int s = 0; s < KS; ++s) {
       // this lane's two voxels of the K-step: kv0 = 8g + q and kv0 + 4 (same output row)
@@ -926,6 +935,42 @@ __global__ __launch_bounds__(512) void wgrad_s2_kernel(Ws2Args a, const float* _
         }
       }
     }
+  };
+  if constexpr (SPB > 0) {
+    load(s0, 0);
+    if (DEPTH == 2 && SPB > 1) load(s0 + 1, DEPTH - 1);
+#pragma unroll
+    for (int k = 0; k < SPB; k += DEPTH) {
+      lds_barrier();
+      store(0);
+      lds_barrier();
+      if (k + DEPTH < SPB) load(s0 + k + DEPTH, 0);
+      mfmas();
+      if (DEPTH == 2 && k + 1 < SPB) {
+        lds_barrier();
+        store(DEPTH - 1);
+        lds_barrier();
+        if (k + 1 + DEPTH < SPB) load(s0 + k + 1 + DEPTH, DEPTH - 1);
+        mfmas();
+      }
+    }
+  } else {
+  if (s0 < s1) load(s0, 0);
+  if (DEPTH == 2 && s0 + 1 < s1) load(s0 + 1, DEPTH - 1);
+  for (int sl = s0; sl < s1; sl += DEPTH) {
+    lds_barrier();  // the previous slab's fragment reads are done
+    store(0);
+    lds_barrier();
+    if (sl + DEPTH < s1) load(sl + DEPTH, 0);
+    mfmas();
+    if (DEPTH == 2 && sl + 1 < s1) {  // block-uniform
+      lds_barrier();
+      store(DEPTH - 1);
+      lds_barrier();
+      if (sl + 1 + DEPTH < s1) load(sl + 1 + DEPTH, DEPTH - 1);
+      mfmas();
+    }
+  }
   }
   // partials ws[p][t][b][a]: lane holds a = 16 at + 4g + jj, b = 16 bt + (lane & 15)
   const int bl = lane & 15;
@@ -1093,13 +1138,20 @@ int wgrad_s2_launch(const cgan3d_conv_geom* g, const float* gathered, const floa
   int P;
   wgrad_s2_geometry(g, &a, &P);
   const bool b16 = g16 && a16;
-#define CG_WS2(CI, CO)                                                                                           \
-  (b16 ? ::cg::launch(wgrad_s2_kernel<CI, CO, true>, dim3(P, CO / 32), dim3(512), 0, st, a, gathered, aligned, g16, a16, \
-                      ws)                                                                                          \
-       : ::cg::launch(wgrad_s2_kernel<CI, CO, false>, dim3(P, CO / 32), dim3(512), 0, st, a, gathered, aligned, g16, \
-                      a16, ws))
-  if (g->cin == 32) CG_WS2(32, 64);
-  else CG_WS2(16, 32);
+  const int spb = a.slabs % a.spb == 0 ? a.spb : 0;  // every block full: the unrolled variants
+#define CG_WS2(CI, CO, B, S) ::cg::launch(wgrad_s2_kernel<CI, CO, B, S>, dim3(P, CO / 32), dim3(512), 0, st, a, \
+                                          gathered, aligned, g16, a16, ws)
+#define CG_WS2_ALL(CI, CO)                                                                  \
+  do {                                                                                      \
+    if (!b16) CG_WS2(CI, CO, false, 0);                                                     \
+    else if (spb == 8) CG_WS2(CI, CO, true, 8);                                             \
+    else if (spb == 4) CG_WS2(CI, CO, true, 4);                                             \
+    else if (spb == 2) CG_WS2(CI, CO, true, 2);                                             \
+    else CG_WS2(CI, CO, true, 0);                                                           \
+  } while (0)
+  if (g->cin == 32) CG_WS2_ALL(32, 64);
+  else CG_WS2_ALL(16, 32);
+#undef CG_WS2_ALL
 #undef CG_WS2
   wgrad_reduce_launch(ws, P, g->cin, g->cout, dw, (long long)g->w_sa, (long long)g->w_sb, accumulate, st);
   return CGAN3D_OK;

@@ -542,6 +542,35 @@ def test_wgrad_bf16(cin, cout, k, s, p, reflect, sp):
     assert_close(dwo.double().cpu().numpy(), 2 * dw.numpy(), 2e-2, "bf16 wgrad accumulate")
 
 
+@pytest.mark.parametrize("cin,cout,sp", [(16, 32, (8, 16, 64)), (32, 64, (8, 16, 32))])
+@pytest.mark.parametrize("blocks", [2, 4, 8, 16])
+def test_wgrad_s2_slab_unrolled_variants(cin, cout, sp, blocks):
+    """Round 6: wgrad_s2_kernel's unrolled slab loops (2, 4 or 8 slabs per block, two slabs in flight
+    for <16, 32>) — tuning key 10 sets the block count, so a 16-slab grid runs 8, 4, 2 or 1 slabs per
+    block — against torch float64 (2e-2), and bit-identical between bf16 shadows and fp32 operands."""
+    from cgan3d_amd import ops, _lib as L
+    g = torch.Generator().manual_seed(17 + cin + blocks)
+    n, k, s, p = 2, 3, 2, 1
+    x = torch.randn(n, cin, *sp, generator=g, dtype=torch.float64)
+    w = (torch.randn(cout, cin, k, k, k, generator=g, dtype=torch.float64) / np.sqrt(cin * k**3)).requires_grad_()
+    y = _ref_conv(x, w, s, p, False)
+    gy = torch.randn(y.shape, generator=g, dtype=torch.float64)
+    dw, = torch.autograd.grad(y, (w,), gy)
+    lib = L.lib()
+    key = blocks * (2 if cin == 32 else 1)  # the 32 <-> 64 level takes half of key 10's blocks
+    try:
+        assert lib.cgan3d_set_tuning(10, key) == 0
+        gw = ops.with_prec(ops.conv_wgrad_geom(n, tuple(sp), tuple(y.shape[2:]), cin, cout, k, s, p, False), L.PREC_BF16)
+        ws = torch.empty(ops.wgrad_ws_floats(gw), device="cuda")
+        dwo, dw16 = torch.empty(w.shape, device="cuda"), torch.empty(w.shape, device="cuda")
+        ops.wgrad(gw, _cl(x), _cl(gy), dwo, ws)
+        ops.wgrad(gw, _cl(x), _cl(gy), dw16, ws, gathered16=_cl(x).bfloat16(), aligned16=_cl(gy).bfloat16())
+    finally:
+        lib.cgan3d_set_tuning(10, 128)
+    assert_close(dwo.double().cpu().numpy(), dw.numpy(), 2e-2, "wgrad_s2 unrolled")
+    assert torch.equal(dw16, dwo), "bf16-shadow vs fp32-operand stride-2 weight grad differ"
+
+
 @pytest.mark.parametrize("cin,cout,sp", [(64, 32, (4, 6, 8)), (32, 16, (4, 8, 32)), (64, 32, (4, 8, 16))])
 def test_wgrad_bf16_conv_transpose(cin, cout, sp):
     """ConvTranspose3d weight gradient (operands swapped); 32 -> 16 at (4, 8, 32) and 64 -> 32 at

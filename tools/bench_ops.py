@@ -50,13 +50,14 @@ def _cases(B=4, S=64):
             return (lambda: ops.conv(geo, x, w, y16, ep)), flops
         return (lambda: ops.conv(geo, x, w, y)), flops
 
-    def wgrad_case(geo, din, dout):
+    def wgrad_case(geo, din, dout, shadows=False):
         x, go = t(B, *din, geo.cin), t(B, *dout, geo.cout)
         dw = torch.empty(geo.cout, geo.cin, geo.k, geo.k, geo.k, device=dev)
         # room for any chunk count a --tune 9=... sweep asks for (wgrad_k3_kernel partials)
         ws = torch.empty(max(ops.wgrad_ws_floats(geo), 256 * 27 * 4096 if geo.cin == geo.cout == 64 else 0), device=dev)
         flops = 2.0 * B * dout[0] * dout[1] * dout[2] * geo.cin * geo.cout * geo.k**3
-        return (lambda: ops.wgrad(geo, x, go, dw, ws)), flops
+        kw = dict(gathered16=x.bfloat16(), aligned16=go.bfloat16()) if shadows else {}
+        return (lambda: ops.wgrad(geo, x, go, dw, ws, **kw)), flops
 
     R3, H3, F3, P3 = (r,) * 3, (2 * r,) * 3, (S,) * 3, (S + 6,) * 3
 
@@ -259,6 +260,10 @@ def _cases(B=4, S=64):
         "res_fwd": lambda: conv_case(ops.conv_fwd_geom(B, R3, R3, 64, 64, 3, 1, 1), 64, 64, R3, R3),
         "res_wgrad": lambda: wgrad_case(ops.with_prec(ops.conv_wgrad_geom(B, R3, R3, 64, 64, 3, 1, 1), BF), R3, R3),
         "down0_wgrad": lambda: wgrad_case(ops.with_prec(ops.conv_wgrad_geom(B, F3, H3, 16, 32, 3, 2, 1), BF), F3, H3),
+        "down0_wgrad_step": lambda: wgrad_case(ops.with_prec(ops.conv_wgrad_geom(B, F3, H3, 16, 32, 3, 2, 1), BF), F3, H3,
+                                               shadows=True),
+        "down1_wgrad_step": lambda: wgrad_case(ops.with_prec(ops.conv_wgrad_geom(B, H3, R3, 32, 64, 3, 2, 1), BF), H3, R3,
+                                               shadows=True),
         "down0_fwd": lambda: conv_case(ops.conv_fwd_geom(B, F3, H3, 16, 32, 3, 2, 1), 16, 32, F3, H3),
         "up0_fwd": lambda: conv_case(ops.convt_fwd_geom(B, R3, H3, 64, 32, 3, 2, 1), 64, 32, R3, H3),
         "down1_fwd": lambda: conv_case(ops.conv_fwd_geom(B, H3, R3, 32, 64, 3, 2, 1), 32, 64, H3, R3),
