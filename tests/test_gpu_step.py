@@ -670,7 +670,7 @@ def test_step_gp_resampled_batches_match_oracle(b_opt, b_sub, seed):
     one pre-activation of the last up-sampling BatchNorm at -1.2e-7: the device's fp32 lands on the
     other side of the ReLU than float64, the channel's bias gradient moves by exactly that voxel's
     dL/d(ReLU out) (6.2e-5 = 2.5 % in the batch-2 diagnostic) and every generator gradient below it by
-    ~3e-3 — a mask flip, not an arithmetic error (tools/dbg/up1_cond.py,
+    ~3e-3 — a mask flip, not an arithmetic error (a one-off diagnostic in git history, round 5,
     profiles/r05_resample_mask_flip.txt).  Seed 140 is an ordinary draw without such a voxel."""
     from oracle import reference_torch as R
     from cgan3d_amd.data.synthetic import synth_patches
