@@ -568,7 +568,8 @@ def main():
     # events (hipExtLaunchKernel's dispatch events; the rest of the step unchanged), run over the
     # bench batches after the timed region
     kern_plan = []
-    if mode == "plan" and args.precision == "bf16" and roof_kname:
+    if mode == "plan" and args.precision == "bf16" and roof_kname and not dist:  # (one process: a DP plan re-recorded
+        # mid-run would re-issue its collectives outside the timed protocol)
         ops.plan_time_filter(roof_kname)
         try:
             tplan = eng.record()
