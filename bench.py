@@ -703,6 +703,7 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         progress("sub-line cpu_baseline")
         out["cpu_baseline"] = cpu_baseline(S, args.cpu_seconds, g_args)
+    progress("bench line")
     if rank == 0:
         print(json.dumps(out), flush=True)
     if dist:
