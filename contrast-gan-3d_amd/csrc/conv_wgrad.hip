@@ -830,6 +830,7 @@ __global__ __launch_bounds__(512) void wgrad_s2_kernel(Ws2Args a, const float* _
   // the window's out-of-volume items load a valid address (element 0) and are zeroed at the LDS store:
   // a select on the loaded value right after the load would make the compiler wait for it there,
   // which turned the prefetch into a serial load
+  static_assert(NXT <= 32, "one validity bit per staged X item");
   unsigned okm[DEPTH];
   auto load = [&](int sl, int rb) {
     okm[rb] = 0u;
