@@ -184,6 +184,8 @@ _SIGS = {
     "cgan3d_plan_destroy": ([_P], _I32),
     "cgan3d_plan_time_filter": ([C.c_char_p], _I32),
     "cgan3d_plan_times": ([_P, _P, _I64], _I64),
+    "cgan3d_plan_timeline": ([_P, _P, _P, _P, _I64], _I64),
+    "cgan3d_plan_timed_name": ([_P, _I64], C.c_char_p),
     "cgan3d_stream_wait": ([_P, _P], _I32),
     "cgan3d_comm_shared_library": ([], _I32),
     "cgan3d_comm_id_bytes": ([], _I32),

@@ -513,6 +513,20 @@ class Plan:
                 out += [float(v) for v in buf[:n]]
         return out
 
+    def timeline(self):
+        """The timed launches of the last ``run()`` as (stream index, start ms, end ms, kernel name), times from
+        each C segment's first timed launch (one segment without collectives); call after synchronising."""
+        lib, out = L.lib(), []
+        for it in self.items:
+            if isinstance(it, int):
+                n = int(lib.cgan3d_plan_timeline(it, None, None, None, 0))
+                a, b, sid = (ctypes.c_float * max(n, 1))(), (ctypes.c_float * max(n, 1))(), (ctypes.c_int32 * max(n, 1))()
+                lib.cgan3d_plan_timeline(it, a, b, sid, n)
+                for i in range(n):
+                    nm = lib.cgan3d_plan_timed_name(it, i)
+                    out.append((int(sid[i]), float(a[i]), float(b[i]), nm.decode() if nm else "?"))
+        return out
+
     def __del__(self):
         if L._lib is not None:
             for it in self.items:

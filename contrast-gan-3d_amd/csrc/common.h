@@ -34,6 +34,7 @@ struct Plan {
   // (start, stop) timing events of the launches cgan3d_plan_time_filter selected at record time
   // (hipExtLaunchKernel's own dispatch events: the kernel's in-plan duration, no extra packets)
   std::vector<std::pair<hipEvent_t, hipEvent_t>> timed;
+  std::vector<std::pair<hipStream_t, const void*>> timed_what;  // (stream, kernel) of each timed launch
   void add(std::function<hipError_t()> op, hipStream_t st, std::shared_ptr<hipEvent_t> stop = nullptr) {
     ops.push_back(std::move(op));
     tail[st] = std::move(stop);
@@ -57,6 +58,7 @@ inline void launch(void (*k)(KArgs...), dim3 grid, dim3 block, size_t lds, hipSt
       g_rec->events.push_back(t0);
       g_rec->events.push_back(t1);
       g_rec->timed.emplace_back(t0, t1);
+      g_rec->timed_what.emplace_back(st, reinterpret_cast<const void*>(k));
     } else {
       (void)hipEventDestroy(t0);
       t0 = nullptr;

@@ -161,3 +161,32 @@ extern "C" int cgan3d_stream_wait(void* waiter, void* signaler) {
   }
   return CGAN3D_OK;
 }
+
+// the timed launches of the last run as a timeline: start / end (ms) relative to the first timed launch's
+// start, the stream (index in order of first appearance among the timed launches); returns the count
+extern "C" int64_t cgan3d_plan_timeline(void* plan, float* start_ms, float* end_ms, int32_t* stream_id, int64_t max) {
+  if (plan == nullptr) return -1;
+  Plan* p = static_cast<Plan*>(plan);
+  const int64_t n = (int64_t)p->timed.size();
+  std::vector<hipStream_t> seen;
+  for (int64_t i = 0; i < n && i < max; ++i) {
+    float a = -1.f, b = -1.f;
+    if (hipEventElapsedTime(&a, p->timed[0].first, p->timed[i].first) != hipSuccess) a = -1.f;
+    if (hipEventElapsedTime(&b, p->timed[0].first, p->timed[i].second) != hipSuccess) b = -1.f;
+    if (start_ms) start_ms[i] = a;
+    if (end_ms) end_ms[i] = b;
+    int sid = -1;
+    for (size_t k = 0; k < seen.size(); ++k)
+      if (seen[k] == p->timed_what[i].first) sid = (int)k;
+    if (sid < 0) { sid = (int)seen.size(); seen.push_back(p->timed_what[i].first); }
+    if (stream_id) stream_id[i] = sid;
+  }
+  return n;
+}
+
+// the (mangled) kernel name of timed launch i, or NULL
+extern "C" const char* cgan3d_plan_timed_name(void* plan, int64_t i) {
+  Plan* p = static_cast<Plan*>(plan);
+  if (p == nullptr || i < 0 || i >= (int64_t)p->timed_what.size()) return nullptr;
+  return hipKernelNameRefByPtr(p->timed_what[i].second, p->timed_what[i].first);
+}

@@ -594,6 +594,12 @@ int cgan3d_plan_destroy(void* plan);
  * each timed launch's duration in ms (up to `max`, in record order) and returns how many there are. */
 int cgan3d_plan_time_filter(const char* substring);
 int64_t cgan3d_plan_times(void* plan, float* ms, int64_t max);
+/* The same launches as a timeline of the last run: start / end in ms from the first timed launch's start,
+ * and the stream of each (index in order of first appearance); cgan3d_plan_timed_name(plan, i) is the
+ * mangled kernel name of launch i.  (A kernel trace without a profiler: rocprofv3's per-dispatch cost
+ * makes the host issue the bottleneck of a traced plan step.) */
+int64_t cgan3d_plan_timeline(void* plan, float* start_ms, float* end_ms, int32_t* stream_id, int64_t max);
+const char* cgan3d_plan_timed_name(void* plan, int64_t i);
 /* `waiter` waits for all work enqueued so far on `signaler` (recorded when inside a plan). */
 int cgan3d_stream_wait(void* waiter, void* signaler);
 
