@@ -45,10 +45,18 @@ static bool bind_disabled() {
 
 static thread_local std::string g_time_filter;  // cgan3d_plan_time_filter
 
-bool plan_time_match(const void* k, hipStream_t st) {
+bool plan_time_match(const void* k, hipStream_t st) {  // the filter: substrings separated by '|'
   if (g_time_filter.empty()) return false;
   const char* n = hipKernelNameRefByPtr(k, st);
-  return n != nullptr && strstr(n, g_time_filter.c_str()) != nullptr;
+  if (n == nullptr) return false;
+  size_t b = 0;
+  while (b <= g_time_filter.size()) {
+    size_t e = g_time_filter.find('|', b);
+    if (e == std::string::npos) e = g_time_filter.size();
+    if (e > b && strstr(n, g_time_filter.substr(b, e - b).c_str()) != nullptr) return true;
+    b = e + 1;
+  }
+  return false;
 }
 
 }  // namespace cg

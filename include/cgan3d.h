@@ -588,7 +588,8 @@ int cgan3d_plan_end(void** plan);
 int64_t cgan3d_plan_size(void* plan);
 int cgan3d_plan_run(void* plan);
 int cgan3d_plan_destroy(void* plan);
-/* Round 6, measurement: launches of kernels whose (mangled) name contains `substring`, recorded while
+/* Round 6, measurement: launches of kernels whose (mangled) name contains `substring` (or one of several
+ * separated by '|'), recorded while
  * it is set (NULL or "" clears it; per host thread), are issued with their own start / stop timing
  * events (hipExtLaunchKernel); after a cgan3d_plan_run and a synchronisation, cgan3d_plan_times writes
  * each timed launch's duration in ms (up to `max`, in record order) and returns how many there are. */

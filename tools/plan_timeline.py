@@ -1,7 +1,8 @@
 """A kernel timeline of the plan-mode bench step without a profiler (round 6): the step recorded with
 every library kernel timed by its own hipExtLaunchKernel start / stop events (cgan3d_plan_time_filter,
 cgan3d_plan_timeline), run over the bench batches; prints the median-length step's launches per stream
-with the idle gap before each, and the main stream's busy / idle totals.
+with the idle gap before each, and the main stream's busy / idle totals (each timeline is the last of four
+runs issued back to back, so the host is ahead of the GPU as in the bench).
 
     python tools/plan_timeline.py [--steps 20] [--out gpurun_out/plan_timeline.txt]
 
@@ -25,6 +26,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--out", default=None)
+    ap.add_argument("--filter", default="2cg", help="kernels to time ('|'-separated name substrings; every timed "
+                    "launch adds its own event cost, so time few to see the untimed step's gaps)")
     a = ap.parse_args()
     from cgan3d_amd import ops
     from cgan3d_amd.data.synthetic import synth_patches
@@ -46,15 +49,18 @@ def main():
     for i in range(5):
         eng.load_inputs(*batches[i % 2])
         eng.step()
-    ops.plan_time_filter("2cg")  # every kernel of the library's namespace (mangled names "_ZN2cg...")
+    ops.plan_time_filter(a.filter)  # default: every kernel of the library's namespace ("_ZN2cg...")
     try:
         plan = eng.record()
     finally:
         ops.plan_time_filter(None)
     runs = []
     for i in range(a.steps):
-        eng.load_inputs(*batches[i % 2])
-        plan.run()
+        # four runs back to back, the timeline read from the last: issued while the GPU is busy with the
+        # previous ones (the host ahead of the GPU, as in the bench's timed region), not from a cold queue
+        for k in range(4):
+            eng.load_inputs(*batches[(i + k) % 2])
+            plan.run()
         torch.cuda.synchronize()
         tl = plan.timeline()
         span = max(e for _, _, e, _ in tl) - min(s for _, s, _, _ in tl)
